@@ -1,0 +1,235 @@
+"""ctypes binding of libaos_gpu.so (include/aos_gpu.h) — the MI355X seed-gen + GVD hot path.
+
+Mirrors the reference nodes' interface (AosSeedGenNode / AosGvdNode callbacks) for Python
+harnesses (tests, bench). There is no fallback: if libaos_gpu.so is missing or no gfx950 device
+is visible, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIB_PATH = os.path.join(HERE, "libaos_gpu.so")
+HEADER = os.path.join(ROOT, "include", "aos_gpu.h")
+
+c_f, c_d, c_i, c_u, c_u64, c_vp = (ctypes.c_float, ctypes.c_double, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64,
+                                   ctypes.c_void_p)
+P = ctypes.POINTER
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("clipping_minz", c_f), ("clipping_maxz", c_f), ("clipping_minx", c_f), ("clipping_maxx", c_f),
+                ("clipping_miny", c_f), ("clipping_maxy", c_f), ("grid_resolution", c_f), ("inflation_radius", c_f),
+                ("cluster_min_length", c_d), ("ror_radius", c_d), ("ror_min_neighbors", c_i),
+                ("subdiv_rect_mode", c_i), ("max_graph_publish_rate", c_d)]
+
+
+class CloudView(ctypes.Structure):
+    _fields_ = [("data", c_vp), ("n_points", c_u64), ("point_step", c_u), ("off_x", c_u), ("off_y", c_u),
+                ("off_z", c_u), ("is_dense", c_i), ("on_device", c_i)]
+
+
+class GridInfo(ctypes.Structure):
+    _fields_ = [("origin_x", c_d), ("origin_y", c_d), ("resolution", c_f), ("width", c_u), ("height", c_u)]
+
+
+class SeedGenOut(ctypes.Structure):
+    _fields_ = [("info", GridInfo), ("thin_iters", c_i), ("n_input", c_u64), ("n_ror_kept", c_u64),
+                ("n_clipped", c_u64), ("occupancy", P(ctypes.c_int8)), ("skeleton", P(ctypes.c_int8)),
+                ("d_occupancy", c_vp), ("d_skeleton", c_vp), ("n_clusters_all", c_i), ("n_rows", c_i),
+                ("row_center", P(c_d)), ("row_start", P(c_d)), ("row_end", P(c_d)), ("row_length", P(c_d)),
+                ("n_virtual", c_i), ("n_ray", c_i), ("n_endpoint", c_i), ("n_voronoi", c_i), ("voronoi_xy", P(c_d)),
+                ("rows_info_xy", P(c_d)), ("n_cluster_info", c_i), ("cluster_info_xy", P(c_d)),
+                ("ms_ror", c_f), ("ms_grid", c_f), ("ms_thin", c_f), ("ms_cluster", c_f), ("ms_seeds", c_f),
+                ("ms_total", c_f)]
+
+
+class GvdIn(ctypes.Structure):
+    _fields_ = [("seeds_xy", P(c_d)), ("n_seeds", c_i), ("rows_info_xy", P(c_d)), ("n_rows_poses", c_i),
+                ("info", GridInfo), ("skeleton", P(ctypes.c_int8))]
+
+
+class GvdOut(ctypes.Structure):
+    _fields_ = [("published", c_i), ("resolution", c_d), ("origin_x", c_d), ("origin_y", c_d), ("num_nodes", c_i),
+                ("num_edges", c_i), ("nodes_xy", P(c_d)), ("node_labels", P(c_i)), ("node_cluster_indices", P(c_i)),
+                ("node_label_counts", P(c_i)), ("n_label_entries", c_i), ("node_label_clusters", P(c_i)),
+                ("node_label_types", P(c_i)), ("edges", P(c_i)), ("edge_lengths", P(c_f)),
+                ("edge_clearances", P(c_f)), ("n_merged_seeds", c_i), ("n_voronoi_edges", c_i),
+                ("n_boundary_points", c_i), ("ms_merge", c_f), ("ms_delaunay", c_f), ("ms_graph", c_f),
+                ("ms_total", c_f)]
+
+
+def build() -> str:
+    subprocess.check_call(["make", "-s", "-C", HERE, "-j8"])
+    return LIB_PATH
+
+
+def header_functions() -> list[str]:
+    """Function names declared in include/aos_gpu.h."""
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(aos_[a-z_]+)\s*\(", txt)))
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: run `make -C {HERE}` (no CPU fallback exists)")
+        L = ctypes.CDLL(LIB_PATH)
+        L.aos_last_error.restype = ctypes.c_char_p
+        L.aos_default_params.argtypes = [P(Params)]
+        L.aos_create.argtypes = [P(Params), c_i, P(c_vp)]
+        L.aos_destroy.argtypes = [c_vp]
+        L.aos_set_polygon.argtypes = [c_vp, c_vp, c_u]
+        L.aos_seedgen_process.argtypes = [c_vp, P(CloudView), c_i, P(SeedGenOut)]
+        L.aos_seedgen_reprocess.argtypes = [c_vp, c_i, P(SeedGenOut)]
+        L.aos_gvd_process.argtypes = [c_vp, P(GvdIn), P(GvdOut)]
+        L.aos_gvd_from_seedgen.argtypes = [c_vp, P(GvdOut)]
+        L.aos_debug_grid.argtypes = [c_vp, ctypes.c_char_p, c_vp, c_u64]
+        L.aos_stream.restype = c_vp
+        L.aos_stream.argtypes = [c_vp]
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise RuntimeError(f"libaos_gpu error {rc}: {lib().aos_last_error().decode()}")
+
+
+def default_params(**kw) -> Params:
+    p = Params()
+    lib().aos_default_params(ctypes.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def _arr(ptr, n, dtype):
+    if n <= 0 or not ptr:
+        return np.zeros(0, dtype=dtype)
+    return np.ctypeslib.as_array(ptr, shape=(n,)).astype(dtype, copy=True)
+
+
+def _seedgen_dict(o: SeedGenOut, want_host: bool) -> dict:
+    W, H = o.info.width, o.info.height
+    nr = o.n_rows
+    r = {
+        "origin": (o.info.origin_x, o.info.origin_y), "resolution": o.info.resolution, "width": W, "height": H,
+        "thin_iters": o.thin_iters, "n_input": o.n_input, "n_clipped": o.n_clipped, "n_clusters_all": o.n_clusters_all,
+        "row_center": _arr(o.row_center, 2 * nr, np.float64).reshape(-1, 2),
+        "row_start": _arr(o.row_start, 2 * nr, np.float64).reshape(-1, 2),
+        "row_end": _arr(o.row_end, 2 * nr, np.float64).reshape(-1, 2),
+        "row_length": _arr(o.row_length, nr, np.float64),
+        "n_virtual": o.n_virtual, "n_ray": o.n_ray, "n_endpoint": o.n_endpoint,
+        "voronoi_seeds": _arr(o.voronoi_xy, 2 * o.n_voronoi, np.float64).reshape(-1, 2),
+        "rows_info": _arr(o.rows_info_xy, 4 * nr, np.float64).reshape(-1, 2),
+        "cluster_info": _arr(o.cluster_info_xy, 2 * o.n_cluster_info, np.float64).reshape(-1, 2),
+        "d_occupancy": o.d_occupancy, "d_skeleton": o.d_skeleton,
+        "ms": {"ror": o.ms_ror, "grid": o.ms_grid, "thin": o.ms_thin, "cluster": o.ms_cluster, "seeds": o.ms_seeds,
+               "total": o.ms_total},
+    }
+    nv, nrr = o.n_virtual, o.n_ray
+    seeds = r["voronoi_seeds"]
+    r["virtual_seeds"], r["ray_seeds"], r["endpoint_seeds"] = seeds[:nv], seeds[nv:nv + nrr], seeds[nv + nrr:]
+    if want_host:
+        r["occupancy"] = _arr(o.occupancy, W * H, np.int8).reshape(H, W)
+        r["skeleton_framed"] = _arr(o.skeleton, W * H, np.int8).reshape(H, W)
+    return r
+
+
+def _gvd_dict(o: GvdOut) -> dict:
+    nn, ne = o.num_nodes, o.num_edges
+    return {
+        "published": bool(o.published), "resolution": o.resolution, "origin": (o.origin_x, o.origin_y),
+        "nodes": _arr(o.nodes_xy, 2 * nn, np.float64).reshape(-1, 2),
+        "node_labels": _arr(o.node_labels, nn, np.int32),
+        "node_cluster_indices": _arr(o.node_cluster_indices, nn, np.int32),
+        "node_label_counts": _arr(o.node_label_counts, nn, np.int32),
+        "node_label_clusters": _arr(o.node_label_clusters, o.n_label_entries, np.int32),
+        "node_label_types": _arr(o.node_label_types, o.n_label_entries, np.int32),
+        "edges": _arr(o.edges, 2 * ne, np.int32).reshape(-1, 2),
+        "edge_lengths": _arr(o.edge_lengths, ne, np.float32),
+        "edge_clearances": _arr(o.edge_clearances, ne, np.float32),
+        "n_merged": o.n_merged_seeds, "n_vor_edges": o.n_voronoi_edges, "n_boundary_raw": o.n_boundary_points,
+        "ms": {"merge": o.ms_merge, "delaunay": o.ms_delaunay, "graph": o.ms_graph, "total": o.ms_total},
+    }
+
+
+class Ctx:
+    """One handle = one GPU + one HIP stream (aos_create)."""
+
+    def __init__(self, params: Params | None = None, device: int = 0):
+        self.params = params or default_params()
+        h = c_vp()
+        _check(lib().aos_create(ctypes.byref(self.params), device, ctypes.byref(h)))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            lib().aos_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_polygon(self, poly_xy: np.ndarray):
+        a = np.ascontiguousarray(poly_xy, dtype=np.float64).reshape(-1)
+        _check(lib().aos_set_polygon(self.h, a.ctypes.data, a.size // 2))
+
+    def seedgen(self, cloud, n_points: int | None = None, point_step=16, offs=(0, 4, 8), is_dense=True,
+                on_device=False, want_host=True) -> dict:
+        """cloud: (n, point_step) uint8 numpy array, or an int device pointer with on_device=True."""
+        if on_device:
+            ptr = int(cloud)
+            n = int(n_points)
+        else:
+            cloud = np.ascontiguousarray(cloud)
+            ptr = cloud.ctypes.data
+            n = cloud.shape[0] if cloud.ndim == 2 else cloud.size // point_step
+        v = CloudView(ptr, n, point_step, offs[0], offs[1], offs[2], int(is_dense), int(on_device))
+        o = SeedGenOut()
+        _check(lib().aos_seedgen_process(self.h, ctypes.byref(v), int(want_host), ctypes.byref(o)))
+        return _seedgen_dict(o, want_host)
+
+    def reprocess(self, want_host=True) -> dict:
+        o = SeedGenOut()
+        _check(lib().aos_seedgen_reprocess(self.h, int(want_host), ctypes.byref(o)))
+        return _seedgen_dict(o, want_host)
+
+    def gvd_from_seedgen(self) -> dict:
+        o = GvdOut()
+        _check(lib().aos_gvd_from_seedgen(self.h, ctypes.byref(o)))
+        return _gvd_dict(o)
+
+    def gvd(self, seeds, rows_info, grid: dict) -> dict:
+        s = np.ascontiguousarray(seeds, dtype=np.float64).reshape(-1)
+        r = np.ascontiguousarray(rows_info, dtype=np.float64).reshape(-1)
+        sk = np.ascontiguousarray(grid["skeleton_framed"], dtype=np.int8).reshape(-1)
+        info = GridInfo(grid["origin"][0], grid["origin"][1], grid["resolution"], grid["width"], grid["height"])
+        gi = GvdIn(s.ctypes.data_as(P(c_d)), s.size // 2, r.ctypes.data_as(P(c_d)), r.size // 2, info,
+                   sk.ctypes.data_as(P(ctypes.c_int8)))
+        o = GvdOut()
+        _check(lib().aos_gvd_process(self.h, ctypes.byref(gi), ctypes.byref(o)))
+        return _gvd_dict(o)
+
+    def debug_grid(self, which: str, shape) -> np.ndarray:
+        out = np.zeros(shape, dtype=np.int8)
+        _check(lib().aos_debug_grid(self.h, which.encode(), out.ctypes.data, out.size))
+        return out
+
+    def stream(self) -> int:
+        return lib().aos_stream(self.h)

@@ -1,0 +1,91 @@
+// Internal declarations of libaos_gpu.so (MI355X / gfx950). Not part of the ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/aos_gpu.h"
+
+namespace aos {
+
+// ------------------------------------------------------------------ errors
+void set_error(const std::string &msg);
+struct HipError { hipError_t e; const char *what; int line; };
+#define AOS_HIP(x)                                                        \
+    do {                                                                  \
+        hipError_t _e = (x);                                              \
+        if (_e != hipSuccess) throw ::aos::HipError{_e, #x, __LINE__};    \
+    } while (0)
+
+// ------------------------------------------------------------------ device buffers
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    void *ensure(size_t bytes) {
+        if (bytes <= cap) return p;
+        if (p) AOS_HIP(hipFree(p));
+        p = nullptr;
+        size_t c = bytes + bytes / 8 + 256;
+        AOS_HIP(hipMalloc(&p, c));
+        cap = c;
+        return p;
+    }
+    template <class T> T *as() const { return static_cast<T *>(p); }
+    void release() { if (p) (void)hipFree(p); p = nullptr; cap = 0; }
+};
+
+struct PinnedBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    void *ensure(size_t bytes) {
+        if (bytes <= cap) return p;
+        if (p) AOS_HIP(hipHostFree(p));
+        p = nullptr;
+        size_t c = bytes + bytes / 8 + 256;
+        AOS_HIP(hipHostMalloc(&p, c, hipHostMallocDefault));
+        cap = c;
+        return p;
+    }
+    template <class T> T *as() const { return static_cast<T *>(p); }
+    void release() { if (p) (void)hipHostFree(p); p = nullptr; cap = 0; }
+};
+
+typedef std::vector<std::pair<double, double>> Poly;
+
+// Geometry of one seed-gen frame (getActiveBounds + generateOccupancyGrid, seed_gen:581-600, 874-890).
+struct FrameGeom {
+    float minx, maxx, miny, maxy;      // polygon bbox +- 2.5 m, float
+    double origin_x, origin_y;         // (double)minx, (double)miny
+    float res;
+    int W, H, WW;                      // WW = 64-bit words per row
+    int R;                             // inflation cells
+};
+
+// ------------------------------------------------------------------ kernels (launchers)
+struct RorLaunch {
+    const uint8_t *cloud; uint64_t n; uint32_t step, ox, oy, oz; int is_dense;
+    float bminx, bminy, bminz, bmaxx, bmaxy, bmaxz, inv_cs; int nbx, nby;
+    float cminx, cmaxx, cminy, cmaxy, cminz, cmaxz;
+    double r2; float r2f; int need;
+    double origin_x, origin_y; float res; int W, H;
+};
+void launch_ror_bin(const RorLaunch &L, int *bin_count, int2 *pt_binslot, hipStream_t s);
+void launch_ror_scatter(const RorLaunch &L, const int *bin_start, const int2 *pt_binslot, float4 *sorted, hipStream_t s);
+void launch_ror_raster(const RorLaunch &L, const int *bin_start, const float4 *sorted, const int *d_n_binned, int n_max,
+                       uint8_t *raster, unsigned long long *counters, hipStream_t s);
+void launch_pack_bits(const uint8_t *bytes, uint64_t *bits, int W, int H, int WW, hipStream_t s);
+void launch_inflate(const uint64_t *in, uint64_t *out, const FrameGeom &g, hipStream_t s);
+void launch_bits_to_bytes(const uint64_t *bits, int8_t *out, const FrameGeom &g, int frame, hipStream_t s);
+void launch_open(const uint64_t *in, uint64_t *out, const FrameGeom &g, hipStream_t s);
+// Zhang-Suen temporal block: KIT iterations per launch; flags[0] = non-empty after iteration 1,
+// flags[1 + k] = iteration k (0-based) deleted something.
+constexpr int kThinItersPerLaunch = 8;
+void launch_thin_block(const uint64_t *in, uint64_t *out, const FrameGeom &g, int base_iter, int *flags, hipStream_t s);
+void launch_draw_rect(int8_t *grid, const FrameGeom &g, int gx0, int gy0, int gx1, int gy1, hipStream_t s);
+size_t scan_temp_bytes(int n);
+void launch_exclusive_scan(const int *in, int *out, int n, void *temp, size_t temp_bytes, hipStream_t s);
+
+}  // namespace aos

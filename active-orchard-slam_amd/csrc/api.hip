@@ -1,0 +1,157 @@
+// libaos_gpu.so — C ABI + per-handle orchestration of the seed-gen / GVD hot path on MI355X.
+// One handle = one device + one HIP stream; all stage buffers stay resident in HBM.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <new>
+
+#include "aos_ctx.h"
+
+namespace aos {
+
+thread_local std::string g_err;
+void set_error(const std::string &msg) { g_err = msg; }
+
+}  // namespace aos
+
+using namespace aos;
+
+#define AOS_GUARD_BEGIN try {
+#define AOS_GUARD_END                                                                                         \
+    }                                                                                                         \
+    catch (const HipError &e) {                                                                               \
+        set_error(std::string("HIP error ") + hipGetErrorString(e.e) + " at api line " + std::to_string(e.line) + \
+                  ": " + e.what);                                                                             \
+        return AOS_E_HIP;                                                                                     \
+    }                                                                                                         \
+    catch (const std::bad_alloc &) {                                                                          \
+        set_error("out of host memory");                                                                      \
+        return AOS_E_NOMEM;                                                                                   \
+    }                                                                                                         \
+    catch (const std::exception &e) {                                                                         \
+        set_error(std::string("error: ") + e.what());                                                         \
+        return AOS_E_STATE;                                                                                   \
+    }
+
+extern "C" {
+
+const char *aos_last_error(void) { return g_err.c_str(); }
+
+void aos_default_params(aos_params *p) {
+    p->clipping_minz = -0.4f; p->clipping_maxz = 0.5f;
+    p->clipping_minx = -5.0f; p->clipping_maxx = 72.0f;
+    p->clipping_miny = -10.0f; p->clipping_maxy = 20.0f;
+    p->grid_resolution = 0.05f;
+    p->inflation_radius = 0.8f;
+    p->cluster_min_length = 2.0;
+    p->ror_radius = 0.2;
+    p->ror_min_neighbors = 2;
+    p->subdiv_rect_mode = 0;
+    p->max_graph_publish_rate = 10.0;
+}
+
+int aos_create(const aos_params *p, int device, aos_ctx **out) {
+    if (!p || !out) { set_error("aos_create: null argument"); return AOS_E_INVALID; }
+    *out = nullptr;
+    AOS_GUARD_BEGIN
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        set_error("aos_create: no HIP device visible (libaos_gpu has no CPU fallback)");
+        return AOS_E_HIP;
+    }
+    if (device < 0 || device >= ndev) { set_error("aos_create: bad device index"); return AOS_E_INVALID; }
+    hipDeviceProp_t prop;
+    AOS_HIP(hipGetDeviceProperties(&prop, device));
+    if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos) {
+        set_error(std::string("aos_create: device is ") + prop.gcnArchName + ", this build targets gfx950 only");
+        return AOS_E_HIP;
+    }
+    auto *c = new aos_ctx();
+    c->P = *p;
+    c->device = device;
+    AOS_HIP(hipSetDevice(device));
+    AOS_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    for (auto &e : c->ev) AOS_HIP(hipEventCreate(&e));
+    // hard-coded default polygon of the reference constructor (seed_gen:196-199)
+    c->poly = {{-1.972916603088379, 7.9420671463012695}, {-2.0726776123046875, 0.022441387176513672},
+               {70.22465515136719, 2.102720260620117}, {69.48777770996094, 9.786612510681152}};
+    *out = c;
+    return AOS_OK;
+    AOS_GUARD_END
+}
+
+void aos_destroy(aos_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    c->release();
+    for (auto &e : c->ev) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+void *aos_stream(aos_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+int aos_set_polygon(aos_ctx *c, const double *xy, uint32_t n) {
+    if (!c) { set_error("null handle"); return AOS_E_INVALID; }
+    if (!xy || n < 3) return AOS_OK;  // explorationAreaCallback ignores < 3 points (seed_gen:253)
+    c->poly.clear();
+    for (uint32_t i = 0; i < n; ++i) c->poly.push_back({xy[2 * i], xy[2 * i + 1]});
+    return AOS_OK;
+}
+
+int aos_seedgen_process(aos_ctx *c, const aos_cloud_view *cloud, int want_host, aos_seedgen_out *out) {
+    if (!c || !cloud || !out) { set_error("aos_seedgen_process: null argument"); return AOS_E_INVALID; }
+    if (cloud->n_points && (!cloud->data || cloud->point_step < 12 || (cloud->point_step & 3) || (cloud->off_x & 3) ||
+                            (cloud->off_y & 3) || (cloud->off_z & 3) || cloud->off_x + 4 > cloud->point_step ||
+                            cloud->off_y + 4 > cloud->point_step || cloud->off_z + 4 > cloud->point_step)) {
+        set_error("aos_seedgen_process: invalid PointCloud2 layout (float32 x/y/z, 4-byte aligned)");
+        return AOS_E_INVALID;
+    }
+    AOS_GUARD_BEGIN
+    AOS_HIP(hipSetDevice(c->device));
+    c->set_cloud(*cloud);
+    c->run_seedgen(want_host != 0, *out);
+    return AOS_OK;
+    AOS_GUARD_END
+}
+
+int aos_seedgen_reprocess(aos_ctx *c, int want_host, aos_seedgen_out *out) {
+    if (!c || !out) { set_error("aos_seedgen_reprocess: null argument"); return AOS_E_INVALID; }
+    if (!c->have_cloud) { std::memset(out, 0, sizeof(*out)); return AOS_OK; }  // last_cloud empty (:283)
+    AOS_GUARD_BEGIN
+    AOS_HIP(hipSetDevice(c->device));
+    c->run_seedgen(want_host != 0, *out);
+    return AOS_OK;
+    AOS_GUARD_END
+}
+
+int aos_gvd_process(aos_ctx *c, const aos_gvd_in *in, aos_gvd_out *out) {
+    if (!c || !in || !out) { set_error("aos_gvd_process: null argument"); return AOS_E_INVALID; }
+    AOS_GUARD_BEGIN
+    AOS_HIP(hipSetDevice(c->device));
+    c->run_gvd_external(*in, *out);
+    return AOS_OK;
+    AOS_GUARD_END
+}
+
+int aos_gvd_from_seedgen(aos_ctx *c, aos_gvd_out *out) {
+    if (!c || !out) { set_error("aos_gvd_from_seedgen: null argument"); return AOS_E_INVALID; }
+    if (!c->have_frame) { set_error("aos_gvd_from_seedgen: no seed-gen frame yet"); return AOS_E_STATE; }
+    AOS_GUARD_BEGIN
+    AOS_HIP(hipSetDevice(c->device));
+    c->run_gvd_from_frame(*out);
+    return AOS_OK;
+    AOS_GUARD_END
+}
+
+int aos_debug_grid(aos_ctx *c, const char *which, int8_t *dst, uint64_t capacity) {
+    if (!c || !which || !dst) { set_error("aos_debug_grid: null argument"); return AOS_E_INVALID; }
+    if (!c->have_frame) { set_error("aos_debug_grid: no frame"); return AOS_E_STATE; }
+    AOS_GUARD_BEGIN
+    AOS_HIP(hipSetDevice(c->device));
+    return c->debug_grid(which, dst, capacity);
+    AOS_GUARD_END
+}
+
+}  // extern "C"

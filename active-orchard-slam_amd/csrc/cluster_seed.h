@@ -1,0 +1,90 @@
+// Cluster / tree-row / seed stage and GVD stage state. Not part of the ABI.
+#pragma once
+#include <vector>
+
+#include "aos_internal.h"
+
+namespace aos {
+
+// Per-cluster result of the cluster-statistics kernel (a8-a10).
+struct ClusterRec {
+    long long sx, sy;        // exact integer sums of cell coordinates
+    int n;                   // cells
+    int maxd2;               // max pairwise squared distance (grid units)
+    float cx, cy;            // cluster.center_x / center_y (grid units, float)
+    float length;            // cluster.length (m)
+    int flags;               // bit0: row (length >= min && centre in polygon); bit1: needs BFS order
+    double2 center, start, end;  // world (double from float)
+};
+
+// ------------------------------------------------------------------ greedy first-come de-duplication
+// Keeps candidate i iff no earlier KEPT candidate conflicts with it (the reference's
+// "if no existing within d: push_back" loops) = the lexicographically-first maximal independent
+// set of the conflict graph; decided on the GPU in rounds over hashed conflict lists.
+enum ConflictMode {
+    kConflictLess = 0,     // sqrt(dx*dx + dy*dy) <  thr  (seed dedups, seed_gen:2076-2085 ...)
+    kConflictLessEq = 1,   // sqrt(dx*dx + dy*dy) <= thr  (GVD seed merge, gvd:107-115)
+    kConflictKeyOrSq = 2,  // same (int)(x*100),(int)(y*100) key, or dx*dx + dy*dy < thr (extractBoundaryPoints)
+};
+struct HashG { double x0, y0, inv; int nx, ny; };
+HashG make_hash(double minx, double maxx, double miny, double maxy, double cell);
+struct DedupScratch { DevBuf keys, idx, skeys, sidx, ccount, coff, clist, state, f, pos, tmp; int n_conf = 0; };
+// cand/ok device arrays of n entries; kept points (in order) -> out; optional kept flags -> state (S.state).
+// Returns the kept count.
+int greedy_dedup(DedupScratch &S, const double2 *cand, const int *ok, int n, int mode, double thr, const HashG &h,
+                 double2 *out, int *kept_index_out, hipStream_t s, int *h_scalar);
+
+struct ClusterSeedState {
+    DedupScratch dedup;
+    DevBuf fg_bits, word_cnt, word_off, fg_list, parent, root_flag, root_rank, cl_count, cl_off, cl_cursor, cl_cells;
+    DevBuf rec, row_idx, bfs_queue, bfs_vis, poly;
+    DevBuf cand_xy, cand_ok, cand_state, hash_count, hash_start, hash_slot, hash_sorted, seed_out, misc, scan_tmp;
+    PinnedBuf h_misc;
+    int n_fg = 0, n_clusters = 0, n_rows = 0;
+    std::vector<ClusterRec> h_rec;
+};
+
+// Everything the seed stage needs from the frame.
+struct SeedStageIn {
+    const uint64_t *skel_bits;   // frameless skeleton
+    const FrameGeom *g;
+    const Poly *poly;
+    double cluster_min_length;
+};
+
+struct SeedStageOut {
+    int n_clusters_all = 0;
+    std::vector<double> row_center, row_start, row_end, row_length;  // all_tree_rows order
+    std::vector<double> virtual_xy, ray_xy, endpoint_xy;
+    std::vector<double> rows_info, cluster_info;
+    const double *d_voronoi = nullptr;  // device copy of the concatenated seeds
+    int n_voronoi = 0;
+};
+
+void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStageOut &out, hipStream_t stream,
+                            hipEvent_t ev_mid);
+
+// ------------------------------------------------------------------ GVD
+struct GvdState {
+    DedupScratch dedup;
+    DevBuf seeds, merge_state, hash_count, hash_start, hash_slot, hash_sorted, scan_tmp, misc;
+    DevBuf edges, bpts, near_idx, cand, cand_ok, skel, grid_bytes_ext;
+    PinnedBuf h_misc;
+    // host outputs
+    std::vector<double> nodes_xy;
+    std::vector<int32_t> labels, cluster_idx, label_counts, label_clusters, label_types, edges_out;
+    std::vector<float> lengths, clearances;
+    int n_merged = 0, n_vor_edges = 0, n_bpts = 0;
+    float ms_merge = 0, ms_delaunay = 0, ms_graph = 0, ms_total = 0;
+};
+
+struct GvdStageIn {
+    const double *seeds_host;  int n_seeds;     // /voronoi_seeds (x, y)
+    const double *rows_info;   int n_rows_poses;
+    aos_grid_info info;
+    const int8_t *d_skeleton;                   // framed skeleton bytes on device
+};
+bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipStream_t stream, hipEvent_t *ev);
+void free_gvd_scratch(GvdState &G);
+
+}  // namespace aos

@@ -1,0 +1,682 @@
+// Clusters -> tree rows -> Voronoi seeds (seed_gen:970-1083, 1258-1512, 1730-2268) on gfx950.
+//
+// a8 clusterOccupiedCells is a raster-order scan + FIFO BFS. Its outputs depend on the BFS
+// order only through (i) float sums of cell coordinates and (ii) "first strict maximum"
+// tie-breaks. The GPU computes the partition with union-find (root = minimum raster index =
+// the reference's discovery order) and every per-cluster statistic order-free, together with a
+// certificate: integer coordinate sums <= 2^24 (so every float partial sum is exact in any
+// order) and no ties in the three argmax searches. A cluster without the certificate is
+// replayed exactly (FIFO BFS with the reference's neighbour order) by a GPU thread.
+//
+// Greedy first-come de-duplications (seeds within 0.5 m) are the lexicographically-first
+// maximal independent set of the conflict graph in candidate order; the GPU builds the graph
+// with a uniform hash and decides the set in rounds (a candidate is kept once every earlier
+// conflicting candidate is removed, removed once one of them is kept).
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "cluster_seed.h"
+
+namespace aos {
+
+static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+// isPointInPolygon seed_gen:1231-1255
+__device__ bool d_pip(double px, double py, const double *poly, int n) {
+    if (n < 3) return false;
+    bool inside = false;
+    int j = n - 1;
+    for (int i = 0; i < n; ++i) {
+        double pix = poly[2 * i], piy = poly[2 * i + 1], pjx = poly[2 * j], pjy = poly[2 * j + 1];
+        double dy = pjy - piy;
+        if (fabs(dy) > 1e-9) {
+            if (((piy > py) != (pjy > py)) && (px < (pjx - pix) * (py - piy) / dy + pix)) inside = !inside;
+        }
+        j = i;
+    }
+    return inside;
+}
+
+struct GridC {
+    double ox, oy;       // origin
+    float res;
+    int W, H, WW;
+    double minx, maxx, miny, maxy;  // origin + W * res (float product), seed_gen:1807-1810
+    double amax;         // castRayFromEndpoint absolute max distance, seed_gen:1838-1840
+};
+
+// float world coordinate of a cell: origin + float(x) * res (float product, double add, to float)
+__device__ __forceinline__ float cell_world(double o, int i, float res) { return (float)(o + (double)((float)i * res)); }
+
+__device__ __forceinline__ bool bit_at(const uint64_t *bits, int WW, int x, int y) {
+    return (bits[(size_t)y * WW + (x >> 6)] >> (x & 63)) & 1ull;
+}
+
+// ------------------------------------------------------------------ foreground = skeleton inside polygon
+__global__ void k_fg(const uint64_t *skel, uint64_t *fg, int *cnt, GridC g, const double *poly, int np) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    if (c >= g.WW || y >= g.H) return;
+    size_t wi = (size_t)y * g.WW + c;
+    uint64_t w = skel[wi], o = 0;
+    const double wy = cell_world(g.oy, y, g.res);
+    while (w) {
+        int b = __ffsll((long long)w) - 1;
+        w &= w - 1;
+        int x = c * 64 + b;
+        if (d_pip(cell_world(g.ox, x, g.res), wy, poly, np)) o |= 1ull << b;
+    }
+    fg[wi] = o;
+    cnt[wi] = __popcll(o);
+}
+
+__global__ void k_fg_list(const uint64_t *fg, const int *off, int *list, GridC g) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    if (c >= g.WW || y >= g.H) return;
+    size_t wi = (size_t)y * g.WW + c;
+    uint64_t w = fg[wi];
+    int k = off[wi];
+    while (w) {
+        int b = __ffsll((long long)w) - 1;
+        w &= w - 1;
+        list[k++] = y * g.W + c * 64 + b;
+    }
+}
+
+__device__ __forceinline__ int fg_index(const uint64_t *fg, const int *off, const GridC &g, int x, int y) {
+    if (x < 0 || y < 0 || x >= g.W || y >= g.H) return -1;
+    size_t wi = (size_t)y * g.WW + (x >> 6);
+    uint64_t w = fg[wi];
+    int b = x & 63;
+    if (!((w >> b) & 1ull)) return -1;
+    return off[wi] + __popcll(w & ((1ull << b) - 1));
+}
+
+// ------------------------------------------------------------------ union-find CCL (8-connectivity)
+__device__ __forceinline__ int ld_parent(int *parent, int i) {
+    return __hip_atomic_load(&parent[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ int uf_find(int *parent, int x) {
+    while (true) {
+        int p = ld_parent(parent, x);
+        if (p == x) return x;
+        x = p;
+    }
+}
+__global__ void k_ccl_init(int *parent, int n) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) parent[i] = i;
+}
+__global__ void k_ccl_union(const int *list, int n, const uint64_t *fg, const int *off, GridC g, int *parent) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int p = list[i], y = p / g.W, x = p - y * g.W;
+    const int ndx[4] = {-1, 0, 1, -1}, ndy[4] = {-1, -1, -1, 0};
+    for (int k = 0; k < 4; ++k) {
+        int j = fg_index(fg, off, g, x + ndx[k], y + ndy[k]);
+        if (j < 0) continue;
+        int a = uf_find(parent, i), b = uf_find(parent, j);
+        while (a != b) {
+            if (a < b) { int t = a; a = b; b = t; }
+            int old = atomicCAS(&parent[a], a, b);  // link the larger root under the smaller
+            if (old == a) break;
+            a = uf_find(parent, old);
+            b = uf_find(parent, b);
+        }
+    }
+}
+__global__ void k_ccl_flatten(int *parent, int *is_root, int n) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int x = i;
+    while (parent[x] != x) x = parent[x];
+    parent[i] = x;
+    is_root[i] = (x == i);
+}
+__global__ void k_cluster_count(const int *parent, const int *rank, int n, int *cid_of, int *count, int *slot) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int c = rank[parent[i]];
+    cid_of[i] = c;
+    slot[i] = atomicAdd(&count[c], 1);
+}
+__global__ void k_cluster_scatter(const int *list, const int *cid_of, const int *slot, const int *off, int n, int *cells) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    cells[off[cid_of[i]] + slot[i]] = list[i];
+}
+
+// ------------------------------------------------------------------ per-cluster statistics
+struct StatArgs {
+    const int *off, *cells;
+    const int *list;          // fg list (raster order); list[root] = first raster cell of a cluster
+    int n_clusters;
+    GridC g;
+    const double *poly; int np;
+    float min_length;
+    ClusterRec *rec;
+};
+
+template <typename T, typename Op>
+__device__ T block_reduce(T v, T *sh, Op op) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int o = 32; o > 0; o >>= 1) v = op(v, __shfl_xor(v, o));
+    __syncthreads();
+    if (lane == 0) sh[wid] = v;
+    __syncthreads();
+    T r = sh[0];
+    for (int k = 1; k < nw; ++k) r = op(r, sh[k]);
+    __syncthreads();
+    return r;
+}
+
+struct MaxOp { template <class T> __device__ T operator()(T a, T b) const { return a > b ? a : b; } };
+struct MinOp { template <class T> __device__ T operator()(T a, T b) const { return a < b ? a : b; } };
+struct AddOp { template <class T> __device__ T operator()(T a, T b) const { return a + b; } };
+
+__device__ __forceinline__ double2 cell_w(const GridC &g, int p) {
+    int y = p / g.W, x = p - y * g.W;
+    return make_double2((double)cell_world(g.ox, x, g.res), (double)cell_world(g.oy, y, g.res));
+}
+
+// one workgroup per cluster
+__global__ __launch_bounds__(256) void k_cluster_stats(StatArgs A) {
+    __shared__ long long shl[8];
+    __shared__ int shi[8];
+    __shared__ double shd[8];
+    __shared__ int cand[2048];
+    __shared__ int ncand;
+    const int cid = blockIdx.x;
+    const int b = A.off[cid], e = A.off[cid + 1], n = e - b;
+    const GridC &g = A.g;
+    long long sx = 0, sy = 0;
+    int mnx = INT_MAX, mxx = INT_MIN, mny = INT_MAX, mxy = INT_MIN;
+    for (int k = b + threadIdx.x; k < e; k += blockDim.x) {
+        int p = A.cells[k], y = p / g.W, x = p - y * g.W;
+        sx += x; sy += y;
+        mnx = min(mnx, x); mxx = max(mxx, x); mny = min(mny, y); mxy = max(mxy, y);
+    }
+    sx = block_reduce(sx, shl, AddOp());
+    sy = block_reduce(sy, shl, AddOp());
+    mnx = block_reduce(mnx, shi, MinOp()); mxx = block_reduce(mxx, shi, MaxOp());
+    mny = block_reduce(mny, shi, MinOp()); mxy = block_reduce(mxy, shi, MaxOp());
+    // ---- max pairwise squared distance (cluster.length, seed_gen:1063-1073), pruned exactly:
+    // LB = d^2 between the cells of extreme x / extreme y; a cell can belong to a farther pair only
+    // if its distance to the farthest bbox corner reaches LB.
+    int ax = INT_MAX, bx_ = INT_MAX, ay = INT_MAX, by_ = INT_MAX;  // pixel ids with min/max x, min/max y
+    for (int k = b + threadIdx.x; k < e; k += blockDim.x) {
+        int p = A.cells[k], y = p / g.W, x = p - y * g.W;
+        if (x == mnx) ax = min(ax, p);
+        if (x == mxx) bx_ = min(bx_, p);
+        if (y == mny) ay = min(ay, p);
+        if (y == mxy) by_ = min(by_, p);
+    }
+    ax = block_reduce(ax, shi, MinOp()); bx_ = block_reduce(bx_, shi, MinOp());
+    ay = block_reduce(ay, shi, MinOp()); by_ = block_reduce(by_, shi, MinOp());
+    auto d2p = [&](int p, int q) {
+        int py = p / g.W, px = p - py * g.W, qy = q / g.W, qx = q - qy * g.W;
+        int dx = px - qx, dy = py - qy;
+        return dx * dx + dy * dy;
+    };
+    const int LB = max(d2p(ax, bx_), d2p(ay, by_));
+    if (threadIdx.x == 0) ncand = 0;
+    __syncthreads();
+    for (int k = b + threadIdx.x; k < e; k += blockDim.x) {
+        int p = A.cells[k], y = p / g.W, x = p - y * g.W;
+        int dxm = max(x - mnx, mxx - x), dym = max(y - mny, mxy - y);
+        if (dxm * dxm + dym * dym >= LB) {
+            int s = atomicAdd(&ncand, 1);
+            if (s < 2048) cand[s] = p;
+        }
+    }
+    __syncthreads();
+    int maxd2 = LB;
+    const int nc = ncand;
+    if (nc <= 2048) {
+        const long long pairs = (long long)nc * nc;
+        for (long long t = threadIdx.x; t < pairs; t += blockDim.x) {
+            int i = (int)(t / nc), j = (int)(t - (long long)i * nc);
+            if (j > i) maxd2 = max(maxd2, d2p(cand[i], cand[j]));
+        }
+    } else {  // too many candidates: exact brute force over all pairs
+        for (int i = b; i < e; ++i)
+            for (int k = i + 1 + threadIdx.x; k < e; k += blockDim.x) maxd2 = max(maxd2, d2p(A.cells[i], A.cells[k]));
+    }
+    maxd2 = block_reduce(maxd2, shi, MaxOp());
+
+    ClusterRec r{};
+    r.sx = sx; r.sy = sy; r.n = n; r.maxd2 = maxd2;
+    r.flags = 0;
+    const bool exact_sums = sx <= (1ll << 24) && sy <= (1ll << 24);
+    r.cx = (float)sx / (float)n;       // sum_x / cells.size() (float / float)
+    r.cy = (float)sy / (float)n;
+    r.length = (float)(sqrt((double)maxd2) * (double)g.res);
+    bool needs_bfs = !exact_sums;
+    bool row = false;
+    if (r.length >= A.min_length) {
+        float cwx = (float)(g.ox + (double)(r.cx * g.res)), cwy = (float)(g.oy + (double)(r.cy * g.res));
+        r.center = make_double2(cwx, cwy);
+        row = d_pip(cwx, cwy, A.poly, A.np);
+    }
+    if (row && !needs_bfs) {
+        // first endpoint: first cell with strictly maximal |wp - centre|^2 (seed_gen:1354-1367)
+        double m1 = 0.0;
+        for (int k = b + threadIdx.x; k < e; k += blockDim.x) {
+            double2 w = cell_w(g, A.cells[k]);
+            double dx = w.x - r.center.x, dy = w.y - r.center.y;
+            m1 = fmax(m1, dx * dx + dy * dy);
+        }
+        m1 = block_reduce(m1, shd, MaxOp());
+        int cnt = 0, arg = INT_MAX;
+        for (int k = b + threadIdx.x; k < e; k += blockDim.x) {
+            double2 w = cell_w(g, A.cells[k]);
+            double dx = w.x - r.center.x, dy = w.y - r.center.y;
+            if (dx * dx + dy * dy == m1 && m1 > 0.0) { ++cnt; arg = min(arg, A.cells[k]); }
+        }
+        cnt = block_reduce(cnt, shi, AddOp());
+        arg = block_reduce(arg, shi, MinOp());
+        if (cnt != 1) needs_bfs = true;
+        if (!needs_bfs) {
+            const double2 wf = cell_w(g, arg);
+            double fdx = wf.x - r.center.x, fdy = wf.y - r.center.y;
+            double z = fdx * fdx + fdy * fdy, s = sqrt(z);
+            const double fx = fdx / s, fy = fdy / s;  // first_direction = diff.normalized()
+            // second endpoint: dot(normalized(diff), first_dir) < 0, strictly maximal (seed_gen:1369-1385)
+            double m2 = 0.0;
+            for (int k = b + threadIdx.x; k < e; k += blockDim.x) {
+                int p = A.cells[k];
+                if (p == arg) continue;
+                double2 w = cell_w(g, p);
+                double dx = w.x - r.center.x, dy = w.y - r.center.y, d2 = dx * dx + dy * dy;
+                double nx = dx, ny = dy;
+                if (d2 > 0.0) { double q = sqrt(d2); nx = dx / q; ny = dy / q; }
+                if (nx * fx + ny * fy < 0.0) m2 = fmax(m2, d2);
+            }
+            m2 = block_reduce(m2, shd, MaxOp());
+            int cnt2 = 0, arg2 = INT_MAX;
+            bool fallback = !(m2 > 0.0);
+            for (int k = b + threadIdx.x; k < e; k += blockDim.x) {
+                int p = A.cells[k];
+                if (p == arg) continue;
+                double2 w = cell_w(g, p);
+                if (!fallback) {
+                    double dx = w.x - r.center.x, dy = w.y - r.center.y, d2 = dx * dx + dy * dy;
+                    double nx = dx, ny = dy;
+                    if (d2 > 0.0) { double q = sqrt(d2); nx = dx / q; ny = dy / q; }
+                    if (nx * fx + ny * fy < 0.0 && d2 == m2) { ++cnt2; arg2 = min(arg2, p); }
+                }
+            }
+            if (fallback) {  // farthest from the first endpoint (seed_gen:1387-1399)
+                double m3 = 0.0;
+                for (int k = b + threadIdx.x; k < e; k += blockDim.x) {
+                    int p = A.cells[k];
+                    if (p == arg) continue;
+                    double2 w = cell_w(g, p);
+                    double dx = w.x - wf.x, dy = w.y - wf.y;
+                    m3 = fmax(m3, dx * dx + dy * dy);
+                }
+                m3 = block_reduce(m3, shd, MaxOp());
+                for (int k = b + threadIdx.x; k < e; k += blockDim.x) {
+                    int p = A.cells[k];
+                    if (p == arg) continue;
+                    double2 w = cell_w(g, p);
+                    double dx = w.x - wf.x, dy = w.y - wf.y;
+                    if (dx * dx + dy * dy == m3 && m3 > 0.0) { ++cnt2; arg2 = min(arg2, p); }
+                }
+            }
+            cnt2 = block_reduce(cnt2, shi, AddOp());
+            arg2 = block_reduce(arg2, shi, MinOp());
+            if (cnt2 != 1) needs_bfs = true;  // (fallback with max 0 keeps index 0 -> BFS replay)
+            r.start = wf;
+            if (!needs_bfs) r.end = cell_w(g, arg2);
+        }
+    }
+    r.flags = (row ? 1 : 0) | (needs_bfs ? 2 : 0);
+    if (threadIdx.x == 0) A.rec[cid] = r;
+}
+
+// Exact replay of clusterOccupiedCells' FIFO BFS (seed_gen:1007-1049) for clusters without the
+// order-free certificate: one thread per flagged cluster (rare).
+__global__ void k_cluster_bfs(StatArgs A, const uint64_t *fg, const int *fg_off, const int *parent, int *queue,
+                              int *visited, int stamp_base) {
+    const int cid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (cid >= A.n_clusters) return;
+    ClusterRec r = A.rec[cid];
+    if (!(r.flags & 2)) return;
+    const GridC &g = A.g;
+    const int b = A.off[cid], n = A.off[cid + 1] - b;
+    int *q = queue + b;
+    // start cell = first raster cell of the component = the root's pixel
+    int root = parent[fg_index(fg, fg_off, g, A.cells[b] % g.W, A.cells[b] / g.W)];
+    int start = A.list[root];
+    const int stamp = stamp_base + cid;
+    visited[root] = stamp;
+    q[0] = start;
+    int head = 0, tail = 1;
+    const int dxs[8] = {-1, -1, -1, 0, 0, 1, 1, 1}, dys[8] = {-1, 0, 1, -1, 1, -1, 0, 1};
+    while (head < tail) {
+        int p = q[head++], cy = p / g.W, cx = p - cy * g.W;
+        for (int i = 0; i < 8; ++i) {
+            int j = fg_index(fg, fg_off, g, cx + dxs[i], cy + dys[i]);
+            if (j < 0 || visited[j] == stamp) continue;
+            visited[j] = stamp;
+            q[tail++] = A.list[j];
+        }
+    }
+    float sum_x = 0.0f, sum_y = 0.0f;
+    for (int k = 0; k < n; ++k) { int p = q[k], y = p / g.W; sum_x += (float)(p - y * g.W); sum_y += (float)y; }
+    r.cx = sum_x / (float)n;
+    r.cy = sum_y / (float)n;
+    bool row = false;
+    if (r.length >= A.min_length) {
+        float cwx = (float)(g.ox + (double)(r.cx * g.res)), cwy = (float)(g.oy + (double)(r.cy * g.res));
+        r.center = make_double2(cwx, cwy);
+        row = d_pip(cwx, cwy, A.poly, A.np);
+    }
+    if (row) {
+        double mx = 0.0; int fi = 0; double fx = 0, fy = 0;
+        for (int k = 0; k < n; ++k) {
+            double2 w = cell_w(g, q[k]);
+            double dx = w.x - r.center.x, dy = w.y - r.center.y, d2 = dx * dx + dy * dy;
+            if (d2 > mx) { mx = d2; fi = k; double s = sqrt(d2); fx = dx / s; fy = dy / s; }
+        }
+        double mo = 0.0; int si = 0;
+        for (int k = 0; k < n; ++k) {
+            if (k == fi) continue;
+            double2 w = cell_w(g, q[k]);
+            double dx = w.x - r.center.x, dy = w.y - r.center.y, d2 = dx * dx + dy * dy;
+            double nx = dx, ny = dy;
+            if (d2 > 0.0) { double s = sqrt(d2); nx = dx / s; ny = dy / s; }
+            if (nx * fx + ny * fy < 0.0 && d2 > mo) { mo = d2; si = k; }
+        }
+        if (mo == 0.0) {
+            double2 wf = cell_w(g, q[fi]);
+            for (int k = 0; k < n; ++k) {
+                if (k == fi) continue;
+                double2 w = cell_w(g, q[k]);
+                double dx = w.x - wf.x, dy = w.y - wf.y, d2 = dx * dx + dy * dy;
+                if (d2 > mo) { mo = d2; si = k; }
+            }
+        }
+        r.start = cell_w(g, q[fi]);
+        r.end = cell_w(g, q[si]);
+    }
+    r.flags = (row ? 1 : 0) | 4;  // 4: replayed
+    A.rec[cid] = r;
+}
+
+// ------------------------------------------------------------------ rays
+struct RowDev { double sx, sy, ex, ey; int k; int slot0; };
+
+// raycastToOccupiedCell seed_gen:1730-1771 on the frameless skeleton
+__device__ bool d_raycast(const uint64_t *skel, const GridC &g, double sx, double sy, double dx, double dy, double maxd,
+                          double &hx, double &hy) {
+    const double step = (double)g.res * 0.5;
+    const int max_steps = (int)(maxd / step);
+    double cx = sx, cy = sy;
+    for (int i = 0; i < max_steps; ++i) {
+        cx += dx * step;
+        cy += dy * step;
+        double ddx = cx - sx, ddy = cy - sy;
+        double dist = sqrt(ddx * ddx + ddy * ddy);
+        if (dist < 1.0) continue;
+        float fx = (float)cx, fy = (float)cy;
+        float rel_x = (float)(((double)fx - g.ox) / (double)g.res);
+        float rel_y = (float)(((double)fy - g.oy) / (double)g.res);
+        int gx = (int)floorf(rel_x), gy = (int)floorf(rel_y);
+        gx = gx < 0 ? 0 : (gx >= g.W ? g.W - 1 : gx);
+        gy = gy < 0 ? 0 : (gy >= g.H ? g.H - 1 : gy);
+        if (bit_at(skel, g.WW, gx, gy)) { hx = cx; hy = cy; return true; }
+    }
+    return false;
+}
+
+// virtual-seed candidates of generateVirtualSeeds (seed_gen:2008-2263): per base seed i of a row,
+// slot 3*(i-1) + {0: base, 1: perp_dir1 ray seed, 2: perp_dir2 ray seed}
+__global__ void k_virtual_candidates(const RowDev *rows, int n_rows, int n_slots, const uint64_t *skel, GridC g,
+                                     const double *poly, int np, double2 *cand, int *ok) {
+    int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n_slots) return;
+    int lo = 0, hi = n_rows - 1;  // row whose slot range contains s
+    while (lo < hi) { int mid = (lo + hi + 1) >> 1; if (rows[mid].slot0 <= s) lo = mid; else hi = mid - 1; }
+    const RowDev R = rows[lo];
+    const int local = s - R.slot0, i = local / 3 + 1, type = local - (i - 1) * 3;
+    double dx = R.ex - R.sx, dy = R.ey - R.sy;
+    double nrm = sqrt(dx * dx + dy * dy);
+    double rdx = dx / nrm, rdy = dy / nrm;
+    double t = (double)i / (R.k + 1);
+    double bx = R.sx + t * dx, by = R.sy + t * dy;
+    if (type == 0) { cand[s] = make_double2(bx, by); ok[s] = 1; return; }
+    double pdx = type == 1 ? -rdy : rdy, pdy = type == 1 ? rdx : -rdx;
+    const double maxd = 4.0;
+    double hx, hy, sx_, sy_;
+    if (d_raycast(skel, g, bx, by, pdx, pdy, maxd, hx, hy)) { sx_ = hx; sy_ = hy; }
+    else { sx_ = bx + pdx * maxd; sy_ = by + pdy * maxd; }
+    cand[s] = make_double2(sx_, sy_);
+    ok[s] = d_pip(sx_, sy_, poly, np) ? 0 : 1;
+}
+
+struct RayAngles { double cs[3], sn[3]; int pos_branch[3]; };  // 0, -90, +90 degrees
+
+// castRayFromEndpoint seed_gen:1774-1891 + the filters of generateRayPointsFromEndpoints :1941-1961
+__global__ void k_endpoint_rays(const RowDev *rows, int n_rows, const uint64_t *skel, GridC g, RayAngles ang,
+                                const double *poly, int np, double2 *cand, int *ok) {
+    int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n_rows * 6) return;
+    const RowDev R = rows[s / 6];
+    const int k = s % 6, a = k % 3;
+    double stx = k < 3 ? R.sx : R.ex, sty = k < 3 ? R.sy : R.ey;
+    double otx = k < 3 ? R.ex : R.sx, oty = k < 3 ? R.ey : R.sy;
+    double ex = otx - stx, ey = oty - sty;
+    double dist = sqrt(ex * ex + ey * ey);
+    if (dist < 1e-6) { ex = 1.0; ey = 0.0; }
+    else { ex = ex / dist; ey = ey / dist; }
+    double ox_ = -ex, oy_ = -ey, px = -ey, py = ex;
+    double rx, ry;
+    if (ang.pos_branch[a]) { rx = ang.cs[a] * ox_ + ang.sn[a] * px; ry = ang.cs[a] * oy_ + ang.sn[a] * py; }
+    else { rx = ang.cs[a] * ox_ + ang.sn[a] * (-px); ry = ang.cs[a] * oy_ + ang.sn[a] * (-py); }
+    { double z = rx * rx + ry * ry; if (z > 0.0) { double q = sqrt(z); rx = rx / q; ry = ry / q; } }
+    double cur = 1.0;
+    double resx = 0, resy = 0;
+    bool done = false;
+    while (cur <= g.amax) {
+        double cx = stx + rx * cur, cy = sty + ry * cur;
+        if (!(cx >= g.minx && cx <= g.maxx && cy >= g.miny && cy <= g.maxy)) {
+            resx = fmax(g.minx, fmin(g.maxx, cx)); resy = fmax(g.miny, fmin(g.maxy, cy));
+            done = true;
+            break;
+        }
+        int mx = (int)((cx - g.ox) / (double)g.res), my = (int)((cy - g.oy) / (double)g.res);
+        if (mx >= 0 && mx < g.W && my >= 0 && my < g.H && bit_at(skel, g.WW, mx, my)) {
+            resx = cx; resy = cy; done = true;
+            break;
+        }
+        cur += 0.1;
+    }
+    if (!done) {
+        double fx = stx + rx * g.amax, fy = sty + ry * g.amax;
+        if (!(fx >= g.minx && fx <= g.maxx && fy >= g.miny && fy <= g.maxy)) {
+            fx = fmax(g.minx, fmin(g.maxx, fx)); fy = fmax(g.miny, fmin(g.maxy, fy));
+        }
+        resx = fx; resy = fy;
+    }
+    int good = isfinite(resx) && isfinite(resy) && resx >= g.minx && resx <= g.maxx && resy >= g.miny && resy <= g.maxy &&
+               !d_pip(resx, resy, poly, np);
+    cand[s] = make_double2(resx, resy);
+    ok[s] = good;
+}
+
+__global__ void k_endpoint_candidates(const RowDev *rows, int n_rows, double2 *cand, int *ok) {
+    int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= 2 * n_rows) return;
+    const RowDev R = rows[s >> 1];
+    cand[s] = (s & 1) ? make_double2(R.ex, R.ey) : make_double2(R.sx, R.sy);
+    ok[s] = 1;
+}
+
+// ------------------------------------------------------------------ host orchestration
+template <class T> static T *dev(DevBuf &b, size_t n) { return static_cast<T *>(b.ensure(sizeof(T) * std::max<size_t>(n, 1))); }
+
+void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStageOut &out, hipStream_t s, hipEvent_t ev_mid) {
+    const FrameGeom &fg = *in.g;
+    GridC g{};
+    g.ox = fg.origin_x; g.oy = fg.origin_y; g.res = fg.res; g.W = fg.W; g.H = fg.H; g.WW = fg.WW;
+    {   // bounds exactly as the reference forms them (uint32 * float -> float, then double add)
+        const uint32_t W = (uint32_t)fg.W, H = (uint32_t)fg.H;
+        const float res = fg.res;
+        g.minx = fg.origin_x; g.maxx = g.minx + W * res;
+        g.miny = fg.origin_y; g.maxy = g.miny + H * res;
+        double gw = W * res, gh = H * res;
+        g.amax = std::sqrt(gw * gw + gh * gh) * 3.0;
+    }
+    const Poly &poly = *in.poly;
+    const int np = (int)poly.size();
+    double *d_poly = dev<double>(S.poly, 2 * np);
+    std::vector<double> hp(2 * np);
+    for (int i = 0; i < np; ++i) { hp[2 * i] = poly[i].first; hp[2 * i + 1] = poly[i].second; }
+    AOS_HIP(hipMemcpyAsync(d_poly, hp.data(), sizeof(double) * 2 * np, hipMemcpyHostToDevice, s));
+    int *h_sc = static_cast<int *>(S.h_misc.ensure(4096));
+
+    // ---- foreground list (raster order)
+    const size_t Cw = (size_t)g.WW * g.H;
+    uint64_t *d_fg = dev<uint64_t>(S.fg_bits, Cw);
+    int *d_wc = dev<int>(S.word_cnt, Cw + 1), *d_wo = dev<int>(S.word_off, Cw + 1);
+    AOS_HIP(hipMemsetAsync(d_wc + Cw, 0, sizeof(int), s));
+    dim3 gw2(cdiv(g.WW, 64), g.H);
+    k_fg<<<gw2, 64, 0, s>>>(in.skel_bits, d_fg, d_wc, g, d_poly, np);
+    size_t tb = 0;
+    hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (int *)nullptr, (int *)nullptr, (int)Cw + 1, s);
+    void *tmp = S.scan_tmp.ensure(tb);
+    AOS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, d_wc, d_wo, (int)Cw + 1, s));
+    AOS_HIP(hipMemcpyAsync(h_sc, d_wo + Cw, sizeof(int), hipMemcpyDeviceToHost, s));
+    AOS_HIP(hipStreamSynchronize(s));
+    const int nf = h_sc[0];
+    S.n_fg = nf;
+    out = SeedStageOut();
+    S.n_clusters = 0;
+    S.h_rec.clear();
+    std::vector<RowDev> rows;
+    if (nf > 0) {
+        int *d_list = dev<int>(S.fg_list, nf);
+        k_fg_list<<<gw2, 64, 0, s>>>(d_fg, d_wo, d_list, g);
+        int *d_par = dev<int>(S.parent, nf), *d_isroot = dev<int>(S.root_flag, nf + 1), *d_rank = dev<int>(S.root_rank, nf + 1);
+        k_ccl_init<<<cdiv(nf, 256), 256, 0, s>>>(d_par, nf);
+        k_ccl_union<<<cdiv(nf, 256), 256, 0, s>>>(d_list, nf, d_fg, d_wo, g, d_par);
+        AOS_HIP(hipMemsetAsync(d_isroot + nf, 0, sizeof(int), s));
+        k_ccl_flatten<<<cdiv(nf, 256), 256, 0, s>>>(d_par, d_isroot, nf);
+        size_t tb2 = 0;
+        hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, (int *)nullptr, (int *)nullptr, nf + 1, s);
+        tmp = S.scan_tmp.ensure(std::max(tb, tb2));
+        AOS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, d_isroot, d_rank, nf + 1, s));
+        AOS_HIP(hipMemcpyAsync(h_sc, d_rank + nf, sizeof(int), hipMemcpyDeviceToHost, s));
+        AOS_HIP(hipStreamSynchronize(s));
+        const int ncl = h_sc[0];
+        S.n_clusters = ncl;
+        int *d_cnt = dev<int>(S.cl_count, ncl + 1), *d_off = dev<int>(S.cl_off, ncl + 1);
+        int *d_cid = dev<int>(S.cl_cursor, 2 * (size_t)nf), *d_slot = d_cid + nf;
+        int *d_cells = dev<int>(S.cl_cells, nf);
+        AOS_HIP(hipMemsetAsync(d_cnt, 0, sizeof(int) * (ncl + 1), s));
+        k_cluster_count<<<cdiv(nf, 256), 256, 0, s>>>(d_par, d_rank, nf, d_cid, d_cnt, d_slot);
+        size_t tb3 = 0;
+        hipcub::DeviceScan::ExclusiveSum(nullptr, tb3, (int *)nullptr, (int *)nullptr, ncl + 1, s);
+        tmp = S.scan_tmp.ensure(std::max(std::max(tb, tb2), tb3));
+        AOS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb3, d_cnt, d_off, ncl + 1, s));
+        k_cluster_scatter<<<cdiv(nf, 256), 256, 0, s>>>(d_list, d_cid, d_slot, d_off, nf, d_cells);
+        ClusterRec *d_rec = dev<ClusterRec>(S.rec, ncl);
+        StatArgs A{d_off, d_cells, d_list, ncl, g, d_poly, np, static_cast<float>(in.cluster_min_length), d_rec};
+        k_cluster_stats<<<ncl, 256, 0, s>>>(A);
+        S.h_rec.resize(ncl);
+        AOS_HIP(hipMemcpyAsync(S.h_rec.data(), d_rec, sizeof(ClusterRec) * ncl, hipMemcpyDeviceToHost, s));
+        AOS_HIP(hipStreamSynchronize(s));
+        bool any_bfs = false;
+        for (const auto &r : S.h_rec) any_bfs |= (r.flags & 2) != 0;
+        if (any_bfs) {
+            int *d_q = dev<int>(S.bfs_queue, nf), *d_vis = dev<int>(S.bfs_vis, nf);
+            AOS_HIP(hipMemsetAsync(d_vis, 0xFF, sizeof(int) * nf, s));
+            k_cluster_bfs<<<cdiv(ncl, 64), 64, 0, s>>>(A, d_fg, d_wo, d_par, d_q, d_vis, 0);
+            AOS_HIP(hipMemcpyAsync(S.h_rec.data(), d_rec, sizeof(ClusterRec) * ncl, hipMemcpyDeviceToHost, s));
+            AOS_HIP(hipStreamSynchronize(s));
+        }
+        // ---- tree rows in cluster order (convertClustersToTreeRows, seed_gen:1329-1406)
+        int slot = 0;
+        for (const auto &r : S.h_rec) {
+            if (!(r.flags & 1)) continue;
+            out.row_center.push_back(r.center.x); out.row_center.push_back(r.center.y);
+            out.row_start.push_back(r.start.x); out.row_start.push_back(r.start.y);
+            out.row_end.push_back(r.end.x); out.row_end.push_back(r.end.y);
+            out.row_length.push_back((double)r.length);
+            RowDev d{r.start.x, r.start.y, r.end.x, r.end.y, 0, slot};
+            double dx = r.end.x - r.start.x, dy = r.end.y - r.start.y;
+            double dist = std::sqrt(dx * dx + dy * dy);
+            if (!(dist < 1.0) && !(std::sqrt(dx * dx + dy * dy) < 1e-6)) d.k = static_cast<int>(std::floor(dist / 1.0));
+            slot += 3 * d.k;
+            rows.push_back(d);
+        }
+    }
+    out.n_clusters_all = S.n_clusters;
+    S.n_rows = (int)rows.size();
+    if (ev_mid) AOS_HIP(hipEventRecord(ev_mid, s));
+
+    // cluster_info (publishClusterInfo :1515-1565) and rows_info (:2546-2582): std::sort on the
+    // host with the reference comparators (same libstdc++ algorithm => same order on ties).
+    {
+        struct CI { size_t index; float cx, cy; };
+        std::vector<CI> infos;
+        for (size_t i = 0; i < S.n_rows; ++i)
+            infos.push_back({i, (float)out.row_center[2 * i], (float)out.row_center[2 * i + 1]});
+        std::sort(infos.begin(), infos.end(), [](const CI &a, const CI &b) { return a.cy < b.cy; });
+        for (const auto &ci : infos) { out.cluster_info.push_back(ci.cx); out.cluster_info.push_back(ci.cy); }
+        struct TR { double cx, cy, sx, sy, ex, ey; };
+        std::vector<TR> tr;
+        for (int i = 0; i < S.n_rows; ++i)
+            tr.push_back({out.row_center[2 * i], out.row_center[2 * i + 1], out.row_start[2 * i], out.row_start[2 * i + 1],
+                          out.row_end[2 * i], out.row_end[2 * i + 1]});
+        std::sort(tr.begin(), tr.end(), [](const TR &a, const TR &b) {
+            if (std::abs(a.cy - b.cy) < 1e-6) return a.cx < b.cx;
+            return a.cy < b.cy;
+        });
+        for (const auto &t : tr) { out.rows_info.insert(out.rows_info.end(), {t.sx, t.sy, t.ex, t.ey}); }
+    }
+    if (rows.empty()) return;
+
+    // ---- seeds
+    DedupScratch &scr = S.dedup;
+    const int nr = (int)rows.size();
+    RowDev *d_rows = dev<RowDev>(S.row_idx, nr);
+    AOS_HIP(hipMemcpyAsync(d_rows, rows.data(), sizeof(RowDev) * nr, hipMemcpyHostToDevice, s));
+    const int nslots = rows.back().slot0 + 3 * rows.back().k;
+    const int ncand = std::max(nslots, 6 * nr);
+    double2 *d_cand = dev<double2>(S.cand_xy, ncand);
+    int *d_ok = dev<int>(S.cand_ok, ncand);
+    double2 *d_seeds = dev<double2>(S.seed_out, (size_t)nslots + 8 * nr);
+    const HashG h = make_hash(g.minx - 50.0, g.maxx + 50.0, g.miny - 50.0, g.maxy + 50.0, 0.5);
+    int n_virtual = 0, n_ray = 0, n_end = 0;
+    if (nslots > 0) {
+        k_virtual_candidates<<<cdiv(nslots, 128), 128, 0, s>>>(d_rows, nr, nslots, in.skel_bits, g, d_poly, np, d_cand, d_ok);
+        n_virtual = greedy_dedup(scr, d_cand, d_ok, nslots, kConflictLess, 0.5, h, d_seeds, nullptr, s, h_sc);
+    }
+    RayAngles ang{};
+    const double degs[3] = {0.0, -90.0, 90.0};
+    for (int a = 0; a < 3; ++a) {  // seed_gen:1796-1803, evaluated with the host libm
+        double rad = degs[a] * M_PI / 180.0;
+        if (degs[a] > 0) { ang.cs[a] = std::cos(rad); ang.sn[a] = std::sin(rad); ang.pos_branch[a] = 1; }
+        else { ang.cs[a] = std::cos(-rad); ang.sn[a] = std::sin(-rad); ang.pos_branch[a] = 0; }
+    }
+    k_endpoint_rays<<<cdiv(6 * nr, 64), 64, 0, s>>>(d_rows, nr, in.skel_bits, g, ang, d_poly, np, d_cand, d_ok);
+    n_ray = greedy_dedup(scr, d_cand, d_ok, 6 * nr, kConflictLess, 0.5, h, d_seeds + n_virtual, nullptr, s, h_sc);
+    k_endpoint_candidates<<<cdiv(2 * nr, 64), 64, 0, s>>>(d_rows, nr, d_cand, d_ok);
+    n_end = greedy_dedup(scr, d_cand, d_ok, 2 * nr, kConflictLess, 0.5, h, d_seeds + n_virtual + n_ray, nullptr, s, h_sc);
+    const int ntot = n_virtual + n_ray + n_end;
+    std::vector<double> all(2 * (size_t)ntot);
+    if (ntot) AOS_HIP(hipMemcpyAsync(all.data(), d_seeds, sizeof(double2) * ntot, hipMemcpyDeviceToHost, s));
+    AOS_HIP(hipStreamSynchronize(s));
+    out.virtual_xy.assign(all.begin(), all.begin() + 2 * n_virtual);
+    out.ray_xy.assign(all.begin() + 2 * n_virtual, all.begin() + 2 * (n_virtual + n_ray));
+    out.endpoint_xy.assign(all.begin() + 2 * (n_virtual + n_ray), all.end());
+    out.d_voronoi = reinterpret_cast<const double *>(d_seeds);
+    out.n_voronoi = ntot;
+}
+
+}  // namespace aos

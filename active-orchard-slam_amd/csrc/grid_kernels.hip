@@ -1,0 +1,400 @@
+// Grid-stage kernels of the seed-gen hot path for gfx950 (MI355X).
+//
+// Numerics: built with -ffp-contract=off and correctly rounded f32/f64 div/sqrt, so every
+// float/double expression below rounds exactly like the reference's x86-64 build
+// (CMakeLists.txt:12: no -march, no FMA). Each kernel cites the reference lines it implements.
+//
+// Layout in HBM: occupancy-type grids are bit-packed, one uint64 word = 64 consecutive cells of
+// a row (bit i = cell x = 64*c + i), WW = ceil(W/64) words per row, padding bits zero. Byte grids
+// (int8 {0,100}) exist only for the published OccupancyGrid outputs.
+#include <hipcub/hipcub.hpp>
+
+#include "aos_internal.h"
+
+namespace aos {
+
+// Exclusion discs of processPointCloud (seed_gen:487-499): x, y, radius.
+__constant__ float c_excl[11 * 3] = {0.646417f, 3.83918f, 1.0f,  2.0405f, 3.62485f, 1.0f,  65.3711f, 2.09755f, 1.0f,
+                                     66.9094f, 2.07515f, 1.0f,  -1.61309f, 5.69933f, 1.0f, -1.97349f, 4.77329f, 1.0f,
+                                     -2.11365f, 3.74464f, 1.0f, -2.26381f, 2.70848f, 1.0f, -2.66426f, 1.72738f, 1.0f,
+                                     68.0229f, 2.31687f, 1.0f,  65.4647f, 2.18653f, 1.0f};
+
+static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+__device__ __forceinline__ void load_xyz(const RorLaunch &L, uint64_t i, float &x, float &y, float &z) {
+    const uint8_t *rec = L.cloud + i * (uint64_t)L.step;
+    if (L.step == 16 && L.ox == 0 && L.oy == 4 && L.oz == 8) {
+        float4 v = *reinterpret_cast<const float4 *>(rec);
+        x = v.x; y = v.y; z = v.z;
+    } else {
+        x = *reinterpret_cast<const float *>(rec + L.ox);
+        y = *reinterpret_cast<const float *>(rec + L.oy);
+        z = *reinterpret_cast<const float *>(rec + L.oz);
+    }
+}
+
+__device__ __forceinline__ bool binned(const RorLaunch &L, float x, float y, float z) {
+    return isfinite(x) && isfinite(y) && isfinite(z) && x >= L.bminx && x <= L.bmaxx && y >= L.bminy &&
+           y <= L.bmaxy && z >= L.bminz && z <= L.bmaxz;
+}
+
+__device__ __forceinline__ int bin_of(const RorLaunch &L, float x, float y, int &bx, int &by) {
+    bx = min(max((int)((x - L.bminx) * L.inv_cs), 0), L.nbx - 1);
+    by = min(max((int)((y - L.bminy) * L.inv_cs), 0), L.nby - 1);
+    return by * L.nbx + bx;
+}
+
+// PassThrough z, x, y (inclusive; PCL 1.12 drops non-finite) + exclusion discs, seed_gen:459-525.
+__device__ __forceinline__ bool candidate(const RorLaunch &L, float x, float y, float z) {
+    if (z < L.cminz || z > L.cmaxz) return false;
+    if (x < L.cminx || x > L.cmaxx) return false;
+    if (y < L.cminy || y > L.cmaxy) return false;
+#pragma unroll
+    for (int e = 0; e < 11; ++e) {
+        float dx = x - c_excl[3 * e], dy = y - c_excl[3 * e + 1];
+        float dist_sq = dx * dx + dy * dy;
+        float rr = c_excl[3 * e + 2] * c_excl[3 * e + 2];
+        if (dist_sq <= rr) return false;
+    }
+    return true;
+}
+
+// ------------------------------------------------------------------------------------------
+// a1 RadiusOutlierRemoval (seed_gen:236-242) restricted to the points that can reach the grid.
+// Only points inside the clip box can be rasterised; their neighbours lie within r of that box,
+// so only that expanded box is binned (2-D columns of >= r, z checked exactly).
+__global__ void k_ror_bin(RorLaunch L, int *bin_count, int2 *pt_binslot) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= L.n) return;
+    float x, y, z;
+    load_xyz(L, i, x, y, z);
+    int2 bs = make_int2(-1, 0);
+    if (binned(L, x, y, z)) {
+        int bx, by;
+        int b = bin_of(L, x, y, bx, by);
+        bs = make_int2(b, atomicAdd(&bin_count[b], 1));
+    }
+    pt_binslot[i] = bs;
+}
+
+__global__ void k_ror_scatter(RorLaunch L, const int *bin_start, const int2 *pt_binslot, float4 *sorted) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= L.n) return;
+    int2 bs = pt_binslot[i];
+    if (bs.x < 0) return;
+    float x, y, z;
+    load_xyz(L, i, x, y, z);
+    int cand = candidate(L, x, y, z) ? 1 : 0;
+    sorted[bin_start[bs.x] + bs.y] = make_float4(x, y, z, __int_as_float(cand));
+}
+
+// Neighbour count with PCL semantics (FLANN L2_Simple: ((dx*dx)+dy*dy)+dz*dz in float):
+//   dense: kNN k = need, keep iff need points have (double)d2 <= r^2;
+//   !dense: radius search d2 < float(r^2), keep iff count >= need.
+// Kept candidates mark their cell (generateOccupancyGrid seed_gen:606-619: double divide, trunc).
+__global__ void k_ror_raster(RorLaunch L, const int *bin_start, const float4 *sorted, const int *d_n_binned, uint8_t *raster,
+                             unsigned long long *counters) {
+    int s = blockIdx.x * blockDim.x + threadIdx.x;
+    const int n_binned = *d_n_binned;
+    bool cand = false, kept = false;
+    if (s < n_binned) {
+        float4 p = sorted[s];
+        cand = __float_as_int(p.w) != 0;
+        if (cand) {
+            int bx, by;
+            bin_of(L, p.x, p.y, bx, by);
+            int cnt = 0;
+            for (int yy = max(by - 1, 0); yy <= min(by + 1, L.nby - 1) && cnt < L.need; ++yy) {
+                int b0 = yy * L.nbx + max(bx - 1, 0), b1 = yy * L.nbx + min(bx + 1, L.nbx - 1);
+                int k0 = bin_start[b0], k1 = bin_start[b1 + 1];
+                for (int k = k0; k < k1; ++k) {
+                    float4 q = sorted[k];
+                    float dx = p.x - q.x, dy = p.y - q.y, dz = p.z - q.z;
+                    float d2 = dx * dx;
+                    d2 = d2 + dy * dy;
+                    d2 = d2 + dz * dz;
+                    bool in = L.is_dense ? ((double)d2 <= L.r2) : (d2 < L.r2f);
+                    if (in && ++cnt >= L.need) break;
+                }
+            }
+            kept = cnt >= L.need;
+            if (kept) {
+                int gx = (int)(((double)p.x - L.origin_x) / (double)L.res);
+                int gy = (int)(((double)p.y - L.origin_y) / (double)L.res);
+                if (gx >= 0 && gx < L.W && gy >= 0 && gy < L.H) raster[(size_t)gy * L.W + gx] = 1;
+            }
+        }
+    }
+    // stats: candidates that survived ROR (n_clipped); wave-aggregated
+    unsigned long long m = __ballot(kept);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(&counters[0], (unsigned long long)__popcll(m));
+}
+
+void launch_ror_bin(const RorLaunch &L, int *bin_count, int2 *pt_binslot, hipStream_t s) {
+    if (!L.n) return;
+    k_ror_bin<<<cdiv(L.n, 256), 256, 0, s>>>(L, bin_count, pt_binslot);
+}
+void launch_ror_scatter(const RorLaunch &L, const int *bin_start, const int2 *pt_binslot, float4 *sorted, hipStream_t s) {
+    if (!L.n) return;
+    k_ror_scatter<<<cdiv(L.n, 256), 256, 0, s>>>(L, bin_start, pt_binslot, sorted);
+}
+void launch_ror_raster(const RorLaunch &L, const int *bin_start, const float4 *sorted, const int *d_n_binned, int n_max,
+                       uint8_t *raster, unsigned long long *counters, hipStream_t s) {
+    if (n_max <= 0) return;
+    k_ror_raster<<<cdiv(n_max, 256), 256, 0, s>>>(L, bin_start, sorted, d_n_binned, raster, counters);
+}
+
+size_t scan_temp_bytes(int n) {
+    size_t t = 0;
+    hipcub::DeviceScan::ExclusiveSum(nullptr, t, (const int *)nullptr, (int *)nullptr, n);
+    return t;
+}
+void launch_exclusive_scan(const int *in, int *out, int n, void *temp, size_t temp_bytes, hipStream_t s) {
+    AOS_HIP(hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, in, out, n, s));
+}
+
+// ------------------------------------------------------------------------------------------
+// bytes (0 / non-zero) -> bits
+__global__ void k_pack_bits(const uint8_t *bytes, uint64_t *bits, int W, int H, int WW) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    if (c >= WW || y >= H) return;
+    const uint8_t *row = bytes + (size_t)y * W;
+    uint64_t w = 0;
+    int x0 = c * 64;
+    if ((W & 15) == 0 && x0 + 64 <= W) {
+        const uint4 *v = reinterpret_cast<const uint4 *>(row + x0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint4 u = v[q];
+            uint32_t wd[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    if ((wd[k] >> (8 * b)) & 0xFF) w |= 1ull << (q * 16 + k * 4 + b);
+        }
+    } else {
+        for (int i = 0; i < 64 && x0 + i < W; ++i)
+            if (row[x0 + i]) w |= 1ull << i;
+    }
+    bits[(size_t)y * WW + c] = w;
+}
+void launch_pack_bits(const uint8_t *bytes, uint64_t *bits, int W, int H, int WW, hipStream_t s) {
+    dim3 g(cdiv(WW, 64), H);
+    k_pack_bits<<<g, 64, 0, s>>>(bytes, bits, W, H, WW);
+}
+
+__device__ __forceinline__ uint64_t pad_mask(int c, int WW, int W) {
+    // bits of word c that lie inside the image
+    int rem = W - c * 64;
+    return rem >= 64 ? ~0ull : (rem <= 0 ? 0ull : ((1ull << rem) - 1));
+}
+
+// ------------------------------------------------------------------------------------------
+// a5 applyInflation (seed_gen:933-967): cell = 100 iff an occupied raster cell lies within the
+// integer disc dx^2 + dy^2 <= R^2 — an exact bounded squared-EDT threshold, computed as an OR
+// of horizontally dilated rows: row y+dy dilated by w(dy) = floor(sqrt(R^2 - dy^2)).
+__constant__ int c_wtab[64];
+__global__ void k_inflate(const uint64_t *in, uint64_t *out, int W, int H, int WW, int R) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    if (c >= WW || y >= H) return;
+    uint64_t acc = 0;
+    for (int dy = -R; dy <= R; ++dy) {
+        int yy = y + dy;
+        if (yy < 0 || yy >= H) continue;
+        const uint64_t *row = in + (size_t)yy * WW;
+        uint64_t b = row[c];
+        uint64_t a = c > 0 ? row[c - 1] : 0ull;
+        uint64_t d = c + 1 < WW ? row[c + 1] : 0ull;
+        int w = c_wtab[dy < 0 ? -dy : dy];
+        uint64_t h = b;
+        for (int s = 1; s <= w; ++s) h |= (b >> s) | (d << (64 - s)) | (b << s) | (a >> (64 - s));
+        acc |= h;
+    }
+    out[(size_t)y * WW + c] = acc & pad_mask(c, WW, W);
+}
+void launch_inflate(const uint64_t *in, uint64_t *out, const FrameGeom &g, hipStream_t s) {
+    int wt[64] = {0};
+    for (int dy = 0; dy <= g.R && dy < 64; ++dy) {
+        int w = 0;
+        while ((w + 1) * (w + 1) + dy * dy <= g.R * g.R) ++w;
+        wt[dy] = w;
+    }
+    AOS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_wtab), wt, sizeof(wt), 0, hipMemcpyHostToDevice, s));
+    dim3 grid(cdiv(g.WW, 64), g.H);
+    k_inflate<<<grid, 64, 0, s>>>(in, out, g.W, g.H, g.WW, g.R);
+}
+
+// bits -> int8 {0,100} with an optional `frame`-cell border (markBoundariesAsOccupied, seed_gen:708-757)
+__global__ void k_bits_to_bytes(const uint64_t *bits, int8_t *out, int W, int H, int WW, int frame) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)W * H) return;
+    int y = (int)(i / W), x = (int)(i - (size_t)y * W);
+    bool v = (bits[(size_t)y * WW + (x >> 6)] >> (x & 63)) & 1ull;
+    if (frame > 0 && (x < frame || y < frame || x >= W - frame || y >= H - frame)) v = true;
+    out[i] = v ? 100 : 0;
+}
+void launch_bits_to_bytes(const uint64_t *bits, int8_t *out, const FrameGeom &g, int frame, hipStream_t s) {
+    size_t n = (size_t)g.W * g.H;
+    k_bits_to_bytes<<<cdiv(n, 256), 256, 0, s>>>(bits, out, g.W, g.H, g.WW, frame);
+}
+
+// ------------------------------------------------------------------------------------------
+// a7 morphologyEx(MORPH_OPEN, 3x3 MORPH_ELLIPSE = cross), BORDER_CONSTANT default value:
+// erosion reads 255 outside the image, dilation reads 0 (seed_gen:678-680).
+__device__ __forceinline__ uint64_t ld_er(const uint64_t *in, int r, int k, int H, int WW, int W) {
+    if (r < 0 || r >= H || k < 0 || k >= WW) return ~0ull;
+    return in[(size_t)r * WW + k] | ~pad_mask(k, WW, W);
+}
+__device__ __forceinline__ uint64_t erode_at(const uint64_t *in, int r, int k, int H, int WW, int W) {
+    if (r < 0 || r >= H || k < 0 || k >= WW) return 0ull;  // dilation reads 0 outside
+    uint64_t c = ld_er(in, r, k, H, WW, W);
+    uint64_t wv = (c << 1) | (ld_er(in, r, k - 1, H, WW, W) >> 63);
+    uint64_t ev = (c >> 1) | (ld_er(in, r, k + 1, H, WW, W) << 63);
+    return (c & wv & ev & ld_er(in, r - 1, k, H, WW, W) & ld_er(in, r + 1, k, H, WW, W)) & pad_mask(k, WW, W);
+}
+__global__ void k_open(const uint64_t *in, uint64_t *out, int W, int H, int WW) {
+    int k = blockIdx.x * blockDim.x + threadIdx.x, r = blockIdx.y;
+    if (k >= WW || r >= H) return;
+    uint64_t e = erode_at(in, r, k, H, WW, W);
+    uint64_t d = e | erode_at(in, r - 1, k, H, WW, W) | erode_at(in, r + 1, k, H, WW, W) |
+                 (e << 1) | (erode_at(in, r, k - 1, H, WW, W) >> 63) | (e >> 1) | (erode_at(in, r, k + 1, H, WW, W) << 63);
+    out[(size_t)r * WW + k] = d & pad_mask(k, WW, W);
+}
+void launch_open(const uint64_t *in, uint64_t *out, const FrameGeom &g, hipStream_t s) {
+    dim3 grid(cdiv(g.WW, 64), g.H);
+    k_open<<<grid, 64, 0, s>>>(in, out, g.W, g.H, g.WW);
+}
+
+// ------------------------------------------------------------------------------------------
+// a7 ximgproc::thinning(THINNING_ZHANGSUEN) with temporal blocking.
+// One workgroup owns a TH x TWW-word tile and loads it with a halo of HR = 2*KIT rows and one
+// word (64 cells) on each side into LDS, then runs KIT full iterations (2*KIT Jacobi
+// sub-iterations) in LDS: each sub-iteration invalidates one more halo row/cell from the outside
+// in, so the interior stays exact. Bit-sliced logic evaluates the Zhang-Suen predicate for 64
+// cells per 64-bit word:
+//   A == 1       : exactly one 0->1 transition in p2,p3,...,p9,p2
+//   2 <= B <= 6  : at least two set and at least two clear among p2..p9
+//   m1 == m2 == 0: iter 0: p2p4p6 = p4p6p8 = 0; iter 1: p2p4p8 = p2p6p8 = 0
+// Rows 0 / H-1 and columns 0 / W-1 of the image are never examined (ximgproc loops 1..n-2).
+constexpr int TH = 64, TWW = 8, KIT = kThinItersPerLaunch, HR = 2 * KIT, NR = TH + 2 * HR, NC = TWW + 2;
+
+__device__ __forceinline__ uint64_t zs_step(uint64_t n0, uint64_t n1, uint64_t n2, uint64_t c0, uint64_t c1,
+                                            uint64_t c2, uint64_t s0, uint64_t s1, uint64_t s2, int sub) {
+    // x0 = word to the west, x1 = this word, x2 = word to the east
+    const uint64_t p2 = n1;
+    const uint64_t p3 = (n1 >> 1) | (n2 << 63);   // (y-1, x+1)
+    const uint64_t p4 = (c1 >> 1) | (c2 << 63);   // (y,   x+1)
+    const uint64_t p5 = (s1 >> 1) | (s2 << 63);   // (y+1, x+1)
+    const uint64_t p6 = s1;                       // (y+1, x)
+    const uint64_t p7 = (s1 << 1) | (s0 >> 63);   // (y+1, x-1)
+    const uint64_t p8 = (c1 << 1) | (c0 >> 63);   // (y,   x-1)
+    const uint64_t p9 = (n1 << 1) | (n0 >> 63);   // (y-1, x-1)
+    const uint64_t seq[9] = {p2, p3, p4, p5, p6, p7, p8, p9, p2};
+    uint64_t one = 0, two = 0;          // transitions
+    uint64_t o1 = 0, o2 = 0;            // set neighbours >= 1, >= 2
+    uint64_t z1 = 0, z2 = 0;            // clear neighbours >= 1, >= 2
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        uint64_t t = ~seq[k] & seq[k + 1];
+        two |= one & t; one |= t;
+        uint64_t p = seq[k];
+        o2 |= o1 & p; o1 |= p;
+        uint64_t q = ~p;
+        z2 |= z1 & q; z1 |= q;
+    }
+    uint64_t A1 = one & ~two;
+    uint64_t B26 = o2 & z2;
+    uint64_t m = sub == 0 ? (~(p2 & p4 & p6) & ~(p4 & p6 & p8)) : (~(p2 & p4 & p8) & ~(p2 & p6 & p8));
+    return c1 & A1 & B26 & m;  // cells to delete
+}
+
+__global__ __launch_bounds__(256) void k_thin_block(const uint64_t *__restrict__ in, uint64_t *__restrict__ out,
+                                                    int W, int H, int WW, int base_iter, int *flags) {
+    if (base_iter >= 2 && flags[1 + base_iter - 1] == 0) return;  // converged in an earlier launch
+    __shared__ uint64_t buf[2][NR][NC];
+    __shared__ int chg_shared;
+    const int ty0 = blockIdx.y * TH, tc0 = blockIdx.x * TWW;
+    if (threadIdx.x == 0) chg_shared = 0;
+    for (int idx = threadIdx.x; idx < NR * NC; idx += blockDim.x) {
+        int r = idx / NC, k = idx - r * NC;
+        int gy = ty0 - HR + r, gc = tc0 - 1 + k;
+        buf[0][r][k] = (gy >= 0 && gy < H && gc >= 0 && gc < WW) ? in[(size_t)gy * WW + gc] : 0ull;
+    }
+    __syncthreads();
+    int chg = 0;        // bit j: iteration base_iter + j deleted something inside this tile
+    int nonempty = 0;   // after iteration 0 (only meaningful when base_iter == 0)
+    int cur = 0;
+    for (int s = 0; s < 2 * KIT; ++s) {
+        const int sub = s & 1;
+        for (int idx = threadIdx.x; idx < NR * NC; idx += blockDim.x) {
+            int r = idx / NC, k = idx - r * NC;
+            uint64_t c1 = buf[cur][r][k];
+            uint64_t nw = c1;
+            if (r > 0 && r < NR - 1) {
+                int gy = ty0 - HR + r, gc = tc0 - 1 + k;
+                uint64_t c0 = k > 0 ? buf[cur][r][k - 1] : 0ull, c2 = k < NC - 1 ? buf[cur][r][k + 1] : 0ull;
+                uint64_t n0 = k > 0 ? buf[cur][r - 1][k - 1] : 0ull, n1 = buf[cur][r - 1][k],
+                         n2 = k < NC - 1 ? buf[cur][r - 1][k + 1] : 0ull;
+                uint64_t s0 = k > 0 ? buf[cur][r + 1][k - 1] : 0ull, s1 = buf[cur][r + 1][k],
+                         s2 = k < NC - 1 ? buf[cur][r + 1][k + 1] : 0ull;
+                uint64_t del = zs_step(n0, n1, n2, c0, c1, c2, s0, s1, s2, sub);
+                // examinable cells: 1 <= y <= H-2, 1 <= x <= W-2
+                uint64_t em = 0;
+                if (gy >= 1 && gy <= H - 2 && gc >= 0 && gc < WW) {
+                    em = pad_mask(gc, WW, W - 1);
+                    if (gc == 0) em &= ~1ull;
+                }
+                del &= em;
+                nw = c1 & ~del;
+                if (del && r >= HR && r < HR + TH && k >= 1 && k <= TWW) chg |= 1 << (s >> 1);
+            }
+            buf[cur ^ 1][r][k] = nw;
+            if (s == 1 && base_iter == 0 && nw && r >= HR && r < HR + TH && k >= 1 && k <= TWW &&
+                ty0 - HR + r < H && tc0 - 1 + k < WW)
+                nonempty = 1;
+        }
+        cur ^= 1;
+        __syncthreads();
+    }
+    for (int idx = threadIdx.x; idx < TH * TWW; idx += blockDim.x) {
+        int r = idx / TWW, k = idx - r * TWW;
+        int gy = ty0 + r, gc = tc0 + k;
+        if (gy < H && gc < WW) out[(size_t)gy * WW + gc] = buf[cur][HR + r][1 + k];
+    }
+    if (chg || nonempty) atomicOr(&chg_shared, chg | (nonempty << 30));
+    __syncthreads();
+    if (threadIdx.x == 0 && chg_shared) {
+        int m = chg_shared;
+        if (m & (1 << 30)) atomicOr(&flags[0], 1);
+        for (int j = 0; j < KIT; ++j)
+            if (m & (1 << j)) atomicOr(&flags[1 + base_iter + j], 1);
+    }
+}
+
+void launch_thin_block(const uint64_t *in, uint64_t *out, const FrameGeom &g, int base_iter, int *flags, hipStream_t s) {
+    dim3 grid(cdiv(g.WW, TWW), cdiv(g.H, TH));
+    k_thin_block<<<grid, 256, 0, s>>>(in, out, g.W, g.H, g.WW, base_iter, flags);
+}
+
+// a16 markPolygonBoundaryAsOccupied (seed_gen:772-825): the bbox +- 2.5 m rectangle in grid cells;
+// drawLineInGrid (Bresenham, :828-870) of an axis-aligned segment is the straight run of cells.
+__global__ void k_draw_rect(int8_t *grid, int W, int H, int gx0, int gy0, int gx1, int gy1) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    int xlo = min(gx0, gx1), xhi = max(gx0, gx1), ylo = min(gy0, gy1), yhi = max(gy0, gy1);
+    int nx = xhi - xlo + 1, ny = yhi - ylo + 1;
+    if (i < nx) {
+        grid[(size_t)gy0 * W + xlo + i] = 100;
+        grid[(size_t)gy1 * W + xlo + i] = 100;
+    } else if (i < nx + ny) {
+        int j = i - nx;
+        grid[(size_t)(ylo + j) * W + gx0] = 100;
+        grid[(size_t)(ylo + j) * W + gx1] = 100;
+    }
+}
+void launch_draw_rect(int8_t *grid, const FrameGeom &g, int gx0, int gy0, int gx1, int gy1, hipStream_t s) {
+    int n = abs(gx1 - gx0) + abs(gy1 - gy0) + 2;
+    k_draw_rect<<<cdiv(n, 256), 256, 0, s>>>(grid, g.W, g.H, gx0, gy0, gx1, gy1);
+}
+
+}  // namespace aos

@@ -1,0 +1,674 @@
+// GVD construction (AosGvdNode::processGraph, src/aos_gvd_node.cpp:255-318) on gfx950.
+//
+//  g1 seed merge (gvd:84-128)                 GPU  greedy LFMIS (<= 0.5 m) + ordered member sums
+//  g4 Subdiv2D insert + facets                host sequential replay (subdiv2d.h explains why)
+//  g5 extractBoundaryPoints                   GPU  greedy LFMIS (1 cm key or < 5 cm)
+//  g6 buildGraphFromBoundaryPoints            GPU  hashed nearest snap + pair search + occupancy
+//                                                  sampling + first-passing-occurrence selection
+//  g7 filterNodesAndEdgesOutsideGrid          GPU  compaction
+//  g8 TL/TR/BL/BR label points                GPU  per (row, label) arg-min / castRay
+//  g9 publishGraph labels                     GPU  per node
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <chrono>
+#include <climits>
+#include <cmath>
+#include <cstring>
+
+#include "aos_ctx.h"
+#include "subdiv2d.h"
+
+namespace aos {
+
+static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+template <class T> static T *dev(DevBuf &b, size_t n) { return static_cast<T *>(b.ensure(sizeof(T) * std::max<size_t>(n, 1))); }
+
+struct GridG {
+    double ox, oy, res;             // info.origin, (double)info.resolution
+    int W, H;
+    double minx, maxx, miny, maxy;  // origin + width * resolution (float product) gvd:278-281
+    double diag2;                   // sqrt(gw^2 + gh^2) * 2 (findVoronoiBoundaryPointNearEndpoint)
+    double diag3;                   // * 3 (castRay)
+    double step;                    // castRay step: max(0.01, res * 0.5)
+};
+
+__device__ __forceinline__ bool occ_trunc(const int8_t *sk, const GridG &g, double px, double py) {
+    double fx = (px - g.ox) / g.res, fy = (py - g.oy) / g.res;
+    // static_cast<int>: x86 gives INT_MIN out of range; either way such samples are outside
+    if (!(fx > -1.0 && fx < (double)g.W) || !(fy > -1.0 && fy < (double)g.H)) return false;
+    int mx = (int)fx, my = (int)fy;
+    if (mx >= 0 && mx < g.W && my >= 0 && my < g.H) return sk[(size_t)my * g.W + mx] == 100;
+    return false;
+}
+
+// ------------------------------------------------------------------ g1 merge
+// owner[j] = smallest earlier kept (leader) candidate conflicting with j, or j for leaders
+__global__ void k_merge_owner(const int *state, const int *coff, const int *clist, int n, int *owner, int *idx) {
+    int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    int o = INT_MAX;
+    if (state[j] == 1) o = j;
+    else if (state[j] == 2)
+        for (int k = coff[j]; k < coff[j + 1]; ++k) { int i = clist[k]; if (state[i] == 1) o = min(o, i); }
+    owner[j] = o;
+    idx[j] = j;
+}
+// members of each leader are contiguous (stable sort by owner keeps ascending j): sum in order
+__global__ void k_merge_sum(const double2 *raw, const int *sorted_owner, const int *sorted_j, int n, const int *leaders,
+                            int n_leaders, double2 *merged) {
+    int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_leaders) return;
+    const int L = leaders[r];
+    int lo = 0, hi = n;
+    while (lo < hi) { int m = (lo + hi) >> 1; if (sorted_owner[m] < L) lo = m + 1; else hi = m; }
+    double sx = 0.0, sy = 0.0;
+    int cnt = 0;
+    for (int k = lo; k < n && sorted_owner[k] == L; ++k) { double2 p = raw[sorted_j[k]]; sx += p.x; sy += p.y; ++cnt; }
+    merged[r] = make_double2(sx / (double)cnt, sy / (double)cnt);
+}
+
+// ------------------------------------------------------------------ g5/g6 helpers
+__global__ void k_edges_to_occ(const float *e, int ne, double2 *occ, int *ok) {
+    int o = blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= 2 * ne) return;
+    int k = o >> 1;
+    occ[o] = (o & 1) ? make_double2((double)e[4 * k + 2], (double)e[4 * k + 3]) : make_double2((double)e[4 * k], (double)e[4 * k + 1]);
+    ok[o] = 1;
+}
+__global__ void k_cell_keys(const double2 *p, int n, HashG h, int *keys, int *idx) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double fx = (p[i].x - h.x0) * h.inv, fy = (p[i].y - h.y0) * h.inv;
+    int cx = !(fx > 0.0) ? 0 : (fx >= (double)(h.nx - 1) ? h.nx - 1 : (int)fx);
+    int cy = !(fy > 0.0) ? 0 : (fy >= (double)(h.ny - 1) ? h.ny - 1 : (int)fy);
+    keys[i] = cy * h.nx + cx;
+    idx[i] = i;
+}
+__device__ __forceinline__ void cell_of(const HashG &h, double x, double y, int &cx, int &cy) {
+    double fx = (x - h.x0) * h.inv, fy = (y - h.y0) * h.inv;
+    cx = !(fx > 0.0) ? 0 : (fx >= (double)(h.nx - 1) ? h.nx - 1 : (int)fx);
+    cy = !(fy > 0.0) ? 0 : (fy >= (double)(h.ny - 1) ? h.ny - 1 : (int)fy);
+}
+__device__ __forceinline__ int lb(const int *keys, int n, int k) {
+    int lo = 0, hi = n;
+    while (lo < hi) { int m = (lo + hi) >> 1; if (keys[m] < k) lo = m + 1; else hi = m; }
+    return lo;
+}
+
+// findNearestBoundaryPoint (gvd:812-824): first strict minimum of |bp_i - q| over i.
+// The nearest lies within 5 cm (extractBoundaryPoints kept it or a conflicting point within
+// 5 cm / the same 1 cm key), so the 3x3 cells of the 5 cm hash suffice; brute force otherwise.
+__global__ void k_nearest(const double2 *occ, int n_occ, const double2 *bp, int M, HashG h, const int *skeys,
+                          const int *sidx, int *near_out) {
+    int o = blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= n_occ) return;
+    const double2 q = occ[o];
+    int cx, cy;
+    cell_of(h, q.x, q.y, cx, cy);
+    double best = 1.7976931348623157e308;
+    int bi = -1;
+    for (int yy = max(cy - 1, 0); yy <= min(cy + 1, h.ny - 1); ++yy) {
+        int k0 = lb(skeys, M, yy * h.nx + max(cx - 1, 0)), k1 = lb(skeys, M, yy * h.nx + min(cx + 1, h.nx - 1) + 1);
+        for (int k = k0; k < k1; ++k) {
+            int i = sidx[k];
+            double dx = bp[i].x - q.x, dy = bp[i].y - q.y, d = sqrt(dx * dx + dy * dy);
+            if (d < best || (d == best && i < bi)) { best = d; bi = i; }
+        }
+    }
+    if (!(best < 0.05)) {  // safety net: exact brute force
+        best = 1.7976931348623157e308; bi = -1;
+        for (int i = 0; i < M; ++i) {
+            double dx = bp[i].x - q.x, dy = bp[i].y - q.y, d = sqrt(dx * dx + dy * dy);
+            if (d < best) { best = d; bi = i; }
+        }
+    }
+    near_out[o] = bi;
+}
+
+// all pairs i < j with 1e-6 < |bp_i - bp_j| <= 0.5 (gvd:861-894), CSR per i, j ascending
+__global__ void k_pairs(const double2 *bp, int M, HashG h, const int *skeys, const int *sidx, const int *poff, int *pcount,
+                        int *plist) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= M) return;
+    const double2 p = bp[i];
+    int cx, cy;
+    cell_of(h, p.x, p.y, cx, cy);
+    int c = 0, w = poff ? poff[i] : 0;
+    for (int yy = max(cy - 1, 0); yy <= min(cy + 1, h.ny - 1); ++yy) {
+        int k0 = lb(skeys, M, yy * h.nx + max(cx - 1, 0)), k1 = lb(skeys, M, yy * h.nx + min(cx + 1, h.nx - 1) + 1);
+        for (int k = k0; k < k1; ++k) {
+            int j = sidx[k];
+            if (j <= i) continue;
+            double dx = p.x - bp[j].x, dy = p.y - bp[j].y, d = sqrt(dx * dx + dy * dy);
+            if (d <= 0.5 && d > 1e-6) {
+                if (poff) {  // insertion into the sorted run
+                    int pos = w + c;
+                    while (pos > w && plist[pos - 1] > j) { plist[pos] = plist[pos - 1]; --pos; }
+                    plist[pos] = j;
+                }
+                ++c;
+            }
+        }
+    }
+    if (!poff) pcount[i] = c;
+}
+
+// candidate edge occurrences: [0, E) Voronoi edges, [E, E + P) pairs. from/to keep the direction
+// in which the reference samples the segment.
+__global__ void k_candidates(const int *near_idx, int ne, const int *poff, const int *plist, int M, int np,
+                             int2 *ft, unsigned long long *key, int *valid) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= ne + np) return;
+    int a, b;
+    if (c < ne) { a = near_idx[2 * c]; b = near_idx[2 * c + 1]; }
+    else {
+        int k = c - ne, lo = 0, hi = M - 1;  // owner i of pair slot k
+        while (lo < hi) { int m = (lo + hi + 1) >> 1; if (poff[m] <= k) lo = m; else hi = m - 1; }
+        a = lo; b = plist[k];
+    }
+    int ok = a >= 0 && b >= 0 && a != b;
+    ft[c] = make_int2(a, b);
+    int lo_ = min(a, b), hi_ = max(a, b);
+    key[c] = ok ? ((unsigned long long)(unsigned)lo_ << 32) | (unsigned)hi_ : ~0ull;
+    valid[c] = ok;
+}
+
+// edgePassesThroughOccupiedPixels (gvd:320-359) on the framed skeleton. Samples whose t-range
+// cannot touch the grid are skipped (they read no cell), which keeps far hull edges cheap.
+__global__ void k_occupancy(const int2 *ft, const int *valid, int nc, const double2 *bp, const int8_t *sk, GridG g,
+                            int *pass) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nc) return;
+    if (!valid[c]) { pass[c] = 0; return; }
+    const double2 s = bp[ft[c].x], e = bp[ft[c].y];
+    double ex = e.x - s.x, ey = e.y - s.y;
+    double len = sqrt(ex * ex + ey * ey);
+    bool hit = false;
+    if (len >= 1e-6) {
+        const double step = g.res * 0.5;
+        double q = len / step;
+        int num = (q > -2147483649.0 && q < 2147483647.0) ? (int)q + 1 : INT_MIN + 1;  // x86 int conversion
+        double dx = ex / len, dy = ey / len;
+        // candidate sample window: cells exist only for world x in (ox - res, ox + W res), same for y
+        int i0 = 0, i1 = num;
+        if (num > 64) {
+            double lo_t = 0.0, hi_t = 1.0;
+            const double gx0 = g.ox - 2 * g.res, gx1 = g.ox + (g.W + 2) * g.res;
+            const double gy0 = g.oy - 2 * g.res, gy1 = g.oy + (g.H + 2) * g.res;
+            auto clip = [&](double p0, double dp, double a, double b) {
+                if (dp == 0.0) { if (p0 < a || p0 > b) { lo_t = 1.0; hi_t = 0.0; } return; }
+                double t0 = (a - p0) / dp, t1 = (b - p0) / dp;
+                if (t0 > t1) { double t = t0; t0 = t1; t1 = t; }
+                lo_t = fmax(lo_t, t0); hi_t = fmin(hi_t, t1);
+            };
+            clip(s.x, ex, gx0, gx1);
+            clip(s.y, ey, gy0, gy1);
+            if (lo_t > hi_t) { i0 = 1; i1 = 0; }
+            else { i0 = max(0, (int)floor(lo_t * num) - 2); i1 = min(num, (int)ceil(hi_t * num) + 2); }
+        }
+        for (int i = i0; i <= i1 && num >= 0; ++i) {
+            double t = (i == num) ? 1.0 : ((double)i / (double)num);
+            double px = s.x + (t * dx) * len, py = s.y + (t * dy) * len;
+            if (occ_trunc(sk, g, px, py)) { hit = true; break; }
+        }
+    }
+    pass[c] = hit ? 0 : 1;
+}
+
+__global__ void k_pass_keys(const unsigned long long *key, const int *pass, int nc, unsigned long long *k2, int *occ_idx) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nc) return;
+    k2[c] = pass[c] ? key[c] : ~0ull;
+    occ_idx[c] = c;
+}
+__global__ void k_first_of_key(const unsigned long long *sk, const int *socc, int nc, int *selected) {
+    int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nc) return;
+    if (sk[k] == ~0ull) return;
+    if (k == 0 || sk[k - 1] != sk[k]) selected[socc[k]] = 1;
+}
+
+// ------------------------------------------------------------------ g7 filter
+__global__ void k_inside(const double2 *bp, int M, GridG g, int *f) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= M) return;
+    double2 p = bp[i];
+    f[i] = p.x >= g.minx && p.x <= g.maxx && p.y >= g.miny && p.y <= g.maxy;
+}
+__global__ void k_gather_nodes(const double2 *bp, const int *f, const int *pos, int M, double2 *nodes) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < M && f[i]) nodes[pos[i]] = bp[i];
+}
+// selected candidate c -> record (a<b); keep if both nodes stay (and stay distinct)
+__global__ void k_edge_keep(const int *selected, const int2 *ft, int nc, const int *inside, const int *pos, int *keep) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nc) return;
+    int k = 0;
+    if (selected[c]) {
+        int a = min(ft[c].x, ft[c].y), b = max(ft[c].x, ft[c].y);
+        k = inside[a] && inside[b] && pos[a] != pos[b];
+    }
+    keep[c] = k;
+}
+__global__ void k_edge_emit(const int *keep, const int *kpos, const int2 *ft, int nc, const int *pos, const double2 *nodes,
+                            int *edges, float *len) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nc || !keep[c]) return;
+    int a = pos[min(ft[c].x, ft[c].y)], b = pos[max(ft[c].x, ft[c].y)];
+    if (a > b) { int t = a; a = b; b = t; }
+    double dx = nodes[b].x - nodes[a].x, dy = nodes[b].y - nodes[a].y;  // (to - from).norm()
+    int r = kpos[c];
+    edges[2 * r] = a; edges[2 * r + 1] = b;
+    len[r] = (float)sqrt(dx * dx + dy * dy);
+}
+
+// ------------------------------------------------------------------ g8 label points
+struct LabelRow { double ex, ey, ox, oy; double deg, cs, sn; };  // endpoint, other endpoint, angle, host cos/sin
+// one workgroup per (row, label): arg-min over the filtered nodes (gvd:731-774); castRay fallback (:788)
+__global__ __launch_bounds__(256) void k_label_points(const LabelRow *jobs, int nj, const double2 *nodes, int Mn, GridG g,
+                                                      const int8_t *sk, double2 *pts, int *valid) {
+    const int jb = blockIdx.x;
+    if (jb >= nj) return;
+    const LabelRow J = jobs[jb];
+    double mdx = J.ox - J.ex, mdy = J.oy - J.ey;
+    double ml = sqrt(mdx * mdx + mdy * mdy);
+    if (ml < 1e-6) { mdx = 1.0; mdy = 0.0; }
+    else { mdx = mdx / ml; mdy = mdy / ml; }
+    const double outx = -mdx, outy = -mdy, perx = -mdy, pery = mdx;
+    const bool m90 = fabs(J.deg - (-90.0)) < 1e-6, p90 = fabs(J.deg - 90.0) < 1e-6;
+    double best = 1.7976931348623157e308;
+    int bi = INT_MAX;
+    for (int i = threadIdx.x; i < Mn; i += blockDim.x) {
+        double dx = nodes[i].x - J.ex, dy = nodes[i].y - J.ey;
+        double dist = sqrt(dx * dx + dy * dy);
+        if (dist < 0.5 || dist > fmax(9.0, g.diag2)) continue;  // radii {5, 7, 9, diag2}: first hit = arg-min
+        double nx = dx, ny = dy;
+        double z = dx * dx + dy * dy;
+        if (z > 0.0) { double s = sqrt(z); nx = dx / s; ny = dy / s; }
+        if (outx * nx + outy * ny < 0.0) continue;
+        double dp = perx * nx + pery * ny;
+        if (m90) { if (dp > 0.0) continue; }
+        else if (p90) { if (dp < 0.0) continue; }
+        if (dist < best || (dist == best && i < bi)) { best = dist; bi = i; }
+    }
+    __shared__ double sb[256];
+    __shared__ int si[256];
+    sb[threadIdx.x] = best; si[threadIdx.x] = bi;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) {
+            double b2 = sb[threadIdx.x + o]; int i2 = si[threadIdx.x + o];
+            if (b2 < sb[threadIdx.x] || (b2 == sb[threadIdx.x] && i2 < si[threadIdx.x])) { sb[threadIdx.x] = b2; si[threadIdx.x] = i2; }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x != 0) return;
+    if (si[0] != INT_MAX) { pts[jb] = nodes[si[0]]; valid[jb] = 1; return; }
+    // castRay gvd:558-684 (angles +-90: cos/sin from the host table in J.deg's sign)
+    double ex = J.ox - J.ex, ey = J.oy - J.ey;
+    double d = sqrt(ex * ex + ey * ey);
+    if (d < 1e-6) { ex = 1.0; ey = 0.0; } else { ex = ex / d; ey = ey / d; }
+    double ox_ = -ex, oy_ = -ey, px = -ey, py = ex;
+    double rx, ry;
+    const double cs = J.cs, sn = J.sn;  // std::cos/std::sin of the angle, evaluated by the host libm
+    if (J.deg > 0) { rx = cs * ox_ + sn * px; ry = cs * oy_ + sn * py; }
+    else { rx = cs * ox_ + sn * (-px); ry = cs * oy_ + sn * (-py); }
+    { double z = rx * rx + ry * ry; if (z > 0.0) { double q = sqrt(z); rx = rx / q; ry = ry / q; } }
+    double cur = 0.5;  // min_distance passed by findVoronoiBoundaryPointNearEndpoint
+    double resx = 0, resy = 0;
+    bool done = false;
+    while (cur <= g.diag3) {
+        double cx = J.ex + rx * cur, cy = J.ey + ry * cur;
+        if (!(cx >= g.minx && cx <= g.maxx && cy >= g.miny && cy <= g.maxy)) {
+            resx = fmax(g.minx, fmin(g.maxx, cx)); resy = fmax(g.miny, fmin(g.maxy, cy)); done = true; break;
+        }
+        if (occ_trunc(sk, g, cx, cy)) { resx = cx; resy = cy; done = true; break; }
+        cur += g.step;
+    }
+    if (!done) {
+        double fx = J.ex + rx * g.diag3, fy = J.ey + ry * g.diag3;
+        if (!(fx >= g.minx && fx <= g.maxx && fy >= g.miny && fy <= g.maxy)) {
+            fx = fmax(g.minx, fmin(g.maxx, fx)); fy = fmax(g.miny, fmin(g.maxy, fy));
+        }
+        resx = fx; resy = fy;
+    }
+    pts[jb] = make_double2(resx, resy);
+    valid[jb] = 1;
+}
+
+// ------------------------------------------------------------------ g9 node labels (publishGraph gvd:920-995)
+__global__ void k_node_labels(const double2 *nodes, int Mn, const double2 *lp, const int *lv, int n_rows, int *mask,
+                              int *cidx, int *count, const int *off, int *lcl, int *lty) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= Mn) return;
+    const double2 p = nodes[i];
+    int m = 0, ci = -1, cnt = 0, w = off ? off[i] : 0;
+    for (int r = 0; r < n_rows; ++r)
+        for (int k = 0; k < 4; ++k) {
+            if (!lv[4 * r + k]) continue;
+            double dx = p.x - lp[4 * r + k].x, dy = p.y - lp[4 * r + k].y;
+            if (sqrt(dx * dx + dy * dy) < 0.1) {
+                m |= 1 << k;
+                if (off) { lcl[w + cnt] = r; lty[w + cnt] = k; }
+                ++cnt;
+                if (ci == -1) ci = r;
+            }
+        }
+    if (!off) { mask[i] = m; cidx[i] = ci; count[i] = cnt; }
+}
+
+// ------------------------------------------------------------------ orchestration
+struct GvdScratch {
+    DevBuf raw, ok, leaders, merged, owner, oidx, sowner, sidx, tmp, edges_f, occ, occ_ok, bp, kept_occ, keys, idx, skeys,
+        sidx2, near_idx, pk, pidx, pskeys, psidx, pcount, poff, plist, ft, ckey, cvalid, pass, k2, occ_idx, sk2, socc, selected,
+        inside, ipos, nodes, keep, kpos, edges, lens, jobs, lpts, lval, lmask, lcidx, lcount, loff, lcl, lty, scan_tmp;
+};
+static GvdScratch &scratch(GvdState &G) {
+    // one scratch per state (per handle); stored behind the misc buffer slot
+    if (!G.misc.p) { G.misc.p = new GvdScratch(); G.misc.cap = 0; }
+    return *static_cast<GvdScratch *>(G.misc.p);
+}
+void free_gvd_scratch(GvdState &G) {
+    if (G.misc.p) {
+        auto *S = static_cast<GvdScratch *>(G.misc.p);
+        DevBuf *all[] = {&S->raw, &S->ok, &S->leaders, &S->merged, &S->owner, &S->oidx, &S->sowner, &S->sidx, &S->tmp,
+                         &S->edges_f, &S->occ, &S->occ_ok, &S->bp, &S->kept_occ, &S->keys, &S->idx, &S->skeys, &S->sidx2,
+                         &S->near_idx, &S->pk, &S->pidx, &S->pskeys, &S->psidx, &S->pcount, &S->poff, &S->plist, &S->ft,
+                         &S->ckey, &S->cvalid, &S->pass, &S->k2, &S->occ_idx, &S->sk2, &S->socc, &S->selected, &S->inside,
+                         &S->ipos, &S->nodes, &S->keep, &S->kpos, &S->edges, &S->lens, &S->jobs, &S->lpts, &S->lval,
+                         &S->lmask, &S->lcidx, &S->lcount, &S->loff, &S->lcl, &S->lty, &S->scan_tmp};
+        for (DevBuf *b : all) b->release();
+        delete S;
+        G.misc.p = nullptr;
+    }
+}
+
+static void scan_excl(DevBuf &tmpb, const int *in, int *out, int n, hipStream_t s) {
+    size_t tb = 0;
+    AOS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, n, s));
+    void *t = tmpb.ensure(tb);
+    AOS_HIP(hipcub::DeviceScan::ExclusiveSum(t, tb, in, out, n, s));
+}
+
+bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipStream_t s, hipEvent_t *ev) {
+    GvdScratch &S = scratch(G);
+    G.nodes_xy.clear(); G.labels.clear(); G.cluster_idx.clear(); G.label_counts.clear();
+    G.label_clusters.clear(); G.label_types.clear(); G.edges_out.clear(); G.lengths.clear(); G.clearances.clear();
+    G.n_merged = G.n_vor_edges = G.n_bpts = 0;
+    G.ms_merge = G.ms_delaunay = G.ms_graph = G.ms_total = 0;
+    int *h_sc = static_cast<int *>(G.h_misc.ensure(4096));
+    const int n = in.n_seeds;
+    AOS_HIP(hipEventRecord(ev[6], s));
+    if (n <= 0) return false;  // processGraph: voronoi_seeds_.empty() -> return (gvd:257)
+
+    GridG g{};
+    g.ox = in.info.origin_x; g.oy = in.info.origin_y; g.res = (double)in.info.resolution;
+    g.W = (int)in.info.width; g.H = (int)in.info.height;
+    g.minx = in.info.origin_x; g.maxx = g.minx + in.info.width * in.info.resolution;
+    g.miny = in.info.origin_y; g.maxy = g.miny + in.info.height * in.info.resolution;
+    {
+        double gw = in.info.width * in.info.resolution, gh = in.info.height * in.info.resolution;
+        g.diag2 = std::sqrt(gw * gw + gh * gh) * 2.0;
+        g.diag3 = std::sqrt(gw * gw + gh * gh) * 3.0;
+        g.step = in.info.resolution * 0.5;
+        if (g.step < 0.01) g.step = 0.01;
+    }
+
+    // ---- g1 merge
+    double2 *d_raw = dev<double2>(S.raw, n);
+    AOS_HIP(hipMemcpyAsync(d_raw, in.seeds_host, sizeof(double2) * n, hipMemcpyHostToDevice, s));
+    int *d_ok = dev<int>(S.ok, n);
+    {
+        std::vector<int> ones(n, 1);
+        AOS_HIP(hipMemcpyAsync(d_ok, ones.data(), sizeof(int) * n, hipMemcpyHostToDevice, s));
+        AOS_HIP(hipStreamSynchronize(s));
+    }
+    const HashG hm = make_hash(g.minx - 60.0, g.maxx + 60.0, g.miny - 60.0, g.maxy + 60.0, 0.5);
+    double2 *d_lead_pts = dev<double2>(S.merged, n);
+    int *d_leaders = dev<int>(S.leaders, n);
+    const int nl = greedy_dedup(G.dedup, d_raw, d_ok, n, kConflictLessEq, 0.5, hm, d_lead_pts, d_leaders, s, h_sc);
+    int *d_owner = dev<int>(S.owner, n), *d_oidx = dev<int>(S.oidx, n), *d_sowner = dev<int>(S.sowner, n),
+        *d_sj = dev<int>(S.sidx, n);
+    k_merge_owner<<<cdiv(n, 256), 256, 0, s>>>(G.dedup.state.as<int>(), G.dedup.coff.as<int>(), G.dedup.clist.as<int>(), n,
+                                                d_owner, d_oidx);
+    {
+        size_t tb = 0;
+        AOS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, d_owner, d_sowner, d_oidx, d_sj, n, 0, 32, s));
+        void *t = S.tmp.ensure(tb);
+        AOS_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, d_owner, d_sowner, d_oidx, d_sj, n, 0, 32, s));
+    }
+    double2 *d_merged = d_lead_pts;  // overwritten in leader order
+    k_merge_sum<<<cdiv(nl, 128), 128, 0, s>>>(d_raw, d_sowner, d_sj, n, d_leaders, nl, d_merged);
+    std::vector<double> merged(2 * (size_t)nl);
+    AOS_HIP(hipMemcpyAsync(merged.data(), d_merged, sizeof(double2) * nl, hipMemcpyDeviceToHost, s));
+    AOS_HIP(hipStreamSynchronize(s));
+    G.n_merged = nl;
+    AOS_HIP(hipEventRecord(ev[7], s));
+
+    // ---- g3/g4 finite filter, bounds, Subdiv2D (host) -> Voronoi edges
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<float> vedges;
+    {
+        double min_x = g.minx, max_x = g.maxx, min_y = g.miny, max_y = g.maxy;
+        if (!std::isfinite(min_x) || !std::isfinite(max_x) || !std::isfinite(min_y) || !std::isfinite(max_y)) return false;
+        bool any_finite = false;
+        for (int i = 0; i < nl; ++i) any_finite |= std::isfinite(merged[2 * i]) && std::isfinite(merged[2 * i + 1]);
+        if (!any_finite) return false;  // gvd:273-275
+        // VoronoiDiagram::compute voronoi_diagram.cpp:27-89
+        if (min_x > max_x) std::swap(min_x, max_x);
+        if (min_y > max_y) std::swap(min_y, max_y);
+        if (max_x - min_x < 1.0) { double c = (min_x + max_x) / 2.0; min_x = c - 0.5; max_x = c + 0.5; }
+        if (max_y - min_y < 1.0) { double c = (min_y + max_y) / 2.0; min_y = c - 0.5; max_y = c + 0.5; }
+        float rx = static_cast<float>(min_x - 1.0), ry = static_cast<float>(min_y - 1.0);
+        float rw = static_cast<float>(std::abs(max_x - min_x) + 2.0), rh = static_cast<float>(std::abs(max_y - min_y) + 2.0);
+        if (!(rw <= 0 || rh <= 0)) {
+            Subdiv2D sd;
+            sd.init_delaunay(rx, ry, rw, rh, P.subdiv_rect_mode);
+            const float margin = 0.1f;
+            for (int i = 0; i < nl; ++i) {
+                const double sx = merged[2 * i], sy = merged[2 * i + 1];
+                if (!std::isfinite(sx) || !std::isfinite(sy)) continue;
+                float x = static_cast<float>(sx), y = static_cast<float>(sy);
+                x = std::max(rx + margin, std::min(rx + rw - margin, x));
+                y = std::max(ry + margin, std::min(ry + rh - margin, y));
+                sd.insert(x, y);
+            }
+            sd.voronoi_edges(vedges);
+        }
+    }
+    auto t1 = std::chrono::steady_clock::now();
+    G.ms_delaunay = std::chrono::duration<float, std::milli>(t1 - t0).count();
+    const int ne = (int)(vedges.size() / 4);
+    G.n_vor_edges = ne;
+    AOS_HIP(hipEventRecord(ev[8], s));
+    if (ne == 0) return true;  // no boundary points: an empty graph is still published
+
+    // ---- g5 boundary points
+    float *d_ef = dev<float>(S.edges_f, 4 * (size_t)ne);
+    AOS_HIP(hipMemcpyAsync(d_ef, vedges.data(), sizeof(float) * 4 * ne, hipMemcpyHostToDevice, s));
+    const int no = 2 * ne;
+    double2 *d_occ = dev<double2>(S.occ, no);
+    int *d_occ_ok = dev<int>(S.occ_ok, no);
+    k_edges_to_occ<<<cdiv(no, 256), 256, 0, s>>>(d_ef, ne, d_occ, d_occ_ok);
+    const HashG h5 = make_hash(g.minx - 10.0, g.maxx + 10.0, g.miny - 10.0, g.maxy + 10.0, 0.05);
+    double2 *d_bp = dev<double2>(S.bp, no);
+    int *d_kept_occ = dev<int>(S.kept_occ, no);
+    const double thr5 = 0.05 * 0.05;
+    const int M = greedy_dedup(G.dedup, d_occ, d_occ_ok, no, kConflictKeyOrSq, thr5, h5, d_bp, d_kept_occ, s, h_sc);
+    G.n_bpts = M;
+
+    // ---- g6 graph edges
+    int *d_keys = dev<int>(S.keys, M), *d_idx = dev<int>(S.idx, M), *d_skeys = dev<int>(S.skeys, M), *d_sidx = dev<int>(S.sidx2, M);
+    k_cell_keys<<<cdiv(M, 256), 256, 0, s>>>(d_bp, M, h5, d_keys, d_idx);
+    {
+        size_t tb = 0;
+        AOS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, d_keys, d_skeys, d_idx, d_sidx, M, 0, 32, s));
+        void *t = S.tmp.ensure(tb);
+        AOS_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, d_keys, d_skeys, d_idx, d_sidx, M, 0, 32, s));
+    }
+    int *d_near = dev<int>(S.near_idx, no);
+    k_nearest<<<cdiv(no, 256), 256, 0, s>>>(d_occ, no, d_bp, M, h5, d_skeys, d_sidx, d_near);
+    const HashG hp = make_hash(g.minx - 10.0, g.maxx + 10.0, g.miny - 10.0, g.maxy + 10.0, 0.5);
+    int *d_pk = dev<int>(S.pk, M), *d_pidx = dev<int>(S.pidx, M), *d_psk = dev<int>(S.pskeys, M), *d_psi = dev<int>(S.psidx, M);
+    k_cell_keys<<<cdiv(M, 256), 256, 0, s>>>(d_bp, M, hp, d_pk, d_pidx);
+    {
+        size_t tb = 0;
+        AOS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, d_pk, d_psk, d_pidx, d_psi, M, 0, 32, s));
+        void *t = S.tmp.ensure(tb);
+        AOS_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, d_pk, d_psk, d_pidx, d_psi, M, 0, 32, s));
+    }
+    int *d_pcount = dev<int>(S.pcount, M + 1), *d_poff = dev<int>(S.poff, M + 1);
+    AOS_HIP(hipMemsetAsync(d_pcount + M, 0, sizeof(int), s));
+    k_pairs<<<cdiv(M, 256), 256, 0, s>>>(d_bp, M, hp, d_psk, d_psi, nullptr, d_pcount, nullptr);
+    scan_excl(S.scan_tmp, d_pcount, d_poff, M + 1, s);
+    AOS_HIP(hipMemcpyAsync(h_sc, d_poff + M, sizeof(int), hipMemcpyDeviceToHost, s));
+    AOS_HIP(hipStreamSynchronize(s));
+    const int np_ = h_sc[0];
+    int *d_plist = dev<int>(S.plist, np_);
+    k_pairs<<<cdiv(M, 256), 256, 0, s>>>(d_bp, M, hp, d_psk, d_psi, d_poff, nullptr, d_plist);
+    const int nc = ne + np_;
+    int2 *d_ft = dev<int2>(S.ft, nc);
+    unsigned long long *d_ck = dev<unsigned long long>(S.ckey, nc);
+    int *d_cv = dev<int>(S.cvalid, nc), *d_pass = dev<int>(S.pass, nc);
+    k_candidates<<<cdiv(nc, 256), 256, 0, s>>>(d_near, ne, d_poff, d_plist, M, np_, d_ft, d_ck, d_cv);
+    k_occupancy<<<cdiv(nc, 64), 64, 0, s>>>(d_ft, d_cv, nc, d_bp, in.d_skeleton, g, d_pass);
+    unsigned long long *d_k2 = dev<unsigned long long>(S.k2, nc), *d_sk2 = dev<unsigned long long>(S.sk2, nc);
+    int *d_oi = dev<int>(S.occ_idx, nc), *d_soi = dev<int>(S.socc, nc);
+    k_pass_keys<<<cdiv(nc, 256), 256, 0, s>>>(d_ck, d_pass, nc, d_k2, d_oi);
+    {
+        size_t tb = 0;
+        AOS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, d_k2, d_sk2, d_oi, d_soi, nc, 0, 64, s));
+        void *t = S.tmp.ensure(tb);
+        AOS_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, d_k2, d_sk2, d_oi, d_soi, nc, 0, 64, s));
+    }
+    int *d_sel = dev<int>(S.selected, nc);
+    AOS_HIP(hipMemsetAsync(d_sel, 0, sizeof(int) * nc, s));
+    k_first_of_key<<<cdiv(nc, 256), 256, 0, s>>>(d_sk2, d_soi, nc, d_sel);
+
+    // ---- g7 filter
+    int *d_in = dev<int>(S.inside, M + 1), *d_ipos = dev<int>(S.ipos, M + 1);
+    AOS_HIP(hipMemsetAsync(d_in + M, 0, sizeof(int), s));
+    k_inside<<<cdiv(M, 256), 256, 0, s>>>(d_bp, M, g, d_in);
+    scan_excl(S.scan_tmp, d_in, d_ipos, M + 1, s);
+    int *d_keep = dev<int>(S.keep, nc + 1), *d_kpos = dev<int>(S.kpos, nc + 1);
+    AOS_HIP(hipMemsetAsync(d_keep + nc, 0, sizeof(int), s));
+    k_edge_keep<<<cdiv(nc, 256), 256, 0, s>>>(d_sel, d_ft, nc, d_in, d_ipos, d_keep);
+    scan_excl(S.scan_tmp, d_keep, d_kpos, nc + 1, s);
+    AOS_HIP(hipMemcpyAsync(h_sc, d_ipos + M, sizeof(int), hipMemcpyDeviceToHost, s));
+    AOS_HIP(hipMemcpyAsync(h_sc + 1, d_kpos + nc, sizeof(int), hipMemcpyDeviceToHost, s));
+    AOS_HIP(hipStreamSynchronize(s));
+    const int Mn = h_sc[0], Ne = h_sc[1];
+    double2 *d_nodes = dev<double2>(S.nodes, Mn);
+    k_gather_nodes<<<cdiv(M, 256), 256, 0, s>>>(d_bp, d_in, d_ipos, M, d_nodes);
+    int *d_edges = dev<int>(S.edges, 2 * (size_t)Ne);
+    float *d_lens = dev<float>(S.lens, Ne);
+    k_edge_emit<<<cdiv(nc, 256), 256, 0, s>>>(d_keep, d_kpos, d_ft, nc, d_ipos, d_nodes, d_edges, d_lens);
+
+    // ---- g8 label points for the exploration rows (gvd:130-150, 485-556)
+    std::vector<LabelRow> jobs;
+    const int nrows = in.n_rows_poses / 2;
+    if (Mn > 0) {
+        for (int r = 0; r < nrows; ++r) {
+            double sx = in.rows_info[4 * r], sy = in.rows_info[4 * r + 1], ex = in.rows_info[4 * r + 2], ey = in.rows_info[4 * r + 3];
+            if (sx > ex) { std::swap(sx, ex); std::swap(sy, ey); }
+            // castRay angle terms (gvd:574-581): +90 -> cos(a), sin(a); -90 -> cos(-a), sin(-a)
+            const double am = -90.0 * M_PI / 180.0, ap = 90.0 * M_PI / 180.0;
+            const double cm = std::cos(-am), sm = std::sin(-am), cp = std::cos(ap), sp = std::sin(ap);
+            jobs.push_back({sx, sy, ex, ey, -90.0, cm, sm});
+            jobs.push_back({sx, sy, ex, ey, 90.0, cp, sp});
+            jobs.push_back({ex, ey, sx, sy, -90.0, cm, sm});
+            jobs.push_back({ex, ey, sx, sy, 90.0, cp, sp});
+        }
+    }
+    const int nj = (int)jobs.size();
+    double2 *d_lp = dev<double2>(S.lpts, nj);
+    int *d_lv = dev<int>(S.lval, nj);
+    if (nj) {
+        LabelRow *d_jobs = dev<LabelRow>(S.jobs, nj);
+        AOS_HIP(hipMemcpyAsync(d_jobs, jobs.data(), sizeof(LabelRow) * nj, hipMemcpyHostToDevice, s));
+        k_label_points<<<nj, 256, 0, s>>>(d_jobs, nj, d_nodes, Mn, g, in.d_skeleton, d_lp, d_lv);
+    }
+    // ---- g9 node labels
+    int *d_mask = dev<int>(S.lmask, Mn), *d_cidx = dev<int>(S.lcidx, Mn), *d_lcnt = dev<int>(S.lcount, Mn + 1),
+        *d_loff = dev<int>(S.loff, Mn + 1);
+    const int nlr = nj / 4;
+    int n_entries = 0;
+    if (Mn > 0) {
+        AOS_HIP(hipMemsetAsync(d_lcnt + Mn, 0, sizeof(int), s));
+        k_node_labels<<<cdiv(Mn, 256), 256, 0, s>>>(d_nodes, Mn, d_lp, d_lv, nlr, d_mask, d_cidx, d_lcnt, nullptr, nullptr, nullptr);
+        scan_excl(S.scan_tmp, d_lcnt, d_loff, Mn + 1, s);
+        AOS_HIP(hipMemcpyAsync(h_sc, d_loff + Mn, sizeof(int), hipMemcpyDeviceToHost, s));
+        AOS_HIP(hipStreamSynchronize(s));
+        n_entries = h_sc[0];
+    }
+    int *d_lcl = dev<int>(S.lcl, n_entries), *d_lty = dev<int>(S.lty, n_entries);
+    if (n_entries) k_node_labels<<<cdiv(Mn, 256), 256, 0, s>>>(d_nodes, Mn, d_lp, d_lv, nlr, nullptr, nullptr, nullptr, d_loff, d_lcl, d_lty);
+
+    // ---- outputs
+    G.nodes_xy.resize(2 * (size_t)Mn); G.labels.resize(Mn); G.cluster_idx.resize(Mn); G.label_counts.resize(Mn);
+    G.label_clusters.resize(n_entries); G.label_types.resize(n_entries);
+    G.edges_out.resize(2 * (size_t)Ne); G.lengths.resize(Ne); G.clearances.assign(Ne, 0.0f);
+    if (Mn) {
+        AOS_HIP(hipMemcpyAsync(G.nodes_xy.data(), d_nodes, sizeof(double2) * Mn, hipMemcpyDeviceToHost, s));
+        AOS_HIP(hipMemcpyAsync(G.labels.data(), d_mask, sizeof(int) * Mn, hipMemcpyDeviceToHost, s));
+        AOS_HIP(hipMemcpyAsync(G.cluster_idx.data(), d_cidx, sizeof(int) * Mn, hipMemcpyDeviceToHost, s));
+        AOS_HIP(hipMemcpyAsync(G.label_counts.data(), d_lcnt, sizeof(int) * Mn, hipMemcpyDeviceToHost, s));
+    }
+    if (n_entries) {
+        AOS_HIP(hipMemcpyAsync(G.label_clusters.data(), d_lcl, sizeof(int) * n_entries, hipMemcpyDeviceToHost, s));
+        AOS_HIP(hipMemcpyAsync(G.label_types.data(), d_lty, sizeof(int) * n_entries, hipMemcpyDeviceToHost, s));
+    }
+    if (Ne) {
+        AOS_HIP(hipMemcpyAsync(G.edges_out.data(), d_edges, sizeof(int) * 2 * Ne, hipMemcpyDeviceToHost, s));
+        AOS_HIP(hipMemcpyAsync(G.lengths.data(), d_lens, sizeof(float) * Ne, hipMemcpyDeviceToHost, s));
+    }
+    AOS_HIP(hipEventRecord(ev[9], s));
+    AOS_HIP(hipStreamSynchronize(s));
+    float a = 0, b = 0;
+    (void)hipEventElapsedTime(&a, ev[6], ev[7]);
+    (void)hipEventElapsedTime(&b, ev[8], ev[9]);
+    G.ms_merge = a; G.ms_graph = b;
+    (void)hipEventElapsedTime(&G.ms_total, ev[6], ev[9]);
+    return true;
+}
+
+}  // namespace aos
+
+// ------------------------------------------------------------------ handle methods
+using namespace aos;
+
+static void fill_gvd_out(const aos_ctx &c, const GvdState &G, const aos_grid_info &info, bool published, aos_gvd_out &out) {
+    std::memset(&out, 0, sizeof(out));
+    out.published = published ? 1 : 0;
+    out.resolution = info.resolution;  // GvdGraph.resolution = skeleton info.resolution (gvd:903)
+    out.origin_x = info.origin_x; out.origin_y = info.origin_y;
+    out.num_nodes = (int32_t)G.labels.size();
+    out.num_edges = (int32_t)G.lengths.size();
+    out.nodes_xy = G.nodes_xy.data();
+    out.node_labels = G.labels.data(); out.node_cluster_indices = G.cluster_idx.data();
+    out.node_label_counts = G.label_counts.data();
+    out.n_label_entries = (int32_t)G.label_clusters.size();
+    out.node_label_clusters = G.label_clusters.data(); out.node_label_types = G.label_types.data();
+    out.edges = G.edges_out.data(); out.edge_lengths = G.lengths.data(); out.edge_clearances = G.clearances.data();
+    out.n_merged_seeds = G.n_merged; out.n_voronoi_edges = G.n_vor_edges; out.n_boundary_points = G.n_bpts;
+    out.ms_merge = G.ms_merge; out.ms_delaunay = G.ms_delaunay; out.ms_graph = G.ms_graph; out.ms_total = G.ms_total;
+    (void)c;
+}
+
+void aos_ctx::run_gvd_external(const aos_gvd_in &in, aos_gvd_out &out) {
+    const size_t C = (size_t)in.info.width * in.info.height;
+    int8_t *d_sk = static_cast<int8_t *>(gs.skel.ensure(std::max<size_t>(C, 1)));
+    if (C && in.skeleton) AOS_HIP(hipMemcpyAsync(d_sk, in.skeleton, C, hipMemcpyHostToDevice, stream));
+    GvdStageIn gi{in.seeds_xy, in.n_seeds, in.rows_info_xy, in.n_rows_poses, in.info, d_sk};
+    const bool pub = run_gvd_stage(gs, P, gi, stream, ev.data());
+    fill_gvd_out(*this, gs, in.info, pub, out);
+}
+
+void aos_ctx::run_gvd_from_frame(aos_gvd_out &out) {
+    aos_grid_info info{geom.origin_x, geom.origin_y, geom.res, (uint32_t)geom.W, (uint32_t)geom.H};
+    GvdStageIn gi{h_voronoi.data(), (int)(h_voronoi.size() / 2), h_rows_info.data(), (int)(h_rows_info.size() / 2), info,
+                  skel_bytes.as<int8_t>()};
+    const bool pub = run_gvd_stage(gs, P, gi, stream, ev.data());
+    fill_gvd_out(*this, gs, info, pub, out);
+}

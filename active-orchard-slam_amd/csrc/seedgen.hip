@@ -1,0 +1,265 @@
+// Seed-gen frame orchestration (AosSeedGenNode::processPointCloud, seed_gen:452-579) on one
+// HIP stream. Host work is limited to launch geometry derived from the polygon (a few scalars);
+// every per-point / per-cell stage runs on the GPU.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "aos_ctx.h"
+
+using namespace aos;
+
+void aos_ctx::release() {
+    for (DevBuf *b : {&cloud_copy, &bin_count, &bin_start, &pt_binslot, &sorted, &scan_tmp, &counters, &raster_bytes,
+                      &raster_bits, &infl_bits, &open_bits, &thin_a, &thin_b, &occ_bytes, &skel_bytes, &flags})
+        b->release();
+    h_small.release();
+    for (DevBuf *b : {&cs.fg_bits, &cs.word_cnt, &cs.word_off, &cs.fg_list, &cs.parent, &cs.root_flag, &cs.root_rank,
+                      &cs.cl_count, &cs.cl_off, &cs.cl_cursor, &cs.cl_cells, &cs.rec, &cs.row_idx, &cs.bfs_queue,
+                      &cs.bfs_vis, &cs.poly, &cs.cand_xy, &cs.cand_ok, &cs.cand_state, &cs.hash_count,
+                      &cs.hash_start, &cs.hash_slot, &cs.hash_sorted, &cs.seed_out, &cs.misc, &cs.scan_tmp})
+        b->release();
+    cs.h_misc.release();
+    free_gvd_scratch(gs);
+    for (DevBuf *b : {&gs.seeds, &gs.merge_state, &gs.hash_count, &gs.hash_start, &gs.hash_slot, &gs.hash_sorted,
+                      &gs.scan_tmp, &gs.edges, &gs.bpts, &gs.near_idx, &gs.cand, &gs.cand_ok, &gs.skel,
+                      &gs.grid_bytes_ext})
+        b->release();
+    gs.h_misc.release();
+}
+
+void aos_ctx::set_cloud(const aos_cloud_view &v) {
+    n_points = v.n_points;
+    step = v.point_step; ox = v.off_x; oy = v.off_y; oz = v.off_z;
+    is_dense = v.is_dense ? 1 : 0;
+    if (v.on_device) {
+        d_cloud = static_cast<const uint8_t *>(v.data);
+    } else {
+        size_t bytes = (size_t)n_points * step;
+        void *dst = cloud_copy.ensure(std::max<size_t>(bytes, 16));
+        if (bytes) AOS_HIP(hipMemcpyAsync(dst, v.data, bytes, hipMemcpyHostToDevice, stream));
+        d_cloud = cloud_copy.as<uint8_t>();
+    }
+    have_cloud = true;
+}
+
+// getActiveBounds (seed_gen:874-890) + generateOccupancyGrid geometry (:584-600)
+static FrameGeom frame_geom(const Poly &poly, const aos_params &P) {
+    FrameGeom g{};
+    double hminx = poly[0].first, hmaxx = poly[0].first, hminy = poly[0].second, hmaxy = poly[0].second;
+    for (const auto &pt : poly) {
+        hminx = std::min(hminx, pt.first); hmaxx = std::max(hmaxx, pt.first);
+        hminy = std::min(hminy, pt.second); hmaxy = std::max(hmaxy, pt.second);
+    }
+    const double margin = 2.5;
+    g.minx = static_cast<float>(hminx - margin); g.maxx = static_cast<float>(hmaxx + margin);
+    g.miny = static_cast<float>(hminy - margin); g.maxy = static_cast<float>(hmaxy + margin);
+    g.res = P.grid_resolution;
+    float width = std::max(0.0f, g.maxx - g.minx), height = std::max(0.0f, g.maxy - g.miny);
+    unsigned int w = static_cast<unsigned int>(std::ceil(width / g.res));
+    unsigned int h = static_cast<unsigned int>(std::ceil(height / g.res));
+    if (w == 0) w = 1;
+    if (h == 0) h = 1;
+    g.W = (int)w; g.H = (int)h; g.WW = (g.W + 63) / 64;
+    g.origin_x = g.minx; g.origin_y = g.miny;
+    g.R = static_cast<int>(P.inflation_radius / P.grid_resolution);  // applyInflation seed_gen:936
+    return g;
+}
+
+void aos_ctx::run_seedgen(bool want_host, aos_seedgen_out &out) {
+    std::memset(&out, 0, sizeof(out));
+    const FrameGeom g = frame_geom(poly, P);
+    geom = g;
+    if (g.R > 63) throw std::runtime_error("inflation radius > 63 cells is not supported by the bit-packed kernel");
+    if ((size_t)g.W * g.H > (size_t)1 << 31) throw std::runtime_error("grid larger than 2^31 cells");
+    hipStream_t s = stream;
+    const size_t C = (size_t)g.W * g.H, Cw = (size_t)g.WW * g.H;
+    AOS_HIP(hipEventRecord(ev[0], s));
+
+    // ---------------- a1-a4: ROR restricted to the clip box, clip, exclusion discs, raster
+    RorLaunch L{};
+    L.cloud = d_cloud; L.n = n_points; L.step = step; L.ox = ox; L.oy = oy; L.oz = oz; L.is_dense = is_dense;
+    L.cminx = g.minx; L.cmaxx = g.maxx; L.cminy = g.miny; L.cmaxy = g.maxy;
+    L.cminz = P.clipping_minz; L.cmaxz = P.clipping_maxz;
+    const float m = (float)(P.ror_radius * 1.01) + 1e-4f;
+    L.bminx = L.cminx - m; L.bmaxx = L.cmaxx + m; L.bminy = L.cminy - m; L.bmaxy = L.cmaxy + m;
+    L.bminz = L.cminz - m; L.bmaxz = L.cmaxz + m;
+    float cs_ = (float)(P.ror_radius * 1.001);
+    const double ext = std::max((double)L.bmaxx - L.bminx, (double)L.bmaxy - L.bminy);
+    if (ext / cs_ > 8192.0) cs_ = (float)(ext / 8192.0);  // cap the bin grid; coarser bins stay exact
+    L.inv_cs = 1.0f / cs_;
+    L.nbx = (int)((L.bmaxx - L.bminx) * L.inv_cs) + 1;
+    L.nby = (int)((L.bmaxy - L.bminy) * L.inv_cs) + 1;
+    L.r2 = P.ror_radius * P.ror_radius;
+    L.r2f = (float)(P.ror_radius * P.ror_radius);
+    L.need = P.ror_min_neighbors + 1;
+    L.origin_x = g.origin_x; L.origin_y = g.origin_y; L.res = g.res; L.W = g.W; L.H = g.H;
+    const int nb = L.nbx * L.nby;
+
+    int *d_bc = static_cast<int *>(bin_count.ensure(sizeof(int) * (nb + 1)));
+    int *d_bs = static_cast<int *>(bin_start.ensure(sizeof(int) * (nb + 1)));
+    int2 *d_ps = static_cast<int2 *>(pt_binslot.ensure(sizeof(int2) * std::max<uint64_t>(n_points, 1)));
+    unsigned long long *d_cnt = static_cast<unsigned long long *>(counters.ensure(64));
+    uint8_t *d_rb = static_cast<uint8_t *>(raster_bytes.ensure(C));
+    size_t st = scan_temp_bytes(nb + 1);
+    void *d_st = scan_tmp.ensure(st);
+    AOS_HIP(hipMemsetAsync(d_bc, 0, sizeof(int) * (nb + 1), s));
+    AOS_HIP(hipMemsetAsync(d_cnt, 0, 64, s));
+    AOS_HIP(hipMemsetAsync(d_rb, 0, C, s));
+    // PCL dense kNN needs k = min_pts + 1 points in the whole cloud (else every point is removed)
+    const bool any = n_points > 0 && !(is_dense && n_points < (uint64_t)L.need);
+    if (any) {
+        launch_ror_bin(L, d_bc, d_ps, s);
+        launch_exclusive_scan(d_bc, d_bs, nb + 1, d_st, st, s);
+        // total binned = bin_start[nb]; bound the sorted buffer by n_points
+        float4 *d_sorted = static_cast<float4 *>(sorted.ensure(sizeof(float4) * std::max<uint64_t>(n_points, 1)));
+        launch_ror_scatter(L, d_bs, d_ps, d_sorted, s);
+        launch_ror_raster(L, d_bs, d_sorted, d_bs + nb, (int)n_points, d_rb, d_cnt, s);
+    }
+    AOS_HIP(hipEventRecord(ev[1], s));
+
+    // ---------------- a5 inflation, a6 frame -> /occupancy_grid
+    uint64_t *d_rbits = static_cast<uint64_t *>(raster_bits.ensure(Cw * 8));
+    uint64_t *d_ibits = static_cast<uint64_t *>(infl_bits.ensure(Cw * 8));
+    int8_t *d_occ = static_cast<int8_t *>(occ_bytes.ensure(C));
+    launch_pack_bits(d_rb, d_rbits, g.W, g.H, g.WW, s);
+    launch_inflate(d_rbits, d_ibits, g, s);
+    launch_bits_to_bytes(d_ibits, d_occ, g, 5, s);
+    AOS_HIP(hipEventRecord(ev[2], s));
+
+    // ---------------- a7 opening + Zhang-Suen (temporal blocks of kThinItersPerLaunch iterations)
+    uint64_t *d_open = static_cast<uint64_t *>(open_bits.ensure(Cw * 8));
+    uint64_t *bufs[2] = {static_cast<uint64_t *>(thin_a.ensure(Cw * 8)), static_cast<uint64_t *>(thin_b.ensure(Cw * 8))};
+    const int K = kThinItersPerLaunch;
+    const int max_iters = std::max(g.W, g.H) + 4;   // Zhang-Suen removes >= 1 cell per changing iteration
+    int *d_flags = static_cast<int *>(flags.ensure(sizeof(int) * (2 + max_iters + K)));
+    AOS_HIP(hipMemsetAsync(d_flags, 0, sizeof(int) * (2 + max_iters + K), s));
+    launch_open(d_ibits, d_open, g, s);
+    int launched = 0;
+    const uint64_t *src = d_open;
+    int *h_flags = static_cast<int *>(h_small.ensure(sizeof(int) * (2 + max_iters + K)));
+    const uint64_t *final_buf = d_open;
+    int T = 0;
+    for (int batch = 0;; ++batch) {
+        const int per_batch = batch == 0 ? 3 : 4;   // typical T <= 24 needs one round trip
+        for (int j = 0; j < per_batch; ++j) {
+            uint64_t *dst = bufs[launched & 1];
+            launch_thin_block(src, dst, g, launched * K, d_flags, s);
+            src = dst;
+            ++launched;
+        }
+        AOS_HIP(hipMemcpyAsync(h_flags, d_flags, sizeof(int) * (1 + launched * K), hipMemcpyDeviceToHost, s));
+        AOS_HIP(hipStreamSynchronize(s));
+        // T: stop after iteration 1 if the image is empty, else after the first iteration
+        // (k >= 2, 1-based) that deletes nothing (ximgproc thinning loop with prev = zeros).
+        T = 0;
+        if (!h_flags[0]) T = 1;
+        else
+            for (int k = 1; k < launched * K; ++k)
+                if (!h_flags[1 + k]) { T = k + 1; break; }
+        if (T) {
+            // the last launch that ran: launch j runs iff j == 0 or iteration j*K-1 deleted something
+            int last = 0;
+            for (int j = 1; j < launched; ++j)
+                if (h_flags[1 + j * K - 1]) last = j; else break;
+            final_buf = bufs[last & 1];
+            break;
+        }
+        if (launched * K > max_iters) throw std::runtime_error("thinning did not converge");
+    }
+    thin_iters = T;
+    skel_bits = final_buf;
+    AOS_HIP(hipEventRecord(ev[3], s));
+
+    // ---------------- a16 /skeletonized_occupancy_grid = skeleton + polygon bbox rectangle
+    int8_t *d_skel = static_cast<int8_t *>(skel_bytes.ensure(C));
+    launch_bits_to_bytes(skel_bits, d_skel, g, 0, s);
+    {
+        double hminx = poly[0].first, hmaxx = poly[0].first, hminy = poly[0].second, hmaxy = poly[0].second;
+        for (const auto &pt : poly) {
+            hminx = std::min(hminx, pt.first); hmaxx = std::max(hmaxx, pt.first);
+            hminy = std::min(hminy, pt.second); hmaxy = std::max(hmaxy, pt.second);
+        }
+        const double margin = 2.5;
+        auto w2g = [&](float wx, float wy, int &gx, int &gy) {  // worldToGrid seed_gen:760-769
+            float rel_x = (wx - g.origin_x) / g.res;
+            float rel_y = (wy - g.origin_y) / g.res;
+            gx = static_cast<int>(std::floor(rel_x)); gy = static_cast<int>(std::floor(rel_y));
+            gx = gx < 0 ? 0 : (gx >= g.W ? g.W - 1 : gx);
+            gy = gy < 0 ? 0 : (gy >= g.H ? g.H - 1 : gy);
+        };
+        int gx0, gy0, gx1, gy1;
+        w2g(static_cast<float>(hminx - margin), static_cast<float>(hminy - margin), gx0, gy0);
+        w2g(static_cast<float>(hmaxx + margin), static_cast<float>(hmaxy + margin), gx1, gy1);
+        launch_draw_rect(d_skel, g, gx0, gy0, gx1, gy1, s);
+    }
+
+    // ---------------- a8-a15 clusters, tree rows, seeds
+    SeedStageIn sin{skel_bits, &geom, &poly, P.cluster_min_length};
+    SeedStageOut so;
+    run_cluster_seed_stage(cs, sin, so, s, ev[4]);
+    AOS_HIP(hipEventRecord(ev[5], s));
+
+    unsigned long long h_cnt = 0;
+    AOS_HIP(hipMemcpyAsync(&h_cnt, d_cnt, sizeof(h_cnt), hipMemcpyDeviceToHost, s));
+    if (want_host) {
+        h_occ.resize(C); h_skel.resize(C);
+        AOS_HIP(hipMemcpyAsync(h_occ.data(), d_occ, C, hipMemcpyDeviceToHost, s));
+        AOS_HIP(hipMemcpyAsync(h_skel.data(), d_skel, C, hipMemcpyDeviceToHost, s));
+    }
+    AOS_HIP(hipStreamSynchronize(s));
+    n_clipped = h_cnt;
+    have_frame = true;
+
+    h_row_center = std::move(so.row_center); h_row_start = std::move(so.row_start);
+    h_row_end = std::move(so.row_end); h_row_length = std::move(so.row_length);
+    n_virtual = (int)so.virtual_xy.size() / 2; n_ray = (int)so.ray_xy.size() / 2; n_endpoint = (int)so.endpoint_xy.size() / 2;
+    h_voronoi.clear();
+    h_voronoi.insert(h_voronoi.end(), so.virtual_xy.begin(), so.virtual_xy.end());
+    h_voronoi.insert(h_voronoi.end(), so.ray_xy.begin(), so.ray_xy.end());
+    h_voronoi.insert(h_voronoi.end(), so.endpoint_xy.begin(), so.endpoint_xy.end());
+    h_rows_info = std::move(so.rows_info);
+    h_cluster_info = std::move(so.cluster_info);
+    n_clusters_all = so.n_clusters_all;
+
+    out.info = aos_grid_info{g.origin_x, g.origin_y, g.res, (uint32_t)g.W, (uint32_t)g.H};
+    out.thin_iters = thin_iters;
+    out.n_input = n_points;
+    out.n_clipped = n_clipped;
+    out.n_ror_kept = 0;  // not materialised (ROR is evaluated only where it can reach the grid)
+    out.occupancy = want_host ? h_occ.data() : nullptr;
+    out.skeleton = want_host ? h_skel.data() : nullptr;
+    out.d_occupancy = d_occ;
+    out.d_skeleton = d_skel;
+    out.n_clusters_all = n_clusters_all;
+    out.n_rows = (int)h_row_length.size();
+    out.row_center = h_row_center.data(); out.row_start = h_row_start.data();
+    out.row_end = h_row_end.data(); out.row_length = h_row_length.data();
+    out.n_virtual = n_virtual; out.n_ray = n_ray; out.n_endpoint = n_endpoint;
+    out.n_voronoi = (int)h_voronoi.size() / 2;
+    out.voronoi_xy = h_voronoi.data();
+    out.rows_info_xy = h_rows_info.data();
+    out.n_cluster_info = (int)h_cluster_info.size() / 2;
+    out.cluster_info_xy = h_cluster_info.data();
+    auto ms = [&](int a, int b) { float t = 0; (void)hipEventElapsedTime(&t, ev[a], ev[b]); return t; };
+    out.ms_ror = ms(0, 1); out.ms_grid = ms(1, 2); out.ms_thin = ms(2, 3); out.ms_cluster = ms(3, 4);
+    out.ms_seeds = ms(4, 5); out.ms_total = ms(0, 5);
+}
+
+int aos_ctx::debug_grid(const char *which, int8_t *dst, uint64_t capacity) {
+    const size_t C = (size_t)geom.W * geom.H;
+    if (capacity < C) { set_error("aos_debug_grid: capacity < width*height"); return AOS_E_INVALID; }
+    const uint64_t *bits = nullptr;
+    if (!std::strcmp(which, "raster")) bits = raster_bits.as<uint64_t>();
+    else if (!std::strcmp(which, "inflated")) bits = infl_bits.as<uint64_t>();
+    else if (!std::strcmp(which, "opened")) bits = open_bits.as<uint64_t>();
+    else if (!std::strcmp(which, "skeleton_frameless")) bits = skel_bits;
+    else { set_error(std::string("aos_debug_grid: unknown grid ") + which); return AOS_E_INVALID; }
+    DevBuf tmp;
+    int8_t *d = static_cast<int8_t *>(tmp.ensure(C));
+    launch_bits_to_bytes(bits, d, geom, 0, stream);
+    AOS_HIP(hipMemcpyAsync(dst, d, C, hipMemcpyDeviceToHost, stream));
+    AOS_HIP(hipStreamSynchronize(stream));
+    tmp.release();
+    return AOS_OK;
+}

@@ -1,0 +1,58 @@
+// Incremental Delaunay / Voronoi facets with OpenCV 4.5.4 cv::Subdiv2D semantics
+// (modules/imgproc/src/subdivision2d.cpp, used by aos::VoronoiDiagram::compute,
+// src/utils/voronoi_diagram.cpp:51-94).
+//
+// Why on the host: insertion is inherently sequential and history-dependent — the quad-edge
+// numbering, vtx[].firstEdge (which decides where each facet starts) and which edge pair computes
+// each circumcentre (float rounding) all depend on the exact locate walk and flip order. GvdGraph
+// node numbering follows that order, so bit-identical topology needs this exact replay; the
+// GPU takes over from the facet list on (boundary points, graph, labels).
+//
+// Layout: structure-of-arrays quad-edges (next[4], pt[4] as flat int arrays), float points.
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+namespace aos {
+
+class Subdiv2D {
+  public:
+    // rect: Subdiv2D(Rect2f) (mode 0) or the implicit Rect2f -> Rect conversion (mode 1)
+    void init_delaunay(float rx, float ry, float rw, float rh, int rect_mode);
+    // Subdiv2D::insert; returns false where OpenCV throws (the reference catches and skips).
+    bool insert(float x, float y);
+    // getVoronoiFacetList(idx = {}): per real vertex (in vertex order) the facet polygon.
+    // Emits the reference's edge list directly: (p_i, p_{i+1 mod n}) for facets with >= 2 points
+    // (voronoi_diagram.cpp:97-114), as float x0, y0, x1, y1.
+    void voronoi_edges(std::vector<float> &edges);
+    size_t num_vertices() const { return vx.size(); }
+
+  private:
+    enum { NEXT_AROUND_LEFT = 0x13, NEXT_AROUND_RIGHT = 0x31, PREV_AROUND_ORG = 0x11, PREV_AROUND_DST = 0x33 };
+    // vertices
+    std::vector<float> vx, vy;
+    std::vector<int> vfirst, vtype;   // type: -1 free, 0 real, 1 virtual
+    // quad-edges: 4 rotations each
+    std::vector<int> qnext, qpt;      // size 4 * nquad
+    int free_q = 0, free_p = 0, recent = 0;
+    float tlx = 0, tly = 0, brx = 0, bry = 0;
+
+    int next_e(int e) const { return qnext[e]; }
+    static int rot(int e, int r) { return (e & ~3) + ((e + r) & 3); }
+    int get_e(int e, int t) const { e = qnext[(e & ~3) + ((e + t) & 3)]; return (e & ~3) + ((e + (t >> 4)) & 3); }
+    int org(int e) const { return qpt[e]; }
+    int dst(int e) const { return qpt[(e & ~3) + ((e + 2) & 3)]; }
+    int right_of(float px, float py, int e) const;
+    int new_edge();
+    int new_point(float x, float y, int type);
+    void splice(int a, int b);
+    void set_pts(int e, int o, int d);
+    int connect(int a, int b);
+    void swap_edge(int e);
+    void delete_edge(int e);
+    int locate(float px, float py, int &edge, int &vertex);
+    void calc_voronoi();
+};
+
+}  // namespace aos

@@ -1,0 +1,148 @@
+/*
+ * aos_gpu.h — C ABI of libaos_gpu.so, the MI355X (gfx950) implementation of the AOS
+ * seed-gen + GVD hot path.
+ *
+ * The reference has no plugin/FFI boundary: the path is two rclcpp nodes wired by topics.
+ * Each entry point below replaces one reference callback; the rclcpp drop-in wrapper
+ * (active-orchard-slam_amd/node/) maps the same topics, QoS and parameter
+ * names onto these calls.
+ *
+ *   aos_seedgen_process   <- AosSeedGenNode::globalMapCallback   src/aos_seed_gen_node.cpp:230-248
+ *   aos_set_polygon       <- AosSeedGenNode::explorationAreaCallback (polygon part) :250-277
+ *   aos_seedgen_reprocess <- explorationAreaCallback -> processPointCloud(last_cloud) :282-285
+ *   aos_gvd_process       <- AosGvdNode::processGraph on the settled inputs of
+ *                            voronoiSeedsCallback :84-128, explorationTreeRowsInfoCallback :130-150,
+ *                            skeletonizedGridCallback :173-177  (src/aos_gvd_node.cpp:255-318)
+ *   aos_gvd_from_seedgen  <- the same, fed directly from this handle's last seed-gen frame
+ *                            (device-resident, no serialisation) — the fused pipeline.
+ *
+ * Conventions
+ *  - Plain C types only; no torch / HIP types cross this boundary.
+ *  - Status: 0 = OK, < 0 = error (AOS_E_*); aos_last_error() returns a thread-local message.
+ *    No C++ exception crosses the ABI. Empty input -> empty outputs with status 0, mirroring the
+ *    reference's early returns (gvd:257-259, 273-275, 284-287).
+ *  - Inputs are caller-owned and only read during the call. Output arrays are library-owned and
+ *    valid until the next call on the same handle or aos_destroy.
+ *  - One handle = one device + one HIP stream; a handle is not re-entrant, different handles may
+ *    run concurrently (one per GPU).
+ *  - There is no CPU fallback: without a usable gfx950 device aos_create fails.
+ */
+#ifndef AOS_GPU_H
+#define AOS_GPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AOS_OK 0
+#define AOS_E_INVALID -1
+#define AOS_E_NOMEM -2
+#define AOS_E_HIP -3
+#define AOS_E_STATE -4
+#define AOS_E_RCCL -5
+
+/* Parameters: names and defaults of the reference nodes (seed_gen:69-100, gvd:26,
+ * config/aos_planner_params.yaml:55-89). */
+typedef struct aos_params {
+    float clipping_minz, clipping_maxz;      /* -0.4, 0.5  (seed-gen node override)     */
+    float clipping_minx, clipping_maxx;      /* -5, 72    (only used without polygon)   */
+    float clipping_miny, clipping_maxy;      /* -10, 20                                  */
+    float grid_resolution;                   /* 0.05                                     */
+    float inflation_radius;                  /* 0.8                                      */
+    double cluster_min_length;               /* 2.0                                      */
+    double ror_radius;                       /* 0.2 (hard-coded, seed_gen:238)           */
+    int32_t ror_min_neighbors;               /* 2   (hard-coded, seed_gen:239)           */
+    int32_t subdiv_rect_mode;                /* 0: Subdiv2D(Rect2f); 1: Rect2f->Rect      */
+    double max_graph_publish_rate;           /* 10 Hz (throttle is the wrapper's job)    */
+} aos_params;
+
+void aos_default_params(aos_params *p);
+
+typedef struct aos_ctx aos_ctx;
+
+/* PointCloud2 view (fields x, y, z float32 at the given byte offsets). */
+typedef struct aos_cloud_view {
+    const void *data;        /* n_points * point_step bytes                                   */
+    uint64_t n_points;
+    uint32_t point_step, off_x, off_y, off_z;
+    int32_t is_dense;        /* PointCloud2.is_dense: selects PCL's kNN vs radius ROR branch   */
+    int32_t on_device;       /* 1: data is a device pointer on this handle's GPU (no H2D copy) */
+} aos_cloud_view;
+
+/* OccupancyGrid.info subset. */
+typedef struct aos_grid_info {
+    double origin_x, origin_y;
+    float resolution;
+    uint32_t width, height;
+} aos_grid_info;
+
+/* Seed-gen frame outputs. Host arrays are filled only when want_host != 0 (aos_seedgen_process
+ * argument); device arrays are always valid (HBM, library-owned). */
+typedef struct aos_seedgen_out {
+    aos_grid_info info;
+    int32_t thin_iters;                  /* Zhang-Suen iterations incl. the final no-change pass */
+    uint64_t n_input, n_ror_kept, n_clipped;
+    /* grids, int8 {0,100}, row-major x + y*width */
+    const int8_t *occupancy;             /* /occupancy_grid (inflated + 5-cell frame)            */
+    const int8_t *skeleton;              /* /skeletonized_occupancy_grid (with polygon frame)    */
+    const int8_t *d_occupancy, *d_skeleton;
+    /* clusters after the length filter, discovery order */
+    int32_t n_clusters_all;              /* before the length filter                             */
+    int32_t n_rows;                      /* tree rows (all_tree_rows order)                      */
+    const double *row_center, *row_start, *row_end, *row_length;  /* 2, 2, 2, 1 per row         */
+    /* /voronoi_seeds = virtual ++ real(empty) ++ ray ++ endpoint seeds (x, y) */
+    int32_t n_virtual, n_ray, n_endpoint, n_voronoi;
+    const double *voronoi_xy;
+    /* /exploration_tree_rows_info: sorted (start.x, start.y, end.x, end.y) per row */
+    const double *rows_info_xy;
+    /* /cluster_info: exploration cluster centres sorted by y */
+    int32_t n_cluster_info;
+    const double *cluster_info_xy;
+    /* per-stage device time (ms), HIP events */
+    float ms_ror, ms_grid, ms_thin, ms_cluster, ms_seeds, ms_total;
+} aos_seedgen_out;
+
+/* GVD inputs when not fed from this handle's seed-gen frame. */
+typedef struct aos_gvd_in {
+    const double *seeds_xy; int32_t n_seeds;          /* /voronoi_seeds poses (x, y)            */
+    const double *rows_info_xy; int32_t n_rows_poses;  /* /exploration_tree_rows_info poses      */
+    aos_grid_info info;
+    const int8_t *skeleton;                            /* /skeletonized_occupancy_grid data      */
+} aos_gvd_in;
+
+/* msg/GvdGraph.msg fields. */
+typedef struct aos_gvd_out {
+    int32_t published;                   /* 0 when processGraph returns early                   */
+    double resolution, origin_x, origin_y;
+    int32_t num_nodes, num_edges;
+    const double *nodes_xy;
+    const int32_t *node_labels, *node_cluster_indices, *node_label_counts;
+    int32_t n_label_entries;
+    const int32_t *node_label_clusters, *node_label_types;
+    const int32_t *edges;                /* 2 per edge                                          */
+    const float *edge_lengths, *edge_clearances;
+    int32_t n_merged_seeds, n_voronoi_edges, n_boundary_points;
+    float ms_merge, ms_delaunay, ms_graph, ms_total;
+} aos_gvd_out;
+
+const char *aos_last_error(void);
+int aos_create(const aos_params *p, int device, aos_ctx **out);
+void aos_destroy(aos_ctx *ctx);
+int aos_set_polygon(aos_ctx *ctx, const double *xy, uint32_t n_points);  /* n < 3: ignored (:253) */
+int aos_seedgen_process(aos_ctx *ctx, const aos_cloud_view *cloud, int want_host, aos_seedgen_out *out);
+int aos_seedgen_reprocess(aos_ctx *ctx, int want_host, aos_seedgen_out *out);
+int aos_gvd_process(aos_ctx *ctx, const aos_gvd_in *in, aos_gvd_out *out);
+int aos_gvd_from_seedgen(aos_ctx *ctx, aos_gvd_out *out);
+
+/* Diagnostics: copy an internal device grid of the last frame to host as int8 {0,100} (or 0/1
+ * for "opened"). which: "raster", "inflated", "opened", "skeleton_frameless". */
+int aos_debug_grid(aos_ctx *ctx, const char *which, int8_t *dst, uint64_t capacity);
+/* Stream of the handle (hipStream_t as void*) for callers that time with their own events. */
+void *aos_stream(aos_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AOS_GPU_H */

@@ -1,0 +1,134 @@
+"""The product's host Subdiv2D replay (active-orchard-slam_amd/csrc/subdiv2d.cpp) vs the oracle's
+restatement and vs scipy's Delaunay triangulation. CPU-only: the file is plain C++ and is compiled
+here into a throw-away test library (the product .so is not involved)."""
+import ctypes
+import os
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+from scipy.spatial import Delaunay
+
+import oracle_py as O
+import orchard
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "active-orchard-slam_amd", "csrc", "subdiv2d.cpp")
+
+SHIM = r"""
+#include "subdiv2d.h"
+#include <algorithm>
+#include <cmath>
+#include <vector>
+extern "C" int subdiv_edges(const double* s, int n, double minx, double maxx, double miny, double maxy, int mode,
+                            float* out, int cap) {
+    // VoronoiDiagram::compute prologue (voronoi_diagram.cpp:27-89)
+    if (minx > maxx) std::swap(minx, maxx);
+    if (miny > maxy) std::swap(miny, maxy);
+    if (maxx - minx < 1.0) { double c = (minx + maxx) / 2.0; minx = c - 0.5; maxx = c + 0.5; }
+    if (maxy - miny < 1.0) { double c = (miny + maxy) / 2.0; miny = c - 0.5; maxy = c + 0.5; }
+    float rx = (float)(minx - 1.0), ry = (float)(miny - 1.0);
+    float rw = (float)(std::abs(maxx - minx) + 2.0), rh = (float)(std::abs(maxy - miny) + 2.0);
+    aos::Subdiv2D sd;
+    sd.init_delaunay(rx, ry, rw, rh, mode);
+    for (int i = 0; i < n; ++i) {
+        float x = (float)s[2 * i], y = (float)s[2 * i + 1];
+        x = std::max(rx + 0.1f, std::min(rx + rw - 0.1f, x));
+        y = std::max(ry + 0.1f, std::min(ry + rh - 0.1f, y));
+        sd.insert(x, y);
+    }
+    std::vector<float> e;
+    sd.voronoi_edges(e);
+    int m = (int)e.size();
+    for (int i = 0; i < m && i < cap; ++i) out[i] = e[i];
+    return m / 4;
+}
+"""
+
+_lib = None
+
+
+def shim():
+    global _lib
+    if _lib is None:
+        d = tempfile.mkdtemp(prefix="subdiv_shim_")
+        src = os.path.join(d, "shim.cpp")
+        open(src, "w").write(SHIM)
+        so = os.path.join(d, "libshim.so")
+        subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-ffp-contract=off", "-shared",
+                               "-I", os.path.dirname(SRC), "-o", so, src, SRC])
+        _lib = ctypes.CDLL(so)
+        _lib.subdiv_edges.restype = ctypes.c_int
+        _lib.subdiv_edges.argtypes = [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_double] * 4 + [ctypes.c_int, ctypes.c_void_p,
+                                                                                                    ctypes.c_int]
+    return _lib
+
+
+def product_edges(seeds, bounds, mode=0):
+    s = np.ascontiguousarray(seeds, np.float64).reshape(-1)
+    cap = 4 * 12 * max(len(seeds), 16) + 4096
+    out = np.zeros(cap, np.float32)
+    n = shim().subdiv_edges(s.ctypes.data, s.size // 2, *bounds, mode, out.ctypes.data, cap)
+    return out[:4 * n].reshape(-1, 4)
+
+
+def oracle_edges(seeds, bounds, mode=0):
+    facets, _ = O.subdiv_facets(seeds, bounds, mode)
+    e = []
+    for f in facets:
+        if len(f) < 2:
+            continue
+        for i in range(len(f)):
+            e.append(np.concatenate([f[i], f[(i + 1) % len(f)]]))
+    return np.array(e, np.float32).reshape(-1, 4)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_product_subdiv_matches_oracle_on_orchard_seeds(mode):
+    cfg = orchard.CONFIGS["C0"]
+    r = O.seedgen(orchard.generate(cfg), orchard.polygon(cfg), O.default_params(grid_resolution=cfg.res))
+    seeds = r["voronoi_seeds"]
+    b = (r["origin"][0], r["origin"][0] + np.float32(r["width"] * np.float32(r["resolution"])),
+         r["origin"][1], r["origin"][1] + np.float32(r["height"] * np.float32(r["resolution"])))
+    assert np.array_equal(product_edges(seeds, b, mode), oracle_edges(seeds, b, mode))
+
+
+def test_product_subdiv_degenerate_inputs():
+    rng = np.random.default_rng(4)
+    lattice = np.stack(np.meshgrid(np.arange(12.0), np.arange(9.0)), -1).reshape(-1, 2)  # co-circular everywhere
+    dup = np.concatenate([lattice, lattice[:20] + 1e-9])                                  # duplicates (L1 < FLT_EPS)
+    line = np.stack([np.arange(30.0) * 0.7, np.zeros(30)], -1)                            # collinear
+    rnd = rng.uniform(0, 40, size=(500, 2))
+    for pts in (lattice, dup, line, rnd):
+        b = (pts[:, 0].min() - 3, pts[:, 0].max() + 3, pts[:, 1].min() - 3, pts[:, 1].max() + 3)
+        assert np.array_equal(product_edges(pts, b), oracle_edges(pts, b))
+
+
+def test_oracle_subdiv_is_delaunay():
+    """Independent pin of the restatement: every finite facet vertex of an interior seed is the
+    circumcentre of one of scipy's Delaunay triangles around it (general-position random seeds)."""
+    rng = np.random.default_rng(12)
+    pts = rng.uniform(0, 50, size=(400, 2))
+    b = (-5.0, 55.0, -5.0, 55.0)
+    facets, centers = O.subdiv_facets(pts, b)
+    tri = Delaunay(pts)
+    P = pts[tri.simplices]
+    ax, ay, bx, by, cx, cy = P[:, 0, 0], P[:, 0, 1], P[:, 1, 0], P[:, 1, 1], P[:, 2, 0], P[:, 2, 1]
+    d = 2 * (ax * (by - cy) + bx * (cy - ay) + cx * (ay - by))
+    ux = ((ax ** 2 + ay ** 2) * (by - cy) + (bx ** 2 + by ** 2) * (cy - ay) + (cx ** 2 + cy ** 2) * (ay - by)) / d
+    uy = ((ax ** 2 + ay ** 2) * (cx - bx) + (bx ** 2 + by ** 2) * (ax - cx) + (cx ** 2 + cy ** 2) * (bx - ax)) / d
+    # Subdiv2D's finite super-triangle (3 x the rect size away) legitimately alters triangles near
+    # the hull, so only seeds well inside the point set are compared with the true Delaunay.
+    checked = 0
+    for k, (f, c) in enumerate(zip(facets, centers)):
+        i = int(np.argmin(np.abs(pts - c.astype(np.float64)).sum(1)))
+        if not (np.all(pts[i] > 12.0) and np.all(pts[i] < 38.0)):
+            continue
+        own = np.nonzero((tri.simplices == i).any(1))[0]
+        cc = np.stack([ux[own], uy[own]], 1)
+        assert len(f) == len(own)
+        for v in f:
+            assert np.min(np.abs(cc - v).max(1)) < 1e-3
+        checked += 1
+    assert checked > 60
