@@ -42,7 +42,8 @@ class GridInfo(ctypes.Structure):
 class SeedGenOut(ctypes.Structure):
     _fields_ = [("info", GridInfo), ("thin_iters", c_i), ("n_input", c_u64), ("n_ror_kept", c_u64),
                 ("n_clipped", c_u64), ("occupancy", P(ctypes.c_int8)), ("skeleton", P(ctypes.c_int8)),
-                ("d_occupancy", c_vp), ("d_skeleton", c_vp), ("n_clusters_all", c_i), ("n_rows", c_i),
+                ("d_occupancy", c_vp), ("d_skeleton", c_vp), ("n_clusters_all", c_i), ("n_bfs_replayed", c_i),
+                ("n_rows", c_i),
                 ("row_center", P(c_d)), ("row_start", P(c_d)), ("row_end", P(c_d)), ("row_length", P(c_d)),
                 ("n_virtual", c_i), ("n_ray", c_i), ("n_endpoint", c_i), ("n_voronoi", c_i), ("voronoi_xy", P(c_d)),
                 ("rows_info_xy", P(c_d)), ("n_cluster_info", c_i), ("cluster_info_xy", P(c_d)),
@@ -83,6 +84,12 @@ _lib = None
 def lib():
     global _lib
     if _lib is None:
+        # torch (if present) bundles its own libamdhip64.so.7; load it first so this library binds
+        # to the same HIP runtime (two runtimes in one process break torch's device init).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"{LIB_PATH} is missing: run `make -C {HERE}` (no CPU fallback exists)")
         L = ctypes.CDLL(LIB_PATH)
@@ -127,6 +134,7 @@ def _seedgen_dict(o: SeedGenOut, want_host: bool) -> dict:
     r = {
         "origin": (o.info.origin_x, o.info.origin_y), "resolution": o.info.resolution, "width": W, "height": H,
         "thin_iters": o.thin_iters, "n_input": o.n_input, "n_clipped": o.n_clipped, "n_clusters_all": o.n_clusters_all,
+        "n_bfs_replayed": o.n_bfs_replayed,
         "row_center": _arr(o.row_center, 2 * nr, np.float64).reshape(-1, 2),
         "row_start": _arr(o.row_start, 2 * nr, np.float64).reshape(-1, 2),
         "row_end": _arr(o.row_end, 2 * nr, np.float64).reshape(-1, 2),

@@ -35,7 +35,7 @@ struct aos_ctx {
     // ---- host-side outputs of the last frame
     std::vector<int8_t> h_occ, h_skel;
     std::vector<double> h_row_center, h_row_start, h_row_end, h_row_length, h_voronoi, h_rows_info, h_cluster_info;
-    int n_virtual = 0, n_ray = 0, n_endpoint = 0, n_clusters_all = 0;
+    int n_virtual = 0, n_ray = 0, n_endpoint = 0, n_clusters_all = 0, n_bfs_replayed = 0;
 
     // ---- GVD (gvd.hip)
     aos::GvdState gs;

@@ -54,6 +54,7 @@ struct SeedStageIn {
 
 struct SeedStageOut {
     int n_clusters_all = 0;
+    int n_bfs = 0;
     std::vector<double> row_center, row_start, row_end, row_length;  // all_tree_rows order
     std::vector<double> virtual_xy, ray_xy, endpoint_xy;
     std::vector<double> rows_info, cluster_info;

@@ -135,17 +135,16 @@ __global__ void k_ccl_flatten(int *parent, int *is_root, int n) {
     parent[i] = x;
     is_root[i] = (x == i);
 }
-__global__ void k_cluster_count(const int *parent, const int *rank, int n, int *cid_of, int *count, int *slot) {
+__global__ void k_cluster_ids(const int *parent, const int *rank, int n, int *cid_of) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    int c = rank[parent[i]];
-    cid_of[i] = c;
-    slot[i] = atomicAdd(&count[c], 1);
+    if (i < n) cid_of[i] = rank[parent[i]];
 }
-__global__ void k_cluster_scatter(const int *list, const int *cid_of, const int *slot, const int *off, int n, int *cells) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    cells[off[cid_of[i]] + slot[i]] = list[i];
+// clusters are contiguous after the stable sort by id: record where each one starts
+__global__ void k_run_starts(const int *sorted_cid, int n, int *off, int ncl) {
+    int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    if (k == 0 || sorted_cid[k - 1] != sorted_cid[k]) off[sorted_cid[k]] = k;
+    if (k == n - 1) off[ncl] = n;
 }
 
 // ------------------------------------------------------------------ per-cluster statistics
@@ -344,7 +343,7 @@ __global__ void k_cluster_bfs(StatArgs A, const uint64_t *fg, const int *fg_off,
     const int cid = blockIdx.x * blockDim.x + threadIdx.x;
     if (cid >= A.n_clusters) return;
     ClusterRec r = A.rec[cid];
-    if (!(r.flags & 2)) return;
+    if (!(r.flags & 2) || (r.flags & 4)) return;
     const GridC &g = A.g;
     const int b = A.off[cid], n = A.off[cid + 1] - b;
     int *q = queue + b;
@@ -407,28 +406,198 @@ __global__ void k_cluster_bfs(StatArgs A, const uint64_t *fg, const int *fg_off,
     A.rec[cid] = r;
 }
 
+// Same replay, one wave per flagged cluster, cluster held in LDS: open-addressing table of the
+// cluster's pixel ids (bit 31 = visited) + the FIFO queue. One popped cell per step: lanes 0-7 test
+// its 8 neighbours in the reference order (seed_gen:986-987); new cells are appended in lane order,
+// exactly like the sequential push order. Clusters larger than kBfsQ cells use k_cluster_bfs.
+constexpr int kBfsTab = 16384, kBfsQ = 12288;
+__device__ __forceinline__ unsigned bfs_hash(int p) { return (unsigned)p * 2654435761u; }
+__device__ __forceinline__ int wave_min_i(int v) { for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o)); return v; }
+__device__ __forceinline__ double wave_max_d(double v) { for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o)); return v; }
+
+__global__ __launch_bounds__(64) void k_cluster_bfs_lds(StatArgs A, const int *flagged) {
+    __shared__ int tab[kBfsTab];
+    __shared__ int q[kBfsQ];
+    const int cid = flagged[blockIdx.x];
+    const int b = A.off[cid], n = A.off[cid + 1] - b, lane = threadIdx.x;
+    if (n > kBfsQ) return;
+    const GridC &g = A.g;
+    int cap = 64;
+    while (cap < 2 * n && cap < kBfsTab) cap <<= 1;
+    const unsigned mask = (unsigned)cap - 1;
+    for (int i = lane; i < cap; i += 64) tab[i] = INT_MAX;
+    __syncthreads();
+    int root = INT_MAX;
+    for (int k = lane; k < n; k += 64) {
+        int p = A.cells[b + k];
+        root = min(root, p);
+        unsigned h = bfs_hash(p) & mask;
+        while (atomicCAS(&tab[h], INT_MAX, p) != INT_MAX) h = (h + 1) & mask;
+    }
+    root = wave_min_i(root);  // first raster cell of the component
+    __syncthreads();
+    auto lookup = [&](int key) -> int {
+        unsigned h = bfs_hash(key) & mask;
+        while (true) {
+            int v = tab[h];
+            if (v == INT_MAX) return -1;
+            if ((v & 0x7fffffff) == key) return (int)h;
+            h = (h + 1) & mask;
+        }
+    };
+    if (lane == 0) { int h = lookup(root); tab[h] |= (int)0x80000000; q[0] = root; }
+    __syncthreads();
+    const int dxs[8] = {-1, -1, -1, 0, 0, 1, 1, 1}, dys[8] = {-1, 0, 1, -1, 1, -1, 0, 1};
+    int head = 0, tail = 1;
+    while (head < tail) {
+        const int p = q[head++];
+        const int cy = p / g.W, cx = p - cy * g.W;
+        bool cand = false;
+        int h = -1, key = 0;
+        if (lane < 8) {
+            int nx = cx + dxs[lane], ny = cy + dys[lane];
+            if (nx >= 0 && nx < g.W && ny >= 0 && ny < g.H) {
+                key = ny * g.W + nx;
+                h = lookup(key);
+                cand = h >= 0 && tab[h] >= 0;
+            }
+        }
+        unsigned long long m = __ballot(cand);
+        if (cand) {
+            int pos = __popcll(m & ((1ull << lane) - 1));
+            q[tail + pos] = key;
+            tab[h] = key | (int)0x80000000;
+        }
+        tail += __popcll(m);
+        __syncthreads();
+    }
+    // ---- order-dependent statistics, sequential where the reference is
+    ClusterRec r = A.rec[cid];
+    float sum_x = 0.0f, sum_y = 0.0f;
+    if (lane == 0)
+        for (int k = 0; k < n; ++k) { int pp = q[k], y = pp / g.W; sum_x += (float)(pp - y * g.W); sum_y += (float)y; }
+    sum_x = __shfl(sum_x, 0); sum_y = __shfl(sum_y, 0);
+    r.cx = sum_x / (float)n;
+    r.cy = sum_y / (float)n;
+    bool row = false;
+    if (r.length >= A.min_length) {
+        float cwx = (float)(g.ox + (double)(r.cx * g.res)), cwy = (float)(g.oy + (double)(r.cy * g.res));
+        r.center = make_double2(cwx, cwy);
+        row = d_pip(cwx, cwy, A.poly, A.np);
+    }
+    if (row) {
+        // first strict maximum in BFS order = (max d2, then min BFS rank)
+        double m1 = 0.0;
+        for (int k = lane; k < n; k += 64) {
+            double2 w = cell_w(g, q[k]);
+            double dx = w.x - r.center.x, dy = w.y - r.center.y;
+            m1 = fmax(m1, dx * dx + dy * dy);
+        }
+        m1 = wave_max_d(m1);
+        int fi = INT_MAX;
+        for (int k = lane; k < n; k += 64) {
+            double2 w = cell_w(g, q[k]);
+            double dx = w.x - r.center.x, dy = w.y - r.center.y;
+            if (dx * dx + dy * dy == m1 && m1 > 0.0) { fi = min(fi, k); }
+        }
+        fi = wave_min_i(fi);
+        if (fi == INT_MAX) fi = 0;
+        const double2 wf = cell_w(g, q[fi]);
+        double fdx = wf.x - r.center.x, fdy = wf.y - r.center.y, fx = 0, fy = 0;
+        { double z = fdx * fdx + fdy * fdy; if (z > 0.0) { double sq = sqrt(z); fx = fdx / sq; fy = fdy / sq; } }
+        double m2 = 0.0;
+        for (int k = lane; k < n; k += 64) {
+            if (k == fi) continue;
+            double2 w = cell_w(g, q[k]);
+            double dx = w.x - r.center.x, dy = w.y - r.center.y, d2 = dx * dx + dy * dy;
+            double nx = dx, ny = dy;
+            if (d2 > 0.0) { double sq = sqrt(d2); nx = dx / sq; ny = dy / sq; }
+            if (nx * fx + ny * fy < 0.0) m2 = fmax(m2, d2);
+        }
+        m2 = wave_max_d(m2);
+        int si = INT_MAX;
+        if (m2 > 0.0) {
+            for (int k = lane; k < n; k += 64) {
+                if (k == fi) continue;
+                double2 w = cell_w(g, q[k]);
+                double dx = w.x - r.center.x, dy = w.y - r.center.y, d2 = dx * dx + dy * dy;
+                double nx = dx, ny = dy;
+                if (d2 > 0.0) { double sq = sqrt(d2); nx = dx / sq; ny = dy / sq; }
+                if (nx * fx + ny * fy < 0.0 && d2 == m2) si = min(si, k);
+            }
+        } else {  // farthest from the first endpoint
+            double m3 = 0.0;
+            for (int k = lane; k < n; k += 64) {
+                if (k == fi) continue;
+                double2 w = cell_w(g, q[k]);
+                double dx = w.x - wf.x, dy = w.y - wf.y;
+                m3 = fmax(m3, dx * dx + dy * dy);
+            }
+            m3 = wave_max_d(m3);
+            for (int k = lane; k < n; k += 64) {
+                if (k == fi) continue;
+                double2 w = cell_w(g, q[k]);
+                double dx = w.x - wf.x, dy = w.y - wf.y;
+                if (dx * dx + dy * dy == m3 && m3 > 0.0) si = min(si, k);
+            }
+        }
+        si = wave_min_i(si);
+        if (si == INT_MAX) si = 0;
+        r.start = wf;
+        r.end = cell_w(g, q[si]);
+    }
+    r.flags = (row ? 1 : 0) | 4;
+    if (lane == 0) A.rec[cid] = r;
+}
+__global__ void k_flag_list(const ClusterRec *rec, int ncl, int *list, int *count, int qmax, int big) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= ncl || !(rec[c].flags & 2)) return;
+    if ((rec[c].n > qmax) != (big != 0)) return;
+    list[atomicAdd(count, 1)] = c;
+}
+
 // ------------------------------------------------------------------ rays
 struct RowDev { double sx, sy, ex, ey; int k; int slot0; };
 
 // raycastToOccupiedCell seed_gen:1730-1771 on the frameless skeleton
+// Marching loops are latency chains of dependent skeleton lookups; the sample positions are not
+// (cur += step / cx += dx*step depend only on the arithmetic), so each thread computes kLook
+// positions ahead with the reference's exact accumulation, issues their lookups together and then
+// resolves them in order.
+constexpr int kLook = 16;
+
 __device__ bool d_raycast(const uint64_t *skel, const GridC &g, double sx, double sy, double dx, double dy, double maxd,
                           double &hx, double &hy) {
     const double step = (double)g.res * 0.5;
     const int max_steps = (int)(maxd / step);
     double cx = sx, cy = sy;
-    for (int i = 0; i < max_steps; ++i) {
-        cx += dx * step;
-        cy += dy * step;
-        double ddx = cx - sx, ddy = cy - sy;
-        double dist = sqrt(ddx * ddx + ddy * ddy);
-        if (dist < 1.0) continue;
-        float fx = (float)cx, fy = (float)cy;
-        float rel_x = (float)(((double)fx - g.ox) / (double)g.res);
-        float rel_y = (float)(((double)fy - g.oy) / (double)g.res);
-        int gx = (int)floorf(rel_x), gy = (int)floorf(rel_y);
-        gx = gx < 0 ? 0 : (gx >= g.W ? g.W - 1 : gx);
-        gy = gy < 0 ? 0 : (gy >= g.H ? g.H - 1 : gy);
-        if (bit_at(skel, g.WW, gx, gy)) { hx = cx; hy = cy; return true; }
+    for (int i0 = 0; i0 < max_steps; i0 += kLook) {
+        double px[kLook], py[kLook];
+        bool hit[kLook];
+#pragma unroll
+        for (int j = 0; j < kLook; ++j) {
+            cx += dx * step;
+            cy += dy * step;
+            px[j] = cx; py[j] = cy;
+        }
+#pragma unroll
+        for (int j = 0; j < kLook; ++j) {
+            hit[j] = false;
+            double ddx = px[j] - sx, ddy = py[j] - sy;
+            double dist = sqrt(ddx * ddx + ddy * ddy);
+            if (i0 + j < max_steps && !(dist < 1.0)) {
+                float fx = (float)px[j], fy = (float)py[j];
+                float rel_x = (float)(((double)fx - g.ox) / (double)g.res);
+                float rel_y = (float)(((double)fy - g.oy) / (double)g.res);
+                int gx = (int)floorf(rel_x), gy = (int)floorf(rel_y);
+                gx = gx < 0 ? 0 : (gx >= g.W ? g.W - 1 : gx);
+                gy = gy < 0 ? 0 : (gy >= g.H ? g.H - 1 : gy);
+                hit[j] = bit_at(skel, g.WW, gx, gy);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kLook; ++j)
+            if (hit[j]) { hx = px[j]; hy = py[j]; return true; }
     }
     return false;
 }
@@ -480,20 +649,32 @@ __global__ void k_endpoint_rays(const RowDev *rows, int n_rows, const uint64_t *
     { double z = rx * rx + ry * ry; if (z > 0.0) { double q = sqrt(z); rx = rx / q; ry = ry / q; } }
     double cur = 1.0;
     double resx = 0, resy = 0;
-    bool done = false;
-    while (cur <= g.amax) {
-        double cx = stx + rx * cur, cy = sty + ry * cur;
-        if (!(cx >= g.minx && cx <= g.maxx && cy >= g.miny && cy <= g.maxy)) {
-            resx = fmax(g.minx, fmin(g.maxx, cx)); resy = fmax(g.miny, fmin(g.maxy, cy));
-            done = true;
-            break;
+    bool done = false, ended = false;
+    while (!done && !ended) {
+        double px[kLook], py[kLook];
+        bool valid[kLook], ins[kLook], occ[kLook];
+#pragma unroll
+        for (int j = 0; j < kLook; ++j) {   // while (current_dist <= max) { p = start + dir*cur; ...; cur += 0.1; }
+            valid[j] = cur <= g.amax;
+            px[j] = stx + rx * cur; py[j] = sty + ry * cur;
+            cur += 0.1;
         }
-        int mx = (int)((cx - g.ox) / (double)g.res), my = (int)((cy - g.oy) / (double)g.res);
-        if (mx >= 0 && mx < g.W && my >= 0 && my < g.H && bit_at(skel, g.WW, mx, my)) {
-            resx = cx; resy = cy; done = true;
-            break;
+#pragma unroll
+        for (int j = 0; j < kLook; ++j) {
+            ins[j] = px[j] >= g.minx && px[j] <= g.maxx && py[j] >= g.miny && py[j] <= g.maxy;
+            occ[j] = false;
+            if (valid[j] && ins[j]) {
+                int mx = (int)((px[j] - g.ox) / (double)g.res), my = (int)((py[j] - g.oy) / (double)g.res);
+                occ[j] = mx >= 0 && mx < g.W && my >= 0 && my < g.H && bit_at(skel, g.WW, mx, my);
+            }
         }
-        cur += 0.1;
+#pragma unroll
+        for (int j = 0; j < kLook; ++j) {
+            if (done || ended) continue;
+            if (!valid[j]) { ended = true; continue; }
+            if (!ins[j]) { resx = fmax(g.minx, fmin(g.maxx, px[j])); resy = fmax(g.miny, fmin(g.maxy, py[j])); done = true; continue; }
+            if (occ[j]) { resx = px[j]; resy = py[j]; done = true; }
+        }
     }
     if (!done) {
         double fx = stx + rx * g.amax, fy = sty + ry * g.amax;
@@ -574,28 +755,41 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         AOS_HIP(hipStreamSynchronize(s));
         const int ncl = h_sc[0];
         S.n_clusters = ncl;
-        int *d_cnt = dev<int>(S.cl_count, ncl + 1), *d_off = dev<int>(S.cl_off, ncl + 1);
-        int *d_cid = dev<int>(S.cl_cursor, 2 * (size_t)nf), *d_slot = d_cid + nf;
+        // bucket the foreground cells by cluster id: stable radix sort (keeps raster order inside a
+        // cluster) instead of per-cell atomics on ~100 hot counters
+        int *d_off = dev<int>(S.cl_off, ncl + 1);
+        int *d_cid = dev<int>(S.cl_cursor, 2 * (size_t)nf), *d_scid = d_cid + nf;
         int *d_cells = dev<int>(S.cl_cells, nf);
-        AOS_HIP(hipMemsetAsync(d_cnt, 0, sizeof(int) * (ncl + 1), s));
-        k_cluster_count<<<cdiv(nf, 256), 256, 0, s>>>(d_par, d_rank, nf, d_cid, d_cnt, d_slot);
-        size_t tb3 = 0;
-        hipcub::DeviceScan::ExclusiveSum(nullptr, tb3, (int *)nullptr, (int *)nullptr, ncl + 1, s);
-        tmp = S.scan_tmp.ensure(std::max(std::max(tb, tb2), tb3));
-        AOS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb3, d_cnt, d_off, ncl + 1, s));
-        k_cluster_scatter<<<cdiv(nf, 256), 256, 0, s>>>(d_list, d_cid, d_slot, d_off, nf, d_cells);
+        k_cluster_ids<<<cdiv(nf, 256), 256, 0, s>>>(d_par, d_rank, nf, d_cid);
+        int bits = 1;
+        while ((1 << bits) <= ncl) ++bits;
+        size_t tbs = 0;
+        AOS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbs, d_cid, d_scid, d_list, d_cells, nf, 0, bits, s));
+        tmp = S.scan_tmp.ensure(std::max(std::max(tb, tb2), tbs));
+        AOS_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tbs, d_cid, d_scid, d_list, d_cells, nf, 0, bits, s));
+        k_run_starts<<<cdiv(nf, 256), 256, 0, s>>>(d_scid, nf, d_off, ncl);
         ClusterRec *d_rec = dev<ClusterRec>(S.rec, ncl);
         StatArgs A{d_off, d_cells, d_list, ncl, g, d_poly, np, static_cast<float>(in.cluster_min_length), d_rec};
         k_cluster_stats<<<ncl, 256, 0, s>>>(A);
         S.h_rec.resize(ncl);
         AOS_HIP(hipMemcpyAsync(S.h_rec.data(), d_rec, sizeof(ClusterRec) * ncl, hipMemcpyDeviceToHost, s));
         AOS_HIP(hipStreamSynchronize(s));
-        bool any_bfs = false;
-        for (const auto &r : S.h_rec) any_bfs |= (r.flags & 2) != 0;
-        if (any_bfs) {
-            int *d_q = dev<int>(S.bfs_queue, nf), *d_vis = dev<int>(S.bfs_vis, nf);
-            AOS_HIP(hipMemsetAsync(d_vis, 0xFF, sizeof(int) * nf, s));
-            k_cluster_bfs<<<cdiv(ncl, 64), 64, 0, s>>>(A, d_fg, d_wo, d_par, d_q, d_vis, 0);
+        int n_bfs = 0;
+        for (const auto &r : S.h_rec) n_bfs += (r.flags & 2) != 0;
+        out.n_bfs = n_bfs;
+        if (n_bfs) {
+            // small/medium clusters: one wave each, LDS-resident replay
+            int *d_fl = dev<int>(S.bfs_vis, ncl + 2), *d_fc = d_fl + ncl;
+            AOS_HIP(hipMemsetAsync(d_fc, 0, sizeof(int), s));
+            k_flag_list<<<cdiv(ncl, 256), 256, 0, s>>>(d_rec, ncl, d_fl, d_fc, kBfsQ, 0);
+            int n_small = 0;
+            for (const auto &r : S.h_rec) n_small += (r.flags & 2) && r.n <= kBfsQ;
+            if (n_small) k_cluster_bfs_lds<<<n_small, 64, 0, s>>>(A, d_fl);
+            if (n_small < n_bfs) {  // very large clusters: global-memory replay, one thread each
+                int *d_q = dev<int>(S.bfs_queue, nf), *d_vis = dev<int>(S.row_idx, nf);
+                AOS_HIP(hipMemsetAsync(d_vis, 0xFF, sizeof(int) * nf, s));
+                k_cluster_bfs<<<cdiv(ncl, 64), 64, 0, s>>>(A, d_fg, d_wo, d_par, d_q, d_vis, 0);
+            }
             AOS_HIP(hipMemcpyAsync(S.h_rec.data(), d_rec, sizeof(ClusterRec) * ncl, hipMemcpyDeviceToHost, s));
             AOS_HIP(hipStreamSynchronize(s));
         }

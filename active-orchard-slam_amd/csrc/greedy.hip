@@ -5,7 +5,7 @@
 // (seed_gen:2076-2085, 1964-1974, 1460-1470; gvd:98-125; voronoi_diagram.cpp:156-204) keep exactly
 // the lexicographically-first maximal independent set (LFMIS) of the conflict graph. We hash the
 // candidates into cells no smaller than the conflict radius, list each candidate's EARLIER
-// conflicting candidates (CSR), and decide the LFMIS in rounds inside one workgroup:
+// conflicting candidates (CSR), and decide the LFMIS in rounds over the whole grid:
 // undecided c becomes kept when all listed predecessors are removed, removed once one is kept.
 // Decisions are facts about the final set, so in-place updates are safe; the smallest undecided
 // index always decides, so the loop terminates.
@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <stdexcept>
 
 #include "cluster_seed.h"
 
@@ -92,29 +93,30 @@ __global__ void k_conflicts(const double2 *p, const int *ok, int n, HashG h, con
     if (!coff) ccount[i] = c;
 }
 
-__global__ __launch_bounds__(1024) void k_greedy(const int *ok, int n, const int *coff, const int *clist, int *state) {
-    __shared__ int undecided;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) state[i] = ok[i] ? 0 : 2;
-    __syncthreads();
-    while (true) {
-        if (threadIdx.x == 0) undecided = 0;
-        __syncthreads();
-        for (int i = threadIdx.x; i < n; i += blockDim.x) {
-            if (__hip_atomic_load(&state[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) continue;
-            bool any_kept = false, any_undec = false;
-            for (int k = coff[i]; k < coff[i + 1]; ++k) {
-                int sj = __hip_atomic_load(&state[clist[k]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (sj == 1) { any_kept = true; break; }
-                if (sj == 0) any_undec = true;
-            }
-            int ns = any_kept ? 2 : (any_undec ? 0 : 1);
-            if (ns) __hip_atomic_store(&state[i], ns, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else undecided = 1;
+__global__ void k_greedy_init(const int *ok, int n, int *state) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) state[i] = ok[i] ? 0 : 2;
+}
+// One round over all undecided candidates, any number of workgroups. States are read with
+// agent-scope loads (another workgroup may have decided a predecessor in this very round); a
+// stale read only postpones a decision to a later round. undecided[0] counts candidates still
+// undecided when this round looked at them: 0 means the set is complete.
+__global__ void k_greedy_round(int n, const int *coff, const int *clist, int *state, int *undecided) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool und = false;
+    if (i < n && __hip_atomic_load(&state[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+        bool any_kept = false, any_undec = false;
+        for (int k = coff[i]; k < coff[i + 1]; ++k) {
+            int sj = __hip_atomic_load(&state[clist[k]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (sj == 1) { any_kept = true; break; }
+            if (sj == 0) any_undec = true;
         }
-        __syncthreads();
-        if (!undecided) break;
-        __syncthreads();
+        int ns = any_kept ? 2 : (any_undec ? 0 : 1);
+        if (ns) __hip_atomic_store(&state[i], ns, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else und = true;
     }
+    unsigned long long m = __ballot(und);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(undecided, (int)__popcll(m));
 }
 
 __global__ void k_kept_flags(const int *state, int n, int *f) {
@@ -151,7 +153,19 @@ int greedy_dedup(DedupScratch &S, const double2 *cand, const int *ok, int n, int
     int *clist = dev<int>(S.clist, S.n_conf);
     k_conflicts<<<cdiv(n, 256), 256, 0, s>>>(cand, ok, n, h, skeys, sidx, mode, thr, coff, nullptr, clist);
     int *state = dev<int>(S.state, n);
-    k_greedy<<<1, 1024, 0, s>>>(ok, n, coff, clist, state);
+    k_greedy_init<<<cdiv(n, 256), 256, 0, s>>>(ok, n, state);
+    // rounds: launch a batch, check the last round's undecided count once per batch
+    constexpr int kBatch = 6;
+    int *und = dev<int>(S.f, std::max(n + 1, kBatch));   // scratch; reused for kept flags below
+    for (int done_rounds = 0;;) {
+        AOS_HIP(hipMemsetAsync(und, 0, sizeof(int) * kBatch, s));
+        for (int r = 0; r < kBatch; ++r) k_greedy_round<<<cdiv(n, 256), 256, 0, s>>>(n, coff, clist, state, und + r);
+        AOS_HIP(hipMemcpyAsync(h_scalar, und, sizeof(int) * kBatch, hipMemcpyDeviceToHost, s));
+        AOS_HIP(hipStreamSynchronize(s));
+        done_rounds += kBatch;
+        if (h_scalar[kBatch - 1] == 0) break;
+        if (done_rounds > n + kBatch) throw std::runtime_error("greedy de-duplication did not converge");
+    }
     int *f = dev<int>(S.f, n + 1), *pos = dev<int>(S.pos, n + 1);
     AOS_HIP(hipMemsetAsync(f + n, 0, sizeof(int), s));
     k_kept_flags<<<cdiv(n, 256), 256, 0, s>>>(state, n, f);

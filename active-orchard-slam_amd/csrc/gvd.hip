@@ -207,10 +207,20 @@ __global__ void k_occupancy(const int2 *ft, const int *valid, int nc, const doub
             if (lo_t > hi_t) { i0 = 1; i1 = 0; }
             else { i0 = max(0, (int)floor(lo_t * num) - 2); i1 = min(num, (int)ceil(hi_t * num) + 2); }
         }
-        for (int i = i0; i <= i1 && num >= 0; ++i) {
-            double t = (i == num) ? 1.0 : ((double)i / (double)num);
-            double px = s.x + (t * dx) * len, py = s.y + (t * dy) * len;
-            if (occ_trunc(sk, g, px, py)) { hit = true; break; }
+        for (int ib = i0; ib <= i1 && num >= 0 && !hit; ib += 16) {   // 16 independent samples in flight
+            bool h16[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int i = ib + j;
+                h16[j] = false;
+                if (i <= i1) {
+                    double t = (i == num) ? 1.0 : ((double)i / (double)num);
+                    double px = s.x + (t * dx) * len, py = s.y + (t * dy) * len;
+                    h16[j] = occ_trunc(sk, g, px, py);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 16; ++j) hit |= h16[j];
         }
     }
     pass[c] = hit ? 0 : 1;
@@ -317,14 +327,28 @@ __global__ __launch_bounds__(256) void k_label_points(const LabelRow *jobs, int 
     { double z = rx * rx + ry * ry; if (z > 0.0) { double q = sqrt(z); rx = rx / q; ry = ry / q; } }
     double cur = 0.5;  // min_distance passed by findVoronoiBoundaryPointNearEndpoint
     double resx = 0, resy = 0;
-    bool done = false;
-    while (cur <= g.diag3) {
-        double cx = J.ex + rx * cur, cy = J.ey + ry * cur;
-        if (!(cx >= g.minx && cx <= g.maxx && cy >= g.miny && cy <= g.maxy)) {
-            resx = fmax(g.minx, fmin(g.maxx, cx)); resy = fmax(g.miny, fmin(g.maxy, cy)); done = true; break;
+    bool done = false, ended = false;
+    while (!done && !ended) {
+        double px[16], py[16];
+        bool valid[16], ins[16], occ[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            valid[j] = cur <= g.diag3;
+            px[j] = J.ex + rx * cur; py[j] = J.ey + ry * cur;
+            cur += g.step;
         }
-        if (occ_trunc(sk, g, cx, cy)) { resx = cx; resy = cy; done = true; break; }
-        cur += g.step;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            ins[j] = px[j] >= g.minx && px[j] <= g.maxx && py[j] >= g.miny && py[j] <= g.maxy;
+            occ[j] = valid[j] && ins[j] && occ_trunc(sk, g, px[j], py[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            if (done || ended) continue;
+            if (!valid[j]) { ended = true; continue; }
+            if (!ins[j]) { resx = fmax(g.minx, fmin(g.maxx, px[j])); resy = fmax(g.miny, fmin(g.maxy, py[j])); done = true; continue; }
+            if (occ[j]) { resx = px[j]; resy = py[j]; done = true; }
+        }
     }
     if (!done) {
         double fx = J.ex + rx * g.diag3, fy = J.ey + ry * g.diag3;

@@ -221,6 +221,7 @@ void aos_ctx::run_seedgen(bool want_host, aos_seedgen_out &out) {
     h_rows_info = std::move(so.rows_info);
     h_cluster_info = std::move(so.cluster_info);
     n_clusters_all = so.n_clusters_all;
+    n_bfs_replayed = so.n_bfs;
 
     out.info = aos_grid_info{g.origin_x, g.origin_y, g.res, (uint32_t)g.W, (uint32_t)g.H};
     out.thin_iters = thin_iters;
@@ -232,6 +233,7 @@ void aos_ctx::run_seedgen(bool want_host, aos_seedgen_out &out) {
     out.d_occupancy = d_occ;
     out.d_skeleton = d_skel;
     out.n_clusters_all = n_clusters_all;
+    out.n_bfs_replayed = n_bfs_replayed;
     out.n_rows = (int)h_row_length.size();
     out.row_center = h_row_center.data(); out.row_start = h_row_start.data();
     out.row_end = h_row_end.data(); out.row_length = h_row_length.data();

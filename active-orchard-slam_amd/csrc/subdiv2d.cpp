@@ -39,47 +39,53 @@ inline bool voronoi_point(float o0x, float o0y, float d0x, float d0y, float o1x,
 }
 }  // namespace
 
+void Subdiv2D::reserve(size_t n) {
+    vp.reserve(2 * n + 8); vfirst.reserve(2 * n + 8); vtype.reserve(2 * n + 8);
+    qe.reserve(3 * n + 8);
+}
+
 int Subdiv2D::right_of(float px, float py, int e) const {
-    int o = org(e), d = dst(e);
-    double cw = tri_area(px, py, vx[d], vy[d], vx[o], vy[o]);
+    const QE &q = qe[e >> 2];
+    const V2f o = vp[q.pt[e & 3]], d = vp[q.pt[(e + 2) & 3]];
+    double cw = tri_area(px, py, d.x, d.y, o.x, o.y);
     return (cw > 0) - (cw < 0);
 }
 
 int Subdiv2D::new_edge() {
     if (free_q <= 0) {
-        qnext.resize(qnext.size() + 4, 0);
-        qpt.resize(qpt.size() + 4, 0);
-        free_q = (int)(qnext.size() / 4) - 1;
+        qe.push_back(QE{{0, 0, 0, 0}, {0, 0, 0, 0}});
+        free_q = (int)qe.size() - 1;
     }
     int e = free_q * 4;
-    free_q = qnext[e + 1];
-    qnext[e] = e; qnext[e + 1] = e + 3; qnext[e + 2] = e + 2; qnext[e + 3] = e + 1;
-    qpt[e] = qpt[e + 1] = qpt[e + 2] = qpt[e + 3] = 0;
+    QE &q = qe[free_q];
+    free_q = q.next[1];
+    q.next[0] = e; q.next[1] = e + 3; q.next[2] = e + 2; q.next[3] = e + 1;
+    q.pt[0] = q.pt[1] = q.pt[2] = q.pt[3] = 0;
     return e;
 }
 
 int Subdiv2D::new_point(float x, float y, int type) {
     if (free_p == 0) {
-        vx.push_back(0.f); vy.push_back(0.f); vfirst.push_back(0); vtype.push_back(-1);
-        free_p = (int)vx.size() - 1;
+        vp.push_back(V2f{0.f, 0.f}); vfirst.push_back(0); vtype.push_back(-1);
+        free_p = (int)vp.size() - 1;
     }
     int v = free_p;
     free_p = vfirst[v];
-    vx[v] = x; vy[v] = y; vfirst[v] = 0; vtype[v] = type;
+    vp[v] = V2f{x, y}; vfirst[v] = 0; vtype[v] = type;
     return v;
 }
 
 void Subdiv2D::splice(int a, int b) {
-    int &an = qnext[a], &bn = qnext[b];
+    int &an = qe[a >> 2].next[a & 3], &bn = qe[b >> 2].next[b & 3];
     int ar = rot(an, 1), br = rot(bn, 1);
-    int &arn = qnext[ar], &brn = qnext[br];
+    int &arn = qe[ar >> 2].next[ar & 3], &brn = qe[br >> 2].next[br & 3];
     std::swap(an, bn);
     std::swap(arn, brn);
 }
 
 void Subdiv2D::set_pts(int e, int o, int d) {
-    qpt[e] = o;
-    qpt[(e & ~3) + ((e + 2) & 3)] = d;
+    qe[e >> 2].pt[e & 3] = o;
+    qe[e >> 2].pt[(e + 2) & 3] = d;
     vfirst[o] = e;
     vfirst[d] = e ^ 2;
 }
@@ -107,8 +113,8 @@ void Subdiv2D::delete_edge(int e) {
     int se = e ^ 2;
     splice(se, get_e(se, PREV_AROUND_ORG));
     int q = e >> 2;
-    qnext[4 * q] = 0;
-    qnext[4 * q + 1] = free_q;
+    qe[q].next[0] = 0;
+    qe[q].next[1] = free_q;
     free_q = q;
 }
 
@@ -118,11 +124,11 @@ void Subdiv2D::init_delaunay(float rx, float ry, float rw, float rh, int rect_mo
         rw = (float)(int)std::lrint(rw); rh = (float)(int)std::lrint(rh);
     }
     const float big = 3.f * std::max(rw, rh);
-    vx.clear(); vy.clear(); vfirst.clear(); vtype.clear(); qnext.clear(); qpt.clear();
+    vp.clear(); vfirst.clear(); vtype.clear(); qe.clear();
     recent = 0;
     tlx = rx; tly = ry; brx = rx + rw; bry = ry + rh;
-    vx.push_back(0.f); vy.push_back(0.f); vfirst.push_back(0); vtype.push_back(-1);   // vtx[0]
-    qnext.assign(4, 0); qpt.assign(4, 0);                                             // qedges[0]
+    vp.push_back(V2f{0.f, 0.f}); vfirst.push_back(0); vtype.push_back(-1);   // vtx[0]
+    qe.push_back(QE{{0, 0, 0, 0}, {0, 0, 0, 0}});                             // qedges[0]
     free_q = 0; free_p = 0;
     int pA = new_point(rx + big, ry, 0), pB = new_point(rx, ry + big, 0), pC = new_point(rx - big, ry - big, 0);
     int eAB = new_edge(), eBC = new_edge(), eCA = new_edge();
@@ -134,7 +140,7 @@ void Subdiv2D::init_delaunay(float rx, float ry, float rw, float rh, int rect_mo
 // Subdiv2D::locate: 0 inside, 1 vertex, 2 on edge, -1 outside rect, -2 error
 int Subdiv2D::locate(float px, float py, int &out_edge, int &out_vertex) {
     int vertex = 0;
-    const int max_edges = (int)qnext.size();  // qedges.size() * 4
+    const int max_edges = (int)qe.size() * 4;
     if (px < tlx || py < tly || px >= brx || py >= bry) return -1;
     int edge = recent;
     int location = -2;
@@ -152,7 +158,7 @@ int Subdiv2D::locate(float px, float py, int &out_edge, int &out_vertex) {
             if (ron > 0) {
                 if (rod == 0 && roc == 0) { location = 0; break; }
                 roc = rod; edge = dprev;
-            } else if (roc == 0 && right_of(vx[dst(onext)], vy[dst(onext)], edge) >= 0) {
+            } else if (roc == 0 && right_of(vp[dst(onext)].x, vp[dst(onext)].y, edge) >= 0) {
                 edge ^= 2;
             } else {
                 roc = ron; edge = onext;
@@ -162,7 +168,7 @@ int Subdiv2D::locate(float px, float py, int &out_edge, int &out_vertex) {
     recent = edge;
     if (location == 0) {
         const int o = org(edge), d = dst(edge);
-        const float ox = vx[o], oy = vy[o], dx = vx[d], dy = vy[d];
+        const float ox = vp[o].x, oy = vp[o].y, dx = vp[d].x, dy = vp[d].y;
         double t1 = std::fabs(px - ox); t1 += std::fabs(py - oy);
         double t2 = std::fabs(px - dx); t2 += std::fabs(py - dy);
         double t3 = std::fabs(ox - dx); t3 += std::fabs(oy - dy);
@@ -196,13 +202,15 @@ bool Subdiv2D::insert(float x, float y) {
         curr_edge = get_e(base, PREV_AROUND_ORG);
     } while (dst(curr_edge) != first_point);
     curr_edge = get_e(base, PREV_AROUND_ORG);
-    const int max_edges = (int)qnext.size();
+    const int max_edges = (int)qe.size() * 4;
+    const V2f np_ = vp[curr_point];
     for (int i = 0; i < max_edges; i++) {
         int temp = get_e(curr_edge, PREV_AROUND_ORG);
         int tdst = dst(temp), corg = org(curr_edge), cdst = dst(curr_edge);
-        if (right_of(vx[tdst], vy[tdst], curr_edge) > 0 &&
+        const V2f T = vp[tdst], O = vp[corg], D = vp[cdst];
+        if (tri_area(T.x, T.y, D.x, D.y, O.x, O.y) > 0 &&   // isRightOf(temp_dst, curr_edge) > 0
             // isPtInCircle3(pt = org, a = temp_dst, b = dst, c = new point)
-            in_circle(vx[corg], vy[corg], vx[tdst], vy[tdst], vx[cdst], vy[cdst], vx[curr_point], vy[curr_point]) < 0) {
+            in_circle(O.x, O.y, T.x, T.y, D.x, D.y, np_.x, np_.y) < 0) {
             swap_edge(curr_edge);
             curr_edge = get_e(curr_edge, PREV_AROUND_ORG);
         } else if (corg == first_point) {
@@ -217,29 +225,29 @@ bool Subdiv2D::insert(float x, float y) {
 // calcVoronoi: quad-edges from #4 (#0 is NULL, #1-#3 the outer triangle); the first quad-edge
 // touching a triangle computes its circumcentre (pt[3] = left face, pt[1] = right face).
 void Subdiv2D::calc_voronoi() {
-    const int total = (int)(qnext.size() / 4);
-    for (int q = 0; q < total; ++q) qpt[4 * q + 1] = qpt[4 * q + 3] = 0;
-    for (size_t i = 0; i < vx.size(); ++i)
+    const int total = (int)qe.size();
+    for (int q = 0; q < total; ++q) qe[q].pt[1] = qe[q].pt[3] = 0;
+    for (size_t i = 0; i < vp.size(); ++i)
         if (vtype[i] > 0) { vfirst[i] = free_p; vtype[i] = -1; free_p = (int)i; }
     for (int q = 4; q < total; q++) {
-        if (qnext[4 * q] <= 0) continue;  // free
+        if (qe[q].next[0] <= 0) continue;  // free
         const int e0 = q * 4;
-        if (!qpt[e0 + 3]) {
+        if (!qe[q].pt[3]) {
             int e1 = get_e(e0, NEXT_AROUND_LEFT), e2 = get_e(e1, NEXT_AROUND_LEFT);
+            const V2f a = vp[org(e0)], b = vp[dst(e0)], c = vp[org(e1)], d = vp[dst(e1)];
             float rx, ry;
-            if (voronoi_point(vx[org(e0)], vy[org(e0)], vx[dst(e0)], vy[dst(e0)], vx[org(e1)], vy[org(e1)], vx[dst(e1)],
-                              vy[dst(e1)], rx, ry)) {
+            if (voronoi_point(a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y, rx, ry)) {
                 int p = new_point(rx, ry, 1);
-                qpt[e0 + 3] = qpt[(e1 & ~3) + 3 - (e1 & 2)] = qpt[(e2 & ~3) + 3 - (e2 & 2)] = p;
+                qe[q].pt[3] = qe[e1 >> 2].pt[3 - (e1 & 2)] = qe[e2 >> 2].pt[3 - (e2 & 2)] = p;
             }
         }
-        if (!qpt[e0 + 1]) {
+        if (!qe[q].pt[1]) {
             int e1 = get_e(e0, NEXT_AROUND_RIGHT), e2 = get_e(e1, NEXT_AROUND_RIGHT);
+            const V2f a = vp[org(e0)], b = vp[dst(e0)], c = vp[org(e1)], d = vp[dst(e1)];
             float rx, ry;
-            if (voronoi_point(vx[org(e0)], vy[org(e0)], vx[dst(e0)], vy[dst(e0)], vx[org(e1)], vy[org(e1)], vx[dst(e1)],
-                              vy[dst(e1)], rx, ry)) {
+            if (voronoi_point(a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y, rx, ry)) {
                 int p = new_point(rx, ry, 1);
-                qpt[e0 + 1] = qpt[(e1 & ~3) + 1 + (e1 & 2)] = qpt[(e2 & ~3) + 1 + (e2 & 2)] = p;
+                qe[q].pt[1] = qe[e1 >> 2].pt[1 + (e1 & 2)] = qe[e2 >> 2].pt[1 + (e2 & 2)] = p;
             }
         }
     }
@@ -249,7 +257,7 @@ void Subdiv2D::voronoi_edges(std::vector<float> &edges) {
     calc_voronoi();
     edges.clear();
     std::vector<int> facet;
-    const size_t total = vx.size();
+    const size_t total = vp.size();
     for (size_t k = 4; k < total; k++) {
         if (vtype[k] != 0) continue;  // free or virtual
         const int start = rot(vfirst[k], 1);
@@ -263,7 +271,7 @@ void Subdiv2D::voronoi_edges(std::vector<float> &edges) {
         if (n < 2) continue;
         for (size_t i = 0; i < n; ++i) {
             int a = facet[i], b = facet[(i + 1) % n];
-            edges.push_back(vx[a]); edges.push_back(vy[a]); edges.push_back(vx[b]); edges.push_back(vy[b]);
+            edges.push_back(vp[a].x); edges.push_back(vp[a].y); edges.push_back(vp[b].x); edges.push_back(vp[b].y);
         }
     }
 }

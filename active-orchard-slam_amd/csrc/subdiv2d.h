@@ -8,7 +8,9 @@
 // node numbering follows that order, so bit-identical topology needs this exact replay; the
 // GPU takes over from the facet list on (boundary points, graph, labels).
 //
-// Layout: structure-of-arrays quad-edges (next[4], pt[4] as flat int arrays), float points.
+// Layout: one 32-byte record per quad-edge ({next[4], pt[4]}, one cache line holds two) and one
+// 8-byte float2 per vertex: the flip walk (~115 iterations per insert on orchard seed rows, where
+// a new row line briefly fans out to the whole previous line) is pure pointer chasing.
 #pragma once
 #include <cstddef>
 #include <cstdint>
@@ -26,23 +28,24 @@ class Subdiv2D {
     // Emits the reference's edge list directly: (p_i, p_{i+1 mod n}) for facets with >= 2 points
     // (voronoi_diagram.cpp:97-114), as float x0, y0, x1, y1.
     void voronoi_edges(std::vector<float> &edges);
-    size_t num_vertices() const { return vx.size(); }
+    size_t num_vertices() const { return vp.size(); }
+    void reserve(size_t n_points);
 
   private:
     enum { NEXT_AROUND_LEFT = 0x13, NEXT_AROUND_RIGHT = 0x31, PREV_AROUND_ORG = 0x11, PREV_AROUND_DST = 0x33 };
-    // vertices
-    std::vector<float> vx, vy;
+    struct alignas(32) QE { int next[4]; int pt[4]; };
+    struct V2f { float x, y; };
+    std::vector<V2f> vp;
     std::vector<int> vfirst, vtype;   // type: -1 free, 0 real, 1 virtual
-    // quad-edges: 4 rotations each
-    std::vector<int> qnext, qpt;      // size 4 * nquad
+    std::vector<QE> qe;
     int free_q = 0, free_p = 0, recent = 0;
     float tlx = 0, tly = 0, brx = 0, bry = 0;
 
-    int next_e(int e) const { return qnext[e]; }
+    int next_e(int e) const { return qe[e >> 2].next[e & 3]; }
     static int rot(int e, int r) { return (e & ~3) + ((e + r) & 3); }
-    int get_e(int e, int t) const { e = qnext[(e & ~3) + ((e + t) & 3)]; return (e & ~3) + ((e + (t >> 4)) & 3); }
-    int org(int e) const { return qpt[e]; }
-    int dst(int e) const { return qpt[(e & ~3) + ((e + 2) & 3)]; }
+    int get_e(int e, int t) const { e = qe[e >> 2].next[(e + t) & 3]; return (e & ~3) + ((e + (t >> 4)) & 3); }
+    int org(int e) const { return qe[e >> 2].pt[e & 3]; }
+    int dst(int e) const { return qe[e >> 2].pt[(e + 2) & 3]; }
     int right_of(float px, float py, int e) const;
     int new_edge();
     int new_point(float x, float y, int type);

@@ -90,6 +90,7 @@ typedef struct aos_seedgen_out {
     const int8_t *d_occupancy, *d_skeleton;
     /* clusters after the length filter, discovery order */
     int32_t n_clusters_all;              /* before the length filter                             */
+    int32_t n_bfs_replayed;              /* clusters without the order-free certificate (exact BFS) */
     int32_t n_rows;                      /* tree rows (all_tree_rows order)                      */
     const double *row_center, *row_start, *row_end, *row_length;  /* 2, 2, 2, 1 per row         */
     /* /voronoi_seeds = virtual ++ real(empty) ++ ray ++ endpoint seeds (x, y) */

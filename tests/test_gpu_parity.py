@@ -132,3 +132,41 @@ def test_device_resident_input_matches_host_input():
     d = c.seedgen(t.data_ptr(), n_points=cloud.shape[0], on_device=True)
     assert_seedgen_parity(d, {**h, "cluster_length": np.zeros(h["n_clusters_all"])})
     c.close()
+
+
+def _line_cloud(segments, step=0.05):
+    """Dense points along horizontal segments (x0, x1, y): thin bands whose skeletons are straight
+    lines, symmetric about their centre (argmax ties on both ends)."""
+    pts = []
+    for x0, x1, y in segments:
+        xs = np.arange(x0, x1 + 1e-9, step)
+        for dy in (-0.05, 0.0, 0.05):
+            pts.append(np.stack([xs, np.full_like(xs, y + dy), np.zeros_like(xs)], 1))
+    p = np.concatenate(pts).astype(np.float32)
+    rec = np.zeros((len(p), 4), np.float32)
+    rec[:, :3] = p
+    return rec.view(np.uint8).reshape(len(p), 16)
+
+
+def test_argmax_ties_force_exact_bfs_replay():
+    # origin 0 (polygon bbox starts at 2.5) and res 0.25: world coordinates are exact in float, so a
+    # straight skeleton bar symmetric about its centre has exactly tied end distances
+    cloud = _line_cloud([(10.0, 60.0, 20.0), (15.0, 55.25, 40.0), (5.0, 5.0, 60.0)])
+    poly = np.array([[2.5, 2.5], [90.0, 2.5], [90.0, 90.0], [2.5, 90.0]])
+    c = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=0.25))
+    c.set_polygon(poly)
+    g = c.seedgen(cloud)
+    o = O.seedgen(cloud, poly, O.default_params(grid_resolution=0.25))
+    assert g["n_bfs_replayed"] >= 1
+    assert_seedgen_parity(g, o)
+    assert_gvd_parity(c.gvd_from_seedgen(), O.gvd(o["voronoi_seeds"], o["rows_info"], o))
+    c.close()
+
+
+def test_c2_seedgen_parity_with_large_sums():
+    """4096^2: two merged-row clusters have coordinate sums > 2^24 (float sums order-dependent)."""
+    cfg = orchard.CONFIGS["C2"]
+    c, g, o = run_both(cfg)
+    assert g["n_bfs_replayed"] >= 1
+    assert_seedgen_parity(g, o)
+    c.close()
