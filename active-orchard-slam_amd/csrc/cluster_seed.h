@@ -37,10 +37,11 @@ int greedy_dedup(DedupScratch &S, const double2 *cand, const int *ok, int n, int
 struct ClusterSeedState {
     DedupScratch dedup;
     DevBuf fg_bits, word_cnt, word_off, fg_list, parent, root_flag, root_rank, cl_count, cl_off, cl_cursor, cl_cells;
-    DevBuf rec, row_idx, bfs_queue, bfs_vis, poly;
+    DevBuf rec, row_idx, poly, cur_tab;
     DevBuf cand_xy, cand_ok, cand_state, hash_count, hash_start, hash_slot, hash_sorted, seed_out, misc, scan_tmp;
     PinnedBuf h_misc;
-    int n_fg = 0, n_clusters = 0, n_rows = 0;
+    int n_fg = 0, n_clusters = 0, n_rows = 0, n_cur_tab = 0;
+    double cur_tab_amax = -1.0;
     std::vector<ClusterRec> h_rec;
 };
 

@@ -18,6 +18,8 @@
 #include <cmath>
 #include <cstring>
 
+#include <stdexcept>
+
 #include "cluster_seed.h"
 
 namespace aos {
@@ -25,7 +27,7 @@ namespace aos {
 static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 // isPointInPolygon seed_gen:1231-1255
-__device__ bool d_pip(double px, double py, const double *poly, int n) {
+__host__ __device__ bool d_pip(double px, double py, const double *poly, int n) {
     if (n < 3) return false;
     bool inside = false;
     int j = n - 1;
@@ -49,7 +51,7 @@ struct GridC {
 };
 
 // float world coordinate of a cell: origin + float(x) * res (float product, double add, to float)
-__device__ __forceinline__ float cell_world(double o, int i, float res) { return (float)(o + (double)((float)i * res)); }
+__host__ __device__ __forceinline__ float cell_world(double o, int i, float res) { return (float)(o + (double)((float)i * res)); }
 
 __device__ __forceinline__ bool bit_at(const uint64_t *bits, int WW, int x, int y) {
     return (bits[(size_t)y * WW + (x >> 6)] >> (x & 63)) & 1ull;
@@ -175,7 +177,7 @@ struct MaxOp { template <class T> __device__ T operator()(T a, T b) const { retu
 struct MinOp { template <class T> __device__ T operator()(T a, T b) const { return a < b ? a : b; } };
 struct AddOp { template <class T> __device__ T operator()(T a, T b) const { return a + b; } };
 
-__device__ __forceinline__ double2 cell_w(const GridC &g, int p) {
+__host__ __device__ __forceinline__ double2 cell_w(const GridC &g, int p) {
     int y = p / g.W, x = p - y * g.W;
     return make_double2((double)cell_world(g.ox, x, g.res), (double)cell_world(g.oy, y, g.res));
 }
@@ -336,50 +338,65 @@ __global__ __launch_bounds__(256) void k_cluster_stats(StatArgs A) {
     if (threadIdx.x == 0) A.rec[cid] = r;
 }
 
-// Exact replay of clusterOccupiedCells' FIFO BFS (seed_gen:1007-1049) for clusters without the
-// order-free certificate: one thread per flagged cluster (rare).
-__global__ void k_cluster_bfs(StatArgs A, const uint64_t *fg, const int *fg_off, const int *parent, int *queue,
-                              int *visited, int stamp_base) {
-    const int cid = blockIdx.x * blockDim.x + threadIdx.x;
-    if (cid >= A.n_clusters) return;
-    ClusterRec r = A.rec[cid];
-    if (!(r.flags & 2) || (r.flags & 4)) return;
-    const GridC &g = A.g;
-    const int b = A.off[cid], n = A.off[cid + 1] - b;
-    int *q = queue + b;
-    // start cell = first raster cell of the component = the root's pixel
-    int root = parent[fg_index(fg, fg_off, g, A.cells[b] % g.W, A.cells[b] / g.W)];
-    int start = A.list[root];
-    const int stamp = stamp_base + cid;
-    visited[root] = stamp;
+// ------------------------------------------------------------------ exact BFS replay (host)
+// clusterOccupiedCells' FIFO BFS (seed_gen:1007-1049) and the order-dependent statistics that follow
+// (float centre sums :1030-1046, first-strict-maximum endpoints :1354-1395) for the rare clusters
+// without the order-free certificate. This is a serial chain of dependent steps: it runs on the host
+// core next to the GPU (the cluster's cells come over in raster order), ~10 ns per step.
+static void host_bfs_replay(const int *cells, int n, const GridC &g, const double *poly, int np, float min_length,
+                            ClusterRec &r, std::vector<int> &q, std::vector<int> &tab) {
+    int cap = 64;
+    while (cap < 2 * n) cap <<= 1;
+    const unsigned mask = (unsigned)cap - 1;
+    tab.assign(cap, -1);
+    auto slot_of = [&](int key) -> int {   // key present -> its slot, else -1
+        unsigned h = ((unsigned)key * 2654435761u) & mask;
+        for (;;) {
+            int v = tab[h];
+            if (v == -1) return -1;
+            if ((v & 0x7fffffff) == key) return (int)h;
+            h = (h + 1) & mask;
+        }
+    };
+    for (int k = 0; k < n; ++k) {
+        unsigned h = ((unsigned)cells[k] * 2654435761u) & mask;
+        while (tab[h] != -1) h = (h + 1) & mask;
+        tab[h] = cells[k];
+    }
+    q.resize(n);
+    const int start = cells[0];   // first raster cell of the component
+    tab[slot_of(start)] |= (int)0x80000000;
     q[0] = start;
     int head = 0, tail = 1;
     const int dxs[8] = {-1, -1, -1, 0, 0, 1, 1, 1}, dys[8] = {-1, 0, 1, -1, 1, -1, 0, 1};
     while (head < tail) {
-        int p = q[head++], cy = p / g.W, cx = p - cy * g.W;
+        const int p = q[head++], cy = p / g.W, cx = p - cy * g.W;
         for (int i = 0; i < 8; ++i) {
-            int j = fg_index(fg, fg_off, g, cx + dxs[i], cy + dys[i]);
-            if (j < 0 || visited[j] == stamp) continue;
-            visited[j] = stamp;
-            q[tail++] = A.list[j];
+            const int nx = cx + dxs[i], ny = cy + dys[i];
+            if (nx < 0 || nx >= g.W || ny < 0 || ny >= g.H) continue;
+            const int h = slot_of(ny * g.W + nx);
+            if (h < 0 || tab[h] < 0) continue;
+            tab[h] |= (int)0x80000000;
+            q[tail++] = ny * g.W + nx;
         }
     }
+    if (tail != n) throw std::runtime_error("BFS replay: cluster is not 8-connected");
     float sum_x = 0.0f, sum_y = 0.0f;
     for (int k = 0; k < n; ++k) { int p = q[k], y = p / g.W; sum_x += (float)(p - y * g.W); sum_y += (float)y; }
     r.cx = sum_x / (float)n;
     r.cy = sum_y / (float)n;
     bool row = false;
-    if (r.length >= A.min_length) {
+    if (r.length >= min_length) {
         float cwx = (float)(g.ox + (double)(r.cx * g.res)), cwy = (float)(g.oy + (double)(r.cy * g.res));
         r.center = make_double2(cwx, cwy);
-        row = d_pip(cwx, cwy, A.poly, A.np);
+        row = d_pip(cwx, cwy, poly, np);
     }
     if (row) {
         double mx = 0.0; int fi = 0; double fx = 0, fy = 0;
         for (int k = 0; k < n; ++k) {
             double2 w = cell_w(g, q[k]);
             double dx = w.x - r.center.x, dy = w.y - r.center.y, d2 = dx * dx + dy * dy;
-            if (d2 > mx) { mx = d2; fi = k; double s = sqrt(d2); fx = dx / s; fy = dy / s; }
+            if (d2 > mx) { mx = d2; fi = k; double s = std::sqrt(d2); fx = dx / s; fy = dy / s; }
         }
         double mo = 0.0; int si = 0;
         for (int k = 0; k < n; ++k) {
@@ -387,7 +404,7 @@ __global__ void k_cluster_bfs(StatArgs A, const uint64_t *fg, const int *fg_off,
             double2 w = cell_w(g, q[k]);
             double dx = w.x - r.center.x, dy = w.y - r.center.y, d2 = dx * dx + dy * dy;
             double nx = dx, ny = dy;
-            if (d2 > 0.0) { double s = sqrt(d2); nx = dx / s; ny = dy / s; }
+            if (d2 > 0.0) { double s = std::sqrt(d2); nx = dx / s; ny = dy / s; }
             if (nx * fx + ny * fy < 0.0 && d2 > mo) { mo = d2; si = k; }
         }
         if (mo == 0.0) {
@@ -403,157 +420,6 @@ __global__ void k_cluster_bfs(StatArgs A, const uint64_t *fg, const int *fg_off,
         r.end = cell_w(g, q[si]);
     }
     r.flags = (row ? 1 : 0) | 4;  // 4: replayed
-    A.rec[cid] = r;
-}
-
-// Same replay, one wave per flagged cluster, cluster held in LDS: open-addressing table of the
-// cluster's pixel ids (bit 31 = visited) + the FIFO queue. One popped cell per step: lanes 0-7 test
-// its 8 neighbours in the reference order (seed_gen:986-987); new cells are appended in lane order,
-// exactly like the sequential push order. Clusters larger than kBfsQ cells use k_cluster_bfs.
-constexpr int kBfsTab = 16384, kBfsQ = 12288;
-__device__ __forceinline__ unsigned bfs_hash(int p) { return (unsigned)p * 2654435761u; }
-__device__ __forceinline__ int wave_min_i(int v) { for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o)); return v; }
-__device__ __forceinline__ double wave_max_d(double v) { for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o)); return v; }
-
-__global__ __launch_bounds__(64) void k_cluster_bfs_lds(StatArgs A, const int *flagged) {
-    __shared__ int tab[kBfsTab];
-    __shared__ int q[kBfsQ];
-    const int cid = flagged[blockIdx.x];
-    const int b = A.off[cid], n = A.off[cid + 1] - b, lane = threadIdx.x;
-    if (n > kBfsQ) return;
-    const GridC &g = A.g;
-    int cap = 64;
-    while (cap < 2 * n && cap < kBfsTab) cap <<= 1;
-    const unsigned mask = (unsigned)cap - 1;
-    for (int i = lane; i < cap; i += 64) tab[i] = INT_MAX;
-    __syncthreads();
-    int root = INT_MAX;
-    for (int k = lane; k < n; k += 64) {
-        int p = A.cells[b + k];
-        root = min(root, p);
-        unsigned h = bfs_hash(p) & mask;
-        while (atomicCAS(&tab[h], INT_MAX, p) != INT_MAX) h = (h + 1) & mask;
-    }
-    root = wave_min_i(root);  // first raster cell of the component
-    __syncthreads();
-    auto lookup = [&](int key) -> int {
-        unsigned h = bfs_hash(key) & mask;
-        while (true) {
-            int v = tab[h];
-            if (v == INT_MAX) return -1;
-            if ((v & 0x7fffffff) == key) return (int)h;
-            h = (h + 1) & mask;
-        }
-    };
-    if (lane == 0) { int h = lookup(root); tab[h] |= (int)0x80000000; q[0] = root; }
-    __syncthreads();
-    const int dxs[8] = {-1, -1, -1, 0, 0, 1, 1, 1}, dys[8] = {-1, 0, 1, -1, 1, -1, 0, 1};
-    int head = 0, tail = 1;
-    while (head < tail) {
-        const int p = q[head++];
-        const int cy = p / g.W, cx = p - cy * g.W;
-        bool cand = false;
-        int h = -1, key = 0;
-        if (lane < 8) {
-            int nx = cx + dxs[lane], ny = cy + dys[lane];
-            if (nx >= 0 && nx < g.W && ny >= 0 && ny < g.H) {
-                key = ny * g.W + nx;
-                h = lookup(key);
-                cand = h >= 0 && tab[h] >= 0;
-            }
-        }
-        unsigned long long m = __ballot(cand);
-        if (cand) {
-            int pos = __popcll(m & ((1ull << lane) - 1));
-            q[tail + pos] = key;
-            tab[h] = key | (int)0x80000000;
-        }
-        tail += __popcll(m);
-        __syncthreads();
-    }
-    // ---- order-dependent statistics, sequential where the reference is
-    ClusterRec r = A.rec[cid];
-    float sum_x = 0.0f, sum_y = 0.0f;
-    if (lane == 0)
-        for (int k = 0; k < n; ++k) { int pp = q[k], y = pp / g.W; sum_x += (float)(pp - y * g.W); sum_y += (float)y; }
-    sum_x = __shfl(sum_x, 0); sum_y = __shfl(sum_y, 0);
-    r.cx = sum_x / (float)n;
-    r.cy = sum_y / (float)n;
-    bool row = false;
-    if (r.length >= A.min_length) {
-        float cwx = (float)(g.ox + (double)(r.cx * g.res)), cwy = (float)(g.oy + (double)(r.cy * g.res));
-        r.center = make_double2(cwx, cwy);
-        row = d_pip(cwx, cwy, A.poly, A.np);
-    }
-    if (row) {
-        // first strict maximum in BFS order = (max d2, then min BFS rank)
-        double m1 = 0.0;
-        for (int k = lane; k < n; k += 64) {
-            double2 w = cell_w(g, q[k]);
-            double dx = w.x - r.center.x, dy = w.y - r.center.y;
-            m1 = fmax(m1, dx * dx + dy * dy);
-        }
-        m1 = wave_max_d(m1);
-        int fi = INT_MAX;
-        for (int k = lane; k < n; k += 64) {
-            double2 w = cell_w(g, q[k]);
-            double dx = w.x - r.center.x, dy = w.y - r.center.y;
-            if (dx * dx + dy * dy == m1 && m1 > 0.0) { fi = min(fi, k); }
-        }
-        fi = wave_min_i(fi);
-        if (fi == INT_MAX) fi = 0;
-        const double2 wf = cell_w(g, q[fi]);
-        double fdx = wf.x - r.center.x, fdy = wf.y - r.center.y, fx = 0, fy = 0;
-        { double z = fdx * fdx + fdy * fdy; if (z > 0.0) { double sq = sqrt(z); fx = fdx / sq; fy = fdy / sq; } }
-        double m2 = 0.0;
-        for (int k = lane; k < n; k += 64) {
-            if (k == fi) continue;
-            double2 w = cell_w(g, q[k]);
-            double dx = w.x - r.center.x, dy = w.y - r.center.y, d2 = dx * dx + dy * dy;
-            double nx = dx, ny = dy;
-            if (d2 > 0.0) { double sq = sqrt(d2); nx = dx / sq; ny = dy / sq; }
-            if (nx * fx + ny * fy < 0.0) m2 = fmax(m2, d2);
-        }
-        m2 = wave_max_d(m2);
-        int si = INT_MAX;
-        if (m2 > 0.0) {
-            for (int k = lane; k < n; k += 64) {
-                if (k == fi) continue;
-                double2 w = cell_w(g, q[k]);
-                double dx = w.x - r.center.x, dy = w.y - r.center.y, d2 = dx * dx + dy * dy;
-                double nx = dx, ny = dy;
-                if (d2 > 0.0) { double sq = sqrt(d2); nx = dx / sq; ny = dy / sq; }
-                if (nx * fx + ny * fy < 0.0 && d2 == m2) si = min(si, k);
-            }
-        } else {  // farthest from the first endpoint
-            double m3 = 0.0;
-            for (int k = lane; k < n; k += 64) {
-                if (k == fi) continue;
-                double2 w = cell_w(g, q[k]);
-                double dx = w.x - wf.x, dy = w.y - wf.y;
-                m3 = fmax(m3, dx * dx + dy * dy);
-            }
-            m3 = wave_max_d(m3);
-            for (int k = lane; k < n; k += 64) {
-                if (k == fi) continue;
-                double2 w = cell_w(g, q[k]);
-                double dx = w.x - wf.x, dy = w.y - wf.y;
-                if (dx * dx + dy * dy == m3 && m3 > 0.0) si = min(si, k);
-            }
-        }
-        si = wave_min_i(si);
-        if (si == INT_MAX) si = 0;
-        r.start = wf;
-        r.end = cell_w(g, q[si]);
-    }
-    r.flags = (row ? 1 : 0) | 4;
-    if (lane == 0) A.rec[cid] = r;
-}
-__global__ void k_flag_list(const ClusterRec *rec, int ncl, int *list, int *count, int qmax, int big) {
-    int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= ncl || !(rec[c].flags & 2)) return;
-    if ((rec[c].n > qmax) != (big != 0)) return;
-    list[atomicAdd(count, 1)] = c;
 }
 
 // ------------------------------------------------------------------ rays
@@ -582,18 +448,16 @@ __device__ bool d_raycast(const uint64_t *skel, const GridC &g, double sx, doubl
         }
 #pragma unroll
         for (int j = 0; j < kLook; ++j) {
-            hit[j] = false;
+            // every lookup is issued (clamped cell), the loop conditions only mask the result
             double ddx = px[j] - sx, ddy = py[j] - sy;
             double dist = sqrt(ddx * ddx + ddy * ddy);
-            if (i0 + j < max_steps && !(dist < 1.0)) {
-                float fx = (float)px[j], fy = (float)py[j];
-                float rel_x = (float)(((double)fx - g.ox) / (double)g.res);
-                float rel_y = (float)(((double)fy - g.oy) / (double)g.res);
-                int gx = (int)floorf(rel_x), gy = (int)floorf(rel_y);
-                gx = gx < 0 ? 0 : (gx >= g.W ? g.W - 1 : gx);
-                gy = gy < 0 ? 0 : (gy >= g.H ? g.H - 1 : gy);
-                hit[j] = bit_at(skel, g.WW, gx, gy);
-            }
+            float fx = (float)px[j], fy = (float)py[j];
+            float rel_x = (float)(((double)fx - g.ox) / (double)g.res);
+            float rel_y = (float)(((double)fy - g.oy) / (double)g.res);
+            float flx = floorf(rel_x), fly = floorf(rel_y);
+            int gx = !(flx > 0.0f) ? 0 : (flx >= (float)(g.W - 1) ? g.W - 1 : (int)flx);
+            int gy = !(fly > 0.0f) ? 0 : (fly >= (float)(g.H - 1) ? g.H - 1 : (int)fly);
+            hit[j] = (i0 + j < max_steps && !(dist < 1.0)) && bit_at(skel, g.WW, gx, gy);
         }
 #pragma unroll
         for (int j = 0; j < kLook; ++j)
@@ -629,10 +493,16 @@ __global__ void k_virtual_candidates(const RowDev *rows, int n_rows, int n_slots
 
 struct RayAngles { double cs[3], sn[3]; int pos_branch[3]; };  // 0, -90, +90 degrees
 
-// castRayFromEndpoint seed_gen:1774-1891 + the filters of generateRayPointsFromEndpoints :1941-1961
-__global__ void k_endpoint_rays(const RowDev *rows, int n_rows, const uint64_t *skel, GridC g, RayAngles ang,
-                                const double *poly, int np, double2 *cand, int *ok) {
-    int s = blockIdx.x * blockDim.x + threadIdx.x;
+// castRayFromEndpoint seed_gen:1774-1891 + the filters of generateRayPointsFromEndpoints :1941-1961.
+// One wave per ray, 64 consecutive march steps per iteration. The reference's distance sequence
+// (current_dist = 1.0; current_dist += 0.1, :1833-1871) is the same for every ray, so the host
+// tabulates it once with the same double adds (cur_tab[i] = value at step i; the table ends with the
+// first value > absolute_max_distance). Each lane evaluates its step with an unconditional (clamped)
+// skeleton load; the first lane with an event (loop end, left the grid, occupied cell) decides.
+__global__ __launch_bounds__(64) void k_endpoint_rays(const RowDev *rows, int n_rows, const uint64_t *skel, GridC g,
+                                                      RayAngles ang, const double *poly, int np, const double *cur_tab,
+                                                      int n_tab, double2 *cand, int *ok) {
+    const int s = blockIdx.x, lane = threadIdx.x;
     if (s >= n_rows * 6) return;
     const RowDev R = rows[s / 6];
     const int k = s % 6, a = k % 3;
@@ -642,38 +512,40 @@ __global__ void k_endpoint_rays(const RowDev *rows, int n_rows, const uint64_t *
     double dist = sqrt(ex * ex + ey * ey);
     if (dist < 1e-6) { ex = 1.0; ey = 0.0; }
     else { ex = ex / dist; ey = ey / dist; }
-    double ox_ = -ex, oy_ = -ey, px = -ey, py = ex;
+    double ox_ = -ex, oy_ = -ey, px0 = -ey, py0 = ex;
     double rx, ry;
-    if (ang.pos_branch[a]) { rx = ang.cs[a] * ox_ + ang.sn[a] * px; ry = ang.cs[a] * oy_ + ang.sn[a] * py; }
-    else { rx = ang.cs[a] * ox_ + ang.sn[a] * (-px); ry = ang.cs[a] * oy_ + ang.sn[a] * (-py); }
+    if (ang.pos_branch[a]) { rx = ang.cs[a] * ox_ + ang.sn[a] * px0; ry = ang.cs[a] * oy_ + ang.sn[a] * py0; }
+    else { rx = ang.cs[a] * ox_ + ang.sn[a] * (-px0); ry = ang.cs[a] * oy_ + ang.sn[a] * (-py0); }
     { double z = rx * rx + ry * ry; if (z > 0.0) { double q = sqrt(z); rx = rx / q; ry = ry / q; } }
-    double cur = 1.0;
     double resx = 0, resy = 0;
-    bool done = false, ended = false;
-    while (!done && !ended) {
-        double px[kLook], py[kLook];
-        bool valid[kLook], ins[kLook], occ[kLook];
-#pragma unroll
-        for (int j = 0; j < kLook; ++j) {   // while (current_dist <= max) { p = start + dir*cur; ...; cur += 0.1; }
-            valid[j] = cur <= g.amax;
-            px[j] = stx + rx * cur; py[j] = sty + ry * cur;
-            cur += 0.1;
+    bool done = false;
+    for (int base = 0; base < n_tab; base += 64) {
+        const int i = base + lane;
+        const double cur = cur_tab[i < n_tab ? i : n_tab - 1];
+        const bool valid = i < n_tab && cur <= g.amax;
+        const double px = stx + rx * cur, py = sty + ry * cur;
+        const bool ins = px >= g.minx && px <= g.maxx && py >= g.miny && py <= g.maxy;
+        bool inr = false;
+        int mx = 0, my = 0;
+        if (ins) {
+            mx = (int)((px - g.ox) / (double)g.res); my = (int)((py - g.oy) / (double)g.res);
+            inr = mx >= 0 && mx < g.W && my >= 0 && my < g.H;
         }
-#pragma unroll
-        for (int j = 0; j < kLook; ++j) {
-            ins[j] = px[j] >= g.minx && px[j] <= g.maxx && py[j] >= g.miny && py[j] <= g.maxy;
-            occ[j] = false;
-            if (valid[j] && ins[j]) {
-                int mx = (int)((px[j] - g.ox) / (double)g.res), my = (int)((py[j] - g.oy) / (double)g.res);
-                occ[j] = mx >= 0 && mx < g.W && my >= 0 && my < g.H && bit_at(skel, g.WW, mx, my);
+        const int cx = inr ? mx : 0, cy = inr ? my : 0;
+        const uint64_t w = skel[(size_t)cy * g.WW + (cx >> 6)];
+        const bool occ = inr && ((w >> (cx & 63)) & 1ull);
+        const bool ev = !valid || !ins || occ;
+        const unsigned long long m = __ballot(ev);
+        if (m) {
+            const int j = __ffsll((long long)m) - 1;
+            const double qx = __shfl(px, j), qy = __shfl(py, j);
+            const bool qvalid = __shfl((int)valid, j), qins = __shfl((int)ins, j);
+            if (qvalid) {
+                done = true;
+                if (!qins) { resx = fmax(g.minx, fmin(g.maxx, qx)); resy = fmax(g.miny, fmin(g.maxy, qy)); }
+                else { resx = qx; resy = qy; }
             }
-        }
-#pragma unroll
-        for (int j = 0; j < kLook; ++j) {
-            if (done || ended) continue;
-            if (!valid[j]) { ended = true; continue; }
-            if (!ins[j]) { resx = fmax(g.minx, fmin(g.maxx, px[j])); resy = fmax(g.miny, fmin(g.maxy, py[j])); done = true; continue; }
-            if (occ[j]) { resx = px[j]; resy = py[j]; done = true; }
+            break;
         }
     }
     if (!done) {
@@ -683,10 +555,12 @@ __global__ void k_endpoint_rays(const RowDev *rows, int n_rows, const uint64_t *
         }
         resx = fx; resy = fy;
     }
-    int good = isfinite(resx) && isfinite(resy) && resx >= g.minx && resx <= g.maxx && resy >= g.miny && resy <= g.maxy &&
-               !d_pip(resx, resy, poly, np);
-    cand[s] = make_double2(resx, resy);
-    ok[s] = good;
+    if (lane == 0) {
+        int good = isfinite(resx) && isfinite(resy) && resx >= g.minx && resx <= g.maxx && resy >= g.miny &&
+                   resy <= g.maxy && !d_pip(resx, resy, poly, np);
+        cand[s] = make_double2(resx, resy);
+        ok[s] = good;
+    }
 }
 
 __global__ void k_endpoint_candidates(const RowDev *rows, int n_rows, double2 *cand, int *ok) {
@@ -728,7 +602,7 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
     dim3 gw2(cdiv(g.WW, 64), g.H);
     k_fg<<<gw2, 64, 0, s>>>(in.skel_bits, d_fg, d_wc, g, d_poly, np);
     size_t tb = 0;
-    hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (int *)nullptr, (int *)nullptr, (int)Cw + 1, s);
+    AOS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (int *)nullptr, (int *)nullptr, (int)Cw + 1, s));
     void *tmp = S.scan_tmp.ensure(tb);
     AOS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, d_wc, d_wo, (int)Cw + 1, s));
     AOS_HIP(hipMemcpyAsync(h_sc, d_wo + Cw, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -748,7 +622,7 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         AOS_HIP(hipMemsetAsync(d_isroot + nf, 0, sizeof(int), s));
         k_ccl_flatten<<<cdiv(nf, 256), 256, 0, s>>>(d_par, d_isroot, nf);
         size_t tb2 = 0;
-        hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, (int *)nullptr, (int *)nullptr, nf + 1, s);
+        AOS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, (int *)nullptr, (int *)nullptr, nf + 1, s));
         tmp = S.scan_tmp.ensure(std::max(tb, tb2));
         AOS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, d_isroot, d_rank, nf + 1, s));
         AOS_HIP(hipMemcpyAsync(h_sc, d_rank + nf, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -778,20 +652,20 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         for (const auto &r : S.h_rec) n_bfs += (r.flags & 2) != 0;
         out.n_bfs = n_bfs;
         if (n_bfs) {
-            // small/medium clusters: one wave each, LDS-resident replay
-            int *d_fl = dev<int>(S.bfs_vis, ncl + 2), *d_fc = d_fl + ncl;
-            AOS_HIP(hipMemsetAsync(d_fc, 0, sizeof(int), s));
-            k_flag_list<<<cdiv(ncl, 256), 256, 0, s>>>(d_rec, ncl, d_fl, d_fc, kBfsQ, 0);
-            int n_small = 0;
-            for (const auto &r : S.h_rec) n_small += (r.flags & 2) && r.n <= kBfsQ;
-            if (n_small) k_cluster_bfs_lds<<<n_small, 64, 0, s>>>(A, d_fl);
-            if (n_small < n_bfs) {  // very large clusters: global-memory replay, one thread each
-                int *d_q = dev<int>(S.bfs_queue, nf), *d_vis = dev<int>(S.row_idx, nf);
-                AOS_HIP(hipMemsetAsync(d_vis, 0xFF, sizeof(int) * nf, s));
-                k_cluster_bfs<<<cdiv(ncl, 64), 64, 0, s>>>(A, d_fg, d_wo, d_par, d_q, d_vis, 0);
-            }
-            AOS_HIP(hipMemcpyAsync(S.h_rec.data(), d_rec, sizeof(ClusterRec) * ncl, hipMemcpyDeviceToHost, s));
+            std::vector<long long> off(ncl + 1, 0);
+            for (int c = 0; c < ncl; ++c) off[c + 1] = off[c] + S.h_rec[c].n;
+            std::vector<int> hc;
+            std::vector<std::pair<int, size_t>> fl;   // (cluster, offset into hc)
+            for (int c = 0; c < ncl; ++c)
+                if (S.h_rec[c].flags & 2) { fl.push_back({c, hc.size()}); hc.resize(hc.size() + S.h_rec[c].n); }
+            for (const auto &f : fl)
+                AOS_HIP(hipMemcpyAsync(hc.data() + f.second, d_cells + off[f.first], sizeof(int) * S.h_rec[f.first].n,
+                                       hipMemcpyDeviceToHost, s));
             AOS_HIP(hipStreamSynchronize(s));
+            std::vector<int> q, tab;
+            for (const auto &f : fl)
+                host_bfs_replay(hc.data() + f.second, S.h_rec[f.first].n, g, hp.data(), np,
+                                static_cast<float>(in.cluster_min_length), S.h_rec[f.first], q, tab);
         }
         // ---- tree rows in cluster order (convertClustersToTreeRows, seed_gen:1329-1406)
         int slot = 0;
@@ -858,7 +732,17 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         if (degs[a] > 0) { ang.cs[a] = std::cos(rad); ang.sn[a] = std::sin(rad); ang.pos_branch[a] = 1; }
         else { ang.cs[a] = std::cos(-rad); ang.sn[a] = std::sin(-rad); ang.pos_branch[a] = 0; }
     }
-    k_endpoint_rays<<<cdiv(6 * nr, 64), 64, 0, s>>>(d_rows, nr, in.skel_bits, g, ang, d_poly, np, d_cand, d_ok);
+    if (S.cur_tab_amax != g.amax) {   // current_dist sequence of castRayFromEndpoint (:1833-1871)
+        std::vector<double> t;
+        for (double cur = 1.0;; cur += 0.1) { t.push_back(cur); if (!(cur <= g.amax)) break; }
+        S.n_cur_tab = (int)t.size();
+        double *d = dev<double>(S.cur_tab, t.size());
+        AOS_HIP(hipMemcpyAsync(d, t.data(), sizeof(double) * t.size(), hipMemcpyHostToDevice, s));
+        AOS_HIP(hipStreamSynchronize(s));
+        S.cur_tab_amax = g.amax;
+    }
+    k_endpoint_rays<<<6 * nr, 64, 0, s>>>(d_rows, nr, in.skel_bits, g, ang, d_poly, np,
+                                          static_cast<const double *>(S.cur_tab.p), S.n_cur_tab, d_cand, d_ok);
     n_ray = greedy_dedup(scr, d_cand, d_ok, 6 * nr, kConflictLess, 0.5, h, d_seeds + n_virtual, nullptr, s, h_sc);
     k_endpoint_candidates<<<cdiv(2 * nr, 64), 64, 0, s>>>(d_rows, nr, d_cand, d_ok);
     n_end = greedy_dedup(scr, d_cand, d_ok, 2 * nr, kConflictLess, 0.5, h, d_seeds + n_virtual + n_ray, nullptr, s, h_sc);

@@ -102,20 +102,35 @@ __global__ void k_ror_raster(RorLaunch L, const int *bin_start, const float4 *so
         cand = __float_as_int(p.w) != 0;
         if (cand) {
             int bx, by;
-            bin_of(L, p.x, p.y, bx, by);
+            const int ob = bin_of(L, p.x, p.y, bx, by);
             int cnt = 0;
+            // The keep decision only needs "at least need points within r", so the scan order is
+            // free: the point's own bin first, starting at the point itself (its nearest neighbours
+            // are adjacent in bin order), then the rest of the 3x3 bins. Four loads per round trip.
+            auto scan = [&](int k0, int k1) {
+                for (int k = k0; k < k1 && cnt < L.need; k += 4) {
+                    float4 q[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) q[j] = sorted[min(k + j, k1 - 1)];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        float dx = p.x - q[j].x, dy = p.y - q[j].y, dz = p.z - q[j].z;
+                        float d2 = dx * dx;
+                        d2 = d2 + dy * dy;
+                        d2 = d2 + dz * dz;
+                        bool in = L.is_dense ? ((double)d2 <= L.r2) : (d2 < L.r2f);
+                        cnt += (k + j < k1 && in) ? 1 : 0;
+                    }
+                }
+            };
+            const int os = bin_start[ob], oe = bin_start[ob + 1];
+            scan(s, oe);
+            scan(os, s);
             for (int yy = max(by - 1, 0); yy <= min(by + 1, L.nby - 1) && cnt < L.need; ++yy) {
                 int b0 = yy * L.nbx + max(bx - 1, 0), b1 = yy * L.nbx + min(bx + 1, L.nbx - 1);
                 int k0 = bin_start[b0], k1 = bin_start[b1 + 1];
-                for (int k = k0; k < k1; ++k) {
-                    float4 q = sorted[k];
-                    float dx = p.x - q.x, dy = p.y - q.y, dz = p.z - q.z;
-                    float d2 = dx * dx;
-                    d2 = d2 + dy * dy;
-                    d2 = d2 + dz * dz;
-                    bool in = L.is_dense ? ((double)d2 <= L.r2) : (d2 < L.r2f);
-                    if (in && ++cnt >= L.need) break;
-                }
+                if (yy == by) { scan(k0, os); scan(oe, k1); }
+                else scan(k0, k1);
             }
             kept = cnt >= L.need;
             if (kept) {
@@ -146,7 +161,7 @@ void launch_ror_raster(const RorLaunch &L, const int *bin_start, const float4 *s
 
 size_t scan_temp_bytes(int n) {
     size_t t = 0;
-    hipcub::DeviceScan::ExclusiveSum(nullptr, t, (const int *)nullptr, (int *)nullptr, n);
+    AOS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t, (const int *)nullptr, (int *)nullptr, n));
     return t;
 }
 void launch_exclusive_scan(const int *in, int *out, int n, void *temp, size_t temp_bytes, hipStream_t s) {

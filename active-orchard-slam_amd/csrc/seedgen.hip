@@ -15,8 +15,8 @@ void aos_ctx::release() {
         b->release();
     h_small.release();
     for (DevBuf *b : {&cs.fg_bits, &cs.word_cnt, &cs.word_off, &cs.fg_list, &cs.parent, &cs.root_flag, &cs.root_rank,
-                      &cs.cl_count, &cs.cl_off, &cs.cl_cursor, &cs.cl_cells, &cs.rec, &cs.row_idx, &cs.bfs_queue,
-                      &cs.bfs_vis, &cs.poly, &cs.cand_xy, &cs.cand_ok, &cs.cand_state, &cs.hash_count,
+                      &cs.cl_count, &cs.cl_off, &cs.cl_cursor, &cs.cl_cells, &cs.rec, &cs.row_idx, &cs.cur_tab,
+                      &cs.poly, &cs.cand_xy, &cs.cand_ok, &cs.cand_state, &cs.hash_count,
                       &cs.hash_start, &cs.hash_slot, &cs.hash_sorted, &cs.seed_out, &cs.misc, &cs.scan_tmp})
         b->release();
     cs.h_misc.release();
