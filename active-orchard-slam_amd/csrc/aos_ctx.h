@@ -23,7 +23,7 @@ struct aos_ctx {
     // ---- device buffers
     aos::DevBuf cloud_copy, bin_count, bin_start, pt_binslot, sorted, scan_tmp, counters;
     aos::DevBuf raster_bytes, raster_bits, infl_bits, open_bits, thin_a, thin_b, occ_bytes, skel_bytes, flags;
-    aos::PinnedBuf h_small;
+    aos::PinnedBuf h_small, h_stats;
     const uint64_t *skel_bits = nullptr;   // final thinning buffer (thin_a or thin_b)
     aos::FrameGeom geom{};
     int thin_iters = 0;

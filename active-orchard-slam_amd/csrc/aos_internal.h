@@ -74,8 +74,8 @@ struct RorLaunch {
 };
 void launch_ror_bin(const RorLaunch &L, int *bin_count, int2 *pt_binslot, hipStream_t s);
 void launch_ror_scatter(const RorLaunch &L, const int *bin_start, const int2 *pt_binslot, float4 *sorted, hipStream_t s);
-void launch_ror_raster(const RorLaunch &L, const int *bin_start, const float4 *sorted, const int *d_n_binned, int n_max,
-                       uint8_t *raster, unsigned long long *counters, hipStream_t s);
+void launch_ror_raster(const RorLaunch &L, const int *bin_start, const float4 *sorted, uint8_t *raster,
+                       unsigned long long *counters, hipStream_t s);
 void launch_pack_bits(const uint8_t *bytes, uint64_t *bits, int W, int H, int WW, hipStream_t s);
 void launch_inflate(const uint64_t *in, uint64_t *out, const FrameGeom &g, hipStream_t s);
 void launch_bits_to_bytes(const uint64_t *bits, int8_t *out, const FrameGeom &g, int frame, hipStream_t s);

@@ -9,6 +9,9 @@
 // (int8 {0,100}) exist only for the published OccupancyGrid outputs.
 #include <hipcub/hipcub.hpp>
 
+#include <climits>
+#include <stdexcept>
+
 #include "aos_internal.h"
 
 namespace aos {
@@ -92,57 +95,94 @@ __global__ void k_ror_scatter(RorLaunch L, const int *bin_start, const int2 *pt_
 //   dense: kNN k = need, keep iff need points have (double)d2 <= r^2;
 //   !dense: radius search d2 < float(r^2), keep iff count >= need.
 // Kept candidates mark their cell (generateOccupancyGrid seed_gen:606-619: double divide, trunc).
-__global__ void k_ror_raster(RorLaunch L, const int *bin_start, const float4 *sorted, const int *d_n_binned, uint8_t *raster,
-                             unsigned long long *counters) {
-    int s = blockIdx.x * blockDim.x + threadIdx.x;
-    const int n_binned = *d_n_binned;
-    bool cand = false, kept = false;
-    if (s < n_binned) {
-        float4 p = sorted[s];
-        cand = __float_as_int(p.w) != 0;
-        if (cand) {
-            int bx, by;
-            const int ob = bin_of(L, p.x, p.y, bx, by);
-            int cnt = 0;
-            // The keep decision only needs "at least need points within r", so the scan order is
-            // free: the point's own bin first, starting at the point itself (its nearest neighbours
-            // are adjacent in bin order), then the rest of the 3x3 bins. Four loads per round trip.
-            auto scan = [&](int k0, int k1) {
-                for (int k = k0; k < k1 && cnt < L.need; k += 4) {
-                    float4 q[4];
+//
+// LDS-staged bins: one workgroup per strip of kSW bins of one bin row. The strip's 3 x (kSW + 2)
+// neighbourhood bins are 3 contiguous ranges of the bin-sorted point array; they are copied into
+// LDS with coalesced loads (~500 points = 8 KB on orchard clouds), then each candidate of the strip
+// counts its neighbours from LDS. A strip whose neighbourhood exceeds kRorCap points reads the
+// same ranges from global memory instead. The keep decision only needs "at least need points
+// within r", so the scan order is free (own bin row first) and stops early.
+constexpr int kSW = 32, kRorCap = 1536, kRorTB = 128;
+
+__device__ __forceinline__ bool ror_in(const RorLaunch &L, float4 p, float4 q) {
+    float dx = p.x - q.x, dy = p.y - q.y, dz = p.z - q.z;
+    float d2 = dx * dx;
+    d2 = d2 + dy * dy;
+    d2 = d2 + dz * dz;
+    return L.is_dense ? ((double)d2 <= L.r2) : (d2 < L.r2f);
+}
+template <class Ptr>
+__device__ __forceinline__ int ror_scan(const RorLaunch &L, float4 p, Ptr pts, int k0, int k1, int cnt) {
+    for (int k = k0; k < k1 && cnt < L.need; k += 4) {
+        float4 q[4];
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) q[j] = sorted[min(k + j, k1 - 1)];
+        for (int j = 0; j < 4; ++j) q[j] = pts[min(k + j, k1 - 1)];
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        float dx = p.x - q[j].x, dy = p.y - q[j].y, dz = p.z - q[j].z;
-                        float d2 = dx * dx;
-                        d2 = d2 + dy * dy;
-                        d2 = d2 + dz * dz;
-                        bool in = L.is_dense ? ((double)d2 <= L.r2) : (d2 < L.r2f);
-                        cnt += (k + j < k1 && in) ? 1 : 0;
-                    }
-                }
-            };
-            const int os = bin_start[ob], oe = bin_start[ob + 1];
-            scan(s, oe);
-            scan(os, s);
-            for (int yy = max(by - 1, 0); yy <= min(by + 1, L.nby - 1) && cnt < L.need; ++yy) {
-                int b0 = yy * L.nbx + max(bx - 1, 0), b1 = yy * L.nbx + min(bx + 1, L.nbx - 1);
-                int k0 = bin_start[b0], k1 = bin_start[b1 + 1];
-                if (yy == by) { scan(k0, os); scan(oe, k1); }
-                else scan(k0, k1);
-            }
-            kept = cnt >= L.need;
-            if (kept) {
-                int gx = (int)(((double)p.x - L.origin_x) / (double)L.res);
-                int gy = (int)(((double)p.y - L.origin_y) / (double)L.res);
-                if (gx >= 0 && gx < L.W && gy >= 0 && gy < L.H) raster[(size_t)gy * L.W + gx] = 1;
-            }
+        for (int j = 0; j < 4; ++j) cnt += (k + j < k1 && ror_in(L, p, q[j])) ? 1 : 0;
+    }
+    return cnt;
+}
+
+__global__ __launch_bounds__(kRorTB) void k_ror_tile(RorLaunch L, const int *bin_start, const float4 *sorted,
+                                                     uint8_t *raster, unsigned long long *counters) {
+    __shared__ float4 pts[kRorCap];
+    __shared__ int offs[3][kSW + 3];   // global offsets of bins xlo .. xhi + 1 in rows by-1, by, by+1
+    __shared__ int base[4];
+    const int nstrip = (L.nbx + kSW - 1) / kSW;
+    const int by = blockIdx.x / nstrip, bx0 = (blockIdx.x - by * nstrip) * kSW;
+    const int bx1 = min(bx0 + kSW, L.nbx);                        // own bins [bx0, bx1)
+    const int xlo = max(bx0 - 1, 0), xhi = min(bx1, L.nbx - 1);  // neighbourhood bins, inclusive
+    const int nbins = xhi - xlo + 1;
+    for (int t = threadIdx.x; t < 3 * (nbins + 1); t += kRorTB) {
+        const int r = t / (nbins + 1), c = t - r * (nbins + 1), yy = by - 1 + r;
+        offs[r][c] = (yy >= 0 && yy < L.nby) ? bin_start[yy * L.nbx + xlo + c] : 0;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        base[0] = 0;
+        base[1] = offs[0][nbins] - offs[0][0];
+        base[2] = base[1] + offs[1][nbins] - offs[1][0];
+        base[3] = base[2] + offs[2][nbins] - offs[2][0];
+    }
+    __syncthreads();
+    const int own0 = offs[1][bx0 - xlo], own1 = offs[1][bx1 - xlo];
+    if (own0 == own1) return;   // uniform across the workgroup
+    const int total = base[3];
+    const bool fits = total <= kRorCap;
+    if (fits) {
+        for (int t = threadIdx.x; t < total; t += kRorTB) {
+            const int r = t < base[1] ? 0 : (t < base[2] ? 1 : 2);
+            pts[t] = sorted[offs[r][0] + (t - base[r])];
+        }
+        __syncthreads();
+    }
+    unsigned kept_n = 0;
+    for (int k = own0 + threadIdx.x; k < own1; k += kRorTB) {
+        const float4 p = fits ? pts[base[1] + (k - offs[1][0])] : sorted[k];
+        if (__float_as_int(p.w) == 0) continue;   // not a clip candidate
+        int bx, byy;
+        bin_of(L, p.x, p.y, bx, byy);
+        const int c0 = max(bx - 1, xlo) - xlo, c1 = min(bx + 1, xhi) - xlo + 1;
+        int cnt = 0;
+#pragma unroll
+        for (int rr = 0; rr < 3; ++rr) {
+            const int r = rr == 0 ? 1 : (rr == 1 ? 0 : 2);   // own bin row first
+            const int yy = by - 1 + r;
+            if (yy < 0 || yy >= L.nby || cnt >= L.need) continue;
+            const int g0 = offs[r][c0], g1 = offs[r][c1];
+            if (fits) cnt = ror_scan(L, p, pts, base[r] + (g0 - offs[r][0]), base[r] + (g1 - offs[r][0]), cnt);
+            else cnt = ror_scan(L, p, sorted, g0, g1, cnt);
+        }
+        if (cnt >= L.need) {
+            ++kept_n;
+            int gx = (int)(((double)p.x - L.origin_x) / (double)L.res);
+            int gy = (int)(((double)p.y - L.origin_y) / (double)L.res);
+            if (gx >= 0 && gx < L.W && gy >= 0 && gy < L.H) raster[(size_t)gy * L.W + gx] = 1;
         }
     }
     // stats: candidates that survived ROR (n_clipped); wave-aggregated
-    unsigned long long m = __ballot(kept);
-    if ((threadIdx.x & 63) == 0 && m) atomicAdd(&counters[0], (unsigned long long)__popcll(m));
+    for (int o = 32; o > 0; o >>= 1) kept_n += __shfl_xor(kept_n, o);
+    if ((threadIdx.x & 63) == 0 && kept_n) atomicAdd(&counters[0], (unsigned long long)kept_n);
 }
 
 void launch_ror_bin(const RorLaunch &L, int *bin_count, int2 *pt_binslot, hipStream_t s) {
@@ -153,10 +193,12 @@ void launch_ror_scatter(const RorLaunch &L, const int *bin_start, const int2 *pt
     if (!L.n) return;
     k_ror_scatter<<<cdiv(L.n, 256), 256, 0, s>>>(L, bin_start, pt_binslot, sorted);
 }
-void launch_ror_raster(const RorLaunch &L, const int *bin_start, const float4 *sorted, const int *d_n_binned, int n_max,
-                       uint8_t *raster, unsigned long long *counters, hipStream_t s) {
-    if (n_max <= 0) return;
-    k_ror_raster<<<cdiv(n_max, 256), 256, 0, s>>>(L, bin_start, sorted, d_n_binned, raster, counters);
+void launch_ror_raster(const RorLaunch &L, const int *bin_start, const float4 *sorted, uint8_t *raster,
+                       unsigned long long *counters, hipStream_t s) {
+    const long long nblk = (long long)L.nby * ((L.nbx + kSW - 1) / kSW);
+    if (nblk <= 0) return;
+    if (nblk > INT_MAX) throw std::runtime_error("ROR bin grid too large");
+    k_ror_tile<<<(int)nblk, kRorTB, 0, s>>>(L, bin_start, sorted, raster, counters);
 }
 
 size_t scan_temp_bytes(int n) {

@@ -14,6 +14,7 @@ void aos_ctx::release() {
                       &raster_bits, &infl_bits, &open_bits, &thin_a, &thin_b, &occ_bytes, &skel_bytes, &flags})
         b->release();
     h_small.release();
+    h_stats.release();
     for (DevBuf *b : {&cs.fg_bits, &cs.word_cnt, &cs.word_off, &cs.fg_list, &cs.parent, &cs.root_flag, &cs.root_rank,
                       &cs.cl_count, &cs.cl_off, &cs.cl_cursor, &cs.cl_cells, &cs.rec, &cs.row_idx, &cs.cur_tab,
                       &cs.poly, &cs.cand_xy, &cs.cand_ok, &cs.cand_state, &cs.hash_count,
@@ -75,6 +76,7 @@ void aos_ctx::run_seedgen(bool want_host, aos_seedgen_out &out) {
     hipStream_t s = stream;
     const size_t C = (size_t)g.W * g.H, Cw = (size_t)g.WW * g.H;
     AOS_HIP(hipEventRecord(ev[0], s));
+    static_cast<int *>(h_stats.ensure(64))[0] = 0;
 
     // ---------------- a1-a4: ROR restricted to the clip box, clip, exclusion discs, raster
     RorLaunch L{};
@@ -114,7 +116,10 @@ void aos_ctx::run_seedgen(bool want_host, aos_seedgen_out &out) {
         // total binned = bin_start[nb]; bound the sorted buffer by n_points
         float4 *d_sorted = static_cast<float4 *>(sorted.ensure(sizeof(float4) * std::max<uint64_t>(n_points, 1)));
         launch_ror_scatter(L, d_bs, d_ps, d_sorted, s);
-        launch_ror_raster(L, d_bs, d_sorted, d_bs + nb, (int)n_points, d_rb, d_cnt, s);
+        AOS_HIP(hipEventRecord(ev[10], s));
+        launch_ror_raster(L, d_bs, d_sorted, d_rb, d_cnt, s);
+        AOS_HIP(hipEventRecord(ev[11], s));
+        AOS_HIP(hipMemcpyAsync(h_stats.ensure(64), d_bs + nb, sizeof(int), hipMemcpyDeviceToHost, s));
     }
     AOS_HIP(hipEventRecord(ev[1], s));
 
@@ -246,6 +251,8 @@ void aos_ctx::run_seedgen(bool want_host, aos_seedgen_out &out) {
     auto ms = [&](int a, int b) { float t = 0; (void)hipEventElapsedTime(&t, ev[a], ev[b]); return t; };
     out.ms_ror = ms(0, 1); out.ms_grid = ms(1, 2); out.ms_thin = ms(2, 3); out.ms_cluster = ms(3, 4);
     out.ms_seeds = ms(4, 5); out.ms_total = ms(0, 5);
+    out.n_binned = static_cast<const int *>(h_stats.p)[0];
+    out.ms_ror_count = out.n_binned ? ms(10, 11) : 0.0f;
 }
 
 int aos_ctx::debug_grid(const char *which, int8_t *dst, uint64_t capacity) {

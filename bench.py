@@ -9,7 +9,7 @@ Workload: config C2 (10 M points, 4096^2 cells @ 0.1 m, BASELINE.json configs[2]
 
 Multi-GPU (--gpus N, launched by torch.distributed.run): weak scaling — every rank processes its
 own independent 4096^2 map tile (scene seed 3 + rank); no data-path collective; the barrier and
-the max-over-ranks time use torch.distributed.
+the max-over-ranks time use torch.distributed (RCCL).
 """
 from __future__ import annotations
 
@@ -23,16 +23,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 for sub in ("tools", "active-orchard-slam_amd"):
     sys.path.insert(0, os.path.join(ROOT, sub))
 
-import torch  # noqa: E402  (import before libaos_gpu: shared HIP runtime, see aos_gpu.lib)
-import torch.distributed as dist  # noqa: E402
-
-import aos_gpu  # noqa: E402
-import orchard  # noqa: E402
-
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+DOMINANT = "k_ror_tile"
+PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -40,11 +36,42 @@ def parse():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-config", default="C1")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def timed_region(step, steps: int, warmup: int, world: int, sync, dist=None, device=None):
+    """The contract's timed region: W untimed steps, barrier + sync, EXACTLY K timed steps, sync +
+    barrier, then the max over ranks. Returns (seconds, per-step results of the last step)."""
+    last = None
+    for _ in range(warmup):
+        last = step()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    results = []
+    for _ in range(steps):
+        results.append(step())
+    sync()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        import torch
+        t = torch.tensor([dt], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt, results or [last]
+
+
+def throughput(units_per_step: float, world: int, steps: int, dt: float) -> float:
+    """Whole-job rate: units processed by all ranks / max-over-ranks wall time."""
+    return units_per_step * world * steps / dt
 
 
 def cpu_baseline(cfg_name: str) -> dict:
     """The oracle (single-threaded CPU restatement of the reference path) on a bounded sample."""
+    import orchard
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py as O
     cfg = orchard.CONFIGS[cfg_name]
@@ -57,7 +84,7 @@ def cpu_baseline(cfg_name: str) -> dict:
     O.gvd(r["voronoi_seeds"], r["rows_info"], r, p)
     t2 = time.perf_counter()
     cells = r["width"] * r["height"]
-    return {"value": cells / (t2 - t0) / 1e6, "unit": "Mcells/s", "cores": 1, "kind": "port",
+    return {"value": round(cells / (t2 - t0) / 1e6, 4), "unit": "Mcells/s", "cores": 1, "kind": "port",
             "sample": f"oracle/ CPU restatement, 1 thread, one full frame of config {cfg_name} "
                       f"({cfg.n_points} pts, {r['width']}x{r['height']} cells): seed-gen {t1 - t0:.2f} s + "
                       f"GVD {t2 - t1:.2f} s (incl. the reference's never-read vertex dedup); the CPU GVD is "
@@ -75,19 +102,37 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc passes (FETCH_SIZE x2 on
+    gfx950 for 16 B/lane streaming reads + WRITE_SIZE, MI355X_MICROARCH.md 'HBM'), or None."""
+    try:
+        with open(PMC_FILE) as f:
+            d = json.load(f)
+        k = d["kernels"][kernel]
+        return k["bytes_per_launch"], d.get("source", PMC_FILE)
+    except (OSError, KeyError, ValueError):
+        return None, None
+
+
 def main():
     a = parse()
+    import torch  # (import before libaos_gpu: shared HIP runtime, see aos_gpu.lib)
+    import torch.distributed as dist
+
+    import aos_gpu
+    import orchard
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("nccl", device_id=dev)
 
     cfg = orchard.CONFIGS[a.config]
     cloud = orchard.generate(cfg, seed=cfg.seed + rank)
     poly = orchard.polygon(cfg)
-    d_cloud = torch.from_numpy(cloud).to(f"cuda:{local}")
+    d_cloud = torch.from_numpy(cloud).to(dev)
     n = cloud.shape[0]
     ctx = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res), device=local)
     ctx.set_polygon(poly)
@@ -97,47 +142,43 @@ def main():
         gg = ctx.gvd_from_seedgen()
         return g, gg
 
-    for _ in range(a.warmup):
-        step()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    dt, res = timed_region(step, a.steps, a.warmup, world, torch.cuda.synchronize, dist, dev)
+    g, gg = res[-1]
     stage = {}
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        g, gg = step()
-        for k, v in g["ms"].items():
+    for gs, ggs in res:
+        for k, v in gs["ms"].items():
             stage["seedgen_" + k] = stage.get("seedgen_" + k, 0.0) + v
-        for k, v in gg["ms"].items():
+        for k, v in ggs["ms"].items():
             stage["gvd_" + k] = stage.get("gvd_" + k, 0.0) + v
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
     cells = g["width"] * g["height"]
-    value = cells * world * a.steps / dt / 1e6
-    avg = {k: v / a.steps for k, v in stage.items()}
+    value = throughput(cells / 1e6, world, len(res), dt)
+    avg = {k: v / len(res) for k, v in stage.items()}
 
-    # roofline of the dominant kernel group, timed live with HIP events on the handle's stream
-    # (aos_seedgen_out.ms_*): Zhang-Suen thinning, algorithmic bytes (SURVEY §8d, 1 B/cell):
-    # 2 sub-iterations x (read + write) per iteration = 4 * C * T bytes per frame.
+    # roofline of the dominant GPU kernel (largest share of device time per frame in the committed
+    # rocprofv3 summary): k_ror_tile, the ROR neighbour count + raster over LDS-staged bins.
+    # Algorithmic bytes per launch: each staged point record read once (float4, 16 B)
+    # + one raster byte per kept candidate. Timed live: HIP events around that single launch on the
+    # handle's stream (aos_seedgen_out.ms_ror_count), averaged over the timed steps.
+    alg = 16.0 * g["n_binned"] + float(g["n_clipped"])
+    ms_k = avg["seedgen_ror_count"]
+    achieved = alg / (ms_k * 1e-3) / 1e9 if ms_k > 0 else 0.0
+    traffic, src = pmc_traffic(DOMINANT)
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "kernel": DOMINANT, "alg_bytes_per_launch": alg, "ms_per_launch": round(ms_k, 4),
+            "units_per_launch": g["n_binned"], "traffic_source": src}
+    # BASELINE.md frame-level figure: B_alg = 12 N + C (6 + 4 T) over the whole frame wall-clock
     T = g["thin_iters"]
-    alg_bytes = 4.0 * cells * T
-    thin_ms = avg["seedgen_thin"]
-    achieved = alg_bytes / (thin_ms * 1e-3) / 1e9
-    roof = {"bound": "hbm", "kernel": "k_open + k_thin_block (Zhang-Suen, T iterations)", "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-            "alg_bytes_per_frame": alg_bytes, "ms_per_frame": round(thin_ms, 4), "T": T}
+    b_frame = 12.0 * n + cells * (6.0 + 4.0 * T)
+    frame_roof = {"alg_bytes": b_frame, "achieved_GBs": round(b_frame / (dt / len(res)) / 1e9, 2),
+                  "frac": round(b_frame / (dt / len(res)) / 1e9 / HBM_PEAK_GBS, 5),
+                  "note": "whole frame incl. the host Subdiv2D replay (DESIGN.md)"}
 
     if rank == 0:
         out = {
             "metric": "Mcells/s skeleton+GVD (seed-gen + GVD frame) on 4096^2 grid",
             "value": round(value, 3), "unit": "Mcells/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-            "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "ms_per_step": round(dt / len(res) * 1e3, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32/f64 (reference float/double arithmetic), u8/bit grids",
             "data": "synthetic orchard (tools/orchard_gen.c, SplitMix64), device-resident PointCloud2",
             "config": {"workload": f"{a.config}: {n} pts, {g['width']}x{g['height']} cells @ {cfg.res} m, "
@@ -145,8 +186,10 @@ def main():
                        "global_batch": world, "parallelism": f"tiles{world}"},
             "stages_ms": {k: round(v, 3) for k, v in avg.items()},
             "frame": {"T": T, "rows": len(g["row_length"]), "seeds": len(g["voronoi_seeds"]),
-                      "nodes": len(gg["nodes"]), "edges": len(gg["edges"])},
+                      "nodes": len(gg["nodes"]), "edges": len(gg["edges"]), "n_binned": g["n_binned"],
+                      "n_clipped": g["n_clipped"]},
             "roofline": roof,
+            "frame_roofline": frame_roof,
         }
         if world == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(a.cpu_config)

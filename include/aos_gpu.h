@@ -103,6 +103,10 @@ typedef struct aos_seedgen_out {
     const double *cluster_info_xy;
     /* per-stage device time (ms), HIP events */
     float ms_ror, ms_grid, ms_thin, ms_cluster, ms_seeds, ms_total;
+    /* ROR neighbour-count kernel (k_ror_tile): points it staged (binned near the clip box) and
+     * its own device time, HIP events on the handle's stream around that single launch */
+    uint64_t n_binned;
+    float ms_ror_count;
 } aos_seedgen_out;
 
 /* GVD inputs when not fed from this handle's seed-gen frame. */

@@ -1,0 +1,67 @@
+"""bench.py's multi-rank path on CPU (gloo, world_size 2): barrier-bracketed timed region, max over
+ranks, whole-job throughput, and one independent tile (scene seed + rank) per rank."""
+import os
+import socket
+import sys
+import time
+
+import numpy as np
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+import orchard  # noqa: E402
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    calls = []
+
+    def step():
+        calls.append(1)
+        time.sleep(0.02 * (rank + 1))   # rank 1 is the slow one
+        return rank
+
+    dt, res = bench.timed_region(step, steps=3, warmup=2, world=world, sync=lambda: None, dist=dist, device="cpu")
+    q.put((rank, dt, len(calls), len(res)))
+    dist.destroy_process_group()
+
+
+def test_timed_region_max_over_ranks_gloo():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = [q.get(timeout=120) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    dts = {r: dt for r, dt, _, _ in out}
+    # both ranks report the same (max) time, at least the slow rank's 3 x 40 ms
+    assert abs(dts[0] - dts[1]) < 1e-12
+    assert dts[0] >= 3 * 0.04
+    for _, _, ncalls, nres in out:
+        assert ncalls == 5 and nres == 3     # W untimed + exactly K timed steps
+
+
+def test_throughput_is_whole_job():
+    # 16.78 Mcells per step per rank, 2 ranks, 4 steps in 0.5 s
+    assert abs(bench.throughput(16.777216, 2, 4, 0.5) - 268.435456) < 1e-9
+
+
+def test_independent_tile_per_rank():
+    cfg = orchard.CONFIGS["C0"]
+    a = orchard.generate(cfg, seed=cfg.seed + 0, n_points=5000)
+    b = orchard.generate(cfg, seed=cfg.seed + 1, n_points=5000)
+    assert a.shape == b.shape and not np.array_equal(a, b)
