@@ -170,3 +170,63 @@ def test_c2_seedgen_parity_with_large_sums():
     assert g["n_bfs_replayed"] >= 1
     assert_seedgen_parity(g, o)
     c.close()
+
+
+# ---------------------------------------------------------------- against the committed fixtures
+def _golden(name):
+    import os
+    return np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", name), allow_pickle=False)
+
+
+def test_c0_against_golden_fixtures():
+    """GPU C0 frame vs tests/golden (oracle outputs frozen by tools/make_golden.py), no oracle call."""
+    import json
+    gs, gg = _golden("c0_seedgen.npz"), _golden("c0_gvd.npz")
+    meta = json.loads(str(gs["meta"]))
+    h, w = meta["height"], meta["width"]
+
+    def grid(k):
+        return np.where(np.unpackbits(gs[f"grid_{k}"])[: h * w].reshape(h, w) != 0, 100, 0).astype(np.int8)
+
+    o = {k: gs[k] for k in gs.files if not k.startswith("grid_") and k not in ("meta", "origin", "resolution")}
+    o.update(meta, origin=tuple(gs["origin"]), resolution=float(gs["resolution"]),
+             occupancy=grid("occupancy"), skeleton_framed=grid("skeleton_framed"))
+    og = {k: gg[k] for k in gg.files}
+    og["published"] = bool(gg["published"])
+    cfg = orchard.CONFIGS["C0"]
+    c = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res))
+    c.set_polygon(orchard.polygon(cfg))
+    g = c.seedgen(orchard.generate(cfg))
+    assert g["n_clipped"] == meta["n_clipped"]
+    assert_seedgen_parity(g, o)
+    assert grid_diff(c.debug_grid("raster", (h, w)) == 100, grid("raster") == 100) == 0
+    assert grid_diff(c.debug_grid("skeleton_frameless", (h, w)), grid("skeleton")) == 0
+    assert_gvd_parity(c.gvd_from_seedgen(), og)
+    c.close()
+
+
+def test_c1_against_golden_hashes():
+    import hashlib
+    import json
+    hs = json.load(open(__import__("os").path.join(__import__("os").path.dirname(__file__), "golden", "c1_sha256.json")))
+
+    def sha(a, dt):
+        a = np.ascontiguousarray(np.asarray(a, dtype=dt))
+        return hashlib.sha256(a.dtype.str.encode() + str(a.shape).encode() + a.tobytes()).hexdigest()
+
+    cfg = orchard.CONFIGS["C1"]
+    c = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res))
+    c.set_polygon(orchard.polygon(cfg))
+    g = c.seedgen(orchard.generate(cfg))
+    gg = c.gvd_from_seedgen()
+    assert g["thin_iters"] == hs["meta"]["thin_iters"] and g["n_clipped"] == hs["meta"]["n_clipped"]
+    for k in ("occupancy", "skeleton_framed"):
+        assert sha(g[k], np.int8) == hs["seedgen"][k], k
+    for k in ("row_center", "row_start", "row_end", "row_length", "virtual_seeds", "ray_seeds", "endpoint_seeds",
+              "voronoi_seeds", "rows_info", "cluster_info"):
+        assert sha(g[k], np.float64) == hs["seedgen"][k], k
+    for k, dt in (("nodes", np.float64), ("edges", np.int32), ("edge_lengths", np.float32),
+                  ("edge_clearances", np.float32), ("node_labels", np.int32), ("node_cluster_indices", np.int32),
+                  ("node_label_counts", np.int32), ("node_label_clusters", np.int32), ("node_label_types", np.int32)):
+        assert sha(gg[k], dt) == hs["gvd"][k], k
+    c.close()
