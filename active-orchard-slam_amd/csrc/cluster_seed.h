@@ -3,6 +3,7 @@
 #include <vector>
 
 #include "aos_internal.h"
+#include "subdiv2d.h"
 
 namespace aos {
 
@@ -72,6 +73,7 @@ struct GvdState {
     DevBuf seeds, merge_state, hash_count, hash_start, hash_slot, hash_sorted, scan_tmp, misc;
     DevBuf edges, bpts, near_idx, cand, cand_ok, skel, grid_bytes_ext;
     PinnedBuf h_misc;
+    Subdiv2D subdiv;   // host insert replay; kept across frames to reuse its allocations
     // host outputs
     std::vector<double> nodes_xy;
     std::vector<int32_t> labels, cluster_idx, label_counts, label_clusters, label_types, edges_out;

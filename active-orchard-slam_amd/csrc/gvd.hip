@@ -1,7 +1,8 @@
 // GVD construction (AosGvdNode::processGraph, src/aos_gvd_node.cpp:255-318) on gfx950.
 //
 //  g1 seed merge (gvd:84-128)                 GPU  greedy LFMIS (<= 0.5 m) + ordered member sums
-//  g4 Subdiv2D insert + facets                host sequential replay (subdiv2d.h explains why)
+//  g4 Subdiv2D inserts                       host sequential replay (subdiv2d.h explains why)
+//     calcVoronoi + facet list               GPU  k_vor_faces / k_facet_count / k_facet_emit
 //  g5 extractBoundaryPoints                   GPU  greedy LFMIS (1 cm key or < 5 cm)
 //  g6 buildGraphFromBoundaryPoints            GPU  hashed nearest snap + pair search + occupancy
 //                                                  sampling + first-passing-occurrence selection
@@ -12,6 +13,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cfloat>
 #include <climits>
 #include <cmath>
 #include <cstring>
@@ -382,11 +384,101 @@ __global__ void k_node_labels(const double2 *nodes, int Mn, const double2 *lp, c
     if (!off) { mask[i] = m; cidx[i] = ci; count[i] = cnt; }
 }
 
+// ------------------------------------------------------------------ g4 facets (calcVoronoi + getVoronoiFacetList)
+// The Subdiv2D inserts are replayed on the host; the facets they imply are built here from the raw
+// quad-edge arrays (8 ints per quad-edge: next[4], pt[4]). calcVoronoi (subdivision2d.cpp) walks
+// quad-edges q = 4.. in id order, left face of q*4 before its right face, and the first of those
+// that touches a triangle computes its circumcentre (computeVoronoiPoint from that edge and its
+// NEXT_AROUND_LEFT / NEXT_AROUND_RIGHT successor). A failed computation (det = 0 or huge) leaves the
+// face unset for the next edge of the triangle. So a face's value is: over its 3 boundary edges in
+// that key order (key = 2*q + right), the first successful computation; (0, 0) = vtx[0] if none.
+__device__ __forceinline__ int q_get(const int *qe, int e, int t) {
+    const int x = qe[(e >> 2) * 8 + ((e + t) & 3)];
+    return (x & ~3) + ((x + (t >> 4)) & 3);
+}
+__device__ __forceinline__ int q_org(const int *qe, int e) { return qe[(e >> 2) * 8 + 4 + (e & 3)]; }
+__device__ __forceinline__ int q_dst(const int *qe, int e) { return qe[(e >> 2) * 8 + 4 + ((e + 2) & 3)]; }
+
+__device__ bool d_voronoi_point(float2 o0, float2 d0, float2 o1, float2 d1, float2 &r) {
+    double a0 = d0.x - o0.x, b0 = d0.y - o0.y;
+    double c0 = -0.5 * (a0 * (d0.x + o0.x) + b0 * (d0.y + o0.y));
+    double a1 = d1.x - o1.x, b1 = d1.y - o1.y;
+    double c1 = -0.5 * (a1 * (d1.x + o1.x) + b1 * (d1.y + o1.y));
+    double det = a0 * b1 - a1 * b0;
+    if (det == 0) return false;
+    det = 1. / det;
+    r.x = (float)((b0 * c1 - b1 * c0) * det);
+    r.y = (float)((a1 * c0 - a0 * c1) * det);
+    return fabsf(r.x) < FLT_MAX * 0.5f && fabsf(r.y) < FLT_MAX * 0.5f;
+}
+
+// face[2*q + side]: side 0 = left face of q*4 (pt[3]), side 1 = right face (pt[1])
+__global__ void k_vor_faces(const int *qe, int n_rec, const float2 *vp, float2 *face) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 2 * n_rec) return;
+    const int q = i >> 1, side = i & 1;
+    float2 res = make_float2(0.f, 0.f);
+    if (q >= 1 && qe[q * 8] > 0) {   // allocated quad-edge
+        const int d1 = q * 4 + 2 * side, d2 = q_get(qe, d1, 0x13), d3 = q_get(qe, d2, 0x13);
+        int k[3];
+        const int ds[3] = {d1, d2, d3};
+#pragma unroll
+        for (int j = 0; j < 3; ++j) k[j] = (ds[j] >> 2) < 4 ? INT_MAX : 2 * (ds[j] >> 2) + ((ds[j] & 2) ? 1 : 0);
+        if (k[0] > k[1]) { int t = k[0]; k[0] = k[1]; k[1] = t; }
+        if (k[1] > k[2]) { int t = k[1]; k[1] = k[2]; k[2] = t; }
+        if (k[0] > k[1]) { int t = k[0]; k[0] = k[1]; k[1] = t; }
+        for (int j = 0; j < 3 && k[j] != INT_MAX; ++j) {
+            const int e0 = (k[j] >> 1) * 4, e1 = (k[j] & 1) ? q_get(qe, e0, 0x31) : q_get(qe, e0, 0x13);
+            float2 r;
+            if (d_voronoi_point(vp[q_org(qe, e0)], vp[q_dst(qe, e0)], vp[q_org(qe, e1)], vp[q_dst(qe, e1)], r)) { res = r; break; }
+        }
+    }
+    face[i] = res;
+}
+
+// getVoronoiFacetList({}) + VoronoiDiagram edges (voronoi_diagram.cpp:97-114): for each real vertex
+// k >= 4 in id order, walk t = rotate(firstEdge, 1) by NEXT_AROUND_LEFT; a facet of n >= 2 points
+// gives the edges (p_i, p_(i+1 mod n)).
+constexpr int kMaxFacet = 1 << 16;
+__device__ __forceinline__ float2 dual_face(const float2 *face, int t) { return face[2 * (t >> 2) + ((t & 3) == 1 ? 1 : 0)]; }
+
+__global__ void k_facet_count(const int *qe, const int *vfirst, const int *vtype, int nv, int *cnt, int *err) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nv) return;
+    int c = 0;
+    if (k >= 4 && vtype[k] == 0) {
+        const int f = vfirst[k], start = (f & ~3) + ((f + 1) & 3);
+        int t = start;
+        do { ++c; t = q_get(qe, t, 0x13); } while (t != start && c < kMaxFacet);
+        if (c >= kMaxFacet) atomicOr(err, 1);
+        if (c < 2) c = 0;
+    }
+    cnt[k] = c;
+}
+__global__ void k_facet_emit(const int *qe, const int *vfirst, const int *off, const int *cnt, int nv, const float2 *face,
+                             float4 *edges) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nv || cnt[k] == 0) return;
+    const int f = vfirst[k], start = (f & ~3) + ((f + 1) & 3), n = cnt[k];
+    float4 *o = edges + off[k];
+    const float2 first = dual_face(face, start);
+    float2 prev = first;
+    int t = q_get(qe, start, 0x13);
+    for (int i = 1; i < n; ++i) {
+        const float2 cur = dual_face(face, t);
+        o[i - 1] = make_float4(prev.x, prev.y, cur.x, cur.y);
+        prev = cur;
+        t = q_get(qe, t, 0x13);
+    }
+    o[n - 1] = make_float4(prev.x, prev.y, first.x, first.y);
+}
+
 // ------------------------------------------------------------------ orchestration
 struct GvdScratch {
     DevBuf raw, ok, leaders, merged, owner, oidx, sowner, sidx, tmp, edges_f, occ, occ_ok, bp, kept_occ, keys, idx, skeys,
         sidx2, near_idx, pk, pidx, pskeys, psidx, pcount, poff, plist, ft, ckey, cvalid, pass, k2, occ_idx, sk2, socc, selected,
-        inside, ipos, nodes, keep, kpos, edges, lens, jobs, lpts, lval, lmask, lcidx, lcount, loff, lcl, lty, scan_tmp;
+        inside, ipos, nodes, keep, kpos, edges, lens, jobs, lpts, lval, lmask, lcidx, lcount, loff, lcl, lty, scan_tmp,
+        sd_qe, sd_vp, sd_vfirst, sd_vtype, sd_face, sd_cnt, sd_off;
 };
 static GvdScratch &scratch(GvdState &G) {
     // one scratch per state (per handle); stored behind the misc buffer slot
@@ -401,7 +493,8 @@ void free_gvd_scratch(GvdState &G) {
                          &S->near_idx, &S->pk, &S->pidx, &S->pskeys, &S->psidx, &S->pcount, &S->poff, &S->plist, &S->ft,
                          &S->ckey, &S->cvalid, &S->pass, &S->k2, &S->occ_idx, &S->sk2, &S->socc, &S->selected, &S->inside,
                          &S->ipos, &S->nodes, &S->keep, &S->kpos, &S->edges, &S->lens, &S->jobs, &S->lpts, &S->lval,
-                         &S->lmask, &S->lcidx, &S->lcount, &S->loff, &S->lcl, &S->lty, &S->scan_tmp};
+                         &S->lmask, &S->lcidx, &S->lcount, &S->loff, &S->lcl, &S->lty, &S->scan_tmp,
+                         &S->sd_qe, &S->sd_vp, &S->sd_vfirst, &S->sd_vtype, &S->sd_face, &S->sd_cnt, &S->sd_off};
         for (DevBuf *b : all) b->release();
         delete S;
         G.misc.p = nullptr;
@@ -470,9 +563,10 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     G.n_merged = nl;
     AOS_HIP(hipEventRecord(ev[7], s));
 
-    // ---- g3/g4 finite filter, bounds, Subdiv2D (host) -> Voronoi edges
+    // ---- g3/g4 finite filter, bounds, Subdiv2D inserts (host replay) -> facets / Voronoi edges (GPU)
     auto t0 = std::chrono::steady_clock::now();
-    std::vector<float> vedges;
+    int ne = 0;
+    float *d_ef = nullptr;
     {
         double min_x = g.minx, max_x = g.maxx, min_y = g.miny, max_y = g.maxy;
         if (!std::isfinite(min_x) || !std::isfinite(max_x) || !std::isfinite(min_y) || !std::isfinite(max_y)) return false;
@@ -487,7 +581,8 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
         float rx = static_cast<float>(min_x - 1.0), ry = static_cast<float>(min_y - 1.0);
         float rw = static_cast<float>(std::abs(max_x - min_x) + 2.0), rh = static_cast<float>(std::abs(max_y - min_y) + 2.0);
         if (!(rw <= 0 || rh <= 0)) {
-            Subdiv2D sd;
+            Subdiv2D &sd = G.subdiv;
+            sd.reserve(nl);
             sd.init_delaunay(rx, ry, rw, rh, P.subdiv_rect_mode);
             const float margin = 0.1f;
             for (int i = 0; i < nl; ++i) {
@@ -498,19 +593,37 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
                 y = std::max(ry + margin, std::min(ry + rh - margin, y));
                 sd.insert(x, y);
             }
-            sd.voronoi_edges(vedges);
+            const Subdiv2D::Raw R = sd.raw();
+            int *d_qe = dev<int>(S.sd_qe, 8 * (size_t)R.n_rec);
+            float2 *d_vp = dev<float2>(S.sd_vp, R.n_vtx);
+            int *d_vf = dev<int>(S.sd_vfirst, R.n_vtx), *d_vt = dev<int>(S.sd_vtype, R.n_vtx);
+            AOS_HIP(hipMemcpyAsync(d_qe, R.qe, sizeof(int) * 8 * (size_t)R.n_rec, hipMemcpyHostToDevice, s));
+            AOS_HIP(hipMemcpyAsync(d_vp, R.vp, sizeof(float2) * R.n_vtx, hipMemcpyHostToDevice, s));
+            AOS_HIP(hipMemcpyAsync(d_vf, R.vfirst, sizeof(int) * R.n_vtx, hipMemcpyHostToDevice, s));
+            AOS_HIP(hipMemcpyAsync(d_vt, R.vtype, sizeof(int) * R.n_vtx, hipMemcpyHostToDevice, s));
+            float2 *d_face = dev<float2>(S.sd_face, 2 * (size_t)R.n_rec);
+            int *d_cnt = dev<int>(S.sd_cnt, R.n_vtx + 2), *d_off = dev<int>(S.sd_off, R.n_vtx + 1);
+            AOS_HIP(hipMemsetAsync(d_cnt + R.n_vtx, 0, 2 * sizeof(int), s));
+            k_vor_faces<<<cdiv(2 * R.n_rec, 256), 256, 0, s>>>(d_qe, R.n_rec, d_vp, d_face);
+            k_facet_count<<<cdiv(R.n_vtx, 256), 256, 0, s>>>(d_qe, d_vf, d_vt, R.n_vtx, d_cnt, d_cnt + R.n_vtx + 1);
+            scan_excl(S.scan_tmp, d_cnt, d_off, R.n_vtx + 1, s);
+            AOS_HIP(hipMemcpyAsync(h_sc, d_off + R.n_vtx, sizeof(int), hipMemcpyDeviceToHost, s));
+            AOS_HIP(hipMemcpyAsync(h_sc + 1, d_cnt + R.n_vtx + 1, sizeof(int), hipMemcpyDeviceToHost, s));
+            AOS_HIP(hipStreamSynchronize(s));
+            if (h_sc[1]) throw std::runtime_error("Subdiv2D facet walk did not close");
+            ne = h_sc[0];
+            d_ef = dev<float>(S.edges_f, 4 * (size_t)std::max(ne, 1));
+            if (ne) k_facet_emit<<<cdiv(R.n_vtx, 256), 256, 0, s>>>(d_qe, d_vf, d_off, d_cnt, R.n_vtx, d_face,
+                                                                    reinterpret_cast<float4 *>(d_ef));
         }
     }
     auto t1 = std::chrono::steady_clock::now();
     G.ms_delaunay = std::chrono::duration<float, std::milli>(t1 - t0).count();
-    const int ne = (int)(vedges.size() / 4);
     G.n_vor_edges = ne;
     AOS_HIP(hipEventRecord(ev[8], s));
     if (ne == 0) return true;  // no boundary points: an empty graph is still published
 
     // ---- g5 boundary points
-    float *d_ef = dev<float>(S.edges_f, 4 * (size_t)ne);
-    AOS_HIP(hipMemcpyAsync(d_ef, vedges.data(), sizeof(float) * 4 * ne, hipMemcpyHostToDevice, s));
     const int no = 2 * ne;
     double2 *d_occ = dev<double2>(S.occ, no);
     int *d_occ_ok = dev<int>(S.occ_ok, no);

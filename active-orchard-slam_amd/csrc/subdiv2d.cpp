@@ -12,15 +12,6 @@ namespace {
 inline double tri_area(float ax, float ay, float bx, float by, float cx, float cy) {
     return ((double)bx - ax) * ((double)cy - ay) - ((double)by - ay) * ((double)cx - ax);
 }
-// isPtInCircle3, eps = FLT_EPSILON / 8
-inline int in_circle(float px, float py, float ax, float ay, float bx, float by, float cx, float cy) {
-    const double eps = FLT_EPSILON * 0.125;
-    double val = ((double)ax * ax + (double)ay * ay) * tri_area(bx, by, cx, cy, px, py);
-    val -= ((double)bx * bx + (double)by * by) * tri_area(ax, ay, cx, cy, px, py);
-    val += ((double)cx * cx + (double)cy * cy) * tri_area(ax, ay, bx, by, px, py);
-    val -= ((double)px * px + (double)py * py) * tri_area(ax, ay, bx, by, cx, cy);
-    return val > eps ? 1 : val < -eps ? -1 : 0;
-}
 // computeVoronoiPoint; returns false for det == 0 (FLT_MAX marker)
 inline bool voronoi_point(float o0x, float o0y, float d0x, float d0y, float o1x, float o1y, float d1x, float d1y,
                           float &rx, float &ry) {
@@ -40,7 +31,7 @@ inline bool voronoi_point(float o0x, float o0y, float d0x, float d0y, float o1x,
 }  // namespace
 
 void Subdiv2D::reserve(size_t n) {
-    vp.reserve(2 * n + 8); vfirst.reserve(2 * n + 8); vtype.reserve(2 * n + 8);
+    vp.reserve(2 * n + 8); vd.reserve(2 * n + 8); vfirst.reserve(2 * n + 8); vtype.reserve(2 * n + 8);
     qe.reserve(3 * n + 8);
 }
 
@@ -72,6 +63,8 @@ int Subdiv2D::new_point(float x, float y, int type) {
     int v = free_p;
     free_p = vfirst[v];
     vp[v] = V2f{x, y}; vfirst[v] = 0; vtype[v] = type;
+    if (vd.size() < vp.size()) vd.resize(vp.size());
+    vd[v] = V2d{(double)x, (double)y, (double)x * x + (double)y * y, 0.0};
     return v;
 }
 
@@ -124,7 +117,7 @@ void Subdiv2D::init_delaunay(float rx, float ry, float rw, float rh, int rect_mo
         rw = (float)(int)std::lrint(rw); rh = (float)(int)std::lrint(rh);
     }
     const float big = 3.f * std::max(rw, rh);
-    vp.clear(); vfirst.clear(); vtype.clear(); qe.clear();
+    vp.clear(); vd.clear(); vfirst.clear(); vtype.clear(); qe.clear();
     recent = 0;
     tlx = rx; tly = ry; brx = rx + rw; bry = ry + rh;
     vp.push_back(V2f{0.f, 0.f}); vfirst.push_back(0); vtype.push_back(-1);   // vtx[0]
@@ -203,14 +196,25 @@ bool Subdiv2D::insert(float x, float y) {
     } while (dst(curr_edge) != first_point);
     curr_edge = get_e(base, PREV_AROUND_ORG);
     const int max_edges = (int)qe.size() * 4;
-    const V2f np_ = vp[curr_point];
+    // Swap loop with the predicates written out on exact double copies of the float coordinates
+    // (the float -> double conversions are exact, so every product and sum rounds as in
+    // triangleArea / isPtInCircle3, and |p|^2 is formed once per vertex in the same order).
+    const V2d P = vd[curr_point];
+    auto area = [](const V2d &a, const V2d &b, const V2d &c) { return (b.x - a.x) * (c.y - a.y) - (b.y - a.y) * (c.x - a.x); };
     for (int i = 0; i < max_edges; i++) {
         int temp = get_e(curr_edge, PREV_AROUND_ORG);
         int tdst = dst(temp), corg = org(curr_edge), cdst = dst(curr_edge);
-        const V2f T = vp[tdst], O = vp[corg], D = vp[cdst];
-        if (tri_area(T.x, T.y, D.x, D.y, O.x, O.y) > 0 &&   // isRightOf(temp_dst, curr_edge) > 0
-            // isPtInCircle3(pt = org, a = temp_dst, b = dst, c = new point)
-            in_circle(O.x, O.y, T.x, T.y, D.x, D.y, np_.x, np_.y) < 0) {
+        const V2d T = vd[tdst], O = vd[corg], D = vd[cdst];
+        bool flip = false;
+        if (area(T, D, O) > 0) {   // isRightOf(temp_dst, curr_edge) > 0
+            // isPtInCircle3(pt = org, a = temp_dst, b = dst, c = new point) < 0, eps = FLT_EPSILON / 8
+            double val = T.n2 * area(D, P, O);
+            val -= D.n2 * area(T, P, O);
+            val += P.n2 * area(T, D, O);
+            val -= O.n2 * area(T, D, P);
+            flip = val < -(FLT_EPSILON * 0.125);
+        }
+        if (flip) {
             swap_edge(curr_edge);
             curr_edge = get_e(curr_edge, PREV_AROUND_ORG);
         } else if (corg == first_point) {

@@ -29,13 +29,22 @@ class Subdiv2D {
     // (voronoi_diagram.cpp:97-114), as float x0, y0, x1, y1.
     void voronoi_edges(std::vector<float> &edges);
     size_t num_vertices() const { return vp.size(); }
+    // Raw quad-edge state after the inserts, for the GPU facet builder (gvd.hip k_vor_faces /
+    // k_facet_*): qe = 8 ints per quad-edge {next[4], pt[4]}, vp = float2 per vertex.
+    struct Raw { const int *qe; int n_rec; const float *vp; const int *vfirst, *vtype; int n_vtx; };
+    Raw raw() const {
+        return Raw{reinterpret_cast<const int *>(qe.data()), (int)qe.size(), reinterpret_cast<const float *>(vp.data()),
+                   vfirst.data(), vtype.data(), (int)vp.size()};
+    }
     void reserve(size_t n_points);
 
   private:
     enum { NEXT_AROUND_LEFT = 0x13, NEXT_AROUND_RIGHT = 0x31, PREV_AROUND_ORG = 0x11, PREV_AROUND_DST = 0x33 };
     struct alignas(32) QE { int next[4]; int pt[4]; };
     struct V2f { float x, y; };
+    struct V2d { double x, y, n2, pad; };
     std::vector<V2f> vp;
+    std::vector<V2d> vd;   // exact double copies of vp plus x*x + y*y, for the flip-loop predicates
     std::vector<int> vfirst, vtype;   // type: -1 free, 0 real, 1 virtual
     std::vector<QE> qe;
     int free_q = 0, free_p = 0, recent = 0;

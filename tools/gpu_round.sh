@@ -20,10 +20,12 @@ echo "[gpu_round] rocprofv3 kernel trace"
 rm -rf gpurun_out/prof_kt gpurun_out/prof_fetch gpurun_out/prof_write
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_kt -o ${TAG}_kt -- python3 $R/bench.py --no-cpu-baseline --steps 5 --warmup 2 > $R/gpurun_out/prof_kt.log 2>&1
+if [ "${PMC:-1}" = "1" ]; then
 echo "[gpu_round] pmc FETCH_SIZE"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/prof_fetch -o ${TAG}_fetch -- python3 $R/bench.py --no-cpu-baseline --steps 3 --warmup 1 > $R/gpurun_out/prof_fetch.log 2>&1
 echo "[gpu_round] pmc WRITE_SIZE"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/prof_write -o ${TAG}_write -- python3 $R/bench.py --no-cpu-baseline --steps 3 --warmup 1 > $R/gpurun_out/prof_write.log 2>&1
+fi
 cd $R
-find gpurun_out/prof_kt gpurun_out/prof_fetch gpurun_out/prof_write -name "*.csv" | sort
+find gpurun_out -name "*.csv" -path "*prof_*" | sort
 echo "[gpu_round] done"
