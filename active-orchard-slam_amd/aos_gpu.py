@@ -15,7 +15,8 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-LIB_PATH = os.path.join(HERE, "libaos_gpu.so")
+# AOS_GPU_LIB: alternative build of the same library (A/B experiments, tools/)
+LIB_PATH = os.environ.get("AOS_GPU_LIB") or os.path.join(HERE, "libaos_gpu.so")
 HEADER = os.path.join(ROOT, "include", "aos_gpu.h")
 
 c_f, c_d, c_i, c_u, c_u64, c_vp = (ctypes.c_float, ctypes.c_double, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64,

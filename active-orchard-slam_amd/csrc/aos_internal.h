@@ -21,9 +21,14 @@ struct HipError { hipError_t e; const char *what; int line; };
     } while (0)
 
 // ------------------------------------------------------------------ device buffers
+// Owning, growable device allocation (freed on destruction; not copyable).
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    ~DevBuf() { release(); }
     void *ensure(size_t bytes) {
         if (bytes <= cap) return p;
         if (p) AOS_HIP(hipFree(p));
@@ -40,6 +45,10 @@ struct DevBuf {
 struct PinnedBuf {
     void *p = nullptr;
     size_t cap = 0;
+    PinnedBuf() = default;
+    PinnedBuf(const PinnedBuf &) = delete;
+    PinnedBuf &operator=(const PinnedBuf &) = delete;
+    ~PinnedBuf() { release(); }
     void *ensure(size_t bytes) {
         if (bytes <= cap) return p;
         if (p) AOS_HIP(hipHostFree(p));
@@ -65,6 +74,7 @@ struct FrameGeom {
 };
 
 // ------------------------------------------------------------------ kernels (launchers)
+constexpr int kRorCounters = 256;   // spread n_clipped counter slots (k_ror_tile)
 struct RorLaunch {
     const uint8_t *cloud; uint64_t n; uint32_t step, ox, oy, oz; int is_dense;
     float bminx, bminy, bminz, bmaxx, bmaxy, bmaxz, inv_cs; int nbx, nby;

@@ -29,7 +29,7 @@ enum ConflictMode {
 };
 struct HashG { double x0, y0, inv; int nx, ny; };
 HashG make_hash(double minx, double maxx, double miny, double maxy, double cell);
-struct DedupScratch { DevBuf keys, idx, skeys, sidx, ccount, coff, clist, state, f, pos, tmp; int n_conf = 0; };
+struct DedupScratch { DevBuf keys, idx, skeys, sidx, ccount, coff, clist, state, f, pos, tmp, und; int n_conf = 0; };
 // cand/ok device arrays of n entries; kept points (in order) -> out; optional kept flags -> state (S.state).
 // Returns the kept count.
 int greedy_dedup(DedupScratch &S, const double2 *cand, const int *ok, int n, int mode, double thr, const HashG &h,
@@ -73,6 +73,7 @@ struct GvdState {
     DevBuf seeds, merge_state, hash_count, hash_start, hash_slot, hash_sorted, scan_tmp, misc;
     DevBuf edges, bpts, near_idx, cand, cand_ok, skel, grid_bytes_ext;
     PinnedBuf h_misc;
+    void *scratch = nullptr;   // GvdScratch (gvd.hip), freed by free_gvd_scratch
     Subdiv2D subdiv;   // host insert replay; kept across frames to reuse its allocations
     // host outputs
     std::vector<double> nodes_xy;

@@ -71,7 +71,7 @@ __device__ __forceinline__ int lower_bound_key(const int *keys, int n, int k) {
 
 // coff == nullptr: count pass; else fill pass
 __global__ void k_conflicts(const double2 *p, const int *ok, int n, HashG h, const int *skeys, const int *sidx,
-                            int mode, double thr, const int *coff, int *ccount, int *clist) {
+                            int mode, double thr, const int *coff, int *ccount, int *clist, long long cap) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     if (!ok[i]) { if (!coff) ccount[i] = 0; return; }
@@ -85,7 +85,7 @@ __global__ void k_conflicts(const double2 *p, const int *ok, int n, HashG h, con
         for (int k = k0; k < k1; ++k) {
             int j = sidx[k];
             if (j < i && conflict(pi, p[j], mode, thr)) {
-                if (coff) clist[w + c] = j;
+                if (coff && (long long)w + c < cap) clist[w + c] = j;   // overflow: host re-runs with the exact size
                 ++c;
             }
         }
@@ -145,35 +145,45 @@ int greedy_dedup(DedupScratch &S, const double2 *cand, const int *ok, int n, int
     AOS_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys, skeys, idx, sidx, n, 0, 32, s));
     int *ccount = dev<int>(S.ccount, n + 1), *coff = dev<int>(S.coff, n + 1);
     AOS_HIP(hipMemsetAsync(ccount + n, 0, sizeof(int), s));
-    k_conflicts<<<cdiv(n, 256), 256, 0, s>>>(cand, ok, n, h, skeys, sidx, mode, thr, nullptr, ccount, nullptr);
+    k_conflicts<<<cdiv(n, 256), 256, 0, s>>>(cand, ok, n, h, skeys, sidx, mode, thr, nullptr, ccount, nullptr, 0);
     AOS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, ccount, coff, n + 1, s));
-    AOS_HIP(hipMemcpyAsync(h_scalar, coff + n, sizeof(int), hipMemcpyDeviceToHost, s));
-    AOS_HIP(hipStreamSynchronize(s));
-    S.n_conf = h_scalar[0];
-    int *clist = dev<int>(S.clist, S.n_conf);
-    k_conflicts<<<cdiv(n, 256), 256, 0, s>>>(cand, ok, n, h, skeys, sidx, mode, thr, coff, nullptr, clist);
+    // Optimistic capacity for the conflict lists (no read-back of the exact total before the rounds):
+    // the total comes back with the first round batch; on overflow the lists are rebuilt exactly.
+    long long cap = std::max<long long>((long long)(S.clist.cap / sizeof(int)), 8LL * n);
+    int *clist = dev<int>(S.clist, (size_t)cap);
     int *state = dev<int>(S.state, n);
-    k_greedy_init<<<cdiv(n, 256), 256, 0, s>>>(ok, n, state);
-    // rounds: launch a batch, check the last round's undecided count once per batch
+    int *f = dev<int>(S.f, n + 1), *pos = dev<int>(S.pos, n + 1);
     constexpr int kBatch = 6;
-    int *und = dev<int>(S.f, std::max(n + 1, kBatch));   // scratch; reused for kept flags below
+    int *und = dev<int>(S.und, kBatch);
+    auto fill = [&]() {
+        k_conflicts<<<cdiv(n, 256), 256, 0, s>>>(cand, ok, n, h, skeys, sidx, mode, thr, coff, nullptr, clist, cap);
+        k_greedy_init<<<cdiv(n, 256), 256, 0, s>>>(ok, n, state);
+    };
+    fill();
+    AOS_HIP(hipMemsetAsync(f + n, 0, sizeof(int), s));
     for (int done_rounds = 0;;) {
+        // a batch of rounds, then (speculatively) the compaction of the kept set, one read-back
         AOS_HIP(hipMemsetAsync(und, 0, sizeof(int) * kBatch, s));
         for (int r = 0; r < kBatch; ++r) k_greedy_round<<<cdiv(n, 256), 256, 0, s>>>(n, coff, clist, state, und + r);
-        AOS_HIP(hipMemcpyAsync(h_scalar, und, sizeof(int) * kBatch, hipMemcpyDeviceToHost, s));
+        k_kept_flags<<<cdiv(n, 256), 256, 0, s>>>(state, n, f);
+        AOS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, f, pos, n + 1, s));
+        k_compact<<<cdiv(n, 256), 256, 0, s>>>(cand, f, pos, n, out, kept_index_out);
+        AOS_HIP(hipMemcpyAsync(h_scalar, und + kBatch - 1, sizeof(int), hipMemcpyDeviceToHost, s));
+        AOS_HIP(hipMemcpyAsync(h_scalar + 1, coff + n, sizeof(int), hipMemcpyDeviceToHost, s));
+        AOS_HIP(hipMemcpyAsync(h_scalar + 2, pos + n, sizeof(int), hipMemcpyDeviceToHost, s));
         AOS_HIP(hipStreamSynchronize(s));
+        S.n_conf = h_scalar[1];
+        if ((long long)S.n_conf > cap) {   // conflict lists were truncated: rebuild at the exact size
+            cap = S.n_conf;
+            clist = dev<int>(S.clist, (size_t)cap);
+            fill();
+            done_rounds = 0;
+            continue;
+        }
         done_rounds += kBatch;
-        if (h_scalar[kBatch - 1] == 0) break;
+        if (h_scalar[0] == 0) return h_scalar[2];
         if (done_rounds > n + kBatch) throw std::runtime_error("greedy de-duplication did not converge");
     }
-    int *f = dev<int>(S.f, n + 1), *pos = dev<int>(S.pos, n + 1);
-    AOS_HIP(hipMemsetAsync(f + n, 0, sizeof(int), s));
-    k_kept_flags<<<cdiv(n, 256), 256, 0, s>>>(state, n, f);
-    AOS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, f, pos, n + 1, s));
-    k_compact<<<cdiv(n, 256), 256, 0, s>>>(cand, f, pos, n, out, kept_index_out);
-    AOS_HIP(hipMemcpyAsync(h_scalar, pos + n, sizeof(int), hipMemcpyDeviceToHost, s));
-    AOS_HIP(hipStreamSynchronize(s));
-    return h_scalar[0];
 }
 
 }  // namespace aos

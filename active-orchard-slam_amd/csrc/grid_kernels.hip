@@ -102,7 +102,32 @@ __global__ void k_ror_scatter(RorLaunch L, const int *bin_start, const int2 *pt_
 // counts its neighbours from LDS. A strip whose neighbourhood exceeds kRorCap points reads the
 // same ranges from global memory instead. The keep decision only needs "at least need points
 // within r", so the scan order is free (own bin row first) and stops early.
-constexpr int kSW = 32, kRorCap = 1536, kRorTB = 128;
+#ifndef AOS_ROR_CAP
+#define AOS_ROR_CAP 2048
+#endif
+#ifndef AOS_ROR_NOSCAN   // timing experiments only (tools/ab_variants.sh): wrong results
+#define AOS_ROR_NOSCAN 0
+#endif
+#ifndef AOS_ROR_NOSTORE
+#define AOS_ROR_NOSTORE 0
+#endif
+#ifndef AOS_ROR_XCD
+#define AOS_ROR_XCD 1
+#endif
+#ifndef AOS_ROR_SW
+#define AOS_ROR_SW 64
+#endif
+#ifndef AOS_ROR_TB
+#define AOS_ROR_TB 256
+#endif
+constexpr int kSW = AOS_ROR_SW, kRorCap = AOS_ROR_CAP, kRorTB = AOS_ROR_TB;
+
+// XCD-aware block order (cdna_hip_programming.md §5.5 T1): blocks b = j (mod 8) share an XCD's L2,
+// so group j gets one contiguous range of logical blocks (neighbouring bin rows stay on one L2).
+__device__ __forceinline__ int xcd_block(int b, int n) {
+    const int q = n >> 3, r = n & 7, j = b & 7, k = b >> 3;
+    return j * q + min(j, r) + k;
+}
 
 __device__ __forceinline__ bool ror_in(const RorLaunch &L, float4 p, float4 q) {
     float dx = p.x - q.x, dy = p.y - q.y, dz = p.z - q.z;
@@ -129,7 +154,8 @@ __global__ __launch_bounds__(kRorTB) void k_ror_tile(RorLaunch L, const int *bin
     __shared__ int offs[3][kSW + 3];   // global offsets of bins xlo .. xhi + 1 in rows by-1, by, by+1
     __shared__ int base[4];
     const int nstrip = (L.nbx + kSW - 1) / kSW;
-    const int by = blockIdx.x / nstrip, bx0 = (blockIdx.x - by * nstrip) * kSW;
+    const int blk = AOS_ROR_XCD ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int by = blk / nstrip, bx0 = (blk - by * nstrip) * kSW;
     const int bx1 = min(bx0 + kSW, L.nbx);                        // own bins [bx0, bx1)
     const int xlo = max(bx0 - 1, 0), xhi = min(bx1, L.nbx - 1);  // neighbourhood bins, inclusive
     const int nbins = xhi - xlo + 1;
@@ -163,7 +189,7 @@ __global__ __launch_bounds__(kRorTB) void k_ror_tile(RorLaunch L, const int *bin
         int bx, byy;
         bin_of(L, p.x, p.y, bx, byy);
         const int c0 = max(bx - 1, xlo) - xlo, c1 = min(bx + 1, xhi) - xlo + 1;
-        int cnt = 0;
+        int cnt = AOS_ROR_NOSCAN ? L.need : 0;
 #pragma unroll
         for (int rr = 0; rr < 3; ++rr) {
             const int r = rr == 0 ? 1 : (rr == 1 ? 0 : 2);   // own bin row first
@@ -177,12 +203,15 @@ __global__ __launch_bounds__(kRorTB) void k_ror_tile(RorLaunch L, const int *bin
             ++kept_n;
             int gx = (int)(((double)p.x - L.origin_x) / (double)L.res);
             int gy = (int)(((double)p.y - L.origin_y) / (double)L.res);
-            if (gx >= 0 && gx < L.W && gy >= 0 && gy < L.H) raster[(size_t)gy * L.W + gx] = 1;
+            if (!AOS_ROR_NOSTORE && gx >= 0 && gx < L.W && gy >= 0 && gy < L.H) raster[(size_t)gy * L.W + gx] = 1;
         }
     }
-    // stats: candidates that survived ROR (n_clipped); wave-aggregated
+    // stats: candidates that survived ROR (n_clipped). Wave-aggregated, then spread over
+    // kRorCounters slots: one hot address would serialise ~10^5 same-address atomics in one L2
+    // channel (it used to bound this kernel at ~0.9 ms). The host sums the slots.
     for (int o = 32; o > 0; o >>= 1) kept_n += __shfl_xor(kept_n, o);
-    if ((threadIdx.x & 63) == 0 && kept_n) atomicAdd(&counters[0], (unsigned long long)kept_n);
+    if ((threadIdx.x & 63) == 0 && kept_n)
+        atomicAdd(&counters[(blk * (kRorTB / 64) + (threadIdx.x >> 6)) & (kRorCounters - 1)], (unsigned long long)kept_n);
 }
 
 void launch_ror_bin(const RorLaunch &L, int *bin_count, int2 *pt_binslot, hipStream_t s) {

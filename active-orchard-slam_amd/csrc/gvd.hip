@@ -481,24 +481,12 @@ struct GvdScratch {
         sd_qe, sd_vp, sd_vfirst, sd_vtype, sd_face, sd_cnt, sd_off;
 };
 static GvdScratch &scratch(GvdState &G) {
-    // one scratch per state (per handle); stored behind the misc buffer slot
-    if (!G.misc.p) { G.misc.p = new GvdScratch(); G.misc.cap = 0; }
-    return *static_cast<GvdScratch *>(G.misc.p);
+    if (!G.scratch) G.scratch = new GvdScratch();
+    return *static_cast<GvdScratch *>(G.scratch);
 }
 void free_gvd_scratch(GvdState &G) {
-    if (G.misc.p) {
-        auto *S = static_cast<GvdScratch *>(G.misc.p);
-        DevBuf *all[] = {&S->raw, &S->ok, &S->leaders, &S->merged, &S->owner, &S->oidx, &S->sowner, &S->sidx, &S->tmp,
-                         &S->edges_f, &S->occ, &S->occ_ok, &S->bp, &S->kept_occ, &S->keys, &S->idx, &S->skeys, &S->sidx2,
-                         &S->near_idx, &S->pk, &S->pidx, &S->pskeys, &S->psidx, &S->pcount, &S->poff, &S->plist, &S->ft,
-                         &S->ckey, &S->cvalid, &S->pass, &S->k2, &S->occ_idx, &S->sk2, &S->socc, &S->selected, &S->inside,
-                         &S->ipos, &S->nodes, &S->keep, &S->kpos, &S->edges, &S->lens, &S->jobs, &S->lpts, &S->lval,
-                         &S->lmask, &S->lcidx, &S->lcount, &S->loff, &S->lcl, &S->lty, &S->scan_tmp,
-                         &S->sd_qe, &S->sd_vp, &S->sd_vfirst, &S->sd_vtype, &S->sd_face, &S->sd_cnt, &S->sd_off};
-        for (DevBuf *b : all) b->release();
-        delete S;
-        G.misc.p = nullptr;
-    }
+    delete static_cast<GvdScratch *>(G.scratch);   // DevBuf members free themselves
+    G.scratch = nullptr;
 }
 
 static void scan_excl(DevBuf &tmpb, const int *in, int *out, int n, hipStream_t s) {

@@ -76,7 +76,7 @@ void aos_ctx::run_seedgen(bool want_host, aos_seedgen_out &out) {
     hipStream_t s = stream;
     const size_t C = (size_t)g.W * g.H, Cw = (size_t)g.WW * g.H;
     AOS_HIP(hipEventRecord(ev[0], s));
-    static_cast<int *>(h_stats.ensure(64))[0] = 0;
+    static_cast<int *>(h_stats.ensure(64 + 8 * kRorCounters))[0] = 0;
 
     // ---------------- a1-a4: ROR restricted to the clip box, clip, exclusion discs, raster
     RorLaunch L{};
@@ -101,12 +101,12 @@ void aos_ctx::run_seedgen(bool want_host, aos_seedgen_out &out) {
     int *d_bc = static_cast<int *>(bin_count.ensure(sizeof(int) * (nb + 1)));
     int *d_bs = static_cast<int *>(bin_start.ensure(sizeof(int) * (nb + 1)));
     int2 *d_ps = static_cast<int2 *>(pt_binslot.ensure(sizeof(int2) * std::max<uint64_t>(n_points, 1)));
-    unsigned long long *d_cnt = static_cast<unsigned long long *>(counters.ensure(64));
+    unsigned long long *d_cnt = static_cast<unsigned long long *>(counters.ensure(8 * kRorCounters));
     uint8_t *d_rb = static_cast<uint8_t *>(raster_bytes.ensure(C));
     size_t st = scan_temp_bytes(nb + 1);
     void *d_st = scan_tmp.ensure(st);
     AOS_HIP(hipMemsetAsync(d_bc, 0, sizeof(int) * (nb + 1), s));
-    AOS_HIP(hipMemsetAsync(d_cnt, 0, 64, s));
+    AOS_HIP(hipMemsetAsync(d_cnt, 0, 8 * kRorCounters, s));
     AOS_HIP(hipMemsetAsync(d_rb, 0, C, s));
     // PCL dense kNN needs k = min_pts + 1 points in the whole cloud (else every point is removed)
     const bool any = n_points > 0 && !(is_dense && n_points < (uint64_t)L.need);
@@ -119,7 +119,7 @@ void aos_ctx::run_seedgen(bool want_host, aos_seedgen_out &out) {
         AOS_HIP(hipEventRecord(ev[10], s));
         launch_ror_raster(L, d_bs, d_sorted, d_rb, d_cnt, s);
         AOS_HIP(hipEventRecord(ev[11], s));
-        AOS_HIP(hipMemcpyAsync(h_stats.ensure(64), d_bs + nb, sizeof(int), hipMemcpyDeviceToHost, s));
+        AOS_HIP(hipMemcpyAsync(h_stats.p, d_bs + nb, sizeof(int), hipMemcpyDeviceToHost, s));
     }
     AOS_HIP(hipEventRecord(ev[1], s));
 
@@ -205,15 +205,16 @@ void aos_ctx::run_seedgen(bool want_host, aos_seedgen_out &out) {
     run_cluster_seed_stage(cs, sin, so, s, ev[4]);
     AOS_HIP(hipEventRecord(ev[5], s));
 
-    unsigned long long h_cnt = 0;
-    AOS_HIP(hipMemcpyAsync(&h_cnt, d_cnt, sizeof(h_cnt), hipMemcpyDeviceToHost, s));
+    unsigned long long *h_cnt = static_cast<unsigned long long *>(h_stats.ensure(64 + 8 * kRorCounters)) + 8;
+    AOS_HIP(hipMemcpyAsync(h_cnt, d_cnt, 8 * kRorCounters, hipMemcpyDeviceToHost, s));
     if (want_host) {
         h_occ.resize(C); h_skel.resize(C);
         AOS_HIP(hipMemcpyAsync(h_occ.data(), d_occ, C, hipMemcpyDeviceToHost, s));
         AOS_HIP(hipMemcpyAsync(h_skel.data(), d_skel, C, hipMemcpyDeviceToHost, s));
     }
     AOS_HIP(hipStreamSynchronize(s));
-    n_clipped = h_cnt;
+    n_clipped = 0;
+    for (int i = 0; i < kRorCounters; ++i) n_clipped += h_cnt[i];
     have_frame = true;
 
     h_row_center = std::move(so.row_center); h_row_start = std::move(so.row_start);

@@ -205,16 +205,20 @@ def test_c0_against_golden_fixtures():
     c.close()
 
 
-def test_c1_against_golden_hashes():
+@pytest.mark.parametrize("name", ["C1", "C2"])
+def test_against_golden_hashes(name):
+    """Full frame (seed gen + GVD) vs the SHA-256 of the oracle's outputs (tests/golden/<name>_sha256.json);
+    C2 is the bench frame, so this pins bench.py's workload bit-exactly without running the oracle."""
     import hashlib
     import json
-    hs = json.load(open(__import__("os").path.join(__import__("os").path.dirname(__file__), "golden", "c1_sha256.json")))
+    import os
+    hs = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", f"{name.lower()}_sha256.json")))
 
     def sha(a, dt):
         a = np.ascontiguousarray(np.asarray(a, dtype=dt))
         return hashlib.sha256(a.dtype.str.encode() + str(a.shape).encode() + a.tobytes()).hexdigest()
 
-    cfg = orchard.CONFIGS["C1"]
+    cfg = orchard.CONFIGS[name]
     c = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res))
     c.set_polygon(orchard.polygon(cfg))
     g = c.seedgen(orchard.generate(cfg))

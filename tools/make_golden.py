@@ -9,11 +9,12 @@ scipy cross-checks (parity unpinned against the reference binary)
 Files:
   c0_seedgen.npz / c0_gvd.npz  config C0 (100 k points, 512^2 @ 0.2 m): every output, grids bit-packed
   c1_sha256.json               config C1 (2 M points, 2048^2 @ 0.1 m): SHA-256 of every output array
+  c2_sha256.json               config C2 (10 M points, 4096^2 @ 0.1 m, the bench frame), with --c2
   subdiv_kat.npz               Subdiv2D micro known-answer cases: co-circular, collinear, duplicate,
                                near-duplicate and on-edge seeds (Voronoi facets per real vertex, both
                                rect modes)
 
-usage: python tools/make_golden.py [--skip-c1]
+usage: python tools/make_golden.py [--skip-c1] [--c2]
 """
 import argparse
 import hashlib
@@ -74,6 +75,7 @@ def subdiv_cases():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-c1", action="store_true")
+    ap.add_argument("--c2", action="store_true", help="also hash config C2 (the bench frame; ~2-3 min of oracle time)")
     a = ap.parse_args()
     os.makedirs(GOLD, exist_ok=True)
     s, g = run("C0")
@@ -94,12 +96,14 @@ def main():
             kat[f"{name}_m{mode}_facet_pts"] = (np.concatenate(facets) if facets else np.zeros((0, 2))).astype(np.float32)
             kat[f"{name}_m{mode}_centers"] = np.asarray(centers, dtype=np.float32)
     np.savez_compressed(os.path.join(GOLD, "subdiv_kat.npz"), **kat)
-    if not a.skip_c1:
-        s1, g1 = run("C1")
+    for name, want in (("C1", not a.skip_c1), ("C2", a.c2)):
+        if not want:
+            continue
+        s1, g1 = run(name)
         h = {"meta": {k: s1[k] for k in ("width", "height", "thin_iters", "n_input", "n_ror_kept", "n_clipped")}}
         h["seedgen"] = {k: sha(s1[k]) for k in GRIDS + SEED_KEYS}
         h["gvd"] = {k: sha(g1[k]) for k in GVD_KEYS}
-        json.dump(h, open(os.path.join(GOLD, "c1_sha256.json"), "w"), indent=1, sort_keys=True)
+        json.dump(h, open(os.path.join(GOLD, f"{name.lower()}_sha256.json"), "w"), indent=1, sort_keys=True)
     print("golden fixtures written to", GOLD)
 
 
