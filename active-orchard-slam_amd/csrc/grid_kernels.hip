@@ -114,6 +114,9 @@ __global__ void k_ror_scatter(RorLaunch L, const int *bin_start, const int2 *pt_
 #ifndef AOS_ROR_XCD
 #define AOS_ROR_XCD 1
 #endif
+#ifndef AOS_ROR_SWEEP
+#define AOS_ROR_SWEEP 1
+#endif
 #ifndef AOS_ROR_SW
 #define AOS_ROR_SW 64
 #endif
@@ -142,6 +145,18 @@ __device__ __forceinline__ int ror_scan(const RorLaunch &L, float4 p, Ptr pts, i
         float4 q[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) q[j] = pts[min(k + j, k1 - 1)];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cnt += (k + j < k1 && ror_in(L, p, q[j])) ? 1 : 0;
+    }
+    return cnt;
+}
+
+// same as ror_scan on one staged LDS row (indexing the __shared__ row keeps ds_read instructions)
+__device__ __forceinline__ int ror_scan_lds(const RorLaunch &L, float4 p, const float4 (&row)[512], int k0, int k1, int cnt) {
+    for (int k = k0; k < k1 && cnt < L.need; k += 4) {
+        float4 q[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) q[j] = row[min(k + j, k1 - 1)];
 #pragma unroll
         for (int j = 0; j < 4; ++j) cnt += (k + j < k1 && ror_in(L, p, q[j])) ? 1 : 0;
     }
@@ -214,6 +229,106 @@ __global__ __launch_bounds__(kRorTB) void k_ror_tile(RorLaunch L, const int *bin
         atomicAdd(&counters[(blk * (kRorTB / 64) + (threadIdx.x >> 6)) & (kRorCounters - 1)], (unsigned long long)kept_n);
 }
 
+// Row-sweep variant: one workgroup per (strip of kSwSW bins) x (segment of kSwSeg bin rows). It keeps
+// a ring of 4 staged point rows (y-1, y, y+1 and y+2 in flight) and 5 rows of bin offsets in LDS.
+// While it scans row y it has already issued the loads of row y+2's points and row y+3's offsets
+// into registers, so each step costs ~max(scan, one load latency) instead of a 3-trip chain per
+// workgroup. Rows with more than kSwCap points stay in global memory (scanned there).
+#ifndef AOS_SW_SEG
+#define AOS_SW_SEG 32
+#endif
+constexpr int kSwSW = 64, kSwTB = 256, kSwCap = 512, kSwSeg = AOS_SW_SEG, kSwPer = kSwCap / kSwTB;
+
+__global__ __launch_bounds__(kSwTB) void k_ror_sweep(RorLaunch L, const int *bin_start, const float4 *sorted,
+                                                     uint8_t *raster, unsigned long long *counters) {
+    __shared__ float4 pts[4][kSwCap];
+    __shared__ int offs[5][kSwSW + 3];
+    __shared__ int staged[4];            // 1: row's points are in pts[slot]; 0: read them from global
+    const int tid = threadIdx.x;
+    const int nstrip = (L.nbx + kSwSW - 1) / kSwSW;
+    const int blk = xcd_block(blockIdx.x, gridDim.x);
+    const int strip = blk % nstrip, seg = blk / nstrip;
+    const int bx0 = strip * kSwSW, bx1 = min(bx0 + kSwSW, L.nbx);
+    const int xlo = max(bx0 - 1, 0), xhi = min(bx1, L.nbx - 1), nbins = xhi - xlo + 1;
+    const int y0 = seg * kSwSeg, y1 = min(y0 + kSwSeg, L.nby);
+    auto row_ok = [&](int yy) { return yy >= 0 && yy < L.nby; };
+    auto offs_of = [&](int yy, int c) { return row_ok(yy) ? bin_start[yy * L.nbx + xlo + c] : 0; };
+    // prologue: offsets of rows y0-1 .. y0+2, points of rows y0-1 .. y0+1
+    for (int t = tid; t < 4 * (nbins + 1); t += kSwTB) {
+        const int r = t / (nbins + 1), c = t - r * (nbins + 1), yy = y0 - 1 + r;
+        offs[(yy + 5) % 5][c] = offs_of(yy, c);
+    }
+    __syncthreads();
+    for (int r = 0; r < 3; ++r) {
+        const int yy = y0 - 1 + r, o = (yy + 5) % 5, sl = (yy + 4) & 3;
+        const int a = offs[o][0], n = offs[o][nbins] - a;
+        if (n <= kSwCap)
+            for (int t = tid; t < n; t += kSwTB) pts[sl][t] = sorted[a + t];
+        if (tid == 0) staged[sl] = n <= kSwCap;
+    }
+    __syncthreads();
+    unsigned kept_n = 0;
+    for (int y = y0; y < y1; ++y) {
+        // (1) issue the loads for row y+2's points and row y+3's offsets
+        const int opf = (y + 2 + 5) % 5, spf = (y + 2) & 3;
+        const int apf = offs[opf][0], npf = offs[opf][nbins] - apf;
+        float4 q[kSwPer];
+#pragma unroll
+        for (int j = 0; j < kSwPer; ++j) {
+            const int t = tid + j * kSwTB;
+            q[j] = sorted[(t < npf && npf <= kSwCap) ? apf + t : 0];
+        }
+        const int onew = tid <= nbins ? offs_of(y + 3, tid) : 0;
+        // (2) count neighbours of row y's candidates from the staged rows y-1, y, y+1. The own point is
+        // read in a branch on the (workgroup-uniform) staged flag: a select of an LDS and a global
+        // pointer would become a flat load, whose vmcnt wait would also wait for the prefetch above.
+        const int ocur = (y + 5) % 5, scur = y & 3;
+        const int own0 = offs[ocur][bx0 - xlo], own1 = offs[ocur][bx1 - xlo], base0 = offs[ocur][0];
+        auto count_one = [&](const float4 p) {
+            if (__float_as_int(p.w) == 0) return;   // not a clip candidate
+            int bx, byy;
+            bin_of(L, p.x, p.y, bx, byy);
+            const int c0 = max(bx - 1, xlo) - xlo, c1 = min(bx + 1, xhi) - xlo + 1;
+            int cnt = AOS_ROR_NOSCAN ? L.need : 0;
+#pragma unroll
+            for (int rr = 0; rr < 3; ++rr) {
+                const int yy = rr == 0 ? y : (rr == 1 ? y - 1 : y + 1);   // own bin row first
+                if (!row_ok(yy) || cnt >= L.need) continue;
+                const int o = (yy + 5) % 5, sl = (yy + 4) & 3;
+                const int g0 = offs[o][c0], g1 = offs[o][c1];
+                if (staged[sl]) cnt = ror_scan_lds(L, p, pts[sl], g0 - offs[o][0], g1 - offs[o][0], cnt);
+                else cnt = ror_scan(L, p, sorted, g0, g1, cnt);
+            }
+            if (cnt >= L.need) {
+                ++kept_n;
+                int gx = (int)(((double)p.x - L.origin_x) / (double)L.res);
+                int gy = (int)(((double)p.y - L.origin_y) / (double)L.res);
+                if (!AOS_ROR_NOSTORE && gx >= 0 && gx < L.W && gy >= 0 && gy < L.H) raster[(size_t)gy * L.W + gx] = 1;
+            }
+        };
+        if (staged[scur]) {
+            for (int k = own0 + tid; k < own1; k += kSwTB) count_one(pts[scur][k - base0]);
+        } else {
+            for (int k = own0 + tid; k < own1; k += kSwTB) count_one(sorted[k]);
+        }
+        // (3) commit the prefetched row y+2 and offsets of row y+3. Their slots held row y-2, which
+        // step y no longer reads, so no barrier is needed before the writes.
+        if (npf <= kSwCap) {
+#pragma unroll
+            for (int j = 0; j < kSwPer; ++j) {
+                const int t = tid + j * kSwTB;
+                if (t < npf) pts[spf][t] = q[j];
+            }
+        }
+        if (tid <= nbins) offs[(y + 3 + 5) % 5][tid] = onew;
+        if (tid == 0) staged[spf] = npf <= kSwCap;
+        __syncthreads();
+    }
+    for (int o = 32; o > 0; o >>= 1) kept_n += __shfl_xor(kept_n, o);
+    if ((tid & 63) == 0 && kept_n)
+        atomicAdd(&counters[(blk * (kSwTB / 64) + (tid >> 6)) & (kRorCounters - 1)], (unsigned long long)kept_n);
+}
+
 void launch_ror_bin(const RorLaunch &L, int *bin_count, int2 *pt_binslot, hipStream_t s) {
     if (!L.n) return;
     k_ror_bin<<<cdiv(L.n, 256), 256, 0, s>>>(L, bin_count, pt_binslot);
@@ -224,10 +339,17 @@ void launch_ror_scatter(const RorLaunch &L, const int *bin_start, const int2 *pt
 }
 void launch_ror_raster(const RorLaunch &L, const int *bin_start, const float4 *sorted, uint8_t *raster,
                        unsigned long long *counters, hipStream_t s) {
+#if AOS_ROR_SWEEP
+    const long long nblk = (long long)((L.nby + kSwSeg - 1) / kSwSeg) * ((L.nbx + kSwSW - 1) / kSwSW);
+    if (nblk <= 0) return;
+    if (nblk > INT_MAX) throw std::runtime_error("ROR bin grid too large");
+    k_ror_sweep<<<(int)nblk, kSwTB, 0, s>>>(L, bin_start, sorted, raster, counters);
+#else
     const long long nblk = (long long)L.nby * ((L.nbx + kSW - 1) / kSW);
     if (nblk <= 0) return;
     if (nblk > INT_MAX) throw std::runtime_error("ROR bin grid too large");
     k_ror_tile<<<(int)nblk, kRorTB, 0, s>>>(L, bin_start, sorted, raster, counters);
+#endif
 }
 
 size_t scan_temp_bytes(int n) {

@@ -289,30 +289,39 @@ __global__ __launch_bounds__(256) void k_label_points(const LabelRow *jobs, int 
     else { mdx = mdx / ml; mdy = mdy / ml; }
     const double outx = -mdx, outy = -mdy, perx = -mdy, pery = mdx;
     const bool m90 = fabs(J.deg - (-90.0)) < 1e-6, p90 = fabs(J.deg - 90.0) < 1e-6;
-    double best = 1.7976931348623157e308;
-    int bi = INT_MAX;
-    for (int i = threadIdx.x; i < Mn; i += blockDim.x) {
-        double dx = nodes[i].x - J.ex, dy = nodes[i].y - J.ey;
-        double dist = sqrt(dx * dx + dy * dy);
-        if (dist < 0.5 || dist > fmax(9.0, g.diag2)) continue;  // radii {5, 7, 9, diag2}: first hit = arg-min
-        double nx = dx, ny = dy;
-        double z = dx * dx + dy * dy;
-        if (z > 0.0) { double s = sqrt(z); nx = dx / s; ny = dy / s; }
-        if (outx * nx + outy * ny < 0.0) continue;
-        double dp = perx * nx + pery * ny;
-        if (m90) { if (dp > 0.0) continue; }
-        else if (p90) { if (dp < 0.0) continue; }
-        if (dist < best || (dist == best && i < bi)) { best = dist; bi = i; }
-    }
+    // The reference returns the nearest valid candidate of the first radius in {5, 7, 9, diag2} that
+    // has one, i.e. the arg-min (first strict minimum) over all valid candidates. Pass 0 evaluates
+    // the exact test only for nodes with z <= 25 (1 + 1e-12) (a superset of dist <= 5); if it finds a
+    // candidate, the global arg-min is among them. Pass 1 (rare) scans everything.
     __shared__ double sb[256];
     __shared__ int si[256];
-    sb[threadIdx.x] = best; si[threadIdx.x] = bi;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if (threadIdx.x < o) {
-            double b2 = sb[threadIdx.x + o]; int i2 = si[threadIdx.x + o];
-            if (b2 < sb[threadIdx.x] || (b2 == sb[threadIdx.x] && i2 < si[threadIdx.x])) { sb[threadIdx.x] = b2; si[threadIdx.x] = i2; }
+    for (int pass = 0; pass < 2; ++pass) {
+        double best = 1.7976931348623157e308;
+        int bi = INT_MAX;
+        for (int i = threadIdx.x; i < Mn; i += blockDim.x) {
+            double dx = nodes[i].x - J.ex, dy = nodes[i].y - J.ey;
+            double z = dx * dx + dy * dy;
+            if (pass == 0 && !(z <= 25.0 * (1.0 + 1e-12))) continue;
+            double dist = sqrt(z);
+            if (dist < 0.5 || dist > fmax(9.0, g.diag2)) continue;
+            double nx = dx, ny = dy;
+            if (z > 0.0) { double s = sqrt(z); nx = dx / s; ny = dy / s; }
+            if (outx * nx + outy * ny < 0.0) continue;
+            double dp = perx * nx + pery * ny;
+            if (m90) { if (dp > 0.0) continue; }
+            else if (p90) { if (dp < 0.0) continue; }
+            if (dist < best || (dist == best && i < bi)) { best = dist; bi = i; }
         }
+        sb[threadIdx.x] = best; si[threadIdx.x] = bi;
+        __syncthreads();
+        for (int o = 128; o > 0; o >>= 1) {
+            if (threadIdx.x < o) {
+                double b2 = sb[threadIdx.x + o]; int i2 = si[threadIdx.x + o];
+                if (b2 < sb[threadIdx.x] || (b2 == sb[threadIdx.x] && i2 < si[threadIdx.x])) { sb[threadIdx.x] = b2; si[threadIdx.x] = i2; }
+            }
+            __syncthreads();
+        }
+        if (si[0] != INT_MAX) break;   // uniform: every thread reads the same shared value
         __syncthreads();
     }
     if (threadIdx.x != 0) return;
@@ -374,6 +383,9 @@ __global__ void k_node_labels(const double2 *nodes, int Mn, const double2 *lp, c
         for (int k = 0; k < 4; ++k) {
             if (!lv[4 * r + k]) continue;
             double dx = p.x - lp[4 * r + k].x, dy = p.y - lp[4 * r + k].y;
+            // exact prefilter: |dx| >= 0.1 implies fl(sqrt(fl(dx*dx) + fl(dy*dy))) >= sqrt(fl(0.1*0.1)) = 0.1
+            // (monotone rounding), so the reference's test below is false anyway
+            if (!(fabs(dx) < 0.1) || !(fabs(dy) < 0.1)) continue;
             if (sqrt(dx * dx + dy * dy) < 0.1) {
                 m |= 1 << k;
                 if (off) { lcl[w + cnt] = r; lty[w + cnt] = k; }
