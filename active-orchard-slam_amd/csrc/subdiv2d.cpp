@@ -12,7 +12,7 @@ namespace {
 inline double tri_area(float ax, float ay, float bx, float by, float cx, float cy) {
     return ((double)bx - ax) * ((double)cy - ay) - ((double)by - ay) * ((double)cx - ax);
 }
-// computeVoronoiPoint; returns false for det == 0 (FLT_MAX marker)
+// computeVoronoiPoint; returns false for det == 0 or a huge result (the vertex is not created)
 inline bool voronoi_point(float o0x, float o0y, float d0x, float d0y, float o1x, float o1y, float d1x, float d1y,
                           float &rx, float &ry) {
     double a0 = d0x - o0x, b0 = d0y - o0y;
@@ -32,26 +32,25 @@ inline bool voronoi_point(float o0x, float o0y, float d0x, float d0y, float o1x,
 
 void Subdiv2D::reserve(size_t n) {
     vp.reserve(2 * n + 8); vd.reserve(2 * n + 8); vfirst.reserve(2 * n + 8); vtype.reserve(2 * n + 8);
-    qe.reserve(3 * n + 8);
+    rec.reserve(3 * n + 8);
 }
 
-int Subdiv2D::right_of(float px, float py, int e) const {
-    const QE &q = qe[e >> 2];
-    const V2f o = vp[q.pt[e & 3]], d = vp[q.pt[(e + 2) & 3]];
-    double cw = tri_area(px, py, d.x, d.y, o.x, o.y);
+int Subdiv2D::right_of(float px, float py, int e) const {   // isRightOf: sign of triangleArea(p, dst, org)
+    const V2d &o = vd[org(e)], &d = vd[dst(e)];
+    const double x = px, y = py;
+    const double cw = (d.x - x) * (o.y - y) - (d.y - y) * (o.x - x);
     return (cw > 0) - (cw < 0);
 }
 
+// newEdge: a fresh quad-edge whose primal edges are singleton rings; free quad-edges are reused LIFO
 int Subdiv2D::new_edge() {
     if (free_q <= 0) {
-        qe.push_back(QE{{0, 0, 0, 0}, {0, 0, 0, 0}});
-        free_q = (int)qe.size() - 1;
+        rec.push_back(Rec{{0, 0}, {0, 0}, {0, 0}, 0, 0});
+        free_q = (int)rec.size() - 1;
     }
-    int e = free_q * 4;
-    QE &q = qe[free_q];
-    free_q = q.next[1];
-    q.next[0] = e; q.next[1] = e + 3; q.next[2] = e + 2; q.next[3] = e + 1;
-    q.pt[0] = q.pt[1] = q.pt[2] = q.pt[3] = 0;
+    const int q = free_q, e = q * 4;
+    free_q = rec[q].link;
+    rec[q] = Rec{{e, e + 2}, {e, e + 2}, {0, 0}, 0, 0};
     return e;
 }
 
@@ -60,7 +59,7 @@ int Subdiv2D::new_point(float x, float y, int type) {
         vp.push_back(V2f{0.f, 0.f}); vfirst.push_back(0); vtype.push_back(-1);
         free_p = (int)vp.size() - 1;
     }
-    int v = free_p;
+    const int v = free_p;
     free_p = vfirst[v];
     vp[v] = V2f{x, y}; vfirst[v] = 0; vtype[v] = type;
     if (vd.size() < vp.size()) vd.resize(vp.size());
@@ -68,46 +67,38 @@ int Subdiv2D::new_point(float x, float y, int type) {
     return v;
 }
 
-void Subdiv2D::splice(int a, int b) {
-    int &an = qe[a >> 2].next[a & 3], &bn = qe[b >> 2].next[b & 3];
-    int ar = rot(an, 1), br = rot(bn, 1);
-    int &arn = qe[ar >> 2].next[ar & 3], &brn = qe[br >> 2].next[br & 3];
-    std::swap(an, bn);
-    std::swap(arn, brn);
-}
-
-void Subdiv2D::set_pts(int e, int o, int d) {
-    qe[e >> 2].pt[e & 3] = o;
-    qe[e >> 2].pt[(e + 2) & 3] = d;
+void Subdiv2D::set_pts(int e, int o, int d) {   // setEdgePoints
+    rec[e >> 2].org[dir(e)] = o;
+    rec[e >> 2].org[dir(e) ^ 1] = d;
     vfirst[o] = e;
-    vfirst[d] = e ^ 2;
+    vfirst[d] = sym(e);
 }
 
-int Subdiv2D::connect(int a, int b) {
-    int e = new_edge();
-    splice(e, get_e(a, NEXT_AROUND_LEFT));
-    splice(e ^ 2, b);
+int Subdiv2D::connect(int a, int b) {   // connectEdges
+    const int e = new_edge();
+    splice(e, lnext(a));
+    splice(sym(e), b);
     set_pts(e, dst(a), org(b));
     return e;
 }
 
-void Subdiv2D::swap_edge(int e) {
-    int se = e ^ 2;
-    int a = get_e(e, PREV_AROUND_ORG), b = get_e(se, PREV_AROUND_ORG);
+void Subdiv2D::swap_edge(int e) {   // swapEdges
+    const int se = sym(e);
+    const int a = oprev(e), b = oprev(se);
     splice(e, a);
     splice(se, b);
     set_pts(e, dst(a), dst(b));
-    splice(e, get_e(a, NEXT_AROUND_LEFT));
-    splice(se, get_e(b, NEXT_AROUND_LEFT));
+    splice(e, lnext(a));
+    splice(se, lnext(b));
 }
 
-void Subdiv2D::delete_edge(int e) {
-    splice(e, get_e(e, PREV_AROUND_ORG));
-    int se = e ^ 2;
-    splice(se, get_e(se, PREV_AROUND_ORG));
-    int q = e >> 2;
-    qe[q].next[0] = 0;
-    qe[q].next[1] = free_q;
+void Subdiv2D::delete_edge(int e) {   // deleteEdge
+    splice(e, oprev(e));
+    const int se = sym(e);
+    splice(se, oprev(se));
+    const int q = e >> 2;
+    rec[q].on[0] = 0;          // free marker (OpenCV: next[0] = 0)
+    rec[q].link = free_q;
     free_q = q;
 }
 
@@ -117,44 +108,44 @@ void Subdiv2D::init_delaunay(float rx, float ry, float rw, float rh, int rect_mo
         rw = (float)(int)std::lrint(rw); rh = (float)(int)std::lrint(rh);
     }
     const float big = 3.f * std::max(rw, rh);
-    vp.clear(); vd.clear(); vfirst.clear(); vtype.clear(); qe.clear();
+    vp.clear(); vd.clear(); vfirst.clear(); vtype.clear(); rec.clear();
     recent = 0;
     tlx = rx; tly = ry; brx = rx + rw; bry = ry + rh;
-    vp.push_back(V2f{0.f, 0.f}); vfirst.push_back(0); vtype.push_back(-1);   // vtx[0]
-    qe.push_back(QE{{0, 0, 0, 0}, {0, 0, 0, 0}});                             // qedges[0]
+    vp.push_back(V2f{0.f, 0.f}); vd.push_back(V2d{0.0, 0.0, 0.0, 0.0}); vfirst.push_back(0); vtype.push_back(-1);
+    rec.push_back(Rec{{0, 0}, {0, 0}, {0, 0}, 0, 0});                          // quad-edge 0 (NULL)
     free_q = 0; free_p = 0;
-    int pA = new_point(rx + big, ry, 0), pB = new_point(rx, ry + big, 0), pC = new_point(rx - big, ry - big, 0);
-    int eAB = new_edge(), eBC = new_edge(), eCA = new_edge();
+    const int pA = new_point(rx + big, ry, 0), pB = new_point(rx, ry + big, 0), pC = new_point(rx - big, ry - big, 0);
+    const int eAB = new_edge(), eBC = new_edge(), eCA = new_edge();
     set_pts(eAB, pA, pB); set_pts(eBC, pB, pC); set_pts(eCA, pC, pA);
-    splice(eAB, eCA ^ 2); splice(eBC, eAB ^ 2); splice(eCA, eBC ^ 2);
+    splice(eAB, sym(eCA)); splice(eBC, sym(eAB)); splice(eCA, sym(eBC));
     recent = eAB;
 }
 
 // Subdiv2D::locate: 0 inside, 1 vertex, 2 on edge, -1 outside rect, -2 error
 int Subdiv2D::locate(float px, float py, int &out_edge, int &out_vertex) {
     int vertex = 0;
-    const int max_edges = (int)qe.size() * 4;
+    const int max_edges = (int)rec.size() * 4;
     if (px < tlx || py < tly || px >= brx || py >= bry) return -1;
     int edge = recent;
     int location = -2;
     int roc = right_of(px, py, edge);
-    if (roc > 0) { edge ^= 2; roc = -roc; }
+    if (roc > 0) { edge = sym(edge); roc = -roc; }
     for (int i = 0; i < max_edges; i++) {
-        int onext = next_e(edge);
-        int dprev = get_e(edge, PREV_AROUND_DST);
-        int ron = right_of(px, py, onext);
-        int rod = right_of(px, py, dprev);
+        const int on_ = onext(edge);
+        const int dp = dprev(edge);
+        const int ron = right_of(px, py, on_);
+        const int rod = right_of(px, py, dp);
         if (rod > 0) {
             if (ron > 0 || (ron == 0 && roc == 0)) { location = 0; break; }
-            roc = ron; edge = onext;
+            roc = ron; edge = on_;
         } else {
             if (ron > 0) {
                 if (rod == 0 && roc == 0) { location = 0; break; }
-                roc = rod; edge = dprev;
-            } else if (roc == 0 && right_of(vp[dst(onext)].x, vp[dst(onext)].y, edge) >= 0) {
-                edge ^= 2;
+                roc = rod; edge = dp;
+            } else if (roc == 0 && right_of(vp[dst(on_)].x, vp[dst(on_)].y, edge) >= 0) {
+                edge = sym(edge);
             } else {
-                roc = ron; edge = onext;
+                roc = ron; edge = on_;
             }
         }
     }
@@ -176,12 +167,12 @@ int Subdiv2D::locate(float px, float py, int &out_edge, int &out_vertex) {
 
 bool Subdiv2D::insert(float x, float y) {
     int curr_edge = 0, curr_point = 0;
-    int loc = locate(x, y, curr_edge, curr_point);
+    const int loc = locate(x, y, curr_edge, curr_point);
     if (loc < 0) return false;        // PTLOC_ERROR (CV_StsBadSize) / outside rect (CV_StsOutOfRange)
     if (loc == 1) return true;        // existing vertex: nothing inserted
     if (loc == 2) {
-        int deleted = curr_edge;
-        recent = curr_edge = get_e(curr_edge, PREV_AROUND_ORG);
+        const int deleted = curr_edge;
+        recent = curr_edge = oprev(curr_edge);
         delete_edge(deleted);
     }
     if (curr_edge == 0) return false;  // CV_Assert
@@ -191,20 +182,20 @@ bool Subdiv2D::insert(float x, float y) {
     set_pts(base, first_point, curr_point);
     splice(base, curr_edge);
     do {
-        base = connect(curr_edge, base ^ 2);
-        curr_edge = get_e(base, PREV_AROUND_ORG);
+        base = connect(curr_edge, sym(base));
+        curr_edge = oprev(base);
     } while (dst(curr_edge) != first_point);
-    curr_edge = get_e(base, PREV_AROUND_ORG);
-    const int max_edges = (int)qe.size() * 4;
+    curr_edge = oprev(base);
+    const int max_edges = (int)rec.size() * 4;
     // Swap loop with the predicates written out on exact double copies of the float coordinates
     // (the float -> double conversions are exact, so every product and sum rounds as in
     // triangleArea / isPtInCircle3, and |p|^2 is formed once per vertex in the same order).
     const V2d P = vd[curr_point];
     auto area = [](const V2d &a, const V2d &b, const V2d &c) { return (b.x - a.x) * (c.y - a.y) - (b.y - a.y) * (c.x - a.x); };
     for (int i = 0; i < max_edges; i++) {
-        int temp = get_e(curr_edge, PREV_AROUND_ORG);
-        int tdst = dst(temp), corg = org(curr_edge), cdst = dst(curr_edge);
-        const V2d T = vd[tdst], O = vd[corg], D = vd[cdst];
+        const int temp = oprev(curr_edge);
+        const int tdst = dst(temp), corg = org(curr_edge), cdst = dst(curr_edge);
+        const V2d &T = vd[tdst], &O = vd[corg], &D = vd[cdst];
         bool flip = false;
         if (area(T, D, O) > 0) {   // isRightOf(temp_dst, curr_edge) > 0
             // isPtInCircle3(pt = org, a = temp_dst, b = dst, c = new point) < 0, eps = FLT_EPSILON / 8
@@ -216,65 +207,84 @@ bool Subdiv2D::insert(float x, float y) {
         }
         if (flip) {
             swap_edge(curr_edge);
-            curr_edge = get_e(curr_edge, PREV_AROUND_ORG);
+            curr_edge = oprev(curr_edge);
         } else if (corg == first_point) {
             break;
         } else {
-            curr_edge = get_e(next_e(curr_edge), 0x20 /* PREV_AROUND_LEFT */);
+            curr_edge = lprev(onext(curr_edge));
         }
     }
     return true;
 }
 
-// calcVoronoi: quad-edges from #4 (#0 is NULL, #1-#3 the outer triangle); the first quad-edge
-// touching a triangle computes its circumcentre (pt[3] = left face, pt[1] = right face).
-void Subdiv2D::calc_voronoi() {
-    const int total = (int)qe.size();
-    for (int q = 0; q < total; ++q) qe[q].pt[1] = qe[q].pt[3] = 0;
+// OpenCV quad-edge layout: next[r] = Onext of rotation r of quad-edge q. Primal rotations come
+// straight from the rings; Onext(Rot e) = Rot^-1 Oprev(e) gives the dual ones. pt[0] / pt[2] are
+// the primal end points; the dual pt[1] / pt[3] (Voronoi vertices) start unset (calcVoronoi).
+Subdiv2D::Raw Subdiv2D::raw() {
+    const int n = (int)rec.size();
+    qx.assign(8 * (size_t)n, 0);
+    auto rot3 = [](int x) { return (x & ~3) + ((x + 3) & 3); };
+    for (int q = 1; q < n; ++q) {
+        const Rec &r = rec[q];
+        int *o = &qx[8 * (size_t)q];
+        if (r.on[0] <= 0) continue;   // free
+        o[0] = r.on[0]; o[1] = rot3(r.op[0]); o[2] = r.on[1]; o[3] = rot3(r.op[1]);
+        o[4] = r.org[0]; o[6] = r.org[1];
+    }
+    return Raw{qx.data(), n, reinterpret_cast<const float *>(vp.data()), vfirst.data(), vtype.data(), (int)vp.size()};
+}
+
+// calcVoronoi + getVoronoiFacetList on the exported layout (host reference of gvd.hip's builder).
+void Subdiv2D::voronoi_edges(std::vector<float> &edges) {
+    raw();
+    const int total = (int)rec.size();
+    auto next = [&](int e) { return qx[8 * (size_t)(e >> 2) + (e & 3)]; };
+    auto get_e = [&](int e, int t) { const int x = next((e & ~3) + ((e + t) & 3)); return (x & ~3) + ((x + (t >> 4)) & 3); };
+    auto pt = [&](int e) -> int & { return qx[8 * (size_t)(e >> 2) + 4 + (e & 3)]; };
     for (size_t i = 0; i < vp.size(); ++i)
         if (vtype[i] > 0) { vfirst[i] = free_p; vtype[i] = -1; free_p = (int)i; }
     for (int q = 4; q < total; q++) {
-        if (qe[q].next[0] <= 0) continue;  // free
+        if (qx[8 * (size_t)q] <= 0) continue;  // free
         const int e0 = q * 4;
-        if (!qe[q].pt[3]) {
-            int e1 = get_e(e0, NEXT_AROUND_LEFT), e2 = get_e(e1, NEXT_AROUND_LEFT);
-            const V2f a = vp[org(e0)], b = vp[dst(e0)], c = vp[org(e1)], d = vp[dst(e1)];
+        if (!pt(e0 + 3)) {   // left face
+            const int e1 = get_e(e0, 0x13), e2 = get_e(e1, 0x13);
+            const V2f a = vp[pt(e0)], b = vp[pt(e0 + 2)], c = vp[pt(e1)], d = vp[pt(e1 ^ 2)];
             float rx, ry;
             if (voronoi_point(a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y, rx, ry)) {
-                int p = new_point(rx, ry, 1);
-                qe[q].pt[3] = qe[e1 >> 2].pt[3 - (e1 & 2)] = qe[e2 >> 2].pt[3 - (e2 & 2)] = p;
+                const int p = new_point(rx, ry, 1);
+                pt(e0 + 3) = p;
+                qx[8 * (size_t)(e1 >> 2) + 4 + 3 - (e1 & 2)] = p;
+                qx[8 * (size_t)(e2 >> 2) + 4 + 3 - (e2 & 2)] = p;
             }
         }
-        if (!qe[q].pt[1]) {
-            int e1 = get_e(e0, NEXT_AROUND_RIGHT), e2 = get_e(e1, NEXT_AROUND_RIGHT);
-            const V2f a = vp[org(e0)], b = vp[dst(e0)], c = vp[org(e1)], d = vp[dst(e1)];
+        if (!pt(e0 + 1)) {   // right face
+            const int e1 = get_e(e0, 0x31), e2 = get_e(e1, 0x31);
+            const V2f a = vp[pt(e0)], b = vp[pt(e0 + 2)], c = vp[pt(e1)], d = vp[pt(e1 ^ 2)];
             float rx, ry;
             if (voronoi_point(a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y, rx, ry)) {
-                int p = new_point(rx, ry, 1);
-                qe[q].pt[1] = qe[e1 >> 2].pt[1 + (e1 & 2)] = qe[e2 >> 2].pt[1 + (e2 & 2)] = p;
+                const int p = new_point(rx, ry, 1);
+                pt(e0 + 1) = p;
+                qx[8 * (size_t)(e1 >> 2) + 4 + 1 + (e1 & 2)] = p;
+                qx[8 * (size_t)(e2 >> 2) + 4 + 1 + (e2 & 2)] = p;
             }
         }
     }
-}
-
-void Subdiv2D::voronoi_edges(std::vector<float> &edges) {
-    calc_voronoi();
     edges.clear();
     std::vector<int> facet;
-    const size_t total = vp.size();
-    for (size_t k = 4; k < total; k++) {
+    const size_t nv = vp.size();
+    for (size_t k = 4; k < nv; k++) {
         if (vtype[k] != 0) continue;  // free or virtual
-        const int start = rot(vfirst[k], 1);
+        const int f = vfirst[k], start = (f & ~3) + ((f + 1) & 3);
         int t = start;
         facet.clear();
         do {
-            facet.push_back(org(t));   // vtx[edgeOrg(t)] (index 0 = the (0,0) NULL vertex)
-            t = get_e(t, NEXT_AROUND_LEFT);
+            facet.push_back(pt(t));   // vtx[edgeOrg(t)] (index 0 = the (0,0) NULL vertex)
+            t = get_e(t, 0x13);
         } while (t != start);
         const size_t n = facet.size();
         if (n < 2) continue;
         for (size_t i = 0; i < n; ++i) {
-            int a = facet[i], b = facet[(i + 1) % n];
+            const int a = facet[i], b = facet[(i + 1) % n];
             edges.push_back(vp[a].x); edges.push_back(vp[a].y); edges.push_back(vp[b].x); edges.push_back(vp[b].y);
         }
     }

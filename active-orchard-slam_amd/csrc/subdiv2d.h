@@ -4,13 +4,21 @@
 //
 // Why on the host: insertion is inherently sequential and history-dependent — the quad-edge
 // numbering, vtx[].firstEdge (which decides where each facet starts) and which edge pair computes
-// each circumcentre (float rounding) all depend on the exact locate walk and flip order. GvdGraph
-// node numbering follows that order, so bit-identical topology needs this exact replay; the
-// GPU takes over from the facet list on (boundary points, graph, labels).
+// each circumcentre (float rounding) all depend on the exact locate walk and flip order. Each
+// insert's locate walk starts where the previous one ended, so there is no independent work to
+// spread. GvdGraph node order follows that history, so bit-identical topology needs this exact
+// replay; the GPU takes over from the facet list on (gvd.hip: k_vor_faces, k_facet_*).
 //
-// Layout: one 32-byte record per quad-edge ({next[4], pt[4]}, one cache line holds two) and one
-// 8-byte float2 per vertex: the flip walk (~115 iterations per insert on orchard seed rows, where
-// a new row line briefly fans out to the whole previous line) is pure pointer chasing.
+// Representation: OpenCV stores all four rotations of a quad-edge (primal and dual rings). Only the
+// primal rings are stored here, doubly linked (onext and its inverse oprev per directed edge), with
+// the same quad-edge ids (directed edge e = 4q + {0, 2}). Every navigation the algorithm uses is an
+// identity of the edge algebra (Oprev = Rot Onext Rot):
+//   Lnext(e) = Oprev(Sym e),  Dprev(e) = Sym Oprev(Sym e),  Lprev(e) = Sym Onext(e),
+// and splice(a, b) = swap(Onext a, Onext b) plus the two inverse links: two independent loads and
+// four stores instead of OpenCV's two-level dependent chain through the dual ring. The dual links
+// are recovered when the structure is exported (Onext(Rot e) = Rot^-1 Oprev(e)). On orchard seed rows
+// an insert performs ~56 swaps (~115 flip-loop steps) as each new seed on the next tree line takes
+// over the fan of the previous one, so these constant factors are the replay's cost.
 #pragma once
 #include <cstddef>
 #include <cstdint>
@@ -26,45 +34,51 @@ class Subdiv2D {
     bool insert(float x, float y);
     // getVoronoiFacetList(idx = {}): per real vertex (in vertex order) the facet polygon.
     // Emits the reference's edge list directly: (p_i, p_{i+1 mod n}) for facets with >= 2 points
-    // (voronoi_diagram.cpp:97-114), as float x0, y0, x1, y1.
+    // (voronoi_diagram.cpp:97-114), as float x0, y0, x1, y1. Host reference of the GPU builder.
     void voronoi_edges(std::vector<float> &edges);
     size_t num_vertices() const { return vp.size(); }
-    // Raw quad-edge state after the inserts, for the GPU facet builder (gvd.hip k_vor_faces /
-    // k_facet_*): qe = 8 ints per quad-edge {next[4], pt[4]}, vp = float2 per vertex.
-    struct Raw { const int *qe; int n_rec; const float *vp; const int *vfirst, *vtype; int n_vtx; };
-    Raw raw() const {
-        return Raw{reinterpret_cast<const int *>(qe.data()), (int)qe.size(), reinterpret_cast<const float *>(vp.data()),
-                   vfirst.data(), vtype.data(), (int)vp.size()};
-    }
     void reserve(size_t n_points);
+    // OpenCV-layout quad-edge state after the inserts, for the GPU facet builder:
+    // qe = 8 ints per quad-edge {next[4], pt[4]} (free quad-edges have next[0] = 0), vp = float2.
+    struct Raw { const int *qe; int n_rec; const float *vp; const int *vfirst, *vtype; int n_vtx; };
+    Raw raw();
 
   private:
-    enum { NEXT_AROUND_LEFT = 0x13, NEXT_AROUND_RIGHT = 0x31, PREV_AROUND_ORG = 0x11, PREV_AROUND_DST = 0x33 };
-    struct alignas(32) QE { int next[4]; int pt[4]; };
+    struct Rec { int on[2], op[2], org[2], link, pad; };   // d = 0: e = 4q, d = 1: Sym e = 4q + 2
     struct V2f { float x, y; };
     struct V2d { double x, y, n2, pad; };
+    std::vector<Rec> rec;
     std::vector<V2f> vp;
-    std::vector<V2d> vd;   // exact double copies of vp plus x*x + y*y, for the flip-loop predicates
+    std::vector<V2d> vd;   // exact double copies of vp plus x*x + y*y, for the predicates
     std::vector<int> vfirst, vtype;   // type: -1 free, 0 real, 1 virtual
-    std::vector<QE> qe;
+    std::vector<int> qx;              // export buffer (Raw::qe)
     int free_q = 0, free_p = 0, recent = 0;
     float tlx = 0, tly = 0, brx = 0, bry = 0;
 
-    int next_e(int e) const { return qe[e >> 2].next[e & 3]; }
-    static int rot(int e, int r) { return (e & ~3) + ((e + r) & 3); }
-    int get_e(int e, int t) const { e = qe[e >> 2].next[(e + t) & 3]; return (e & ~3) + ((e + (t >> 4)) & 3); }
-    int org(int e) const { return qe[e >> 2].pt[e & 3]; }
-    int dst(int e) const { return qe[e >> 2].pt[(e + 2) & 3]; }
+    static int sym(int e) { return e ^ 2; }
+    static int dir(int e) { return (e >> 1) & 1; }
+    int &on(int e) { return rec[e >> 2].on[dir(e)]; }
+    int &op(int e) { return rec[e >> 2].op[dir(e)]; }
+    int onext(int e) const { return rec[e >> 2].on[dir(e)]; }
+    int oprev(int e) const { return rec[e >> 2].op[dir(e)]; }
+    int org(int e) const { return rec[e >> 2].org[dir(e)]; }
+    int dst(int e) const { return rec[e >> 2].org[dir(e) ^ 1]; }
+    int lnext(int e) const { return oprev(sym(e)); }          // NEXT_AROUND_LEFT
+    int dprev(int e) const { return sym(oprev(sym(e))); }     // PREV_AROUND_DST
+    int lprev(int e) const { return sym(onext(e)); }          // PREV_AROUND_LEFT
     int right_of(float px, float py, int e) const;
     int new_edge();
     int new_point(float x, float y, int type);
-    void splice(int a, int b);
+    void splice(int a, int b) {
+        const int an = on(a), bn = on(b);
+        on(a) = bn; on(b) = an;
+        op(bn) = a; op(an) = b;
+    }
     void set_pts(int e, int o, int d);
     int connect(int a, int b);
     void swap_edge(int e);
     void delete_edge(int e);
     int locate(float px, float py, int &edge, int &vertex);
-    void calc_voronoi();
 };
 
 }  // namespace aos
