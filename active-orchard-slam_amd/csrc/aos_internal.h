@@ -74,7 +74,7 @@ struct FrameGeom {
 };
 
 // ------------------------------------------------------------------ kernels (launchers)
-constexpr int kRorCounters = 256;   // spread n_clipped counter slots (k_ror_tile)
+constexpr int kRorCounters = 256;   // spread n_clipped counter slots (k_ror_sweep)
 struct RorLaunch {
     const uint8_t *cloud; uint64_t n; uint32_t step, ox, oy, oz; int is_dense;
     float bminx, bminy, bminz, bmaxx, bmaxy, bmaxz, inv_cs; int nbx, nby;

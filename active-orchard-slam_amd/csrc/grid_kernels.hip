@@ -96,34 +96,14 @@ __global__ void k_ror_scatter(RorLaunch L, const int *bin_start, const int2 *pt_
 //   !dense: radius search d2 < float(r^2), keep iff count >= need.
 // Kept candidates mark their cell (generateOccupancyGrid seed_gen:606-619: double divide, trunc).
 //
-// LDS-staged bins: one workgroup per strip of kSW bins of one bin row. The strip's 3 x (kSW + 2)
-// neighbourhood bins are 3 contiguous ranges of the bin-sorted point array; they are copied into
-// LDS with coalesced loads (~500 points = 8 KB on orchard clouds), then each candidate of the strip
-// counts its neighbours from LDS. A strip whose neighbourhood exceeds kRorCap points reads the
-// same ranges from global memory instead. The keep decision only needs "at least need points
-// within r", so the scan order is free (own bin row first) and stops early.
-#ifndef AOS_ROR_CAP
-#define AOS_ROR_CAP 2048
-#endif
+// The keep decision only needs "at least need points within r", so the scan order is free (own
+// bin row first) and stops early.
 #ifndef AOS_ROR_NOSCAN   // timing experiments only (tools/ab_variants.sh): wrong results
 #define AOS_ROR_NOSCAN 0
 #endif
 #ifndef AOS_ROR_NOSTORE
 #define AOS_ROR_NOSTORE 0
 #endif
-#ifndef AOS_ROR_XCD
-#define AOS_ROR_XCD 1
-#endif
-#ifndef AOS_ROR_SWEEP
-#define AOS_ROR_SWEEP 1
-#endif
-#ifndef AOS_ROR_SW
-#define AOS_ROR_SW 64
-#endif
-#ifndef AOS_ROR_TB
-#define AOS_ROR_TB 256
-#endif
-constexpr int kSW = AOS_ROR_SW, kRorCap = AOS_ROR_CAP, kRorTB = AOS_ROR_TB;
 
 // XCD-aware block order (cdna_hip_programming.md §5.5 T1): blocks b = j (mod 8) share an XCD's L2,
 // so group j gets one contiguous range of logical blocks (neighbouring bin rows stay on one L2).
@@ -163,73 +143,9 @@ __device__ __forceinline__ int ror_scan_lds(const RorLaunch &L, float4 p, const 
     return cnt;
 }
 
-__global__ __launch_bounds__(kRorTB) void k_ror_tile(RorLaunch L, const int *bin_start, const float4 *sorted,
-                                                     uint8_t *raster, unsigned long long *counters) {
-    __shared__ float4 pts[kRorCap];
-    __shared__ int offs[3][kSW + 3];   // global offsets of bins xlo .. xhi + 1 in rows by-1, by, by+1
-    __shared__ int base[4];
-    const int nstrip = (L.nbx + kSW - 1) / kSW;
-    const int blk = AOS_ROR_XCD ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
-    const int by = blk / nstrip, bx0 = (blk - by * nstrip) * kSW;
-    const int bx1 = min(bx0 + kSW, L.nbx);                        // own bins [bx0, bx1)
-    const int xlo = max(bx0 - 1, 0), xhi = min(bx1, L.nbx - 1);  // neighbourhood bins, inclusive
-    const int nbins = xhi - xlo + 1;
-    for (int t = threadIdx.x; t < 3 * (nbins + 1); t += kRorTB) {
-        const int r = t / (nbins + 1), c = t - r * (nbins + 1), yy = by - 1 + r;
-        offs[r][c] = (yy >= 0 && yy < L.nby) ? bin_start[yy * L.nbx + xlo + c] : 0;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        base[0] = 0;
-        base[1] = offs[0][nbins] - offs[0][0];
-        base[2] = base[1] + offs[1][nbins] - offs[1][0];
-        base[3] = base[2] + offs[2][nbins] - offs[2][0];
-    }
-    __syncthreads();
-    const int own0 = offs[1][bx0 - xlo], own1 = offs[1][bx1 - xlo];
-    if (own0 == own1) return;   // uniform across the workgroup
-    const int total = base[3];
-    const bool fits = total <= kRorCap;
-    if (fits) {
-        for (int t = threadIdx.x; t < total; t += kRorTB) {
-            const int r = t < base[1] ? 0 : (t < base[2] ? 1 : 2);
-            pts[t] = sorted[offs[r][0] + (t - base[r])];
-        }
-        __syncthreads();
-    }
-    unsigned kept_n = 0;
-    for (int k = own0 + threadIdx.x; k < own1; k += kRorTB) {
-        const float4 p = fits ? pts[base[1] + (k - offs[1][0])] : sorted[k];
-        if (__float_as_int(p.w) == 0) continue;   // not a clip candidate
-        int bx, byy;
-        bin_of(L, p.x, p.y, bx, byy);
-        const int c0 = max(bx - 1, xlo) - xlo, c1 = min(bx + 1, xhi) - xlo + 1;
-        int cnt = AOS_ROR_NOSCAN ? L.need : 0;
-#pragma unroll
-        for (int rr = 0; rr < 3; ++rr) {
-            const int r = rr == 0 ? 1 : (rr == 1 ? 0 : 2);   // own bin row first
-            const int yy = by - 1 + r;
-            if (yy < 0 || yy >= L.nby || cnt >= L.need) continue;
-            const int g0 = offs[r][c0], g1 = offs[r][c1];
-            if (fits) cnt = ror_scan(L, p, pts, base[r] + (g0 - offs[r][0]), base[r] + (g1 - offs[r][0]), cnt);
-            else cnt = ror_scan(L, p, sorted, g0, g1, cnt);
-        }
-        if (cnt >= L.need) {
-            ++kept_n;
-            int gx = (int)(((double)p.x - L.origin_x) / (double)L.res);
-            int gy = (int)(((double)p.y - L.origin_y) / (double)L.res);
-            if (!AOS_ROR_NOSTORE && gx >= 0 && gx < L.W && gy >= 0 && gy < L.H) raster[(size_t)gy * L.W + gx] = 1;
-        }
-    }
-    // stats: candidates that survived ROR (n_clipped). Wave-aggregated, then spread over
-    // kRorCounters slots: one hot address would serialise ~10^5 same-address atomics in one L2
-    // channel (it used to bound this kernel at ~0.9 ms). The host sums the slots.
-    for (int o = 32; o > 0; o >>= 1) kept_n += __shfl_xor(kept_n, o);
-    if ((threadIdx.x & 63) == 0 && kept_n)
-        atomicAdd(&counters[(blk * (kRorTB / 64) + (threadIdx.x >> 6)) & (kRorCounters - 1)], (unsigned long long)kept_n);
-}
-
-// Row-sweep variant: one workgroup per (strip of kSwSW bins) x (segment of kSwSeg bin rows). It keeps
+// LDS-staged bins, row sweep: one workgroup per (strip of kSwSW bins) x (segment of kSwSeg bin rows).
+// A candidate's neighbours lie in 3 x 3 bins; the bins of one row of a strip (plus one bin on each
+// side) are one contiguous range of the bin-sorted point array, copied into LDS coalesced. It keeps
 // a ring of 4 staged point rows (y-1, y, y+1 and y+2 in flight) and 5 rows of bin offsets in LDS.
 // While it scans row y it has already issued the loads of row y+2's points and row y+3's offsets
 // into registers, so each step costs ~max(scan, one load latency) instead of a 3-trip chain per
@@ -326,7 +242,8 @@ __global__ __launch_bounds__(kSwTB) void k_ror_sweep(RorLaunch L, const int *bin
     }
     for (int o = 32; o > 0; o >>= 1) kept_n += __shfl_xor(kept_n, o);
     if ((tid & 63) == 0 && kept_n)
-        atomicAdd(&counters[(blk * (kSwTB / 64) + (tid >> 6)) & (kRorCounters - 1)], (unsigned long long)kept_n);
+        atomicAdd(&counters[(blk * (kSwTB / 64) + (tid >> 6)) & (kRorCounters - 1)], (unsigned long long)kept_n);   // spread: one
+    // hot address would serialise ~10^5 same-address atomics in one L2 channel
 }
 
 void launch_ror_bin(const RorLaunch &L, int *bin_count, int2 *pt_binslot, hipStream_t s) {
@@ -339,17 +256,11 @@ void launch_ror_scatter(const RorLaunch &L, const int *bin_start, const int2 *pt
 }
 void launch_ror_raster(const RorLaunch &L, const int *bin_start, const float4 *sorted, uint8_t *raster,
                        unsigned long long *counters, hipStream_t s) {
-#if AOS_ROR_SWEEP
     const long long nblk = (long long)((L.nby + kSwSeg - 1) / kSwSeg) * ((L.nbx + kSwSW - 1) / kSwSW);
     if (nblk <= 0) return;
     if (nblk > INT_MAX) throw std::runtime_error("ROR bin grid too large");
     k_ror_sweep<<<(int)nblk, kSwTB, 0, s>>>(L, bin_start, sorted, raster, counters);
-#else
-    const long long nblk = (long long)L.nby * ((L.nbx + kSW - 1) / kSW);
-    if (nblk <= 0) return;
-    if (nblk > INT_MAX) throw std::runtime_error("ROR bin grid too large");
-    k_ror_tile<<<(int)nblk, kRorTB, 0, s>>>(L, bin_start, sorted, raster, counters);
-#endif
+
 }
 
 size_t scan_temp_bytes(int n) {

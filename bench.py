@@ -24,7 +24,7 @@ for sub in ("tools", "active-orchard-slam_amd"):
     sys.path.insert(0, os.path.join(ROOT, sub))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-DOMINANT = "k_ror_tile"
+DOMINANT = "k_ror_sweep"
 PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
 
 
@@ -155,7 +155,7 @@ def main():
     avg = {k: v / len(res) for k, v in stage.items()}
 
     # roofline of the dominant GPU kernel (largest share of device time per frame in the committed
-    # rocprofv3 summary): k_ror_tile, the ROR neighbour count + raster over LDS-staged bins.
+    # rocprofv3 summary): k_ror_sweep, the ROR neighbour count + raster over LDS-staged bin rows.
     # Algorithmic bytes per launch: each staged point record read once (float4, 16 B)
     # + one raster byte per kept candidate. Timed live: HIP events around that single launch on the
     # handle's stream (aos_seedgen_out.ms_ror_count), averaged over the timed steps.

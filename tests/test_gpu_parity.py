@@ -234,3 +234,51 @@ def test_against_golden_hashes(name):
                   ("node_label_counts", np.int32), ("node_label_clusters", np.int32), ("node_label_types", np.int32)):
         assert sha(gg[k], dt) == hs["gvd"][k], k
     c.close()
+
+
+# ---------------------------------------------------------------- paths the orchard scenes rarely hit
+def _full_frame_parity(cloud, poly, res, **kw):
+    c = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=res))
+    c.set_polygon(poly)
+    g = c.seedgen(cloud, **kw)
+    o = O.seedgen(cloud, poly, O.default_params(grid_resolution=res), is_dense=kw.get("is_dense", True))
+    assert_seedgen_parity(g, o)
+    assert_gvd_parity(c.gvd_from_seedgen(), O.gvd(o["voronoi_seeds"], o["rows_info"], o))
+    c.close()
+    return g
+
+
+def test_dense_patches_overflow_the_lds_row_ring():
+    """Bin rows with more than 512 staged points are scanned from global memory (k_ror_sweep)."""
+    cfg = orchard.CONFIGS["C0"]
+    base = orchard.generate(cfg)
+    rng = np.random.default_rng(11)
+    extra = []
+    for cx, cy in ((20.0, 2.0), (40.3, 5.5), (71.9, 12.5), (10.0, 30.0)):   # on rows and between them
+        n = 4000
+        p = np.zeros((n, 4), np.float32)
+        p[:, 0] = cx + rng.uniform(-0.25, 0.25, n)
+        p[:, 1] = cy + rng.uniform(-0.25, 0.25, n)
+        p[:, 2] = rng.uniform(-0.3, 0.4, n)
+        extra.append(p)
+    cloud = np.concatenate([base.view(np.float32).reshape(-1, 4)] + extra).view(np.uint8).reshape(-1, 16)
+    _full_frame_parity(cloud, orchard.polygon(cfg), cfg.res)
+
+
+def test_rotated_orchard_concave_polygon_and_odd_resolution():
+    """Rows at 30 degrees, an L-shaped exploration polygon, 0.15 m cells (R = 5)."""
+    cfg = orchard.CONFIGS["C0"]
+    cloud = orchard.generate(cfg, n_points=80000).copy()
+    f = cloud.view(np.float32).reshape(-1, 4)
+    a = np.deg2rad(30.0)
+    x, y = f[:, 0].astype(np.float64) - 50.0, f[:, 1].astype(np.float64) - 10.0
+    f[:, 0] = (x * np.cos(a) - y * np.sin(a) + 50.0).astype(np.float32)
+    f[:, 1] = (x * np.sin(a) + y * np.cos(a) + 30.0).astype(np.float32)
+    poly = np.array([[5.0, 5.0], [95.0, 5.0], [95.0, 40.0], [55.0, 40.0], [55.0, 75.0], [5.0, 75.0]])
+    g = _full_frame_parity(cloud, poly, 0.15)
+    assert len(g["row_length"]) > 0
+
+
+def test_grid_resolution_0_3_and_non_dense():
+    cfg = orchard.CONFIGS["C0"]
+    _full_frame_parity(orchard.generate(cfg, n_points=70000), orchard.polygon(cfg), 0.3, is_dense=False)
