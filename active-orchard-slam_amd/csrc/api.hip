@@ -33,6 +33,20 @@ using namespace aos;
         return AOS_E_STATE;                                                                                   \
     }
 
+// Makes the handle's device current for one ABI call and restores the caller's device afterwards
+// (a multi-GPU caller, e.g. torch with one device per thread, keeps its own current device).
+struct DeviceScope {
+    int prev = -1;
+    explicit DeviceScope(int d) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != d) (void)hipSetDevice(d);   // a failure surfaces in the next HIP call
+    }
+    ~DeviceScope() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
 extern "C" {
 
 const char *aos_last_error(void) { return g_err.c_str(); }
@@ -69,7 +83,7 @@ int aos_create(const aos_params *p, int device, aos_ctx **out) {
     auto *c = new aos_ctx();
     c->P = *p;
     c->device = device;
-    AOS_HIP(hipSetDevice(device));
+    DeviceScope dev_scope(device);
     AOS_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (auto &e : c->ev) AOS_HIP(hipEventCreate(&e));
     // hard-coded default polygon of the reference constructor (seed_gen:196-199)
@@ -82,7 +96,7 @@ int aos_create(const aos_params *p, int device, aos_ctx **out) {
 
 void aos_destroy(aos_ctx *c) {
     if (!c) return;
-    (void)hipSetDevice(c->device);
+    DeviceScope dev_scope(c->device);
     (void)hipStreamSynchronize(c->stream);
     c->release();
     for (auto &e : c->ev) (void)hipEventDestroy(e);
@@ -109,7 +123,7 @@ int aos_seedgen_process(aos_ctx *c, const aos_cloud_view *cloud, int want_host, 
         return AOS_E_INVALID;
     }
     AOS_GUARD_BEGIN
-    AOS_HIP(hipSetDevice(c->device));
+    DeviceScope dev_scope(c->device);
     c->set_cloud(*cloud);
     c->run_seedgen(want_host != 0, *out);
     return AOS_OK;
@@ -120,7 +134,7 @@ int aos_seedgen_reprocess(aos_ctx *c, int want_host, aos_seedgen_out *out) {
     if (!c || !out) { set_error("aos_seedgen_reprocess: null argument"); return AOS_E_INVALID; }
     if (!c->have_cloud) { std::memset(out, 0, sizeof(*out)); return AOS_OK; }  // last_cloud empty (:283)
     AOS_GUARD_BEGIN
-    AOS_HIP(hipSetDevice(c->device));
+    DeviceScope dev_scope(c->device);
     c->run_seedgen(want_host != 0, *out);
     return AOS_OK;
     AOS_GUARD_END
@@ -129,7 +143,7 @@ int aos_seedgen_reprocess(aos_ctx *c, int want_host, aos_seedgen_out *out) {
 int aos_gvd_process(aos_ctx *c, const aos_gvd_in *in, aos_gvd_out *out) {
     if (!c || !in || !out) { set_error("aos_gvd_process: null argument"); return AOS_E_INVALID; }
     AOS_GUARD_BEGIN
-    AOS_HIP(hipSetDevice(c->device));
+    DeviceScope dev_scope(c->device);
     c->run_gvd_external(*in, *out);
     return AOS_OK;
     AOS_GUARD_END
@@ -139,7 +153,7 @@ int aos_gvd_from_seedgen(aos_ctx *c, aos_gvd_out *out) {
     if (!c || !out) { set_error("aos_gvd_from_seedgen: null argument"); return AOS_E_INVALID; }
     if (!c->have_frame) { set_error("aos_gvd_from_seedgen: no seed-gen frame yet"); return AOS_E_STATE; }
     AOS_GUARD_BEGIN
-    AOS_HIP(hipSetDevice(c->device));
+    DeviceScope dev_scope(c->device);
     c->run_gvd_from_frame(*out);
     return AOS_OK;
     AOS_GUARD_END
@@ -149,7 +163,7 @@ int aos_debug_grid(aos_ctx *c, const char *which, int8_t *dst, uint64_t capacity
     if (!c || !which || !dst) { set_error("aos_debug_grid: null argument"); return AOS_E_INVALID; }
     if (!c->have_frame) { set_error("aos_debug_grid: no frame"); return AOS_E_STATE; }
     AOS_GUARD_BEGIN
-    AOS_HIP(hipSetDevice(c->device));
+    DeviceScope dev_scope(c->device);
     return c->debug_grid(which, dst, capacity);
     AOS_GUARD_END
 }

@@ -124,17 +124,25 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # AOS_BENCH_BACKEND=gloo rehearses the N > 1 flow on fewer GPUs than ranks (ranks share devices;
+    # the timing all-reduce runs on the host). The default, and the driver's run, is RCCL.
+    backend = os.environ.get("AOS_BENCH_BACKEND", "nccl")
+    gpu = local % torch.cuda.device_count() if backend == "gloo" else local
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    red_dev = dev if backend == "nccl" else torch.device("cpu")
 
     cfg = orchard.CONFIGS[a.config]
     cloud = orchard.generate(cfg, seed=cfg.seed + rank)
     poly = orchard.polygon(cfg)
     d_cloud = torch.from_numpy(cloud).to(dev)
     n = cloud.shape[0]
-    ctx = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res), device=local)
+    ctx = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res), device=gpu)
     ctx.set_polygon(poly)
 
     def step():
@@ -142,7 +150,7 @@ def main():
         gg = ctx.gvd_from_seedgen()
         return g, gg
 
-    dt, res = timed_region(step, a.steps, a.warmup, world, torch.cuda.synchronize, dist, dev)
+    dt, res = timed_region(step, a.steps, a.warmup, world, torch.cuda.synchronize, dist, red_dev)
     g, gg = res[-1]
     stage = {}
     for gs, ggs in res:

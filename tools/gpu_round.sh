@@ -16,6 +16,11 @@ tail -1 gpurun_out/smoke.log
 echo "[gpu_round] bench"
 timeout -k 10 400 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1 || { tail -20 gpurun_out/bench.log; exit 1; }
 grep '^{' gpurun_out/bench.log
+if [ "${DIST:-0}" = "1" ]; then
+echo "[gpu_round] 2-rank rehearsal of the --gpus N flow (gloo timing reduction, ranks share the GPU)"
+AOS_BENCH_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/bench_dist.log 2>&1 || { tail -30 gpurun_out/bench_dist.log; exit 1; }
+grep '^{' gpurun_out/bench_dist.log | cut -c1-400
+fi
 echo "[gpu_round] rocprofv3 kernel trace"
 rm -rf gpurun_out/prof_kt gpurun_out/prof_fetch gpurun_out/prof_write
 cd /tmp
