@@ -67,6 +67,22 @@ class GvdOut(ctypes.Structure):
                 ("ms_total", c_f)]
 
 
+AllGatherFn = ctypes.CFUNCTYPE(c_i, c_vp, c_u64)
+AllReduceMaxFn = ctypes.CFUNCTYPE(c_i, c_vp, P(c_i), c_i)
+
+
+class Comm(ctypes.Structure):
+    _fields_ = [("user", c_vp), ("rank", c_i), ("world", c_i), ("send_buf", c_vp), ("recv_buf", c_vp),
+                ("buf_bytes", c_u64), ("all_gather", AllGatherFn), ("all_reduce_max", AllReduceMaxFn)]
+
+
+class TilePlan(ctypes.Structure):
+    _fields_ = [("tiles_x", c_i), ("tiles_y", c_i), ("rank", c_i), ("tile_x", c_i), ("tile_y", c_i),
+                ("halo_rows", c_i), ("halo_words", c_i), ("row0", c_i), ("row1", c_i), ("word0", c_i),
+                ("word1", c_i), ("win_row0", c_i), ("win_row1", c_i), ("win_word0", c_i), ("win_word1", c_i),
+                ("points_box", c_d * 4), ("exchange_bytes", c_u64), ("info", GridInfo)]
+
+
 def build() -> str:
     subprocess.check_call(["make", "-s", "-C", HERE, "-j8"])
     return LIB_PATH
@@ -104,6 +120,8 @@ def lib():
         L.aos_gvd_process.argtypes = [c_vp, P(GvdIn), P(GvdOut)]
         L.aos_gvd_from_seedgen.argtypes = [c_vp, P(GvdOut)]
         L.aos_debug_grid.argtypes = [c_vp, ctypes.c_char_p, c_vp, c_u64]
+        L.aos_tile_plan_compute.argtypes = [P(Params), c_vp, c_u, c_i, c_i, c_i, P(TilePlan)]
+        L.aos_tiled_seedgen_process.argtypes = [c_vp, P(Comm), c_i, c_i, c_i, P(CloudView), c_i, P(SeedGenOut)]
         L.aos_stream.restype = c_vp
         L.aos_stream.argtypes = [c_vp]
         _lib = L
@@ -200,20 +218,43 @@ class Ctx:
         a = np.ascontiguousarray(poly_xy, dtype=np.float64).reshape(-1)
         _check(lib().aos_set_polygon(self.h, a.ctypes.data, a.size // 2))
 
-    def seedgen(self, cloud, n_points: int | None = None, point_step=16, offs=(0, 4, 8), is_dense=True,
-                on_device=False, want_host=True) -> dict:
-        """cloud: (n, point_step) uint8 numpy array, or an int device pointer with on_device=True."""
+    @staticmethod
+    def _view(cloud, n_points, point_step, offs, is_dense, on_device):
+        """(CloudView, keep-alive): cloud is a (n, point_step) uint8 array or, with on_device, a device pointer."""
         if on_device:
-            ptr = int(cloud)
-            n = int(n_points)
+            ptr, n = int(cloud), int(n_points)
         else:
             cloud = np.ascontiguousarray(cloud)
             ptr = cloud.ctypes.data
             n = cloud.shape[0] if cloud.ndim == 2 else cloud.size // point_step
-        v = CloudView(ptr, n, point_step, offs[0], offs[1], offs[2], int(is_dense), int(on_device))
+        return CloudView(ptr, n, point_step, offs[0], offs[1], offs[2], int(is_dense), int(on_device)), cloud
+
+    def seedgen(self, cloud, n_points: int | None = None, point_step=16, offs=(0, 4, 8), is_dense=True,
+                on_device=False, want_host=True) -> dict:
+        """cloud: (n, point_step) uint8 numpy array, or an int device pointer with on_device=True."""
+        v, _keep = self._view(cloud, n_points, point_step, offs, is_dense, on_device)
         o = SeedGenOut()
         _check(lib().aos_seedgen_process(self.h, ctypes.byref(v), int(want_host), ctypes.byref(o)))
         return _seedgen_dict(o, want_host)
+
+    def tiled_seedgen(self, comm, tiles_x: int, tiles_y: int, cloud, root: int = 0, n_points: int | None = None,
+                      point_step=16, offs=(0, 4, 8), is_dense=True, on_device=False, want_host=True) -> dict:
+        """One tiled frame on this rank (aos_tiled_seedgen_process); comm: a TorchDistComm / ThreadGroup comm.
+        The root gets the whole frame; other ranks get the map info, T, n_clipped and their timings."""
+        v, _keep = self._view(cloud, n_points, point_step, offs, is_dense, on_device)
+        o = SeedGenOut()
+        comm.error = None
+        rc = lib().aos_tiled_seedgen_process(self.h, ctypes.byref(comm.c), tiles_x, tiles_y, root, ctypes.byref(v),
+                                             int(want_host), ctypes.byref(o))
+        if comm.error is not None:
+            raise RuntimeError(f"communicator failed: {comm.error!r}") from comm.error
+        _check(rc)
+        if comm.rank == root:
+            return {**_seedgen_dict(o, want_host), "root": True}
+        return {"root": False, "width": o.info.width, "height": o.info.height, "thin_iters": o.thin_iters,
+                "n_clipped": o.n_clipped, "n_input": o.n_input, "n_binned": o.n_binned,
+                "ms": {"ror": o.ms_ror, "grid": o.ms_grid, "thin": o.ms_thin, "total": o.ms_total,
+                       "ror_count": o.ms_ror_count}}
 
     def reprocess(self, want_host=True) -> dict:
         o = SeedGenOut()

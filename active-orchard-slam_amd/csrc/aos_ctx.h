@@ -23,9 +23,11 @@ struct aos_ctx {
     // ---- device buffers
     aos::DevBuf cloud_copy, bin_count, bin_start, pt_binslot, sorted, scan_tmp, counters;
     aos::DevBuf raster_bytes, raster_bits, infl_bits, open_bits, thin_a, thin_b, occ_bytes, skel_bytes, flags;
+    aos::DevBuf full_infl, full_skel;      // tiled frames: the whole map, assembled on the root rank
     aos::PinnedBuf h_small, h_stats;
-    const uint64_t *skel_bits = nullptr;   // final thinning buffer (thin_a or thin_b)
-    aos::FrameGeom geom{};
+    const uint64_t *skel_bits = nullptr;   // final thinning buffer (thin_a / thin_b, or full_skel)
+    aos::FrameGeom geom{};                 // the whole map
+    bool tiled_frame = false;
     int thin_iters = 0;
     uint64_t n_ror_kept = 0, n_clipped = 0;
 
@@ -40,8 +42,16 @@ struct aos_ctx {
     // ---- GVD (gvd.hip)
     aos::GvdState gs;
 
+    // Cells a frame rasterises / counts: [rx0, rx1) x [ry0, ry1) (clamped cell), stored into the
+    // Wr x Hr byte window at cell (wx0, wy0); limit_box: bin only points in box (a tile's shard).
+    struct RorOwn { int rx0, ry0, rx1, ry1, wx0, wy0, Wr, Hr; bool limit_box; float box[4]; };
+
     void set_cloud(const aos_cloud_view &v);
+    void ror_stage(const aos::FrameGeom &g, const RorOwn &o);
+    void finish_frame(const aos::FrameGeom &g, bool want_host, const uint64_t *clipped_total, aos_seedgen_out &out);
     void run_seedgen(bool want_host, aos_seedgen_out &out);
+    void run_tiled(const aos_comm &cm, int tiles_x, int tiles_y, int root, bool want_host, aos_seedgen_out &out);
+    void tile_halo_exchange(uint64_t *win, const aos::TilePlan &t, const aos_comm &cm);
     void run_gvd_external(const aos_gvd_in &in, aos_gvd_out &out);
     void run_gvd_from_frame(aos_gvd_out &out);
     int debug_grid(const char *which, int8_t *dst, uint64_t capacity);

@@ -81,6 +81,10 @@ struct RorLaunch {
     float cminx, cmaxx, cminy, cmaxy, cminz, cmaxz;
     double r2; float r2f; int need;
     double origin_x, origin_y; float res; int W, H;
+    // Ownership (tiled frames, tiled.hip): a kept candidate is counted iff its cell, clamped to the
+    // grid, lies in [rx0, rx1) x [ry0, ry1); it is rastered (if inside the grid) into the byte window
+    // whose cell (wx0, wy0) is element 0, row pitch Wr. Single-GPU frames own the whole grid.
+    int rx0, ry0, rx1, ry1, wx0, wy0, Wr;
 };
 void launch_ror_bin(const RorLaunch &L, int *bin_count, int2 *pt_binslot, hipStream_t s);
 void launch_ror_scatter(const RorLaunch &L, const int *bin_start, const int2 *pt_binslot, float4 *sorted, hipStream_t s);
@@ -93,9 +97,37 @@ void launch_open(const uint64_t *in, uint64_t *out, const FrameGeom &g, hipStrea
 // Zhang-Suen temporal block: KIT iterations per launch; flags[0] = non-empty after iteration 1,
 // flags[1 + k] = iteration k (0-based) deleted something.
 constexpr int kThinItersPerLaunch = 8;
-void launch_thin_block(const uint64_t *in, uint64_t *out, const FrameGeom &g, int base_iter, int *flags, hipStream_t s);
+// Cells whose deletions a launch reports in flags (rows [y0, y1), words [c0, c1) of the image it is
+// given: a tile's own cells inside its halo window), and whether a launch may skip itself once an
+// earlier iteration deleted nothing (single GPU only: a tile must keep pace with its neighbours).
+struct ThinOwn { int y0, y1, c0, c1, early_exit; };
+void launch_thin_block(const uint64_t *in, uint64_t *out, const FrameGeom &g, int base_iter, int *flags,
+                       const ThinOwn &own, hipStream_t s);
 void launch_draw_rect(int8_t *grid, const FrameGeom &g, int gx0, int gy0, int gx1, int gy1, hipStream_t s);
 size_t scan_temp_bytes(int n);
 void launch_exclusive_scan(const int *in, int *out, int n, void *temp, size_t temp_bytes, hipStream_t s);
+
+// ------------------------------------------------------------------ frame helpers (seedgen.hip)
+FrameGeom frame_geom(const Poly &poly, const aos_params &P);
+float ror_margin(const aos_params &P);
+Poly default_polygon();
+int thin_iterations(const int *flags, int iters_run);
+
+// ------------------------------------------------------------------ tiled frames (tiled.hip)
+struct CommError { std::string what; };
+constexpr int kMaxTiles = 16;   // per dimension
+struct TilePlan {
+    int tiles_x, tiles_y, rank, tx, ty;
+    int G, gw;                  // halo depth: G rows / gw = G / 64 words
+    int hy, hw;                 // halo in use: 0 along an untiled dimension
+    int rs[kMaxTiles + 1], cs[kMaxTiles + 1];   // first row / word of each tile row / column
+    int y0, y1, c0, c1;         // own rows / words
+    int wy0, wy1, wc0, wc1;     // halo window, clamped to the map
+    FrameGeom lg;               // the window as an image (W, H, WW; R of the map)
+    long long max_border, max_own;   // words per rank: border strips / own tile, max over tiles
+    float box[4];               // x/y box of the points this rank needs (xmin, ymin, xmax, ymax)
+    uint64_t exchange_bytes;    // per-rank all-gather chunk
+};
+TilePlan make_tile_plan(const FrameGeom &g, float margin, int tiles_x, int tiles_y, int rank);
 
 }  // namespace aos

@@ -28,6 +28,14 @@ using namespace aos;
         set_error("out of host memory");                                                                      \
         return AOS_E_NOMEM;                                                                                   \
     }                                                                                                         \
+    catch (const CommError &e) {                                                                              \
+        set_error("communicator error: " + e.what);                                                           \
+        return AOS_E_RCCL;                                                                                    \
+    }                                                                                                         \
+    catch (const std::invalid_argument &e) {                                                                  \
+        set_error(std::string("invalid argument: ") + e.what());                                              \
+        return AOS_E_INVALID;                                                                                 \
+    }                                                                                                         \
     catch (const std::exception &e) {                                                                         \
         set_error(std::string("error: ") + e.what());                                                         \
         return AOS_E_STATE;                                                                                   \
@@ -86,9 +94,7 @@ int aos_create(const aos_params *p, int device, aos_ctx **out) {
     DeviceScope dev_scope(device);
     AOS_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (auto &e : c->ev) AOS_HIP(hipEventCreate(&e));
-    // hard-coded default polygon of the reference constructor (seed_gen:196-199)
-    c->poly = {{-1.972916603088379, 7.9420671463012695}, {-2.0726776123046875, 0.022441387176513672},
-               {70.22465515136719, 2.102720260620117}, {69.48777770996094, 9.786612510681152}};
+    c->poly = default_polygon();
     *out = c;
     return AOS_OK;
     AOS_GUARD_END
@@ -114,11 +120,16 @@ int aos_set_polygon(aos_ctx *c, const double *xy, uint32_t n) {
     return AOS_OK;
 }
 
+static bool cloud_layout_ok(const aos_cloud_view *cloud) {
+    if (!cloud->n_points) return true;
+    return cloud->data && cloud->point_step >= 12 && !(cloud->point_step & 3) && !(cloud->off_x & 3) &&
+           !(cloud->off_y & 3) && !(cloud->off_z & 3) && cloud->off_x + 4 <= cloud->point_step &&
+           cloud->off_y + 4 <= cloud->point_step && cloud->off_z + 4 <= cloud->point_step;
+}
+
 int aos_seedgen_process(aos_ctx *c, const aos_cloud_view *cloud, int want_host, aos_seedgen_out *out) {
     if (!c || !cloud || !out) { set_error("aos_seedgen_process: null argument"); return AOS_E_INVALID; }
-    if (cloud->n_points && (!cloud->data || cloud->point_step < 12 || (cloud->point_step & 3) || (cloud->off_x & 3) ||
-                            (cloud->off_y & 3) || (cloud->off_z & 3) || cloud->off_x + 4 > cloud->point_step ||
-                            cloud->off_y + 4 > cloud->point_step || cloud->off_z + 4 > cloud->point_step)) {
+    if (!cloud_layout_ok(cloud)) {
         set_error("aos_seedgen_process: invalid PointCloud2 layout (float32 x/y/z, 4-byte aligned)");
         return AOS_E_INVALID;
     }
@@ -155,6 +166,44 @@ int aos_gvd_from_seedgen(aos_ctx *c, aos_gvd_out *out) {
     AOS_GUARD_BEGIN
     DeviceScope dev_scope(c->device);
     c->run_gvd_from_frame(*out);
+    return AOS_OK;
+    AOS_GUARD_END
+}
+
+int aos_tile_plan_compute(const aos_params *p, const double *poly_xy, uint32_t n_poly, int32_t tiles_x,
+                          int32_t tiles_y, int32_t rank, aos_tile_plan *out) {
+    if (!p || !out) { set_error("aos_tile_plan_compute: null argument"); return AOS_E_INVALID; }
+    AOS_GUARD_BEGIN
+    Poly poly = default_polygon();
+    if (poly_xy && n_poly >= 3) {
+        poly.clear();
+        for (uint32_t i = 0; i < n_poly; ++i) poly.push_back({poly_xy[2 * i], poly_xy[2 * i + 1]});
+    }
+    const FrameGeom g = frame_geom(poly, *p);
+    const TilePlan t = make_tile_plan(g, ror_margin(*p), tiles_x, tiles_y, rank);
+    std::memset(out, 0, sizeof(*out));
+    out->tiles_x = tiles_x; out->tiles_y = tiles_y; out->rank = rank; out->tile_x = t.tx; out->tile_y = t.ty;
+    out->halo_rows = t.hy; out->halo_words = t.hw;
+    out->row0 = t.y0; out->row1 = t.y1; out->word0 = t.c0; out->word1 = t.c1;
+    out->win_row0 = t.wy0; out->win_row1 = t.wy1; out->win_word0 = t.wc0; out->win_word1 = t.wc1;
+    for (int i = 0; i < 4; ++i) out->points_box[i] = t.box[i];
+    out->exchange_bytes = t.exchange_bytes;
+    out->info = aos_grid_info{g.origin_x, g.origin_y, g.res, (uint32_t)g.W, (uint32_t)g.H};
+    return AOS_OK;
+    AOS_GUARD_END
+}
+
+int aos_tiled_seedgen_process(aos_ctx *c, const aos_comm *comm, int32_t tiles_x, int32_t tiles_y, int32_t root,
+                              const aos_cloud_view *cloud, int want_host, aos_seedgen_out *out) {
+    if (!c || !comm || !cloud || !out) { set_error("aos_tiled_seedgen_process: null argument"); return AOS_E_INVALID; }
+    if (!cloud_layout_ok(cloud)) {
+        set_error("aos_tiled_seedgen_process: invalid PointCloud2 layout (float32 x/y/z, 4-byte aligned)");
+        return AOS_E_INVALID;
+    }
+    AOS_GUARD_BEGIN
+    DeviceScope dev_scope(c->device);
+    c->set_cloud(*cloud);
+    c->run_tiled(*comm, tiles_x, tiles_y, root, want_host != 0, *out);
     return AOS_OK;
     AOS_GUARD_END
 }

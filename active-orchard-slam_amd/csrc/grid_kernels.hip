@@ -216,10 +216,14 @@ __global__ __launch_bounds__(kSwTB) void k_ror_sweep(RorLaunch L, const int *bin
                 else cnt = ror_scan(L, p, sorted, g0, g1, cnt);
             }
             if (cnt >= L.need) {
-                ++kept_n;
                 int gx = (int)(((double)p.x - L.origin_x) / (double)L.res);
                 int gy = (int)(((double)p.y - L.origin_y) / (double)L.res);
-                if (!AOS_ROR_NOSTORE && gx >= 0 && gx < L.W && gy >= 0 && gy < L.H) raster[(size_t)gy * L.W + gx] = 1;
+                const int cx = min(max(gx, 0), L.W - 1), cy = min(max(gy, 0), L.H - 1);
+                if (cx >= L.rx0 && cx < L.rx1 && cy >= L.ry0 && cy < L.ry1) {   // this tile's candidate
+                    ++kept_n;
+                    if (!AOS_ROR_NOSTORE && gx >= 0 && gx < L.W && gy >= 0 && gy < L.H)
+                        raster[(size_t)(gy - L.wy0) * L.Wr + (gx - L.wx0)] = 1;
+                }
             }
         };
         if (staged[scur]) {
@@ -313,8 +317,8 @@ __device__ __forceinline__ uint64_t pad_mask(int c, int WW, int W) {
 // a5 applyInflation (seed_gen:933-967): cell = 100 iff an occupied raster cell lies within the
 // integer disc dx^2 + dy^2 <= R^2 — an exact bounded squared-EDT threshold, computed as an OR
 // of horizontally dilated rows: row y+dy dilated by w(dy) = floor(sqrt(R^2 - dy^2)).
-__constant__ int c_wtab[64];
-__global__ void k_inflate(const uint64_t *in, uint64_t *out, int W, int H, int WW, int R) {
+struct InflTab { int w[64]; };   // w(dy), passed by value: concurrent handles share no device global
+__global__ void k_inflate(const uint64_t *in, uint64_t *out, int W, int H, int WW, int R, InflTab wt) {
     int c = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
     if (c >= WW || y >= H) return;
     uint64_t acc = 0;
@@ -325,7 +329,7 @@ __global__ void k_inflate(const uint64_t *in, uint64_t *out, int W, int H, int W
         uint64_t b = row[c];
         uint64_t a = c > 0 ? row[c - 1] : 0ull;
         uint64_t d = c + 1 < WW ? row[c + 1] : 0ull;
-        int w = c_wtab[dy < 0 ? -dy : dy];
+        int w = wt.w[dy < 0 ? -dy : dy];
         uint64_t h = b;
         for (int s = 1; s <= w; ++s) h |= (b >> s) | (d << (64 - s)) | (b << s) | (a >> (64 - s));
         acc |= h;
@@ -333,15 +337,14 @@ __global__ void k_inflate(const uint64_t *in, uint64_t *out, int W, int H, int W
     out[(size_t)y * WW + c] = acc & pad_mask(c, WW, W);
 }
 void launch_inflate(const uint64_t *in, uint64_t *out, const FrameGeom &g, hipStream_t s) {
-    int wt[64] = {0};
+    InflTab wt{};
     for (int dy = 0; dy <= g.R && dy < 64; ++dy) {
         int w = 0;
         while ((w + 1) * (w + 1) + dy * dy <= g.R * g.R) ++w;
-        wt[dy] = w;
+        wt.w[dy] = w;
     }
-    AOS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_wtab), wt, sizeof(wt), 0, hipMemcpyHostToDevice, s));
     dim3 grid(cdiv(g.WW, 64), g.H);
-    k_inflate<<<grid, 64, 0, s>>>(in, out, g.W, g.H, g.WW, g.R);
+    k_inflate<<<grid, 64, 0, s>>>(in, out, g.W, g.H, g.WW, g.R, wt);
 }
 
 // bits -> int8 {0,100} with an optional `frame`-cell border (markBoundariesAsOccupied, seed_gen:708-757)
@@ -429,8 +432,8 @@ __device__ __forceinline__ uint64_t zs_step(uint64_t n0, uint64_t n1, uint64_t n
 }
 
 __global__ __launch_bounds__(256) void k_thin_block(const uint64_t *__restrict__ in, uint64_t *__restrict__ out,
-                                                    int W, int H, int WW, int base_iter, int *flags) {
-    if (base_iter >= 2 && flags[1 + base_iter - 1] == 0) return;  // converged in an earlier launch
+                                                    int W, int H, int WW, int base_iter, int *flags, ThinOwn own) {
+    if (own.early_exit && base_iter >= 2 && flags[1 + base_iter - 1] == 0) return;  // converged in an earlier launch
     __shared__ uint64_t buf[2][NR][NC];
     __shared__ int chg_shared;
     const int ty0 = blockIdx.y * TH, tc0 = blockIdx.x * TWW;
@@ -448,10 +451,13 @@ __global__ __launch_bounds__(256) void k_thin_block(const uint64_t *__restrict__
         const int sub = s & 1;
         for (int idx = threadIdx.x; idx < NR * NC; idx += blockDim.x) {
             int r = idx / NC, k = idx - r * NC;
+            const int gy = ty0 - HR + r, gc = tc0 - 1 + k;
+            // cells this launch reports: its tile interior, within the caller's own rectangle
+            const bool mine = r >= HR && r < HR + TH && k >= 1 && k <= TWW && gy >= own.y0 && gy < own.y1 &&
+                              gc >= own.c0 && gc < own.c1;
             uint64_t c1 = buf[cur][r][k];
             uint64_t nw = c1;
             if (r > 0 && r < NR - 1) {
-                int gy = ty0 - HR + r, gc = tc0 - 1 + k;
                 uint64_t c0 = k > 0 ? buf[cur][r][k - 1] : 0ull, c2 = k < NC - 1 ? buf[cur][r][k + 1] : 0ull;
                 uint64_t n0 = k > 0 ? buf[cur][r - 1][k - 1] : 0ull, n1 = buf[cur][r - 1][k],
                          n2 = k < NC - 1 ? buf[cur][r - 1][k + 1] : 0ull;
@@ -466,12 +472,10 @@ __global__ __launch_bounds__(256) void k_thin_block(const uint64_t *__restrict__
                 }
                 del &= em;
                 nw = c1 & ~del;
-                if (del && r >= HR && r < HR + TH && k >= 1 && k <= TWW) chg |= 1 << (s >> 1);
+                if (del && mine) chg |= 1 << (s >> 1);
             }
             buf[cur ^ 1][r][k] = nw;
-            if (s == 1 && base_iter == 0 && nw && r >= HR && r < HR + TH && k >= 1 && k <= TWW &&
-                ty0 - HR + r < H && tc0 - 1 + k < WW)
-                nonempty = 1;
+            if (s == 1 && base_iter == 0 && nw && mine) nonempty = 1;
         }
         cur ^= 1;
         __syncthreads();
@@ -491,9 +495,10 @@ __global__ __launch_bounds__(256) void k_thin_block(const uint64_t *__restrict__
     }
 }
 
-void launch_thin_block(const uint64_t *in, uint64_t *out, const FrameGeom &g, int base_iter, int *flags, hipStream_t s) {
+void launch_thin_block(const uint64_t *in, uint64_t *out, const FrameGeom &g, int base_iter, int *flags,
+                       const ThinOwn &own, hipStream_t s) {
     dim3 grid(cdiv(g.WW, TWW), cdiv(g.H, TH));
-    k_thin_block<<<grid, 256, 0, s>>>(in, out, g.W, g.H, g.WW, base_iter, flags);
+    k_thin_block<<<grid, 256, 0, s>>>(in, out, g.W, g.H, g.WW, base_iter, flags, own);
 }
 
 // a16 markPolygonBoundaryAsOccupied (seed_gen:772-825): the bbox +- 2.5 m rectangle in grid cells;

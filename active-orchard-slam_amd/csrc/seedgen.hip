@@ -1,6 +1,7 @@
 // Seed-gen frame orchestration (AosSeedGenNode::processPointCloud, seed_gen:452-579) on one
 // HIP stream. Host work is limited to launch geometry derived from the polygon (a few scalars);
-// every per-point / per-cell stage runs on the GPU.
+// every per-point / per-cell stage runs on the GPU. The tiled multi-GPU frame (tiled.hip) reuses
+// ror_stage and finish_frame.
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -11,7 +12,8 @@ using namespace aos;
 
 void aos_ctx::release() {
     for (DevBuf *b : {&cloud_copy, &bin_count, &bin_start, &pt_binslot, &sorted, &scan_tmp, &counters, &raster_bytes,
-                      &raster_bits, &infl_bits, &open_bits, &thin_a, &thin_b, &occ_bytes, &skel_bytes, &flags})
+                      &raster_bits, &infl_bits, &open_bits, &thin_a, &thin_b, &occ_bytes, &skel_bytes, &flags,
+                      &full_infl, &full_skel})
         b->release();
     h_small.release();
     h_stats.release();
@@ -44,8 +46,10 @@ void aos_ctx::set_cloud(const aos_cloud_view &v) {
     have_cloud = true;
 }
 
+namespace aos {
+
 // getActiveBounds (seed_gen:874-890) + generateOccupancyGrid geometry (:584-600)
-static FrameGeom frame_geom(const Poly &poly, const aos_params &P) {
+FrameGeom frame_geom(const Poly &poly, const aos_params &P) {
     FrameGeom g{};
     double hminx = poly[0].first, hmaxx = poly[0].first, hminy = poly[0].second, hmaxy = poly[0].second;
     for (const auto &pt : poly) {
@@ -67,48 +71,70 @@ static FrameGeom frame_geom(const Poly &poly, const aos_params &P) {
     return g;
 }
 
-void aos_ctx::run_seedgen(bool want_host, aos_seedgen_out &out) {
-    std::memset(&out, 0, sizeof(out));
-    const FrameGeom g = frame_geom(poly, P);
-    geom = g;
-    if (g.R > 63) throw std::runtime_error("inflation radius > 63 cells is not supported by the bit-packed kernel");
-    if ((size_t)g.W * g.H > (size_t)1 << 31) throw std::runtime_error("grid larger than 2^31 cells");
-    hipStream_t s = stream;
-    const size_t C = (size_t)g.W * g.H, Cw = (size_t)g.WW * g.H;
-    AOS_HIP(hipEventRecord(ev[0], s));
-    static_cast<int *>(h_stats.ensure(64 + 8 * kRorCounters))[0] = 0;
+// Half-width of the band around the clip box (or a tile's cells) whose points can be ROR
+// neighbours of a candidate: r plus slack for the float box arithmetic.
+float ror_margin(const aos_params &P) { return (float)(P.ror_radius * 1.01) + 1e-4f; }
 
-    // ---------------- a1-a4: ROR restricted to the clip box, clip, exclusion discs, raster
+Poly default_polygon() {   // hard-coded default polygon of the reference constructor (seed_gen:196-199)
+    return {{-1.972916603088379, 7.9420671463012695}, {-2.0726776123046875, 0.022441387176513672},
+            {70.22465515136719, 2.102720260620117}, {69.48777770996094, 9.786612510681152}};
+}
+
+// ximgproc thinning loop: T = 1 if the image is empty after iteration 1, else the first iteration
+// (k >= 2, 1-based) that deletes nothing; 0 while undecided. flags as written by k_thin_block.
+int thin_iterations(const int *flags, int iters_run) {
+    if (!flags[0]) return 1;
+    for (int k = 1; k < iters_run; ++k)
+        if (!flags[1 + k]) return k + 1;
+    return 0;
+}
+
+}  // namespace aos
+
+// a1-a4: ROR restricted to the points that can reach the (own) cells, clip, exclusion discs, raster
+// into raster_bytes (o.Wr x o.Hr window, zeroed here). Records ev[10] / ev[11] around the neighbour
+// count kernel and copies the number of binned points to h_stats[0].
+void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o) {
+    hipStream_t s = stream;
+    static_cast<int *>(h_stats.ensure(64 + 8 * kRorCounters))[0] = 0;
     RorLaunch L{};
     L.cloud = d_cloud; L.n = n_points; L.step = step; L.ox = ox; L.oy = oy; L.oz = oz; L.is_dense = is_dense;
     L.cminx = g.minx; L.cmaxx = g.maxx; L.cminy = g.miny; L.cmaxy = g.maxy;
     L.cminz = P.clipping_minz; L.cmaxz = P.clipping_maxz;
-    const float m = (float)(P.ror_radius * 1.01) + 1e-4f;
+    const float m = ror_margin(P);
     L.bminx = L.cminx - m; L.bmaxx = L.cmaxx + m; L.bminy = L.cminy - m; L.bmaxy = L.cmaxy + m;
     L.bminz = L.cminz - m; L.bmaxz = L.cmaxz + m;
+    if (o.limit_box) {   // a tile: only the neighbourhood of its own cells
+        L.bminx = std::max(L.bminx, o.box[0]); L.bminy = std::max(L.bminy, o.box[1]);
+        L.bmaxx = std::min(L.bmaxx, o.box[2]); L.bmaxy = std::min(L.bmaxy, o.box[3]);
+    }
     float cs_ = (float)(P.ror_radius * 1.001);
     const double ext = std::max((double)L.bmaxx - L.bminx, (double)L.bmaxy - L.bminy);
     if (ext / cs_ > 8192.0) cs_ = (float)(ext / 8192.0);  // cap the bin grid; coarser bins stay exact
     L.inv_cs = 1.0f / cs_;
-    L.nbx = (int)((L.bmaxx - L.bminx) * L.inv_cs) + 1;
-    L.nby = (int)((L.bmaxy - L.bminy) * L.inv_cs) + 1;
+    L.nbx = std::max(1, (int)((L.bmaxx - L.bminx) * L.inv_cs) + 1);
+    L.nby = std::max(1, (int)((L.bmaxy - L.bminy) * L.inv_cs) + 1);
     L.r2 = P.ror_radius * P.ror_radius;
     L.r2f = (float)(P.ror_radius * P.ror_radius);
     L.need = P.ror_min_neighbors + 1;
     L.origin_x = g.origin_x; L.origin_y = g.origin_y; L.res = g.res; L.W = g.W; L.H = g.H;
+    L.rx0 = o.rx0; L.ry0 = o.ry0; L.rx1 = o.rx1; L.ry1 = o.ry1; L.wx0 = o.wx0; L.wy0 = o.wy0; L.Wr = o.Wr;
     const int nb = L.nbx * L.nby;
+    const size_t Cr = (size_t)o.Wr * o.Hr;
 
     int *d_bc = static_cast<int *>(bin_count.ensure(sizeof(int) * (nb + 1)));
     int *d_bs = static_cast<int *>(bin_start.ensure(sizeof(int) * (nb + 1)));
     int2 *d_ps = static_cast<int2 *>(pt_binslot.ensure(sizeof(int2) * std::max<uint64_t>(n_points, 1)));
     unsigned long long *d_cnt = static_cast<unsigned long long *>(counters.ensure(8 * kRorCounters));
-    uint8_t *d_rb = static_cast<uint8_t *>(raster_bytes.ensure(C));
+    uint8_t *d_rb = static_cast<uint8_t *>(raster_bytes.ensure(std::max<size_t>(Cr, 1)));
     size_t st = scan_temp_bytes(nb + 1);
     void *d_st = scan_tmp.ensure(st);
     AOS_HIP(hipMemsetAsync(d_bc, 0, sizeof(int) * (nb + 1), s));
     AOS_HIP(hipMemsetAsync(d_cnt, 0, 8 * kRorCounters, s));
-    AOS_HIP(hipMemsetAsync(d_rb, 0, C, s));
-    // PCL dense kNN needs k = min_pts + 1 points in the whole cloud (else every point is removed)
+    AOS_HIP(hipMemsetAsync(d_rb, 0, Cr, s));
+    // PCL dense kNN needs k = min_pts + 1 points in the whole cloud (else every point is removed).
+    // A tile's shard holds every neighbour of its own candidates, so a shard with fewer points has
+    // no keepable candidate either: the local test is exact.
     const bool any = n_points > 0 && !(is_dense && n_points < (uint64_t)L.need);
     if (any) {
         launch_ror_bin(L, d_bc, d_ps, s);
@@ -121,13 +147,30 @@ void aos_ctx::run_seedgen(bool want_host, aos_seedgen_out &out) {
         AOS_HIP(hipEventRecord(ev[11], s));
         AOS_HIP(hipMemcpyAsync(h_stats.p, d_bs + nb, sizeof(int), hipMemcpyDeviceToHost, s));
     }
+}
+
+void aos_ctx::run_seedgen(bool want_host, aos_seedgen_out &out) {
+    std::memset(&out, 0, sizeof(out));
+    tiled_frame = false;
+    have_frame = false;
+    const FrameGeom g = frame_geom(poly, P);
+    geom = g;
+    if (g.R > 63) throw std::runtime_error("inflation radius > 63 cells is not supported by the bit-packed kernel");
+    if ((size_t)g.W * g.H > (size_t)1 << 31) throw std::runtime_error("grid larger than 2^31 cells");
+    hipStream_t s = stream;
+    const size_t Cw = (size_t)g.WW * g.H;
+    AOS_HIP(hipEventRecord(ev[0], s));
+
+    // ---------------- a1-a4: ROR restricted to the clip box, clip, exclusion discs, raster
+    RorOwn own{0, 0, g.W, g.H, 0, 0, g.W, g.H, false, {0, 0, 0, 0}};
+    ror_stage(g, own);
     AOS_HIP(hipEventRecord(ev[1], s));
 
     // ---------------- a5 inflation, a6 frame -> /occupancy_grid
     uint64_t *d_rbits = static_cast<uint64_t *>(raster_bits.ensure(Cw * 8));
     uint64_t *d_ibits = static_cast<uint64_t *>(infl_bits.ensure(Cw * 8));
-    int8_t *d_occ = static_cast<int8_t *>(occ_bytes.ensure(C));
-    launch_pack_bits(d_rb, d_rbits, g.W, g.H, g.WW, s);
+    int8_t *d_occ = static_cast<int8_t *>(occ_bytes.ensure((size_t)g.W * g.H));
+    launch_pack_bits(raster_bytes.as<uint8_t>(), d_rbits, g.W, g.H, g.WW, s);
     launch_inflate(d_rbits, d_ibits, g, s);
     launch_bits_to_bytes(d_ibits, d_occ, g, 5, s);
     AOS_HIP(hipEventRecord(ev[2], s));
@@ -144,24 +187,19 @@ void aos_ctx::run_seedgen(bool want_host, aos_seedgen_out &out) {
     const uint64_t *src = d_open;
     int *h_flags = static_cast<int *>(h_small.ensure(sizeof(int) * (2 + max_iters + K)));
     const uint64_t *final_buf = d_open;
+    const ThinOwn whole{0, g.H, 0, g.WW, 1};
     int T = 0;
     for (int batch = 0;; ++batch) {
         const int per_batch = batch == 0 ? 3 : 4;   // typical T <= 24 needs one round trip
         for (int j = 0; j < per_batch; ++j) {
             uint64_t *dst = bufs[launched & 1];
-            launch_thin_block(src, dst, g, launched * K, d_flags, s);
+            launch_thin_block(src, dst, g, launched * K, d_flags, whole, s);
             src = dst;
             ++launched;
         }
         AOS_HIP(hipMemcpyAsync(h_flags, d_flags, sizeof(int) * (1 + launched * K), hipMemcpyDeviceToHost, s));
         AOS_HIP(hipStreamSynchronize(s));
-        // T: stop after iteration 1 if the image is empty, else after the first iteration
-        // (k >= 2, 1-based) that deletes nothing (ximgproc thinning loop with prev = zeros).
-        T = 0;
-        if (!h_flags[0]) T = 1;
-        else
-            for (int k = 1; k < launched * K; ++k)
-                if (!h_flags[1 + k]) { T = k + 1; break; }
+        T = thin_iterations(h_flags, launched * K);
         if (T) {
             // the last launch that ran: launch j runs iff j == 0 or iteration j*K-1 deleted something
             int last = 0;
@@ -175,6 +213,15 @@ void aos_ctx::run_seedgen(bool want_host, aos_seedgen_out &out) {
     thin_iters = T;
     skel_bits = final_buf;
     AOS_HIP(hipEventRecord(ev[3], s));
+    finish_frame(g, want_host, nullptr, out);
+}
+
+// a16 + a8-a15 on the whole map from skel_bits / occ_bytes, then the frame outputs. clipped_total:
+// the kept-candidate count when it was reduced over tiles (else read from this handle's counters).
+void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *clipped_total, aos_seedgen_out &out) {
+    hipStream_t s = stream;
+    const size_t C = (size_t)g.W * g.H;
+    int8_t *d_occ = occ_bytes.as<int8_t>();
 
     // ---------------- a16 /skeletonized_occupancy_grid = skeleton + polygon bbox rectangle
     int8_t *d_skel = static_cast<int8_t *>(skel_bytes.ensure(C));
@@ -206,15 +253,19 @@ void aos_ctx::run_seedgen(bool want_host, aos_seedgen_out &out) {
     AOS_HIP(hipEventRecord(ev[5], s));
 
     unsigned long long *h_cnt = static_cast<unsigned long long *>(h_stats.ensure(64 + 8 * kRorCounters)) + 8;
-    AOS_HIP(hipMemcpyAsync(h_cnt, d_cnt, 8 * kRorCounters, hipMemcpyDeviceToHost, s));
+    if (!clipped_total) AOS_HIP(hipMemcpyAsync(h_cnt, counters.p, 8 * kRorCounters, hipMemcpyDeviceToHost, s));
     if (want_host) {
         h_occ.resize(C); h_skel.resize(C);
         AOS_HIP(hipMemcpyAsync(h_occ.data(), d_occ, C, hipMemcpyDeviceToHost, s));
         AOS_HIP(hipMemcpyAsync(h_skel.data(), d_skel, C, hipMemcpyDeviceToHost, s));
     }
     AOS_HIP(hipStreamSynchronize(s));
-    n_clipped = 0;
-    for (int i = 0; i < kRorCounters; ++i) n_clipped += h_cnt[i];
+    if (clipped_total) {
+        n_clipped = *clipped_total;
+    } else {
+        n_clipped = 0;
+        for (int i = 0; i < kRorCounters; ++i) n_clipped += h_cnt[i];
+    }
     have_frame = true;
 
     h_row_center = std::move(so.row_center); h_row_start = std::move(so.row_start);
@@ -260,11 +311,14 @@ int aos_ctx::debug_grid(const char *which, int8_t *dst, uint64_t capacity) {
     const size_t C = (size_t)geom.W * geom.H;
     if (capacity < C) { set_error("aos_debug_grid: capacity < width*height"); return AOS_E_INVALID; }
     const uint64_t *bits = nullptr;
-    if (!std::strcmp(which, "raster")) bits = raster_bits.as<uint64_t>();
-    else if (!std::strcmp(which, "inflated")) bits = infl_bits.as<uint64_t>();
-    else if (!std::strcmp(which, "opened")) bits = open_bits.as<uint64_t>();
+    if (!std::strcmp(which, "inflated")) bits = tiled_frame ? full_infl.as<uint64_t>() : infl_bits.as<uint64_t>();
     else if (!std::strcmp(which, "skeleton_frameless")) bits = skel_bits;
-    else { set_error(std::string("aos_debug_grid: unknown grid ") + which); return AOS_E_INVALID; }
+    else if (!tiled_frame && !std::strcmp(which, "raster")) bits = raster_bits.as<uint64_t>();
+    else if (!tiled_frame && !std::strcmp(which, "opened")) bits = open_bits.as<uint64_t>();
+    else {
+        set_error(std::string("aos_debug_grid: unknown grid (or not kept by a tiled frame) ") + which);
+        return AOS_E_INVALID;
+    }
     DevBuf tmp;
     int8_t *d = static_cast<int8_t *>(tmp.ensure(C));
     launch_bits_to_bytes(bits, d, geom, 0, stream);

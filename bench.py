@@ -33,10 +33,15 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="C2")
+    ap.add_argument("--config", default=None, help="C2 (default), or C3 with --tiled")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-config", default="C1")
-    return ap.parse_args(argv)
+    ap.add_argument("--tiled", action="store_true",
+                    help="one map split into tiles over the ranks (SURVEY §8e, BASELINE configs[3]); strong scaling")
+    a = ap.parse_args(argv)
+    if a.config is None:
+        a.config = "C3" if a.tiled else "C2"
+    return a
 
 
 def timed_region(step, steps: int, warmup: int, world: int, sync, dist=None, device=None):
@@ -138,15 +143,34 @@ def main():
     red_dev = dev if backend == "nccl" else torch.device("cpu")
 
     cfg = orchard.CONFIGS[a.config]
-    cloud = orchard.generate(cfg, seed=cfg.seed + rank)
     poly = orchard.polygon(cfg)
+    params = aos_gpu.default_params(grid_resolution=cfg.res)
+    ctx = aos_gpu.Ctx(params, device=gpu)
+    ctx.set_polygon(poly)
+    if a.tiled:
+        # one map: every rank holds the points of its tile's box (tile + ROR margin), resident in HBM
+        import aos_tiles
+        tx, ty = aos_tiles.tiling_for(world)
+        plan = aos_tiles.tile_plan(params, poly, tx, ty, rank)
+        cloud = aos_tiles.shard(orchard.generate(cfg), plan["points_box"])
+        if world > 1:
+            comm = aos_tiles.TorchDistComm(plan["exchange_bytes"], dev)
+        else:
+            comm = aos_tiles.ThreadGroup(1).comm(0, plan["exchange_bytes"], dev)
+    else:
+        cloud = orchard.generate(cfg, seed=cfg.seed + rank)
     d_cloud = torch.from_numpy(cloud).to(dev)
     n = cloud.shape[0]
-    ctx = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res), device=gpu)
-    ctx.set_polygon(poly)
+    del cloud
 
     def step():
-        g = ctx.seedgen(d_cloud.data_ptr(), n_points=n, on_device=True, want_host=False)
+        if a.tiled:
+            g = ctx.tiled_seedgen(comm, tx, ty, d_cloud.data_ptr(), root=0, n_points=n, on_device=True,
+                                  want_host=False)
+            if not g["root"]:
+                return g, {"ms": {}, "nodes": (), "edges": ()}
+        else:
+            g = ctx.seedgen(d_cloud.data_ptr(), n_points=n, on_device=True, want_host=False)
         gg = ctx.gvd_from_seedgen()
         return g, gg
 
@@ -159,7 +183,8 @@ def main():
         for k, v in ggs["ms"].items():
             stage["gvd_" + k] = stage.get("gvd_" + k, 0.0) + v
     cells = g["width"] * g["height"]
-    value = throughput(cells / 1e6, world, len(res), dt)
+    # weak: every rank processes its own map; tiled: the ranks share one map (strong scaling)
+    value = throughput(cells / 1e6, 1 if a.tiled else world, len(res), dt)
     avg = {k: v / len(res) for k, v in stage.items()}
 
     # roofline of the dominant GPU kernel (largest share of device time per frame in the committed
@@ -167,7 +192,8 @@ def main():
     # Algorithmic bytes per launch: each staged point record read once (float4, 16 B)
     # + one raster byte per kept candidate. Timed live: HIP events around that single launch on the
     # handle's stream (aos_seedgen_out.ms_ror_count), averaged over the timed steps.
-    alg = 16.0 * g["n_binned"] + float(g["n_clipped"])
+    # (tiled: rank 0's launch; its share of the kept candidates is not reported, so only the 16 B/point term)
+    alg = 16.0 * g["n_binned"] + (0.0 if a.tiled else float(g["n_clipped"]))
     ms_k = avg["seedgen_ror_count"]
     achieved = alg / (ms_k * 1e-3) / 1e9 if ms_k > 0 else 0.0
     traffic, src = pmc_traffic(DOMINANT)
@@ -177,21 +203,27 @@ def main():
             "units_per_launch": g["n_binned"], "traffic_source": src}
     # BASELINE.md frame-level figure: B_alg = 12 N + C (6 + 4 T) over the whole frame wall-clock
     T = g["thin_iters"]
-    b_frame = 12.0 * n + cells * (6.0 + 4.0 * T)
+    b_frame = 12.0 * (cfg.n_points if a.tiled else n) + cells * (6.0 + 4.0 * T)
     frame_roof = {"alg_bytes": b_frame, "achieved_GBs": round(b_frame / (dt / len(res)) / 1e9, 2),
                   "frac": round(b_frame / (dt / len(res)) / 1e9 / HBM_PEAK_GBS, 5),
                   "note": "whole frame incl. the host Subdiv2D replay (DESIGN.md)"}
 
     if rank == 0:
+        if a.tiled:
+            workload = (f"{a.config}: {cfg.n_points} pts, {g['width']}x{g['height']} cells @ {cfg.res} m, one map in "
+                        f"{tx}x{ty} tiles (rank 0 holds {n} pts), halo all-gathers, GVD on rank 0")
+        else:
+            workload = (f"{a.config}: {n} pts, {g['width']}x{g['height']} cells @ {cfg.res} m, "
+                        f"full seed-gen + GVD per frame, one independent tile per GPU")
         out = {
             "metric": "Mcells/s skeleton+GVD (seed-gen + GVD frame) on 4096^2 grid",
             "value": round(value, 3), "unit": "Mcells/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-            "ms_per_step": round(dt / len(res) * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "ms_per_step": round(dt / len(res) * 1e3, 3), "higher_is_better": True,
+            "scaling": "strong" if a.tiled else "weak",
             "vs_baseline": None, "dtype": "f32/f64 (reference float/double arithmetic), u8/bit grids",
             "data": "synthetic orchard (tools/orchard_gen.c, SplitMix64), device-resident PointCloud2",
-            "config": {"workload": f"{a.config}: {n} pts, {g['width']}x{g['height']} cells @ {cfg.res} m, "
-                                   f"full seed-gen + GVD per frame, one independent tile per GPU",
-                       "global_batch": world, "parallelism": f"tiles{world}"},
+            "config": {"workload": workload, "global_batch": 1 if a.tiled else world,
+                       "parallelism": f"tiled{tx}x{ty}" if a.tiled else f"tiles{world}"},
             "stages_ms": {k: round(v, 3) for k, v in avg.items()},
             "frame": {"T": T, "rows": len(g["row_length"]), "seeds": len(g["voronoi_seeds"]),
                       "nodes": len(gg["nodes"]), "edges": len(gg["edges"]), "n_binned": g["n_binned"],

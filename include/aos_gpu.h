@@ -141,6 +141,54 @@ int aos_seedgen_reprocess(aos_ctx *ctx, int want_host, aos_seedgen_out *out);
 int aos_gvd_process(aos_ctx *ctx, const aos_gvd_in *in, aos_gvd_out *out);
 int aos_gvd_from_seedgen(aos_ctx *ctx, aos_gvd_out *out);
 
+/* ---------------------------------------------------------------------------------------------
+ * Multi-GPU tiled frame (BASELINE.json configs[3]: 8192^2 in 2 x 4 tiles).
+ * One map is split into tiles_x x tiles_y tiles, one rank (process or thread) per tile, each with
+ * its own handle on its own GPU. Ranks refresh the halos of their bit-packed grids by all-gathering
+ * every tile's border strips, and max-reduce the thinning convergence flags. After thinning, the
+ * skeleton and inflated tiles are all-gathered and the root rank finishes the frame on the whole
+ * map. The root's outputs are byte-identical to aos_seedgen_process on the whole cloud. The
+ * reference has no counterpart: its node processes the whole map on one core (seed_gen:230-248).
+ * ------------------------------------------------------------------------------------------- */
+
+/* Communicator supplied by the caller: RCCL over xGMI in production (torch.distributed 'nccl', or
+ * ncclAllGather / ncclAllReduce on the same buffers). send_buf / recv_buf are device memory on
+ * this rank's GPU, registered once; the library packs into send_buf and reads recv_buf. Both
+ * callbacks are collective (every rank makes the same calls in the same order), are called with
+ * the handle's stream idle, and must have completed when they return. Return 0 on success. */
+typedef struct aos_comm {
+    void *user;
+    int32_t rank, world;                 /* world = tiles_x * tiles_y; rank r = tile (r % tiles_x, r / tiles_x) */
+    void *send_buf;                      /* >= buf_bytes                                       */
+    void *recv_buf;                      /* >= world * buf_bytes                               */
+    uint64_t buf_bytes;                  /* >= aos_tile_plan.exchange_bytes                    */
+    /* recv_buf[r * bytes, (r + 1) * bytes) = send_buf[0, bytes) of rank r, for every rank r */
+    int (*all_gather)(void *user, uint64_t bytes);
+    /* element-wise max over ranks of n int32 values in host memory, in place */
+    int (*all_reduce_max)(void *user, int32_t *values, int32_t n);
+} aos_comm;
+
+typedef struct aos_tile_plan {
+    int32_t tiles_x, tiles_y, rank, tile_x, tile_y;
+    int32_t halo_rows, halo_words;       /* halo depth (0 along an untiled dimension)          */
+    int32_t row0, row1, word0, word1;    /* own rows and 64-cell words of the map              */
+    int32_t win_row0, win_row1, win_word0, win_word1;   /* own tile + halo, clamped to the map */
+    double points_box[4];                /* xmin, ymin, xmax, ymax: the points this rank needs  */
+    uint64_t exchange_bytes;             /* minimum aos_comm.buf_bytes                         */
+    aos_grid_info info;                  /* the whole map                                      */
+} aos_tile_plan;
+
+/* Host arithmetic only (no device needed): the tile of `rank` for this polygon (n_poly < 3: the
+ * reference's default polygon, seed_gen:196-199) and these parameters. */
+int aos_tile_plan_compute(const aos_params *p, const double *poly_xy, uint32_t n_poly, int32_t tiles_x,
+                          int32_t tiles_y, int32_t rank, aos_tile_plan *out);
+/* One tiled frame on this rank (uses the handle's polygon, see aos_set_polygon). `cloud` must hold
+ * every point inside this rank's points_box; points outside it are ignored, so the whole cloud
+ * also works. Root: the full aos_seedgen_out, and aos_gvd_from_seedgen works afterwards. Other
+ * ranks: info, thin_iters, n_clipped (whole map) and timings only. */
+int aos_tiled_seedgen_process(aos_ctx *ctx, const aos_comm *comm, int32_t tiles_x, int32_t tiles_y, int32_t root,
+                              const aos_cloud_view *cloud, int want_host, aos_seedgen_out *out);
+
 /* Diagnostics: copy an internal device grid of the last frame to host as int8 {0,100} (or 0/1
  * for "opened"). which: "raster", "inflated", "opened", "skeleton_frameless". */
 int aos_debug_grid(aos_ctx *ctx, const char *which, int8_t *dst, uint64_t capacity);

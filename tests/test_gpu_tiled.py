@@ -1,0 +1,138 @@
+"""Tiled multi-GPU frame on the one GPU of a test box: the tiles of one map run as
+threads (aos_tiles.ThreadGroup, one handle + stream each) or as processes over torch.distributed
+(gloo). The root's outputs must be byte-identical to the oracle / the single-GPU frame of the whole
+cloud, and the GVD graph built from them identical as well."""
+import hashlib
+import json
+import os
+import threading
+
+import numpy as np
+import pytest
+
+import aos_gpu
+import aos_tiles as T
+import oracle_py as O
+import orchard
+from parity_util import assert_gvd_parity, assert_seedgen_parity
+
+pytestmark = pytest.mark.gpu
+
+GVD_KEYS = ("nodes", "edges", "edge_lengths", "edge_clearances", "node_labels", "node_cluster_indices",
+            "node_label_counts", "node_label_clusters", "node_label_types")
+GRIDS = ("inflated", "skeleton_frameless")
+
+
+def _single(cloud, poly, res):
+    c = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=res))
+    c.set_polygon(poly)
+    g = c.seedgen(cloud)
+    grids = {w: c.debug_grid(w, (g["height"], g["width"])) for w in GRIDS}
+    gg = c.gvd_from_seedgen()
+    c.close()
+    return g, grids, gg
+
+
+def _tiled_threads(cloud, poly, res, tiles_x, tiles_y, root, shard=True):
+    world = tiles_x * tiles_y
+    params = aos_gpu.default_params(grid_resolution=res)
+    plans = [T.tile_plan(params, poly, tiles_x, tiles_y, r) for r in range(world)]
+    group = T.ThreadGroup(world, timeout=120)
+    ctxs = [aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=res)) for _ in range(world)]
+    comms = [group.comm(r, plans[r]["exchange_bytes"], "cuda:0") for r in range(world)]
+    out, errors = [None] * world, []
+
+    def work(r):
+        try:
+            ctxs[r].set_polygon(poly)
+            part = T.shard(cloud, plans[r]["points_box"]) if shard else cloud
+            out[r] = ctxs[r].tiled_seedgen(comms[r], tiles_x, tiles_y, part, root=root)
+        except BaseException as e:   # noqa: BLE001
+            errors.append(e)
+            group.abort()
+
+    ts = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(300)
+    if errors:
+        raise errors[0]
+    c = ctxs[root]
+    g = out[root]
+    assert g["root"] and all(not o["root"] for i, o in enumerate(out) if i != root)
+    grids = {w: c.debug_grid(w, (g["height"], g["width"])) for w in GRIDS}
+    gg = c.gvd_from_seedgen()
+    for x in ctxs:
+        x.close()
+    return g, out, grids, gg
+
+
+def _assert_same(single, tiled):
+    g1, grids1, gg1 = single
+    g, out, grids, gg = tiled
+    assert_seedgen_parity(g, {**g1, "cluster_length": np.zeros(g1["n_clusters_all"])})
+    assert (g["n_clipped"], g["n_bfs_replayed"]) == (g1["n_clipped"], g1["n_bfs_replayed"])
+    for w in GRIDS:
+        assert np.array_equal(grids[w], grids1[w]), w
+    for o in out:
+        assert (o["thin_iters"], o["n_clipped"]) == (g1["thin_iters"], g1["n_clipped"])
+    assert gg["published"] == gg1["published"]
+    for k in GVD_KEYS:
+        assert np.array_equal(gg[k], gg1[k]), k
+
+
+@pytest.mark.parametrize("tiles,root", [((1, 1), 0), ((2, 1), 1), ((1, 2), 0), ((2, 2), 3), ((3, 2), 2)])
+def test_tiled_c1_equals_single_gpu(tiles, root):
+    cfg = orchard.CONFIGS["C1"]
+    cloud, poly = orchard.generate(cfg), orchard.polygon(cfg)
+    _assert_same(_single(cloud, poly, cfg.res), _tiled_threads(cloud, poly, cfg.res, *tiles, root))
+
+
+def test_tiled_c1_against_golden_hashes():
+    """2 x 2 tiles, every rank handed the whole cloud (points outside a tile's box are ignored):
+    the root's frame + GVD vs the SHA-256 of the oracle's outputs (tests/golden/c1_sha256.json)."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    hs = json.load(open(os.path.join(here, "golden", "c1_sha256.json")))
+
+    def sha(a, dt):
+        a = np.ascontiguousarray(np.asarray(a, dtype=dt))
+        return hashlib.sha256(a.dtype.str.encode() + str(a.shape).encode() + a.tobytes()).hexdigest()
+
+    cfg = orchard.CONFIGS["C1"]
+    g, _, _, gg = _tiled_threads(orchard.generate(cfg), orchard.polygon(cfg), cfg.res, 2, 2, 0, shard=False)
+    assert g["thin_iters"] == hs["meta"]["thin_iters"] and g["n_clipped"] == hs["meta"]["n_clipped"]
+    for k in ("occupancy", "skeleton_framed"):
+        assert sha(g[k], np.int8) == hs["seedgen"][k], k
+    for k in ("row_center", "row_start", "row_end", "row_length", "voronoi_seeds", "rows_info", "cluster_info"):
+        assert sha(g[k], np.float64) == hs["seedgen"][k], k
+    for k, dt in (("nodes", np.float64), ("edges", np.int32), ("edge_lengths", np.float32),
+                  ("node_labels", np.int32), ("node_label_clusters", np.int32)):
+        assert sha(gg[k], dt) == hs["gvd"][k], k
+
+
+def _blob_scene():
+    """C0 orchard plus a 12 m x 12 m filled square across the map centre (~34 Zhang-Suen iterations:
+    the thinning needs more than one halo period, so halos are refreshed mid-thinning)."""
+    cfg = orchard.CONFIGS["C0"]
+    base = orchard.generate(cfg).view(np.float32).reshape(-1, 4)
+    rng = np.random.default_rng(5)
+    n = 40000
+    blob = np.zeros((n, 4), np.float32)
+    blob[:, 0] = rng.uniform(42.6, 54.6, n)
+    blob[:, 1] = rng.uniform(42.6, 54.6, n)
+    blob[:, 2] = rng.uniform(-0.3, 0.4, n)
+    return cfg, np.concatenate([base, blob]).view(np.uint8).reshape(-1, 16), orchard.polygon(cfg)
+
+
+@pytest.mark.parametrize("tiles", [(2, 2), (4, 1), (1, 4)])
+def test_tiled_blob_refreshes_halos_mid_thinning_vs_oracle(tiles):
+    cfg, cloud, poly = _blob_scene()
+    g, out, grids, gg = _tiled_threads(cloud, poly, cfg.res, *tiles, 0)
+    o = O.seedgen(cloud, poly, O.default_params(grid_resolution=cfg.res))
+    assert o["thin_iters"] > 29
+    assert_seedgen_parity(g, o)
+    assert np.array_equal(grids["skeleton_frameless"], o["skeleton"])
+    assert np.array_equal(grids["inflated"], o["inflated"])
+    assert g["n_clipped"] == o["n_clipped"]
+    assert_gvd_parity(gg, O.gvd(o["voronoi_seeds"], o["rows_info"], o))

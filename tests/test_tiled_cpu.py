@@ -1,0 +1,261 @@
+"""CPU coverage of the tiled multi-GPU frame (libaos_gpu tiled.hip):
+- the tile plan the C-ABI computes (aos_tile_plan_compute needs no GPU);
+- the communicator adapters (aos_tiles.TorchDistComm over gloo at world size 2, ThreadGroup), called
+  through the same C function pointers libaos_gpu calls;
+- a numpy emulation of tiled.hip's schedule (own-cell raster -> halo exchange -> inflate -> open ->
+  Zhang-Suen in halo periods with max-reduced own-cell change flags) run by gloo ranks, whose gathered
+  tiles must equal the oracle's whole-map grids and iteration count.
+"""
+import ctypes
+import os
+import socket
+import threading
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import aos_gpu
+import aos_tiles as T
+import oracle_py as O
+import orchard
+
+KIT = 8   # kThinItersPerLaunch (aos_internal.h)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawn(target, world, *args):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = [q.get(timeout=300) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return sorted(out, key=lambda o: o[0])
+
+
+def _init(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+# ---------------------------------------------------------------- plan
+def test_plan_c3_is_2x4_tiles_of_4096_rows_by_2048_columns():
+    cfg = orchard.CONFIGS["C3"]
+    poly = orchard.polygon(cfg)
+    p = aos_gpu.default_params(grid_resolution=cfg.res)
+    plans = [T.tile_plan(p, poly, 4, 2, r) for r in range(8)]
+    W, H = plans[0]["width"], plans[0]["height"]
+    assert (W, H) == (8192, 8192)
+    cover = np.zeros((H, W // 64), np.int32)
+    for t in plans:
+        assert (t["row1"] - t["row0"], t["word1"] - t["word0"]) == (4096, 32)
+        assert (t["halo_rows"], t["halo_words"]) == (64, 1)
+        cover[t["row0"]:t["row1"], t["word0"]:t["word1"]] += 1
+        assert t["win_row0"] == max(0, t["row0"] - 64) and t["win_row1"] == min(H, t["row1"] + 64)
+        assert t["win_word0"] == max(0, t["word0"] - 1) and t["win_word1"] == min(W // 64, t["word1"] + 1)
+        ox, oy = t["origin"]
+        res = t["resolution"]
+        b = t["points_box"]   # the own cells' world box plus the ROR radius
+        assert b[0] <= ox + 64 * t["word0"] * res - 0.2 and b[2] >= ox + min(W, 64 * t["word1"]) * res + 0.2
+        assert b[1] <= oy + t["row0"] * res - 0.2 and b[3] >= oy + t["row1"] * res + 0.2
+        assert t["exchange_bytes"] == 8 * max(2 * 64 * 32 + 2 * 4096, 2 * 4096 * 32)
+    assert (cover == 1).all()
+
+
+def test_plan_single_tile_and_too_small_tiles():
+    cfg = orchard.CONFIGS["C0"]
+    poly = orchard.polygon(cfg)
+    p = aos_gpu.default_params(grid_resolution=cfg.res)
+    t = T.tile_plan(p, poly, 1, 1, 0)
+    assert (t["halo_rows"], t["halo_words"]) == (0, 0)
+    assert (t["win_row0"], t["win_row1"], t["win_word0"], t["win_word1"]) == (0, 512, 0, 8)
+    with pytest.raises(RuntimeError, match="smaller than its halo"):
+        T.tile_plan(p, poly, 2, 16, 0)          # 32-row tiles, 64-row halo
+    with pytest.raises(RuntimeError, match="rank outside"):
+        T.tile_plan(p, poly, 2, 2, 4)
+
+
+def test_tiling_for():
+    assert [T.tiling_for(n) for n in (1, 2, 4, 6, 8)] == [(1, 1), (2, 1), (2, 2), (3, 2), (4, 2)]
+
+
+def test_shard_keeps_the_points_box():
+    cfg = orchard.CONFIGS["C0"]
+    cloud = orchard.generate(cfg, n_points=20000)
+    box = (10.0, 20.0, 30.5, 40.0)
+    s = T.shard(cloud, box)
+    xyz = orchard.xyz(cloud)
+    inside = (xyz[:, 0] >= box[0]) & (xyz[:, 0] <= box[2]) & (xyz[:, 1] >= box[1]) & (xyz[:, 1] <= box[3])
+    assert np.array_equal(s, cloud[inside])
+
+
+# ---------------------------------------------------------------- communicators
+def _comm_worker(rank, world, port, q):
+    _init(rank, world, port)
+    c = T.TorchDistComm(64, "cpu")
+    c.send[:48] = torch.arange(48, dtype=torch.uint8) + 10 * rank
+    rc = c.c.all_gather(None, 48)                      # as libaos_gpu calls it
+    v = (ctypes.c_int32 * 3)(rank, 5 - rank, -rank)
+    rc2 = c.c.all_reduce_max(None, v, 3)
+    q.put((rank, rc, rc2, c.recv[: 48 * world].numpy().copy(), list(v)))
+    dist.destroy_process_group()
+
+
+def test_torch_dist_comm_gloo_world2():
+    for rank, rc, rc2, recv, v in _spawn(_comm_worker, 2):
+        assert rc == 0 and rc2 == 0
+        assert np.array_equal(recv, np.concatenate([np.arange(48, dtype=np.uint8) + 10 * r for r in range(2)]))
+        assert v == [1, 5, 0]
+
+
+def test_thread_group_comm():
+    world = 3
+    g = T.ThreadGroup(world, timeout=30)
+    comms = [g.comm(r, 16, "cpu") for r in range(world)]
+    res = [None] * world
+
+    def work(r):
+        c = comms[r]
+        c.send[:8] = r + 1
+        rc = c.c.all_gather(None, 8)
+        v = (ctypes.c_int32 * 2)(r, -r)
+        rc2 = c.c.all_reduce_max(None, v, 2)
+        res[r] = (rc, rc2, c.recv[:24].numpy().copy(), list(v))
+
+    ts = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(60)
+    for rc, rc2, recv, v in res:
+        assert rc == 0 and rc2 == 0 and v == [2, 0]
+        assert np.array_equal(recv, np.repeat(np.arange(1, 4, dtype=np.uint8), 8))
+
+
+# ---------------------------------------------------------------- schedule emulation
+def _zs_sub(img, it):
+    """One ximgproc Zhang-Suen sub-iteration on a 0/1 image (border pixels untouched)."""
+    P = np.pad(img, 1).astype(np.int32)
+    p2, p3, p4, p5 = P[:-2, 1:-1], P[:-2, 2:], P[1:-1, 2:], P[2:, 2:]
+    p6, p7, p8, p9 = P[2:, 1:-1], P[2:, :-2], P[1:-1, :-2], P[:-2, :-2]
+    seq = [p2, p3, p4, p5, p6, p7, p8, p9, p2]
+    A = sum(((seq[k] == 0) & (seq[k + 1] == 1)).astype(np.int32) for k in range(8))
+    B = sum(seq[:8])
+    m1, m2 = (p2 * p4 * p6, p4 * p6 * p8) if it == 0 else (p2 * p4 * p8, p2 * p6 * p8)
+    d = (img == 1) & (A == 1) & (B >= 2) & (B <= 6) & (m1 == 0) & (m2 == 0)
+    d[0, :] = d[-1, :] = d[:, 0] = d[:, -1] = False
+    return np.where(d, 0, img).astype(np.uint8)
+
+
+def _emu_worker(rank, world, port, q, tx, ty, res, poly, raster, R):
+    _init(rank, world, port)
+    p = aos_gpu.default_params(grid_resolution=res)
+    plans = [T.tile_plan(p, poly, tx, ty, r) for r in range(world)]
+    me = plans[rank]
+    W = me["width"]
+
+    def own(t):
+        return t["row0"], t["row1"], 64 * t["word0"], min(W, 64 * t["word1"])
+
+    wy0, wy1, wx0, wx1 = me["win_row0"], me["win_row1"], 64 * me["win_word0"], min(W, 64 * me["win_word1"])
+    y0, y1, x0, x1 = own(me)
+    mine = (slice(y0 - wy0, y1 - wy0), slice(x0 - wx0, x1 - wx0))
+
+    def exchange(win):   # every rank publishes its own block; halo cells come from their owners
+        blocks = [None] * world
+        dist.all_gather_object(blocks, win[mine].copy())
+        out = win.copy()
+        for r, t in enumerate(plans):
+            a0, a1, b0, b1 = own(t)
+            ya, yb, xa, xb = max(a0, wy0), min(a1, wy1), max(b0, wx0), min(b1, wx1)
+            if r != rank and ya < yb and xa < xb:
+                out[ya - wy0:yb - wy0, xa - wx0:xb - wx0] = blocks[r][ya - a0:yb - a0, xa - b0:xb - b0]
+        return out
+
+    win = np.zeros((wy1 - wy0, wx1 - wx0), np.uint8)
+    win[mine] = raster[y0:y1, x0:x1] != 0          # this tile's own kept candidates
+    win = exchange(win)
+    infl = (O.inflate(np.where(win == 1, 100, 0).astype(np.int8), R) == 100).astype(np.uint8)
+    img = O.open_cross(infl)
+    G = max(me["halo_rows"], 64 * me["halo_words"])
+    halo = G > 0
+    budget = G - R - 2 if halo else 1 << 30
+    flags, nonempty, it, Tn, periods = [], 0, 0, 0, 0
+    while True:
+        nl = budget // (2 * KIT) if halo else (3 if it == 0 else 4)
+        assert nl >= 1
+        for _ in range(nl * KIT):
+            chg = 0
+            for sub in (0, 1):
+                new = _zs_sub(img, sub)
+                chg |= int((new[mine] != img[mine]).any())
+                img = new
+            if it == 0:
+                nonempty = int(img[mine].any())
+            flags.append(chg)
+            it += 1
+        budget -= nl * 2 * KIT
+        periods += 1
+        fl = torch.tensor([nonempty] + flags, dtype=torch.int32)
+        dist.all_reduce(fl, op=dist.ReduceOp.MAX)
+        fl = fl.numpy()
+        Tn = 1 if not fl[0] else next((k + 1 for k in range(1, it) if not fl[1 + k]), 0)
+        if Tn:
+            break
+        if halo:
+            img = exchange(img)
+            budget = G
+    parts = [None] * world
+    dist.all_gather_object(parts, (img[mine].copy(), infl[mine].copy()))
+    if rank == 0:
+        H = me["height"]
+        sk, inf = np.zeros((H, W), np.uint8), np.zeros((H, W), np.uint8)
+        for t, (a, b) in zip(plans, parts):
+            a0, a1, b0, b1 = own(t)
+            sk[a0:a1, b0:b1], inf[a0:a1, b0:b1] = a, b
+        q.put((rank, Tn, periods, sk, inf))
+    else:
+        q.put((rank, Tn, periods, None, None))
+    dist.destroy_process_group()
+
+
+def _blob_scene():
+    """C0 orchard plus a 12 m x 12 m filled square across the map centre: ~34 Zhang-Suen iterations,
+    more than one halo period (the first period covers (64 - R - 2) / 2 = 29 sub-iteration pairs)."""
+    cfg = orchard.CONFIGS["C0"]
+    base = orchard.generate(cfg).view(np.float32).reshape(-1, 4)
+    rng = np.random.default_rng(5)
+    n = 40000
+    blob = np.zeros((n, 4), np.float32)
+    blob[:, 0] = rng.uniform(42.6, 54.6, n)
+    blob[:, 1] = rng.uniform(42.6, 54.6, n)
+    blob[:, 2] = rng.uniform(-0.3, 0.4, n)
+    cloud = np.concatenate([base, blob]).view(np.uint8).reshape(-1, 16)
+    return cfg, cloud, orchard.polygon(cfg)
+
+
+@pytest.mark.parametrize("tiles", [(2, 2), (2, 1)])
+def test_tiled_schedule_emulation_matches_oracle(tiles):
+    cfg, cloud, poly = _blob_scene()
+    ref = O.seedgen(cloud, poly, O.default_params(grid_resolution=cfg.res))
+    assert ref["thin_iters"] > 29
+    R = int(np.float32(0.8) / np.float32(cfg.res))
+    tx, ty = tiles
+    out = _spawn(_emu_worker, tx * ty, tx, ty, cfg.res, poly, ref["raster"], R)
+    for _, Tn, periods, _, _ in out:
+        assert Tn == ref["thin_iters"] and periods >= 2
+    sk, inf = out[0][3], out[0][4]
+    assert np.array_equal(inf, (ref["inflated"] != 0).astype(np.uint8))
+    assert np.array_equal(sk, (ref["skeleton"] != 0).astype(np.uint8))
