@@ -28,7 +28,13 @@ class Params(ctypes.Structure):
     _fields_ = [("clipping_minz", c_f), ("clipping_maxz", c_f), ("clipping_minx", c_f), ("clipping_maxx", c_f),
                 ("clipping_miny", c_f), ("clipping_maxy", c_f), ("grid_resolution", c_f), ("inflation_radius", c_f),
                 ("cluster_min_length", c_d), ("ror_radius", c_d), ("ror_min_neighbors", c_i),
-                ("subdiv_rect_mode", c_i), ("max_graph_publish_rate", c_d)]
+                ("subdiv_rect_mode", c_i), ("max_graph_publish_rate", c_d), ("gvd_markers", c_i)]
+
+
+class GvdMarkers(ctypes.Structure):
+    _fields_ = [("n_seeds", c_i), ("seeds_xy", P(c_d)), ("n_rows", c_i), ("row_label_xy", P(c_d)),
+                ("row_label_valid", P(c_i)), ("n_cells", c_i), ("cell_offsets", P(c_i)), ("cell_xy", P(c_d)),
+                ("cell_center_xy", P(c_d)), ("cell_rgba", P(c_f)), ("ms_cells", c_f)]
 
 
 class CloudView(ctypes.Structure):
@@ -64,7 +70,7 @@ class GvdOut(ctypes.Structure):
                 ("node_label_types", P(c_i)), ("edges", P(c_i)), ("edge_lengths", P(c_f)),
                 ("edge_clearances", P(c_f)), ("n_merged_seeds", c_i), ("n_voronoi_edges", c_i),
                 ("n_boundary_points", c_i), ("ms_merge", c_f), ("ms_delaunay", c_f), ("ms_graph", c_f),
-                ("ms_total", c_f)]
+                ("ms_total", c_f), ("ms_cells", c_f)]
 
 
 AllGatherFn = ctypes.CFUNCTYPE(c_i, c_vp, c_u64)
@@ -120,6 +126,7 @@ def lib():
         L.aos_gvd_process.argtypes = [c_vp, P(GvdIn), P(GvdOut)]
         L.aos_gvd_from_seedgen.argtypes = [c_vp, P(GvdOut)]
         L.aos_debug_grid.argtypes = [c_vp, ctypes.c_char_p, c_vp, c_u64]
+        L.aos_gvd_markers_get.argtypes = [c_vp, P(GvdMarkers)]
         L.aos_tile_plan_compute.argtypes = [P(Params), c_vp, c_u, c_i, c_i, c_i, P(TilePlan)]
         L.aos_tiled_seedgen_process.argtypes = [c_vp, P(Comm), c_i, c_i, c_i, P(CloudView), c_i, P(SeedGenOut)]
         L.aos_stream.restype = c_vp
@@ -190,7 +197,8 @@ def _gvd_dict(o: GvdOut) -> dict:
         "edge_lengths": _arr(o.edge_lengths, ne, np.float32),
         "edge_clearances": _arr(o.edge_clearances, ne, np.float32),
         "n_merged": o.n_merged_seeds, "n_vor_edges": o.n_voronoi_edges, "n_boundary_raw": o.n_boundary_points,
-        "ms": {"merge": o.ms_merge, "delaunay": o.ms_delaunay, "graph": o.ms_graph, "total": o.ms_total},
+        "ms": {"merge": o.ms_merge, "delaunay": o.ms_delaunay, "graph": o.ms_graph, "total": o.ms_total,
+               "cells": o.ms_cells},
     }
 
 
@@ -265,6 +273,20 @@ class Ctx:
         o = GvdOut()
         _check(lib().aos_gvd_from_seedgen(self.h, ctypes.byref(o)))
         return _gvd_dict(o)
+
+    def gvd_markers(self) -> dict:
+        """/gvd/markers content of the last GVD call (aos_gvd_markers_get)."""
+        m = GvdMarkers()
+        _check(lib().aos_gvd_markers_get(self.h, ctypes.byref(m)))
+        nc = m.n_cells
+        off = _arr(m.cell_offsets, nc + 1, np.int32)
+        return {"seeds": _arr(m.seeds_xy, 2 * m.n_seeds, np.float64).reshape(-1, 2),
+                "row_label_pts": _arr(m.row_label_xy, 8 * m.n_rows, np.float64).reshape(-1, 4, 2),
+                "row_label_valid": _arr(m.row_label_valid, 4 * m.n_rows, np.int32).reshape(-1, 4),
+                "cell_offsets": off,
+                "cell_xy": _arr(m.cell_xy, 2 * int(off[-1]) if nc else 0, np.float64).reshape(-1, 2),
+                "cell_center": _arr(m.cell_center_xy, 2 * nc, np.float64).reshape(-1, 2),
+                "cell_rgba": _arr(m.cell_rgba, 4 * nc, np.float32).reshape(-1, 4), "ms_cells": m.ms_cells}
 
     def gvd(self, seeds, rows_info, grid: dict) -> dict:
         s = np.ascontiguousarray(seeds, dtype=np.float64).reshape(-1)

@@ -70,6 +70,7 @@ void aos_default_params(aos_params *p) {
     p->ror_min_neighbors = 2;
     p->subdiv_rect_mode = 0;
     p->max_graph_publish_rate = 10.0;
+    p->gvd_markers = 1;
 }
 
 int aos_create(const aos_params *p, int device, aos_ctx **out) {
@@ -206,6 +207,21 @@ int aos_tiled_seedgen_process(aos_ctx *c, const aos_comm *comm, int32_t tiles_x,
     c->run_tiled(*comm, tiles_x, tiles_y, root, want_host != 0, *out);
     return AOS_OK;
     AOS_GUARD_END
+}
+
+int aos_gvd_markers_get(aos_ctx *c, aos_gvd_markers *out) {
+    if (!c || !out) { set_error("aos_gvd_markers_get: null argument"); return AOS_E_INVALID; }
+    const GvdState &G = c->gs;
+    if (!G.have_markers) { set_error("aos_gvd_markers_get: no markers (gvd_markers = 0 or no GVD frame)"); return AOS_E_STATE; }
+    std::memset(out, 0, sizeof(*out));
+    out->n_seeds = (int32_t)(G.merged_xy.size() / 2); out->seeds_xy = G.merged_xy.data();
+    out->n_rows = (int32_t)(G.row_label_valid.size() / 4);
+    out->row_label_xy = G.row_label_xy.data(); out->row_label_valid = G.row_label_valid.data();
+    out->n_cells = (int32_t)G.cell_off.size() - 1;
+    out->cell_offsets = G.cell_off.data(); out->cell_xy = G.cell_xy.data();
+    out->cell_center_xy = G.cell_center.data(); out->cell_rgba = G.cell_rgba.data();
+    out->ms_cells = G.ms_cells;
+    return AOS_OK;
 }
 
 int aos_debug_grid(aos_ctx *c, const char *which, int8_t *dst, uint64_t capacity) {

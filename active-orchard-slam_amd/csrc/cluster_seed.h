@@ -75,12 +75,19 @@ struct GvdState {
     PinnedBuf h_misc;
     void *scratch = nullptr;   // GvdScratch (gvd.hip), freed by free_gvd_scratch
     Subdiv2D subdiv;   // host insert replay; kept across frames to reuse its allocations
+    Subdiv2D subdiv_cells;   // publishMarkers' extractCellBoundaries (second replay, worker thread)
     // host outputs
     std::vector<double> nodes_xy;
     std::vector<int32_t> labels, cluster_idx, label_counts, label_clusters, label_types, edges_out;
     std::vector<float> lengths, clearances;
     int n_merged = 0, n_vor_edges = 0, n_bpts = 0;
     float ms_merge = 0, ms_delaunay = 0, ms_graph = 0, ms_total = 0;
+    // markers (aos_gvd_markers)
+    bool have_markers = false;
+    std::vector<double> merged_xy, row_label_xy, cell_xy, cell_center;
+    std::vector<int32_t> row_label_valid, cell_off;
+    std::vector<float> cell_rgba;
+    float ms_cells = 0;
 };
 
 struct GvdStageIn {

@@ -6,7 +6,8 @@
 // the reference's discovery order) and every per-cluster statistic order-free, together with a
 // certificate: integer coordinate sums <= 2^24 (so every float partial sum is exact in any
 // order) and no ties in the three argmax searches. A cluster without the certificate is
-// replayed exactly (FIFO BFS with the reference's neighbour order) by a GPU thread.
+// replayed exactly (FIFO BFS with the reference's neighbour order) on the host, in parallel over
+// such clusters (host_bfs_replay).
 //
 // Greedy first-come de-duplications (seeds within 0.5 m) are the lexicographically-first
 // maximal independent set of the conflict graph in candidate order; the GPU builds the graph
@@ -15,16 +16,20 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstring>
-
+#include <exception>
+#include <mutex>
 #include <stdexcept>
+#include <thread>
 
 #include "cluster_seed.h"
 
 namespace aos {
 
 static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+constexpr int kReplayThreads = 8;   // host threads for the exact BFS replays of one frame
 
 // isPointInPolygon seed_gen:1231-1255
 __host__ __device__ bool d_pip(double px, double py, const double *poly, int n) {
@@ -652,20 +657,41 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         for (const auto &r : S.h_rec) n_bfs += (r.flags & 2) != 0;
         out.n_bfs = n_bfs;
         if (n_bfs) {
+            // The replayed clusters' cells (raster order) come over in one copy. Replays are independent
+            // (each writes only its own ClusterRec), so they run in parallel over clusters on up to
+            // kReplayThreads host threads: at 8192^2 every row cluster needs one (sums > 2^24).
             std::vector<long long> off(ncl + 1, 0);
             for (int c = 0; c < ncl; ++c) off[c + 1] = off[c] + S.h_rec[c].n;
-            std::vector<int> hc;
-            std::vector<std::pair<int, size_t>> fl;   // (cluster, offset into hc)
+            std::vector<int> ids;
             for (int c = 0; c < ncl; ++c)
-                if (S.h_rec[c].flags & 2) { fl.push_back({c, hc.size()}); hc.resize(hc.size() + S.h_rec[c].n); }
-            for (const auto &f : fl)
-                AOS_HIP(hipMemcpyAsync(hc.data() + f.second, d_cells + off[f.first], sizeof(int) * S.h_rec[f.first].n,
-                                       hipMemcpyDeviceToHost, s));
+                if (S.h_rec[c].flags & 2) ids.push_back(c);
+            const long long lo = off[ids.front()], hi = off[ids.back() + 1];
+            std::vector<int> hc((size_t)(hi - lo));
+            AOS_HIP(hipMemcpyAsync(hc.data(), d_cells + lo, sizeof(int) * (hi - lo), hipMemcpyDeviceToHost, s));
             AOS_HIP(hipStreamSynchronize(s));
-            std::vector<int> q, tab;
-            for (const auto &f : fl)
-                host_bfs_replay(hc.data() + f.second, S.h_rec[f.first].n, g, hp.data(), np,
-                                static_cast<float>(in.cluster_min_length), S.h_rec[f.first], q, tab);
+            const float min_len = static_cast<float>(in.cluster_min_length);
+            std::atomic<int> next{0};
+            std::exception_ptr err;
+            std::mutex mu;
+            auto work = [&]() {
+                std::vector<int> q, tab;
+                for (int i; (i = next.fetch_add(1)) < (int)ids.size();) {
+                    const int c = ids[i];
+                    try {
+                        host_bfs_replay(hc.data() + (off[c] - lo), S.h_rec[c].n, g, hp.data(), np, min_len, S.h_rec[c], q,
+                                        tab);
+                    } catch (...) {
+                        std::lock_guard<std::mutex> lk(mu);
+                        if (!err) err = std::current_exception();
+                    }
+                }
+            };
+            const int nt = std::min<int>((int)ids.size(), kReplayThreads);
+            std::vector<std::thread> th;
+            for (int t = 1; t < nt; ++t) th.emplace_back(work);
+            work();
+            for (auto &t : th) t.join();
+            if (err) std::rethrow_exception(err);
         }
         // ---- tree rows in cluster order (convertClustersToTreeRows, seed_gen:1329-1406)
         int slot = 0;

@@ -17,6 +17,9 @@
 #include <climits>
 #include <cmath>
 #include <cstring>
+#include <exception>
+#include <limits>
+#include <thread>
 
 #include "aos_ctx.h"
 #include "subdiv2d.h"
@@ -508,12 +511,103 @@ static void scan_excl(DevBuf &tmpb, const int *in, int *out, int n, hipStream_t 
     AOS_HIP(hipcub::DeviceScan::ExclusiveSum(t, tb, in, out, n, s));
 }
 
+// publishMarkers' Voronoi cells (gvd:1098-1194): VoronoiDiagram::extractCellBoundaries
+// (voronoi_diagram.cpp:209-311), a second Subdiv2D over the finite merged seeds with their own
+// bounding box as the rectangle, then cell i = facet i (i < seeds, facets) with >= 3 points, closed
+// when its ends are more than 1 cm apart, paired with seeds_[i] and coloured from hue = i / cells.
+// Pure host work on the merged seeds: it runs on a worker thread next to the main replay.
+static void compute_cells(GvdState &G, int rect_mode) {
+    const auto t0 = std::chrono::steady_clock::now();
+    G.cell_off.assign(1, 0);
+    G.cell_xy.clear(); G.cell_center.clear(); G.cell_rgba.clear();
+    std::vector<double> seeds;   // VoronoiDiagram::seeds_ = the finite merged seeds
+    for (size_t i = 0; i + 1 < G.merged_xy.size(); i += 2)
+        if (std::isfinite(G.merged_xy[i]) && std::isfinite(G.merged_xy[i + 1])) {
+            seeds.push_back(G.merged_xy[i]); seeds.push_back(G.merged_xy[i + 1]);
+        }
+    const int ns = (int)seeds.size() / 2;
+    if (ns == 0) return;
+    double min_x = std::numeric_limits<double>::max(), max_x = std::numeric_limits<double>::lowest();
+    double min_y = min_x, max_y = max_x;
+    for (int i = 0; i < ns; ++i) {
+        min_x = std::min(min_x, seeds[2 * i]); max_x = std::max(max_x, seeds[2 * i]);
+        min_y = std::min(min_y, seeds[2 * i + 1]); max_y = std::max(max_y, seeds[2 * i + 1]);
+    }
+    if (max_x - min_x < 1.0) { double cx = (min_x + max_x) / 2.0; min_x = cx - 0.5; max_x = cx + 0.5; }
+    if (max_y - min_y < 1.0) { double cy = (min_y + max_y) / 2.0; min_y = cy - 0.5; max_y = cy + 0.5; }
+    const float rx = static_cast<float>(min_x - 1.0), ry = static_cast<float>(min_y - 1.0);
+    const float rw = static_cast<float>(std::abs(max_x - min_x) + 2.0), rh = static_cast<float>(std::abs(max_y - min_y) + 2.0);
+    if (rw <= 0 || rh <= 0) return;
+    Subdiv2D &sd = G.subdiv_cells;
+    sd.reserve(ns);
+    sd.init_delaunay(rx, ry, rw, rh, rect_mode);
+    const float margin = 0.1f;
+    for (int i = 0; i < ns; ++i) {
+        float x = static_cast<float>(seeds[2 * i]), y = static_cast<float>(seeds[2 * i + 1]);
+        x = std::max(rx + margin, std::min(rx + rw - margin, x));
+        y = std::max(ry + margin, std::min(ry + rh - margin, y));
+        sd.insert(x, y);   // insertion failures are skipped (voronoi_diagram.cpp:280-285)
+    }
+    std::vector<int> off;
+    std::vector<float> xy;
+    sd.voronoi_facets(off, xy);
+    const int nf = (int)off.size() - 1;
+    int ncell = 0;
+    for (int i = 0; i < ns && i < nf; ++i) {
+        const int b = off[i], n = off[i + 1] - b;
+        if (n < 3) continue;
+        for (int k = 0; k < n; ++k) { G.cell_xy.push_back(xy[2 * (b + k)]); G.cell_xy.push_back(xy[2 * (b + k) + 1]); }
+        const double dx = (double)xy[2 * b] - (double)xy[2 * (b + n - 1)], dy = (double)xy[2 * b + 1] - (double)xy[2 * (b + n - 1) + 1];
+        if (std::sqrt(dx * dx + dy * dy) > 0.01) { G.cell_xy.push_back(xy[2 * b]); G.cell_xy.push_back(xy[2 * b + 1]); }
+        G.cell_off.push_back((int32_t)(G.cell_xy.size() / 2));
+        ++ncell;
+    }
+    for (int i = 0; i < ncell; ++i) {   // gvd:1117-1145 (float arithmetic as written)
+        G.cell_center.push_back(seeds[2 * i]); G.cell_center.push_back(seeds[2 * i + 1]);
+        float hue = static_cast<float>(i) / std::max(1.0f, static_cast<float>(ncell));
+        float saturation = 0.7f, value = 0.9f;
+        float cc = value * saturation;
+        float x = cc * (1.0f - std::abs(std::fmod(hue * 6.0f, 2.0f) - 1.0f));
+        float m = value - cc;
+        float r = 0.0f, g = 0.0f, b = 0.0f;
+        if (hue < 1.0f / 6.0f) { r = cc; g = x; b = 0.0f; }
+        else if (hue < 2.0f / 6.0f) { r = x; g = cc; b = 0.0f; }
+        else if (hue < 3.0f / 6.0f) { r = 0.0f; g = cc; b = x; }
+        else if (hue < 4.0f / 6.0f) { r = 0.0f; g = x; b = cc; }
+        else if (hue < 5.0f / 6.0f) { r = x; g = 0.0f; b = cc; }
+        else { r = cc; g = 0.0f; b = x; }
+        G.cell_rgba.push_back(r + m); G.cell_rgba.push_back(g + m); G.cell_rgba.push_back(b + m); G.cell_rgba.push_back(0.4f);
+    }
+    G.ms_cells = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// The cells' worker thread of one GVD call; joined on every exit of run_gvd_stage.
+struct CellsJob {
+    std::thread t;
+    std::exception_ptr err;
+    void start(GvdState &G, int rect_mode) {
+        t = std::thread([this, &G, rect_mode]() {
+            try { compute_cells(G, rect_mode); } catch (...) { err = std::current_exception(); }
+        });
+    }
+    void finish(GvdState &G) {
+        if (t.joinable()) t.join();
+        if (err) { std::exception_ptr e = err; err = nullptr; std::rethrow_exception(e); }
+        G.have_markers = true;
+    }
+    ~CellsJob() { if (t.joinable()) t.join(); }
+};
+
 bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipStream_t s, hipEvent_t *ev) {
     GvdScratch &S = scratch(G);
     G.nodes_xy.clear(); G.labels.clear(); G.cluster_idx.clear(); G.label_counts.clear();
     G.label_clusters.clear(); G.label_types.clear(); G.edges_out.clear(); G.lengths.clear(); G.clearances.clear();
     G.n_merged = G.n_vor_edges = G.n_bpts = 0;
     G.ms_merge = G.ms_delaunay = G.ms_graph = G.ms_total = 0;
+    G.have_markers = false;
+    G.merged_xy.clear(); G.row_label_xy.clear(); G.row_label_valid.clear();
+    G.cell_off.assign(1, 0); G.cell_xy.clear(); G.cell_center.clear(); G.cell_rgba.clear(); G.ms_cells = 0;
+    CellsJob cells;
     int *h_sc = static_cast<int *>(G.h_misc.ensure(4096));
     const int n = in.n_seeds;
     AOS_HIP(hipEventRecord(ev[6], s));
@@ -562,6 +656,8 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     AOS_HIP(hipStreamSynchronize(s));
     G.n_merged = nl;
     AOS_HIP(hipEventRecord(ev[7], s));
+    G.merged_xy = merged;
+    if (P.gvd_markers) cells.start(G, P.subdiv_rect_mode);
 
     // ---- g3/g4 finite filter, bounds, Subdiv2D inserts (host replay) -> facets / Voronoi edges (GPU)
     auto t0 = std::chrono::steady_clock::now();
@@ -621,7 +717,10 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     G.ms_delaunay = std::chrono::duration<float, std::milli>(t1 - t0).count();
     G.n_vor_edges = ne;
     AOS_HIP(hipEventRecord(ev[8], s));
-    if (ne == 0) return true;  // no boundary points: an empty graph is still published
+    if (ne == 0) {   // no boundary points: an empty graph is still published
+        if (P.gvd_markers) cells.finish(G);
+        return true;
+    }
 
     // ---- g5 boundary points
     const int no = 2 * ne;
@@ -760,8 +859,14 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
         AOS_HIP(hipMemcpyAsync(G.edges_out.data(), d_edges, sizeof(int) * 2 * Ne, hipMemcpyDeviceToHost, s));
         AOS_HIP(hipMemcpyAsync(G.lengths.data(), d_lens, sizeof(float) * Ne, hipMemcpyDeviceToHost, s));
     }
+    G.row_label_xy.resize(2 * (size_t)nj); G.row_label_valid.resize(nj);
+    if (nj) {
+        AOS_HIP(hipMemcpyAsync(G.row_label_xy.data(), d_lp, sizeof(double2) * nj, hipMemcpyDeviceToHost, s));
+        AOS_HIP(hipMemcpyAsync(G.row_label_valid.data(), d_lv, sizeof(int) * nj, hipMemcpyDeviceToHost, s));
+    }
     AOS_HIP(hipEventRecord(ev[9], s));
     AOS_HIP(hipStreamSynchronize(s));
+    if (P.gvd_markers) cells.finish(G);
     float a = 0, b = 0;
     (void)hipEventElapsedTime(&a, ev[6], ev[7]);
     (void)hipEventElapsedTime(&b, ev[8], ev[9]);
@@ -790,6 +895,7 @@ static void fill_gvd_out(const aos_ctx &c, const GvdState &G, const aos_grid_inf
     out.edges = G.edges_out.data(); out.edge_lengths = G.lengths.data(); out.edge_clearances = G.clearances.data();
     out.n_merged_seeds = G.n_merged; out.n_voronoi_edges = G.n_vor_edges; out.n_boundary_points = G.n_bpts;
     out.ms_merge = G.ms_merge; out.ms_delaunay = G.ms_delaunay; out.ms_graph = G.ms_graph; out.ms_total = G.ms_total;
+    out.ms_cells = G.ms_cells;
     (void)c;
 }
 

@@ -234,8 +234,14 @@ Subdiv2D::Raw Subdiv2D::raw() {
     return Raw{qx.data(), n, reinterpret_cast<const float *>(vp.data()), vfirst.data(), vtype.data(), (int)vp.size()};
 }
 
-// calcVoronoi + getVoronoiFacetList on the exported layout (host reference of gvd.hip's builder).
-void Subdiv2D::voronoi_edges(std::vector<float> &edges) {
+// calcVoronoi on the exported layout (host reference of gvd.hip's builder): quad-edges from #4;
+// the first quad-edge touching a triangle computes its circumcentre (pt[3] left face, pt[1] right).
+int Subdiv2D::facet_next(int e) const {   // getEdge(e, NEXT_AROUND_LEFT = 0x13) on the exported layout
+    const int x = qx[8 * (size_t)(e >> 2) + ((e + 3) & 3)];
+    return (x & ~3) + ((x + 1) & 3);
+}
+
+void Subdiv2D::calc_voronoi() {
     raw();
     const int total = (int)rec.size();
     auto next = [&](int e) { return qx[8 * (size_t)(e >> 2) + (e & 3)]; };
@@ -269,23 +275,40 @@ void Subdiv2D::voronoi_edges(std::vector<float> &edges) {
             }
         }
     }
-    edges.clear();
-    std::vector<int> facet;
+}
+
+// getVoronoiFacetList: per real vertex (vertex order) the ring of Voronoi points, starting at
+// rotateEdge(firstEdge, 1) and walking NEXT_AROUND_LEFT; vtx[edgeOrg(t)] (index 0 = the (0,0)
+// NULL vertex when a circumcentre was not created).
+void Subdiv2D::voronoi_facets(std::vector<int> &off, std::vector<float> &xy) {
+    calc_voronoi();
+    off.assign(1, 0);
+    xy.clear();
     const size_t nv = vp.size();
     for (size_t k = 4; k < nv; k++) {
         if (vtype[k] != 0) continue;  // free or virtual
         const int f = vfirst[k], start = (f & ~3) + ((f + 1) & 3);
         int t = start;
-        facet.clear();
         do {
-            facet.push_back(pt(t));   // vtx[edgeOrg(t)] (index 0 = the (0,0) NULL vertex)
-            t = get_e(t, 0x13);
+            const int p = qx[8 * (size_t)(t >> 2) + 4 + (t & 3)];
+            xy.push_back(vp[p].x); xy.push_back(vp[p].y);
+            t = facet_next(t);
         } while (t != start);
-        const size_t n = facet.size();
+        off.push_back((int)(xy.size() / 2));
+    }
+}
+
+void Subdiv2D::voronoi_edges(std::vector<float> &edges) {
+    std::vector<int> off;
+    std::vector<float> xy;
+    voronoi_facets(off, xy);
+    edges.clear();
+    for (size_t f = 0; f + 1 < off.size(); ++f) {
+        const int b = off[f], n = off[f + 1] - b;
         if (n < 2) continue;
-        for (size_t i = 0; i < n; ++i) {
-            const int a = facet[i], b = facet[(i + 1) % n];
-            edges.push_back(vp[a].x); edges.push_back(vp[a].y); edges.push_back(vp[b].x); edges.push_back(vp[b].y);
+        for (int i = 0; i < n; ++i) {
+            const int a = b + i, c = b + (i + 1) % n;
+            edges.push_back(xy[2 * a]); edges.push_back(xy[2 * a + 1]); edges.push_back(xy[2 * c]); edges.push_back(xy[2 * c + 1]);
         }
     }
 }

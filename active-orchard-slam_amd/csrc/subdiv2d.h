@@ -36,6 +36,9 @@ class Subdiv2D {
     // Emits the reference's edge list directly: (p_i, p_{i+1 mod n}) for facets with >= 2 points
     // (voronoi_diagram.cpp:97-114), as float x0, y0, x1, y1. Host reference of the GPU builder.
     void voronoi_edges(std::vector<float> &edges);
+    // getVoronoiFacetList(idx = {}) as polygons: facet f (real vertices in vertex order) is the float
+    // points xy[2 * off[f] .. 2 * off[f + 1]) (extractCellBoundaries, voronoi_diagram.cpp:288-290).
+    void voronoi_facets(std::vector<int> &off, std::vector<float> &xy);
     size_t num_vertices() const { return vp.size(); }
     void reserve(size_t n_points);
     // OpenCV-layout quad-edge state after the inserts, for the GPU facet builder:
@@ -79,6 +82,8 @@ class Subdiv2D {
     void swap_edge(int e);
     void delete_edge(int e);
     int locate(float px, float py, int &edge, int &vertex);
+    void calc_voronoi();   // calcVoronoi on the exported layout (qx), creating the virtual vertices
+    int facet_next(int e) const;
 };
 
 }  // namespace aos

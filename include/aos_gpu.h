@@ -56,6 +56,8 @@ typedef struct aos_params {
     int32_t ror_min_neighbors;               /* 2   (hard-coded, seed_gen:239)           */
     int32_t subdiv_rect_mode;                /* 0: Subdiv2D(Rect2f); 1: Rect2f->Rect      */
     double max_graph_publish_rate;           /* 10 Hz (throttle is the wrapper's job)    */
+    int32_t gvd_markers;                     /* 1: also publishMarkers' Voronoi cells (gvd:1098-1194),
+                                                a second Subdiv2D on its own host thread */
 } aos_params;
 
 void aos_default_params(aos_params *p);
@@ -130,6 +132,7 @@ typedef struct aos_gvd_out {
     const float *edge_lengths, *edge_clearances;
     int32_t n_merged_seeds, n_voronoi_edges, n_boundary_points;
     float ms_merge, ms_delaunay, ms_graph, ms_total;
+    float ms_cells;                      /* publishMarkers' cells on the worker thread (gvd_markers) */
 } aos_gvd_out;
 
 const char *aos_last_error(void);
@@ -188,6 +191,22 @@ int aos_tile_plan_compute(const aos_params *p, const double *poly_xy, uint32_t n
  * ranks: info, thin_iters, n_clipped (whole map) and timings only. */
 int aos_tiled_seedgen_process(aos_ctx *ctx, const aos_comm *comm, int32_t tiles_x, int32_t tiles_y, int32_t root,
                               const aos_cloud_view *cloud, int want_host, aos_seedgen_out *out);
+
+/* /gvd/markers content of the last GVD call (publishMarkers gvd:1012-1591) that is not already in
+ * aos_gvd_out; the wrapper adds styles, ids and text. Needs aos_params.gvd_markers = 1. */
+typedef struct aos_gvd_markers {
+    int32_t n_seeds; const double *seeds_xy;   /* /gvd_voronoi_seeds: the merged seeds (gvd:1019-1041)        */
+    int32_t n_rows;                            /* exploration rows (sorted rows_info pairs)                   */
+    const double *row_label_xy;                /* TL, TR, BL, BR boundary points per row, (x, y) x 4          */
+    const int32_t *row_label_valid;            /* 4 per row (gvd:1370-1450 draws the valid ones)             */
+    int32_t n_cells;                           /* VoronoiDiagram::extractCellBoundaries voronoi_diagram.cpp:209-311 */
+    const int32_t *cell_offsets;               /* n_cells + 1, into cell_xy points                            */
+    const double *cell_xy;                     /* cell boundary, closed when its ends are > 1 cm apart        */
+    const double *cell_center_xy;              /* seeds_[i]: the centre publishMarkers pairs with cell i      */
+    const float *cell_rgba;                    /* /gvd_voronoi_cells i colour: HSV(i / n_cells, 0.7, 0.9), a 0.4 */
+    float ms_cells;                            /* host time of the cells' Subdiv2D + facets (parallel thread) */
+} aos_gvd_markers;
+int aos_gvd_markers_get(aos_ctx *ctx, aos_gvd_markers *out);
 
 /* Diagnostics: copy an internal device grid of the last frame to host as int8 {0,100} (or 0/1
  * for "opened"). which: "raster", "inflated", "opened", "skeleton_frameless". */

@@ -31,7 +31,7 @@ typedef struct orc_params {
     int32_t ror_min_neighbors;        /* seed_gen:239 (hard-coded 2)    */
     int32_t subdiv_rect_mode;         /* 0: Subdiv2D(Rect2f); 1: Rect2f -> Rect (cvRound) conversion */
     int32_t faithful_dead_work;       /* 1: also run work whose result is never read (CPU-cost parity) */
-    int32_t _pad;
+    int32_t markers;                  /* 1: also publishMarkers' extractCellBoundaries (gvd:1098-1194) */
 } orc_params;
 
 void orc_default_params(orc_params *p);
@@ -90,6 +90,8 @@ typedef struct orc_gvd_out {
     int32_t n_label_entries; const int32_t *node_label_clusters, *node_label_types;
     int32_t num_edges; const int32_t *edges; const float *edge_lengths, *edge_clearances;
     int32_t n_label_rows; const double *row_label_pts; const int32_t *row_label_valid;
+    /* markers (p->markers): extractCellBoundaries + the /gvd_voronoi_cells colours and centres */
+    int32_t n_cells; const int32_t *cell_offsets; const double *cell_xy, *cell_center_xy; const float *cell_rgba;
 } orc_gvd_out;
 
 void *orc_gvd_run(const orc_params *p, const orc_gvd_in *in, orc_gvd_out *out);

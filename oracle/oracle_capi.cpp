@@ -19,7 +19,7 @@ void orc_default_params(orc_params *p) {
     p->ror_min_neighbors = 2;
     p->subdiv_rect_mode = 0;
     p->faithful_dead_work = 0;
-    p->_pad = 0;
+    p->markers = 0;
 }
 
 void *orc_seedgen_run(const orc_params *p, const uint8_t *cloud, uint64_t n, uint32_t point_step, uint32_t ox,
@@ -110,6 +110,9 @@ void *orc_gvd_run(const orc_params *p, const orc_gvd_in *in, orc_gvd_out *out) {
     out->edge_lengths = R.lengths.data(); out->edge_clearances = R.clearances.data();
     out->n_label_rows = (int32_t)(R.row_label_valid.size() / 4);
     out->row_label_pts = R.row_label_pts.data(); out->row_label_valid = R.row_label_valid.data();
+    out->n_cells = R.cell_off.empty() ? 0 : (int32_t)R.cell_off.size() - 1;
+    out->cell_offsets = R.cell_off.data(); out->cell_xy = R.cell_xy.data();
+    out->cell_center_xy = R.cell_center.data(); out->cell_rgba = R.cell_rgba.data();
     return H;
 }
 

@@ -357,6 +357,52 @@ void voronoi_compute(const std::vector<V2> &seeds, double min_x, double max_x, d
     }
 }
 
+// VoronoiDiagram::extractCellBoundaries voronoi_diagram.cpp:209-311: a second Subdiv2D over the
+// seeds' own bounding box; cell i = facet i (i < seeds, facets) with >= 3 points, closed when its
+// ends are more than 1 cm apart. publishMarkers (gvd:1098-1194) pairs cell i with seeds_[i] and
+// colours it from hue = i / max(1, cells) (HSV, s = 0.7, v = 0.9, alpha 0.4), all in float.
+static void cell_markers(const std::vector<V2> &seeds, int rect_mode, GvdResult &R) {
+    R.cell_off.assign(1, 0);
+    if (seeds.empty()) return;
+    double min_x = std::numeric_limits<double>::max(), max_x = std::numeric_limits<double>::lowest();
+    double min_y = std::numeric_limits<double>::max(), max_y = std::numeric_limits<double>::lowest();
+    for (const auto &s : seeds)
+        if (std::isfinite(s.x) && std::isfinite(s.y)) {
+            min_x = std::min(min_x, s.x); max_x = std::max(max_x, s.x);
+            min_y = std::min(min_y, s.y); max_y = std::max(max_y, s.y);
+        }
+    if (min_x > max_x || min_y > max_y) return;
+    Facets f;
+    subdiv_voronoi_facets(seeds, min_x, max_x, min_y, max_y, rect_mode, f);   // same rect rules as compute()
+    std::vector<std::vector<V2>> cells;
+    for (size_t i = 0; i < seeds.size() && i < f.facets.size(); ++i) {
+        std::vector<V2> cp;
+        for (const auto &pt : f.facets[i]) cp.push_back(V2{pt.first, pt.second});
+        if (cp.size() >= 3) {
+            if (norm(cp.front() - cp.back()) > 0.01) cp.push_back(cp.front());
+            cells.push_back(cp);
+        }
+    }
+    for (size_t i = 0; i < cells.size(); ++i) {
+        for (const auto &v : cells[i]) { R.cell_xy.push_back(v.x); R.cell_xy.push_back(v.y); }
+        R.cell_off.push_back((int32_t)(R.cell_xy.size() / 2));
+        R.cell_center.push_back(seeds[i].x); R.cell_center.push_back(seeds[i].y);
+        float hue = static_cast<float>(i) / std::max(1.0f, static_cast<float>(cells.size()));
+        float saturation = 0.7f, value = 0.9f;
+        float c = value * saturation;
+        float x = c * (1.0f - std::abs(std::fmod(hue * 6.0f, 2.0f) - 1.0f));
+        float m = value - c;
+        float r = 0.0f, g = 0.0f, b = 0.0f;
+        if (hue < 1.0f / 6.0f) { r = c; g = x; b = 0.0f; }
+        else if (hue < 2.0f / 6.0f) { r = x; g = c; b = 0.0f; }
+        else if (hue < 3.0f / 6.0f) { r = 0.0f; g = c; b = x; }
+        else if (hue < 4.0f / 6.0f) { r = 0.0f; g = x; b = c; }
+        else if (hue < 5.0f / 6.0f) { r = x; g = 0.0f; b = c; }
+        else { r = c; g = 0.0f; b = x; }
+        R.cell_rgba.push_back(r + m); R.cell_rgba.push_back(g + m); R.cell_rgba.push_back(b + m); R.cell_rgba.push_back(0.4f);
+    }
+}
+
 // extractBoundaryPoints voronoi_diagram.cpp:149-207
 static std::vector<V2> extract_boundary_points(const std::vector<VEdge> &edges) {
     std::vector<V2> bp;
@@ -518,6 +564,7 @@ void gvd(const Params &P, const GvdInput &in, GvdResult &R) {
     double minx = g.minx(), maxx = g.maxx(), miny = g.miny(), maxy = g.maxy();
     if (!std::isfinite(minx) || !std::isfinite(maxx) || !std::isfinite(miny) || !std::isfinite(maxy)) return;
     voronoi_compute(all, minx, maxx, miny, maxy, P.subdiv_rect_mode, P.faithful_dead_work != 0, R.vor_edges, R.n_vertices_dead);
+    if (P.markers) cell_markers(all, P.subdiv_rect_mode, R);
     std::vector<V2> bp = extract_boundary_points(R.vor_edges);
     R.boundary_raw = bp;
 

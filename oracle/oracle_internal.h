@@ -77,6 +77,10 @@ struct GvdResult {
     std::vector<double> row_label_pts;
     std::vector<int32_t> row_label_valid;
     std::vector<double> flat_merged, flat_edges, flat_braw, flat_nodes;
+    // publishMarkers (P.markers): cells of extractCellBoundaries, closed like the reference
+    std::vector<int32_t> cell_off;
+    std::vector<double> cell_xy, cell_center;
+    std::vector<float> cell_rgba;
 };
 
 struct GvdInput {

@@ -25,7 +25,7 @@ class Params(ctypes.Structure):
     _fields_ = [("clip_minz", c_f), ("clip_maxz", c_f), ("clip_minx", c_f), ("clip_maxx", c_f),
                 ("clip_miny", c_f), ("clip_maxy", c_f), ("grid_resolution", c_f), ("inflation_radius", c_f),
                 ("cluster_min_length", c_d), ("ror_radius", c_d), ("ror_min_neighbors", c_i),
-                ("subdiv_rect_mode", c_i), ("faithful_dead_work", c_i), ("_pad", c_i)]
+                ("subdiv_rect_mode", c_i), ("faithful_dead_work", c_i), ("markers", c_i)]
 
 
 class SeedGenOut(ctypes.Structure):
@@ -55,7 +55,9 @@ class GvdOut(ctypes.Structure):
                 ("node_cluster_indices", P(c_i)), ("node_label_counts", P(c_i)), ("n_label_entries", c_i),
                 ("node_label_clusters", P(c_i)), ("node_label_types", P(c_i)), ("num_edges", c_i),
                 ("edges", P(c_i)), ("edge_lengths", P(c_f)), ("edge_clearances", P(c_f)),
-                ("n_label_rows", c_i), ("row_label_pts", P(c_d)), ("row_label_valid", P(c_i))]
+                ("n_label_rows", c_i), ("row_label_pts", P(c_d)), ("row_label_valid", P(c_i)),
+                ("n_cells", c_i), ("cell_offsets", P(c_i)), ("cell_xy", P(c_d)), ("cell_center_xy", P(c_d)),
+                ("cell_rgba", P(c_f))]
 
 
 def build_lib() -> str:
@@ -185,6 +187,11 @@ def gvd(seeds: np.ndarray, rows_info: np.ndarray, grid: dict, params: Params | N
             "row_label_pts": _arr(out.row_label_pts, 8 * out.n_label_rows, np.float64).reshape(-1, 4, 2),
             "row_label_valid": _arr(out.row_label_valid, 4 * out.n_label_rows, np.int32).reshape(-1, 4),
         }
+        nc = out.n_cells
+        off = _arr(out.cell_offsets, nc + 1, np.int32) if nc else np.zeros(1, np.int32)
+        r.update(cell_offsets=off, cell_xy=_arr(out.cell_xy, 2 * int(off[-1]), np.float64).reshape(-1, 2),
+                 cell_center=_arr(out.cell_center_xy, 2 * nc, np.float64).reshape(-1, 2),
+                 cell_rgba=_arr(out.cell_rgba, 4 * nc, np.float32).reshape(-1, 4))
     finally:
         lib().orc_free_gvd(h)
     return r

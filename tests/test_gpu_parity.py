@@ -282,3 +282,46 @@ def test_rotated_orchard_concave_polygon_and_odd_resolution():
 def test_grid_resolution_0_3_and_non_dense():
     cfg = orchard.CONFIGS["C0"]
     _full_frame_parity(orchard.generate(cfg, n_points=70000), orchard.polygon(cfg), 0.3, is_dense=False)
+
+
+# ---------------------------------------------------------------- /gvd/markers
+def _assert_markers(m, og):
+    assert np.array_equal(m["seeds"], og["merged"])
+    assert np.array_equal(m["row_label_valid"], og["row_label_valid"])
+    v = og["row_label_valid"].astype(bool)
+    assert np.array_equal(m["row_label_pts"][v], og["row_label_pts"][v])
+    assert np.array_equal(m["cell_offsets"], og["cell_offsets"])
+    assert np.array_equal(m["cell_xy"], og["cell_xy"]), "cell boundaries differ"
+    assert np.array_equal(m["cell_center"], og["cell_center"])
+    assert np.array_equal(m["cell_rgba"], og["cell_rgba"])
+
+
+@pytest.mark.parametrize("name", ["C0", "C1"])
+def test_gvd_markers_cells_vs_oracle(name):
+    """publishMarkers' Voronoi cells: extractCellBoundaries' second Subdiv2D (seed bounding box),
+    computed on a worker thread next to the main replay, plus the merged seeds and label points."""
+    cfg = orchard.CONFIGS[name]
+    c, g, o = run_both(cfg)
+    gg = c.gvd_from_seedgen()
+    m = c.gvd_markers()
+    og = O.gvd(o["voronoi_seeds"], o["rows_info"], o, O.default_params(grid_resolution=cfg.res, markers=1))
+    assert_gvd_parity(gg, og)
+    assert len(m["cell_offsets"]) > 100
+    _assert_markers(m, og)
+    c.close()
+
+
+def test_gvd_markers_external_input_and_disabled():
+    cfg = orchard.CONFIGS["C0"]
+    cloud, poly = orchard.generate(cfg), orchard.polygon(cfg)
+    o = O.seedgen(cloud, poly, O.default_params(grid_resolution=cfg.res))
+    og = O.gvd(o["voronoi_seeds"], o["rows_info"], o, O.default_params(grid_resolution=cfg.res, markers=1))
+    c = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res))
+    c.gvd(o["voronoi_seeds"], o["rows_info"], o)
+    _assert_markers(c.gvd_markers(), og)
+    c.close()
+    c = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res, gvd_markers=0))
+    c.gvd(o["voronoi_seeds"], o["rows_info"], o)
+    with pytest.raises(RuntimeError, match="no markers"):
+        c.gvd_markers()
+    c.close()
