@@ -212,15 +212,19 @@ int aos_tiled_seedgen_process(aos_ctx *c, const aos_comm *comm, int32_t tiles_x,
 int aos_gvd_markers_get(aos_ctx *c, aos_gvd_markers *out) {
     if (!c || !out) { set_error("aos_gvd_markers_get: null argument"); return AOS_E_INVALID; }
     const GvdState &G = c->gs;
-    if (!G.have_markers) { set_error("aos_gvd_markers_get: no markers (gvd_markers = 0 or no GVD frame)"); return AOS_E_STATE; }
+    if (!G.have_markers || !G.cells) {
+        set_error("aos_gvd_markers_get: no markers (gvd_markers = 0 or no GVD frame)");
+        return AOS_E_STATE;
+    }
+    const CellsWork &W = *G.cells;
     std::memset(out, 0, sizeof(*out));
     out->n_seeds = (int32_t)(G.merged_xy.size() / 2); out->seeds_xy = G.merged_xy.data();
     out->n_rows = (int32_t)(G.row_label_valid.size() / 4);
     out->row_label_xy = G.row_label_xy.data(); out->row_label_valid = G.row_label_valid.data();
-    out->n_cells = (int32_t)G.cell_off.size() - 1;
-    out->cell_offsets = G.cell_off.data(); out->cell_xy = G.cell_xy.data();
-    out->cell_center_xy = G.cell_center.data(); out->cell_rgba = G.cell_rgba.data();
-    out->ms_cells = G.ms_cells;
+    out->n_cells = (int32_t)W.cell_off.size() - 1;
+    out->cell_offsets = W.cell_off.data(); out->cell_xy = W.cell_xy.data();
+    out->cell_center_xy = W.cell_center.data(); out->cell_rgba = W.cell_rgba.data();
+    out->ms_cells = W.ms;
     return AOS_OK;
 }
 

@@ -1,5 +1,6 @@
 // Cluster / tree-row / seed stage and GVD stage state. Not part of the ABI.
 #pragma once
+#include <memory>
 #include <vector>
 
 #include "aos_internal.h"
@@ -68,6 +69,18 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
                             hipEvent_t ev_mid);
 
 // ------------------------------------------------------------------ GVD
+// publishMarkers' Voronoi cells, computed by a worker thread next to the main Subdiv2D replay. It
+// lives in its own cache-line-aligned heap object: the two replays write their state on every step,
+// and sharing lines with the main replay's fields slowed both down by ~40 % on the EPYC host.
+struct alignas(128) CellsWork {
+    Subdiv2D sd;                               // extractCellBoundaries' Subdiv2D
+    std::vector<double> seeds;                 // VoronoiDiagram::seeds_ (finite merged seeds)
+    std::vector<double> cell_xy, cell_center;
+    std::vector<int32_t> cell_off;
+    std::vector<float> cell_rgba;
+    float ms = 0;
+};
+
 struct GvdState {
     DedupScratch dedup;
     DevBuf seeds, merge_state, hash_count, hash_start, hash_slot, hash_sorted, scan_tmp, misc;
@@ -75,7 +88,6 @@ struct GvdState {
     PinnedBuf h_misc;
     void *scratch = nullptr;   // GvdScratch (gvd.hip), freed by free_gvd_scratch
     Subdiv2D subdiv;   // host insert replay; kept across frames to reuse its allocations
-    Subdiv2D subdiv_cells;   // publishMarkers' extractCellBoundaries (second replay, worker thread)
     // host outputs
     std::vector<double> nodes_xy;
     std::vector<int32_t> labels, cluster_idx, label_counts, label_clusters, label_types, edges_out;
@@ -84,10 +96,9 @@ struct GvdState {
     float ms_merge = 0, ms_delaunay = 0, ms_graph = 0, ms_total = 0;
     // markers (aos_gvd_markers)
     bool have_markers = false;
-    std::vector<double> merged_xy, row_label_xy, cell_xy, cell_center;
-    std::vector<int32_t> row_label_valid, cell_off;
-    std::vector<float> cell_rgba;
-    float ms_cells = 0;
+    std::vector<double> merged_xy, row_label_xy;
+    std::vector<int32_t> row_label_valid;
+    std::unique_ptr<CellsWork> cells;   // the worker thread's own heap object (no false sharing)
 };
 
 struct GvdStageIn {

@@ -516,15 +516,11 @@ static void scan_excl(DevBuf &tmpb, const int *in, int *out, int n, hipStream_t 
 // bounding box as the rectangle, then cell i = facet i (i < seeds, facets) with >= 3 points, closed
 // when its ends are more than 1 cm apart, paired with seeds_[i] and coloured from hue = i / cells.
 // Pure host work on the merged seeds: it runs on a worker thread next to the main replay.
-static void compute_cells(GvdState &G, int rect_mode) {
+static void compute_cells(CellsWork &W, int rect_mode) {
     const auto t0 = std::chrono::steady_clock::now();
-    G.cell_off.assign(1, 0);
-    G.cell_xy.clear(); G.cell_center.clear(); G.cell_rgba.clear();
-    std::vector<double> seeds;   // VoronoiDiagram::seeds_ = the finite merged seeds
-    for (size_t i = 0; i + 1 < G.merged_xy.size(); i += 2)
-        if (std::isfinite(G.merged_xy[i]) && std::isfinite(G.merged_xy[i + 1])) {
-            seeds.push_back(G.merged_xy[i]); seeds.push_back(G.merged_xy[i + 1]);
-        }
+    W.cell_off.assign(1, 0);
+    W.cell_xy.clear(); W.cell_center.clear(); W.cell_rgba.clear();
+    const std::vector<double> &seeds = W.seeds;   // VoronoiDiagram::seeds_ = the finite merged seeds
     const int ns = (int)seeds.size() / 2;
     if (ns == 0) return;
     double min_x = std::numeric_limits<double>::max(), max_x = std::numeric_limits<double>::lowest();
@@ -538,7 +534,7 @@ static void compute_cells(GvdState &G, int rect_mode) {
     const float rx = static_cast<float>(min_x - 1.0), ry = static_cast<float>(min_y - 1.0);
     const float rw = static_cast<float>(std::abs(max_x - min_x) + 2.0), rh = static_cast<float>(std::abs(max_y - min_y) + 2.0);
     if (rw <= 0 || rh <= 0) return;
-    Subdiv2D &sd = G.subdiv_cells;
+    Subdiv2D &sd = W.sd;
     sd.reserve(ns);
     sd.init_delaunay(rx, ry, rw, rh, rect_mode);
     const float margin = 0.1f;
@@ -556,14 +552,14 @@ static void compute_cells(GvdState &G, int rect_mode) {
     for (int i = 0; i < ns && i < nf; ++i) {
         const int b = off[i], n = off[i + 1] - b;
         if (n < 3) continue;
-        for (int k = 0; k < n; ++k) { G.cell_xy.push_back(xy[2 * (b + k)]); G.cell_xy.push_back(xy[2 * (b + k) + 1]); }
+        for (int k = 0; k < n; ++k) { W.cell_xy.push_back(xy[2 * (b + k)]); W.cell_xy.push_back(xy[2 * (b + k) + 1]); }
         const double dx = (double)xy[2 * b] - (double)xy[2 * (b + n - 1)], dy = (double)xy[2 * b + 1] - (double)xy[2 * (b + n - 1) + 1];
-        if (std::sqrt(dx * dx + dy * dy) > 0.01) { G.cell_xy.push_back(xy[2 * b]); G.cell_xy.push_back(xy[2 * b + 1]); }
-        G.cell_off.push_back((int32_t)(G.cell_xy.size() / 2));
+        if (std::sqrt(dx * dx + dy * dy) > 0.01) { W.cell_xy.push_back(xy[2 * b]); W.cell_xy.push_back(xy[2 * b + 1]); }
+        W.cell_off.push_back((int32_t)(W.cell_xy.size() / 2));
         ++ncell;
     }
     for (int i = 0; i < ncell; ++i) {   // gvd:1117-1145 (float arithmetic as written)
-        G.cell_center.push_back(seeds[2 * i]); G.cell_center.push_back(seeds[2 * i + 1]);
+        W.cell_center.push_back(seeds[2 * i]); W.cell_center.push_back(seeds[2 * i + 1]);
         float hue = static_cast<float>(i) / std::max(1.0f, static_cast<float>(ncell));
         float saturation = 0.7f, value = 0.9f;
         float cc = value * saturation;
@@ -576,9 +572,9 @@ static void compute_cells(GvdState &G, int rect_mode) {
         else if (hue < 4.0f / 6.0f) { r = 0.0f; g = x; b = cc; }
         else if (hue < 5.0f / 6.0f) { r = x; g = 0.0f; b = cc; }
         else { r = cc; g = 0.0f; b = x; }
-        G.cell_rgba.push_back(r + m); G.cell_rgba.push_back(g + m); G.cell_rgba.push_back(b + m); G.cell_rgba.push_back(0.4f);
+        W.cell_rgba.push_back(r + m); W.cell_rgba.push_back(g + m); W.cell_rgba.push_back(b + m); W.cell_rgba.push_back(0.4f);
     }
-    G.ms_cells = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    W.ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
 // The cells' worker thread of one GVD call; joined on every exit of run_gvd_stage.
@@ -586,8 +582,15 @@ struct CellsJob {
     std::thread t;
     std::exception_ptr err;
     void start(GvdState &G, int rect_mode) {
-        t = std::thread([this, &G, rect_mode]() {
-            try { compute_cells(G, rect_mode); } catch (...) { err = std::current_exception(); }
+        if (!G.cells) G.cells.reset(new CellsWork());
+        CellsWork &W = *G.cells;
+        W.seeds.clear();
+        for (size_t i = 0; i + 1 < G.merged_xy.size(); i += 2)
+            if (std::isfinite(G.merged_xy[i]) && std::isfinite(G.merged_xy[i + 1])) {
+                W.seeds.push_back(G.merged_xy[i]); W.seeds.push_back(G.merged_xy[i + 1]);
+            }
+        t = std::thread([this, &W, rect_mode]() {
+            try { compute_cells(W, rect_mode); } catch (...) { err = std::current_exception(); }
         });
     }
     void finish(GvdState &G) {
@@ -606,7 +609,7 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     G.ms_merge = G.ms_delaunay = G.ms_graph = G.ms_total = 0;
     G.have_markers = false;
     G.merged_xy.clear(); G.row_label_xy.clear(); G.row_label_valid.clear();
-    G.cell_off.assign(1, 0); G.cell_xy.clear(); G.cell_center.clear(); G.cell_rgba.clear(); G.ms_cells = 0;
+    if (G.cells) { G.cells->cell_off.assign(1, 0); G.cells->ms = 0; }
     CellsJob cells;
     int *h_sc = static_cast<int *>(G.h_misc.ensure(4096));
     const int n = in.n_seeds;
@@ -895,7 +898,7 @@ static void fill_gvd_out(const aos_ctx &c, const GvdState &G, const aos_grid_inf
     out.edges = G.edges_out.data(); out.edge_lengths = G.lengths.data(); out.edge_clearances = G.clearances.data();
     out.n_merged_seeds = G.n_merged; out.n_voronoi_edges = G.n_vor_edges; out.n_boundary_points = G.n_bpts;
     out.ms_merge = G.ms_merge; out.ms_delaunay = G.ms_delaunay; out.ms_graph = G.ms_graph; out.ms_total = G.ms_total;
-    out.ms_cells = G.ms_cells;
+    out.ms_cells = G.cells ? G.cells->ms : 0.0f;
     (void)c;
 }
 
