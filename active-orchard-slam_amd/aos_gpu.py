@@ -55,7 +55,8 @@ class SeedGenOut(ctypes.Structure):
                 ("n_virtual", c_i), ("n_ray", c_i), ("n_endpoint", c_i), ("n_voronoi", c_i), ("voronoi_xy", P(c_d)),
                 ("rows_info_xy", P(c_d)), ("n_cluster_info", c_i), ("cluster_info_xy", P(c_d)),
                 ("ms_ror", c_f), ("ms_grid", c_f), ("ms_thin", c_f), ("ms_cluster", c_f), ("ms_seeds", c_f),
-                ("ms_total", c_f), ("n_binned", ctypes.c_uint64), ("ms_ror_count", c_f)]
+                ("ms_total", c_f), ("n_binned", ctypes.c_uint64), ("ms_ror_count", c_f),
+                ("ms_ror_bin", c_f), ("ms_ror_scatter", c_f)]
 
 
 class GvdIn(ctypes.Structure):
@@ -171,7 +172,8 @@ def _seedgen_dict(o: SeedGenOut, want_host: bool) -> dict:
         "cluster_info": _arr(o.cluster_info_xy, 2 * o.n_cluster_info, np.float64).reshape(-1, 2),
         "d_occupancy": o.d_occupancy, "d_skeleton": o.d_skeleton,
         "ms": {"ror": o.ms_ror, "grid": o.ms_grid, "thin": o.ms_thin, "cluster": o.ms_cluster, "seeds": o.ms_seeds,
-               "total": o.ms_total, "ror_count": o.ms_ror_count},
+               "total": o.ms_total, "ror_count": o.ms_ror_count,
+               "ror_bin": o.ms_ror_bin, "ror_scatter": o.ms_ror_scatter},
         "n_binned": o.n_binned,
     }
     nv, nrr = o.n_virtual, o.n_ray

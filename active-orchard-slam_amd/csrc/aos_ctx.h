@@ -10,7 +10,7 @@ struct aos_ctx {
     aos_params P{};
     int device = 0;
     hipStream_t stream = nullptr;
-    std::array<hipEvent_t, 12> ev{};
+    std::array<hipEvent_t, 16> ev{};
     aos::Poly poly;
 
     // ---- last cloud (reprocess reuses it: seed_gen:244, 283-285)

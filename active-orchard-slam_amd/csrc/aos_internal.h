@@ -79,7 +79,7 @@ struct RorLaunch {
     const uint8_t *cloud; uint64_t n; uint32_t step, ox, oy, oz; int is_dense;
     float bminx, bminy, bminz, bmaxx, bmaxy, bmaxz, inv_cs; int nbx, nby;
     float cminx, cmaxx, cminy, cmaxy, cminz, cmaxz;
-    double r2; float r2f; int need;
+    double r2; float r2f, r2df; int need;   // r2df: largest float f with (double)f <= r2
     double origin_x, origin_y; float res; int W, H;
     // Ownership (tiled frames, tiled.hip): a kept candidate is counted iff its cell, clamped to the
     // grid, lies in [rx0, rx1) x [ry0, ry1); it is rastered (if inside the grid) into the byte window
@@ -88,6 +88,8 @@ struct RorLaunch {
 };
 void launch_ror_bin(const RorLaunch &L, int *bin_count, int2 *pt_binslot, hipStream_t s);
 void launch_ror_scatter(const RorLaunch &L, const int *bin_start, const int2 *pt_binslot, float4 *sorted, hipStream_t s);
+void launch_ror_count(const RorLaunch &L, int *bin_count, hipStream_t s);
+void launch_ror_place(const RorLaunch &L, int *cursor, float4 *sorted, hipStream_t s);
 void launch_ror_raster(const RorLaunch &L, const int *bin_start, const float4 *sorted, uint8_t *raster,
                        unsigned long long *counters, hipStream_t s);
 void launch_pack_bits(const uint8_t *bytes, uint64_t *bits, int W, int H, int WW, hipStream_t s);

@@ -117,7 +117,8 @@ __device__ __forceinline__ bool ror_in(const RorLaunch &L, float4 p, float4 q) {
     float d2 = dx * dx;
     d2 = d2 + dy * dy;
     d2 = d2 + dz * dz;
-    return L.is_dense ? ((double)d2 <= L.r2) : (d2 < L.r2f);
+    // dense: (double)d2 <= r2 is the same test as d2 <= r2df for every float d2 (incl. inf / NaN)
+    return L.is_dense ? (d2 <= L.r2df) : (d2 < L.r2f);
 }
 template <class Ptr>
 __device__ __forceinline__ int ror_scan(const RorLaunch &L, float4 p, Ptr pts, int k0, int k1, int cnt) {
@@ -250,6 +251,100 @@ __global__ __launch_bounds__(kSwTB) void k_ror_sweep(RorLaunch L, const int *bin
     // hot address would serialise ~10^5 same-address atomics in one L2 channel
 }
 
+// Kept candidate: count it if its (clamped) cell is owned, raster it if inside the grid.
+__device__ __forceinline__ void ror_keep(const RorLaunch &L, float4 p, uint8_t *raster, unsigned &kept_n) {
+    int gx = (int)(((double)p.x - L.origin_x) / (double)L.res);
+    int gy = (int)(((double)p.y - L.origin_y) / (double)L.res);
+    const int cx = min(max(gx, 0), L.W - 1), cy = min(max(gy, 0), L.H - 1);
+    if (cx >= L.rx0 && cx < L.rx1 && cy >= L.ry0 && cy < L.ry1) {
+        ++kept_n;
+        if (!AOS_ROR_NOSTORE && gx >= 0 && gx < L.W && gy >= 0 && gy < L.H)
+            raster[(size_t)(gy - L.wy0) * L.Wr + (gx - L.wx0)] = 1;
+    }
+}
+
+// Direct variant: one thread per staged point, in bin order, reading the 3 x 3 neighbour bins
+// straight from global memory (consecutive lanes scan nearly the same ranges, so the loads hit
+// the same cache lines). No LDS, no barriers: occupancy is bounded by registers only.
+__global__ __launch_bounds__(256) void k_ror_direct(RorLaunch L, const int *bin_start, const float4 *sorted,
+                                                    const int *n_binned, uint8_t *raster,
+                                                    unsigned long long *counters) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned kept_n = 0;
+    if (i < *n_binned) {
+        const float4 p = sorted[i];
+        if (__float_as_int(p.w)) {
+            int bx, by;
+            bin_of(L, p.x, p.y, bx, by);
+            const int c0 = max(bx - 1, 0), c1 = min(bx + 1, L.nbx - 1);
+            int cnt = AOS_ROR_NOSCAN ? L.need : 0;
+#if AOS_ROR_DIRECT == 2
+            // the point itself (d2 = 0 passes both tests), then its own bin around it, then the
+            // other 8 bins: the own bin holds the likeliest neighbours, so most scans stop early
+            const int ob = by * L.nbx + bx, b0 = bin_start[ob], b1 = bin_start[ob + 1];
+            cnt = 1;
+            cnt = ror_scan(L, p, sorted, i + 1, b1, cnt);
+            cnt = ror_scan(L, p, sorted, b0, i, cnt);
+            if (cnt < L.need) cnt = ror_scan(L, p, sorted, bin_start[by * L.nbx + c0], b0, cnt);
+            if (cnt < L.need) cnt = ror_scan(L, p, sorted, b1, bin_start[by * L.nbx + c1 + 1], cnt);
+            for (int rr = 1; rr < 3; ++rr) {
+                const int yy = rr == 1 ? by - 1 : by + 1;
+                if (yy < 0 || yy >= L.nby || cnt >= L.need) continue;
+                cnt = ror_scan(L, p, sorted, bin_start[yy * L.nbx + c0], bin_start[yy * L.nbx + c1 + 1], cnt);
+            }
+#else
+#pragma unroll
+            for (int rr = 0; rr < 3; ++rr) {
+                const int yy = rr == 0 ? by : (rr == 1 ? by - 1 : by + 1);   // own bin row first
+                if (yy < 0 || yy >= L.nby || cnt >= L.need) continue;
+                cnt = ror_scan(L, p, sorted, bin_start[yy * L.nbx + c0], bin_start[yy * L.nbx + c1 + 1], cnt);
+            }
+#endif
+            if (cnt >= L.need) ror_keep(L, p, raster, kept_n);
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) kept_n += __shfl_xor(kept_n, o);
+    if ((threadIdx.x & 63) == 0 && kept_n)
+        atomicAdd(&counters[(blockIdx.x * 4 + (threadIdx.x >> 6)) & (kRorCounters - 1)], (unsigned long long)kept_n);
+}
+
+// Counting sort without a per-point slot array: k_ror_count counts points per bin with
+// non-returning atomics (fire and forget), the exclusive scan is written one element to the right
+// (cursor[1 + b] = start of bin b), and k_ror_place claims each point's position with a returning
+// atomic on that cursor. After the placement cursor[b] = start of bin b for every b <= nb, i.e.
+// the cursor array IS bin_start. Order inside a bin is arbitrary, as before (the ROR decision is
+// order-free).
+__global__ void k_ror_count(RorLaunch L, int *bin_count) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= L.n) return;
+    float x, y, z;
+    load_xyz(L, i, x, y, z);
+    if (binned(L, x, y, z)) {
+        int bx, by;
+        atomicAdd(&bin_count[bin_of(L, x, y, bx, by)], 1);
+    }
+}
+
+__global__ void k_ror_place(RorLaunch L, int *cursor, float4 *sorted) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= L.n) return;
+    float x, y, z;
+    load_xyz(L, i, x, y, z);
+    if (!binned(L, x, y, z)) return;
+    int bx, by;
+    const int pos = atomicAdd(&cursor[1 + bin_of(L, x, y, bx, by)], 1);
+    sorted[pos] = make_float4(x, y, z, __int_as_float(candidate(L, x, y, z) ? 1 : 0));
+}
+
+void launch_ror_count(const RorLaunch &L, int *bin_count, hipStream_t s) {
+    if (!L.n) return;
+    k_ror_count<<<cdiv(L.n, 256), 256, 0, s>>>(L, bin_count);
+}
+void launch_ror_place(const RorLaunch &L, int *cursor, float4 *sorted, hipStream_t s) {
+    if (!L.n) return;
+    k_ror_place<<<cdiv(L.n, 256), 256, 0, s>>>(L, cursor, sorted);
+}
+
 void launch_ror_bin(const RorLaunch &L, int *bin_count, int2 *pt_binslot, hipStream_t s) {
     if (!L.n) return;
     k_ror_bin<<<cdiv(L.n, 256), 256, 0, s>>>(L, bin_count, pt_binslot);
@@ -258,8 +353,16 @@ void launch_ror_scatter(const RorLaunch &L, const int *bin_start, const int2 *pt
     if (!L.n) return;
     k_ror_scatter<<<cdiv(L.n, 256), 256, 0, s>>>(L, bin_start, pt_binslot, sorted);
 }
+#ifndef AOS_ROR_DIRECT
+#define AOS_ROR_DIRECT 1
+#endif
 void launch_ror_raster(const RorLaunch &L, const int *bin_start, const float4 *sorted, uint8_t *raster,
                        unsigned long long *counters, hipStream_t s) {
+    if (AOS_ROR_DIRECT) {
+        if (!L.n) return;
+        k_ror_direct<<<cdiv(L.n, 256), 256, 0, s>>>(L, bin_start, sorted, bin_start + L.nbx * L.nby, raster, counters);
+        return;
+    }
     const long long nblk = (long long)((L.nby + kSwSeg - 1) / kSwSeg) * ((L.nbx + kSwSW - 1) / kSwSW);
     if (nblk <= 0) return;
     if (nblk > INT_MAX) throw std::runtime_error("ROR bin grid too large");

@@ -8,6 +8,10 @@
 
 #include "aos_ctx.h"
 
+#ifndef AOS_ROR_BIN2
+#define AOS_ROR_BIN2 0
+#endif
+
 using namespace aos;
 
 void aos_ctx::release() {
@@ -116,6 +120,8 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o) {
     L.nby = std::max(1, (int)((L.bmaxy - L.bminy) * L.inv_cs) + 1);
     L.r2 = P.ror_radius * P.ror_radius;
     L.r2f = (float)(P.ror_radius * P.ror_radius);
+    L.r2df = (float)L.r2;
+    if ((double)L.r2df > L.r2) L.r2df = std::nextafter(L.r2df, 0.0f);
     L.need = P.ror_min_neighbors + 1;
     L.origin_x = g.origin_x; L.origin_y = g.origin_y; L.res = g.res; L.W = g.W; L.H = g.H;
     L.rx0 = o.rx0; L.ry0 = o.ry0; L.rx1 = o.rx1; L.ry1 = o.ry1; L.wx0 = o.wx0; L.wy0 = o.wy0; L.Wr = o.Wr;
@@ -137,11 +143,24 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o) {
     // no keepable candidate either: the local test is exact.
     const bool any = n_points > 0 && !(is_dense && n_points < (uint64_t)L.need);
     if (any) {
-        launch_ror_bin(L, d_bc, d_ps, s);
-        launch_exclusive_scan(d_bc, d_bs, nb + 1, d_st, st, s);
         // total binned = bin_start[nb]; bound the sorted buffer by n_points
         float4 *d_sorted = static_cast<float4 *>(sorted.ensure(sizeof(float4) * std::max<uint64_t>(n_points, 1)));
+        AOS_HIP(hipEventRecord(ev[12], s));
+#if AOS_ROR_BIN2
+        (void)d_ps;
+        launch_ror_count(L, d_bc, s);
+        AOS_HIP(hipEventRecord(ev[13], s));
+        AOS_HIP(hipMemsetAsync(d_bs, 0, sizeof(int), s));
+        launch_exclusive_scan(d_bc, d_bs + 1, nb, d_st, st, s);   // cursor[1 + b] = start of bin b
+        AOS_HIP(hipEventRecord(ev[14], s));
+        launch_ror_place(L, d_bs, d_sorted, s);                    // afterwards d_bs[b] = start of bin b
+#else
+        launch_ror_bin(L, d_bc, d_ps, s);
+        AOS_HIP(hipEventRecord(ev[13], s));
+        launch_exclusive_scan(d_bc, d_bs, nb + 1, d_st, st, s);
+        AOS_HIP(hipEventRecord(ev[14], s));
         launch_ror_scatter(L, d_bs, d_ps, d_sorted, s);
+#endif
         AOS_HIP(hipEventRecord(ev[10], s));
         launch_ror_raster(L, d_bs, d_sorted, d_rb, d_cnt, s);
         AOS_HIP(hipEventRecord(ev[11], s));
@@ -305,6 +324,8 @@ void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *c
     out.ms_seeds = ms(4, 5); out.ms_total = ms(0, 5);
     out.n_binned = static_cast<const int *>(h_stats.p)[0];
     out.ms_ror_count = out.n_binned ? ms(10, 11) : 0.0f;
+    out.ms_ror_bin = out.n_binned ? ms(12, 13) : 0.0f;
+    out.ms_ror_scatter = out.n_binned ? ms(14, 10) : 0.0f;
 }
 
 int aos_ctx::debug_grid(const char *which, int8_t *dst, uint64_t capacity) {

@@ -294,4 +294,6 @@ void aos_ctx::run_tiled(const aos_comm &cm, int tiles_x, int tiles_y, int root, 
     out.ms_ror = ms(0, 1); out.ms_grid = ms(1, 2); out.ms_thin = ms(2, 3); out.ms_total = ms(0, 3);
     out.n_binned = static_cast<const int *>(h_stats.p)[0];
     out.ms_ror_count = out.n_binned ? ms(10, 11) : 0.0f;
+    out.ms_ror_bin = out.n_binned ? ms(12, 13) : 0.0f;
+    out.ms_ror_scatter = out.n_binned ? ms(14, 10) : 0.0f;
 }

@@ -24,8 +24,7 @@ for sub in ("tools", "active-orchard-slam_amd"):
     sys.path.insert(0, os.path.join(ROOT, sub))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-DOMINANT = "k_ror_sweep"
-PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r01_k_pmc_traffic.json")
 
 
 def parse(argv=None):
@@ -188,20 +187,33 @@ def main():
     value = throughput(cells / 1e6, 1 if a.tiled else world, len(res), dt)
     avg = {k: v / len(res) for k, v in stage.items()}
 
-    # roofline of the dominant GPU kernel (largest share of device time per frame in the committed
-    # rocprofv3 summary): k_ror_sweep, the ROR neighbour count + raster over LDS-staged bin rows.
-    # Algorithmic bytes per launch: each staged point record read once (float4, 16 B)
-    # + one raster byte per kept candidate. Timed live: HIP events around that single launch on the
-    # handle's stream (aos_seedgen_out.ms_ror_count), averaged over the timed steps.
-    # (tiled: rank 0's launch; its share of the kept candidates is not reported, so only the 16 B/point term)
-    alg = 16.0 * g["n_binned"] + (0.0 if a.tiled else float(g["n_clipped"]))
-    ms_k = avg["seedgen_ror_count"]
-    achieved = alg / (ms_k * 1e-3) / 1e9 if ms_k > 0 else 0.0
-    traffic, src = pmc_traffic(DOMINANT)
-    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": DOMINANT, "alg_bytes_per_launch": alg, "ms_per_launch": round(ms_k, 4),
-            "units_per_launch": g["n_binned"], "traffic_source": src}
+    # roofline of the dominant GPU kernel: the largest per-frame device time among the three ROR
+    # kernels (bin, scatter, neighbour count), timed live with HIP events recorded on the handle's
+    # stream around each single launch (aos_seedgen_out.ms_ror_*), averaged over the timed steps.
+    # Algorithmic bytes per launch, N = input points, Nb = binned (staged) points:
+    #   k_ror_bin     16 N (cloud record) + 8 N (bin/slot pair) + 8 Nb (bin counter read-modify-write)
+    #   k_ror_scatter 8 N (bin/slot pair) + 16 Nb (cloud record) + 4 Nb (bin start) + 16 Nb (staged write)
+    #   k_ror_direct  16 Nb (staged point, read once) + 1 B per kept candidate (raster byte)
+    nb_pts = float(g["n_binned"])
+    n_all = float(cfg.n_points if a.tiled else n)
+    kept = 0.0 if a.tiled else float(g["n_clipped"])   # (tiled: rank 0's share is not reported)
+    kernels = {
+        "k_ror_bin": (24.0 * n_all + 8.0 * nb_pts, avg["seedgen_ror_bin"], n_all),
+        "k_ror_scatter": (8.0 * n_all + 36.0 * nb_pts, avg["seedgen_ror_scatter"], n_all),
+        "k_ror_direct": (16.0 * nb_pts + kept, avg["seedgen_ror_count"], nb_pts),
+    }
+    per_kernel = {}
+    for k, (alg_b, ms_k, units) in kernels.items():
+        ach = alg_b / (ms_k * 1e-3) / 1e9 if ms_k > 0 else 0.0
+        per_kernel[k] = {"ms_per_launch": round(ms_k, 4), "alg_bytes_per_launch": alg_b, "achieved_GBs": round(ach, 1),
+                         "frac": round(ach / HBM_PEAK_GBS, 4), "units_per_launch": units}
+    dom = max(per_kernel, key=lambda k: per_kernel[k]["ms_per_launch"])
+    traffic, src = pmc_traffic(dom)
+    pk = per_kernel[dom]
+    roof = {"bound": "hbm", "achieved": pk["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": pk["frac"], "traffic": traffic, "kernel": dom, "alg_bytes_per_launch": pk["alg_bytes_per_launch"],
+            "ms_per_launch": pk["ms_per_launch"], "units_per_launch": pk["units_per_launch"], "traffic_source": src,
+            "ror_kernels": per_kernel}
     # BASELINE.md frame-level figure: B_alg = 12 N + C (6 + 4 T) over the whole frame wall-clock
     T = g["thin_iters"]
     b_frame = 12.0 * (cfg.n_points if a.tiled else n) + cells * (6.0 + 4.0 * T)

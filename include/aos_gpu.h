@@ -109,6 +109,7 @@ typedef struct aos_seedgen_out {
      * its own device time, HIP events on the handle's stream around that single launch */
     uint64_t n_binned;
     float ms_ror_count;
+    float ms_ror_bin, ms_ror_scatter;    /* the two counting-sort kernels before it, same events */
 } aos_seedgen_out;
 
 /* GVD inputs when not fed from this handle's seed-gen frame. */
