@@ -30,7 +30,7 @@ enum ConflictMode {
 };
 struct HashG { double x0, y0, inv; int nx, ny; };
 HashG make_hash(double minx, double maxx, double miny, double maxy, double cell);
-struct DedupScratch { DevBuf keys, idx, skeys, sidx, ccount, coff, clist, state, f, pos, tmp, und; int n_conf = 0; };
+struct DedupScratch { DevBuf keys, idx, skeys, sidx, ccount, coff, clist, state, f, pos, tmp, und, rows; int n_conf = 0; };
 // cand/ok device arrays of n entries; kept points (in order) -> out; optional kept flags -> state (S.state).
 // Returns the kept count.
 int greedy_dedup(DedupScratch &S, const double2 *cand, const int *ok, int n, int mode, double thr, const HashG &h,

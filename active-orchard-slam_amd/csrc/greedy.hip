@@ -69,9 +69,22 @@ __device__ __forceinline__ int lower_bound_key(const int *keys, int n, int k) {
     return lo;
 }
 
+__device__ __forceinline__ int lower_bound_in(const int *keys, int lo, int hi, int k) {
+    while (lo < hi) { int m = (lo + hi) >> 1; if (keys[m] < k) lo = m + 1; else hi = m; }
+    return lo;
+}
+
+// First sorted index of every hash row (cell ids are row-major): narrows each cell lookup of
+// k_conflicts from a binary search over all n keys (~17 dependent loads) to one over one row's keys.
+__global__ void k_row_starts(const int *skeys, int n, HashG h, int *rowstart) {
+    const int yy = blockIdx.x * blockDim.x + threadIdx.x;
+    if (yy <= h.ny) rowstart[yy] = lower_bound_key(skeys, n, yy * h.nx);
+}
+
 // coff == nullptr: count pass; else fill pass
 __global__ void k_conflicts(const double2 *p, const int *ok, int n, HashG h, const int *skeys, const int *sidx,
-                            int mode, double thr, const int *coff, int *ccount, int *clist, long long cap) {
+                            const int *rowstart, int mode, double thr, const int *coff, int *ccount, int *clist,
+                            long long cap) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     if (!ok[i]) { if (!coff) ccount[i] = 0; return; }
@@ -80,8 +93,9 @@ __global__ void k_conflicts(const double2 *p, const int *ok, int n, HashG h, con
     const double2 pi = p[i];
     int c = 0, w = coff ? coff[i] : 0;
     for (int yy = max(cy - 1, 0); yy <= min(cy + 1, h.ny - 1); ++yy) {
-        int k0 = lower_bound_key(skeys, n, yy * h.nx + max(cx - 1, 0));
-        int k1 = lower_bound_key(skeys, n, yy * h.nx + min(cx + 1, h.nx - 1) + 1);
+        const int hi = rowstart[yy + 1];
+        const int k0 = lower_bound_in(skeys, rowstart[yy], hi, yy * h.nx + max(cx - 1, 0));
+        const int k1 = lower_bound_in(skeys, k0, hi, yy * h.nx + min(cx + 1, h.nx - 1) + 1);
         for (int k = k0; k < k1; ++k) {
             int j = sidx[k];
             if (j < i && conflict(pi, p[j], mode, thr)) {
@@ -100,8 +114,11 @@ __global__ void k_greedy_init(const int *ok, int n, int *state) {
 // One round over all undecided candidates, any number of workgroups. States are read with
 // agent-scope loads (another workgroup may have decided a predecessor in this very round); a
 // stale read only postpones a decision to a later round. undecided[0] counts candidates still
-// undecided when this round looked at them: 0 means the set is complete.
-__global__ void k_greedy_round(int n, const int *coff, const int *clist, int *state, int *undecided) {
+// undecided when this round looked at them: 0 means the set is complete, and the later rounds of a
+// batch (prev_undecided = the previous round's counter) return at once.
+__global__ void k_greedy_round(int n, const int *coff, const int *clist, int *state, int *undecided,
+                               const int *prev_undecided) {
+    if (prev_undecided && *prev_undecided == 0) return;
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     bool und = false;
     if (i < n && __hip_atomic_load(&state[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
@@ -144,8 +161,10 @@ int greedy_dedup(DedupScratch &S, const double2 *cand, const int *ok, int n, int
     void *tmp = S.tmp.ensure(std::max(tb, tb2));
     AOS_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys, skeys, idx, sidx, n, 0, 32, s));
     int *ccount = dev<int>(S.ccount, n + 1), *coff = dev<int>(S.coff, n + 1);
+    int *rows = dev<int>(S.rows, (size_t)h.ny + 1);
+    k_row_starts<<<cdiv(h.ny + 1, 256), 256, 0, s>>>(skeys, n, h, rows);
     AOS_HIP(hipMemsetAsync(ccount + n, 0, sizeof(int), s));
-    k_conflicts<<<cdiv(n, 256), 256, 0, s>>>(cand, ok, n, h, skeys, sidx, mode, thr, nullptr, ccount, nullptr, 0);
+    k_conflicts<<<cdiv(n, 256), 256, 0, s>>>(cand, ok, n, h, skeys, sidx, rows, mode, thr, nullptr, ccount, nullptr, 0);
     AOS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, ccount, coff, n + 1, s));
     // Optimistic capacity for the conflict lists (no read-back of the exact total before the rounds):
     // the total comes back with the first round batch; on overflow the lists are rebuilt exactly.
@@ -156,7 +175,7 @@ int greedy_dedup(DedupScratch &S, const double2 *cand, const int *ok, int n, int
     constexpr int kBatch = 6;
     int *und = dev<int>(S.und, kBatch);
     auto fill = [&]() {
-        k_conflicts<<<cdiv(n, 256), 256, 0, s>>>(cand, ok, n, h, skeys, sidx, mode, thr, coff, nullptr, clist, cap);
+        k_conflicts<<<cdiv(n, 256), 256, 0, s>>>(cand, ok, n, h, skeys, sidx, rows, mode, thr, coff, nullptr, clist, cap);
         k_greedy_init<<<cdiv(n, 256), 256, 0, s>>>(ok, n, state);
     };
     fill();
@@ -164,7 +183,8 @@ int greedy_dedup(DedupScratch &S, const double2 *cand, const int *ok, int n, int
     for (int done_rounds = 0;;) {
         // a batch of rounds, then (speculatively) the compaction of the kept set, one read-back
         AOS_HIP(hipMemsetAsync(und, 0, sizeof(int) * kBatch, s));
-        for (int r = 0; r < kBatch; ++r) k_greedy_round<<<cdiv(n, 256), 256, 0, s>>>(n, coff, clist, state, und + r);
+        for (int r = 0; r < kBatch; ++r)
+            k_greedy_round<<<cdiv(n, 256), 256, 0, s>>>(n, coff, clist, state, und + r, r ? und + r - 1 : nullptr);
         k_kept_flags<<<cdiv(n, 256), 256, 0, s>>>(state, n, f);
         AOS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, f, pos, n + 1, s));
         k_compact<<<cdiv(n, 256), 256, 0, s>>>(cand, f, pos, n, out, kept_index_out);
