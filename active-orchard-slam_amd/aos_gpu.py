@@ -128,6 +128,8 @@ def lib():
         L.aos_gvd_from_seedgen.argtypes = [c_vp, P(GvdOut)]
         L.aos_debug_grid.argtypes = [c_vp, ctypes.c_char_p, c_vp, c_u64]
         L.aos_gvd_markers_get.argtypes = [c_vp, P(GvdMarkers)]
+        L.aos_map_reset.argtypes = [c_vp, c_u64]
+        L.aos_map_append.argtypes = [c_vp, P(CloudView), c_i, P(SeedGenOut)]
         L.aos_tile_plan_compute.argtypes = [P(Params), c_vp, c_u, c_i, c_i, c_i, P(TilePlan)]
         L.aos_tiled_seedgen_process.argtypes = [c_vp, P(Comm), c_i, c_i, c_i, P(CloudView), c_i, P(SeedGenOut)]
         L.aos_stream.restype = c_vp
@@ -245,6 +247,18 @@ class Ctx:
         v, _keep = self._view(cloud, n_points, point_step, offs, is_dense, on_device)
         o = SeedGenOut()
         _check(lib().aos_seedgen_process(self.h, ctypes.byref(v), int(want_host), ctypes.byref(o)))
+        return _seedgen_dict(o, want_host)
+
+    def map_reset(self, reserve_points: int = 0):
+        """Empty the device-resident streaming map (aos_map_reset)."""
+        _check(lib().aos_map_reset(self.h, int(reserve_points)))
+
+    def map_append(self, scan, n_points: int | None = None, point_step=16, offs=(0, 4, 8), is_dense=True,
+                   on_device=False, want_host=True) -> dict:
+        """Append one scan to the streaming map and process the whole map (aos_map_append)."""
+        v, _keep = self._view(scan, n_points, point_step, offs, is_dense, on_device)
+        o = SeedGenOut()
+        _check(lib().aos_map_append(self.h, ctypes.byref(v), int(want_host), ctypes.byref(o)))
         return _seedgen_dict(o, want_host)
 
     def tiled_seedgen(self, comm, tiles_x: int, tiles_y: int, cloud, root: int = 0, n_points: int | None = None,

@@ -20,6 +20,16 @@ struct aos_ctx {
     uint32_t step = 16, ox = 0, oy = 4, oz = 8;
     int is_dense = 1;
 
+    // ---- streaming map (aos_map_append): float4 x, y, z, 0
+    aos::DevBuf map_buf, scan_stage;
+    uint64_t map_n = 0;
+    int map_dense = 1;
+    // ---- hipGraph of the first thinning batch (opening + 3 launches + flags read-back), replayed
+    // while the geometry and buffers stay the same (a streaming map keeps them)
+    hipGraphExec_t thin_graph = nullptr;
+    std::array<const void *, 6> thin_graph_key{};
+    int thin_graph_dims[3] = {-1, -1, -1};
+
     // ---- device buffers
     aos::DevBuf cloud_copy, bin_count, bin_start, pt_binslot, sorted, scan_tmp, counters;
     aos::DevBuf raster_bytes, raster_bits, infl_bits, open_bits, thin_a, thin_b, occ_bytes, skel_bytes, flags;
@@ -47,6 +57,7 @@ struct aos_ctx {
     struct RorOwn { int rx0, ry0, rx1, ry1, wx0, wy0, Wr, Hr; bool limit_box; float box[4]; };
 
     void set_cloud(const aos_cloud_view &v);
+    void map_append(const aos_cloud_view &scan);
     void ror_stage(const aos::FrameGeom &g, const RorOwn &o);
     void finish_frame(const aos::FrameGeom &g, bool want_host, const uint64_t *clipped_total, aos_seedgen_out &out);
     void run_seedgen(bool want_host, aos_seedgen_out &out);

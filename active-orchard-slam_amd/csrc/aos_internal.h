@@ -93,6 +93,9 @@ void launch_ror_place(const RorLaunch &L, int *cursor, float4 *sorted, hipStream
 void launch_ror_raster(const RorLaunch &L, const int *bin_start, const float4 *sorted, uint8_t *raster,
                        unsigned long long *counters, hipStream_t s);
 void launch_pack_bits(const uint8_t *bytes, uint64_t *bits, int W, int H, int WW, hipStream_t s);
+// PointCloud2 records (any float32 x/y/z offsets) -> float4 (x, y, z, 0)
+void launch_pack_xyz(const uint8_t *cloud, uint64_t n, uint32_t step, uint32_t ox, uint32_t oy, uint32_t oz, float4 *out,
+                     hipStream_t s);
 void launch_inflate(const uint64_t *in, uint64_t *out, const FrameGeom &g, hipStream_t s);
 void launch_bits_to_bytes(const uint64_t *bits, int8_t *out, const FrameGeom &g, int frame, hipStream_t s);
 void launch_open(const uint64_t *in, uint64_t *out, const FrameGeom &g, hipStream_t s);

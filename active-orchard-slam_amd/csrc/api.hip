@@ -152,6 +152,31 @@ int aos_seedgen_reprocess(aos_ctx *c, int want_host, aos_seedgen_out *out) {
     AOS_GUARD_END
 }
 
+int aos_map_reset(aos_ctx *c, uint64_t reserve_points) {
+    if (!c) { set_error("aos_map_reset: null handle"); return AOS_E_INVALID; }
+    AOS_GUARD_BEGIN
+    DeviceScope dev_scope(c->device);
+    c->map_n = 0;
+    c->map_dense = 1;
+    if (reserve_points) c->map_buf.ensure(sizeof(float4) * reserve_points);
+    return AOS_OK;
+    AOS_GUARD_END
+}
+
+int aos_map_append(aos_ctx *c, const aos_cloud_view *scan, int want_host, aos_seedgen_out *out) {
+    if (!c || !scan || !out) { set_error("aos_map_append: null argument"); return AOS_E_INVALID; }
+    if (!cloud_layout_ok(scan)) {
+        set_error("aos_map_append: invalid PointCloud2 layout (float32 x/y/z, 4-byte aligned)");
+        return AOS_E_INVALID;
+    }
+    AOS_GUARD_BEGIN
+    DeviceScope dev_scope(c->device);
+    c->map_append(*scan);
+    c->run_seedgen(want_host != 0, *out);
+    return AOS_OK;
+    AOS_GUARD_END
+}
+
 int aos_gvd_process(aos_ctx *c, const aos_gvd_in *in, aos_gvd_out *out) {
     if (!c || !in || !out) { set_error("aos_gvd_process: null argument"); return AOS_E_INVALID; }
     AOS_GUARD_BEGIN

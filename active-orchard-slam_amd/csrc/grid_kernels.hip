@@ -380,6 +380,22 @@ void launch_exclusive_scan(const int *in, int *out, int n, void *temp, size_t te
 }
 
 // ------------------------------------------------------------------------------------------
+// Streaming ingest: a scan's records -> the map's float4 (x, y, z, 0) layout (aos_map_append).
+__global__ void k_pack_xyz(const uint8_t *cloud, uint64_t n, uint32_t step, uint32_t ox, uint32_t oy, uint32_t oz,
+                           float4 *out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t *rec = cloud + i * (uint64_t)step;
+    out[i] = make_float4(*reinterpret_cast<const float *>(rec + ox), *reinterpret_cast<const float *>(rec + oy),
+                         *reinterpret_cast<const float *>(rec + oz), 0.0f);
+}
+void launch_pack_xyz(const uint8_t *cloud, uint64_t n, uint32_t step, uint32_t ox, uint32_t oy, uint32_t oz, float4 *out,
+                     hipStream_t s) {
+    if (!n) return;
+    k_pack_xyz<<<cdiv(n, 256), 256, 0, s>>>(cloud, n, step, ox, oy, oz, out);
+}
+
+// ------------------------------------------------------------------------------------------
 // bytes (0 / non-zero) -> bits
 __global__ void k_pack_bits(const uint8_t *bytes, uint64_t *bits, int W, int H, int WW) {
     int c = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;

@@ -17,8 +17,9 @@ using namespace aos;
 void aos_ctx::release() {
     for (DevBuf *b : {&cloud_copy, &bin_count, &bin_start, &pt_binslot, &sorted, &scan_tmp, &counters, &raster_bytes,
                       &raster_bits, &infl_bits, &open_bits, &thin_a, &thin_b, &occ_bytes, &skel_bytes, &flags,
-                      &full_infl, &full_skel})
+                      &full_infl, &full_skel, &map_buf, &scan_stage})
         b->release();
+    if (thin_graph) { (void)hipGraphExecDestroy(thin_graph); thin_graph = nullptr; }
     h_small.release();
     h_stats.release();
     for (DevBuf *b : {&cs.fg_bits, &cs.word_cnt, &cs.word_off, &cs.fg_list, &cs.parent, &cs.root_flag, &cs.root_rank,
@@ -47,6 +48,36 @@ void aos_ctx::set_cloud(const aos_cloud_view &v) {
         if (bytes) AOS_HIP(hipMemcpyAsync(dst, v.data, bytes, hipMemcpyHostToDevice, stream));
         d_cloud = cloud_copy.as<uint8_t>();
     }
+    have_cloud = true;
+}
+
+// Streaming ingest: append one scan to the device-resident map (aos_map_append) and make the map
+// this frame's cloud. Only the scan crosses PCIe; the map grows by 1.5x when full.
+void aos_ctx::map_append(const aos_cloud_view &v) {
+    hipStream_t s = stream;
+    const uint64_t n = v.n_points;
+    if (map_n + n > map_buf.cap / sizeof(float4)) {
+        const uint64_t want = std::max<uint64_t>(map_n + n, map_n + map_n / 2);
+        DevBuf grown;
+        void *dst = grown.ensure(sizeof(float4) * std::max<uint64_t>(want, 1));
+        if (map_n) AOS_HIP(hipMemcpyAsync(dst, map_buf.p, sizeof(float4) * map_n, hipMemcpyDeviceToDevice, s));
+        AOS_HIP(hipStreamSynchronize(s));
+        std::swap(map_buf.p, grown.p);
+        std::swap(map_buf.cap, grown.cap);
+    }
+    const uint8_t *src = static_cast<const uint8_t *>(v.data);
+    if (n && !v.on_device) {
+        void *st = scan_stage.ensure((size_t)n * v.point_step);
+        AOS_HIP(hipMemcpyAsync(st, v.data, (size_t)n * v.point_step, hipMemcpyHostToDevice, s));
+        src = static_cast<const uint8_t *>(st);
+    }
+    launch_pack_xyz(src, n, v.point_step, v.off_x, v.off_y, v.off_z, map_buf.as<float4>() + map_n, s);
+    map_n += n;
+    map_dense = map_dense && v.is_dense;
+    n_points = map_n;
+    step = 16; ox = 0; oy = 4; oz = 8;
+    is_dense = map_dense;
+    d_cloud = map_buf.as<uint8_t>();
     have_cloud = true;
 }
 
@@ -201,22 +232,48 @@ void aos_ctx::run_seedgen(bool want_host, aos_seedgen_out &out) {
     const int max_iters = std::max(g.W, g.H) + 4;   // Zhang-Suen removes >= 1 cell per changing iteration
     int *d_flags = static_cast<int *>(flags.ensure(sizeof(int) * (2 + max_iters + K)));
     AOS_HIP(hipMemsetAsync(d_flags, 0, sizeof(int) * (2 + max_iters + K), s));
-    launch_open(d_ibits, d_open, g, s);
-    int launched = 0;
-    const uint64_t *src = d_open;
     int *h_flags = static_cast<int *>(h_small.ensure(sizeof(int) * (2 + max_iters + K)));
-    const uint64_t *final_buf = d_open;
     const ThinOwn whole{0, g.H, 0, g.WW, 1};
+    // first batch: opening + 3 temporal blocks + flags read-back (typical T <= 24 needs no more). It
+    // is a fixed sequence on fixed buffers, so it is captured once into a hipGraph and replayed while
+    // the geometry and buffers are unchanged (every frame of a streaming map).
+    auto first_batch = [&]() {
+        AOS_HIP(hipMemsetAsync(d_flags, 0, sizeof(int) * (2 + max_iters + K), s));
+        launch_open(d_ibits, d_open, g, s);
+        launch_thin_block(d_open, bufs[0], g, 0, d_flags, whole, s);
+        launch_thin_block(bufs[0], bufs[1], g, K, d_flags, whole, s);
+        launch_thin_block(bufs[1], bufs[0], g, 2 * K, d_flags, whole, s);
+        AOS_HIP(hipMemcpyAsync(h_flags, d_flags, sizeof(int) * (1 + 3 * K), hipMemcpyDeviceToHost, s));
+    };
+    const std::array<const void *, 6> key{d_ibits, d_open, bufs[0], bufs[1], d_flags, h_flags};
+    if (!thin_graph || key != thin_graph_key || thin_graph_dims[0] != g.W || thin_graph_dims[1] != g.H ||
+        thin_graph_dims[2] != g.R) {
+        if (thin_graph) { AOS_HIP(hipGraphExecDestroy(thin_graph)); thin_graph = nullptr; }
+        hipGraph_t graph = nullptr;
+        AOS_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        first_batch();
+        AOS_HIP(hipStreamEndCapture(s, &graph));
+        const hipError_t e = hipGraphInstantiate(&thin_graph, graph, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(graph);
+        AOS_HIP(e);
+        thin_graph_key = key;
+        thin_graph_dims[0] = g.W; thin_graph_dims[1] = g.H; thin_graph_dims[2] = g.R;
+    }
+    AOS_HIP(hipGraphLaunch(thin_graph, s));
+    int launched = 3;
+    const uint64_t *src = bufs[0];
+    const uint64_t *final_buf = d_open;
     int T = 0;
     for (int batch = 0;; ++batch) {
-        const int per_batch = batch == 0 ? 3 : 4;   // typical T <= 24 needs one round trip
-        for (int j = 0; j < per_batch; ++j) {
-            uint64_t *dst = bufs[launched & 1];
-            launch_thin_block(src, dst, g, launched * K, d_flags, whole, s);
-            src = dst;
-            ++launched;
+        if (batch > 0) {
+            for (int j = 0; j < 4; ++j) {
+                uint64_t *dst = bufs[launched & 1];
+                launch_thin_block(src, dst, g, launched * K, d_flags, whole, s);
+                src = dst;
+                ++launched;
+            }
+            AOS_HIP(hipMemcpyAsync(h_flags, d_flags, sizeof(int) * (1 + launched * K), hipMemcpyDeviceToHost, s));
         }
-        AOS_HIP(hipMemcpyAsync(h_flags, d_flags, sizeof(int) * (1 + launched * K), hipMemcpyDeviceToHost, s));
         AOS_HIP(hipStreamSynchronize(s));
         T = thin_iterations(h_flags, launched * K);
         if (T) {

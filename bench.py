@@ -35,6 +35,8 @@ def parse(argv=None):
     ap.add_argument("--config", default=None, help="C2 (default), or C3 with --tiled")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-config", default="C1")
+    ap.add_argument("--stream", action="store_true",
+                    help="C4 (BASELINE configs[4]): 1 M-point 20 Hz scans appended to the device-resident C2 map")
     ap.add_argument("--tiled", action="store_true",
                     help="one map split into tiles over the ranks (SURVEY §8e, BASELINE configs[3]); strong scaling")
     a = ap.parse_args(argv)
@@ -162,8 +164,21 @@ def main():
     d_cloud = torch.from_numpy(cloud).to(dev)
     n = cloud.shape[0]
     del cloud
+    if a.stream:
+        # the map so far (the C2 cloud) is already device-resident; each step appends the next scan
+        # from host memory (only the 16 MB scan crosses PCIe) and processes the whole map + GVD
+        scans = [orchard.generate_scan(cfg, k) for k in range(a.warmup + a.steps)]
+        ctx.map_reset(reserve_points=n + len(scans) * orchard.SCAN_POINTS)
+        ctx.map_append(d_cloud.data_ptr(), n_points=n, on_device=True, want_host=False)
+        latency, it = [], iter(range(len(scans)))
 
     def step():
+        if a.stream:
+            t0 = time.perf_counter()
+            g = ctx.map_append(scans[next(it)], want_host=False)
+            gg = ctx.gvd_from_seedgen()
+            latency.append(time.perf_counter() - t0)
+            return g, gg
         if a.tiled:
             g = ctx.tiled_seedgen(comm, tx, ty, d_cloud.data_ptr(), root=0, n_points=n, on_device=True,
                                   want_host=False)
@@ -222,7 +237,11 @@ def main():
                   "note": "whole frame incl. the host Subdiv2D replay (DESIGN.md)"}
 
     if rank == 0:
-        if a.tiled:
+        if a.stream:
+            workload = (f"C4: 1 M-point scans at {orchard.SCAN_HZ:g} Hz appended to the device-resident {a.config} map "
+                        f"({n} pts at start, {g['n_input']} after the last step), {g['width']}x{g['height']} cells "
+                        f"@ {cfg.res} m, full seed-gen + GVD of the whole map per scan")
+        elif a.tiled:
             workload = (f"{a.config}: {cfg.n_points} pts, {g['width']}x{g['height']} cells @ {cfg.res} m, one map in "
                         f"{tx}x{ty} tiles (rank 0 holds {n} pts), halo all-gathers, GVD on rank 0")
         else:
@@ -244,7 +263,12 @@ def main():
             "roofline": roof,
             "frame_roofline": frame_roof,
         }
-        if world == 1 and not a.no_cpu_baseline:
+        if a.stream:
+            lat = sorted(x * 1e3 for x in latency[a.warmup:])
+            out["stream"] = {"scan_latency_ms_p50": round(lat[len(lat) // 2], 2), "scan_latency_ms_max": round(lat[-1], 2),
+                             "budget_ms": 1e3 / orchard.SCAN_HZ, "keeps_up": lat[-1] <= 1e3 / orchard.SCAN_HZ,
+                             "note": "latency = scan H2D + pack + whole-map seed-gen + GVD, host clock"}
+        if world == 1 and not a.no_cpu_baseline and not a.stream:
             out["cpu_baseline"] = cpu_baseline(a.cpu_config)
         print(json.dumps(out), flush=True)
     ctx.close()

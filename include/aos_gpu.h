@@ -146,6 +146,16 @@ int aos_gvd_process(aos_ctx *ctx, const aos_gvd_in *in, aos_gvd_out *out);
 int aos_gvd_from_seedgen(aos_ctx *ctx, aos_gvd_out *out);
 
 /* ---------------------------------------------------------------------------------------------
+ * Streaming ingest (BASELINE.json configs[4]). The handle keeps the global
+ * map device-resident. Each aos_map_append call uploads only the new scan (packed to x, y, z float4
+ * on the GPU), then processes the frame on the whole accumulated map. The outputs equal
+ * aos_seedgen_process on the concatenation of the scans (the reference reprocesses its whole
+ * global map on every callback, seed_gen:230-248). The map is dense iff every scan was.
+ * ------------------------------------------------------------------------------------------- */
+int aos_map_reset(aos_ctx *ctx, uint64_t reserve_points);
+int aos_map_append(aos_ctx *ctx, const aos_cloud_view *scan, int want_host, aos_seedgen_out *out);
+
+/* ---------------------------------------------------------------------------------------------
  * Multi-GPU tiled frame (BASELINE.json configs[3]: 8192^2 in 2 x 4 tiles).
  * One map is split into tiles_x x tiles_y tiles, one rank (process or thread) per tile, each with
  * its own handle on its own GPU. Ranks refresh the halos of their bit-packed grids by all-gathering

@@ -70,6 +70,9 @@ def _load():
         _lib.orchard_polygon.argtypes = [ctypes.POINTER(_Cfg), ctypes.c_void_p]
         _lib.orchard_generate_range.argtypes = [ctypes.POINTER(_Cfg), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                                 ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]
+        _lib.orchard_generate_scan.argtypes = [ctypes.POINTER(_Cfg), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                               ctypes.c_uint64, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                               ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]
     return _lib
 
 
@@ -104,6 +107,52 @@ def generate(c: OrchardConfig, seed: int | None = None, n_points: int | None = N
                                    out.ctypes.data)
 
     ts = [threading.Thread(target=work, args=(k,)) for k in range(threads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    return out
+
+
+# ------------------------------------------------------------------ C4 streaming
+SCAN_HZ, SPEED, SCAN_R, SCAN_POINTS = 20.0, 1.5, 30.0, 1_000_000
+
+
+def scan_pose(c: OrchardConfig, k: int) -> tuple[float, float]:
+    """Pose of scan k: 1.5 m/s at 20 Hz along a serpentine between the tree rows (lanes at y = 3.75 +
+    3.5 j, x from 2 to L - 2 and back)."""
+    L = float(_load().orchard_side_length(c.grid_n, c.res))
+    run = (L - 2.0) - 2.0
+    s = k * SPEED / SCAN_HZ
+    lane = int(s // (run + 3.5))
+    u = s - lane * (run + 3.5)
+    y = 3.75 + 3.5 * lane
+    if u > run:                      # turning to the next lane
+        return (2.0 + run if lane % 2 == 0 else 2.0), y + (u - run)
+    return (2.0 + u if lane % 2 == 0 else 2.0 + run - u), y
+
+
+def generate_scan(c: OrchardConfig, k: int, n_points: int = SCAN_POINTS, seed: int | None = None,
+                  threads: int = 8) -> np.ndarray:
+    """Scan k of config c's scene (PointCloud2 bytes, point_step 16): n points within 30 m of scan_pose(k)."""
+    lib = _load()
+    cfg = _cfg(c, 5 if seed is None else seed, n_points)
+    nt = lib.orchard_num_trees(ctypes.byref(cfg))
+    tx = np.zeros(max(nt, 1), np.float64)
+    ty = np.zeros(max(nt, 1), np.float64)
+    lib.orchard_tree_centres(ctypes.byref(cfg), tx.ctypes.data, ty.ctypes.data, nt)
+    px, py = scan_pose(c, k)
+    near = (tx[:nt] - px) ** 2 + (ty[:nt] - py) ** 2 <= (SCAN_R + 0.5) ** 2
+    tx, ty = np.ascontiguousarray(tx[:nt][near]), np.ascontiguousarray(ty[:nt][near])
+    out = np.empty((n_points, POINT_STEP), dtype=np.uint8)
+    threads = max(1, min(threads, n_points // 65536 + 1))
+    bounds = [n_points * j // threads for j in range(threads + 1)]
+
+    def work(j):
+        lib.orchard_generate_scan(ctypes.byref(cfg), tx.ctypes.data, ty.ctypes.data, len(tx), k, px, py, SCAN_R,
+                                  bounds[j], bounds[j + 1], out.ctypes.data)
+
+    ts = [threading.Thread(target=work, args=(j,)) for j in range(threads)]
     for t in ts:
         t.start()
     for t in ts:

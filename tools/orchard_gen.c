@@ -103,3 +103,41 @@ void orchard_generate_range(const orchard_cfg *c, const double *tree_x, const do
 int64_t orchard_tree_centres(const orchard_cfg *c, double *tree_x, double *tree_y, int64_t cap) {
     return orchard_trees(c, tree_x, tree_y, cap);
 }
+
+/* One scan of the streaming config C4: points [begin, end) of scan `scan`, i.e. the
+ * scene restricted to the disc of radius scan_r around the pose (px, py). Canopy points come from
+ * the trees given (the caller passes those whose disc can reach the scan disc), ground and outliers
+ * are uniform in the scan disc (rejection from its bounding square). Every point owns its own
+ * SplitMix64 stream seeded from (seed, scan, index). */
+void orchard_generate_scan(const orchard_cfg *c, const double *tree_x, const double *tree_y, int64_t n_trees,
+                           uint64_t scan, double px, double py, double scan_r, uint64_t begin, uint64_t end,
+                           uint8_t *out) {
+    const double r2 = scan_r * scan_r;
+    for (uint64_t i = begin; i < end; ++i) {
+        uint64_t s = (c->seed * 0xD1B54A32D192ED03ULL) ^ (scan * 0xA24BAED4963EE407ULL) ^
+                     (i * 0x9E3779B97F4A7C15ULL + 0x632BE59BD9B4E019ULL);
+        sm64_next(&s);
+        const double kind = u01(&s);
+        double x = px, y = py, z;
+        if (kind < 0.6 && n_trees > 0) {
+            for (int tries = 0; tries < 64; ++tries) {
+                int64_t t = (int64_t)(u01(&s) * (double)n_trees);
+                if (t >= n_trees) t = n_trees - 1;
+                double dx, dy;
+                do { dx = uab(&s, -0.5, 0.5); dy = uab(&s, -0.5, 0.5); } while (dx * dx + dy * dy > 0.25);
+                x = tree_x[t] + dx;
+                y = tree_y[t] + dy;
+                if ((x - px) * (x - px) + (y - py) * (y - py) <= r2) break;
+            }
+            z = (u01(&s) < 0.8) ? uab(&s, -0.3, 0.4) : uab(&s, 0.6, 3.0);
+        } else {
+            double dx, dy;
+            do { dx = uab(&s, -scan_r, scan_r); dy = uab(&s, -scan_r, scan_r); } while (dx * dx + dy * dy > r2);
+            x = px + dx;
+            y = py + dy;
+            z = (kind < 1.0 - c->outlier_frac) ? uab(&s, -1.3, -1.1) : uab(&s, -0.4, 0.5);
+        }
+        float rec[4] = {(float)x, (float)y, (float)z, (float)(i & 0xFF)};
+        memcpy(out + 16 * i, rec, 16);
+    }
+}
