@@ -236,7 +236,10 @@ int aos_tiled_seedgen_process(aos_ctx *c, const aos_comm *comm, int32_t tiles_x,
 
 int aos_gvd_markers_get(aos_ctx *c, aos_gvd_markers *out) {
     if (!c || !out) { set_error("aos_gvd_markers_get: null argument"); return AOS_E_INVALID; }
-    const GvdState &G = c->gs;
+    GvdState &G = c->gs;
+    AOS_GUARD_BEGIN
+    markers_wait(G, true);   // the cells run on after the graph is returned
+    AOS_GUARD_END
     if (!G.have_markers || !G.cells) {
         set_error("aos_gvd_markers_get: no markers (gvd_markers = 0 or no GVD frame)");
         return AOS_E_STATE;

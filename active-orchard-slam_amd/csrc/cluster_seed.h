@@ -1,6 +1,10 @@
 // Cluster / tree-row / seed stage and GVD stage state. Not part of the ABI.
 #pragma once
+#include <condition_variable>
+#include <exception>
 #include <memory>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "aos_internal.h"
@@ -72,6 +76,9 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
 // publishMarkers' Voronoi cells, computed by a worker thread next to the main Subdiv2D replay. It
 // lives in its own cache-line-aligned heap object: the two replays write their state on every step,
 // and sharing lines with the main replay's fields slowed both down by ~40 % on the EPYC host.
+// Device buffers of the facet builder (calcVoronoi + getVoronoiFacetList on the GPU, gvd.hip).
+struct FacetBufs { DevBuf qe, vp, vfirst, vtype, face, cnt, off, scan_tmp; };
+
 struct alignas(128) CellsWork {
     Subdiv2D sd;                               // extractCellBoundaries' Subdiv2D
     std::vector<double> seeds;                 // VoronoiDiagram::seeds_ (finite merged seeds)
@@ -79,6 +86,31 @@ struct alignas(128) CellsWork {
     std::vector<int32_t> cell_off;
     std::vector<float> cell_rgba;
     float ms = 0;
+    // its facets are built on the GPU too, on the worker's own stream
+    int device = 0;
+    hipStream_t stream = nullptr;
+    FacetBufs fb;
+    DevBuf edges;
+    PinnedBuf h;
+    // One persistent worker per handle: it sleeps between frames and keeps its core (and the
+    // replay's ~6 MB of quad-edges in that core's caches); a thread per frame landed on a cold core.
+    std::thread worker;
+    std::mutex mu;
+    std::condition_variable cv;
+    bool busy = false, quit = false;
+    int rect_mode = 0;
+    std::exception_ptr err;     // the last job's error (markers_wait raises or discards it)
+    CellsWork() = default;
+    CellsWork(const CellsWork &) = delete;
+    CellsWork &operator=(const CellsWork &) = delete;
+    ~CellsWork() {
+        if (worker.joinable()) {
+            { std::lock_guard<std::mutex> l(mu); quit = true; }
+            cv.notify_all();
+            worker.join();
+        }
+        if (stream) (void)hipStreamDestroy(stream);
+    }
 };
 
 struct GvdState {
@@ -109,5 +141,7 @@ struct GvdStageIn {
 };
 bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipStream_t stream, hipEvent_t *ev);
 void free_gvd_scratch(GvdState &G);
+// Joins the markers' cells job of the last GVD call; rethrow: raise its error (else discard it).
+void markers_wait(GvdState &G, bool rethrow);
 
 }  // namespace aos

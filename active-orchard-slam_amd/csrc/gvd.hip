@@ -492,8 +492,8 @@ __global__ void k_facet_emit(const int *qe, const int *vfirst, const int *off, c
 struct GvdScratch {
     DevBuf raw, ok, leaders, merged, owner, oidx, sowner, sidx, tmp, edges_f, occ, occ_ok, bp, kept_occ, keys, idx, skeys,
         sidx2, near_idx, pk, pidx, pskeys, psidx, pcount, poff, plist, ft, ckey, cvalid, pass, k2, occ_idx, sk2, socc, selected,
-        inside, ipos, nodes, keep, kpos, edges, lens, jobs, lpts, lval, lmask, lcidx, lcount, loff, lcl, lty, scan_tmp,
-        sd_qe, sd_vp, sd_vfirst, sd_vtype, sd_face, sd_cnt, sd_off;
+        inside, ipos, nodes, keep, kpos, edges, lens, jobs, lpts, lval, lmask, lcidx, lcount, loff, lcl, lty, scan_tmp;
+    FacetBufs fb;
 };
 static GvdScratch &scratch(GvdState &G) {
     if (!G.scratch) G.scratch = new GvdScratch();
@@ -509,6 +509,35 @@ static void scan_excl(DevBuf &tmpb, const int *in, int *out, int n, hipStream_t 
     AOS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, n, s));
     void *t = tmpb.ensure(tb);
     AOS_HIP(hipcub::DeviceScan::ExclusiveSum(t, tb, in, out, n, s));
+}
+
+// Facets of a replayed Subdiv2D on the GPU: uploads the quad-edge state, computes every face's
+// circumcentre (k_vor_faces) and the per-vertex facet sizes (k_facet_count, 0 below 2 points), and
+// scans them into edge offsets. Returns the edge total (F.cnt / F.off stay on the device); h_sc =
+// 2 pinned ints. The caller launches k_facet_emit into a buffer of that many float4.
+static int facets_count(FacetBufs &F, const Subdiv2D::Raw &R, int *h_sc, hipStream_t s) {
+    int *d_qe = dev<int>(F.qe, 8 * (size_t)R.n_rec);
+    float2 *d_vp = dev<float2>(F.vp, R.n_vtx);
+    int *d_vf = dev<int>(F.vfirst, R.n_vtx), *d_vt = dev<int>(F.vtype, R.n_vtx);
+    AOS_HIP(hipMemcpyAsync(d_qe, R.qe, sizeof(int) * 8 * (size_t)R.n_rec, hipMemcpyHostToDevice, s));
+    AOS_HIP(hipMemcpyAsync(d_vp, R.vp, sizeof(float2) * R.n_vtx, hipMemcpyHostToDevice, s));
+    AOS_HIP(hipMemcpyAsync(d_vf, R.vfirst, sizeof(int) * R.n_vtx, hipMemcpyHostToDevice, s));
+    AOS_HIP(hipMemcpyAsync(d_vt, R.vtype, sizeof(int) * R.n_vtx, hipMemcpyHostToDevice, s));
+    float2 *d_face = dev<float2>(F.face, 2 * (size_t)R.n_rec);
+    int *d_cnt = dev<int>(F.cnt, R.n_vtx + 2), *d_off = dev<int>(F.off, R.n_vtx + 1);
+    AOS_HIP(hipMemsetAsync(d_cnt + R.n_vtx, 0, 2 * sizeof(int), s));
+    k_vor_faces<<<cdiv(2 * R.n_rec, 256), 256, 0, s>>>(d_qe, R.n_rec, d_vp, d_face);
+    k_facet_count<<<cdiv(R.n_vtx, 256), 256, 0, s>>>(d_qe, d_vf, d_vt, R.n_vtx, d_cnt, d_cnt + R.n_vtx + 1);
+    scan_excl(F.scan_tmp, d_cnt, d_off, R.n_vtx + 1, s);
+    AOS_HIP(hipMemcpyAsync(h_sc, d_off + R.n_vtx, sizeof(int), hipMemcpyDeviceToHost, s));
+    AOS_HIP(hipMemcpyAsync(h_sc + 1, d_cnt + R.n_vtx + 1, sizeof(int), hipMemcpyDeviceToHost, s));
+    AOS_HIP(hipStreamSynchronize(s));
+    if (h_sc[1]) throw std::runtime_error("Subdiv2D facet walk did not close");
+    return h_sc[0];
+}
+static void facets_emit(FacetBufs &F, const Subdiv2D::Raw &R, float4 *edges, hipStream_t s) {
+    k_facet_emit<<<cdiv(R.n_vtx, 256), 256, 0, s>>>(F.qe.as<int>(), F.vfirst.as<int>(), F.off.as<int>(), F.cnt.as<int>(),
+                                                   R.n_vtx, F.face.as<float2>(), edges);
 }
 
 // publishMarkers' Voronoi cells (gvd:1098-1194): VoronoiDiagram::extractCellBoundaries
@@ -544,17 +573,36 @@ static void compute_cells(CellsWork &W, int rect_mode) {
         y = std::max(ry + margin, std::min(ry + rh - margin, y));
         sd.insert(x, y);   // insertion failures are skipped (voronoi_diagram.cpp:280-285)
     }
-    std::vector<int> off;
-    std::vector<float> xy;
-    sd.voronoi_facets(off, xy);
-    const int nf = (int)off.size() - 1;
+    // getVoronoiFacetList on the GPU (the builder of the main graph, on the worker's stream): the
+    // facet of real vertex k is the start points of its k_facet_emit edges, cnt[k] of them (0 for a
+    // facet of fewer than 2 points: never a cell).
+    const Subdiv2D::Raw R = sd.raw();
+    AOS_HIP(hipSetDevice(W.device));
+    if (!W.stream) AOS_HIP(hipStreamCreateWithFlags(&W.stream, hipStreamNonBlocking));
+    int *h_sc = static_cast<int *>(W.h.ensure(4096));
+    const int ne = facets_count(W.fb, R, h_sc, W.stream);
+    const size_t need = sizeof(float4) * (size_t)std::max(ne, 1) + sizeof(int) * (size_t)R.n_vtx;
+    float4 *d_e = dev<float4>(W.edges, std::max(ne, 1));
+    if (ne) facets_emit(W.fb, R, d_e, W.stream);
+    char *hb = static_cast<char *>(W.h.ensure(need + 4096)) + 4096;   // h_sc stays in the first 4 KiB
+    const float4 *he = reinterpret_cast<const float4 *>(hb);
+    const int *hcnt = reinterpret_cast<const int *>(hb + sizeof(float4) * (size_t)std::max(ne, 1));
+    if (ne) AOS_HIP(hipMemcpyAsync(const_cast<float4 *>(he), d_e, sizeof(float4) * (size_t)ne, hipMemcpyDeviceToHost, W.stream));
+    AOS_HIP(hipMemcpyAsync(const_cast<int *>(hcnt), W.fb.cnt.p, sizeof(int) * (size_t)R.n_vtx, hipMemcpyDeviceToHost, W.stream));
+    AOS_HIP(hipStreamSynchronize(W.stream));
     int ncell = 0;
-    for (int i = 0; i < ns && i < nf; ++i) {
-        const int b = off[i], n = off[i + 1] - b;
+    size_t b = 0;
+    for (int k = 4, i = 0; k < R.n_vtx && i < ns; ++k) {
+        if (R.vtype[k] != 0) continue;
+        const int n = hcnt[k];
+        const size_t b0 = b;
+        b += (size_t)n;
+        ++i;
         if (n < 3) continue;
-        for (int k = 0; k < n; ++k) { W.cell_xy.push_back(xy[2 * (b + k)]); W.cell_xy.push_back(xy[2 * (b + k) + 1]); }
-        const double dx = (double)xy[2 * b] - (double)xy[2 * (b + n - 1)], dy = (double)xy[2 * b + 1] - (double)xy[2 * (b + n - 1) + 1];
-        if (std::sqrt(dx * dx + dy * dy) > 0.01) { W.cell_xy.push_back(xy[2 * b]); W.cell_xy.push_back(xy[2 * b + 1]); }
+        for (int j = 0; j < n; ++j) { W.cell_xy.push_back(he[b0 + j].x); W.cell_xy.push_back(he[b0 + j].y); }
+        const float4 f = he[b0], l = he[b0 + n - 1];
+        const double dx = (double)f.x - (double)l.x, dy = (double)f.y - (double)l.y;
+        if (std::sqrt(dx * dx + dy * dy) > 0.01) { W.cell_xy.push_back(f.x); W.cell_xy.push_back(f.y); }
         W.cell_off.push_back((int32_t)(W.cell_xy.size() / 2));
         ++ncell;
     }
@@ -577,29 +625,55 @@ static void compute_cells(CellsWork &W, int rect_mode) {
     W.ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
-// The cells' worker thread of one GVD call; joined on every exit of run_gvd_stage.
-struct CellsJob {
-    std::thread t;
-    std::exception_ptr err;
-    void start(GvdState &G, int rect_mode) {
-        if (!G.cells) G.cells.reset(new CellsWork());
-        CellsWork &W = *G.cells;
-        W.seeds.clear();
-        for (size_t i = 0; i + 1 < G.merged_xy.size(); i += 2)
-            if (std::isfinite(G.merged_xy[i]) && std::isfinite(G.merged_xy[i + 1])) {
-                W.seeds.push_back(G.merged_xy[i]); W.seeds.push_back(G.merged_xy[i + 1]);
+// The cells' worker thread. publishMarkers runs after publishGraph (gvd:310-313), so the graph is
+// returned as soon as it is ready and the cells finish in the background: aos_gvd_markers_get, the
+// next GVD call and release() join the job (markers_wait). An error of the job is raised by
+// aos_gvd_markers_get; a job nobody asked about is discarded by the next call.
+static void markers_start(GvdState &G, int rect_mode) {
+    if (!G.cells) G.cells.reset(new CellsWork());
+    CellsWork &W = *G.cells;
+    AOS_HIP(hipGetDevice(&W.device));
+    W.seeds.clear();
+    for (size_t i = 0; i + 1 < G.merged_xy.size(); i += 2)
+        if (std::isfinite(G.merged_xy[i]) && std::isfinite(G.merged_xy[i + 1])) {
+            W.seeds.push_back(G.merged_xy[i]); W.seeds.push_back(G.merged_xy[i + 1]);
+        }
+    if (!W.worker.joinable())
+        W.worker = std::thread([&W]() {
+            std::unique_lock<std::mutex> l(W.mu);
+            for (;;) {
+                W.cv.wait(l, [&W] { return W.busy || W.quit; });
+                if (W.quit) return;
+                l.unlock();
+                std::exception_ptr e;
+                try { compute_cells(W, W.rect_mode); } catch (...) { e = std::current_exception(); }
+                l.lock();
+                W.err = e;
+                W.busy = false;
+                W.cv.notify_all();
             }
-        t = std::thread([this, &W, rect_mode]() {
-            try { compute_cells(W, rect_mode); } catch (...) { err = std::current_exception(); }
         });
+    {
+        std::lock_guard<std::mutex> l(W.mu);
+        W.rect_mode = rect_mode;
+        W.err = nullptr;
+        W.busy = true;
     }
-    void finish(GvdState &G) {
-        if (t.joinable()) t.join();
-        if (err) { std::exception_ptr e = err; err = nullptr; std::rethrow_exception(e); }
-        G.have_markers = true;
+    W.cv.notify_all();
+}
+
+void markers_wait(GvdState &G, bool rethrow) {
+    if (!G.cells) return;
+    CellsWork &W = *G.cells;
+    std::unique_lock<std::mutex> l(W.mu);
+    W.cv.wait(l, [&W] { return !W.busy; });
+    if (W.err) {
+        std::exception_ptr e = W.err;
+        W.err = nullptr;
+        G.have_markers = false;
+        if (rethrow) std::rethrow_exception(e);
     }
-    ~CellsJob() { if (t.joinable()) t.join(); }
-};
+}
 
 bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipStream_t s, hipEvent_t *ev) {
     GvdScratch &S = scratch(G);
@@ -607,10 +681,10 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     G.label_clusters.clear(); G.label_types.clear(); G.edges_out.clear(); G.lengths.clear(); G.clearances.clear();
     G.n_merged = G.n_vor_edges = G.n_bpts = 0;
     G.ms_merge = G.ms_delaunay = G.ms_graph = G.ms_total = 0;
+    markers_wait(G, false);
     G.have_markers = false;
     G.merged_xy.clear(); G.row_label_xy.clear(); G.row_label_valid.clear();
     if (G.cells) { G.cells->cell_off.assign(1, 0); G.cells->ms = 0; }
-    CellsJob cells;
     int *h_sc = static_cast<int *>(G.h_misc.ensure(4096));
     const int n = in.n_seeds;
     AOS_HIP(hipEventRecord(ev[6], s));
@@ -660,7 +734,7 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     G.n_merged = nl;
     AOS_HIP(hipEventRecord(ev[7], s));
     G.merged_xy = merged;
-    if (P.gvd_markers) cells.start(G, P.subdiv_rect_mode);
+    if (P.gvd_markers) markers_start(G, P.subdiv_rect_mode);
 
     // ---- g3/g4 finite filter, bounds, Subdiv2D inserts (host replay) -> facets / Voronoi edges (GPU)
     auto t0 = std::chrono::steady_clock::now();
@@ -693,27 +767,9 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
                 sd.insert(x, y);
             }
             const Subdiv2D::Raw R = sd.raw();
-            int *d_qe = dev<int>(S.sd_qe, 8 * (size_t)R.n_rec);
-            float2 *d_vp = dev<float2>(S.sd_vp, R.n_vtx);
-            int *d_vf = dev<int>(S.sd_vfirst, R.n_vtx), *d_vt = dev<int>(S.sd_vtype, R.n_vtx);
-            AOS_HIP(hipMemcpyAsync(d_qe, R.qe, sizeof(int) * 8 * (size_t)R.n_rec, hipMemcpyHostToDevice, s));
-            AOS_HIP(hipMemcpyAsync(d_vp, R.vp, sizeof(float2) * R.n_vtx, hipMemcpyHostToDevice, s));
-            AOS_HIP(hipMemcpyAsync(d_vf, R.vfirst, sizeof(int) * R.n_vtx, hipMemcpyHostToDevice, s));
-            AOS_HIP(hipMemcpyAsync(d_vt, R.vtype, sizeof(int) * R.n_vtx, hipMemcpyHostToDevice, s));
-            float2 *d_face = dev<float2>(S.sd_face, 2 * (size_t)R.n_rec);
-            int *d_cnt = dev<int>(S.sd_cnt, R.n_vtx + 2), *d_off = dev<int>(S.sd_off, R.n_vtx + 1);
-            AOS_HIP(hipMemsetAsync(d_cnt + R.n_vtx, 0, 2 * sizeof(int), s));
-            k_vor_faces<<<cdiv(2 * R.n_rec, 256), 256, 0, s>>>(d_qe, R.n_rec, d_vp, d_face);
-            k_facet_count<<<cdiv(R.n_vtx, 256), 256, 0, s>>>(d_qe, d_vf, d_vt, R.n_vtx, d_cnt, d_cnt + R.n_vtx + 1);
-            scan_excl(S.scan_tmp, d_cnt, d_off, R.n_vtx + 1, s);
-            AOS_HIP(hipMemcpyAsync(h_sc, d_off + R.n_vtx, sizeof(int), hipMemcpyDeviceToHost, s));
-            AOS_HIP(hipMemcpyAsync(h_sc + 1, d_cnt + R.n_vtx + 1, sizeof(int), hipMemcpyDeviceToHost, s));
-            AOS_HIP(hipStreamSynchronize(s));
-            if (h_sc[1]) throw std::runtime_error("Subdiv2D facet walk did not close");
-            ne = h_sc[0];
+            ne = facets_count(S.fb, R, h_sc, s);
             d_ef = dev<float>(S.edges_f, 4 * (size_t)std::max(ne, 1));
-            if (ne) k_facet_emit<<<cdiv(R.n_vtx, 256), 256, 0, s>>>(d_qe, d_vf, d_off, d_cnt, R.n_vtx, d_face,
-                                                                    reinterpret_cast<float4 *>(d_ef));
+            if (ne) facets_emit(S.fb, R, reinterpret_cast<float4 *>(d_ef), s);
         }
     }
     auto t1 = std::chrono::steady_clock::now();
@@ -721,7 +777,7 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     G.n_vor_edges = ne;
     AOS_HIP(hipEventRecord(ev[8], s));
     if (ne == 0) {   // no boundary points: an empty graph is still published
-        if (P.gvd_markers) cells.finish(G);
+        G.have_markers = P.gvd_markers != 0;
         return true;
     }
 
@@ -869,7 +925,7 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     }
     AOS_HIP(hipEventRecord(ev[9], s));
     AOS_HIP(hipStreamSynchronize(s));
-    if (P.gvd_markers) cells.finish(G);
+    G.have_markers = P.gvd_markers != 0;
     float a = 0, b = 0;
     (void)hipEventElapsedTime(&a, ev[6], ev[7]);
     (void)hipEventElapsedTime(&b, ev[8], ev[9]);
@@ -898,7 +954,7 @@ static void fill_gvd_out(const aos_ctx &c, const GvdState &G, const aos_grid_inf
     out.edges = G.edges_out.data(); out.edge_lengths = G.lengths.data(); out.edge_clearances = G.clearances.data();
     out.n_merged_seeds = G.n_merged; out.n_voronoi_edges = G.n_vor_edges; out.n_boundary_points = G.n_bpts;
     out.ms_merge = G.ms_merge; out.ms_delaunay = G.ms_delaunay; out.ms_graph = G.ms_graph; out.ms_total = G.ms_total;
-    out.ms_cells = G.cells ? G.cells->ms : 0.0f;
+    out.ms_cells = 0.0f;   // the cells job may still run: aos_gvd_markers.ms_cells
     (void)c;
 }
 

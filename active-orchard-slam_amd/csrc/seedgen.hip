@@ -28,7 +28,9 @@ void aos_ctx::release() {
                       &cs.hash_start, &cs.hash_slot, &cs.hash_sorted, &cs.seed_out, &cs.misc, &cs.scan_tmp})
         b->release();
     cs.h_misc.release();
+    markers_wait(gs, false);
     free_gvd_scratch(gs);
+    gs.cells.reset();
     for (DevBuf *b : {&gs.seeds, &gs.merge_state, &gs.hash_count, &gs.hash_start, &gs.hash_slot, &gs.hash_sorted,
                       &gs.scan_tmp, &gs.edges, &gs.bpts, &gs.near_idx, &gs.cand, &gs.cand_ok, &gs.skel,
                       &gs.grid_bytes_ext})

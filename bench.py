@@ -170,23 +170,43 @@ def main():
         scans = [orchard.generate_scan(cfg, k) for k in range(a.warmup + a.steps)]
         ctx.map_reset(reserve_points=n + len(scans) * orchard.SCAN_POINTS)
         ctx.map_append(d_cloud.data_ptr(), n_points=n, on_device=True, want_host=False)
-        latency, it = [], iter(range(len(scans)))
+        latency, mk_latency = [], []
+    # The markers' cells of a frame finish in the background after its graph (publishGraph before
+    # publishMarkers, gvd:310-313): every step collects the previous frame's markers after its own
+    # seed-gen, and the last step collects its own, so each timed frame includes its markers.
+    n_calls = a.warmup + a.steps
+    pend = {"k": 0, "t0": None, "ms": 0.0}
+
+    def collect():
+        m = ctx.gvd_markers()
+        if pend["t0"] is not None and a.stream:
+            mk_latency.append(time.perf_counter() - pend["t0"])
+        pend["ms"] = m["ms_cells"]
+        pend["t0"] = None
+        return m
 
     def step():
+        k = pend["k"]
+        pend["k"] += 1
+        t0 = time.perf_counter()
         if a.stream:
-            t0 = time.perf_counter()
-            g = ctx.map_append(scans[next(it)], want_host=False)
-            gg = ctx.gvd_from_seedgen()
-            latency.append(time.perf_counter() - t0)
-            return g, gg
-        if a.tiled:
+            g = ctx.map_append(scans[k], want_host=False)
+        elif a.tiled:
             g = ctx.tiled_seedgen(comm, tx, ty, d_cloud.data_ptr(), root=0, n_points=n, on_device=True,
                                   want_host=False)
             if not g["root"]:
                 return g, {"ms": {}, "nodes": (), "edges": ()}
         else:
             g = ctx.seedgen(d_cloud.data_ptr(), n_points=n, on_device=True, want_host=False)
+        if k > 0:
+            collect()
         gg = ctx.gvd_from_seedgen()
+        if a.stream:
+            latency.append(time.perf_counter() - t0)
+        pend["t0"] = t0
+        if k == n_calls - 1:
+            collect()
+        gg["ms"]["cells"] = pend["ms"]   # the previous frame's (the last step: its own)
         return g, gg
 
     dt, res = timed_region(step, a.steps, a.warmup, world, torch.cuda.synchronize, dist, red_dev)
@@ -265,9 +285,15 @@ def main():
         }
         if a.stream:
             lat = sorted(x * 1e3 for x in latency[a.warmup:])
+            mlat = sorted(x * 1e3 for x in mk_latency[a.warmup:])
             out["stream"] = {"scan_latency_ms_p50": round(lat[len(lat) // 2], 2), "scan_latency_ms_max": round(lat[-1], 2),
-                             "budget_ms": 1e3 / orchard.SCAN_HZ, "keeps_up": lat[-1] <= 1e3 / orchard.SCAN_HZ,
-                             "note": "latency = scan H2D + pack + whole-map seed-gen + GVD, host clock"}
+                             "markers_latency_ms_p50": round(mlat[len(mlat) // 2], 2),
+                             "markers_latency_ms_max": round(mlat[-1], 2),
+                             "budget_ms": 1e3 / orchard.SCAN_HZ,
+                             "keeps_up": max(lat[-1], dt / len(res) * 1e3) <= 1e3 / orchard.SCAN_HZ,
+                             "note": "scan latency = scan H2D + pack + whole-map seed-gen + GVD graph (host clock); "
+                                     "markers latency = until that scan's /gvd/markers cells are collected; "
+                                     "keeps_up: graph latency and time per scan (markers included) within the budget"}
         if world == 1 and not a.no_cpu_baseline and not a.stream:
             out["cpu_baseline"] = cpu_baseline(a.cpu_config)
         print(json.dumps(out), flush=True)

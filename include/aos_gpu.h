@@ -133,7 +133,8 @@ typedef struct aos_gvd_out {
     const float *edge_lengths, *edge_clearances;
     int32_t n_merged_seeds, n_voronoi_edges, n_boundary_points;
     float ms_merge, ms_delaunay, ms_graph, ms_total;
-    float ms_cells;                      /* publishMarkers' cells on the worker thread (gvd_markers) */
+    float ms_cells;                      /* always 0: the cells finish after the call returns;
+                                            see aos_gvd_markers.ms_cells                          */
 } aos_gvd_out;
 
 const char *aos_last_error(void);
@@ -204,7 +205,11 @@ int aos_tiled_seedgen_process(aos_ctx *ctx, const aos_comm *comm, int32_t tiles_
                               const aos_cloud_view *cloud, int want_host, aos_seedgen_out *out);
 
 /* /gvd/markers content of the last GVD call (publishMarkers gvd:1012-1591) that is not already in
- * aos_gvd_out; the wrapper adds styles, ids and text. Needs aos_params.gvd_markers = 1. */
+ * aos_gvd_out; the wrapper adds styles, ids and text. Needs aos_params.gvd_markers = 1.
+ * The reference publishes the graph before the markers (gvd:310-313). Likewise a GVD call returns
+ * once the graph is ready, and the cells (a second Subdiv2D) finish on a background thread: this
+ * call waits for them, and raises their error if they failed. They overlap the next seed-gen
+ * frame; the next GVD call and aos_destroy wait for them. The pointers stay valid until then. */
 typedef struct aos_gvd_markers {
     int32_t n_seeds; const double *seeds_xy;   /* /gvd_voronoi_seeds: the merged seeds (gvd:1019-1041)        */
     int32_t n_rows;                            /* exploration rows (sorted rows_info pairs)                   */

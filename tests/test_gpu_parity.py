@@ -325,3 +325,24 @@ def test_gvd_markers_external_input_and_disabled():
     with pytest.raises(RuntimeError, match="no markers"):
         c.gvd_markers()
     c.close()
+
+
+def test_gvd_markers_background_job_overlaps_next_frame():
+    """The cells finish in the background after the graph (publishGraph before publishMarkers,
+    gvd:310-313): a seed-gen frame may run before they are collected, a GVD call that nobody
+    collected is superseded by the next one, and closing a handle with a job in flight joins it."""
+    cfg = orchard.CONFIGS["C0"]
+    cloud, poly = orchard.generate(cfg), orchard.polygon(cfg)
+    o = O.seedgen(cloud, poly, O.default_params(grid_resolution=cfg.res))
+    og = O.gvd(o["voronoi_seeds"], o["rows_info"], o, O.default_params(grid_resolution=cfg.res, markers=1))
+    c = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res))
+    c.set_polygon(poly)
+    c.seedgen(cloud)
+    c.gvd_from_seedgen()
+    c.gvd_from_seedgen()          # the first call's job is joined and replaced
+    c.seedgen(cloud)              # overlaps the second job
+    m = c.gvd_markers()
+    assert m["ms_cells"] > 0
+    _assert_markers(m, og)
+    c.gvd_from_seedgen()
+    c.close()                     # job still in flight
