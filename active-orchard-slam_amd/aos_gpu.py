@@ -74,6 +74,70 @@ class GvdOut(ctypes.Structure):
                 ("ms_total", c_f), ("ms_cells", c_f)]
 
 
+class PathGraph(ctypes.Structure):
+    _fields_ = [("num_nodes", c_i), ("nodes_xy", P(c_d)), ("node_labels", P(c_i)), ("node_cluster_indices", P(c_i)),
+                ("node_label_counts", P(c_i)), ("n_label_entries", c_i), ("node_label_clusters", P(c_i)),
+                ("node_label_types", P(c_i)), ("num_edges", c_i), ("edges", P(c_i)), ("edge_lengths", P(c_f))]
+
+
+class PathQuery(ctypes.Structure):
+    _fields_ = [("initial_waypoint_reached", c_i), ("initial_waypoint_xy", c_d * 2), ("target_waypoint_index", c_i),
+                ("have_saved_target", c_i), ("saved_target_xy", c_d * 2), ("previous_waypoint_index", c_i),
+                ("use_current_position", c_i), ("current_xy", c_d * 2), ("exploration_completed", c_i)]
+
+
+class PathOut(ctypes.Structure):
+    _fields_ = [("status", c_i), ("target_waypoint_index", c_i), ("cluster_index", c_i), ("n_clusters", c_i),
+                ("cluster_ids", P(c_i)), ("cluster_nodes", P(c_i)), ("n_waypoints", c_i), ("waypoints_xy", P(c_d)),
+                ("waypoint_nodes", P(c_i)), ("n_node_path", c_i), ("node_path", P(c_i)), ("n_poses", c_i),
+                ("poses", P(c_d)), ("trimmed_from", c_i), ("ms_plan", c_f)]
+
+
+def path_query(initial_waypoint_reached=True, initial_waypoint=(8.0, 0.0), target=-1, saved_target=None, previous=-1,
+               current=None, exploration_completed=False) -> PathQuery:
+    """aos_path_gen_node state when a graph arrives (aos_path_query)."""
+    q = PathQuery()
+    q.initial_waypoint_reached = int(bool(initial_waypoint_reached))
+    q.initial_waypoint_xy[:] = list(initial_waypoint)
+    q.target_waypoint_index = target
+    if saved_target is not None:
+        q.have_saved_target = 1
+        q.saved_target_xy[:] = list(saved_target)
+    q.previous_waypoint_index = previous
+    if current is not None:
+        q.use_current_position = 1
+        q.current_xy[:] = list(current)
+    q.exploration_completed = int(bool(exploration_completed))
+    return q
+
+
+def path_graph(g: dict):
+    """aos_path_graph view of a GvdGraph dict (Ctx.gvd / oracle gvd keys); returns (struct, keep-alive)."""
+    nodes = np.ascontiguousarray(g["nodes"], dtype=np.float64).reshape(-1)
+    arrs = {k: np.ascontiguousarray(g[k], dtype=np.int32).reshape(-1)
+            for k in ("node_labels", "node_cluster_indices", "node_label_counts", "node_label_clusters",
+                      "node_label_types", "edges")}
+    lens = np.ascontiguousarray(g["edge_lengths"], dtype=np.float32).reshape(-1)
+    ip = lambda a: a.ctypes.data_as(P(c_i))  # noqa: E731
+    s = PathGraph(nodes.size // 2, nodes.ctypes.data_as(P(c_d)), ip(arrs["node_labels"]),
+                  ip(arrs["node_cluster_indices"]), ip(arrs["node_label_counts"]), arrs["node_label_clusters"].size,
+                  ip(arrs["node_label_clusters"]), ip(arrs["node_label_types"]), arrs["edges"].size // 2,
+                  ip(arrs["edges"]), lens.ctypes.data_as(P(c_f)))
+    return s, (nodes, arrs, lens)
+
+
+def _path_dict(o: PathOut) -> dict:
+    nc = o.n_clusters
+    return {"status": o.status, "target": o.target_waypoint_index, "cluster_index": o.cluster_index,
+            "cluster_ids": _arr(o.cluster_ids, nc, np.int32),
+            "cluster_nodes": _arr(o.cluster_nodes, 4 * nc, np.int32).reshape(-1, 4),
+            "waypoints": _arr(o.waypoints_xy, 2 * o.n_waypoints, np.float64).reshape(-1, 2),
+            "waypoint_nodes": _arr(o.waypoint_nodes, o.n_waypoints, np.int32),
+            "node_path": _arr(o.node_path, o.n_node_path, np.int32),
+            "poses": _arr(o.poses, 4 * o.n_poses, np.float64).reshape(-1, 4),
+            "trimmed_from": o.trimmed_from, "ms": o.ms_plan}
+
+
 AllGatherFn = ctypes.CFUNCTYPE(c_i, c_vp, c_u64)
 AllReduceMaxFn = ctypes.CFUNCTYPE(c_i, c_vp, P(c_i), c_i)
 
@@ -132,6 +196,7 @@ def lib():
         L.aos_map_append.argtypes = [c_vp, P(CloudView), c_i, P(SeedGenOut)]
         L.aos_tile_plan_compute.argtypes = [P(Params), c_vp, c_u, c_i, c_i, c_i, P(TilePlan)]
         L.aos_tiled_seedgen_process.argtypes = [c_vp, P(Comm), c_i, c_i, c_i, P(CloudView), c_i, P(SeedGenOut)]
+        L.aos_path_plan.argtypes = [c_vp, P(PathGraph), c_vp, c_i, P(GridInfo), P(PathQuery), P(PathOut)]
         L.aos_stream.restype = c_vp
         L.aos_stream.argtypes = [c_vp]
         _lib = L
@@ -289,6 +354,26 @@ class Ctx:
         o = GvdOut()
         _check(lib().aos_gvd_from_seedgen(self.h, ctypes.byref(o)))
         return _gvd_dict(o)
+
+    def path_plan(self, query: PathQuery | None = None, graph: dict | None = None, skeleton=None, info: dict | None = None,
+                  on_device: bool = False) -> dict:
+        """aos_path_gen_node graphCallback + planAndPublishPath (aos_path_plan). graph None: this
+        handle's last GVD graph; skeleton None: the skeleton that graph was built on."""
+        q = query if query is not None else path_query()
+        gs, keep = path_graph(graph) if graph is not None else (None, None)
+        gi, sk = None, None
+        if skeleton is not None:
+            gi = GridInfo(info["origin"][0], info["origin"][1], info["resolution"], info["width"], info["height"])
+            if on_device:
+                sk = c_vp(int(skeleton))
+            else:
+                keep = (keep, np.ascontiguousarray(skeleton, dtype=np.int8).reshape(-1))
+                sk = keep[1].ctypes.data_as(c_vp)
+        o = PathOut()
+        _check(lib().aos_path_plan(self.h, ctypes.byref(gs) if gs is not None else None, sk, int(on_device),
+                                   ctypes.byref(gi) if gi is not None else None, ctypes.byref(q), ctypes.byref(o)))
+        del keep
+        return _path_dict(o)
 
     def gvd_markers(self) -> dict:
         """/gvd/markers content of the last GVD call (aos_gvd_markers_get)."""

@@ -51,6 +51,13 @@ struct aos_ctx {
 
     // ---- GVD (gvd.hip)
     aos::GvdState gs;
+    bool have_gvd = false, gvd_from_frame = false;
+    uint64_t frame_gen = 0, gvd_frame_gen = 0, gvd_gen = 0;   // seed-gen frames / GVD calls so far
+    const int8_t *gvd_skel = nullptr;                          // the skeleton the last GVD call used
+    aos_grid_info gvd_info{};
+
+    // ---- path planning (path.hip)
+    void *path_state = nullptr;   // aos::PathState
 
     // Cells a frame rasterises / counts: [rx0, rx1) x [ry0, ry1) (clamped cell), stored into the
     // Wr x Hr byte window at cell (wx0, wy0); limit_box: bin only points in box (a tile's shard).
@@ -65,6 +72,8 @@ struct aos_ctx {
     void tile_halo_exchange(uint64_t *win, const aos::TilePlan &t, const aos_comm &cm);
     void run_gvd_external(const aos_gvd_in &in, aos_gvd_out &out);
     void run_gvd_from_frame(aos_gvd_out &out);
+    void run_path_plan(const aos_path_graph *graph, const int8_t *skeleton, int skeleton_on_device,
+                       const aos_grid_info *info, const aos_path_query &q, aos_path_out &out);
     int debug_grid(const char *which, int8_t *dst, uint64_t capacity);
     void release();
 };

@@ -133,6 +133,8 @@ struct TilePlan {
     float box[4];               // x/y box of the points this rank needs (xmin, ymin, xmax, ymax)
     uint64_t exchange_bytes;    // per-rank all-gather chunk
 };
+void free_path_state(void *p);   // path.hip
+
 TilePlan make_tile_plan(const FrameGeom &g, float margin, int tiles_x, int tiles_y, int rank);
 
 }  // namespace aos

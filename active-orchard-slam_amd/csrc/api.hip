@@ -256,6 +256,29 @@ int aos_gvd_markers_get(aos_ctx *c, aos_gvd_markers *out) {
     return AOS_OK;
 }
 
+int aos_path_plan(aos_ctx *c, const aos_path_graph *graph, const int8_t *skeleton, int skeleton_on_device,
+                  const aos_grid_info *info, const aos_path_query *query, aos_path_out *out) {
+    if (!c || !query || !out) { set_error("aos_path_plan: null argument"); return AOS_E_INVALID; }
+    if (skeleton && !info) { set_error("aos_path_plan: skeleton without grid info"); return AOS_E_INVALID; }
+    if (skeleton && (info->width == 0 || info->height == 0 || !(info->resolution > 0.0f))) {
+        set_error("aos_path_plan: empty skeleton grid or resolution <= 0");
+        return AOS_E_INVALID;
+    }
+    if (graph && (graph->num_nodes < 0 || graph->num_edges < 0 || graph->n_label_entries < 0 ||
+                  (graph->num_nodes && (!graph->nodes_xy || !graph->node_labels || !graph->node_cluster_indices ||
+                                        !graph->node_label_counts)) ||
+                  (graph->num_edges && (!graph->edges || !graph->edge_lengths)) ||
+                  (graph->n_label_entries && (!graph->node_label_clusters || !graph->node_label_types)))) {
+        set_error("aos_path_plan: inconsistent graph arrays");
+        return AOS_E_INVALID;
+    }
+    AOS_GUARD_BEGIN
+    DeviceScope dev_scope(c->device);
+    c->run_path_plan(graph, skeleton, skeleton_on_device, info, *query, *out);
+    return AOS_OK;
+    AOS_GUARD_END
+}
+
 int aos_debug_grid(aos_ctx *c, const char *which, int8_t *dst, uint64_t capacity) {
     if (!c || !which || !dst) { set_error("aos_debug_grid: null argument"); return AOS_E_INVALID; }
     if (!c->have_frame) { set_error("aos_debug_grid: no frame"); return AOS_E_STATE; }

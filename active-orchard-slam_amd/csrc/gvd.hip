@@ -963,7 +963,9 @@ void aos_ctx::run_gvd_external(const aos_gvd_in &in, aos_gvd_out &out) {
     int8_t *d_sk = static_cast<int8_t *>(gs.skel.ensure(std::max<size_t>(C, 1)));
     if (C && in.skeleton) AOS_HIP(hipMemcpyAsync(d_sk, in.skeleton, C, hipMemcpyHostToDevice, stream));
     GvdStageIn gi{in.seeds_xy, in.n_seeds, in.rows_info_xy, in.n_rows_poses, in.info, d_sk};
+    have_gvd = false;
     const bool pub = run_gvd_stage(gs, P, gi, stream, ev.data());
+    have_gvd = true; gvd_from_frame = false; gvd_skel = d_sk; gvd_info = in.info; ++gvd_gen;
     fill_gvd_out(*this, gs, in.info, pub, out);
 }
 
@@ -971,6 +973,8 @@ void aos_ctx::run_gvd_from_frame(aos_gvd_out &out) {
     aos_grid_info info{geom.origin_x, geom.origin_y, geom.res, (uint32_t)geom.W, (uint32_t)geom.H};
     GvdStageIn gi{h_voronoi.data(), (int)(h_voronoi.size() / 2), h_rows_info.data(), (int)(h_rows_info.size() / 2), info,
                   skel_bytes.as<int8_t>()};
+    have_gvd = false;
     const bool pub = run_gvd_stage(gs, P, gi, stream, ev.data());
+    have_gvd = true; gvd_from_frame = true; gvd_frame_gen = frame_gen; gvd_skel = gi.d_skeleton; gvd_info = info; ++gvd_gen;
     fill_gvd_out(*this, gs, info, pub, out);
 }

@@ -29,6 +29,9 @@ void aos_ctx::release() {
         b->release();
     cs.h_misc.release();
     markers_wait(gs, false);
+    free_path_state(path_state);
+    path_state = nullptr;
+    have_gvd = false;
     free_gvd_scratch(gs);
     gs.cells.reset();
     for (DevBuf *b : {&gs.seeds, &gs.merge_state, &gs.hash_count, &gs.hash_start, &gs.hash_slot, &gs.hash_sorted,
@@ -298,6 +301,7 @@ void aos_ctx::run_seedgen(bool want_host, aos_seedgen_out &out) {
 // the kept-candidate count when it was reduced over tiles (else read from this handle's counters).
 void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *clipped_total, aos_seedgen_out &out) {
     hipStream_t s = stream;
+    ++frame_gen;   // skel_bytes is rewritten below
     const size_t C = (size_t)g.W * g.H;
     int8_t *d_occ = occ_bytes.as<int8_t>();
 

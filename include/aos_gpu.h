@@ -224,6 +224,54 @@ typedef struct aos_gvd_markers {
 } aos_gvd_markers;
 int aos_gvd_markers_get(aos_ctx *ctx, aos_gvd_markers *out);
 
+/* ---------------------------------------------------------------------------------------------
+ * Path planning over the GvdGraph (aos_path_gen_node): graphCallback
+ * (path_gen:418-579) = cluster waypoint mapping (:704-765) + waypoint sequence (:588-702) + target
+ * restore (:496-560), then planAndPublishPath (:976-1567): weighted A* (:800-896) from the 5 nodes
+ * nearest the start (:914-932), the straight 0.2 m segments, orientations, and
+ * trimPathNearOccupiedRegions (:1570-1630) on the skeleton. The node's state goes in as
+ * aos_path_query; the published /path poses, the status and the indices come out.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct aos_path_graph {          /* msg/GvdGraph.msg */
+    int32_t num_nodes; const double *nodes_xy;
+    const int32_t *node_labels, *node_cluster_indices, *node_label_counts;
+    int32_t n_label_entries; const int32_t *node_label_clusters, *node_label_types;
+    int32_t num_edges; const int32_t *edges; const float *edge_lengths;
+} aos_path_graph;
+
+typedef struct aos_path_query {
+    int32_t initial_waypoint_reached;    /* 0: straight line (0, 0) -> initial waypoint (:983-1031) */
+    double initial_waypoint_xy[2];       /* (8, 0) in the reference (:81-83)                      */
+    int32_t target_waypoint_index;       /* current_target_waypoint_index_ before this graph (-1)  */
+    int32_t have_saved_target;           /* that index was valid: its position follows            */
+    double saved_target_xy[2];
+    int32_t previous_waypoint_index;     /* previous_waypoint_index_ (-1: start at the initial waypoint) */
+    int32_t use_current_position;        /* service call with a received position (:1062-1066)    */
+    double current_xy[2];
+    int32_t exploration_completed;       /* the origin (0, 0) ends the sequence (node -1, :1096-1280);
+                                            modelled as this graph's sequence plus the origin      */
+} aos_path_query;
+
+typedef struct aos_path_out {
+    int32_t status;                      /* publishPlanningStatus: 1 "Success", 0 "Failed"          */
+    int32_t target_waypoint_index;       /* after the restore                                       */
+    int32_t cluster_index;               /* calculateClusterIndex (:1633-1652)                      */
+    int32_t n_clusters;                  /* cluster_waypoint_nodes_, ascending cluster id           */
+    const int32_t *cluster_ids, *cluster_nodes;   /* 4 per cluster: TL, TR, BL, BR node (-1: none) */
+    int32_t n_waypoints; const double *waypoints_xy; const int32_t *waypoint_nodes;
+    int32_t n_node_path; const int32_t *node_path;   /* the chosen A* node path                   */
+    int32_t n_poses; const double *poses;            /* x, y, qz, qw per /path pose (z = 0)       */
+    int32_t trimmed_from;                /* pose count before the trim, or -1                       */
+    float ms_plan;
+} aos_path_out;
+
+/* graph: NULL = this handle's last GVD graph. skeleton: /skeletonized_occupancy_grid bytes, host
+ * memory (skeleton_on_device = 0) or device memory on the handle's GPU (1), with `info`; NULL = the
+ * skeleton that graph was built on (AOS_E_STATE if a later seed-gen frame replaced it). On
+ * "Failed" the outputs hold no poses: the node republishes its last path. */
+int aos_path_plan(aos_ctx *ctx, const aos_path_graph *graph, const int8_t *skeleton, int skeleton_on_device,
+                  const aos_grid_info *info, const aos_path_query *query, aos_path_out *out);
+
 /* Diagnostics: copy an internal device grid of the last frame to host as int8 {0,100} (or 0/1
  * for "opened"). which: "raster", "inflated", "opened", "skeleton_frameless". */
 int aos_debug_grid(aos_ctx *ctx, const char *which, int8_t *dst, uint64_t capacity);

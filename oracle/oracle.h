@@ -96,6 +96,37 @@ typedef struct orc_gvd_out {
 
 void *orc_gvd_run(const orc_params *p, const orc_gvd_in *in, orc_gvd_out *out);
 
+/* ---------- path planning over the GvdGraph (aos_path_gen_node) ---------- */
+typedef struct orc_path_graph {      /* msg/GvdGraph.msg */
+    int32_t num_nodes; const double *nodes_xy;
+    const int32_t *node_labels, *node_cluster_indices, *node_label_counts;
+    int32_t n_label_entries; const int32_t *node_label_clusters, *node_label_types;
+    int32_t num_edges; const int32_t *edges; const float *edge_lengths;
+} orc_path_graph;
+
+typedef struct orc_path_query {      /* the node's state when the graph arrives */
+    int32_t initial_waypoint_reached; double initial_waypoint_xy[2];
+    int32_t target_waypoint_index;    /* current_target_waypoint_index_ before the graph (-1: none) */
+    int32_t have_saved_target; double saved_target_xy[2];   /* its position in the old sequence */
+    int32_t previous_waypoint_index;
+    int32_t use_current_position; double current_xy[2];
+    int32_t exploration_completed;    /* with the origin (0, 0) as the last waypoint (node -1) */
+} orc_path_query;
+
+typedef struct orc_path_out {
+    int32_t status;                   /* publishPlanningStatus: 1 Success, 0 Failed */
+    int32_t target_waypoint_index, cluster_index;
+    int32_t n_clusters; const int32_t *cluster_ids, *cluster_nodes;   /* 4 per cluster: TL TR BL BR */
+    int32_t n_waypoints; const double *waypoints_xy; const int32_t *waypoint_nodes;
+    int32_t n_node_path; const int32_t *node_path;   /* the chosen A* path */
+    int32_t n_poses; const double *poses;            /* x, y, qz, qw per pose (published /path) */
+    int32_t trimmed_from;             /* poses before trimPathNearOccupiedRegions, or -1 */
+} orc_path_out;
+
+void *orc_path_plan(const orc_path_graph *g, const int8_t *skeleton, double origin_x, double origin_y,
+                    float resolution, uint32_t width, uint32_t height, const orc_path_query *q, orc_path_out *out);
+void orc_free_path(void *handle);
+
 void orc_free_seedgen(void *handle);
 void orc_free_gvd(void *handle);
 void orc_free_facets(void *handle);

@@ -465,8 +465,8 @@ static V2 cast_ray(const GridView &g, V2 start_point, V2 other, double angle_off
     V2 perp{-e2o.y, e2o.x};
     double a = angle_offset_deg * M_PI / 180.0;
     V2 ray;
-    if (angle_offset_deg > 0) ray = std::cos(a) * outward + std::sin(a) * perp;
-    else ray = std::cos(-a) * outward + std::sin(-a) * (-perp);
+    if (angle_offset_deg > 0) ray = lib_cos(a) * outward + lib_sin(a) * perp;
+    else ray = lib_cos(-a) * outward + lib_sin(-a) * (-perp);
     ray = normalized(ray);
     auto inside = [&](V2 p) { return p.x >= g.minx() && p.x <= g.maxx() && p.y >= g.miny() && p.y <= g.maxy(); };
     double step_size = g.gi.resolution * 0.5;

@@ -29,6 +29,11 @@ inline V2 normalized(V2 a) {
     return a;
 }
 
+// The reference is built without optimisation (colcon without CMAKE_BUILD_TYPE; CMakeLists.txt:12):
+// sin and cos are separate libm calls, never fused into one sincos (which can differ by an ulp).
+__attribute__((noinline)) inline double lib_sin(double a) { return std::sin(a); }
+__attribute__((noinline)) inline double lib_cos(double a) { return std::cos(a); }
+
 struct GridInfo { double origin_x, origin_y; float resolution; uint32_t width, height; };
 
 struct Cluster {

@@ -60,8 +60,27 @@ class GvdOut(ctypes.Structure):
                 ("cell_rgba", P(c_f))]
 
 
+class PathGraph(ctypes.Structure):
+    _fields_ = [("num_nodes", c_i), ("nodes_xy", P(c_d)), ("node_labels", P(c_i)), ("node_cluster_indices", P(c_i)),
+                ("node_label_counts", P(c_i)), ("n_label_entries", c_i), ("node_label_clusters", P(c_i)),
+                ("node_label_types", P(c_i)), ("num_edges", c_i), ("edges", P(c_i)), ("edge_lengths", P(c_f))]
+
+
+class PathQuery(ctypes.Structure):
+    _fields_ = [("initial_waypoint_reached", c_i), ("initial_waypoint_xy", c_d * 2), ("target_waypoint_index", c_i),
+                ("have_saved_target", c_i), ("saved_target_xy", c_d * 2), ("previous_waypoint_index", c_i),
+                ("use_current_position", c_i), ("current_xy", c_d * 2), ("exploration_completed", c_i)]
+
+
+class PathOut(ctypes.Structure):
+    _fields_ = [("status", c_i), ("target_waypoint_index", c_i), ("cluster_index", c_i), ("n_clusters", c_i),
+                ("cluster_ids", P(c_i)), ("cluster_nodes", P(c_i)), ("n_waypoints", c_i), ("waypoints_xy", P(c_d)),
+                ("waypoint_nodes", P(c_i)), ("n_node_path", c_i), ("node_path", P(c_i)), ("n_poses", c_i),
+                ("poses", P(c_d)), ("trimmed_from", c_i)]
+
+
 def build_lib() -> str:
-    srcs = [os.path.join(_HERE, f) for f in ("oracle_seedgen.cpp", "oracle_gvd.cpp", "oracle_capi.cpp",
+    srcs = [os.path.join(_HERE, f) for f in ("oracle_seedgen.cpp", "oracle_gvd.cpp", "oracle_path.cpp", "oracle_capi.cpp",
                                                "oracle.h", "oracle_internal.h")]
     if not os.path.exists(_LIB) or os.path.getmtime(_LIB) < max(os.path.getmtime(s) for s in srcs):
         subprocess.check_call(["make", "-s", "-C", _HERE, "liboracle.so"])
@@ -82,7 +101,9 @@ def lib():
                                       c_i, P(SeedGenOut)]
         L.orc_gvd_run.restype = ctypes.c_void_p
         L.orc_gvd_run.argtypes = [P(Params), P(GvdIn), P(GvdOut)]
-        for f in ("orc_free_seedgen", "orc_free_gvd", "orc_free_facets"):
+        L.orc_path_plan.restype = ctypes.c_void_p
+        L.orc_path_plan.argtypes = [P(PathGraph), ctypes.c_void_p, c_d, c_d, c_f, c_u, c_u, P(PathQuery), P(PathOut)]
+        for f in ("orc_free_seedgen", "orc_free_gvd", "orc_free_facets", "orc_free_path"):
             getattr(L, f).argtypes = [ctypes.c_void_p]
         L.orc_ror.argtypes = [ctypes.c_void_p, c_u64, c_i, c_d, c_i, ctypes.c_void_p]
         L.orc_inflate.argtypes = [ctypes.c_void_p, c_u, c_u, c_i, ctypes.c_void_p]
@@ -241,3 +262,46 @@ def subdiv_facets(seeds: np.ndarray, bounds, rect_mode=0):
     finally:
         lib().orc_free_facets(h)
     return [facets[o[i]:o[i + 1]] for i in range(n)], centers
+
+
+def path_plan(graph: dict, grid: dict, initial_waypoint_reached=True, initial_waypoint=(8.0, 0.0), target=-1,
+              saved_target=None, previous=-1, current=None, exploration_completed=False) -> dict:
+    """aos_path_gen_node graphCallback + planAndPublishPath on a GvdGraph dict and the
+    /skeletonized_occupancy_grid (grid: origin/resolution/width/height/skeleton_framed)."""
+    nodes = np.ascontiguousarray(graph["nodes"], dtype=np.float64).reshape(-1)
+    a = {k: np.ascontiguousarray(graph[k], dtype=np.int32).reshape(-1)
+         for k in ("node_labels", "node_cluster_indices", "node_label_counts", "node_label_clusters",
+                   "node_label_types", "edges")}
+    lens = np.ascontiguousarray(graph["edge_lengths"], dtype=np.float32).reshape(-1)
+    ip = lambda x: x.ctypes.data_as(P(c_i))  # noqa: E731
+    g = PathGraph(nodes.size // 2, nodes.ctypes.data_as(P(c_d)), ip(a["node_labels"]), ip(a["node_cluster_indices"]),
+                  ip(a["node_label_counts"]), a["node_label_clusters"].size, ip(a["node_label_clusters"]),
+                  ip(a["node_label_types"]), a["edges"].size // 2, ip(a["edges"]), lens.ctypes.data_as(P(c_f)))
+    q = PathQuery()
+    q.initial_waypoint_reached = int(bool(initial_waypoint_reached))
+    q.initial_waypoint_xy[:] = list(initial_waypoint)
+    q.target_waypoint_index = target
+    if saved_target is not None:
+        q.have_saved_target = 1
+        q.saved_target_xy[:] = list(saved_target)
+    q.previous_waypoint_index = previous
+    if current is not None:
+        q.use_current_position = 1
+        q.current_xy[:] = list(current)
+    q.exploration_completed = int(bool(exploration_completed))
+    sk = np.ascontiguousarray(grid["skeleton_framed"], dtype=np.int8).reshape(-1)
+    out = PathOut()
+    h = lib().orc_path_plan(ctypes.byref(g), sk.ctypes.data, grid["origin"][0], grid["origin"][1], grid["resolution"],
+                            grid["width"], grid["height"], ctypes.byref(q), ctypes.byref(out))
+    try:
+        nc = out.n_clusters
+        return {"status": out.status, "target": out.target_waypoint_index, "cluster_index": out.cluster_index,
+                "cluster_ids": _arr(out.cluster_ids, nc, np.int32),
+                "cluster_nodes": _arr(out.cluster_nodes, 4 * nc, np.int32).reshape(-1, 4),
+                "waypoints": _arr(out.waypoints_xy, 2 * out.n_waypoints, np.float64).reshape(-1, 2),
+                "waypoint_nodes": _arr(out.waypoint_nodes, out.n_waypoints, np.int32),
+                "node_path": _arr(out.node_path, out.n_node_path, np.int32),
+                "poses": _arr(out.poses, 4 * out.n_poses, np.float64).reshape(-1, 4),
+                "trimmed_from": out.trimmed_from}
+    finally:
+        lib().orc_free_path(h)

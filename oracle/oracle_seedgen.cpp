@@ -309,8 +309,8 @@ static V2 cast_ray_from_endpoint(V2 start, V2 other, double angle_offset_deg, co
     V2 perp{-e2o.y, e2o.x};
     double a = angle_offset_deg * M_PI / 180.0;
     V2 ray;
-    if (angle_offset_deg > 0) ray = std::cos(a) * outward + std::sin(a) * perp;
-    else ray = std::cos(-a) * outward + std::sin(-a) * (-perp);
+    if (angle_offset_deg > 0) ray = lib_cos(a) * outward + lib_sin(a) * perp;
+    else ray = lib_cos(-a) * outward + lib_sin(-a) * (-perp);
     ray = normalized(ray);
     const double minx = gi.origin_x, maxx = minx + gi.width * gi.resolution;
     const double miny = gi.origin_y, maxy = miny + gi.height * gi.resolution;
