@@ -190,6 +190,8 @@ def lib():
         L.aos_seedgen_reprocess.argtypes = [c_vp, c_i, P(SeedGenOut)]
         L.aos_gvd_process.argtypes = [c_vp, P(GvdIn), P(GvdOut)]
         L.aos_gvd_from_seedgen.argtypes = [c_vp, P(GvdOut)]
+        L.aos_gvd_from_seedgen_async.argtypes = [c_vp]
+        L.aos_gvd_wait.argtypes = [c_vp, P(GvdOut)]
         L.aos_debug_grid.argtypes = [c_vp, ctypes.c_char_p, c_vp, c_u64]
         L.aos_gvd_markers_get.argtypes = [c_vp, P(GvdMarkers)]
         L.aos_map_reset.argtypes = [c_vp, c_u64]
@@ -374,6 +376,16 @@ class Ctx:
                                    ctypes.byref(gi) if gi is not None else None, ctypes.byref(q), ctypes.byref(o)))
         del keep
         return _path_dict(o)
+
+    def gvd_async(self) -> None:
+        """Start the GVD of the last seed-gen frame in the background (aos_gvd_from_seedgen_async)."""
+        _check(lib().aos_gvd_from_seedgen_async(self.h))
+
+    def gvd_wait(self) -> dict:
+        """The graph of the background GVD (aos_gvd_wait)."""
+        o = GvdOut()
+        _check(lib().aos_gvd_wait(self.h, ctypes.byref(o)))
+        return _gvd_dict(o)
 
     def gvd_markers(self) -> dict:
         """/gvd/markers content of the last GVD call (aos_gvd_markers_get)."""

@@ -1,6 +1,10 @@
 // Per-handle state of libaos_gpu.so. Not part of the ABI.
 #pragma once
 #include <array>
+#include <condition_variable>
+#include <exception>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "aos_internal.h"
@@ -56,6 +60,26 @@ struct aos_ctx {
     const int8_t *gvd_skel = nullptr;                          // the skeleton the last GVD call used
     aos_grid_info gvd_info{};
 
+    // ---- pipelined GVD (aos_gvd_from_seedgen_async): the reference runs seed-gen and the GVD as two
+    // nodes, so frame k + 1's seed-gen overlaps frame k's graph. The GVD of a snapshot of the frame
+    // (seeds, rows, skeleton) runs on a persistent worker thread and its own stream.
+    struct AsyncGvd {
+        std::thread worker;
+        std::mutex mu;
+        std::condition_variable cv;
+        bool busy = false, quit = false, pub = false, done = false, applied = false, prefix = false;
+        std::exception_ptr err;
+        hipStream_t stream = nullptr;
+        std::array<hipEvent_t, 16> ev{};
+        hipEvent_t ready = nullptr;               // the snapshot copy on the seed-gen stream
+        std::vector<double> seeds, rows;          // snapshot of h_voronoi / h_rows_info
+        aos_grid_info info{};
+    } ag;
+    void gvd_async_start();
+    bool gvd_async_wait(bool rethrow, bool consume);   // true if a finished job's graph is in gs
+    void gvd_async_drop();
+    void gvd_async_stop();
+
     // ---- path planning (path.hip)
     void *path_state = nullptr;   // aos::PathState
 
@@ -77,3 +101,8 @@ struct aos_ctx {
     int debug_grid(const char *which, int8_t *dst, uint64_t capacity);
     void release();
 };
+
+namespace aos {
+// aos_gvd_wait: collects the pipelined GVD job's graph into out; 0 if no job was started (gvd.hip)
+int gvd_wait_out(aos_ctx *c, aos_gvd_out *out);
+}  // namespace aos

@@ -196,6 +196,25 @@ int aos_gvd_from_seedgen(aos_ctx *c, aos_gvd_out *out) {
     AOS_GUARD_END
 }
 
+int aos_gvd_from_seedgen_async(aos_ctx *c) {
+    if (!c) { set_error("aos_gvd_from_seedgen_async: null handle"); return AOS_E_INVALID; }
+    if (!c->have_frame) { set_error("aos_gvd_from_seedgen_async: no seed-gen frame yet"); return AOS_E_STATE; }
+    AOS_GUARD_BEGIN
+    DeviceScope dev_scope(c->device);
+    c->gvd_async_start();
+    return AOS_OK;
+    AOS_GUARD_END
+}
+
+int aos_gvd_wait(aos_ctx *c, aos_gvd_out *out) {
+    if (!c || !out) { set_error("aos_gvd_wait: null argument"); return AOS_E_INVALID; }
+    AOS_GUARD_BEGIN
+    DeviceScope dev_scope(c->device);
+    if (!gvd_wait_out(c, out)) { set_error("aos_gvd_wait: no GVD job started since the last wait"); return AOS_E_STATE; }
+    return AOS_OK;
+    AOS_GUARD_END
+}
+
 int aos_tile_plan_compute(const aos_params *p, const double *poly_xy, uint32_t n_poly, int32_t tiles_x,
                           int32_t tiles_y, int32_t rank, aos_tile_plan *out) {
     if (!p || !out) { set_error("aos_tile_plan_compute: null argument"); return AOS_E_INVALID; }
@@ -238,6 +257,7 @@ int aos_gvd_markers_get(aos_ctx *c, aos_gvd_markers *out) {
     if (!c || !out) { set_error("aos_gvd_markers_get: null argument"); return AOS_E_INVALID; }
     GvdState &G = c->gs;
     AOS_GUARD_BEGIN
+    c->gvd_async_wait(false, false);
     markers_wait(G, true);   // the cells run on after the graph is returned
     AOS_GUARD_END
     if (!G.have_markers || !G.cells) {

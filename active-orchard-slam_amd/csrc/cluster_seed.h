@@ -138,6 +138,10 @@ struct GvdStageIn {
     const double *rows_info;   int n_rows_poses;
     aos_grid_info info;
     const int8_t *d_skeleton;                   // framed skeleton bytes on device
+    // called once the merged seeds are on the host, when the GPU prefix is done and the host
+    // Subdiv2D replay starts (the pipelined caller lets the next seed-gen frame go from here)
+    void (*on_host_phase)(void *) = nullptr;
+    void *hook_arg = nullptr;
 };
 bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipStream_t stream, hipEvent_t *ev);
 void free_gvd_scratch(GvdState &G);

@@ -735,6 +735,7 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     AOS_HIP(hipEventRecord(ev[7], s));
     G.merged_xy = merged;
     if (P.gvd_markers) markers_start(G, P.subdiv_rect_mode);
+    if (in.on_host_phase) in.on_host_phase(in.hook_arg);
 
     // ---- g3/g4 finite filter, bounds, Subdiv2D inserts (host replay) -> facets / Voronoi edges (GPU)
     auto t0 = std::chrono::steady_clock::now();
@@ -959,6 +960,7 @@ static void fill_gvd_out(const aos_ctx &c, const GvdState &G, const aos_grid_inf
 }
 
 void aos_ctx::run_gvd_external(const aos_gvd_in &in, aos_gvd_out &out) {
+    gvd_async_drop();
     const size_t C = (size_t)in.info.width * in.info.height;
     int8_t *d_sk = static_cast<int8_t *>(gs.skel.ensure(std::max<size_t>(C, 1)));
     if (C && in.skeleton) AOS_HIP(hipMemcpyAsync(d_sk, in.skeleton, C, hipMemcpyHostToDevice, stream));
@@ -970,6 +972,7 @@ void aos_ctx::run_gvd_external(const aos_gvd_in &in, aos_gvd_out &out) {
 }
 
 void aos_ctx::run_gvd_from_frame(aos_gvd_out &out) {
+    gvd_async_drop();
     aos_grid_info info{geom.origin_x, geom.origin_y, geom.res, (uint32_t)geom.W, (uint32_t)geom.H};
     GvdStageIn gi{h_voronoi.data(), (int)(h_voronoi.size() / 2), h_rows_info.data(), (int)(h_rows_info.size() / 2), info,
                   skel_bytes.as<int8_t>()};
@@ -977,4 +980,125 @@ void aos_ctx::run_gvd_from_frame(aos_gvd_out &out) {
     const bool pub = run_gvd_stage(gs, P, gi, stream, ev.data());
     have_gvd = true; gvd_from_frame = true; gvd_frame_gen = frame_gen; gvd_skel = gi.d_skeleton; gvd_info = info; ++gvd_gen;
     fill_gvd_out(*this, gs, info, pub, out);
+}
+
+// ------------------------------------------------------------------ pipelined GVD
+// aos_gvd_from_seedgen_async: snapshot the frame's GVD inputs (host seeds and rows, a device copy of
+// the skeleton ordered on the seed-gen stream) and hand them to the worker, which runs the same
+// run_gvd_stage on its own stream. The next seed-gen frame may run meanwhile; it rewrites only
+// seed-gen state. Every other GVD-side call waits for the job first.
+void aos_ctx::gvd_async_start() {
+    gvd_async_drop();
+    AsyncGvd &A = ag;
+    if (!A.stream) {
+        AOS_HIP(hipStreamCreateWithFlags(&A.stream, hipStreamNonBlocking));
+        for (auto &e : A.ev) AOS_HIP(hipEventCreate(&e));
+        AOS_HIP(hipEventCreateWithFlags(&A.ready, hipEventDisableTiming));
+    }
+    A.seeds = h_voronoi;
+    A.rows = h_rows_info;
+    A.info = aos_grid_info{geom.origin_x, geom.origin_y, geom.res, (uint32_t)geom.W, (uint32_t)geom.H};
+    const size_t C = (size_t)geom.W * geom.H;
+    int8_t *d_sk = static_cast<int8_t *>(gs.skel.ensure(std::max<size_t>(C, 1)));
+    AOS_HIP(hipMemcpyAsync(d_sk, skel_bytes.p, C, hipMemcpyDeviceToDevice, stream));
+    AOS_HIP(hipEventRecord(A.ready, stream));
+    AOS_HIP(hipStreamWaitEvent(A.stream, A.ready, 0));
+    have_gvd = false;
+    if (!A.worker.joinable())
+        A.worker = std::thread([this]() {
+            AsyncGvd &W = ag;
+            std::unique_lock<std::mutex> l(W.mu);
+            for (;;) {
+                W.cv.wait(l, [&W] { return W.busy || W.quit; });
+                if (W.quit) return;
+                l.unlock();
+                std::exception_ptr e;
+                bool pub = false;
+                try {
+                    AOS_HIP(hipSetDevice(device));
+                    GvdStageIn gi{W.seeds.data(), (int)(W.seeds.size() / 2), W.rows.data(), (int)(W.rows.size() / 2),
+                                  W.info, gs.skel.as<int8_t>()};
+                    gi.hook_arg = &W;
+                    gi.on_host_phase = [](void *p) {
+                        AsyncGvd *A = static_cast<AsyncGvd *>(p);
+                        { std::lock_guard<std::mutex> g(A->mu); A->prefix = true; }
+                        A->cv.notify_all();
+                    };
+                    pub = run_gvd_stage(gs, P, gi, W.stream, W.ev.data());
+                } catch (...) { e = std::current_exception(); }
+                l.lock();
+                W.err = e;
+                W.pub = pub;
+                W.busy = false;
+                W.done = true;
+                W.cv.notify_all();
+            }
+        });
+    {
+        std::lock_guard<std::mutex> l(A.mu);
+        A.err = nullptr;
+        A.done = false;
+        A.applied = false;
+        A.prefix = false;
+        A.busy = true;
+    }
+    A.cv.notify_all();
+    // Return once the job's short GPU prefix (seed merge) is done and its host replay runs: a
+    // seed-gen frame launched earlier would occupy the GPU and hold the prefix back, and the replay
+    // would start late instead of overlapping it.
+    std::unique_lock<std::mutex> l(A.mu);
+    A.cv.wait(l, [&A] { return A.prefix || !A.busy; });
+}
+
+// Waits for the job in flight. consume (aos_gvd_wait): collect its result once, raising its error
+// if rethrow. Otherwise (any other GVD-side call): only settle the handle's GVD bookkeeping.
+bool aos_ctx::gvd_async_wait(bool rethrow, bool consume) {
+    AsyncGvd &A = ag;
+    if (!A.worker.joinable()) return false;
+    std::unique_lock<std::mutex> l(A.mu);
+    A.cv.wait(l, [&A] { return !A.busy; });
+    if (!A.done) return false;
+    if (!A.err && !A.applied) {
+        have_gvd = true; gvd_from_frame = false; gvd_skel = gs.skel.as<int8_t>(); gvd_info = A.info; ++gvd_gen;
+        A.applied = true;
+    }
+    if (!consume) return true;
+    A.done = false;
+    if (A.err) {
+        std::exception_ptr e = A.err;
+        A.err = nullptr;
+        if (rethrow) std::rethrow_exception(e);
+        return false;
+    }
+    return true;
+}
+
+// A synchronous GVD call or a new job supersedes an uncollected result.
+void aos_ctx::gvd_async_drop() {
+    gvd_async_wait(false, false);
+    std::lock_guard<std::mutex> l(ag.mu);
+    ag.done = false;
+    ag.err = nullptr;
+}
+
+void aos_ctx::gvd_async_stop() {
+    AsyncGvd &A = ag;
+    if (A.worker.joinable()) {
+        { std::lock_guard<std::mutex> l(A.mu); A.quit = true; }
+        A.cv.notify_all();
+        A.worker.join();
+    }
+    if (A.stream) {
+        (void)hipStreamSynchronize(A.stream);
+        for (auto &e : A.ev) (void)hipEventDestroy(e);
+        (void)hipEventDestroy(A.ready);
+        (void)hipStreamDestroy(A.stream);
+        A.stream = nullptr;
+    }
+}
+
+int aos::gvd_wait_out(aos_ctx *c, aos_gvd_out *out) {   // aos_gvd_wait (api.hip)
+    if (!c->gvd_async_wait(true, true)) return 0;
+    fill_gvd_out(*c, c->gs, c->ag.info, c->ag.pub, *out);
+    return 1;
 }

@@ -499,6 +499,7 @@ using namespace aos;
 void aos_ctx::run_path_plan(const aos_path_graph *graph, const int8_t *skeleton, int skeleton_on_device,
                             const aos_grid_info *info, const aos_path_query &q, aos_path_out &out) {
     const auto t0 = std::chrono::steady_clock::now();
+    gvd_async_wait(false, false);
     if (!path_state) path_state = new PathState();
     PathState &S = *static_cast<PathState *>(path_state);
     // the graph

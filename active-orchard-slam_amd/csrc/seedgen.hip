@@ -28,6 +28,7 @@ void aos_ctx::release() {
                       &cs.hash_start, &cs.hash_slot, &cs.hash_sorted, &cs.seed_out, &cs.misc, &cs.scan_tmp})
         b->release();
     cs.h_misc.release();
+    gvd_async_stop();   // joins a job in flight (it uses gs)
     markers_wait(gs, false);
     free_path_state(path_state);
     path_state = nullptr;

@@ -37,6 +37,10 @@ def parse(argv=None):
     ap.add_argument("--cpu-config", default="C1")
     ap.add_argument("--stream", action="store_true",
                     help="C4 (BASELINE configs[4]): 1 M-point 20 Hz scans appended to the device-resident C2 map")
+    ap.add_argument("--trace", action="store_true", help="per-step timeline of the pipelined loop on stderr")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="overlap frame k's seed-gen with frame k-1's GVD (aos_gvd_from_seedgen_async); the last "
+                         "frame's GVD drains inside the timed region, so it pays off only for many steps")
     ap.add_argument("--tiled", action="store_true",
                     help="one map split into tiles over the ranks (SURVEY §8e, BASELINE configs[3]); strong scaling")
     a = ap.parse_args(argv)
@@ -174,21 +178,37 @@ def main():
     # The markers' cells of a frame finish in the background after its graph (publishGraph before
     # publishMarkers, gvd:310-313): every step collects the previous frame's markers after its own
     # seed-gen, and the last step collects its own, so each timed frame includes its markers.
+    # Default (sequential): step k = seed-gen k, the markers of frame k - 1, then the GVD of frame k.
+    # --pipeline: the reference's seed-gen and GVD are two nodes, so frame k's seed-gen runs while
+    # frame k - 1's graph is built (aos_gvd_from_seedgen_async on the handle's GVD worker). Step k =
+    # seed-gen k, collect graph + markers of frame k - 1, start the GVD of frame k; the last step also
+    # collects its own frame, so every frame of the timed region completes inside it.
     n_calls = a.warmup + a.steps
-    pend = {"k": 0, "t0": None, "ms": 0.0}
+    pend = {"k": 0, "t0": {}, "mt0": None, "ms": 0.0}
+    pipeline = a.pipeline
 
     def collect():
         m = ctx.gvd_markers()
-        if pend["t0"] is not None and a.stream:
-            mk_latency.append(time.perf_counter() - pend["t0"])
+        if pend["mt0"] is not None and a.stream:
+            mk_latency.append(time.perf_counter() - pend["mt0"])
         pend["ms"] = m["ms_cells"]
-        pend["t0"] = None
+        pend["mt0"] = None
         return m
+
+    def finish(j):   # pipelined: frame j's graph, then its markers
+        gg = ctx.gvd_wait()
+        if a.stream:
+            latency.append(time.perf_counter() - pend["t0"][j])
+        pend["mt0"] = pend["t0"][j]
+        collect()
+        gg["ms"]["cells"] = pend["ms"]
+        return gg
 
     def step():
         k = pend["k"]
         pend["k"] += 1
         t0 = time.perf_counter()
+        pend["t0"][k] = t0
         if a.stream:
             g = ctx.map_append(scans[k], want_host=False)
         elif a.tiled:
@@ -198,12 +218,27 @@ def main():
                 return g, {"ms": {}, "nodes": (), "edges": ()}
         else:
             g = ctx.seedgen(d_cloud.data_ptr(), n_points=n, on_device=True, want_host=False)
+        if pipeline:
+            t1 = time.perf_counter()
+            gg = finish(k - 1) if k > 0 else None
+            t2 = time.perf_counter()
+            ctx.gvd_async()
+            t3 = time.perf_counter()
+            if k == n_calls - 1:
+                gg = finish(k)
+            if a.trace:
+                ms = gg["ms"] if gg is not None else {}
+                print(f"[trace] step {k}: seed-gen {1e3 * (t1 - t0):.2f} ms, wait graph+markers k-1 "
+                      f"{1e3 * (t2 - t1):.2f} ms, start GVD {1e3 * (t3 - t2):.2f} ms | frame k-1: delaunay "
+                      f"{ms.get('delaunay', 0):.1f} total {ms.get('total', 0):.1f} cells {ms.get('cells', 0):.1f}",
+                      file=sys.stderr, flush=True)
+            return g, gg
         if k > 0:
             collect()
         gg = ctx.gvd_from_seedgen()
         if a.stream:
             latency.append(time.perf_counter() - t0)
-        pend["t0"] = t0
+        pend["mt0"] = t0
         if k == n_calls - 1:
             collect()
         gg["ms"]["cells"] = pend["ms"]   # the previous frame's (the last step: its own)
@@ -212,15 +247,16 @@ def main():
     dt, res = timed_region(step, a.steps, a.warmup, world, torch.cuda.synchronize, dist, red_dev)
     g, gg = res[-1]
     stage = {}
+    n_gvd = sum(1 for _, ggs in res if ggs is not None)
     for gs, ggs in res:
         for k, v in gs["ms"].items():
-            stage["seedgen_" + k] = stage.get("seedgen_" + k, 0.0) + v
-        for k, v in ggs["ms"].items():
-            stage["gvd_" + k] = stage.get("gvd_" + k, 0.0) + v
+            stage["seedgen_" + k] = stage.get("seedgen_" + k, 0.0) + v / len(res)
+        for k, v in (ggs["ms"].items() if ggs is not None else ()):
+            stage["gvd_" + k] = stage.get("gvd_" + k, 0.0) + v / n_gvd
     cells = g["width"] * g["height"]
     # weak: every rank processes its own map; tiled: the ranks share one map (strong scaling)
     value = throughput(cells / 1e6, 1 if a.tiled else world, len(res), dt)
-    avg = {k: v / len(res) for k, v in stage.items()}
+    avg = stage
 
     # roofline of the dominant GPU kernel: the largest per-frame device time among the three ROR
     # kernels (bin, scatter, neighbour count), timed live with HIP events recorded on the handle's
@@ -276,6 +312,8 @@ def main():
             "data": "synthetic orchard (tools/orchard_gen.c, SplitMix64), device-resident PointCloud2",
             "config": {"workload": workload, "global_batch": 1 if a.tiled else world,
                        "parallelism": f"tiled{tx}x{ty}" if a.tiled else f"tiles{world}"},
+            "pipeline": "seed-gen of frame k overlaps the GVD of frame k-1 (the reference's two nodes)"
+                        if pipeline else "sequential",
             "stages_ms": {k: round(v, 3) for k, v in avg.items()},
             "frame": {"T": T, "rows": len(g["row_length"]), "seeds": len(g["voronoi_seeds"]),
                       "nodes": len(gg["nodes"]), "edges": len(gg["edges"]), "n_binned": g["n_binned"],

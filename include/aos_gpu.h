@@ -145,6 +145,14 @@ int aos_seedgen_process(aos_ctx *ctx, const aos_cloud_view *cloud, int want_host
 int aos_seedgen_reprocess(aos_ctx *ctx, int want_host, aos_seedgen_out *out);
 int aos_gvd_process(aos_ctx *ctx, const aos_gvd_in *in, aos_gvd_out *out);
 int aos_gvd_from_seedgen(aos_ctx *ctx, aos_gvd_out *out);
+/* Pipelined form: the reference runs seed-gen and the GVD as two nodes, so frame k + 1's seed-gen
+ * overlaps frame k's graph. _async snapshots the last seed-gen frame's GVD inputs (seeds, rows,
+ * skeleton) and starts the GVD on a worker thread and its own stream; aos_seedgen_process /
+ * aos_map_append may run meanwhile. aos_gvd_wait returns that graph (the same as
+ * aos_gvd_from_seedgen would have). Every other GVD-side call waits for the job first; a GVD call
+ * made before aos_gvd_wait supersedes the job's result. */
+int aos_gvd_from_seedgen_async(aos_ctx *ctx);
+int aos_gvd_wait(aos_ctx *ctx, aos_gvd_out *out);
 
 /* ---------------------------------------------------------------------------------------------
  * Streaming ingest (BASELINE.json configs[4]). The handle keeps the global

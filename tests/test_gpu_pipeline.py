@@ -1,0 +1,81 @@
+"""Pipelined GVD (aos_gvd_from_seedgen_async / aos_gvd_wait): the next seed-gen frame runs while the
+previous frame's graph is built, as the reference's two nodes do. The graph, the markers and the
+path planner must equal the sequential calls on the same frames."""
+import numpy as np
+import pytest
+
+import aos_gpu
+import orchard
+
+pytestmark = pytest.mark.gpu
+
+GRAPH_KEYS = ("nodes", "node_labels", "node_cluster_indices", "node_label_counts", "node_label_clusters",
+              "node_label_types", "edges", "edge_lengths", "edge_clearances")
+
+
+def assert_same_graph(a, b, what):
+    assert a["published"] == b["published"], what
+    for k in GRAPH_KEYS:
+        assert np.array_equal(a[k], b[k]), f"{what}: {k}"
+
+
+def assert_same_markers(a, b, what):
+    for k in ("seeds", "row_label_valid", "cell_offsets", "cell_xy", "cell_center", "cell_rgba"):
+        assert np.array_equal(a[k], b[k]), f"{what}: markers {k}"
+
+
+def frames():
+    cfg = orchard.CONFIGS["C1"]
+    poly = orchard.polygon(cfg)
+    return cfg, poly, [orchard.generate(cfg), orchard.generate(cfg, seed=cfg.seed + 7)]
+
+
+def test_pipelined_graph_equals_sequential():
+    cfg, poly, clouds = frames()
+    ref = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res))
+    ref.set_polygon(poly)
+    seq = []
+    for cl in clouds:
+        ref.seedgen(cl, want_host=False)
+        seq.append((ref.gvd_from_seedgen(), ref.gvd_markers(), ref.path_plan(aos_gpu.path_query(target=3, previous=2))))
+    ref.close()
+
+    c = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res))
+    c.set_polygon(poly)
+    c.seedgen(clouds[0], want_host=False)
+    c.gvd_async()
+    c.seedgen(clouds[1], want_host=False)      # overlaps frame 0's graph
+    g0 = c.gvd_wait()
+    assert_same_graph(g0, seq[0][0], "frame 0")
+    assert_same_markers(c.gvd_markers(), seq[0][1], "frame 0")
+    # frame 0's skeleton was snapshotted: planning on its graph still works after frame 1's seed-gen
+    p0 = c.path_plan(aos_gpu.path_query(target=3, previous=2))
+    assert np.array_equal(p0["poses"], seq[0][2]["poses"]) and np.array_equal(p0["node_path"], seq[0][2]["node_path"])
+    c.gvd_async()                              # frame 1
+    m_first = None
+    try:
+        m_first = c.gvd_markers()              # waits for the job without collecting it
+    finally:
+        g1 = c.gvd_wait()
+    assert_same_graph(g1, seq[1][0], "frame 1")
+    assert_same_markers(m_first, seq[1][1], "frame 1")
+    c.close()
+
+
+def test_pipeline_state_rules():
+    cfg, poly, clouds = frames()
+    c = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res))
+    c.set_polygon(poly)
+    with pytest.raises(RuntimeError, match="no seed-gen frame"):
+        c.gvd_async()
+    c.seedgen(clouds[0], want_host=False)
+    with pytest.raises(RuntimeError, match="no GVD job"):
+        c.gvd_wait()
+    c.gvd_async()
+    g_sync = c.gvd_from_seedgen()               # supersedes the job's result
+    with pytest.raises(RuntimeError, match="no GVD job"):
+        c.gvd_wait()
+    c.gvd_async()
+    assert_same_graph(c.gvd_wait(), g_sync, "re-run")
+    c.gvd_async()
+    c.close()                                  # a job in flight is joined
