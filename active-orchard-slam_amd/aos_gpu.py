@@ -199,6 +199,13 @@ def lib():
         L.aos_tile_plan_compute.argtypes = [P(Params), c_vp, c_u, c_i, c_i, c_i, P(TilePlan)]
         L.aos_tiled_seedgen_process.argtypes = [c_vp, P(Comm), c_i, c_i, c_i, P(CloudView), c_i, P(SeedGenOut)]
         L.aos_path_plan.argtypes = [c_vp, P(PathGraph), c_vp, c_i, P(GridInfo), P(PathQuery), P(PathOut)]
+        L.aos_group_create.argtypes = [P(Params), P(c_i), c_i, c_i, P(c_vp)]
+        L.aos_group_destroy.argtypes = [c_vp]
+        L.aos_group_set_polygon.argtypes = [c_vp, c_vp, c_u]
+        L.aos_group_plan.argtypes = [c_vp, c_i, P(TilePlan)]
+        L.aos_group_rank.restype = c_vp
+        L.aos_group_rank.argtypes = [c_vp, c_i]
+        L.aos_group_process.argtypes = [c_vp, P(CloudView), c_i, c_i, P(SeedGenOut)]
         L.aos_stream.restype = c_vp
         L.aos_stream.argtypes = [c_vp]
         _lib = L
@@ -282,9 +289,19 @@ class Ctx:
         _check(lib().aos_create(ctypes.byref(self.params), device, ctypes.byref(h)))
         self.h = h
 
+    @classmethod
+    def borrow(cls, handle: int, params: Params | None = None) -> "Ctx":
+        """A non-owning view of a handle owned elsewhere (aos_group_rank): close() does not destroy it."""
+        c = cls.__new__(cls)
+        c.params = params or default_params()
+        c.h = c_vp(handle)
+        c._borrowed = True
+        return c
+
     def close(self):
         if self.h:
-            lib().aos_destroy(self.h)
+            if not getattr(self, "_borrowed", False):
+                lib().aos_destroy(self.h)
             self.h = None
 
     def __del__(self):
@@ -419,3 +436,56 @@ class Ctx:
 
     def stream(self) -> int:
         return lib().aos_stream(self.h)
+
+
+class Group:
+    """One map over several GPUs from one process (aos_group_*): one handle per tile, ranks driven by
+    the library's own threads and an in-process communicator (peer copies, host max-reduction)."""
+
+    def __init__(self, params: Params, devices, tiles_x: int, tiles_y: int):
+        self.params = params
+        self.tiles_x, self.tiles_y = tiles_x, tiles_y
+        d = (c_i * len(devices))(*devices)
+        h = c_vp()
+        _check(lib().aos_group_create(ctypes.byref(params), d, tiles_x, tiles_y, ctypes.byref(h)))
+        self.h = h
+        self.world = tiles_x * tiles_y
+
+    def set_polygon(self, poly_xy: np.ndarray):
+        a = np.ascontiguousarray(poly_xy, dtype=np.float64).reshape(-1)
+        _check(lib().aos_group_set_polygon(self.h, a.ctypes.data, a.size // 2))
+
+    def plan(self, rank: int) -> dict:
+        t = TilePlan()
+        _check(lib().aos_group_plan(self.h, rank, ctypes.byref(t)))
+        return {"points_box": tuple(t.points_box), "exchange_bytes": t.exchange_bytes, "row0": t.row0, "row1": t.row1,
+                "word0": t.word0, "word1": t.word1}
+
+    def rank(self, r: int) -> Ctx:
+        return Ctx.borrow(lib().aos_group_rank(self.h, r), self.params)
+
+    def process(self, clouds, root: int = 0, want_host: bool = True, on_device: bool = False, n_points=None,
+                point_step=16, offs=(0, 4, 8), is_dense=True) -> dict:
+        """clouds[r]: rank r's points (host (n, point_step) uint8 arrays, or device pointers with
+        on_device and n_points[r]). Returns the root's frame."""
+        views, keep = [], []
+        for r in range(self.world):
+            v, k = Ctx._view(clouds[r], None if n_points is None else n_points[r], point_step, offs, is_dense,
+                             on_device)
+            views.append(v)
+            keep.append(k)
+        arr = (CloudView * self.world)(*views)
+        o = SeedGenOut()
+        _check(lib().aos_group_process(self.h, arr, root, int(want_host), ctypes.byref(o)))
+        return _seedgen_dict(o, want_host)
+
+    def close(self):
+        if self.h:
+            lib().aos_group_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

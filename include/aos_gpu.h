@@ -212,6 +212,21 @@ int aos_tile_plan_compute(const aos_params *p, const double *poly_xy, uint32_t n
 int aos_tiled_seedgen_process(aos_ctx *ctx, const aos_comm *comm, int32_t tiles_x, int32_t tiles_y, int32_t root,
                               const aos_cloud_view *cloud, int want_host, aos_seedgen_out *out);
 
+/* One map over several GPUs from one process (SURVEY §8b's multi-GPU handle). The group owns one
+ * handle per tile (devices[r] for rank r = tile (r % tiles_x, r / tiles_x); devices may repeat) and
+ * drives the ranks with its own threads and an in-process aos_comm (peer copies over xGMI, host
+ * max-reduction). clouds[r] must hold every point in rank r's points_box (aos_group_plan); the whole
+ * cloud works too. The root's outputs equal aos_seedgen_process on the whole cloud; aos_group_rank
+ * returns a rank's handle for aos_gvd_from_seedgen, markers and path planning on the root. */
+typedef struct aos_group aos_group;
+int aos_group_create(const aos_params *p, const int32_t *devices, int32_t tiles_x, int32_t tiles_y, aos_group **out);
+void aos_group_destroy(aos_group *group);
+int aos_group_set_polygon(aos_group *group, const double *xy, uint32_t n_points);
+int aos_group_plan(aos_group *group, int32_t rank, aos_tile_plan *out);
+aos_ctx *aos_group_rank(aos_group *group, int32_t rank);
+int aos_group_process(aos_group *group, const aos_cloud_view *clouds, int32_t root, int want_host,
+                      aos_seedgen_out *root_out);
+
 /* /gvd/markers content of the last GVD call (publishMarkers gvd:1012-1591) that is not already in
  * aos_gvd_out; the wrapper adds styles, ids and text. Needs aos_params.gvd_markers = 1.
  * The reference publishes the graph before the markers (gvd:310-313). Likewise a GVD call returns

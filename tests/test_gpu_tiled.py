@@ -136,3 +136,47 @@ def test_tiled_blob_refreshes_halos_mid_thinning_vs_oracle(tiles):
     assert np.array_equal(grids["inflated"], o["inflated"])
     assert g["n_clipped"] == o["n_clipped"]
     assert_gvd_parity(gg, O.gvd(o["voronoi_seeds"], o["rows_info"], o))
+
+
+def _group(cloud, poly, res, tiles_x, tiles_y, root, shard=True, on_device=False):
+    """The same frame through aos_group_* (the library's own rank threads and in-process comm)."""
+    import torch
+    world = tiles_x * tiles_y
+    grp = aos_gpu.Group(aos_gpu.default_params(grid_resolution=res), [0] * world, tiles_x, tiles_y)
+    grp.set_polygon(poly)
+    parts = [T.shard(cloud, grp.plan(r)["points_box"]) if shard else cloud for r in range(world)]
+    if on_device:
+        dev = [torch.from_numpy(np.ascontiguousarray(p)).to("cuda:0") for p in parts]
+        g = grp.process([d.data_ptr() for d in dev], root=root, on_device=True, n_points=[p.shape[0] for p in parts])
+    else:
+        g = grp.process(parts, root=root)
+    c = grp.rank(root)
+    grids = {w: c.debug_grid(w, (g["height"], g["width"])) for w in GRIDS}
+    gg = c.gvd_from_seedgen()
+    grp.close()
+    return g, [g], grids, gg
+
+
+@pytest.mark.parametrize("tiles,root,on_device", [((2, 1), 0, False), ((2, 2), 3, True), ((1, 3), 1, False)])
+def test_group_c1_equals_single_gpu(tiles, root, on_device):
+    cfg = orchard.CONFIGS["C1"]
+    cloud, poly = orchard.generate(cfg), orchard.polygon(cfg)
+    _assert_same(_single(cloud, poly, cfg.res), _group(cloud, poly, cfg.res, *tiles, root, on_device=on_device))
+
+
+def test_group_blob_vs_oracle_and_bad_cloud():
+    cfg, cloud, poly = _blob_scene()
+    g, _, grids, gg = _group(cloud, poly, cfg.res, 2, 2, 0)
+    o = O.seedgen(cloud, poly, O.default_params(grid_resolution=cfg.res))
+    assert_seedgen_parity(g, o)
+    assert np.array_equal(grids["skeleton_frameless"], o["skeleton"])
+    assert_gvd_parity(gg, O.gvd(o["voronoi_seeds"], o["rows_info"], o))
+    # an invalid PointCloud2 layout fails the frame with the rank's own error, without hanging
+    grp = aos_gpu.Group(aos_gpu.default_params(grid_resolution=cfg.res), [0, 0], 2, 1)
+    grp.set_polygon(poly)
+    with pytest.raises(RuntimeError, match=r"rank \d: .*invalid PointCloud2 layout"):
+        grp.process([cloud, cloud], point_step=16, offs=(0, 4, 13))
+    # and the group still works afterwards
+    g2 = grp.process([cloud, cloud])
+    assert g2["thin_iters"] == o["thin_iters"]
+    grp.close()
