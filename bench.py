@@ -37,6 +37,8 @@ def parse(argv=None):
     ap.add_argument("--cpu-config", default="C1")
     ap.add_argument("--stream", action="store_true",
                     help="C4 (BASELINE configs[4]): 1 M-point 20 Hz scans appended to the device-resident C2 map")
+    ap.add_argument("--host-io", action="store_true",
+                    help="PCIe-inclusive variant: host cloud in, host OccupancyGrids out (DESIGN.md; not the metric)")
     ap.add_argument("--trace", action="store_true", help="per-step timeline of the pipelined loop on stderr")
     ap.add_argument("--pipeline", action="store_true",
                     help="overlap frame k's seed-gen with frame k-1's GVD (aos_gvd_from_seedgen_async); the last "
@@ -167,6 +169,7 @@ def main():
         cloud = orchard.generate(cfg, seed=cfg.seed + rank)
     d_cloud = torch.from_numpy(cloud).to(dev)
     n = cloud.shape[0]
+    h_cloud = cloud if a.host_io else None   # --host-io: PCIe-inclusive variant (not the contract's value)
     del cloud
     if a.stream:
         # the map so far (the C2 cloud) is already device-resident; each step appends the next scan
@@ -217,7 +220,10 @@ def main():
             if not g["root"]:
                 return g, {"ms": {}, "nodes": (), "edges": ()}
         else:
-            g = ctx.seedgen(d_cloud.data_ptr(), n_points=n, on_device=True, want_host=False)
+            if a.host_io:   # PointCloud2 bytes from host memory in, both OccupancyGrids to host out
+                g = ctx.seedgen(h_cloud, want_host=True)
+            else:
+                g = ctx.seedgen(d_cloud.data_ptr(), n_points=n, on_device=True, want_host=False)
         if pipeline:
             t1 = time.perf_counter()
             gg = finish(k - 1) if k > 0 else None
@@ -312,6 +318,8 @@ def main():
             "data": "synthetic orchard (tools/orchard_gen.c, SplitMix64), device-resident PointCloud2",
             "config": {"workload": workload, "global_batch": 1 if a.tiled else world,
                        "parallelism": f"tiled{tx}x{ty}" if a.tiled else f"tiles{world}"},
+            "io": "host cloud in + host OccupancyGrids out (PCIe-inclusive)" if a.host_io else
+                  "device-resident cloud, device-resident grids",
             "pipeline": "seed-gen of frame k overlaps the GVD of frame k-1 (the reference's two nodes)"
                         if pipeline else "sequential",
             "stages_ms": {k: round(v, 3) for k, v in avg.items()},
