@@ -39,6 +39,17 @@ struct aos_ctx {
     aos::DevBuf raster_bytes, raster_bits, infl_bits, open_bits, thin_a, thin_b, occ_bytes, skel_bytes, flags;
     aos::DevBuf full_infl, full_skel;      // tiled frames: the whole map, assembled on the root rank
     aos::PinnedBuf h_small, h_stats;
+    // Host -> device upload of a large pageable buffer (a PointCloud2 message): kUpThreads host
+    // threads copy 8 MB chunks into double-buffered pinned slots, each DMA'd on the thread's stream.
+    static constexpr int kUpThreads = 4;
+    struct Uploader {
+        aos::PinnedBuf slot[kUpThreads][2];
+        hipStream_t st[kUpThreads] = {};
+        hipEvent_t ev[kUpThreads][2] = {}, done[kUpThreads] = {};
+        bool used[kUpThreads][2] = {};
+    } up;
+    void upload_h2d(void *dst, const void *src, size_t bytes);
+    void release_uploader();
     const uint64_t *skel_bits = nullptr;   // final thinning buffer (thin_a / thin_b, or full_skel)
     aos::FrameGeom geom{};                 // the whole map
     bool tiled_frame = false;
@@ -49,7 +60,7 @@ struct aos_ctx {
     aos::ClusterSeedState cs;
 
     // ---- host-side outputs of the last frame
-    std::vector<int8_t> h_occ, h_skel;
+    aos::PinnedBuf h_occ, h_skel;   // the two OccupancyGrids (pinned: the D2H runs at DMA speed)
     std::vector<double> h_row_center, h_row_start, h_row_end, h_row_length, h_voronoi, h_rows_info, h_cluster_info;
     int n_virtual = 0, n_ray = 0, n_endpoint = 0, n_clusters_all = 0, n_bfs_replayed = 0;
 

@@ -5,6 +5,8 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <exception>
+#include <thread>
 
 #include "aos_ctx.h"
 
@@ -22,6 +24,8 @@ void aos_ctx::release() {
     if (thin_graph) { (void)hipGraphExecDestroy(thin_graph); thin_graph = nullptr; }
     h_small.release();
     h_stats.release();
+    h_occ.release();
+    h_skel.release();
     for (DevBuf *b : {&cs.fg_bits, &cs.word_cnt, &cs.word_off, &cs.fg_list, &cs.parent, &cs.root_flag, &cs.root_rank,
                       &cs.cl_count, &cs.cl_off, &cs.cl_cursor, &cs.cl_cells, &cs.rec, &cs.row_idx, &cs.cur_tab,
                       &cs.poly, &cs.cand_xy, &cs.cand_ok, &cs.cand_state, &cs.hash_count,
@@ -29,6 +33,7 @@ void aos_ctx::release() {
         b->release();
     cs.h_misc.release();
     gvd_async_stop();   // joins a job in flight (it uses gs)
+    release_uploader();
     markers_wait(gs, false);
     free_path_state(path_state);
     path_state = nullptr;
@@ -42,6 +47,67 @@ void aos_ctx::release() {
     gs.h_misc.release();
 }
 
+// A pageable hipMemcpyAsync of the 160 MB C2 cloud runs at ~20 GB/s: the runtime stages it through
+// pinned memory on one thread. Here kUpThreads threads stage disjoint ranges in 8 MB chunks and DMA
+// them on their own streams; the handle's stream waits for all of them. The caller's buffer is only
+// read during the call (every memcpy has finished when this returns).
+void aos_ctx::upload_h2d(void *dst, const void *src, size_t bytes) {
+    constexpr size_t kChunk = 8u << 20;
+    if (bytes < 4 * kChunk) {
+        AOS_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream));
+        return;
+    }
+    for (int t = 0; t < kUpThreads; ++t)
+        if (!up.st[t]) {
+            AOS_HIP(hipStreamCreateWithFlags(&up.st[t], hipStreamNonBlocking));
+            for (int k = 0; k < 2; ++k) AOS_HIP(hipEventCreateWithFlags(&up.ev[t][k], hipEventDisableTiming));
+            AOS_HIP(hipEventCreateWithFlags(&up.done[t], hipEventDisableTiming));
+            for (int k = 0; k < 2; ++k) up.slot[t][k].ensure(kChunk);
+        }
+    // the handle's stream may still read dst (the previous frame): the copies start after it
+    AOS_HIP(hipEventRecord(ev[15], stream));
+    const size_t per = (bytes / kUpThreads + 4095) & ~(size_t)4095;
+    std::exception_ptr err[kUpThreads];
+    auto work = [&](int t) {
+        try {
+            AOS_HIP(hipSetDevice(device));
+            AOS_HIP(hipStreamWaitEvent(up.st[t], ev[15], 0));
+            const size_t b0 = std::min(bytes, per * t), b1 = std::min(bytes, per * (t + 1));
+            int k = 0;
+            for (size_t off = b0; off < b1; off += kChunk, k ^= 1) {
+                const size_t len = std::min(kChunk, b1 - off);
+                if (up.used[t][k]) AOS_HIP(hipEventSynchronize(up.ev[t][k]));   // its last DMA is done
+                std::memcpy(up.slot[t][k].p, static_cast<const char *>(src) + off, len);
+                AOS_HIP(hipMemcpyAsync(static_cast<char *>(dst) + off, up.slot[t][k].p, len, hipMemcpyHostToDevice,
+                                       up.st[t]));
+                AOS_HIP(hipEventRecord(up.ev[t][k], up.st[t]));
+                up.used[t][k] = true;
+            }
+            AOS_HIP(hipEventRecord(up.done[t], up.st[t]));
+        } catch (...) { err[t] = std::current_exception(); }
+    };
+    std::thread th[kUpThreads - 1];
+    for (int t = 1; t < kUpThreads; ++t) th[t - 1] = std::thread(work, t);
+    work(0);
+    for (auto &x : th) x.join();
+    for (int t = 0; t < kUpThreads; ++t)
+        if (err[t]) std::rethrow_exception(err[t]);
+    for (int t = 0; t < kUpThreads; ++t) AOS_HIP(hipStreamWaitEvent(stream, up.done[t], 0));
+}
+
+void aos_ctx::release_uploader() {
+    for (int t = 0; t < kUpThreads; ++t) {
+        if (up.st[t]) {
+            (void)hipStreamSynchronize(up.st[t]);
+            for (int k = 0; k < 2; ++k) (void)hipEventDestroy(up.ev[t][k]);
+            (void)hipEventDestroy(up.done[t]);
+            (void)hipStreamDestroy(up.st[t]);
+            up.st[t] = nullptr;
+        }
+        for (int k = 0; k < 2; ++k) { up.slot[t][k].release(); up.used[t][k] = false; }
+    }
+}
+
 void aos_ctx::set_cloud(const aos_cloud_view &v) {
     n_points = v.n_points;
     step = v.point_step; ox = v.off_x; oy = v.off_y; oz = v.off_z;
@@ -51,7 +117,7 @@ void aos_ctx::set_cloud(const aos_cloud_view &v) {
     } else {
         size_t bytes = (size_t)n_points * step;
         void *dst = cloud_copy.ensure(std::max<size_t>(bytes, 16));
-        if (bytes) AOS_HIP(hipMemcpyAsync(dst, v.data, bytes, hipMemcpyHostToDevice, stream));
+        if (bytes) upload_h2d(dst, v.data, bytes);
         d_cloud = cloud_copy.as<uint8_t>();
     }
     have_cloud = true;
@@ -338,9 +404,9 @@ void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *c
     unsigned long long *h_cnt = static_cast<unsigned long long *>(h_stats.ensure(64 + 8 * kRorCounters)) + 8;
     if (!clipped_total) AOS_HIP(hipMemcpyAsync(h_cnt, counters.p, 8 * kRorCounters, hipMemcpyDeviceToHost, s));
     if (want_host) {
-        h_occ.resize(C); h_skel.resize(C);
-        AOS_HIP(hipMemcpyAsync(h_occ.data(), d_occ, C, hipMemcpyDeviceToHost, s));
-        AOS_HIP(hipMemcpyAsync(h_skel.data(), d_skel, C, hipMemcpyDeviceToHost, s));
+        h_occ.ensure(std::max<size_t>(C, 1)); h_skel.ensure(std::max<size_t>(C, 1));
+        AOS_HIP(hipMemcpyAsync(h_occ.p, d_occ, C, hipMemcpyDeviceToHost, s));
+        AOS_HIP(hipMemcpyAsync(h_skel.p, d_skel, C, hipMemcpyDeviceToHost, s));
     }
     AOS_HIP(hipStreamSynchronize(s));
     if (clipped_total) {
@@ -368,8 +434,8 @@ void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *c
     out.n_input = n_points;
     out.n_clipped = n_clipped;
     out.n_ror_kept = 0;  // not materialised (ROR is evaluated only where it can reach the grid)
-    out.occupancy = want_host ? h_occ.data() : nullptr;
-    out.skeleton = want_host ? h_skel.data() : nullptr;
+    out.occupancy = want_host ? h_occ.as<int8_t>() : nullptr;
+    out.skeleton = want_host ? h_skel.as<int8_t>() : nullptr;
     out.d_occupancy = d_occ;
     out.d_skeleton = d_skel;
     out.n_clusters_all = n_clusters_all;
