@@ -11,7 +11,7 @@ int main(int argc, char**argv) {
     float rx = (float)(b[0] - 1.0), ry = (float)(b[2] - 1.0);
     float rw = (float)(std::abs(b[1] - b[0]) + 2.0), rh = (float)(std::abs(b[3] - b[2]) + 2.0);
     double best = 1e9; unsigned long long h = 0;
-    for (int rep = 0; rep < 7; ++rep) {
+    for (int rep = 0; rep < 15; ++rep) {
         auto t0 = std::chrono::steady_clock::now();
         aos::Subdiv2D sd; sd.reserve(n);
         sd.init_delaunay(rx, ry, rw, rh, 0);
