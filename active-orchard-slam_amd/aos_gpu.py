@@ -445,6 +445,9 @@ class Group:
     def __init__(self, params: Params, devices, tiles_x: int, tiles_y: int):
         self.params = params
         self.tiles_x, self.tiles_y = tiles_x, tiles_y
+        devices = list(devices)
+        if len(devices) != tiles_x * tiles_y:   # aos_group_create reads devices[r] for every rank
+            raise ValueError(f"Group: {len(devices)} devices for {tiles_x}x{tiles_y} tiles")
         d = (c_i * len(devices))(*devices)
         h = c_vp()
         _check(lib().aos_group_create(ctypes.byref(params), d, tiles_x, tiles_y, ctypes.byref(h)))

@@ -35,8 +35,8 @@ struct aos_ctx {
     int thin_graph_dims[3] = {-1, -1, -1};
 
     // ---- device buffers
-    aos::DevBuf cloud_copy, bin_count, bin_start, pt_binslot, sorted, scan_tmp, counters;
-    aos::DevBuf raster_bytes, raster_bits, infl_bits, open_bits, thin_a, thin_b, occ_bytes, skel_bytes, flags;
+    aos::DevBuf cloud_copy, bin_count, bin_start, pt_binslot, sorted, ror_scratch, scan_tmp, counters;
+    aos::DevBuf raster_bits, infl_bits, open_bits, thin_a, thin_b, occ_bytes, skel_bytes, flags;
     aos::DevBuf full_infl, full_skel;      // tiled frames: the whole map, assembled on the root rank
     aos::PinnedBuf h_small, h_stats;
     // Host -> device upload of a large pageable buffer (a PointCloud2 message): kUpThreads host
@@ -95,12 +95,13 @@ struct aos_ctx {
     void *path_state = nullptr;   // aos::PathState
 
     // Cells a frame rasterises / counts: [rx0, rx1) x [ry0, ry1) (clamped cell), stored into the
-    // Wr x Hr byte window at cell (wx0, wy0); limit_box: bin only points in box (a tile's shard).
+    // Wr x Hr bit window at cell (wx0, wy0), wx0 a multiple of 64; limit_box: bin only points in box
+    // (a tile's shard).
     struct RorOwn { int rx0, ry0, rx1, ry1, wx0, wy0, Wr, Hr; bool limit_box; float box[4]; };
 
     void set_cloud(const aos_cloud_view &v);
     void map_append(const aos_cloud_view &scan);
-    void ror_stage(const aos::FrameGeom &g, const RorOwn &o);
+    void ror_stage(const aos::FrameGeom &g, const RorOwn &o, uint64_t *rbits);
     void finish_frame(const aos::FrameGeom &g, bool want_host, const uint64_t *clipped_total, aos_seedgen_out &out);
     void run_seedgen(bool want_host, aos_seedgen_out &out);
     void run_tiled(const aos_comm &cm, int tiles_x, int tiles_y, int root, bool want_host, aos_seedgen_out &out);

@@ -20,6 +20,22 @@ struct HipError { hipError_t e; const char *what; int line; };
         if (_e != hipSuccess) throw ::aos::HipError{_e, #x, __LINE__};    \
     } while (0)
 
+// Makes a device current for one scope and restores the caller's device afterwards (also on an
+// exception), so a multi-GPU caller (e.g. torch with one device per thread) keeps its own device.
+struct DeviceScope {
+    int prev = -1;
+    explicit DeviceScope(int d) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != d) (void)hipSetDevice(d);   // a failure surfaces in the next HIP call
+    }
+    ~DeviceScope() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+    DeviceScope(const DeviceScope &) = delete;
+    DeviceScope &operator=(const DeviceScope &) = delete;
+};
+
 // ------------------------------------------------------------------ device buffers
 // Owning, growable device allocation (freed on destruction; not copyable).
 struct DevBuf {
@@ -74,7 +90,7 @@ struct FrameGeom {
 };
 
 // ------------------------------------------------------------------ kernels (launchers)
-constexpr int kRorCounters = 256;   // spread n_clipped counter slots (k_ror_sweep)
+constexpr int kRorCounters = 256;   // spread n_clipped counter slots (k_rt_ror)
 struct RorLaunch {
     const uint8_t *cloud; uint64_t n; uint32_t step, ox, oy, oz; int is_dense;
     float bminx, bminy, bminz, bmaxx, bmaxy, bmaxz, inv_cs; int nbx, nby;
@@ -85,14 +101,16 @@ struct RorLaunch {
     // grid, lies in [rx0, rx1) x [ry0, ry1); it is rastered (if inside the grid) into the byte window
     // whose cell (wx0, wy0) is element 0, row pitch Wr. Single-GPU frames own the whole grid.
     int rx0, ry0, rx1, ry1, wx0, wy0, Wr;
+    // tile walk (ror.hip): TB x TB bins per tile, ntx x nty tiles; the raster window as bits (Hr rows
+    // of WWr words, wx0 a multiple of 64); a tile's LDS raster window (win_rows x win_w words, 0: none)
+    int TB, ntx, nty, ntiles, max_touch, Hr, WWr, win_rows, win_w;
 };
-void launch_ror_bin(const RorLaunch &L, int *bin_count, int2 *pt_binslot, hipStream_t s);
-void launch_ror_scatter(const RorLaunch &L, const int *bin_start, const int2 *pt_binslot, float4 *sorted, hipStream_t s);
-void launch_ror_count(const RorLaunch &L, int *bin_count, hipStream_t s);
-void launch_ror_place(const RorLaunch &L, int *cursor, float4 *sorted, hipStream_t s);
-void launch_ror_raster(const RorLaunch &L, const int *bin_start, const float4 *sorted, uint8_t *raster,
-                       unsigned long long *counters, hipStream_t s);
-void launch_pack_bits(const uint8_t *bytes, uint64_t *bits, int W, int H, int WW, hipStream_t s);
+constexpr int kRtMaxTiles = 20000;   // tiles per frame (LDS histogram of the partition passes)
+void rt_configure(RorLaunch &L, int Hr, int WWr);
+void launch_rt_count(const RorLaunch &L, int *tile_count, unsigned long long *n_own, int n_blocks, hipStream_t s);
+void launch_rt_scatter(const RorLaunch &L, int *tile_cursor, float4 *staged, int n_blocks, hipStream_t s);
+void launch_rt_ror(const RorLaunch &L, const int *tile_start, const float4 *staged, float4 *scratch, uint64_t *rbits,
+                   unsigned long long *counters, hipStream_t s);
 // PointCloud2 records (any float32 x/y/z offsets) -> float4 (x, y, z, 0)
 void launch_pack_xyz(const uint8_t *cloud, uint64_t n, uint32_t step, uint32_t ox, uint32_t oy, uint32_t oz, float4 *out,
                      hipStream_t s);

@@ -41,20 +41,6 @@ using namespace aos;
         return AOS_E_STATE;                                                                                   \
     }
 
-// Makes the handle's device current for one ABI call and restores the caller's device afterwards
-// (a multi-GPU caller, e.g. torch with one device per thread, keeps its own current device).
-struct DeviceScope {
-    int prev = -1;
-    explicit DeviceScope(int d) {
-        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-        if (prev != d) (void)hipSetDevice(d);   // a failure surfaces in the next HIP call
-    }
-    ~DeviceScope() {
-        int cur = -1;
-        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
-    }
-};
-
 extern "C" {
 
 const char *aos_last_error(void) { return g_err.c_str(); }

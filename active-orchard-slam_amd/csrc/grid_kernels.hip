@@ -16,376 +16,9 @@
 
 namespace aos {
 
-// Exclusion discs of processPointCloud (seed_gen:487-499): x, y, radius.
-__constant__ float c_excl[11 * 3] = {0.646417f, 3.83918f, 1.0f,  2.0405f, 3.62485f, 1.0f,  65.3711f, 2.09755f, 1.0f,
-                                     66.9094f, 2.07515f, 1.0f,  -1.61309f, 5.69933f, 1.0f, -1.97349f, 4.77329f, 1.0f,
-                                     -2.11365f, 3.74464f, 1.0f, -2.26381f, 2.70848f, 1.0f, -2.66426f, 1.72738f, 1.0f,
-                                     68.0229f, 2.31687f, 1.0f,  65.4647f, 2.18653f, 1.0f};
-
 static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
-__device__ __forceinline__ void load_xyz(const RorLaunch &L, uint64_t i, float &x, float &y, float &z) {
-    const uint8_t *rec = L.cloud + i * (uint64_t)L.step;
-    if (L.step == 16 && L.ox == 0 && L.oy == 4 && L.oz == 8) {
-        float4 v = *reinterpret_cast<const float4 *>(rec);
-        x = v.x; y = v.y; z = v.z;
-    } else {
-        x = *reinterpret_cast<const float *>(rec + L.ox);
-        y = *reinterpret_cast<const float *>(rec + L.oy);
-        z = *reinterpret_cast<const float *>(rec + L.oz);
-    }
-}
-
-__device__ __forceinline__ bool binned(const RorLaunch &L, float x, float y, float z) {
-    return isfinite(x) && isfinite(y) && isfinite(z) && x >= L.bminx && x <= L.bmaxx && y >= L.bminy &&
-           y <= L.bmaxy && z >= L.bminz && z <= L.bmaxz;
-}
-
-__device__ __forceinline__ int bin_of(const RorLaunch &L, float x, float y, int &bx, int &by) {
-    bx = min(max((int)((x - L.bminx) * L.inv_cs), 0), L.nbx - 1);
-    by = min(max((int)((y - L.bminy) * L.inv_cs), 0), L.nby - 1);
-    return by * L.nbx + bx;
-}
-
-// PassThrough z, x, y (inclusive; PCL 1.12 drops non-finite) + exclusion discs, seed_gen:459-525.
-__device__ __forceinline__ bool candidate(const RorLaunch &L, float x, float y, float z) {
-    if (z < L.cminz || z > L.cmaxz) return false;
-    if (x < L.cminx || x > L.cmaxx) return false;
-    if (y < L.cminy || y > L.cmaxy) return false;
-#pragma unroll
-    for (int e = 0; e < 11; ++e) {
-        float dx = x - c_excl[3 * e], dy = y - c_excl[3 * e + 1];
-        float dist_sq = dx * dx + dy * dy;
-        float rr = c_excl[3 * e + 2] * c_excl[3 * e + 2];
-        if (dist_sq <= rr) return false;
-    }
-    return true;
-}
-
-// ------------------------------------------------------------------------------------------
-// a1 RadiusOutlierRemoval (seed_gen:236-242) restricted to the points that can reach the grid.
-// Only points inside the clip box can be rasterised; their neighbours lie within r of that box,
-// so only that expanded box is binned (2-D columns of >= r, z checked exactly).
-__global__ void k_ror_bin(RorLaunch L, int *bin_count, int2 *pt_binslot) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= L.n) return;
-    float x, y, z;
-    load_xyz(L, i, x, y, z);
-    int2 bs = make_int2(-1, 0);
-    if (binned(L, x, y, z)) {
-        int bx, by;
-        int b = bin_of(L, x, y, bx, by);
-        bs = make_int2(b, atomicAdd(&bin_count[b], 1));
-    }
-    pt_binslot[i] = bs;
-}
-
-__global__ void k_ror_scatter(RorLaunch L, const int *bin_start, const int2 *pt_binslot, float4 *sorted) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= L.n) return;
-    int2 bs = pt_binslot[i];
-    if (bs.x < 0) return;
-    float x, y, z;
-    load_xyz(L, i, x, y, z);
-    int cand = candidate(L, x, y, z) ? 1 : 0;
-    sorted[bin_start[bs.x] + bs.y] = make_float4(x, y, z, __int_as_float(cand));
-}
-
-// Neighbour count with PCL semantics (FLANN L2_Simple: ((dx*dx)+dy*dy)+dz*dz in float):
-//   dense: kNN k = need, keep iff need points have (double)d2 <= r^2;
-//   !dense: radius search d2 < float(r^2), keep iff count >= need.
-// Kept candidates mark their cell (generateOccupancyGrid seed_gen:606-619: double divide, trunc).
-//
-// The keep decision only needs "at least need points within r", so the scan order is free (own
-// bin row first) and stops early.
-#ifndef AOS_ROR_NOSCAN   // timing experiments only (tools/ab_variants.sh): wrong results
-#define AOS_ROR_NOSCAN 0
-#endif
-#ifndef AOS_ROR_NOSTORE
-#define AOS_ROR_NOSTORE 0
-#endif
-// k_ror_direct scan order: 1 row order, 2 own bin first, 3 own bin first for dense bins only
-// (0 selects the LDS row sweep k_ror_sweep instead of k_ror_direct)
-#ifndef AOS_ROR_DIRECT
-#define AOS_ROR_DIRECT 3
-#endif
-constexpr int kRorDenseBin = 32;
-
-// XCD-aware block order (cdna_hip_programming.md §5.5 T1): blocks b = j (mod 8) share an XCD's L2,
-// so group j gets one contiguous range of logical blocks (neighbouring bin rows stay on one L2).
-__device__ __forceinline__ int xcd_block(int b, int n) {
-    const int q = n >> 3, r = n & 7, j = b & 7, k = b >> 3;
-    return j * q + min(j, r) + k;
-}
-
-__device__ __forceinline__ bool ror_in(const RorLaunch &L, float4 p, float4 q) {
-    float dx = p.x - q.x, dy = p.y - q.y, dz = p.z - q.z;
-    float d2 = dx * dx;
-    d2 = d2 + dy * dy;
-    d2 = d2 + dz * dz;
-    // dense: (double)d2 <= r2 is the same test as d2 <= r2df for every float d2 (incl. inf / NaN)
-    return L.is_dense ? (d2 <= L.r2df) : (d2 < L.r2f);
-}
-template <class Ptr>
-__device__ __forceinline__ int ror_scan(const RorLaunch &L, float4 p, Ptr pts, int k0, int k1, int cnt) {
-    for (int k = k0; k < k1 && cnt < L.need; k += 4) {
-        float4 q[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) q[j] = pts[min(k + j, k1 - 1)];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) cnt += (k + j < k1 && ror_in(L, p, q[j])) ? 1 : 0;
-    }
-    return cnt;
-}
-
-// same as ror_scan on one staged LDS row (indexing the __shared__ row keeps ds_read instructions)
-__device__ __forceinline__ int ror_scan_lds(const RorLaunch &L, float4 p, const float4 (&row)[512], int k0, int k1, int cnt) {
-    for (int k = k0; k < k1 && cnt < L.need; k += 4) {
-        float4 q[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) q[j] = row[min(k + j, k1 - 1)];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) cnt += (k + j < k1 && ror_in(L, p, q[j])) ? 1 : 0;
-    }
-    return cnt;
-}
-
-// LDS-staged bins, row sweep: one workgroup per (strip of kSwSW bins) x (segment of kSwSeg bin rows).
-// A candidate's neighbours lie in 3 x 3 bins; the bins of one row of a strip (plus one bin on each
-// side) are one contiguous range of the bin-sorted point array, copied into LDS coalesced. It keeps
-// a ring of 4 staged point rows (y-1, y, y+1 and y+2 in flight) and 5 rows of bin offsets in LDS.
-// While it scans row y it has already issued the loads of row y+2's points and row y+3's offsets
-// into registers, so each step costs ~max(scan, one load latency) instead of a 3-trip chain per
-// workgroup. Rows with more than kSwCap points stay in global memory (scanned there).
-#ifndef AOS_SW_SEG
-#define AOS_SW_SEG 32
-#endif
-constexpr int kSwSW = 64, kSwTB = 256, kSwCap = 512, kSwSeg = AOS_SW_SEG, kSwPer = kSwCap / kSwTB;
-
-__global__ __launch_bounds__(kSwTB) void k_ror_sweep(RorLaunch L, const int *bin_start, const float4 *sorted,
-                                                     uint8_t *raster, unsigned long long *counters) {
-    __shared__ float4 pts[4][kSwCap];
-    __shared__ int offs[5][kSwSW + 3];
-    __shared__ int staged[4];            // 1: row's points are in pts[slot]; 0: read them from global
-    const int tid = threadIdx.x;
-    const int nstrip = (L.nbx + kSwSW - 1) / kSwSW;
-    const int blk = xcd_block(blockIdx.x, gridDim.x);
-    const int strip = blk % nstrip, seg = blk / nstrip;
-    const int bx0 = strip * kSwSW, bx1 = min(bx0 + kSwSW, L.nbx);
-    const int xlo = max(bx0 - 1, 0), xhi = min(bx1, L.nbx - 1), nbins = xhi - xlo + 1;
-    const int y0 = seg * kSwSeg, y1 = min(y0 + kSwSeg, L.nby);
-    auto row_ok = [&](int yy) { return yy >= 0 && yy < L.nby; };
-    auto offs_of = [&](int yy, int c) { return row_ok(yy) ? bin_start[yy * L.nbx + xlo + c] : 0; };
-    // prologue: offsets of rows y0-1 .. y0+2, points of rows y0-1 .. y0+1
-    for (int t = tid; t < 4 * (nbins + 1); t += kSwTB) {
-        const int r = t / (nbins + 1), c = t - r * (nbins + 1), yy = y0 - 1 + r;
-        offs[(yy + 5) % 5][c] = offs_of(yy, c);
-    }
-    __syncthreads();
-    for (int r = 0; r < 3; ++r) {
-        const int yy = y0 - 1 + r, o = (yy + 5) % 5, sl = (yy + 4) & 3;
-        const int a = offs[o][0], n = offs[o][nbins] - a;
-        if (n <= kSwCap)
-            for (int t = tid; t < n; t += kSwTB) pts[sl][t] = sorted[a + t];
-        if (tid == 0) staged[sl] = n <= kSwCap;
-    }
-    __syncthreads();
-    unsigned kept_n = 0;
-    for (int y = y0; y < y1; ++y) {
-        // (1) issue the loads for row y+2's points and row y+3's offsets
-        const int opf = (y + 2 + 5) % 5, spf = (y + 2) & 3;
-        const int apf = offs[opf][0], npf = offs[opf][nbins] - apf;
-        float4 q[kSwPer];
-#pragma unroll
-        for (int j = 0; j < kSwPer; ++j) {
-            const int t = tid + j * kSwTB;
-            q[j] = sorted[(t < npf && npf <= kSwCap) ? apf + t : 0];
-        }
-        const int onew = tid <= nbins ? offs_of(y + 3, tid) : 0;
-        // (2) count neighbours of row y's candidates from the staged rows y-1, y, y+1. The own point is
-        // read in a branch on the (workgroup-uniform) staged flag: a select of an LDS and a global
-        // pointer would become a flat load, whose vmcnt wait would also wait for the prefetch above.
-        const int ocur = (y + 5) % 5, scur = y & 3;
-        const int own0 = offs[ocur][bx0 - xlo], own1 = offs[ocur][bx1 - xlo], base0 = offs[ocur][0];
-        auto count_one = [&](const float4 p) {
-            if (__float_as_int(p.w) == 0) return;   // not a clip candidate
-            int bx, byy;
-            bin_of(L, p.x, p.y, bx, byy);
-            const int c0 = max(bx - 1, xlo) - xlo, c1 = min(bx + 1, xhi) - xlo + 1;
-            int cnt = AOS_ROR_NOSCAN ? L.need : 0;
-#pragma unroll
-            for (int rr = 0; rr < 3; ++rr) {
-                const int yy = rr == 0 ? y : (rr == 1 ? y - 1 : y + 1);   // own bin row first
-                if (!row_ok(yy) || cnt >= L.need) continue;
-                const int o = (yy + 5) % 5, sl = (yy + 4) & 3;
-                const int g0 = offs[o][c0], g1 = offs[o][c1];
-                if (staged[sl]) cnt = ror_scan_lds(L, p, pts[sl], g0 - offs[o][0], g1 - offs[o][0], cnt);
-                else cnt = ror_scan(L, p, sorted, g0, g1, cnt);
-            }
-            if (cnt >= L.need) {
-                int gx = (int)(((double)p.x - L.origin_x) / (double)L.res);
-                int gy = (int)(((double)p.y - L.origin_y) / (double)L.res);
-                const int cx = min(max(gx, 0), L.W - 1), cy = min(max(gy, 0), L.H - 1);
-                if (cx >= L.rx0 && cx < L.rx1 && cy >= L.ry0 && cy < L.ry1) {   // this tile's candidate
-                    ++kept_n;
-                    if (!AOS_ROR_NOSTORE && gx >= 0 && gx < L.W && gy >= 0 && gy < L.H)
-                        raster[(size_t)(gy - L.wy0) * L.Wr + (gx - L.wx0)] = 1;
-                }
-            }
-        };
-        if (staged[scur]) {
-            for (int k = own0 + tid; k < own1; k += kSwTB) count_one(pts[scur][k - base0]);
-        } else {
-            for (int k = own0 + tid; k < own1; k += kSwTB) count_one(sorted[k]);
-        }
-        // (3) commit the prefetched row y+2 and offsets of row y+3. Their slots held row y-2, which
-        // step y no longer reads, so no barrier is needed before the writes.
-        if (npf <= kSwCap) {
-#pragma unroll
-            for (int j = 0; j < kSwPer; ++j) {
-                const int t = tid + j * kSwTB;
-                if (t < npf) pts[spf][t] = q[j];
-            }
-        }
-        if (tid <= nbins) offs[(y + 3 + 5) % 5][tid] = onew;
-        if (tid == 0) staged[spf] = npf <= kSwCap;
-        __syncthreads();
-    }
-    for (int o = 32; o > 0; o >>= 1) kept_n += __shfl_xor(kept_n, o);
-    if ((tid & 63) == 0 && kept_n)
-        atomicAdd(&counters[(blk * (kSwTB / 64) + (tid >> 6)) & (kRorCounters - 1)], (unsigned long long)kept_n);   // spread: one
-    // hot address would serialise ~10^5 same-address atomics in one L2 channel
-}
-
-// Kept candidate: count it if its (clamped) cell is owned, raster it if inside the grid.
-__device__ __forceinline__ void ror_keep(const RorLaunch &L, float4 p, uint8_t *raster, unsigned &kept_n) {
-    int gx = (int)(((double)p.x - L.origin_x) / (double)L.res);
-    int gy = (int)(((double)p.y - L.origin_y) / (double)L.res);
-    const int cx = min(max(gx, 0), L.W - 1), cy = min(max(gy, 0), L.H - 1);
-    if (cx >= L.rx0 && cx < L.rx1 && cy >= L.ry0 && cy < L.ry1) {
-        ++kept_n;
-        if (!AOS_ROR_NOSTORE && gx >= 0 && gx < L.W && gy >= 0 && gy < L.H)
-            raster[(size_t)(gy - L.wy0) * L.Wr + (gx - L.wx0)] = 1;
-    }
-}
-
-// Direct variant: one thread per staged point, in bin order, reading the 3 x 3 neighbour bins
-// straight from global memory (consecutive lanes scan nearly the same ranges, so the loads hit
-// the same cache lines). No LDS, no barriers: occupancy is bounded by registers only.
-__global__ __launch_bounds__(256) void k_ror_direct(RorLaunch L, const int *bin_start, const float4 *sorted,
-                                                    const int *n_binned, uint8_t *raster,
-                                                    unsigned long long *counters) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    unsigned kept_n = 0;
-    if (i < *n_binned) {
-        const float4 p = sorted[i];
-        if (__float_as_int(p.w)) {
-            int bx, by;
-            bin_of(L, p.x, p.y, bx, by);
-            const int c0 = max(bx - 1, 0), c1 = min(bx + 1, L.nbx - 1);
-            int cnt = AOS_ROR_NOSCAN ? L.need : 0;
-            // Scan order. Row order: the own bin row, then the rows above and below (3 bins each).
-            // Own-first: the point itself (d2 = 0 passes both tests), its own bin around it, then the
-            // other 8 bins; the own bin holds the likeliest neighbours, so most scans stop early.
-            // Variant 3 (default) goes own-first only for a dense own bin (>= kRorDenseBin points):
-            // there a row scan starts in the left bin and wades through its points, most of them > r
-            // away in x (a streaming map stacks ~300 points in a canopy bin: 0.85 -> 0.34 ms). Sparse
-            // bins keep the row order, which needs fewer, longer loops (C2: 0.154 ms against 0.196
-            // with own-first everywhere). The keep decision does not depend on the order.
-            bool own_first = AOS_ROR_DIRECT == 2;
-            int b0 = 0, b1 = 0;
-            if (AOS_ROR_DIRECT >= 2) {
-                const int ob = by * L.nbx + bx;
-                b0 = bin_start[ob];
-                b1 = bin_start[ob + 1];
-                own_first = own_first || b1 - b0 >= kRorDenseBin;
-            }
-            if (own_first) {
-                cnt = 1;
-                cnt = ror_scan(L, p, sorted, i + 1, b1, cnt);
-                cnt = ror_scan(L, p, sorted, b0, i, cnt);
-                if (cnt < L.need) cnt = ror_scan(L, p, sorted, bin_start[by * L.nbx + c0], b0, cnt);
-                if (cnt < L.need) cnt = ror_scan(L, p, sorted, b1, bin_start[by * L.nbx + c1 + 1], cnt);
-                for (int rr = 1; rr < 3; ++rr) {
-                    const int yy = rr == 1 ? by - 1 : by + 1;
-                    if (yy < 0 || yy >= L.nby || cnt >= L.need) continue;
-                    cnt = ror_scan(L, p, sorted, bin_start[yy * L.nbx + c0], bin_start[yy * L.nbx + c1 + 1], cnt);
-                }
-            } else {
-#pragma unroll
-                for (int rr = 0; rr < 3; ++rr) {
-                    const int yy = rr == 0 ? by : (rr == 1 ? by - 1 : by + 1);   // own bin row first
-                    if (yy < 0 || yy >= L.nby || cnt >= L.need) continue;
-                    cnt = ror_scan(L, p, sorted, bin_start[yy * L.nbx + c0], bin_start[yy * L.nbx + c1 + 1], cnt);
-                }
-            }
-            if (cnt >= L.need) ror_keep(L, p, raster, kept_n);
-        }
-    }
-    for (int o = 32; o > 0; o >>= 1) kept_n += __shfl_xor(kept_n, o);
-    if ((threadIdx.x & 63) == 0 && kept_n)
-        atomicAdd(&counters[(blockIdx.x * 4 + (threadIdx.x >> 6)) & (kRorCounters - 1)], (unsigned long long)kept_n);
-}
-
-// Counting sort without a per-point slot array: k_ror_count counts points per bin with
-// non-returning atomics (fire and forget), the exclusive scan is written one element to the right
-// (cursor[1 + b] = start of bin b), and k_ror_place claims each point's position with a returning
-// atomic on that cursor. After the placement cursor[b] = start of bin b for every b <= nb, i.e.
-// the cursor array IS bin_start. Order inside a bin is arbitrary, as before (the ROR decision is
-// order-free).
-__global__ void k_ror_count(RorLaunch L, int *bin_count) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= L.n) return;
-    float x, y, z;
-    load_xyz(L, i, x, y, z);
-    if (binned(L, x, y, z)) {
-        int bx, by;
-        atomicAdd(&bin_count[bin_of(L, x, y, bx, by)], 1);
-    }
-}
-
-__global__ void k_ror_place(RorLaunch L, int *cursor, float4 *sorted) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= L.n) return;
-    float x, y, z;
-    load_xyz(L, i, x, y, z);
-    if (!binned(L, x, y, z)) return;
-    int bx, by;
-    const int pos = atomicAdd(&cursor[1 + bin_of(L, x, y, bx, by)], 1);
-    sorted[pos] = make_float4(x, y, z, __int_as_float(candidate(L, x, y, z) ? 1 : 0));
-}
-
-void launch_ror_count(const RorLaunch &L, int *bin_count, hipStream_t s) {
-    if (!L.n) return;
-    k_ror_count<<<cdiv(L.n, 256), 256, 0, s>>>(L, bin_count);
-}
-void launch_ror_place(const RorLaunch &L, int *cursor, float4 *sorted, hipStream_t s) {
-    if (!L.n) return;
-    k_ror_place<<<cdiv(L.n, 256), 256, 0, s>>>(L, cursor, sorted);
-}
-
-void launch_ror_bin(const RorLaunch &L, int *bin_count, int2 *pt_binslot, hipStream_t s) {
-    if (!L.n) return;
-    k_ror_bin<<<cdiv(L.n, 256), 256, 0, s>>>(L, bin_count, pt_binslot);
-}
-void launch_ror_scatter(const RorLaunch &L, const int *bin_start, const int2 *pt_binslot, float4 *sorted, hipStream_t s) {
-    if (!L.n) return;
-    k_ror_scatter<<<cdiv(L.n, 256), 256, 0, s>>>(L, bin_start, pt_binslot, sorted);
-}
-
-void launch_ror_raster(const RorLaunch &L, const int *bin_start, const float4 *sorted, uint8_t *raster,
-                       unsigned long long *counters, hipStream_t s) {
-    if (AOS_ROR_DIRECT) {
-        if (!L.n) return;
-        k_ror_direct<<<cdiv(L.n, 256), 256, 0, s>>>(L, bin_start, sorted, bin_start + L.nbx * L.nby, raster, counters);
-        return;
-    }
-    const long long nblk = (long long)((L.nby + kSwSeg - 1) / kSwSeg) * ((L.nbx + kSwSW - 1) / kSwSW);
-    if (nblk <= 0) return;
-    if (nblk > INT_MAX) throw std::runtime_error("ROR bin grid too large");
-    k_ror_sweep<<<(int)nblk, kSwTB, 0, s>>>(L, bin_start, sorted, raster, counters);
-
-}
+// (a1-a4, ROR + clip + raster: ror.hip)
 
 size_t scan_temp_bytes(int n) {
     size_t t = 0;
@@ -410,37 +43,6 @@ void launch_pack_xyz(const uint8_t *cloud, uint64_t n, uint32_t step, uint32_t o
                      hipStream_t s) {
     if (!n) return;
     k_pack_xyz<<<cdiv(n, 256), 256, 0, s>>>(cloud, n, step, ox, oy, oz, out);
-}
-
-// ------------------------------------------------------------------------------------------
-// bytes (0 / non-zero) -> bits
-__global__ void k_pack_bits(const uint8_t *bytes, uint64_t *bits, int W, int H, int WW) {
-    int c = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
-    if (c >= WW || y >= H) return;
-    const uint8_t *row = bytes + (size_t)y * W;
-    uint64_t w = 0;
-    int x0 = c * 64;
-    if ((W & 15) == 0 && x0 + 64 <= W) {
-        const uint4 *v = reinterpret_cast<const uint4 *>(row + x0);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            uint4 u = v[q];
-            uint32_t wd[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-#pragma unroll
-                for (int b = 0; b < 4; ++b)
-                    if ((wd[k] >> (8 * b)) & 0xFF) w |= 1ull << (q * 16 + k * 4 + b);
-        }
-    } else {
-        for (int i = 0; i < 64 && x0 + i < W; ++i)
-            if (row[x0 + i]) w |= 1ull << i;
-    }
-    bits[(size_t)y * WW + c] = w;
-}
-void launch_pack_bits(const uint8_t *bytes, uint64_t *bits, int W, int H, int WW, hipStream_t s) {
-    dim3 g(cdiv(WW, 64), H);
-    k_pack_bits<<<g, 64, 0, s>>>(bytes, bits, W, H, WW);
 }
 
 __device__ __forceinline__ uint64_t pad_mask(int c, int WW, int W) {

@@ -137,11 +137,9 @@ int aos_group_create(const aos_params *p, const int32_t *devices, int32_t tiles_
         m.device = devices[r];
     }
     try {
-        int prev = 0;
-        AOS_HIP(hipGetDevice(&prev));
         for (int r = 0; r < world; ++r) {
             Member &m = *G->g.m[r];
-            AOS_HIP(hipSetDevice(m.device));
+            DeviceScope dev(m.device);
             AOS_HIP(hipStreamCreateWithFlags(&m.stream, hipStreamNonBlocking));
             for (int q = 0; q < world; ++q) {   // peer access for the all-gather pulls (xGMI)
                 const int d = devices[q];
@@ -153,7 +151,6 @@ int aos_group_create(const aos_params *p, const int32_t *devices, int32_t tiles_
                 }
             }
         }
-        AOS_HIP(hipSetDevice(prev));
     } catch (const HipError &e) {
         set_error(std::string("aos_group_create: HIP error ") + hipGetErrorString(e.e) + ": " + e.what);
         aos_group_destroy(G);
@@ -212,12 +209,9 @@ int aos_group_process(aos_group *G, const aos_cloud_view *clouds, int32_t root, 
         if (rc != AOS_OK) return rc;
         Member &m = *G->g.m[r];
         try {
-            int prev = 0;
-            AOS_HIP(hipGetDevice(&prev));
-            AOS_HIP(hipSetDevice(m.device));
+            DeviceScope dev(m.device);
             m.send.ensure(std::max<uint64_t>(plan.exchange_bytes, 1));
             m.recv.ensure((size_t)world * std::max<uint64_t>(plan.exchange_bytes, 1));
-            AOS_HIP(hipSetDevice(prev));
         } catch (const HipError &e) {
             set_error(std::string("aos_group_process: HIP error ") + hipGetErrorString(e.e));
             return AOS_E_HIP;

@@ -1,0 +1,385 @@
+// a1-a4 RadiusOutlierRemoval + PassThrough + exclusion discs + raster (seed_gen:230-248, 452-622) as
+// a two-level spatial partition for gfx950.
+//
+// The reference runs PCL's RadiusOutlierRemoval (kd-tree, k = minN + 1 nearest neighbours in 3-D)
+// over the whole cloud, then clips and rasterises. Only points inside the clip box can reach the
+// grid, and their neighbours lie within r of that box, so only that expanded ("binned") box matters.
+// Here the binned box is cut into square bins of side >= r (a neighbour of p lies in p's 3 x 3 bins)
+// and the bins into tiles of TB x TB bins:
+//   k_rt_part<false>  count: per tile, the points whose 3 x 3 bins reach it (own tile + up to 3
+//                     halo tiles). Per-workgroup LDS histograms, one global atomic per touched tile.
+//   scan              tile_start = exclusive sum of the counts.
+//   k_rt_part<true>   scatter: the same walk, each workgroup claims one run per touched tile with a
+//                     returning atomic and writes its points there (w = 1: an own clip candidate,
+//                     else 0: a neighbour only — non-candidates and halo copies).
+//   k_rt_ror          one workgroup per tile: the tile's points (own + halo) are counting-sorted by
+//                     bin into LDS, every own candidate counts neighbours in its 3 x 3 bins from
+//                     LDS with early exit, and kept candidates set their cell in an LDS bitmap of
+//                     the tile's cells that is OR-ed into the bit-packed raster at the end.
+// The cloud is read twice (count, scatter) and every staged point written and read once; no
+// per-point global atomic, no random gather. Results are order-free: the keep decision needs only
+// "at least need points within r", and the raster is an OR.
+//
+// Numerics: FLANN's squared distance ((dx*dx)+dy*dy)+dz*dz in float, no FMA (-ffp-contract=off);
+// dense clouds: kNN keeps iff the need-th nearest has (double)d2 <= r^2, i.e. d2 <= r2df (the
+// largest float whose double is <= r^2); non-dense: radius search d2 < float(r^2). The point itself
+// has d2 = 0 and is counted by the same test (not counted when r = 0 on a non-dense cloud, as FLANN's
+// strict test does). Cells: generateOccupancyGrid's (int)(((double)x - origin) / (double)res).
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <stdexcept>
+
+#include "aos_internal.h"
+
+namespace aos {
+
+// Exclusion discs of processPointCloud (seed_gen:487-499): x, y, radius.
+__constant__ float c_excl_rt[11 * 3] = {0.646417f, 3.83918f, 1.0f,  2.0405f, 3.62485f, 1.0f,  65.3711f, 2.09755f, 1.0f,
+                                        66.9094f, 2.07515f, 1.0f,  -1.61309f, 5.69933f, 1.0f, -1.97349f, 4.77329f, 1.0f,
+                                        -2.11365f, 3.74464f, 1.0f, -2.26381f, 2.70848f, 1.0f, -2.66426f, 1.72738f, 1.0f,
+                                        68.0229f, 2.31687f, 1.0f,  65.4647f, 2.18653f, 1.0f};
+
+static inline int cdiv_i(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+__device__ __forceinline__ void rt_load(const RorLaunch &L, uint64_t i, float &x, float &y, float &z) {
+    const uint8_t *rec = L.cloud + i * (uint64_t)L.step;
+    if (L.step == 16 && L.ox == 0 && L.oy == 4 && L.oz == 8) {
+        const float4 v = *reinterpret_cast<const float4 *>(rec);
+        x = v.x; y = v.y; z = v.z;
+    } else {
+        x = *reinterpret_cast<const float *>(rec + L.ox);
+        y = *reinterpret_cast<const float *>(rec + L.oy);
+        z = *reinterpret_cast<const float *>(rec + L.oz);
+    }
+}
+
+__device__ __forceinline__ bool rt_binned(const RorLaunch &L, float x, float y, float z) {
+    return isfinite(x) && isfinite(y) && isfinite(z) && x >= L.bminx && x <= L.bmaxx && y >= L.bminy &&
+           y <= L.bmaxy && z >= L.bminz && z <= L.bmaxz;
+}
+
+__device__ __forceinline__ void rt_bin(const RorLaunch &L, float x, float y, int &bx, int &by) {
+    bx = min(max((int)((x - L.bminx) * L.inv_cs), 0), L.nbx - 1);
+    by = min(max((int)((y - L.bminy) * L.inv_cs), 0), L.nby - 1);
+}
+
+// PassThrough z, x, y (inclusive; PCL 1.12 drops non-finite) + exclusion discs, seed_gen:459-525.
+__device__ __forceinline__ bool rt_candidate(const RorLaunch &L, float x, float y, float z) {
+    if (z < L.cminz || z > L.cmaxz) return false;
+    if (x < L.cminx || x > L.cmaxx) return false;
+    if (y < L.cminy || y > L.cmaxy) return false;
+#pragma unroll
+    for (int e = 0; e < 11; ++e) {
+        float dx = x - c_excl_rt[3 * e], dy = y - c_excl_rt[3 * e + 1];
+        float dist_sq = dx * dx + dy * dy;
+        float rr = c_excl_rt[3 * e + 2] * c_excl_rt[3 * e + 2];
+        if (dist_sq <= rr) return false;
+    }
+    return true;
+}
+
+__device__ __forceinline__ bool rt_in(const RorLaunch &L, float4 p, float4 q) {
+    float dx = p.x - q.x, dy = p.y - q.y, dz = p.z - q.z;
+    float d2 = dx * dx;
+    d2 = d2 + dy * dy;
+    d2 = d2 + dz * dz;
+    return L.is_dense ? (d2 <= L.r2df) : (d2 < L.r2f);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Passes 1 and 3: count / scatter. One sub-chunk = kRtSub consecutive points (kRtPer per thread,
+// strided by the block size so every load instruction is coalesced).
+constexpr int kRtTB = 256, kRtPer = 8, kRtSub = kRtTB * kRtPer, kRtMaxPairs = 4 * kRtSub;
+
+// tiles whose bins a point's 3 x 3 bins touch: [tx0, tx1] x [ty0, ty1], own tile (bx / TB, by / TB)
+__device__ __forceinline__ void rt_tiles(const RorLaunch &L, int bx, int by, int &tx0, int &tx1, int &ty0, int &ty1) {
+    tx0 = max(bx - 1, 0) / L.TB; tx1 = min(bx + 1, L.nbx - 1) / L.TB;
+    ty0 = max(by - 1, 0) / L.TB; ty1 = min(by + 1, L.nby - 1) / L.TB;
+}
+
+template <bool SCATTER>
+__global__ __launch_bounds__(kRtTB) void k_rt_part(RorLaunch L, int *tile_count, int *tile_cursor, float4 *staged,
+                                                   unsigned long long *n_own) {
+    extern __shared__ int sh[];
+    int *hist = sh;                      // [ntiles]: count, then (scatter) the run's base
+    int *touched = sh + L.ntiles;        // tiles touched in this sub-chunk
+    int *ntouch = touched + L.max_touch;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < L.ntiles; i += kRtTB) hist[i] = 0;
+    if (tid == 0) *ntouch = 0;
+    __syncthreads();
+    unsigned own = 0;
+    for (uint64_t base = (uint64_t)blockIdx.x * kRtSub; base < L.n; base += (uint64_t)gridDim.x * kRtSub) {
+        float4 pt[kRtPer];
+        int slot[kRtPer][4];   // (tile << 13 | rank) per copy, -1 unused
+        // all loads first (kRtPer independent 16 B loads in flight per lane), then the LDS walk
+#pragma unroll
+        for (int j = 0; j < kRtPer; ++j) {
+            const uint64_t i = base + (uint64_t)j * kRtTB + tid;
+            pt[j] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+            if (i < L.n) rt_load(L, i, pt[j].x, pt[j].y, pt[j].z);
+            if (i < L.n) pt[j].w = 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < kRtPer; ++j) {
+            slot[j][0] = slot[j][1] = slot[j][2] = slot[j][3] = -1;
+            const float x = pt[j].x, y = pt[j].y, z = pt[j].z;
+            if (__float_as_int(pt[j].w) < 0 || !rt_binned(L, x, y, z)) continue;
+            ++own;
+            int bx, by, tx0, tx1, ty0, ty1;
+            rt_bin(L, x, y, bx, by);
+            rt_tiles(L, bx, by, tx0, tx1, ty0, ty1);
+            const int otile = (by / L.TB) * L.ntx + bx / L.TB;
+            if (SCATTER) pt[j].w = __int_as_float(rt_candidate(L, x, y, z) ? 1 : 0);
+            int c = 0;
+            for (int ty = ty0; ty <= ty1; ++ty)
+                for (int tx = tx0; tx <= tx1; ++tx) {
+                    const int t = ty * L.ntx + tx;
+                    const int r = atomicAdd(&hist[t], 1);
+                    if (r == 0) touched[atomicAdd(ntouch, 1)] = t;
+                    if (SCATTER) slot[j][c] = (t == otile ? 0 : 1 << 30) | (t << 13) | r;   // bit 30: halo copy
+                    ++c;
+                }
+        }
+        __syncthreads();
+        const int nt = *ntouch;
+        for (int k = tid; k < nt; k += kRtTB) {
+            const int t = touched[k];
+            if (SCATTER) hist[t] = atomicAdd(&tile_cursor[t], hist[t]);
+            else { atomicAdd(&tile_count[t], hist[t]); hist[t] = 0; }
+        }
+        __syncthreads();
+        if (SCATTER) {
+#pragma unroll
+            for (int j = 0; j < kRtPer; ++j)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int s = slot[j][c];
+                    if (s < 0) continue;
+                    const int t = (s >> 13) & ((1 << 17) - 1), r = s & 8191;
+                    float4 q = pt[j];
+                    if (s & (1 << 30)) q.w = __int_as_float(0);   // a halo copy is never tested here
+                    staged[hist[t] + r] = q;
+                }
+            __syncthreads();
+            for (int k = tid; k < nt; k += kRtTB) hist[touched[k]] = 0;
+        }
+        if (tid == 0) *ntouch = 0;
+        __syncthreads();
+    }
+    if (!SCATTER) {
+        for (int o = 32; o > 0; o >>= 1) own += __shfl_xor(own, o);
+        if ((tid & 63) == 0 && own) atomicAdd(n_own, (unsigned long long)own);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Pass 4: per tile, counting sort by bin in LDS, neighbour counts, raster bitmap.
+constexpr int kRorThreads = 1024, kRorCap = 4096, kRorPer = kRorCap / kRorThreads;
+
+// XCD-aware block order (cdna_hip_programming.md §5.5): consecutive blocks b = j (mod 8) run on XCD j.
+__device__ __forceinline__ int rt_xcd_block(int b, int n) {
+    const int q = n >> 3, r = n & 7, j = b & 7, k = b >> 3;
+    return j * q + min(j, r) + k;
+}
+
+template <class Pts>
+__device__ __forceinline__ int rt_scan(const RorLaunch &L, float4 p, Pts pts, int k0, int k1, int cnt) {
+    for (int k = k0; k < k1 && cnt < L.need; k += 4) {
+        float4 q[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) q[j] = pts[min(k + j, k1 - 1)];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cnt += (k + j < k1 && rt_in(L, p, q[j])) ? 1 : 0;
+    }
+    return cnt;
+}
+
+// LDS of k_rt_ror: kRorCap staged points (64 KB), the bin offsets of the largest tile (TB = 64 bins
+// + ring: 66^2), and the tile's raster window (kRtWinWords 64-bit words)
+constexpr int kRtMaxLocalBins = 66 * 66, kRtWinWords = 512;
+
+__global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *tile_start, const float4 *staged,
+                                                        float4 *scratch, uint64_t *rbits,
+                                                        unsigned long long *counters) {
+    __shared__ float4 pts[kRorCap];
+    __shared__ int bstart[kRtMaxLocalBins + 1];
+    __shared__ unsigned long long win[kRtWinWords];
+    const int tid = threadIdx.x;
+    const int t = rt_xcd_block(blockIdx.x, gridDim.x);
+    const int tx = t % L.ntx, ty = t / L.ntx;
+    const int a = tile_start[t], n = tile_start[t + 1] - a;
+    if (n == 0) return;
+    const int LB = L.TB + 2;                        // local bins: the tile's bins and a ring of halo bins
+    const int bx0 = tx * L.TB - 1, by0 = ty * L.TB - 1;
+    const int nlb = LB * LB;
+    // raster window: rows [cy0, cy0 + L.win_rows), words [cw0, cw0 + L.win_w) of the raster window bits
+    const float wx_lo = L.bminx + (float)(tx * L.TB) / L.inv_cs, wy_lo = L.bminy + (float)(ty * L.TB) / L.inv_cs;
+    const int cy0 = (int)floor(((double)wy_lo - L.origin_y) / (double)L.res) - 2;
+    const int cx0 = (int)floor(((double)wx_lo - L.origin_x) / (double)L.res) - 2;
+    const int cw0 = (int)floor((double)(cx0 - L.wx0) / 64.0);
+    const bool use_win = L.win_rows > 0;
+    for (int i = tid; i <= nlb; i += kRorThreads) bstart[i] = 0;
+    if (use_win)
+        for (int i = tid; i < L.win_rows * L.win_w; i += kRorThreads) win[i] = 0ull;
+    __syncthreads();
+    auto lbin = [&](float4 q) {
+        int bx, by;
+        rt_bin(L, q.x, q.y, bx, by);
+        return (by - by0) * LB + (bx - bx0);       // in [0, nlb): a copy lies in the tile's 3 x 3 reach
+    };
+    const bool fits = n <= kRorCap;
+    // counting sort: histogram (ranks kept in registers when the tile fits), scan, place
+    float4 q[kRorPer];
+    int rk[kRorPer];
+    if (fits) {
+#pragma unroll
+        for (int j = 0; j < kRorPer; ++j) {
+            const int k = tid + j * kRorThreads;
+            rk[j] = -1;
+            if (k < n) {
+                q[j] = staged[a + k];
+                rk[j] = atomicAdd(&bstart[lbin(q[j]) + 1], 1);
+            }
+        }
+    } else {
+        for (int k = tid; k < n; k += kRorThreads) atomicAdd(&bstart[lbin(staged[a + k]) + 1], 1);
+    }
+    __syncthreads();
+    if (tid < 64) {   // inclusive scan of bstart[1..nlb] by one wave (nlb <= kRtMaxLocalBins)
+        int carry = 0;
+        for (int c0 = 1; c0 <= nlb; c0 += 64) {
+            const int i = c0 + tid;
+            int v = i <= nlb ? bstart[i] : 0;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int u = __shfl_up(v, o);
+                if (tid >= o) v += u;
+            }
+            if (i <= nlb) bstart[i] = v + carry;
+            carry += __shfl(v, 63);
+        }
+    }
+    __syncthreads();
+    const float4 *P;
+    if (fits) {
+#pragma unroll
+        for (int j = 0; j < kRorPer; ++j)
+            if (rk[j] >= 0) pts[bstart[lbin(q[j])] + rk[j]] = q[j];
+        P = pts;
+    } else {
+        // too many points for LDS: place them in the tile's range of the global scratch (L2-resident
+        // for one tile) with a cursor per bin, then scan from there
+        float4 *S = scratch + a;
+        __syncthreads();
+        int *cur = reinterpret_cast<int *>(pts);   // reuse LDS as the cursors (nlb + 1 <= kRorCap * 4)
+        for (int i = tid; i <= nlb; i += kRorThreads) cur[i] = bstart[i];
+        __syncthreads();
+        for (int k = tid; k < n; k += kRorThreads) {
+            const float4 v = staged[a + k];
+            S[atomicAdd(&cur[lbin(v)], 1)] = v;
+        }
+        __threadfence();
+        P = S;
+    }
+    __syncthreads();
+    unsigned kept_n = 0;
+    for (int k = tid; k < n; k += kRorThreads) {
+        const float4 p = fits ? pts[k] : P[k];
+        if (!__float_as_int(p.w)) continue;     // neighbour only
+        int bx, by;
+        rt_bin(L, p.x, p.y, bx, by);
+        const int lx = bx - bx0, ly = by - by0;
+        int cnt = 0;
+#pragma unroll
+        for (int rr = 0; rr < 3; ++rr) {        // own bin row first: the likeliest neighbours
+            const int yy = ly + (rr == 0 ? 0 : (rr == 1 ? -1 : 1));
+            if (cnt >= L.need) break;
+            const int r0 = yy * LB + lx - 1;
+            cnt = fits ? rt_scan(L, p, pts, bstart[r0], bstart[r0 + 3], cnt)
+                       : rt_scan(L, p, P, bstart[r0], bstart[r0 + 3], cnt);
+        }
+        if (cnt < L.need) continue;
+        // kept: counted iff its clamped cell is owned, rastered iff inside the grid (seed_gen:606-619)
+        const int gx = (int)(((double)p.x - L.origin_x) / (double)L.res);
+        const int gy = (int)(((double)p.y - L.origin_y) / (double)L.res);
+        const int cx = min(max(gx, 0), L.W - 1), cy = min(max(gy, 0), L.H - 1);
+        if (cx < L.rx0 || cx >= L.rx1 || cy < L.ry0 || cy >= L.ry1) continue;
+        ++kept_n;
+        if (gx < 0 || gx >= L.W || gy < 0 || gy >= L.H) continue;
+        const int bxw = gx - L.wx0, r = gy - L.wy0;
+        const int wr = r - (cy0 - L.wy0), ww = (bxw >> 6) - cw0;
+        const unsigned long long bit = 1ull << (bxw & 63);
+        if (use_win && wr >= 0 && wr < L.win_rows && ww >= 0 && ww < L.win_w)
+            atomicOr(&win[wr * L.win_w + ww], bit);
+        else
+            atomicOr(reinterpret_cast<unsigned long long *>(&rbits[(size_t)r * L.WWr + (bxw >> 6)]), bit);
+    }
+    __syncthreads();
+    if (use_win)
+        for (int i = tid; i < L.win_rows * L.win_w; i += kRorThreads) {
+            const unsigned long long v = win[i];
+            if (!v) continue;
+            const int r = cy0 - L.wy0 + i / L.win_w, w = cw0 + i % L.win_w;
+            if (r >= 0 && r < L.Hr && w >= 0 && w < L.WWr)
+                atomicOr(reinterpret_cast<unsigned long long *>(&rbits[(size_t)r * L.WWr + w]), v);
+        }
+    for (int o = 32; o > 0; o >>= 1) kept_n += __shfl_xor(kept_n, o);
+    if ((tid & 63) == 0 && kept_n)
+        atomicAdd(&counters[(blockIdx.x * (kRorThreads / 64) + (tid >> 6)) & (kRorCounters - 1)],
+                  (unsigned long long)kept_n);
+}
+
+// ---------------------------------------------------------------------------------------------
+void rt_configure(RorLaunch &L, int Hr, int WWr) {
+    L.TB = 32;
+    for (;;) {
+        L.ntx = (L.nbx + L.TB - 1) / L.TB;
+        L.nty = (L.nby + L.TB - 1) / L.TB;
+        if ((long long)L.ntx * L.nty <= kRtMaxTiles || L.TB >= 1024) break;
+        L.TB *= 2;
+    }
+    if ((L.TB + 2) * (L.TB + 2) > kRtMaxLocalBins) throw std::runtime_error("ROR bin grid too large for the tile walk");
+    L.ntiles = L.ntx * L.nty;
+    L.max_touch = std::min(L.ntiles, kRtMaxPairs);
+    L.Hr = Hr; L.WWr = WWr;
+    // raster window of one tile: its cells (TB bins of 1/inv_cs) + 2 cells of slack on each side
+    const double span = (double)L.TB / (double)L.inv_cs / (double)L.res;
+    const int cells = (int)std::ceil(span) + 6;
+    L.win_rows = cells;
+    L.win_w = (cells + 63) / 64 + 1;
+    if (L.win_rows * L.win_w > kRtWinWords) L.win_rows = 0;   // windows too large: OR straight into HBM
+}
+
+size_t rt_part_lds(const RorLaunch &L) { return sizeof(int) * ((size_t)L.ntiles + L.max_touch + 1); }
+
+void launch_rt_count(const RorLaunch &L, int *tile_count, unsigned long long *n_own, int n_blocks, hipStream_t s) {
+    if (!L.n) return;
+    const size_t lds = rt_part_lds(L);
+    if (lds > 64 * 1024) {   // the tile histogram exceeds the default dynamic-LDS limit (gfx950: 160 KB)
+        AOS_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rt_part<false>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        AOS_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rt_part<true>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    }
+    const int nb = std::max(1, std::min(n_blocks, cdiv_i((long long)L.n, kRtSub)));
+    k_rt_part<false><<<nb, kRtTB, lds, s>>>(L, tile_count, nullptr, nullptr, n_own);
+    AOS_HIP(hipGetLastError());
+}
+
+void launch_rt_scatter(const RorLaunch &L, int *tile_cursor, float4 *staged, int n_blocks, hipStream_t s) {
+    if (!L.n) return;
+    const int nb = std::max(1, std::min(n_blocks, cdiv_i((long long)L.n, kRtSub)));
+    k_rt_part<true><<<nb, kRtTB, rt_part_lds(L), s>>>(L, nullptr, tile_cursor, staged, nullptr);
+    AOS_HIP(hipGetLastError());
+}
+
+void launch_rt_ror(const RorLaunch &L, const int *tile_start, const float4 *staged, float4 *scratch, uint64_t *rbits,
+                   unsigned long long *counters, hipStream_t s) {
+    if (!L.n || !L.ntiles) return;
+    k_rt_ror<<<L.ntiles, kRorThreads, 0, s>>>(L, tile_start, staged, scratch, rbits, counters);
+    AOS_HIP(hipGetLastError());
+}
+
+}  // namespace aos

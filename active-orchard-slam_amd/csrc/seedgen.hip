@@ -10,14 +10,10 @@
 
 #include "aos_ctx.h"
 
-#ifndef AOS_ROR_BIN2
-#define AOS_ROR_BIN2 0
-#endif
-
 using namespace aos;
 
 void aos_ctx::release() {
-    for (DevBuf *b : {&cloud_copy, &bin_count, &bin_start, &pt_binslot, &sorted, &scan_tmp, &counters, &raster_bytes,
+    for (DevBuf *b : {&cloud_copy, &bin_count, &bin_start, &pt_binslot, &sorted, &ror_scratch, &scan_tmp, &counters,
                       &raster_bits, &infl_bits, &open_bits, &thin_a, &thin_b, &occ_bytes, &skel_bytes, &flags,
                       &full_infl, &full_skel, &map_buf, &scan_stage})
         b->release();
@@ -66,7 +62,7 @@ void aos_ctx::upload_h2d(void *dst, const void *src, size_t bytes) {
         }
     // the handle's stream may still read dst (the previous frame): the copies start after it
     AOS_HIP(hipEventRecord(ev[15], stream));
-    const size_t per = (bytes / kUpThreads + 4095) & ~(size_t)4095;
+    const size_t per = ((bytes + kUpThreads - 1) / kUpThreads + 4095) & ~(size_t)4095;   // covers all bytes
     std::exception_ptr err[kUpThreads];
     auto work = [&](int t) {
         try {
@@ -108,18 +104,23 @@ void aos_ctx::release_uploader() {
     }
 }
 
+// The cloud state is committed only after the upload succeeded: a failed upload leaves no cloud
+// (aos_seedgen_reprocess then fails instead of reading a partly copied buffer).
 void aos_ctx::set_cloud(const aos_cloud_view &v) {
+    have_cloud = false;
+    const uint8_t *dc;
+    if (v.on_device) {
+        dc = static_cast<const uint8_t *>(v.data);
+    } else {
+        size_t bytes = (size_t)v.n_points * v.point_step;
+        void *dst = cloud_copy.ensure(std::max<size_t>(bytes, 16));
+        if (bytes) upload_h2d(dst, v.data, bytes);
+        dc = cloud_copy.as<uint8_t>();
+    }
     n_points = v.n_points;
     step = v.point_step; ox = v.off_x; oy = v.off_y; oz = v.off_z;
     is_dense = v.is_dense ? 1 : 0;
-    if (v.on_device) {
-        d_cloud = static_cast<const uint8_t *>(v.data);
-    } else {
-        size_t bytes = (size_t)n_points * step;
-        void *dst = cloud_copy.ensure(std::max<size_t>(bytes, 16));
-        if (bytes) upload_h2d(dst, v.data, bytes);
-        d_cloud = cloud_copy.as<uint8_t>();
-    }
+    d_cloud = dc;
     have_cloud = true;
 }
 
@@ -199,9 +200,10 @@ int thin_iterations(const int *flags, int iters_run) {
 }  // namespace aos
 
 // a1-a4: ROR restricted to the points that can reach the (own) cells, clip, exclusion discs, raster
-// into raster_bytes (o.Wr x o.Hr window, zeroed here). Records ev[10] / ev[11] around the neighbour
-// count kernel and copies the number of binned points to h_stats[0].
-void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o) {
+// straight into the bit-packed window rbits (o.Hr rows of ceil(o.Wr / 64) words, zeroed here), by the
+// tile walk of ror.hip. Records ev[12] / ev[13] / ev[14] / ev[10] / ev[11] around its passes and
+// leaves the number of binned points in h_stats[0].
+void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits) {
     hipStream_t s = stream;
     static_cast<int *>(h_stats.ensure(64 + 8 * kRorCounters))[0] = 0;
     RorLaunch L{};
@@ -228,47 +230,45 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o) {
     L.need = P.ror_min_neighbors + 1;
     L.origin_x = g.origin_x; L.origin_y = g.origin_y; L.res = g.res; L.W = g.W; L.H = g.H;
     L.rx0 = o.rx0; L.ry0 = o.ry0; L.rx1 = o.rx1; L.ry1 = o.ry1; L.wx0 = o.wx0; L.wy0 = o.wy0; L.Wr = o.Wr;
-    const int nb = L.nbx * L.nby;
-    const size_t Cr = (size_t)o.Wr * o.Hr;
+    const int WWr = (o.Wr + 63) / 64;
+    rt_configure(L, o.Hr, WWr);
+    const int nt = L.ntiles;
 
-    int *d_bc = static_cast<int *>(bin_count.ensure(sizeof(int) * (nb + 1)));
-    int *d_bs = static_cast<int *>(bin_start.ensure(sizeof(int) * (nb + 1)));
-    int2 *d_ps = static_cast<int2 *>(pt_binslot.ensure(sizeof(int2) * std::max<uint64_t>(n_points, 1)));
-    unsigned long long *d_cnt = static_cast<unsigned long long *>(counters.ensure(8 * kRorCounters));
-    uint8_t *d_rb = static_cast<uint8_t *>(raster_bytes.ensure(std::max<size_t>(Cr, 1)));
-    size_t st = scan_temp_bytes(nb + 1);
+    int *d_tc = static_cast<int *>(bin_count.ensure(sizeof(int) * (nt + 1)));
+    int *d_ts = static_cast<int *>(bin_start.ensure(sizeof(int) * (nt + 1)));
+    int *d_cur = static_cast<int *>(pt_binslot.ensure(sizeof(int) * (nt + 1)));
+    unsigned long long *d_cnt = static_cast<unsigned long long *>(counters.ensure(8 * kRorCounters + 8));
+    unsigned long long *d_own = d_cnt + kRorCounters;
+    size_t st = scan_temp_bytes(nt + 1);
     void *d_st = scan_tmp.ensure(st);
-    AOS_HIP(hipMemsetAsync(d_bc, 0, sizeof(int) * (nb + 1), s));
-    AOS_HIP(hipMemsetAsync(d_cnt, 0, 8 * kRorCounters, s));
-    AOS_HIP(hipMemsetAsync(d_rb, 0, Cr, s));
+    AOS_HIP(hipMemsetAsync(d_tc, 0, sizeof(int) * (nt + 1), s));
+    AOS_HIP(hipMemsetAsync(d_cnt, 0, 8 * kRorCounters + 8, s));
+    AOS_HIP(hipMemsetAsync(rbits, 0, sizeof(uint64_t) * (size_t)o.Hr * WWr, s));
     // PCL dense kNN needs k = min_pts + 1 points in the whole cloud (else every point is removed).
     // A tile's shard holds every neighbour of its own candidates, so a shard with fewer points has
     // no keepable candidate either: the local test is exact.
     const bool any = n_points > 0 && !(is_dense && n_points < (uint64_t)L.need);
-    if (any) {
-        // total binned = bin_start[nb]; bound the sorted buffer by n_points
-        float4 *d_sorted = static_cast<float4 *>(sorted.ensure(sizeof(float4) * std::max<uint64_t>(n_points, 1)));
-        AOS_HIP(hipEventRecord(ev[12], s));
-#if AOS_ROR_BIN2
-        (void)d_ps;
-        launch_ror_count(L, d_bc, s);
-        AOS_HIP(hipEventRecord(ev[13], s));
-        AOS_HIP(hipMemsetAsync(d_bs, 0, sizeof(int), s));
-        launch_exclusive_scan(d_bc, d_bs + 1, nb, d_st, st, s);   // cursor[1 + b] = start of bin b
-        AOS_HIP(hipEventRecord(ev[14], s));
-        launch_ror_place(L, d_bs, d_sorted, s);                    // afterwards d_bs[b] = start of bin b
-#else
-        launch_ror_bin(L, d_bc, d_ps, s);
-        AOS_HIP(hipEventRecord(ev[13], s));
-        launch_exclusive_scan(d_bc, d_bs, nb + 1, d_st, st, s);
-        AOS_HIP(hipEventRecord(ev[14], s));
-        launch_ror_scatter(L, d_bs, d_ps, d_sorted, s);
-#endif
-        AOS_HIP(hipEventRecord(ev[10], s));
-        launch_ror_raster(L, d_bs, d_sorted, d_rb, d_cnt, s);
-        AOS_HIP(hipEventRecord(ev[11], s));
-        AOS_HIP(hipMemcpyAsync(h_stats.p, d_bs + nb, sizeof(int), hipMemcpyDeviceToHost, s));
-    }
+    if (!any) return;
+    const int nblk = 1024;   // 4 workgroups (34 KB LDS each at C2) per CU
+    AOS_HIP(hipEventRecord(ev[12], s));
+    launch_rt_count(L, d_tc, d_own, nblk, s);
+    AOS_HIP(hipEventRecord(ev[13], s));
+    launch_exclusive_scan(d_tc, d_ts, nt + 1, d_st, st, s);
+    // the staged array holds own + halo copies: size it from the count (one small read-back)
+    int *h = static_cast<int *>(h_stats.p);
+    AOS_HIP(hipMemcpyAsync(h + 2, d_ts + nt, sizeof(int), hipMemcpyDeviceToHost, s));
+    AOS_HIP(hipMemcpyAsync(h + 4, d_own, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    AOS_HIP(hipMemcpyAsync(d_cur, d_ts, sizeof(int) * (nt + 1), hipMemcpyDeviceToDevice, s));
+    AOS_HIP(hipStreamSynchronize(s));
+    const size_t n_staged = (size_t)std::max(h[2], 1);
+    h[0] = (int)*reinterpret_cast<unsigned long long *>(h + 4);
+    float4 *d_staged = static_cast<float4 *>(sorted.ensure(sizeof(float4) * n_staged));
+    float4 *d_scratch = static_cast<float4 *>(ror_scratch.ensure(sizeof(float4) * n_staged));
+    AOS_HIP(hipEventRecord(ev[14], s));
+    launch_rt_scatter(L, d_cur, d_staged, nblk, s);
+    AOS_HIP(hipEventRecord(ev[10], s));
+    launch_rt_ror(L, d_ts, d_staged, d_scratch, rbits, d_cnt, s);
+    AOS_HIP(hipEventRecord(ev[11], s));
 }
 
 void aos_ctx::run_seedgen(bool want_host, aos_seedgen_out &out) {
@@ -285,14 +285,13 @@ void aos_ctx::run_seedgen(bool want_host, aos_seedgen_out &out) {
 
     // ---------------- a1-a4: ROR restricted to the clip box, clip, exclusion discs, raster
     RorOwn own{0, 0, g.W, g.H, 0, 0, g.W, g.H, false, {0, 0, 0, 0}};
-    ror_stage(g, own);
+    uint64_t *d_rbits = static_cast<uint64_t *>(raster_bits.ensure(Cw * 8));
+    ror_stage(g, own, d_rbits);
     AOS_HIP(hipEventRecord(ev[1], s));
 
     // ---------------- a5 inflation, a6 frame -> /occupancy_grid
-    uint64_t *d_rbits = static_cast<uint64_t *>(raster_bits.ensure(Cw * 8));
     uint64_t *d_ibits = static_cast<uint64_t *>(infl_bits.ensure(Cw * 8));
     int8_t *d_occ = static_cast<int8_t *>(occ_bytes.ensure((size_t)g.W * g.H));
-    launch_pack_bits(raster_bytes.as<uint8_t>(), d_rbits, g.W, g.H, g.WW, s);
     launch_inflate(d_rbits, d_ibits, g, s);
     launch_bits_to_bytes(d_ibits, d_occ, g, 5, s);
     AOS_HIP(hipEventRecord(ev[2], s));

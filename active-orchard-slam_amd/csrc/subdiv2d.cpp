@@ -177,6 +177,8 @@ bool Subdiv2D::insert(float x, float y) {
     }
     if (curr_edge == 0) return false;  // CV_Assert
     curr_point = new_point(x, y, 0);
+    if (loc == 0 && !force_loop && insert_cavity(curr_edge, curr_point)) { ++n_cavity; return true; }
+    ++n_loop;
     int base = new_edge();
     const int first_point = org(curr_edge);
     set_pts(base, first_point, curr_point);
@@ -185,7 +187,12 @@ bool Subdiv2D::insert(float x, float y) {
         base = connect(curr_edge, sym(base));
         curr_edge = oprev(base);
     } while (dst(curr_edge) != first_point);
-    curr_edge = oprev(base);
+    swap_loop(oprev(base), first_point, curr_point);
+    return true;
+}
+
+// OpenCV's swap loop (Subdiv2D::insert after the connects), the reference path.
+void Subdiv2D::swap_loop(int curr_edge, int first_point, int curr_point) {
     const int max_edges = (int)rec.size() * 4;
     // Swap loop with the predicates written out on exact double copies of the float coordinates
     // (the float -> double conversions are exact, so every product and sum rounds as in
@@ -214,6 +221,111 @@ bool Subdiv2D::insert(float x, float y) {
             curr_edge = lprev(onext(curr_edge));
         }
     }
+}
+
+// Cavity form of an INSIDE insert (subdiv2d.h). e0 = locate's edge: p lies left of it, inside the
+// triangle (e0, Lnext e0, Lnext^2 e0). Returns false, having changed nothing but the scratch, when
+// the DFS cannot certify the cavity; the caller then runs the connects and the swap loop.
+bool Subdiv2D::insert_cavity(int e0, int p) {
+    const size_t nv = vp.size();
+    if (vstamp.size() < nv) { vstamp.resize(2 * nv + 64, 0); vspoke.resize(2 * nv + 64, 0); }
+    if (++stamp >= (1 << 29)) { std::fill(vstamp.begin(), vstamp.end(), 0); stamp = 1; }
+    const int sA = 2 * stamp, sUsed = 2 * stamp + 1;   // two marks per insert: has a spoke / on the boundary
+    const int eB = lnext(e0), eA = lnext(eB);          // root link edges in walk order: eA, eB, e0
+    if (lnext(eA) != e0) return false;
+    const int first = org(e0), v1 = org(eB), v2 = org(eA);
+    if (first == v1 || v1 == v2 || v2 == first) return false;
+    vstamp[first] = vstamp[v1] = vstamp[v2] = sA;
+
+    const V2d P = vd[p];
+    auto area = [](const V2d &a, const V2d &b, const V2d &c) { return (b.x - a.x) * (c.y - a.y) - (b.y - a.y) * (c.x - a.x); };
+    // scratch sized for the worst case: every swap adds one apex, one stacked edge and one boundary edge
+    const size_t cap = vp.size() + 8;
+    if (dfs_stack.size() < cap) { dfs_stack.resize(2 * cap); cav_flip.resize(2 * cap); cav_apex.resize(2 * cap); cav_bnd.resize(2 * cap); }
+    int *stk = dfs_stack.data(), *fl = cav_flip.data(), *ap = cav_apex.data(), *bd = cav_bnd.data();
+    int sp = 0, nf = 0, nb = 0;
+    stk[sp++] = e0; stk[sp++] = eB;
+    int e = eA;
+    // Pre-order walk; every test reads the old triangle right of the link edge (never incident to p).
+    // The first child (w -> v) is walked at once; the second (u -> w) waits on the stack.
+    for (;;) {
+        const int t = oprev(e);
+        const int w = dst(t), u = org(e), v = dst(e);
+        const V2d &T = vd[w], &O = vd[u], &D = vd[v];
+        bool flip = false;
+        if (area(T, D, O) > 0) {   // same expression order as swap_loop
+            double val = T.n2 * area(D, P, O);
+            val -= D.n2 * area(T, P, O);
+            val += P.n2 * area(T, D, O);
+            val -= O.n2 * area(T, D, P);
+            flip = val < -(FLT_EPSILON * 0.125);
+        }
+        if (flip) {
+            if (vstamp[w] == sA || w == p || nf + 4 >= (int)cap) return false;   // the cavity would wrap a vertex
+            vstamp[w] = sA;
+            vspoke[w] = e;                                   // e becomes w -> p
+            fl[nf] = e; ap[nf] = w; ++nf;
+            stk[sp++] = t;                                   // u -> w, after the w -> v subtree
+            e = sym(onext(sym(e)));                          // w -> v
+        } else {
+            bd[nb++] = e;
+            if (sp == 0) break;
+            e = stk[--sp];
+        }
+    }
+    const int m = nb;
+    if (m != 3 + nf) return false;
+    int *xs = dfs_stack.data();   // the stack is empty now: reuse it for Org(L_k)
+    for (int k = 0; k < m; ++k) xs[k] = org(bd[k]);
+    for (int k = 0; k < m; ++k) {   // the boundary closes: Org(L_k) = Dst(L_k+1), each vertex once
+        const int x = xs[k];
+        if (dst(bd[k + 1 == m ? 0 : k + 1]) != x || vstamp[x] != sA) return false;
+        vstamp[x] = sUsed;
+    }
+
+    // ---- certified: the connects (reference code, they number the three new quad-edges), then
+    // the bulk write of the swaps' outcome
+    int base = new_edge();
+    set_pts(base, first, p);
+    splice(base, e0);
+    vspoke[first] = base;
+    int ce = e0;
+    do {
+        base = connect(ce, sym(base));
+        vspoke[org(base)] = base;
+        ce = oprev(base);
+    } while (dst(ce) != first);
+    for (int i = 0; i < nf; ++i) {   // swapEdges: setEdgePoints(e, apex, p)
+        const int e = fl[i], w = ap[i];
+        rec[e >> 2].org[dir(e)] = w;
+        rec[e >> 2].org[dir(e) ^ 1] = p;
+        vfirst[w] = e;
+    }
+    if (nf) vfirst[p] = sym(fl[nf - 1]);
+    // rings: around x_k = Org(L_k) the wedge between L_k and Sym L_k+1 now holds only the spoke;
+    // around p the spokes run counter-clockwise x_k -> x_k-1 (the walk is clockwise)
+    int *sp_ = cav_apex.data();   // apexes are written: reuse for the spokes S_k (x_k -> p)
+    for (int k = 0; k < m; ++k) sp_[k] = vspoke[xs[k]];
+    for (int k = 0; k < m; ++k) {
+        const int k1 = k + 1 == m ? 0 : k + 1, k0 = k == 0 ? m - 1 : k - 1;
+        const int L = bd[k], Ln = bd[k1], S = sp_[k];
+        on(L) = S; on(S) = sym(Ln); op(S) = L; op(sym(Ln)) = S;
+        on(sym(S)) = sym(sp_[k0]); op(sym(S)) = sym(sp_[k1]);
+    }
+    return true;
+}
+
+bool Subdiv2D::same_state(const Subdiv2D &o) const {
+    if (rec.size() != o.rec.size() || vp.size() != o.vp.size() || recent != o.recent || free_q != o.free_q ||
+        free_p != o.free_p)
+        return false;
+    for (size_t q = 0; q < rec.size(); ++q)
+        for (int d = 0; d < 2; ++d)
+            if (rec[q].on[d] != o.rec[q].on[d] || rec[q].op[d] != o.rec[q].op[d] || rec[q].org[d] != o.rec[q].org[d])
+                return false;
+    for (size_t v = 0; v < vp.size(); ++v)
+        if (vfirst[v] != o.vfirst[v] || vtype[v] != o.vtype[v] || vp[v].x != o.vp[v].x || vp[v].y != o.vp[v].y)
+            return false;
     return true;
 }
 

@@ -19,6 +19,21 @@
 // are recovered when the structure is exported (Onext(Rot e) = Rot^-1 Oprev(e)). On orchard seed rows
 // an insert performs ~56 swaps (~115 flip-loop steps) as each new seed on the next tree line takes
 // over the fan of the previous one, so these constant factors are the replay's cost.
+//
+// Cavity form of the swap loop (insert_cavity). Every triangle the swap loop tests lies across a
+// link edge from the new point p, so it is never incident to p: it is an *old* triangle, untouched
+// when it is tested. Each test is therefore a pure function of the triangulation before the insert,
+// and the loop is a depth-first pre-order walk of the cavity tree (children in clockwise order
+// around p). A read-only DFS over the old structure replays exactly the same tests with the same
+// arguments, then the outcome is written in one pass:
+//   * the internal edge e through which the walk entered cavity triangle T (directed as the loop's
+//     curr_edge) becomes T's apex -> p with pt[dir(e)] = apex (setEdgePoints in swapEdges);
+//   * vtx[apex].firstEdge = e, and vtx[p].firstEdge = Sym of the last swap in walk order;
+//   * the rings are the cyclic orders of the final star, which the walk order of the boundary
+//     (link) edges fixes; the unique onext/oprev values are stored directly.
+// The swap loop stays as the reference path (on-edge inserts, and any cavity the DFS cannot
+// certify: a vertex seen twice, a boundary that does not close). tools/sdcheck compares the two
+// paths' complete state after every insert.
 #pragma once
 #include <cstddef>
 #include <cstdint>
@@ -32,6 +47,11 @@ class Subdiv2D {
     void init_delaunay(float rx, float ry, float rw, float rh, int rect_mode);
     // Subdiv2D::insert; returns false where OpenCV throws (the reference catches and skips).
     bool insert(float x, float y);
+    // 0: cavity DFS + bulk write (default); 1: always OpenCV's swap loop (reference / cross-check)
+    void set_swap_loop(bool on) { force_loop = on; }
+    // full internal state (for the equivalence checker): rings, end points, firstEdge, recentEdge
+    bool same_state(const Subdiv2D &o) const;
+    long n_cavity = 0, n_loop = 0;   // inserts done by each path
     // getVoronoiFacetList(idx = {}): per real vertex (in vertex order) the facet polygon.
     // Emits the reference's edge list directly: (p_i, p_{i+1 mod n}) for facets with >= 2 points
     // (voronoi_diagram.cpp:97-114), as float x0, y0, x1, y1. Host reference of the GPU builder.
@@ -56,6 +76,11 @@ class Subdiv2D {
     std::vector<int> vfirst, vtype;   // type: -1 free, 0 real, 1 virtual
     std::vector<int> qx;              // export buffer (Raw::qe)
     int free_q = 0, free_p = 0, recent = 0;
+    bool force_loop = false;
+    // cavity DFS scratch: stack of link edges, swapped edges with their apex, boundary edges in walk
+    // order, per-vertex spoke (valid while vstamp[v] == stamp)
+    std::vector<int> dfs_stack, cav_flip, cav_apex, cav_bnd, vspoke, vstamp;
+    int stamp = 0;
     float tlx = 0, tly = 0, brx = 0, bry = 0;
 
     static int sym(int e) { return e ^ 2; }
@@ -82,6 +107,8 @@ class Subdiv2D {
     void swap_edge(int e);
     void delete_edge(int e);
     int locate(float px, float py, int &edge, int &vertex);
+    void swap_loop(int curr_edge, int first_point, int curr_point);
+    bool insert_cavity(int e0, int curr_point);
     void calc_voronoi();   // calcVoronoi on the exported layout (qx), creating the virtual vertices
     int facet_next(int e) const;
 };

@@ -198,13 +198,12 @@ void aos_ctx::run_tiled(const aos_comm &cm, int tiles_x, int tiles_y, int root, 
     // ---- a1-a4 for the candidates whose cell is an own cell, rastered into the window
     RorOwn own{64 * t.c0, t.y0, std::min(g.W, 64 * t.c1), t.y1, 64 * t.wc0, t.wy0, lg.W, lg.H, true,
                {t.box[0], t.box[1], t.box[2], t.box[3]}};
-    ror_stage(g, own);
+    uint64_t *d_rbits = static_cast<uint64_t *>(raster_bits.ensure(Cwl * 8));
+    ror_stage(g, own, d_rbits);
     AOS_HIP(hipEventRecord(ev[1], s));
 
     // ---- raster halo from the neighbours, a5 inflation on the window
-    uint64_t *d_rbits = static_cast<uint64_t *>(raster_bits.ensure(Cwl * 8));
     uint64_t *d_ibits = static_cast<uint64_t *>(infl_bits.ensure(Cwl * 8));
-    launch_pack_bits(raster_bytes.as<uint8_t>(), d_rbits, lg.W, lg.H, lg.WW, s);
     tile_halo_exchange(d_rbits, t, cm);
     launch_inflate(d_rbits, d_ibits, lg, s);
     AOS_HIP(hipEventRecord(ev[2], s));

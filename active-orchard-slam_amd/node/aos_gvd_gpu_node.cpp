@@ -61,8 +61,6 @@ class AosGvdGpuNode : public rclcpp::Node {
   private:
     void process() {
         if (seeds_.empty() || !skel_) return;   // gvd:257-259
-        const auto now = std::chrono::steady_clock::now();
-        if (std::chrono::duration<double>(now - last_).count() < 1.0 / rate_) return;
         aos_gvd_in in{};
         in.seeds_xy = seeds_.data(); in.n_seeds = (int32_t)(seeds_.size() / 2);
         in.rows_info_xy = rows_.data(); in.n_rows_poses = (int32_t)(rows_.size() / 2);
@@ -78,6 +76,10 @@ class AosGvdGpuNode : public rclcpp::Node {
             return;
         }
         if (!o.published) return;
+        // The graph is built on every callback; only publishing is throttled, with the time taken
+        // after the graph is built and measured from construction (gvd:80, 306-314).
+        const auto now = std::chrono::steady_clock::now();
+        if (std::chrono::duration<double>(now - last_).count() < 1.0 / rate_) return;
         aos::msg::GvdGraph g;                  // publishGraph gvd:897-1010
         g.header.frame_id = "map";
         g.header.stamp = this->now();
@@ -219,7 +221,7 @@ class AosGvdGpuNode : public rclcpp::Node {
 
     aos_ctx *ctx_ = nullptr;
     double rate_ = 10.0;
-    std::chrono::steady_clock::time_point last_{};
+    std::chrono::steady_clock::time_point last_ = std::chrono::steady_clock::now();   // gvd:80
     std::vector<double> seeds_, rows_;
     nav_msgs::msg::OccupancyGrid::SharedPtr skel_;
     rclcpp::Subscription<geometry_msgs::msg::PoseArray>::SharedPtr sub_seeds_, sub_rows_;

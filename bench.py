@@ -1,11 +1,13 @@
 #!/usr/bin/env python3
 """bench.py — Mcells/s of the AOS seed-gen + GVD hot path on MI355X (BASELINE.json metric).
 
-One step = one full frame of the path on one GPU: PointCloud2 (already resident in HBM) ->
-ROR / clip / raster -> inflation -> opening + Zhang-Suen -> clusters / tree rows / seeds ->
-GVD graph (seed merge, Delaunay replay, boundary points, edges, labels) -> host GvdGraph +
-seeds/rows arrays; the OccupancyGrid outputs stay device-resident (their D2H is PCIe, see DESIGN).
-Workload: config C2 (10 M points, 4096^2 cells @ 0.1 m, BASELINE.json configs[2]).
+One step = one full frame of the path on one GPU, measured as SURVEY §8d defines it: the
+PointCloud2 bytes in host memory -> ROR / clip / raster -> inflation -> opening + Zhang-Suen ->
+clusters / tree rows / seeds -> GVD graph (seed merge, Delaunay replay, boundary points, edges,
+labels) -> host GvdGraph, seeds / rows arrays and both OccupancyGrids in host memory.
+`value` = W*H / median frame time. The device-resident rate (cloud already in HBM, grids left in
+HBM) is reported beside it (`device_resident`). Workload: config C2 (10 M points, 4096^2 cells @
+0.1 m, BASELINE.json configs[2]).
 
 Multi-GPU (--gpus N, launched by torch.distributed.run): weak scaling — every rank processes its
 own independent 4096^2 map tile (scene seed 3 + rank); no data-path collective; the barrier and
@@ -24,7 +26,7 @@ for sub in ("tools", "active-orchard-slam_amd"):
     sys.path.insert(0, os.path.join(ROOT, sub))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-PMC_FILE = os.path.join(ROOT, "profiles", "r01_s_pmc_traffic.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
 
 
 def parse(argv=None):
@@ -34,11 +36,13 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default=None, help="C2 (default), or C3 with --tiled")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-config", default="C1")
+    ap.add_argument("--cpu-config", default="C2", help="config of the CPU baseline frame (default: the bench's C2)")
     ap.add_argument("--stream", action="store_true",
                     help="C4 (BASELINE configs[4]): 1 M-point 20 Hz scans appended to the device-resident C2 map")
-    ap.add_argument("--host-io", action="store_true",
-                    help="PCIe-inclusive variant: host cloud in, host OccupancyGrids out (DESIGN.md; not the metric)")
+    ap.add_argument("--device-io", action="store_true",
+                    help="time the device-resident frame (cloud in HBM, grids left in HBM) instead of SURVEY §8d's "
+                         "host-in / host-out frame")
+    ap.add_argument("--no-device-rate", action="store_true", help="skip the extra device-resident loop")
     ap.add_argument("--trace", action="store_true", help="per-step timeline of the pipelined loop on stderr")
     ap.add_argument("--pipeline", action="store_true",
                     help="overlap frame k's seed-gen with frame k-1's GVD (aos_gvd_from_seedgen_async); the last "
@@ -53,7 +57,9 @@ def parse(argv=None):
 
 def timed_region(step, steps: int, warmup: int, world: int, sync, dist=None, device=None):
     """The contract's timed region: W untimed steps, barrier + sync, EXACTLY K timed steps, sync +
-    barrier, then the max over ranks. Returns (seconds, per-step results of the last step)."""
+    barrier, then the max over ranks. Every step ends with its outputs in host memory, so the host
+    clock between steps is a frame time. Returns (seconds, per-step results, per-step seconds, max
+    over ranks per step)."""
     last = None
     for _ in range(warmup):
         last = step()
@@ -61,19 +67,21 @@ def timed_region(step, steps: int, warmup: int, world: int, sync, dist=None, dev
         dist.barrier()
     sync()
     t0 = time.perf_counter()
-    results = []
+    results, marks = [], [t0]
     for _ in range(steps):
         results.append(step())
+        marks.append(time.perf_counter())
     sync()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    per = [b - a for a, b in zip(marks[:-1], marks[1:])]
     if world > 1:
         import torch
-        t = torch.tensor([dt], dtype=torch.float64, device=device)
+        t = torch.tensor([dt] + per, dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    return dt, results or [last]
+        dt, per = float(t[0].item()), [float(x) for x in t[1:].tolist()]
+    return dt, results or [last], per
 
 
 def throughput(units_per_step: float, world: int, steps: int, dt: float) -> float:
@@ -169,7 +177,11 @@ def main():
         cloud = orchard.generate(cfg, seed=cfg.seed + rank)
     d_cloud = torch.from_numpy(cloud).to(dev)
     n = cloud.shape[0]
-    h_cloud = cloud if a.host_io else None   # --host-io: PCIe-inclusive variant (not the contract's value)
+    # the frame starts from the PointCloud2 bytes in host memory (a ROS message) and ends
+    # with the OccupancyGrids in host memory. Stream / tiled modes start from their own HBM-resident maps.
+    host_io = not (a.device_io or a.stream or a.tiled)
+    mode = {"host": host_io}
+    h_cloud = cloud if host_io else None
     del cloud
     if a.stream:
         # the map so far (the C2 cloud) is already device-resident; each step appends the next scan
@@ -220,7 +232,7 @@ def main():
             if not g["root"]:
                 return g, {"ms": {}, "nodes": (), "edges": ()}
         else:
-            if a.host_io:   # PointCloud2 bytes from host memory in, both OccupancyGrids to host out
+            if mode["host"]:   # PointCloud2 bytes from host memory in, both OccupancyGrids to host out
                 g = ctx.seedgen(h_cloud, want_host=True)
             else:
                 g = ctx.seedgen(d_cloud.data_ptr(), n_points=n, on_device=True, want_host=False)
@@ -250,8 +262,18 @@ def main():
         gg["ms"]["cells"] = pend["ms"]   # the previous frame's (the last step: its own)
         return g, gg
 
-    dt, res = timed_region(step, a.steps, a.warmup, world, torch.cuda.synchronize, dist, red_dev)
+    dt, res, per = timed_region(step, a.steps, a.warmup, world, torch.cuda.synchronize, dist, red_dev)
     g, gg = res[-1]
+    dev_rate = None
+    if host_io and not a.no_device_rate and not pipeline:
+        # the same frame with the cloud already in HBM and the grids left there (no PCIe)
+        mode["host"] = False
+        pend["k"], n_calls = 0, 2 + a.steps
+        ddt, _, dper = timed_region(step, a.steps, 2, world, torch.cuda.synchronize, dist, red_dev)
+        dmed = sorted(dper)[len(dper) // 2]
+        dev_rate = {"value": round((g["width"] * g["height"] / 1e6) * world / dmed, 3), "median_ms": round(dmed * 1e3, 3),
+                    "ms_per_step": round(ddt / a.steps * 1e3, 3),
+                    "io": "cloud already in HBM, OccupancyGrids left in HBM, GvdGraph + seeds to host"}
     stage = {}
     n_gvd = sum(1 for _, ggs in res if ggs is not None)
     for gs, ggs in res:
@@ -260,43 +282,48 @@ def main():
         for k, v in (ggs["ms"].items() if ggs is not None else ()):
             stage["gvd_" + k] = stage.get("gvd_" + k, 0.0) + v / n_gvd
     cells = g["width"] * g["height"]
-    # weak: every rank processes its own map; tiled: the ranks share one map (strong scaling)
-    value = throughput(cells / 1e6, 1 if a.tiled else world, len(res), dt)
+    # weak: every rank processes its own map; tiled: the ranks share one map (strong scaling).
+    # value = cells / median frame time (median of the warm frames), the contract's
+    # timed-region mean beside it (value_mean).
+    med = sorted(per)[len(per) // 2]
+    value = (cells / 1e6) * (1 if a.tiled else world) / med
+    value_mean = throughput(cells / 1e6, 1 if a.tiled else world, len(res), dt)
     avg = stage
 
-    # roofline of the dominant GPU kernel: the largest per-frame device time among the three ROR
-    # kernels (bin, scatter, neighbour count), timed live with HIP events recorded on the handle's
-    # stream around each single launch (aos_seedgen_out.ms_ror_*), averaged over the timed steps.
-    # Algorithmic bytes per launch, N = input points, Nb = binned (staged) points:
-    #   k_ror_bin     16 N (cloud record) + 8 N (bin/slot pair) + 8 Nb (bin counter read-modify-write)
-    #   k_ror_scatter 8 N (bin/slot pair) + 16 Nb (cloud record) + 4 Nb (bin start) + 16 Nb (staged write)
-    #   k_ror_direct  16 Nb (staged point, read once) + 1 B per kept candidate (raster byte)
-    nb_pts = float(g["n_binned"])
+    # Roofline (SURVEY §8d algorithmic bytes, HBM-bound; no MFMA). Per frame B_alg = 12 N + C (6 + 4 T):
+    # 12 B per input point to read the cloud once and C for the raster write (the ROR stage), 2 C
+    # inflation, 2 C opening, 4 C T thinning, C labelling. The ROR stage (a1-a4) is the dominant GPU
+    # stage and is reported as `roofline`: its §8d bytes 12 N + C over the device time of its four
+    # launches (count, tile scan, scatter, per-tile neighbour count), timed live with HIP events on the
+    # handle's stream (aos_seedgen_out.ms_ror_*), averaged over the timed frames. `kernels` gives each
+    # launch's time and the count pass's own figure (it is the one launch that reads the cloud: 12 N).
     n_all = float(cfg.n_points if a.tiled else n)
-    kept = 0.0 if a.tiled else float(g["n_clipped"])   # (tiled: rank 0's share is not reported)
-    kernels = {
-        "k_ror_bin": (24.0 * n_all + 8.0 * nb_pts, avg["seedgen_ror_bin"], n_all),
-        "k_ror_scatter": (8.0 * n_all + 36.0 * nb_pts, avg["seedgen_ror_scatter"], n_all),
-        "k_ror_direct": (16.0 * nb_pts + kept, avg["seedgen_ror_count"], nb_pts),
-    }
-    per_kernel = {}
-    for k, (alg_b, ms_k, units) in kernels.items():
-        ach = alg_b / (ms_k * 1e-3) / 1e9 if ms_k > 0 else 0.0
-        per_kernel[k] = {"ms_per_launch": round(ms_k, 4), "alg_bytes_per_launch": alg_b, "achieved_GBs": round(ach, 1),
-                         "frac": round(ach / HBM_PEAK_GBS, 4), "units_per_launch": units}
-    dom = max(per_kernel, key=lambda k: per_kernel[k]["ms_per_launch"])
-    traffic, src = pmc_traffic(dom)
-    pk = per_kernel[dom]
-    roof = {"bound": "hbm", "achieved": pk["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": pk["frac"], "traffic": traffic, "kernel": dom, "alg_bytes_per_launch": pk["alg_bytes_per_launch"],
-            "ms_per_launch": pk["ms_per_launch"], "units_per_launch": pk["units_per_launch"], "traffic_source": src,
-            "ror_kernels": per_kernel}
-    # BASELINE.md frame-level figure: B_alg = 12 N + C (6 + 4 T) over the whole frame wall-clock
     T = g["thin_iters"]
-    b_frame = 12.0 * (cfg.n_points if a.tiled else n) + cells * (6.0 + 4.0 * T)
-    frame_roof = {"alg_bytes": b_frame, "achieved_GBs": round(b_frame / (dt / len(res)) / 1e9, 2),
-                  "frac": round(b_frame / (dt / len(res)) / 1e9 / HBM_PEAK_GBS, 5),
-                  "note": "whole frame incl. the host Subdiv2D replay (DESIGN.md)"}
+    t_cnt, t_scat, t_ror = avg["seedgen_ror_bin"], avg["seedgen_ror_scatter"], avg["seedgen_ror_count"]
+    t_stage = avg.get("seedgen_ror_kernels", t_cnt + t_scat + t_ror)
+    b_ror = 12.0 * n_all + cells
+    ach = b_ror / (t_stage * 1e-3) / 1e9 if t_stage > 0 else 0.0
+    traffic, src = pmc_traffic("ror_stage")
+    kern = {"k_rt_part<count>": {"ms": round(t_cnt, 4), "alg_bytes": 12.0 * n_all,
+                                  "achieved_GBs": round(12.0 * n_all / (t_cnt * 1e-3) / 1e9, 1) if t_cnt > 0 else 0.0},
+            "k_rt_part<scatter>": {"ms": round(t_scat, 4)}, "k_rt_ror": {"ms": round(t_ror, 4)}}
+    kern["k_rt_part<count>"]["frac"] = round(kern["k_rt_part<count>"]["achieved_GBs"] / HBM_PEAK_GBS, 4)
+    roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "kernel": "ROR stage a1-a4 (k_rt_part<count>, tile scan, k_rt_part<scatter>, k_rt_ror)",
+            "alg_bytes_per_launch": b_ror, "alg_bytes_model": "SURVEY §8d: 12 B per input point + 1 B per cell (raster)",
+            "ms_per_launch": round(t_stage, 4), "units_per_launch": n_all, "traffic_source": src, "kernels": kern}
+    # thinning: 4 C T bytes over the thinning stage (opening + temporal blocks, one read-back)
+    b_thin = 4.0 * cells * T
+    t_thin = avg.get("seedgen_thin", 0.0)
+    thin_roof = {"alg_bytes": b_thin, "ms": round(t_thin, 4),
+                 "achieved_GBs": round(b_thin / (t_thin * 1e-3) / 1e9, 1) if t_thin > 0 else 0.0}
+    thin_roof["frac"] = round(thin_roof["achieved_GBs"] / HBM_PEAK_GBS, 4)
+    # BASELINE.md frame-level figure: B_alg = 12 N + C (6 + 4 T) over the whole frame wall-clock
+    b_frame = 12.0 * n_all + cells * (6.0 + 4.0 * T)
+    frame_roof = {"alg_bytes": b_frame, "achieved_GBs": round(b_frame / med / 1e9, 2),
+                  "frac": round(b_frame / med / 1e9 / HBM_PEAK_GBS, 5),
+                  "note": "whole frame (median) incl. PCIe and the host Subdiv2D replay (DESIGN.md)"}
 
     if rank == 0:
         if a.stream:
@@ -313,13 +340,19 @@ def main():
             "metric": "Mcells/s skeleton+GVD (seed-gen + GVD frame) on 4096^2 grid",
             "value": round(value, 3), "unit": "Mcells/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(dt / len(res) * 1e3, 3), "higher_is_better": True,
+            "value_mean": round(value_mean, 3), "median_ms": round(med * 1e3, 3),
             "scaling": "strong" if a.tiled else "weak",
             "vs_baseline": None, "dtype": "f32/f64 (reference float/double arithmetic), u8/bit grids",
-            "data": "synthetic orchard (tools/orchard_gen.c, SplitMix64), device-resident PointCloud2",
+            "data": ("synthetic orchard (tools/orchard_gen.c, SplitMix64; 1 % in-clip outliers, not SURVEY §8d's 10 %, "
+                     "which bridge every row at 0.1 m: DESIGN.md §8), "
+                     + ("PointCloud2 bytes in host memory" if host_io else
+                        "scans from host memory into the HBM-resident map" if a.stream else
+                        "HBM-resident PointCloud2 shards" if a.tiled else "HBM-resident PointCloud2")),
             "config": {"workload": workload, "global_batch": 1 if a.tiled else world,
                        "parallelism": f"tiled{tx}x{ty}" if a.tiled else f"tiles{world}"},
-            "io": "host cloud in + host OccupancyGrids out (PCIe-inclusive)" if a.host_io else
-                  "device-resident cloud, device-resident grids",
+            "io": "host PointCloud2 in, host OccupancyGrids + GvdGraph out (SURVEY §8d)" if host_io else
+                  "device-resident cloud, device-resident grids, host GvdGraph",
+            "device_resident": dev_rate,
             "pipeline": "seed-gen of frame k overlaps the GVD of frame k-1 (the reference's two nodes)"
                         if pipeline else "sequential",
             "stages_ms": {k: round(v, 3) for k, v in avg.items()},
@@ -327,6 +360,7 @@ def main():
                       "nodes": len(gg["nodes"]), "edges": len(gg["edges"]), "n_binned": g["n_binned"],
                       "n_clipped": g["n_clipped"]},
             "roofline": roof,
+            "thin_roofline": thin_roof,
             "frame_roofline": frame_roof,
         }
         if a.stream:

@@ -31,8 +31,8 @@ def _worker(rank, world, port, q):
         time.sleep(0.02 * (rank + 1))   # rank 1 is the slow one
         return rank
 
-    dt, res = bench.timed_region(step, steps=3, warmup=2, world=world, sync=lambda: None, dist=dist, device="cpu")
-    q.put((rank, dt, len(calls), len(res)))
+    dt, res, per = bench.timed_region(step, steps=3, warmup=2, world=world, sync=lambda: None, dist=dist, device="cpu")
+    q.put((rank, dt, len(calls), len(res), per))
     dist.destroy_process_group()
 
 
@@ -47,11 +47,14 @@ def test_timed_region_max_over_ranks_gloo():
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
-    dts = {r: dt for r, dt, _, _ in out}
+    dts = {r: dt for r, dt, _, _, _ in out}
+    pers = {r: per for r, _, _, _, per in out}
     # both ranks report the same (max) time, at least the slow rank's 3 x 40 ms
     assert abs(dts[0] - dts[1]) < 1e-12
     assert dts[0] >= 3 * 0.04
-    for _, _, ncalls, nres in out:
+    # per-step times are max-reduced too (the median frame time is taken over them)
+    assert pers[0] == pers[1] and len(pers[0]) == 3 and min(pers[0]) >= 0.04
+    for _, _, ncalls, nres, _ in out:
         assert ncalls == 5 and nres == 3     # W untimed + exactly K timed steps
 
 

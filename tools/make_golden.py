@@ -10,11 +10,12 @@ Files:
   c0_seedgen.npz / c0_gvd.npz  config C0 (100 k points, 512^2 @ 0.2 m): every output, grids bit-packed
   c1_sha256.json               config C1 (2 M points, 2048^2 @ 0.1 m): SHA-256 of every output array
   c2_sha256.json               config C2 (10 M points, 4096^2 @ 0.1 m, the bench frame), with --c2
+  c3_sha256.json               config C3 (40 M points, 8192^2 @ 0.1 m, the tiled config), with --c3
   subdiv_kat.npz               Subdiv2D micro known-answer cases: co-circular, collinear, duplicate,
                                near-duplicate and on-edge seeds (Voronoi facets per real vertex, both
                                rect modes)
 
-usage: python tools/make_golden.py [--skip-c1] [--c2]
+usage: python tools/make_golden.py [--skip-c1] [--c2] [--c3] [--only-big]
 """
 import argparse
 import hashlib
@@ -76,8 +77,27 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-c1", action="store_true")
     ap.add_argument("--c2", action="store_true", help="also hash config C2 (the bench frame; ~2-3 min of oracle time)")
+    ap.add_argument("--c3", action="store_true", help="also hash config C3 (8192^2, 40 M points; ~30+ min of oracle time)")
+    ap.add_argument("--only-big", action="store_true", help="skip C0 / KAT / C1 and write only the --c2 / --c3 hashes")
     a = ap.parse_args()
     os.makedirs(GOLD, exist_ok=True)
+    if a.only_big:
+        a.skip_c1 = True
+    else:
+        small_fixtures()
+    for name, want in (("C1", not a.skip_c1), ("C2", a.c2), ("C3", a.c3)):
+        if not want:
+            continue
+        s1, g1 = run(name)
+        h = {"meta": {k: s1[k] for k in ("width", "height", "thin_iters", "n_input", "n_ror_kept", "n_clipped")}}
+        h["seedgen"] = {k: sha(s1[k]) for k in GRIDS + SEED_KEYS}
+        h["gvd"] = {k: sha(g1[k]) for k in GVD_KEYS}
+        json.dump(h, open(os.path.join(GOLD, f"{name.lower()}_sha256.json"), "w"), indent=1, sort_keys=True)
+        print(name, "hashed", flush=True)
+    print("golden fixtures written to", GOLD)
+
+
+def small_fixtures():
     s, g = run("C0")
     meta = {k: s[k] for k in ("width", "height", "thin_iters", "n_input", "n_ror_kept", "n_clipped")}
     np.savez_compressed(os.path.join(GOLD, "c0_seedgen.npz"), origin=np.array(s["origin"]),
@@ -96,15 +116,6 @@ def main():
             kat[f"{name}_m{mode}_facet_pts"] = (np.concatenate(facets) if facets else np.zeros((0, 2))).astype(np.float32)
             kat[f"{name}_m{mode}_centers"] = np.asarray(centers, dtype=np.float32)
     np.savez_compressed(os.path.join(GOLD, "subdiv_kat.npz"), **kat)
-    for name, want in (("C1", not a.skip_c1), ("C2", a.c2)):
-        if not want:
-            continue
-        s1, g1 = run(name)
-        h = {"meta": {k: s1[k] for k in ("width", "height", "thin_iters", "n_input", "n_ror_kept", "n_clipped")}}
-        h["seedgen"] = {k: sha(s1[k]) for k in GRIDS + SEED_KEYS}
-        h["gvd"] = {k: sha(g1[k]) for k in GVD_KEYS}
-        json.dump(h, open(os.path.join(GOLD, f"{name.lower()}_sha256.json"), "w"), indent=1, sort_keys=True)
-    print("golden fixtures written to", GOLD)
 
 
 if __name__ == "__main__":
