@@ -55,6 +55,7 @@ struct aos_ctx {
     bool tiled_frame = false;
     int thin_iters = 0;
     uint64_t n_ror_kept = 0, n_clipped = 0;
+    double ror_est_binned = 0;             // binned points of the last frame (sizes the ROR tiles)
 
     // ---- cluster / row / seed stage (cluster_seed.hip)
     aos::ClusterSeedState cs;

@@ -103,13 +103,15 @@ struct RorLaunch {
     int rx0, ry0, rx1, ry1, wx0, wy0, Wr;
     // tile walk (ror.hip): TB x TB bins per tile, ntx x nty tiles; the raster window as bits (Hr rows
     // of WWr words, wx0 a multiple of 64); a tile's LDS raster window (win_rows x win_w words, 0: none)
-    int TB, ntx, nty, ntiles, max_touch, Hr, WWr, win_rows, win_w;
+    int TB, ntx, nty, ntiles, Hr, WWr, win_rows, win_w;
 };
-constexpr int kRtMaxTiles = 20000;   // tiles per frame (LDS histogram of the partition passes)
-void rt_configure(RorLaunch &L, int Hr, int WWr);
-void launch_rt_count(const RorLaunch &L, int *tile_count, unsigned long long *n_own, int n_blocks, hipStream_t s);
-void launch_rt_scatter(const RorLaunch &L, int *tile_cursor, float4 *staged, int n_blocks, hipStream_t s);
-void launch_rt_ror(const RorLaunch &L, const int *tile_start, const float4 *staged, float4 *scratch, uint64_t *rbits,
+constexpr int kRtMaxTiles = 36000;   // tiles per frame (LDS histogram of the partition passes: 144 KB)
+void rt_configure(RorLaunch &L, int Hr, int WWr, double est_binned);
+int rt_part_blocks(const RorLaunch &L);   // G: workgroups (= cloud chunks) of the partition passes
+// H: ntiles x G + 1 ints (tile-major); after the count pass and an exclusive scan, O = H offsets
+void launch_rt_count(const RorLaunch &L, int *H, int G, unsigned long long *n_own, hipStream_t s);
+void launch_rt_scatter(const RorLaunch &L, int *O, int G, float4 *staged, hipStream_t s);
+void launch_rt_ror(const RorLaunch &L, const int *O, int G, const float4 *staged, float4 *scratch, uint64_t *rbits,
                    unsigned long long *counters, hipStream_t s);
 // PointCloud2 records (any float32 x/y/z offsets) -> float4 (x, y, z, 0)
 void launch_pack_xyz(const uint8_t *cloud, uint64_t n, uint32_t step, uint32_t ox, uint32_t oy, uint32_t oz, float4 *out,

@@ -40,7 +40,6 @@ __constant__ float c_excl_rt[11 * 3] = {0.646417f, 3.83918f, 1.0f,  2.0405f, 3.6
                                         -2.11365f, 3.74464f, 1.0f, -2.26381f, 2.70848f, 1.0f, -2.66426f, 1.72738f, 1.0f,
                                         68.0229f, 2.31687f, 1.0f,  65.4647f, 2.18653f, 1.0f};
 
-static inline int cdiv_i(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 __device__ __forceinline__ void rt_load(const RorLaunch &L, uint64_t i, float &x, float &y, float &z) {
     const uint8_t *rec = L.cloud + i * (uint64_t)L.step;
@@ -88,9 +87,13 @@ __device__ __forceinline__ bool rt_in(const RorLaunch &L, float4 p, float4 q) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Passes 1 and 3: count / scatter. One sub-chunk = kRtSub consecutive points (kRtPer per thread,
-// strided by the block size so every load instruction is coalesced).
-constexpr int kRtTB = 256, kRtPer = 8, kRtSub = kRtTB * kRtPer, kRtMaxPairs = 4 * kRtSub;
+// Passes 1 and 3: count / scatter, a radix-sort style partition with one digit per tile. Workgroup
+// w owns one contiguous chunk of the cloud. The count pass accumulates an LDS histogram over the
+// chunk and stores it as column w of H (tile-major, H[t * G + w]); one exclusive scan of H gives
+// every (tile, workgroup) run its offset; the scatter pass walks the same chunk again with LDS
+// cursors starting at those offsets. No global atomics; a tile's run from workgroup w sits right
+// after workgroup w - 1's.
+constexpr int kRtTB = 256, kRtPer = 8, kRtSub = kRtTB * kRtPer;
 
 // tiles whose bins a point's 3 x 3 bins touch: [tx0, tx1] x [ty0, ty1], own tile (bx / TB, by / TB)
 __device__ __forceinline__ void rt_tiles(const RorLaunch &L, int bx, int by, int &tx0, int &tx1, int &ty0, int &ty1) {
@@ -99,31 +102,26 @@ __device__ __forceinline__ void rt_tiles(const RorLaunch &L, int bx, int by, int
 }
 
 template <bool SCATTER>
-__global__ __launch_bounds__(kRtTB) void k_rt_part(RorLaunch L, int *tile_count, int *tile_cursor, float4 *staged,
+__global__ __launch_bounds__(kRtTB) void k_rt_part(RorLaunch L, int *H, uint64_t chunk, float4 *staged,
                                                    unsigned long long *n_own) {
-    extern __shared__ int sh[];
-    int *hist = sh;                      // [ntiles]: count, then (scatter) the run's base
-    int *touched = sh + L.ntiles;        // tiles touched in this sub-chunk
-    int *ntouch = touched + L.max_touch;
-    const int tid = threadIdx.x;
-    for (int i = tid; i < L.ntiles; i += kRtTB) hist[i] = 0;
-    if (tid == 0) *ntouch = 0;
+    extern __shared__ int hist[];        // [ntiles]: counts (count pass) / cursors (scatter pass)
+    const int tid = threadIdx.x, G = gridDim.x, w = blockIdx.x;
+    for (int t = tid; t < L.ntiles; t += kRtTB) hist[t] = SCATTER ? H[(size_t)t * G + w] : 0;
     __syncthreads();
     unsigned own = 0;
-    for (uint64_t base = (uint64_t)blockIdx.x * kRtSub; base < L.n; base += (uint64_t)gridDim.x * kRtSub) {
+    const uint64_t begin = (uint64_t)w * chunk, end = min(L.n, begin + chunk);
+    for (uint64_t base = begin; base < end; base += kRtSub) {
         float4 pt[kRtPer];
-        int slot[kRtPer][4];   // (tile << 13 | rank) per copy, -1 unused
         // all loads first (kRtPer independent 16 B loads in flight per lane), then the LDS walk
 #pragma unroll
         for (int j = 0; j < kRtPer; ++j) {
             const uint64_t i = base + (uint64_t)j * kRtTB + tid;
             pt[j] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
-            if (i < L.n) rt_load(L, i, pt[j].x, pt[j].y, pt[j].z);
-            if (i < L.n) pt[j].w = 0.f;
+            if (i < end) rt_load(L, i, pt[j].x, pt[j].y, pt[j].z);
+            if (i < end) pt[j].w = 0.f;
         }
 #pragma unroll
         for (int j = 0; j < kRtPer; ++j) {
-            slot[j][0] = slot[j][1] = slot[j][2] = slot[j][3] = -1;
             const float x = pt[j].x, y = pt[j].y, z = pt[j].z;
             if (__float_as_int(pt[j].w) < 0 || !rt_binned(L, x, y, z)) continue;
             ++own;
@@ -131,44 +129,23 @@ __global__ __launch_bounds__(kRtTB) void k_rt_part(RorLaunch L, int *tile_count,
             rt_bin(L, x, y, bx, by);
             rt_tiles(L, bx, by, tx0, tx1, ty0, ty1);
             const int otile = (by / L.TB) * L.ntx + bx / L.TB;
-            if (SCATTER) pt[j].w = __int_as_float(rt_candidate(L, x, y, z) ? 1 : 0);
-            int c = 0;
+            const float4 q = make_float4(x, y, z, __int_as_float(SCATTER && rt_candidate(L, x, y, z) ? 1 : 0));
             for (int ty = ty0; ty <= ty1; ++ty)
                 for (int tx = tx0; tx <= tx1; ++tx) {
                     const int t = ty * L.ntx + tx;
-                    const int r = atomicAdd(&hist[t], 1);
-                    if (r == 0) touched[atomicAdd(ntouch, 1)] = t;
-                    if (SCATTER) slot[j][c] = (t == otile ? 0 : 1 << 30) | (t << 13) | r;   // bit 30: halo copy
-                    ++c;
+                    if (SCATTER) {
+                        float4 v = q;
+                        if (t != otile) v.w = __int_as_float(0);   // a halo copy is never tested there
+                        staged[atomicAdd(&hist[t], 1)] = v;
+                    } else {
+                        atomicAdd(&hist[t], 1);
+                    }
                 }
         }
-        __syncthreads();
-        const int nt = *ntouch;
-        for (int k = tid; k < nt; k += kRtTB) {
-            const int t = touched[k];
-            if (SCATTER) hist[t] = atomicAdd(&tile_cursor[t], hist[t]);
-            else { atomicAdd(&tile_count[t], hist[t]); hist[t] = 0; }
-        }
-        __syncthreads();
-        if (SCATTER) {
-#pragma unroll
-            for (int j = 0; j < kRtPer; ++j)
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const int s = slot[j][c];
-                    if (s < 0) continue;
-                    const int t = (s >> 13) & ((1 << 17) - 1), r = s & 8191;
-                    float4 q = pt[j];
-                    if (s & (1 << 30)) q.w = __int_as_float(0);   // a halo copy is never tested here
-                    staged[hist[t] + r] = q;
-                }
-            __syncthreads();
-            for (int k = tid; k < nt; k += kRtTB) hist[touched[k]] = 0;
-        }
-        if (tid == 0) *ntouch = 0;
-        __syncthreads();
     }
     if (!SCATTER) {
+        __syncthreads();
+        for (int t = tid; t < L.ntiles; t += kRtTB) H[(size_t)t * G + w] = hist[t];
         for (int o = 32; o > 0; o >>= 1) own += __shfl_xor(own, o);
         if ((tid & 63) == 0 && own) atomicAdd(n_own, (unsigned long long)own);
     }
@@ -176,7 +153,7 @@ __global__ __launch_bounds__(kRtTB) void k_rt_part(RorLaunch L, int *tile_count,
 
 // ---------------------------------------------------------------------------------------------
 // Pass 4: per tile, counting sort by bin in LDS, neighbour counts, raster bitmap.
-constexpr int kRorThreads = 1024, kRorCap = 4096, kRorPer = kRorCap / kRorThreads;
+constexpr int kRorThreads = 256, kRorCap = 2048, kRorPer = kRorCap / kRorThreads;
 
 // XCD-aware block order (cdna_hip_programming.md §5.5): consecutive blocks b = j (mod 8) run on XCD j.
 __device__ __forceinline__ int rt_xcd_block(int b, int n) {
@@ -196,11 +173,11 @@ __device__ __forceinline__ int rt_scan(const RorLaunch &L, float4 p, Pts pts, in
     return cnt;
 }
 
-// LDS of k_rt_ror: kRorCap staged points (64 KB), the bin offsets of the largest tile (TB = 64 bins
-// + ring: 66^2), and the tile's raster window (kRtWinWords 64-bit words)
+// LDS of k_rt_ror: kRorCap staged points (32 KB), the bin offsets of the largest tile (TB = 64 bins
+// + ring: 66^2), and the tile's raster window (kRtWinWords 64-bit words): ~53 KB, 3 workgroups per CU
 constexpr int kRtMaxLocalBins = 66 * 66, kRtWinWords = 512;
 
-__global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *tile_start, const float4 *staged,
+__global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *O, int G, const float4 *staged,
                                                         float4 *scratch, uint64_t *rbits,
                                                         unsigned long long *counters) {
     __shared__ float4 pts[kRorCap];
@@ -209,7 +186,7 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
     const int tid = threadIdx.x;
     const int t = rt_xcd_block(blockIdx.x, gridDim.x);
     const int tx = t % L.ntx, ty = t / L.ntx;
-    const int a = tile_start[t], n = tile_start[t + 1] - a;
+    const int a = O[(size_t)t * G], n = O[(size_t)(t + 1) * G] - a;   // the tile's runs, scanned
     if (n == 0) return;
     const int LB = L.TB + 2;                        // local bins: the tile's bins and a ring of halo bins
     const int bx0 = tx * L.TB - 1, by0 = ty * L.TB - 1;
@@ -332,17 +309,24 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
 }
 
 // ---------------------------------------------------------------------------------------------
-void rt_configure(RorLaunch &L, int Hr, int WWr) {
-    L.TB = 32;
-    for (;;) {
-        L.ntx = (L.nbx + L.TB - 1) / L.TB;
-        L.nty = (L.nby + L.TB - 1) / L.TB;
-        if ((long long)L.ntx * L.nty <= kRtMaxTiles || L.TB >= 1024) break;
-        L.TB *= 2;
+// est_binned: expected binned points (the previous frame's count, or a guess); it only sizes the
+// tiles (TB = 32 bins, or 16 where tiles would average more than ~1400 points) — results do not
+// depend on it.
+void rt_configure(RorLaunch &L, int Hr, int WWr, double est_binned) {
+    auto tiles = [&](int tb) {
+        L.TB = tb;
+        L.ntx = (L.nbx + tb - 1) / tb;
+        L.nty = (L.nby + tb - 1) / tb;
+        return (long long)L.ntx * L.nty;
+    };
+    const double per32 = est_binned * 1.15 / (double)tiles(32);
+    if (!(per32 > 1400.0 && tiles(16) <= kRtMaxTiles)) {
+        int tb = 32;
+        while (tiles(tb) > kRtMaxTiles && tb < 64) tb *= 2;
     }
-    if ((L.TB + 2) * (L.TB + 2) > kRtMaxLocalBins) throw std::runtime_error("ROR bin grid too large for the tile walk");
+    if (tiles(L.TB) > kRtMaxTiles || (L.TB + 2) * (L.TB + 2) > kRtMaxLocalBins)
+        throw std::runtime_error("ROR bin grid too large for the tile walk");
     L.ntiles = L.ntx * L.nty;
-    L.max_touch = std::min(L.ntiles, kRtMaxPairs);
     L.Hr = Hr; L.WWr = WWr;
     // raster window of one tile: its cells (TB bins of 1/inv_cs) + 2 cells of slack on each side
     const double span = (double)L.TB / (double)L.inv_cs / (double)L.res;
@@ -352,33 +336,44 @@ void rt_configure(RorLaunch &L, int Hr, int WWr) {
     if (L.win_rows * L.win_w > kRtWinWords) L.win_rows = 0;   // windows too large: OR straight into HBM
 }
 
-size_t rt_part_lds(const RorLaunch &L) { return sizeof(int) * ((size_t)L.ntiles + L.max_touch + 1); }
+int rt_part_blocks(const RorLaunch &L) {
+    // one contiguous chunk per workgroup; H has ntiles x G ints
+    long long g = 512;
+    while (g > 64 && (long long)L.ntiles * g > (16ll << 20)) g /= 2;
+    return (int)std::max<long long>(1, std::min<long long>(g, ((long long)L.n + kRtSub - 1) / kRtSub));
+}
+uint64_t rt_chunk(const RorLaunch &L, int G) {
+    const uint64_t c = (L.n + G - 1) / G;
+    return (c + kRtSub - 1) / kRtSub * kRtSub;
+}
 
-void launch_rt_count(const RorLaunch &L, int *tile_count, unsigned long long *n_own, int n_blocks, hipStream_t s) {
-    if (!L.n) return;
-    const size_t lds = rt_part_lds(L);
+static void rt_lds_attr(const RorLaunch &L) {
+    const size_t lds = sizeof(int) * (size_t)L.ntiles;
     if (lds > 64 * 1024) {   // the tile histogram exceeds the default dynamic-LDS limit (gfx950: 160 KB)
         AOS_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rt_part<false>),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         AOS_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rt_part<true>),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     }
-    const int nb = std::max(1, std::min(n_blocks, cdiv_i((long long)L.n, kRtSub)));
-    k_rt_part<false><<<nb, kRtTB, lds, s>>>(L, tile_count, nullptr, nullptr, n_own);
-    AOS_HIP(hipGetLastError());
 }
 
-void launch_rt_scatter(const RorLaunch &L, int *tile_cursor, float4 *staged, int n_blocks, hipStream_t s) {
+void launch_rt_count(const RorLaunch &L, int *H, int G, unsigned long long *n_own, hipStream_t s) {
     if (!L.n) return;
-    const int nb = std::max(1, std::min(n_blocks, cdiv_i((long long)L.n, kRtSub)));
-    k_rt_part<true><<<nb, kRtTB, rt_part_lds(L), s>>>(L, nullptr, tile_cursor, staged, nullptr);
+    rt_lds_attr(L);
+    k_rt_part<false><<<G, kRtTB, sizeof(int) * (size_t)L.ntiles, s>>>(L, H, rt_chunk(L, G), nullptr, n_own);
     AOS_HIP(hipGetLastError());
 }
 
-void launch_rt_ror(const RorLaunch &L, const int *tile_start, const float4 *staged, float4 *scratch, uint64_t *rbits,
+void launch_rt_scatter(const RorLaunch &L, int *O, int G, float4 *staged, hipStream_t s) {
+    if (!L.n) return;
+    k_rt_part<true><<<G, kRtTB, sizeof(int) * (size_t)L.ntiles, s>>>(L, O, rt_chunk(L, G), staged, nullptr);
+    AOS_HIP(hipGetLastError());
+}
+
+void launch_rt_ror(const RorLaunch &L, const int *O, int G, const float4 *staged, float4 *scratch, uint64_t *rbits,
                    unsigned long long *counters, hipStream_t s) {
     if (!L.n || !L.ntiles) return;
-    k_rt_ror<<<L.ntiles, kRorThreads, 0, s>>>(L, tile_start, staged, scratch, rbits, counters);
+    k_rt_ror<<<L.ntiles, kRorThreads, 0, s>>>(L, O, G, staged, scratch, rbits, counters);
     AOS_HIP(hipGetLastError());
 }
 

@@ -231,17 +231,18 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits) {
     L.origin_x = g.origin_x; L.origin_y = g.origin_y; L.res = g.res; L.W = g.W; L.H = g.H;
     L.rx0 = o.rx0; L.ry0 = o.ry0; L.rx1 = o.rx1; L.ry1 = o.ry1; L.wx0 = o.wx0; L.wy0 = o.wy0; L.Wr = o.Wr;
     const int WWr = (o.Wr + 63) / 64;
-    rt_configure(L, o.Hr, WWr);
+    rt_configure(L, o.Hr, WWr, ror_est_binned > 0 ? ror_est_binned : 0.5 * (double)n_points);
     const int nt = L.ntiles;
+    const int G = rt_part_blocks(L);
+    const size_t nH = (size_t)nt * G + 1;
 
-    int *d_tc = static_cast<int *>(bin_count.ensure(sizeof(int) * (nt + 1)));
-    int *d_ts = static_cast<int *>(bin_start.ensure(sizeof(int) * (nt + 1)));
-    int *d_cur = static_cast<int *>(pt_binslot.ensure(sizeof(int) * (nt + 1)));
+    int *d_H = static_cast<int *>(bin_count.ensure(sizeof(int) * nH));
+    int *d_O = static_cast<int *>(bin_start.ensure(sizeof(int) * nH));
     unsigned long long *d_cnt = static_cast<unsigned long long *>(counters.ensure(8 * kRorCounters + 8));
     unsigned long long *d_own = d_cnt + kRorCounters;
-    size_t st = scan_temp_bytes(nt + 1);
+    size_t st = scan_temp_bytes((int)nH);
     void *d_st = scan_tmp.ensure(st);
-    AOS_HIP(hipMemsetAsync(d_tc, 0, sizeof(int) * (nt + 1), s));
+    AOS_HIP(hipMemsetAsync(d_H + nH - 1, 0, sizeof(int), s));
     AOS_HIP(hipMemsetAsync(d_cnt, 0, 8 * kRorCounters + 8, s));
     AOS_HIP(hipMemsetAsync(rbits, 0, sizeof(uint64_t) * (size_t)o.Hr * WWr, s));
     // PCL dense kNN needs k = min_pts + 1 points in the whole cloud (else every point is removed).
@@ -249,25 +250,26 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits) {
     // no keepable candidate either: the local test is exact.
     const bool any = n_points > 0 && !(is_dense && n_points < (uint64_t)L.need);
     if (!any) return;
-    const int nblk = 1024;   // 4 workgroups (34 KB LDS each at C2) per CU
     AOS_HIP(hipEventRecord(ev[12], s));
-    launch_rt_count(L, d_tc, d_own, nblk, s);
+    launch_rt_count(L, d_H, G, d_own, s);
     AOS_HIP(hipEventRecord(ev[13], s));
-    launch_exclusive_scan(d_tc, d_ts, nt + 1, d_st, st, s);
+    launch_exclusive_scan(d_H, d_O, (int)nH, d_st, st, s);
     // the staged array holds own + halo copies: size it from the count (one small read-back)
     int *h = static_cast<int *>(h_stats.p);
-    AOS_HIP(hipMemcpyAsync(h + 2, d_ts + nt, sizeof(int), hipMemcpyDeviceToHost, s));
+    AOS_HIP(hipMemcpyAsync(h + 2, d_O + nH - 1, sizeof(int), hipMemcpyDeviceToHost, s));
     AOS_HIP(hipMemcpyAsync(h + 4, d_own, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
-    AOS_HIP(hipMemcpyAsync(d_cur, d_ts, sizeof(int) * (nt + 1), hipMemcpyDeviceToDevice, s));
     AOS_HIP(hipStreamSynchronize(s));
     const size_t n_staged = (size_t)std::max(h[2], 1);
     h[0] = (int)*reinterpret_cast<unsigned long long *>(h + 4);
+    ror_est_binned = (double)h[0];
     float4 *d_staged = static_cast<float4 *>(sorted.ensure(sizeof(float4) * n_staged));
     float4 *d_scratch = static_cast<float4 *>(ror_scratch.ensure(sizeof(float4) * n_staged));
+    // the scatter pass advances its cursors in a copy: pass 4 reads the offsets
+    AOS_HIP(hipMemcpyAsync(d_H, d_O, sizeof(int) * nH, hipMemcpyDeviceToDevice, s));
     AOS_HIP(hipEventRecord(ev[14], s));
-    launch_rt_scatter(L, d_cur, d_staged, nblk, s);
+    launch_rt_scatter(L, d_H, G, d_staged, s);
     AOS_HIP(hipEventRecord(ev[10], s));
-    launch_rt_ror(L, d_ts, d_staged, d_scratch, rbits, d_cnt, s);
+    launch_rt_ror(L, d_O, G, d_staged, d_scratch, rbits, d_cnt, s);
     AOS_HIP(hipEventRecord(ev[11], s));
 }
 
