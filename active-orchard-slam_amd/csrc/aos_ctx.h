@@ -56,6 +56,7 @@ struct aos_ctx {
     int thin_iters = 0;
     uint64_t n_ror_kept = 0, n_clipped = 0;
     double ror_est_binned = 0;             // binned points of the last frame (sizes the ROR tiles)
+    double ror_staged_max = 0;             // largest staged (own + halo) count seen (sizes the scatter)
 
     // ---- cluster / row / seed stage (cluster_seed.hip)
     aos::ClusterSeedState cs;
@@ -102,9 +103,11 @@ struct aos_ctx {
 
     void set_cloud(const aos_cloud_view &v);
     void map_append(const aos_cloud_view &scan);
-    void ror_stage(const aos::FrameGeom &g, const RorOwn &o, uint64_t *rbits);
+    void ror_stage(const aos::FrameGeom &g, const RorOwn &o, uint64_t *rbits, bool allow_guess);
+    bool ror_collect();   // after the stream synchronised: true if the ROR scatter overflowed
     void finish_frame(const aos::FrameGeom &g, bool want_host, const uint64_t *clipped_total, aos_seedgen_out &out);
     void run_seedgen(bool want_host, aos_seedgen_out &out);
+    bool run_seedgen_once(bool want_host, aos_seedgen_out &out, bool allow_guess);   // true: redo
     void run_tiled(const aos_comm &cm, int tiles_x, int tiles_y, int root, bool want_host, aos_seedgen_out &out);
     void tile_halo_exchange(uint64_t *win, const aos::TilePlan &t, const aos_comm &cm);
     void run_gvd_external(const aos_gvd_in &in, aos_gvd_out &out);

@@ -104,6 +104,7 @@ struct RorLaunch {
     // tile walk (ror.hip): TB x TB bins per tile, ntx x nty tiles; the raster window as bits (Hr rows
     // of WWr words, wx0 a multiple of 64); a tile's LDS raster window (win_rows x win_w words, 0: none)
     int TB, ntx, nty, ntiles, Hr, WWr, win_rows, win_w;
+    int staged_cap; int *overflow;   // staged array capacity; set to 1 when the scatter exceeds it
 };
 constexpr int kRtMaxTiles = 36000;   // tiles per frame (LDS histogram of the partition passes: 144 KB)
 void rt_configure(RorLaunch &L, int Hr, int WWr, double est_binned);

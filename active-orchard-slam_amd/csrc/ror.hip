@@ -25,6 +25,8 @@
 // largest float whose double is <= r^2); non-dense: radius search d2 < float(r^2). The point itself
 // has d2 = 0 and is counted by the same test (not counted when r = 0 on a non-dense cloud, as FLANN's
 // strict test does). Cells: generateOccupancyGrid's (int)(((double)x - origin) / (double)res).
+#include <hipcub/hipcub.hpp>
+
 #include <algorithm>
 #include <climits>
 #include <cmath>
@@ -41,9 +43,11 @@ __constant__ float c_excl_rt[11 * 3] = {0.646417f, 3.83918f, 1.0f,  2.0405f, 3.6
                                         68.0229f, 2.31687f, 1.0f,  65.4647f, 2.18653f, 1.0f};
 
 
+// STD: the common PointCloud2 layout (point_step 16, x/y/z at 0/4/8): one 16 B load per point
+template <bool STD>
 __device__ __forceinline__ void rt_load(const RorLaunch &L, uint64_t i, float &x, float &y, float &z) {
-    const uint8_t *rec = L.cloud + i * (uint64_t)L.step;
-    if (L.step == 16 && L.ox == 0 && L.oy == 4 && L.oz == 8) {
+    const uint8_t *rec = L.cloud + i * (uint64_t)(STD ? 16 : L.step);
+    if (STD) {
         const float4 v = *reinterpret_cast<const float4 *>(rec);
         x = v.x; y = v.y; z = v.z;
     } else {
@@ -93,7 +97,10 @@ __device__ __forceinline__ bool rt_in(const RorLaunch &L, float4 p, float4 q) {
 // every (tile, workgroup) run its offset; the scatter pass walks the same chunk again with LDS
 // cursors starting at those offsets. No global atomics; a tile's run from workgroup w sits right
 // after workgroup w - 1's.
-constexpr int kRtTB = 256, kRtPer = 8, kRtSub = kRtTB * kRtPer;
+#ifndef AOS_RT_PART_TB
+#define AOS_RT_PART_TB 256
+#endif
+constexpr int kRtTB = AOS_RT_PART_TB, kRtPer = 8, kRtSub = kRtTB * kRtPer;
 
 // tiles whose bins a point's 3 x 3 bins touch: [tx0, tx1] x [ty0, ty1], own tile (bx / TB, by / TB)
 __device__ __forceinline__ void rt_tiles(const RorLaunch &L, int bx, int by, int &tx0, int &tx1, int &ty0, int &ty1) {
@@ -101,7 +108,7 @@ __device__ __forceinline__ void rt_tiles(const RorLaunch &L, int bx, int by, int
     ty0 = max(by - 1, 0) / L.TB; ty1 = min(by + 1, L.nby - 1) / L.TB;
 }
 
-template <bool SCATTER>
+template <bool SCATTER, bool STD>
 __global__ __launch_bounds__(kRtTB) void k_rt_part(RorLaunch L, int *H, uint64_t chunk, float4 *staged,
                                                    unsigned long long *n_own) {
     extern __shared__ int hist[];        // [ntiles]: counts (count pass) / cursors (scatter pass)
@@ -110,16 +117,25 @@ __global__ __launch_bounds__(kRtTB) void k_rt_part(RorLaunch L, int *H, uint64_t
     __syncthreads();
     unsigned own = 0;
     const uint64_t begin = (uint64_t)w * chunk, end = min(L.n, begin + chunk);
-    for (uint64_t base = begin; base < end; base += kRtSub) {
-        float4 pt[kRtPer];
-        // all loads first (kRtPer independent 16 B loads in flight per lane), then the LDS walk
+    // software pipelined: the next sub-chunk's kRtPer loads are in flight while this one is walked
+    float4 nxt[kRtPer];
+    auto issue = [&](uint64_t base) {
 #pragma unroll
         for (int j = 0; j < kRtPer; ++j) {
             const uint64_t i = base + (uint64_t)j * kRtTB + tid;
-            pt[j] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
-            if (i < end) rt_load(L, i, pt[j].x, pt[j].y, pt[j].z);
-            if (i < end) pt[j].w = 0.f;
+            nxt[j] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+            if (i < end) {
+                rt_load<STD>(L, i, nxt[j].x, nxt[j].y, nxt[j].z);
+                nxt[j].w = 0.f;
+            }
         }
+    };
+    if (begin < end) issue(begin);
+    for (uint64_t base = begin; base < end; base += kRtSub) {
+        float4 pt[kRtPer];
+#pragma unroll
+        for (int j = 0; j < kRtPer; ++j) pt[j] = nxt[j];
+        if (base + kRtSub < end) issue(base + kRtSub);
 #pragma unroll
         for (int j = 0; j < kRtPer; ++j) {
             const float x = pt[j].x, y = pt[j].y, z = pt[j].z;
@@ -136,7 +152,9 @@ __global__ __launch_bounds__(kRtTB) void k_rt_part(RorLaunch L, int *H, uint64_t
                     if (SCATTER) {
                         float4 v = q;
                         if (t != otile) v.w = __int_as_float(0);   // a halo copy is never tested there
-                        staged[atomicAdd(&hist[t], 1)] = v;
+                        const int pos = atomicAdd(&hist[t], 1);
+                        if (pos < L.staged_cap) staged[pos] = v;    // else: overflow, the frame is redone
+                        else *L.overflow = 1;
                     } else {
                         atomicAdd(&hist[t], 1);
                     }
@@ -153,7 +171,13 @@ __global__ __launch_bounds__(kRtTB) void k_rt_part(RorLaunch L, int *H, uint64_t
 
 // ---------------------------------------------------------------------------------------------
 // Pass 4: per tile, counting sort by bin in LDS, neighbour counts, raster bitmap.
-constexpr int kRorThreads = 256, kRorCap = 2048, kRorPer = kRorCap / kRorThreads;
+#ifndef AOS_RT_THREADS
+#define AOS_RT_THREADS 512
+#endif
+constexpr int kRorThreads = AOS_RT_THREADS, kRorCap = 2048, kRorPer = kRorCap / kRorThreads;
+#ifndef AOS_RT_VARIANT   // timing experiments only (tools/ab_rt.sh): 1 = no neighbour scan, 2 = no raster
+#define AOS_RT_VARIANT 0
+#endif
 
 // XCD-aware block order (cdna_hip_programming.md §5.5): consecutive blocks b = j (mod 8) run on XCD j.
 __device__ __forceinline__ int rt_xcd_block(int b, int n) {
@@ -173,9 +197,9 @@ __device__ __forceinline__ int rt_scan(const RorLaunch &L, float4 p, Pts pts, in
     return cnt;
 }
 
-// LDS of k_rt_ror: kRorCap staged points (32 KB), the bin offsets of the largest tile (TB = 64 bins
-// + ring: 66^2), and the tile's raster window (kRtWinWords 64-bit words): ~53 KB, 3 workgroups per CU
-constexpr int kRtMaxLocalBins = 66 * 66, kRtWinWords = 512;
+// LDS of k_rt_ror: kRorCap staged points (32 KB), the bin offsets of the largest tile (TB = 32 bins
+// + ring: 34^2), and the tile's raster window (kRtWinWords 64-bit words): ~40 KB, 3 workgroups per CU
+constexpr int kRtMaxLocalBins = 34 * 34, kRtWinWords = 320;
 
 __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *O, int G, const float4 *staged,
                                                         float4 *scratch, uint64_t *rbits,
@@ -187,7 +211,7 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
     const int t = rt_xcd_block(blockIdx.x, gridDim.x);
     const int tx = t % L.ntx, ty = t / L.ntx;
     const int a = O[(size_t)t * G], n = O[(size_t)(t + 1) * G] - a;   // the tile's runs, scanned
-    if (n == 0) return;
+    if (n == 0 || a + n > L.staged_cap) return;   // (an overflowed scatter: the frame is redone)
     const int LB = L.TB + 2;                        // local bins: the tile's bins and a ring of halo bins
     const int bx0 = tx * L.TB - 1, by0 = ty * L.TB - 1;
     const int nlb = LB * LB;
@@ -224,18 +248,26 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
         for (int k = tid; k < n; k += kRorThreads) atomicAdd(&bstart[lbin(staged[a + k]) + 1], 1);
     }
     __syncthreads();
-    if (tid < 64) {   // inclusive scan of bstart[1..nlb] by one wave (nlb <= kRtMaxLocalBins)
-        int carry = 0;
-        for (int c0 = 1; c0 <= nlb; c0 += 64) {
-            const int i = c0 + tid;
-            int v = i <= nlb ? bstart[i] : 0;
+    {   // exclusive bin offsets: bstart[b] = points in bins < b. Thread t sums a run of kSeg bins,
+        // one block scan over the 256 run totals, then each run is written back.
+        constexpr int kSeg = (kRtMaxLocalBins + kRorThreads - 1) / kRorThreads;
+        typedef hipcub::BlockScan<int, kRorThreads> Scan;
+        __shared__ typename Scan::TempStorage scan_tmp;
+        int v[kSeg], run = 0;
 #pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int u = __shfl_up(v, o);
-                if (tid >= o) v += u;
-            }
-            if (i <= nlb) bstart[i] = v + carry;
-            carry += __shfl(v, 63);
+        for (int j = 0; j < kSeg; ++j) {
+            const int b = tid * kSeg + j + 1;
+            v[j] = b <= nlb ? bstart[b] : 0;
+            run += v[j];
+        }
+        int before;
+        Scan(scan_tmp).ExclusiveSum(run, before);
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kSeg; ++j) {
+            const int b = tid * kSeg + j + 1;
+            before += v[j];
+            if (b <= nlb) bstart[b] = before;
         }
     }
     __syncthreads();
@@ -268,7 +300,7 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
         int bx, by;
         rt_bin(L, p.x, p.y, bx, by);
         const int lx = bx - bx0, ly = by - by0;
-        int cnt = 0;
+        int cnt = AOS_RT_VARIANT == 1 ? L.need : 0;
 #pragma unroll
         for (int rr = 0; rr < 3; ++rr) {        // own bin row first: the likeliest neighbours
             const int yy = ly + (rr == 0 ? 0 : (rr == 1 ? -1 : 1));
@@ -284,7 +316,7 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
         const int cx = min(max(gx, 0), L.W - 1), cy = min(max(gy, 0), L.H - 1);
         if (cx < L.rx0 || cx >= L.rx1 || cy < L.ry0 || cy >= L.ry1) continue;
         ++kept_n;
-        if (gx < 0 || gx >= L.W || gy < 0 || gy >= L.H) continue;
+        if (AOS_RT_VARIANT == 2 || gx < 0 || gx >= L.W || gy < 0 || gy >= L.H) continue;
         const int bxw = gx - L.wx0, r = gy - L.wy0;
         const int wr = r - (cy0 - L.wy0), ww = (bxw >> 6) - cw0;
         const unsigned long long bit = 1ull << (bxw & 63);
@@ -321,8 +353,7 @@ void rt_configure(RorLaunch &L, int Hr, int WWr, double est_binned) {
     };
     const double per32 = est_binned * 1.15 / (double)tiles(32);
     if (!(per32 > 1400.0 && tiles(16) <= kRtMaxTiles)) {
-        int tb = 32;
-        while (tiles(tb) > kRtMaxTiles && tb < 64) tb *= 2;
+        tiles(32);
     }
     if (tiles(L.TB) > kRtMaxTiles || (L.TB + 2) * (L.TB + 2) > kRtMaxLocalBins)
         throw std::runtime_error("ROR bin grid too large for the tile walk");
@@ -338,7 +369,7 @@ void rt_configure(RorLaunch &L, int Hr, int WWr, double est_binned) {
 
 int rt_part_blocks(const RorLaunch &L) {
     // one contiguous chunk per workgroup; H has ntiles x G ints
-    long long g = 512;
+    long long g = 512 * 256 / kRtTB;
     while (g > 64 && (long long)L.ntiles * g > (16ll << 20)) g /= 2;
     return (int)std::max<long long>(1, std::min<long long>(g, ((long long)L.n + kRtSub - 1) / kRtSub));
 }
@@ -347,27 +378,27 @@ uint64_t rt_chunk(const RorLaunch &L, int G) {
     return (c + kRtSub - 1) / kRtSub * kRtSub;
 }
 
-static void rt_lds_attr(const RorLaunch &L) {
+template <bool SCATTER, bool STD>
+static void rt_part(const RorLaunch &L, int *H, int G, float4 *staged, unsigned long long *n_own, hipStream_t s) {
     const size_t lds = sizeof(int) * (size_t)L.ntiles;
-    if (lds > 64 * 1024) {   // the tile histogram exceeds the default dynamic-LDS limit (gfx950: 160 KB)
-        AOS_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rt_part<false>),
+    if (lds > 64 * 1024)   // the tile histogram exceeds the default dynamic-LDS limit (gfx950: 160 KB)
+        AOS_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rt_part<SCATTER, STD>),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        AOS_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rt_part<true>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    }
+    k_rt_part<SCATTER, STD><<<G, kRtTB, lds, s>>>(L, H, rt_chunk(L, G), staged, n_own);
+    AOS_HIP(hipGetLastError());
 }
+static bool rt_std(const RorLaunch &L) { return L.step == 16 && L.ox == 0 && L.oy == 4 && L.oz == 8; }
 
 void launch_rt_count(const RorLaunch &L, int *H, int G, unsigned long long *n_own, hipStream_t s) {
     if (!L.n) return;
-    rt_lds_attr(L);
-    k_rt_part<false><<<G, kRtTB, sizeof(int) * (size_t)L.ntiles, s>>>(L, H, rt_chunk(L, G), nullptr, n_own);
-    AOS_HIP(hipGetLastError());
+    if (rt_std(L)) rt_part<false, true>(L, H, G, nullptr, n_own, s);
+    else rt_part<false, false>(L, H, G, nullptr, n_own, s);
 }
 
 void launch_rt_scatter(const RorLaunch &L, int *O, int G, float4 *staged, hipStream_t s) {
     if (!L.n) return;
-    k_rt_part<true><<<G, kRtTB, sizeof(int) * (size_t)L.ntiles, s>>>(L, O, rt_chunk(L, G), staged, nullptr);
-    AOS_HIP(hipGetLastError());
+    if (rt_std(L)) rt_part<true, true>(L, O, G, staged, nullptr, s);
+    else rt_part<true, false>(L, O, G, staged, nullptr, s);
 }
 
 void launch_rt_ror(const RorLaunch &L, const int *O, int G, const float4 *staged, float4 *scratch, uint64_t *rbits,

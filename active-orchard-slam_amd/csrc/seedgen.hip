@@ -3,6 +3,7 @@
 // every per-point / per-cell stage runs on the GPU. The tiled multi-GPU frame (tiled.hip) reuses
 // ror_stage and finish_frame.
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstring>
 #include <exception>
@@ -203,9 +204,9 @@ int thin_iterations(const int *flags, int iters_run) {
 // straight into the bit-packed window rbits (o.Hr rows of ceil(o.Wr / 64) words, zeroed here), by the
 // tile walk of ror.hip. Records ev[12] / ev[13] / ev[14] / ev[10] / ev[11] around its passes and
 // leaves the number of binned points in h_stats[0].
-void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits) {
+void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bool allow_guess) {
     hipStream_t s = stream;
-    static_cast<int *>(h_stats.ensure(64 + 8 * kRorCounters))[0] = 0;
+    std::memset(h_stats.ensure(64 + 8 * kRorCounters), 0, 32);   // binned, staged, ror_collect's counters
     RorLaunch L{};
     L.cloud = d_cloud; L.n = n_points; L.step = step; L.ox = ox; L.oy = oy; L.oz = oz; L.is_dense = is_dense;
     L.cminx = g.minx; L.cmaxx = g.maxx; L.cminy = g.miny; L.cmaxy = g.maxy;
@@ -238,12 +239,12 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits) {
 
     int *d_H = static_cast<int *>(bin_count.ensure(sizeof(int) * nH));
     int *d_O = static_cast<int *>(bin_start.ensure(sizeof(int) * nH));
-    unsigned long long *d_cnt = static_cast<unsigned long long *>(counters.ensure(8 * kRorCounters + 8));
-    unsigned long long *d_own = d_cnt + kRorCounters;
+    unsigned long long *d_cnt = static_cast<unsigned long long *>(counters.ensure(8 * kRorCounters + 16));
+    unsigned long long *d_own = d_cnt + kRorCounters;   // [0] binned points, [1] overflow flag
     size_t st = scan_temp_bytes((int)nH);
     void *d_st = scan_tmp.ensure(st);
     AOS_HIP(hipMemsetAsync(d_H + nH - 1, 0, sizeof(int), s));
-    AOS_HIP(hipMemsetAsync(d_cnt, 0, 8 * kRorCounters + 8, s));
+    AOS_HIP(hipMemsetAsync(d_cnt, 0, 8 * kRorCounters + 16, s));
     AOS_HIP(hipMemsetAsync(rbits, 0, sizeof(uint64_t) * (size_t)o.Hr * WWr, s));
     // PCL dense kNN needs k = min_pts + 1 points in the whole cloud (else every point is removed).
     // A tile's shard holds every neighbour of its own candidates, so a shard with fewer points has
@@ -254,16 +255,24 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits) {
     launch_rt_count(L, d_H, G, d_own, s);
     AOS_HIP(hipEventRecord(ev[13], s));
     launch_exclusive_scan(d_H, d_O, (int)nH, d_st, st, s);
-    // the staged array holds own + halo copies: size it from the count (one small read-back)
+    // The staged array holds own + halo copies. With a capacity from an earlier frame the scatter
+    // runs at once and reports an overflow (the frame is then redone with the size it read back,
+    // run_seedgen); without one, or when the caller cannot redo (a tiled frame), the size is read
+    // back first.
     int *h = static_cast<int *>(h_stats.p);
-    AOS_HIP(hipMemcpyAsync(h + 2, d_O + nH - 1, sizeof(int), hipMemcpyDeviceToHost, s));
-    AOS_HIP(hipMemcpyAsync(h + 4, d_own, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
-    AOS_HIP(hipStreamSynchronize(s));
-    const size_t n_staged = (size_t)std::max(h[2], 1);
-    h[0] = (int)*reinterpret_cast<unsigned long long *>(h + 4);
-    ror_est_binned = (double)h[0];
-    float4 *d_staged = static_cast<float4 *>(sorted.ensure(sizeof(float4) * n_staged));
-    float4 *d_scratch = static_cast<float4 *>(ror_scratch.ensure(sizeof(float4) * n_staged));
+    const size_t cap_now = sorted.cap / sizeof(float4);
+    const bool guess = allow_guess && ror_staged_max > 0 && cap_now >= (size_t)(ror_staged_max * 1.1);
+    if (!guess) {
+        AOS_HIP(hipMemcpyAsync(h + 2, d_O + nH - 1, sizeof(int), hipMemcpyDeviceToHost, s));
+        AOS_HIP(hipStreamSynchronize(s));
+        const size_t need = (size_t)std::max(h[2], 1);
+        ror_staged_max = std::max<double>(ror_staged_max, (double)need);
+        sorted.ensure(sizeof(float4) * (size_t)(need * 1.15 + 1024));
+    }
+    float4 *d_staged = sorted.as<float4>();
+    L.staged_cap = (int)std::min<size_t>(sorted.cap / sizeof(float4), (size_t)INT_MAX);
+    float4 *d_scratch = static_cast<float4 *>(ror_scratch.ensure(sizeof(float4) * (size_t)L.staged_cap));
+    L.overflow = reinterpret_cast<int *>(d_own + 1);
     // the scatter pass advances its cursors in a copy: pass 4 reads the offsets
     AOS_HIP(hipMemcpyAsync(d_H, d_O, sizeof(int) * nH, hipMemcpyDeviceToDevice, s));
     AOS_HIP(hipEventRecord(ev[14], s));
@@ -271,9 +280,29 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits) {
     AOS_HIP(hipEventRecord(ev[10], s));
     launch_rt_ror(L, d_O, G, d_staged, d_scratch, rbits, d_cnt, s);
     AOS_HIP(hipEventRecord(ev[11], s));
+    // binned points, staged total, overflow flag: read with the frame's other stats (finish_frame)
+    AOS_HIP(hipMemcpyAsync(h + 2, d_O + nH - 1, sizeof(int), hipMemcpyDeviceToHost, s));
+    AOS_HIP(hipMemcpyAsync(h + 4, d_own, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+}
+
+// After the frame's sync: binned count, staged size, and whether the scatter overflowed its guess.
+bool aos_ctx::ror_collect() {
+    int *h = static_cast<int *>(h_stats.p);
+    const unsigned long long *u = reinterpret_cast<const unsigned long long *>(h + 4);
+    h[0] = (int)u[0];
+    ror_est_binned = (double)u[0];
+    ror_staged_max = std::max<double>(ror_staged_max, (double)h[2]);
+    return u[1] != 0;
 }
 
 void aos_ctx::run_seedgen(bool want_host, aos_seedgen_out &out) {
+    // a frame whose ROR scatter outgrew its size guess is redone once with the size it read back
+    for (int attempt = 0; attempt < 2; ++attempt)
+        if (!run_seedgen_once(want_host, out, attempt == 0)) return;
+    throw std::runtime_error("ROR staging overflowed twice");
+}
+
+bool aos_ctx::run_seedgen_once(bool want_host, aos_seedgen_out &out, bool allow_guess) {
     std::memset(&out, 0, sizeof(out));
     tiled_frame = false;
     have_frame = false;
@@ -288,7 +317,7 @@ void aos_ctx::run_seedgen(bool want_host, aos_seedgen_out &out) {
     // ---------------- a1-a4: ROR restricted to the clip box, clip, exclusion discs, raster
     RorOwn own{0, 0, g.W, g.H, 0, 0, g.W, g.H, false, {0, 0, 0, 0}};
     uint64_t *d_rbits = static_cast<uint64_t *>(raster_bits.ensure(Cw * 8));
-    ror_stage(g, own, d_rbits);
+    ror_stage(g, own, d_rbits, allow_guess);
     AOS_HIP(hipEventRecord(ev[1], s));
 
     // ---------------- a5 inflation, a6 frame -> /occupancy_grid
@@ -362,7 +391,9 @@ void aos_ctx::run_seedgen(bool want_host, aos_seedgen_out &out) {
     thin_iters = T;
     skel_bits = final_buf;
     AOS_HIP(hipEventRecord(ev[3], s));
+    if (ror_collect()) return true;   // (the thinning read-back above synchronised the stream)
     finish_frame(g, want_host, nullptr, out);
+    return false;
 }
 
 // a16 + a8-a15 on the whole map from skel_bits / occ_bytes, then the frame outputs. clipped_total:
@@ -453,7 +484,7 @@ void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *c
     auto ms = [&](int a, int b) { float t = 0; (void)hipEventElapsedTime(&t, ev[a], ev[b]); return t; };
     out.ms_ror = ms(0, 1); out.ms_grid = ms(1, 2); out.ms_thin = ms(2, 3); out.ms_cluster = ms(3, 4);
     out.ms_seeds = ms(4, 5); out.ms_total = ms(0, 5);
-    out.n_binned = static_cast<const int *>(h_stats.p)[0];
+    out.n_binned = static_cast<const int *>(h_stats.p)[0];   // (ror_collect)
     out.ms_ror_count = out.n_binned ? ms(10, 11) : 0.0f;
     out.ms_ror_bin = out.n_binned ? ms(12, 13) : 0.0f;
     out.ms_ror_scatter = out.n_binned ? ms(14, 10) : 0.0f;

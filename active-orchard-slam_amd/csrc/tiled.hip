@@ -199,7 +199,7 @@ void aos_ctx::run_tiled(const aos_comm &cm, int tiles_x, int tiles_y, int root, 
     RorOwn own{64 * t.c0, t.y0, std::min(g.W, 64 * t.c1), t.y1, 64 * t.wc0, t.wy0, lg.W, lg.H, true,
                {t.box[0], t.box[1], t.box[2], t.box[3]}};
     uint64_t *d_rbits = static_cast<uint64_t *>(raster_bits.ensure(Cwl * 8));
-    ror_stage(g, own, d_rbits);
+    ror_stage(g, own, d_rbits, false);   // sized by a read-back: a rank cannot redo a frame alone
     AOS_HIP(hipEventRecord(ev[1], s));
 
     // ---- raster halo from the neighbours, a5 inflation on the window
@@ -254,6 +254,7 @@ void aos_ctx::run_tiled(const aos_comm &cm, int tiles_x, int tiles_y, int root, 
     unsigned long long *h_cnt = static_cast<unsigned long long *>(h_stats.ensure(64 + 8 * kRorCounters)) + 8;
     AOS_HIP(hipMemcpyAsync(h_cnt, counters.p, 8 * kRorCounters, hipMemcpyDeviceToHost, s));
     AOS_HIP(hipStreamSynchronize(s));
+    (void)ror_collect();   // sized by a read-back: no overflow
     uint64_t mine_cnt = 0;
     for (int i = 0; i < kRorCounters; ++i) mine_cnt += h_cnt[i];
     std::vector<int32_t> slots(2 * (size_t)cm.world, 0);

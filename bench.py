@@ -135,8 +135,14 @@ def pmc_traffic(kernel: str):
         return None, None
 
 
+def _progress(msg: str) -> None:
+    """Phase markers on stderr (a long silent run looks hung to the GPU harness)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     a = parse()
+    _progress("importing torch")
     import torch  # (import before libaos_gpu: shared HIP runtime, see aos_gpu.lib)
     import torch.distributed as dist
 
@@ -159,6 +165,7 @@ def main():
     red_dev = dev if backend == "nccl" else torch.device("cpu")
 
     cfg = orchard.CONFIGS[a.config]
+    _progress(f"generating {a.config}")
     poly = orchard.polygon(cfg)
     params = aos_gpu.default_params(grid_resolution=cfg.res)
     ctx = aos_gpu.Ctx(params, device=gpu)
@@ -262,6 +269,7 @@ def main():
         gg["ms"]["cells"] = pend["ms"]   # the previous frame's (the last step: its own)
         return g, gg
 
+    _progress(f"{a.warmup} warmup + {a.steps} timed frames")
     dt, res, per = timed_region(step, a.steps, a.warmup, world, torch.cuda.synchronize, dist, red_dev)
     g, gg = res[-1]
     dev_rate = None
@@ -375,6 +383,7 @@ def main():
                                      "markers latency = until that scan's /gvd/markers cells are collected; "
                                      "keeps_up: graph latency and time per scan (markers included) within the budget"}
         if world == 1 and not a.no_cpu_baseline and not a.stream:
+            _progress(f"CPU baseline (oracle, 1 thread) on {a.cpu_config}")
             out["cpu_baseline"] = cpu_baseline(a.cpu_config)
         print(json.dumps(out), flush=True)
     ctx.close()

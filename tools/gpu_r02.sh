@@ -29,7 +29,7 @@ if has smoke; then
 fi
 if has bench; then
   echo "[gpu] bench ${BENCH_ARGS:-}"
-  timeout -k 10 500 python -u bench.py ${BENCH_ARGS:-} > gpurun_out/${TAG}_bench.log 2>&1 || { tail -30 gpurun_out/${TAG}_bench.log; exit 1; }
+  timeout -k 10 500 python -u bench.py ${BENCH_ARGS:-} > gpurun_out/${TAG}_bench.log 2> gpurun_out/${TAG}_bench.err || { tail -30 gpurun_out/${TAG}_bench.log; exit 1; }
   grep '^{' gpurun_out/${TAG}_bench.log
 fi
 cd /tmp

@@ -1,0 +1,157 @@
+// ROR-stage microbenchmark (a1-a4 only): the C2 synthetic cloud, the tile walk of ror.hip compiled in,
+// each pass timed with HIP events over several frames; prints the raster popcount and kept count so
+// variants (-DAOS_RT_VARIANT=..., tile / LDS constants) can be checked against each other.
+// Build: tools/rorbench/build.sh   Run: tools/rorbench/rorbench [grid_n] [n_points] [frames]
+#include "../../active-orchard-slam_amd/csrc/ror.hip"
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+extern "C" {
+typedef struct orchard_cfg {
+    uint64_t seed;
+    uint64_t n_points;
+    int32_t grid_n;
+    float res;
+    int32_t max_rows;
+    double row_x_end;
+    double outlier_frac;
+} orchard_cfg;
+int64_t orchard_num_trees(const orchard_cfg *c);
+int64_t orchard_tree_centres(const orchard_cfg *c, double *tree_x, double *tree_y, int64_t cap);
+void orchard_polygon(const orchard_cfg *c, double *poly_xy);
+void orchard_generate_range(const orchard_cfg *c, const double *tree_x, const double *tree_y, int64_t n_trees,
+                            uint64_t begin, uint64_t end, uint8_t *out);
+}
+
+namespace aos {
+size_t scan_temp_bytes(int n) {
+    size_t t = 0;
+    AOS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t, (const int *)nullptr, (int *)nullptr, n));
+    return t;
+}
+void launch_exclusive_scan(const int *in, int *out, int n, void *temp, size_t temp_bytes, hipStream_t s) {
+    AOS_HIP(hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, in, out, n, s));
+}
+}  // namespace aos
+
+using namespace aos;
+
+int main(int argc, char **argv) {
+    const int grid_n = argc > 1 ? atoi(argv[1]) : 4096;
+    const uint64_t n = argc > 2 ? strtoull(argv[2], 0, 10) : 10000000ull;
+    const int frames = argc > 3 ? atoi(argv[3]) : 10;
+    orchard_cfg c{3, n, grid_n, 0.1f, 0, 0.0, 0.01};
+    const int64_t nt = orchard_num_trees(&c);
+    std::vector<double> tx(nt), ty(nt);
+    orchard_tree_centres(&c, tx.data(), ty.data(), nt);
+    std::vector<uint8_t> cloud(16 * n);
+    orchard_generate_range(&c, tx.data(), ty.data(), nt, 0, n, cloud.data());
+    double poly[8];
+    orchard_polygon(&c, poly);
+    double hminx = poly[0], hmaxx = poly[0], hminy = poly[1], hmaxy = poly[1];
+    for (int k = 0; k < 4; ++k) {
+        hminx = std::min(hminx, poly[2 * k]); hmaxx = std::max(hmaxx, poly[2 * k]);
+        hminy = std::min(hminy, poly[2 * k + 1]); hmaxy = std::max(hmaxy, poly[2 * k + 1]);
+    }
+    const float minx = (float)(hminx - 2.5), maxx = (float)(hmaxx + 2.5), miny = (float)(hminy - 2.5), maxy = (float)(hmaxy + 2.5);
+    const float res = 0.1f;
+    const int W = (int)std::ceil(std::max(0.f, maxx - minx) / res), H = (int)std::ceil(std::max(0.f, maxy - miny) / res);
+    const int WW = (W + 63) / 64;
+    uint8_t *d_cloud;
+    AOS_HIP(hipMalloc(&d_cloud, 16 * n));
+    AOS_HIP(hipMemcpy(d_cloud, cloud.data(), 16 * n, hipMemcpyHostToDevice));
+
+    RorLaunch L{};
+    L.cloud = d_cloud; L.n = n; L.step = 16; L.ox = 0; L.oy = 4; L.oz = 8; L.is_dense = 1;
+    L.cminx = minx; L.cmaxx = maxx; L.cminy = miny; L.cmaxy = maxy; L.cminz = -0.4f; L.cmaxz = 0.5f;
+    const float m = (float)(0.2 * 1.01) + 1e-4f;
+    L.bminx = L.cminx - m; L.bmaxx = L.cmaxx + m; L.bminy = L.cminy - m; L.bmaxy = L.cmaxy + m;
+    L.bminz = L.cminz - m; L.bmaxz = L.cmaxz + m;
+    float cs_ = (float)(0.2 * 1.001);
+    const double ext = std::max((double)L.bmaxx - L.bminx, (double)L.bmaxy - L.bminy);
+    if (ext / cs_ > 8192.0) cs_ = (float)(ext / 8192.0);
+    L.inv_cs = 1.0f / cs_;
+    L.nbx = std::max(1, (int)((L.bmaxx - L.bminx) * L.inv_cs) + 1);
+    L.nby = std::max(1, (int)((L.bmaxy - L.bminy) * L.inv_cs) + 1);
+    L.r2 = 0.2 * 0.2; L.r2f = (float)L.r2; L.r2df = (float)L.r2;
+    if ((double)L.r2df > L.r2) L.r2df = std::nextafter(L.r2df, 0.0f);
+    L.need = 3;
+    L.origin_x = minx; L.origin_y = miny; L.res = res; L.W = W; L.H = H;
+    L.rx0 = 0; L.ry0 = 0; L.rx1 = W; L.ry1 = H; L.wx0 = 0; L.wy0 = 0; L.Wr = W;
+    double est = 0.5 * (double)n;
+    hipStream_t s;
+    AOS_HIP(hipStreamCreate(&s));
+    hipEvent_t e[6];
+    for (auto &x : e) AOS_HIP(hipEventCreate(&x));
+    int *d_H = nullptr, *d_O = nullptr; void *d_st = nullptr; float4 *d_staged = nullptr, *d_scr = nullptr;
+    unsigned long long *d_cnt; uint64_t *d_bits;
+    AOS_HIP(hipMalloc(&d_cnt, 8 * (kRorCounters + 1)));
+    AOS_HIP(hipMalloc(&d_bits, 8ull * WW * H));
+    size_t cap_H = 0, cap_st = 0, cap_staged = 0;
+    double acc[5] = {0, 0, 0, 0, 0};
+    for (int f = 0; f < frames + 2; ++f) {
+        rt_configure(L, H, WW, est);
+        const int G = rt_part_blocks(L);
+        const size_t nH = (size_t)L.ntiles * G + 1;
+        if (nH > cap_H) {
+            if (d_H) { AOS_HIP(hipFree(d_H)); AOS_HIP(hipFree(d_O)); }
+            AOS_HIP(hipMalloc(&d_H, 4 * nH)); AOS_HIP(hipMalloc(&d_O, 4 * nH)); cap_H = nH;
+        }
+        const size_t st = scan_temp_bytes((int)nH);
+        if (st > cap_st) { if (d_st) AOS_HIP(hipFree(d_st)); AOS_HIP(hipMalloc(&d_st, st)); cap_st = st; }
+        AOS_HIP(hipMemsetAsync(d_H + nH - 1, 0, 4, s));
+        AOS_HIP(hipMemsetAsync(d_cnt, 0, 8 * (kRorCounters + 1), s));
+        AOS_HIP(hipMemsetAsync(d_bits, 0, 8ull * WW * H, s));
+        AOS_HIP(hipEventRecord(e[0], s));
+        launch_rt_count(L, d_H, G, d_cnt + kRorCounters, s);
+        AOS_HIP(hipEventRecord(e[1], s));
+        launch_exclusive_scan(d_H, d_O, (int)nH, d_st, st, s);
+        AOS_HIP(hipEventRecord(e[2], s));
+        int total = 0;
+        unsigned long long own = 0;
+        AOS_HIP(hipMemcpyAsync(&total, d_O + nH - 1, 4, hipMemcpyDeviceToHost, s));
+        AOS_HIP(hipMemcpyAsync(&own, d_cnt + kRorCounters, 8, hipMemcpyDeviceToHost, s));
+        AOS_HIP(hipStreamSynchronize(s));
+        est = (double)own;
+        if ((size_t)total > cap_staged) {
+            if (d_staged) { AOS_HIP(hipFree(d_staged)); AOS_HIP(hipFree(d_scr)); }
+            AOS_HIP(hipMalloc(&d_staged, 16ull * total)); AOS_HIP(hipMalloc(&d_scr, 16ull * total)); cap_staged = total;
+        }
+        L.staged_cap = (int)cap_staged;
+        L.overflow = reinterpret_cast<int *>(d_cnt + kRorCounters) + 1;
+        AOS_HIP(hipMemcpyAsync(d_H, d_O, 4 * nH, hipMemcpyDeviceToDevice, s));
+        AOS_HIP(hipEventRecord(e[3], s));
+        launch_rt_scatter(L, d_H, G, d_staged, s);
+        AOS_HIP(hipEventRecord(e[4], s));
+        launch_rt_ror(L, d_O, G, d_staged, d_scr, d_bits, d_cnt, s);
+        AOS_HIP(hipEventRecord(e[5], s));
+        AOS_HIP(hipStreamSynchronize(s));
+        float t[5];
+        AOS_HIP(hipEventElapsedTime(&t[0], e[0], e[1]));
+        AOS_HIP(hipEventElapsedTime(&t[1], e[1], e[2]));
+        AOS_HIP(hipEventElapsedTime(&t[2], e[3], e[4]));
+        AOS_HIP(hipEventElapsedTime(&t[3], e[4], e[5]));
+        AOS_HIP(hipEventElapsedTime(&t[4], e[0], e[5]));
+        if (f >= 2) for (int k = 0; k < 5; ++k) acc[k] += t[k] / frames;
+        if (f == frames + 1) {
+            std::vector<uint64_t> bits((size_t)WW * H);
+            std::vector<unsigned long long> cnt(kRorCounters);
+            AOS_HIP(hipMemcpy(bits.data(), d_bits, 8 * bits.size(), hipMemcpyDeviceToHost));
+            AOS_HIP(hipMemcpy(cnt.data(), d_cnt, 8 * kRorCounters, hipMemcpyDeviceToHost));
+            unsigned long long pc = 0, kept = 0, hsh = 1469598103934665603ull;
+            for (uint64_t w : bits) { pc += __builtin_popcountll(w); hsh = (hsh ^ w) * 1099511628211ull; }
+            for (auto v : cnt) kept += v;
+            printf("grid %dx%d n %llu TB %d tiles %d G %d staged %d binned %llu | raster cells %llu kept %llu hash %016llx\n", W, H,
+                   (unsigned long long)n, L.TB, L.ntiles, G, total, own, pc, kept, hsh);
+        }
+    }
+    const double b = 12.0 * n + (double)W * H;
+    printf("count %.1f us  scan %.1f us  scatter %.1f us  tiles %.1f us  | stage %.1f us (incl. read-back gap)  "
+           "§8d bytes %.0f MB -> %.3f TB/s = %.3f of 8 TB/s; count pass 12N: %.3f of peak\n",
+           1e3 * acc[0], 1e3 * acc[1], 1e3 * acc[2], 1e3 * acc[3], 1e3 * acc[4], b / 1e6, b / (acc[4] * 1e-3) / 1e12,
+           b / (acc[4] * 1e-3) / 8e12, 12.0 * n / (acc[0] * 1e-3) / 8e12);
+    return 0;
+}
