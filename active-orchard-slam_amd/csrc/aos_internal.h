@@ -109,10 +109,11 @@ struct RorLaunch {
 constexpr int kRtMaxTiles = 36000;   // tiles per frame (LDS histogram of the partition passes: 144 KB)
 void rt_configure(RorLaunch &L, int Hr, int WWr, double est_binned);
 int rt_part_blocks(const RorLaunch &L);   // G: workgroups (= cloud chunks) of the partition passes
-// H: ntiles x G + 1 ints (tile-major); after the count pass and an exclusive scan, O = H offsets
-void launch_rt_count(const RorLaunch &L, int *H, int G, unsigned long long *n_own, hipStream_t s);
-void launch_rt_scatter(const RorLaunch &L, int *O, int G, float4 *staged, hipStream_t s);
-void launch_rt_ror(const RorLaunch &L, const int *O, int G, const float4 *staged, float4 *scratch, uint64_t *rbits,
+// H: G x ntiles ints (row per workgroup). The count pass leaves per-tile prefixes over the workgroups
+// in H and the tile totals in tot[0..ntiles); tstart = exclusive scan of tot (ntiles + 1 entries).
+void launch_rt_count(const RorLaunch &L, int *H, int G, int *tot, unsigned long long *n_own, hipStream_t s);
+void launch_rt_scatter(const RorLaunch &L, int *H, const int *tstart, int G, float4 *staged, hipStream_t s);
+void launch_rt_ror(const RorLaunch &L, const int *tstart, const float4 *staged, float4 *scratch, uint64_t *rbits,
                    unsigned long long *counters, hipStream_t s);
 // PointCloud2 records (any float32 x/y/z offsets) -> float4 (x, y, z, 0)
 void launch_pack_xyz(const uint8_t *cloud, uint64_t n, uint32_t step, uint32_t ox, uint32_t oy, uint32_t oz, float4 *out,

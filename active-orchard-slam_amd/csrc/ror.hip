@@ -93,14 +93,21 @@ __device__ __forceinline__ bool rt_in(const RorLaunch &L, float4 p, float4 q) {
 // ---------------------------------------------------------------------------------------------
 // Passes 1 and 3: count / scatter, a radix-sort style partition with one digit per tile. Workgroup
 // w owns one contiguous chunk of the cloud. The count pass accumulates an LDS histogram over the
-// chunk and stores it as column w of H (tile-major, H[t * G + w]); one exclusive scan of H gives
-// every (tile, workgroup) run its offset; the scatter pass walks the same chunk again with LDS
-// cursors starting at those offsets. No global atomics; a tile's run from workgroup w sits right
-// after workgroup w - 1's.
+// chunk and stores it as row w of H (H[w * ntiles + t], a coalesced store); k_rt_colscan turns the
+// columns into per-tile exclusive prefixes over the workgroups plus tile totals, one small scan of
+// the totals gives the tile starts, and the scatter pass walks the same chunk again with LDS
+// cursors starting at tile start + prefix. No global atomics; a tile's run from workgroup w sits
+// right after workgroup w - 1's.
 #ifndef AOS_RT_PART_TB
 #define AOS_RT_PART_TB 256
 #endif
-constexpr int kRtTB = AOS_RT_PART_TB, kRtPer = 8, kRtSub = kRtTB * kRtPer;
+#ifndef AOS_RT_PER
+#define AOS_RT_PER 8
+#endif
+#ifndef AOS_RT_G
+#define AOS_RT_G 512
+#endif
+constexpr int kRtTB = AOS_RT_PART_TB, kRtPer = AOS_RT_PER, kRtSub = kRtTB * kRtPer;
 
 // tiles whose bins a point's 3 x 3 bins touch: [tx0, tx1] x [ty0, ty1], own tile (bx / TB, by / TB)
 __device__ __forceinline__ void rt_tiles(const RorLaunch &L, int bx, int by, int &tx0, int &tx1, int &ty0, int &ty1) {
@@ -109,25 +116,25 @@ __device__ __forceinline__ void rt_tiles(const RorLaunch &L, int bx, int by, int
 }
 
 template <bool SCATTER, bool STD>
-__global__ __launch_bounds__(kRtTB) void k_rt_part(RorLaunch L, int *H, uint64_t chunk, float4 *staged,
-                                                   unsigned long long *n_own) {
+__global__ __launch_bounds__(kRtTB) void k_rt_part(RorLaunch L, int *H, const int *tstart, uint64_t chunk,
+                                                   float4 *staged, unsigned long long *n_own) {
     extern __shared__ int hist[];        // [ntiles]: counts (count pass) / cursors (scatter pass)
-    const int tid = threadIdx.x, G = gridDim.x, w = blockIdx.x;
-    for (int t = tid; t < L.ntiles; t += kRtTB) hist[t] = SCATTER ? H[(size_t)t * G + w] : 0;
+    const int tid = threadIdx.x, w = blockIdx.x;
+    int *row = H + (size_t)w * L.ntiles;
+    for (int t = tid; t < L.ntiles; t += kRtTB) hist[t] = SCATTER ? tstart[t] + row[t] : 0;
     __syncthreads();
     unsigned own = 0;
     const uint64_t begin = (uint64_t)w * chunk, end = min(L.n, begin + chunk);
     // software pipelined: the next sub-chunk's kRtPer loads are in flight while this one is walked
     float4 nxt[kRtPer];
+    // (branch-free: an index past the chunk re-reads its last point and is marked invalid, so the
+    // compiler issues the kRtPer loads back to back without intervening waits)
     auto issue = [&](uint64_t base) {
 #pragma unroll
         for (int j = 0; j < kRtPer; ++j) {
             const uint64_t i = base + (uint64_t)j * kRtTB + tid;
-            nxt[j] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
-            if (i < end) {
-                rt_load<STD>(L, i, nxt[j].x, nxt[j].y, nxt[j].z);
-                nxt[j].w = 0.f;
-            }
+            rt_load<STD>(L, i < end ? i : end - 1, nxt[j].x, nxt[j].y, nxt[j].z);
+            nxt[j].w = __int_as_float(i < end ? 0 : -1);
         }
     };
     if (begin < end) issue(begin);
@@ -163,9 +170,36 @@ __global__ __launch_bounds__(kRtTB) void k_rt_part(RorLaunch L, int *H, uint64_t
     }
     if (!SCATTER) {
         __syncthreads();
-        for (int t = tid; t < L.ntiles; t += kRtTB) H[(size_t)t * G + w] = hist[t];
+        for (int t = tid; t < L.ntiles; t += kRtTB) row[t] = hist[t];
         for (int o = 32; o > 0; o >>= 1) own += __shfl_xor(own, o);
         if ((tid & 63) == 0 && own) atomicAdd(n_own, (unsigned long long)own);
+    }
+}
+
+// H rows -> per-tile exclusive prefixes over the workgroups (in place) and tile totals. A block owns
+// 64 tiles (one per lane) and the 8 waves split the G rows: each wave sums its rows, the partial sums
+// are scanned in LDS, and each wave rewrites its rows as prefixes. Every access is a 256 B row run.
+constexpr int kColWaves = 8;
+__global__ __launch_bounds__(64 * kColWaves) void k_rt_colscan(int *H, int *tot, int ntiles, int G) {
+    __shared__ int part[kColWaves][64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int t = blockIdx.x * 64 + lane;
+    const int per = (G + kColWaves - 1) / kColWaves, r0 = wv * per, r1 = min(G, r0 + per);
+    int sum = 0;
+    if (t < ntiles)
+        for (int r = r0; r < r1; ++r) sum += H[(size_t)r * ntiles + t];
+    part[wv][lane] = sum;
+    __syncthreads();
+    int before = 0;
+    for (int k = 0; k < wv; ++k) before += part[k][lane];
+    if (t < ntiles) {
+        for (int r = r0; r < r1; ++r) {
+            const size_t i = (size_t)r * ntiles + t;
+            const int v = H[i];
+            H[i] = before;
+            before += v;
+        }
+        if (wv == kColWaves - 1) tot[t] = before;
     }
 }
 
@@ -201,7 +235,7 @@ __device__ __forceinline__ int rt_scan(const RorLaunch &L, float4 p, Pts pts, in
 // + ring: 34^2), and the tile's raster window (kRtWinWords 64-bit words): ~40 KB, 3 workgroups per CU
 constexpr int kRtMaxLocalBins = 34 * 34, kRtWinWords = 320;
 
-__global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *O, int G, const float4 *staged,
+__global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *tstart, const float4 *staged,
                                                         float4 *scratch, uint64_t *rbits,
                                                         unsigned long long *counters) {
     __shared__ float4 pts[kRorCap];
@@ -210,7 +244,7 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
     const int tid = threadIdx.x;
     const int t = rt_xcd_block(blockIdx.x, gridDim.x);
     const int tx = t % L.ntx, ty = t / L.ntx;
-    const int a = O[(size_t)t * G], n = O[(size_t)(t + 1) * G] - a;   // the tile's runs, scanned
+    const int a = tstart[t], n = tstart[t + 1] - a;   // the tile's runs
     if (n == 0 || a + n > L.staged_cap) return;   // (an overflowed scatter: the frame is redone)
     const int LB = L.TB + 2;                        // local bins: the tile's bins and a ring of halo bins
     const int bx0 = tx * L.TB - 1, by0 = ty * L.TB - 1;
@@ -369,7 +403,7 @@ void rt_configure(RorLaunch &L, int Hr, int WWr, double est_binned) {
 
 int rt_part_blocks(const RorLaunch &L) {
     // one contiguous chunk per workgroup; H has ntiles x G ints
-    long long g = 512 * 256 / kRtTB;
+    long long g = AOS_RT_G * 256 / kRtTB;
     while (g > 64 && (long long)L.ntiles * g > (16ll << 20)) g /= 2;
     return (int)std::max<long long>(1, std::min<long long>(g, ((long long)L.n + kRtSub - 1) / kRtSub));
 }
@@ -379,32 +413,35 @@ uint64_t rt_chunk(const RorLaunch &L, int G) {
 }
 
 template <bool SCATTER, bool STD>
-static void rt_part(const RorLaunch &L, int *H, int G, float4 *staged, unsigned long long *n_own, hipStream_t s) {
+static void rt_part(const RorLaunch &L, int *H, const int *tstart, int G, float4 *staged, unsigned long long *n_own,
+                    hipStream_t s) {
     const size_t lds = sizeof(int) * (size_t)L.ntiles;
     if (lds > 64 * 1024)   // the tile histogram exceeds the default dynamic-LDS limit (gfx950: 160 KB)
         AOS_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rt_part<SCATTER, STD>),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    k_rt_part<SCATTER, STD><<<G, kRtTB, lds, s>>>(L, H, rt_chunk(L, G), staged, n_own);
+    k_rt_part<SCATTER, STD><<<G, kRtTB, lds, s>>>(L, H, tstart, rt_chunk(L, G), staged, n_own);
     AOS_HIP(hipGetLastError());
 }
 static bool rt_std(const RorLaunch &L) { return L.step == 16 && L.ox == 0 && L.oy == 4 && L.oz == 8; }
 
-void launch_rt_count(const RorLaunch &L, int *H, int G, unsigned long long *n_own, hipStream_t s) {
+void launch_rt_count(const RorLaunch &L, int *H, int G, int *tot, unsigned long long *n_own, hipStream_t s) {
     if (!L.n) return;
-    if (rt_std(L)) rt_part<false, true>(L, H, G, nullptr, n_own, s);
-    else rt_part<false, false>(L, H, G, nullptr, n_own, s);
+    if (rt_std(L)) rt_part<false, true>(L, H, nullptr, G, nullptr, n_own, s);
+    else rt_part<false, false>(L, H, nullptr, G, nullptr, n_own, s);
+    k_rt_colscan<<<(L.ntiles + 63) / 64, 64 * kColWaves, 0, s>>>(H, tot, L.ntiles, G);
+    AOS_HIP(hipGetLastError());
 }
 
-void launch_rt_scatter(const RorLaunch &L, int *O, int G, float4 *staged, hipStream_t s) {
+void launch_rt_scatter(const RorLaunch &L, int *H, const int *tstart, int G, float4 *staged, hipStream_t s) {
     if (!L.n) return;
-    if (rt_std(L)) rt_part<true, true>(L, O, G, staged, nullptr, s);
-    else rt_part<true, false>(L, O, G, staged, nullptr, s);
+    if (rt_std(L)) rt_part<true, true>(L, H, tstart, G, staged, nullptr, s);
+    else rt_part<true, false>(L, H, tstart, G, staged, nullptr, s);
 }
 
-void launch_rt_ror(const RorLaunch &L, const int *O, int G, const float4 *staged, float4 *scratch, uint64_t *rbits,
+void launch_rt_ror(const RorLaunch &L, const int *tstart, const float4 *staged, float4 *scratch, uint64_t *rbits,
                    unsigned long long *counters, hipStream_t s) {
     if (!L.n || !L.ntiles) return;
-    k_rt_ror<<<L.ntiles, kRorThreads, 0, s>>>(L, O, G, staged, scratch, rbits, counters);
+    k_rt_ror<<<L.ntiles, kRorThreads, 0, s>>>(L, tstart, staged, scratch, rbits, counters);
     AOS_HIP(hipGetLastError());
 }
 

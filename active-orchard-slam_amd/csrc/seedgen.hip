@@ -235,15 +235,16 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
     rt_configure(L, o.Hr, WWr, ror_est_binned > 0 ? ror_est_binned : 0.5 * (double)n_points);
     const int nt = L.ntiles;
     const int G = rt_part_blocks(L);
-    const size_t nH = (size_t)nt * G + 1;
+    const size_t nH = (size_t)nt * G;
 
     int *d_H = static_cast<int *>(bin_count.ensure(sizeof(int) * nH));
-    int *d_O = static_cast<int *>(bin_start.ensure(sizeof(int) * nH));
+    int *d_tot = static_cast<int *>(bin_start.ensure(sizeof(int) * 2 * (nt + 1)));
+    int *d_ts = d_tot + (nt + 1);
     unsigned long long *d_cnt = static_cast<unsigned long long *>(counters.ensure(8 * kRorCounters + 16));
     unsigned long long *d_own = d_cnt + kRorCounters;   // [0] binned points, [1] overflow flag
-    size_t st = scan_temp_bytes((int)nH);
+    size_t st = scan_temp_bytes(nt + 1);
     void *d_st = scan_tmp.ensure(st);
-    AOS_HIP(hipMemsetAsync(d_H + nH - 1, 0, sizeof(int), s));
+    AOS_HIP(hipMemsetAsync(d_tot + nt, 0, sizeof(int), s));
     AOS_HIP(hipMemsetAsync(d_cnt, 0, 8 * kRorCounters + 16, s));
     AOS_HIP(hipMemsetAsync(rbits, 0, sizeof(uint64_t) * (size_t)o.Hr * WWr, s));
     // PCL dense kNN needs k = min_pts + 1 points in the whole cloud (else every point is removed).
@@ -252,9 +253,9 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
     const bool any = n_points > 0 && !(is_dense && n_points < (uint64_t)L.need);
     if (!any) return;
     AOS_HIP(hipEventRecord(ev[12], s));
-    launch_rt_count(L, d_H, G, d_own, s);
+    launch_rt_count(L, d_H, G, d_tot, d_own, s);
     AOS_HIP(hipEventRecord(ev[13], s));
-    launch_exclusive_scan(d_H, d_O, (int)nH, d_st, st, s);
+    launch_exclusive_scan(d_tot, d_ts, nt + 1, d_st, st, s);
     // The staged array holds own + halo copies. With a capacity from an earlier frame the scatter
     // runs at once and reports an overflow (the frame is then redone with the size it read back,
     // run_seedgen); without one, or when the caller cannot redo (a tiled frame), the size is read
@@ -263,7 +264,7 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
     const size_t cap_now = sorted.cap / sizeof(float4);
     const bool guess = allow_guess && ror_staged_max > 0 && cap_now >= (size_t)(ror_staged_max * 1.1);
     if (!guess) {
-        AOS_HIP(hipMemcpyAsync(h + 2, d_O + nH - 1, sizeof(int), hipMemcpyDeviceToHost, s));
+        AOS_HIP(hipMemcpyAsync(h + 2, d_ts + nt, sizeof(int), hipMemcpyDeviceToHost, s));
         AOS_HIP(hipStreamSynchronize(s));
         const size_t need = (size_t)std::max(h[2], 1);
         ror_staged_max = std::max<double>(ror_staged_max, (double)need);
@@ -273,15 +274,13 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
     L.staged_cap = (int)std::min<size_t>(sorted.cap / sizeof(float4), (size_t)INT_MAX);
     float4 *d_scratch = static_cast<float4 *>(ror_scratch.ensure(sizeof(float4) * (size_t)L.staged_cap));
     L.overflow = reinterpret_cast<int *>(d_own + 1);
-    // the scatter pass advances its cursors in a copy: pass 4 reads the offsets
-    AOS_HIP(hipMemcpyAsync(d_H, d_O, sizeof(int) * nH, hipMemcpyDeviceToDevice, s));
     AOS_HIP(hipEventRecord(ev[14], s));
-    launch_rt_scatter(L, d_H, G, d_staged, s);
+    launch_rt_scatter(L, d_H, d_ts, G, d_staged, s);
     AOS_HIP(hipEventRecord(ev[10], s));
-    launch_rt_ror(L, d_O, G, d_staged, d_scratch, rbits, d_cnt, s);
+    launch_rt_ror(L, d_ts, d_staged, d_scratch, rbits, d_cnt, s);
     AOS_HIP(hipEventRecord(ev[11], s));
     // binned points, staged total, overflow flag: read with the frame's other stats (finish_frame)
-    AOS_HIP(hipMemcpyAsync(h + 2, d_O + nH - 1, sizeof(int), hipMemcpyDeviceToHost, s));
+    AOS_HIP(hipMemcpyAsync(h + 2, d_ts + nt, sizeof(int), hipMemcpyDeviceToHost, s));
     AOS_HIP(hipMemcpyAsync(h + 4, d_own, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
 }
 

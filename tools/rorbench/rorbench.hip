@@ -86,33 +86,33 @@ int main(int argc, char **argv) {
     AOS_HIP(hipStreamCreate(&s));
     hipEvent_t e[6];
     for (auto &x : e) AOS_HIP(hipEventCreate(&x));
-    int *d_H = nullptr, *d_O = nullptr; void *d_st = nullptr; float4 *d_staged = nullptr, *d_scr = nullptr;
+    int *d_H = nullptr, *d_tot = nullptr; void *d_st = nullptr; float4 *d_staged = nullptr, *d_scr = nullptr;
     unsigned long long *d_cnt; uint64_t *d_bits;
-    AOS_HIP(hipMalloc(&d_cnt, 8 * (kRorCounters + 1)));
+    AOS_HIP(hipMalloc(&d_cnt, 8 * (kRorCounters + 2)));
     AOS_HIP(hipMalloc(&d_bits, 8ull * WW * H));
-    size_t cap_H = 0, cap_st = 0, cap_staged = 0;
+    size_t cap_H = 0, cap_st = 0, cap_staged = 0, cap_t = 0;
     double acc[5] = {0, 0, 0, 0, 0};
     for (int f = 0; f < frames + 2; ++f) {
         rt_configure(L, H, WW, est);
         const int G = rt_part_blocks(L);
-        const size_t nH = (size_t)L.ntiles * G + 1;
-        if (nH > cap_H) {
-            if (d_H) { AOS_HIP(hipFree(d_H)); AOS_HIP(hipFree(d_O)); }
-            AOS_HIP(hipMalloc(&d_H, 4 * nH)); AOS_HIP(hipMalloc(&d_O, 4 * nH)); cap_H = nH;
-        }
-        const size_t st = scan_temp_bytes((int)nH);
+        const int nt = L.ntiles;
+        const size_t nH = (size_t)nt * G;
+        if (nH > cap_H) { if (d_H) AOS_HIP(hipFree(d_H)); AOS_HIP(hipMalloc(&d_H, 4 * nH)); cap_H = nH; }
+        if ((size_t)nt + 1 > cap_t) { if (d_tot) AOS_HIP(hipFree(d_tot)); AOS_HIP(hipMalloc(&d_tot, 8 * (nt + 1))); cap_t = nt + 1; }
+        int *d_ts = d_tot + (nt + 1);
+        const size_t st = scan_temp_bytes(nt + 1);
         if (st > cap_st) { if (d_st) AOS_HIP(hipFree(d_st)); AOS_HIP(hipMalloc(&d_st, st)); cap_st = st; }
-        AOS_HIP(hipMemsetAsync(d_H + nH - 1, 0, 4, s));
-        AOS_HIP(hipMemsetAsync(d_cnt, 0, 8 * (kRorCounters + 1), s));
+        AOS_HIP(hipMemsetAsync(d_tot + nt, 0, 4, s));
+        AOS_HIP(hipMemsetAsync(d_cnt, 0, 8 * (kRorCounters + 2), s));
         AOS_HIP(hipMemsetAsync(d_bits, 0, 8ull * WW * H, s));
         AOS_HIP(hipEventRecord(e[0], s));
-        launch_rt_count(L, d_H, G, d_cnt + kRorCounters, s);
+        launch_rt_count(L, d_H, G, d_tot, d_cnt + kRorCounters, s);
         AOS_HIP(hipEventRecord(e[1], s));
-        launch_exclusive_scan(d_H, d_O, (int)nH, d_st, st, s);
+        launch_exclusive_scan(d_tot, d_ts, nt + 1, d_st, st, s);
         AOS_HIP(hipEventRecord(e[2], s));
         int total = 0;
         unsigned long long own = 0;
-        AOS_HIP(hipMemcpyAsync(&total, d_O + nH - 1, 4, hipMemcpyDeviceToHost, s));
+        AOS_HIP(hipMemcpyAsync(&total, d_ts + nt, 4, hipMemcpyDeviceToHost, s));
         AOS_HIP(hipMemcpyAsync(&own, d_cnt + kRorCounters, 8, hipMemcpyDeviceToHost, s));
         AOS_HIP(hipStreamSynchronize(s));
         est = (double)own;
@@ -121,12 +121,11 @@ int main(int argc, char **argv) {
             AOS_HIP(hipMalloc(&d_staged, 16ull * total)); AOS_HIP(hipMalloc(&d_scr, 16ull * total)); cap_staged = total;
         }
         L.staged_cap = (int)cap_staged;
-        L.overflow = reinterpret_cast<int *>(d_cnt + kRorCounters) + 1;
-        AOS_HIP(hipMemcpyAsync(d_H, d_O, 4 * nH, hipMemcpyDeviceToDevice, s));
+        L.overflow = reinterpret_cast<int *>(d_cnt + kRorCounters + 1);
         AOS_HIP(hipEventRecord(e[3], s));
-        launch_rt_scatter(L, d_H, G, d_staged, s);
+        launch_rt_scatter(L, d_H, d_ts, G, d_staged, s);
         AOS_HIP(hipEventRecord(e[4], s));
-        launch_rt_ror(L, d_O, G, d_staged, d_scr, d_bits, d_cnt, s);
+        launch_rt_ror(L, d_ts, d_staged, d_scr, d_bits, d_cnt, s);
         AOS_HIP(hipEventRecord(e[5], s));
         AOS_HIP(hipStreamSynchronize(s));
         float t[5];
