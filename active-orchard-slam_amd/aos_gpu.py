@@ -231,7 +231,14 @@ def _arr(ptr, n, dtype):
     return np.ctypeslib.as_array(ptr, shape=(n,)).astype(dtype, copy=True)
 
 
-def _seedgen_dict(o: SeedGenOut, want_host: bool) -> dict:
+def _view_arr(ptr, n, dtype):
+    """Zero-copy numpy view of a library-owned output (valid until the next call on the handle)."""
+    if n <= 0 or not ptr:
+        return np.zeros(0, dtype=dtype)
+    return np.ctypeslib.as_array(ptr, shape=(n,)).view(dtype)
+
+
+def _seedgen_dict(o: SeedGenOut, want_host: bool, copy_grids: bool = True) -> dict:
     W, H = o.info.width, o.info.height
     nr = o.n_rows
     r = {
@@ -256,8 +263,9 @@ def _seedgen_dict(o: SeedGenOut, want_host: bool) -> dict:
     seeds = r["voronoi_seeds"]
     r["virtual_seeds"], r["ray_seeds"], r["endpoint_seeds"] = seeds[:nv], seeds[nv:nv + nrr], seeds[nv + nrr:]
     if want_host:
-        r["occupancy"] = _arr(o.occupancy, W * H, np.int8).reshape(H, W)
-        r["skeleton_framed"] = _arr(o.skeleton, W * H, np.int8).reshape(H, W)
+        grid = _arr if copy_grids else _view_arr
+        r["occupancy"] = grid(o.occupancy, W * H, np.int8).reshape(H, W)
+        r["skeleton_framed"] = grid(o.skeleton, W * H, np.int8).reshape(H, W)
     return r
 
 
@@ -326,12 +334,14 @@ class Ctx:
         return CloudView(ptr, n, point_step, offs[0], offs[1], offs[2], int(is_dense), int(on_device)), cloud
 
     def seedgen(self, cloud, n_points: int | None = None, point_step=16, offs=(0, 4, 8), is_dense=True,
-                on_device=False, want_host=True) -> dict:
-        """cloud: (n, point_step) uint8 numpy array, or an int device pointer with on_device=True."""
+                on_device=False, want_host=True, copy_grids=True) -> dict:
+        """cloud: (n, point_step) uint8 numpy array, or an int device pointer with on_device=True.
+        copy_grids=False returns the two OccupancyGrids as views of the library's pinned host buffers
+        (the ABI's ownership rule: valid until the next call on this handle)."""
         v, _keep = self._view(cloud, n_points, point_step, offs, is_dense, on_device)
         o = SeedGenOut()
         _check(lib().aos_seedgen_process(self.h, ctypes.byref(v), int(want_host), ctypes.byref(o)))
-        return _seedgen_dict(o, want_host)
+        return _seedgen_dict(o, want_host, copy_grids)
 
     def map_reset(self, reserve_points: int = 0):
         """Empty the device-resident streaming map (aos_map_reset)."""

@@ -44,9 +44,9 @@ def parse(argv=None):
                          "host-in / host-out frame")
     ap.add_argument("--no-device-rate", action="store_true", help="skip the extra device-resident loop")
     ap.add_argument("--trace", action="store_true", help="per-step timeline of the pipelined loop on stderr")
-    ap.add_argument("--pipeline", action="store_true",
-                    help="overlap frame k's seed-gen with frame k-1's GVD (aos_gvd_from_seedgen_async); the last "
-                         "frame's GVD drains inside the timed region, so it pays off only for many steps")
+    ap.add_argument("--sequential", action="store_true",
+                    help="run seed-gen and GVD of a frame back to back instead of the default pipeline (frame k's "
+                         "seed-gen overlaps frame k-1's GVD, as the reference's two nodes do)")
     ap.add_argument("--tiled", action="store_true",
                     help="one map split into tiles over the ranks (SURVEY §8e, BASELINE configs[3]); strong scaling")
     a = ap.parse_args(argv)
@@ -200,14 +200,14 @@ def main():
     # The markers' cells of a frame finish in the background after its graph (publishGraph before
     # publishMarkers, gvd:310-313): every step collects the previous frame's markers after its own
     # seed-gen, and the last step collects its own, so each timed frame includes its markers.
-    # Default (sequential): step k = seed-gen k, the markers of frame k - 1, then the GVD of frame k.
-    # --pipeline: the reference's seed-gen and GVD are two nodes, so frame k's seed-gen runs while
+    # --sequential: step k = seed-gen k, the markers of frame k - 1, then the GVD of frame k.
+    # Pipelined (default): the reference's seed-gen and GVD are two nodes, so frame k's seed-gen runs while
     # frame k - 1's graph is built (aos_gvd_from_seedgen_async on the handle's GVD worker). Step k =
     # seed-gen k, collect graph + markers of frame k - 1, start the GVD of frame k; the last step also
     # collects its own frame, so every frame of the timed region completes inside it.
     n_calls = a.warmup + a.steps
     pend = {"k": 0, "t0": {}, "mt0": None, "ms": 0.0}
-    pipeline = a.pipeline
+    pipeline = not (a.sequential or a.stream or a.tiled)
 
     def collect():
         m = ctx.gvd_markers()
@@ -240,7 +240,8 @@ def main():
                 return g, {"ms": {}, "nodes": (), "edges": ()}
         else:
             if mode["host"]:   # PointCloud2 bytes from host memory in, both OccupancyGrids to host out
-                g = ctx.seedgen(h_cloud, want_host=True)
+                # (the grids are returned as views of the library's pinned buffers: the ABI's ownership rule)
+                g = ctx.seedgen(h_cloud, want_host=True, copy_grids=False)
             else:
                 g = ctx.seedgen(d_cloud.data_ptr(), n_points=n, on_device=True, want_host=False)
         if pipeline:
@@ -273,7 +274,7 @@ def main():
     dt, res, per = timed_region(step, a.steps, a.warmup, world, torch.cuda.synchronize, dist, red_dev)
     g, gg = res[-1]
     dev_rate = None
-    if host_io and not a.no_device_rate and not pipeline:
+    if host_io and not a.no_device_rate:
         # the same frame with the cloud already in HBM and the grids left there (no PCIe)
         mode["host"] = False
         pend["k"], n_calls = 0, 2 + a.steps
