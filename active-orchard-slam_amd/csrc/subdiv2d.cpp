@@ -1,6 +1,8 @@
 // Host Delaunay with cv::Subdiv2D semantics — see subdiv2d.h. Compiled -ffp-contract=off.
 #include "subdiv2d.h"
 
+#include <immintrin.h>
+
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
@@ -101,6 +103,10 @@ void Subdiv2D::delete_edge(int e) {   // deleteEdge
     rec[q].link = free_q;
     free_q = q;
 }
+
+// The batched AVX2 tests are exact but not faster on the EPYC 9575F host (the 4 x 4 transposes take
+// the FP pipes the scalar tests use): off by default, kept for tools/sdcheck and set_simd().
+Subdiv2D::Subdiv2D() = default;
 
 void Subdiv2D::init_delaunay(float rx, float ry, float rw, float rh, int rect_mode) {
     if (rect_mode == 1) {  // Rect_<float> -> Rect_<int>: saturate_cast<int> = cvRound (nearest even)
@@ -223,6 +229,65 @@ void Subdiv2D::swap_loop(int curr_edge, int first_point, int curr_point) {
     }
 }
 
+// The swap loop's flip test for link edges es[0..n) (n <= 4) against the new point P, written into
+// out[] (1 = swap): isRightOf(temp_dst, e) > 0 && isPtInCircle3(org, temp_dst, dst, P) < -eps, with
+// temp_dst = Dst(Oprev e). Same operands and operation order as swap_loop in every lane.
+void Subdiv2D::flip_tests_scalar(const int *es, int n, const V2d &P, int *out) const {
+    auto area = [](const V2d &a, const V2d &b, const V2d &c) { return (b.x - a.x) * (c.y - a.y) - (b.y - a.y) * (c.x - a.x); };
+    for (int i = 0; i < n; ++i) {
+        const int e = es[i];
+        const V2d &T = vd[dst(oprev(e))], &O = vd[org(e)], &D = vd[dst(e)];
+        bool flip = false;
+        if (area(T, D, O) > 0) {
+            double val = T.n2 * area(D, P, O);
+            val -= D.n2 * area(T, P, O);
+            val += P.n2 * area(T, D, O);
+            val -= O.n2 * area(T, D, P);
+            flip = val < -(FLT_EPSILON * 0.125);
+        }
+        out[i] = flip;
+    }
+}
+
+// Four tests at once on AVX2 (one lane each; every lane rounds exactly like the scalar form: plain
+// IEEE double sub / mul in the same order, no FMA).
+#define AOS_AVX2 __attribute__((target("avx2")))
+AOS_AVX2 static inline void transpose3(const __m256d *r, __m256d &X, __m256d &Y, __m256d &N) {
+    const __m256d t0 = _mm256_unpacklo_pd(r[0], r[1]), t1 = _mm256_unpackhi_pd(r[0], r[1]);
+    const __m256d t2 = _mm256_unpacklo_pd(r[2], r[3]), t3 = _mm256_unpackhi_pd(r[2], r[3]);
+    X = _mm256_permute2f128_pd(t0, t2, 0x20);
+    N = _mm256_permute2f128_pd(t0, t2, 0x31);
+    Y = _mm256_permute2f128_pd(t1, t3, 0x20);
+}
+AOS_AVX2 static inline __m256d area4(__m256d ax, __m256d ay, __m256d bx, __m256d by, __m256d cx, __m256d cy) {
+    return _mm256_sub_pd(_mm256_mul_pd(_mm256_sub_pd(bx, ax), _mm256_sub_pd(cy, ay)),
+                         _mm256_mul_pd(_mm256_sub_pd(by, ay), _mm256_sub_pd(cx, ax)));
+}
+
+AOS_AVX2 void Subdiv2D::flip_tests_avx2(const int *es, int n, const V2d &P, int *out) const {
+    __m256d rT[4], rO[4], rD[4];
+    for (int i = 0; i < 4; ++i) {
+        const int e = es[i < n ? i : 0];
+        rT[i] = _mm256_loadu_pd(&vd[dst(oprev(e))].x);
+        rO[i] = _mm256_loadu_pd(&vd[org(e)].x);
+        rD[i] = _mm256_loadu_pd(&vd[dst(e)].x);
+    }
+    __m256d Tx, Ty, Tn, Ox, Oy, On, Dx, Dy, Dn;
+    transpose3(rT, Tx, Ty, Tn);
+    transpose3(rO, Ox, Oy, On);
+    transpose3(rD, Dx, Dy, Dn);
+    const __m256d Px = _mm256_set1_pd(P.x), Py = _mm256_set1_pd(P.y), Pn = _mm256_set1_pd(P.n2);
+    const __m256d aTDO = area4(Tx, Ty, Dx, Dy, Ox, Oy);
+    __m256d val = _mm256_mul_pd(Tn, area4(Dx, Dy, Px, Py, Ox, Oy));
+    val = _mm256_sub_pd(val, _mm256_mul_pd(Dn, area4(Tx, Ty, Px, Py, Ox, Oy)));
+    val = _mm256_add_pd(val, _mm256_mul_pd(Pn, aTDO));
+    val = _mm256_sub_pd(val, _mm256_mul_pd(On, area4(Tx, Ty, Dx, Dy, Px, Py)));
+    const __m256d right = _mm256_cmp_pd(aTDO, _mm256_setzero_pd(), _CMP_GT_OQ);
+    const __m256d inside = _mm256_cmp_pd(val, _mm256_set1_pd(-(FLT_EPSILON * 0.125)), _CMP_LT_OQ);
+    const int mask = _mm256_movemask_pd(_mm256_and_pd(right, inside));
+    for (int i = 0; i < n; ++i) out[i] = (mask >> i) & 1;
+}
+
 // Cavity form of an INSIDE insert (subdiv2d.h). e0 = locate's edge: p lies left of it, inside the
 // triangle (e0, Lnext e0, Lnext^2 e0). Returns false, having changed nothing but the scratch, when
 // the DFS cannot certify the cavity; the caller then runs the connects and the swap loop.
@@ -241,45 +306,72 @@ bool Subdiv2D::insert_cavity(int e0, int p) {
     auto area = [](const V2d &a, const V2d &b, const V2d &c) { return (b.x - a.x) * (c.y - a.y) - (b.y - a.y) * (c.x - a.x); };
     // scratch sized for the worst case: every swap adds one apex, one stacked edge and one boundary edge
     const size_t cap = vp.size() + 8;
-    if (dfs_stack.size() < cap) { dfs_stack.resize(2 * cap); cav_flip.resize(2 * cap); cav_apex.resize(2 * cap); cav_bnd.resize(2 * cap); }
+    if (dfs_stack.size() < cap) {
+        dfs_stack.resize(2 * cap); cav_flip.resize(2 * cap); cav_apex.resize(2 * cap); cav_bnd.resize(2 * cap);
+        cav_bu.resize(2 * cap); cav_bv.resize(2 * cap);
+    }
     int *stk = dfs_stack.data(), *fl = cav_flip.data(), *ap = cav_apex.data(), *bd = cav_bnd.data();
+    int *bu = cav_bu.data(), *bv = cav_bv.data();
     int sp = 0, nf = 0, nb = 0;
     stk[sp++] = e0; stk[sp++] = eB;
     int e = eA;
     // Pre-order walk; every test reads the old triangle right of the link edge (never incident to p).
-    // The first child (w -> v) is walked at once; the second (u -> w) waits on the stack.
+    // The first child (w -> v) is walked at once; the second (u -> w) waits on the stack. Once the walk
+    // reaches a boundary edge it pops the stacked edges, whose tests are independent of each other:
+    // they are evaluated four at a time (AVX2) until one swaps.
+    const bool simd = use_avx2;
+    int known = -1;   // 1: e is known to swap (decided in a batch)
     for (;;) {
-        const int t = oprev(e);
-        const int w = dst(t), u = org(e), v = dst(e);
-        const V2d &T = vd[w], &O = vd[u], &D = vd[v];
-        bool flip = false;
-        if (area(T, D, O) > 0) {   // same expression order as swap_loop
-            double val = T.n2 * area(D, P, O);
-            val -= D.n2 * area(T, P, O);
-            val += P.n2 * area(T, D, O);
-            val -= O.n2 * area(T, D, P);
-            flip = val < -(FLT_EPSILON * 0.125);
+        bool flip;
+        if (known == 1) {
+            flip = true;
+        } else {
+            const int t = oprev(e);
+            const V2d &T = vd[dst(t)], &O = vd[org(e)], &D = vd[dst(e)];
+            flip = false;
+            if (area(T, D, O) > 0) {   // same expression order as swap_loop
+                double val = T.n2 * area(D, P, O);
+                val -= D.n2 * area(T, P, O);
+                val += P.n2 * area(T, D, O);
+                val -= O.n2 * area(T, D, P);
+                flip = val < -(FLT_EPSILON * 0.125);
+            }
         }
+        known = -1;
         if (flip) {
+            const int t = oprev(e), w = dst(t);
             if (vstamp[w] == sA || w == p || nf + 4 >= (int)cap) return false;   // the cavity would wrap a vertex
             vstamp[w] = sA;
             vspoke[w] = e;                                   // e becomes w -> p
             fl[nf] = e; ap[nf] = w; ++nf;
             stk[sp++] = t;                                   // u -> w, after the w -> v subtree
             e = sym(onext(sym(e)));                          // w -> v
-        } else {
-            bd[nb++] = e;
-            if (sp == 0) break;
-            e = stk[--sp];
+            continue;
         }
+        bd[nb] = e; bu[nb] = org(e); bv[nb] = dst(e); ++nb;
+        if (simd) {
+            int d[4];
+            while (sp >= 4) {
+                const int b[4] = {stk[sp - 1], stk[sp - 2], stk[sp - 3], stk[sp - 4]};
+                flip_tests_avx2(b, 4, P, d);
+                int i = 0;
+                for (; i < 4 && !d[i]; ++i) {
+                    const int x = b[i];
+                    bd[nb] = x; bu[nb] = org(x); bv[nb] = dst(x); ++nb;
+                }
+                sp -= i;
+                if (i < 4) { known = 1; break; }
+            }
+        }
+        if (sp == 0) break;
+        e = stk[--sp];
     }
     const int m = nb;
     if (m != 3 + nf) return false;
-    int *xs = dfs_stack.data();   // the stack is empty now: reuse it for Org(L_k)
-    for (int k = 0; k < m; ++k) xs[k] = org(bd[k]);
+    const int *xs = bu;
     for (int k = 0; k < m; ++k) {   // the boundary closes: Org(L_k) = Dst(L_k+1), each vertex once
         const int x = xs[k];
-        if (dst(bd[k + 1 == m ? 0 : k + 1]) != x || vstamp[x] != sA) return false;
+        if (bv[k + 1 == m ? 0 : k + 1] != x || vstamp[x] != sA) return false;
         vstamp[x] = sUsed;
     }
 

@@ -43,12 +43,21 @@ namespace aos {
 
 class Subdiv2D {
   public:
+    Subdiv2D();
     // rect: Subdiv2D(Rect2f) (mode 0) or the implicit Rect2f -> Rect conversion (mode 1)
     void init_delaunay(float rx, float ry, float rw, float rh, int rect_mode);
     // Subdiv2D::insert; returns false where OpenCV throws (the reference catches and skips).
     bool insert(float x, float y);
     // 0: cavity DFS + bulk write (default); 1: always OpenCV's swap loop (reference / cross-check)
     void set_swap_loop(bool on) { force_loop = on; }
+    void set_simd(bool on) { use_avx2 = on && simd_ok(); }   // batched boundary flip tests on AVX2 (off by default)
+    static bool simd_ok() {
+#if defined(__x86_64__)
+        return __builtin_cpu_supports("avx2");
+#else
+        return false;
+#endif
+    }
     // full internal state (for the equivalence checker): rings, end points, firstEdge, recentEdge
     bool same_state(const Subdiv2D &o) const;
     long n_cavity = 0, n_loop = 0;   // inserts done by each path
@@ -76,10 +85,10 @@ class Subdiv2D {
     std::vector<int> vfirst, vtype;   // type: -1 free, 0 real, 1 virtual
     std::vector<int> qx;              // export buffer (Raw::qe)
     int free_q = 0, free_p = 0, recent = 0;
-    bool force_loop = false;
+    bool force_loop = false, use_avx2 = false;
     // cavity DFS scratch: stack of link edges, swapped edges with their apex, boundary edges in walk
-    // order, per-vertex spoke (valid while vstamp[v] == stamp)
-    std::vector<int> dfs_stack, cav_flip, cav_apex, cav_bnd, vspoke, vstamp;
+    // order (with their end points), per-vertex spoke (valid while vstamp[v] == stamp)
+    std::vector<int> dfs_stack, cav_flip, cav_apex, cav_bnd, cav_bu, cav_bv, vspoke, vstamp;
     int stamp = 0;
     float tlx = 0, tly = 0, brx = 0, bry = 0;
 
@@ -108,6 +117,8 @@ class Subdiv2D {
     void delete_edge(int e);
     int locate(float px, float py, int &edge, int &vertex);
     void swap_loop(int curr_edge, int first_point, int curr_point);
+    void flip_tests_scalar(const int *es, int n, const V2d &P, int *out) const;
+    void flip_tests_avx2(const int *es, int n, const V2d &P, int *out) const;
     bool insert_cavity(int e0, int curr_point);
     void calc_voronoi();   // calcVoronoi on the exported layout (qx), creating the virtual vertices
     int facet_next(int e) const;

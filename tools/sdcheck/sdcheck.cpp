@@ -23,10 +23,11 @@ static double uni() { return (splitmix() >> 11) * (1.0 / 9007199254740992.0); }
 
 struct Case { const char *name; std::vector<double> s; double b[4]; };
 
-static bool check(const Case &c, bool verbose) {
+static bool check(const Case &c, bool verbose, bool simd) {
     float rx = (float)(c.b[0] - 1.0), ry = (float)(c.b[2] - 1.0);
     float rw = (float)(std::abs(c.b[1] - c.b[0]) + 2.0), rh = (float)(std::abs(c.b[3] - c.b[2]) + 2.0);
     aos::Subdiv2D a, r;
+    a.set_simd(simd);
     r.set_swap_loop(true);
     const int n = (int)c.s.size() / 2;
     a.reserve(n); r.reserve(n);
@@ -50,7 +51,7 @@ static bool check(const Case &c, bool verbose) {
     return true;
 }
 
-static double time_inserts(const Case &c, bool loop, uint64_t &hash) {
+static double time_inserts(const Case &c, bool loop, bool simd, uint64_t &hash) {
     float rx = (float)(c.b[0] - 1.0), ry = (float)(c.b[2] - 1.0);
     float rw = (float)(std::abs(c.b[1] - c.b[0]) + 2.0), rh = (float)(std::abs(c.b[3] - c.b[2]) + 2.0);
     const int n = (int)c.s.size() / 2;
@@ -58,6 +59,7 @@ static double time_inserts(const Case &c, bool loop, uint64_t &hash) {
     for (int rep = 0; rep < 7; ++rep) {
         aos::Subdiv2D sd;
         sd.set_swap_loop(loop);
+        sd.set_simd(simd);
         sd.reserve(n);
         auto t0 = std::chrono::steady_clock::now();
         sd.init_delaunay(rx, ry, rw, rh, 0);
@@ -131,14 +133,19 @@ int main(int argc, char **argv) {
         cases.push_back(file);
     }
     int fails = 0;
-    for (size_t i = 0; i < cases.size(); ++i) fails += !check(cases[i], i < 6 || i + 1 == cases.size());
-    printf("%zu cases, %d failed\n", cases.size(), fails);
+    const bool simd = aos::Subdiv2D::simd_ok();
+    for (int pass = 0; pass < (simd ? 2 : 1); ++pass) {
+        for (size_t i = 0; i < cases.size(); ++i) fails += !check(cases[i], pass == 0 && (i < 6 || i + 1 == cases.size()), pass == 0 && simd);
+        printf("%zu cases (%s flip tests), %d failed so far\n", cases.size(), pass == 0 && simd ? "AVX2" : "scalar", fails);
+    }
     if (path) {
-        uint64_t ha = 0, hr = 0;
-        const double ta = time_inserts(file, false, ha), tr = time_inserts(file, true, hr);
-        printf("%s inserts: cavity %.2f ms, swap loop %.2f ms (x%.2f); facet-edge hash %016llx %s\n", path, ta, tr, tr / ta,
-               (unsigned long long)ha, ha == hr ? "equal" : "DIFFERENT");
-        if (ha != hr) fails++;
+        uint64_t ha = 0, hs = 0, hr = 0;
+        const double ta = time_inserts(file, false, simd, ha), ts = time_inserts(file, false, false, hs),
+                     tr = time_inserts(file, true, false, hr);
+        printf("%s inserts: cavity+%s %.2f ms, cavity+scalar %.2f ms, swap loop %.2f ms (x%.2f); facet-edge hash %016llx %s\n",
+               path, simd ? "AVX2" : "scalar", ta, ts, tr, tr / ta, (unsigned long long)ha,
+               ha == hr && hs == hr ? "equal" : "DIFFERENT");
+        if (ha != hr || hs != hr) fails++;
     }
     return fails ? 1 : 0;
 }
