@@ -89,26 +89,33 @@ def test_tiled_c1_equals_single_gpu(tiles, root):
     _assert_same(_single(cloud, poly, cfg.res), _tiled_threads(cloud, poly, cfg.res, *tiles, root))
 
 
-def test_tiled_c1_against_golden_hashes():
-    """2 x 2 tiles, every rank handed the whole cloud (points outside a tile's box are ignored):
-    the root's frame + GVD vs the SHA-256 of the oracle's outputs (tests/golden/c1_sha256.json)."""
+def _sha(a, dt):
+    a = np.ascontiguousarray(np.asarray(a, dtype=dt))
+    return hashlib.sha256(a.dtype.str.encode() + str(a.shape).encode() + a.tobytes()).hexdigest()
+
+
+def _assert_golden(name, g, gg):
+    """The root's frame + GVD vs the SHA-256 of the oracle's outputs (tests/golden/<name>_sha256.json,
+    tools/make_golden.py)."""
     here = os.path.dirname(os.path.abspath(__file__))
-    hs = json.load(open(os.path.join(here, "golden", "c1_sha256.json")))
-
-    def sha(a, dt):
-        a = np.ascontiguousarray(np.asarray(a, dtype=dt))
-        return hashlib.sha256(a.dtype.str.encode() + str(a.shape).encode() + a.tobytes()).hexdigest()
-
-    cfg = orchard.CONFIGS["C1"]
-    g, _, _, gg = _tiled_threads(orchard.generate(cfg), orchard.polygon(cfg), cfg.res, 2, 2, 0, shard=False)
+    hs = json.load(open(os.path.join(here, "golden", f"{name}_sha256.json")))
     assert g["thin_iters"] == hs["meta"]["thin_iters"] and g["n_clipped"] == hs["meta"]["n_clipped"]
     for k in ("occupancy", "skeleton_framed"):
-        assert sha(g[k], np.int8) == hs["seedgen"][k], k
+        assert _sha(g[k], np.int8) == hs["seedgen"][k], k
     for k in ("row_center", "row_start", "row_end", "row_length", "voronoi_seeds", "rows_info", "cluster_info"):
-        assert sha(g[k], np.float64) == hs["seedgen"][k], k
-    for k, dt in (("nodes", np.float64), ("edges", np.int32), ("edge_lengths", np.float32),
-                  ("node_labels", np.int32), ("node_label_clusters", np.int32)):
-        assert sha(gg[k], dt) == hs["gvd"][k], k
+        assert _sha(g[k], np.float64) == hs["seedgen"][k], k
+    for k, dt in (("merged", np.float64), ("nodes", np.float64), ("edges", np.int32), ("edge_lengths", np.float32),
+                  ("edge_clearances", np.float32), ("node_labels", np.int32), ("node_cluster_indices", np.int32),
+                  ("node_label_counts", np.int32), ("node_label_clusters", np.int32), ("node_label_types", np.int32)):
+        if k in gg:
+            assert _sha(gg[k], dt) == hs["gvd"][k], k
+
+
+def test_tiled_c1_against_golden_hashes():
+    """2 x 2 tiles, every rank handed the whole cloud (points outside a tile's box are ignored)."""
+    cfg = orchard.CONFIGS["C1"]
+    g, _, _, gg = _tiled_threads(orchard.generate(cfg), orchard.polygon(cfg), cfg.res, 2, 2, 0, shard=False)
+    _assert_golden("c1", g, gg)
 
 
 def _blob_scene():
@@ -162,6 +169,48 @@ def test_group_c1_equals_single_gpu(tiles, root, on_device):
     cfg = orchard.CONFIGS["C1"]
     cloud, poly = orchard.generate(cfg), orchard.polygon(cfg)
     _assert_same(_single(cloud, poly, cfg.res), _group(cloud, poly, cfg.res, *tiles, root, on_device=on_device))
+
+
+def test_group_c1_tiling_for_8_equals_single_gpu():
+    """The 8-rank split SURVEY §8e names (tiling_for(8) = 4 x 2 tiles) at C1 size, ranks on one GPU."""
+    cfg = orchard.CONFIGS["C1"]
+    tiles = T.tiling_for(8)
+    assert tiles == (4, 2)
+    cloud, poly = orchard.generate(cfg), orchard.polygon(cfg)
+    single = _single(cloud, poly, cfg.res)
+    _assert_same(single, _group(cloud, poly, cfg.res, *tiles, 5))
+    _assert_golden("c1", single[0], single[2])
+
+
+@pytest.fixture(scope="module")
+def c3_scene():
+    cfg = orchard.CONFIGS["C3"]
+    return cfg, orchard.generate(cfg), orchard.polygon(cfg)
+
+
+@pytest.fixture(scope="module")
+def c3_single(c3_scene):
+    cfg, cloud, poly = c3_scene
+    return _single(cloud, poly, cfg.res)
+
+
+def test_c3_single_gpu_against_golden(c3_single):
+    """BASELINE configs[3]'s map (40 M points, 8192^2 @ 0.1 m) as one frame on one GPU vs the oracle's
+    hashes (tests/golden/c3_sha256.json)."""
+    g, _, gg = c3_single
+    assert (g["width"], g["height"]) == (8192, 8192)
+    _assert_golden("c3", g, gg)
+
+
+def test_group_c3_tiling_for_8_vs_single_and_golden(c3_scene, c3_single):
+    """C3 through aos_group with the SURVEY §8e split (8 ranks, 4 x 2 tiles of 2048 columns x 4096 rows)
+    on one GPU: the root's grids, seeds and GvdGraph equal the single-GPU frame and the oracle's hashes."""
+    cfg, cloud, poly = c3_scene
+    tiles = T.tiling_for(8)
+    tiled = _group(cloud, poly, cfg.res, *tiles, 0)
+    _assert_same(c3_single, tiled)
+    g, _, _, gg = tiled
+    _assert_golden("c3", g, gg)
 
 
 def test_group_blob_vs_oracle_and_bad_cloud():
