@@ -28,6 +28,20 @@ struct aos_ctx {
     aos::DevBuf map_buf, scan_stage;
     uint64_t map_n = 0;
     int map_dense = 1;
+    // ---- tile store of the streaming map (incremental ROR, seedgen.hip ror_stage): the map's binned
+    // points partitioned by ROR tile (own + halo copies, ping-pong), tile starts, kept candidates per
+    // tile; valid while the geometry, density and raster bits are the ones it was built with
+    struct MapStore {
+        bool valid = false;
+        aos::RorLaunch L{};          // geometry it was built with (pointers / counts cleared)
+        aos::DevBuf st[2], ts[2], kept, scan_st, scan_H, scan_ts;
+        int cur = 0, dense = 1;
+        uint64_t n_points = 0;       // map points it covers
+        double n_binned = 0;         // binned (own) points it holds
+        size_t n_staged = 0;         // staged copies it holds
+        bool last_incremental = false;
+    } ms;
+    uint64_t map_scan_begin = 0;     // map points before the last aos_map_append
     // ---- hipGraph of the first thinning batch (opening + 3 launches + flags read-back), replayed
     // while the geometry and buffers stay the same (a streaming map keeps them)
     hipGraphExec_t thin_graph = nullptr;
@@ -105,6 +119,7 @@ struct aos_ctx {
     void map_append(const aos_cloud_view &scan);
     void ror_stage(const aos::FrameGeom &g, const RorOwn &o, uint64_t *rbits, bool allow_guess);
     bool ror_collect();   // after the stream synchronised: true if the ROR scatter overflowed
+    void ror_stage_append(aos::RorLaunch L, uint64_t *rbits);   // streaming map: one scan on the tile store
     void finish_frame(const aos::FrameGeom &g, bool want_host, const uint64_t *clipped_total, aos_seedgen_out &out);
     void run_seedgen(bool want_host, aos_seedgen_out &out);
     bool run_seedgen_once(bool want_host, aos_seedgen_out &out, bool allow_guess);   // true: redo

@@ -107,14 +107,19 @@ struct RorLaunch {
     int staged_cap; int *overflow;   // staged array capacity; set to 1 when the scatter exceeds it
 };
 constexpr int kRtMaxTiles = 36000;   // tiles per frame (LDS histogram of the partition passes: 144 KB)
-void rt_configure(RorLaunch &L, int Hr, int WWr, double est_binned);
+void rt_configure(RorLaunch &L, int Hr, int WWr, double est_binned, int force_tb = 0);
 int rt_part_blocks(const RorLaunch &L);   // G: workgroups (= cloud chunks) of the partition passes
 // H: G x ntiles ints (row per workgroup). The count pass leaves per-tile prefixes over the workgroups
 // in H and the tile totals in tot[0..ntiles); tstart = exclusive scan of tot (ntiles + 1 entries).
 void launch_rt_count(const RorLaunch &L, int *H, int G, int *tot, unsigned long long *n_own, hipStream_t s);
 void launch_rt_scatter(const RorLaunch &L, int *H, const int *tstart, int G, float4 *staged, hipStream_t s);
+// kept_tile (nullable): per-tile kept counts; dirty (nullable): a tile is counted iff dirty[t+1] > dirty[t]
 void launch_rt_ror(const RorLaunch &L, const int *tstart, const float4 *staged, float4 *scratch, uint64_t *rbits,
-                   unsigned long long *counters, hipStream_t s);
+                   unsigned long long *counters, int *kept_tile, const int *dirty, hipStream_t s);
+// streaming map: merge the map's tile store with a scan's partition; n_clipped from per-tile counts
+void launch_rt_merge(const float4 *old_st, const int *old_ts, const float4 *scan_st, const int *scan_ts, float4 *new_st,
+                     int *new_ts, int ntiles, hipStream_t s);
+void launch_rt_sum_kept(const int *kept_tile, int ntiles, unsigned long long *counters, hipStream_t s);
 // PointCloud2 records (any float32 x/y/z offsets) -> float4 (x, y, z, 0)
 void launch_pack_xyz(const uint8_t *cloud, uint64_t n, uint32_t step, uint32_t ox, uint32_t oy, uint32_t oz, float4 *out,
                      hipStream_t s);

@@ -143,6 +143,7 @@ int aos_map_reset(aos_ctx *c, uint64_t reserve_points) {
     AOS_GUARD_BEGIN
     DeviceScope dev_scope(c->device);
     c->map_n = 0;
+    c->ms.valid = false;
     c->map_dense = 1;
     if (reserve_points) c->map_buf.ensure(sizeof(float4) * reserve_points);
     return AOS_OK;

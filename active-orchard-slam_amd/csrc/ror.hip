@@ -235,17 +235,26 @@ __device__ __forceinline__ int rt_scan(const RorLaunch &L, float4 p, Pts pts, in
 // + ring: 34^2), and the tile's raster window (kRtWinWords 64-bit words): ~40 KB, 3 workgroups per CU
 constexpr int kRtMaxLocalBins = 34 * 34, kRtWinWords = 320;
 
+// kept_tile (optional): the tile's count of kept owned candidates; dirty (optional): only tiles with
+// dirty[t + 1] > dirty[t] are (re)counted — the streaming map's tiles that received scan points.
 __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *tstart, const float4 *staged,
                                                         float4 *scratch, uint64_t *rbits,
-                                                        unsigned long long *counters) {
+                                                        unsigned long long *counters, int *kept_tile,
+                                                        const int *dirty) {
     __shared__ float4 pts[kRorCap];
     __shared__ int bstart[kRtMaxLocalBins + 1];
     __shared__ unsigned long long win[kRtWinWords];
+    __shared__ unsigned kept_wg;
     const int tid = threadIdx.x;
     const int t = rt_xcd_block(blockIdx.x, gridDim.x);
     const int tx = t % L.ntx, ty = t / L.ntx;
+    if (dirty && dirty[t + 1] == dirty[t]) return;
     const int a = tstart[t], n = tstart[t + 1] - a;   // the tile's runs
-    if (n == 0 || a + n > L.staged_cap) return;   // (an overflowed scatter: the frame is redone)
+    if (n == 0 || a + n > L.staged_cap) {             // (an overflowed scatter: the frame is redone)
+        if (kept_tile && tid == 0) kept_tile[t] = 0;
+        return;
+    }
+    if (tid == 0) kept_wg = 0;
     const int LB = L.TB + 2;                        // local bins: the tile's bins and a ring of halo bins
     const int bx0 = tx * L.TB - 1, by0 = ty * L.TB - 1;
     const int nlb = LB * LB;
@@ -369,25 +378,63 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
                 atomicOr(reinterpret_cast<unsigned long long *>(&rbits[(size_t)r * L.WWr + w]), v);
         }
     for (int o = 32; o > 0; o >>= 1) kept_n += __shfl_xor(kept_n, o);
-    if ((tid & 63) == 0 && kept_n)
+    if ((tid & 63) == 0 && kept_n) {
         atomicAdd(&counters[(blockIdx.x * (kRorThreads / 64) + (tid >> 6)) & (kRorCounters - 1)],
                   (unsigned long long)kept_n);
+        if (kept_tile) atomicAdd(&kept_wg, kept_n);
+    }
+    if (kept_tile) {
+        __syncthreads();
+        if (tid == 0) kept_tile[t] = (int)kept_wg;
+    }
+}
+
+// Streaming map: the map's tile store (old) and the scan's partition (scan) -> the new store; per tile
+// the old run, then the scan's run. tstart_new[t] = old[t] + scan[t] for t <= ntiles.
+__global__ __launch_bounds__(256) void k_rt_merge(const float4 *old_st, const int *old_ts, const float4 *scan_st,
+                                                  const int *scan_ts, float4 *new_st, int *new_ts, int ntiles) {
+    const int t = blockIdx.x;
+    if (t > ntiles) return;
+    const int o0 = old_ts[t], s0 = scan_ts[t], d0 = o0 + s0;
+    if (threadIdx.x == 0) new_ts[t] = d0;
+    if (t == ntiles) return;
+    const int no = old_ts[t + 1] - o0, ns = scan_ts[t + 1] - s0;
+    for (int i = threadIdx.x; i < no; i += 256) new_st[d0 + i] = old_st[o0 + i];
+    for (int i = threadIdx.x; i < ns; i += 256) new_st[d0 + no + i] = scan_st[s0 + i];
+}
+
+// n_clipped of the streaming map = the sum of the tiles' kept counts (into counters[0])
+__global__ __launch_bounds__(1024) void k_rt_sum_kept(const int *kept_tile, int ntiles, unsigned long long *counters) {
+    __shared__ unsigned long long part[16];
+    unsigned long long v = 0;
+    for (int t = threadIdx.x; t < ntiles; t += 1024) v += (unsigned)kept_tile[t];
+    if (threadIdx.x > 0 && threadIdx.x < kRorCounters) counters[threadIdx.x] = 0;   // (pass 4's partial adds)
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long s = 0;
+        for (int i = 0; i < 16; ++i) s += part[i];
+        counters[0] = s;
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
 // est_binned: expected binned points (the previous frame's count, or a guess); it only sizes the
 // tiles (TB = 32 bins, or 16 where tiles would average more than ~1400 points) — results do not
 // depend on it.
-void rt_configure(RorLaunch &L, int Hr, int WWr, double est_binned) {
+void rt_configure(RorLaunch &L, int Hr, int WWr, double est_binned, int force_tb) {
     auto tiles = [&](int tb) {
         L.TB = tb;
         L.ntx = (L.nbx + tb - 1) / tb;
         L.nty = (L.nby + tb - 1) / tb;
         return (long long)L.ntx * L.nty;
     };
-    const double per32 = est_binned * 1.15 / (double)tiles(32);
-    if (!(per32 > 1400.0 && tiles(16) <= kRtMaxTiles)) {
-        tiles(32);
+    if (force_tb) {
+        tiles(force_tb);
+    } else {
+        const double per32 = est_binned * 1.15 / (double)tiles(32);
+        if (!(per32 > 1400.0 && tiles(16) <= kRtMaxTiles)) tiles(32);
     }
     if (tiles(L.TB) > kRtMaxTiles || (L.TB + 2) * (L.TB + 2) > kRtMaxLocalBins)
         throw std::runtime_error("ROR bin grid too large for the tile walk");
@@ -439,9 +486,20 @@ void launch_rt_scatter(const RorLaunch &L, int *H, const int *tstart, int G, flo
 }
 
 void launch_rt_ror(const RorLaunch &L, const int *tstart, const float4 *staged, float4 *scratch, uint64_t *rbits,
-                   unsigned long long *counters, hipStream_t s) {
-    if (!L.n || !L.ntiles) return;
-    k_rt_ror<<<L.ntiles, kRorThreads, 0, s>>>(L, tstart, staged, scratch, rbits, counters);
+                   unsigned long long *counters, int *kept_tile, const int *dirty, hipStream_t s) {
+    if (!L.ntiles) return;
+    k_rt_ror<<<L.ntiles, kRorThreads, 0, s>>>(L, tstart, staged, scratch, rbits, counters, kept_tile, dirty);
+    AOS_HIP(hipGetLastError());
+}
+
+void launch_rt_merge(const float4 *old_st, const int *old_ts, const float4 *scan_st, const int *scan_ts, float4 *new_st,
+                     int *new_ts, int ntiles, hipStream_t s) {
+    k_rt_merge<<<ntiles + 1, 256, 0, s>>>(old_st, old_ts, scan_st, scan_ts, new_st, new_ts, ntiles);
+    AOS_HIP(hipGetLastError());
+}
+
+void launch_rt_sum_kept(const int *kept_tile, int ntiles, unsigned long long *counters, hipStream_t s) {
+    k_rt_sum_kept<<<1, 1024, 0, s>>>(kept_tile, ntiles, counters);
     AOS_HIP(hipGetLastError());
 }
 

@@ -109,6 +109,7 @@ void aos_ctx::release_uploader() {
 // (aos_seedgen_reprocess then fails instead of reading a partly copied buffer).
 void aos_ctx::set_cloud(const aos_cloud_view &v) {
     have_cloud = false;
+    ms.valid = false;
     const uint8_t *dc;
     if (v.on_device) {
         dc = static_cast<const uint8_t *>(v.data);
@@ -146,6 +147,7 @@ void aos_ctx::map_append(const aos_cloud_view &v) {
         src = static_cast<const uint8_t *>(st);
     }
     launch_pack_xyz(src, n, v.point_step, v.off_x, v.off_y, v.off_z, map_buf.as<float4>() + map_n, s);
+    map_scan_begin = map_n;
     map_n += n;
     map_dense = map_dense && v.is_dense;
     n_points = map_n;
@@ -232,7 +234,20 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
     L.origin_x = g.origin_x; L.origin_y = g.origin_y; L.res = g.res; L.W = g.W; L.H = g.H;
     L.rx0 = o.rx0; L.ry0 = o.ry0; L.rx1 = o.rx1; L.ry1 = o.ry1; L.wx0 = o.wx0; L.wy0 = o.wy0; L.Wr = o.Wr;
     const int WWr = (o.Wr + 63) / 64;
-    rt_configure(L, o.Hr, WWr, ror_est_binned > 0 ? ror_est_binned : 0.5 * (double)n_points);
+    // the streaming map keeps a tile store across appends (its tile size stays fixed)
+    const bool map_mode = !o.limit_box && map_n > 0 && d_cloud == map_buf.as<uint8_t>() && n_points == map_n;
+    if (!map_mode) ms.valid = false;
+    ms.last_incremental = false;
+    rt_configure(L, o.Hr, WWr, ror_est_binned > 0 ? ror_est_binned : 0.5 * (double)n_points,
+                 map_mode && ms.valid ? ms.L.TB : 0);
+    auto geom_of = [](RorLaunch x) {
+        x.cloud = nullptr; x.n = 0; x.step = x.ox = x.oy = x.oz = 0; x.staged_cap = 0; x.overflow = nullptr;
+        return x;
+    };
+    if (map_mode && ms.valid && ms.dense == is_dense && ms.n_points == map_scan_begin && n_points > ms.n_points) {
+        const RorLaunch a = geom_of(L), b = ms.L;
+        if (!std::memcmp(&a, &b, sizeof(RorLaunch))) { ror_stage_append(L, rbits); return; }
+    }
     const int nt = L.ntiles;
     const int G = rt_part_blocks(L);
     const size_t nH = (size_t)nt * G;
@@ -240,6 +255,9 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
     int *d_H = static_cast<int *>(bin_count.ensure(sizeof(int) * nH));
     int *d_tot = static_cast<int *>(bin_start.ensure(sizeof(int) * 2 * (nt + 1)));
     int *d_ts = d_tot + (nt + 1);
+    if (map_mode) d_ts = static_cast<int *>(ms.ts[ms.cur].ensure(sizeof(int) * (nt + 1)));
+    int *d_kept = map_mode ? static_cast<int *>(ms.kept.ensure(sizeof(int) * nt)) : nullptr;
+    DevBuf &stage_buf = map_mode ? ms.st[ms.cur] : sorted;
     unsigned long long *d_cnt = static_cast<unsigned long long *>(counters.ensure(8 * kRorCounters + 16));
     unsigned long long *d_own = d_cnt + kRorCounters;   // [0] binned points, [1] overflow flag
     size_t st = scan_temp_bytes(nt + 1);
@@ -247,6 +265,8 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
     AOS_HIP(hipMemsetAsync(d_tot + nt, 0, sizeof(int), s));
     AOS_HIP(hipMemsetAsync(d_cnt, 0, 8 * kRorCounters + 16, s));
     AOS_HIP(hipMemsetAsync(rbits, 0, sizeof(uint64_t) * (size_t)o.Hr * WWr, s));
+    if (d_kept) AOS_HIP(hipMemsetAsync(d_kept, 0, sizeof(int) * nt, s));
+    ms.valid = false;
     // PCL dense kNN needs k = min_pts + 1 points in the whole cloud (else every point is removed).
     // A tile's shard holds every neighbour of its own candidates, so a shard with fewer points has
     // no keepable candidate either: the local test is exact.
@@ -261,36 +281,101 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
     // run_seedgen); without one, or when the caller cannot redo (a tiled frame), the size is read
     // back first.
     int *h = static_cast<int *>(h_stats.p);
-    const size_t cap_now = sorted.cap / sizeof(float4);
+    const size_t cap_now = stage_buf.cap / sizeof(float4);
     const bool guess = allow_guess && ror_staged_max > 0 && cap_now >= (size_t)(ror_staged_max * 1.1);
     if (!guess) {
         AOS_HIP(hipMemcpyAsync(h + 2, d_ts + nt, sizeof(int), hipMemcpyDeviceToHost, s));
         AOS_HIP(hipStreamSynchronize(s));
         const size_t need = (size_t)std::max(h[2], 1);
         ror_staged_max = std::max<double>(ror_staged_max, (double)need);
-        sorted.ensure(sizeof(float4) * (size_t)(need * 1.15 + 1024));
+        stage_buf.ensure(sizeof(float4) * (size_t)(need * 1.15 + 1024));
     }
-    float4 *d_staged = sorted.as<float4>();
-    L.staged_cap = (int)std::min<size_t>(sorted.cap / sizeof(float4), (size_t)INT_MAX);
+    float4 *d_staged = stage_buf.as<float4>();
+    L.staged_cap = (int)std::min<size_t>(stage_buf.cap / sizeof(float4), (size_t)INT_MAX);
     float4 *d_scratch = static_cast<float4 *>(ror_scratch.ensure(sizeof(float4) * (size_t)L.staged_cap));
     L.overflow = reinterpret_cast<int *>(d_own + 1);
     AOS_HIP(hipEventRecord(ev[14], s));
     launch_rt_scatter(L, d_H, d_ts, G, d_staged, s);
     AOS_HIP(hipEventRecord(ev[10], s));
-    launch_rt_ror(L, d_ts, d_staged, d_scratch, rbits, d_cnt, s);
+    launch_rt_ror(L, d_ts, d_staged, d_scratch, rbits, d_cnt, d_kept, nullptr, s);
     AOS_HIP(hipEventRecord(ev[11], s));
     // binned points, staged total, overflow flag: read with the frame's other stats (finish_frame)
     AOS_HIP(hipMemcpyAsync(h + 2, d_ts + nt, sizeof(int), hipMemcpyDeviceToHost, s));
     AOS_HIP(hipMemcpyAsync(h + 4, d_own, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    if (map_mode) {   // the store holds the whole map now (confirmed by ror_collect: no overflow)
+        ms.valid = true;
+        ms.L = geom_of(L);
+        ms.dense = is_dense;
+        ms.n_points = n_points;
+    }
+}
+
+// Streaming map, one appended scan: the keep decision is monotone in the point set
+// (adding points only adds neighbours: PCL's kNN distance can only shrink, a radius count only grow),
+// and a candidate's neighbours all sit in its own tile's list. So only the scan is partitioned; each
+// tile's list becomes old run + scan run (k_rt_merge); only tiles that received scan points (own or
+// halo copies) are recounted, OR-ing into the raster bits the map already has; the kept count is the
+// sum of the per-tile counts. Equal to reprocessing the whole map (tests/test_gpu_stream.py).
+void aos_ctx::ror_stage_append(RorLaunch L, uint64_t *rbits) {
+    hipStream_t s = stream;
+    const int nt = L.ntiles;
+    const uint64_t scan_n = n_points - ms.n_points;
+    RorLaunch Ls = L;   // the scan's float4 records in the map buffer
+    Ls.cloud = map_buf.as<uint8_t>() + sizeof(float4) * ms.n_points;
+    Ls.n = scan_n; Ls.step = 16; Ls.ox = 0; Ls.oy = 4; Ls.oz = 8;
+    const int G = rt_part_blocks(Ls);
+    int *d_H = static_cast<int *>(ms.scan_H.ensure(sizeof(int) * (size_t)nt * G));
+    int *d_tot = static_cast<int *>(bin_start.ensure(sizeof(int) * 2 * (nt + 1)));
+    int *d_sts = static_cast<int *>(ms.scan_ts.ensure(sizeof(int) * (nt + 1)));
+    unsigned long long *d_cnt = static_cast<unsigned long long *>(counters.ensure(8 * kRorCounters + 16));
+    unsigned long long *d_own = d_cnt + kRorCounters;
+    size_t st = scan_temp_bytes(nt + 1);
+    void *d_st = scan_tmp.ensure(st);
+    // a point lands in at most 4 tiles: the scan's staging and the merged store cannot overflow
+    const size_t scan_cap = 4 * (size_t)scan_n + 1024;
+    float4 *d_scan = static_cast<float4 *>(ms.scan_st.ensure(sizeof(float4) * scan_cap));
+    const int nxt = ms.cur ^ 1;
+    const size_t cap = ms.n_staged + scan_cap;
+    if (cap > (size_t)INT_MAX) throw std::runtime_error("streaming map: ROR store exceeds 2^31 points");
+    float4 *d_new = static_cast<float4 *>(ms.st[nxt].ensure(sizeof(float4) * cap));
+    int *d_nts = static_cast<int *>(ms.ts[nxt].ensure(sizeof(int) * (nt + 1)));
+    float4 *d_scratch = static_cast<float4 *>(ror_scratch.ensure(sizeof(float4) * cap));
+    AOS_HIP(hipMemsetAsync(d_tot + nt, 0, sizeof(int), s));
+    AOS_HIP(hipMemsetAsync(d_cnt, 0, 8 * kRorCounters + 16, s));
+    Ls.staged_cap = (int)scan_cap;
+    Ls.overflow = reinterpret_cast<int *>(d_own + 1);
+    AOS_HIP(hipEventRecord(ev[12], s));
+    launch_rt_count(Ls, d_H, G, d_tot, d_own, s);
+    AOS_HIP(hipEventRecord(ev[13], s));
+    launch_exclusive_scan(d_tot, d_sts, nt + 1, d_st, st, s);
+    AOS_HIP(hipEventRecord(ev[14], s));
+    launch_rt_scatter(Ls, d_H, d_sts, G, d_scan, s);
+    AOS_HIP(hipEventRecord(ev[10], s));
+    launch_rt_merge(ms.st[ms.cur].as<float4>(), ms.ts[ms.cur].as<int>(), d_scan, d_sts, d_new, d_nts, nt, s);
+    L.staged_cap = (int)cap;
+    L.overflow = Ls.overflow;
+    launch_rt_ror(L, d_nts, d_new, d_scratch, rbits, d_cnt, ms.kept.as<int>(), d_sts, s);
+    launch_rt_sum_kept(ms.kept.as<int>(), nt, d_cnt, s);
+    AOS_HIP(hipEventRecord(ev[11], s));
+    int *h = static_cast<int *>(h_stats.p);
+    AOS_HIP(hipMemcpyAsync(h + 2, d_nts + nt, sizeof(int), hipMemcpyDeviceToHost, s));
+    AOS_HIP(hipMemcpyAsync(h + 4, d_own, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    ms.cur = nxt;
+    ms.n_points = n_points;
+    ms.last_incremental = true;
 }
 
 // After the frame's sync: binned count, staged size, and whether the scatter overflowed its guess.
 bool aos_ctx::ror_collect() {
     int *h = static_cast<int *>(h_stats.p);
     const unsigned long long *u = reinterpret_cast<const unsigned long long *>(h + 4);
-    h[0] = (int)u[0];
-    ror_est_binned = (double)u[0];
+    double binned = (double)u[0];
+    if (ms.last_incremental) binned += ms.n_binned;   // the scan's binned points on top of the map's
+    h[0] = (int)binned;
+    ror_est_binned = binned;
     ror_staged_max = std::max<double>(ror_staged_max, (double)h[2]);
+    if (ms.valid) { ms.n_binned = binned; ms.n_staged = (size_t)h[2]; }
+    if (u[1] != 0) ms.valid = false;
     return u[1] != 0;
 }
 

@@ -63,3 +63,40 @@ def test_stream_custom_layout_and_non_dense_scan():
     g2 = s.map_append(a)
     assert_seedgen_parity(g2, O.seedgen(a, poly, O.default_params(grid_resolution=cfg.res)))
     s.close()
+
+
+def test_stream_c2_map_20_scans_incremental_equals_full_reprocessing():
+    """BASELINE configs[4] at full size: the C2 map (10 M points) then 20 scans of 1 M points. From the
+    second frame on each append only partitions the scan and recounts the tiles it reached (the
+    incremental ROR, seedgen.hip ror_stage_append); every frame must equal reprocessing the whole
+    concatenated cloud (grids, counts, rows, seeds), and the GvdGraph every fourth scan."""
+    import torch
+    cfg = orchard.CONFIGS["C2"]
+    poly = orchard.polygon(cfg)
+    base = orchard.generate(cfg)
+    n_scans = 20
+    s = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res))
+    s.set_polygon(poly)
+    s.map_reset(reserve_points=base.shape[0] + n_scans * orchard.SCAN_POINTS)
+    ref = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res))
+    ref.set_polygon(poly)
+    g = s.map_append(base)
+    full = torch.from_numpy(base).to("cuda:0")
+    ror_inc, ror_full = [], []
+    for k in range(n_scans):
+        scan = orchard.generate_scan(cfg, 40 * k)
+        g = s.map_append(scan)
+        full = torch.cat([full, torch.from_numpy(scan).to("cuda:0")])
+        r = ref.seedgen(full.data_ptr(), n_points=full.shape[0], on_device=True)
+        assert_seedgen_parity(g, {**r, "cluster_length": np.zeros(r["n_clusters_all"])})
+        assert (g["n_clipped"], g["n_binned"], g["n_input"]) == (r["n_clipped"], r["n_binned"], full.shape[0]), k
+        ror_inc.append(g["ms"]["ror"])
+        ror_full.append(r["ms"]["ror"])
+        if k % 4 == 3 or k == n_scans - 1:
+            gg, rg = s.gvd_from_seedgen(), ref.gvd_from_seedgen()
+            for key in GVD_KEYS:
+                assert np.array_equal(gg[key], rg[key]), (k, key)
+    # the appends do not reprocess the map: their ROR stage stays well below the whole-map one
+    assert np.median(ror_inc) < 0.5 * np.median(ror_full), (ror_inc, ror_full)
+    s.close()
+    ref.close()

@@ -125,7 +125,7 @@ int main(int argc, char **argv) {
         AOS_HIP(hipEventRecord(e[3], s));
         launch_rt_scatter(L, d_H, d_ts, G, d_staged, s);
         AOS_HIP(hipEventRecord(e[4], s));
-        launch_rt_ror(L, d_ts, d_staged, d_scr, d_bits, d_cnt, s);
+        launch_rt_ror(L, d_ts, d_staged, d_scr, d_bits, d_cnt, nullptr, nullptr, s);
         AOS_HIP(hipEventRecord(e[5], s));
         AOS_HIP(hipStreamSynchronize(s));
         float t[5];
