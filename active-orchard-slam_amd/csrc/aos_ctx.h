@@ -42,14 +42,9 @@ struct aos_ctx {
         bool last_incremental = false;
     } ms;
     uint64_t map_scan_begin = 0;     // map points before the last aos_map_append
-    // ---- hipGraph of the first thinning batch (opening + 3 launches + flags read-back), replayed
-    // while the geometry and buffers stay the same (a streaming map keeps them)
-    hipGraphExec_t thin_graph = nullptr;
-    std::array<const void *, 6> thin_graph_key{};
-    int thin_graph_dims[3] = {-1, -1, -1};
 
     // ---- device buffers
-    aos::DevBuf cloud_copy, bin_count, bin_start, pt_binslot, sorted, ror_scratch, scan_tmp, counters;
+    aos::DevBuf cloud_copy, bin_count, bin_start, pt_binslot, sorted, ror_scratch, ror_bigbins, scan_tmp, counters;
     aos::DevBuf raster_bits, infl_bits, open_bits, thin_a, thin_b, occ_bytes, skel_bytes, flags;
     aos::DevBuf full_infl, full_skel;      // tiled frames: the whole map, assembled on the root rank
     aos::PinnedBuf h_small, h_stats;

@@ -114,8 +114,12 @@ int rt_part_blocks(const RorLaunch &L);   // G: workgroups (= cloud chunks) of t
 void launch_rt_count(const RorLaunch &L, int *H, int G, int *tot, unsigned long long *n_own, hipStream_t s);
 void launch_rt_scatter(const RorLaunch &L, int *H, const int *tstart, int G, float4 *staged, hipStream_t s);
 // kept_tile (nullable): per-tile kept counts; dirty (nullable): a tile is counted iff dirty[t+1] > dirty[t]
-void launch_rt_ror(const RorLaunch &L, const int *tstart, const float4 *staged, float4 *scratch, uint64_t *rbits,
-                   unsigned long long *counters, int *kept_tile, const int *dirty, hipStream_t s);
+// scratch: staged-sized; bigbins: rt_bigbins_ints(L) ints (tiles beyond the LDS capacity are sorted there)
+size_t rt_bigbins_ints(const RorLaunch &L);
+// kept_tile != nullptr (a streaming map's store): kept candidates are marked (w = 2) in staged, which
+// is rewritten bin-sorted per tile
+void launch_rt_ror(const RorLaunch &L, const int *tstart, float4 *staged, float4 *scratch, int *bigbins,
+                   uint64_t *rbits, unsigned long long *counters, int *kept_tile, const int *dirty, hipStream_t s);
 // streaming map: merge the map's tile store with a scan's partition; n_clipped from per-tile counts
 void launch_rt_merge(const float4 *old_st, const int *old_ts, const float4 *scan_st, const int *scan_ts, float4 *new_st,
                      int *new_ts, int ntiles, hipStream_t s);

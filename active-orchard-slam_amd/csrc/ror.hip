@@ -235,12 +235,45 @@ __device__ __forceinline__ int rt_scan(const RorLaunch &L, float4 p, Pts pts, in
 // + ring: 34^2), and the tile's raster window (kRtWinWords 64-bit words): ~40 KB, 3 workgroups per CU
 constexpr int kRtMaxLocalBins = 34 * 34, kRtWinWords = 320;
 
+// Tiles with more than kRorCap points (a streaming map's scan footprint): counting sort by bin into the
+// tile's range of the scratch array, bin offsets to bigbins[t * (nlb + 1) ...]. A separate launch, so
+// k_rt_ror reads both through a kernel boundary (a workgroup must not re-read global data it wrote
+// itself in the same launch: the CU's vector L1 may hold stale lines of that range).
+__global__ __launch_bounds__(kRorThreads) void k_rt_bigsort(RorLaunch L, const int *tstart, const float4 *staged,
+                                                            float4 *scratch, int *bigbins, const int *dirty) {
+    __shared__ int bstart[kRtMaxLocalBins + 1];
+    const int tid = threadIdx.x, t = blockIdx.x;
+    if (dirty && dirty[t + 1] == dirty[t]) return;
+    const int a = tstart[t], n = tstart[t + 1] - a;
+    if (n <= kRorCap || a + n > L.staged_cap) return;
+    const int tx = t % L.ntx, ty = t / L.ntx;
+    const int LB = L.TB + 2, nlb = LB * LB, bx0 = tx * L.TB - 1, by0 = ty * L.TB - 1;
+    auto lbin = [&](float4 q) {
+        int bx, by;
+        rt_bin(L, q.x, q.y, bx, by);
+        return (by - by0) * LB + (bx - bx0);
+    };
+    for (int i = tid; i <= nlb; i += kRorThreads) bstart[i] = 0;
+    __syncthreads();
+    for (int k = tid; k < n; k += kRorThreads) atomicAdd(&bstart[lbin(staged[a + k]) + 1], 1);
+    __syncthreads();
+    if (tid == 0)   // (rare tiles: a serial scan is fine)
+        for (int i = 1; i <= nlb; ++i) bstart[i] += bstart[i - 1];
+    __syncthreads();
+    for (int i = tid; i <= nlb; i += kRorThreads) bigbins[(size_t)t * (nlb + 1) + i] = bstart[i];
+    __syncthreads();
+    for (int k = tid; k < n; k += kRorThreads) {   // bstart becomes the cursor
+        const float4 v = staged[a + k];
+        scratch[a + atomicAdd(&bstart[lbin(v)], 1)] = v;
+    }
+}
+
 // kept_tile (optional): the tile's count of kept owned candidates; dirty (optional): only tiles with
 // dirty[t + 1] > dirty[t] are (re)counted — the streaming map's tiles that received scan points.
-__global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *tstart, const float4 *staged,
+__global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *tstart, float4 *staged,
                                                         float4 *scratch, uint64_t *rbits,
                                                         unsigned long long *counters, int *kept_tile,
-                                                        const int *dirty) {
+                                                        const int *dirty, const int *bigbins) {
     __shared__ float4 pts[kRorCap];
     __shared__ int bstart[kRtMaxLocalBins + 1];
     __shared__ unsigned long long win[kRtWinWords];
@@ -288,10 +321,12 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
             }
         }
     } else {
-        for (int k = tid; k < n; k += kRorThreads) atomicAdd(&bstart[lbin(staged[a + k]) + 1], 1);
+        // too many points for LDS: k_rt_bigsort (the launch before) placed them bin-sorted in the tile's
+        // range of the scratch array and left the bin offsets in bigbins
+        for (int i = tid; i <= nlb; i += kRorThreads) bstart[i] = bigbins[(size_t)t * (nlb + 1) + i];
     }
     __syncthreads();
-    {   // exclusive bin offsets: bstart[b] = points in bins < b. Thread t sums a run of kSeg bins,
+    if (fits) {   // exclusive bin offsets: bstart[b] = points in bins < b. Thread t sums a run of kSeg bins,
         // one block scan over the 256 run totals, then each run is written back.
         constexpr int kSeg = (kRtMaxLocalBins + kRorThreads - 1) / kRorThreads;
         typedef hipcub::BlockScan<int, kRorThreads> Scan;
@@ -314,32 +349,28 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
         }
     }
     __syncthreads();
-    const float4 *P;
+    const float4 *P = scratch + a;
     if (fits) {
 #pragma unroll
         for (int j = 0; j < kRorPer; ++j)
             if (rk[j] >= 0) pts[bstart[lbin(q[j])] + rk[j]] = q[j];
-        P = pts;
-    } else {
-        // too many points for LDS: place them in the tile's range of the global scratch (L2-resident
-        // for one tile) with a cursor per bin, then scan from there
-        float4 *S = scratch + a;
-        __syncthreads();
-        int *cur = reinterpret_cast<int *>(pts);   // reuse LDS as the cursors (nlb + 1 <= kRorCap * 4)
-        for (int i = tid; i <= nlb; i += kRorThreads) cur[i] = bstart[i];
-        __syncthreads();
-        for (int k = tid; k < n; k += kRorThreads) {
-            const float4 v = staged[a + k];
-            S[atomicAdd(&cur[lbin(v)], 1)] = v;
-        }
-        __threadfence();
-        P = S;
     }
     __syncthreads();
     unsigned kept_n = 0;
+    // w: 0 a neighbour only, 1 a candidate, 2 a candidate a streaming map already found kept (the keep
+    // decision is monotone as points are added: it stays kept, its cell is already in the raster)
+    const bool store = kept_tile != nullptr;
     for (int k = tid; k < n; k += kRorThreads) {
         const float4 p = fits ? pts[k] : P[k];
-        if (!__float_as_int(p.w)) continue;     // neighbour only
+        const int w = __float_as_int(p.w);
+        if (!w) continue;                       // neighbour only
+        if (w == 2) {                           // kept in an earlier frame: counted, not re-tested
+            const int gx = (int)(((double)p.x - L.origin_x) / (double)L.res);
+            const int gy = (int)(((double)p.y - L.origin_y) / (double)L.res);
+            const int cx = min(max(gx, 0), L.W - 1), cy = min(max(gy, 0), L.H - 1);
+            if (cx >= L.rx0 && cx < L.rx1 && cy >= L.ry0 && cy < L.ry1) ++kept_n;
+            continue;
+        }
         int bx, by;
         rt_bin(L, p.x, p.y, bx, by);
         const int lx = bx - bx0, ly = by - by0;
@@ -353,6 +384,10 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
                        : rt_scan(L, p, P, bstart[r0], bstart[r0 + 3], cnt);
         }
         if (cnt < L.need) continue;
+        if (store) {   // remembered in the tile store (written back below)
+            if (fits) pts[k].w = __int_as_float(2);
+            else const_cast<float4 *>(P)[k].w = __int_as_float(2);
+        }
         // kept: counted iff its clamped cell is owned, rastered iff inside the grid (seed_gen:606-619)
         const int gx = (int)(((double)p.x - L.origin_x) / (double)L.res);
         const int gy = (int)(((double)p.y - L.origin_y) / (double)L.res);
@@ -368,6 +403,8 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
         else
             atomicOr(reinterpret_cast<unsigned long long *>(&rbits[(size_t)r * L.WWr + (bxw >> 6)]), bit);
     }
+    if (store)   // the tile's list goes back bin-sorted with its kept marks (each k by the thread that marked it)
+        for (int k = tid; k < n; k += kRorThreads) staged[a + k] = fits ? pts[k] : P[k];
     __syncthreads();
     if (use_win)
         for (int i = tid; i < L.win_rows * L.win_w; i += kRorThreads) {
@@ -485,10 +522,13 @@ void launch_rt_scatter(const RorLaunch &L, int *H, const int *tstart, int G, flo
     else rt_part<true, false>(L, H, tstart, G, staged, nullptr, s);
 }
 
-void launch_rt_ror(const RorLaunch &L, const int *tstart, const float4 *staged, float4 *scratch, uint64_t *rbits,
-                   unsigned long long *counters, int *kept_tile, const int *dirty, hipStream_t s) {
+size_t rt_bigbins_ints(const RorLaunch &L) { return (size_t)L.ntiles * ((L.TB + 2) * (L.TB + 2) + 1); }
+
+void launch_rt_ror(const RorLaunch &L, const int *tstart, float4 *staged, float4 *scratch, int *bigbins,
+                   uint64_t *rbits, unsigned long long *counters, int *kept_tile, const int *dirty, hipStream_t s) {
     if (!L.ntiles) return;
-    k_rt_ror<<<L.ntiles, kRorThreads, 0, s>>>(L, tstart, staged, scratch, rbits, counters, kept_tile, dirty);
+    k_rt_bigsort<<<L.ntiles, kRorThreads, 0, s>>>(L, tstart, staged, scratch, bigbins, dirty);
+    k_rt_ror<<<L.ntiles, kRorThreads, 0, s>>>(L, tstart, staged, scratch, rbits, counters, kept_tile, dirty, bigbins);
     AOS_HIP(hipGetLastError());
 }
 

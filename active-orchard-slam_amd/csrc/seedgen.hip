@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <climits>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <exception>
 #include <thread>
@@ -14,11 +15,10 @@
 using namespace aos;
 
 void aos_ctx::release() {
-    for (DevBuf *b : {&cloud_copy, &bin_count, &bin_start, &pt_binslot, &sorted, &ror_scratch, &scan_tmp, &counters,
+    for (DevBuf *b : {&cloud_copy, &bin_count, &bin_start, &pt_binslot, &sorted, &ror_scratch, &ror_bigbins, &scan_tmp, &counters,
                       &raster_bits, &infl_bits, &open_bits, &thin_a, &thin_b, &occ_bytes, &skel_bytes, &flags,
                       &full_infl, &full_skel, &map_buf, &scan_stage})
         b->release();
-    if (thin_graph) { (void)hipGraphExecDestroy(thin_graph); thin_graph = nullptr; }
     h_small.release();
     h_stats.release();
     h_occ.release();
@@ -297,7 +297,8 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
     AOS_HIP(hipEventRecord(ev[14], s));
     launch_rt_scatter(L, d_H, d_ts, G, d_staged, s);
     AOS_HIP(hipEventRecord(ev[10], s));
-    launch_rt_ror(L, d_ts, d_staged, d_scratch, rbits, d_cnt, d_kept, nullptr, s);
+    int *d_big = static_cast<int *>(ror_bigbins.ensure(sizeof(int) * rt_bigbins_ints(L)));
+    launch_rt_ror(L, d_ts, d_staged, d_scratch, d_big, rbits, d_cnt, d_kept, nullptr, s);
     AOS_HIP(hipEventRecord(ev[11], s));
     // binned points, staged total, overflow flag: read with the frame's other stats (finish_frame)
     AOS_HIP(hipMemcpyAsync(h + 2, d_ts + nt, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -354,7 +355,8 @@ void aos_ctx::ror_stage_append(RorLaunch L, uint64_t *rbits) {
     launch_rt_merge(ms.st[ms.cur].as<float4>(), ms.ts[ms.cur].as<int>(), d_scan, d_sts, d_new, d_nts, nt, s);
     L.staged_cap = (int)cap;
     L.overflow = Ls.overflow;
-    launch_rt_ror(L, d_nts, d_new, d_scratch, rbits, d_cnt, ms.kept.as<int>(), d_sts, s);
+    int *d_big = static_cast<int *>(ror_bigbins.ensure(sizeof(int) * rt_bigbins_ints(L)));
+    launch_rt_ror(L, d_nts, d_new, d_scratch, d_big, rbits, d_cnt, ms.kept.as<int>(), d_sts, s);
     launch_rt_sum_kept(ms.kept.as<int>(), nt, d_cnt, s);
     AOS_HIP(hipEventRecord(ev[11], s));
     int *h = static_cast<int *>(h_stats.p);
@@ -417,35 +419,19 @@ bool aos_ctx::run_seedgen_once(bool want_host, aos_seedgen_out &out, bool allow_
     const int K = kThinItersPerLaunch;
     const int max_iters = std::max(g.W, g.H) + 4;   // Zhang-Suen removes >= 1 cell per changing iteration
     int *d_flags = static_cast<int *>(flags.ensure(sizeof(int) * (2 + max_iters + K)));
-    AOS_HIP(hipMemsetAsync(d_flags, 0, sizeof(int) * (2 + max_iters + K), s));
     int *h_flags = static_cast<int *>(h_small.ensure(sizeof(int) * (2 + max_iters + K)));
     const ThinOwn whole{0, g.H, 0, g.WW, 1};
-    // first batch: opening + 3 temporal blocks + flags read-back (typical T <= 24 needs no more). It
-    // is a fixed sequence on fixed buffers, so it is captured once into a hipGraph and replayed while
-    // the geometry and buffers are unchanged (every frame of a streaming map).
-    auto first_batch = [&]() {
-        AOS_HIP(hipMemsetAsync(d_flags, 0, sizeof(int) * (2 + max_iters + K), s));
-        launch_open(d_ibits, d_open, g, s);
-        launch_thin_block(d_open, bufs[0], g, 0, d_flags, whole, s);
-        launch_thin_block(bufs[0], bufs[1], g, K, d_flags, whole, s);
-        launch_thin_block(bufs[1], bufs[0], g, 2 * K, d_flags, whole, s);
-        AOS_HIP(hipMemcpyAsync(h_flags, d_flags, sizeof(int) * (1 + 3 * K), hipMemcpyDeviceToHost, s));
-    };
-    const std::array<const void *, 6> key{d_ibits, d_open, bufs[0], bufs[1], d_flags, h_flags};
-    if (!thin_graph || key != thin_graph_key || thin_graph_dims[0] != g.W || thin_graph_dims[1] != g.H ||
-        thin_graph_dims[2] != g.R) {
-        if (thin_graph) { AOS_HIP(hipGraphExecDestroy(thin_graph)); thin_graph = nullptr; }
-        hipGraph_t graph = nullptr;
-        AOS_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-        first_batch();
-        AOS_HIP(hipStreamEndCapture(s, &graph));
-        const hipError_t e = hipGraphInstantiate(&thin_graph, graph, nullptr, nullptr, 0);
-        (void)hipGraphDestroy(graph);
-        AOS_HIP(e);
-        thin_graph_key = key;
-        thin_graph_dims[0] = g.W; thin_graph_dims[1] = g.H; thin_graph_dims[2] = g.R;
-    }
-    AOS_HIP(hipGraphLaunch(thin_graph, s));
+    // first batch: opening + 3 temporal blocks (typical T <= 24 needs no more), then the flags read-back.
+    // (Round 1 replayed this batch as a hipGraph captured on the first frame. On ROCm 7.2 a replay on a
+    // later frame with new data left garbage in the flags buffer in some frame sequences — the
+    // thinning count then ran to the iteration cap while the grids stayed right; repro:
+    // tools/dbg_stream7.py. Five plain launches cost a few microseconds, so they are issued directly.)
+    AOS_HIP(hipMemsetAsync(d_flags, 0, sizeof(int) * (2 + max_iters + K), s));
+    launch_open(d_ibits, d_open, g, s);
+    launch_thin_block(d_open, bufs[0], g, 0, d_flags, whole, s);
+    launch_thin_block(bufs[0], bufs[1], g, K, d_flags, whole, s);
+    launch_thin_block(bufs[1], bufs[0], g, 2 * K, d_flags, whole, s);
+    AOS_HIP(hipMemcpyAsync(h_flags, d_flags, sizeof(int) * (1 + 3 * K), hipMemcpyDeviceToHost, s));
     int launched = 3;
     const uint64_t *src = bufs[0];
     const uint64_t *final_buf = d_open;

@@ -87,7 +87,7 @@ int main(int argc, char **argv) {
     hipEvent_t e[6];
     for (auto &x : e) AOS_HIP(hipEventCreate(&x));
     int *d_H = nullptr, *d_tot = nullptr; void *d_st = nullptr; float4 *d_staged = nullptr, *d_scr = nullptr;
-    unsigned long long *d_cnt; uint64_t *d_bits;
+    unsigned long long *d_cnt; uint64_t *d_bits; int *d_big = nullptr; size_t cap_big = 0;
     AOS_HIP(hipMalloc(&d_cnt, 8 * (kRorCounters + 2)));
     AOS_HIP(hipMalloc(&d_bits, 8ull * WW * H));
     size_t cap_H = 0, cap_st = 0, cap_staged = 0, cap_t = 0;
@@ -125,7 +125,8 @@ int main(int argc, char **argv) {
         AOS_HIP(hipEventRecord(e[3], s));
         launch_rt_scatter(L, d_H, d_ts, G, d_staged, s);
         AOS_HIP(hipEventRecord(e[4], s));
-        launch_rt_ror(L, d_ts, d_staged, d_scr, d_bits, d_cnt, nullptr, nullptr, s);
+        if (rt_bigbins_ints(L) > cap_big) { if (d_big) AOS_HIP(hipFree(d_big)); cap_big = rt_bigbins_ints(L); AOS_HIP(hipMalloc(&d_big, 4 * cap_big)); }
+        launch_rt_ror(L, d_ts, d_staged, d_scr, d_big, d_bits, d_cnt, nullptr, nullptr, s);
         AOS_HIP(hipEventRecord(e[5], s));
         AOS_HIP(hipStreamSynchronize(s));
         float t[5];
