@@ -62,7 +62,7 @@ struct aos_ctx {
     const uint64_t *skel_bits = nullptr;   // final thinning buffer (thin_a / thin_b, or full_skel)
     aos::FrameGeom geom{};                 // the whole map
     bool tiled_frame = false;
-    int thin_iters = 0;
+    int thin_iters = 0, thin_iters_prev = 0;   // (the previous frame's T sizes the first thinning batch)
     uint64_t n_ror_kept = 0, n_clipped = 0;
     double ror_est_binned = 0;             // binned points of the last frame (sizes the ROR tiles)
     double ror_staged_max = 0;             // largest staged (own + halo) count seen (sizes the scatter)

@@ -426,26 +426,25 @@ bool aos_ctx::run_seedgen_once(bool want_host, aos_seedgen_out &out, bool allow_
     // later frame with new data left garbage in the flags buffer in some frame sequences — the
     // thinning count then ran to the iteration cap while the grids stayed right; repro:
     // tools/dbg_stream7.py. Five plain launches cost a few microseconds, so they are issued directly.)
+    // Launches past convergence return at once (k_thin_block reads the previous iteration's flag on the
+    // device), so the first batch is sized from the last frame's T (at least 3 launches) and later
+    // batches double: a frame pays one host round trip in the common case, a few when T jumps.
     AOS_HIP(hipMemsetAsync(d_flags, 0, sizeof(int) * (2 + max_iters + K), s));
     launch_open(d_ibits, d_open, g, s);
-    launch_thin_block(d_open, bufs[0], g, 0, d_flags, whole, s);
-    launch_thin_block(bufs[0], bufs[1], g, K, d_flags, whole, s);
-    launch_thin_block(bufs[1], bufs[0], g, 2 * K, d_flags, whole, s);
-    AOS_HIP(hipMemcpyAsync(h_flags, d_flags, sizeof(int) * (1 + 3 * K), hipMemcpyDeviceToHost, s));
-    int launched = 3;
-    const uint64_t *src = bufs[0];
+    const int cap_launches = std::max(3, max_iters / K);
+    int launched = 0, batch_n = std::min(cap_launches, std::max(3, (thin_iters_prev + 2 + K - 1) / K));
+    const uint64_t *src = d_open;
     const uint64_t *final_buf = d_open;
     int T = 0;
     for (int batch = 0;; ++batch) {
-        if (batch > 0) {
-            for (int j = 0; j < 4; ++j) {
-                uint64_t *dst = bufs[launched & 1];
-                launch_thin_block(src, dst, g, launched * K, d_flags, whole, s);
-                src = dst;
-                ++launched;
-            }
-            AOS_HIP(hipMemcpyAsync(h_flags, d_flags, sizeof(int) * (1 + launched * K), hipMemcpyDeviceToHost, s));
+        for (int j = 0; j < batch_n && launched < cap_launches; ++j) {
+            uint64_t *dst = bufs[launched & 1];
+            launch_thin_block(src, dst, g, launched * K, d_flags, whole, s);
+            src = dst;
+            ++launched;
         }
+        batch_n *= 2;
+        AOS_HIP(hipMemcpyAsync(h_flags, d_flags, sizeof(int) * (1 + launched * K), hipMemcpyDeviceToHost, s));
         AOS_HIP(hipStreamSynchronize(s));
         T = thin_iterations(h_flags, launched * K);
         if (T) {
@@ -456,9 +455,10 @@ bool aos_ctx::run_seedgen_once(bool want_host, aos_seedgen_out &out, bool allow_
             final_buf = bufs[last & 1];
             break;
         }
-        if (launched * K > max_iters) throw std::runtime_error("thinning did not converge");
+        if (launched >= cap_launches) throw std::runtime_error("thinning did not converge");
     }
     thin_iters = T;
+    thin_iters_prev = T;
     skel_bits = final_buf;
     AOS_HIP(hipEventRecord(ev[3], s));
     if (ror_collect()) return true;   // (the thinning read-back above synchronised the stream)
