@@ -98,16 +98,15 @@ __device__ __forceinline__ bool rt_in(const RorLaunch &L, float4 p, float4 q) {
 // the totals gives the tile starts, and the scatter pass walks the same chunk again with LDS
 // cursors starting at tile start + prefix. No global atomics; a tile's run from workgroup w sits
 // right after workgroup w - 1's.
-#ifndef AOS_RT_PART_TB
-#define AOS_RT_PART_TB 256
-#endif
+// block sizes: the count pass runs best at 256 threads, the scatter pass at 512 (measured,
+// tools/rorbench); both walk the same per-workgroup chunks (a multiple of kRtChunkQ points)
 #ifndef AOS_RT_PER
 #define AOS_RT_PER 8
 #endif
 #ifndef AOS_RT_G
 #define AOS_RT_G 512
 #endif
-constexpr int kRtTB = AOS_RT_PART_TB, kRtPer = AOS_RT_PER, kRtSub = kRtTB * kRtPer;
+constexpr int kRtPer = AOS_RT_PER, kRtCountTB = 256, kRtScatterTB = 512, kRtChunkQ = kRtScatterTB * kRtPer;
 
 // tiles whose bins a point's 3 x 3 bins touch: [tx0, tx1] x [ty0, ty1], own tile (bx / TB, by / TB)
 __device__ __forceinline__ void rt_tiles(const RorLaunch &L, int bx, int by, int &tx0, int &tx1, int &ty0, int &ty1) {
@@ -115,9 +114,10 @@ __device__ __forceinline__ void rt_tiles(const RorLaunch &L, int bx, int by, int
     ty0 = max(by - 1, 0) / L.TB; ty1 = min(by + 1, L.nby - 1) / L.TB;
 }
 
-template <bool SCATTER, bool STD>
+template <bool SCATTER, bool STD, int kRtTB>
 __global__ __launch_bounds__(kRtTB) void k_rt_part(RorLaunch L, int *H, const int *tstart, uint64_t chunk,
                                                    float4 *staged, unsigned long long *n_own) {
+    constexpr int kRtSub = kRtTB * kRtPer;
     extern __shared__ int hist[];        // [ntiles]: counts (count pass) / cursors (scatter pass)
     const int tid = threadIdx.x, w = blockIdx.x;
     int *row = H + (size_t)w * L.ntiles;
@@ -176,30 +176,40 @@ __global__ __launch_bounds__(kRtTB) void k_rt_part(RorLaunch L, int *H, const in
     }
 }
 
-// H rows -> per-tile exclusive prefixes over the workgroups (in place) and tile totals. A block owns
-// 64 tiles (one per lane) and the 8 waves split the G rows: each wave sums its rows, the partial sums
-// are scanned in LDS, and each wave rewrites its rows as prefixes. Every access is a 256 B row run.
-constexpr int kColWaves = 8;
-__global__ __launch_bounds__(64 * kColWaves) void k_rt_colscan(int *H, int *tot, int ntiles, int G) {
-    __shared__ int part[kColWaves][64];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int t = blockIdx.x * 64 + lane;
-    const int per = (G + kColWaves - 1) / kColWaves, r0 = wv * per, r1 = min(G, r0 + per);
+// H rows -> per-tile exclusive prefixes over the workgroups (in place) and tile totals, in three fully
+// parallel steps over (tile, group of kColRows rows): group sums, a scan of the group sums per tile,
+// then each group rewrites its rows as running prefixes. Thread = tile, so every access is a row run.
+constexpr int kColRows = 32, kColTB = 256;
+__global__ __launch_bounds__(kColTB) void k_rt_colsum(const int *H, int *part, int ntiles, int G) {
+    const int t = blockIdx.x * kColTB + threadIdx.x, g = blockIdx.y;
+    if (t >= ntiles) return;
+    const int r1 = min(G, (g + 1) * kColRows);
     int sum = 0;
-    if (t < ntiles)
-        for (int r = r0; r < r1; ++r) sum += H[(size_t)r * ntiles + t];
-    part[wv][lane] = sum;
-    __syncthreads();
-    int before = 0;
-    for (int k = 0; k < wv; ++k) before += part[k][lane];
-    if (t < ntiles) {
-        for (int r = r0; r < r1; ++r) {
-            const size_t i = (size_t)r * ntiles + t;
-            const int v = H[i];
-            H[i] = before;
-            before += v;
-        }
-        if (wv == kColWaves - 1) tot[t] = before;
+    for (int r = g * kColRows; r < r1; ++r) sum += H[(size_t)r * ntiles + t];
+    part[(size_t)g * ntiles + t] = sum;
+}
+__global__ __launch_bounds__(kColTB) void k_rt_colpre(int *part, int *tot, int ntiles, int ng) {
+    const int t = blockIdx.x * kColTB + threadIdx.x;
+    if (t >= ntiles) return;
+    int run = 0;
+    for (int g = 0; g < ng; ++g) {
+        const size_t i = (size_t)g * ntiles + t;
+        const int v = part[i];
+        part[i] = run;
+        run += v;
+    }
+    tot[t] = run;
+}
+__global__ __launch_bounds__(kColTB) void k_rt_colfix(int *H, const int *part, int ntiles, int G) {
+    const int t = blockIdx.x * kColTB + threadIdx.x, g = blockIdx.y;
+    if (t >= ntiles) return;
+    const int r1 = min(G, (g + 1) * kColRows);
+    int run = part[(size_t)g * ntiles + t];
+    for (int r = g * kColRows; r < r1; ++r) {
+        const size_t i = (size_t)r * ntiles + t;
+        const int v = H[i];
+        H[i] = run;
+        run += v;
     }
 }
 
@@ -487,32 +497,40 @@ void rt_configure(RorLaunch &L, int Hr, int WWr, double est_binned, int force_tb
 
 int rt_part_blocks(const RorLaunch &L) {
     // one contiguous chunk per workgroup; H has ntiles x G ints
-    long long g = AOS_RT_G * 256 / kRtTB;
+    long long g = AOS_RT_G;
+    const long long kRtSub = kRtChunkQ;
     while (g > 64 && (long long)L.ntiles * g > (16ll << 20)) g /= 2;
     return (int)std::max<long long>(1, std::min<long long>(g, ((long long)L.n + kRtSub - 1) / kRtSub));
 }
 uint64_t rt_chunk(const RorLaunch &L, int G) {
     const uint64_t c = (L.n + G - 1) / G;
-    return (c + kRtSub - 1) / kRtSub * kRtSub;
+    return (c + kRtChunkQ - 1) / kRtChunkQ * kRtChunkQ;
 }
 
 template <bool SCATTER, bool STD>
 static void rt_part(const RorLaunch &L, int *H, const int *tstart, int G, float4 *staged, unsigned long long *n_own,
                     hipStream_t s) {
+    constexpr int TB = SCATTER ? kRtScatterTB : kRtCountTB;
     const size_t lds = sizeof(int) * (size_t)L.ntiles;
     if (lds > 64 * 1024)   // the tile histogram exceeds the default dynamic-LDS limit (gfx950: 160 KB)
-        AOS_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rt_part<SCATTER, STD>),
+        AOS_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rt_part<SCATTER, STD, TB>),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    k_rt_part<SCATTER, STD><<<G, kRtTB, lds, s>>>(L, H, tstart, rt_chunk(L, G), staged, n_own);
+    k_rt_part<SCATTER, STD, TB><<<G, TB, lds, s>>>(L, H, tstart, rt_chunk(L, G), staged, n_own);
     AOS_HIP(hipGetLastError());
 }
 static bool rt_std(const RorLaunch &L) { return L.step == 16 && L.ox == 0 && L.oy == 4 && L.oz == 8; }
 
-void launch_rt_count(const RorLaunch &L, int *H, int G, int *tot, unsigned long long *n_own, hipStream_t s) {
+size_t rt_colpart_ints(const RorLaunch &L, int G) { return (size_t)L.ntiles * ((G + kColRows - 1) / kColRows); }
+
+void launch_rt_count(const RorLaunch &L, int *H, int G, int *part, int *tot, unsigned long long *n_own, hipStream_t s) {
     if (!L.n) return;
     if (rt_std(L)) rt_part<false, true>(L, H, nullptr, G, nullptr, n_own, s);
     else rt_part<false, false>(L, H, nullptr, G, nullptr, n_own, s);
-    k_rt_colscan<<<(L.ntiles + 63) / 64, 64 * kColWaves, 0, s>>>(H, tot, L.ntiles, G);
+    const int ng = (G + kColRows - 1) / kColRows;
+    const dim3 grid((L.ntiles + kColTB - 1) / kColTB, ng);
+    k_rt_colsum<<<grid, kColTB, 0, s>>>(H, part, L.ntiles, G);
+    k_rt_colpre<<<grid.x, kColTB, 0, s>>>(part, tot, L.ntiles, ng);
+    k_rt_colfix<<<grid, kColTB, 0, s>>>(H, part, L.ntiles, G);
     AOS_HIP(hipGetLastError());
 }
 

@@ -273,7 +273,8 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
     const bool any = n_points > 0 && !(is_dense && n_points < (uint64_t)L.need);
     if (!any) return;
     AOS_HIP(hipEventRecord(ev[12], s));
-    launch_rt_count(L, d_H, G, d_tot, d_own, s);
+    int *d_part = static_cast<int *>(pt_binslot.ensure(sizeof(int) * rt_colpart_ints(L, G)));
+    launch_rt_count(L, d_H, G, d_part, d_tot, d_own, s);
     AOS_HIP(hipEventRecord(ev[13], s));
     launch_exclusive_scan(d_tot, d_ts, nt + 1, d_st, st, s);
     // The staged array holds own + halo copies. With a capacity from an earlier frame the scatter
@@ -346,7 +347,8 @@ void aos_ctx::ror_stage_append(RorLaunch L, uint64_t *rbits) {
     Ls.staged_cap = (int)scan_cap;
     Ls.overflow = reinterpret_cast<int *>(d_own + 1);
     AOS_HIP(hipEventRecord(ev[12], s));
-    launch_rt_count(Ls, d_H, G, d_tot, d_own, s);
+    int *d_part = static_cast<int *>(pt_binslot.ensure(sizeof(int) * rt_colpart_ints(Ls, G)));
+    launch_rt_count(Ls, d_H, G, d_part, d_tot, d_own, s);
     AOS_HIP(hipEventRecord(ev[13], s));
     launch_exclusive_scan(d_tot, d_sts, nt + 1, d_st, st, s);
     AOS_HIP(hipEventRecord(ev[14], s));

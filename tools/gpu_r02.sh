@@ -44,6 +44,7 @@ if has pmc; then
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/prof_fetch -o ${TAG}_fetch -- python3 $R/bench.py --no-cpu-baseline --no-device-rate --steps 3 --warmup 1 > $R/gpurun_out/${TAG}_prof_fetch.log 2>&1
   echo "[gpu] pmc WRITE_SIZE"
   timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/prof_write -o ${TAG}_write -- python3 $R/bench.py --no-cpu-baseline --no-device-rate --steps 3 --warmup 1 > $R/gpurun_out/${TAG}_prof_write.log 2>&1
+  cd $R && python3 tools/pmc_traffic.py $(ls gpurun_out/prof_fetch/*counter_collection.csv | head -1) $(ls gpurun_out/prof_write/*counter_collection.csv | head -1) gpurun_out/${TAG}_pmc_traffic.json; cd /tmp
 fi
 cd $R
 echo "[gpu] done"

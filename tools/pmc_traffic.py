@@ -17,7 +17,7 @@ def per_kernel(path, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        name = r["Kernel_Name"].split("(")[0].replace("aos::", "")
+        name = r["Kernel_Name"].split("(")[0].replace("aos::", "").replace("void ", "").strip()
         acc[name].append(float(r["Counter_Value"]) * 1024.0)
     return {k: (sum(v) / len(v), len(v)) for k, v in acc.items()}
 
@@ -32,6 +32,11 @@ def main():
         w, nw = write[k]
         out["kernels"][k] = {"fetch_bytes_raw": f, "fetch_bytes": 2.0 * f, "write_bytes": w,
                              "bytes_per_launch": 2.0 * f + w, "launches": [nf, nw]}
+    # the ROR stage a1-a4 (one launch of each per frame): count + column scan + scatter + big-tile sort + tiles
+    parts = [k for k in out["kernels"] if k.startswith(("k_rt_part", "k_rt_colscan", "k_rt_bigsort", "k_rt_ror"))]
+    if parts:
+        out["kernels"]["ror_stage"] = {"bytes_per_launch": sum(out["kernels"][k]["bytes_per_launch"] for k in parts),
+                                       "kernels": sorted(parts)}
     json.dump(out, open(sys.argv[3], "w"), indent=1)
     top = sorted(out["kernels"].items(), key=lambda kv: -kv[1]["bytes_per_launch"])[:8]
     for k, v in top:

@@ -84,14 +84,14 @@ int main(int argc, char **argv) {
     double est = 0.5 * (double)n;
     hipStream_t s;
     AOS_HIP(hipStreamCreate(&s));
-    hipEvent_t e[6];
+    hipEvent_t e[7];
     for (auto &x : e) AOS_HIP(hipEventCreate(&x));
     int *d_H = nullptr, *d_tot = nullptr; void *d_st = nullptr; float4 *d_staged = nullptr, *d_scr = nullptr;
     unsigned long long *d_cnt; uint64_t *d_bits; int *d_big = nullptr; size_t cap_big = 0;
     AOS_HIP(hipMalloc(&d_cnt, 8 * (kRorCounters + 2)));
     AOS_HIP(hipMalloc(&d_bits, 8ull * WW * H));
     size_t cap_H = 0, cap_st = 0, cap_staged = 0, cap_t = 0;
-    double acc[5] = {0, 0, 0, 0, 0};
+    double acc[6] = {0, 0, 0, 0, 0, 0};
     for (int f = 0; f < frames + 2; ++f) {
         rt_configure(L, H, WW, est);
         const int G = rt_part_blocks(L);
@@ -106,7 +106,17 @@ int main(int argc, char **argv) {
         AOS_HIP(hipMemsetAsync(d_cnt, 0, 8 * (kRorCounters + 2), s));
         AOS_HIP(hipMemsetAsync(d_bits, 0, 8ull * WW * H, s));
         AOS_HIP(hipEventRecord(e[0], s));
-        launch_rt_count(L, d_H, G, d_tot, d_cnt + kRorCounters, s);
+        rt_part<false, true>(L, d_H, nullptr, G, nullptr, d_cnt + kRorCounters, s);   // (launch_rt_count, split)
+        AOS_HIP(hipEventRecord(e[6], s));
+        {
+            static int *d_part = nullptr;
+            if (!d_part) AOS_HIP(hipMalloc(&d_part, 4 * rt_colpart_ints(L, G) * 4));
+            const int ng = (G + kColRows - 1) / kColRows;
+            const dim3 grid((L.ntiles + kColTB - 1) / kColTB, ng);
+            k_rt_colsum<<<grid, kColTB, 0, s>>>(d_H, d_part, L.ntiles, G);
+            k_rt_colpre<<<grid.x, kColTB, 0, s>>>(d_part, d_tot, L.ntiles, ng);
+            k_rt_colfix<<<grid, kColTB, 0, s>>>(d_H, d_part, L.ntiles, G);
+        }
         AOS_HIP(hipEventRecord(e[1], s));
         launch_exclusive_scan(d_tot, d_ts, nt + 1, d_st, st, s);
         AOS_HIP(hipEventRecord(e[2], s));
@@ -129,13 +139,14 @@ int main(int argc, char **argv) {
         launch_rt_ror(L, d_ts, d_staged, d_scr, d_big, d_bits, d_cnt, nullptr, nullptr, s);
         AOS_HIP(hipEventRecord(e[5], s));
         AOS_HIP(hipStreamSynchronize(s));
-        float t[5];
+        float t[6];
         AOS_HIP(hipEventElapsedTime(&t[0], e[0], e[1]));
         AOS_HIP(hipEventElapsedTime(&t[1], e[1], e[2]));
         AOS_HIP(hipEventElapsedTime(&t[2], e[3], e[4]));
         AOS_HIP(hipEventElapsedTime(&t[3], e[4], e[5]));
         AOS_HIP(hipEventElapsedTime(&t[4], e[0], e[5]));
-        if (f >= 2) for (int k = 0; k < 5; ++k) acc[k] += t[k] / frames;
+        AOS_HIP(hipEventElapsedTime(&t[5], e[0], e[6]));
+        if (f >= 2) for (int k = 0; k < 6; ++k) acc[k] += t[k] / frames;
         if (f == frames + 1) {
             std::vector<uint64_t> bits((size_t)WW * H);
             std::vector<unsigned long long> cnt(kRorCounters);
@@ -149,6 +160,7 @@ int main(int argc, char **argv) {
         }
     }
     const double b = 12.0 * n + (double)W * H;
+    printf("(count kernel %.1f us, column scan %.1f us)\n", 1e3 * acc[5], 1e3 * (acc[0] - acc[5]));
     printf("count %.1f us  scan %.1f us  scatter %.1f us  tiles %.1f us  | stage %.1f us (incl. read-back gap)  "
            "§8d bytes %.0f MB -> %.3f TB/s = %.3f of 8 TB/s; count pass 12N: %.3f of peak\n",
            1e3 * acc[0], 1e3 * acc[1], 1e3 * acc[2], 1e3 * acc[3], 1e3 * acc[4], b / 1e6, b / (acc[4] * 1e-3) / 1e12,
