@@ -111,7 +111,8 @@ void rt_configure(RorLaunch &L, int Hr, int WWr, double est_binned, int force_tb
 int rt_part_blocks(const RorLaunch &L);   // G: workgroups (= cloud chunks) of the partition passes
 // H: G x ntiles ints (row per workgroup). The count pass leaves per-tile prefixes over the workgroups
 // in H and the tile totals in tot[0..ntiles); tstart = exclusive scan of tot (ntiles + 1 entries).
-void launch_rt_count(const RorLaunch &L, int *H, int G, int *tot, unsigned long long *n_own, hipStream_t s);
+size_t rt_colpart_ints(const RorLaunch &L, int G);   // scratch of the column scan (part)
+void launch_rt_count(const RorLaunch &L, int *H, int G, int *part, int *tot, unsigned long long *n_own, hipStream_t s);
 void launch_rt_scatter(const RorLaunch &L, int *H, const int *tstart, int G, float4 *staged, hipStream_t s);
 // kept_tile (nullable): per-tile kept counts; dirty (nullable): a tile is counted iff dirty[t+1] > dirty[t]
 // scratch: staged-sized; bigbins: rt_bigbins_ints(L) ints (tiles beyond the LDS capacity are sorted there)
