@@ -192,6 +192,7 @@ def lib():
         L.aos_gvd_from_seedgen.argtypes = [c_vp, P(GvdOut)]
         L.aos_gvd_from_seedgen_async.argtypes = [c_vp]
         L.aos_gvd_wait.argtypes = [c_vp, P(GvdOut)]
+        L.aos_gvd_pipeline_depth.argtypes = [c_vp, c_i]
         L.aos_debug_grid.argtypes = [c_vp, ctypes.c_char_p, c_vp, c_u64]
         L.aos_gvd_markers_get.argtypes = [c_vp, P(GvdMarkers)]
         L.aos_map_reset.argtypes = [c_vp, c_u64]
@@ -407,6 +408,10 @@ class Ctx:
     def gvd_async(self) -> None:
         """Start the GVD of the last seed-gen frame in the background (aos_gvd_from_seedgen_async)."""
         _check(lib().aos_gvd_from_seedgen_async(self.h))
+
+    def gvd_pipeline_depth(self, depth: int) -> None:
+        """Up to `depth` background GVD jobs in flight (aos_gvd_pipeline_depth)."""
+        _check(lib().aos_gvd_pipeline_depth(self.h, int(depth)))
 
     def gvd_wait(self) -> dict:
         """The graph of the background GVD (aos_gvd_wait)."""

@@ -2,7 +2,9 @@
 #pragma once
 #include <array>
 #include <condition_variable>
+#include <deque>
 #include <exception>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -76,7 +78,6 @@ struct aos_ctx {
     int n_virtual = 0, n_ray = 0, n_endpoint = 0, n_clusters_all = 0, n_bfs_replayed = 0;
 
     // ---- GVD (gvd.hip)
-    aos::GvdState gs;
     bool have_gvd = false, gvd_from_frame = false;
     uint64_t frame_gen = 0, gvd_frame_gen = 0, gvd_gen = 0;   // seed-gen frames / GVD calls so far
     const int8_t *gvd_skel = nullptr;                          // the skeleton the last GVD call used
@@ -84,23 +85,38 @@ struct aos_ctx {
 
     // ---- pipelined GVD (aos_gvd_from_seedgen_async): the reference runs seed-gen and the GVD as two
     // nodes, so frame k + 1's seed-gen overlaps frame k's graph. The GVD of a snapshot of the frame
-    // (seeds, rows, skeleton) runs on a persistent worker thread and its own stream.
+    // (seeds, rows, skeleton) runs on a lane: a GvdState with a persistent worker thread and its own
+    // stream. Frames are independent, so up to gvd_depth jobs may be in flight on gvd_depth lanes
+    // (aos_gvd_pipeline_depth); one more lane holds the handle's current result (markers, planning).
     struct AsyncGvd {
         std::thread worker;
         std::mutex mu;
         std::condition_variable cv;
-        bool busy = false, quit = false, pub = false, done = false, applied = false, prefix = false;
+        bool busy = false, quit = false, pub = false, done = false, prefix = false;
         std::exception_ptr err;
         hipStream_t stream = nullptr;
         std::array<hipEvent_t, 16> ev{};
         hipEvent_t ready = nullptr;               // the snapshot copy on the seed-gen stream
         std::vector<double> seeds, rows;          // snapshot of h_voronoi / h_rows_info
         aos_grid_info info{};
-    } ag;
+    };
+    struct alignas(128) GvdLane {
+        aos::GvdState gs;
+        AsyncGvd ag;
+    };
+    std::vector<std::unique_ptr<GvdLane>> lanes{};   // lanes[cur_lane] holds the current result
+    int cur_lane = 0, gvd_depth = 1;
+    std::deque<int> inflight;                        // lanes with uncollected jobs, oldest first
+    bool view_newest = false;                        // no aos_gvd_wait since the last job started
+    aos::GvdState &gs() { return lanes[cur_lane]->gs; }
+    void gvd_lanes_ensure();
     void gvd_async_start();
-    bool gvd_async_wait(bool rethrow, bool consume);   // true if a finished job's graph is in gs
-    void gvd_async_drop();
+    bool gvd_async_wait(bool rethrow);   // aos_gvd_wait: collect the oldest job; false if none
+    void gvd_view_settle();              // markers / planning: settle which result is current
+    void gvd_async_drop();               // a synchronous GVD call supersedes every job in flight
     void gvd_async_stop();
+    void lane_join(int l);               // waits for lane l's job (no bookkeeping)
+    void lane_apply(int l);              // lane l's finished job becomes the current result
 
     // ---- path planning (path.hip)
     void *path_state = nullptr;   // aos::PathState

@@ -82,6 +82,7 @@ int aos_create(const aos_params *p, int device, aos_ctx **out) {
     AOS_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (auto &e : c->ev) AOS_HIP(hipEventCreate(&e));
     c->poly = default_polygon();
+    c->gvd_lanes_ensure();
     *out = c;
     return AOS_OK;
     AOS_GUARD_END
@@ -202,6 +203,17 @@ int aos_gvd_wait(aos_ctx *c, aos_gvd_out *out) {
     AOS_GUARD_END
 }
 
+int aos_gvd_pipeline_depth(aos_ctx *c, int32_t depth) {
+    if (!c) { set_error("aos_gvd_pipeline_depth: null handle"); return AOS_E_INVALID; }
+    if (depth < 1 || depth > 8) { set_error("aos_gvd_pipeline_depth: depth must be in [1, 8]"); return AOS_E_INVALID; }
+    AOS_GUARD_BEGIN
+    DeviceScope dev_scope(c->device);
+    c->gvd_depth = depth;
+    c->gvd_lanes_ensure();
+    return AOS_OK;
+    AOS_GUARD_END
+}
+
 int aos_tile_plan_compute(const aos_params *p, const double *poly_xy, uint32_t n_poly, int32_t tiles_x,
                           int32_t tiles_y, int32_t rank, aos_tile_plan *out) {
     if (!p || !out) { set_error("aos_tile_plan_compute: null argument"); return AOS_E_INVALID; }
@@ -242,11 +254,11 @@ int aos_tiled_seedgen_process(aos_ctx *c, const aos_comm *comm, int32_t tiles_x,
 
 int aos_gvd_markers_get(aos_ctx *c, aos_gvd_markers *out) {
     if (!c || !out) { set_error("aos_gvd_markers_get: null argument"); return AOS_E_INVALID; }
-    GvdState &G = c->gs;
     AOS_GUARD_BEGIN
-    c->gvd_async_wait(false, false);
-    markers_wait(G, true);   // the cells run on after the graph is returned
+    c->gvd_view_settle();
+    markers_wait(c->gs(), true);   // the cells run on after the graph is returned
     AOS_GUARD_END
+    GvdState &G = c->gs();
     if (!G.have_markers || !G.cells) {
         set_error("aos_gvd_markers_get: no markers (gvd_markers = 0 or no GVD frame)");
         return AOS_E_STATE;

@@ -961,35 +961,70 @@ static void fill_gvd_out(const aos_ctx &c, const GvdState &G, const aos_grid_inf
 
 void aos_ctx::run_gvd_external(const aos_gvd_in &in, aos_gvd_out &out) {
     gvd_async_drop();
+    GvdState &G = gs();
     const size_t C = (size_t)in.info.width * in.info.height;
-    int8_t *d_sk = static_cast<int8_t *>(gs.skel.ensure(std::max<size_t>(C, 1)));
+    int8_t *d_sk = static_cast<int8_t *>(G.skel.ensure(std::max<size_t>(C, 1)));
     if (C && in.skeleton) AOS_HIP(hipMemcpyAsync(d_sk, in.skeleton, C, hipMemcpyHostToDevice, stream));
     GvdStageIn gi{in.seeds_xy, in.n_seeds, in.rows_info_xy, in.n_rows_poses, in.info, d_sk};
     have_gvd = false;
-    const bool pub = run_gvd_stage(gs, P, gi, stream, ev.data());
+    const bool pub = run_gvd_stage(G, P, gi, stream, ev.data());
     have_gvd = true; gvd_from_frame = false; gvd_skel = d_sk; gvd_info = in.info; ++gvd_gen;
-    fill_gvd_out(*this, gs, in.info, pub, out);
+    fill_gvd_out(*this, G, in.info, pub, out);
 }
 
 void aos_ctx::run_gvd_from_frame(aos_gvd_out &out) {
     gvd_async_drop();
+    GvdState &G = gs();
     aos_grid_info info{geom.origin_x, geom.origin_y, geom.res, (uint32_t)geom.W, (uint32_t)geom.H};
     GvdStageIn gi{h_voronoi.data(), (int)(h_voronoi.size() / 2), h_rows_info.data(), (int)(h_rows_info.size() / 2), info,
                   skel_bytes.as<int8_t>()};
     have_gvd = false;
-    const bool pub = run_gvd_stage(gs, P, gi, stream, ev.data());
+    const bool pub = run_gvd_stage(G, P, gi, stream, ev.data());
     have_gvd = true; gvd_from_frame = true; gvd_frame_gen = frame_gen; gvd_skel = gi.d_skeleton; gvd_info = info; ++gvd_gen;
-    fill_gvd_out(*this, gs, info, pub, out);
+    fill_gvd_out(*this, G, info, pub, out);
 }
 
 // ------------------------------------------------------------------ pipelined GVD
 // aos_gvd_from_seedgen_async: snapshot the frame's GVD inputs (host seeds and rows, a device copy of
-// the skeleton ordered on the seed-gen stream) and hand them to the worker, which runs the same
-// run_gvd_stage on its own stream. The next seed-gen frame may run meanwhile; it rewrites only
-// seed-gen state. Every other GVD-side call waits for the job first.
+// the skeleton ordered on the seed-gen stream) into a free lane, whose worker runs the same
+// run_gvd_stage on the lane's stream. The next seed-gen frame may run meanwhile; it rewrites only
+// seed-gen state. Frames are independent, so with aos_gvd_pipeline_depth(D) up to D jobs run at once
+// (each Subdiv2D replay on its own host core); aos_gvd_wait collects them in start order.
+void aos_ctx::gvd_lanes_ensure() {
+    if (lanes.empty()) lanes.emplace_back(new GvdLane());
+    while ((int)lanes.size() < gvd_depth + 1) lanes.emplace_back(new GvdLane());
+}
+
+void aos_ctx::lane_join(int l) {
+    AsyncGvd &A = lanes[l]->ag;
+    if (!A.worker.joinable()) return;
+    std::unique_lock<std::mutex> lk(A.mu);
+    A.cv.wait(lk, [&A] { return !A.busy; });
+}
+
+void aos_ctx::lane_apply(int l) {
+    cur_lane = l;
+    have_gvd = true; gvd_from_frame = false; gvd_skel = lanes[l]->gs.skel.as<int8_t>(); gvd_info = lanes[l]->ag.info;
+    ++gvd_gen;
+}
+
 void aos_ctx::gvd_async_start() {
-    gvd_async_drop();
-    AsyncGvd &A = ag;
+    gvd_lanes_ensure();
+    // D jobs in flight already: the oldest is superseded (joined, its result dropped)
+    while ((int)inflight.size() >= gvd_depth) {
+        const int l = inflight.front();
+        inflight.pop_front();
+        lane_join(l);
+        std::lock_guard<std::mutex> lk(lanes[l]->ag.mu);
+        lanes[l]->ag.done = false;
+        lanes[l]->ag.err = nullptr;
+    }
+    int L = -1;   // a lane that holds neither the current result nor a job
+    for (int i = 0; i < (int)lanes.size() && L < 0; ++i)
+        if (i != cur_lane && std::find(inflight.begin(), inflight.end(), i) == inflight.end()) L = i;
+    if (L < 0) throw std::logic_error("gvd_async_start: no free lane");
+    GvdLane &ln = *lanes[L];
+    AsyncGvd &A = ln.ag;
     if (!A.stream) {
         AOS_HIP(hipStreamCreateWithFlags(&A.stream, hipStreamNonBlocking));
         for (auto &e : A.ev) AOS_HIP(hipEventCreate(&e));
@@ -999,14 +1034,13 @@ void aos_ctx::gvd_async_start() {
     A.rows = h_rows_info;
     A.info = aos_grid_info{geom.origin_x, geom.origin_y, geom.res, (uint32_t)geom.W, (uint32_t)geom.H};
     const size_t C = (size_t)geom.W * geom.H;
-    int8_t *d_sk = static_cast<int8_t *>(gs.skel.ensure(std::max<size_t>(C, 1)));
+    int8_t *d_sk = static_cast<int8_t *>(ln.gs.skel.ensure(std::max<size_t>(C, 1)));
     AOS_HIP(hipMemcpyAsync(d_sk, skel_bytes.p, C, hipMemcpyDeviceToDevice, stream));
     AOS_HIP(hipEventRecord(A.ready, stream));
     AOS_HIP(hipStreamWaitEvent(A.stream, A.ready, 0));
-    have_gvd = false;
     if (!A.worker.joinable())
-        A.worker = std::thread([this]() {
-            AsyncGvd &W = ag;
+        A.worker = std::thread([this, &ln]() {
+            AsyncGvd &W = ln.ag;
             std::unique_lock<std::mutex> l(W.mu);
             for (;;) {
                 W.cv.wait(l, [&W] { return W.busy || W.quit; });
@@ -1017,14 +1051,14 @@ void aos_ctx::gvd_async_start() {
                 try {
                     AOS_HIP(hipSetDevice(device));
                     GvdStageIn gi{W.seeds.data(), (int)(W.seeds.size() / 2), W.rows.data(), (int)(W.rows.size() / 2),
-                                  W.info, gs.skel.as<int8_t>()};
+                                  W.info, ln.gs.skel.as<int8_t>()};
                     gi.hook_arg = &W;
                     gi.on_host_phase = [](void *p) {
                         AsyncGvd *A = static_cast<AsyncGvd *>(p);
                         { std::lock_guard<std::mutex> g(A->mu); A->prefix = true; }
                         A->cv.notify_all();
                     };
-                    pub = run_gvd_stage(gs, P, gi, W.stream, W.ev.data());
+                    pub = run_gvd_stage(ln.gs, P, gi, W.stream, W.ev.data());
                 } catch (...) { e = std::current_exception(); }
                 l.lock();
                 W.err = e;
@@ -1038,11 +1072,12 @@ void aos_ctx::gvd_async_start() {
         std::lock_guard<std::mutex> l(A.mu);
         A.err = nullptr;
         A.done = false;
-        A.applied = false;
         A.prefix = false;
         A.busy = true;
     }
     A.cv.notify_all();
+    inflight.push_back(L);
+    view_newest = true;
     // Return once the job's short GPU prefix (seed merge) is done and its host replay runs: a
     // seed-gen frame launched earlier would occupy the GPU and hold the prefix back, and the replay
     // would start late instead of overlapping it.
@@ -1050,55 +1085,81 @@ void aos_ctx::gvd_async_start() {
     A.cv.wait(l, [&A] { return A.prefix || !A.busy; });
 }
 
-// Waits for the job in flight. consume (aos_gvd_wait): collect its result once, raising its error
-// if rethrow. Otherwise (any other GVD-side call): only settle the handle's GVD bookkeeping.
-bool aos_ctx::gvd_async_wait(bool rethrow, bool consume) {
-    AsyncGvd &A = ag;
-    if (!A.worker.joinable()) return false;
-    std::unique_lock<std::mutex> l(A.mu);
-    A.cv.wait(l, [&A] { return !A.busy; });
-    if (!A.done) return false;
-    if (!A.err && !A.applied) {
-        have_gvd = true; gvd_from_frame = false; gvd_skel = gs.skel.as<int8_t>(); gvd_info = A.info; ++gvd_gen;
-        A.applied = true;
-    }
-    if (!consume) return true;
-    A.done = false;
-    if (A.err) {
-        std::exception_ptr e = A.err;
+// aos_gvd_wait: collects the oldest job in flight (raising its error if rethrow); its lane becomes
+// the handle's current result (markers, planning).
+bool aos_ctx::gvd_async_wait(bool rethrow) {
+    if (inflight.empty()) return false;
+    const int l = inflight.front();
+    inflight.pop_front();
+    view_newest = false;
+    lane_join(l);
+    AsyncGvd &A = lanes[l]->ag;
+    std::exception_ptr e;
+    {
+        std::lock_guard<std::mutex> lk(A.mu);
+        A.done = false;
+        e = A.err;
         A.err = nullptr;
+    }
+    if (e) {
         if (rethrow) std::rethrow_exception(e);
         return false;
     }
+    lane_apply(l);
     return true;
 }
 
-// A synchronous GVD call or a new job supersedes an uncollected result.
+// Markers and planning on the handle's own graph: right after aos_gvd_wait they see the collected
+// job; with no wait since the last start they see the newest job (waited for, still collectable).
+void aos_ctx::gvd_view_settle() {
+    if (!view_newest || inflight.empty()) return;
+    const int l = inflight.back();
+    lane_join(l);
+    AsyncGvd &A = lanes[l]->ag;
+    bool ok;
+    {
+        std::lock_guard<std::mutex> lk(A.mu);
+        ok = A.done && !A.err;
+    }
+    if (ok && (cur_lane != l || !have_gvd)) lane_apply(l);
+}
+
+// A synchronous GVD call (or the handle's release) supersedes every job in flight.
 void aos_ctx::gvd_async_drop() {
-    gvd_async_wait(false, false);
-    std::lock_guard<std::mutex> l(ag.mu);
-    ag.done = false;
-    ag.err = nullptr;
+    gvd_lanes_ensure();
+    for (int l : inflight) {
+        lane_join(l);
+        std::lock_guard<std::mutex> lk(lanes[l]->ag.mu);
+        lanes[l]->ag.done = false;
+        lanes[l]->ag.err = nullptr;
+    }
+    inflight.clear();
+    view_newest = false;
 }
 
 void aos_ctx::gvd_async_stop() {
-    AsyncGvd &A = ag;
-    if (A.worker.joinable()) {
-        { std::lock_guard<std::mutex> l(A.mu); A.quit = true; }
-        A.cv.notify_all();
-        A.worker.join();
+    for (auto &lp : lanes) {
+        AsyncGvd &A = lp->ag;
+        if (A.worker.joinable()) {
+            { std::lock_guard<std::mutex> l(A.mu); A.quit = true; }
+            A.cv.notify_all();
+            A.worker.join();
+        }
+        if (A.stream) {
+            (void)hipStreamSynchronize(A.stream);
+            for (auto &e : A.ev) (void)hipEventDestroy(e);
+            (void)hipEventDestroy(A.ready);
+            (void)hipStreamDestroy(A.stream);
+            A.stream = nullptr;
+        }
     }
-    if (A.stream) {
-        (void)hipStreamSynchronize(A.stream);
-        for (auto &e : A.ev) (void)hipEventDestroy(e);
-        (void)hipEventDestroy(A.ready);
-        (void)hipStreamDestroy(A.stream);
-        A.stream = nullptr;
-    }
+    inflight.clear();
+    view_newest = false;
 }
 
 int aos::gvd_wait_out(aos_ctx *c, aos_gvd_out *out) {   // aos_gvd_wait (api.hip)
-    if (!c->gvd_async_wait(true, true)) return 0;
-    fill_gvd_out(*c, c->gs, c->ag.info, c->ag.pub, *out);
+    if (!c->gvd_async_wait(true)) return 0;
+    const aos_ctx::GvdLane &ln = *c->lanes[c->cur_lane];
+    fill_gvd_out(*c, ln.gs, ln.ag.info, ln.ag.pub, *out);
     return 1;
 }

@@ -499,7 +499,7 @@ using namespace aos;
 void aos_ctx::run_path_plan(const aos_path_graph *graph, const int8_t *skeleton, int skeleton_on_device,
                             const aos_grid_info *info, const aos_path_query &q, aos_path_out &out) {
     const auto t0 = std::chrono::steady_clock::now();
-    gvd_async_wait(false, false);
+    gvd_view_settle();
     if (!path_state) path_state = new PathState();
     PathState &S = *static_cast<PathState *>(path_state);
     // the graph
@@ -508,6 +508,7 @@ void aos_ctx::run_path_plan(const aos_path_graph *graph, const int8_t *skeleton,
     uint64_t gen = 0;
     if (!graph) {
         if (!have_gvd) throw std::runtime_error("aos_path_plan: no GVD graph on this handle");
+        GvdState &gs = this->gs();
         markers_wait(gs, false);
         own.num_nodes = (int32_t)gs.labels.size(); own.nodes_xy = gs.nodes_xy.data();
         own.node_labels = gs.labels.data(); own.node_cluster_indices = gs.cluster_idx.data();

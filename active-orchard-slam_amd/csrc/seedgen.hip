@@ -29,19 +29,22 @@ void aos_ctx::release() {
                       &cs.hash_start, &cs.hash_slot, &cs.hash_sorted, &cs.seed_out, &cs.misc, &cs.scan_tmp})
         b->release();
     cs.h_misc.release();
-    gvd_async_stop();   // joins a job in flight (it uses gs)
+    gvd_async_stop();   // joins the jobs in flight (they use the lanes' GvdStates)
     release_uploader();
-    markers_wait(gs, false);
     free_path_state(path_state);
     path_state = nullptr;
     have_gvd = false;
-    free_gvd_scratch(gs);
-    gs.cells.reset();
-    for (DevBuf *b : {&gs.seeds, &gs.merge_state, &gs.hash_count, &gs.hash_start, &gs.hash_slot, &gs.hash_sorted,
-                      &gs.scan_tmp, &gs.edges, &gs.bpts, &gs.near_idx, &gs.cand, &gs.cand_ok, &gs.skel,
-                      &gs.grid_bytes_ext})
-        b->release();
-    gs.h_misc.release();
+    for (auto &lp : lanes) {
+        GvdState &gs = lp->gs;
+        markers_wait(gs, false);
+        free_gvd_scratch(gs);
+        gs.cells.reset();
+        for (DevBuf *b : {&gs.seeds, &gs.merge_state, &gs.hash_count, &gs.hash_start, &gs.hash_slot, &gs.hash_sorted,
+                          &gs.scan_tmp, &gs.edges, &gs.bpts, &gs.near_idx, &gs.cand, &gs.cand_ok, &gs.skel,
+                          &gs.grid_bytes_ext})
+            b->release();
+        gs.h_misc.release();
+    }
 }
 
 // A pageable hipMemcpyAsync of the 160 MB C2 cloud runs at ~20 GB/s: the runtime stages it through
@@ -438,7 +441,7 @@ bool aos_ctx::run_seedgen_once(bool want_host, aos_seedgen_out &out, bool allow_
     const uint64_t *src = d_open;
     const uint64_t *final_buf = d_open;
     int T = 0;
-    for (int batch = 0;; ++batch) {
+    for (;;) {
         for (int j = 0; j < batch_n && launched < cap_launches; ++j) {
             uint64_t *dst = bufs[launched & 1];
             launch_thin_block(src, dst, g, launched * K, d_flags, whole, s);

@@ -5,7 +5,8 @@ One step = one full frame of the path on one GPU, measured as SURVEY §8d define
 PointCloud2 bytes in host memory -> ROR / clip / raster -> inflation -> opening + Zhang-Suen ->
 clusters / tree rows / seeds -> GVD graph (seed merge, Delaunay replay, boundary points, edges,
 labels) -> host GvdGraph, seeds / rows arrays and both OccupancyGrids in host memory.
-`value` = W*H / median frame time. The device-resident rate (cloud already in HBM, grids left in
+`value` = W*H x K / the timed region (pipelined GVD jobs, --depth; the frame latency beside it), or
+W*H / median frame time with --sequential. The device-resident rate (cloud already in HBM, grids left in
 HBM) is reported beside it (`device_resident`). Workload: config C2 (10 M points, 4096^2 cells @
 0.1 m, BASELINE.json configs[2]).
 
@@ -44,6 +45,9 @@ def parse(argv=None):
                          "host-in / host-out frame")
     ap.add_argument("--no-device-rate", action="store_true", help="skip the extra device-resident loop")
     ap.add_argument("--trace", action="store_true", help="per-step timeline of the pipelined loop on stderr")
+    ap.add_argument("--depth", type=int, default=4,
+                    help="pipelined GVD jobs in flight (aos_gvd_pipeline_depth): frames are independent, so frame "
+                         "k's GVD runs beside the GVDs of frames k-1 .. k-depth+1, each Subdiv2D replay on its own core")
     ap.add_argument("--sequential", action="store_true",
                     help="run seed-gen and GVD of a frame back to back instead of the default pipeline (frame k's "
                          "seed-gen overlaps frame k-1's GVD, as the reference's two nodes do)")
@@ -206,8 +210,11 @@ def main():
     # seed-gen k, collect graph + markers of frame k - 1, start the GVD of frame k; the last step also
     # collects its own frame, so every frame of the timed region completes inside it.
     n_calls = a.warmup + a.steps
-    pend = {"k": 0, "t0": {}, "mt0": None, "ms": 0.0}
+    pend = {"k": 0, "t0": {}, "mt0": None, "ms": 0.0, "fifo": [], "lat": {}}
     pipeline = not (a.sequential or a.stream or a.tiled)
+    depth = max(1, a.depth) if pipeline else 1
+    if pipeline:
+        ctx.gvd_pipeline_depth(depth)
 
     def collect():
         m = ctx.gvd_markers()
@@ -223,6 +230,7 @@ def main():
             latency.append(time.perf_counter() - pend["t0"][j])
         pend["mt0"] = pend["t0"][j]
         collect()
+        pend["lat"][j] = time.perf_counter() - pend["t0"][j]   # PointCloud2 in -> graph + markers out
         gg["ms"]["cells"] = pend["ms"]
         return gg
 
@@ -245,17 +253,21 @@ def main():
             else:
                 g = ctx.seedgen(d_cloud.data_ptr(), n_points=n, on_device=True, want_host=False)
         if pipeline:
+            # at most `depth` GVD jobs in flight: collect the oldest (graph + markers), start this frame's;
+            # the last step drains every job, so each frame started in the timed region ends inside it
             t1 = time.perf_counter()
-            gg = finish(k - 1) if k > 0 else None
+            gg = finish(pend["fifo"].pop(0)) if len(pend["fifo"]) >= depth else None
             t2 = time.perf_counter()
             ctx.gvd_async()
+            pend["fifo"].append(k)
             t3 = time.perf_counter()
             if k == n_calls - 1:
-                gg = finish(k)
+                while pend["fifo"]:
+                    gg = finish(pend["fifo"].pop(0))
             if a.trace:
                 ms = gg["ms"] if gg is not None else {}
-                print(f"[trace] step {k}: seed-gen {1e3 * (t1 - t0):.2f} ms, wait graph+markers k-1 "
-                      f"{1e3 * (t2 - t1):.2f} ms, start GVD {1e3 * (t3 - t2):.2f} ms | frame k-1: delaunay "
+                print(f"[trace] step {k}: seed-gen {1e3 * (t1 - t0):.2f} ms, wait oldest graph+markers "
+                      f"{1e3 * (t2 - t1):.2f} ms, start GVD {1e3 * (t3 - t2):.2f} ms | collected frame: delaunay "
                       f"{ms.get('delaunay', 0):.1f} total {ms.get('total', 0):.1f} cells {ms.get('cells', 0):.1f}",
                       file=sys.stderr, flush=True)
             return g, gg
@@ -267,12 +279,14 @@ def main():
         pend["mt0"] = t0
         if k == n_calls - 1:
             collect()
+        pend["lat"][k] = time.perf_counter() - t0
         gg["ms"]["cells"] = pend["ms"]   # the previous frame's (the last step: its own)
         return g, gg
 
     _progress(f"{a.warmup} warmup + {a.steps} timed frames")
     dt, res, per = timed_region(step, a.steps, a.warmup, world, torch.cuda.synchronize, dist, red_dev)
     g, gg = res[-1]
+    frame_lat = sorted(1e3 * pend["lat"][k] for k in range(a.warmup, a.warmup + a.steps) if k in pend["lat"])
     dev_rate = None
     if host_io and not a.no_device_rate:
         # the same frame with the cloud already in HBM and the grids left there (no PCIe)
@@ -280,7 +294,9 @@ def main():
         pend["k"], n_calls = 0, 2 + a.steps
         ddt, _, dper = timed_region(step, a.steps, 2, world, torch.cuda.synchronize, dist, red_dev)
         dmed = sorted(dper)[len(dper) // 2]
-        dev_rate = {"value": round((g["width"] * g["height"] / 1e6) * world / dmed, 3), "median_ms": round(dmed * 1e3, 3),
+        dval = (throughput(g["width"] * g["height"] / 1e6, world, a.steps, ddt) if pipeline
+                else (g["width"] * g["height"] / 1e6) * world / dmed)
+        dev_rate = {"value": round(dval, 3), "median_ms": round(dmed * 1e3, 3),
                     "ms_per_step": round(ddt / a.steps * 1e3, 3),
                     "io": "cloud already in HBM, OccupancyGrids left in HBM, GvdGraph + seeds to host"}
     stage = {}
@@ -294,9 +310,13 @@ def main():
     # weak: every rank processes its own map; tiled: the ranks share one map (strong scaling).
     # value = cells / median frame time (median of the warm frames), the contract's
     # timed-region mean beside it (value_mean).
+    # pipelined (default): frames overlap, so a step's wall time is not a frame time; value = the
+    # contract's timed-region throughput (K frames, the drain of the last jobs included), and the
+    # frame latency (PointCloud2 in -> graph + markers out) is reported beside it
     med = sorted(per)[len(per) // 2]
-    value = (cells / 1e6) * (1 if a.tiled else world) / med
+    value_median = (cells / 1e6) * (1 if a.tiled else world) / med
     value_mean = throughput(cells / 1e6, 1 if a.tiled else world, len(res), dt)
+    value = value_mean if pipeline else value_median
     avg = stage
 
     # Roofline (SURVEY §8d algorithmic bytes, HBM-bound; no MFMA). Per frame B_alg = 12 N + C (6 + 4 T):
@@ -349,7 +369,9 @@ def main():
             "metric": "Mcells/s skeleton+GVD (seed-gen + GVD frame) on 4096^2 grid",
             "value": round(value, 3), "unit": "Mcells/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(dt / len(res) * 1e3, 3), "higher_is_better": True,
-            "value_mean": round(value_mean, 3), "median_ms": round(med * 1e3, 3),
+            "value_mean": round(value_mean, 3), "value_median": round(value_median, 3), "median_ms": round(med * 1e3, 3),
+            "frame_latency_ms": {"p50": round(frame_lat[len(frame_lat) // 2], 2), "max": round(frame_lat[-1], 2)}
+            if frame_lat else None,
             "scaling": "strong" if a.tiled else "weak",
             "vs_baseline": None, "dtype": "f32/f64 (reference float/double arithmetic), u8/bit grids",
             "data": ("synthetic orchard (tools/orchard_gen.c, SplitMix64; 1 % in-clip outliers, not SURVEY §8d's 10 %, "
@@ -362,7 +384,8 @@ def main():
             "io": "host PointCloud2 in, host OccupancyGrids + GvdGraph out (SURVEY §8d)" if host_io else
                   "device-resident cloud, device-resident grids, host GvdGraph",
             "device_resident": dev_rate,
-            "pipeline": "seed-gen of frame k overlaps the GVD of frame k-1 (the reference's two nodes)"
+            "pipeline": (f"depth {depth}: frame k's seed-gen overlaps the GVDs of frames k-1 .. k-{depth} (the "
+                         f"reference's two nodes; frames are independent, each GVD's Subdiv2D replay on its own core)")
                         if pipeline else "sequential",
             "stages_ms": {k: round(v, 3) for k, v in avg.items()},
             "frame": {"T": T, "rows": len(g["row_length"]), "seeds": len(g["voronoi_seeds"]),

@@ -149,10 +149,15 @@ int aos_gvd_from_seedgen(aos_ctx *ctx, aos_gvd_out *out);
  * overlaps frame k's graph. _async snapshots the last seed-gen frame's GVD inputs (seeds, rows,
  * skeleton) and starts the GVD on a worker thread and its own stream; aos_seedgen_process /
  * aos_map_append may run meanwhile. aos_gvd_wait returns that graph (the same as
- * aos_gvd_from_seedgen would have). Every other GVD-side call waits for the job first; a GVD call
- * made before aos_gvd_wait supersedes the job's result. */
+ * aos_gvd_from_seedgen would have). A synchronous GVD call supersedes every job in flight.
+ * Frames are independent, so up to `depth` jobs (aos_gvd_pipeline_depth, default 1) may be in flight,
+ * each replaying its Subdiv2D on its own host thread; aos_gvd_wait collects them in start order, and
+ * starting one more than `depth` supersedes the oldest. aos_gvd_markers_get / aos_path_plan on the
+ * handle's graph use the job aos_gvd_wait collected last, or the newest job if none was collected
+ * since it started (they wait for it without collecting it). */
 int aos_gvd_from_seedgen_async(aos_ctx *ctx);
 int aos_gvd_wait(aos_ctx *ctx, aos_gvd_out *out);
+int aos_gvd_pipeline_depth(aos_ctx *ctx, int32_t depth);   /* 1..8 GVD jobs in flight */
 
 /* ---------------------------------------------------------------------------------------------
  * Streaming ingest (BASELINE.json configs[4]). The handle keeps the global

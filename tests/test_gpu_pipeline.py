@@ -79,3 +79,51 @@ def test_pipeline_state_rules():
     assert_same_graph(c.gvd_wait(), g_sync, "re-run")
     c.gvd_async()
     c.close()                                  # a job in flight is joined
+
+
+def test_pipeline_depth_frames_in_flight():
+    """aos_gvd_pipeline_depth(3): three frames' GVDs run at once, collected in start order; each graph,
+    its markers and a plan on it equal the sequential calls. One start past the depth supersedes the
+    oldest job."""
+    cfg, poly, clouds = frames()
+    clouds = clouds + [orchard.generate(cfg, seed=cfg.seed + 11), orchard.generate(cfg, seed=cfg.seed + 13)]
+    ref = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res))
+    ref.set_polygon(poly)
+    seq = []
+    for cl in clouds:
+        ref.seedgen(cl, want_host=False)
+        seq.append((ref.gvd_from_seedgen(), ref.gvd_markers(), ref.path_plan(aos_gpu.path_query(target=3, previous=2))))
+    ref.close()
+
+    c = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res))
+    c.set_polygon(poly)
+    with pytest.raises(RuntimeError, match="depth"):
+        c.gvd_pipeline_depth(0)
+    c.gvd_pipeline_depth(3)
+    for k in range(3):                         # frames 0-2 in flight together
+        c.seedgen(clouds[k], want_host=False)
+        c.gvd_async()
+    c.seedgen(clouds[3], want_host=False)
+    for k in range(4):
+        if k == 1:
+            c.gvd_async()                      # frame 3 starts while frames 1 and 2 are in flight
+        g = c.gvd_wait()
+        assert_same_graph(g, seq[k][0], f"frame {k}")
+        assert_same_markers(c.gvd_markers(), seq[k][1], f"frame {k}")
+        p = c.path_plan(aos_gpu.path_query(target=3, previous=2))
+        assert np.array_equal(p["poses"], seq[k][2]["poses"]), f"frame {k} plan"
+    with pytest.raises(RuntimeError, match="no GVD job"):
+        c.gvd_wait()
+    # depth 2: a third start supersedes the oldest job
+    c.gvd_pipeline_depth(2)
+    for k in (1, 2, 3):
+        c.seedgen(clouds[k], want_host=False)
+        c.gvd_async()
+    assert_same_graph(c.gvd_wait(), seq[2][0], "superseded: frame 2 first")
+    assert_same_graph(c.gvd_wait(), seq[3][0], "superseded: frame 3")
+    with pytest.raises(RuntimeError, match="no GVD job"):
+        c.gvd_wait()
+    c.seedgen(clouds[0], want_host=False)
+    c.gvd_async()
+    c.gvd_async()                              # (the same frame twice: both jobs run)
+    c.close()                                  # jobs in flight are joined
