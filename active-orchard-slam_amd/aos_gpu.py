@@ -193,6 +193,12 @@ def lib():
         L.aos_gvd_from_seedgen_async.argtypes = [c_vp]
         L.aos_gvd_wait.argtypes = [c_vp, P(GvdOut)]
         L.aos_gvd_pipeline_depth.argtypes = [c_vp, c_i]
+        L.aos_rccl_unique_id.argtypes = [c_vp]
+        L.aos_rccl_create.argtypes = [c_vp, c_i, c_i, c_i, c_u64, P(c_vp)]
+        L.aos_rccl_comm.argtypes = [c_vp]
+        L.aos_rccl_comm.restype = c_vp
+        L.aos_rccl_destroy.argtypes = [c_vp]
+        L.aos_rccl_destroy.restype = None
         L.aos_debug_grid.argtypes = [c_vp, ctypes.c_char_p, c_vp, c_u64]
         L.aos_gvd_markers_get.argtypes = [c_vp, P(GvdMarkers)]
         L.aos_map_reset.argtypes = [c_vp, c_u64]

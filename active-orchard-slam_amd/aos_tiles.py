@@ -6,6 +6,8 @@ the communicators the library calls back into (aos_comm):
   - TorchDistComm: a torch.distributed process group; 'nccl' is RCCL, whose all-gather moves the
     device buffers over xGMI directly; gloo stages through host memory (CPU tests, rehearsals).
   - ThreadGroup: ranks as threads of one process (e.g. every tile of a map on the one GPU of a test box).
+  - RcclComm: the library's own C++ communicator over RCCL (aos_rccl_*): one process per GPU, the
+    collectives run without calling back into Python.
 """
 from __future__ import annotations
 
@@ -117,6 +119,42 @@ class TorchDistComm(_CommBase):
             t = t.to(self.device)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
         return t.cpu().numpy()
+
+
+class RcclComm:
+    """aos_comm implemented in libaos_gpu.so over RCCL (aos_rccl_create): ncclAllGather of the library's
+    HBM exchange buffers and ncclAllReduce(max) of the flags, no Python in the collectives. Rank 0 makes
+    the unique id; a torch.distributed group (any backend) carries it to the other ranks, or pass
+    `unique_id` (128 bytes) directly. Collective: every rank constructs it at the same time."""
+
+    def __init__(self, buf_bytes: int, device: int, rank: int = 0, world: int = 1, group=None,
+                 unique_id: bytes | None = None):
+        self.rank, self.world, self.error = rank, world, None
+        if unique_id is None:
+            uid = (ctypes.c_uint8 * 128)()
+            if rank == 0:
+                _check(lib().aos_rccl_unique_id(uid))
+            if world > 1:
+                import torch.distributed as dist
+                box = [bytes(uid)]
+                dist.broadcast_object_list(box, src=0, group=group)
+                uid = (ctypes.c_uint8 * 128).from_buffer_copy(box[0])
+        else:
+            uid = (ctypes.c_uint8 * 128).from_buffer_copy(bytes(unique_id))
+        self._h = ctypes.c_void_p()
+        _check(lib().aos_rccl_create(uid, rank, world, int(device), int(buf_bytes), ctypes.byref(self._h)))
+        self.c = Comm.from_buffer_copy(ctypes.string_at(lib().aos_rccl_comm(self._h), ctypes.sizeof(Comm)))
+
+    def close(self):
+        if self._h:
+            lib().aos_rccl_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:   # noqa: BLE001 — interpreter shutdown
+            pass
 
 
 class ThreadGroup:

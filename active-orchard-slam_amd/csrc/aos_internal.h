@@ -103,7 +103,7 @@ struct RorLaunch {
     int rx0, ry0, rx1, ry1, wx0, wy0, Wr;
     // tile walk (ror.hip): TB x TB bins per tile, ntx x nty tiles; the raster window as bits (Hr rows
     // of WWr words, wx0 a multiple of 64); a tile's LDS raster window (win_rows x win_w words, 0: none)
-    int TB, ntx, nty, ntiles, Hr, WWr, win_rows, win_w;
+    int TB, TBs, ntx, nty, ntiles, Hr, WWr, win_rows, win_w;   // TB = 1 << TBs
     int staged_cap; int *overflow;   // staged array capacity; set to 1 when the scatter exceeds it
 };
 constexpr int kRtMaxTiles = 36000;   // tiles per frame (LDS histogram of the partition passes: 144 KB)
@@ -152,6 +152,11 @@ int thin_iterations(const int *flags, int iters_run);
 
 // ------------------------------------------------------------------ tiled frames (tiled.hip)
 struct CommError { std::string what; };
+// RCCL communicator (rccl_comm.hip; aos_rccl_* in the ABI)
+void rccl_unique_id(uint8_t *id);
+aos_rccl *rccl_create(const uint8_t *id, int rank, int world, int device, uint64_t buf_bytes);
+const aos_comm *rccl_comm(aos_rccl *r);
+void rccl_destroy(aos_rccl *r);
 constexpr int kMaxTiles = 16;   // per dimension
 struct TilePlan {
     int tiles_x, tiles_y, rank, tx, ty;

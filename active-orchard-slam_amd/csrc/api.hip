@@ -203,6 +203,28 @@ int aos_gvd_wait(aos_ctx *c, aos_gvd_out *out) {
     AOS_GUARD_END
 }
 
+int aos_rccl_unique_id(uint8_t *id) {
+    if (!id) { set_error("aos_rccl_unique_id: null argument"); return AOS_E_INVALID; }
+    AOS_GUARD_BEGIN
+    rccl_unique_id(id);
+    return AOS_OK;
+    AOS_GUARD_END
+}
+
+int aos_rccl_create(const uint8_t *id, int32_t rank, int32_t world, int32_t device, uint64_t buf_bytes,
+                    aos_rccl **out) {
+    if (!id || !out) { set_error("aos_rccl_create: null argument"); return AOS_E_INVALID; }
+    *out = nullptr;
+    AOS_GUARD_BEGIN
+    *out = rccl_create(id, rank, world, device, buf_bytes);
+    return AOS_OK;
+    AOS_GUARD_END
+}
+
+const aos_comm *aos_rccl_comm(aos_rccl *r) { return r ? rccl_comm(r) : nullptr; }
+
+void aos_rccl_destroy(aos_rccl *r) { rccl_destroy(r); }
+
 int aos_gvd_pipeline_depth(aos_ctx *c, int32_t depth) {
     if (!c) { set_error("aos_gvd_pipeline_depth: null handle"); return AOS_E_INVALID; }
     if (depth < 1 || depth > 8) { set_error("aos_gvd_pipeline_depth: depth must be in [1, 8]"); return AOS_E_INVALID; }

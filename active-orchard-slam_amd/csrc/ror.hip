@@ -100,21 +100,31 @@ __device__ __forceinline__ bool rt_in(const RorLaunch &L, float4 p, float4 q) {
 // right after workgroup w - 1's.
 // block sizes: the count pass runs best at 256 threads, the scatter pass at 512 (measured,
 // tools/rorbench); both walk the same per-workgroup chunks (a multiple of kRtChunkQ points)
-#ifndef AOS_RT_PER
-#define AOS_RT_PER 8
+#ifndef AOS_RT_CPER
+#define AOS_RT_CPER 8
+#endif
+#ifndef AOS_RT_SPER
+#define AOS_RT_SPER 4
+#endif
+#ifndef AOS_RT_CTB
+#define AOS_RT_CTB 256
 #endif
 #ifndef AOS_RT_G
 #define AOS_RT_G 512
 #endif
-constexpr int kRtPer = AOS_RT_PER, kRtCountTB = 256, kRtScatterTB = 512, kRtChunkQ = kRtScatterTB * kRtPer;
+#ifndef AOS_RT_COUNT_EXP
+#define AOS_RT_COUNT_EXP 0
+#endif
+constexpr int kRtCountPer = AOS_RT_CPER, kRtScatterPer = AOS_RT_SPER, kRtCountTB = AOS_RT_CTB, kRtScatterTB = 512;
+constexpr int kRtChunkQ = 4096;   // chunk granularity (points): a multiple of both passes' sub-chunks
 
 // tiles whose bins a point's 3 x 3 bins touch: [tx0, tx1] x [ty0, ty1], own tile (bx / TB, by / TB)
 __device__ __forceinline__ void rt_tiles(const RorLaunch &L, int bx, int by, int &tx0, int &tx1, int &ty0, int &ty1) {
-    tx0 = max(bx - 1, 0) / L.TB; tx1 = min(bx + 1, L.nbx - 1) / L.TB;
-    ty0 = max(by - 1, 0) / L.TB; ty1 = min(by + 1, L.nby - 1) / L.TB;
+    tx0 = max(bx - 1, 0) >> L.TBs; tx1 = min(bx + 1, L.nbx - 1) >> L.TBs;   // (bins are >= 0)
+    ty0 = max(by - 1, 0) >> L.TBs; ty1 = min(by + 1, L.nby - 1) >> L.TBs;
 }
 
-template <bool SCATTER, bool STD, int kRtTB>
+template <bool SCATTER, bool STD, int kRtTB, int kRtPer>
 __global__ __launch_bounds__(kRtTB) void k_rt_part(RorLaunch L, int *H, const int *tstart, uint64_t chunk,
                                                    float4 *staged, unsigned long long *n_own) {
     constexpr int kRtSub = kRtTB * kRtPer;
@@ -148,10 +158,13 @@ __global__ __launch_bounds__(kRtTB) void k_rt_part(RorLaunch L, int *H, const in
             const float x = pt[j].x, y = pt[j].y, z = pt[j].z;
             if (__float_as_int(pt[j].w) < 0 || !rt_binned(L, x, y, z)) continue;
             ++own;
+#if AOS_RT_COUNT_EXP == 2   // (timing experiment: 2 = loads and the bounds test only)
+            if (!SCATTER) continue;
+#endif
             int bx, by, tx0, tx1, ty0, ty1;
             rt_bin(L, x, y, bx, by);
             rt_tiles(L, bx, by, tx0, tx1, ty0, ty1);
-            const int otile = (by / L.TB) * L.ntx + bx / L.TB;
+            const int otile = (by >> L.TBs) * L.ntx + (bx >> L.TBs);
             const float4 q = make_float4(x, y, z, __int_as_float(SCATTER && rt_candidate(L, x, y, z) ? 1 : 0));
             for (int ty = ty0; ty <= ty1; ++ty)
                 for (int tx = tx0; tx <= tx1; ++tx) {
@@ -163,7 +176,9 @@ __global__ __launch_bounds__(kRtTB) void k_rt_part(RorLaunch L, int *H, const in
                         if (pos < L.staged_cap) staged[pos] = v;    // else: overflow, the frame is redone
                         else *L.overflow = 1;
                     } else {
+#if AOS_RT_COUNT_EXP != 1   // (timing experiment: 1 = no LDS histogram)
                         atomicAdd(&hist[t], 1);
+#endif
                     }
                 }
         }
@@ -472,7 +487,9 @@ __global__ __launch_bounds__(1024) void k_rt_sum_kept(const int *kept_tile, int 
 // depend on it.
 void rt_configure(RorLaunch &L, int Hr, int WWr, double est_binned, int force_tb) {
     auto tiles = [&](int tb) {
+        if (tb <= 0 || (tb & (tb - 1))) throw std::runtime_error("ROR tile size must be a power of two");
         L.TB = tb;
+        L.TBs = __builtin_ctz((unsigned)tb);
         L.ntx = (L.nbx + tb - 1) / tb;
         L.nty = (L.nby + tb - 1) / tb;
         return (long long)L.ntx * L.nty;
@@ -510,12 +527,13 @@ uint64_t rt_chunk(const RorLaunch &L, int G) {
 template <bool SCATTER, bool STD>
 static void rt_part(const RorLaunch &L, int *H, const int *tstart, int G, float4 *staged, unsigned long long *n_own,
                     hipStream_t s) {
-    constexpr int TB = SCATTER ? kRtScatterTB : kRtCountTB;
+    constexpr int TB = SCATTER ? kRtScatterTB : kRtCountTB, PER = SCATTER ? kRtScatterPer : kRtCountPer;
+    static_assert(kRtChunkQ % (TB * PER) == 0 || (TB * PER) % kRtChunkQ == 0, "chunk granularity");
     const size_t lds = sizeof(int) * (size_t)L.ntiles;
     if (lds > 64 * 1024)   // the tile histogram exceeds the default dynamic-LDS limit (gfx950: 160 KB)
-        AOS_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rt_part<SCATTER, STD, TB>),
+        AOS_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rt_part<SCATTER, STD, TB, PER>),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    k_rt_part<SCATTER, STD, TB><<<G, TB, lds, s>>>(L, H, tstart, rt_chunk(L, G), staged, n_own);
+    k_rt_part<SCATTER, STD, TB, PER><<<G, TB, lds, s>>>(L, H, tstart, rt_chunk(L, G), staged, n_own);
     AOS_HIP(hipGetLastError());
 }
 static bool rt_std(const RorLaunch &L) { return L.step == 16 && L.ox == 0 && L.oy == 4 && L.oz == 8; }

@@ -180,7 +180,9 @@ def main():
         tx, ty = aos_tiles.tiling_for(world)
         plan = aos_tiles.tile_plan(params, poly, tx, ty, rank)
         cloud = aos_tiles.shard(orchard.generate(cfg), plan["points_box"])
-        if world > 1:
+        if world > 1 and backend == "nccl":   # the library's C++ RCCL communicator (no Python callbacks)
+            comm = aos_tiles.RcclComm(plan["exchange_bytes"], gpu, rank, world)
+        elif world > 1:                        # gloo rehearsal (ranks sharing a GPU)
             comm = aos_tiles.TorchDistComm(plan["exchange_bytes"], dev)
         else:
             comm = aos_tiles.ThreadGroup(1).comm(0, plan["exchange_bytes"], dev)

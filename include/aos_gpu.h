@@ -196,6 +196,19 @@ typedef struct aos_comm {
     int (*all_reduce_max)(void *user, int32_t *values, int32_t n);
 } aos_comm;
 
+/* RCCL communicator (one process per GPU, e.g. a torch.distributed launch): an aos_comm whose
+ * exchange buffers live in HBM, all-gather = ncclAllGather over xGMI, max all-reduce =
+ * ncclAllReduce(ncclMax) of the int32 flags. Rank 0 makes the id (NCCL_UNIQUE_ID_BYTES = 128 bytes)
+ * and hands it to every rank out of band; aos_rccl_create is collective (every rank, at once).
+ * RCCL (librccl.so.1) is loaded at run time by aos_rccl_unique_id / aos_rccl_create only. This
+ * replaces the in-process group's peer copies when the ranks are separate processes. */
+typedef struct aos_rccl aos_rccl;
+int aos_rccl_unique_id(uint8_t *id128);
+int aos_rccl_create(const uint8_t *id128, int32_t rank, int32_t world, int32_t device, uint64_t buf_bytes,
+                    aos_rccl **out);
+const aos_comm *aos_rccl_comm(aos_rccl *comm);   /* valid until aos_rccl_destroy */
+void aos_rccl_destroy(aos_rccl *comm);
+
 typedef struct aos_tile_plan {
     int32_t tiles_x, tiles_y, rank, tile_x, tile_y;
     int32_t halo_rows, halo_words;       /* halo depth (0 along an untiled dimension)          */

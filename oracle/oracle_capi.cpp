@@ -6,6 +6,9 @@
 
 using namespace orc;
 
+// (x, y) doubles of a V2 vector; null when empty (taking ->x of an empty vector's data() is UB)
+template <class V> static const double *xy_of(const V &v) { return v.empty() ? nullptr : &v[0].x; }
+
 extern "C" {
 
 void orc_default_params(orc_params *p) {
@@ -70,12 +73,12 @@ void *orc_seedgen_run(const orc_params *p, const uint8_t *cloud, uint64_t n, uin
     out->n_rows = (int32_t)R->rows.size();
     out->row_center = R->row_center.data(); out->row_start = R->row_start.data();
     out->row_end = R->row_end.data(); out->row_length = R->row_length.data();
-    out->n_virtual = (int32_t)R->virtual_seeds.size(); out->virtual_xy = &R->virtual_seeds.data()->x;
-    out->n_ray = (int32_t)R->ray_seeds.size(); out->ray_xy = &R->ray_seeds.data()->x;
-    out->n_endpoint = (int32_t)R->endpoint_seeds.size(); out->endpoint_xy = &R->endpoint_seeds.data()->x;
-    out->n_voronoi = (int32_t)R->voronoi_seeds.size(); out->voronoi_xy = &R->voronoi_seeds.data()->x;
-    out->rows_info_xy = &R->rows_info.data()->x;
-    out->n_cluster_info = (int32_t)R->cluster_info.size(); out->cluster_info_xy = &R->cluster_info.data()->x;
+    out->n_virtual = (int32_t)R->virtual_seeds.size(); out->virtual_xy = xy_of(R->virtual_seeds);
+    out->n_ray = (int32_t)R->ray_seeds.size(); out->ray_xy = xy_of(R->ray_seeds);
+    out->n_endpoint = (int32_t)R->endpoint_seeds.size(); out->endpoint_xy = xy_of(R->endpoint_seeds);
+    out->n_voronoi = (int32_t)R->voronoi_seeds.size(); out->voronoi_xy = xy_of(R->voronoi_seeds);
+    out->rows_info_xy = xy_of(R->rows_info);
+    out->n_cluster_info = (int32_t)R->cluster_info.size(); out->cluster_info_xy = xy_of(R->cluster_info);
     return R;
 }
 

@@ -21,7 +21,7 @@ namespace orc {
 // FLANN L2_Simple distance: ((0 + dx*dx) + dy*dy) + dz*dz in float.
 // Non-finite points are never neighbours and are always removed.
 void ror(const float *xyz, uint64_t n, bool is_dense, double radius, int min_pts, uint8_t *keep) {
-    std::memset(keep, 0, n);
+    if (n) std::memset(keep, 0, n);
     const double cell = radius * 1.0001;
     double mnx = 1e300, mny = 1e300, mnz = 1e300, mxx = -1e300, mxy = -1e300, mxz = -1e300;
     uint64_t nfin = 0;

@@ -229,3 +229,28 @@ def test_group_blob_vs_oracle_and_bad_cloud():
     g2 = grp.process([cloud, cloud])
     assert g2["thin_iters"] == o["thin_iters"]
     grp.close()
+
+
+def test_rccl_comm_single_rank_frame():
+    """The library's C++ RCCL communicator (aos_rccl_*: ncclAllGather / ncclAllReduce(max) on its own
+    HBM buffers, no Python callbacks) drives a 1 x 1 tiled C1 frame: the root's outputs equal the
+    single-GPU frame. (One GPU per box: RCCL refuses two ranks on one device, so the multi-rank path is
+    covered by the thread/gloo tests through the same aos_comm contract.)"""
+    cfg = orchard.CONFIGS["C1"]
+    cloud, poly = orchard.generate(cfg), orchard.polygon(cfg)
+    single = _single(cloud, poly, cfg.res)
+    params = aos_gpu.default_params(grid_resolution=cfg.res)
+    plan = T.tile_plan(params, poly, 1, 1, 0)
+    comm = T.RcclComm(plan["exchange_bytes"], device=0, rank=0, world=1)
+    c = aos_gpu.Ctx(params)
+    c.set_polygon(poly)
+    g = c.tiled_seedgen(comm, 1, 1, cloud, root=0)
+    g2 = c.tiled_seedgen(comm, 1, 1, cloud, root=0)   # the communicator is reusable across frames
+    assert g2["thin_iters"] == g["thin_iters"]
+    grids = {w: c.debug_grid(w, (g["height"], g["width"])) for w in GRIDS}
+    gg = c.gvd_from_seedgen()
+    c.close()
+    comm.close()
+    _assert_same(single, (g, [g], grids, gg))
+    with pytest.raises(RuntimeError, match="rank"):
+        T.RcclComm(plan["exchange_bytes"], device=0, rank=1, world=1, unique_id=bytes(128))

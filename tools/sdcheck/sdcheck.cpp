@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -82,7 +83,9 @@ int main(int argc, char **argv) {
     std::vector<Case> cases;
     // random uniform, lattices (co-circular everywhere), lattice rows in row-by-row order (orchard-like),
     // jittered lattices, duplicates / near-duplicates, collinear runs, tiny clusters
-    for (int rep = 0; rep < 40; ++rep) {
+    const char *reps_env = getenv("AOS_SDCHECK_REPS");   // (the sanitizer build runs a few repetitions)
+    const int reps = reps_env ? atoi(reps_env) : 40;
+    for (int rep = 0; rep < reps; ++rep) {
         sm_state = 1000 + rep;
         Case u{"uniform", {}, {0, 50, 0, 50}};
         const int n = 200 + (int)(uni() * 3000);
