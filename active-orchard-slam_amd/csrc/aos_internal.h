@@ -137,7 +137,11 @@ constexpr int kThinItersPerLaunch = 8;
 // Cells whose deletions a launch reports in flags (rows [y0, y1), words [c0, c1) of the image it is
 // given: a tile's own cells inside its halo window), and whether a launch may skip itself once an
 // earlier iteration deleted nothing (single GPU only: a tile must keep pace with its neighbours).
-struct ThinOwn { int y0, y1, c0, c1, early_exit; };
+// act_prev / act_next (optional, whole-map frames only): per tile, 1 iff its interior deleted something
+// in the last two sub-iterations of the previous / this launch (thin_tiles(g) ints each); a tile whose
+// 3 x 3 tile neighbourhood was quiet is a fixed point for the next KIT iterations and is copied.
+struct ThinOwn { int y0, y1, c0, c1, early_exit; const int *act_prev = nullptr; int *act_next = nullptr; };
+int thin_tiles(const FrameGeom &g);
 void launch_thin_block(const uint64_t *in, uint64_t *out, const FrameGeom &g, int base_iter, int *flags,
                        const ThinOwn &own, hipStream_t s);
 void launch_draw_rect(int8_t *grid, const FrameGeom &g, int gx0, int gy0, int gx1, int gy1, hipStream_t s);

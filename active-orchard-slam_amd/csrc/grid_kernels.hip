@@ -137,7 +137,14 @@ void launch_open(const uint64_t *in, uint64_t *out, const FrameGeom &g, hipStrea
 //   2 <= B <= 6  : at least two set and at least two clear among p2..p9
 //   m1 == m2 == 0: iter 0: p2p4p6 = p4p6p8 = 0; iter 1: p2p4p8 = p2p6p8 = 0
 // Rows 0 / H-1 and columns 0 / W-1 of the image are never examined (ximgproc loops 1..n-2).
-constexpr int TH = 64, TWW = 8, KIT = kThinItersPerLaunch, HR = 2 * KIT, NR = TH + 2 * HR, NC = TWW + 2;
+#ifndef AOS_THIN_TB
+#define AOS_THIN_TB 256
+#endif
+#ifndef AOS_THIN_TH
+#define AOS_THIN_TH 64
+#endif
+constexpr int TH = AOS_THIN_TH, TWW = 8, KIT = kThinItersPerLaunch, HR = 2 * KIT, NR = TH + 2 * HR, NC = TWW + 2;
+constexpr int kThinTB = AOS_THIN_TB;
 
 __device__ __forceinline__ uint64_t zs_step(uint64_t n0, uint64_t n1, uint64_t n2, uint64_t c0, uint64_t c1,
                                             uint64_t c2, uint64_t s0, uint64_t s1, uint64_t s2, int sub) {
@@ -169,12 +176,34 @@ __device__ __forceinline__ uint64_t zs_step(uint64_t n0, uint64_t n1, uint64_t n
     return c1 & A1 & B26 & m;  // cells to delete
 }
 
-__global__ __launch_bounds__(256) void k_thin_block(const uint64_t *__restrict__ in, uint64_t *__restrict__ out,
+__global__ __launch_bounds__(kThinTB) void k_thin_block(const uint64_t *__restrict__ in, uint64_t *__restrict__ out,
                                                     int W, int H, int WW, int base_iter, int *flags, ThinOwn own) {
     if (own.early_exit && base_iter >= 2 && flags[1 + base_iter - 1] == 0) return;  // converged in an earlier launch
     __shared__ uint64_t buf[2][NR][NC];
     __shared__ int chg_shared;
     const int ty0 = blockIdx.y * TH, tc0 = blockIdx.x * TWW;
+    const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+    if (own.act_prev) {
+        // No tile interior within one tile of this one deleted anything in the last two sub-iterations
+        // of the previous launch: the 3 x 3 tiles are a fixed point of both sub-iterations, and a change
+        // outside them travels one cell per sub-iteration, so it cannot reach this tile (>= TH rows /
+        // 64 * TWW cells away) within this launch's 2 * KIT <= HR sub-iterations. Copy it through.
+        bool quiet_nb = true;
+        for (int dy = -1; dy <= 1; ++dy)
+            for (int dx = -1; dx <= 1; ++dx) {
+                const int by = (int)blockIdx.y + dy, bx = (int)blockIdx.x + dx;
+                if (by >= 0 && by < (int)gridDim.y && bx >= 0 && bx < (int)gridDim.x && own.act_prev[by * gridDim.x + bx])
+                    quiet_nb = false;
+            }
+        if (quiet_nb) {
+            for (int idx = threadIdx.x; idx < TH * TWW; idx += blockDim.x) {
+                const int r = idx / TWW, k = idx - r * TWW, gy = ty0 + r, gc = tc0 + k;
+                if (gy < H && gc < WW) out[(size_t)gy * WW + gc] = in[(size_t)gy * WW + gc];
+            }
+            if (threadIdx.x == 0) own.act_next[tile] = 0;
+            return;
+        }
+    }
     if (threadIdx.x == 0) chg_shared = 0;
     for (int idx = threadIdx.x; idx < NR * NC; idx += blockDim.x) {
         int r = idx / NC, k = idx - r * NC;
@@ -185,8 +214,14 @@ __global__ __launch_bounds__(256) void k_thin_block(const uint64_t *__restrict__
     int chg = 0;        // bit j: iteration base_iter + j deleted something inside this tile
     int nonempty = 0;   // after iteration 0 (only meaningful when base_iter == 0)
     int cur = 0;
+    // Two consecutive sub-iterations (one of each parity) that delete nothing anywhere in the loaded
+    // window leave it a fixed point of both: the remaining sub-iterations of this launch would
+    // recompute the same window, so the block stops there (its later iterations delete nothing).
+    int quiet = 0;
+    int late_del = 0;   // this tile's interior deleted something in the launch's last two sub-iterations
     for (int s = 0; s < 2 * KIT; ++s) {
         const int sub = s & 1;
+        int any_del = 0;
         for (int idx = threadIdx.x; idx < NR * NC; idx += blockDim.x) {
             int r = idx / NC, k = idx - r * NC;
             const int gy = ty0 - HR + r, gc = tc0 - 1 + k;
@@ -195,7 +230,7 @@ __global__ __launch_bounds__(256) void k_thin_block(const uint64_t *__restrict__
                               gc >= own.c0 && gc < own.c1;
             uint64_t c1 = buf[cur][r][k];
             uint64_t nw = c1;
-            if (r > 0 && r < NR - 1) {
+            if (c1 && r > 0 && r < NR - 1) {   // (an empty word deletes nothing: whole waves skip)
                 uint64_t c0 = k > 0 ? buf[cur][r][k - 1] : 0ull, c2 = k < NC - 1 ? buf[cur][r][k + 1] : 0ull;
                 uint64_t n0 = k > 0 ? buf[cur][r - 1][k - 1] : 0ull, n1 = buf[cur][r - 1][k],
                          n2 = k < NC - 1 ? buf[cur][r - 1][k + 1] : 0ull;
@@ -211,12 +246,15 @@ __global__ __launch_bounds__(256) void k_thin_block(const uint64_t *__restrict__
                 del &= em;
                 nw = c1 & ~del;
                 if (del && mine) chg |= 1 << (s >> 1);
+                if (del && s >= 2 * KIT - 2 && r >= HR && r < HR + TH && k >= 1 && k <= TWW) late_del = 1;
+                any_del |= del != 0;
             }
             buf[cur ^ 1][r][k] = nw;
             if (s == 1 && base_iter == 0 && nw && mine) nonempty = 1;
         }
         cur ^= 1;
-        __syncthreads();
+        quiet = __syncthreads_or(any_del) ? 0 : quiet + 1;
+        if (quiet >= 2) break;   // (block-uniform)
     }
     for (int idx = threadIdx.x; idx < TH * TWW; idx += blockDim.x) {
         int r = idx / TWW, k = idx - r * TWW;
@@ -224,7 +262,8 @@ __global__ __launch_bounds__(256) void k_thin_block(const uint64_t *__restrict__
         if (gy < H && gc < WW) out[(size_t)gy * WW + gc] = buf[cur][HR + r][1 + k];
     }
     if (chg || nonempty) atomicOr(&chg_shared, chg | (nonempty << 30));
-    __syncthreads();
+    const int late_any = __syncthreads_or(late_del);
+    if (own.act_next && threadIdx.x == 0) own.act_next[tile] = late_any;
     if (threadIdx.x == 0 && chg_shared) {
         int m = chg_shared;
         if (m & (1 << 30)) atomicOr(&flags[0], 1);
@@ -233,10 +272,13 @@ __global__ __launch_bounds__(256) void k_thin_block(const uint64_t *__restrict__
     }
 }
 
+int thin_tiles(const FrameGeom &g) { return cdiv(g.WW, TWW) * cdiv(g.H, TH); }
+
 void launch_thin_block(const uint64_t *in, uint64_t *out, const FrameGeom &g, int base_iter, int *flags,
                        const ThinOwn &own, hipStream_t s) {
+    static_assert(2 * KIT <= HR && 2 * KIT <= TH && 2 * KIT <= 64 * TWW, "the copy-through rule needs a tile >= 2 KIT cells");
     dim3 grid(cdiv(g.WW, TWW), cdiv(g.H, TH));
-    k_thin_block<<<grid, 256, 0, s>>>(in, out, g.W, g.H, g.WW, base_iter, flags, own);
+    k_thin_block<<<grid, kThinTB, 0, s>>>(in, out, g.W, g.H, g.WW, base_iter, flags, own);
 }
 
 // a16 markPolygonBoundaryAsOccupied (seed_gen:772-825): the bbox +- 2.5 m rectangle in grid cells;

@@ -16,7 +16,7 @@ using namespace aos;
 
 void aos_ctx::release() {
     for (DevBuf *b : {&cloud_copy, &bin_count, &bin_start, &pt_binslot, &sorted, &ror_scratch, &ror_bigbins, &scan_tmp, &counters,
-                      &raster_bits, &infl_bits, &open_bits, &thin_a, &thin_b, &occ_bytes, &skel_bytes, &flags,
+                      &raster_bits, &infl_bits, &open_bits, &thin_a, &thin_b, &thin_act, &occ_bytes, &skel_bytes, &flags,
                       &full_infl, &full_skel, &map_buf, &scan_stage})
         b->release();
     h_small.release();
@@ -425,25 +425,29 @@ bool aos_ctx::run_seedgen_once(bool want_host, aos_seedgen_out &out, bool allow_
     const int max_iters = std::max(g.W, g.H) + 4;   // Zhang-Suen removes >= 1 cell per changing iteration
     int *d_flags = static_cast<int *>(flags.ensure(sizeof(int) * (2 + max_iters + K)));
     int *h_flags = static_cast<int *>(h_small.ensure(sizeof(int) * (2 + max_iters + K)));
-    const ThinOwn whole{0, g.H, 0, g.WW, 1};
-    // first batch: opening + 3 temporal blocks (typical T <= 24 needs no more), then the flags read-back.
+    ThinOwn whole{0, g.H, 0, g.WW, 1};
+    int *d_act = static_cast<int *>(thin_act.ensure(sizeof(int) * 2 * (size_t)thin_tiles(g)));
+    // first batch: opening + temporal blocks sized from the last frame's T, then the flags read-back.
     // (Round 1 replayed this batch as a hipGraph captured on the first frame. On ROCm 7.2 a replay on a
     // later frame with new data left garbage in the flags buffer in some frame sequences — the
     // thinning count then ran to the iteration cap while the grids stayed right; repro:
     // tools/dbg_stream7.py. Five plain launches cost a few microseconds, so they are issued directly.)
     // Launches past convergence return at once (k_thin_block reads the previous iteration's flag on the
-    // device), so the first batch is sized from the last frame's T (at least 3 launches) and later
+    // device), so the first batch is sized from the last frame's T (at least 2 launches) and later
     // batches double: a frame pays one host round trip in the common case, a few when T jumps.
     AOS_HIP(hipMemsetAsync(d_flags, 0, sizeof(int) * (2 + max_iters + K), s));
     launch_open(d_ibits, d_open, g, s);
     const int cap_launches = std::max(3, max_iters / K);
-    int launched = 0, batch_n = std::min(cap_launches, std::max(3, (thin_iters_prev + 2 + K - 1) / K));
+    int launched = 0, batch_n = std::min(cap_launches, std::max(2, (thin_iters_prev + 2 + K - 1) / K));
     const uint64_t *src = d_open;
     const uint64_t *final_buf = d_open;
     int T = 0;
     for (;;) {
         for (int j = 0; j < batch_n && launched < cap_launches; ++j) {
             uint64_t *dst = bufs[launched & 1];
+            // tile activity of the previous launch (none for the first: every tile runs)
+            whole.act_prev = launched ? d_act + (size_t)((launched - 1) & 1) * thin_tiles(g) : nullptr;
+            whole.act_next = d_act + (size_t)(launched & 1) * thin_tiles(g);
             launch_thin_block(src, dst, g, launched * K, d_flags, whole, s);
             src = dst;
             ++launched;
