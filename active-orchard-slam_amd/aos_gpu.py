@@ -379,7 +379,7 @@ class Ctx:
         return {"root": False, "width": o.info.width, "height": o.info.height, "thin_iters": o.thin_iters,
                 "n_clipped": o.n_clipped, "n_input": o.n_input, "n_binned": o.n_binned,
                 "ms": {"ror": o.ms_ror, "grid": o.ms_grid, "thin": o.ms_thin, "total": o.ms_total,
-                       "ror_count": o.ms_ror_count}}
+                       "ror_count": o.ms_ror_count, "ror_bin": o.ms_ror_bin, "ror_scatter": o.ms_ror_scatter}}
 
     def reprocess(self, want_host=True) -> dict:
         o = SeedGenOut()

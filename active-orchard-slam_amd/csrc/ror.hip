@@ -260,57 +260,161 @@ __device__ __forceinline__ int rt_scan(const RorLaunch &L, float4 p, Pts pts, in
 // + ring: 34^2), and the tile's raster window (kRtWinWords 64-bit words): ~40 KB, 3 workgroups per CU
 constexpr int kRtMaxLocalBins = 34 * 34, kRtWinWords = 320;
 
-// Tiles with more than kRorCap points (a streaming map's scan footprint): counting sort by bin into the
-// tile's range of the scratch array, bin offsets to bigbins[t * (nlb + 1) ...]. A separate launch, so
-// k_rt_ror reads both through a kernel boundary (a workgroup must not re-read global data it wrote
-// itself in the same launch: the CU's vector L1 may hold stale lines of that range).
-__global__ __launch_bounds__(kRorThreads) void k_rt_bigsort(RorLaunch L, const int *tstart, const float4 *staged,
-                                                            float4 *scratch, int *bigbins, const int *dirty) {
-    __shared__ int bstart[kRtMaxLocalBins + 1];
-    const int tid = threadIdx.x, t = blockIdx.x;
-    if (dirty && dirty[t + 1] == dirty[t]) return;
-    const int a = tstart[t], n = tstart[t + 1] - a;
-    if (n <= kRorCap || a + n > L.staged_cap) return;
-    const int tx = t % L.ntx, ty = t / L.ntx;
-    const int LB = L.TB + 2, nlb = LB * LB, bx0 = tx * L.TB - 1, by0 = ty * L.TB - 1;
-    auto lbin = [&](float4 q) {
-        int bx, by;
-        rt_bin(L, q.x, q.y, bx, by);
-        return (by - by0) * LB + (bx - bx0);
-    };
-    for (int i = tid; i <= nlb; i += kRorThreads) bstart[i] = 0;
+// Tiles with more than kRorCap points (a streaming map's scan footprint: up to ~10^6 points in one
+// tile after a few dozen scans) do not fit LDS, and one workgroup per such tile leaves most CUs idle
+// while a few walk a huge list. They are listed (k_rt_biglist) and each is split into kBigC chunks of
+// its list, one workgroup per (tile, chunk) in grids of kBigC x kBigY that loop over the list:
+//   k_rt_bighist     per-chunk LDS bin histogram, added into the tile's global bin totals
+//   k_rt_bigscan     per tile: bin starts (bigbins row) and bin cursors (= starts)
+//   k_rt_bigscatter  per chunk: one global atomic per (chunk, non-empty bin) reserves its runs, then the
+//                    chunk's points go bin-sorted into the tile's range of the scratch array
+//   k_rt_ror_big     per chunk: the neighbour counts of the chunk's points, searched in the tile's
+//                    bin-sorted scratch range (through the kernel boundary; see k_rt_ror for the rules)
+// The order inside a bin depends on the atomics' order; the keep decision and the raster do not.
+constexpr int kBigC = 16, kBigY = 128, kBigTB = 512;
+struct BigBufs { int *starts, *cur, *list; };   // rt_bigbins_ints(L) ints: 2 x ntiles x (nlb + 1), 1 + ntiles
+static BigBufs big_bufs(const RorLaunch &L, int *B) {
+    const size_t row = (size_t)(L.TB + 2) * (L.TB + 2) + 1, nt = (size_t)L.ntiles;
+    return BigBufs{B, B + nt * row, B + 2 * nt * row};
+}
+
+__device__ __forceinline__ int rt_lbin(const RorLaunch &L, float4 q, int bx0, int by0, int LB) {
+    int bx, by;
+    rt_bin(L, q.x, q.y, bx, by);
+    return (by - by0) * LB + (bx - bx0);   // in [0, LB^2): a copy lies in the tile's 3 x 3 reach
+}
+
+// list[0] = number of big tiles, list[1..]: the tiles; their cursor rows zeroed, kept_tile reset
+__global__ __launch_bounds__(256) void k_rt_biglist(RorLaunch L, const int *tstart, BigBufs B, int *kept_tile,
+                                                    const int *dirty) {
+    __shared__ int big;
+    const int t = blockIdx.x;
+    if (threadIdx.x == 0) {
+        const int a = tstart[t], n = tstart[t + 1] - a;
+        big = (!dirty || dirty[t + 1] != dirty[t]) && n > kRorCap && a + n <= L.staged_cap;
+        if (big) {
+            B.list[1 + atomicAdd(&B.list[0], 1)] = t;
+            if (kept_tile) kept_tile[t] = 0;
+        }
+    }
     __syncthreads();
-    for (int k = tid; k < n; k += kRorThreads) atomicAdd(&bstart[lbin(staged[a + k]) + 1], 1);
-    __syncthreads();
-    if (tid == 0)   // (rare tiles: a serial scan is fine)
-        for (int i = 1; i <= nlb; ++i) bstart[i] += bstart[i - 1];
-    __syncthreads();
-    for (int i = tid; i <= nlb; i += kRorThreads) bigbins[(size_t)t * (nlb + 1) + i] = bstart[i];
-    __syncthreads();
-    for (int k = tid; k < n; k += kRorThreads) {   // bstart becomes the cursor
-        const float4 v = staged[a + k];
-        scratch[a + atomicAdd(&bstart[lbin(v)], 1)] = v;
+    if (!big) return;
+    const int nlb1 = (L.TB + 2) * (L.TB + 2) + 1;
+    for (int i = threadIdx.x; i < nlb1; i += 256) B.cur[(size_t)t * nlb1 + i] = 0;
+}
+
+// the chunk [k0, k1) of big tile i of the list
+__device__ __forceinline__ void big_chunk(const RorLaunch &L, const int *tstart, int t, int &a, int &k0, int &k1) {
+    a = tstart[t];
+    const int n = tstart[t + 1] - a;
+    k0 = (int)((long long)n * blockIdx.x / kBigC);
+    k1 = (int)((long long)n * (blockIdx.x + 1) / kBigC);
+}
+
+__global__ __launch_bounds__(kBigTB) void k_rt_bighist(RorLaunch L, const int *tstart, const float4 *staged, BigBufs B) {
+    __shared__ int h[kRtMaxLocalBins + 1];
+    const int nbig = B.list[0], LB = L.TB + 2, nlb = LB * LB;
+    for (int i = blockIdx.y; i < nbig; i += gridDim.y) {
+        const int t = B.list[1 + i], tx = t % L.ntx, ty = t / L.ntx;
+        int a, k0, k1;
+        big_chunk(L, tstart, t, a, k0, k1);
+        for (int b = threadIdx.x; b < nlb; b += kBigTB) h[b] = 0;
+        __syncthreads();
+        for (int k = k0 + threadIdx.x; k < k1; k += kBigTB)
+            atomicAdd(&h[rt_lbin(L, staged[a + k], tx * L.TB - 1, ty * L.TB - 1, LB)], 1);
+        __syncthreads();
+        int *tot = B.cur + (size_t)t * (nlb + 1);
+        for (int b = threadIdx.x; b < nlb; b += kBigTB)
+            if (h[b]) atomicAdd(&tot[b], h[b]);
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_rt_bigscan(RorLaunch L, const int *tstart, BigBufs B) {
+    constexpr int kSeg = (kRtMaxLocalBins + 1023) / 1024;
+    typedef hipcub::BlockScan<int, 1024> Scan;
+    __shared__ typename Scan::TempStorage tmp;
+    const int nbig = B.list[0], nlb = (L.TB + 2) * (L.TB + 2);
+    for (int i = blockIdx.x; i < nbig; i += gridDim.x) {
+        const int t = B.list[1 + i];
+        int *tot = B.cur + (size_t)t * (nlb + 1), *st = B.starts + (size_t)t * (nlb + 1);
+        int v[kSeg], run = 0;
+#pragma unroll
+        for (int j = 0; j < kSeg; ++j) {
+            const int b = threadIdx.x * kSeg + j;
+            v[j] = b < nlb ? tot[b] : 0;
+            run += v[j];
+        }
+        int before;
+        Scan(tmp).ExclusiveSum(run, before);
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kSeg; ++j) {
+            const int b = threadIdx.x * kSeg + j;
+            if (b < nlb) { st[b] = before; tot[b] = before; }
+            before += v[j];
+        }
+        if (threadIdx.x == 1023) st[nlb] = before;   // = the tile's point count
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(kBigTB) void k_rt_bigscatter(RorLaunch L, const int *tstart, const float4 *staged,
+                                                          float4 *scratch, BigBufs B) {
+    __shared__ int h[kRtMaxLocalBins + 1];
+    const int nbig = B.list[0], LB = L.TB + 2, nlb = LB * LB;
+    for (int i = blockIdx.y; i < nbig; i += gridDim.y) {
+        const int t = B.list[1 + i], tx = t % L.ntx, ty = t / L.ntx;
+        const int bx0 = tx * L.TB - 1, by0 = ty * L.TB - 1;
+        int a, k0, k1;
+        big_chunk(L, tstart, t, a, k0, k1);
+        for (int b = threadIdx.x; b < nlb; b += kBigTB) h[b] = 0;
+        __syncthreads();
+        for (int k = k0 + threadIdx.x; k < k1; k += kBigTB) atomicAdd(&h[rt_lbin(L, staged[a + k], bx0, by0, LB)], 1);
+        __syncthreads();
+        int *cur = B.cur + (size_t)t * (nlb + 1);
+        for (int b = threadIdx.x; b < nlb; b += kBigTB)
+            if (h[b]) h[b] = atomicAdd(&cur[b], h[b]);   // this chunk's run in bin b
+        __syncthreads();
+        for (int k = k0 + threadIdx.x; k < k1; k += kBigTB) {
+            const float4 v = staged[a + k];
+            scratch[a + atomicAdd(&h[rt_lbin(L, v, bx0, by0, LB)], 1)] = v;
+        }
+        __syncthreads();
     }
 }
 
 // kept_tile (optional): the tile's count of kept owned candidates; dirty (optional): only tiles with
 // dirty[t + 1] > dirty[t] are (re)counted — the streaming map's tiles that received scan points.
+// BIG = false: one workgroup per tile that fits LDS (the others are left to BIG); BIG = true: one
+// workgroup per (listed big tile, chunk of its list), points searched in the scratch range.
+template <bool BIG>
 __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *tstart, float4 *staged,
-                                                        float4 *scratch, uint64_t *rbits,
+                                                        const float4 *scratch, uint64_t *rbits,
                                                         unsigned long long *counters, int *kept_tile,
-                                                        const int *dirty, const int *bigbins) {
-    __shared__ float4 pts[kRorCap];
+                                                        const int *dirty, BigBufs B) {
+    __shared__ float4 pts[BIG ? 1 : kRorCap];
     __shared__ int bstart[kRtMaxLocalBins + 1];
     __shared__ unsigned long long win[kRtWinWords];
     __shared__ unsigned kept_wg;
     const int tid = threadIdx.x;
-    const int t = rt_xcd_block(blockIdx.x, gridDim.x);
+    const int nbig = BIG ? B.list[0] : 1;
+    for (int it = BIG ? blockIdx.y : 0; it < nbig; it += BIG ? gridDim.y : 1) {
+    const int t = BIG ? B.list[1 + it] : rt_xcd_block(blockIdx.x, gridDim.x);
     const int tx = t % L.ntx, ty = t / L.ntx;
-    if (dirty && dirty[t + 1] == dirty[t]) return;
+    if (!BIG && dirty && dirty[t + 1] == dirty[t]) return;
     const int a = tstart[t], n = tstart[t + 1] - a;   // the tile's runs
-    if (n == 0 || a + n > L.staged_cap) {             // (an overflowed scatter: the frame is redone)
-        if (kept_tile && tid == 0) kept_tile[t] = 0;
-        return;
+    if (!BIG) {
+        if (n > kRorCap && a + n <= L.staged_cap) return;   // a big tile: k_rt_ror<true>
+        if (n == 0 || a + n > L.staged_cap) {               // (an overflowed scatter: the frame is redone)
+            if (kept_tile && tid == 0) kept_tile[t] = 0;
+            return;
+        }
+    }
+    int k0 = 0, k1 = n;
+    if (BIG) {
+        int a_;
+        big_chunk(L, tstart, t, a_, k0, k1);
     }
     if (tid == 0) kept_wg = 0;
     const int LB = L.TB + 2;                        // local bins: the tile's bins and a ring of halo bins
@@ -322,37 +426,30 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
     const int cx0 = (int)floor(((double)wx_lo - L.origin_x) / (double)L.res) - 2;
     const int cw0 = (int)floor((double)(cx0 - L.wx0) / 64.0);
     const bool use_win = L.win_rows > 0;
-    for (int i = tid; i <= nlb; i += kRorThreads) bstart[i] = 0;
     if (use_win)
         for (int i = tid; i < L.win_rows * L.win_w; i += kRorThreads) win[i] = 0ull;
+    if (BIG) {   // bin offsets from k_rt_bigscan (through the kernel boundary)
+        for (int i = tid; i <= nlb; i += kRorThreads) bstart[i] = B.starts[(size_t)t * (nlb + 1) + i];
+    } else {
+        for (int i = tid; i <= nlb; i += kRorThreads) bstart[i] = 0;
+    }
     __syncthreads();
-    auto lbin = [&](float4 q) {
-        int bx, by;
-        rt_bin(L, q.x, q.y, bx, by);
-        return (by - by0) * LB + (bx - bx0);       // in [0, nlb): a copy lies in the tile's 3 x 3 reach
-    };
-    const bool fits = n <= kRorCap;
-    // counting sort: histogram (ranks kept in registers when the tile fits), scan, place
-    float4 q[kRorPer];
-    int rk[kRorPer];
-    if (fits) {
+    // counting sort of a fitting tile: histogram (ranks kept in registers), scan, place
+    float4 q[BIG ? 1 : kRorPer];
+    int rk[BIG ? 1 : kRorPer];
+    if (!BIG) {
 #pragma unroll
         for (int j = 0; j < kRorPer; ++j) {
             const int k = tid + j * kRorThreads;
             rk[j] = -1;
             if (k < n) {
                 q[j] = staged[a + k];
-                rk[j] = atomicAdd(&bstart[lbin(q[j]) + 1], 1);
+                rk[j] = atomicAdd(&bstart[rt_lbin(L, q[j], bx0, by0, LB) + 1], 1);
             }
         }
-    } else {
-        // too many points for LDS: k_rt_bigsort (the launch before) placed them bin-sorted in the tile's
-        // range of the scratch array and left the bin offsets in bigbins
-        for (int i = tid; i <= nlb; i += kRorThreads) bstart[i] = bigbins[(size_t)t * (nlb + 1) + i];
-    }
-    __syncthreads();
-    if (fits) {   // exclusive bin offsets: bstart[b] = points in bins < b. Thread t sums a run of kSeg bins,
-        // one block scan over the 256 run totals, then each run is written back.
+        __syncthreads();
+        // exclusive bin offsets: bstart[b] = points in bins < b. Thread t sums a run of kSeg bins,
+        // one block scan over the run totals, then each run is written back.
         constexpr int kSeg = (kRtMaxLocalBins + kRorThreads - 1) / kRorThreads;
         typedef hipcub::BlockScan<int, kRorThreads> Scan;
         __shared__ typename Scan::TempStorage scan_tmp;
@@ -372,21 +469,19 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
             before += v[j];
             if (b <= nlb) bstart[b] = before;
         }
-    }
-    __syncthreads();
-    const float4 *P = scratch + a;
-    if (fits) {
+        __syncthreads();
 #pragma unroll
         for (int j = 0; j < kRorPer; ++j)
-            if (rk[j] >= 0) pts[bstart[lbin(q[j])] + rk[j]] = q[j];
+            if (rk[j] >= 0) pts[bstart[rt_lbin(L, q[j], bx0, by0, LB)] + rk[j]] = q[j];
+        __syncthreads();
     }
-    __syncthreads();
+    float4 *P = const_cast<float4 *>(scratch) + a;
     unsigned kept_n = 0;
     // w: 0 a neighbour only, 1 a candidate, 2 a candidate a streaming map already found kept (the keep
     // decision is monotone as points are added: it stays kept, its cell is already in the raster)
     const bool store = kept_tile != nullptr;
-    for (int k = tid; k < n; k += kRorThreads) {
-        const float4 p = fits ? pts[k] : P[k];
+    for (int k = k0 + tid; k < k1; k += kRorThreads) {
+        const float4 p = BIG ? P[k] : pts[k];
         const int w = __float_as_int(p.w);
         if (!w) continue;                       // neighbour only
         if (w == 2) {                           // kept in an earlier frame: counted, not re-tested
@@ -405,13 +500,13 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
             const int yy = ly + (rr == 0 ? 0 : (rr == 1 ? -1 : 1));
             if (cnt >= L.need) break;
             const int r0 = yy * LB + lx - 1;
-            cnt = fits ? rt_scan(L, p, pts, bstart[r0], bstart[r0 + 3], cnt)
-                       : rt_scan(L, p, P, bstart[r0], bstart[r0 + 3], cnt);
+            cnt = BIG ? rt_scan(L, p, P, bstart[r0], bstart[r0 + 3], cnt)
+                      : rt_scan(L, p, pts, bstart[r0], bstart[r0 + 3], cnt);
         }
         if (cnt < L.need) continue;
         if (store) {   // remembered in the tile store (written back below)
-            if (fits) pts[k].w = __int_as_float(2);
-            else const_cast<float4 *>(P)[k].w = __int_as_float(2);
+            if (BIG) P[k].w = __int_as_float(2);   // (neighbour scans of other threads read only x, y, z)
+            else pts[k].w = __int_as_float(2);
         }
         // kept: counted iff its clamped cell is owned, rastered iff inside the grid (seed_gen:606-619)
         const int gx = (int)(((double)p.x - L.origin_x) / (double)L.res);
@@ -428,8 +523,10 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
         else
             atomicOr(reinterpret_cast<unsigned long long *>(&rbits[(size_t)r * L.WWr + (bxw >> 6)]), bit);
     }
-    if (store)   // the tile's list goes back bin-sorted with its kept marks (each k by the thread that marked it)
-        for (int k = tid; k < n; k += kRorThreads) staged[a + k] = fits ? pts[k] : P[k];
+    // the store goes back bin-sorted with its kept marks: a fitting tile rewrites its list, a big tile's
+    // chunk its range of the sorted scratch list (each k by the thread that marked it)
+    if (store)
+        for (int k = k0 + tid; k < k1; k += kRorThreads) staged[a + k] = BIG ? P[k] : pts[k];
     __syncthreads();
     if (use_win)
         for (int i = tid; i < L.win_rows * L.win_w; i += kRorThreads) {
@@ -447,7 +544,12 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
     }
     if (kept_tile) {
         __syncthreads();
-        if (tid == 0) kept_tile[t] = (int)kept_wg;
+        if (tid == 0) {
+            if (BIG) atomicAdd(&kept_tile[t], (int)kept_wg);
+            else kept_tile[t] = (int)kept_wg;
+        }
+    }
+    __syncthreads();
     }
 }
 
@@ -458,11 +560,13 @@ __global__ __launch_bounds__(256) void k_rt_merge(const float4 *old_st, const in
     const int t = blockIdx.x;
     if (t > ntiles) return;
     const int o0 = old_ts[t], s0 = scan_ts[t], d0 = o0 + s0;
-    if (threadIdx.x == 0) new_ts[t] = d0;
+    if (threadIdx.x == 0 && blockIdx.y == 0) new_ts[t] = d0;
     if (t == ntiles) return;
     const int no = old_ts[t + 1] - o0, ns = scan_ts[t + 1] - s0;
-    for (int i = threadIdx.x; i < no; i += 256) new_st[d0 + i] = old_st[o0 + i];
-    for (int i = threadIdx.x; i < ns; i += 256) new_st[d0 + no + i] = scan_st[s0 + i];
+    // blockIdx.y-th of gridDim.y slices of the tile's runs (a big tile's copy spreads over CUs)
+    const int stride = 256 * gridDim.y;
+    for (int i = blockIdx.y * 256 + threadIdx.x; i < no; i += stride) new_st[d0 + i] = old_st[o0 + i];
+    for (int i = blockIdx.y * 256 + threadIdx.x; i < ns; i += stride) new_st[d0 + no + i] = scan_st[s0 + i];
 }
 
 // n_clipped of the streaming map = the sum of the tiles' kept counts (into counters[0])
@@ -558,19 +662,26 @@ void launch_rt_scatter(const RorLaunch &L, int *H, const int *tstart, int G, flo
     else rt_part<true, false>(L, H, tstart, G, staged, nullptr, s);
 }
 
-size_t rt_bigbins_ints(const RorLaunch &L) { return (size_t)L.ntiles * ((L.TB + 2) * (L.TB + 2) + 1); }
+size_t rt_bigbins_ints(const RorLaunch &L) { return 2 * (size_t)L.ntiles * ((L.TB + 2) * (L.TB + 2) + 1) + 1 + L.ntiles; }
 
 void launch_rt_ror(const RorLaunch &L, const int *tstart, float4 *staged, float4 *scratch, int *bigbins,
                    uint64_t *rbits, unsigned long long *counters, int *kept_tile, const int *dirty, hipStream_t s) {
     if (!L.ntiles) return;
-    k_rt_bigsort<<<L.ntiles, kRorThreads, 0, s>>>(L, tstart, staged, scratch, bigbins, dirty);
-    k_rt_ror<<<L.ntiles, kRorThreads, 0, s>>>(L, tstart, staged, scratch, rbits, counters, kept_tile, dirty, bigbins);
+    const BigBufs B = big_bufs(L, bigbins);
+    AOS_HIP(hipMemsetAsync(B.list, 0, sizeof(int), s));
+    k_rt_biglist<<<L.ntiles, 256, 0, s>>>(L, tstart, B, kept_tile, dirty);
+    const dim3 gb(kBigC, kBigY);
+    k_rt_bighist<<<gb, kBigTB, 0, s>>>(L, tstart, staged, B);
+    k_rt_bigscan<<<kBigY, 1024, 0, s>>>(L, tstart, B);
+    k_rt_bigscatter<<<gb, kBigTB, 0, s>>>(L, tstart, staged, scratch, B);
+    k_rt_ror<false><<<L.ntiles, kRorThreads, 0, s>>>(L, tstart, staged, scratch, rbits, counters, kept_tile, dirty, B);
+    k_rt_ror<true><<<gb, kRorThreads, 0, s>>>(L, tstart, staged, scratch, rbits, counters, kept_tile, dirty, B);
     AOS_HIP(hipGetLastError());
 }
 
 void launch_rt_merge(const float4 *old_st, const int *old_ts, const float4 *scan_st, const int *scan_ts, float4 *new_st,
                      int *new_ts, int ntiles, hipStream_t s) {
-    k_rt_merge<<<ntiles + 1, 256, 0, s>>>(old_st, old_ts, scan_st, scan_ts, new_st, new_ts, ntiles);
+    k_rt_merge<<<dim3(ntiles + 1, 8), 256, 0, s>>>(old_st, old_ts, scan_st, scan_ts, new_st, new_ts, ntiles);
     AOS_HIP(hipGetLastError());
 }
 

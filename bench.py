@@ -53,6 +53,9 @@ def parse(argv=None):
                          "seed-gen overlaps frame k-1's GVD, as the reference's two nodes do)")
     ap.add_argument("--tiled", action="store_true",
                     help="one map split into tiles over the ranks (SURVEY §8e, BASELINE configs[3]); strong scaling")
+    ap.add_argument("--fixed-root", action="store_true",
+                    help="--tiled: rank 0 finishes every frame (default: frame k's root is rank k mod N, so the "
+                         "whole-map stages and the GVD jobs rotate over the ranks)")
     a = ap.parse_args(argv)
     if a.config is None:
         a.config = "C3" if a.tiled else "C2"
@@ -213,7 +216,8 @@ def main():
     # collects its own frame, so every frame of the timed region completes inside it.
     n_calls = a.warmup + a.steps
     pend = {"k": 0, "t0": {}, "mt0": None, "ms": 0.0, "fifo": [], "lat": {}}
-    pipeline = not (a.sequential or a.stream or a.tiled)
+    pipeline = not (a.sequential or a.stream)
+    rotate = a.tiled and world > 1 and not a.fixed_root
     depth = max(1, a.depth) if pipeline else 1
     if pipeline:
         ctx.gvd_pipeline_depth(depth)
@@ -244,10 +248,20 @@ def main():
         if a.stream:
             g = ctx.map_append(scans[k], want_host=False)
         elif a.tiled:
-            g = ctx.tiled_seedgen(comm, tx, ty, d_cloud.data_ptr(), root=0, n_points=n, on_device=True,
+            # every rank receives the gathered skeleton and inflated tiles, so any rank can finish a frame:
+            # frame k's root (a6, a8-a16 and its GVD job) is rank k mod N, which spreads the whole-map
+            # stages and the GVD replays over the ranks' GPUs and host cores
+            root_k = (k % world) if rotate else 0
+            g = ctx.tiled_seedgen(comm, tx, ty, d_cloud.data_ptr(), root=root_k, n_points=n, on_device=True,
                                   want_host=False)
             if not g["root"]:
-                return g, {"ms": {}, "nodes": (), "edges": ()}
+                gg = None
+                if pipeline and k == n_calls - 1:   # drain this rank's GVD jobs (its earlier root frames)
+                    while pend["fifo"]:
+                        gg = finish(pend["fifo"].pop(0))
+                elif not pipeline and k == n_calls - 1 and pend.get("mk_pending"):
+                    collect()
+                return g, gg
         else:
             if mode["host"]:   # PointCloud2 bytes from host memory in, both OccupancyGrids to host out
                 # (the grids are returned as views of the library's pinned buffers: the ABI's ownership rule)
@@ -273,9 +287,10 @@ def main():
                       f"{ms.get('delaunay', 0):.1f} total {ms.get('total', 0):.1f} cells {ms.get('cells', 0):.1f}",
                       file=sys.stderr, flush=True)
             return g, gg
-        if k > 0:
+        if k > 0 and pend.get("mk_pending", False):
             collect()
         gg = ctx.gvd_from_seedgen()
+        pend["mk_pending"] = True
         if a.stream:
             latency.append(time.perf_counter() - t0)
         pend["mt0"] = t0
@@ -288,6 +303,11 @@ def main():
     _progress(f"{a.warmup} warmup + {a.steps} timed frames")
     dt, res, per = timed_region(step, a.steps, a.warmup, world, torch.cuda.synchronize, dist, red_dev)
     g, gg = res[-1]
+    if a.tiled:   # the frame statistics of this rank's last root frame (its seeds, rows and graph)
+        roots = [(gs, ggs) for gs, ggs in res if gs.get("root") and ggs is not None] or \
+                [(gs, ggs) for gs, ggs in res if ggs is not None]
+        if roots:
+            g, gg = roots[-1]
     frame_lat = sorted(1e3 * pend["lat"][k] for k in range(a.warmup, a.warmup + a.steps) if k in pend["lat"])
     dev_rate = None
     if host_io and not a.no_device_rate:
@@ -328,7 +348,7 @@ def main():
     # launches (count, tile scan, scatter, per-tile neighbour count), timed live with HIP events on the
     # handle's stream (aos_seedgen_out.ms_ror_*), averaged over the timed frames. `kernels` gives each
     # launch's time and the count pass's own figure (it is the one launch that reads the cloud: 12 N).
-    n_all = float(cfg.n_points if a.tiled else n)
+    n_all = float(n)   # the points this rank's ROR kernels read (tiled: its tile's shard)
     T = g["thin_iters"]
     t_cnt, t_scat, t_ror = avg["seedgen_ror_bin"], avg["seedgen_ror_scatter"], avg["seedgen_ror_count"]
     t_stage = avg.get("seedgen_ror_kernels", t_cnt + t_scat + t_ror)
@@ -363,7 +383,8 @@ def main():
                         f"@ {cfg.res} m, full seed-gen + GVD of the whole map per scan")
         elif a.tiled:
             workload = (f"{a.config}: {cfg.n_points} pts, {g['width']}x{g['height']} cells @ {cfg.res} m, one map in "
-                        f"{tx}x{ty} tiles (rank 0 holds {n} pts), halo all-gathers, GVD on rank 0")
+                        f"{tx}x{ty} tiles (rank 0 holds {n} pts), halo all-gathers, "
+                        + (f"frame k finished (a6, a8-a16, GVD) by rank k mod {world}" if rotate else "GVD on rank 0"))
         else:
             workload = (f"{a.config}: {n} pts, {g['width']}x{g['height']} cells @ {cfg.res} m, "
                         f"full seed-gen + GVD per frame, one independent tile per GPU")
@@ -403,6 +424,7 @@ def main():
             out["stream"] = {"scan_latency_ms_p50": round(lat[len(lat) // 2], 2), "scan_latency_ms_max": round(lat[-1], 2),
                              "markers_latency_ms_p50": round(mlat[len(mlat) // 2], 2),
                              "markers_latency_ms_max": round(mlat[-1], 2),
+                             "scan_latency_ms": [round(x * 1e3, 1) for x in latency[a.warmup:]],
                              "budget_ms": 1e3 / orchard.SCAN_HZ,
                              "keeps_up": max(lat[-1], dt / len(res) * 1e3) <= 1e3 / orchard.SCAN_HZ,
                              "note": "scan latency = scan H2D + pack + whole-map seed-gen + GVD graph (host clock); "

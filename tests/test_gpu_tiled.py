@@ -89,6 +89,60 @@ def test_tiled_c1_equals_single_gpu(tiles, root):
     _assert_same(_single(cloud, poly, cfg.res), _tiled_threads(cloud, poly, cfg.res, *tiles, root))
 
 
+def test_tiled_rotating_roots_with_background_gvd():
+    """The tiled bench's schedule (bench.py --tiled): frame k's root is rank k mod N, and the root starts
+    the frame's GVD in the background (aos_gvd_from_seedgen_async) and goes on with the next frames'
+    tile stages while it runs. Two C1 scenes alternate over 8 frames on 2 x 2 tiles, so every rank
+    finishes two frames of different scenes with both jobs in flight; every graph must equal the
+    single-GPU graph of its scene."""
+    cfg = orchard.CONFIGS["C1"]
+    poly = orchard.polygon(cfg)
+    clouds = [orchard.generate(cfg), orchard.generate(cfg, seed=cfg.seed + 1)]
+    singles = [_single(c, poly, cfg.res) for c in clouds]
+    tiles_x, tiles_y, frames = 2, 2, 8
+    world = tiles_x * tiles_y
+    params = aos_gpu.default_params(grid_resolution=cfg.res)
+    plans = [T.tile_plan(params, poly, tiles_x, tiles_y, r) for r in range(world)]
+    group = T.ThreadGroup(world, timeout=120)
+    ctxs = [aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res)) for _ in range(world)]
+    comms = [group.comm(r, plans[r]["exchange_bytes"], "cuda:0") for r in range(world)]
+    graphs, errors = {}, []
+
+    def work(r):
+        try:
+            ctxs[r].set_polygon(poly)
+            ctxs[r].gvd_pipeline_depth(2)
+            parts = [T.shard(c, plans[r]["points_box"]) for c in clouds]
+            mine = []
+            for k in range(frames):
+                g = ctxs[r].tiled_seedgen(comms[r], tiles_x, tiles_y, parts[k % 2], root=k % world, want_host=False)
+                assert g["root"] == (k % world == r)
+                if g["root"]:
+                    ctxs[r].gvd_async()
+                    mine.append(k)
+            for k in mine:   # jobs complete in start order
+                graphs[k] = ctxs[r].gvd_wait()
+        except BaseException as e:   # noqa: BLE001
+            errors.append(e)
+            group.abort()
+
+    ts = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(600)
+    for x in ctxs:
+        x.close()
+    if errors:
+        raise errors[0]
+    assert sorted(graphs) == list(range(frames))
+    for k, gg in graphs.items():
+        gg1 = singles[k % 2][2]
+        assert gg["published"] == gg1["published"]
+        for key in GVD_KEYS:
+            assert np.array_equal(gg[key], gg1[key]), (k, key)
+
+
 def _sha(a, dt):
     a = np.ascontiguousarray(np.asarray(a, dtype=dt))
     return hashlib.sha256(a.dtype.str.encode() + str(a.shape).encode() + a.tobytes()).hexdigest()
