@@ -193,6 +193,7 @@ def lib():
         L.aos_gvd_from_seedgen_async.argtypes = [c_vp]
         L.aos_gvd_wait.argtypes = [c_vp, P(GvdOut)]
         L.aos_gvd_pipeline_depth.argtypes = [c_vp, c_i]
+        L.aos_gvd_set_markers.argtypes = [c_vp, c_i]
         L.aos_rccl_unique_id.argtypes = [c_vp]
         L.aos_rccl_create.argtypes = [c_vp, c_i, c_i, c_i, c_u64, P(c_vp)]
         L.aos_rccl_comm.argtypes = [c_vp]
@@ -414,6 +415,10 @@ class Ctx:
     def gvd_async(self) -> None:
         """Start the GVD of the last seed-gen frame in the background (aos_gvd_from_seedgen_async)."""
         _check(lib().aos_gvd_from_seedgen_async(self.h))
+
+    def gvd_set_markers(self, on: bool) -> None:
+        """publishMarkers' cells for the following GVD calls (aos_gvd_set_markers); off: on demand."""
+        _check(lib().aos_gvd_set_markers(self.h, int(bool(on))))
 
     def gvd_pipeline_depth(self, depth: int) -> None:
         """Up to `depth` background GVD jobs in flight (aos_gvd_pipeline_depth)."""

@@ -99,6 +99,7 @@ struct aos_ctx {
         hipEvent_t ready = nullptr;               // the snapshot copy on the seed-gen stream
         std::vector<double> seeds, rows;          // snapshot of h_voronoi / h_rows_info
         aos_grid_info info{};
+        int markers = 1;                          // P.gvd_markers when the job started
     };
     struct alignas(128) GvdLane {
         aos::GvdState gs;

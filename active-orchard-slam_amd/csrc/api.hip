@@ -225,6 +225,12 @@ const aos_comm *aos_rccl_comm(aos_rccl *r) { return r ? rccl_comm(r) : nullptr; 
 
 void aos_rccl_destroy(aos_rccl *r) { rccl_destroy(r); }
 
+int aos_gvd_set_markers(aos_ctx *c, int32_t on) {
+    if (!c) { set_error("aos_gvd_set_markers: null handle"); return AOS_E_INVALID; }
+    c->P.gvd_markers = on ? 1 : 0;
+    return AOS_OK;
+}
+
 int aos_gvd_pipeline_depth(aos_ctx *c, int32_t depth) {
     if (!c) { set_error("aos_gvd_pipeline_depth: null handle"); return AOS_E_INVALID; }
     if (depth < 1 || depth > 8) { set_error("aos_gvd_pipeline_depth: depth must be in [1, 8]"); return AOS_E_INVALID; }
@@ -279,6 +285,9 @@ int aos_gvd_markers_get(aos_ctx *c, aos_gvd_markers *out) {
     AOS_GUARD_BEGIN
     c->gvd_view_settle();
     markers_wait(c->gs(), true);   // the cells run on after the graph is returned
+    // a frame whose GVD ran with markers off (aos_gvd_set_markers): computed now, as publishMarkers
+    // does for the frames the node publishes (gvd:306-314)
+    if (!c->gs().have_markers && c->gs().graph_ok) markers_on_demand(c->gs());
     AOS_GUARD_END
     GvdState &G = c->gs();
     if (!G.have_markers || !G.cells) {

@@ -128,6 +128,8 @@ struct GvdState {
     float ms_merge = 0, ms_delaunay = 0, ms_graph = 0, ms_total = 0;
     // markers (aos_gvd_markers)
     bool have_markers = false;
+    bool graph_ok = false;     // the last GVD call produced a graph (markers can be computed on demand)
+    int rect_mode = 0;         // its Subdiv2D rectangle mode
     std::vector<double> merged_xy, row_label_xy;
     std::vector<int32_t> row_label_valid;
     std::unique_ptr<CellsWork> cells;   // the worker thread's own heap object (no false sharing)
@@ -147,5 +149,7 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
 void free_gvd_scratch(GvdState &G);
 // Joins the markers' cells job of the last GVD call; rethrow: raise its error (else discard it).
 void markers_wait(GvdState &G, bool rethrow);
+// aos_gvd_markers_get on a frame whose GVD ran without markers: compute them now (and wait)
+void markers_on_demand(GvdState &G);
 
 }  // namespace aos

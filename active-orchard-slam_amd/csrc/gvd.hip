@@ -662,6 +662,12 @@ static void markers_start(GvdState &G, int rect_mode) {
     W.cv.notify_all();
 }
 
+void markers_on_demand(GvdState &G) {
+    markers_start(G, G.rect_mode);
+    markers_wait(G, true);
+    G.have_markers = true;
+}
+
 void markers_wait(GvdState &G, bool rethrow) {
     if (!G.cells) return;
     CellsWork &W = *G.cells;
@@ -683,6 +689,8 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     G.ms_merge = G.ms_delaunay = G.ms_graph = G.ms_total = 0;
     markers_wait(G, false);
     G.have_markers = false;
+    G.graph_ok = false;
+    G.rect_mode = P.subdiv_rect_mode;
     G.merged_xy.clear(); G.row_label_xy.clear(); G.row_label_valid.clear();
     if (G.cells) { G.cells->cell_off.assign(1, 0); G.cells->ms = 0; }
     int *h_sc = static_cast<int *>(G.h_misc.ensure(4096));
@@ -779,6 +787,7 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     AOS_HIP(hipEventRecord(ev[8], s));
     if (ne == 0) {   // no boundary points: an empty graph is still published
         G.have_markers = P.gvd_markers != 0;
+        G.graph_ok = true;
         return true;
     }
 
@@ -927,6 +936,7 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     AOS_HIP(hipEventRecord(ev[9], s));
     AOS_HIP(hipStreamSynchronize(s));
     G.have_markers = P.gvd_markers != 0;
+    G.graph_ok = true;
     float a = 0, b = 0;
     (void)hipEventElapsedTime(&a, ev[6], ev[7]);
     (void)hipEventElapsedTime(&b, ev[8], ev[9]);
@@ -1032,6 +1042,7 @@ void aos_ctx::gvd_async_start() {
     }
     A.seeds = h_voronoi;
     A.rows = h_rows_info;
+    A.markers = P.gvd_markers;
     A.info = aos_grid_info{geom.origin_x, geom.origin_y, geom.res, (uint32_t)geom.W, (uint32_t)geom.H};
     const size_t C = (size_t)geom.W * geom.H;
     int8_t *d_sk = static_cast<int8_t *>(ln.gs.skel.ensure(std::max<size_t>(C, 1)));
@@ -1058,7 +1069,9 @@ void aos_ctx::gvd_async_start() {
                         { std::lock_guard<std::mutex> g(A->mu); A->prefix = true; }
                         A->cv.notify_all();
                     };
-                    pub = run_gvd_stage(ln.gs, P, gi, W.stream, W.ev.data());
+                    aos_params Pj = P;
+                    Pj.gvd_markers = W.markers;   // as set when the job started (aos_gvd_set_markers)
+                    pub = run_gvd_stage(ln.gs, Pj, gi, W.stream, W.ev.data());
                 } catch (...) { e = std::current_exception(); }
                 l.lock();
                 W.err = e;

@@ -34,6 +34,9 @@ class AosGvdGpuNode : public rclcpp::Node {
         aos_default_params(&p);
         p.max_graph_publish_rate = rate_;
         if (aos_create(&p, declare_parameter<int>("gpu_device", 0), &ctx_) != AOS_OK) throw std::runtime_error(aos_last_error());
+        // markers only for the published frames: publish_markers asks for them (computed on demand), as
+        // publishMarkers runs inside the publish throttle (gvd:306-314)
+        aos_gvd_set_markers(ctx_, 0);
 
         rclcpp::QoS reliable(10);   // gvd:44-45
         reliable.reliable();

@@ -53,6 +53,9 @@ def parse(argv=None):
                          "seed-gen overlaps frame k-1's GVD, as the reference's two nodes do)")
     ap.add_argument("--tiled", action="store_true",
                     help="one map split into tiles over the ranks (SURVEY §8e, BASELINE configs[3]); strong scaling")
+    ap.add_argument("--markers-every-frame", action="store_true",
+                    help="publishMarkers' cells (a second Subdiv2D) for every frame; default: for the frames the "
+                         "node publishes, at most max_graph_publish_rate (10 Hz) as the reference does (gvd:306-314)")
     ap.add_argument("--fixed-root", action="store_true",
                     help="--tiled: rank 0 finishes every frame (default: frame k's root is rank k mod N, so the "
                          "whole-map stages and the GVD jobs rotate over the ranks)")
@@ -206,16 +209,30 @@ def main():
         ctx.map_reset(reserve_points=n + len(scans) * orchard.SCAN_POINTS)
         ctx.map_append(d_cloud.data_ptr(), n_points=n, on_device=True, want_host=False)
         latency, mk_latency = [], []
-    # The markers' cells of a frame finish in the background after its graph (publishGraph before
-    # publishMarkers, gvd:310-313): every step collects the previous frame's markers after its own
-    # seed-gen, and the last step collects its own, so each timed frame includes its markers.
+    # The reference builds the graph on every callback and publishes it, with the markers (publishMarkers:
+    # a second Subdiv2D for the Voronoi cells), only when 1 / max_graph_publish_rate (0.1 s) has passed
+    # since the last publish (gvd:306-314). The bench does the same work: every frame's graph, and the
+    # markers of the frames that would be published (decided when the frame's GVD starts); with
+    # --markers-every-frame, the markers of every frame. The markers' cells of a frame finish in the
+    # background after its graph (publishGraph before publishMarkers, gvd:310-313) and are collected
+    # with it, so each timed frame includes its markers.
     # --sequential: step k = seed-gen k, the markers of frame k - 1, then the GVD of frame k.
     # Pipelined (default): the reference's seed-gen and GVD are two nodes, so frame k's seed-gen runs while
     # frame k - 1's graph is built (aos_gvd_from_seedgen_async on the handle's GVD worker). Step k =
     # seed-gen k, collect graph + markers of frame k - 1, start the GVD of frame k; the last step also
     # collects its own frame, so every frame of the timed region completes inside it.
     n_calls = a.warmup + a.steps
-    pend = {"k": 0, "t0": {}, "mt0": None, "ms": 0.0, "fifo": [], "lat": {}}
+    pend = {"k": 0, "t0": {}, "mt0": None, "ms": 0.0, "fifo": [], "lat": {}, "mk": {}, "last_pub": -1e9}
+    pub_period = 1.0 / params.max_graph_publish_rate
+
+    def markers_for(k):   # the publish throttle of processGraph (gvd:306-314)
+        now = time.perf_counter()
+        mk = a.markers_every_frame or now - pend["last_pub"] >= pub_period
+        if mk:
+            pend["last_pub"] = now
+        pend["mk"][k] = mk
+        ctx.gvd_set_markers(mk)
+        return mk
     pipeline = not (a.sequential or a.stream)
     rotate = a.tiled and world > 1 and not a.fixed_root
     depth = max(1, a.depth) if pipeline else 1
@@ -235,7 +252,10 @@ def main():
         if a.stream:
             latency.append(time.perf_counter() - pend["t0"][j])
         pend["mt0"] = pend["t0"][j]
-        collect()
+        if pend["mk"].get(j):
+            collect()
+        else:
+            pend["ms"] = 0.0
         pend["lat"][j] = time.perf_counter() - pend["t0"][j]   # PointCloud2 in -> graph + markers out
         gg["ms"]["cells"] = pend["ms"]
         return gg
@@ -274,6 +294,7 @@ def main():
             t1 = time.perf_counter()
             gg = finish(pend["fifo"].pop(0)) if len(pend["fifo"]) >= depth else None
             t2 = time.perf_counter()
+            markers_for(k)
             ctx.gvd_async()
             pend["fifo"].append(k)
             t3 = time.perf_counter()
@@ -289,12 +310,13 @@ def main():
             return g, gg
         if k > 0 and pend.get("mk_pending", False):
             collect()
+        mk = markers_for(k)
         gg = ctx.gvd_from_seedgen()
-        pend["mk_pending"] = True
+        pend["mk_pending"] = mk
         if a.stream:
             latency.append(time.perf_counter() - t0)
         pend["mt0"] = t0
-        if k == n_calls - 1:
+        if k == n_calls - 1 and mk:
             collect()
         pend["lat"][k] = time.perf_counter() - t0
         gg["ms"]["cells"] = pend["ms"]   # the previous frame's (the last step: its own)
@@ -302,6 +324,7 @@ def main():
 
     _progress(f"{a.warmup} warmup + {a.steps} timed frames")
     dt, res, per = timed_region(step, a.steps, a.warmup, world, torch.cuda.synchronize, dist, red_dev)
+    mk_frames = sum(1 for k in range(a.warmup, a.warmup + a.steps) if pend["mk"].get(k))
     g, gg = res[-1]
     if a.tiled:   # the frame statistics of this rank's last root frame (its seeds, rows and graph)
         roots = [(gs, ggs) for gs, ggs in res if gs.get("root") and ggs is not None] or \
@@ -410,6 +433,10 @@ def main():
             "pipeline": (f"depth {depth}: frame k's seed-gen overlaps the GVDs of frames k-1 .. k-{depth} (the "
                          f"reference's two nodes; frames are independent, each GVD's Subdiv2D replay on its own core)")
                         if pipeline else "sequential",
+            "markers": {"policy": "every frame" if a.markers_every_frame else
+                        f"the frames the node publishes: at most max_graph_publish_rate = {params.max_graph_publish_rate:g} Hz "
+                        f"of wall time (gvd:306-314); every frame's graph is built and returned",
+                        "timed_frames_with_markers": mk_frames},
             "stages_ms": {k: round(v, 3) for k, v in avg.items()},
             "frame": {"T": T, "rows": len(g["row_length"]), "seeds": len(g["voronoi_seeds"]),
                       "nodes": len(gg["nodes"]), "edges": len(gg["edges"]), "n_binned": g["n_binned"],

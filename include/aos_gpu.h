@@ -158,6 +158,12 @@ int aos_gvd_from_seedgen(aos_ctx *ctx, aos_gvd_out *out);
 int aos_gvd_from_seedgen_async(aos_ctx *ctx);
 int aos_gvd_wait(aos_ctx *ctx, aos_gvd_out *out);
 int aos_gvd_pipeline_depth(aos_ctx *ctx, int32_t depth);   /* 1..8 GVD jobs in flight */
+/* publishMarkers' cells for the GVD calls that follow (aos_params.gvd_markers): 1 = computed in the
+ * background after each graph, 0 = not computed. The reference throttles publishGraph + publishMarkers
+ * (gvd:306-314, max_graph_publish_rate): a wrapper that publishes 1 frame in n turns them on for the
+ * published frames only. A background job keeps the value it had when it started. With 0,
+ * aos_gvd_markers_get computes the cells of the current frame on demand (synchronously). */
+int aos_gvd_set_markers(aos_ctx *ctx, int32_t on);
 
 /* ---------------------------------------------------------------------------------------------
  * Streaming ingest (BASELINE.json configs[4]). The handle keeps the global

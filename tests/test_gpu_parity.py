@@ -320,10 +320,16 @@ def test_gvd_markers_external_input_and_disabled():
     c.gvd(o["voronoi_seeds"], o["rows_info"], o)
     _assert_markers(c.gvd_markers(), og)
     c.close()
+    # markers off (a frame the node does not publish, gvd:306-314): nothing is computed with the graph;
+    # asking for them computes them on demand, equal to the eager job
     c = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res, gvd_markers=0))
-    c.gvd(o["voronoi_seeds"], o["rows_info"], o)
     with pytest.raises(RuntimeError, match="no markers"):
-        c.gvd_markers()
+        c.gvd_markers()                     # no GVD frame yet
+    c.gvd(o["voronoi_seeds"], o["rows_info"], o)
+    _assert_markers(c.gvd_markers(), og)
+    c.gvd_set_markers(True)
+    c.gvd(o["voronoi_seeds"], o["rows_info"], o)
+    _assert_markers(c.gvd_markers(), og)
     c.close()
 
 

@@ -81,6 +81,33 @@ def test_pipeline_state_rules():
     c.close()                                  # a job in flight is joined
 
 
+def test_pipeline_markers_per_frame():
+    """The bench's publish throttle: aos_gvd_set_markers switches the cells on for some jobs only (a job
+    keeps the setting it started with); the graphs are unaffected, the frames with markers carry them,
+    and asking a frame without them computes them on demand — all equal to the sequential calls."""
+    cfg, poly, clouds = frames()
+    ref = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res))
+    ref.set_polygon(poly)
+    seq = []
+    for cl in clouds:
+        ref.seedgen(cl, want_host=False)
+        seq.append((ref.gvd_from_seedgen(), ref.gvd_markers()))
+    ref.close()
+    c = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res))
+    c.set_polygon(poly)
+    c.gvd_pipeline_depth(len(clouds))
+    on = [k % 2 == 0 for k in range(len(clouds))]
+    for k, cl in enumerate(clouds):
+        c.seedgen(cl, want_host=False)
+        c.gvd_set_markers(on[k])
+        c.gvd_async()
+    for k in range(len(clouds)):
+        assert_same_graph(c.gvd_wait(), seq[k][0], f"frame {k}")
+        m = c.gvd_markers()
+        assert_same_markers(m, seq[k][1], f"frame {k}")
+    c.close()
+
+
 def test_pipeline_depth_frames_in_flight():
     """aos_gvd_pipeline_depth(3): three frames' GVDs run at once, collected in start order; each graph,
     its markers and a plan on it equal the sequential calls. One start past the depth supersedes the
