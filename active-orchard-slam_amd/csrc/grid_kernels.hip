@@ -134,14 +134,15 @@ void launch_open(const uint64_t *in, uint64_t *out, const FrameGeom &g, hipStrea
 // in, so the interior stays exact. Bit-sliced logic evaluates the Zhang-Suen predicate for 64
 // cells per 64-bit word:
 //   A == 1       : exactly one 0->1 transition in p2,p3,...,p9,p2
-//   2 <= B <= 6  : at least two set and at least two clear among p2..p9
+//   2 <= B <= 6  : B = p2 + ... + p9 as four bit planes from carry-save adders (3 full adders and a
+//                  half adder per word, then two carries): B >= 2 and not (B == 7 or B == 8)
 //   m1 == m2 == 0: iter 0: p2p4p6 = p4p6p8 = 0; iter 1: p2p4p8 = p2p6p8 = 0
 // Rows 0 / H-1 and columns 0 / W-1 of the image are never examined (ximgproc loops 1..n-2).
 #ifndef AOS_THIN_TB
-#define AOS_THIN_TB 256
+#define AOS_THIN_TB 512
 #endif
 #ifndef AOS_THIN_TH
-#define AOS_THIN_TH 64
+#define AOS_THIN_TH 128
 #endif
 constexpr int TH = AOS_THIN_TH, TWW = 8, KIT = kThinItersPerLaunch, HR = 2 * KIT, NR = TH + 2 * HR, NC = TWW + 2;
 constexpr int kThinTB = AOS_THIN_TB;
@@ -158,20 +159,26 @@ __device__ __forceinline__ uint64_t zs_step(uint64_t n0, uint64_t n1, uint64_t n
     const uint64_t p8 = (c1 << 1) | (c0 >> 63);   // (y,   x-1)
     const uint64_t p9 = (n1 << 1) | (n0 >> 63);   // (y-1, x-1)
     const uint64_t seq[9] = {p2, p3, p4, p5, p6, p7, p8, p9, p2};
-    uint64_t one = 0, two = 0;          // transitions
-    uint64_t o1 = 0, o2 = 0;            // set neighbours >= 1, >= 2
-    uint64_t z1 = 0, z2 = 0;            // clear neighbours >= 1, >= 2
+    uint64_t one = 0, two = 0;          // 0 -> 1 transitions: >= 1, >= 2
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         uint64_t t = ~seq[k] & seq[k + 1];
         two |= one & t; one |= t;
-        uint64_t p = seq[k];
-        o2 |= o1 & p; o1 |= p;
-        uint64_t q = ~p;
-        z2 |= z1 & q; z1 |= q;
     }
+    auto fa = [](uint64_t a, uint64_t b, uint64_t c, uint64_t &s, uint64_t &cy) {
+        const uint64_t x = a ^ b;
+        s = x ^ c;
+        cy = (a & b) | (c & x);
+    };
+    uint64_t sa, ca, sb, cb, b0, c4, t2, c5;
+    fa(p2, p3, p4, sa, ca);
+    fa(p5, p6, p7, sb, cb);
+    fa(sa, sb, p8 ^ p9, b0, c4);        // bit 0 of B; carry of weight 2
+    fa(ca, cb, p8 & p9, t2, c5);        // weight 2; carry of weight 4
+    const uint64_t b1 = c4 ^ t2, c6 = c4 & t2;
+    const uint64_t b2 = c5 ^ c6, b3 = c5 & c6;
     uint64_t A1 = one & ~two;
-    uint64_t B26 = o2 & z2;
+    uint64_t B26 = (b1 | b2 | b3) & ~(b3 | (b2 & b1 & b0));
     uint64_t m = sub == 0 ? (~(p2 & p4 & p6) & ~(p4 & p6 & p8)) : (~(p2 & p4 & p8) & ~(p2 & p6 & p8));
     return c1 & A1 & B26 & m;  // cells to delete
 }
@@ -222,7 +229,11 @@ __global__ __launch_bounds__(kThinTB) void k_thin_block(const uint64_t *__restri
     for (int s = 0; s < 2 * KIT; ++s) {
         const int sub = s & 1;
         int any_del = 0;
-        for (int idx = threadIdx.x; idx < NR * NC; idx += blockDim.x) {
+        // sub-iteration s is exact on rows [s + 1, NR - 1 - s) of the window (one row of the halo goes
+        // stale per sub-iteration); rows outside are never read again, so they are not computed. Row 0
+        // and NR - 1 (s = 0) are kept as loaded.
+        const int r_lo = s == 0 ? 0 : s + 1, r_hi = s == 0 ? NR : NR - 1 - s;
+        for (int idx = threadIdx.x + r_lo * NC; idx < r_hi * NC; idx += blockDim.x) {
             int r = idx / NC, k = idx - r * NC;
             const int gy = ty0 - HR + r, gc = tc0 - 1 + k;
             // cells this launch reports: its tile interior, within the caller's own rectangle
