@@ -271,7 +271,7 @@ constexpr int kRtMaxLocalBins = 34 * 34, kRtWinWords = 320;
 //   k_rt_ror_big     per chunk: the neighbour counts of the chunk's points, searched in the tile's
 //                    bin-sorted scratch range (through the kernel boundary; see k_rt_ror for the rules)
 // The order inside a bin depends on the atomics' order; the keep decision and the raster do not.
-constexpr int kBigC = 16, kBigY = 128, kBigTB = 512;
+constexpr int kBigC = 16, kBigY = 32, kBigTB = 512;
 struct BigBufs { int *starts, *cur, *list; };   // rt_bigbins_ints(L) ints: 2 x ntiles x (nlb + 1), 1 + ntiles
 static BigBufs big_bufs(const RorLaunch &L, int *B) {
     const size_t row = (size_t)(L.TB + 2) * (L.TB + 2) + 1, nt = (size_t)L.ntiles;
@@ -284,23 +284,19 @@ __device__ __forceinline__ int rt_lbin(const RorLaunch &L, float4 q, int bx0, in
     return (by - by0) * LB + (bx - bx0);   // in [0, LB^2): a copy lies in the tile's 3 x 3 reach
 }
 
-// list[0] = number of big tiles, list[1..]: the tiles; their cursor rows zeroed, kept_tile reset
+// list[0] = number of big tiles, list[1..]: the tiles; their cursor rows zeroed, kept_tile reset. One
+// thread per tile (a frame without big tiles pays one short launch; a big tile's thread zeroes its row)
 __global__ __launch_bounds__(256) void k_rt_biglist(RorLaunch L, const int *tstart, BigBufs B, int *kept_tile,
                                                     const int *dirty) {
-    __shared__ int big;
-    const int t = blockIdx.x;
-    if (threadIdx.x == 0) {
-        const int a = tstart[t], n = tstart[t + 1] - a;
-        big = (!dirty || dirty[t + 1] != dirty[t]) && n > kRorCap && a + n <= L.staged_cap;
-        if (big) {
-            B.list[1 + atomicAdd(&B.list[0], 1)] = t;
-            if (kept_tile) kept_tile[t] = 0;
-        }
-    }
-    __syncthreads();
-    if (!big) return;
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= L.ntiles) return;
+    const int a = tstart[t], n = tstart[t + 1] - a;
+    if (!((!dirty || dirty[t + 1] != dirty[t]) && n > kRorCap && a + n <= L.staged_cap)) return;
+    B.list[1 + atomicAdd(&B.list[0], 1)] = t;
+    if (kept_tile) kept_tile[t] = 0;
     const int nlb1 = (L.TB + 2) * (L.TB + 2) + 1;
-    for (int i = threadIdx.x; i < nlb1; i += 256) B.cur[(size_t)t * nlb1 + i] = 0;
+    int *row = B.cur + (size_t)t * nlb1;   // (rows are not 16 B aligned: plain stores)
+    for (int i = 0; i < nlb1; ++i) row[i] = 0;
 }
 
 // the chunk [k0, k1) of big tile i of the list
@@ -669,7 +665,7 @@ void launch_rt_ror(const RorLaunch &L, const int *tstart, float4 *staged, float4
     if (!L.ntiles) return;
     const BigBufs B = big_bufs(L, bigbins);
     AOS_HIP(hipMemsetAsync(B.list, 0, sizeof(int), s));
-    k_rt_biglist<<<L.ntiles, 256, 0, s>>>(L, tstart, B, kept_tile, dirty);
+    k_rt_biglist<<<(L.ntiles + 255) / 256, 256, 0, s>>>(L, tstart, B, kept_tile, dirty);
     const dim3 gb(kBigC, kBigY);
     k_rt_bighist<<<gb, kBigTB, 0, s>>>(L, tstart, staged, B);
     k_rt_bigscan<<<kBigY, 1024, 0, s>>>(L, tstart, B);

@@ -27,7 +27,7 @@ for sub in ("tools", "active-orchard-slam_amd"):
     sys.path.insert(0, os.path.join(ROOT, sub))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-PMC_FILE = os.path.join(ROOT, "profiles", "r02b_pmc_traffic.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r02n_pmc_traffic.json")
 
 
 def parse(argv=None):
@@ -452,6 +452,8 @@ def main():
                              "markers_latency_ms_p50": round(mlat[len(mlat) // 2], 2),
                              "markers_latency_ms_max": round(mlat[-1], 2),
                              "scan_latency_ms": [round(x * 1e3, 1) for x in latency[a.warmup:]],
+                             "scan_markers": [int(bool(pend["mk"].get(k))) for k in range(a.warmup, a.warmup + a.steps)],
+                             "scan_delaunay_ms": [round(gs[1]["ms"].get("delaunay", 0.0), 1) for gs in res],
                              "budget_ms": 1e3 / orchard.SCAN_HZ,
                              "keeps_up": max(lat[-1], dt / len(res) * 1e3) <= 1e3 / orchard.SCAN_HZ,
                              "note": "scan latency = scan H2D + pack + whole-map seed-gen + GVD graph (host clock); "
