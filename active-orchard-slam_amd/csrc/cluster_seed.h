@@ -77,7 +77,7 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
 // lives in its own cache-line-aligned heap object: the two replays write their state on every step,
 // and sharing lines with the main replay's fields slowed both down by ~40 % on the EPYC host.
 // Device buffers of the facet builder (calcVoronoi + getVoronoiFacetList on the GPU, gvd.hip).
-struct FacetBufs { DevBuf qe, vp, vfirst, vtype, face, cnt, off, scan_tmp; };
+struct FacetBufs { DevBuf qe, vp, vfirst, vtype, face, cnt, off, scan_tmp; PinnedBuf h_stage; };
 
 struct alignas(128) CellsWork {
     Subdiv2D sd;                               // extractCellBoundaries' Subdiv2D
@@ -119,6 +119,7 @@ struct GvdState {
     DevBuf edges, bpts, near_idx, cand, cand_ok, skel, grid_bytes_ext;
     PinnedBuf h_misc;
     void *scratch = nullptr;   // GvdScratch (gvd.hip), freed by free_gvd_scratch
+    PinnedBuf h_seeds;   // seeds in / merged seeds out (g1)
     Subdiv2D subdiv;   // host insert replay; kept across frames to reuse its allocations
     // host outputs
     std::vector<double> nodes_xy;

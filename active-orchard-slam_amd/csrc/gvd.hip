@@ -49,6 +49,11 @@ __device__ __forceinline__ bool occ_trunc(const int8_t *sk, const GridG &g, doub
 
 // ------------------------------------------------------------------ g1 merge
 // owner[j] = smallest earlier kept (leader) candidate conflicting with j, or j for leaders
+__global__ void k_fill_ones(int *a, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) a[i] = 1;
+}
+
 __global__ void k_merge_owner(const int *state, const int *coff, const int *clist, int n, int *owner, int *idx) {
     int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
@@ -519,10 +524,18 @@ static int facets_count(FacetBufs &F, const Subdiv2D::Raw &R, int *h_sc, hipStre
     int *d_qe = dev<int>(F.qe, 8 * (size_t)R.n_rec);
     float2 *d_vp = dev<float2>(F.vp, R.n_vtx);
     int *d_vf = dev<int>(F.vfirst, R.n_vtx), *d_vt = dev<int>(F.vtype, R.n_vtx);
-    AOS_HIP(hipMemcpyAsync(d_qe, R.qe, sizeof(int) * 8 * (size_t)R.n_rec, hipMemcpyHostToDevice, s));
-    AOS_HIP(hipMemcpyAsync(d_vp, R.vp, sizeof(float2) * R.n_vtx, hipMemcpyHostToDevice, s));
-    AOS_HIP(hipMemcpyAsync(d_vf, R.vfirst, sizeof(int) * R.n_vtx, hipMemcpyHostToDevice, s));
-    AOS_HIP(hipMemcpyAsync(d_vt, R.vtype, sizeof(int) * R.n_vtx, hipMemcpyHostToDevice, s));
+    // the quad-edge export (~5 MB at C2) goes through the builder's own pinned buffer (a pageable copy
+    // is staged by the runtime through its own buffers and blocks the calling thread)
+    const size_t bq = sizeof(int) * 8 * (size_t)R.n_rec, bv = sizeof(float2) * R.n_vtx, bi = sizeof(int) * R.n_vtx;
+    char *hs = static_cast<char *>(F.h_stage.ensure(bq + bv + 2 * bi));
+    std::memcpy(hs, R.qe, bq);
+    std::memcpy(hs + bq, R.vp, bv);
+    std::memcpy(hs + bq + bv, R.vfirst, bi);
+    std::memcpy(hs + bq + bv + bi, R.vtype, bi);
+    AOS_HIP(hipMemcpyAsync(d_qe, hs, bq, hipMemcpyHostToDevice, s));
+    AOS_HIP(hipMemcpyAsync(d_vp, hs + bq, bv, hipMemcpyHostToDevice, s));
+    AOS_HIP(hipMemcpyAsync(d_vf, hs + bq + bv, bi, hipMemcpyHostToDevice, s));
+    AOS_HIP(hipMemcpyAsync(d_vt, hs + bq + bv + bi, bi, hipMemcpyHostToDevice, s));
     float2 *d_face = dev<float2>(F.face, 2 * (size_t)R.n_rec);
     int *d_cnt = dev<int>(F.cnt, R.n_vtx + 2), *d_off = dev<int>(F.off, R.n_vtx + 1);
     AOS_HIP(hipMemsetAsync(d_cnt + R.n_vtx, 0, 2 * sizeof(int), s));
@@ -545,6 +558,12 @@ static void facets_emit(FacetBufs &F, const Subdiv2D::Raw &R, float4 *edges, hip
 // bounding box as the rectangle, then cell i = facet i (i < seeds, facets) with >= 3 points, closed
 // when its ends are more than 1 cm apart, paired with seeds_[i] and coloured from hue = i / cells.
 // Pure host work on the merged seeds: it runs on a worker thread next to the main replay.
+static void cells_colours(CellsWork &W, const std::vector<double> &seeds, int ncell);
+static bool markers_gpu_facets() {   // AOS_MARKERS_GPU_FACETS=1: the markers' facets on the GPU builder
+    static const bool on = getenv("AOS_MARKERS_GPU_FACETS") != nullptr;
+    return on;
+}
+
 static void compute_cells(CellsWork &W, int rect_mode) {
     const auto t0 = std::chrono::steady_clock::now();
     W.cell_off.assign(1, 0);
@@ -572,6 +591,28 @@ static void compute_cells(CellsWork &W, int rect_mode) {
         x = std::max(rx + margin, std::min(rx + rw - margin, x));
         y = std::max(ry + margin, std::min(ry + rh - margin, y));
         sd.insert(x, y);   // insertion failures are skipped (voronoi_diagram.cpp:280-285)
+    }
+    if (!markers_gpu_facets()) {
+        // getVoronoiFacetList on the worker's own core (calcVoronoi + the facet walk of subdiv2d.cpp, the
+        // host reference of the GPU builder, bit-identical to it): the markers job then needs no stream,
+        // pinned buffers or GPU time of its own; the walk costs the worker a few ms next to its replay
+        std::vector<int> off;
+        std::vector<float> xy;
+        sd.voronoi_facets(off, xy);
+        int ncell = 0;
+        for (size_t f = 0; f + 1 < off.size() && (int)f < ns; ++f) {
+            const int b0 = off[f], n = off[f + 1] - b0;
+            if (n < 3) continue;
+            for (int j = 0; j < n; ++j) { W.cell_xy.push_back(xy[2 * (b0 + j)]); W.cell_xy.push_back(xy[2 * (b0 + j) + 1]); }
+            const double dx = (double)xy[2 * b0] - (double)xy[2 * (b0 + n - 1)];
+            const double dy = (double)xy[2 * b0 + 1] - (double)xy[2 * (b0 + n - 1) + 1];
+            if (std::sqrt(dx * dx + dy * dy) > 0.01) { W.cell_xy.push_back(xy[2 * b0]); W.cell_xy.push_back(xy[2 * b0 + 1]); }
+            W.cell_off.push_back((int32_t)(W.cell_xy.size() / 2));
+            ++ncell;
+        }
+        cells_colours(W, seeds, ncell);
+        W.ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        return;
     }
     // getVoronoiFacetList on the GPU (the builder of the main graph, on the worker's stream): the
     // facet of real vertex k is the start points of its k_facet_emit edges, cnt[k] of them (0 for a
@@ -606,7 +647,13 @@ static void compute_cells(CellsWork &W, int rect_mode) {
         W.cell_off.push_back((int32_t)(W.cell_xy.size() / 2));
         ++ncell;
     }
-    for (int i = 0; i < ncell; ++i) {   // gvd:1117-1145 (float arithmetic as written)
+    cells_colours(W, seeds, ncell);
+    W.ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// cell i's centre and colour (gvd:1117-1145, float arithmetic as written)
+static void cells_colours(CellsWork &W, const std::vector<double> &seeds, int ncell) {
+    for (int i = 0; i < ncell; ++i) {
         W.cell_center.push_back(seeds[2 * i]); W.cell_center.push_back(seeds[2 * i + 1]);
         float hue = static_cast<float>(i) / std::max(1.0f, static_cast<float>(ncell));
         float saturation = 0.7f, value = 0.9f;
@@ -622,7 +669,6 @@ static void compute_cells(CellsWork &W, int rect_mode) {
         else { r = cc; g = 0.0f; b = x; }
         W.cell_rgba.push_back(r + m); W.cell_rgba.push_back(g + m); W.cell_rgba.push_back(b + m); W.cell_rgba.push_back(0.4f);
     }
-    W.ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
 // The cells' worker thread. publishMarkers runs after publishGraph (gvd:310-313), so the graph is
@@ -713,13 +759,13 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
 
     // ---- g1 merge
     double2 *d_raw = dev<double2>(S.raw, n);
-    AOS_HIP(hipMemcpyAsync(d_raw, in.seeds_host, sizeof(double2) * n, hipMemcpyHostToDevice, s));
+    // seeds in and merged seeds out through the state's pinned buffer (a pageable copy is staged by the
+    // runtime and, measured on the streaming map, could stall ~20 ms behind unrelated copy traffic)
+    double *h_seeds = static_cast<double *>(G.h_seeds.ensure(sizeof(double2) * (size_t)n));
+    std::memcpy(h_seeds, in.seeds_host, sizeof(double2) * (size_t)n);
+    AOS_HIP(hipMemcpyAsync(d_raw, h_seeds, sizeof(double2) * n, hipMemcpyHostToDevice, s));
     int *d_ok = dev<int>(S.ok, n);
-    {
-        std::vector<int> ones(n, 1);
-        AOS_HIP(hipMemcpyAsync(d_ok, ones.data(), sizeof(int) * n, hipMemcpyHostToDevice, s));
-        AOS_HIP(hipStreamSynchronize(s));
-    }
+    k_fill_ones<<<cdiv(n, 256), 256, 0, s>>>(d_ok, n);
     const HashG hm = make_hash(g.minx - 60.0, g.maxx + 60.0, g.miny - 60.0, g.maxy + 60.0, 0.5);
     double2 *d_lead_pts = dev<double2>(S.merged, n);
     int *d_leaders = dev<int>(S.leaders, n);
@@ -737,8 +783,9 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     double2 *d_merged = d_lead_pts;  // overwritten in leader order
     k_merge_sum<<<cdiv(nl, 128), 128, 0, s>>>(d_raw, d_sowner, d_sj, n, d_leaders, nl, d_merged);
     std::vector<double> merged(2 * (size_t)nl);
-    AOS_HIP(hipMemcpyAsync(merged.data(), d_merged, sizeof(double2) * nl, hipMemcpyDeviceToHost, s));
+    AOS_HIP(hipMemcpyAsync(h_seeds, d_merged, sizeof(double2) * nl, hipMemcpyDeviceToHost, s));
     AOS_HIP(hipStreamSynchronize(s));
+    std::memcpy(merged.data(), h_seeds, sizeof(double2) * (size_t)nl);
     G.n_merged = nl;
     AOS_HIP(hipEventRecord(ev[7], s));
     G.merged_xy = merged;

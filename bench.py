@@ -227,7 +227,9 @@ def main():
 
     def markers_for(k):   # the publish throttle of processGraph (gvd:306-314)
         now = time.perf_counter()
-        mk = a.markers_every_frame or now - pend["last_pub"] >= pub_period
+        # (--stream keeps the markers on every scan: with the throttle, the scan after a markers scan
+        # showed a ~25 ms stall of its first stream sync with the GPU idle, not understood)
+        mk = a.markers_every_frame or a.stream or now - pend["last_pub"] >= pub_period
         if mk:
             pend["last_pub"] = now
         pend["mk"][k] = mk
@@ -308,11 +310,17 @@ def main():
                       f"{ms.get('delaunay', 0):.1f} total {ms.get('total', 0):.1f} cells {ms.get('cells', 0):.1f}",
                       file=sys.stderr, flush=True)
             return g, gg
+        ta = time.perf_counter()
         if k > 0 and pend.get("mk_pending", False):
             collect()
+        tb = time.perf_counter()
         mk = markers_for(k)
         gg = ctx.gvd_from_seedgen()
         pend["mk_pending"] = mk
+        if a.trace:
+            print(f"[trace] step {k}: seed-gen {1e3 * (ta - t0):.2f} ms, collect previous markers {1e3 * (tb - ta):.2f} ms "
+                  f"(cells {pend['ms']:.1f} ms), GVD {1e3 * (time.perf_counter() - tb):.2f} ms (delaunay "
+                  f"{gg['ms'].get('delaunay', 0):.1f}, all {gg['ms']}), markers {int(mk)}", file=sys.stderr, flush=True)
         if a.stream:
             latency.append(time.perf_counter() - t0)
         pend["mt0"] = t0
@@ -433,7 +441,7 @@ def main():
             "pipeline": (f"depth {depth}: frame k's seed-gen overlaps the GVDs of frames k-1 .. k-{depth} (the "
                          f"reference's two nodes; frames are independent, each GVD's Subdiv2D replay on its own core)")
                         if pipeline else "sequential",
-            "markers": {"policy": "every frame" if a.markers_every_frame else
+            "markers": {"policy": "every frame" if a.markers_every_frame or a.stream else
                         f"the frames the node publishes: at most max_graph_publish_rate = {params.max_graph_publish_rate:g} Hz "
                         f"of wall time (gvd:306-314); every frame's graph is built and returned",
                         "timed_frames_with_markers": mk_frames},
