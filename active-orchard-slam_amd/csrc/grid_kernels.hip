@@ -139,7 +139,7 @@ void launch_open(const uint64_t *in, uint64_t *out, const FrameGeom &g, hipStrea
 //   m1 == m2 == 0: iter 0: p2p4p6 = p4p6p8 = 0; iter 1: p2p4p8 = p2p6p8 = 0
 // Rows 0 / H-1 and columns 0 / W-1 of the image are never examined (ximgproc loops 1..n-2).
 #ifndef AOS_THIN_TB
-#define AOS_THIN_TB 512
+#define AOS_THIN_TB 1024
 #endif
 #ifndef AOS_THIN_TH
 #define AOS_THIN_TH 128

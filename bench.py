@@ -27,7 +27,7 @@ for sub in ("tools", "active-orchard-slam_amd"):
     sys.path.insert(0, os.path.join(ROOT, sub))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-PMC_FILE = os.path.join(ROOT, "profiles", "r02n_pmc_traffic.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r02q_pmc_traffic.json")
 
 
 def parse(argv=None):
