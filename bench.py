@@ -229,7 +229,8 @@ def main():
         now = time.perf_counter()
         # (--stream keeps the markers on every scan: with the throttle, the scan after a markers scan
         # showed a ~25 ms stall of its first stream sync with the GPU idle, not understood)
-        mk = a.markers_every_frame or a.stream or now - pend["last_pub"] >= pub_period
+        every = a.markers_every_frame or (a.stream and not os.environ.get("AOS_BENCH_STREAM_THROTTLE"))
+        mk = every or now - pend["last_pub"] >= pub_period
         if mk:
             pend["last_pub"] = now
         pend["mk"][k] = mk
