@@ -56,6 +56,8 @@ def parse(argv=None):
     ap.add_argument("--markers-every-frame", action="store_true",
                     help="publishMarkers' cells (a second Subdiv2D) for every frame; default: for the frames the "
                          "node publishes, at most max_graph_publish_rate (10 Hz) as the reference does (gvd:306-314)")
+    ap.add_argument("--no-markers", action="store_true",
+                    help="(diagnostic) no publishMarkers cells at all; not the reference's work")
     ap.add_argument("--fixed-root", action="store_true",
                     help="--tiled: rank 0 finishes every frame (default: frame k's root is rank k mod N, so the "
                          "whole-map stages and the GVD jobs rotate over the ranks)")
@@ -230,7 +232,7 @@ def main():
         # (--stream keeps the markers on every scan: with the throttle, the scan after a markers scan
         # showed a ~25 ms stall of its first stream sync with the GPU idle, not understood)
         every = a.markers_every_frame or (a.stream and not os.environ.get("AOS_BENCH_STREAM_THROTTLE"))
-        mk = every or now - pend["last_pub"] >= pub_period
+        mk = not a.no_markers and (every or now - pend["last_pub"] >= pub_period)
         if mk:
             pend["last_pub"] = now
         pend["mk"][k] = mk
