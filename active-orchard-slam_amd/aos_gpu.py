@@ -202,6 +202,7 @@ def lib():
         L.aos_rccl_destroy.restype = None
         L.aos_debug_grid.argtypes = [c_vp, ctypes.c_char_p, c_vp, c_u64]
         L.aos_gvd_markers_get.argtypes = [c_vp, P(GvdMarkers)]
+        L.aos_gvd_collected_markers_get.argtypes = [c_vp, P(GvdMarkers)]
         L.aos_map_reset.argtypes = [c_vp, c_u64]
         L.aos_map_append.argtypes = [c_vp, P(CloudView), c_i, P(SeedGenOut)]
         L.aos_tile_plan_compute.argtypes = [P(Params), c_vp, c_u, c_i, c_i, c_i, P(TilePlan)]
@@ -430,10 +431,12 @@ class Ctx:
         _check(lib().aos_gvd_wait(self.h, ctypes.byref(o)))
         return _gvd_dict(o)
 
-    def gvd_markers(self) -> dict:
-        """/gvd/markers content of the last GVD call (aos_gvd_markers_get)."""
+    def gvd_markers(self, collected: bool = False) -> dict:
+        """/gvd/markers content of the last GVD call (aos_gvd_markers_get); collected=True: of the frame
+        last returned by gvd_wait, even with newer jobs in flight (aos_gvd_collected_markers_get)."""
         m = GvdMarkers()
-        _check(lib().aos_gvd_markers_get(self.h, ctypes.byref(m)))
+        fn = lib().aos_gvd_collected_markers_get if collected else lib().aos_gvd_markers_get
+        _check(fn(self.h, ctypes.byref(m)))
         nc = m.n_cells
         off = _arr(m.cell_offsets, nc + 1, np.int32)
         return {"seeds": _arr(m.seeds_xy, 2 * m.n_seeds, np.float64).reshape(-1, 2),

@@ -280,10 +280,12 @@ int aos_tiled_seedgen_process(aos_ctx *c, const aos_comm *comm, int32_t tiles_x,
     AOS_GUARD_END
 }
 
-int aos_gvd_markers_get(aos_ctx *c, aos_gvd_markers *out) {
+// settle = true: the handle's newest result (a job started since the last aos_gvd_wait is waited for);
+// false: the frame last returned by aos_gvd_wait / a synchronous GVD call, even with newer jobs in flight
+static int markers_get(aos_ctx *c, aos_gvd_markers *out, bool settle) {
     if (!c || !out) { set_error("aos_gvd_markers_get: null argument"); return AOS_E_INVALID; }
     AOS_GUARD_BEGIN
-    c->gvd_view_settle();
+    if (settle) c->gvd_view_settle();
     markers_wait(c->gs(), true);   // the cells run on after the graph is returned
     // a frame whose GVD ran with markers off (aos_gvd_set_markers): computed now, as publishMarkers
     // does for the frames the node publishes (gvd:306-314)
@@ -305,6 +307,10 @@ int aos_gvd_markers_get(aos_ctx *c, aos_gvd_markers *out) {
     out->ms_cells = W.ms;
     return AOS_OK;
 }
+
+int aos_gvd_markers_get(aos_ctx *c, aos_gvd_markers *out) { return markers_get(c, out, true); }
+
+int aos_gvd_collected_markers_get(aos_ctx *c, aos_gvd_markers *out) { return markers_get(c, out, false); }
 
 int aos_path_plan(aos_ctx *c, const aos_path_graph *graph, const int8_t *skeleton, int skeleton_on_device,
                   const aos_grid_info *info, const aos_path_query *query, aos_path_out *out) {

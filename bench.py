@@ -244,24 +244,34 @@ def main():
     if pipeline:
         ctx.gvd_pipeline_depth(depth)
 
-    def collect():
-        m = ctx.gvd_markers()
+    def collect(collected=False):
+        m = ctx.gvd_markers(collected=collected)
         if pend["mt0"] is not None and a.stream:
             mk_latency.append(time.perf_counter() - pend["mt0"])
         pend["ms"] = m["ms_cells"]
         pend["mt0"] = None
         return m
 
-    def finish(j):   # pipelined: frame j's graph, then its markers
+    def flush_markers():
+        # the markers of the last frame collected with markers: its cells job finishes on its own core
+        # after the graph, so it is collected one step later (before the next aos_gvd_wait makes another
+        # frame the handle's current result) instead of holding the pipeline at once
+        j = pend.pop("mk_frame", None)
+        if j is not None:
+            pend["mt0"] = pend["t0"][j]
+            collect(collected=True)
+            pend["lat"][j] = time.perf_counter() - pend["t0"][j]   # PointCloud2 in -> graph + markers out
+
+    def finish(j):   # pipelined: frame j's graph; its markers at the next finish (or the drain)
+        flush_markers()
         gg = ctx.gvd_wait()
         if a.stream:
             latency.append(time.perf_counter() - pend["t0"][j])
-        pend["mt0"] = pend["t0"][j]
         if pend["mk"].get(j):
-            collect()
+            pend["mk_frame"] = j
         else:
             pend["ms"] = 0.0
-        pend["lat"][j] = time.perf_counter() - pend["t0"][j]   # PointCloud2 in -> graph + markers out
+            pend["lat"][j] = time.perf_counter() - pend["t0"][j]
         gg["ms"]["cells"] = pend["ms"]
         return gg
 
@@ -284,6 +294,7 @@ def main():
                 if pipeline and k == n_calls - 1:   # drain this rank's GVD jobs (its earlier root frames)
                     while pend["fifo"]:
                         gg = finish(pend["fifo"].pop(0))
+                    flush_markers()
                 elif not pipeline and k == n_calls - 1 and pend.get("mk_pending"):
                     collect()
                 return g, gg
@@ -306,6 +317,7 @@ def main():
             if k == n_calls - 1:
                 while pend["fifo"]:
                     gg = finish(pend["fifo"].pop(0))
+                flush_markers()
             if a.trace:
                 ms = gg["ms"] if gg is not None else {}
                 print(f"[trace] step {k}: seed-gen {1e3 * (t1 - t0):.2f} ms, wait oldest graph+markers "

@@ -270,6 +270,10 @@ typedef struct aos_gvd_markers {
     float ms_cells;                            /* host time of the cells' Subdiv2D + facets (parallel thread) */
 } aos_gvd_markers;
 int aos_gvd_markers_get(aos_ctx *ctx, aos_gvd_markers *out);
+/* The markers of the frame last returned by aos_gvd_wait (or the last synchronous GVD call), without
+ * waiting for the jobs started since: a pipelined caller collects a frame's cells one step later,
+ * while the next frames' jobs run (aos_gvd_markers_get would wait for the newest job). */
+int aos_gvd_collected_markers_get(aos_ctx *ctx, aos_gvd_markers *out);
 
 /* ---------------------------------------------------------------------------------------------
  * Path planning over the GvdGraph (aos_path_gen_node): graphCallback

@@ -108,6 +108,32 @@ def test_pipeline_markers_per_frame():
     c.close()
 
 
+def test_collected_markers_while_next_job_runs():
+    """aos_gvd_collected_markers_get: the markers of the frame last returned by aos_gvd_wait, collected
+    after the next frame's job has started (the bench's one-step-later collection), equal the
+    sequential markers; aos_gvd_markers_get would address the newest job instead."""
+    cfg, poly, clouds = frames()
+    ref = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res))
+    ref.set_polygon(poly)
+    seq = []
+    for cl in clouds:
+        ref.seedgen(cl, want_host=False)
+        seq.append((ref.gvd_from_seedgen(), ref.gvd_markers()))
+    ref.close()
+    c = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res))
+    c.set_polygon(poly)
+    c.gvd_pipeline_depth(2)
+    c.seedgen(clouds[0], want_host=False)
+    c.gvd_async()
+    assert_same_graph(c.gvd_wait(), seq[0][0], "frame 0")
+    c.seedgen(clouds[1], want_host=False)
+    c.gvd_async()                                   # frame 1's job runs
+    assert_same_markers(c.gvd_markers(collected=True), seq[0][1], "frame 0 collected")
+    assert_same_markers(c.gvd_markers(), seq[1][1], "frame 1 (newest)")
+    assert_same_graph(c.gvd_wait(), seq[1][0], "frame 1")
+    c.close()
+
+
 def test_pipeline_depth_frames_in_flight():
     """aos_gvd_pipeline_depth(3): three frames' GVDs run at once, collected in start order; each graph,
     its markers and a plan on it equal the sequential calls. One start past the depth supersedes the
