@@ -190,6 +190,7 @@ def lib():
         L.aos_seedgen_reprocess.argtypes = [c_vp, c_i, P(SeedGenOut)]
         L.aos_gvd_process.argtypes = [c_vp, P(GvdIn), P(GvdOut)]
         L.aos_gvd_from_seedgen.argtypes = [c_vp, P(GvdOut)]
+        L.aos_seedgen_grids_copy.argtypes = [c_vp, c_vp, c_vp]
         L.aos_gvd_from_seedgen_async.argtypes = [c_vp]
         L.aos_gvd_wait.argtypes = [c_vp, P(GvdOut)]
         L.aos_gvd_pipeline_depth.argtypes = [c_vp, c_i]
@@ -412,6 +413,13 @@ class Ctx:
                                    ctypes.byref(gi) if gi is not None else None, ctypes.byref(q), ctypes.byref(o)))
         del keep
         return _path_dict(o)
+
+    def grids_copy(self, shape) -> tuple:
+        """The last frame's /occupancy_grid and /skeletonized_occupancy_grid straight from HBM into new
+        arrays (aos_seedgen_grids_copy)."""
+        occ, skel = np.empty(shape, np.int8), np.empty(shape, np.int8)
+        _check(lib().aos_seedgen_grids_copy(self.h, occ.ctypes.data, skel.ctypes.data))
+        return occ, skel
 
     def gvd_async(self) -> None:
         """Start the GVD of the last seed-gen frame in the background (aos_gvd_from_seedgen_async)."""

@@ -184,6 +184,19 @@ int aos_gvd_from_seedgen(aos_ctx *c, aos_gvd_out *out) {
     AOS_GUARD_END
 }
 
+int aos_seedgen_grids_copy(aos_ctx *c, int8_t *occupancy, int8_t *skeleton) {
+    if (!c) { set_error("aos_seedgen_grids_copy: null handle"); return AOS_E_INVALID; }
+    if (!c->have_frame) { set_error("aos_seedgen_grids_copy: no seed-gen frame yet"); return AOS_E_STATE; }
+    AOS_GUARD_BEGIN
+    DeviceScope dev_scope(c->device);
+    const size_t C = (size_t)c->geom.W * c->geom.H;
+    if (occupancy) AOS_HIP(hipMemcpyAsync(occupancy, c->occ_bytes.p, C, hipMemcpyDeviceToHost, c->stream));
+    if (skeleton) AOS_HIP(hipMemcpyAsync(skeleton, c->skel_bytes.p, C, hipMemcpyDeviceToHost, c->stream));
+    AOS_HIP(hipStreamSynchronize(c->stream));
+    return AOS_OK;
+    AOS_GUARD_END
+}
+
 int aos_gvd_from_seedgen_async(aos_ctx *c) {
     if (!c) { set_error("aos_gvd_from_seedgen_async: null handle"); return AOS_E_INVALID; }
     if (!c->have_frame) { set_error("aos_gvd_from_seedgen_async: no seed-gen frame yet"); return AOS_E_STATE; }

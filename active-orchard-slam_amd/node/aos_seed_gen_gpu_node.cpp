@@ -25,7 +25,9 @@ uint32_t field_offset(const sensor_msgs::msg::PointCloud2 &m, const char *name) 
     throw std::runtime_error(std::string("PointCloud2 has no float32 field ") + name);
 }
 
-void fill_grid(nav_msgs::msg::OccupancyGrid &g, const aos_grid_info &info, const int8_t *data, const rclcpp::Time &t) {
+// header and info of a published grid; the data vector is sized here and filled by aos_seedgen_grids_copy
+// straight from HBM (no intermediate host copy)
+void grid_header(nav_msgs::msg::OccupancyGrid &g, const aos_grid_info &info, const rclcpp::Time &t) {
     g.header.frame_id = "map";   // seed_gen:542-576
     g.header.stamp = t;
     g.info.resolution = info.resolution;
@@ -34,7 +36,7 @@ void fill_grid(nav_msgs::msg::OccupancyGrid &g, const aos_grid_info &info, const
     g.info.origin.position.x = info.origin_x;
     g.info.origin.position.y = info.origin_y;
     g.info.origin.orientation.w = 1.0;
-    g.data.assign(data, data + (size_t)info.width * info.height);
+    g.data.resize((size_t)info.width * info.height);
 }
 
 geometry_msgs::msg::PoseArray poses(const double *xy, int n, const rclcpp::Time &t) {
@@ -102,7 +104,7 @@ class AosSeedGenGpuNode : public rclcpp::Node {
         v.is_dense = m.is_dense;
         v.on_device = 0;
         aos_seedgen_out out{};
-        if (aos_seedgen_process(ctx_, &v, 1, &out) != AOS_OK) {
+        if (aos_seedgen_process(ctx_, &v, 0, &out) != AOS_OK) {   // grids: aos_seedgen_grids_copy in publish()
             RCLCPP_ERROR(get_logger(), "seed gen failed: %s", aos_last_error());
             return;
         }
@@ -114,15 +116,19 @@ class AosSeedGenGpuNode : public rclcpp::Node {
         for (const auto &p : m.polygon.points) { xy.push_back(p.x); xy.push_back(p.y); }
         if (aos_set_polygon(ctx_, xy.data(), (uint32_t)m.polygon.points.size()) != AOS_OK) return;
         aos_seedgen_out out{};
-        const int rc = aos_seedgen_reprocess(ctx_, 1, &out);
+        const int rc = aos_seedgen_reprocess(ctx_, 0, &out);
         if (rc == AOS_OK) publish(out);
         else if (rc != AOS_E_STATE) RCLCPP_ERROR(get_logger(), "reprocess failed: %s", aos_last_error());
     }
     void publish(const aos_seedgen_out &o) {
         const rclcpp::Time t = now();
         nav_msgs::msg::OccupancyGrid occ, skel;
-        fill_grid(occ, o.info, o.occupancy, t);
-        fill_grid(skel, o.info, o.skeleton, t);
+        grid_header(occ, o.info, t);
+        grid_header(skel, o.info, t);
+        if (aos_seedgen_grids_copy(ctx_, occ.data.data(), skel.data.data()) != AOS_OK) {
+            RCLCPP_ERROR(get_logger(), "grid copy failed: %s", aos_last_error());
+            return;
+        }
         pub_occ_->publish(occ);
         pub_skel_->publish(skel);
         pub_cluster_info_->publish(poses(o.cluster_info_xy, o.n_cluster_info, t));

@@ -155,6 +155,11 @@ int aos_gvd_from_seedgen(aos_ctx *ctx, aos_gvd_out *out);
  * starting one more than `depth` supersedes the oldest. aos_gvd_markers_get / aos_path_plan on the
  * handle's graph use the job aos_gvd_wait collected last, or the newest job if none was collected
  * since it started (they wait for it without collecting it). */
+/* The last seed-gen frame's two published OccupancyGrids (W*H bytes each, x + y*width), copied from HBM
+ * straight into caller memory — e.g. the data vectors of the outgoing nav_msgs/OccupancyGrid messages
+ * (seed_gen:552-577), so a frame run with want_host = 0 publishes without the library's host copies.
+ * Either pointer may be null. */
+int aos_seedgen_grids_copy(aos_ctx *ctx, int8_t *occupancy, int8_t *skeleton);
 int aos_gvd_from_seedgen_async(aos_ctx *ctx);
 int aos_gvd_wait(aos_ctx *ctx, aos_gvd_out *out);
 int aos_gvd_pipeline_depth(aos_ctx *ctx, int32_t depth);   /* 1..8 GVD jobs in flight */

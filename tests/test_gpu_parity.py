@@ -24,6 +24,24 @@ def run_both(cfg, poly=None, cloud=None, res=None, **kw):
     return g_ctx, g, o
 
 
+def test_grids_copy_into_caller_memory():
+    """aos_seedgen_grids_copy (the node's publish path: a frame with want_host = 0, both OccupancyGrids
+    copied from HBM straight into the outgoing messages' data) equals the frame's host grids and the
+    oracle's."""
+    cfg = orchard.CONFIGS["C0"]
+    c, g, o = run_both(cfg)
+    c2 = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res))
+    with pytest.raises(RuntimeError, match="no seed-gen frame"):
+        c2.grids_copy((g["height"], g["width"]))
+    c2.set_polygon(orchard.polygon(cfg))
+    g2 = c2.seedgen(orchard.generate(cfg), want_host=False)
+    occ, skel = c2.grids_copy((g2["height"], g2["width"]))
+    assert np.array_equal(occ, g["occupancy"]) and np.array_equal(skel, g["skeleton_framed"])
+    assert np.array_equal(occ, o["occupancy"]) and np.array_equal(skel, o["skeleton_framed"])
+    c.close()
+    c2.close()
+
+
 def test_c0_full_frame():
     cfg = orchard.CONFIGS["C0"]
     c, g, o = run_both(cfg)
