@@ -190,6 +190,7 @@ def lib():
         L.aos_seedgen_reprocess.argtypes = [c_vp, c_i, P(SeedGenOut)]
         L.aos_gvd_process.argtypes = [c_vp, P(GvdIn), P(GvdOut)]
         L.aos_gvd_from_seedgen.argtypes = [c_vp, P(GvdOut)]
+        L.aos_cloud_prefetch.argtypes = [c_vp, c_vp]
         L.aos_seedgen_grids_copy.argtypes = [c_vp, c_vp, c_vp]
         L.aos_gvd_from_seedgen_async.argtypes = [c_vp]
         L.aos_gvd_wait.argtypes = [c_vp, P(GvdOut)]
@@ -413,6 +414,16 @@ class Ctx:
                                    ctypes.byref(gi) if gi is not None else None, ctypes.byref(q), ctypes.byref(o)))
         del keep
         return _path_dict(o)
+
+    def cloud_prefetch(self, cloud, n_points: int | None = None, point_step=16, offs=(0, 4, 8), is_dense=True) -> None:
+        """Start uploading a host PointCloud2 for the next seedgen() of the same array (aos_cloud_prefetch)."""
+        v, keep = self._view(cloud, n_points, point_step, offs, is_dense, False)
+        self._prefetch_keep = keep
+        _check(lib().aos_cloud_prefetch(self.h, ctypes.byref(v)))
+
+    def cloud_prefetch_wait(self) -> None:
+        """Wait for the prefetch in flight and drop it (aos_cloud_prefetch(ctx, NULL))."""
+        _check(lib().aos_cloud_prefetch(self.h, None))
 
     def grids_copy(self, shape) -> tuple:
         """The last frame's /occupancy_grid and /skeletonized_occupancy_grid straight from HBM into new

@@ -59,8 +59,21 @@ struct aos_ctx {
         hipEvent_t ev[kUpThreads][2] = {}, done[kUpThreads] = {};
         bool used[kUpThreads][2] = {};
     } up;
-    void upload_h2d(void *dst, const void *src, size_t bytes);
+    // prefetch = true (aos_cloud_prefetch): dst is not read by queued work and the handle's stream is not
+    // made to wait; the consumer waits for up.done[] (set_cloud)
+    void upload_h2d(void *dst, const void *src, size_t bytes, bool prefetch = false);
     void release_uploader();
+    // aos_cloud_prefetch: the next frame's cloud uploaded into cloud_next on a background thread
+    struct Prefetch {
+        std::thread th;
+        const void *src = nullptr;
+        size_t bytes = 0;
+        bool active = false;
+        std::exception_ptr err;
+    } pf;
+    aos::DevBuf cloud_next;
+    void prefetch_start(const aos_cloud_view &v);
+    bool prefetch_join();   // true: a prefetch was in flight and succeeded
     const uint64_t *skel_bits = nullptr;   // final thinning buffer (thin_a / thin_b, or full_skel)
     aos::FrameGeom geom{};                 // the whole map
     bool tiled_frame = false;

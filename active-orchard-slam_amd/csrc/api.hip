@@ -184,6 +184,17 @@ int aos_gvd_from_seedgen(aos_ctx *c, aos_gvd_out *out) {
     AOS_GUARD_END
 }
 
+int aos_cloud_prefetch(aos_ctx *c, const aos_cloud_view *cloud) {
+    if (!c) { set_error("aos_cloud_prefetch: null handle"); return AOS_E_INVALID; }
+    if (cloud && !cloud_layout_ok(cloud)) { set_error("aos_cloud_prefetch: invalid PointCloud2 layout"); return AOS_E_INVALID; }
+    AOS_GUARD_BEGIN
+    DeviceScope dev_scope(c->device);
+    if (cloud) c->prefetch_start(*cloud);
+    else c->prefetch_join();   // wait for (and drop) the prefetch in flight
+    return AOS_OK;
+    AOS_GUARD_END
+}
+
 int aos_seedgen_grids_copy(aos_ctx *c, int8_t *occupancy, int8_t *skeleton) {
     if (!c) { set_error("aos_seedgen_grids_copy: null handle"); return AOS_E_INVALID; }
     if (!c->have_frame) { set_error("aos_seedgen_grids_copy: no seed-gen frame yet"); return AOS_E_STATE; }

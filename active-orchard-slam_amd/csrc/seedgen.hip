@@ -30,6 +30,7 @@ void aos_ctx::release() {
         b->release();
     cs.h_misc.release();
     gvd_async_stop();   // joins the jobs in flight (they use the lanes' GvdStates)
+    try { prefetch_join(); } catch (...) {}
     release_uploader();
     free_path_state(path_state);
     path_state = nullptr;
@@ -51,9 +52,10 @@ void aos_ctx::release() {
 // pinned memory on one thread. Here kUpThreads threads stage disjoint ranges in 8 MB chunks and DMA
 // them on their own streams; the handle's stream waits for all of them. The caller's buffer is only
 // read during the call (every memcpy has finished when this returns).
-void aos_ctx::upload_h2d(void *dst, const void *src, size_t bytes) {
+void aos_ctx::upload_h2d(void *dst, const void *src, size_t bytes, bool prefetch) {
     constexpr size_t kChunk = 8u << 20;
     if (bytes < 4 * kChunk) {
+        if (prefetch) throw std::logic_error("upload_h2d: prefetch of a small buffer");
         AOS_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream));
         return;
     }
@@ -64,14 +66,15 @@ void aos_ctx::upload_h2d(void *dst, const void *src, size_t bytes) {
             AOS_HIP(hipEventCreateWithFlags(&up.done[t], hipEventDisableTiming));
             for (int k = 0; k < 2; ++k) up.slot[t][k].ensure(kChunk);
         }
-    // the handle's stream may still read dst (the previous frame): the copies start after it
-    AOS_HIP(hipEventRecord(ev[15], stream));
+    // the handle's stream may still read dst (the previous frame): the copies start after it (a prefetch
+    // writes the spare buffer, which no queued work reads)
+    if (!prefetch) AOS_HIP(hipEventRecord(ev[15], stream));
     const size_t per = ((bytes + kUpThreads - 1) / kUpThreads + 4095) & ~(size_t)4095;   // covers all bytes
     std::exception_ptr err[kUpThreads];
     auto work = [&](int t) {
         try {
             AOS_HIP(hipSetDevice(device));
-            AOS_HIP(hipStreamWaitEvent(up.st[t], ev[15], 0));
+            if (!prefetch) AOS_HIP(hipStreamWaitEvent(up.st[t], ev[15], 0));
             const size_t b0 = std::min(bytes, per * t), b1 = std::min(bytes, per * (t + 1));
             int k = 0;
             for (size_t off = b0; off < b1; off += kChunk, k ^= 1) {
@@ -92,7 +95,32 @@ void aos_ctx::upload_h2d(void *dst, const void *src, size_t bytes) {
     for (auto &x : th) x.join();
     for (int t = 0; t < kUpThreads; ++t)
         if (err[t]) std::rethrow_exception(err[t]);
-    for (int t = 0; t < kUpThreads; ++t) AOS_HIP(hipStreamWaitEvent(stream, up.done[t], 0));
+    if (!prefetch)
+        for (int t = 0; t < kUpThreads; ++t) AOS_HIP(hipStreamWaitEvent(stream, up.done[t], 0));
+}
+
+// aos_cloud_prefetch: the host stages and DMAs the next cloud into cloud_next on a background thread
+// (the same four-thread uploader), while this frame's kernels and the GVD jobs run.
+void aos_ctx::prefetch_start(const aos_cloud_view &v) {
+    prefetch_join();
+    const size_t bytes = (size_t)v.n_points * v.point_step;
+    if (v.on_device || bytes < (32u << 20)) return;   // nothing to hide
+    void *dst = cloud_next.ensure(bytes);
+    pf.src = v.data;
+    pf.bytes = bytes;
+    pf.err = nullptr;
+    pf.active = true;
+    pf.th = std::thread([this, dst]() {
+        try { upload_h2d(dst, pf.src, pf.bytes, true); } catch (...) { pf.err = std::current_exception(); }
+    });
+}
+
+bool aos_ctx::prefetch_join() {
+    if (!pf.active) return false;
+    pf.th.join();
+    pf.active = false;
+    if (pf.err) { std::exception_ptr e = pf.err; pf.err = nullptr; std::rethrow_exception(e); }
+    return true;
 }
 
 void aos_ctx::release_uploader() {
@@ -118,8 +146,17 @@ void aos_ctx::set_cloud(const aos_cloud_view &v) {
         dc = static_cast<const uint8_t *>(v.data);
     } else {
         size_t bytes = (size_t)v.n_points * v.point_step;
-        void *dst = cloud_copy.ensure(std::max<size_t>(bytes, 16));
-        if (bytes) upload_h2d(dst, v.data, bytes);
+        const void *pf_src = pf.src;
+        const size_t pf_bytes = pf.bytes;
+        if (prefetch_join() && pf_src == v.data && pf_bytes == bytes) {
+            // the prefetched copy of this very view: it becomes the frame's cloud once its DMAs are done
+            std::swap(cloud_copy.p, cloud_next.p);
+            std::swap(cloud_copy.cap, cloud_next.cap);
+            for (int t = 0; t < kUpThreads; ++t) AOS_HIP(hipStreamWaitEvent(stream, up.done[t], 0));
+        } else {
+            void *dst = cloud_copy.ensure(std::max<size_t>(bytes, 16));
+            if (bytes) upload_h2d(dst, v.data, bytes);
+        }
         dc = cloud_copy.as<uint8_t>();
     }
     n_points = v.n_points;

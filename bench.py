@@ -56,6 +56,8 @@ def parse(argv=None):
     ap.add_argument("--markers-every-frame", action="store_true",
                     help="publishMarkers' cells (a second Subdiv2D) for every frame; default: for the frames the "
                          "node publishes, at most max_graph_publish_rate (10 Hz) as the reference does (gvd:306-314)")
+    ap.add_argument("--no-prefetch", action="store_true",
+                    help="upload each frame's PointCloud2 inside its own seed-gen call (no aos_cloud_prefetch)")
     ap.add_argument("--no-markers", action="store_true",
                     help="(diagnostic) no publishMarkers cells at all; not the reference's work")
     ap.add_argument("--fixed-root", action="store_true",
@@ -302,6 +304,13 @@ def main():
             if mode["host"]:   # PointCloud2 bytes from host memory in, both OccupancyGrids to host out
                 # (the grids are returned as views of the library's pinned buffers: the ABI's ownership rule)
                 g = ctx.seedgen(h_cloud, want_host=True, copy_grids=False)
+                if pipeline and not a.no_prefetch:
+                    # the next frame's PointCloud2 crosses PCIe while this frame's GVD starts and the next
+                    # step begins (aos_cloud_prefetch); the last step waits for its (unused) upload, so the
+                    # timed region holds one upload per frame
+                    ctx.cloud_prefetch(h_cloud)
+                    if k == n_calls - 1:
+                        ctx.cloud_prefetch_wait()
             else:
                 g = ctx.seedgen(d_cloud.data_ptr(), n_points=n, on_device=True, want_host=False)
         if pipeline:

@@ -155,6 +155,12 @@ int aos_gvd_from_seedgen(aos_ctx *ctx, aos_gvd_out *out);
  * starting one more than `depth` supersedes the oldest. aos_gvd_markers_get / aos_path_plan on the
  * handle's graph use the job aos_gvd_wait collected last, or the newest job if none was collected
  * since it started (they wait for it without collecting it). */
+/* Starts copying a host PointCloud2 to the device in the background (a node can start as soon as the
+ * message arrives, while the previous frame is processed). The next aos_seedgen_process of the same view
+ * (same data pointer and size) uses that copy instead of uploading; any other call discards it. The
+ * caller keeps the bytes unchanged until then. Device views and clouds under 32 MB are ignored.
+ * cloud = NULL waits for the prefetch in flight and drops it. */
+int aos_cloud_prefetch(aos_ctx *ctx, const aos_cloud_view *cloud);
 /* The last seed-gen frame's two published OccupancyGrids (W*H bytes each, x + y*width), copied from HBM
  * straight into caller memory — e.g. the data vectors of the outgoing nav_msgs/OccupancyGrid messages
  * (seed_gen:552-577), so a frame run with want_host = 0 publishes without the library's host copies.

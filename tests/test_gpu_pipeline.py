@@ -134,6 +134,39 @@ def test_collected_markers_while_next_job_runs():
     c.close()
 
 
+def test_cloud_prefetch():
+    """aos_cloud_prefetch: the next frame's PointCloud2 uploaded in the background is used by the next
+    seed-gen of the same view, a mismatching view discards it, NULL waits and drops it; every frame equals
+    the plain upload's."""
+    cfg = orchard.CONFIGS["C1"]
+    poly = orchard.polygon(cfg)
+    a = orchard.generate(cfg, n_points=2_500_000)                    # 40 MB: above the 32 MB floor
+    b = orchard.generate(cfg, seed=cfg.seed + 3, n_points=2_500_000)
+    keys = ("occupancy", "skeleton_framed", "voronoi_seeds", "rows_info")
+    ref = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res))
+    ref.set_polygon(poly)
+    ra, rb = ref.seedgen(a), ref.seedgen(b)
+    ref.close()
+
+    def same(g, r, what):
+        assert g["thin_iters"] == r["thin_iters"], what
+        for k in keys:
+            assert np.array_equal(g[k], r[k]), (what, k)
+
+    c = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res))
+    c.set_polygon(poly)
+    same(c.seedgen(a), ra, "plain a")
+    c.cloud_prefetch(b)
+    same(c.seedgen(b), rb, "prefetched b")
+    c.cloud_prefetch(a)
+    same(c.seedgen(b), rb, "b while a was prefetched")
+    c.cloud_prefetch(a)
+    c.cloud_prefetch_wait()
+    same(c.seedgen(a), ra, "a after a dropped prefetch")
+    c.cloud_prefetch(b)
+    c.close()                                                        # a prefetch in flight at close
+
+
 def test_pipeline_depth_frames_in_flight():
     """aos_gvd_pipeline_depth(3): three frames' GVDs run at once, collected in start order; each graph,
     its markers and a plan on it equal the sequential calls. One start past the depth supersedes the
