@@ -45,7 +45,7 @@ def parse(argv=None):
                          "host-in / host-out frame")
     ap.add_argument("--no-device-rate", action="store_true", help="skip the extra device-resident loop")
     ap.add_argument("--trace", action="store_true", help="per-step timeline of the pipelined loop on stderr")
-    ap.add_argument("--depth", type=int, default=6,
+    ap.add_argument("--depth", type=int, default=8,
                     help="pipelined GVD jobs in flight (aos_gvd_pipeline_depth): frames are independent, so frame "
                          "k's GVD runs beside the GVDs of frames k-1 .. k-depth+1, each Subdiv2D replay on its own core")
     ap.add_argument("--sequential", action="store_true",
