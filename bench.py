@@ -463,7 +463,9 @@ def main():
                   "device-resident cloud, device-resident grids, host GvdGraph",
             "device_resident": dev_rate,
             "pipeline": (f"depth {depth}: frame k's seed-gen overlaps the GVDs of frames k-1 .. k-{depth} (the "
-                         f"reference's two nodes; frames are independent, each GVD's Subdiv2D replay on its own core)")
+                         f"reference's two nodes; frames are independent, each GVD's Subdiv2D replay on its own core)"
+                         + ("; frame k+1's PointCloud2 upload (aos_cloud_prefetch) overlaps frame k's GVD start, one "
+                            "upload per frame inside the timed region" if host_io and not a.no_prefetch else ""))
                         if pipeline else "sequential",
             "markers": {"policy": "every frame" if a.markers_every_frame or a.stream else
                         f"the frames the node publishes: at most max_graph_publish_rate = {params.max_graph_publish_rate:g} Hz "
