@@ -33,8 +33,8 @@ PMC_FILE = os.path.join(ROOT, "profiles", "r02q_pmc_traffic.json")
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default=None, help="C2 (default), or C3 with --tiled")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-config", default="C2", help="config of the CPU baseline frame (default: the bench's C2)")
