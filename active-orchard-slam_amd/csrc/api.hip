@@ -257,7 +257,7 @@ int aos_gvd_set_markers(aos_ctx *c, int32_t on) {
 
 int aos_gvd_pipeline_depth(aos_ctx *c, int32_t depth) {
     if (!c) { set_error("aos_gvd_pipeline_depth: null handle"); return AOS_E_INVALID; }
-    if (depth < 1 || depth > 8) { set_error("aos_gvd_pipeline_depth: depth must be in [1, 8]"); return AOS_E_INVALID; }
+    if (depth < 1 || depth > 16) { set_error("aos_gvd_pipeline_depth: depth must be in [1, 16]"); return AOS_E_INVALID; }
     AOS_GUARD_BEGIN
     DeviceScope dev_scope(c->device);
     c->gvd_depth = depth;

@@ -168,7 +168,7 @@ int aos_cloud_prefetch(aos_ctx *ctx, const aos_cloud_view *cloud);
 int aos_seedgen_grids_copy(aos_ctx *ctx, int8_t *occupancy, int8_t *skeleton);
 int aos_gvd_from_seedgen_async(aos_ctx *ctx);
 int aos_gvd_wait(aos_ctx *ctx, aos_gvd_out *out);
-int aos_gvd_pipeline_depth(aos_ctx *ctx, int32_t depth);   /* 1..8 GVD jobs in flight */
+int aos_gvd_pipeline_depth(aos_ctx *ctx, int32_t depth);   /* 1..16 GVD jobs in flight */
 /* publishMarkers' cells for the GVD calls that follow (aos_params.gvd_markers): 1 = computed in the
  * background after each graph, 0 = not computed. The reference throttles publishGraph + publishMarkers
  * (gvd:306-314, max_graph_publish_rate): a wrapper that publishes 1 frame in n turns them on for the
