@@ -329,6 +329,26 @@ def test_gvd_markers_cells_vs_oracle(name):
     c.close()
 
 
+@pytest.mark.parametrize("name", ["C0", "C1"])
+def test_gvd_rect_mode_1_vs_oracle(name):
+    """The unpinned Subdiv2D constructor choice: subdiv_rect_mode = 1 (the Rect2f -> Rect
+    conversion) on full frames — graph and markers' cells vs the oracle in the same mode."""
+    cfg = orchard.CONFIGS[name]
+    cloud, poly = orchard.generate(cfg), orchard.polygon(cfg)
+    c = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res, subdiv_rect_mode=1))
+    c.set_polygon(poly)
+    g = c.seedgen(cloud)
+    gg = c.gvd_from_seedgen()
+    m = c.gvd_markers()
+    o = O.seedgen(cloud, poly, O.default_params(grid_resolution=cfg.res))
+    op = O.default_params(grid_resolution=cfg.res, markers=1, subdiv_rect_mode=1)
+    og = O.gvd(o["voronoi_seeds"], o["rows_info"], o, op)
+    assert_seedgen_parity(g, o)
+    assert_gvd_parity(gg, og)
+    _assert_markers(m, og)
+    c.close()
+
+
 def test_gvd_markers_external_input_and_disabled():
     cfg = orchard.CONFIGS["C0"]
     cloud, poly = orchard.generate(cfg), orchard.polygon(cfg)
