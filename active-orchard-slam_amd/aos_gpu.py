@@ -28,7 +28,7 @@ class Params(ctypes.Structure):
     _fields_ = [("clipping_minz", c_f), ("clipping_maxz", c_f), ("clipping_minx", c_f), ("clipping_maxx", c_f),
                 ("clipping_miny", c_f), ("clipping_maxy", c_f), ("grid_resolution", c_f), ("inflation_radius", c_f),
                 ("cluster_min_length", c_d), ("ror_radius", c_d), ("ror_min_neighbors", c_i),
-                ("subdiv_rect_mode", c_i), ("max_graph_publish_rate", c_d), ("gvd_markers", c_i)]
+                ("subdiv_rect_mode", c_i), ("max_graph_publish_rate", c_d), ("gvd_markers", c_i), ("thin_graph", c_i)]
 
 
 class GvdMarkers(ctypes.Structure):
@@ -56,7 +56,7 @@ class SeedGenOut(ctypes.Structure):
                 ("rows_info_xy", P(c_d)), ("n_cluster_info", c_i), ("cluster_info_xy", P(c_d)),
                 ("ms_ror", c_f), ("ms_grid", c_f), ("ms_thin", c_f), ("ms_cluster", c_f), ("ms_seeds", c_f),
                 ("ms_total", c_f), ("n_binned", ctypes.c_uint64), ("ms_ror_count", c_f),
-                ("ms_ror_bin", c_f), ("ms_ror_scatter", c_f)]
+                ("ms_ror_bin", c_f), ("ms_ror_scatter", c_f), ("thin_graph", c_i), ("thin_launches", c_i)]
 
 
 class GvdIn(ctypes.Structure):
@@ -217,6 +217,9 @@ def lib():
         L.aos_group_rank.restype = c_vp
         L.aos_group_rank.argtypes = [c_vp, c_i]
         L.aos_group_process.argtypes = [c_vp, P(CloudView), c_i, c_i, P(SeedGenOut)]
+        L.aos_group_map_reset.argtypes = [c_vp, c_u64]
+        L.aos_group_map_append.argtypes = [c_vp, P(CloudView), c_i, c_i, P(SeedGenOut)]
+        L.aos_tiled_map_append.argtypes = [c_vp, P(Comm), c_i, c_i, c_i, P(CloudView), c_i, P(SeedGenOut)]
         L.aos_stream.restype = c_vp
         L.aos_stream.argtypes = [c_vp]
         _lib = L
@@ -268,7 +271,7 @@ def _seedgen_dict(o: SeedGenOut, want_host: bool, copy_grids: bool = True) -> di
         "ms": {"ror": o.ms_ror, "grid": o.ms_grid, "thin": o.ms_thin, "cluster": o.ms_cluster, "seeds": o.ms_seeds,
                "total": o.ms_total, "ror_count": o.ms_ror_count,
                "ror_bin": o.ms_ror_bin, "ror_scatter": o.ms_ror_scatter},
-        "n_binned": o.n_binned,
+        "n_binned": o.n_binned, "thin_graph": o.thin_graph, "thin_launches": o.thin_launches,
     }
     nv, nrr = o.n_virtual, o.n_ray
     seeds = r["voronoi_seeds"]
@@ -375,6 +378,25 @@ class Ctx:
         comm.error = None
         rc = lib().aos_tiled_seedgen_process(self.h, ctypes.byref(comm.c), tiles_x, tiles_y, root, ctypes.byref(v),
                                              int(want_host), ctypes.byref(o))
+        if comm.error is not None:
+            raise RuntimeError(f"communicator failed: {comm.error!r}") from comm.error
+        _check(rc)
+        if comm.rank == root:
+            return {**_seedgen_dict(o, want_host), "root": True}
+        return {"root": False, "width": o.info.width, "height": o.info.height, "thin_iters": o.thin_iters,
+                "n_clipped": o.n_clipped, "n_input": o.n_input, "n_binned": o.n_binned,
+                "ms": {"ror": o.ms_ror, "grid": o.ms_grid, "thin": o.ms_thin, "total": o.ms_total,
+                       "ror_count": o.ms_ror_count, "ror_bin": o.ms_ror_bin, "ror_scatter": o.ms_ror_scatter}}
+
+    def tiled_map_append(self, comm, tiles_x: int, tiles_y: int, scan, root: int = 0, n_points: int | None = None,
+                         point_step=16, offs=(0, 4, 8), is_dense=True, on_device=False, want_host=True) -> dict:
+        """Append a scan to this rank's tiled streaming map (its points box) and run the tiled frame on it
+        (aos_tiled_map_append). Returns like tiled_seedgen."""
+        v, _keep = self._view(scan, n_points, point_step, offs, is_dense, on_device)
+        o = SeedGenOut()
+        comm.error = None
+        rc = lib().aos_tiled_map_append(self.h, ctypes.byref(comm.c), tiles_x, tiles_y, root, ctypes.byref(v),
+                                        int(want_host), ctypes.byref(o))
         if comm.error is not None:
             raise RuntimeError(f"communicator failed: {comm.error!r}") from comm.error
         _check(rc)
@@ -528,6 +550,18 @@ class Group:
         arr = (CloudView * self.world)(*views)
         o = SeedGenOut()
         _check(lib().aos_group_process(self.h, arr, root, int(want_host), ctypes.byref(o)))
+        return _seedgen_dict(o, want_host)
+
+    def map_reset(self, reserve_points: int = 0):
+        """Empty every rank's tiled streaming map (aos_group_map_reset)."""
+        _check(lib().aos_group_map_reset(self.h, int(reserve_points)))
+
+    def map_append(self, scan, root: int = 0, want_host: bool = True, on_device: bool = False, n_points=None,
+                   point_step=16, offs=(0, 4, 8), is_dense=True) -> dict:
+        """One scan into the tiled streaming map (aos_group_map_append); returns the root's frame."""
+        v, _keep = Ctx._view(scan, n_points, point_step, offs, is_dense, on_device)
+        o = SeedGenOut()
+        _check(lib().aos_group_map_append(self.h, ctypes.byref(v), root, int(want_host), ctypes.byref(o)))
         return _seedgen_dict(o, want_host)
 
     def close(self):

@@ -4,6 +4,7 @@
 #include <condition_variable>
 #include <deque>
 #include <exception>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <thread>
@@ -30,6 +31,13 @@ struct aos_ctx {
     aos::DevBuf map_buf, scan_stage;
     uint64_t map_n = 0;
     int map_dense = 1;
+    // tiled streaming map (aos_tiled_map_append): the rank's map holds only the points of its points
+    // box; map_total counts every point appended (the frame's n_input, as on one GPU)
+    bool map_boxed = false;
+    float map_box[4] = {0, 0, 0, 0};
+    uint64_t map_total = 0;
+    aos::DevBuf map_count;
+    aos::PinnedBuf h_map_count;
     // ---- tile store of the streaming map (incremental ROR, seedgen.hip ror_stage): the map's binned
     // points partitioned by ROR tile (own + halo copies, ping-pong), tile starts, kept candidates per
     // tile; valid while the geometry, density and raster bits are the ones it was built with
@@ -41,7 +49,14 @@ struct aos_ctx {
         uint64_t n_points = 0;       // map points it covers
         double n_binned = 0;         // binned (own) points it holds
         size_t n_staged = 0;         // staged copies it holds
-        bool last_incremental = false;
+        // what this frame's ROR stage built, committed by ror_collect after the read-back
+        struct Pending {
+            bool on = false, incremental = false;
+            aos::RorLaunch L{};
+            int dense = 1;
+            uint64_t n_points = 0;
+            int cur = 0;
+        } pend;
     } ms;
     uint64_t map_scan_begin = 0;     // map points before the last aos_map_append
 
@@ -78,6 +93,24 @@ struct aos_ctx {
     aos::FrameGeom geom{};                 // the whole map
     bool tiled_frame = false;
     int thin_iters = 0, thin_iters_prev = 0;   // (the previous frame's T sizes the first thinning batch)
+    // First thinning batch (flags reset, opening, n temporal-block launches) as hipGraphs, one per batch
+    // size n (a power of two), captured on first use and replayed while every pointer and size baked into
+    // the graph is unchanged (seedgen.hip thin_first_batch). Graph shape: AOS_THIN_GRAPH (see there).
+    struct ThinGraph {
+        hipGraphExec_t exec = nullptr;
+        std::array<const void *, 8> ptrs{};   // every device / host pointer a node holds
+        std::array<int, 8> dims{};            // W, H, WW, R, launches, flag ints, shape, tiles
+    };
+    std::vector<ThinGraph> thin_graphs;
+    int thin_graph_shape = -1;                // AOS_THIN_GRAPH at create (default 1)
+    int last_thin_graph = 0, last_thin_launches = 0;
+    bool thin_graph_check = false;            // AOS_THIN_GRAPH_CHECK (diagnosis)
+    long thin_checks = 0, thin_check_failures = 0;
+    void thin_graphs_release();
+    bool thin_first_batch(const aos::FrameGeom &g, const uint64_t *d_ibits, uint64_t *d_open, uint64_t *const bufs[2],
+                          int *d_flags, int *h_flags, int *d_act, int nflags, int &batch_n, int cap_launches,
+                          const std::function<void(int)> &launch_next);
+    void thin_check_flags(const int *d_flags, const int *h_flags, int n_read, int nflags);
     uint64_t n_ror_kept = 0, n_clipped = 0;
     double ror_est_binned = 0;             // binned points of the last frame (sizes the ROR tiles)
     double ror_staged_max = 0;             // largest staged (own + halo) count seen (sizes the scatter)
@@ -112,7 +145,8 @@ struct aos_ctx {
         hipEvent_t ready = nullptr;               // the snapshot copy on the seed-gen stream
         std::vector<double> seeds, rows;          // snapshot of h_voronoi / h_rows_info
         aos_grid_info info{};
-        int markers = 1;                          // P.gvd_markers when the job started
+        aos_params P{};                           // the handle's parameters when the job started (markers incl.)
+        bool applied = false;                     // its result was made current by a settle (gvd_view_settle)
     };
     struct alignas(128) GvdLane {
         aos::GvdState gs;
@@ -142,6 +176,8 @@ struct aos_ctx {
 
     void set_cloud(const aos_cloud_view &v);
     void map_append(const aos_cloud_view &scan);
+    void map_append_box(const aos_cloud_view &scan, const float box[4]);   // tiled streaming map
+    void map_grow(uint64_t n);
     void ror_stage(const aos::FrameGeom &g, const RorOwn &o, uint64_t *rbits, bool allow_guess);
     bool ror_collect();   // after the stream synchronised: true if the ROR scatter overflowed
     void ror_stage_append(aos::RorLaunch L, uint64_t *rbits);   // streaming map: one scan on the tile store

@@ -122,12 +122,16 @@ size_t rt_bigbins_ints(const RorLaunch &L);
 void launch_rt_ror(const RorLaunch &L, const int *tstart, float4 *staged, float4 *scratch, int *bigbins,
                    uint64_t *rbits, unsigned long long *counters, int *kept_tile, const int *dirty, hipStream_t s);
 // streaming map: merge the map's tile store with a scan's partition; n_clipped from per-tile counts
+// (cap: new_st capacity in records; a merge that would exceed it writes nothing past it and sets *overflow)
 void launch_rt_merge(const float4 *old_st, const int *old_ts, const float4 *scan_st, const int *scan_ts, float4 *new_st,
-                     int *new_ts, int ntiles, hipStream_t s);
+                     int *new_ts, int ntiles, int cap, int *overflow, hipStream_t s);
 void launch_rt_sum_kept(const int *kept_tile, int ntiles, unsigned long long *counters, hipStream_t s);
 // PointCloud2 records (any float32 x/y/z offsets) -> float4 (x, y, z, 0)
 void launch_pack_xyz(const uint8_t *cloud, uint64_t n, uint32_t step, uint32_t ox, uint32_t oy, uint32_t oz, float4 *out,
                      hipStream_t s);
+// the records with x in [box[0], box[2]] and y in [box[1], box[3]] -> out[*count ...] (atomics order)
+void launch_pack_xyz_box(const uint8_t *cloud, uint64_t n, uint32_t step, uint32_t ox, uint32_t oy, uint32_t oz,
+                         const float box[4], float4 *out, unsigned long long *count, hipStream_t s);
 void launch_inflate(const uint64_t *in, uint64_t *out, const FrameGeom &g, hipStream_t s);
 void launch_bits_to_bytes(const uint64_t *bits, int8_t *out, const FrameGeom &g, int frame, hipStream_t s);
 void launch_open(const uint64_t *in, uint64_t *out, const FrameGeom &g, hipStream_t s);
@@ -145,6 +149,7 @@ int thin_tiles(const FrameGeom &g);
 void launch_thin_block(const uint64_t *in, uint64_t *out, const FrameGeom &g, int base_iter, int *flags,
                        const ThinOwn &own, hipStream_t s);
 void launch_draw_rect(int8_t *grid, const FrameGeom &g, int gx0, int gy0, int gx1, int gy1, hipStream_t s);
+void launch_zero_ints(int *p, int n, hipStream_t s);   // a kernel (no memset node in a captured graph)
 size_t scan_temp_bytes(int n);
 void launch_exclusive_scan(const int *in, int *out, int n, void *temp, size_t temp_bytes, hipStream_t s);
 

@@ -57,6 +57,7 @@ void aos_default_params(aos_params *p) {
     p->subdiv_rect_mode = 0;
     p->max_graph_publish_rate = 10.0;
     p->gvd_markers = 1;
+    p->thin_graph = 1;
 }
 
 int aos_create(const aos_params *p, int device, aos_ctx **out) {
@@ -144,6 +145,8 @@ int aos_map_reset(aos_ctx *c, uint64_t reserve_points) {
     AOS_GUARD_BEGIN
     DeviceScope dev_scope(c->device);
     c->map_n = 0;
+    c->map_total = 0;
+    c->map_boxed = false;
     c->ms.valid = false;
     c->map_dense = 1;
     if (reserve_points) c->map_buf.ensure(sizeof(float4) * reserve_points);
@@ -299,6 +302,23 @@ int aos_tiled_seedgen_process(aos_ctx *c, const aos_comm *comm, int32_t tiles_x,
     AOS_GUARD_BEGIN
     DeviceScope dev_scope(c->device);
     c->set_cloud(*cloud);
+    c->run_tiled(*comm, tiles_x, tiles_y, root, want_host != 0, *out);
+    return AOS_OK;
+    AOS_GUARD_END
+}
+
+int aos_tiled_map_append(aos_ctx *c, const aos_comm *comm, int32_t tiles_x, int32_t tiles_y, int32_t root,
+                         const aos_cloud_view *scan, int want_host, aos_seedgen_out *out) {
+    if (!c || !comm || !scan || !out) { set_error("aos_tiled_map_append: null argument"); return AOS_E_INVALID; }
+    if (!cloud_layout_ok(scan)) {
+        set_error("aos_tiled_map_append: invalid PointCloud2 layout (float32 x/y/z, 4-byte aligned)");
+        return AOS_E_INVALID;
+    }
+    AOS_GUARD_BEGIN
+    DeviceScope dev_scope(c->device);
+    const FrameGeom g = frame_geom(c->poly, c->P);
+    const TilePlan t = make_tile_plan(g, ror_margin(c->P), tiles_x, tiles_y, comm->rank);
+    c->map_append_box(*scan, t.box);
     c->run_tiled(*comm, tiles_x, tiles_y, root, want_host != 0, *out);
     return AOS_OK;
     AOS_GUARD_END

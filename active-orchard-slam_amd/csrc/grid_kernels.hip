@@ -45,6 +45,35 @@ void launch_pack_xyz(const uint8_t *cloud, uint64_t n, uint32_t step, uint32_t o
     k_pack_xyz<<<cdiv(n, 256), 256, 0, s>>>(cloud, n, step, ox, oy, oz, out);
 }
 
+// Tiled streaming map (aos_tiled_map_append): the scan's records inside this rank's points box (the
+// points its tile can rasterise or count as ROR neighbours, tiled.hip make_tile_plan) are appended to
+// the rank's map. Their order in the map is the atomics' order: the ROR keep decision and the raster
+// do not depend on point order (ror.hip).
+__global__ void k_pack_xyz_box(const uint8_t *cloud, uint64_t n, uint32_t step, uint32_t ox, uint32_t oy, uint32_t oz,
+                               float bx0, float by0, float bx1, float by1, float4 *out, unsigned long long *count) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool keep = false;
+    float4 v;
+    if (i < n) {
+        const uint8_t *rec = cloud + i * (uint64_t)step;
+        v = make_float4(*reinterpret_cast<const float *>(rec + ox), *reinterpret_cast<const float *>(rec + oy),
+                        *reinterpret_cast<const float *>(rec + oz), 0.0f);
+        keep = v.x >= bx0 && v.x <= bx1 && v.y >= by0 && v.y <= by1;   // (NaN fails: never binned)
+    }
+    const unsigned long long m = __ballot(keep);
+    if (!m) return;
+    const int lane = threadIdx.x & 63;
+    unsigned long long base = 0;
+    if (lane == __ffsll((long long)m) - 1) base = atomicAdd(count, (unsigned long long)__popcll(m));
+    base = __shfl(base, __ffsll((long long)m) - 1);
+    if (keep) out[base + __popcll(m & ((1ull << lane) - 1))] = v;
+}
+void launch_pack_xyz_box(const uint8_t *cloud, uint64_t n, uint32_t step, uint32_t ox, uint32_t oy, uint32_t oz,
+                         const float box[4], float4 *out, unsigned long long *count, hipStream_t s) {
+    if (!n) return;
+    k_pack_xyz_box<<<cdiv(n, 256), 256, 0, s>>>(cloud, n, step, ox, oy, oz, box[0], box[1], box[2], box[3], out, count);
+}
+
 __device__ __forceinline__ uint64_t pad_mask(int c, int WW, int W) {
     // bits of word c that lie inside the image
     int rem = W - c * 64;
@@ -284,6 +313,14 @@ __global__ __launch_bounds__(kThinTB) void k_thin_block(const uint64_t *__restri
 }
 
 int thin_tiles(const FrameGeom &g) { return cdiv(g.WW, TWW) * cdiv(g.H, TH); }
+
+__global__ void k_zero_ints(int *p, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = 0;
+}
+void launch_zero_ints(int *p, int n, hipStream_t s) {
+    if (n > 0) k_zero_ints<<<cdiv(n, 256), 256, 0, s>>>(p, n);
+}
 
 void launch_thin_block(const uint64_t *in, uint64_t *out, const FrameGeom &g, int base_iter, int *flags,
                        const ThinOwn &own, hipStream_t s) {

@@ -197,11 +197,14 @@ aos_ctx *aos_group_rank(aos_group *G, int32_t rank) {
     return G->ranks[rank];
 }
 
-int aos_group_process(aos_group *G, const aos_cloud_view *clouds, int32_t root, int want_host, aos_seedgen_out *root_out) {
-    if (!G || !clouds || !root_out) { set_error("aos_group_process: null argument"); return AOS_E_INVALID; }
+}  // extern "C"
+
+// Runs frame(rank, comm, out) on every rank (one thread each, plans and communicator buffers sized for
+// the current geometry); the first failing rank aborts the others' collectives.
+template <class F>
+static int group_run(aos_group *G, int32_t root, aos_seedgen_out *root_out, const char *what, F frame) {
     const int world = (int)G->ranks.size();
-    if (root < 0 || root >= world) { set_error("aos_group_process: bad root"); return AOS_E_INVALID; }
-    // plans and communicator buffers (sized once per geometry)
+    if (root < 0 || root >= world) { set_error(std::string(what) + ": bad root"); return AOS_E_INVALID; }
     std::vector<aos_comm> comms(world);
     for (int r = 0; r < world; ++r) {
         aos_tile_plan plan{};
@@ -213,7 +216,7 @@ int aos_group_process(aos_group *G, const aos_cloud_view *clouds, int32_t root, 
             m.send.ensure(std::max<uint64_t>(plan.exchange_bytes, 1));
             m.recv.ensure((size_t)world * std::max<uint64_t>(plan.exchange_bytes, 1));
         } catch (const HipError &e) {
-            set_error(std::string("aos_group_process: HIP error ") + hipGetErrorString(e.e));
+            set_error(std::string(what) + ": HIP error " + hipGetErrorString(e.e));
             return AOS_E_HIP;
         }
         comms[r] = aos_comm{&m, r, world, m.send.p, m.recv.p, plan.exchange_bytes, local_all_gather, local_all_reduce_max};
@@ -228,8 +231,7 @@ int aos_group_process(aos_group *G, const aos_cloud_view *clouds, int32_t root, 
     int fail_rank = -1, fail_rc = AOS_OK;
     std::string fail_msg;
     auto run = [&](int r) {
-        const int rc = aos_tiled_seedgen_process(G->ranks[r], &comms[r], G->tiles_x, G->tiles_y, root, &clouds[r],
-                                                 r == root ? want_host : 0, &outs[r]);
+        const int rc = frame(r, &comms[r], &outs[r]);
         if (rc != AOS_OK) {
             {
                 std::lock_guard<std::mutex> l(fail_mu);
@@ -243,11 +245,36 @@ int aos_group_process(aos_group *G, const aos_cloud_view *clouds, int32_t root, 
     run(0);
     for (auto &t : th) t.join();
     if (fail_rank >= 0) {
-        set_error("aos_group_process: rank " + std::to_string(fail_rank) + ": " + fail_msg);
+        set_error(std::string(what) + ": rank " + std::to_string(fail_rank) + ": " + fail_msg);
         return fail_rc;
     }
     *root_out = outs[root];
     return AOS_OK;
+}
+
+extern "C" {
+
+int aos_group_process(aos_group *G, const aos_cloud_view *clouds, int32_t root, int want_host, aos_seedgen_out *root_out) {
+    if (!G || !clouds || !root_out) { set_error("aos_group_process: null argument"); return AOS_E_INVALID; }
+    return group_run(G, root, root_out, "aos_group_process", [&](int r, const aos_comm *cm, aos_seedgen_out *o) {
+        return aos_tiled_seedgen_process(G->ranks[r], cm, G->tiles_x, G->tiles_y, root, &clouds[r], r == root ? want_host : 0, o);
+    });
+}
+
+int aos_group_map_reset(aos_group *G, uint64_t reserve_points) {
+    if (!G) { set_error("aos_group_map_reset: null handle"); return AOS_E_INVALID; }
+    for (aos_ctx *c : G->ranks) {
+        const int rc = aos_map_reset(c, reserve_points);
+        if (rc != AOS_OK) return rc;
+    }
+    return AOS_OK;
+}
+
+int aos_group_map_append(aos_group *G, const aos_cloud_view *scan, int32_t root, int want_host, aos_seedgen_out *root_out) {
+    if (!G || !scan || !root_out) { set_error("aos_group_map_append: null argument"); return AOS_E_INVALID; }
+    return group_run(G, root, root_out, "aos_group_map_append", [&](int r, const aos_comm *cm, aos_seedgen_out *o) {
+        return aos_tiled_map_append(G->ranks[r], cm, G->tiles_x, G->tiles_y, root, scan, r == root ? want_host : 0, o);
+    });
 }
 
 }  // extern "C"

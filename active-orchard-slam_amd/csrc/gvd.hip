@@ -1060,6 +1060,7 @@ void aos_ctx::lane_join(int l) {
 }
 
 void aos_ctx::lane_apply(int l) {
+    lanes[l]->ag.applied = true;
     cur_lane = l;
     have_gvd = true; gvd_from_frame = false; gvd_skel = lanes[l]->gs.skel.as<int8_t>(); gvd_info = lanes[l]->ag.info;
     ++gvd_gen;
@@ -1089,7 +1090,8 @@ void aos_ctx::gvd_async_start() {
     }
     A.seeds = h_voronoi;
     A.rows = h_rows_info;
-    A.markers = P.gvd_markers;
+    A.P = P;   // snapshot on the caller's thread: aos_gvd_set_markers may change P while the job runs
+    A.applied = false;
     A.info = aos_grid_info{geom.origin_x, geom.origin_y, geom.res, (uint32_t)geom.W, (uint32_t)geom.H};
     const size_t C = (size_t)geom.W * geom.H;
     int8_t *d_sk = static_cast<int8_t *>(ln.gs.skel.ensure(std::max<size_t>(C, 1)));
@@ -1116,9 +1118,7 @@ void aos_ctx::gvd_async_start() {
                         { std::lock_guard<std::mutex> g(A->mu); A->prefix = true; }
                         A->cv.notify_all();
                     };
-                    aos_params Pj = P;
-                    Pj.gvd_markers = W.markers;   // as set when the job started (aos_gvd_set_markers)
-                    pub = run_gvd_stage(ln.gs, Pj, gi, W.stream, W.ev.data());
+                    pub = run_gvd_stage(ln.gs, W.P, gi, W.stream, W.ev.data());
                 } catch (...) { e = std::current_exception(); }
                 l.lock();
                 W.err = e;
@@ -1165,7 +1165,9 @@ bool aos_ctx::gvd_async_wait(bool rethrow) {
         if (rethrow) std::rethrow_exception(e);
         return false;
     }
-    lane_apply(l);
+    // a settle (markers / planning before this wait) already made this lane current: same graph, so the
+    // path planner's graph cache (keyed on gvd_gen) stays valid
+    if (!(cur_lane == l && A.applied && have_gvd)) lane_apply(l);
     return true;
 }
 

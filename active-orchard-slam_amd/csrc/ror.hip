@@ -552,13 +552,18 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
 // Streaming map: the map's tile store (old) and the scan's partition (scan) -> the new store; per tile
 // the old run, then the scan's run. tstart_new[t] = old[t] + scan[t] for t <= ntiles.
 __global__ __launch_bounds__(256) void k_rt_merge(const float4 *old_st, const int *old_ts, const float4 *scan_st,
-                                                  const int *scan_ts, float4 *new_st, int *new_ts, int ntiles) {
+                                                  const int *scan_ts, float4 *new_st, int *new_ts, int ntiles, int cap,
+                                                  int *overflow) {
     const int t = blockIdx.x;
     if (t > ntiles) return;
     const int o0 = old_ts[t], s0 = scan_ts[t], d0 = o0 + s0;
     if (threadIdx.x == 0 && blockIdx.y == 0) new_ts[t] = d0;
     if (t == ntiles) return;
     const int no = old_ts[t + 1] - o0, ns = scan_ts[t + 1] - s0;
+    if ((long long)d0 + no + ns > cap) {   // the host's store size was stale: nothing is written past cap
+        if (threadIdx.x == 0) *overflow = 1;
+        return;
+    }
     // blockIdx.y-th of gridDim.y slices of the tile's runs (a big tile's copy spreads over CUs)
     const int stride = 256 * gridDim.y;
     for (int i = blockIdx.y * 256 + threadIdx.x; i < no; i += stride) new_st[d0 + i] = old_st[o0 + i];
@@ -594,7 +599,7 @@ void rt_configure(RorLaunch &L, int Hr, int WWr, double est_binned, int force_tb
         L.nty = (L.nby + tb - 1) / tb;
         return (long long)L.ntx * L.nty;
     };
-    if (force_tb) {
+    if (force_tb && tiles(force_tb) <= kRtMaxTiles) {
         tiles(force_tb);
     } else {
         const double per32 = est_binned * 1.15 / (double)tiles(32);
@@ -676,8 +681,8 @@ void launch_rt_ror(const RorLaunch &L, const int *tstart, float4 *staged, float4
 }
 
 void launch_rt_merge(const float4 *old_st, const int *old_ts, const float4 *scan_st, const int *scan_ts, float4 *new_st,
-                     int *new_ts, int ntiles, hipStream_t s) {
-    k_rt_merge<<<dim3(ntiles + 1, 8), 256, 0, s>>>(old_st, old_ts, scan_st, scan_ts, new_st, new_ts, ntiles);
+                     int *new_ts, int ntiles, int cap, int *overflow, hipStream_t s) {
+    k_rt_merge<<<dim3(ntiles + 1, 8), 256, 0, s>>>(old_st, old_ts, scan_st, scan_ts, new_st, new_ts, ntiles, cap, overflow);
     AOS_HIP(hipGetLastError());
 }
 

@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstring>
 #include <exception>
+#include <functional>
 #include <thread>
 
 #include "aos_ctx.h"
@@ -19,6 +20,7 @@ void aos_ctx::release() {
                       &raster_bits, &infl_bits, &open_bits, &thin_a, &thin_b, &thin_act, &occ_bytes, &skel_bytes, &flags,
                       &full_infl, &full_skel, &map_buf, &scan_stage})
         b->release();
+    thin_graphs_release();
     h_small.release();
     h_stats.release();
     h_occ.release();
@@ -148,7 +150,14 @@ void aos_ctx::set_cloud(const aos_cloud_view &v) {
         size_t bytes = (size_t)v.n_points * v.point_step;
         const void *pf_src = pf.src;
         const size_t pf_bytes = pf.bytes;
-        if (prefetch_join() && pf_src == v.data && pf_bytes == bytes) {
+        const bool same_view = pf_src == v.data && pf_bytes == bytes;
+        bool pf_ok = false;
+        try {
+            pf_ok = prefetch_join();
+        } catch (...) {
+            if (same_view) throw;   // the prefetch of this very cloud failed; another view's is dropped
+        }
+        if (pf_ok && same_view) {
             // the prefetched copy of this very view: it becomes the frame's cloud once its DMAs are done
             std::swap(cloud_copy.p, cloud_next.p);
             std::swap(cloud_copy.cap, cloud_next.cap);
@@ -168,18 +177,23 @@ void aos_ctx::set_cloud(const aos_cloud_view &v) {
 
 // Streaming ingest: append one scan to the device-resident map (aos_map_append) and make the map
 // this frame's cloud. Only the scan crosses PCIe; the map grows by 1.5x when full.
+void aos_ctx::map_grow(uint64_t n) {
+    if (map_n + n <= map_buf.cap / sizeof(float4)) return;
+    const uint64_t want = std::max<uint64_t>(map_n + n, map_n + map_n / 2);
+    DevBuf grown;
+    void *dst = grown.ensure(sizeof(float4) * std::max<uint64_t>(want, 1));
+    if (map_n) AOS_HIP(hipMemcpyAsync(dst, map_buf.p, sizeof(float4) * map_n, hipMemcpyDeviceToDevice, stream));
+    AOS_HIP(hipStreamSynchronize(stream));
+    std::swap(map_buf.p, grown.p);
+    std::swap(map_buf.cap, grown.cap);
+}
+
 void aos_ctx::map_append(const aos_cloud_view &v) {
     hipStream_t s = stream;
     const uint64_t n = v.n_points;
-    if (map_n + n > map_buf.cap / sizeof(float4)) {
-        const uint64_t want = std::max<uint64_t>(map_n + n, map_n + map_n / 2);
-        DevBuf grown;
-        void *dst = grown.ensure(sizeof(float4) * std::max<uint64_t>(want, 1));
-        if (map_n) AOS_HIP(hipMemcpyAsync(dst, map_buf.p, sizeof(float4) * map_n, hipMemcpyDeviceToDevice, s));
-        AOS_HIP(hipStreamSynchronize(s));
-        std::swap(map_buf.p, grown.p);
-        std::swap(map_buf.cap, grown.cap);
-    }
+    if (map_boxed && map_n) throw std::logic_error("aos_map_append on a tiled streaming map (aos_map_reset first)");
+    map_boxed = false;
+    map_grow(n);
     const uint8_t *src = static_cast<const uint8_t *>(v.data);
     if (n && !v.on_device) {
         void *st = scan_stage.ensure((size_t)n * v.point_step);
@@ -189,6 +203,46 @@ void aos_ctx::map_append(const aos_cloud_view &v) {
     launch_pack_xyz(src, n, v.point_step, v.off_x, v.off_y, v.off_z, map_buf.as<float4>() + map_n, s);
     map_scan_begin = map_n;
     map_n += n;
+    map_total = map_n;
+    map_dense = map_dense && v.is_dense;
+    n_points = map_n;
+    step = 16; ox = 0; oy = 4; oz = 8;
+    is_dense = map_dense;
+    d_cloud = map_buf.as<uint8_t>();
+    have_cloud = true;
+}
+
+// Tiled streaming map (aos_tiled_map_append, BASELINE configs[4] over several GPUs): every rank receives
+// the whole scan (each subscriber of /global_map does) and keeps, on its GPU, the points inside its tile's
+// points box — all its tile can rasterise or count as ROR neighbours (make_tile_plan) — so the ROR stage
+// of the tiled frame sees exactly the points it would see in the whole map. The box is fixed by the
+// polygon the map was started with.
+void aos_ctx::map_append_box(const aos_cloud_view &v, const float box[4]) {
+    hipStream_t s = stream;
+    const uint64_t n = v.n_points;
+    if (map_n && (!map_boxed || std::memcmp(map_box, box, sizeof(map_box)))) {
+        throw std::invalid_argument(map_boxed ? "tiled streaming map: the tile's points box changed (polygon or tiling); "
+                                                "aos_map_reset and append the map again"
+                                              : "aos_tiled_map_append on a whole streaming map (aos_map_reset first)");
+    }
+    map_boxed = true;
+    std::memcpy(map_box, box, sizeof(map_box));
+    map_grow(n);   // (an upper bound: every point of the scan may be in the box)
+    const uint8_t *src = static_cast<const uint8_t *>(v.data);
+    if (n && !v.on_device) {
+        void *st = scan_stage.ensure((size_t)n * v.point_step);
+        AOS_HIP(hipMemcpyAsync(st, v.data, (size_t)n * v.point_step, hipMemcpyHostToDevice, s));
+        src = static_cast<const uint8_t *>(st);
+    }
+    unsigned long long *d_cnt = static_cast<unsigned long long *>(map_count.ensure(8));
+    unsigned long long *h_cnt = static_cast<unsigned long long *>(h_map_count.ensure(8));
+    AOS_HIP(hipMemsetAsync(d_cnt, 0, 8, s));
+    launch_pack_xyz_box(src, n, v.point_step, v.off_x, v.off_y, v.off_z, box, map_buf.as<float4>() + map_n, d_cnt, s);
+    AOS_HIP(hipMemcpyAsync(h_cnt, d_cnt, 8, hipMemcpyDeviceToHost, s));
+    AOS_HIP(hipStreamSynchronize(s));
+    map_scan_begin = map_n;
+    map_n += *h_cnt;
+    map_total += n;
     map_dense = map_dense && v.is_dense;
     n_points = map_n;
     step = 16; ox = 0; oy = 4; oz = 8;
@@ -263,9 +317,13 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
     float cs_ = (float)(P.ror_radius * 1.001);
     const double ext = std::max((double)L.bmaxx - L.bminx, (double)L.bmaxy - L.bminy);
     if (ext / cs_ > 8192.0) cs_ = (float)(ext / 8192.0);  // cap the bin grid; coarser bins stay exact
-    L.inv_cs = 1.0f / cs_;
-    L.nbx = std::max(1, (int)((L.bmaxx - L.bminx) * L.inv_cs) + 1);
-    L.nby = std::max(1, (int)((L.bmaxy - L.bminy) * L.inv_cs) + 1);
+    for (;;) {   // and keep the tiles of 32 x 32 bins within the tile walk's capacity (coarser: still exact)
+        L.inv_cs = 1.0f / cs_;
+        L.nbx = std::max(1, (int)((L.bmaxx - L.bminx) * L.inv_cs) + 1);
+        L.nby = std::max(1, (int)((L.bmaxy - L.bminy) * L.inv_cs) + 1);
+        if ((long long)((L.nbx + 31) / 32) * ((L.nby + 31) / 32) <= kRtMaxTiles) break;
+        cs_ *= 1.25f;
+    }
     L.r2 = P.ror_radius * P.ror_radius;
     L.r2f = (float)(P.ror_radius * P.ror_radius);
     L.r2df = (float)L.r2;
@@ -274,17 +332,24 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
     L.origin_x = g.origin_x; L.origin_y = g.origin_y; L.res = g.res; L.W = g.W; L.H = g.H;
     L.rx0 = o.rx0; L.ry0 = o.ry0; L.rx1 = o.rx1; L.ry1 = o.ry1; L.wx0 = o.wx0; L.wy0 = o.wy0; L.Wr = o.Wr;
     const int WWr = (o.Wr + 63) / 64;
-    // the streaming map keeps a tile store across appends (its tile size stays fixed)
-    const bool map_mode = !o.limit_box && map_n > 0 && d_cloud == map_buf.as<uint8_t>() && n_points == map_n;
-    if (!map_mode) ms.valid = false;
-    ms.last_incremental = false;
+    // the streaming map keeps a tile store across appends (its tile size stays fixed); a tiled rank's
+    // map (limit_box) holds the points of its box only
+    const bool map_mode = map_n > 0 && d_cloud == map_buf.as<uint8_t>() && n_points == map_n && map_boxed == o.limit_box;
+    // the store becomes valid again only in ror_collect, once this frame's read-back shows no overflow
+    // (a frame that fails in between leaves it invalid: the next append reprocesses the whole map)
+    const bool store_ok = map_mode && ms.valid;
+    ms.valid = false;
+    ms.pend.on = false;
+    // a streaming store keeps its tile size, but only while the bin grid is the one it was built on
+    const bool same_bins = store_ok && ms.L.nbx == L.nbx && ms.L.nby == L.nby && ms.L.inv_cs == L.inv_cs &&
+                           ms.L.bminx == L.bminx && ms.L.bminy == L.bminy;
     rt_configure(L, o.Hr, WWr, ror_est_binned > 0 ? ror_est_binned : 0.5 * (double)n_points,
-                 map_mode && ms.valid ? ms.L.TB : 0);
+                 same_bins ? ms.L.TB : 0);
     auto geom_of = [](RorLaunch x) {
         x.cloud = nullptr; x.n = 0; x.step = x.ox = x.oy = x.oz = 0; x.staged_cap = 0; x.overflow = nullptr;
         return x;
     };
-    if (map_mode && ms.valid && ms.dense == is_dense && ms.n_points == map_scan_begin && n_points > ms.n_points) {
+    if (store_ok && ms.dense == is_dense && ms.n_points == map_scan_begin && n_points > ms.n_points) {
         const RorLaunch a = geom_of(L), b = ms.L;
         if (!std::memcmp(&a, &b, sizeof(RorLaunch))) { ror_stage_append(L, rbits); return; }
     }
@@ -306,7 +371,6 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
     AOS_HIP(hipMemsetAsync(d_cnt, 0, 8 * kRorCounters + 16, s));
     AOS_HIP(hipMemsetAsync(rbits, 0, sizeof(uint64_t) * (size_t)o.Hr * WWr, s));
     if (d_kept) AOS_HIP(hipMemsetAsync(d_kept, 0, sizeof(int) * nt, s));
-    ms.valid = false;
     // PCL dense kNN needs k = min_pts + 1 points in the whole cloud (else every point is removed).
     // A tile's shard holds every neighbour of its own candidates, so a shard with fewer points has
     // no keepable candidate either: the local test is exact.
@@ -344,12 +408,8 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
     // binned points, staged total, overflow flag: read with the frame's other stats (finish_frame)
     AOS_HIP(hipMemcpyAsync(h + 2, d_ts + nt, sizeof(int), hipMemcpyDeviceToHost, s));
     AOS_HIP(hipMemcpyAsync(h + 4, d_own, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
-    if (map_mode) {   // the store holds the whole map now (confirmed by ror_collect: no overflow)
-        ms.valid = true;
-        ms.L = geom_of(L);
-        ms.dense = is_dense;
-        ms.n_points = n_points;
-    }
+    if (map_mode)   // the store will hold the whole map (committed by ror_collect: no overflow)
+        ms.pend = MapStore::Pending{true, false, geom_of(L), is_dense, n_points, ms.cur};
 }
 
 // Streaming map, one appended scan: the keep decision is monotone in the point set
@@ -394,7 +454,8 @@ void aos_ctx::ror_stage_append(RorLaunch L, uint64_t *rbits) {
     AOS_HIP(hipEventRecord(ev[14], s));
     launch_rt_scatter(Ls, d_H, d_sts, G, d_scan, s);
     AOS_HIP(hipEventRecord(ev[10], s));
-    launch_rt_merge(ms.st[ms.cur].as<float4>(), ms.ts[ms.cur].as<int>(), d_scan, d_sts, d_new, d_nts, nt, s);
+    launch_rt_merge(ms.st[ms.cur].as<float4>(), ms.ts[ms.cur].as<int>(), d_scan, d_sts, d_new, d_nts, nt, (int)cap,
+                    Ls.overflow, s);
     L.staged_cap = (int)cap;
     L.overflow = Ls.overflow;
     int *d_big = static_cast<int *>(ror_bigbins.ensure(sizeof(int) * rt_bigbins_ints(L)));
@@ -404,9 +465,8 @@ void aos_ctx::ror_stage_append(RorLaunch L, uint64_t *rbits) {
     int *h = static_cast<int *>(h_stats.p);
     AOS_HIP(hipMemcpyAsync(h + 2, d_nts + nt, sizeof(int), hipMemcpyDeviceToHost, s));
     AOS_HIP(hipMemcpyAsync(h + 4, d_own, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
-    ms.cur = nxt;
-    ms.n_points = n_points;
-    ms.last_incremental = true;
+    // committed by ror_collect (the old store ms.st[ms.cur] stays intact until then)
+    ms.pend = MapStore::Pending{true, true, ms.L, ms.dense, n_points, nxt};
 }
 
 // After the frame's sync: binned count, staged size, and whether the scatter overflowed its guess.
@@ -414,13 +474,133 @@ bool aos_ctx::ror_collect() {
     int *h = static_cast<int *>(h_stats.p);
     const unsigned long long *u = reinterpret_cast<const unsigned long long *>(h + 4);
     double binned = (double)u[0];
-    if (ms.last_incremental) binned += ms.n_binned;   // the scan's binned points on top of the map's
+    if (ms.pend.on && ms.pend.incremental) binned += ms.n_binned;   // the scan's binned points on top of the map's
     h[0] = (int)binned;
     ror_est_binned = binned;
     ror_staged_max = std::max<double>(ror_staged_max, (double)h[2]);
-    if (ms.valid) { ms.n_binned = binned; ms.n_staged = (size_t)h[2]; }
-    if (u[1] != 0) ms.valid = false;
+    if (ms.pend.on && u[1] == 0) {   // commit the streaming map's tile store
+        ms.valid = true;
+        ms.L = ms.pend.L;
+        ms.dense = ms.pend.dense;
+        ms.n_points = ms.pend.n_points;
+        ms.cur = ms.pend.cur;
+        ms.n_binned = binned;
+        ms.n_staged = (size_t)h[2];
+    }
+    ms.pend.on = false;
     return u[1] != 0;
+}
+
+// First thinning batch of a whole-map frame: flags reset, opening, batch_n temporal-block launches
+// (launch_next issues them and keeps the caller's launch state). With AOS_THIN_GRAPH != 0 the batch is a
+// hipGraph (BASELINE configs[4]: hipGraph-captured thinning; aos_params.thin_graph), one per batch size,
+// batch_n rounded up to a
+// power of two. A graph bakes every argument in by value, so it is keyed on every pointer and size its
+// nodes hold (the input, opening and ping-pong bit grids, the flags, the tile-activity rows, the host
+// flags buffer when it copies them, and W, H, WW, R, the launch count, the flags length) and re-captured
+// when any of them changes; the per-launch act_prev / act_next alternation is a function of the launch
+// index from 0, the same on every replay. Graph shapes (AOS_THIN_GRAPH, for the diagnosis of round 2's
+// failure, tools/thin_graph_probe.py): 1 (default) kernels only, the flags cleared by a kernel and read
+// back outside the graph; 2 round 1's shape: memset node + kernels + D2H copy node; 3 memset node +
+// kernels; 4 clearing kernel + kernels + D2H copy node. Returns true when the graph copied the flags
+// of the batch to h_flags itself.
+bool aos_ctx::thin_first_batch(const FrameGeom &g, const uint64_t *d_ibits, uint64_t *d_open, uint64_t *const bufs[2],
+                               int *d_flags, int *h_flags, int *d_act, int nflags, int &batch_n, int cap_launches,
+                               const std::function<void(int)> &launch_next) {
+    hipStream_t s = stream;
+    const int K = kThinItersPerLaunch;
+    if (thin_graph_shape < 0) {
+        const char *e = getenv("AOS_THIN_GRAPH");   // (diagnosis: overrides aos_params.thin_graph)
+        thin_graph_shape = e ? std::max(0, std::min(4, atoi(e))) : (P.thin_graph ? 1 : 0);
+        thin_graph_check = getenv("AOS_THIN_GRAPH_CHECK") != nullptr;
+    }
+    const int shape = thin_graph_shape;
+    last_thin_graph = 0;
+    if (shape == 0) {
+        AOS_HIP(hipMemsetAsync(d_flags, 0, sizeof(int) * nflags, s));
+        launch_open(d_ibits, d_open, g, s);
+        launch_next(batch_n);
+        return false;
+    }
+    int bn = 2;
+    while (bn < batch_n) bn *= 2;
+    batch_n = std::min(bn, cap_launches);
+    const bool memset_node = shape == 2 || shape == 3, copy_node = shape == 2 || shape == 4;
+    const std::array<const void *, 8> ptrs{d_ibits, d_open, bufs[0], bufs[1], d_flags, d_act,
+                                           copy_node ? h_flags : nullptr, nullptr};
+    const std::array<int, 8> dims{g.W, g.H, g.WW, g.R, batch_n, nflags, shape, thin_tiles(g)};
+    ThinGraph *tg = nullptr;
+    for (auto &t : thin_graphs)
+        if (t.dims[4] == batch_n) tg = &t;
+    if (tg && tg->exec && (tg->ptrs != ptrs || tg->dims != dims)) {
+        AOS_HIP(hipGraphExecDestroy(tg->exec));
+        tg->exec = nullptr;
+    }
+    if (!tg) {
+        thin_graphs.emplace_back();
+        tg = &thin_graphs.back();
+    }
+    if (!tg->exec) {
+        hipGraph_t graph = nullptr;
+        AOS_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        try {
+            if (memset_node) AOS_HIP(hipMemsetAsync(d_flags, 0, sizeof(int) * nflags, s));
+            else launch_zero_ints(d_flags, nflags, s);
+            launch_open(d_ibits, d_open, g, s);
+            launch_next(batch_n);
+            if (copy_node)
+                AOS_HIP(hipMemcpyAsync(h_flags, d_flags, sizeof(int) * (1 + batch_n * K), hipMemcpyDeviceToHost, s));
+        } catch (...) {
+            (void)hipStreamEndCapture(s, &graph);
+            if (graph) (void)hipGraphDestroy(graph);
+            throw;
+        }
+        AOS_HIP(hipStreamEndCapture(s, &graph));
+        const hipError_t e = hipGraphInstantiate(&tg->exec, graph, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(graph);
+        if (e != hipSuccess) tg->exec = nullptr;
+        AOS_HIP(e);
+        tg->ptrs = ptrs;
+        tg->dims = dims;
+        last_thin_graph = 2;
+    } else {
+        last_thin_graph = 1;
+    }
+    AOS_HIP(hipGraphLaunch(tg->exec, s));
+    return copy_node;
+}
+
+void aos_ctx::thin_graphs_release() {
+    for (auto &t : thin_graphs)
+        if (t.exec) (void)hipGraphExecDestroy(t.exec);
+    thin_graphs.clear();
+}
+
+// AOS_THIN_GRAPH_CHECK: after the flags read-back, compare the host copy with a fresh synchronous read of
+// the device flags (after a device-wide sync) and check that no flag word holds anything but 0 / 1 and
+// that the words past the iterations run are still 0. Reports to stderr; diagnosis only.
+void aos_ctx::thin_check_flags(const int *d_flags, const int *h_flags, int n_read, int nflags) {
+    AOS_HIP(hipDeviceSynchronize());
+    std::vector<int> dv(nflags);
+    AOS_HIP(hipMemcpy(dv.data(), d_flags, sizeof(int) * nflags, hipMemcpyDeviceToHost));
+    int host_diff = 0, not01 = 0, tail = 0, first = -1;
+    char vals[160] = "";
+    for (int i = 0, nv = 0; i < nflags; ++i) {
+        if (i < n_read && dv[i] != h_flags[i]) { ++host_diff; if (first < 0) first = i; }
+        if (dv[i] != 0 && dv[i] != 1) {
+            ++not01;
+            if (nv < 6) { const size_t l = strlen(vals); snprintf(vals + l, sizeof(vals) - l, " [%d]=0x%08x", i, (unsigned)dv[i]); ++nv; }
+        }
+        if (i >= n_read && dv[i] != 0) ++tail;
+    }
+    ++thin_checks;
+    if (host_diff || not01 || tail) {
+        ++thin_check_failures;
+        fprintf(stderr, "[aos thin check] graph %d shape %d: %d of %d read words differ host vs device (first %d: host %d "
+                        "device %d), %d words not 0/1 (%s), %d nonzero words past the read range\n", last_thin_graph,
+                thin_graph_shape, host_diff, n_read, first, first >= 0 ? h_flags[first] : 0, first >= 0 ? dv[first] : 0,
+                not01, vals, tail);
+    }
 }
 
 void aos_ctx::run_seedgen(bool want_host, aos_seedgen_out &out) {
@@ -460,38 +640,42 @@ bool aos_ctx::run_seedgen_once(bool want_host, aos_seedgen_out &out, bool allow_
     uint64_t *bufs[2] = {static_cast<uint64_t *>(thin_a.ensure(Cw * 8)), static_cast<uint64_t *>(thin_b.ensure(Cw * 8))};
     const int K = kThinItersPerLaunch;
     const int max_iters = std::max(g.W, g.H) + 4;   // Zhang-Suen removes >= 1 cell per changing iteration
-    int *d_flags = static_cast<int *>(flags.ensure(sizeof(int) * (2 + max_iters + K)));
-    int *h_flags = static_cast<int *>(h_small.ensure(sizeof(int) * (2 + max_iters + K)));
-    ThinOwn whole{0, g.H, 0, g.WW, 1};
-    int *d_act = static_cast<int *>(thin_act.ensure(sizeof(int) * 2 * (size_t)thin_tiles(g)));
-    // first batch: opening + temporal blocks sized from the last frame's T, then the flags read-back.
-    // (Round 1 replayed this batch as a hipGraph captured on the first frame. On ROCm 7.2 a replay on a
-    // later frame with new data left garbage in the flags buffer in some frame sequences — the
-    // thinning count then ran to the iteration cap while the grids stayed right; repro:
-    // tools/dbg_stream7.py. Five plain launches cost a few microseconds, so they are issued directly.)
+    const int nflags = 2 + max_iters + K;
+    int *d_flags = static_cast<int *>(flags.ensure(sizeof(int) * nflags));
+    int *h_flags = static_cast<int *>(h_small.ensure(sizeof(int) * nflags));
+    const int ntt = thin_tiles(g);
+    int *d_act = static_cast<int *>(thin_act.ensure(sizeof(int) * 2 * (size_t)ntt));
     // Launches past convergence return at once (k_thin_block reads the previous iteration's flag on the
     // device), so the first batch is sized from the last frame's T (at least 2 launches) and later
     // batches double: a frame pays one host round trip in the common case, a few when T jumps.
-    AOS_HIP(hipMemsetAsync(d_flags, 0, sizeof(int) * (2 + max_iters + K), s));
-    launch_open(d_ibits, d_open, g, s);
     const int cap_launches = std::max(3, max_iters / K);
-    int launched = 0, batch_n = std::min(cap_launches, std::max(2, (thin_iters_prev + 2 + K - 1) / K));
+    int launched = 0;
     const uint64_t *src = d_open;
-    const uint64_t *final_buf = d_open;
-    int T = 0;
-    for (;;) {
-        for (int j = 0; j < batch_n && launched < cap_launches; ++j) {
+    ThinOwn whole{0, g.H, 0, g.WW, 1};
+    auto launch_next = [&](int count) {
+        for (int j = 0; j < count && launched < cap_launches; ++j) {
             uint64_t *dst = bufs[launched & 1];
             // tile activity of the previous launch (none for the first: every tile runs)
-            whole.act_prev = launched ? d_act + (size_t)((launched - 1) & 1) * thin_tiles(g) : nullptr;
-            whole.act_next = d_act + (size_t)(launched & 1) * thin_tiles(g);
+            whole.act_prev = launched ? d_act + (size_t)((launched - 1) & 1) * ntt : nullptr;
+            whole.act_next = d_act + (size_t)(launched & 1) * ntt;
             launch_thin_block(src, dst, g, launched * K, d_flags, whole, s);
             src = dst;
             ++launched;
         }
-        batch_n *= 2;
-        AOS_HIP(hipMemcpyAsync(h_flags, d_flags, sizeof(int) * (1 + launched * K), hipMemcpyDeviceToHost, s));
+    };
+    int batch_n = std::min(cap_launches, std::max(2, (thin_iters_prev + 2 + K - 1) / K));
+    const bool flags_in_graph = thin_first_batch(g, d_ibits, d_open, bufs, d_flags, h_flags, d_act, nflags, batch_n,
+                                                 cap_launches, launch_next);
+    launched = batch_n;
+    src = bufs[(batch_n - 1) & 1];
+    const uint64_t *final_buf = d_open;
+    int T = 0;
+    for (int round = 0;; ++round) {
+        if (round > 0) launch_next(batch_n << round);
+        if (round > 0 || !flags_in_graph)
+            AOS_HIP(hipMemcpyAsync(h_flags, d_flags, sizeof(int) * (1 + launched * K), hipMemcpyDeviceToHost, s));
         AOS_HIP(hipStreamSynchronize(s));
+        if (thin_graph_check) thin_check_flags(d_flags, h_flags, 1 + launched * K, nflags);
         T = thin_iterations(h_flags, launched * K);
         if (T) {
             // the last launch that ran: launch j runs iff j == 0 or iteration j*K-1 deleted something
@@ -503,6 +687,7 @@ bool aos_ctx::run_seedgen_once(bool want_host, aos_seedgen_out &out, bool allow_
         }
         if (launched >= cap_launches) throw std::runtime_error("thinning did not converge");
     }
+    last_thin_launches = launched;
     thin_iters = T;
     thin_iters_prev = T;
     skel_bits = final_buf;
@@ -579,7 +764,7 @@ void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *c
 
     out.info = aos_grid_info{g.origin_x, g.origin_y, g.res, (uint32_t)g.W, (uint32_t)g.H};
     out.thin_iters = thin_iters;
-    out.n_input = n_points;
+    out.n_input = (d_cloud == map_buf.as<uint8_t>() && n_points == map_n) ? map_total : n_points;
     out.n_clipped = n_clipped;
     out.n_ror_kept = 0;  // not materialised (ROR is evaluated only where it can reach the grid)
     out.occupancy = want_host ? h_occ.as<int8_t>() : nullptr;
@@ -604,6 +789,8 @@ void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *c
     out.ms_ror_count = out.n_binned ? ms(10, 11) : 0.0f;
     out.ms_ror_bin = out.n_binned ? ms(12, 13) : 0.0f;
     out.ms_ror_scatter = out.n_binned ? ms(14, 10) : 0.0f;
+    out.thin_graph = tiled_frame ? 0 : last_thin_graph;
+    out.thin_launches = last_thin_launches;
 }
 
 int aos_ctx::debug_grid(const char *which, int8_t *dst, uint64_t capacity) {

@@ -288,7 +288,7 @@ void aos_ctx::run_tiled(const aos_comm &cm, int tiles_x, int tiles_y, int root, 
     n_clipped = total;
     out.info = aos_grid_info{g.origin_x, g.origin_y, g.res, (uint32_t)g.W, (uint32_t)g.H};
     out.thin_iters = T;
-    out.n_input = n_points;
+    out.n_input = (d_cloud == map_buf.as<uint8_t>() && n_points == map_n) ? map_total : n_points;
     out.n_clipped = total;
     auto ms = [&](int a, int b) { float v = 0; (void)hipEventElapsedTime(&v, ev[a], ev[b]); return v; };
     out.ms_ror = ms(0, 1); out.ms_grid = ms(1, 2); out.ms_thin = ms(2, 3); out.ms_total = ms(0, 3);

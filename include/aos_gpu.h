@@ -58,6 +58,8 @@ typedef struct aos_params {
     double max_graph_publish_rate;           /* 10 Hz (throttle is the wrapper's job)    */
     int32_t gvd_markers;                     /* 1: also publishMarkers' Voronoi cells (gvd:1098-1194),
                                                 a second Subdiv2D on its own host thread */
+    int32_t thin_graph;                      /* 1 (default): the first thinning batch of a frame is a
+                                                replayed hipGraph; 0: plain kernel launches */
 } aos_params;
 
 void aos_default_params(aos_params *p);
@@ -105,11 +107,16 @@ typedef struct aos_seedgen_out {
     const double *cluster_info_xy;
     /* per-stage device time (ms), HIP events */
     float ms_ror, ms_grid, ms_thin, ms_cluster, ms_seeds, ms_total;
-    /* ROR neighbour-count kernel (k_ror_tile): points it staged (binned near the clip box) and
-     * its own device time, HIP events on the handle's stream around that single launch */
+    /* ROR stage (ror.hip): points it binned (near the clip box); device time of the per-tile
+     * neighbour counts (k_rt_ror + the big-tile kernels), of the count pass + tile scan (ms_ror_bin)
+     * and of the scatter pass (ms_ror_scatter), HIP events on the handle's stream */
     uint64_t n_binned;
     float ms_ror_count;
-    float ms_ror_bin, ms_ror_scatter;    /* the two counting-sort kernels before it, same events */
+    float ms_ror_bin, ms_ror_scatter;
+    /* thinning launches of this frame: thin_graph = 0 plain launches, 1 the first batch replayed from
+     * a hipGraph, 2 that graph captured this frame (then launched); thin_launches = k_thin_block
+     * launches issued (8 Zhang-Suen iterations each, launches past convergence return at once) */
+    int32_t thin_graph, thin_launches;
 } aos_seedgen_out;
 
 /* GVD inputs when not fed from this handle's seed-gen frame. */
@@ -156,9 +163,13 @@ int aos_gvd_from_seedgen(aos_ctx *ctx, aos_gvd_out *out);
  * handle's graph use the job aos_gvd_wait collected last, or the newest job if none was collected
  * since it started (they wait for it without collecting it). */
 /* Starts copying a host PointCloud2 to the device in the background (a node can start as soon as the
- * message arrives, while the previous frame is processed). The next aos_seedgen_process of the same view
- * (same data pointer and size) uses that copy instead of uploading; any other call discards it. The
- * caller keeps the bytes unchanged until then. Device views and clouds under 32 MB are ignored.
+ * message arrives, while the previous frame is processed). The next aos_seedgen_process with a host view
+ * joins it: the same view (same data pointer and size) uses that copy instead of uploading (a failed
+ * prefetch of it is raised there); another host view drops it (and any error it had) and uploads
+ * normally. aos_cloud_prefetch (another cloud or NULL) joins it too and raises its error; aos_destroy
+ * joins and drops it;
+ * aos_seedgen_process with a device view and aos_map_append leave it in flight. The caller keeps the
+ * bytes unchanged until it is joined. Device views and clouds under 32 MB are ignored.
  * cloud = NULL waits for the prefetch in flight and drops it. */
 int aos_cloud_prefetch(aos_ctx *ctx, const aos_cloud_view *cloud);
 /* The last seed-gen frame's two published OccupancyGrids (W*H bytes each, x + y*width), copied from HBM
@@ -247,6 +258,16 @@ int aos_tile_plan_compute(const aos_params *p, const double *poly_xy, uint32_t n
 int aos_tiled_seedgen_process(aos_ctx *ctx, const aos_comm *comm, int32_t tiles_x, int32_t tiles_y, int32_t root,
                               const aos_cloud_view *cloud, int want_host, aos_seedgen_out *out);
 
+/* Streaming ingest on a tiled map (BASELINE.json configs[4] over several GPUs). Every rank keeps its own
+ * device-resident map of the points inside its tile's points_box (aos_map_reset on the rank's handle
+ * starts it) and its own incremental ROR tile store. Each call hands every rank the whole scan (as every
+ * subscriber of /global_map receives it); the rank keeps its box's points on the GPU, then runs the tiled
+ * frame on its map (halo all-gathers, global thinning convergence, root finishes the frame). The root's
+ * outputs equal aos_map_append of the same scans on one GPU (n_input counts every appended point). The
+ * box follows from the polygon and the tiling: changing either needs aos_map_reset and a new map. */
+int aos_tiled_map_append(aos_ctx *ctx, const aos_comm *comm, int32_t tiles_x, int32_t tiles_y, int32_t root,
+                         const aos_cloud_view *scan, int want_host, aos_seedgen_out *out);
+
 /* One map over several GPUs from one process (SURVEY §8b's multi-GPU handle). The group owns one
  * handle per tile (devices[r] for rank r = tile (r % tiles_x, r / tiles_x); devices may repeat) and
  * drives the ranks with its own threads and an in-process aos_comm (peer copies over xGMI, host
@@ -261,6 +282,10 @@ int aos_group_plan(aos_group *group, int32_t rank, aos_tile_plan *out);
 aos_ctx *aos_group_rank(aos_group *group, int32_t rank);
 int aos_group_process(aos_group *group, const aos_cloud_view *clouds, int32_t root, int want_host,
                       aos_seedgen_out *root_out);
+/* The group's tiled streaming map (aos_tiled_map_append on every rank with the same scan). */
+int aos_group_map_reset(aos_group *group, uint64_t reserve_points_per_rank);
+int aos_group_map_append(aos_group *group, const aos_cloud_view *scan, int32_t root, int want_host,
+                         aos_seedgen_out *root_out);
 
 /* /gvd/markers content of the last GVD call (publishMarkers gvd:1012-1591) that is not already in
  * aos_gvd_out; the wrapper adds styles, ids and text. Needs aos_params.gvd_markers = 1.
@@ -334,8 +359,8 @@ typedef struct aos_path_out {
 int aos_path_plan(aos_ctx *ctx, const aos_path_graph *graph, const int8_t *skeleton, int skeleton_on_device,
                   const aos_grid_info *info, const aos_path_query *query, aos_path_out *out);
 
-/* Diagnostics: copy an internal device grid of the last frame to host as int8 {0,100} (or 0/1
- * for "opened"). which: "raster", "inflated", "opened", "skeleton_frameless". */
+/* Diagnostics: copy an internal device grid of the last frame to host as int8 {0,100}.
+ * which: "raster", "inflated", "opened", "skeleton_frameless". */
 int aos_debug_grid(aos_ctx *ctx, const char *which, int8_t *dst, uint64_t capacity);
 /* Stream of the handle (hipStream_t as void*) for callers that time with their own events. */
 void *aos_stream(aos_ctx *ctx);

@@ -42,3 +42,26 @@ def assert_gvd_parity(g: dict, o: dict):
     assert np.array_equal(g["edge_clearances"], o["edge_clearances"])
     for k in ("node_labels", "node_cluster_indices", "node_label_counts", "node_label_clusters", "node_label_types"):
         assert np.array_equal(g[k], o[k]), k
+
+
+def sha_of(a, dt):
+    """SHA-256 of an array as tools/make_golden.py hashes it (dtype, shape, bytes)."""
+    import hashlib
+    a = np.ascontiguousarray(np.asarray(a, dtype=dt))
+    return hashlib.sha256(a.dtype.str.encode() + str(a.shape).encode() + a.tobytes()).hexdigest()
+
+
+def assert_golden_hashes(g: dict, gg: dict, hs: dict, check_grids=True):
+    """A GPU frame (seed-gen dict g, GVD dict gg) vs the oracle's SHA-256 fixture hs (make_golden.py)."""
+    assert g["thin_iters"] == hs["meta"]["thin_iters"], (g["thin_iters"], hs["meta"]["thin_iters"])
+    assert g["n_clipped"] == hs["meta"]["n_clipped"], (g["n_clipped"], hs["meta"]["n_clipped"])
+    if check_grids:
+        for k in ("occupancy", "skeleton_framed"):
+            assert sha_of(g[k], np.int8) == hs["seedgen"][k], k
+    for k in ("row_center", "row_start", "row_end", "row_length", "virtual_seeds", "ray_seeds", "endpoint_seeds",
+              "voronoi_seeds", "rows_info", "cluster_info"):
+        assert sha_of(g[k], np.float64) == hs["seedgen"][k], k
+    for k, dt in (("nodes", np.float64), ("edges", np.int32), ("edge_lengths", np.float32),
+                  ("edge_clearances", np.float32), ("node_labels", np.int32), ("node_cluster_indices", np.int32),
+                  ("node_label_counts", np.int32), ("node_label_clusters", np.int32), ("node_label_types", np.int32)):
+        assert sha_of(gg[k], dt) == hs["gvd"][k], k

@@ -8,7 +8,7 @@ import pytest
 import aos_gpu
 import oracle_py as O
 import orchard
-from parity_util import assert_gvd_parity, assert_seedgen_parity, grid_diff
+from parity_util import assert_golden_hashes, assert_gvd_parity, assert_seedgen_parity, grid_diff
 
 pytestmark = pytest.mark.gpu
 
@@ -227,30 +227,15 @@ def test_c0_against_golden_fixtures():
 def test_against_golden_hashes(name):
     """Full frame (seed gen + GVD) vs the SHA-256 of the oracle's outputs (tests/golden/<name>_sha256.json);
     C2 is the bench frame, so this pins bench.py's workload bit-exactly without running the oracle."""
-    import hashlib
     import json
     import os
     hs = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", f"{name.lower()}_sha256.json")))
-
-    def sha(a, dt):
-        a = np.ascontiguousarray(np.asarray(a, dtype=dt))
-        return hashlib.sha256(a.dtype.str.encode() + str(a.shape).encode() + a.tobytes()).hexdigest()
-
     cfg = orchard.CONFIGS[name]
     c = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res))
     c.set_polygon(orchard.polygon(cfg))
     g = c.seedgen(orchard.generate(cfg))
     gg = c.gvd_from_seedgen()
-    assert g["thin_iters"] == hs["meta"]["thin_iters"] and g["n_clipped"] == hs["meta"]["n_clipped"]
-    for k in ("occupancy", "skeleton_framed"):
-        assert sha(g[k], np.int8) == hs["seedgen"][k], k
-    for k in ("row_center", "row_start", "row_end", "row_length", "virtual_seeds", "ray_seeds", "endpoint_seeds",
-              "voronoi_seeds", "rows_info", "cluster_info"):
-        assert sha(g[k], np.float64) == hs["seedgen"][k], k
-    for k, dt in (("nodes", np.float64), ("edges", np.int32), ("edge_lengths", np.float32),
-                  ("edge_clearances", np.float32), ("node_labels", np.int32), ("node_cluster_indices", np.int32),
-                  ("node_label_counts", np.int32), ("node_label_clusters", np.int32), ("node_label_types", np.int32)):
-        assert sha(gg[k], dt) == hs["gvd"][k], k
+    assert_golden_hashes(g, gg, hs)
     c.close()
 
 

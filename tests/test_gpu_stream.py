@@ -1,14 +1,18 @@
 """Streaming ingest (BASELINE.json configs[4]): scans appended to the
 device-resident map with aos_map_append must give exactly the frame of aos_seedgen_process on the
-concatenated cloud, and the oracle's frame at the end. Repeated frames on one geometry also exercise
-the hipGraph replay of the first thinning batch."""
+concatenated cloud, and the oracle's frame. The C2 test also covers configs[4]'s hipGraph-captured
+thinning: the appending handle replays its first thinning batch from hipGraphs (aos_params.thin_graph),
+the reprocessing handle launches plainly, over 20 frames whose T changes."""
+import json
+import os
+
 import numpy as np
 import pytest
 
 import aos_gpu
 import oracle_py as O
 import orchard
-from parity_util import assert_gvd_parity, assert_seedgen_parity
+from parity_util import assert_golden_hashes, assert_gvd_parity, assert_seedgen_parity
 
 pytestmark = pytest.mark.gpu
 
@@ -68,35 +72,54 @@ def test_stream_custom_layout_and_non_dense_scan():
 def test_stream_c2_map_20_scans_incremental_equals_full_reprocessing():
     """BASELINE configs[4] at full size: the C2 map (10 M points) then 20 scans of 1 M points. From the
     second frame on each append only partitions the scan and recounts the tiles it reached (the
-    incremental ROR, seedgen.hip ror_stage_append); every frame must equal reprocessing the whole
-    concatenated cloud (grids, counts, rows, seeds), and the GvdGraph every fourth scan."""
+    incremental ROR, seedgen.hip ror_stage_append), and its first thinning batch is a replayed hipGraph;
+    the reference handle reprocesses the whole concatenated cloud with plain launches. Every frame must be
+    equal (grids, T, counts, rows, seeds), the GvdGraph every fourth scan; the frames after 5 and 20 scans
+    must match the oracle's SHA-256 fixtures (tests/golden/c4_stream_sha256.json), and on the last frame
+    the oracle's Zhang-Suen on the GPU's opened grid must give the same T and skeleton."""
     import torch
     cfg = orchard.CONFIGS["C2"]
     poly = orchard.polygon(cfg)
     base = orchard.generate(cfg)
+    gpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c4_stream_sha256.json")
+    gold = json.load(open(gpath)) if os.path.exists(gpath) else {}
     n_scans = 20
-    s = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res))
+    s = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res, thin_graph=1))
     s.set_polygon(poly)
     s.map_reset(reserve_points=base.shape[0] + n_scans * orchard.SCAN_POINTS)
-    ref = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res))
+    ref = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res, thin_graph=0))
     ref.set_polygon(poly)
     g = s.map_append(base)
     full = torch.from_numpy(base).to("cuda:0")
-    ror_inc, ror_full = [], []
+    ror_inc, ror_full, Ts, graph_use = [], [], [], []
     for k in range(n_scans):
         scan = orchard.generate_scan(cfg, 40 * k)
         g = s.map_append(scan)
         full = torch.cat([full, torch.from_numpy(scan).to("cuda:0")])
         torch.cuda.synchronize()   # the library reads on its own stream
         r = ref.seedgen(full.data_ptr(), n_points=full.shape[0], on_device=True)
+        assert r["thin_graph"] == 0
         assert_seedgen_parity(g, {**r, "cluster_length": np.zeros(r["n_clusters_all"])})
         assert (g["n_clipped"], g["n_binned"], g["n_input"]) == (r["n_clipped"], r["n_binned"], full.shape[0]), k
+        Ts.append(g["thin_iters"])
+        graph_use.append(g["thin_graph"])
         ror_inc.append(g["ms"]["ror"])
         ror_full.append(r["ms"]["ror"])
-        if k % 4 == 3 or k == n_scans - 1:
+        if k % 4 == 3 or k == n_scans - 1 or k + 1 in (5, 20):
             gg, rg = s.gvd_from_seedgen(), ref.gvd_from_seedgen()
             for key in GVD_KEYS:
                 assert np.array_equal(gg[key], rg[key]), (k, key)
+            if f"scans_{k + 1}" in gold:   # the accumulated 15 M / 30 M-point frames vs the oracle
+                assert_golden_hashes(g, gg, gold[f"scans_{k + 1}"])
+    print("T per scan:", Ts, "graph use per scan:", graph_use)
+    assert all(x in (1, 2) for x in graph_use) and graph_use.count(1) >= 10, graph_use
+    assert len(set(Ts)) >= 3, Ts   # the replayed batches saw different thinning depths
+    # the oracle's ximgproc thinning on the last frame's opened grid: same T, same skeleton
+    H, W = g["height"], g["width"]
+    opened = (s.debug_grid("opened", (H, W)) != 0).astype(np.uint8)
+    skel_o, T_o = O.thin(opened)
+    assert T_o == g["thin_iters"], (T_o, g["thin_iters"])
+    assert np.array_equal(skel_o != 0, s.debug_grid("skeleton_frameless", (H, W)) != 0)
     # the appends do not reprocess the map: their ROR stage stays below the whole-map one
     print("ROR stage ms, incremental:", np.round(ror_inc, 2).tolist(), "whole map:", np.round(ror_full, 2).tolist())
     assert np.median(ror_inc) < np.median(ror_full), (ror_inc, ror_full)

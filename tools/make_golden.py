@@ -11,6 +11,9 @@ Files:
   c1_sha256.json               config C1 (2 M points, 2048^2 @ 0.1 m): SHA-256 of every output array
   c2_sha256.json               config C2 (10 M points, 4096^2 @ 0.1 m, the bench frame), with --c2
   c3_sha256.json               config C3 (40 M points, 8192^2 @ 0.1 m, the tiled config), with --c3
+  c4_stream_sha256.json        config C4 (BASELINE configs[4]): the C2 map plus the scans
+                               orchard.generate_scan(C2, 40 k), k = 0..n-1, after n = 5 and n = 20 scans
+                               (the accumulated 15 M / 30 M-point clouds), with --c4
   subdiv_kat.npz               Subdiv2D micro known-answer cases: co-circular, collinear, duplicate,
                                near-duplicate and on-edge seeds (Voronoi facets per real vertex, both
                                rect modes)
@@ -78,7 +81,8 @@ def main():
     ap.add_argument("--skip-c1", action="store_true")
     ap.add_argument("--c2", action="store_true", help="also hash config C2 (the bench frame; ~2-3 min of oracle time)")
     ap.add_argument("--c3", action="store_true", help="also hash config C3 (8192^2, 40 M points; ~30+ min of oracle time)")
-    ap.add_argument("--only-big", action="store_true", help="skip C0 / KAT / C1 and write only the --c2 / --c3 hashes")
+    ap.add_argument("--c4", action="store_true", help="also hash the C4 stream frames after 5 and 20 scans")
+    ap.add_argument("--only-big", action="store_true", help="skip C0 / KAT / C1 and write only the --c2 / --c3 / --c4 hashes")
     a = ap.parse_args()
     os.makedirs(GOLD, exist_ok=True)
     if a.only_big:
@@ -89,12 +93,38 @@ def main():
         if not want:
             continue
         s1, g1 = run(name)
-        h = {"meta": {k: s1[k] for k in ("width", "height", "thin_iters", "n_input", "n_ror_kept", "n_clipped")}}
-        h["seedgen"] = {k: sha(s1[k]) for k in GRIDS + SEED_KEYS}
-        h["gvd"] = {k: sha(g1[k]) for k in GVD_KEYS}
+        h = frame_hashes(s1, g1)
         json.dump(h, open(os.path.join(GOLD, f"{name.lower()}_sha256.json"), "w"), indent=1, sort_keys=True)
         print(name, "hashed", flush=True)
+    if a.c4:
+        stream_hashes()
     print("golden fixtures written to", GOLD)
+
+
+def frame_hashes(s1, g1):
+    h = {"meta": {k: s1[k] for k in ("width", "height", "thin_iters", "n_input", "n_ror_kept", "n_clipped")}}
+    h["seedgen"] = {k: sha(s1[k]) for k in GRIDS + SEED_KEYS}
+    h["gvd"] = {k: sha(g1[k]) for k in GVD_KEYS}
+    return h
+
+
+def stream_hashes(counts=(5, 20)):
+    """C4: the C2 map followed by scans generate_scan(C2, 40 k); the oracle reprocesses the whole
+    accumulated cloud, as the reference's globalMapCallback does (seed_gen:230-248)."""
+    cfg = orchard.CONFIGS["C2"]
+    poly = orchard.polygon(cfg)
+    p = O.default_params(grid_resolution=cfg.res)
+    parts = [orchard.generate(cfg)]
+    out = {"sequence": "C2 map, then orchard.generate_scan(C2, 40 * k) for k = 0 .. n - 1"}
+    for k in range(max(counts)):
+        parts.append(orchard.generate_scan(cfg, 40 * k))
+        if k + 1 in counts:
+            cloud = np.concatenate(parts)
+            s1 = O.seedgen(cloud, poly, p)
+            g1 = O.gvd(s1["voronoi_seeds"], s1["rows_info"], s1, p)
+            out[f"scans_{k + 1}"] = frame_hashes(s1, g1)
+            print("C4 after", k + 1, "scans hashed", flush=True)
+    json.dump(out, open(os.path.join(GOLD, "c4_stream_sha256.json"), "w"), indent=1, sort_keys=True)
 
 
 def small_fixtures():
