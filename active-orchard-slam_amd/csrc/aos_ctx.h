@@ -76,11 +76,12 @@ struct aos_ctx {
     } up;
     // prefetch = true (aos_cloud_prefetch): dst is not read by queued work and the handle's stream is not
     // made to wait; the consumer waits for up.done[] (set_cloud)
-    void upload_h2d(void *dst, const void *src, size_t bytes, bool prefetch = false);
+    void upload_pack(void *dst, const aos_cloud_view &v, bool prefetch = false);   // -> packed x, y, z (12 B)
     void release_uploader();
     // aos_cloud_prefetch: the next frame's cloud uploaded into cloud_next on a background thread
     struct Prefetch {
         std::thread th;
+        aos_cloud_view view{};
         const void *src = nullptr;
         size_t bytes = 0;
         bool active = false;
@@ -114,6 +115,7 @@ struct aos_ctx {
     uint64_t n_ror_kept = 0, n_clipped = 0;
     double ror_est_binned = 0;             // binned points of the last frame (sizes the ROR tiles)
     double ror_staged_max = 0;             // largest staged (own + halo) count seen (sizes the scatter)
+    bool ror_big_seen = false;             // a frame had a ROR tile beyond the LDS capacity (ror.hip big_ok)
 
     // ---- cluster / row / seed stage (cluster_seed.hip)
     aos::ClusterSeedState cs;

@@ -104,7 +104,9 @@ struct RorLaunch {
     // tile walk (ror.hip): TB x TB bins per tile, ntx x nty tiles; the raster window as bits (Hr rows
     // of WWr words, wx0 a multiple of 64); a tile's LDS raster window (win_rows x win_w words, 0: none)
     int TB, TBs, ntx, nty, ntiles, Hr, WWr, win_rows, win_w;   // TB = 1 << TBs
-    int staged_cap; int *overflow;   // staged array capacity; set to 1 when the scatter exceeds it
+    int staged_cap; int *overflow;   // staged array capacity; | 1 when the scatter exceeds it, | 2 when a tile
+                                     // beyond the LDS capacity was found with big_ok = 0 (the frame is redone)
+    int big_ok;                      // launch the big-tile kernels (ror.hip); 0 skips their five launches
 };
 constexpr int kRtMaxTiles = 36000;   // tiles per frame (LDS histogram of the partition passes: 144 KB)
 void rt_configure(RorLaunch &L, int Hr, int WWr, double est_binned, int force_tb = 0);

@@ -77,7 +77,8 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
 // lives in its own cache-line-aligned heap object: the two replays write their state on every step,
 // and sharing lines with the main replay's fields slowed both down by ~40 % on the EPYC host.
 // Device buffers of the facet builder (calcVoronoi + getVoronoiFacetList on the GPU, gvd.hip).
-struct FacetBufs { DevBuf qe, vp, vfirst, vtype, face, cnt, off, scan_tmp; PinnedBuf h_stage; };
+// raw = the exported Subdiv2D state in one buffer (quad-edges | points | firstEdge | type), one H2D copy
+struct FacetBufs { DevBuf raw, face, cnt, off, scan_tmp; PinnedBuf h_stage; int *qe = nullptr, *vf = nullptr, *vt = nullptr; };
 
 struct alignas(128) CellsWork {
     Subdiv2D sd;                               // extractCellBoundaries' Subdiv2D
@@ -120,6 +121,7 @@ struct GvdState {
     PinnedBuf h_misc;
     void *scratch = nullptr;   // GvdScratch (gvd.hip), freed by free_gvd_scratch
     PinnedBuf h_seeds;   // seeds in / merged seeds out (g1)
+    PinnedBuf h_out;     // the GvdGraph arrays, gathered on the device and copied back in one DMA
     Subdiv2D subdiv;   // host insert replay; kept across frames to reuse its allocations
     // host outputs
     std::vector<double> nodes_xy;

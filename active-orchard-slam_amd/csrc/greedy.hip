@@ -54,8 +54,11 @@ __device__ __forceinline__ bool conflict(double2 a, double2 b, int mode, double 
     return mode == kConflictLessEq ? (d <= thr) : (d < thr);
 }
 
-__global__ void k_hash_keys(const double2 *p, const int *ok, int n, HashG h, int *keys, int *idx) {
+// (also zeroes the scans' tail slots ccount[n] and f[n], instead of two memset blits)
+__global__ void k_hash_keys(const double2 *p, const int *ok, int n, HashG h, int *keys, int *idx, int *tail0,
+                            int *tail1) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) { *tail0 = 0; *tail1 = 0; }
     if (i >= n) return;
     int cx, cy;
     hash_cell(h, p[i].x, p[i].y, cx, cy);
@@ -140,8 +143,11 @@ __global__ void k_kept_flags(const int *state, int n, int *f) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) f[i] = state[i] == 1;
 }
-__global__ void k_compact(const double2 *p, const int *f, const int *pos, int n, double2 *out, int *kept_index) {
+// (thread 0 also gathers the batch's three read-back scalars into one slot run: one D2H copy, not three)
+__global__ void k_compact(const double2 *p, const int *f, const int *pos, int n, double2 *out, int *kept_index,
+                          const int *und_last, const int *n_conf, int *scalars) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) { scalars[0] = *und_last; scalars[1] = *n_conf; scalars[2] = pos[n]; }
     if (i < n && f[i]) {
         out[pos[i]] = p[i];
         if (kept_index) kept_index[pos[i]] = i;
@@ -154,16 +160,16 @@ int greedy_dedup(DedupScratch &S, const double2 *cand, const int *ok, int n, int
                  double2 *out, int *kept_index_out, hipStream_t s, int *h_scalar) {
     if (n <= 0) return 0;
     int *keys = dev<int>(S.keys, n), *idx = dev<int>(S.idx, n), *skeys = dev<int>(S.skeys, n), *sidx = dev<int>(S.sidx, n);
-    k_hash_keys<<<cdiv(n, 256), 256, 0, s>>>(cand, ok, n, h, keys, idx);
+    int *ccount = dev<int>(S.ccount, n + 1), *coff = dev<int>(S.coff, n + 1);
+    int *f = dev<int>(S.f, n + 1), *pos = dev<int>(S.pos, n + 1);
+    k_hash_keys<<<cdiv(n, 256), 256, 0, s>>>(cand, ok, n, h, keys, idx, ccount + n, f + n);
     size_t tb = 0, tb2 = 0;
     AOS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys, skeys, idx, sidx, n, 0, 32, s));
     AOS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, (int *)nullptr, (int *)nullptr, n + 1, s));
     void *tmp = S.tmp.ensure(std::max(tb, tb2));
     AOS_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys, skeys, idx, sidx, n, 0, 32, s));
-    int *ccount = dev<int>(S.ccount, n + 1), *coff = dev<int>(S.coff, n + 1);
     int *rows = dev<int>(S.rows, (size_t)h.ny + 1);
     k_row_starts<<<cdiv(h.ny + 1, 256), 256, 0, s>>>(skeys, n, h, rows);
-    AOS_HIP(hipMemsetAsync(ccount + n, 0, sizeof(int), s));
     k_conflicts<<<cdiv(n, 256), 256, 0, s>>>(cand, ok, n, h, skeys, sidx, rows, mode, thr, nullptr, ccount, nullptr, 0);
     AOS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, ccount, coff, n + 1, s));
     // Optimistic capacity for the conflict lists (no read-back of the exact total before the rounds):
@@ -171,15 +177,13 @@ int greedy_dedup(DedupScratch &S, const double2 *cand, const int *ok, int n, int
     long long cap = std::max<long long>((long long)(S.clist.cap / sizeof(int)), 8LL * n);
     int *clist = dev<int>(S.clist, (size_t)cap);
     int *state = dev<int>(S.state, n);
-    int *f = dev<int>(S.f, n + 1), *pos = dev<int>(S.pos, n + 1);
     constexpr int kBatch = 6;
-    int *und = dev<int>(S.und, kBatch);
+    int *und = dev<int>(S.und, kBatch + 3);   // round counters, then the three read-back scalars
     auto fill = [&]() {
         k_conflicts<<<cdiv(n, 256), 256, 0, s>>>(cand, ok, n, h, skeys, sidx, rows, mode, thr, coff, nullptr, clist, cap);
         k_greedy_init<<<cdiv(n, 256), 256, 0, s>>>(ok, n, state);
     };
     fill();
-    AOS_HIP(hipMemsetAsync(f + n, 0, sizeof(int), s));
     for (int done_rounds = 0;;) {
         // a batch of rounds, then (speculatively) the compaction of the kept set, one read-back
         AOS_HIP(hipMemsetAsync(und, 0, sizeof(int) * kBatch, s));
@@ -187,10 +191,8 @@ int greedy_dedup(DedupScratch &S, const double2 *cand, const int *ok, int n, int
             k_greedy_round<<<cdiv(n, 256), 256, 0, s>>>(n, coff, clist, state, und + r, r ? und + r - 1 : nullptr);
         k_kept_flags<<<cdiv(n, 256), 256, 0, s>>>(state, n, f);
         AOS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, f, pos, n + 1, s));
-        k_compact<<<cdiv(n, 256), 256, 0, s>>>(cand, f, pos, n, out, kept_index_out);
-        AOS_HIP(hipMemcpyAsync(h_scalar, und + kBatch - 1, sizeof(int), hipMemcpyDeviceToHost, s));
-        AOS_HIP(hipMemcpyAsync(h_scalar + 1, coff + n, sizeof(int), hipMemcpyDeviceToHost, s));
-        AOS_HIP(hipMemcpyAsync(h_scalar + 2, pos + n, sizeof(int), hipMemcpyDeviceToHost, s));
+        k_compact<<<cdiv(n, 256), 256, 0, s>>>(cand, f, pos, n, out, kept_index_out, und + kBatch - 1, coff + n, und + kBatch);
+        AOS_HIP(hipMemcpyAsync(h_scalar, und + kBatch, 3 * sizeof(int), hipMemcpyDeviceToHost, s));
         AOS_HIP(hipStreamSynchronize(s));
         S.n_conf = h_scalar[1];
         if ((long long)S.n_conf > cap) {   // conflict lists were truncated: rebuild at the exact size

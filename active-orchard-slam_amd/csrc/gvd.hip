@@ -404,6 +404,19 @@ __global__ void k_node_labels(const double2 *nodes, int Mn, const double2 *lp, c
     if (!off) { mask[i] = m; cidx[i] = ci; count[i] = cnt; }
 }
 
+// ------------------------------------------------------------------ output gather
+// The GvdGraph arrays (4-byte words) packed back to back into one device buffer, so the host receives them
+// with one DMA instead of one copy per array.
+constexpr int kMaxSegs = 12;
+struct SegList { const int *src[kMaxSegs]; long long off[kMaxSegs + 1]; int n; };
+__global__ void k_gather_words(SegList L, int *dst) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= L.off[L.n]) return;
+    int k = 0;
+    while (i >= L.off[k + 1]) ++k;
+    dst[i] = L.src[k][i - L.off[k]];
+}
+
 // ------------------------------------------------------------------ g4 facets (calcVoronoi + getVoronoiFacetList)
 // The Subdiv2D inserts are replayed on the host; the facets they imply are built here from the raw
 // quad-edge arrays (8 ints per quad-edge: next[4], pt[4]). calcVoronoi (subdivision2d.cpp) walks
@@ -433,8 +446,9 @@ __device__ bool d_voronoi_point(float2 o0, float2 d0, float2 o1, float2 d1, floa
 }
 
 // face[2*q + side]: side 0 = left face of q*4 (pt[3]), side 1 = right face (pt[1])
-__global__ void k_vor_faces(const int *qe, int n_rec, const float2 *vp, float2 *face) {
+__global__ void k_vor_faces(const int *qe, int n_rec, const float2 *vp, float2 *face, int *err) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) *err = 0;   // (k_facet_count's flag, launched after this kernel)
     if (i >= 2 * n_rec) return;
     const int q = i >> 1, side = i & 1;
     float2 res = make_float2(0.f, 0.f);
@@ -464,6 +478,7 @@ __device__ __forceinline__ float2 dual_face(const float2 *face, int t) { return 
 
 __global__ void k_facet_count(const int *qe, const int *vfirst, const int *vtype, int nv, int *cnt, int *err) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k == 0) cnt[nv] = 0;   // the scan's tail slot
     if (k >= nv) return;
     int c = 0;
     if (k >= 4 && vtype[k] == 0) {
@@ -497,7 +512,8 @@ __global__ void k_facet_emit(const int *qe, const int *vfirst, const int *off, c
 struct GvdScratch {
     DevBuf raw, ok, leaders, merged, owner, oidx, sowner, sidx, tmp, edges_f, occ, occ_ok, bp, kept_occ, keys, idx, skeys,
         sidx2, near_idx, pk, pidx, pskeys, psidx, pcount, poff, plist, ft, ckey, cvalid, pass, k2, occ_idx, sk2, socc, selected,
-        inside, ipos, nodes, keep, kpos, edges, lens, jobs, lpts, lval, lmask, lcidx, lcount, loff, lcl, lty, scan_tmp;
+        inside, ipos, nodes, keep, kpos, edges, lens, jobs, lpts, lval, lmask, lcidx, lcount, loff, lcl, lty, scan_tmp,
+        gather;
     FacetBufs fb;
 };
 static GvdScratch &scratch(GvdState &G) {
@@ -521,36 +537,33 @@ static void scan_excl(DevBuf &tmpb, const int *in, int *out, int n, hipStream_t 
 // scans them into edge offsets. Returns the edge total (F.cnt / F.off stay on the device); h_sc =
 // 2 pinned ints. The caller launches k_facet_emit into a buffer of that many float4.
 static int facets_count(FacetBufs &F, const Subdiv2D::Raw &R, int *h_sc, hipStream_t s) {
-    int *d_qe = dev<int>(F.qe, 8 * (size_t)R.n_rec);
-    float2 *d_vp = dev<float2>(F.vp, R.n_vtx);
-    int *d_vf = dev<int>(F.vfirst, R.n_vtx), *d_vt = dev<int>(F.vtype, R.n_vtx);
     // the quad-edge export (~5 MB at C2) goes through the builder's own pinned buffer (a pageable copy
-    // is staged by the runtime through its own buffers and blocks the calling thread)
+    // is staged by the runtime through its own buffers and blocks the calling thread), as one copy
     const size_t bq = sizeof(int) * 8 * (size_t)R.n_rec, bv = sizeof(float2) * R.n_vtx, bi = sizeof(int) * R.n_vtx;
     char *hs = static_cast<char *>(F.h_stage.ensure(bq + bv + 2 * bi));
     std::memcpy(hs, R.qe, bq);
     std::memcpy(hs + bq, R.vp, bv);
     std::memcpy(hs + bq + bv, R.vfirst, bi);
     std::memcpy(hs + bq + bv + bi, R.vtype, bi);
-    AOS_HIP(hipMemcpyAsync(d_qe, hs, bq, hipMemcpyHostToDevice, s));
-    AOS_HIP(hipMemcpyAsync(d_vp, hs + bq, bv, hipMemcpyHostToDevice, s));
-    AOS_HIP(hipMemcpyAsync(d_vf, hs + bq + bv, bi, hipMemcpyHostToDevice, s));
-    AOS_HIP(hipMemcpyAsync(d_vt, hs + bq + bv + bi, bi, hipMemcpyHostToDevice, s));
+    char *d = static_cast<char *>(F.raw.ensure(bq + bv + 2 * bi));
+    AOS_HIP(hipMemcpyAsync(d, hs, bq + bv + 2 * bi, hipMemcpyHostToDevice, s));
+    F.qe = reinterpret_cast<int *>(d);
+    const float2 *d_vp = reinterpret_cast<const float2 *>(d + bq);
+    F.vf = reinterpret_cast<int *>(d + bq + bv);
+    F.vt = reinterpret_cast<int *>(d + bq + bv + bi);
     float2 *d_face = dev<float2>(F.face, 2 * (size_t)R.n_rec);
-    int *d_cnt = dev<int>(F.cnt, R.n_vtx + 2), *d_off = dev<int>(F.off, R.n_vtx + 1);
-    AOS_HIP(hipMemsetAsync(d_cnt + R.n_vtx, 0, 2 * sizeof(int), s));
-    k_vor_faces<<<cdiv(2 * R.n_rec, 256), 256, 0, s>>>(d_qe, R.n_rec, d_vp, d_face);
-    k_facet_count<<<cdiv(R.n_vtx, 256), 256, 0, s>>>(d_qe, d_vf, d_vt, R.n_vtx, d_cnt, d_cnt + R.n_vtx + 1);
+    int *d_cnt = dev<int>(F.cnt, R.n_vtx + 1), *d_off = dev<int>(F.off, R.n_vtx + 2);   // off[n_vtx + 1]: walk error
+    k_vor_faces<<<cdiv(2 * R.n_rec, 256), 256, 0, s>>>(F.qe, R.n_rec, d_vp, d_face, d_off + R.n_vtx + 1);
+    k_facet_count<<<cdiv(R.n_vtx, 256), 256, 0, s>>>(F.qe, F.vf, F.vt, R.n_vtx, d_cnt, d_off + R.n_vtx + 1);
     scan_excl(F.scan_tmp, d_cnt, d_off, R.n_vtx + 1, s);
-    AOS_HIP(hipMemcpyAsync(h_sc, d_off + R.n_vtx, sizeof(int), hipMemcpyDeviceToHost, s));
-    AOS_HIP(hipMemcpyAsync(h_sc + 1, d_cnt + R.n_vtx + 1, sizeof(int), hipMemcpyDeviceToHost, s));
+    AOS_HIP(hipMemcpyAsync(h_sc, d_off + R.n_vtx, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
     AOS_HIP(hipStreamSynchronize(s));
     if (h_sc[1]) throw std::runtime_error("Subdiv2D facet walk did not close");
     return h_sc[0];
 }
 static void facets_emit(FacetBufs &F, const Subdiv2D::Raw &R, float4 *edges, hipStream_t s) {
-    k_facet_emit<<<cdiv(R.n_vtx, 256), 256, 0, s>>>(F.qe.as<int>(), F.vfirst.as<int>(), F.off.as<int>(), F.cnt.as<int>(),
-                                                   R.n_vtx, F.face.as<float2>(), edges);
+    k_facet_emit<<<cdiv(R.n_vtx, 256), 256, 0, s>>>(F.qe, F.vf, F.off.as<int>(), F.cnt.as<int>(), R.n_vtx,
+                                                   F.face.as<float2>(), edges);
 }
 
 // publishMarkers' Voronoi cells (gvd:1098-1194): VoronoiDiagram::extractCellBoundaries
@@ -727,13 +740,30 @@ void markers_wait(GvdState &G, bool rethrow) {
     }
 }
 
+// AOS_TRACE=1: host timeline of each GVD call on stderr (ms since the call started, at each host sync)
+struct HostTrace {
+    const bool on = getenv("AOS_TRACE") != nullptr;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    std::string line;
+    void mark(const char *what) {
+        if (!on) return;
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        char b[64];
+        snprintf(b, sizeof(b), " %s %.2f", what, ms);
+        line += b;
+    }
+    ~HostTrace() { if (on) fprintf(stderr, "[aos trace gvd]%s\n", line.c_str()); }
+};
+
 bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipStream_t s, hipEvent_t *ev) {
+    HostTrace tr;
     GvdScratch &S = scratch(G);
     G.nodes_xy.clear(); G.labels.clear(); G.cluster_idx.clear(); G.label_counts.clear();
     G.label_clusters.clear(); G.label_types.clear(); G.edges_out.clear(); G.lengths.clear(); G.clearances.clear();
     G.n_merged = G.n_vor_edges = G.n_bpts = 0;
     G.ms_merge = G.ms_delaunay = G.ms_graph = G.ms_total = 0;
     markers_wait(G, false);
+    tr.mark("markers_wait");
     G.have_markers = false;
     G.graph_ok = false;
     G.rect_mode = P.subdiv_rect_mode;
@@ -785,6 +815,7 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     std::vector<double> merged(2 * (size_t)nl);
     AOS_HIP(hipMemcpyAsync(h_seeds, d_merged, sizeof(double2) * nl, hipMemcpyDeviceToHost, s));
     AOS_HIP(hipStreamSynchronize(s));
+    tr.mark("merge");
     std::memcpy(merged.data(), h_seeds, sizeof(double2) * (size_t)nl);
     G.n_merged = nl;
     AOS_HIP(hipEventRecord(ev[7], s));
@@ -822,8 +853,10 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
                 y = std::max(ry + margin, std::min(ry + rh - margin, y));
                 sd.insert(x, y);
             }
+            tr.mark("inserts");
             const Subdiv2D::Raw R = sd.raw();
             ne = facets_count(S.fb, R, h_sc, s);
+            tr.mark("facets");
             d_ef = dev<float>(S.edges_f, 4 * (size_t)std::max(ne, 1));
             if (ne) facets_emit(S.fb, R, reinterpret_cast<float4 *>(d_ef), s);
         }
@@ -849,6 +882,7 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     const double thr5 = 0.05 * 0.05;
     const int M = greedy_dedup(G.dedup, d_occ, d_occ_ok, no, kConflictKeyOrSq, thr5, h5, d_bp, d_kept_occ, s, h_sc);
     G.n_bpts = M;
+    tr.mark("bpts");
 
     // ---- g6 graph edges
     int *d_keys = dev<int>(S.keys, M), *d_idx = dev<int>(S.idx, M), *d_skeys = dev<int>(S.skeys, M), *d_sidx = dev<int>(S.sidx2, M);
@@ -877,6 +911,7 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     AOS_HIP(hipMemcpyAsync(h_sc, d_poff + M, sizeof(int), hipMemcpyDeviceToHost, s));
     AOS_HIP(hipStreamSynchronize(s));
     const int np_ = h_sc[0];
+    tr.mark("pairs");
     int *d_plist = dev<int>(S.plist, np_);
     k_pairs<<<cdiv(M, 256), 256, 0, s>>>(d_bp, M, hp, d_psk, d_psi, d_poff, nullptr, d_plist);
     const int nc = ne + np_;
@@ -911,6 +946,7 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     AOS_HIP(hipMemcpyAsync(h_sc + 1, d_kpos + nc, sizeof(int), hipMemcpyDeviceToHost, s));
     AOS_HIP(hipStreamSynchronize(s));
     const int Mn = h_sc[0], Ne = h_sc[1];
+    tr.mark("filter");
     double2 *d_nodes = dev<double2>(S.nodes, Mn);
     k_gather_nodes<<<cdiv(M, 256), 256, 0, s>>>(d_bp, d_in, d_ipos, M, d_nodes);
     int *d_edges = dev<int>(S.edges, 2 * (size_t)Ne);
@@ -954,34 +990,40 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
         AOS_HIP(hipStreamSynchronize(s));
         n_entries = h_sc[0];
     }
+    tr.mark("labels");
     int *d_lcl = dev<int>(S.lcl, n_entries), *d_lty = dev<int>(S.lty, n_entries);
     if (n_entries) k_node_labels<<<cdiv(Mn, 256), 256, 0, s>>>(d_nodes, Mn, d_lp, d_lv, nlr, nullptr, nullptr, nullptr, d_loff, d_lcl, d_lty);
 
-    // ---- outputs
+    // ---- outputs: one gather kernel, one D2H copy into the state's pinned buffer, host copies out
     G.nodes_xy.resize(2 * (size_t)Mn); G.labels.resize(Mn); G.cluster_idx.resize(Mn); G.label_counts.resize(Mn);
     G.label_clusters.resize(n_entries); G.label_types.resize(n_entries);
     G.edges_out.resize(2 * (size_t)Ne); G.lengths.resize(Ne); G.clearances.assign(Ne, 0.0f);
-    if (Mn) {
-        AOS_HIP(hipMemcpyAsync(G.nodes_xy.data(), d_nodes, sizeof(double2) * Mn, hipMemcpyDeviceToHost, s));
-        AOS_HIP(hipMemcpyAsync(G.labels.data(), d_mask, sizeof(int) * Mn, hipMemcpyDeviceToHost, s));
-        AOS_HIP(hipMemcpyAsync(G.cluster_idx.data(), d_cidx, sizeof(int) * Mn, hipMemcpyDeviceToHost, s));
-        AOS_HIP(hipMemcpyAsync(G.label_counts.data(), d_lcnt, sizeof(int) * Mn, hipMemcpyDeviceToHost, s));
-    }
-    if (n_entries) {
-        AOS_HIP(hipMemcpyAsync(G.label_clusters.data(), d_lcl, sizeof(int) * n_entries, hipMemcpyDeviceToHost, s));
-        AOS_HIP(hipMemcpyAsync(G.label_types.data(), d_lty, sizeof(int) * n_entries, hipMemcpyDeviceToHost, s));
-    }
-    if (Ne) {
-        AOS_HIP(hipMemcpyAsync(G.edges_out.data(), d_edges, sizeof(int) * 2 * Ne, hipMemcpyDeviceToHost, s));
-        AOS_HIP(hipMemcpyAsync(G.lengths.data(), d_lens, sizeof(float) * Ne, hipMemcpyDeviceToHost, s));
-    }
     G.row_label_xy.resize(2 * (size_t)nj); G.row_label_valid.resize(nj);
-    if (nj) {
-        AOS_HIP(hipMemcpyAsync(G.row_label_xy.data(), d_lp, sizeof(double2) * nj, hipMemcpyDeviceToHost, s));
-        AOS_HIP(hipMemcpyAsync(G.row_label_valid.data(), d_lv, sizeof(int) * nj, hipMemcpyDeviceToHost, s));
+    struct Out { const void *d; void *h; long long words; };
+    const Out outs[] = {{d_nodes, G.nodes_xy.data(), 4LL * Mn}, {d_mask, G.labels.data(), Mn}, {d_cidx, G.cluster_idx.data(), Mn},
+                        {d_lcnt, G.label_counts.data(), Mn}, {d_lcl, G.label_clusters.data(), n_entries},
+                        {d_lty, G.label_types.data(), n_entries}, {d_edges, G.edges_out.data(), 2LL * Ne},
+                        {d_lens, G.lengths.data(), Ne}, {d_lp, G.row_label_xy.data(), 4LL * nj},
+                        {d_lv, G.row_label_valid.data(), nj}};
+    SegList sl{};
+    for (const Out &o : outs) {
+        if (o.words <= 0) continue;
+        sl.src[sl.n] = static_cast<const int *>(o.d);
+        sl.off[sl.n + 1] = sl.off[sl.n] + o.words;
+        ++sl.n;
+    }
+    const long long total = sl.off[sl.n];
+    int *h_out = static_cast<int *>(G.h_out.ensure(sizeof(int) * (size_t)std::max(total, 1LL)));
+    if (total) {
+        int *d_g = dev<int>(S.gather, (size_t)total);
+        k_gather_words<<<cdiv(total, 256), 256, 0, s>>>(sl, d_g);
+        AOS_HIP(hipMemcpyAsync(h_out, d_g, sizeof(int) * (size_t)total, hipMemcpyDeviceToHost, s));
     }
     AOS_HIP(hipEventRecord(ev[9], s));
     AOS_HIP(hipStreamSynchronize(s));
+    tr.mark("out");
+    for (const Out &o : outs)
+        if (o.words > 0) { std::memcpy(o.h, h_out, sizeof(int) * (size_t)o.words); h_out += o.words; }
     G.have_markers = P.gvd_markers != 0;
     G.graph_ok = true;
     float a = 0, b = 0;

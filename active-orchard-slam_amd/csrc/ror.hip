@@ -43,13 +43,17 @@ __constant__ float c_excl_rt[11 * 3] = {0.646417f, 3.83918f, 1.0f,  2.0405f, 3.6
                                         68.0229f, 2.31687f, 1.0f,  65.4647f, 2.18653f, 1.0f};
 
 
-// STD: the common PointCloud2 layout (point_step 16, x/y/z at 0/4/8): one 16 B load per point
-template <bool STD>
+// Record layout LAY: 1 = the common PointCloud2 layout (point_step 16, x/y/z at 0/4/8): one 16 B load per
+// point; 2 = the packed float3 cloud the host upload writes (step 12); 0 = any float32 x/y/z offsets
+template <int LAY>
 __device__ __forceinline__ void rt_load(const RorLaunch &L, uint64_t i, float &x, float &y, float &z) {
-    const uint8_t *rec = L.cloud + i * (uint64_t)(STD ? 16 : L.step);
-    if (STD) {
+    const uint8_t *rec = L.cloud + i * (uint64_t)(LAY == 1 ? 16 : LAY == 2 ? 12 : L.step);
+    if (LAY == 1) {
         const float4 v = *reinterpret_cast<const float4 *>(rec);
         x = v.x; y = v.y; z = v.z;
+    } else if (LAY == 2) {
+        const float *r = reinterpret_cast<const float *>(rec);
+        x = r[0]; y = r[1]; z = r[2];
     } else {
         x = *reinterpret_cast<const float *>(rec + L.ox);
         y = *reinterpret_cast<const float *>(rec + L.oy);
@@ -124,12 +128,20 @@ __device__ __forceinline__ void rt_tiles(const RorLaunch &L, int bx, int by, int
     ty0 = max(by - 1, 0) >> L.TBs; ty1 = min(by + 1, L.nby - 1) >> L.TBs;
 }
 
-template <bool SCATTER, bool STD, int kRtTB, int kRtPer>
+// XCD-aware block order (cdna_hip_programming.md §5.5): consecutive blocks b = j (mod 8) run on XCD j.
+__device__ __forceinline__ int rt_xcd_block(int b, int n) {
+    const int q = n >> 3, r = n & 7, j = b & 7, k = b >> 3;
+    return j * q + min(j, r) + k;
+}
+
+template <bool SCATTER, int LAY, int kRtTB, int kRtPer>
 __global__ __launch_bounds__(kRtTB) void k_rt_part(RorLaunch L, int *H, const int *tstart, uint64_t chunk,
                                                    float4 *staged, unsigned long long *n_own) {
     constexpr int kRtSub = kRtTB * kRtPer;
     extern __shared__ int hist[];        // [ntiles]: counts (count pass) / cursors (scatter pass)
-    const int tid = threadIdx.x, w = blockIdx.x;
+    // chunk w: the chunks of one XCD are contiguous, so the scatter runs of chunks w and w + 1 (adjacent in
+    // every tile's range) are written through the same L2 and their shared lines merge there
+    const int tid = threadIdx.x, w = rt_xcd_block(blockIdx.x, gridDim.x);
     int *row = H + (size_t)w * L.ntiles;
     for (int t = tid; t < L.ntiles; t += kRtTB) hist[t] = SCATTER ? tstart[t] + row[t] : 0;
     __syncthreads();
@@ -143,7 +155,7 @@ __global__ __launch_bounds__(kRtTB) void k_rt_part(RorLaunch L, int *H, const in
 #pragma unroll
         for (int j = 0; j < kRtPer; ++j) {
             const uint64_t i = base + (uint64_t)j * kRtTB + tid;
-            rt_load<STD>(L, i < end ? i : end - 1, nxt[j].x, nxt[j].y, nxt[j].z);
+            rt_load<LAY>(L, i < end ? i : end - 1, nxt[j].x, nxt[j].y, nxt[j].z);
             nxt[j].w = __int_as_float(i < end ? 0 : -1);
         }
     };
@@ -237,12 +249,10 @@ constexpr int kRorThreads = AOS_RT_THREADS, kRorCap = 2048, kRorPer = kRorCap / 
 #ifndef AOS_RT_VARIANT   // timing experiments only (tools/ab_rt.sh): 1 = no neighbour scan, 2 = no raster
 #define AOS_RT_VARIANT 0
 #endif
+#ifndef AOS_RT_BALANCE   // 1: load-balanced neighbour counts in k_rt_ror<false> (see there)
+#define AOS_RT_BALANCE 1
+#endif
 
-// XCD-aware block order (cdna_hip_programming.md §5.5): consecutive blocks b = j (mod 8) run on XCD j.
-__device__ __forceinline__ int rt_xcd_block(int b, int n) {
-    const int q = n >> 3, r = n & 7, j = b & 7, k = b >> 3;
-    return j * q + min(j, r) + k;
-}
 
 template <class Pts>
 __device__ __forceinline__ int rt_scan(const RorLaunch &L, float4 p, Pts pts, int k0, int k1, int cnt) {
@@ -393,6 +403,7 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
     __shared__ int bstart[kRtMaxLocalBins + 1];
     __shared__ unsigned long long win[kRtWinWords];
     __shared__ unsigned kept_wg;
+    __shared__ int q_next;                              // the balanced scan's candidate queue (AOS_RT_BALANCE)
     const int tid = threadIdx.x;
     const int nbig = BIG ? B.list[0] : 1;
     for (int it = BIG ? blockIdx.y : 0; it < nbig; it += BIG ? gridDim.y : 1) {
@@ -401,7 +412,11 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
     if (!BIG && dirty && dirty[t + 1] == dirty[t]) return;
     const int a = tstart[t], n = tstart[t + 1] - a;   // the tile's runs
     if (!BIG) {
-        if (n > kRorCap && a + n <= L.staged_cap) return;   // a big tile: k_rt_ror<true>
+        if (n > kRorCap && a + n <= L.staged_cap) {   // a big tile: k_rt_ror<true>
+            // (not launched this frame: the frame is redone with the big-tile kernels, seedgen.hip)
+            if (!L.big_ok && tid == 0) atomicOr(L.overflow, 2);
+            return;
+        }
         if (n == 0 || a + n > L.staged_cap) {               // (an overflowed scatter: the frame is redone)
             if (kept_tile && tid == 0) kept_tile[t] = 0;
             return;
@@ -412,7 +427,7 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
         int a_;
         big_chunk(L, tstart, t, a_, k0, k1);
     }
-    if (tid == 0) kept_wg = 0;
+    if (tid == 0) { kept_wg = 0; q_next = 0; }
     const int LB = L.TB + 2;                        // local bins: the tile's bins and a ring of halo bins
     const int bx0 = tx * L.TB - 1, by0 = ty * L.TB - 1;
     const int nlb = LB * LB;
@@ -476,30 +491,13 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
     // w: 0 a neighbour only, 1 a candidate, 2 a candidate a streaming map already found kept (the keep
     // decision is monotone as points are added: it stays kept, its cell is already in the raster)
     const bool store = kept_tile != nullptr;
-    for (int k = k0 + tid; k < k1; k += kRorThreads) {
-        const float4 p = BIG ? P[k] : pts[k];
-        const int w = __float_as_int(p.w);
-        if (!w) continue;                       // neighbour only
-        if (w == 2) {                           // kept in an earlier frame: counted, not re-tested
-            const int gx = (int)(((double)p.x - L.origin_x) / (double)L.res);
-            const int gy = (int)(((double)p.y - L.origin_y) / (double)L.res);
-            const int cx = min(max(gx, 0), L.W - 1), cy = min(max(gy, 0), L.H - 1);
-            if (cx >= L.rx0 && cx < L.rx1 && cy >= L.ry0 && cy < L.ry1) ++kept_n;
-            continue;
-        }
-        int bx, by;
-        rt_bin(L, p.x, p.y, bx, by);
-        const int lx = bx - bx0, ly = by - by0;
-        int cnt = AOS_RT_VARIANT == 1 ? L.need : 0;
-#pragma unroll
-        for (int rr = 0; rr < 3; ++rr) {        // own bin row first: the likeliest neighbours
-            const int yy = ly + (rr == 0 ? 0 : (rr == 1 ? -1 : 1));
-            if (cnt >= L.need) break;
-            const int r0 = yy * LB + lx - 1;
-            cnt = BIG ? rt_scan(L, p, P, bstart[r0], bstart[r0 + 3], cnt)
-                      : rt_scan(L, p, pts, bstart[r0], bstart[r0 + 3], cnt);
-        }
-        if (cnt < L.need) continue;
+    auto prev_kept = [&](float4 p) {   // kept in an earlier frame: counted, not re-tested
+        const int gx = (int)(((double)p.x - L.origin_x) / (double)L.res);
+        const int gy = (int)(((double)p.y - L.origin_y) / (double)L.res);
+        const int cx = min(max(gx, 0), L.W - 1), cy = min(max(gy, 0), L.H - 1);
+        if (cx >= L.rx0 && cx < L.rx1 && cy >= L.ry0 && cy < L.ry1) ++kept_n;
+    };
+    auto on_kept = [&](float4 p, int k) {
         if (store) {   // remembered in the tile store (written back below)
             if (BIG) P[k].w = __int_as_float(2);   // (neighbour scans of other threads read only x, y, z)
             else pts[k].w = __int_as_float(2);
@@ -508,9 +506,9 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
         const int gx = (int)(((double)p.x - L.origin_x) / (double)L.res);
         const int gy = (int)(((double)p.y - L.origin_y) / (double)L.res);
         const int cx = min(max(gx, 0), L.W - 1), cy = min(max(gy, 0), L.H - 1);
-        if (cx < L.rx0 || cx >= L.rx1 || cy < L.ry0 || cy >= L.ry1) continue;
+        if (cx < L.rx0 || cx >= L.rx1 || cy < L.ry0 || cy >= L.ry1) return;
         ++kept_n;
-        if (AOS_RT_VARIANT == 2 || gx < 0 || gx >= L.W || gy < 0 || gy >= L.H) continue;
+        if (AOS_RT_VARIANT == 2 || gx < 0 || gx >= L.W || gy < 0 || gy >= L.H) return;
         const int bxw = gx - L.wx0, r = gy - L.wy0;
         const int wr = r - (cy0 - L.wy0), ww = (bxw >> 6) - cw0;
         const unsigned long long bit = 1ull << (bxw & 63);
@@ -518,9 +516,93 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
             atomicOr(&win[wr * L.win_w + ww], bit);
         else
             atomicOr(reinterpret_cast<unsigned long long *>(&rbits[(size_t)r * L.WWr + (bxw >> 6)]), bit);
+    };
+    if (BIG || !AOS_RT_BALANCE) {
+        for (int k = k0 + tid; k < k1; k += kRorThreads) {
+            const float4 p = BIG ? P[k] : pts[k];
+            const int w = __float_as_int(p.w);
+            if (!w) continue;                       // neighbour only
+            if (w == 2) { prev_kept(p); continue; }
+            int bx, by;
+            rt_bin(L, p.x, p.y, bx, by);
+            const int lx = bx - bx0, ly = by - by0;
+            int cnt = AOS_RT_VARIANT == 1 ? L.need : 0;
+#pragma unroll
+            for (int rr = 0; rr < 3; ++rr) {        // own bin row first: the likeliest neighbours
+                const int yy = ly + (rr == 0 ? 0 : (rr == 1 ? -1 : 1));
+                if (cnt >= L.need) break;
+                const int r0 = yy * LB + lx - 1;
+                cnt = BIG ? rt_scan(L, p, P, bstart[r0], bstart[r0 + 3], cnt)
+                          : rt_scan(L, p, pts, bstart[r0], bstart[r0 + 3], cnt);
+            }
+            if (cnt >= L.need) on_kept(p, k);
+        }
+    } else {
+        // Load-balanced neighbour counts: a candidate's scan ends early once `need` neighbours are found,
+        // so per-candidate work varies a lot and a wave that takes one candidate per lane waits for its
+        // slowest lane. Here every lane steps its own candidate 4 points at a time (own bin row, then the
+        // rows above and below) and, when it is done, takes the next one from the block's queue.
+        const int lane = tid & 63;
+        const unsigned long long below = (1ull << lane) - 1;
+        int k = -1, rr = 0, pos = 0, end = 0, cnt = 0, lx = 0, ly = 0;
+        bool done = false;
+        float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (;;) {
+            for (;;) {   // refill the idle lanes (wave-uniform loop)
+                const bool idle = k < 0 && !done;
+                const unsigned long long im = __ballot(idle);
+                if (!im) break;
+                const int first = __ffsll((long long)im) - 1;
+                int base = 0;
+                if (lane == first) base = atomicAdd(&q_next, (int)__popcll(im));
+                base = __shfl(base, first);
+                if (idle) {
+                    const int kk = k0 + base + (int)__popcll(im & below);
+                    if (kk >= k1) {
+                        done = true;
+                    } else {
+                        const float4 q = pts[kk];
+                        const int w = __float_as_int(q.w);
+                        if (w == 2) prev_kept(q);
+                        else if (w == 1) {
+                            int bx, by;
+                            rt_bin(L, q.x, q.y, bx, by);
+                            lx = bx - bx0; ly = by - by0;
+                            p = q; k = kk; rr = 0;
+                            cnt = AOS_RT_VARIANT == 1 ? L.need : 0;
+                            const int r0 = ly * LB + lx - 1;
+                            pos = bstart[r0]; end = bstart[r0 + 3];
+                        }
+                    }
+                }
+            }
+            if (!__ballot(k >= 0)) break;   // every lane done
+            if (k >= 0) {
+                if (cnt < L.need && pos < end) {
+                    float4 q[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) q[j] = pts[min(pos + j, end - 1)];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) cnt += (pos + j < end && rt_in(L, p, q[j])) ? 1 : 0;
+                    pos += 4;
+                }
+                if (cnt >= L.need) {
+                    on_kept(p, k);
+                    k = -1;
+                } else if (pos >= end) {
+                    if (++rr == 3) {
+                        k = -1;   // fewer than `need` points within r: removed
+                    } else {
+                        const int r0 = (ly + (rr == 1 ? -1 : 1)) * LB + lx - 1;
+                        pos = bstart[r0]; end = bstart[r0 + 3];
+                    }
+                }
+            }
+        }
+        if (store) __syncthreads();   // (a point's kept mark may come from another thread)
     }
     // the store goes back bin-sorted with its kept marks: a fitting tile rewrites its list, a big tile's
-    // chunk its range of the sorted scratch list (each k by the thread that marked it)
+    // chunk its range of the sorted scratch list
     if (store)
         for (int k = k0 + tid; k < k1; k += kRorThreads) staged[a + k] = BIG ? P[k] : pts[k];
     __syncthreads();
@@ -629,26 +711,32 @@ uint64_t rt_chunk(const RorLaunch &L, int G) {
     return (c + kRtChunkQ - 1) / kRtChunkQ * kRtChunkQ;
 }
 
-template <bool SCATTER, bool STD>
+template <bool SCATTER, int LAY>
 static void rt_part(const RorLaunch &L, int *H, const int *tstart, int G, float4 *staged, unsigned long long *n_own,
                     hipStream_t s) {
     constexpr int TB = SCATTER ? kRtScatterTB : kRtCountTB, PER = SCATTER ? kRtScatterPer : kRtCountPer;
     static_assert(kRtChunkQ % (TB * PER) == 0 || (TB * PER) % kRtChunkQ == 0, "chunk granularity");
     const size_t lds = sizeof(int) * (size_t)L.ntiles;
     if (lds > 64 * 1024)   // the tile histogram exceeds the default dynamic-LDS limit (gfx950: 160 KB)
-        AOS_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rt_part<SCATTER, STD, TB, PER>),
+        AOS_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rt_part<SCATTER, LAY, TB, PER>),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    k_rt_part<SCATTER, STD, TB, PER><<<G, TB, lds, s>>>(L, H, tstart, rt_chunk(L, G), staged, n_own);
+    k_rt_part<SCATTER, LAY, TB, PER><<<G, TB, lds, s>>>(L, H, tstart, rt_chunk(L, G), staged, n_own);
     AOS_HIP(hipGetLastError());
 }
-static bool rt_std(const RorLaunch &L) { return L.step == 16 && L.ox == 0 && L.oy == 4 && L.oz == 8; }
+static int rt_layout(const RorLaunch &L) {
+    if (L.ox == 0 && L.oy == 4 && L.oz == 8) return L.step == 16 ? 1 : (L.step == 12 ? 2 : 0);
+    return 0;
+}
 
 size_t rt_colpart_ints(const RorLaunch &L, int G) { return (size_t)L.ntiles * ((G + kColRows - 1) / kColRows); }
 
 void launch_rt_count(const RorLaunch &L, int *H, int G, int *part, int *tot, unsigned long long *n_own, hipStream_t s) {
     if (!L.n) return;
-    if (rt_std(L)) rt_part<false, true>(L, H, nullptr, G, nullptr, n_own, s);
-    else rt_part<false, false>(L, H, nullptr, G, nullptr, n_own, s);
+    switch (rt_layout(L)) {
+        case 1: rt_part<false, 1>(L, H, nullptr, G, nullptr, n_own, s); break;
+        case 2: rt_part<false, 2>(L, H, nullptr, G, nullptr, n_own, s); break;
+        default: rt_part<false, 0>(L, H, nullptr, G, nullptr, n_own, s);
+    }
     const int ng = (G + kColRows - 1) / kColRows;
     const dim3 grid((L.ntiles + kColTB - 1) / kColTB, ng);
     k_rt_colsum<<<grid, kColTB, 0, s>>>(H, part, L.ntiles, G);
@@ -659,8 +747,11 @@ void launch_rt_count(const RorLaunch &L, int *H, int G, int *part, int *tot, uns
 
 void launch_rt_scatter(const RorLaunch &L, int *H, const int *tstart, int G, float4 *staged, hipStream_t s) {
     if (!L.n) return;
-    if (rt_std(L)) rt_part<true, true>(L, H, tstart, G, staged, nullptr, s);
-    else rt_part<true, false>(L, H, tstart, G, staged, nullptr, s);
+    switch (rt_layout(L)) {
+        case 1: rt_part<true, 1>(L, H, tstart, G, staged, nullptr, s); break;
+        case 2: rt_part<true, 2>(L, H, tstart, G, staged, nullptr, s); break;
+        default: rt_part<true, 0>(L, H, tstart, G, staged, nullptr, s);
+    }
 }
 
 size_t rt_bigbins_ints(const RorLaunch &L) { return 2 * (size_t)L.ntiles * ((L.TB + 2) * (L.TB + 2) + 1) + 1 + L.ntiles; }
@@ -669,14 +760,17 @@ void launch_rt_ror(const RorLaunch &L, const int *tstart, float4 *staged, float4
                    uint64_t *rbits, unsigned long long *counters, int *kept_tile, const int *dirty, hipStream_t s) {
     if (!L.ntiles) return;
     const BigBufs B = big_bufs(L, bigbins);
-    AOS_HIP(hipMemsetAsync(B.list, 0, sizeof(int), s));
-    k_rt_biglist<<<(L.ntiles + 255) / 256, 256, 0, s>>>(L, tstart, B, kept_tile, dirty);
     const dim3 gb(kBigC, kBigY);
-    k_rt_bighist<<<gb, kBigTB, 0, s>>>(L, tstart, staged, B);
-    k_rt_bigscan<<<kBigY, 1024, 0, s>>>(L, tstart, B);
-    k_rt_bigscatter<<<gb, kBigTB, 0, s>>>(L, tstart, staged, scratch, B);
+    if (L.big_ok) {   // tiles beyond the LDS capacity: listed, chunked, sorted and counted by the big kernels
+        AOS_HIP(hipMemsetAsync(B.list, 0, sizeof(int), s));
+        k_rt_biglist<<<(L.ntiles + 255) / 256, 256, 0, s>>>(L, tstart, B, kept_tile, dirty);
+        k_rt_bighist<<<gb, kBigTB, 0, s>>>(L, tstart, staged, B);
+        k_rt_bigscan<<<kBigY, 1024, 0, s>>>(L, tstart, B);
+        k_rt_bigscatter<<<gb, kBigTB, 0, s>>>(L, tstart, staged, scratch, B);
+    }
     k_rt_ror<false><<<L.ntiles, kRorThreads, 0, s>>>(L, tstart, staged, scratch, rbits, counters, kept_tile, dirty, B);
-    k_rt_ror<true><<<gb, kRorThreads, 0, s>>>(L, tstart, staged, scratch, rbits, counters, kept_tile, dirty, B);
+    if (L.big_ok)
+        k_rt_ror<true><<<gb, kRorThreads, 0, s>>>(L, tstart, staged, scratch, rbits, counters, kept_tile, dirty, B);
     AOS_HIP(hipGetLastError());
 }
 

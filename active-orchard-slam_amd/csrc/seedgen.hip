@@ -3,6 +3,7 @@
 // every per-point / per-cell stage runs on the GPU. The tiled multi-GPU frame (tiled.hip) reuses
 // ror_stage and finish_frame.
 #include <algorithm>
+#include <chrono>
 #include <climits>
 #include <cmath>
 #include <cstdio>
@@ -50,41 +51,51 @@ void aos_ctx::release() {
     }
 }
 
-// A pageable hipMemcpyAsync of the 160 MB C2 cloud runs at ~20 GB/s: the runtime stages it through
-// pinned memory on one thread. Here kUpThreads threads stage disjoint ranges in 8 MB chunks and DMA
-// them on their own streams; the handle's stream waits for all of them. The caller's buffer is only
-// read during the call (every memcpy has finished when this returns).
-void aos_ctx::upload_h2d(void *dst, const void *src, size_t bytes, bool prefetch) {
-    constexpr size_t kChunk = 8u << 20;
-    if (bytes < 4 * kChunk) {
-        if (prefetch) throw std::logic_error("upload_h2d: prefetch of a small buffer");
-        AOS_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream));
-        return;
-    }
+// Host PointCloud2 -> HBM. A pageable hipMemcpyAsync of the 160 MB C2 cloud runs at ~20 GB/s: the runtime
+// stages it through pinned memory on one thread. Here kUpThreads threads each take a range of points,
+// gather their x, y, z floats (12 of the record's point_step bytes: the only fields the path reads) into
+// double-buffered pinned slots of ~8 MB and DMA them on their own streams, so 25 % fewer bytes cross PCIe
+// for the common 16-byte record and the device gets a packed float3 cloud (step 12). The handle's stream
+// waits for all of them. The caller's buffer is only read during the call.
+void aos_ctx::upload_pack(void *dst, const aos_cloud_view &v, bool prefetch) {
+    constexpr uint64_t kChunkPts = (8u << 20) / 12;
+    const uint64_t n = v.n_points;
     for (int t = 0; t < kUpThreads; ++t)
         if (!up.st[t]) {
             AOS_HIP(hipStreamCreateWithFlags(&up.st[t], hipStreamNonBlocking));
             for (int k = 0; k < 2; ++k) AOS_HIP(hipEventCreateWithFlags(&up.ev[t][k], hipEventDisableTiming));
             AOS_HIP(hipEventCreateWithFlags(&up.done[t], hipEventDisableTiming));
-            for (int k = 0; k < 2; ++k) up.slot[t][k].ensure(kChunk);
+            for (int k = 0; k < 2; ++k) up.slot[t][k].ensure(12 * kChunkPts);
         }
     // the handle's stream may still read dst (the previous frame): the copies start after it (a prefetch
     // writes the spare buffer, which no queued work reads)
     if (!prefetch) AOS_HIP(hipEventRecord(ev[15], stream));
-    const size_t per = ((bytes + kUpThreads - 1) / kUpThreads + 4095) & ~(size_t)4095;   // covers all bytes
+    const uint64_t per = (n + kUpThreads - 1) / kUpThreads;
+    const uint8_t *src = static_cast<const uint8_t *>(v.data);
+    const bool std16 = v.point_step == 16 && v.off_x == 0 && v.off_y == 4 && v.off_z == 8;
     std::exception_ptr err[kUpThreads];
     auto work = [&](int t) {
         try {
             AOS_HIP(hipSetDevice(device));
             if (!prefetch) AOS_HIP(hipStreamWaitEvent(up.st[t], ev[15], 0));
-            const size_t b0 = std::min(bytes, per * t), b1 = std::min(bytes, per * (t + 1));
+            const uint64_t p0 = std::min(n, per * t), p1 = std::min(n, per * (t + 1));
             int k = 0;
-            for (size_t off = b0; off < b1; off += kChunk, k ^= 1) {
-                const size_t len = std::min(kChunk, b1 - off);
+            for (uint64_t c = p0; c < p1; c += kChunkPts, k ^= 1) {
+                const uint64_t m = std::min(kChunkPts, p1 - c);
                 if (up.used[t][k]) AOS_HIP(hipEventSynchronize(up.ev[t][k]));   // its last DMA is done
-                std::memcpy(up.slot[t][k].p, static_cast<const char *>(src) + off, len);
-                AOS_HIP(hipMemcpyAsync(static_cast<char *>(dst) + off, up.slot[t][k].p, len, hipMemcpyHostToDevice,
-                                       up.st[t]));
+                float *o = static_cast<float *>(up.slot[t][k].p);
+                if (std16) {
+                    const float *r = reinterpret_cast<const float *>(src + 16 * c);
+                    for (uint64_t i = 0; i < m; ++i) { o[3 * i] = r[4 * i]; o[3 * i + 1] = r[4 * i + 1]; o[3 * i + 2] = r[4 * i + 2]; }
+                } else {
+                    for (uint64_t i = 0; i < m; ++i) {
+                        const uint8_t *rec = src + (c + i) * (uint64_t)v.point_step;
+                        std::memcpy(o + 3 * i, rec + v.off_x, 4);
+                        std::memcpy(o + 3 * i + 1, rec + v.off_y, 4);
+                        std::memcpy(o + 3 * i + 2, rec + v.off_z, 4);
+                    }
+                }
+                AOS_HIP(hipMemcpyAsync(static_cast<char *>(dst) + 12 * c, o, 12 * m, hipMemcpyHostToDevice, up.st[t]));
                 AOS_HIP(hipEventRecord(up.ev[t][k], up.st[t]));
                 up.used[t][k] = true;
             }
@@ -107,13 +118,14 @@ void aos_ctx::prefetch_start(const aos_cloud_view &v) {
     prefetch_join();
     const size_t bytes = (size_t)v.n_points * v.point_step;
     if (v.on_device || bytes < (32u << 20)) return;   // nothing to hide
-    void *dst = cloud_next.ensure(bytes);
+    void *dst = cloud_next.ensure(12 * (size_t)v.n_points);
+    pf.view = v;
     pf.src = v.data;
     pf.bytes = bytes;
     pf.err = nullptr;
     pf.active = true;
     pf.th = std::thread([this, dst]() {
-        try { upload_h2d(dst, pf.src, pf.bytes, true); } catch (...) { pf.err = std::current_exception(); }
+        try { upload_pack(dst, pf.view, true); } catch (...) { pf.err = std::current_exception(); }
     });
 }
 
@@ -163,13 +175,14 @@ void aos_ctx::set_cloud(const aos_cloud_view &v) {
             std::swap(cloud_copy.cap, cloud_next.cap);
             for (int t = 0; t < kUpThreads; ++t) AOS_HIP(hipStreamWaitEvent(stream, up.done[t], 0));
         } else {
-            void *dst = cloud_copy.ensure(std::max<size_t>(bytes, 16));
-            if (bytes) upload_h2d(dst, v.data, bytes);
+            void *dst = cloud_copy.ensure(std::max<size_t>(12 * (size_t)v.n_points, 16));
+            if (bytes) upload_pack(dst, v);
         }
         dc = cloud_copy.as<uint8_t>();
     }
     n_points = v.n_points;
-    step = v.point_step; ox = v.off_x; oy = v.off_y; oz = v.off_z;
+    if (v.on_device) { step = v.point_step; ox = v.off_x; oy = v.off_y; oz = v.off_z; }
+    else { step = 12; ox = 0; oy = 4; oz = 8; }   // packed by upload_pack
     is_dense = v.is_dense ? 1 : 0;
     d_cloud = dc;
     have_cloud = true;
@@ -347,8 +360,12 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
                  same_bins ? ms.L.TB : 0);
     auto geom_of = [](RorLaunch x) {
         x.cloud = nullptr; x.n = 0; x.step = x.ox = x.oy = x.oz = 0; x.staged_cap = 0; x.overflow = nullptr;
+        x.big_ok = 0;
         return x;
     };
+    // the big-tile kernels run once a frame of this handle has needed them, and on every frame that cannot
+    // be redone (a tiled rank, a redo); a frame that finds a big tile without them is redone (ror_collect)
+    L.big_ok = ror_big_seen || !allow_guess || o.limit_box;
     if (store_ok && ms.dense == is_dense && ms.n_points == map_scan_begin && n_points > ms.n_points) {
         const RorLaunch a = geom_of(L), b = ms.L;
         if (!std::memcmp(&a, &b, sizeof(RorLaunch))) { ror_stage_append(L, rbits); return; }
@@ -478,6 +495,7 @@ bool aos_ctx::ror_collect() {
     h[0] = (int)binned;
     ror_est_binned = binned;
     ror_staged_max = std::max<double>(ror_staged_max, (double)h[2]);
+    if (u[1] & 2) ror_big_seen = true;
     if (ms.pend.on && u[1] == 0) {   // commit the streaming map's tile store
         ms.valid = true;
         ms.L = ms.pend.L;
@@ -611,6 +629,9 @@ void aos_ctx::run_seedgen(bool want_host, aos_seedgen_out &out) {
 }
 
 bool aos_ctx::run_seedgen_once(bool want_host, aos_seedgen_out &out, bool allow_guess) {
+    const bool trace = getenv("AOS_TRACE") != nullptr;
+    const auto t_in = std::chrono::steady_clock::now();
+    auto since = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_in).count(); };
     std::memset(&out, 0, sizeof(out));
     tiled_frame = false;
     have_frame = false;
@@ -692,8 +713,12 @@ bool aos_ctx::run_seedgen_once(bool want_host, aos_seedgen_out &out, bool allow_
     thin_iters_prev = T;
     skel_bits = final_buf;
     AOS_HIP(hipEventRecord(ev[3], s));
+    const double t_thin = since();
     if (ror_collect()) return true;   // (the thinning read-back above synchronised the stream)
     finish_frame(g, want_host, nullptr, out);
+    if (trace)
+        fprintf(stderr, "[aos trace seedgen] thin-sync %.2f finish %.2f (T %d, launches %d, graph %d)\n", t_thin, since(),
+                T, launched, last_thin_graph);
     return false;
 }
 

@@ -54,6 +54,8 @@ def parse(argv=None):
                          "host-in / host-out frame")
     ap.add_argument("--no-device-rate", action="store_true", help="skip the extra device-resident loop")
     ap.add_argument("--no-pipelined-rate", action="store_true", help="skip the extra pipelined loop")
+    ap.add_argument("--no-tiled-rate", action="store_true",
+                    help="--gpus N > 1: skip the extra tiled C3 measurement (tiled key)")
     ap.add_argument("--trace", action="store_true", help="per-step timeline on stderr")
     ap.add_argument("--depth", type=int, default=8,
                     help="pipelined loop: GVD jobs in flight (aos_gvd_pipeline_depth): frames are independent, so "
@@ -187,8 +189,6 @@ def main():
     import torch  # (import before libaos_gpu: shared HIP runtime, see aos_gpu.lib)
     import torch.distributed as dist
 
-    import aos_gpu
-    import orchard
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -204,6 +204,60 @@ def main():
         else:
             dist.init_process_group(backend)
     red_dev = dev if backend == "nccl" else torch.device("cpu")
+    E = {"world": world, "rank": rank, "gpu": gpu, "dev": dev, "red_dev": red_dev, "backend": backend}
+    out = run(a, E, dist)
+    if world > 1 and not (a.tiled or a.stream or a.no_tiled_rate):
+        # the multi-GPU launch also measures the one-map design (BASELINE configs[3]): C3 split
+        # into tiling_for(N) tiles over the same ranks, halos and flags over the library's RCCL communicator
+        t = tiled_extra(a, E, dist, out)
+        if out is not None:
+            out["tiled"] = t
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def tiled_extra(a, E, dist, main_out) -> dict:
+    """One map (C3, 8192^2, 40 M points) in tiling_for(N) tiles over the N ranks, rotating roots with
+    background GVD jobs: Mcells/s, frame latency and the root's serial whole-map finish. Guarded by a
+    watchdog: if the collectives do not finish in time every rank reports the timeout and exits."""
+    import copy
+    import threading
+    b = copy.copy(a)
+    b.tiled, b.config, b.steps, b.warmup = True, "C3", max(4, min(a.steps, 12)), 3
+    b.no_cpu_baseline = True
+    limit = float(os.environ.get("AOS_BENCH_TILED_TIMEOUT", "300"))
+    res = {"main_out": main_out}
+
+    def watchdog():
+        res["error"] = f"tiled C3 section did not finish within {limit:.0f} s (collective hang?)"
+        if E["rank"] == 0 and res["main_out"] is not None:
+            res["main_out"]["tiled"] = {"error": res["error"]}
+            print(json.dumps(res["main_out"]), flush=True)
+        os._exit(0)   # every rank's own watchdog fires: none is left waiting in a collective
+    timer = threading.Timer(limit, watchdog)
+    timer.daemon = True
+    timer.start()
+    try:
+        o = run(b, E, dist, quiet=True)
+    except Exception as e:   # a failing communicator must not cost the main result
+        timer.cancel()
+        return {"error": f"{type(e).__name__}: {e}"}
+    timer.cancel()
+    if o is None:
+        return None
+    keep = ("value", "unit", "ms_per_step", "frame_latency_ms", "root_serial_ms", "config", "frame", "stages_ms")
+    return {k: o[k] for k in keep if k in o}
+
+
+def run(a, E, dist, quiet=False):
+    """One timed configuration; returns rank 0's result dict (None on other ranks)."""
+    import torch
+
+    import aos_gpu
+    import orchard
+    world, rank, gpu, dev, red_dev, backend = E["world"], E["rank"], E["gpu"], E["dev"], E["red_dev"], E["backend"]
 
     cfg = orchard.CONFIGS[a.config]
     _progress(f"generating {a.config}")
@@ -541,13 +595,20 @@ def main():
                              "note": "scan latency = scan H2D + pack + whole-map seed-gen + GVD graph (host clock); "
                                      "markers latency = until that scan's /gvd/markers cells are collected; "
                                      "keeps_up: graph latency and time per scan (markers included) within the budget"}
+        if a.tiled:
+            roots = [gs for gs, _ in res if gs.get("root")]
+            if roots:
+                out["root_serial_ms"] = round(sum(gs["ms"].get("cluster", 0.0) + gs["ms"].get("seeds", 0.0)
+                                                  for gs in roots) / len(roots), 3)
+            if frame_lat:
+                out["frame_latency_ms"] = {"p50": round(_median(frame_lat), 2), "max": round(frame_lat[-1], 2)}
         if world == 1 and not a.no_cpu_baseline and not a.stream:
             _progress(f"CPU baseline (oracle, 1 thread pinned) on {a.cpu_config}")
             out["cpu_baseline"] = cpu_baseline(a.cpu_config)
-        print(json.dumps(out), flush=True)
     ctx.close()
-    if world > 1:
-        dist.destroy_process_group()
+    if a.tiled and hasattr(comm, "close"):
+        comm.close()
+    return out if rank == 0 else None
 
 
 if __name__ == "__main__":

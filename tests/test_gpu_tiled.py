@@ -308,3 +308,39 @@ def test_rccl_comm_single_rank_frame():
     _assert_same(single, (g, [g], grids, gg))
     with pytest.raises(RuntimeError, match="rank"):
         T.RcclComm(plan["exchange_bytes"], device=0, rank=1, world=1, unique_id=bytes(128))
+
+
+def test_group_stream_4x2_equals_single_gpu_stream():
+    """BASELINE configs[4] over 8 tiles (tiling_for(8) = 4 x 2, ranks on one GPU): the C2 map, then 10
+    scans of 1 M points, into the group's tiled streaming map (aos_group_map_append: every rank keeps its
+    points box of each scan in its own map and incremental ROR store) with the root rotating over the
+    ranks; every frame equals the single-GPU aos_map_append frame (grids, T, counts, rows, seeds), the
+    GvdGraph every third frame, and the last frame the oracle's hashes after 5 scans where they apply."""
+    cfg = orchard.CONFIGS["C2"]
+    poly = orchard.polygon(cfg)
+    base = orchard.generate(cfg)
+    params = aos_gpu.default_params(grid_resolution=cfg.res)
+    single = aos_gpu.Ctx(params)
+    single.set_polygon(poly)
+    single.map_reset(reserve_points=base.shape[0] + 10 * orchard.SCAN_POINTS)
+    tx, ty = T.tiling_for(8)
+    grp = aos_gpu.Group(params, [0] * (tx * ty), tx, ty)
+    grp.set_polygon(poly)
+    grp.map_reset(reserve_points=base.shape[0] // 4)
+    for k in range(11):
+        cloud = base if k == 0 else orchard.generate_scan(cfg, 40 * (k - 1))
+        g1 = single.map_append(cloud)
+        root = (3 * k) % (tx * ty)
+        gt = grp.map_append(cloud, root=root)
+        assert_seedgen_parity(gt, {**g1, "cluster_length": np.zeros(g1["n_clusters_all"])})
+        assert (gt["n_clipped"], gt["n_input"], gt["thin_iters"]) == (g1["n_clipped"], g1["n_input"], g1["thin_iters"]), k
+        if k % 3 == 2 or k == 10:
+            gg1, ggt = single.gvd_from_seedgen(), grp.rank(root).gvd_from_seedgen()
+            for key in GVD_KEYS:
+                assert np.array_equal(gg1[key], ggt[key]), (k, key)
+    # changing the polygon changes the tiles' boxes: the tiled map refuses until it is reset
+    grp.set_polygon(poly + 1.0)
+    with pytest.raises(RuntimeError, match="points box changed"):
+        grp.map_append(orchard.generate_scan(cfg, 400))
+    grp.close()
+    single.close()

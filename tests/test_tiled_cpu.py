@@ -120,6 +120,51 @@ def test_torch_dist_comm_gloo_world2():
         assert v == [1, 5, 0]
 
 
+# ---------------------------------------------------------------- tiled streaming: scan routing
+def _route_worker(rank, world, port, q, tx, ty):
+    """One rank of a tiled streaming map: it receives every scan (broadcast, as every subscriber of
+    /global_map does) and keeps the points of its tile's points box (aos_tiled_map_append's rule,
+    grid_kernels.hip k_pack_xyz_box = aos_tiles.shard). Checks on the accumulated map: every point whose
+    clamped cell the rank owns, and every point within the ROR radius of it, is in the rank's map; the
+    owned counts all-reduced over the ranks cover every point once."""
+    from scipy.spatial import cKDTree
+    _init(rank, world, port)
+    cfg = orchard.CONFIGS["C1"]
+    poly = orchard.polygon(cfg)
+    params = aos_gpu.default_params(grid_resolution=cfg.res)
+    plan = T.tile_plan(params, poly, tx, ty, rank)
+    scans = [orchard.generate_scan(cfg, k, n_points=40_000) for k in (0, 1300, 2500)]   # across both tiles
+    whole = np.concatenate(scans)
+    mine = np.concatenate([T.shard(s, plan["points_box"]) for s in scans])   # the rank's map after 3 appends
+    pts = orchard.xyz(whole).astype(np.float64)
+    ox, oy = plan["origin"]
+    res = np.float64(np.float32(plan["resolution"]))
+    W, H = plan["width"], plan["height"]
+    cx = np.clip(np.trunc((pts[:, 0] - ox) / res), 0, W - 1).astype(np.int64)   # generateOccupancyGrid cell, clamped
+    cy = np.clip(np.trunc((pts[:, 1] - oy) / res), 0, H - 1).astype(np.int64)
+    # ROR candidates (PassThrough: inside the grid's clip box and z range) whose clamped cell is an own cell
+    cand = ((pts[:, 0] >= ox) & (pts[:, 0] <= ox + W * res) & (pts[:, 1] >= oy) & (pts[:, 1] <= oy + H * res) &
+            (pts[:, 2] >= params.clipping_minz) & (pts[:, 2] <= params.clipping_maxz))
+    own = cand & (cx >= 64 * plan["word0"]) & (cx < min(W, 64 * plan["word1"])) & (cy >= plan["row0"]) & (cy < plan["row1"])
+    in_map = {r.tobytes() for r in mine}
+    tree = cKDTree(pts[:, :2])
+    need = set(np.nonzero(own)[0].tolist())
+    for nb in tree.query_ball_point(pts[own, :2], r=params.ror_radius):   # (2-D: a superset of the 3-D ball)
+        need.update(nb)
+    missing = sum(1 for i in need if whole[i].tobytes() not in in_map)
+    cnt = torch.tensor([int(own.sum())], dtype=torch.int64)
+    dist.all_reduce(cnt)
+    q.put((rank, missing, len(need), mine.shape[0], int(cnt.item()), int(cand.sum()), whole.shape[0]))
+    dist.destroy_process_group()
+
+
+def test_tiled_stream_routing_gloo_world2():
+    for rank, missing, needed, kept, owned_total, n_cand, n in _spawn(_route_worker, 2, 2, 1):
+        assert missing == 0, (rank, missing, needed)
+        assert needed > 1000 and kept < n          # each rank keeps a part of the broadcast scans
+        assert owned_total == n_cand               # every candidate is owned by exactly one rank
+
+
 def test_thread_group_comm():
     world = 3
     g = T.ThreadGroup(world, timeout=30)

@@ -1,7 +1,7 @@
 // ROR-stage microbenchmark (a1-a4 only): the C2 synthetic cloud, the tile walk of ror.hip compiled in,
 // each pass timed with HIP events over several frames; prints the raster popcount and kept count so
 // variants (-DAOS_RT_VARIANT=..., tile / LDS constants) can be checked against each other.
-// Build: tools/rorbench/build.sh   Run: tools/rorbench/rorbench [grid_n] [n_points] [frames]
+// Build: tools/rorbench/build.sh   Run: tools/rorbench/rorbench [grid_n] [n_points] [frames] [step: 16 | 12]
 #include "../../active-orchard-slam_amd/csrc/ror.hip"
 
 #include <cstdio>
@@ -43,6 +43,7 @@ int main(int argc, char **argv) {
     const int grid_n = argc > 1 ? atoi(argv[1]) : 4096;
     const uint64_t n = argc > 2 ? strtoull(argv[2], 0, 10) : 10000000ull;
     const int frames = argc > 3 ? atoi(argv[3]) : 10;
+    const int pstep = argc > 4 ? atoi(argv[4]) : 16;   // 12: the packed float3 cloud of the host upload
     orchard_cfg c{3, n, grid_n, 0.1f, 0, 0.0, 0.01};
     const int64_t nt = orchard_num_trees(&c);
     std::vector<double> tx(nt), ty(nt);
@@ -60,12 +61,14 @@ int main(int argc, char **argv) {
     const float res = 0.1f;
     const int W = (int)std::ceil(std::max(0.f, maxx - minx) / res), H = (int)std::ceil(std::max(0.f, maxy - miny) / res);
     const int WW = (W + 63) / 64;
+    if (pstep == 12)
+        for (uint64_t i = 0; i < n; ++i) std::memmove(cloud.data() + 12 * i, cloud.data() + 16 * i, 12);
     uint8_t *d_cloud;
-    AOS_HIP(hipMalloc(&d_cloud, 16 * n));
-    AOS_HIP(hipMemcpy(d_cloud, cloud.data(), 16 * n, hipMemcpyHostToDevice));
+    AOS_HIP(hipMalloc(&d_cloud, (size_t)pstep * n));
+    AOS_HIP(hipMemcpy(d_cloud, cloud.data(), (size_t)pstep * n, hipMemcpyHostToDevice));
 
     RorLaunch L{};
-    L.cloud = d_cloud; L.n = n; L.step = 16; L.ox = 0; L.oy = 4; L.oz = 8; L.is_dense = 1;
+    L.cloud = d_cloud; L.n = n; L.step = pstep; L.ox = 0; L.oy = 4; L.oz = 8; L.is_dense = 1;
     L.cminx = minx; L.cmaxx = maxx; L.cminy = miny; L.cmaxy = maxy; L.cminz = -0.4f; L.cmaxz = 0.5f;
     const float m = (float)(0.2 * 1.01) + 1e-4f;
     L.bminx = L.cminx - m; L.bmaxx = L.cmaxx + m; L.bminy = L.cminy - m; L.bmaxy = L.cmaxy + m;
@@ -106,7 +109,8 @@ int main(int argc, char **argv) {
         AOS_HIP(hipMemsetAsync(d_cnt, 0, 8 * (kRorCounters + 2), s));
         AOS_HIP(hipMemsetAsync(d_bits, 0, 8ull * WW * H, s));
         AOS_HIP(hipEventRecord(e[0], s));
-        rt_part<false, true>(L, d_H, nullptr, G, nullptr, d_cnt + kRorCounters, s);   // (launch_rt_count, split)
+        if (pstep == 12) rt_part<false, 2>(L, d_H, nullptr, G, nullptr, d_cnt + kRorCounters, s);   // (launch_rt_count, split)
+        else rt_part<false, 1>(L, d_H, nullptr, G, nullptr, d_cnt + kRorCounters, s);
         AOS_HIP(hipEventRecord(e[6], s));
         {
             static int *d_part = nullptr;
