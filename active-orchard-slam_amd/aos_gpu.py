@@ -472,13 +472,16 @@ class Ctx:
         _check(lib().aos_gvd_wait(self.h, ctypes.byref(o)))
         return _gvd_dict(o)
 
-    def gvd_markers(self, collected: bool = False) -> dict:
+    def gvd_markers(self, collected: bool = False, copy: bool = True) -> dict:
         """/gvd/markers content of the last GVD call (aos_gvd_markers_get); collected=True: of the frame
-        last returned by gvd_wait, even with newer jobs in flight (aos_gvd_collected_markers_get)."""
+        last returned by gvd_wait, even with newer jobs in flight (aos_gvd_collected_markers_get).
+        copy=False (diagnostic): wait for the cells, return only their counts and time."""
         m = GvdMarkers()
         fn = lib().aos_gvd_collected_markers_get if collected else lib().aos_gvd_markers_get
         _check(fn(self.h, ctypes.byref(m)))
         nc = m.n_cells
+        if not copy:
+            return {"n_cells": nc, "n_seeds": m.n_seeds, "ms_cells": m.ms_cells}
         off = _arr(m.cell_offsets, nc + 1, np.int32)
         return {"seeds": _arr(m.seeds_xy, 2 * m.n_seeds, np.float64).reshape(-1, 2),
                 "row_label_pts": _arr(m.row_label_xy, 8 * m.n_rows, np.float64).reshape(-1, 4, 2),

@@ -122,6 +122,8 @@ struct aos_ctx {
 
     // ---- host-side outputs of the last frame
     aos::PinnedBuf h_occ, h_skel;   // the two OccupancyGrids (pinned: the D2H runs at DMA speed)
+    hipStream_t copy_stream = nullptr;   // their D2H, beside the cluster / seed stage
+    hipEvent_t copy_ready = nullptr;
     std::vector<double> h_row_center, h_row_start, h_row_end, h_row_length, h_voronoi, h_rows_info, h_cluster_info;
     int n_virtual = 0, n_ray = 0, n_endpoint = 0, n_clusters_all = 0, n_bfs_replayed = 0;
 
@@ -156,6 +158,7 @@ struct aos_ctx {
     };
     std::vector<std::unique_ptr<GvdLane>> lanes{};   // lanes[cur_lane] holds the current result
     int cur_lane = 0, gvd_depth = 1;
+    hipStream_t gvd_stream = nullptr;                // the lanes' shared GPU stream
     std::deque<int> inflight;                        // lanes with uncollected jobs, oldest first
     bool view_newest = false;                        // no aos_gvd_wait since the last job started
     aos::GvdState &gs() { return lanes[cur_lane]->gs; }

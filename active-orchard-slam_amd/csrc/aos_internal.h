@@ -37,6 +37,11 @@ struct DeviceScope {
 };
 
 // ------------------------------------------------------------------ device buffers
+// AOS_TRACE: growth of a buffer (a free + malloc, which may synchronise the device) is logged on stderr
+// with its host time, against the process-wide trace clock (trace_ms)
+double trace_ms();
+bool trace_on();
+void trace_alloc(const char *kind, size_t bytes, double t0);
 // Owning, growable device allocation (freed on destruction; not copyable).
 struct DevBuf {
     void *p = nullptr;
@@ -47,11 +52,13 @@ struct DevBuf {
     ~DevBuf() { release(); }
     void *ensure(size_t bytes) {
         if (bytes <= cap) return p;
+        const double t0 = trace_on() ? trace_ms() : 0.0;
         if (p) AOS_HIP(hipFree(p));
         p = nullptr;
         size_t c = bytes + bytes / 8 + 256;
         AOS_HIP(hipMalloc(&p, c));
         cap = c;
+        if (trace_on()) trace_alloc("device", c, t0);
         return p;
     }
     template <class T> T *as() const { return static_cast<T *>(p); }
@@ -67,11 +74,13 @@ struct PinnedBuf {
     ~PinnedBuf() { release(); }
     void *ensure(size_t bytes) {
         if (bytes <= cap) return p;
+        const double t0 = trace_on() ? trace_ms() : 0.0;
         if (p) AOS_HIP(hipHostFree(p));
         p = nullptr;
         size_t c = bytes + bytes / 8 + 256;
         AOS_HIP(hipHostMalloc(&p, c, hipHostMallocDefault));
         cap = c;
+        if (trace_on()) trace_alloc("pinned", c, t0);
         return p;
     }
     template <class T> T *as() const { return static_cast<T *>(p); }

@@ -1,7 +1,9 @@
 // libaos_gpu.so — C ABI + per-handle orchestration of the seed-gen / GVD hot path on MI355X.
 // One handle = one device + one HIP stream; all stage buffers stay resident in HBM.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <new>
 
@@ -11,6 +13,16 @@ namespace aos {
 
 thread_local std::string g_err;
 void set_error(const std::string &msg) { g_err = msg; }
+
+static const auto g_epoch = std::chrono::steady_clock::now();
+double trace_ms() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - g_epoch).count(); }
+bool trace_on() {
+    static const bool on = getenv("AOS_TRACE") != nullptr;
+    return on;
+}
+void trace_alloc(const char *kind, size_t bytes, double t0) {
+    fprintf(stderr, "[aos trace alloc] %s %.1f MB at %.2f ms took %.2f ms\n", kind, bytes / 1e6, t0, trace_ms() - t0);
+}
 
 }  // namespace aos
 

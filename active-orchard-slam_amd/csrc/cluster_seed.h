@@ -34,7 +34,22 @@ enum ConflictMode {
 };
 struct HashG { double x0, y0, inv; int nx, ny; };
 HashG make_hash(double minx, double maxx, double miny, double maxy, double cell);
-struct DedupScratch { DevBuf keys, idx, skeys, sidx, ccount, coff, clist, state, f, pos, tmp, und, rows; int n_conf = 0; };
+// Waits for the work queued so far on a stream through an event of the caller's own: a GVD lane's host
+// thread waits for its own work only, not for other lanes' work queued on the shared GVD stream.
+struct SyncEvent {
+    hipEvent_t e = nullptr;
+    SyncEvent() = default;
+    SyncEvent(const SyncEvent &) = delete;
+    SyncEvent &operator=(const SyncEvent &) = delete;
+    ~SyncEvent() { if (e) (void)hipEventDestroy(e); }
+    void sync(hipStream_t s) {
+        if (!e) AOS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        AOS_HIP(hipEventRecord(e, s));
+        AOS_HIP(hipEventSynchronize(e));
+    }
+};
+
+struct DedupScratch { DevBuf keys, idx, skeys, sidx, ccount, coff, clist, state, f, pos, tmp, und, rows; int n_conf = 0; SyncEvent sev; };
 // cand/ok device arrays of n entries; kept points (in order) -> out; optional kept flags -> state (S.state).
 // Returns the kept count.
 int greedy_dedup(DedupScratch &S, const double2 *cand, const int *ok, int n, int mode, double thr, const HashG &h,
@@ -122,6 +137,7 @@ struct GvdState {
     void *scratch = nullptr;   // GvdScratch (gvd.hip), freed by free_gvd_scratch
     PinnedBuf h_seeds;   // seeds in / merged seeds out (g1)
     PinnedBuf h_out;     // the GvdGraph arrays, gathered on the device and copied back in one DMA
+    SyncEvent sev;       // host waits of this state's GVD calls (the stream may be shared by several lanes)
     Subdiv2D subdiv;   // host insert replay; kept across frames to reuse its allocations
     // host outputs
     std::vector<double> nodes_xy;

@@ -611,7 +611,7 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
     void *tmp = S.scan_tmp.ensure(tb);
     AOS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, d_wc, d_wo, (int)Cw + 1, s));
     AOS_HIP(hipMemcpyAsync(h_sc, d_wo + Cw, sizeof(int), hipMemcpyDeviceToHost, s));
-    AOS_HIP(hipStreamSynchronize(s));
+    S.dedup.sev.sync(s);
     const int nf = h_sc[0];
     S.n_fg = nf;
     out = SeedStageOut();
@@ -631,7 +631,7 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         tmp = S.scan_tmp.ensure(std::max(tb, tb2));
         AOS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, d_isroot, d_rank, nf + 1, s));
         AOS_HIP(hipMemcpyAsync(h_sc, d_rank + nf, sizeof(int), hipMemcpyDeviceToHost, s));
-        AOS_HIP(hipStreamSynchronize(s));
+        S.dedup.sev.sync(s);
         const int ncl = h_sc[0];
         S.n_clusters = ncl;
         // bucket the foreground cells by cluster id: stable radix sort (keeps raster order inside a
@@ -652,7 +652,7 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         k_cluster_stats<<<ncl, 256, 0, s>>>(A);
         S.h_rec.resize(ncl);
         AOS_HIP(hipMemcpyAsync(S.h_rec.data(), d_rec, sizeof(ClusterRec) * ncl, hipMemcpyDeviceToHost, s));
-        AOS_HIP(hipStreamSynchronize(s));
+        S.dedup.sev.sync(s);
         int n_bfs = 0;
         for (const auto &r : S.h_rec) n_bfs += (r.flags & 2) != 0;
         out.n_bfs = n_bfs;
@@ -668,7 +668,7 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
             const long long lo = off[ids.front()], hi = off[ids.back() + 1];
             std::vector<int> hc((size_t)(hi - lo));
             AOS_HIP(hipMemcpyAsync(hc.data(), d_cells + lo, sizeof(int) * (hi - lo), hipMemcpyDeviceToHost, s));
-            AOS_HIP(hipStreamSynchronize(s));
+            S.dedup.sev.sync(s);
             const float min_len = static_cast<float>(in.cluster_min_length);
             std::atomic<int> next{0};
             std::exception_ptr err;
@@ -764,7 +764,7 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         S.n_cur_tab = (int)t.size();
         double *d = dev<double>(S.cur_tab, t.size());
         AOS_HIP(hipMemcpyAsync(d, t.data(), sizeof(double) * t.size(), hipMemcpyHostToDevice, s));
-        AOS_HIP(hipStreamSynchronize(s));
+        S.dedup.sev.sync(s);
         S.cur_tab_amax = g.amax;
     }
     k_endpoint_rays<<<6 * nr, 64, 0, s>>>(d_rows, nr, in.skel_bits, g, ang, d_poly, np,
@@ -775,7 +775,7 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
     const int ntot = n_virtual + n_ray + n_end;
     std::vector<double> all(2 * (size_t)ntot);
     if (ntot) AOS_HIP(hipMemcpyAsync(all.data(), d_seeds, sizeof(double2) * ntot, hipMemcpyDeviceToHost, s));
-    AOS_HIP(hipStreamSynchronize(s));
+    S.dedup.sev.sync(s);
     out.virtual_xy.assign(all.begin(), all.begin() + 2 * n_virtual);
     out.ray_xy.assign(all.begin() + 2 * n_virtual, all.begin() + 2 * (n_virtual + n_ray));
     out.endpoint_xy.assign(all.begin() + 2 * (n_virtual + n_ray), all.end());

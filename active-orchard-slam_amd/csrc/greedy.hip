@@ -193,7 +193,7 @@ int greedy_dedup(DedupScratch &S, const double2 *cand, const int *ok, int n, int
         AOS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, f, pos, n + 1, s));
         k_compact<<<cdiv(n, 256), 256, 0, s>>>(cand, f, pos, n, out, kept_index_out, und + kBatch - 1, coff + n, und + kBatch);
         AOS_HIP(hipMemcpyAsync(h_scalar, und + kBatch, 3 * sizeof(int), hipMemcpyDeviceToHost, s));
-        AOS_HIP(hipStreamSynchronize(s));
+        S.sev.sync(s);
         S.n_conf = h_scalar[1];
         if ((long long)S.n_conf > cap) {   // conflict lists were truncated: rebuild at the exact size
             cap = S.n_conf;

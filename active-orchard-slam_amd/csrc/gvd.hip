@@ -536,7 +536,7 @@ static void scan_excl(DevBuf &tmpb, const int *in, int *out, int n, hipStream_t 
 // circumcentre (k_vor_faces) and the per-vertex facet sizes (k_facet_count, 0 below 2 points), and
 // scans them into edge offsets. Returns the edge total (F.cnt / F.off stay on the device); h_sc =
 // 2 pinned ints. The caller launches k_facet_emit into a buffer of that many float4.
-static int facets_count(FacetBufs &F, const Subdiv2D::Raw &R, int *h_sc, hipStream_t s) {
+static int facets_count(FacetBufs &F, const Subdiv2D::Raw &R, int *h_sc, hipStream_t s, SyncEvent &sev) {
     // the quad-edge export (~5 MB at C2) goes through the builder's own pinned buffer (a pageable copy
     // is staged by the runtime through its own buffers and blocks the calling thread), as one copy
     const size_t bq = sizeof(int) * 8 * (size_t)R.n_rec, bv = sizeof(float2) * R.n_vtx, bi = sizeof(int) * R.n_vtx;
@@ -557,7 +557,7 @@ static int facets_count(FacetBufs &F, const Subdiv2D::Raw &R, int *h_sc, hipStre
     k_facet_count<<<cdiv(R.n_vtx, 256), 256, 0, s>>>(F.qe, F.vf, F.vt, R.n_vtx, d_cnt, d_off + R.n_vtx + 1);
     scan_excl(F.scan_tmp, d_cnt, d_off, R.n_vtx + 1, s);
     AOS_HIP(hipMemcpyAsync(h_sc, d_off + R.n_vtx, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
-    AOS_HIP(hipStreamSynchronize(s));
+    sev.sync(s);
     if (h_sc[1]) throw std::runtime_error("Subdiv2D facet walk did not close");
     return h_sc[0];
 }
@@ -579,6 +579,10 @@ static bool markers_gpu_facets() {   // AOS_MARKERS_GPU_FACETS=1: the markers' f
 
 static void compute_cells(CellsWork &W, int rect_mode) {
     const auto t0 = std::chrono::steady_clock::now();
+    struct CellTrace {
+        const double t = trace_on() ? trace_ms() : 0.0;
+        ~CellTrace() { if (trace_on()) fprintf(stderr, "[aos trace cells] %.2f -> %.2f\n", t, trace_ms()); }
+    } ctr;
     W.cell_off.assign(1, 0);
     W.cell_xy.clear(); W.cell_center.clear(); W.cell_rgba.clear();
     const std::vector<double> &seeds = W.seeds;   // VoronoiDiagram::seeds_ = the finite merged seeds
@@ -634,7 +638,8 @@ static void compute_cells(CellsWork &W, int rect_mode) {
     AOS_HIP(hipSetDevice(W.device));
     if (!W.stream) AOS_HIP(hipStreamCreateWithFlags(&W.stream, hipStreamNonBlocking));
     int *h_sc = static_cast<int *>(W.h.ensure(4096));
-    const int ne = facets_count(W.fb, R, h_sc, W.stream);
+    SyncEvent sev;
+    const int ne = facets_count(W.fb, R, h_sc, W.stream, sev);
     const size_t need = sizeof(float4) * (size_t)std::max(ne, 1) + sizeof(int) * (size_t)R.n_vtx;
     float4 *d_e = dev<float4>(W.edges, std::max(ne, 1));
     if (ne) facets_emit(W.fb, R, d_e, W.stream);
@@ -742,17 +747,16 @@ void markers_wait(GvdState &G, bool rethrow) {
 
 // AOS_TRACE=1: host timeline of each GVD call on stderr (ms since the call started, at each host sync)
 struct HostTrace {
-    const bool on = getenv("AOS_TRACE") != nullptr;
-    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    const bool on = trace_on();
+    const double t0 = on ? trace_ms() : 0.0;
     std::string line;
     void mark(const char *what) {
         if (!on) return;
-        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         char b[64];
-        snprintf(b, sizeof(b), " %s %.2f", what, ms);
+        snprintf(b, sizeof(b), " %s %.2f", what, trace_ms() - t0);
         line += b;
     }
-    ~HostTrace() { if (on) fprintf(stderr, "[aos trace gvd]%s\n", line.c_str()); }
+    ~HostTrace() { if (on) fprintf(stderr, "[aos trace gvd] at %.2f:%s\n", t0, line.c_str()); }
 };
 
 bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipStream_t s, hipEvent_t *ev) {
@@ -794,12 +798,14 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     double *h_seeds = static_cast<double *>(G.h_seeds.ensure(sizeof(double2) * (size_t)n));
     std::memcpy(h_seeds, in.seeds_host, sizeof(double2) * (size_t)n);
     AOS_HIP(hipMemcpyAsync(d_raw, h_seeds, sizeof(double2) * n, hipMemcpyHostToDevice, s));
+    tr.mark("h2d");
     int *d_ok = dev<int>(S.ok, n);
     k_fill_ones<<<cdiv(n, 256), 256, 0, s>>>(d_ok, n);
     const HashG hm = make_hash(g.minx - 60.0, g.maxx + 60.0, g.miny - 60.0, g.maxy + 60.0, 0.5);
     double2 *d_lead_pts = dev<double2>(S.merged, n);
     int *d_leaders = dev<int>(S.leaders, n);
     const int nl = greedy_dedup(G.dedup, d_raw, d_ok, n, kConflictLessEq, 0.5, hm, d_lead_pts, d_leaders, s, h_sc);
+    tr.mark("dedup");
     int *d_owner = dev<int>(S.owner, n), *d_oidx = dev<int>(S.oidx, n), *d_sowner = dev<int>(S.sowner, n),
         *d_sj = dev<int>(S.sidx, n);
     k_merge_owner<<<cdiv(n, 256), 256, 0, s>>>(G.dedup.state.as<int>(), G.dedup.coff.as<int>(), G.dedup.clist.as<int>(), n,
@@ -814,7 +820,7 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     k_merge_sum<<<cdiv(nl, 128), 128, 0, s>>>(d_raw, d_sowner, d_sj, n, d_leaders, nl, d_merged);
     std::vector<double> merged(2 * (size_t)nl);
     AOS_HIP(hipMemcpyAsync(h_seeds, d_merged, sizeof(double2) * nl, hipMemcpyDeviceToHost, s));
-    AOS_HIP(hipStreamSynchronize(s));
+    G.sev.sync(s);
     tr.mark("merge");
     std::memcpy(merged.data(), h_seeds, sizeof(double2) * (size_t)nl);
     G.n_merged = nl;
@@ -855,7 +861,7 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
             }
             tr.mark("inserts");
             const Subdiv2D::Raw R = sd.raw();
-            ne = facets_count(S.fb, R, h_sc, s);
+            ne = facets_count(S.fb, R, h_sc, s, G.sev);
             tr.mark("facets");
             d_ef = dev<float>(S.edges_f, 4 * (size_t)std::max(ne, 1));
             if (ne) facets_emit(S.fb, R, reinterpret_cast<float4 *>(d_ef), s);
@@ -909,7 +915,7 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     k_pairs<<<cdiv(M, 256), 256, 0, s>>>(d_bp, M, hp, d_psk, d_psi, nullptr, d_pcount, nullptr);
     scan_excl(S.scan_tmp, d_pcount, d_poff, M + 1, s);
     AOS_HIP(hipMemcpyAsync(h_sc, d_poff + M, sizeof(int), hipMemcpyDeviceToHost, s));
-    AOS_HIP(hipStreamSynchronize(s));
+    G.sev.sync(s);
     const int np_ = h_sc[0];
     tr.mark("pairs");
     int *d_plist = dev<int>(S.plist, np_);
@@ -944,7 +950,7 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     scan_excl(S.scan_tmp, d_keep, d_kpos, nc + 1, s);
     AOS_HIP(hipMemcpyAsync(h_sc, d_ipos + M, sizeof(int), hipMemcpyDeviceToHost, s));
     AOS_HIP(hipMemcpyAsync(h_sc + 1, d_kpos + nc, sizeof(int), hipMemcpyDeviceToHost, s));
-    AOS_HIP(hipStreamSynchronize(s));
+    G.sev.sync(s);
     const int Mn = h_sc[0], Ne = h_sc[1];
     tr.mark("filter");
     double2 *d_nodes = dev<double2>(S.nodes, Mn);
@@ -987,7 +993,7 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
         k_node_labels<<<cdiv(Mn, 256), 256, 0, s>>>(d_nodes, Mn, d_lp, d_lv, nlr, d_mask, d_cidx, d_lcnt, nullptr, nullptr, nullptr);
         scan_excl(S.scan_tmp, d_lcnt, d_loff, Mn + 1, s);
         AOS_HIP(hipMemcpyAsync(h_sc, d_loff + Mn, sizeof(int), hipMemcpyDeviceToHost, s));
-        AOS_HIP(hipStreamSynchronize(s));
+        G.sev.sync(s);
         n_entries = h_sc[0];
     }
     tr.mark("labels");
@@ -1020,7 +1026,7 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
         AOS_HIP(hipMemcpyAsync(h_out, d_g, sizeof(int) * (size_t)total, hipMemcpyDeviceToHost, s));
     }
     AOS_HIP(hipEventRecord(ev[9], s));
-    AOS_HIP(hipStreamSynchronize(s));
+    G.sev.sync(s);
     tr.mark("out");
     for (const Out &o : outs)
         if (o.words > 0) { std::memcpy(o.h, h_out, sizeof(int) * (size_t)o.words); h_out += o.words; }
@@ -1125,8 +1131,11 @@ void aos_ctx::gvd_async_start() {
     if (L < 0) throw std::logic_error("gvd_async_start: no free lane");
     GvdLane &ln = *lanes[L];
     AsyncGvd &A = ln.ag;
+    if (!gvd_stream) AOS_HIP(hipStreamCreateWithFlags(&gvd_stream, hipStreamNonBlocking));
     if (!A.stream) {
-        AOS_HIP(hipStreamCreateWithFlags(&A.stream, hipStreamNonBlocking));
+        // every lane queues its GPU work on the handle's one GVD stream (few streams for the GPU's 4 hardware
+        // queues: no false dependencies behind unrelated streams); each lane waits on its own events
+        A.stream = gvd_stream;
         for (auto &e : A.ev) AOS_HIP(hipEventCreate(&e));
         AOS_HIP(hipEventCreateWithFlags(&A.ready, hipEventDisableTiming));
     }
@@ -1253,9 +1262,12 @@ void aos_ctx::gvd_async_stop() {
             (void)hipStreamSynchronize(A.stream);
             for (auto &e : A.ev) (void)hipEventDestroy(e);
             (void)hipEventDestroy(A.ready);
-            (void)hipStreamDestroy(A.stream);
-            A.stream = nullptr;
+            A.stream = nullptr;   // (the shared gvd_stream)
         }
+    }
+    if (gvd_stream) {
+        (void)hipStreamDestroy(gvd_stream);
+        gvd_stream = nullptr;
     }
     inflight.clear();
     view_newest = false;

@@ -249,9 +249,6 @@ constexpr int kRorThreads = AOS_RT_THREADS, kRorCap = 2048, kRorPer = kRorCap / 
 #ifndef AOS_RT_VARIANT   // timing experiments only (tools/ab_rt.sh): 1 = no neighbour scan, 2 = no raster
 #define AOS_RT_VARIANT 0
 #endif
-#ifndef AOS_RT_BALANCE   // 1: load-balanced neighbour counts in k_rt_ror<false> (see there)
-#define AOS_RT_BALANCE 1
-#endif
 
 
 template <class Pts>
@@ -403,7 +400,6 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
     __shared__ int bstart[kRtMaxLocalBins + 1];
     __shared__ unsigned long long win[kRtWinWords];
     __shared__ unsigned kept_wg;
-    __shared__ int q_next;                              // the balanced scan's candidate queue (AOS_RT_BALANCE)
     const int tid = threadIdx.x;
     const int nbig = BIG ? B.list[0] : 1;
     for (int it = BIG ? blockIdx.y : 0; it < nbig; it += BIG ? gridDim.y : 1) {
@@ -427,7 +423,7 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
         int a_;
         big_chunk(L, tstart, t, a_, k0, k1);
     }
-    if (tid == 0) { kept_wg = 0; q_next = 0; }
+    if (tid == 0) kept_wg = 0;
     const int LB = L.TB + 2;                        // local bins: the tile's bins and a ring of halo bins
     const int bx0 = tx * L.TB - 1, by0 = ty * L.TB - 1;
     const int nlb = LB * LB;
@@ -517,92 +513,27 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
         else
             atomicOr(reinterpret_cast<unsigned long long *>(&rbits[(size_t)r * L.WWr + (bxw >> 6)]), bit);
     };
-    if (BIG || !AOS_RT_BALANCE) {
-        for (int k = k0 + tid; k < k1; k += kRorThreads) {
-            const float4 p = BIG ? P[k] : pts[k];
-            const int w = __float_as_int(p.w);
-            if (!w) continue;                       // neighbour only
-            if (w == 2) { prev_kept(p); continue; }
-            int bx, by;
-            rt_bin(L, p.x, p.y, bx, by);
-            const int lx = bx - bx0, ly = by - by0;
-            int cnt = AOS_RT_VARIANT == 1 ? L.need : 0;
+    for (int k = k0 + tid; k < k1; k += kRorThreads) {
+        const float4 p = BIG ? P[k] : pts[k];
+        const int w = __float_as_int(p.w);
+        if (!w) continue;                       // neighbour only
+        if (w == 2) { prev_kept(p); continue; }
+        int bx, by;
+        rt_bin(L, p.x, p.y, bx, by);
+        const int lx = bx - bx0, ly = by - by0;
+        int cnt = AOS_RT_VARIANT == 1 ? L.need : 0;
 #pragma unroll
-            for (int rr = 0; rr < 3; ++rr) {        // own bin row first: the likeliest neighbours
-                const int yy = ly + (rr == 0 ? 0 : (rr == 1 ? -1 : 1));
-                if (cnt >= L.need) break;
-                const int r0 = yy * LB + lx - 1;
-                cnt = BIG ? rt_scan(L, p, P, bstart[r0], bstart[r0 + 3], cnt)
-                          : rt_scan(L, p, pts, bstart[r0], bstart[r0 + 3], cnt);
-            }
-            if (cnt >= L.need) on_kept(p, k);
+        for (int rr = 0; rr < 3; ++rr) {        // own bin row first: the likeliest neighbours
+            const int yy = ly + (rr == 0 ? 0 : (rr == 1 ? -1 : 1));
+            if (cnt >= L.need) break;
+            const int r0 = yy * LB + lx - 1;
+            cnt = BIG ? rt_scan(L, p, P, bstart[r0], bstart[r0 + 3], cnt)
+                      : rt_scan(L, p, pts, bstart[r0], bstart[r0 + 3], cnt);
         }
-    } else {
-        // Load-balanced neighbour counts: a candidate's scan ends early once `need` neighbours are found,
-        // so per-candidate work varies a lot and a wave that takes one candidate per lane waits for its
-        // slowest lane. Here every lane steps its own candidate 4 points at a time (own bin row, then the
-        // rows above and below) and, when it is done, takes the next one from the block's queue.
-        const int lane = tid & 63;
-        const unsigned long long below = (1ull << lane) - 1;
-        int k = -1, rr = 0, pos = 0, end = 0, cnt = 0, lx = 0, ly = 0;
-        bool done = false;
-        float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (;;) {
-            for (;;) {   // refill the idle lanes (wave-uniform loop)
-                const bool idle = k < 0 && !done;
-                const unsigned long long im = __ballot(idle);
-                if (!im) break;
-                const int first = __ffsll((long long)im) - 1;
-                int base = 0;
-                if (lane == first) base = atomicAdd(&q_next, (int)__popcll(im));
-                base = __shfl(base, first);
-                if (idle) {
-                    const int kk = k0 + base + (int)__popcll(im & below);
-                    if (kk >= k1) {
-                        done = true;
-                    } else {
-                        const float4 q = pts[kk];
-                        const int w = __float_as_int(q.w);
-                        if (w == 2) prev_kept(q);
-                        else if (w == 1) {
-                            int bx, by;
-                            rt_bin(L, q.x, q.y, bx, by);
-                            lx = bx - bx0; ly = by - by0;
-                            p = q; k = kk; rr = 0;
-                            cnt = AOS_RT_VARIANT == 1 ? L.need : 0;
-                            const int r0 = ly * LB + lx - 1;
-                            pos = bstart[r0]; end = bstart[r0 + 3];
-                        }
-                    }
-                }
-            }
-            if (!__ballot(k >= 0)) break;   // every lane done
-            if (k >= 0) {
-                if (cnt < L.need && pos < end) {
-                    float4 q[4];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) q[j] = pts[min(pos + j, end - 1)];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) cnt += (pos + j < end && rt_in(L, p, q[j])) ? 1 : 0;
-                    pos += 4;
-                }
-                if (cnt >= L.need) {
-                    on_kept(p, k);
-                    k = -1;
-                } else if (pos >= end) {
-                    if (++rr == 3) {
-                        k = -1;   // fewer than `need` points within r: removed
-                    } else {
-                        const int r0 = (ly + (rr == 1 ? -1 : 1)) * LB + lx - 1;
-                        pos = bstart[r0]; end = bstart[r0 + 3];
-                    }
-                }
-            }
-        }
-        if (store) __syncthreads();   // (a point's kept mark may come from another thread)
+        if (cnt >= L.need) on_kept(p, k);
     }
     // the store goes back bin-sorted with its kept marks: a fitting tile rewrites its list, a big tile's
-    // chunk its range of the sorted scratch list
+    // chunk its range of the sorted scratch list (each k by the thread that marked it)
     if (store)
         for (int k = k0 + tid; k < k1; k += kRorThreads) staged[a + k] = BIG ? P[k] : pts[k];
     __syncthreads();

@@ -22,6 +22,12 @@ void aos_ctx::release() {
                       &full_infl, &full_skel, &map_buf, &scan_stage})
         b->release();
     thin_graphs_release();
+    if (copy_stream) {
+        (void)hipStreamSynchronize(copy_stream);
+        (void)hipEventDestroy(copy_ready);
+        (void)hipStreamDestroy(copy_stream);
+        copy_stream = nullptr;
+    }
     h_small.release();
     h_stats.release();
     h_occ.release();
@@ -717,8 +723,8 @@ bool aos_ctx::run_seedgen_once(bool want_host, aos_seedgen_out &out, bool allow_
     if (ror_collect()) return true;   // (the thinning read-back above synchronised the stream)
     finish_frame(g, want_host, nullptr, out);
     if (trace)
-        fprintf(stderr, "[aos trace seedgen] thin-sync %.2f finish %.2f (T %d, launches %d, graph %d)\n", t_thin, since(),
-                T, launched, last_thin_graph);
+        fprintf(stderr, "[aos trace seedgen] at %.2f: thin-sync %.2f finish %.2f (T %d, launches %d, graph %d)\n",
+                trace_ms() - since(), t_thin, since(), T, launched, last_thin_graph);
     return false;
 }
 
@@ -752,6 +758,18 @@ void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *c
         w2g(static_cast<float>(hmaxx + margin), static_cast<float>(hmaxy + margin), gx1, gy1);
         launch_draw_rect(d_skel, g, gx0, gy0, gx1, gy1, s);
     }
+    // the two published grids go to host memory on the copy stream while the cluster / seed stage runs
+    if (want_host) {
+        h_occ.ensure(std::max<size_t>(C, 1)); h_skel.ensure(std::max<size_t>(C, 1));
+        if (!copy_stream) {
+            AOS_HIP(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
+            AOS_HIP(hipEventCreateWithFlags(&copy_ready, hipEventDisableTiming));
+        }
+        AOS_HIP(hipEventRecord(copy_ready, s));
+        AOS_HIP(hipStreamWaitEvent(copy_stream, copy_ready, 0));
+        AOS_HIP(hipMemcpyAsync(h_occ.p, d_occ, C, hipMemcpyDeviceToHost, copy_stream));
+        AOS_HIP(hipMemcpyAsync(h_skel.p, d_skel, C, hipMemcpyDeviceToHost, copy_stream));
+    }
 
     // ---------------- a8-a15 clusters, tree rows, seeds
     SeedStageIn sin{skel_bits, &geom, &poly, P.cluster_min_length};
@@ -761,12 +779,8 @@ void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *c
 
     unsigned long long *h_cnt = static_cast<unsigned long long *>(h_stats.ensure(64 + 8 * kRorCounters)) + 8;
     if (!clipped_total) AOS_HIP(hipMemcpyAsync(h_cnt, counters.p, 8 * kRorCounters, hipMemcpyDeviceToHost, s));
-    if (want_host) {
-        h_occ.ensure(std::max<size_t>(C, 1)); h_skel.ensure(std::max<size_t>(C, 1));
-        AOS_HIP(hipMemcpyAsync(h_occ.p, d_occ, C, hipMemcpyDeviceToHost, s));
-        AOS_HIP(hipMemcpyAsync(h_skel.p, d_skel, C, hipMemcpyDeviceToHost, s));
-    }
     AOS_HIP(hipStreamSynchronize(s));
+    if (want_host) AOS_HIP(hipStreamSynchronize(copy_stream));
     if (clipped_total) {
         n_clipped = *clipped_total;
     } else {

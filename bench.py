@@ -73,6 +73,8 @@ def parse(argv=None):
                     help="pipelined loop: upload each frame's PointCloud2 inside its own seed-gen call")
     ap.add_argument("--no-markers", action="store_true",
                     help="(diagnostic) no publishMarkers cells at all; not the reference's work")
+    ap.add_argument("--markers-no-copy", action="store_true",
+                    help="(diagnostic) wait for the markers' cells but do not copy them into Python arrays")
     ap.add_argument("--fixed-root", action="store_true",
                     help="--tiled: rank 0 finishes every frame (default: frame k's root is rank k mod N, so the "
                          "whole-map stages and the GVD jobs rotate over the ranks)")
@@ -185,6 +187,9 @@ def _progress(msg: str) -> None:
 
 def main():
     a = parse()
+    if os.environ.get("AOS_BENCH_NUMPY_HUGEPAGE") == "0":   # (diagnostic: numpy's madvise(MADV_HUGEPAGE) on >= 4 MB arrays)
+        import numpy as np
+        np._core.multiarray._set_madvise_hugepage(False)
     _progress("importing torch")
     import torch  # (import before libaos_gpu: shared HIP runtime, see aos_gpu.lib)
     import torch.distributed as dist
@@ -330,7 +335,7 @@ def run(a, E, dist, quiet=False):
         return mk
 
     def collect(collected=False):
-        m = ctx.gvd_markers(collected=collected)
+        m = ctx.gvd_markers(collected=collected, copy=not a.markers_no_copy)
         if pend["mt0"] is not None and a.stream:
             mk_latency.append(time.perf_counter() - pend["mt0"])
         pend["ms"] = m["ms_cells"]

@@ -68,3 +68,37 @@ def test_independent_tile_per_rank():
     a = orchard.generate(cfg, seed=cfg.seed + 0, n_points=5000)
     b = orchard.generate(cfg, seed=cfg.seed + 1, n_points=5000)
     assert a.shape == b.shape and not np.array_equal(a, b)
+
+
+def _hang_worker(q):
+    """bench.tiled_extra with a tiled run that never returns (a collective that hangs): its watchdog must
+    print rank 0's main result with the tiled error and end the process with status 0."""
+    import argparse
+    os.environ["AOS_BENCH_TILED_TIMEOUT"] = "1"
+    bench.run = lambda *a, **k: time.sleep(3600)
+    a = argparse.Namespace(steps=20, warmup=5, tiled=False, config="C2", no_cpu_baseline=False)
+    bench.tiled_extra(a, {"rank": 0}, None, {"value": 1.0})
+
+
+def test_tiled_extra_watchdog_and_error(capfd):
+    import subprocess
+    code = ("import sys; sys.path.insert(0, %r); sys.path.insert(0, %r); import test_bench_dist as t; "
+            "t._hang_worker(None)" % (ROOT, os.path.join(ROOT, "tests")))
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0
+    line = [x for x in p.stdout.splitlines() if x.startswith("{")][-1]
+    import json
+    d = json.loads(line)
+    assert d["value"] == 1.0 and "did not finish" in d["tiled"]["error"]
+    # a tiled run that raises is reported without losing the main result
+    import argparse
+    old = bench.run
+    try:
+        def boom(*a, **k):
+            raise RuntimeError("rccl init failed")
+        bench.run = boom
+        a = argparse.Namespace(steps=20, warmup=5, tiled=False, config="C2", no_cpu_baseline=False)
+        t = bench.tiled_extra(a, {"rank": 0}, None, {"value": 1.0})
+        assert t == {"error": "RuntimeError: rccl init failed"}
+    finally:
+        bench.run = old
