@@ -13,6 +13,14 @@ import subprocess
 
 import numpy as np
 
+# numpy madvise(MADV_HUGEPAGE)s every allocation >= 4 MB. Copying the /gvd/markers arrays out of
+# the library then stalls the next GPU synchronisation of the process by 10-30 ms (measured on the
+# MI355X box: profiles/r03d_stream*.json with the copies, r03f with this switch), most
+# likely the transparent-huge-page work on those pages invalidating the device's view of the address
+# space. The binding turns the madvise off for the process; AOS_NUMPY_HUGEPAGE=1 keeps numpy's default.
+if os.environ.get("AOS_NUMPY_HUGEPAGE") != "1" and hasattr(np._core.multiarray, "_set_madvise_hugepage"):
+    np._core.multiarray._set_madvise_hugepage(False)
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 # AOS_GPU_LIB: alternative build of the same library (A/B experiments, tools/)
@@ -222,6 +230,7 @@ def lib():
         L.aos_tiled_map_append.argtypes = [c_vp, P(Comm), c_i, c_i, c_i, P(CloudView), c_i, P(SeedGenOut)]
         L.aos_stream.restype = c_vp
         L.aos_stream.argtypes = [c_vp]
+        L.aos_cluster_union.argtypes = [c_i, c_i, c_i, c_vp, c_i, c_vp, c_vp, c_vp, P(c_i)]
         _lib = L
     return _lib
 
@@ -229,6 +238,21 @@ def lib():
 def _check(rc):
     if rc != 0:
         raise RuntimeError(f"libaos_gpu error {rc}: {lib().aos_last_error().decode()}")
+
+
+def cluster_union(width: int, height: int, piece_root, border_cell, border_root):
+    """aos_cluster_union (host code, no GPU): the border union-find of the tiled frame's distributed
+    cluster stage. -> (cluster id per piece, clusters numbered in raster order of their first cell; count)."""
+    pr = np.ascontiguousarray(piece_root, dtype=np.int32)
+    bc = np.ascontiguousarray(border_cell, dtype=np.int32)
+    br = np.ascontiguousarray(border_root, dtype=np.int32)
+    if bc.shape != br.shape:
+        raise ValueError("border_cell and border_root differ in length")
+    out = np.empty(pr.size, np.int32)
+    n = c_i(0)
+    _check(lib().aos_cluster_union(int(width), int(height), pr.size, pr.ctypes.data, bc.size, bc.ctypes.data,
+                                   br.ctypes.data, out.ctypes.data, ctypes.byref(n)))
+    return out, n.value
 
 
 def default_params(**kw) -> Params:

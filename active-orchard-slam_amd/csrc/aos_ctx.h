@@ -117,8 +117,10 @@ struct aos_ctx {
     double ror_staged_max = 0;             // largest staged (own + halo) count seen (sizes the scatter)
     bool ror_big_seen = false;             // a frame had a ROR tile beyond the LDS capacity (ror.hip big_ok)
 
-    // ---- cluster / row / seed stage (cluster_seed.hip)
+    // ---- cluster / row / seed stage (cluster_seed.hip); tiled frames: distributed a8-a10 (cluster_dist.hip)
     aos::ClusterSeedState cs;
+    aos::ClusterDistState cdist;
+    aos::ClusterDistStats cdist_stats;
 
     // ---- host-side outputs of the last frame
     aos::PinnedBuf h_occ, h_skel;   // the two OccupancyGrids (pinned: the D2H runs at DMA speed)
@@ -186,7 +188,8 @@ struct aos_ctx {
     void ror_stage(const aos::FrameGeom &g, const RorOwn &o, uint64_t *rbits, bool allow_guess);
     bool ror_collect();   // after the stream synchronised: true if the ROR scatter overflowed
     void ror_stage_append(aos::RorLaunch L, uint64_t *rbits);   // streaming map: one scan on the tile store
-    void finish_frame(const aos::FrameGeom &g, bool want_host, const uint64_t *clipped_total, aos_seedgen_out &out);
+    void finish_frame(const aos::FrameGeom &g, bool want_host, const uint64_t *clipped_total, aos_seedgen_out &out,
+                      const aos::PreClusters *pre = nullptr);
     void run_seedgen(bool want_host, aos_seedgen_out &out);
     bool run_seedgen_once(bool want_host, aos_seedgen_out &out, bool allow_guess);   // true: redo
     void run_tiled(const aos_comm &cm, int tiles_x, int tiles_y, int root, bool want_host, aos_seedgen_out &out);

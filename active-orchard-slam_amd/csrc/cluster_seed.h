@@ -66,13 +66,30 @@ struct ClusterSeedState {
     std::vector<ClusterRec> h_rec;
 };
 
+// a8-a10 computed elsewhere (the tiled frame's distributed cluster stage, cluster_dist.hip): every
+// cluster's record in cluster order, exactly as the whole-map stage makes it.
+struct PreClusters {
+    std::vector<ClusterRec> rec;
+    int n_fg = 0, n_bfs = 0;
+};
+
 // Everything the seed stage needs from the frame.
 struct SeedStageIn {
     const uint64_t *skel_bits;   // frameless skeleton
     const FrameGeom *g;
     const Poly *poly;
     double cluster_min_length;
+    const PreClusters *pre = nullptr;   // set: skip a8-a10 (labelling, statistics, replays)
 };
+
+struct GridC;
+// k_cluster_stats over clusters given as runs of raster-ordered cells (off[n_clusters + 1], cells)
+void launch_cluster_stats(const int *off, const int *cells, int n_clusters, const GridC &g, const double *poly, int np,
+                          float min_length, ClusterRec *rec, hipStream_t s);
+// exact FIFO-BFS replays (host, parallel over clusters); cells of a job in raster order, n of them
+struct ReplayJob { int c; const int *cells; int n; };
+void replay_clusters(const std::vector<ReplayJob> &jobs, const GridC &g, const double *poly, int np, float min_len,
+                     ClusterRec *rec);
 
 struct SeedStageOut {
     int n_clusters_all = 0;
@@ -86,6 +103,22 @@ struct SeedStageOut {
 
 void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStageOut &out, hipStream_t stream,
                             hipEvent_t ev_mid);
+
+// ------------------------------------------------------------------ distributed a8-a10 (cluster_dist.hip)
+struct ClusterDistState {
+    DevBuf poly, fg, cnt, off, list, parent, isroot, rank, pieces, border, counts, lidx, keys, keys_all, cells, coff, rec, tmp;
+    PinnedBuf h;
+};
+struct ClusterDistStats {
+    int n_pieces = 0, n_border = 0, n_long = 0, long_cells = 0, n_replayed_here = 0;
+    float ms_local = 0, ms_global = 0;   // own labelling / tables, union-find, long-cluster statistics and replays
+};
+// The tiled frame's cluster stage on one rank (collective over the tile ranks): win = the rank's
+// window skeleton (own cells exact). The root receives every cluster's record in pre.
+int cluster_union(int W, int H, int n_pieces, const int *piece_root, int n_border, const int *bcell, const int *broot,
+                  int *piece_cluster);
+void cluster_dist(ClusterDistState &D, const aos_comm &cm, const TilePlan &t, const FrameGeom &g, const Poly &poly,
+                  float min_len, const uint64_t *win, int root, hipStream_t s, PreClusters &pre, ClusterDistStats &st);
 
 // ------------------------------------------------------------------ GVD
 // publishMarkers' Voronoi cells, computed by a worker thread next to the main Subdiv2D replay. It

@@ -24,43 +24,13 @@
 #include <stdexcept>
 #include <thread>
 
+#include "cluster_dev.h"
 #include "cluster_seed.h"
 
 namespace aos {
 
 static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 constexpr int kReplayThreads = 8;   // host threads for the exact BFS replays of one frame
-
-// isPointInPolygon seed_gen:1231-1255
-__host__ __device__ bool d_pip(double px, double py, const double *poly, int n) {
-    if (n < 3) return false;
-    bool inside = false;
-    int j = n - 1;
-    for (int i = 0; i < n; ++i) {
-        double pix = poly[2 * i], piy = poly[2 * i + 1], pjx = poly[2 * j], pjy = poly[2 * j + 1];
-        double dy = pjy - piy;
-        if (fabs(dy) > 1e-9) {
-            if (((piy > py) != (pjy > py)) && (px < (pjx - pix) * (py - piy) / dy + pix)) inside = !inside;
-        }
-        j = i;
-    }
-    return inside;
-}
-
-struct GridC {
-    double ox, oy;       // origin
-    float res;
-    int W, H, WW;
-    double minx, maxx, miny, maxy;  // origin + W * res (float product), seed_gen:1807-1810
-    double amax;         // castRayFromEndpoint absolute max distance, seed_gen:1838-1840
-};
-
-// float world coordinate of a cell: origin + float(x) * res (float product, double add, to float)
-__host__ __device__ __forceinline__ float cell_world(double o, int i, float res) { return (float)(o + (double)((float)i * res)); }
-
-__device__ __forceinline__ bool bit_at(const uint64_t *bits, int WW, int x, int y) {
-    return (bits[(size_t)y * WW + (x >> 6)] >> (x & 63)) & 1ull;
-}
 
 // ------------------------------------------------------------------ foreground = skeleton inside polygon
 __global__ void k_fg(const uint64_t *skel, uint64_t *fg, int *cnt, GridC g, const double *poly, int np) {
@@ -102,16 +72,6 @@ __device__ __forceinline__ int fg_index(const uint64_t *fg, const int *off, cons
 }
 
 // ------------------------------------------------------------------ union-find CCL (8-connectivity)
-__device__ __forceinline__ int ld_parent(int *parent, int i) {
-    return __hip_atomic_load(&parent[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ int uf_find(int *parent, int x) {
-    while (true) {
-        int p = ld_parent(parent, x);
-        if (p == x) return x;
-        x = p;
-    }
-}
 __global__ void k_ccl_init(int *parent, int n) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) parent[i] = i;
@@ -123,15 +83,7 @@ __global__ void k_ccl_union(const int *list, int n, const uint64_t *fg, const in
     const int ndx[4] = {-1, 0, 1, -1}, ndy[4] = {-1, -1, -1, 0};
     for (int k = 0; k < 4; ++k) {
         int j = fg_index(fg, off, g, x + ndx[k], y + ndy[k]);
-        if (j < 0) continue;
-        int a = uf_find(parent, i), b = uf_find(parent, j);
-        while (a != b) {
-            if (a < b) { int t = a; a = b; b = t; }
-            int old = atomicCAS(&parent[a], a, b);  // link the larger root under the smaller
-            if (old == a) break;
-            a = uf_find(parent, old);
-            b = uf_find(parent, b);
-        }
+        if (j >= 0) uf_union(parent, i, j);
     }
 }
 __global__ void k_ccl_flatten(int *parent, int *is_root, int n) {
@@ -181,11 +133,6 @@ __device__ T block_reduce(T v, T *sh, Op op) {
 struct MaxOp { template <class T> __device__ T operator()(T a, T b) const { return a > b ? a : b; } };
 struct MinOp { template <class T> __device__ T operator()(T a, T b) const { return a < b ? a : b; } };
 struct AddOp { template <class T> __device__ T operator()(T a, T b) const { return a + b; } };
-
-__host__ __device__ __forceinline__ double2 cell_w(const GridC &g, int p) {
-    int y = p / g.W, x = p - y * g.W;
-    return make_double2((double)cell_world(g.ox, x, g.res), (double)cell_world(g.oy, y, g.res));
-}
 
 // one workgroup per cluster
 __global__ __launch_bounds__(256) void k_cluster_stats(StatArgs A) {
@@ -427,6 +374,42 @@ static void host_bfs_replay(const int *cells, int n, const GridC &g, const doubl
     r.flags = (row ? 1 : 0) | 4;  // 4: replayed
 }
 
+// The exact replays of a frame, in parallel over clusters on up to kReplayThreads host threads (each
+// writes only its own record).
+void replay_clusters(const std::vector<ReplayJob> &jobs, const GridC &g, const double *poly, int np, float min_len,
+                     ClusterRec *rec) {
+    if (jobs.empty()) return;
+    std::atomic<int> next{0};
+    std::exception_ptr err;
+    std::mutex mu;
+    auto work = [&]() {
+        std::vector<int> q, tab;
+        for (int i; (i = next.fetch_add(1)) < (int)jobs.size();) {
+            const ReplayJob &j = jobs[i];
+            try {
+                host_bfs_replay(j.cells, j.n, g, poly, np, min_len, rec[j.c], q, tab);
+            } catch (...) {
+                std::lock_guard<std::mutex> lk(mu);
+                if (!err) err = std::current_exception();
+            }
+        }
+    };
+    const int nt = std::min<int>((int)jobs.size(), kReplayThreads);
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(work);
+    work();
+    for (auto &t : th) t.join();
+    if (err) std::rethrow_exception(err);
+}
+
+void launch_cluster_stats(const int *off, const int *cells, int n_clusters, const GridC &g, const double *poly, int np,
+                          float min_length, ClusterRec *rec, hipStream_t s) {
+    if (n_clusters <= 0) return;
+    StatArgs A{off, cells, nullptr, n_clusters, g, poly, np, min_length, rec};
+    k_cluster_stats<<<n_clusters, 256, 0, s>>>(A);
+    AOS_HIP(hipGetLastError());
+}
+
 // ------------------------------------------------------------------ rays
 struct RowDev { double sx, sy, ex, ey; int k; int slot0; };
 
@@ -581,16 +564,7 @@ template <class T> static T *dev(DevBuf &b, size_t n) { return static_cast<T *>(
 
 void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStageOut &out, hipStream_t s, hipEvent_t ev_mid) {
     const FrameGeom &fg = *in.g;
-    GridC g{};
-    g.ox = fg.origin_x; g.oy = fg.origin_y; g.res = fg.res; g.W = fg.W; g.H = fg.H; g.WW = fg.WW;
-    {   // bounds exactly as the reference forms them (uint32 * float -> float, then double add)
-        const uint32_t W = (uint32_t)fg.W, H = (uint32_t)fg.H;
-        const float res = fg.res;
-        g.minx = fg.origin_x; g.maxx = g.minx + W * res;
-        g.miny = fg.origin_y; g.maxy = g.miny + H * res;
-        double gw = W * res, gh = H * res;
-        g.amax = std::sqrt(gw * gw + gh * gh) * 3.0;
-    }
+    const GridC g = make_gridc(fg);
     const Poly &poly = *in.poly;
     const int np = (int)poly.size();
     double *d_poly = dev<double>(S.poly, 2 * np);
@@ -601,24 +575,31 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
 
     // ---- foreground list (raster order)
     const size_t Cw = (size_t)g.WW * g.H;
-    uint64_t *d_fg = dev<uint64_t>(S.fg_bits, Cw);
-    int *d_wc = dev<int>(S.word_cnt, Cw + 1), *d_wo = dev<int>(S.word_off, Cw + 1);
-    AOS_HIP(hipMemsetAsync(d_wc + Cw, 0, sizeof(int), s));
-    dim3 gw2(cdiv(g.WW, 64), g.H);
-    k_fg<<<gw2, 64, 0, s>>>(in.skel_bits, d_fg, d_wc, g, d_poly, np);
+    uint64_t *d_fg = nullptr;
+    int *d_wc = nullptr, *d_wo = nullptr;
     size_t tb = 0;
-    AOS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (int *)nullptr, (int *)nullptr, (int)Cw + 1, s));
-    void *tmp = S.scan_tmp.ensure(tb);
-    AOS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, d_wc, d_wo, (int)Cw + 1, s));
-    AOS_HIP(hipMemcpyAsync(h_sc, d_wo + Cw, sizeof(int), hipMemcpyDeviceToHost, s));
-    S.dedup.sev.sync(s);
-    const int nf = h_sc[0];
+    const dim3 gw2(cdiv(g.WW, 64), g.H);
+    if (!in.pre) {
+        d_fg = dev<uint64_t>(S.fg_bits, Cw);
+        d_wc = dev<int>(S.word_cnt, Cw + 1); d_wo = dev<int>(S.word_off, Cw + 1);
+        AOS_HIP(hipMemsetAsync(d_wc + Cw, 0, sizeof(int), s));
+        k_fg<<<gw2, 64, 0, s>>>(in.skel_bits, d_fg, d_wc, g, d_poly, np);
+        AOS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (int *)nullptr, (int *)nullptr, (int)Cw + 1, s));
+        AOS_HIP(hipcub::DeviceScan::ExclusiveSum(S.scan_tmp.ensure(tb), tb, d_wc, d_wo, (int)Cw + 1, s));
+        AOS_HIP(hipMemcpyAsync(h_sc, d_wo + Cw, sizeof(int), hipMemcpyDeviceToHost, s));
+        S.dedup.sev.sync(s);
+    }
+    const int nf = in.pre ? in.pre->n_fg : h_sc[0];
     S.n_fg = nf;
     out = SeedStageOut();
     S.n_clusters = 0;
     S.h_rec.clear();
     std::vector<RowDev> rows;
-    if (nf > 0) {
+    if (in.pre) {   // labelled and measured by the tile ranks (cluster_dist.hip)
+        S.h_rec = in.pre->rec;
+        S.n_clusters = (int)S.h_rec.size();
+        out.n_bfs = in.pre->n_bfs;
+    } else if (nf > 0) {
         int *d_list = dev<int>(S.fg_list, nf);
         k_fg_list<<<gw2, 64, 0, s>>>(d_fg, d_wo, d_list, g);
         int *d_par = dev<int>(S.parent, nf), *d_isroot = dev<int>(S.root_flag, nf + 1), *d_rank = dev<int>(S.root_rank, nf + 1);
@@ -628,7 +609,7 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         k_ccl_flatten<<<cdiv(nf, 256), 256, 0, s>>>(d_par, d_isroot, nf);
         size_t tb2 = 0;
         AOS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, (int *)nullptr, (int *)nullptr, nf + 1, s));
-        tmp = S.scan_tmp.ensure(std::max(tb, tb2));
+        void *tmp = S.scan_tmp.ensure(std::max(tb, tb2));
         AOS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, d_isroot, d_rank, nf + 1, s));
         AOS_HIP(hipMemcpyAsync(h_sc, d_rank + nf, sizeof(int), hipMemcpyDeviceToHost, s));
         S.dedup.sev.sync(s);
@@ -648,8 +629,7 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         AOS_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tbs, d_cid, d_scid, d_list, d_cells, nf, 0, bits, s));
         k_run_starts<<<cdiv(nf, 256), 256, 0, s>>>(d_scid, nf, d_off, ncl);
         ClusterRec *d_rec = dev<ClusterRec>(S.rec, ncl);
-        StatArgs A{d_off, d_cells, d_list, ncl, g, d_poly, np, static_cast<float>(in.cluster_min_length), d_rec};
-        k_cluster_stats<<<ncl, 256, 0, s>>>(A);
+        launch_cluster_stats(d_off, d_cells, ncl, g, d_poly, np, static_cast<float>(in.cluster_min_length), d_rec, s);
         S.h_rec.resize(ncl);
         AOS_HIP(hipMemcpyAsync(S.h_rec.data(), d_rec, sizeof(ClusterRec) * ncl, hipMemcpyDeviceToHost, s));
         S.dedup.sev.sync(s);
@@ -669,31 +649,12 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
             std::vector<int> hc((size_t)(hi - lo));
             AOS_HIP(hipMemcpyAsync(hc.data(), d_cells + lo, sizeof(int) * (hi - lo), hipMemcpyDeviceToHost, s));
             S.dedup.sev.sync(s);
-            const float min_len = static_cast<float>(in.cluster_min_length);
-            std::atomic<int> next{0};
-            std::exception_ptr err;
-            std::mutex mu;
-            auto work = [&]() {
-                std::vector<int> q, tab;
-                for (int i; (i = next.fetch_add(1)) < (int)ids.size();) {
-                    const int c = ids[i];
-                    try {
-                        host_bfs_replay(hc.data() + (off[c] - lo), S.h_rec[c].n, g, hp.data(), np, min_len, S.h_rec[c], q,
-                                        tab);
-                    } catch (...) {
-                        std::lock_guard<std::mutex> lk(mu);
-                        if (!err) err = std::current_exception();
-                    }
-                }
-            };
-            const int nt = std::min<int>((int)ids.size(), kReplayThreads);
-            std::vector<std::thread> th;
-            for (int t = 1; t < nt; ++t) th.emplace_back(work);
-            work();
-            for (auto &t : th) t.join();
-            if (err) std::rethrow_exception(err);
+            std::vector<ReplayJob> jobs;
+            for (int c : ids) jobs.push_back({c, hc.data() + (off[c] - lo), S.h_rec[c].n});
+            replay_clusters(jobs, g, hp.data(), np, static_cast<float>(in.cluster_min_length), S.h_rec.data());
         }
-        // ---- tree rows in cluster order (convertClustersToTreeRows, seed_gen:1329-1406)
+    }
+    {   // ---- tree rows in cluster order (convertClustersToTreeRows, seed_gen:1329-1406)
         int slot = 0;
         for (const auto &r : S.h_rec) {
             if (!(r.flags & 1)) continue;

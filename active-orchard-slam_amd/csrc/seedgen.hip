@@ -730,7 +730,8 @@ bool aos_ctx::run_seedgen_once(bool want_host, aos_seedgen_out &out, bool allow_
 
 // a16 + a8-a15 on the whole map from skel_bits / occ_bytes, then the frame outputs. clipped_total:
 // the kept-candidate count when it was reduced over tiles (else read from this handle's counters).
-void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *clipped_total, aos_seedgen_out &out) {
+void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *clipped_total, aos_seedgen_out &out,
+                           const PreClusters *pre) {
     hipStream_t s = stream;
     ++frame_gen;   // skel_bytes is rewritten below
     const size_t C = (size_t)g.W * g.H;
@@ -772,7 +773,7 @@ void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *c
     }
 
     // ---------------- a8-a15 clusters, tree rows, seeds
-    SeedStageIn sin{skel_bits, &geom, &poly, P.cluster_min_length};
+    SeedStageIn sin{skel_bits, &geom, &poly, P.cluster_min_length, pre};
     SeedStageOut so;
     run_cluster_seed_stage(cs, sin, so, s, ev[4]);
     AOS_HIP(hipEventRecord(ev[5], s));
@@ -822,7 +823,8 @@ void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *c
     out.n_cluster_info = (int)h_cluster_info.size() / 2;
     out.cluster_info_xy = h_cluster_info.data();
     auto ms = [&](int a, int b) { float t = 0; (void)hipEventElapsedTime(&t, ev[a], ev[b]); return t; };
-    out.ms_ror = ms(0, 1); out.ms_grid = ms(1, 2); out.ms_thin = ms(2, 3); out.ms_cluster = ms(3, 4);
+    // (a tiled frame: its cluster stage starts at ev[6], after the grids' all-gather)
+    out.ms_ror = ms(0, 1); out.ms_grid = ms(1, 2); out.ms_thin = ms(2, 3); out.ms_cluster = ms(pre ? 6 : 3, 4);
     out.ms_seeds = ms(4, 5); out.ms_total = ms(0, 5);
     out.n_binned = static_cast<const int *>(h_stats.p)[0];   // (ror_collect)
     out.ms_ror_count = out.n_binned ? ms(10, 11) : 0.0f;

@@ -271,9 +271,10 @@ void aos_ctx::run_tiled(const aos_comm &cm, int tiles_x, int tiles_y, int root, 
     AOS_HIP(hipGetLastError());
     AOS_HIP(hipStreamSynchronize(s));
     comm_all_gather(cm, 16ull * (uint64_t)t.max_own);
+    uint64_t *fs = nullptr;
     if (cm.rank == root) {
         const size_t Cw = (size_t)g.WW * g.H;
-        uint64_t *fs = static_cast<uint64_t *>(full_skel.ensure(Cw * 8));
+        fs = static_cast<uint64_t *>(full_skel.ensure(Cw * 8));
         uint64_t *fi = static_cast<uint64_t *>(full_infl.ensure(Cw * 8));
         const TileSplit S = split_of(t, 2 * t.max_own);
         k_unpack_full2<<<dim3(cdiv(g.WW, 64), g.H), 64, 0, s>>>(static_cast<const uint64_t *>(cm.recv_buf), S, g.WW,
@@ -281,8 +282,15 @@ void aos_ctx::run_tiled(const aos_comm &cm, int tiles_x, int tiles_y, int root, 
         AOS_HIP(hipGetLastError());
         int8_t *d_occ = static_cast<int8_t *>(occ_bytes.ensure((size_t)g.W * g.H));
         launch_bits_to_bytes(fi, d_occ, g, 5, s);   // a6 /occupancy_grid
+    }
+
+    // ---- a8-a10 over the ranks: own-tile labelling, border union-find, shared statistics / replays
+    AOS_HIP(hipEventRecord(ev[6], s));
+    PreClusters pre;
+    cluster_dist(cdist, cm, t, g, poly, static_cast<float>(P.cluster_min_length), cur, root, s, pre, cdist_stats);
+    if (cm.rank == root) {
         skel_bits = fs;
-        finish_frame(g, want_host, &total, out);
+        finish_frame(g, want_host, &total, out, &pre);
         return;
     }
     n_clipped = total;
@@ -291,7 +299,10 @@ void aos_ctx::run_tiled(const aos_comm &cm, int tiles_x, int tiles_y, int root, 
     out.n_input = (d_cloud == map_buf.as<uint8_t>() && n_points == map_n) ? map_total : n_points;
     out.n_clipped = total;
     auto ms = [&](int a, int b) { float v = 0; (void)hipEventElapsedTime(&v, ev[a], ev[b]); return v; };
-    out.ms_ror = ms(0, 1); out.ms_grid = ms(1, 2); out.ms_thin = ms(2, 3); out.ms_total = ms(0, 3);
+    AOS_HIP(hipEventRecord(ev[4], s));
+    AOS_HIP(hipEventSynchronize(ev[4]));
+    out.ms_ror = ms(0, 1); out.ms_grid = ms(1, 2); out.ms_thin = ms(2, 3); out.ms_cluster = ms(6, 4);
+    out.ms_total = ms(0, 4);
     out.n_binned = static_cast<const int *>(h_stats.p)[0];
     out.ms_ror_count = out.n_binned ? ms(10, 11) : 0.0f;
     out.ms_ror_bin = out.n_binned ? ms(12, 13) : 0.0f;

@@ -187,9 +187,6 @@ def _progress(msg: str) -> None:
 
 def main():
     a = parse()
-    if os.environ.get("AOS_BENCH_NUMPY_HUGEPAGE") == "0":   # (diagnostic: numpy's madvise(MADV_HUGEPAGE) on >= 4 MB arrays)
-        import numpy as np
-        np._core.multiarray._set_madvise_hugepage(False)
     _progress("importing torch")
     import torch  # (import before libaos_gpu: shared HIP runtime, see aos_gpu.lib)
     import torch.distributed as dist

@@ -268,6 +268,18 @@ int aos_tiled_seedgen_process(aos_ctx *ctx, const aos_comm *comm, int32_t tiles_
 int aos_tiled_map_append(aos_ctx *ctx, const aos_comm *comm, int32_t tiles_x, int32_t tiles_y, int32_t root,
                          const aos_cloud_view *scan, int want_host, aos_seedgen_out *out);
 
+/* Border union-find of per-tile cluster pieces: the numbering step of the tiled frame's distributed
+ * cluster stage (csrc/cluster_dist.hip; it replaces clusterOccupiedCells' whole-map raster scan + BFS
+ * labelling, aos_seed_gen_node.cpp:970-1049, for clusters that cross tiles). Host code: no GPU needed.
+ * A piece is a tile's 8-connected component of foreground cells, named by its first cell in raster
+ * order (y * width + x, distinct over pieces); border_cell[i] (a piece's cell on its tile's edge)
+ * belongs to the piece named border_root[i]. Two pieces are one cluster iff two of their border cells
+ * are 8-adjacent. piece_cluster[i] = the cluster of piece i, clusters numbered in raster order of
+ * their first cell (the reference's discovery order); *n_clusters = their number. */
+int aos_cluster_union(int32_t width, int32_t height, int32_t n_pieces, const int32_t *piece_root, int32_t n_border,
+                      const int32_t *border_cell, const int32_t *border_root, int32_t *piece_cluster,
+                      int32_t *n_clusters);
+
 /* One map over several GPUs from one process (SURVEY §8b's multi-GPU handle). The group owns one
  * handle per tile (devices[r] for rank r = tile (r % tiles_x, r / tiles_x); devices may repeat) and
  * drives the ranks with its own threads and an in-process aos_comm (peer copies over xGMI, host

@@ -2,6 +2,7 @@
 - the tile plan the C-ABI computes (aos_tile_plan_compute needs no GPU);
 - the communicator adapters (aos_tiles.TorchDistComm over gloo at world size 2, ThreadGroup), called
   through the same C function pointers libaos_gpu calls;
+- the border union-find of the distributed cluster stage (aos_cluster_union, host code) over gloo ranks;
 - a numpy emulation of tiled.hip's schedule (own-cell raster -> halo exchange -> inflate -> open ->
   Zhang-Suen in halo periods with max-reduced own-cell change flags) run by gloo ranks, whose gathered
   tiles must equal the oracle's whole-map grids and iteration count.
@@ -118,6 +119,98 @@ def test_torch_dist_comm_gloo_world2():
         assert rc == 0 and rc2 == 0
         assert np.array_equal(recv, np.concatenate([np.arange(48, dtype=np.uint8) + 10 * r for r in range(2)]))
         assert v == [1, 5, 0]
+
+
+# ---------------------------------------------------------------- distributed cluster labelling
+def _pieces_of_tile(fg, y0, y1, x0, x1):
+    """One rank's part of cluster_dist.hip step 1 on the CPU: 8-connected pieces of its own cells
+    (scipy stands in for the GPU union-find), named by their first raster cell, the piece's n and
+    integer sums, and its cells on the tile's edge."""
+    from scipy import ndimage
+    H, W = fg.shape
+    sub = fg[y0:y1, x0:x1]
+    lab, n = ndimage.label(sub, structure=np.ones((3, 3), bool))
+    ys, xs = np.nonzero(lab)
+    gid = (ys + y0) * W + (xs + x0)                  # raster order (np.nonzero is row-major)
+    lv = lab[ys, xs] - 1
+    root = np.full(n, np.iinfo(np.int32).max, np.int64)
+    np.minimum.at(root, lv, gid)
+    cnt = np.bincount(lv, minlength=n)
+    sx = np.bincount(lv, weights=xs + x0, minlength=n).astype(np.int64)
+    edge = (ys == 0) | (xs == 0) | (ys == sub.shape[0] - 1) | (xs == sub.shape[1] - 1)
+    return root.astype(np.int32), cnt, sx, gid[edge].astype(np.int32), root[lv[edge]].astype(np.int32)
+
+
+def _union_worker(rank, world, port, q, fg, tx, ty):
+    _init(rank, world, port)
+    H, W = fg.shape
+    x_cut = [W * i // tx for i in range(tx + 1)]
+    y_cut = [H * i // ty for i in range(ty + 1)]
+    cx, cy = rank % tx, rank // tx
+    mine = _pieces_of_tile(fg, y_cut[cy], y_cut[cy + 1], x_cut[cx], x_cut[cx + 1])
+    tables = [None] * world
+    dist.all_gather_object(tables, mine)             # the pieces / border all-gather
+    root = np.concatenate([t[0] for t in tables])
+    cnt = np.concatenate([t[1] for t in tables])
+    sx = np.concatenate([t[2] for t in tables])
+    bcell = np.concatenate([t[3] for t in tables])
+    broot = np.concatenate([t[4] for t in tables])
+    pc, ncl = aos_gpu.cluster_union(W, H, root, bcell, broot)
+    q.put((rank, root, cnt, sx, pc, ncl))
+    dist.destroy_process_group()
+
+
+def _reference_clusters(fg):
+    """Whole-map labelling in the reference's numbering (raster order of the first cell)."""
+    from scipy import ndimage
+    lab, n = ndimage.label(fg, structure=np.ones((3, 3), bool))
+    ys, xs = np.nonzero(lab)
+    first = np.full(n, np.iinfo(np.int64).max)
+    np.minimum.at(first, lab[ys, xs] - 1, ys * fg.shape[1] + xs)
+    order = np.argsort(first)
+    cid = np.empty(n, np.int64)
+    cid[order] = np.arange(n)
+    return cid[lab - 1], lab > 0, first[order], n
+
+
+@pytest.mark.parametrize("tiles", [(2, 1), (1, 2)])
+def test_cluster_union_gloo_world2(tiles):
+    """cluster_dist.hip's numbering: pieces labelled per tile, tables all-gathered over gloo, the
+    library's aos_cluster_union on every rank -> the whole-map clusters in raster order of their first
+    cell, with n and integer sums added over pieces (rows, blobs and diagonal contacts across the cut)."""
+    rng = np.random.default_rng(7)
+    H, W = 96, 160
+    fg = rng.random((H, W)) < 0.12                   # noise: many small clusters, diagonal contacts
+    fg[20, 5:150] = True                             # rows that cross the vertical cut
+    fg[60, 10:140] = True
+    fg[10:90, 80] = True                             # a column crossing the horizontal cut
+    fg[47, 79], fg[48, 80] = True, True              # diagonal contact at the corner region
+    tx, ty = tiles
+    out = _spawn(_union_worker, 2, fg, tx, ty)
+    cid_map, mask, first, n = _reference_clusters(fg)
+    ys, xs = np.nonzero(mask)
+    ref_n = np.bincount(cid_map[ys, xs], minlength=n)
+    ref_sx = np.bincount(cid_map[ys, xs], weights=xs, minlength=n).astype(np.int64)
+    for rank, root, cnt, sx, pc, ncl in out:
+        assert ncl == n
+        # every piece lies in its cluster, clusters numbered as the reference discovers them
+        ry, rx = root // W, root % W
+        assert np.array_equal(pc, cid_map[ry, rx])
+        assert np.array_equal(np.bincount(pc, weights=cnt, minlength=n).astype(np.int64), ref_n)
+        assert np.array_equal(np.bincount(pc, weights=sx, minlength=n).astype(np.int64), ref_sx)
+        first_of = np.full(n, np.iinfo(np.int64).max)
+        np.minimum.at(first_of, pc, root.astype(np.int64))
+        assert np.array_equal(first_of, first)
+    assert any((np.bincount(o[4]) > 1).any() for o in out)   # some clusters really cross the cut
+
+
+def test_cluster_union_rejects_bad_tables():
+    with pytest.raises(RuntimeError, match="unknown piece"):
+        aos_gpu.cluster_union(8, 8, [0, 9], [3], [5])
+    with pytest.raises(RuntimeError, match="duplicate"):
+        aos_gpu.cluster_union(8, 8, [4, 4], [], [])
+    pc, n = aos_gpu.cluster_union(8, 8, [], [], [])
+    assert n == 0 and pc.size == 0
 
 
 # ---------------------------------------------------------------- tiled streaming: scan routing
