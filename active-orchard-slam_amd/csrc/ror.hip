@@ -263,14 +263,50 @@ __device__ __forceinline__ int rt_scan(const RorLaunch &L, float4 p, Pts pts, in
     return cnt;
 }
 
+// A thread examines at most kRtBudget points for its candidate; a candidate still undecided (a dense
+// neighbourhood in which it finds too few neighbours: an outlier, up to ~10^4 points in a streaming
+// map's big tile) goes to the workgroup's queue and is counted by a whole wave, 64 points per step.
+// One lane walking such a neighbourhood alone bounded the kernel (~1 ms per scan at C4).
+template <class Pts>
+__device__ __forceinline__ int rt_scan_b(const RorLaunch &L, float4 p, Pts pts, int k0, int k1, int cnt, int &budget) {
+    int k = k0;
+    for (; k < k1 && cnt < L.need && budget > 0; k += 4, budget -= 4) {
+        float4 q[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) q[j] = pts[min(k + j, k1 - 1)];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cnt += (k + j < k1 && rt_in(L, p, q[j])) ? 1 : 0;
+    }
+    if (k < k1 && cnt < L.need) budget = -1;   // cut short: undecided
+    return cnt;
+}
+template <class Pts>
+__device__ __forceinline__ int rt_wave_scan(const RorLaunch &L, float4 p, Pts pts, int k0, int k1, int cnt, int lane) {
+    for (int base = k0; base < k1 && cnt < L.need; base += 64) {   // (cnt is wave-uniform)
+        const int j = base + lane;
+        const bool hit = j < k1 && rt_in(L, p, pts[min(j, k1 - 1)]);
+        cnt += (int)__popcll(__ballot(hit));
+    }
+    return cnt;
+}
+#ifndef AOS_RT_BUDGET_LDS
+#define AOS_RT_BUDGET_LDS 64
+#endif
+constexpr int kRtBudgetBig = 64, kRtBudgetLds = AOS_RT_BUDGET_LDS, kRtQCap = 512;
+
 // LDS of k_rt_ror: kRorCap staged points (32 KB), the bin offsets of the largest tile (TB = 32 bins
-// + ring: 34^2), and the tile's raster window (kRtWinWords 64-bit words): ~40 KB, 3 workgroups per CU
+// + ring: 34^2), the tile's raster window (kRtWinWords 64-bit words) and the wave queue: ~42 KB, 3
+// workgroups per CU
 constexpr int kRtMaxLocalBins = 34 * 34, kRtWinWords = 320;
+// staged record w (int bits): bits 0-1 the class (0 a neighbour only, 1 an own clip candidate, 2 a
+// candidate a streaming map already found kept); streaming store only: kWOld = written back by an
+// earlier frame, kWCounted = a candidate below need whose count over the store is in bits kWCntShift+
+constexpr int kWClass = 3, kWCounted = 4, kWOld = 8, kWCntShift = 8;
 
 // Tiles with more than kRorCap points (a streaming map's scan footprint: up to ~10^6 points in one
 // tile after a few dozen scans) do not fit LDS, and one workgroup per such tile leaves most CUs idle
-// while a few walk a huge list. They are listed (k_rt_biglist) and each is split into kBigC chunks of
-// its list, one workgroup per (tile, chunk) in grids of kBigC x kBigY that loop over the list:
+// while a few walk a huge list. They are listed (k_rt_biglist) and cut into chunks of kBigChunk points
+// (k_rt_bigchunks), one workgroup per chunk in grids of kBigGrid that loop over the chunks:
 //   k_rt_bighist     per-chunk LDS bin histogram, added into the tile's global bin totals
 //   k_rt_bigscan     per tile: bin starts (bigbins row) and bin cursors (= starts)
 //   k_rt_bigscatter  per chunk: one global atomic per (chunk, non-empty bin) reserves its runs, then the
@@ -278,17 +314,31 @@ constexpr int kRtMaxLocalBins = 34 * 34, kRtWinWords = 320;
 //   k_rt_ror_big     per chunk: the neighbour counts of the chunk's points, searched in the tile's
 //                    bin-sorted scratch range (through the kernel boundary; see k_rt_ror for the rules)
 // The order inside a bin depends on the atomics' order; the keep decision and the raster do not.
-constexpr int kBigC = 16, kBigY = 32, kBigTB = 512;
-struct BigBufs { int *starts, *cur, *list; };   // rt_bigbins_ints(L) ints: 2 x ntiles x (nlb + 1), 1 + ntiles
+// A big tile's bins are split in two: first the points the store already held (kWOld), then this
+// frame's new points. A candidate that stayed below need in an earlier frame carries its neighbour count
+// over the store's points (kWCounted, count in bits kWCntShift+); points are only ever added, so its new
+// count is that count plus its neighbours among the new points, found in the new halves of its 3 x 3
+// bins alone. (Without it, every dirty big tile re-scanned the whole 3 x 3 neighbourhood, thousands of
+// points, for each of its lasting outliers on every scan.)
+// Work is split in chunks of kBigChunk points over all big tiles (choff: the chunks' prefix over the
+// list), so a grid of kBigGrid workgroups stays balanced however unequal the tiles are (round 2's 16
+// chunks per tile left a 10^6-point tile's 16 workgroups walking 60 k points each while the rest idled).
+constexpr int kBigY = 32, kBigTB = 512, kBigBins = 2 * kRtMaxLocalBins, kBigChunk = 4096, kBigGrid = 1024;
+// rt_bigbins_ints(L) ints: starts and cursors 2 x ntiles x (2 nlb + 1), list 1 + ntiles, choff ntiles + 1
+struct BigBufs { int *starts, *cur, *list, *choff; };
 static BigBufs big_bufs(const RorLaunch &L, int *B) {
-    const size_t row = (size_t)(L.TB + 2) * (L.TB + 2) + 1, nt = (size_t)L.ntiles;
-    return BigBufs{B, B + nt * row, B + 2 * nt * row};
+    const size_t row = 2 * (size_t)(L.TB + 2) * (L.TB + 2) + 1, nt = (size_t)L.ntiles;
+    return BigBufs{B, B + nt * row, B + 2 * nt * row, B + 2 * nt * row + 1 + nt};
 }
 
 __device__ __forceinline__ int rt_lbin(const RorLaunch &L, float4 q, int bx0, int by0, int LB) {
     int bx, by;
     rt_bin(L, q.x, q.y, bx, by);
     return (by - by0) * LB + (bx - bx0);   // in [0, LB^2): a copy lies in the tile's 3 x 3 reach
+}
+// big tiles: local bin b -> sub-bins 2 b (store points) and 2 b + 1 (new points)
+__device__ __forceinline__ int rt_sbin(const RorLaunch &L, float4 q, int bx0, int by0, int LB) {
+    return 2 * rt_lbin(L, q, bx0, by0, LB) + ((__float_as_int(q.w) & kWOld) ? 0 : 1);
 }
 
 // list[0] = number of big tiles, list[1..]: the tiles; their cursor rows zeroed, kept_tile reset. One
@@ -301,30 +351,59 @@ __global__ __launch_bounds__(256) void k_rt_biglist(RorLaunch L, const int *tsta
     if (!((!dirty || dirty[t + 1] != dirty[t]) && n > kRorCap && a + n <= L.staged_cap)) return;
     B.list[1 + atomicAdd(&B.list[0], 1)] = t;
     if (kept_tile) kept_tile[t] = 0;
-    const int nlb1 = (L.TB + 2) * (L.TB + 2) + 1;
+    const int nlb1 = 2 * (L.TB + 2) * (L.TB + 2) + 1;
     int *row = B.cur + (size_t)t * nlb1;   // (rows are not 16 B aligned: plain stores)
     for (int i = 0; i < nlb1; ++i) row[i] = 0;
 }
 
-// the chunk [k0, k1) of big tile i of the list
-__device__ __forceinline__ void big_chunk(const RorLaunch &L, const int *tstart, int t, int &a, int &k0, int &k1) {
+// choff[i] = chunks of the big tiles before list entry i; choff[nbig] = all chunks
+__global__ __launch_bounds__(1024) void k_rt_bigchunks(const int *tstart, BigBufs B) {
+    typedef hipcub::BlockScan<int, 1024> Scan;
+    __shared__ typename Scan::TempStorage tmp;
+    const int nbig = B.list[0];
+    int base = 0;
+    for (int i0 = 0; i0 < nbig; i0 += 1024) {
+        const int i = i0 + threadIdx.x;
+        int c = 0;
+        if (i < nbig) {
+            const int t = B.list[1 + i];
+            c = (tstart[t + 1] - tstart[t] + kBigChunk - 1) / kBigChunk;
+        }
+        int before, total;
+        Scan(tmp).ExclusiveSum(c, before, total);
+        if (i < nbig) B.choff[i] = base + before;
+        base += total;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) B.choff[nbig] = base;
+}
+__device__ __forceinline__ int big_nchunks(const BigBufs &B) { return B.choff[B.list[0]]; }
+// chunk c of all big tiles -> its tile t (first record a) and the range [k0, k1) of the tile's list
+__device__ __forceinline__ void big_chunk(const int *tstart, const BigBufs &B, int c, int &t, int &a, int &k0, int &k1) {
+    int lo = 0, hi = B.list[0] - 1;   // the last list entry i with choff[i] <= c
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (B.choff[mid] <= c) lo = mid;
+        else hi = mid - 1;
+    }
+    t = B.list[1 + lo];
     a = tstart[t];
     const int n = tstart[t + 1] - a;
-    k0 = (int)((long long)n * blockIdx.x / kBigC);
-    k1 = (int)((long long)n * (blockIdx.x + 1) / kBigC);
+    k0 = (c - B.choff[lo]) * kBigChunk;
+    k1 = min(n, k0 + kBigChunk);
 }
 
 __global__ __launch_bounds__(kBigTB) void k_rt_bighist(RorLaunch L, const int *tstart, const float4 *staged, BigBufs B) {
-    __shared__ int h[kRtMaxLocalBins + 1];
-    const int nbig = B.list[0], LB = L.TB + 2, nlb = LB * LB;
-    for (int i = blockIdx.y; i < nbig; i += gridDim.y) {
-        const int t = B.list[1 + i], tx = t % L.ntx, ty = t / L.ntx;
-        int a, k0, k1;
-        big_chunk(L, tstart, t, a, k0, k1);
+    __shared__ int h[kBigBins + 1];
+    const int nch = big_nchunks(B), LB = L.TB + 2, nlb = 2 * LB * LB;
+    for (int c = blockIdx.x; c < nch; c += gridDim.x) {
+        int t, a, k0, k1;
+        big_chunk(tstart, B, c, t, a, k0, k1);
+        const int tx = t % L.ntx, ty = t / L.ntx;
         for (int b = threadIdx.x; b < nlb; b += kBigTB) h[b] = 0;
         __syncthreads();
         for (int k = k0 + threadIdx.x; k < k1; k += kBigTB)
-            atomicAdd(&h[rt_lbin(L, staged[a + k], tx * L.TB - 1, ty * L.TB - 1, LB)], 1);
+            atomicAdd(&h[rt_sbin(L, staged[a + k], tx * L.TB - 1, ty * L.TB - 1, LB)], 1);
         __syncthreads();
         int *tot = B.cur + (size_t)t * (nlb + 1);
         for (int b = threadIdx.x; b < nlb; b += kBigTB)
@@ -334,10 +413,10 @@ __global__ __launch_bounds__(kBigTB) void k_rt_bighist(RorLaunch L, const int *t
 }
 
 __global__ __launch_bounds__(1024) void k_rt_bigscan(RorLaunch L, const int *tstart, BigBufs B) {
-    constexpr int kSeg = (kRtMaxLocalBins + 1023) / 1024;
+    constexpr int kSeg = (kBigBins + 1023) / 1024;
     typedef hipcub::BlockScan<int, 1024> Scan;
     __shared__ typename Scan::TempStorage tmp;
-    const int nbig = B.list[0], nlb = (L.TB + 2) * (L.TB + 2);
+    const int nbig = B.list[0], nlb = 2 * (L.TB + 2) * (L.TB + 2);
     for (int i = blockIdx.x; i < nbig; i += gridDim.x) {
         const int t = B.list[1 + i];
         int *tot = B.cur + (size_t)t * (nlb + 1), *st = B.starts + (size_t)t * (nlb + 1);
@@ -364,16 +443,16 @@ __global__ __launch_bounds__(1024) void k_rt_bigscan(RorLaunch L, const int *tst
 
 __global__ __launch_bounds__(kBigTB) void k_rt_bigscatter(RorLaunch L, const int *tstart, const float4 *staged,
                                                           float4 *scratch, BigBufs B) {
-    __shared__ int h[kRtMaxLocalBins + 1];
-    const int nbig = B.list[0], LB = L.TB + 2, nlb = LB * LB;
-    for (int i = blockIdx.y; i < nbig; i += gridDim.y) {
-        const int t = B.list[1 + i], tx = t % L.ntx, ty = t / L.ntx;
+    __shared__ int h[kBigBins + 1];
+    const int nch = big_nchunks(B), LB = L.TB + 2, nlb = 2 * LB * LB;
+    for (int c = blockIdx.x; c < nch; c += gridDim.x) {
+        int t, a, k0, k1;
+        big_chunk(tstart, B, c, t, a, k0, k1);
+        const int tx = t % L.ntx, ty = t / L.ntx;
         const int bx0 = tx * L.TB - 1, by0 = ty * L.TB - 1;
-        int a, k0, k1;
-        big_chunk(L, tstart, t, a, k0, k1);
         for (int b = threadIdx.x; b < nlb; b += kBigTB) h[b] = 0;
         __syncthreads();
-        for (int k = k0 + threadIdx.x; k < k1; k += kBigTB) atomicAdd(&h[rt_lbin(L, staged[a + k], bx0, by0, LB)], 1);
+        for (int k = k0 + threadIdx.x; k < k1; k += kBigTB) atomicAdd(&h[rt_sbin(L, staged[a + k], bx0, by0, LB)], 1);
         __syncthreads();
         int *cur = B.cur + (size_t)t * (nlb + 1);
         for (int b = threadIdx.x; b < nlb; b += kBigTB)
@@ -381,7 +460,7 @@ __global__ __launch_bounds__(kBigTB) void k_rt_bigscatter(RorLaunch L, const int
         __syncthreads();
         for (int k = k0 + threadIdx.x; k < k1; k += kBigTB) {
             const float4 v = staged[a + k];
-            scratch[a + atomicAdd(&h[rt_lbin(L, v, bx0, by0, LB)], 1)] = v;
+            scratch[a + atomicAdd(&h[rt_sbin(L, v, bx0, by0, LB)], 1)] = v;
         }
         __syncthreads();
     }
@@ -389,24 +468,33 @@ __global__ __launch_bounds__(kBigTB) void k_rt_bigscatter(RorLaunch L, const int
 
 // kept_tile (optional): the tile's count of kept owned candidates; dirty (optional): only tiles with
 // dirty[t + 1] > dirty[t] are (re)counted — the streaming map's tiles that received scan points.
-// BIG = false: one workgroup per tile that fits LDS (the others are left to BIG); BIG = true: one
-// workgroup per (listed big tile, chunk of its list), points searched in the scratch range.
+// BIG = false: one workgroup per tile that fits LDS (the others are left to BIG); BIG = true: workgroups
+// loop over the big tiles' chunks, points searched in the scratch range.
 template <bool BIG>
 __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *tstart, float4 *staged,
                                                         const float4 *scratch, uint64_t *rbits,
                                                         unsigned long long *counters, int *kept_tile,
                                                         const int *dirty, BigBufs B) {
     __shared__ float4 pts[BIG ? 1 : kRorCap];
-    __shared__ int bstart[kRtMaxLocalBins + 1];
+    __shared__ int bstart[(BIG ? kBigBins : kRtMaxLocalBins) + 1];
     __shared__ unsigned long long win[kRtWinWords];
     __shared__ unsigned kept_wg;
+    __shared__ int q_n, q_k[kRtQCap];   // candidates left to the waves
     const int tid = threadIdx.x;
-    const int nbig = BIG ? B.list[0] : 1;
-    for (int it = BIG ? blockIdx.y : 0; it < nbig; it += BIG ? gridDim.y : 1) {
-    const int t = BIG ? B.list[1 + it] : rt_xcd_block(blockIdx.x, gridDim.x);
+    const int nit = BIG ? big_nchunks(B) : 1;
+    for (int it = BIG ? blockIdx.x : 0; it < nit; it += BIG ? gridDim.x : 1) {
+    int t, a, k0, k1;                               // the tile, its first record, the range of its runs
+    if (BIG) {
+        big_chunk(tstart, B, it, t, a, k0, k1);
+    } else {
+        t = rt_xcd_block(blockIdx.x, gridDim.x);
+        a = tstart[t];
+        k0 = 0;
+        k1 = tstart[t + 1] - a;
+    }
+    const int n = tstart[t + 1] - a;
     const int tx = t % L.ntx, ty = t / L.ntx;
     if (!BIG && dirty && dirty[t + 1] == dirty[t]) return;
-    const int a = tstart[t], n = tstart[t + 1] - a;   // the tile's runs
     if (!BIG) {
         if (n > kRorCap && a + n <= L.staged_cap) {   // a big tile: k_rt_ror<true>
             // (not launched this frame: the frame is redone with the big-tile kernels, seedgen.hip)
@@ -418,12 +506,7 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
             return;
         }
     }
-    int k0 = 0, k1 = n;
-    if (BIG) {
-        int a_;
-        big_chunk(L, tstart, t, a_, k0, k1);
-    }
-    if (tid == 0) kept_wg = 0;
+    if (tid == 0) { kept_wg = 0; q_n = 0; }
     const int LB = L.TB + 2;                        // local bins: the tile's bins and a ring of halo bins
     const int bx0 = tx * L.TB - 1, by0 = ty * L.TB - 1;
     const int nlb = LB * LB;
@@ -435,8 +518,8 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
     const bool use_win = L.win_rows > 0;
     if (use_win)
         for (int i = tid; i < L.win_rows * L.win_w; i += kRorThreads) win[i] = 0ull;
-    if (BIG) {   // bin offsets from k_rt_bigscan (through the kernel boundary)
-        for (int i = tid; i <= nlb; i += kRorThreads) bstart[i] = B.starts[(size_t)t * (nlb + 1) + i];
+    if (BIG) {   // sub-bin offsets from k_rt_bigscan (through the kernel boundary)
+        for (int i = tid; i <= 2 * nlb; i += kRorThreads) bstart[i] = B.starts[(size_t)t * (2 * nlb + 1) + i];
     } else {
         for (int i = tid; i <= nlb; i += kRorThreads) bstart[i] = 0;
     }
@@ -513,29 +596,83 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
         else
             atomicOr(reinterpret_cast<unsigned long long *>(&rbits[(size_t)r * L.WWr + (bxw >> 6)]), bit);
     };
+    // the neighbour ranges of a candidate, in scan order: a big tile's counted candidate -> the new halves
+    // of its 3 x 3 bins (9 ranges); else its 3 bin rows, own row first
+    auto range = [&](bool counted, int lx, int ly, int i, int &r0, int &r1) {
+        if (counted) {
+            const int b = (ly - 1 + i / 3) * LB + lx - 1 + i % 3;
+            r0 = bstart[2 * b + 1]; r1 = bstart[2 * b + 2];
+        } else {
+            const int rb = (ly + (i == 0 ? 0 : (i == 1 ? -1 : 1))) * LB + lx - 1;
+            if (BIG) { r0 = bstart[2 * rb]; r1 = bstart[2 * rb + 6]; }
+            else { r0 = bstart[rb]; r1 = bstart[rb + 3]; }
+        }
+    };
+    auto decide = [&](float4 p, int k, int cnt) {
+        if (cnt >= L.need) on_kept(p, k);
+        else if (store) {                       // below need: remember the full count
+            const float cw = __int_as_float(1 | kWCounted | (cnt << kWCntShift));
+            if (BIG) P[k].w = cw;
+            else pts[k].w = cw;
+        }
+    };
     for (int k = k0 + tid; k < k1; k += kRorThreads) {
         const float4 p = BIG ? P[k] : pts[k];
-        const int w = __float_as_int(p.w);
-        if (!w) continue;                       // neighbour only
-        if (w == 2) { prev_kept(p); continue; }
+        const int w = __float_as_int(p.w), cls = w & kWClass;
+        if (!cls) continue;                     // neighbour only
+        if (cls == 2) { prev_kept(p); continue; }
         int bx, by;
         rt_bin(L, p.x, p.y, bx, by);
         const int lx = bx - bx0, ly = by - by0;
-        int cnt = AOS_RT_VARIANT == 1 ? L.need : 0;
-#pragma unroll
-        for (int rr = 0; rr < 3; ++rr) {        // own bin row first: the likeliest neighbours
-            const int yy = ly + (rr == 0 ? 0 : (rr == 1 ? -1 : 1));
-            if (cnt >= L.need) break;
-            const int r0 = yy * LB + lx - 1;
-            cnt = BIG ? rt_scan(L, p, P, bstart[r0], bstart[r0 + 3], cnt)
-                      : rt_scan(L, p, pts, bstart[r0], bstart[r0 + 3], cnt);
+        const bool counted = BIG && (w & kWCounted);   // the store's points are counted: the new ones only
+        const int nr = counted ? 9 : 3, cnt0 = AOS_RT_VARIANT == 1 ? L.need : (counted ? w >> kWCntShift : 0);
+        int cnt = cnt0, budget = BIG ? kRtBudgetBig : kRtBudgetLds;
+        for (int i = 0; i < nr && cnt < L.need && budget >= 0; ++i) {
+            int r0, r1;
+            range(counted, lx, ly, i, r0, r1);
+            cnt = BIG ? rt_scan_b(L, p, P, r0, r1, cnt, budget) : rt_scan_b(L, p, pts, r0, r1, cnt, budget);
         }
-        if (cnt >= L.need) on_kept(p, k);
+        if (cnt < L.need && budget < 0) {        // undecided within the budget
+            const int slot = atomicAdd(&q_n, 1);
+            if (slot < kRtQCap) { q_k[slot] = k; continue; }
+            cnt = cnt0;                          // (queue full: this thread counts it alone)
+            for (int i = 0; i < nr && cnt < L.need; ++i) {
+                int r0, r1;
+                range(counted, lx, ly, i, r0, r1);
+                cnt = BIG ? rt_scan(L, p, P, r0, r1, cnt) : rt_scan(L, p, pts, r0, r1, cnt);
+            }
+        }
+        decide(p, k, cnt);
     }
-    // the store goes back bin-sorted with its kept marks: a fitting tile rewrites its list, a big tile's
-    // chunk its range of the sorted scratch list (each k by the thread that marked it)
+    __syncthreads();
+    {   // the queued candidates, one wave each
+        const int nq = min(q_n, kRtQCap), lane = tid & 63;
+        for (int i = tid >> 6; i < nq; i += kRorThreads / 64) {
+            const int k = q_k[i];
+            const float4 p = BIG ? P[k] : pts[k];
+            const int w = __float_as_int(p.w);
+            int bx, by;
+            rt_bin(L, p.x, p.y, bx, by);
+            const int lx = bx - bx0, ly = by - by0;
+            const bool counted = BIG && (w & kWCounted);
+            int cnt = counted ? w >> kWCntShift : 0;
+            for (int r = 0; r < (counted ? 9 : 3) && cnt < L.need; ++r) {
+                int r0, r1;
+                range(counted, lx, ly, r, r0, r1);
+                cnt = BIG ? rt_wave_scan(L, p, P, r0, r1, cnt, lane) : rt_wave_scan(L, p, pts, r0, r1, cnt, lane);
+            }
+            if (lane == 0) decide(p, k, cnt);
+        }
+    }
+    __syncthreads();
+    // the store goes back bin-sorted with its kept marks and counts, every point marked as the store's: a
+    // fitting tile rewrites its list, a big tile's chunk its range of the sorted scratch list
     if (store)
-        for (int k = k0 + tid; k < k1; k += kRorThreads) staged[a + k] = BIG ? P[k] : pts[k];
+        for (int k = k0 + tid; k < k1; k += kRorThreads) {
+            float4 v = BIG ? P[k] : pts[k];
+            v.w = __int_as_float(__float_as_int(v.w) | kWOld);
+            staged[a + k] = v;
+        }
     __syncthreads();
     if (use_win)
         for (int i = tid; i < L.win_rows * L.win_w; i += kRorThreads) {
@@ -685,23 +822,25 @@ void launch_rt_scatter(const RorLaunch &L, int *H, const int *tstart, int G, flo
     }
 }
 
-size_t rt_bigbins_ints(const RorLaunch &L) { return 2 * (size_t)L.ntiles * ((L.TB + 2) * (L.TB + 2) + 1) + 1 + L.ntiles; }
+size_t rt_bigbins_ints(const RorLaunch &L) {
+    return 2 * (size_t)L.ntiles * (2 * (L.TB + 2) * (L.TB + 2) + 1) + 1 + L.ntiles + L.ntiles + 1;
+}
 
 void launch_rt_ror(const RorLaunch &L, const int *tstart, float4 *staged, float4 *scratch, int *bigbins,
                    uint64_t *rbits, unsigned long long *counters, int *kept_tile, const int *dirty, hipStream_t s) {
     if (!L.ntiles) return;
     const BigBufs B = big_bufs(L, bigbins);
-    const dim3 gb(kBigC, kBigY);
     if (L.big_ok) {   // tiles beyond the LDS capacity: listed, chunked, sorted and counted by the big kernels
         AOS_HIP(hipMemsetAsync(B.list, 0, sizeof(int), s));
         k_rt_biglist<<<(L.ntiles + 255) / 256, 256, 0, s>>>(L, tstart, B, kept_tile, dirty);
-        k_rt_bighist<<<gb, kBigTB, 0, s>>>(L, tstart, staged, B);
+        k_rt_bigchunks<<<1, 1024, 0, s>>>(tstart, B);
+        k_rt_bighist<<<kBigGrid, kBigTB, 0, s>>>(L, tstart, staged, B);
         k_rt_bigscan<<<kBigY, 1024, 0, s>>>(L, tstart, B);
-        k_rt_bigscatter<<<gb, kBigTB, 0, s>>>(L, tstart, staged, scratch, B);
+        k_rt_bigscatter<<<kBigGrid, kBigTB, 0, s>>>(L, tstart, staged, scratch, B);
     }
     k_rt_ror<false><<<L.ntiles, kRorThreads, 0, s>>>(L, tstart, staged, scratch, rbits, counters, kept_tile, dirty, B);
     if (L.big_ok)
-        k_rt_ror<true><<<gb, kRorThreads, 0, s>>>(L, tstart, staged, scratch, rbits, counters, kept_tile, dirty, B);
+        k_rt_ror<true><<<kBigGrid, kRorThreads, 0, s>>>(L, tstart, staged, scratch, rbits, counters, kept_tile, dirty, B);
     AOS_HIP(hipGetLastError());
 }
 

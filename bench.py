@@ -57,9 +57,11 @@ def parse(argv=None):
     ap.add_argument("--no-tiled-rate", action="store_true",
                     help="--gpus N > 1: skip the extra tiled C3 measurement (tiled key)")
     ap.add_argument("--trace", action="store_true", help="per-step timeline on stderr")
-    ap.add_argument("--depth", type=int, default=8,
+    ap.add_argument("--depth", type=int, default=4,
                     help="pipelined loop: GVD jobs in flight (aos_gvd_pipeline_depth): frames are independent, so "
-                         "frame k's GVD runs beside the GVDs of frames k-1 .. k-depth+1, each replay on its own core")
+                         "frame k's GVD runs beside the GVDs of frames k-1 .. k-depth+1, each replay on its own core. "
+                         "4 keeps the frame latency near the sequential frame's; 8 adds ~10 %% throughput for "
+                         "~20 ms of latency (DESIGN.md §5)")
     ap.add_argument("--pipelined", action="store_true",
                     help="make the pipelined loop the timed region (value = its throughput) instead of the "
                          "sequential per-frame loop")
