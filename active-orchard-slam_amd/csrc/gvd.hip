@@ -286,8 +286,12 @@ __global__ void k_edge_emit(const int *keep, const int *kpos, const int2 *ft, in
 // ------------------------------------------------------------------ g8 label points
 struct LabelRow { double ex, ey, ox, oy; double deg, cs, sn; };  // endpoint, other endpoint, angle, host cos/sin
 // one workgroup per (row, label): arg-min over the filtered nodes (gvd:731-774); castRay fallback (:788)
+// Pass 0 reads only the nodes of the 3 x 3 cells (of >= 5.01 m: the hash hl over the sorted node keys
+// lsk / lsi) around the endpoint, which hold every node with z <= 25 (1 + 1e-12); a job scanned all
+// ~10^5 nodes before (≈ 177 us per C2 frame).
 __global__ __launch_bounds__(256) void k_label_points(const LabelRow *jobs, int nj, const double2 *nodes, int Mn, GridG g,
-                                                      const int8_t *sk, double2 *pts, int *valid) {
+                                                      const int8_t *sk, HashG hl, const int *lsk, const int *lsi,
+                                                      double2 *pts, int *valid) {
     const int jb = blockIdx.x;
     if (jb >= nj) return;
     const LabelRow J = jobs[jb];
@@ -303,22 +307,32 @@ __global__ __launch_bounds__(256) void k_label_points(const LabelRow *jobs, int 
     // candidate, the global arg-min is among them. Pass 1 (rare) scans everything.
     __shared__ double sb[256];
     __shared__ int si[256];
+    int cx, cy;
+    cell_of(hl, J.ex, J.ey, cx, cy);
     for (int pass = 0; pass < 2; ++pass) {
         double best = 1.7976931348623157e308;
         int bi = INT_MAX;
-        for (int i = threadIdx.x; i < Mn; i += blockDim.x) {
+        auto test = [&](int i) {
             double dx = nodes[i].x - J.ex, dy = nodes[i].y - J.ey;
             double z = dx * dx + dy * dy;
-            if (pass == 0 && !(z <= 25.0 * (1.0 + 1e-12))) continue;
+            if (pass == 0 && !(z <= 25.0 * (1.0 + 1e-12))) return;
             double dist = sqrt(z);
-            if (dist < 0.5 || dist > fmax(9.0, g.diag2)) continue;
+            if (dist < 0.5 || dist > fmax(9.0, g.diag2)) return;
             double nx = dx, ny = dy;
             if (z > 0.0) { double s = sqrt(z); nx = dx / s; ny = dy / s; }
-            if (outx * nx + outy * ny < 0.0) continue;
+            if (outx * nx + outy * ny < 0.0) return;
             double dp = perx * nx + pery * ny;
-            if (m90) { if (dp > 0.0) continue; }
-            else if (p90) { if (dp < 0.0) continue; }
+            if (m90) { if (dp > 0.0) return; }
+            else if (p90) { if (dp < 0.0) return; }
             if (dist < best || (dist == best && i < bi)) { best = dist; bi = i; }
+        };
+        if (pass == 0) {
+            for (int yy = max(cy - 1, 0); yy <= min(cy + 1, hl.ny - 1); ++yy) {
+                const int k0 = lb(lsk, Mn, yy * hl.nx + max(cx - 1, 0)), k1 = lb(lsk, Mn, yy * hl.nx + min(cx + 1, hl.nx - 1) + 1);
+                for (int k = k0 + threadIdx.x; k < k1; k += blockDim.x) test(lsi[k]);
+            }
+        } else {
+            for (int i = threadIdx.x; i < Mn; i += blockDim.x) test(i);
         }
         sb[threadIdx.x] = best; si[threadIdx.x] = bi;
         __syncthreads();
@@ -381,12 +395,58 @@ __global__ __launch_bounds__(256) void k_label_points(const LabelRow *jobs, int 
 }
 
 // ------------------------------------------------------------------ g9 node labels (publishGraph gvd:920-995)
-__global__ void k_node_labels(const double2 *nodes, int Mn, const double2 *lp, const int *lv, int n_rows, int *mask,
-                              int *cidx, int *count, const int *off, int *lcl, int *lty) {
+// label point j = 4 r + k (valid ones) -> its cell of the 0.1 m hash hq; invalid -> INT_MAX
+__global__ void k_label_keys(const double2 *lp, const int *lv, int nj, HashG hq, int *keys, int *idx) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nj) return;
+    int cx, cy;
+    cell_of(hq, lp[j].x, lp[j].y, cx, cy);
+    keys[j] = lv[j] ? cy * hq.nx + cx : INT_MAX;
+    idx[j] = j;
+}
+// A node matches label point j iff |dx|, |dy| < 0.1 (and the reference's distance test), so only the
+// label points of its 3 x 3 cells of the 0.1 m hash can match (qsk / qsj: sorted keys and their j); the
+// matches are put back in (r, k) order. More than kNodeMatch matches: the plain loop over every label point.
+constexpr int kNodeMatch = 16;
+__global__ void k_node_labels(const double2 *nodes, int Mn, const double2 *lp, const int *lv, int n_rows, HashG hq,
+                              const int *qsk, const int *qsj, int *mask, int *cidx, int *count, const int *off,
+                              int *lcl, int *lty) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= Mn) return;
     const double2 p = nodes[i];
     int m = 0, ci = -1, cnt = 0, w = off ? off[i] : 0;
+    {
+        int js[kNodeMatch], nm = 0;
+        bool over = false;
+        int cx, cy;
+        cell_of(hq, p.x, p.y, cx, cy);
+        const int nq = 4 * n_rows;
+        for (int yy = max(cy - 1, 0); yy <= min(cy + 1, hq.ny - 1); ++yy) {
+            const int k0 = lb(qsk, nq, yy * hq.nx + max(cx - 1, 0)), k1 = lb(qsk, nq, yy * hq.nx + min(cx + 1, hq.nx - 1) + 1);
+            for (int q = k0; q < k1; ++q) {
+                const int j = qsj[q];
+                double dx = p.x - lp[j].x, dy = p.y - lp[j].y;
+                if (!(fabs(dx) < 0.1) || !(fabs(dy) < 0.1)) continue;
+                if (sqrt(dx * dx + dy * dy) < 0.1) {
+                    if (nm < kNodeMatch) js[nm++] = j;
+                    else over = true;
+                }
+            }
+        }
+        if (!over) {
+            for (int a = 1; a < nm; ++a)   // (r, k) order
+                for (int b = a; b > 0 && js[b - 1] > js[b]; --b) { const int t = js[b]; js[b] = js[b - 1]; js[b - 1] = t; }
+            for (int a = 0; a < nm; ++a) {
+                const int r = js[a] >> 2, k = js[a] & 3;
+                m |= 1 << k;
+                if (off) { lcl[w + cnt] = r; lty[w + cnt] = k; }
+                ++cnt;
+                if (ci == -1) ci = r;
+            }
+            if (!off) { mask[i] = m; cidx[i] = ci; count[i] = cnt; }
+            return;
+        }
+    }
     for (int r = 0; r < n_rows; ++r)
         for (int k = 0; k < 4; ++k) {
             if (!lv[4 * r + k]) continue;
@@ -512,7 +572,7 @@ __global__ void k_facet_emit(const int *qe, const int *vfirst, const int *off, c
 struct GvdScratch {
     DevBuf raw, ok, leaders, merged, owner, oidx, sowner, sidx, tmp, edges_f, occ, occ_ok, bp, kept_occ, keys, idx, skeys,
         sidx2, near_idx, pk, pidx, pskeys, psidx, pcount, poff, plist, ft, ckey, cvalid, pass, k2, occ_idx, sk2, socc, selected,
-        inside, ipos, nodes, keep, kpos, edges, lens, jobs, lpts, lval, lmask, lcidx, lcount, loff, lcl, lty, scan_tmp,
+        inside, ipos, nodes, keep, kpos, edges, lens, jobs, nkeys, nidx, qkeys, qidx, lpts, lval, lmask, lcidx, lcount, loff, lcl, lty, scan_tmp,
         gather;
     FacetBufs fb;
 };
@@ -981,16 +1041,32 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     if (nj) {
         LabelRow *d_jobs = dev<LabelRow>(S.jobs, nj);
         AOS_HIP(hipMemcpyAsync(d_jobs, jobs.data(), sizeof(LabelRow) * nj, hipMemcpyHostToDevice, s));
-        k_label_points<<<nj, 256, 0, s>>>(d_jobs, nj, d_nodes, Mn, g, in.d_skeleton, d_lp, d_lv);
+        // the nodes hashed in cells of 5.01 m (k_label_points' pass 0)
+        const HashG hl = make_hash(g.minx - 10.0, g.maxx + 10.0, g.miny - 10.0, g.maxy + 10.0, 5.01);
+        int *d_nk = dev<int>(S.nkeys, 2 * (size_t)Mn), *d_ni = dev<int>(S.nidx, 2 * (size_t)Mn);
+        k_cell_keys<<<cdiv(Mn, 256), 256, 0, s>>>(d_nodes, Mn, hl, d_nk, d_ni);
+        size_t tb = 0;
+        AOS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, d_nk, d_nk + Mn, d_ni, d_ni + Mn, Mn, 0, 32, s));
+        AOS_HIP(hipcub::DeviceRadixSort::SortPairs(S.tmp.ensure(tb), tb, d_nk, d_nk + Mn, d_ni, d_ni + Mn, Mn, 0, 32, s));
+        k_label_points<<<nj, 256, 0, s>>>(d_jobs, nj, d_nodes, Mn, g, in.d_skeleton, hl, d_nk + Mn, d_ni + Mn, d_lp, d_lv);
     }
     // ---- g9 node labels
     int *d_mask = dev<int>(S.lmask, Mn), *d_cidx = dev<int>(S.lcidx, Mn), *d_lcnt = dev<int>(S.lcount, Mn + 1),
         *d_loff = dev<int>(S.loff, Mn + 1);
     const int nlr = nj / 4;
     int n_entries = 0;
+    const HashG hq = make_hash(g.minx - 1.0, g.maxx + 1.0, g.miny - 1.0, g.maxy + 1.0, 0.1);
+    int *d_qk = dev<int>(S.qkeys, 2 * (size_t)std::max(nj, 1)), *d_qj = dev<int>(S.qidx, 2 * (size_t)std::max(nj, 1));
+    if (Mn > 0 && nj > 0) {   // the label points hashed in cells of 0.1 m (k_node_labels)
+        k_label_keys<<<cdiv(nj, 256), 256, 0, s>>>(d_lp, d_lv, nj, hq, d_qk, d_qj);
+        size_t tb = 0;
+        AOS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, d_qk, d_qk + nj, d_qj, d_qj + nj, nj, 0, 32, s));
+        AOS_HIP(hipcub::DeviceRadixSort::SortPairs(S.tmp.ensure(tb), tb, d_qk, d_qk + nj, d_qj, d_qj + nj, nj, 0, 32, s));
+    }
     if (Mn > 0) {
         AOS_HIP(hipMemsetAsync(d_lcnt + Mn, 0, sizeof(int), s));
-        k_node_labels<<<cdiv(Mn, 256), 256, 0, s>>>(d_nodes, Mn, d_lp, d_lv, nlr, d_mask, d_cidx, d_lcnt, nullptr, nullptr, nullptr);
+        k_node_labels<<<cdiv(Mn, 256), 256, 0, s>>>(d_nodes, Mn, d_lp, d_lv, nlr, hq, d_qk + nj, d_qj + nj, d_mask, d_cidx,
+                                                    d_lcnt, nullptr, nullptr, nullptr);
         scan_excl(S.scan_tmp, d_lcnt, d_loff, Mn + 1, s);
         AOS_HIP(hipMemcpyAsync(h_sc, d_loff + Mn, sizeof(int), hipMemcpyDeviceToHost, s));
         G.sev.sync(s);
@@ -998,7 +1074,9 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     }
     tr.mark("labels");
     int *d_lcl = dev<int>(S.lcl, n_entries), *d_lty = dev<int>(S.lty, n_entries);
-    if (n_entries) k_node_labels<<<cdiv(Mn, 256), 256, 0, s>>>(d_nodes, Mn, d_lp, d_lv, nlr, nullptr, nullptr, nullptr, d_loff, d_lcl, d_lty);
+    if (n_entries)
+        k_node_labels<<<cdiv(Mn, 256), 256, 0, s>>>(d_nodes, Mn, d_lp, d_lv, nlr, hq, d_qk + nj, d_qj + nj, nullptr, nullptr,
+                                                    nullptr, d_loff, d_lcl, d_lty);
 
     // ---- outputs: one gather kernel, one D2H copy into the state's pinned buffer, host copies out
     G.nodes_xy.resize(2 * (size_t)Mn); G.labels.resize(Mn); G.cluster_idx.resize(Mn); G.label_counts.resize(Mn);

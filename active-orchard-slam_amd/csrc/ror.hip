@@ -290,7 +290,7 @@ __device__ __forceinline__ int rt_wave_scan(const RorLaunch &L, float4 p, Pts pt
     return cnt;
 }
 #ifndef AOS_RT_BUDGET_LDS
-#define AOS_RT_BUDGET_LDS 64
+#define AOS_RT_BUDGET_LDS 256
 #endif
 constexpr int kRtBudgetBig = 64, kRtBudgetLds = AOS_RT_BUDGET_LDS, kRtQCap = 512;
 
