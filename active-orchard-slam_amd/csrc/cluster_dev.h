@@ -48,6 +48,34 @@ __host__ __device__ inline bool d_pip(double px, double py, const double *poly, 
     return inside;
 }
 
+// isPointInPolygon for every cell of one grid row: the crossing abscissa of an edge,
+// (pjx - pix) * (py - piy) / dy + pix, does not depend on px, so a workgroup whose cells share py
+// computes the crossings of the edges that straddle py once (LDS) and a cell's test is its parity of
+// px < crossing: the same double operations and comparisons as d_pip. Polygons with more than
+// kRowCrossMax straddling edges fall back to d_pip.
+constexpr int kRowCrossMax = 256;
+__device__ inline bool row_crossings(const double *poly, int n, double py, double *xc, int *nxc) {
+    if (threadIdx.x == 0) *nxc = 0;
+    __syncthreads();
+    if (n >= 3)
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            const int j = i == 0 ? n - 1 : i - 1;
+            const double pix = poly[2 * i], piy = poly[2 * i + 1], pjx = poly[2 * j], pjy = poly[2 * j + 1];
+            const double dy = pjy - piy;
+            if (fabs(dy) > 1e-9 && ((piy > py) != (pjy > py))) {
+                const int k = atomicAdd(nxc, 1);
+                if (k < kRowCrossMax) xc[k] = (pjx - pix) * (py - piy) / dy + pix;
+            }
+        }
+    __syncthreads();
+    return *nxc <= kRowCrossMax;
+}
+__device__ __forceinline__ bool pip_row(double px, const double *xc, int nxc) {
+    bool inside = false;
+    for (int k = 0; k < nxc; ++k) inside ^= px < xc[k];
+    return inside;
+}
+
 // float world coordinate of a cell: origin + float(x) * res (float product, double add, to float)
 __host__ __device__ __forceinline__ float cell_world(double o, int i, float res) { return (float)(o + (double)((float)i * res)); }
 

@@ -97,16 +97,21 @@ struct TileView {
 };
 
 __global__ void k_dist_fg(const uint64_t *win, TileView T, GridC g, const double *poly, int np, uint64_t *fg, int *cnt) {
+    __shared__ double xc[kRowCrossMax];
+    __shared__ int nxc;
     const int k = blockIdx.x * blockDim.x + threadIdx.x, r = blockIdx.y;
-    if (k >= T.nc || r >= T.nr) return;
-    uint64_t w = win[(size_t)(T.oy + r) * T.WWl + T.oc + k], o = 0;
     const int gy = T.y0 + r;
     const double wy = cell_world(g.oy, gy, g.res);
+    const bool rowwise = row_crossings(poly, np, wy, xc, &nxc);   // (block-uniform; synchronises)
+    if (k >= T.nc || r >= T.nr) return;
+    uint64_t w = win[(size_t)(T.oy + r) * T.WWl + T.oc + k], o = 0;
     while (w) {
         const int b = __ffsll((long long)w) - 1;
         w &= w - 1;
         const int gx = 64 * (T.c0 + k) + b;
-        if (gx < g.W && d_pip(cell_world(g.ox, gx, g.res), wy, poly, np)) o |= 1ull << b;
+        if (gx >= g.W) continue;
+        const double wx = cell_world(g.ox, gx, g.res);
+        if (rowwise ? pip_row(wx, xc, nxc) : d_pip(wx, wy, poly, np)) o |= 1ull << b;
     }
     fg[(size_t)r * T.nc + k] = o;
     cnt[(size_t)r * T.nc + k] = __popcll(o);

@@ -34,16 +34,20 @@ constexpr int kReplayThreads = 8;   // host threads for the exact BFS replays of
 
 // ------------------------------------------------------------------ foreground = skeleton inside polygon
 __global__ void k_fg(const uint64_t *skel, uint64_t *fg, int *cnt, GridC g, const double *poly, int np) {
-    int c = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    __shared__ double xc[kRowCrossMax];
+    __shared__ int nxc;
+    const int c = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    const double wy = y < g.H ? cell_world(g.oy, y, g.res) : 0.0;
+    const bool rowwise = row_crossings(poly, np, wy, xc, &nxc);   // (block-uniform; synchronises)
     if (c >= g.WW || y >= g.H) return;
     size_t wi = (size_t)y * g.WW + c;
     uint64_t w = skel[wi], o = 0;
-    const double wy = cell_world(g.oy, y, g.res);
     while (w) {
         int b = __ffsll((long long)w) - 1;
         w &= w - 1;
         int x = c * 64 + b;
-        if (d_pip(cell_world(g.ox, x, g.res), wy, poly, np)) o |= 1ull << b;
+        const double wx = cell_world(g.ox, x, g.res);
+        if (rowwise ? pip_row(wx, xc, nxc) : d_pip(wx, wy, poly, np)) o |= 1ull << b;
     }
     fg[wi] = o;
     cnt[wi] = __popcll(o);

@@ -760,7 +760,9 @@ void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *c
         launch_draw_rect(d_skel, g, gx0, gy0, gx1, gy1, s);
     }
     // the two published grids go to host memory on the copy stream while the cluster / seed stage runs
-    if (want_host) {
+    // (AOS_GRID_COPY=1: after it instead; the copy's blit kernels share the CUs with the stage's kernels)
+    static const int grid_copy_mode = [] { const char *e = getenv("AOS_GRID_COPY"); return e ? atoi(e) : 0; }();
+    auto issue_grid_copy = [&]() {
         h_occ.ensure(std::max<size_t>(C, 1)); h_skel.ensure(std::max<size_t>(C, 1));
         if (!copy_stream) {
             AOS_HIP(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
@@ -770,13 +772,15 @@ void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *c
         AOS_HIP(hipStreamWaitEvent(copy_stream, copy_ready, 0));
         AOS_HIP(hipMemcpyAsync(h_occ.p, d_occ, C, hipMemcpyDeviceToHost, copy_stream));
         AOS_HIP(hipMemcpyAsync(h_skel.p, d_skel, C, hipMemcpyDeviceToHost, copy_stream));
-    }
+    };
+    if (want_host && grid_copy_mode == 0) issue_grid_copy();
 
     // ---------------- a8-a15 clusters, tree rows, seeds
     SeedStageIn sin{skel_bits, &geom, &poly, P.cluster_min_length, pre};
     SeedStageOut so;
     run_cluster_seed_stage(cs, sin, so, s, ev[4]);
     AOS_HIP(hipEventRecord(ev[5], s));
+    if (want_host && grid_copy_mode == 1) issue_grid_copy();
 
     unsigned long long *h_cnt = static_cast<unsigned long long *>(h_stats.ensure(64 + 8 * kRorCounters)) + 8;
     if (!clipped_total) AOS_HIP(hipMemcpyAsync(h_cnt, counters.p, 8 * kRorCounters, hipMemcpyDeviceToHost, s));
