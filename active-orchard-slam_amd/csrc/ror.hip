@@ -31,6 +31,7 @@
 #include <climits>
 #include <cmath>
 #include <stdexcept>
+#include <type_traits>
 
 #include "aos_internal.h"
 
@@ -76,6 +77,10 @@ __device__ __forceinline__ bool rt_candidate(const RorLaunch &L, float x, float 
     if (z < L.cminz || z > L.cmaxz) return false;
     if (x < L.cminx || x > L.cmaxx) return false;
     if (y < L.cminy || y > L.cmaxy) return false;
+    // the discs' union lies in x [-3.664, 69.023], y [0.727, 6.700] (centres +- 1): a point 0.01 or more
+    // outside that box has dx^2 >= 1.02 > 1 for every disc (float rounding moves dx^2 by 1 ulp), so the
+    // loop below cannot remove it
+    if (x < -3.68f || x > 69.04f || y < 0.71f || y > 6.72f) return true;
 #pragma unroll
     for (int e = 0; e < 11; ++e) {
         float dx = x - c_excl_rt[3 * e], dy = y - c_excl_rt[3 * e + 1];
@@ -249,6 +254,12 @@ constexpr int kRorThreads = AOS_RT_THREADS, kRorCap = 2048, kRorPer = kRorCap / 
 #ifndef AOS_RT_VARIANT   // timing experiments only (tools/ab_rt.sh): 1 = no neighbour scan, 2 = no raster
 #define AOS_RT_VARIANT 0
 #endif
+#ifndef AOS_RT_GROUP     // lanes per candidate in a fitting tile's neighbour counts (0: one lane each + wave queue)
+#define AOS_RT_GROUP 0
+#endif
+#ifndef AOS_RT_QLANE     // fitting tiles: queued (over-budget) candidates one lane each instead of one wave each
+#define AOS_RT_QLANE 1
+#endif
 
 
 template <class Pts>
@@ -267,6 +278,12 @@ __device__ __forceinline__ int rt_scan(const RorLaunch &L, float4 p, Pts pts, in
 // neighbourhood in which it finds too few neighbours: an outlier, up to ~10^4 points in a streaming
 // map's big tile) goes to the workgroup's queue and is counted by a whole wave, 64 points per step.
 // One lane walking such a neighbourhood alone bounded the kernel (~1 ms per scan at C4).
+// Fitting tiles (round 3, AOS_RT_QLANE): the kernel was VALU-issue-bound on divergence (C2: 1.1e8 VALU
+// wave-instructions for 5.6 M points; ~3 % of candidates are not kept and walk their whole 3 x 3
+// neighbourhood, so nearly every wave waited on one or two long walks). The first pass now gives each
+// lane 12 points; the queued candidates (~10 %) are walked one lane each with a budget of 96, packed
+// together, and only the few left after that go to the waves (k_rt_ror 171 -> 150 us at C2,
+// profiles/r03x_rorbench.log; 4 / 8 / 16 / 32 lanes per candidate were 238-411 us, r03t).
 template <class Pts>
 __device__ __forceinline__ int rt_scan_b(const RorLaunch &L, float4 p, Pts pts, int k0, int k1, int cnt, int &budget) {
     int k = k0;
@@ -290,14 +307,17 @@ __device__ __forceinline__ int rt_wave_scan(const RorLaunch &L, float4 p, Pts pt
     return cnt;
 }
 #ifndef AOS_RT_BUDGET_LDS
-#define AOS_RT_BUDGET_LDS 256
+#define AOS_RT_BUDGET_LDS 12
 #endif
-constexpr int kRtBudgetBig = 64, kRtBudgetLds = AOS_RT_BUDGET_LDS, kRtQCap = 512;
+#ifndef AOS_RT_BUDGET2
+#define AOS_RT_BUDGET2 96
+#endif
+constexpr int kRtBudgetBig = 64, kRtBudgetLds = AOS_RT_BUDGET_LDS, kRtQCap = 512, kRtBudget2 = AOS_RT_BUDGET2, kRtQ2Cap = 128;
 
 // LDS of k_rt_ror: kRorCap staged points (32 KB), the bin offsets of the largest tile (TB = 32 bins
-// + ring: 34^2), the tile's raster window (kRtWinWords 64-bit words) and the wave queue: ~42 KB, 3
-// workgroups per CU
-constexpr int kRtMaxLocalBins = 34 * 34, kRtWinWords = 320;
+// + ring: 34^2), the tile's raster window (kRtWinWords 64-bit words: 70 rows x 3 words at 0.1 m cells)
+// and the two queues (16-bit indices): 40.8 KB, 4 workgroups per CU
+constexpr int kRtMaxLocalBins = 34 * 34, kRtWinWords = 256;
 // staged record w (int bits): bits 0-1 the class (0 a neighbour only, 1 an own clip candidate, 2 a
 // candidate a streaming map already found kept); streaming store only: kWOld = written back by an
 // earlier frame, kWCounted = a candidate below need whose count over the store is in bits kWCntShift+
@@ -479,7 +499,10 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
     __shared__ int bstart[(BIG ? kBigBins : kRtMaxLocalBins) + 1];
     __shared__ unsigned long long win[kRtWinWords];
     __shared__ unsigned kept_wg;
-    __shared__ int q_n, q_k[kRtQCap];   // candidates left to the waves
+    // candidates left to the queues: tile-local indices (< kRorCap, 16 bits) in a fitting tile
+    using QIdx = typename std::conditional<BIG, int, unsigned short>::type;
+    __shared__ int q_n, q2_n;
+    __shared__ QIdx q_k[kRtQCap], q2_k[AOS_RT_QLANE ? kRtQ2Cap : 1];
     const int tid = threadIdx.x;
     const int nit = BIG ? big_nchunks(B) : 1;
     for (int it = BIG ? blockIdx.x : 0; it < nit; it += BIG ? gridDim.x : 1) {
@@ -506,7 +529,7 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
             return;
         }
     }
-    if (tid == 0) { kept_wg = 0; q_n = 0; }
+    if (tid == 0) { kept_wg = 0; q_n = 0; q2_n = 0; }
     const int LB = L.TB + 2;                        // local bins: the tile's bins and a ring of halo bins
     const int bx0 = tx * L.TB - 1, by0 = ty * L.TB - 1;
     const int nlb = LB * LB;
@@ -541,8 +564,9 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
         // exclusive bin offsets: bstart[b] = points in bins < b. Thread t sums a run of kSeg bins,
         // one block scan over the run totals, then each run is written back.
         constexpr int kSeg = (kRtMaxLocalBins + kRorThreads - 1) / kRorThreads;
-        typedef hipcub::BlockScan<int, kRorThreads> Scan;
-        __shared__ typename Scan::TempStorage scan_tmp;
+        // (wave shuffles + one LDS slot per wave: 32 B of LDS where hipcub's BlockScan takes ~2 KB, which
+        // kept the workgroup above the 40 KB that lets 4 of them share a CU)
+        __shared__ int wsum[kRorThreads / 64];
         int v[kSeg], run = 0;
 #pragma unroll
         for (int j = 0; j < kSeg; ++j) {
@@ -550,9 +574,16 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
             v[j] = b <= nlb ? bstart[b] : 0;
             run += v[j];
         }
-        int before;
-        Scan(scan_tmp).ExclusiveSum(run, before);
+        int incl = run;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(incl, o);
+            if ((tid & 63) >= o) incl += t;
+        }
+        if ((tid & 63) == 63) wsum[tid >> 6] = incl;
         __syncthreads();
+        int before = incl - run;
+        for (int w = 0; w < (tid >> 6); ++w) before += wsum[w];
 #pragma unroll
         for (int j = 0; j < kSeg; ++j) {
             const int b = tid * kSeg + j + 1;
@@ -616,6 +647,35 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
             else pts[k].w = cw;
         }
     };
+#if AOS_RT_GROUP
+    // group-cooperative counts (fitting tiles): kRtGroup lanes share one candidate and test kRtGroup
+    // consecutive points of its bin rows per step (one ballot), so a wave's lanes no longer wait for its
+    // slowest candidate's walk
+    if (!BIG) {
+        constexpr int GS = AOS_RT_GROUP, NG = kRorThreads / GS;
+        const int lane = tid & 63, gl = lane & (GS - 1), gshift = lane & ~(GS - 1);
+        for (int k = k0 + tid / GS; k < k1; k += NG) {
+            const float4 p = pts[k];
+            const int w = __float_as_int(p.w), cls = w & kWClass;
+            if (!cls) continue;                 // (group-uniform: every lane of the group read the same p)
+            if (cls == 2) { if (!gl) prev_kept(p); continue; }
+            int bx, by;
+            rt_bin(L, p.x, p.y, bx, by);
+            const int lx = bx - bx0, ly = by - by0;
+            int cnt = AOS_RT_VARIANT == 1 ? L.need : 0;
+            for (int i = 0; i < 3 && cnt < L.need; ++i) {
+                int r0, r1;
+                range(false, lx, ly, i, r0, r1);
+                for (int base = r0; base < r1 && cnt < L.need; base += GS) {
+                    const int j = base + gl;
+                    const bool hit = j < r1 && rt_in(L, p, pts[min(j, r1 - 1)]);
+                    cnt += (int)__popcll((__ballot(hit) >> gshift) & ((GS == 64) ? ~0ull : ((1ull << GS) - 1)));
+                }
+            }
+            if (!gl) decide(p, k, cnt);
+        }
+    } else
+#endif
     for (int k = k0 + tid; k < k1; k += kRorThreads) {
         const float4 p = BIG ? P[k] : pts[k];
         const int w = __float_as_int(p.w), cls = w & kWClass;
@@ -634,7 +694,7 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
         }
         if (cnt < L.need && budget < 0) {        // undecided within the budget
             const int slot = atomicAdd(&q_n, 1);
-            if (slot < kRtQCap) { q_k[slot] = k; continue; }
+            if (slot < kRtQCap) { q_k[slot] = (QIdx)k; continue; }
             cnt = cnt0;                          // (queue full: this thread counts it alone)
             for (int i = 0; i < nr && cnt < L.need; ++i) {
                 int r0, r1;
@@ -647,6 +707,52 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
     __syncthreads();
     {   // the queued candidates, one wave each
         const int nq = min(q_n, kRtQCap), lane = tid & 63;
+#if AOS_RT_QLANE
+        if (!BIG) {
+            // fitting tiles: the over-budget candidates one lane each (restarted, budget kRtBudget2), so the
+            // long walks run packed together; the few still undecided after that, one wave each
+            for (int i = tid; i < nq; i += kRorThreads) {
+                const int k = q_k[i];
+                const float4 p = pts[k];
+                int bx, by;
+                rt_bin(L, p.x, p.y, bx, by);
+                const int lx = bx - bx0, ly = by - by0;
+                int cnt = 0, budget = kRtBudget2;
+                for (int r = 0; r < 3 && cnt < L.need && budget >= 0; ++r) {
+                    int r0, r1;
+                    range(false, lx, ly, r, r0, r1);
+                    cnt = rt_scan_b(L, p, pts, r0, r1, cnt, budget);
+                }
+                if (cnt < L.need && budget < 0) {
+                    const int slot = atomicAdd(&q2_n, 1);
+                    if (slot < kRtQ2Cap) { q2_k[slot] = (QIdx)k; continue; }
+                    cnt = 0;
+                    for (int r = 0; r < 3 && cnt < L.need; ++r) {
+                        int r0, r1;
+                        range(false, lx, ly, r, r0, r1);
+                        cnt = rt_scan(L, p, pts, r0, r1, cnt);
+                    }
+                }
+                decide(p, k, cnt);
+            }
+            __syncthreads();
+            const int nq2 = min(q2_n, kRtQ2Cap);
+            for (int i = tid >> 6; i < nq2; i += kRorThreads / 64) {
+                const int k = q2_k[i];
+                const float4 p = pts[k];
+                int bx, by;
+                rt_bin(L, p.x, p.y, bx, by);
+                const int lx = bx - bx0, ly = by - by0;
+                int cnt = 0;
+                for (int r = 0; r < 3 && cnt < L.need; ++r) {
+                    int r0, r1;
+                    range(false, lx, ly, r, r0, r1);
+                    cnt = rt_wave_scan(L, p, pts, r0, r1, cnt, lane);
+                }
+                if (lane == 0) decide(p, k, cnt);
+            }
+        } else
+#endif
         for (int i = tid >> 6; i < nq; i += kRorThreads / 64) {
             const int k = q_k[i];
             const float4 p = BIG ? P[k] : pts[k];
