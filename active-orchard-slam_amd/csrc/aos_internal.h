@@ -105,6 +105,7 @@ struct RorLaunch {
     float bminx, bminy, bminz, bmaxx, bmaxy, bmaxz, inv_cs; int nbx, nby;
     float cminx, cmaxx, cminy, cmaxy, cminz, cmaxz;
     double r2; float r2f, r2df; int need;   // r2df: largest float f with (double)f <= r2
+    float r2cmp;   // the keep test as one compare, d2 <= r2cmp (rt_configure: r2df, or the float below r2f)
     double origin_x, origin_y; float res; int W, H;
     // Ownership (tiled frames, tiled.hip): a kept candidate is counted iff its cell, clamped to the
     // grid, lies in [rx0, rx1) x [ry0, ry1); it is rastered (if inside the grid) into the byte window

@@ -91,12 +91,23 @@ __device__ __forceinline__ bool rt_candidate(const RorLaunch &L, float x, float 
     return true;
 }
 
+// dense: (double)d2 <= r2, i.e. d2 <= r2df; non-dense: d2 < r2f, i.e. d2 <= the float below r2f: both are
+// d2 <= L.r2cmp (rt_configure), one compare in the inner loops
 __device__ __forceinline__ bool rt_in(const RorLaunch &L, float4 p, float4 q) {
+#if AOS_RT_PK
+    // x and y as one packed pair (v_pk_add_f32 / v_pk_mul_f32 round each lane like the scalar ops)
+    const float2 dxy = make_float2(p.x, p.y) - make_float2(q.x, q.y);
+    const float2 sq = dxy * dxy;
+    const float dz = p.z - q.z;
+    float d2 = sq.x + sq.y;
+    d2 = d2 + dz * dz;
+#else
     float dx = p.x - q.x, dy = p.y - q.y, dz = p.z - q.z;
     float d2 = dx * dx;
     d2 = d2 + dy * dy;
     d2 = d2 + dz * dz;
-    return L.is_dense ? (d2 <= L.r2df) : (d2 < L.r2f);
+#endif
+    return d2 <= L.r2cmp;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -256,6 +267,9 @@ constexpr int kRorThreads = AOS_RT_THREADS, kRorCap = 2048, kRorPer = kRorCap / 
 #endif
 #ifndef AOS_RT_GROUP     // lanes per candidate in a fitting tile's neighbour counts (0: one lane each + wave queue)
 #define AOS_RT_GROUP 0
+#endif
+#ifndef AOS_RT_PK       // packed x / y arithmetic in the distance test
+#define AOS_RT_PK 1
 #endif
 #ifndef AOS_RT_QLANE     // fitting tiles: queued (over-budget) candidates one lane each instead of one wave each
 #define AOS_RT_QLANE 1
@@ -864,6 +878,7 @@ void rt_configure(RorLaunch &L, int Hr, int WWr, double est_binned, int force_tb
     if (tiles(L.TB) > kRtMaxTiles || (L.TB + 2) * (L.TB + 2) > kRtMaxLocalBins)
         throw std::runtime_error("ROR bin grid too large for the tile walk");
     L.ntiles = L.ntx * L.nty;
+    L.r2cmp = L.is_dense ? L.r2df : (L.r2f > 0.0f ? std::nextafter(L.r2f, 0.0f) : -1.0f);
     L.Hr = Hr; L.WWr = WWr;
     // raster window of one tile: its cells (TB bins of 1/inv_cs) + 2 cells of slack on each side
     const double span = (double)L.TB / (double)L.inv_cs / (double)L.res;
