@@ -66,13 +66,16 @@ struct aos_ctx {
     aos::DevBuf full_infl, full_skel;      // tiled frames: the whole map, assembled on the root rank
     aos::PinnedBuf h_small, h_stats;
     // Host -> device upload of a large pageable buffer (a PointCloud2 message): kUpThreads host
-    // threads copy 8 MB chunks into double-buffered pinned slots, each DMA'd on the thread's stream.
-    static constexpr int kUpThreads = 4;
+    // threads copy 2 MB chunks into rings of pinned slots, each DMA'd on the thread's stream (tools/upload_ab.py:
+    // 4-8 threads and 1-8 MB chunks all upload C2's 120 MB in 3-4 ms on the box, the H2D DMA's ~40 GB/s).
+    static constexpr int kUpThreads = 16;   // capacity; up_threads() of them gather (AOS_UP_THREADS, default 4)
+    static int up_threads();
+    static constexpr int kUpSlots = 4;      // pinned slots per thread (a ring: gather one while others DMA)
     struct Uploader {
-        aos::PinnedBuf slot[kUpThreads][2];
+        aos::PinnedBuf slot[kUpThreads][kUpSlots];
         hipStream_t st[kUpThreads] = {};
-        hipEvent_t ev[kUpThreads][2] = {}, done[kUpThreads] = {};
-        bool used[kUpThreads][2] = {};
+        hipEvent_t ev[kUpThreads][kUpSlots] = {}, done[kUpThreads] = {};
+        bool used[kUpThreads][kUpSlots] = {};
     } up;
     // prefetch = true (aos_cloud_prefetch): dst is not read by queued work and the handle's stream is not
     // made to wait; the consumer waits for up.done[] (set_cloud)

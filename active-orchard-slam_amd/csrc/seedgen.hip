@@ -58,25 +58,40 @@ void aos_ctx::release() {
 }
 
 // Host PointCloud2 -> HBM. A pageable hipMemcpyAsync of the 160 MB C2 cloud runs at ~20 GB/s: the runtime
-// stages it through pinned memory on one thread. Here kUpThreads threads each take a range of points,
+// stages it through pinned memory on one thread. Here up_threads() threads each take a range of points,
 // gather their x, y, z floats (12 of the record's point_step bytes: the only fields the path reads) into
-// double-buffered pinned slots of ~8 MB and DMA them on their own streams, so 25 % fewer bytes cross PCIe
+// a ring of kUpSlots pinned 2 MB slots and DMA them on their own streams, so 25 % fewer bytes cross PCIe
 // for the common 16-byte record and the device gets a packed float3 cloud (step 12). The handle's stream
 // waits for all of them. The caller's buffer is only read during the call.
+int aos_ctx::up_threads() {
+    static const int n = [] {
+        const char *e = getenv("AOS_UP_THREADS");
+        return e ? std::max(1, std::min(kUpThreads, atoi(e))) : 4;
+    }();
+    return n;
+}
+
 void aos_ctx::upload_pack(void *dst, const aos_cloud_view &v, bool prefetch) {
-    constexpr uint64_t kChunkPts = (8u << 20) / 12;
+    // chunks of AOS_UP_CHUNK_KB (default 2 MB): the last DMAs start soon after the last gather, so the upload
+    // ends ~one chunk's DMA after the gather instead of one slot per thread later (8 MB slots: ~1 ms)
+    static const uint64_t kChunkPts = [] {
+        const char *e = getenv("AOS_UP_CHUNK_KB");
+        const long kb = e ? std::max(64L, std::min(65536L, atol(e))) : 2048L;
+        return (uint64_t)(kb << 10) / 12;
+    }();
     const uint64_t n = v.n_points;
-    for (int t = 0; t < kUpThreads; ++t)
+    const int nth = up_threads();
+    for (int t = 0; t < nth; ++t)
         if (!up.st[t]) {
             AOS_HIP(hipStreamCreateWithFlags(&up.st[t], hipStreamNonBlocking));
-            for (int k = 0; k < 2; ++k) AOS_HIP(hipEventCreateWithFlags(&up.ev[t][k], hipEventDisableTiming));
+            for (int k = 0; k < kUpSlots; ++k) AOS_HIP(hipEventCreateWithFlags(&up.ev[t][k], hipEventDisableTiming));
             AOS_HIP(hipEventCreateWithFlags(&up.done[t], hipEventDisableTiming));
-            for (int k = 0; k < 2; ++k) up.slot[t][k].ensure(12 * kChunkPts);
+            for (int k = 0; k < kUpSlots; ++k) up.slot[t][k].ensure(12 * kChunkPts);
         }
     // the handle's stream may still read dst (the previous frame): the copies start after it (a prefetch
     // writes the spare buffer, which no queued work reads)
     if (!prefetch) AOS_HIP(hipEventRecord(ev[15], stream));
-    const uint64_t per = (n + kUpThreads - 1) / kUpThreads;
+    const uint64_t per = (n + nth - 1) / nth;
     const uint8_t *src = static_cast<const uint8_t *>(v.data);
     const bool std16 = v.point_step == 16 && v.off_x == 0 && v.off_y == 4 && v.off_z == 8;
     std::exception_ptr err[kUpThreads];
@@ -86,7 +101,7 @@ void aos_ctx::upload_pack(void *dst, const aos_cloud_view &v, bool prefetch) {
             if (!prefetch) AOS_HIP(hipStreamWaitEvent(up.st[t], ev[15], 0));
             const uint64_t p0 = std::min(n, per * t), p1 = std::min(n, per * (t + 1));
             int k = 0;
-            for (uint64_t c = p0; c < p1; c += kChunkPts, k ^= 1) {
+            for (uint64_t c = p0; c < p1; c += kChunkPts, k = (k + 1) % kUpSlots) {
                 const uint64_t m = std::min(kChunkPts, p1 - c);
                 if (up.used[t][k]) AOS_HIP(hipEventSynchronize(up.ev[t][k]));   // its last DMA is done
                 float *o = static_cast<float *>(up.slot[t][k].p);
@@ -109,13 +124,13 @@ void aos_ctx::upload_pack(void *dst, const aos_cloud_view &v, bool prefetch) {
         } catch (...) { err[t] = std::current_exception(); }
     };
     std::thread th[kUpThreads - 1];
-    for (int t = 1; t < kUpThreads; ++t) th[t - 1] = std::thread(work, t);
+    for (int t = 1; t < nth; ++t) th[t - 1] = std::thread(work, t);
     work(0);
-    for (auto &x : th) x.join();
-    for (int t = 0; t < kUpThreads; ++t)
+    for (int t = 1; t < nth; ++t) th[t - 1].join();
+    for (int t = 0; t < nth; ++t)
         if (err[t]) std::rethrow_exception(err[t]);
     if (!prefetch)
-        for (int t = 0; t < kUpThreads; ++t) AOS_HIP(hipStreamWaitEvent(stream, up.done[t], 0));
+        for (int t = 0; t < nth; ++t) AOS_HIP(hipStreamWaitEvent(stream, up.done[t], 0));
 }
 
 // aos_cloud_prefetch: the host stages and DMAs the next cloud into cloud_next on a background thread
@@ -147,12 +162,12 @@ void aos_ctx::release_uploader() {
     for (int t = 0; t < kUpThreads; ++t) {
         if (up.st[t]) {
             (void)hipStreamSynchronize(up.st[t]);
-            for (int k = 0; k < 2; ++k) (void)hipEventDestroy(up.ev[t][k]);
+            for (int k = 0; k < kUpSlots; ++k) (void)hipEventDestroy(up.ev[t][k]);
             (void)hipEventDestroy(up.done[t]);
             (void)hipStreamDestroy(up.st[t]);
             up.st[t] = nullptr;
         }
-        for (int k = 0; k < 2; ++k) { up.slot[t][k].release(); up.used[t][k] = false; }
+        for (int k = 0; k < kUpSlots; ++k) { up.slot[t][k].release(); up.used[t][k] = false; }
     }
 }
 
@@ -179,7 +194,7 @@ void aos_ctx::set_cloud(const aos_cloud_view &v) {
             // the prefetched copy of this very view: it becomes the frame's cloud once its DMAs are done
             std::swap(cloud_copy.p, cloud_next.p);
             std::swap(cloud_copy.cap, cloud_next.cap);
-            for (int t = 0; t < kUpThreads; ++t) AOS_HIP(hipStreamWaitEvent(stream, up.done[t], 0));
+            for (int t = 0; t < up_threads(); ++t) AOS_HIP(hipStreamWaitEvent(stream, up.done[t], 0));
         } else {
             void *dst = cloud_copy.ensure(std::max<size_t>(12 * (size_t)v.n_points, 16));
             if (bytes) upload_pack(dst, v);
