@@ -18,7 +18,9 @@ Workload: config C2 (10 M points, 4096^2 cells @ 0.1 m, BASELINE.json configs[2]
 Multi-GPU (--gpus N, launched by torch.distributed.run): weak scaling — every rank processes its
 own independent 4096^2 map (scene seed 3 + rank); no data-path collective; the barrier and the
 max-over-ranks time use torch.distributed (RCCL). --tiled: one map split into tiles over the ranks
-(SURVEY §8e, strong scaling).
+(SURVEY §8e, strong scaling). --tiled --stream: C4 over the ranks (BASELINE configs[4], 8 x MI355X
+streaming): every rank receives each scan and keeps its tile's points box in its own HBM map. With N > 1
+the same launch also reports the tiled C3 map (`tiled`) and the tiled C4 stream (`tiled_stream`).
 """
 from __future__ import annotations
 
@@ -56,7 +58,7 @@ def parse(argv=None):
     ap.add_argument("--no-device-rate", action="store_true", help="skip the extra device-resident loop")
     ap.add_argument("--no-pipelined-rate", action="store_true", help="skip the extra pipelined loop")
     ap.add_argument("--no-tiled-rate", action="store_true",
-                    help="--gpus N > 1: skip the extra tiled C3 measurement (tiled key)")
+                    help="--gpus N > 1: skip the extra tiled C3 / tiled C4 measurements (tiled, tiled_stream keys)")
     ap.add_argument("--trace", action="store_true", help="per-step timeline on stderr")
     ap.add_argument("--depth", type=int, default=4,
                     help="pipelined loop: GVD jobs in flight (aos_gvd_pipeline_depth): frames are independent, so "
@@ -83,7 +85,7 @@ def parse(argv=None):
                          "whole-map stages and the GVD jobs rotate over the ranks)")
     a = ap.parse_args(argv)
     if a.config is None:
-        a.config = "C3" if a.tiled else "C2"
+        a.config = "C3" if a.tiled and not a.stream else "C2"
     return a
 
 
@@ -217,28 +219,35 @@ def main():
         t = tiled_extra(a, E, dist, out)
         if out is not None:
             out["tiled"] = t
+        t = tiled_extra(a, E, dist, out, stream=True)
+        if out is not None:
+            out["tiled_stream"] = t
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def tiled_extra(a, E, dist, main_out) -> dict:
+def tiled_extra(a, E, dist, main_out, stream: bool = False) -> dict:
     """One map (C3, 8192^2, 40 M points) in tiling_for(N) tiles over the N ranks, rotating roots with
-    background GVD jobs: Mcells/s, frame latency and the root's serial whole-map finish. Guarded by a
-    watchdog: if the collectives do not finish in time every rank reports the timeout and exits."""
+    background GVD jobs: Mcells/s, frame latency and the root's serial whole-map finish. stream: C4 over the
+    ranks instead (the C2 map, then 1 M-point scans; each rank keeps its tile's points box; frame k's root is
+    rank k mod N): per-scan latency. Guarded by a watchdog: if the collectives do not finish in time every
+    rank reports the timeout and exits."""
     import copy
     import threading
     b = copy.copy(a)
-    b.tiled, b.config, b.steps, b.warmup = True, "C3", max(4, min(a.steps, 12)), 3
-    b.no_cpu_baseline = True
+    b.tiled, b.stream, b.no_cpu_baseline = True, stream, True
+    b.config = "C2" if stream else "C3"
+    b.steps, b.warmup = (max(4, min(a.steps, 16)), 2) if stream else (max(4, min(a.steps, 12)), 3)
+    key = "tiled_stream" if stream else "tiled"
     limit = float(os.environ.get("AOS_BENCH_TILED_TIMEOUT", "300"))
     res = {"main_out": main_out}
 
     def watchdog():
-        res["error"] = f"tiled C3 section did not finish within {limit:.0f} s (collective hang?)"
+        res["error"] = f"{key} section did not finish within {limit:.0f} s (collective hang?)"
         if E["rank"] == 0 and res["main_out"] is not None:
-            res["main_out"]["tiled"] = {"error": res["error"]}
+            res["main_out"][key] = {"error": res["error"]}
             print(json.dumps(res["main_out"]), flush=True)
         os._exit(0)   # every rank's own watchdog fires: none is left waiting in a collective
     timer = threading.Timer(limit, watchdog)
@@ -252,7 +261,7 @@ def tiled_extra(a, E, dist, main_out) -> dict:
     timer.cancel()
     if o is None:
         return None
-    keep = ("value", "unit", "ms_per_step", "frame_latency_ms", "root_serial_ms", "config", "frame", "stages_ms")
+    keep = ("value", "unit", "ms_per_step", "frame_latency_ms", "root_serial_ms", "config", "frame", "stages_ms", "stream")
     return {k: o[k] for k in keep if k in o}
 
 
@@ -271,11 +280,12 @@ def run(a, E, dist, quiet=False):
     ctx = aos_gpu.Ctx(params, device=gpu)
     ctx.set_polygon(poly)
     if a.tiled:
-        # one map: every rank holds the points of its tile's box (tile + ROR margin), resident in HBM
+        # one map: every rank holds the points of its tile's box (tile + ROR margin), resident in HBM (a
+        # tiled stream: every rank receives the whole map and each whole scan; the library keeps the box)
         import aos_tiles
         tx, ty = aos_tiles.tiling_for(world)
         plan = aos_tiles.tile_plan(params, poly, tx, ty, rank)
-        cloud = aos_tiles.shard(orchard.generate(cfg), plan["points_box"])
+        cloud = orchard.generate(cfg) if a.stream else aos_tiles.shard(orchard.generate(cfg), plan["points_box"])
         if world > 1 and backend == "nccl":   # the library's C++ RCCL communicator (no Python callbacks)
             comm = aos_tiles.RcclComm(plan["exchange_bytes"], gpu, rank, world)
         elif world > 1:                        # gloo rehearsal (ranks sharing a GPU)
@@ -296,7 +306,10 @@ def run(a, E, dist, quiet=False):
         # from host memory (only the 16 MB scan crosses PCIe) and processes the whole map + GVD
         scans = [orchard.generate_scan(cfg, k) for k in range(a.warmup + a.steps)]
         ctx.map_reset(reserve_points=n + len(scans) * orchard.SCAN_POINTS)
-        ctx.map_append(d_cloud.data_ptr(), n_points=n, on_device=True, want_host=False)
+        if a.tiled:   # the map's first tiled frame (every rank keeps its box; rank 0 finishes it)
+            ctx.tiled_map_append(comm, tx, ty, d_cloud.data_ptr(), root=0, n_points=n, on_device=True, want_host=False)
+        else:
+            ctx.map_append(d_cloud.data_ptr(), n_points=n, on_device=True, want_host=False)
     latency, mk_latency = [], []
     # The reference builds the graph on every callback and publishes it, with the markers (publishMarkers:
     # a second Subdiv2D for the Voronoi cells), only when 1 / max_graph_publish_rate (0.1 s) has passed
@@ -369,7 +382,17 @@ def run(a, E, dist, quiet=False):
         last = k == mode["n_calls"] - 1
         t0 = time.perf_counter()
         pend["t0"][k] = t0
-        if a.stream:
+        if a.stream and a.tiled:
+            # C4 over the ranks: every rank appends the whole scan to its box's map and runs its tiles; the
+            # frame's root (rank k mod N) finishes it and builds the graph
+            root_k = k % world
+            g = ctx.tiled_map_append(comm, tx, ty, scans[k], root=root_k, want_host=False)
+            if not g["root"]:
+                if last and pend.get("mk_pending"):
+                    collect()
+                    pend["mk_pending"] = False
+                return g, None
+        elif a.stream:
             g = ctx.map_append(scans[k], want_host=False)
         elif a.tiled:
             # every rank receives the gathered skeleton and inflated tiles, so any rank can finish a frame:
@@ -444,12 +467,21 @@ def run(a, E, dist, quiet=False):
 
     sync = torch.cuda.synchronize
     # the timed region: sequential frames (default), the tiled map's rotating-root pipeline, or --pipelined
-    main_pipe = a.pipelined or (a.tiled and not a.sequential)
+    main_pipe = a.pipelined or (a.tiled and not a.sequential and not a.stream)
     reset(main_pipe, host_io, a.steps, a.warmup)
     _progress(f"{a.warmup} warmup + {a.steps} timed frames ({'pipelined' if main_pipe else 'sequential'})")
     dt, res, per = timed_region(step, a.steps, a.warmup, world, sync, dist, red_dev)
     mk_frames = sum(1 for k in range(a.warmup, a.warmup + a.steps) if pend["mk"].get(k))
     frame_lat = sorted(1e3 * pend["lat"][k] for k in range(a.warmup, a.warmup + a.steps) if k in pend["lat"])
+    if a.tiled and a.stream:
+        # every step is one scan's frame, finished by its root (rank k mod N): the root's own latency (its
+        # seed-gen call start -> GvdGraph), gathered by a max over ranks (the other ranks report 0)
+        root_lat = [pend["lat"].get(k, 0.0) for k in range(a.warmup, a.warmup + a.steps)]
+        if world > 1:
+            t = torch.tensor(root_lat, dtype=torch.float64, device=red_dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            root_lat = [float(x) for x in t.tolist()]
+        frame_lat = sorted(1e3 * x for x in root_lat)
     g, gg = res[-1]
     if a.tiled:   # the frame statistics of this rank's last root frame (its seeds, rows and graph)
         roots = [(gs, ggs) for gs, ggs in res if gs.get("root") and ggs is not None] or \
@@ -540,7 +572,11 @@ def run(a, E, dist, quiet=False):
                   "note": "whole frame (median per-frame wall-clock) incl. PCIe and the host Subdiv2D replay"}
 
     if rank == 0:
-        if a.stream:
+        if a.stream and a.tiled:
+            workload = (f"C4 on {world} GPU(s): 1 M-point scans at {orchard.SCAN_HZ:g} Hz appended to the {a.config} map, "
+                        f"one map in {tx}x{ty} tiles (each rank keeps its tile's points box), {g['width']}x{g['height']} "
+                        f"cells @ {cfg.res} m, full seed-gen + GVD per scan, root rotating")
+        elif a.stream:
             workload = (f"C4: 1 M-point scans at {orchard.SCAN_HZ:g} Hz appended to the device-resident {a.config} map "
                         f"({n} pts at start, {g['n_input']} after the last step), {g['width']}x{g['height']} cells "
                         f"@ {cfg.res} m, full seed-gen + GVD of the whole map per scan")
@@ -585,7 +621,18 @@ def run(a, E, dist, quiet=False):
             "thin_roofline": thin_roof,
             "frame_roofline": frame_roof,
         }
-        if a.stream:
+        if a.stream and a.tiled:
+            out["stream"] = {"scan_latency_ms_p50": round(_median(frame_lat), 2), "scan_latency_ms_max": round(frame_lat[-1], 2),
+                             "scan_latency_ms": [round(x * 1e3, 1) for x in root_lat],
+                             "step_ms_max_over_ranks": [round(x * 1e3, 1) for x in per],
+                             "budget_ms": 1e3 / orchard.SCAN_HZ,
+                             "keeps_up": frame_lat[-1] <= 1e3 / orchard.SCAN_HZ,
+                             "map_points": g["n_input"],
+                             "note": f"C4 over {world} rank(s) in {tx}x{ty} tiles: every rank appends each whole scan "
+                                     f"to its tile's points box (aos_tiled_map_append); frame k's root (rank k mod "
+                                     f"{world}) finishes it and builds the GvdGraph; scan latency = the root's wall-clock "
+                                     f"from its append call to the GvdGraph; value = W.H / the median step (max over ranks)"}
+        elif a.stream:
             lat = sorted(x * 1e3 for x in latency[a.warmup:])
             mlat = sorted(x * 1e3 for x in mk_latency[a.warmup:]) or [0.0]
             out["stream"] = {"scan_latency_ms_p50": round(_median(lat), 2), "scan_latency_ms_max": round(lat[-1], 2),

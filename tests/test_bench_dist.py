@@ -102,3 +102,24 @@ def test_tiled_extra_watchdog_and_error(capfd):
         assert t == {"error": "RuntimeError: rccl init failed"}
     finally:
         bench.run = old
+
+
+def test_tiled_stream_extra_configuration():
+    """The --gpus N launch's second extra (tiled_stream, BASELINE configs[4] over the ranks): bench.run gets a
+    tiled C4 configuration (C2 map + scans, sequential scans), and a failure is reported under its own key."""
+    import argparse
+    seen = {}
+    old = bench.run
+    try:
+        def fake(b, E, dist, quiet=False):
+            seen.update(tiled=b.tiled, stream=b.stream, config=b.config, steps=b.steps, warmup=b.warmup,
+                        cpu=b.no_cpu_baseline)
+            return {"value": 2.0, "stream": {"scan_latency_ms_p50": 1.0}, "extra": 1}
+        bench.run = fake
+        a = argparse.Namespace(steps=20, warmup=5, tiled=False, stream=False, config="C2", no_cpu_baseline=False)
+        t = bench.tiled_extra(a, {"rank": 0}, None, {"value": 1.0}, stream=True)
+        assert seen == {"tiled": True, "stream": True, "config": "C2", "steps": 16, "warmup": 2, "cpu": True}
+        assert t == {"value": 2.0, "stream": {"scan_latency_ms_p50": 1.0}}
+        assert bench.parse(["--tiled", "--stream"]).config == "C2" and bench.parse(["--tiled"]).config == "C3"
+    finally:
+        bench.run = old
