@@ -21,6 +21,8 @@
 // "at least need points within r", and the raster is an OR.
 //
 // Numerics: FLANN's squared distance ((dx*dx)+dy*dy)+dz*dz in float, no FMA (-ffp-contract=off);
+// this file is built with -fno-slp-vectorize (Makefile): the SLP vectorizer paired y / z of the partition
+// passes' dwordx3 loads into aligned register pairs, and the moves made every load wait before use;
 // dense clouds: kNN keeps iff the need-th nearest has (double)d2 <= r^2, i.e. d2 <= r2df (the
 // largest float whose double is <= r^2); non-dense: radius search d2 < float(r^2). The point itself
 // has d2 = 0 and is counted by the same test (not counted when r = 0 on a non-dense cloud, as FLANN's
@@ -94,19 +96,10 @@ __device__ __forceinline__ bool rt_candidate(const RorLaunch &L, float x, float 
 // dense: (double)d2 <= r2, i.e. d2 <= r2df; non-dense: d2 < r2f, i.e. d2 <= the float below r2f: both are
 // d2 <= L.r2cmp (rt_configure), one compare in the inner loops
 __device__ __forceinline__ bool rt_in(const RorLaunch &L, float4 p, float4 q) {
-#if AOS_RT_PK
-    // x and y as one packed pair (v_pk_add_f32 / v_pk_mul_f32 round each lane like the scalar ops)
-    const float2 dxy = make_float2(p.x, p.y) - make_float2(q.x, q.y);
-    const float2 sq = dxy * dxy;
-    const float dz = p.z - q.z;
-    float d2 = sq.x + sq.y;
-    d2 = d2 + dz * dz;
-#else
     float dx = p.x - q.x, dy = p.y - q.y, dz = p.z - q.z;
     float d2 = dx * dx;
     d2 = d2 + dy * dy;
     d2 = d2 + dz * dz;
-#endif
     return d2 <= L.r2cmp;
 }
 
@@ -163,28 +156,38 @@ __global__ __launch_bounds__(kRtTB) void k_rt_part(RorLaunch L, int *H, const in
     __syncthreads();
     unsigned own = 0;
     const uint64_t begin = (uint64_t)w * chunk, end = min(L.n, begin + chunk);
-    // software pipelined: the next sub-chunk's kRtPer loads are in flight while this one is walked
-    float4 nxt[kRtPer];
-    // (branch-free: an index past the chunk re-reads its last point and is marked invalid, so the
-    // compiler issues the kRtPer loads back to back without intervening waits)
-    auto issue = [&](uint64_t base) {
-#pragma unroll
-        for (int j = 0; j < kRtPer; ++j) {
-            const uint64_t i = base + (uint64_t)j * kRtTB + tid;
-            rt_load<LAY>(L, i < end ? i : end - 1, nxt[j].x, nxt[j].y, nxt[j].z);
-            nxt[j].w = __int_as_float(i < end ? 0 : -1);
+    const unsigned cnt = begin < end ? (unsigned)(end - begin) : 0u;   // (chunks are < 2^32 points)
+    // the chunk's records from a 64-bit base, then 32-bit offsets (LAY 0: the caller's point_step)
+    const uint8_t *cbase = L.cloud + begin * (uint64_t)(LAY == 1 ? 16 : LAY == 2 ? 12 : L.step);
+    // a record is loaded straight into the registers it is used from (float3 for the packed 12-B cloud: a
+    // float4 with a validity word made the compiler wait on each load to move x, y, z into place)
+    using Rec = typename std::conditional<LAY == 1, float4, float3>::type;
+    auto ld = [&](unsigned i, Rec &o) {
+        const uint8_t *rec = cbase + i * (unsigned)(LAY == 1 ? 16 : LAY == 2 ? 12 : L.step);
+        if (LAY == 0) {
+            o.x = *reinterpret_cast<const float *>(rec + L.ox);
+            o.y = *reinterpret_cast<const float *>(rec + L.oy);
+            o.z = *reinterpret_cast<const float *>(rec + L.oz);
+        } else {
+            o = *reinterpret_cast<const Rec *>(rec);
         }
     };
-    if (begin < end) issue(begin);
-    for (uint64_t base = begin; base < end; base += kRtSub) {
-        float4 pt[kRtPer];
+    // software pipelined over two register buffers that alternate (no register copies between them, so
+    // the compiler does not wait on the next sub-chunk's loads to move them: round 3 found the single
+    // prefetch buffer + copy waiting on 6 of its 8 loads before the current points were walked)
+    // (branch-free: an index past the chunk re-reads the chunk's last point; the walk skips it)
+    auto issue = [&](Rec (&buf)[kRtPer], unsigned base) {
 #pragma unroll
-        for (int j = 0; j < kRtPer; ++j) pt[j] = nxt[j];
-        if (base + kRtSub < end) issue(base + kRtSub);
+        for (int j = 0; j < kRtPer; ++j) {
+            const unsigned i = base + (unsigned)(j * kRtTB + tid);
+            ld(i < cnt ? i : cnt - 1, buf[j]);
+        }
+    };
+    auto walk = [&](const Rec (&pt)[kRtPer], unsigned base) {
 #pragma unroll
         for (int j = 0; j < kRtPer; ++j) {
             const float x = pt[j].x, y = pt[j].y, z = pt[j].z;
-            if (__float_as_int(pt[j].w) < 0 || !rt_binned(L, x, y, z)) continue;
+            if (base + (unsigned)(j * kRtTB + tid) >= cnt || !rt_binned(L, x, y, z)) continue;
             ++own;
 #if AOS_RT_COUNT_EXP == 2   // (timing experiment: 2 = loads and the bounds test only)
             if (!SCATTER) continue;
@@ -210,6 +213,15 @@ __global__ __launch_bounds__(kRtTB) void k_rt_part(RorLaunch L, int *H, const in
                     }
                 }
         }
+    };
+    Rec bufA[kRtPer], bufB[kRtPer];
+    if (cnt) issue(bufA, 0);
+    for (unsigned base = 0; base < cnt; base += 2 * kRtSub) {
+        if (base + kRtSub < cnt) issue(bufB, base + kRtSub);
+        walk(bufA, base);
+        if (base + kRtSub >= cnt) break;
+        if (base + 2 * kRtSub < cnt) issue(bufA, base + 2 * kRtSub);
+        walk(bufB, base + kRtSub);
     }
     if (!SCATTER) {
         __syncthreads();
@@ -267,9 +279,6 @@ constexpr int kRorThreads = AOS_RT_THREADS, kRorCap = 2048, kRorPer = kRorCap / 
 #endif
 #ifndef AOS_RT_GROUP     // lanes per candidate in a fitting tile's neighbour counts (0: one lane each + wave queue)
 #define AOS_RT_GROUP 0
-#endif
-#ifndef AOS_RT_PK       // packed x / y arithmetic in the distance test
-#define AOS_RT_PK 1
 #endif
 #ifndef AOS_RT_QLANE     // fitting tiles: queued (over-budget) candidates one lane each instead of one wave each
 #define AOS_RT_QLANE 1
