@@ -2,6 +2,8 @@
 // each pass timed with HIP events over several frames; prints the raster popcount and kept count so
 // variants (-DAOS_RT_VARIANT=..., tile / LDS constants) can be checked against each other.
 // Build: tools/rorbench/build.sh   Run: tools/rorbench/rorbench [grid_n] [n_points] [frames] [step: 16 | 12]
+// [flush_mb: overwrite this many MB between frames, so the cloud and the staged array start cold as in a
+// product frame (MALL 256 MB); 0: warm, the previous frame's lines still cached]
 #include "../../active-orchard-slam_amd/csrc/ror.hip"
 
 #include <cstdio>
@@ -44,6 +46,9 @@ int main(int argc, char **argv) {
     const uint64_t n = argc > 2 ? strtoull(argv[2], 0, 10) : 10000000ull;
     const int frames = argc > 3 ? atoi(argv[3]) : 10;
     const int pstep = argc > 4 ? atoi(argv[4]) : 16;   // 12: the packed float3 cloud of the host upload
+    const int flush_mb = argc > 5 ? atoi(argv[5]) : 0;   // > 0: overwrite this many MB between frames (evicts MALL / L2)
+    void *d_flush = nullptr;
+    if (flush_mb > 0) AOS_HIP(hipMalloc(&d_flush, (size_t)flush_mb << 20));
     orchard_cfg c{3, n, grid_n, 0.1f, 0, 0.0, 0.01};
     const int64_t nt = orchard_num_trees(&c);
     std::vector<double> tx(nt), ty(nt);
@@ -108,6 +113,7 @@ int main(int argc, char **argv) {
         AOS_HIP(hipMemsetAsync(d_tot + nt, 0, 4, s));
         AOS_HIP(hipMemsetAsync(d_cnt, 0, 8 * (kRorCounters + 2), s));
         AOS_HIP(hipMemsetAsync(d_bits, 0, 8ull * WW * H, s));
+        if (d_flush) AOS_HIP(hipMemsetAsync(d_flush, f & 0xff, (size_t)flush_mb << 20, s));
         AOS_HIP(hipEventRecord(e[0], s));
         if (pstep == 12) rt_part<false, 2>(L, d_H, nullptr, G, nullptr, d_cnt + kRorCounters, s);   // (launch_rt_count, split)
         else rt_part<false, 1>(L, d_H, nullptr, G, nullptr, d_cnt + kRorCounters, s);
