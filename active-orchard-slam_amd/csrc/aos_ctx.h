@@ -63,6 +63,7 @@ struct aos_ctx {
     // ---- device buffers
     aos::DevBuf cloud_copy, bin_count, bin_start, pt_binslot, sorted, ror_scratch, ror_bigbins, scan_tmp, counters;
     aos::DevBuf raster_bits, infl_bits, open_bits, thin_a, thin_b, thin_act, occ_bytes, skel_bytes, flags;
+    aos::DevBuf thin_out;   // the converged skeleton bits, picked on the device (launch_thin_pick)
     aos::DevBuf full_infl, full_skel;      // tiled frames: the whole map, assembled on the root rank
     aos::PinnedBuf h_small, h_stats;
     // Host -> device upload of a large pageable buffer (a PointCloud2 message): kUpThreads host

@@ -161,6 +161,9 @@ int thin_tiles(const FrameGeom &g);
 void launch_thin_block(const uint64_t *in, uint64_t *out, const FrameGeom &g, int base_iter, int *flags,
                        const ThinOwn &own, hipStream_t s);
 void launch_draw_rect(int8_t *grid, const FrameGeom &g, int gx0, int gy0, int gx1, int gy1, hipStream_t s);
+// the converged thinning buffer (from the device flags) -> out, n words (no host round trip)
+void launch_thin_pick(const int *flags, int launched, const uint64_t *b0, const uint64_t *b1, uint64_t *out, size_t n,
+                      hipStream_t s);
 void launch_zero_ints(int *p, int n, hipStream_t s);   // a kernel (no memset node in a captured graph)
 size_t scan_temp_bytes(int n);
 void launch_exclusive_scan(const int *in, int *out, int n, void *temp, size_t temp_bytes, hipStream_t s);

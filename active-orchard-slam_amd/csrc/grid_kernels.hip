@@ -322,6 +322,29 @@ void launch_zero_ints(int *p, int n, hipStream_t s) {
     if (n > 0) k_zero_ints<<<cdiv(n, 256), 256, 0, s>>>(p, n);
 }
 
+// The thinning result without a host round trip: the last launch that ran (launch j runs iff j == 0 or
+// iteration j*K-1 deleted something) wrote bufs[last & 1]; it is copied into out for the later stages.
+__global__ void k_thin_pick(const int *flags, int launched, int K, const uint64_t *b0, const uint64_t *b1, uint64_t *out,
+                            size_t n) {
+    __shared__ int last_s;
+    if (threadIdx.x == 0) {
+        int last = 0;
+        for (int j = 1; j < launched; ++j) {
+            if (!flags[1 + j * K - 1]) break;
+            last = j;
+        }
+        last_s = last;
+    }
+    __syncthreads();
+    const uint64_t *src = (last_s & 1) ? b1 : b0;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) out[i] = src[i];
+}
+void launch_thin_pick(const int *flags, int launched, const uint64_t *b0, const uint64_t *b1, uint64_t *out, size_t n,
+                      hipStream_t s) {
+    k_thin_pick<<<512, 256, 0, s>>>(flags, launched, KIT, b0, b1, out, n);
+    AOS_HIP(hipGetLastError());
+}
+
 void launch_thin_block(const uint64_t *in, uint64_t *out, const FrameGeom &g, int base_iter, int *flags,
                        const ThinOwn &own, hipStream_t s) {
     static_assert(2 * KIT <= HR && 2 * KIT <= TH && 2 * KIT <= 64 * TWW, "the copy-through rule needs a tile >= 2 KIT cells");
