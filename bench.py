@@ -39,7 +39,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # for the kernels of this build's ROR design. A config or design without a committed PMC run gets null.
 ROR_DESIGN = "r03"
 PMC_FILES = {("C2", "r02"): os.path.join(ROOT, "profiles", "r02q_pmc_traffic.json"),
-             ("C2", "r03"): os.path.join(ROOT, "profiles", "r03n_pmc_traffic.json")}
+             ("C2", "r03"): os.path.join(ROOT, "profiles", "r03fin_pmc_traffic.json")}
 
 
 def parse(argv=None):
