@@ -915,6 +915,9 @@ static void rt_part(const RorLaunch &L, int *H, const int *tstart, int G, float4
     constexpr int TB = SCATTER ? kRtScatterTB : kRtCountTB, PER = SCATTER ? kRtScatterPer : kRtCountPer;
     static_assert(kRtChunkQ % (TB * PER) == 0 || (TB * PER) % kRtChunkQ == 0, "chunk granularity");
     const size_t lds = sizeof(int) * (size_t)L.ntiles;
+    const uint64_t stride = LAY == 1 ? 16 : LAY == 2 ? 12 : L.step;
+    if (rt_chunk(L, G) * stride >= (1ull << 32))   // (k_rt_part addresses a chunk with 32-bit byte offsets)
+        throw std::runtime_error("ROR partition: a workgroup's chunk of the cloud exceeds 4 GB");
     if (lds > 64 * 1024)   // the tile histogram exceeds the default dynamic-LDS limit (gfx950: 160 KB)
         AOS_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rt_part<SCATTER, LAY, TB, PER>),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
