@@ -60,6 +60,26 @@ def test_c0_full_frame():
     c.close()
 
 
+def test_gvd_external_near_duplicate_seeds():
+    """voronoiSeedsCallback's greedy 0.5 m merge (gvd:84-128) actually firing: the C0 seeds with jittered
+    copies of every third seed interleaved (0.1-0.45 m away) through the external-input entry point."""
+    cfg = orchard.CONFIGS["C0"]
+    c, g, o = run_both(cfg)
+    rng = np.random.default_rng(7)
+    seeds = []
+    for i, s in enumerate(np.asarray(o["voronoi_seeds"], np.float64)):
+        seeds.append(s)
+        if i % 3 == 0:
+            a, d = rng.uniform(0, 2 * np.pi), rng.uniform(0.1, 0.45)
+            seeds.append(s + d * np.array([np.cos(a), np.sin(a)]))
+    seeds = np.array(seeds)
+    go = O.gvd(seeds, o["rows_info"], o, O.default_params(grid_resolution=cfg.res, markers=1))
+    assert len(go["merged"]) < len(seeds)
+    assert_gvd_parity(c.gvd(seeds, o["rows_info"], o), go)
+    _assert_markers(c.gvd_markers(), go)      # markers' seeds = the merged seeds
+    c.close()
+
+
 def test_c1_full_frame():
     cfg = orchard.CONFIGS["C1"]
     c, g, o = run_both(cfg)
