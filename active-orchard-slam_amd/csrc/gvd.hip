@@ -596,15 +596,13 @@ static void scan_excl(DevBuf &tmpb, const int *in, int *out, int n, hipStream_t 
 // circumcentre (k_vor_faces) and the per-vertex facet sizes (k_facet_count, 0 below 2 points), and
 // scans them into edge offsets. Returns the edge total (F.cnt / F.off stay on the device); h_sc =
 // 2 pinned ints. The caller launches k_facet_emit into a buffer of that many float4.
-static int facets_count(FacetBufs &F, const Subdiv2D::Raw &R, int *h_sc, hipStream_t s, SyncEvent &sev) {
-    // the quad-edge export (~5 MB at C2) goes through the builder's own pinned buffer (a pageable copy
-    // is staged by the runtime through its own buffers and blocks the calling thread), as one copy
+static int facets_count(FacetBufs &F, const Subdiv2D &sd, Subdiv2D::Raw &R, int *h_sc, hipStream_t s, SyncEvent &sev) {
+    // the quad-edge export (~6 MB at C2) is written straight into the builder's own pinned buffer (a
+    // pageable copy is staged by the runtime through its own buffers and blocks the calling thread) and
+    // goes up as one copy
+    char *hs = static_cast<char *>(F.h_stage.ensure(sd.raw_bytes()));
+    R = sd.raw_into(hs);
     const size_t bq = sizeof(int) * 8 * (size_t)R.n_rec, bv = sizeof(float2) * R.n_vtx, bi = sizeof(int) * R.n_vtx;
-    char *hs = static_cast<char *>(F.h_stage.ensure(bq + bv + 2 * bi));
-    std::memcpy(hs, R.qe, bq);
-    std::memcpy(hs + bq, R.vp, bv);
-    std::memcpy(hs + bq + bv, R.vfirst, bi);
-    std::memcpy(hs + bq + bv + bi, R.vtype, bi);
     char *d = static_cast<char *>(F.raw.ensure(bq + bv + 2 * bi));
     AOS_HIP(hipMemcpyAsync(d, hs, bq + bv + 2 * bi, hipMemcpyHostToDevice, s));
     F.qe = reinterpret_cast<int *>(d);
@@ -694,12 +692,12 @@ static void compute_cells(CellsWork &W, int rect_mode) {
     // getVoronoiFacetList on the GPU (the builder of the main graph, on the worker's stream): the
     // facet of real vertex k is the start points of its k_facet_emit edges, cnt[k] of them (0 for a
     // facet of fewer than 2 points: never a cell).
-    const Subdiv2D::Raw R = sd.raw();
     AOS_HIP(hipSetDevice(W.device));
     if (!W.stream) AOS_HIP(hipStreamCreateWithFlags(&W.stream, hipStreamNonBlocking));
     int *h_sc = static_cast<int *>(W.h.ensure(4096));
     SyncEvent sev;
-    const int ne = facets_count(W.fb, R, h_sc, W.stream, sev);
+    Subdiv2D::Raw R{};
+    const int ne = facets_count(W.fb, sd, R, h_sc, W.stream, sev);
     const size_t need = sizeof(float4) * (size_t)std::max(ne, 1) + sizeof(int) * (size_t)R.n_vtx;
     float4 *d_e = dev<float4>(W.edges, std::max(ne, 1));
     if (ne) facets_emit(W.fb, R, d_e, W.stream);
@@ -920,8 +918,8 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
                 sd.insert(x, y);
             }
             tr.mark("inserts");
-            const Subdiv2D::Raw R = sd.raw();
-            ne = facets_count(S.fb, R, h_sc, s, G.sev);
+            Subdiv2D::Raw R{};
+            ne = facets_count(S.fb, sd, R, h_sc, s, G.sev);
             tr.mark("facets");
             d_ef = dev<float>(S.edges_f, 4 * (size_t)std::max(ne, 1));
             if (ne) facets_emit(S.fb, R, reinterpret_cast<float4 *>(d_ef), s);

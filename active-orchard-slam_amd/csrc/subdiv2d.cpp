@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstring>
 
 namespace aos {
 
@@ -436,6 +437,28 @@ Subdiv2D::Raw Subdiv2D::raw() {
         o[4] = r.org[0]; o[6] = r.org[1];
     }
     return Raw{qx.data(), n, reinterpret_cast<const float *>(vp.data()), vfirst.data(), vtype.data(), (int)vp.size()};
+}
+
+Subdiv2D::Raw Subdiv2D::raw_into(void *dst) const {
+    const int n = (int)rec.size(), nv = (int)vp.size();
+    int *qe = static_cast<int *>(dst);
+    auto rot3 = [](int x) { return (x & ~3) + ((x + 3) & 3); };
+    for (int q = 0; q < n; ++q) {   // every record written (free ones and #0 as zeros), as raw()'s zero-filled qx
+        const Rec &r = rec[q];
+        int o[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (q > 0 && r.on[0] > 0) {
+            o[0] = r.on[0]; o[1] = rot3(r.op[0]); o[2] = r.on[1]; o[3] = rot3(r.op[1]);
+            o[4] = r.org[0]; o[6] = r.org[1];
+        }
+        std::memcpy(qe + 8 * (size_t)q, o, sizeof(o));
+    }
+    char *p = reinterpret_cast<char *>(qe + 8 * (size_t)n);
+    float *vpo = reinterpret_cast<float *>(p);
+    std::memcpy(vpo, vp.data(), sizeof(V2f) * (size_t)nv);
+    int *vf = reinterpret_cast<int *>(p + sizeof(V2f) * (size_t)nv), *vt = vf + nv;
+    std::memcpy(vf, vfirst.data(), sizeof(int) * (size_t)nv);
+    std::memcpy(vt, vtype.data(), sizeof(int) * (size_t)nv);
+    return Raw{qe, n, vpo, vf, vt, nv};
 }
 
 // calcVoronoi on the exported layout (host reference of gvd.hip's builder): quad-edges from #4;

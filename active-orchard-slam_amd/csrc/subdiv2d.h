@@ -74,6 +74,10 @@ class Subdiv2D {
     // qe = 8 ints per quad-edge {next[4], pt[4]} (free quad-edges have next[0] = 0), vp = float2.
     struct Raw { const int *qe; int n_rec; const float *vp; const int *vfirst, *vtype; int n_vtx; };
     Raw raw();
+    // the same state written straight into dst (raw_bytes() bytes: qe | vp | vfirst | vtype), e.g. the
+    // pinned staging buffer of the GPU facet builder: no zero-fill, export buffer or second copy
+    size_t raw_bytes() const { return (8 * sizeof(int) * rec.size()) + (sizeof(V2f) + 2 * sizeof(int)) * vp.size(); }
+    Raw raw_into(void *dst) const;
 
   private:
     struct Rec { int on[2], op[2], org[2], link, pad; };   // d = 0: e = 4q, d = 1: Sym e = 4q + 2
