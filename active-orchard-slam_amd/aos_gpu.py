@@ -496,9 +496,11 @@ class Ctx:
         _check(lib().aos_gvd_wait(self.h, ctypes.byref(o)))
         return _gvd_dict(o)
 
-    def gvd_markers(self, collected: bool = False, copy: bool = True) -> dict:
+    def gvd_markers(self, collected: bool = False, copy: bool = True, view: bool = False) -> dict:
         """/gvd/markers content of the last GVD call (aos_gvd_markers_get); collected=True: of the frame
         last returned by gvd_wait, even with newer jobs in flight (aos_gvd_collected_markers_get).
+        view=True: zero-copy views of the library-owned arrays (the ABI's ownership rule: valid until the
+        next GVD call on the handle), as seedgen(copy_grids=False) returns the grids.
         copy=False (diagnostic): wait for the cells, return only their counts and time."""
         m = GvdMarkers()
         fn = lib().aos_gvd_collected_markers_get if collected else lib().aos_gvd_markers_get
@@ -506,14 +508,15 @@ class Ctx:
         nc = m.n_cells
         if not copy:
             return {"n_cells": nc, "n_seeds": m.n_seeds, "ms_cells": m.ms_cells}
-        off = _arr(m.cell_offsets, nc + 1, np.int32)
-        return {"seeds": _arr(m.seeds_xy, 2 * m.n_seeds, np.float64).reshape(-1, 2),
-                "row_label_pts": _arr(m.row_label_xy, 8 * m.n_rows, np.float64).reshape(-1, 4, 2),
-                "row_label_valid": _arr(m.row_label_valid, 4 * m.n_rows, np.int32).reshape(-1, 4),
+        get = _view_arr if view else _arr
+        off = get(m.cell_offsets, nc + 1, np.int32)
+        return {"seeds": get(m.seeds_xy, 2 * m.n_seeds, np.float64).reshape(-1, 2),
+                "row_label_pts": get(m.row_label_xy, 8 * m.n_rows, np.float64).reshape(-1, 4, 2),
+                "row_label_valid": get(m.row_label_valid, 4 * m.n_rows, np.int32).reshape(-1, 4),
                 "cell_offsets": off,
-                "cell_xy": _arr(m.cell_xy, 2 * int(off[-1]) if nc else 0, np.float64).reshape(-1, 2),
-                "cell_center": _arr(m.cell_center_xy, 2 * nc, np.float64).reshape(-1, 2),
-                "cell_rgba": _arr(m.cell_rgba, 4 * nc, np.float32).reshape(-1, 4), "ms_cells": m.ms_cells}
+                "cell_xy": get(m.cell_xy, 2 * int(off[-1]) if nc else 0, np.float64).reshape(-1, 2),
+                "cell_center": get(m.cell_center_xy, 2 * nc, np.float64).reshape(-1, 2),
+                "cell_rgba": get(m.cell_rgba, 4 * nc, np.float32).reshape(-1, 4), "ms_cells": m.ms_cells}
 
     def gvd(self, seeds, rows_info, grid: dict) -> dict:
         s = np.ascontiguousarray(seeds, dtype=np.float64).reshape(-1)

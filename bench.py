@@ -80,6 +80,9 @@ def parse(argv=None):
                     help="(diagnostic) no publishMarkers cells at all; not the reference's work")
     ap.add_argument("--markers-no-copy", action="store_true",
                     help="(diagnostic) wait for the markers' cells but do not copy them into Python arrays")
+    ap.add_argument("--markers-copy", action="store_true",
+                    help="copy the markers into fresh Python arrays (default: views of the library-owned arrays, "
+                         "as the grids are returned)")
     ap.add_argument("--fixed-root", action="store_true",
                     help="--tiled: rank 0 finishes every frame (default: frame k's root is rank k mod N, so the "
                          "whole-map stages and the GVD jobs rotate over the ranks)")
@@ -348,7 +351,7 @@ def run(a, E, dist, quiet=False):
         return mk
 
     def collect(collected=False):
-        m = ctx.gvd_markers(collected=collected, copy=not a.markers_no_copy)
+        m = ctx.gvd_markers(collected=collected, copy=not a.markers_no_copy, view=not a.markers_copy)
         if pend["mt0"] is not None and a.stream:
             mk_latency.append(time.perf_counter() - pend["mt0"])
         pend["ms"] = m["ms_cells"]
@@ -612,7 +615,8 @@ def run(a, E, dist, quiet=False):
             "markers": {"policy": "every frame" if a.markers_every_frame else
                         f"the frames the node publishes: at most max_graph_publish_rate = {params.max_graph_publish_rate:g} Hz "
                         f"of wall time (gvd:306-314); every frame's graph is built and returned",
-                        "timed_frames_with_markers": mk_frames},
+                        "timed_frames_with_markers": mk_frames,
+                        "returned_as": "copies" if a.markers_copy else "views of the library-owned arrays (ABI ownership rule)"},
             "stages_ms": {k: round(v, 3) for k, v in avg.items()},
             "frame": {"T": T, "rows": len(g["row_length"]), "seeds": len(g["voronoi_seeds"]),
                       "nodes": len(gg["nodes"]), "edges": len(gg["edges"]), "n_binned": g["n_binned"],

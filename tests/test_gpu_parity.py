@@ -331,6 +331,7 @@ def test_gvd_markers_cells_vs_oracle(name):
     assert_gvd_parity(gg, og)
     assert len(m["cell_offsets"]) > 100
     _assert_markers(m, og)
+    _assert_markers(c.gvd_markers(view=True), og)   # zero-copy views of the same arrays (bench.py's way)
     c.close()
 
 
