@@ -1,0 +1,54 @@
+"""Parameter sweep: seeded random node parameters (ROR radius / min neighbours, PassThrough z range,
+inflation radius, cluster_min_length, grid resolution, markers rectangle mode, dense / non-dense) and a jittered exploration
+polygon on a C0-size cloud, each full frame (seed-gen a1-a16 + GVD g1-g9 + markers) bit-exact against
+the oracle run with the same parameters. The other parity tests fix the node's defaults except the
+resolution; this covers the parameter space the reference's YAML exposes."""
+import numpy as np
+import pytest
+
+import aos_gpu
+import oracle_py as O
+import orchard
+from parity_util import assert_gvd_parity, assert_seedgen_parity
+
+pytestmark = pytest.mark.gpu
+
+# field name in aos_params -> in the oracle's params
+_ORACLE_NAME = {"clipping_minz": "clip_minz", "clipping_maxz": "clip_maxz"}
+
+
+def case(seed: int):
+    rng = np.random.default_rng(1000 + seed)
+    kw = {
+        "ror_radius": float(rng.choice([0.12, 0.2, 0.3])),
+        "ror_min_neighbors": int(rng.choice([1, 2, 4, 6])),
+        "inflation_radius": float(np.float32(rng.choice([0.4, 0.8, 1.2]))),
+        "cluster_min_length": float(rng.choice([1.0, 2.0, 3.5])),
+        "grid_resolution": float(np.float32(rng.choice([0.1, 0.15, 0.2, 0.25]))),
+        "subdiv_rect_mode": int(rng.integers(0, 2)),
+    }
+    kw["clipping_minz"], kw["clipping_maxz"] = [(-0.4, 0.5), (-0.2, 0.3), (-1.0, 1.0)][int(rng.integers(0, 3))]
+    poly = orchard.polygon(orchard.CONFIGS["C0"]) + rng.uniform(-3.0, 3.0, size=(4, 2))
+    dense = bool(rng.integers(0, 4))   # a quarter of the cases: is_dense = false (PCL's radius-search branch)
+    return kw, poly, dense
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_random_parameters_full_frame(seed):
+    kw, poly, dense = case(seed)
+    cfg = orchard.CONFIGS["C0"]
+    cloud = orchard.generate(cfg, seed=20 + seed)
+    c = aos_gpu.Ctx(aos_gpu.default_params(**kw))
+    c.set_polygon(poly)
+    g = c.seedgen(cloud, is_dense=dense)
+    okw = {_ORACLE_NAME.get(k, k): v for k, v in kw.items()}
+    o = O.seedgen(cloud, poly, O.default_params(**okw), is_dense=dense)
+    assert_seedgen_parity(g, o)
+    gg = c.gvd_from_seedgen()
+    og = O.gvd(o["voronoi_seeds"], o["rows_info"], o, O.default_params(markers=1, **okw))
+    assert_gvd_parity(gg, og)
+    if og["published"]:
+        m = c.gvd_markers()
+        assert np.array_equal(m["seeds"], og["merged"])
+        assert np.array_equal(m["cell_offsets"], og["cell_offsets"]) and np.array_equal(m["cell_xy"], og["cell_xy"])
+    c.close()
