@@ -277,12 +277,6 @@ constexpr int kRorThreads = AOS_RT_THREADS, kRorCap = 2048, kRorPer = kRorCap / 
 #ifndef AOS_RT_VARIANT   // timing experiments only (tools/ab_rt.sh): 1 = no neighbour scan, 2 = no raster
 #define AOS_RT_VARIANT 0
 #endif
-#ifndef AOS_RT_GROUP     // lanes per candidate in a fitting tile's neighbour counts (0: one lane each + wave queue)
-#define AOS_RT_GROUP 0
-#endif
-#ifndef AOS_RT_QLANE     // fitting tiles: queued (over-budget) candidates one lane each instead of one wave each
-#define AOS_RT_QLANE 1
-#endif
 
 
 template <class Pts>
@@ -301,7 +295,7 @@ __device__ __forceinline__ int rt_scan(const RorLaunch &L, float4 p, Pts pts, in
 // neighbourhood in which it finds too few neighbours: an outlier, up to ~10^4 points in a streaming
 // map's big tile) goes to the workgroup's queue and is counted by a whole wave, 64 points per step.
 // One lane walking such a neighbourhood alone bounded the kernel (~1 ms per scan at C4).
-// Fitting tiles (round 3, AOS_RT_QLANE): the kernel was VALU-issue-bound on divergence (C2: 1.1e8 VALU
+// Fitting tiles (round 3): the kernel was VALU-issue-bound on divergence (C2: 1.1e8 VALU
 // wave-instructions for 5.6 M points; ~3 % of candidates are not kept and walk their whole 3 x 3
 // neighbourhood, so nearly every wave waited on one or two long walks). The first pass now gives each
 // lane 12 points; the queued candidates (~10 %) are walked one lane each with a budget of 96, packed
@@ -525,7 +519,7 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
     // candidates left to the queues: tile-local indices (< kRorCap, 16 bits) in a fitting tile
     using QIdx = typename std::conditional<BIG, int, unsigned short>::type;
     __shared__ int q_n, q2_n;
-    __shared__ QIdx q_k[kRtQCap], q2_k[AOS_RT_QLANE ? kRtQ2Cap : 1];
+    __shared__ QIdx q_k[kRtQCap], q2_k[BIG ? 1 : kRtQ2Cap];
     const int tid = threadIdx.x;
     const int nit = BIG ? big_nchunks(B) : 1;
     for (int it = BIG ? blockIdx.x : 0; it < nit; it += BIG ? gridDim.x : 1) {
@@ -670,35 +664,6 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
             else pts[k].w = cw;
         }
     };
-#if AOS_RT_GROUP
-    // group-cooperative counts (fitting tiles): kRtGroup lanes share one candidate and test kRtGroup
-    // consecutive points of its bin rows per step (one ballot), so a wave's lanes no longer wait for its
-    // slowest candidate's walk
-    if (!BIG) {
-        constexpr int GS = AOS_RT_GROUP, NG = kRorThreads / GS;
-        const int lane = tid & 63, gl = lane & (GS - 1), gshift = lane & ~(GS - 1);
-        for (int k = k0 + tid / GS; k < k1; k += NG) {
-            const float4 p = pts[k];
-            const int w = __float_as_int(p.w), cls = w & kWClass;
-            if (!cls) continue;                 // (group-uniform: every lane of the group read the same p)
-            if (cls == 2) { if (!gl) prev_kept(p); continue; }
-            int bx, by;
-            rt_bin(L, p.x, p.y, bx, by);
-            const int lx = bx - bx0, ly = by - by0;
-            int cnt = AOS_RT_VARIANT == 1 ? L.need : 0;
-            for (int i = 0; i < 3 && cnt < L.need; ++i) {
-                int r0, r1;
-                range(false, lx, ly, i, r0, r1);
-                for (int base = r0; base < r1 && cnt < L.need; base += GS) {
-                    const int j = base + gl;
-                    const bool hit = j < r1 && rt_in(L, p, pts[min(j, r1 - 1)]);
-                    cnt += (int)__popcll((__ballot(hit) >> gshift) & ((GS == 64) ? ~0ull : ((1ull << GS) - 1)));
-                }
-            }
-            if (!gl) decide(p, k, cnt);
-        }
-    } else
-#endif
     for (int k = k0 + tid; k < k1; k += kRorThreads) {
         const float4 p = BIG ? P[k] : pts[k];
         const int w = __float_as_int(p.w), cls = w & kWClass;
@@ -728,9 +693,8 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
         decide(p, k, cnt);
     }
     __syncthreads();
-    {   // the queued candidates, one wave each
+    {   // the queued candidates
         const int nq = min(q_n, kRtQCap), lane = tid & 63;
-#if AOS_RT_QLANE
         if (!BIG) {
             // fitting tiles: the over-budget candidates one lane each (restarted, budget kRtBudget2), so the
             // long walks run packed together; the few still undecided after that, one wave each
@@ -774,8 +738,7 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
                 }
                 if (lane == 0) decide(p, k, cnt);
             }
-        } else
-#endif
+        } else   // big tiles: one wave each
         for (int i = tid >> 6; i < nq; i += kRorThreads / 64) {
             const int k = q_k[i];
             const float4 p = BIG ? P[k] : pts[k];
