@@ -1,3 +1,6 @@
+#!/bin/bash
+# A/B of the Subdiv2D export straight into pinned memory (profiles/r03k_gvd_trace_export_ab.log): the base is
+# the previous commit built beside the product (git stash; make BUILD=build_base LIB=libaos_gpu_base.so)
 set -e
 mkdir -p gpurun_out
 for i in 1 2; do
