@@ -52,3 +52,30 @@ def test_random_parameters_full_frame(seed):
         assert np.array_equal(m["seeds"], og["merged"])
         assert np.array_equal(m["cell_offsets"], og["cell_offsets"]) and np.array_equal(m["cell_xy"], og["cell_xy"])
     c.close()
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_parameters_stream(seed):
+    """The streaming map (aos_map_append) under the same random parameters: its incremental
+    ROR (tile store, kept marks, stored neighbour counts of the big tiles) and every later stage must equal
+    the oracle's full reprocessing of the concatenated scans after every append."""
+    kw, _, dense = case(100 + seed)
+    kw["grid_resolution"] = 0.1   # (C1's grid)
+    cfg = orchard.CONFIGS["C1"]
+    poly = orchard.polygon(cfg)
+    rng = np.random.default_rng(seed)
+    poses = sorted(int(k) for k in rng.integers(0, 400, size=4))
+    scans = [orchard.generate_scan(cfg, k, n_points=int(rng.integers(60_000, 200_000))) for k in poses]
+    okw = {_ORACLE_NAME.get(k, k): v for k, v in kw.items()}
+    s = aos_gpu.Ctx(aos_gpu.default_params(**kw))
+    s.set_polygon(poly)
+    s.map_reset(reserve_points=100_000)
+    for k in range(len(scans)):
+        g = s.map_append(scans[k], is_dense=dense)
+        full = np.concatenate(scans[:k + 1])
+        o = O.seedgen(full, poly, O.default_params(**okw), is_dense=dense)
+        assert_seedgen_parity(g, o)
+        assert g["n_clipped"] == o["n_clipped"] and g["n_input"] == o["n_input"] == full.shape[0]
+        gg = s.gvd_from_seedgen()
+        assert_gvd_parity(gg, O.gvd(o["voronoi_seeds"], o["rows_info"], o, O.default_params(**okw)))
+    s.close()
