@@ -79,3 +79,31 @@ def test_random_parameters_stream(seed):
         gg = s.gvd_from_seedgen()
         assert_gvd_parity(gg, O.gvd(o["voronoi_seeds"], o["rows_info"], o, O.default_params(**okw)))
     s.close()
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_parameters_tiled(seed):
+    """The tiled frame (halo exchange, distributed cluster labelling and numbering, BFS
+    replays split over the ranks) under random parameters, tilings and roots (ranks as threads on one
+    GPU, aos_group_*): the root's frame and graph bit-exact vs the oracle."""
+    import aos_tiles as T
+    kw, poly, dense = case(200 + seed)
+    kw["grid_resolution"] = float(np.float32([0.1, 0.15, 0.2][seed % 3]))
+    rng = np.random.default_rng(300 + seed)
+    tiles = [(2, 1), (1, 2), (2, 2), (3, 1), (4, 2), (2, 3)][seed]
+    world = tiles[0] * tiles[1]
+    root = int(rng.integers(0, world))
+    cfg = orchard.CONFIGS["C1"]
+    cloud = orchard.generate(cfg, seed=40 + seed, n_points=600_000)
+    poly = orchard.polygon(cfg) + rng.uniform(-4.0, 4.0, size=(4, 2))
+    grp = aos_gpu.Group(aos_gpu.default_params(**kw), [0] * world, *tiles)
+    grp.set_polygon(poly)
+    parts = [T.shard(cloud, grp.plan(r)["points_box"]) for r in range(world)]
+    g = grp.process(parts, root=root, is_dense=dense)
+    gg = grp.rank(root).gvd_from_seedgen()
+    grp.close()
+    okw = {_ORACLE_NAME.get(k, k): v for k, v in kw.items()}
+    o = O.seedgen(cloud, poly, O.default_params(**okw), is_dense=dense)
+    assert_seedgen_parity(g, o)
+    assert g["n_clipped"] == o["n_clipped"]
+    assert_gvd_parity(gg, O.gvd(o["voronoi_seeds"], o["rows_info"], o, O.default_params(**okw)))
