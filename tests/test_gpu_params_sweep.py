@@ -107,3 +107,40 @@ def test_random_parameters_tiled(seed):
     assert_seedgen_parity(g, o)
     assert g["n_clipped"] == o["n_clipped"]
     assert_gvd_parity(gg, O.gvd(o["voronoi_seeds"], o["rows_info"], o, O.default_params(**okw)))
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_parameters_path_queries(seed):
+    """aos_path_plan on the graph of a random-parameter frame, for 24 seeded node states
+    (targets in and out of range, previous waypoints, robot positions, the initial waypoint, saved targets,
+    exploration completed): every output field bit-exact vs the oracle's aos_path_gen_node."""
+    from test_gpu_path import assert_path_equal
+    kw, poly, dense = case(400 + seed)
+    cfg = orchard.CONFIGS["C0"] if seed % 2 else orchard.CONFIGS["C1"]
+    cloud = orchard.generate(cfg, seed=60 + seed, n_points=None if seed % 2 else 800_000)
+    if not seed % 2:
+        kw["grid_resolution"] = 0.1
+    c = aos_gpu.Ctx(aos_gpu.default_params(**kw))
+    c.set_polygon(poly if seed % 2 else orchard.polygon(cfg))
+    f = c.seedgen(cloud, is_dense=dense)
+    gg = c.gvd_from_seedgen()
+    grid = {"origin": f["origin"], "resolution": f["resolution"], "width": f["width"], "height": f["height"],
+            "skeleton_framed": f["skeleton_framed"]}
+    n_wp = len(O.path_plan(gg, grid, target=0)["waypoints"])
+    rng = np.random.default_rng(500 + seed)
+    W, H = f["width"] * f["resolution"], f["height"] * f["resolution"]
+    ox, oy = f["origin"]
+    for i in range(24):
+        q = {"target": int(rng.integers(-1, n_wp + 3)), "previous": int(rng.integers(-1, n_wp + 1))}
+        if rng.random() < 0.3:
+            q["current"] = (float(ox + rng.uniform(0, W)), float(oy + rng.uniform(0, H)))
+        if rng.random() < 0.2:
+            q["initial_waypoint_reached"] = False
+            q["initial_waypoint"] = (float(ox + rng.uniform(0, W)), float(oy + rng.uniform(0, H)))
+        if rng.random() < 0.2:
+            q["saved_target"] = (float(ox + rng.uniform(0, W)), float(oy + rng.uniform(0, H)))
+        if rng.random() < 0.15:
+            q["exploration_completed"] = True
+        ref = O.path_plan(gg, grid, **q)
+        assert_path_equal(c.path_plan(aos_gpu.path_query(**q)), ref, f"{seed}/{i} {q}")
+    c.close()
