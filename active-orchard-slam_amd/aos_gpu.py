@@ -13,13 +13,29 @@ import subprocess
 
 import numpy as np
 
-# numpy madvise(MADV_HUGEPAGE)s every allocation >= 4 MB. Copying the /gvd/markers arrays out of
-# the library then stalls the next GPU synchronisation of the process by 10-30 ms (measured on the
-# MI355X box: profiles/r03d_stream*.json with the copies, r03f with this switch), most
-# likely the transparent-huge-page work on those pages invalidating the device's view of the address
-# space. The binding turns the madvise off for the process; AOS_NUMPY_HUGEPAGE=1 keeps numpy's default.
-if os.environ.get("AOS_NUMPY_HUGEPAGE") != "1" and hasattr(np._core.multiarray, "_set_madvise_hugepage"):
-    np._core.multiarray._set_madvise_hugepage(False)
+
+
+def disable_numpy_hugepage() -> bool:
+    """Turn off numpy's madvise(MADV_HUGEPAGE) of allocations >= 4 MB for this process.
+
+    Copying the /gvd/markers arrays out of the library into fresh numpy arrays stalled the next GPU
+    synchronisation of the process by 10-30 ms (measured on the MI355X box: profiles/r03d_stream*.json
+    with the copies, r03f with the switch), most likely the transparent-huge-page work on
+    those pages invalidating the device's view of the address space. This changes numpy's behaviour for
+    every user in the process, so it is opt-in: the bench (a long-running loop that copies the markers)
+    calls it; importing the binding does not. Returns whether the switch exists in this numpy.
+    """
+    try:
+        core = getattr(np, "_core", None) or getattr(np, "core", None)
+        mod = getattr(core, "multiarray", None)
+        fn = getattr(mod, "_set_madvise_hugepage", None)
+        if fn is None:
+            return False
+        fn(False)
+        return True
+    except Exception:  # a private numpy API: absent or changed -> leave numpy's default
+        return False
+
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
@@ -162,6 +178,13 @@ class TilePlan(ctypes.Structure):
                 ("points_box", c_d * 4), ("exchange_bytes", c_u64), ("info", GridInfo)]
 
 
+class TiledStats(ctypes.Structure):
+    _fields_ = [("ms_frame", c_f), ("ms_comm_gather", c_f), ("ms_comm_reduce", c_f), ("n_gather", c_i),
+                ("n_reduce", c_i), ("bytes_gather", c_u64), ("ms_ror", c_f), ("ms_thin", c_f), ("ms_cluster", c_f),
+                ("ms_seeds", c_f), ("ms_cluster_local", c_f), ("ms_cluster_global", c_f), ("ms_replay", c_f),
+                ("n_replayed", c_i), ("ror_skipped", c_i), ("is_root", c_i)]
+
+
 def build() -> str:
     subprocess.check_call(["make", "-s", "-C", HERE, "-j8"])
     return LIB_PATH
@@ -217,6 +240,7 @@ def lib():
         L.aos_map_append.argtypes = [c_vp, P(CloudView), c_i, P(SeedGenOut)]
         L.aos_tile_plan_compute.argtypes = [P(Params), c_vp, c_u, c_i, c_i, c_i, P(TilePlan)]
         L.aos_tiled_seedgen_process.argtypes = [c_vp, P(Comm), c_i, c_i, c_i, P(CloudView), c_i, P(SeedGenOut)]
+        L.aos_tiled_stats_get.argtypes = [c_vp, P(TiledStats)]
         L.aos_path_plan.argtypes = [c_vp, P(PathGraph), c_vp, c_i, P(GridInfo), P(PathQuery), P(PathOut)]
         L.aos_group_create.argtypes = [P(Params), P(c_i), c_i, c_i, P(c_vp)]
         L.aos_group_destroy.argtypes = [c_vp]
@@ -393,6 +417,21 @@ class Ctx:
         _check(lib().aos_map_append(self.h, ctypes.byref(v), int(want_host), ctypes.byref(o)))
         return _seedgen_dict(o, want_host)
 
+    def tiled_stats(self) -> dict:
+        """Where this rank's last tiled frame spent its time (aos_tiled_stats_get)."""
+        t = TiledStats()
+        _check(lib().aos_tiled_stats_get(self.h, ctypes.byref(t)))
+        return {name: getattr(t, name) for name, _ in TiledStats._fields_}
+
+    def _tiled_result(self, o, is_root: bool, want_host: bool) -> dict:
+        if is_root:
+            return {**_seedgen_dict(o, want_host), "root": True, "tiled_stats": self.tiled_stats()}
+        return {"root": False, "width": o.info.width, "height": o.info.height, "thin_iters": o.thin_iters,
+                "n_clipped": o.n_clipped, "n_input": o.n_input, "n_binned": o.n_binned,
+                "ms": {"ror": o.ms_ror, "grid": o.ms_grid, "thin": o.ms_thin, "total": o.ms_total,
+                       "ror_count": o.ms_ror_count, "ror_bin": o.ms_ror_bin, "ror_scatter": o.ms_ror_scatter},
+                "tiled_stats": self.tiled_stats()}
+
     def tiled_seedgen(self, comm, tiles_x: int, tiles_y: int, cloud, root: int = 0, n_points: int | None = None,
                       point_step=16, offs=(0, 4, 8), is_dense=True, on_device=False, want_host=True) -> dict:
         """One tiled frame on this rank (aos_tiled_seedgen_process); comm: a TorchDistComm / ThreadGroup comm.
@@ -405,12 +444,7 @@ class Ctx:
         if comm.error is not None:
             raise RuntimeError(f"communicator failed: {comm.error!r}") from comm.error
         _check(rc)
-        if comm.rank == root:
-            return {**_seedgen_dict(o, want_host), "root": True}
-        return {"root": False, "width": o.info.width, "height": o.info.height, "thin_iters": o.thin_iters,
-                "n_clipped": o.n_clipped, "n_input": o.n_input, "n_binned": o.n_binned,
-                "ms": {"ror": o.ms_ror, "grid": o.ms_grid, "thin": o.ms_thin, "total": o.ms_total,
-                       "ror_count": o.ms_ror_count, "ror_bin": o.ms_ror_bin, "ror_scatter": o.ms_ror_scatter}}
+        return self._tiled_result(o, comm.rank == root, want_host)
 
     def tiled_map_append(self, comm, tiles_x: int, tiles_y: int, scan, root: int = 0, n_points: int | None = None,
                          point_step=16, offs=(0, 4, 8), is_dense=True, on_device=False, want_host=True) -> dict:
@@ -424,12 +458,7 @@ class Ctx:
         if comm.error is not None:
             raise RuntimeError(f"communicator failed: {comm.error!r}") from comm.error
         _check(rc)
-        if comm.rank == root:
-            return {**_seedgen_dict(o, want_host), "root": True}
-        return {"root": False, "width": o.info.width, "height": o.info.height, "thin_iters": o.thin_iters,
-                "n_clipped": o.n_clipped, "n_input": o.n_input, "n_binned": o.n_binned,
-                "ms": {"ror": o.ms_ror, "grid": o.ms_grid, "thin": o.ms_thin, "total": o.ms_total,
-                       "ror_count": o.ms_ror_count, "ror_bin": o.ms_ror_bin, "ror_scatter": o.ms_ror_scatter}}
+        return self._tiled_result(o, comm.rank == root, want_host)
 
     def reprocess(self, want_host=True) -> dict:
         o = SeedGenOut()

@@ -64,6 +64,7 @@ struct aos_ctx {
     aos::DevBuf cloud_copy, bin_count, bin_start, pt_binslot, sorted, ror_scratch, ror_bigbins, scan_tmp, counters;
     aos::DevBuf raster_bits, infl_bits, open_bits, thin_a, thin_b, thin_act, occ_bytes, skel_bytes, flags;
     aos::DevBuf thin_out;   // the converged skeleton bits, picked on the device (launch_thin_pick)
+    aos::LookBackScratch ror_lb;           // single-pass scans of the ROR stage (tile starts)
     aos::DevBuf full_infl, full_skel;      // tiled frames: the whole map, assembled on the root rank
     aos::PinnedBuf h_small, h_stats;
     // Host -> device upload of a large pageable buffer (a PointCloud2 message): kUpThreads host
@@ -192,11 +193,15 @@ struct aos_ctx {
     void ror_stage(const aos::FrameGeom &g, const RorOwn &o, uint64_t *rbits, bool allow_guess);
     bool ror_collect();   // after the stream synchronised: true if the ROR scatter overflowed
     void ror_stage_append(aos::RorLaunch L, uint64_t *rbits);   // streaming map: one scan on the tile store
+    void ror_stage_unchanged();   // streaming map: no new points since the committed store
+    uint64_t ror_skipped = 0;     // frames that skipped the ROR stage that way
     void finish_frame(const aos::FrameGeom &g, bool want_host, const uint64_t *clipped_total, aos_seedgen_out &out,
                       const aos::PreClusters *pre = nullptr);
     void run_seedgen(bool want_host, aos_seedgen_out &out);
     bool run_seedgen_once(bool want_host, aos_seedgen_out &out, bool allow_guess);   // true: redo
     void run_tiled(const aos_comm &cm, int tiles_x, int tiles_y, int root, bool want_host, aos_seedgen_out &out);
+    void run_tiled_frame(const aos_comm &cm, int tiles_x, int tiles_y, int root, bool want_host, aos_seedgen_out &out);
+    aos_tiled_stats tstats{};   // the last tiled frame's breakdown (aos_tiled_stats_get)
     void tile_halo_exchange(uint64_t *win, const aos::TilePlan &t, const aos_comm &cm);
     void run_gvd_external(const aos_gvd_in &in, aos_gvd_out &out);
     void run_gvd_from_frame(aos_gvd_out &out);

@@ -336,6 +336,12 @@ int aos_tiled_map_append(aos_ctx *c, const aos_comm *comm, int32_t tiles_x, int3
     AOS_GUARD_END
 }
 
+int aos_tiled_stats_get(aos_ctx *c, aos_tiled_stats *out) {
+    if (!c || !out) { set_error("aos_tiled_stats_get: null argument"); return AOS_E_INVALID; }
+    *out = c->tstats;
+    return AOS_OK;
+}
+
 // settle = true: the handle's newest result (a job started since the last aos_gvd_wait is waited for);
 // false: the frame last returned by aos_gvd_wait / a synchronous GVD call, even with newer jobs in flight
 static int markers_get(aos_ctx *c, aos_gvd_markers *out, bool settle) {

@@ -436,7 +436,9 @@ void cluster_dist(ClusterDistState &D, const aos_comm &cm, const TilePlan &t, co
             at += lrec[l].n;
         }
         AOS_HIP(hipStreamSynchronize(s));
+        const auto tr0 = clk::now();
         replay_clusters(jobs, g, hp.data(), np, min_len, lrec.data());
+        st.ms_replay = std::chrono::duration<float, std::milli>(clk::now() - tr0).count();
         st.n_replayed_here = (int)my_jobs.size();
         std::vector<ReplayOut> outs;
         for (int l : my_jobs) outs.push_back(ReplayOut{l, 0, lrec[l]});

@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "aos_internal.h"
+#include "dev_prims.h"
 #include "subdiv2d.h"
 
 namespace aos {
@@ -26,14 +27,12 @@ struct ClusterRec {
 // ------------------------------------------------------------------ greedy first-come de-duplication
 // Keeps candidate i iff no earlier KEPT candidate conflicts with it (the reference's
 // "if no existing within d: push_back" loops) = the lexicographically-first maximal independent
-// set of the conflict graph; decided on the GPU in rounds over hashed conflict lists.
+// set of the conflict graph; decided on the GPU by one fused kernel over a hashed cell index (greedy.hip).
 enum ConflictMode {
     kConflictLess = 0,     // sqrt(dx*dx + dy*dy) <  thr  (seed dedups, seed_gen:2076-2085 ...)
     kConflictLessEq = 1,   // sqrt(dx*dx + dy*dy) <= thr  (GVD seed merge, gvd:107-115)
     kConflictKeyOrSq = 2,  // same (int)(x*100),(int)(y*100) key, or dx*dx + dy*dy < thr (extractBoundaryPoints)
 };
-struct HashG { double x0, y0, inv; int nx, ny; };
-HashG make_hash(double minx, double maxx, double miny, double maxy, double cell);
 // Waits for the work queued so far on a stream through an event of the caller's own: a GVD lane's host
 // thread waits for its own work only, not for other lanes' work queued on the shared GVD stream.
 struct SyncEvent {
@@ -49,17 +48,43 @@ struct SyncEvent {
     }
 };
 
-struct DedupScratch { DevBuf keys, idx, skeys, sidx, ccount, coff, clist, state, f, pos, tmp, und, rows; int n_conf = 0; SyncEvent sev; };
-// cand/ok device arrays of n entries; kept points (in order) -> out; optional kept flags -> state (S.state).
-// Returns the kept count.
+struct DedupScratch {
+    CellScratch cells;
+    CellIdx ci{};          // the cell index of the last de-duplication (the GVD merge finds members through it)
+    LookBackScratch lb;
+    DevBuf state, misc;
+    unsigned epoch = 0;    // of the state words
+    SyncEvent sev;
+};
+// Enqueues one de-duplication (no host synchronisation): cand / ok (nullable: all ok) device arrays of n
+// entries, h a hash with cells >= the conflict radius and a bounded bucket count (make_hash_n); the kept
+// points in order -> out, their indices -> kept_index (nullable), the kept count -> *d_count (device).
+// owner (nullable): per candidate, the smallest kept candidate it conflicts with (itself if kept, INT_MAX
+// if not ok): the members of each merged seed (gvd:93-125). pos_of (nullable): per candidate, its position
+// in out or -1 (the GVD graph finds boundary points through the de-duplication's own index, S.ci).
+void greedy_dedup_async(DedupScratch &S, const double2 *cand, const int *ok, int n, int mode, double thr, const HashG &h,
+                        double2 *out, int *kept_index, int *owner, int *d_count, hipStream_t s, int *pos_of = nullptr);
+// The same, then waits and returns the kept count (h_scalar: 2 pinned ints).
 int greedy_dedup(DedupScratch &S, const double2 *cand, const int *ok, int n, int mode, double thr, const HashG &h,
                  double2 *out, int *kept_index_out, hipStream_t s, int *h_scalar);
+// Problems of at most kSmallMax candidates (up to 2 per launch), one workgroup each, the index and the
+// rounds in LDS: one launch. h: small_hash (at most 2048 buckets).
+constexpr int kSmallMax = 4096;
+struct SmallProb { const double2 *p; const int *ok; int n; HashG h; double2 *out; int *count; };
+struct SmallDedup { SmallProb prob[2]; int mode; double thr; int *err; };
+void greedy_dedup_small(DedupScratch &S, SmallDedup A, int nprob, hipStream_t s);
+HashG small_hash(double minx, double maxx, double miny, double maxy, double cell);
+// The device error word of S's launches (0 = fine) and the check of its value once read back.
+int *dedup_err(DedupScratch &S, hipStream_t s);
+void dedup_check(DedupScratch &S, int err_word);
 
 struct ClusterSeedState {
     DedupScratch dedup;
     DevBuf fg_bits, word_cnt, word_off, fg_list, parent, root_flag, root_rank, cl_count, cl_off, cl_cursor, cl_cells;
     DevBuf rec, row_idx, poly, cur_tab;
     DevBuf cand_xy, cand_ok, cand_state, hash_count, hash_start, hash_slot, hash_sorted, seed_out, misc, scan_tmp;
+    LookBackScratch lb;           // the stage's single-pass scans
+    bool cl_count_dirty = true;   // cl_count (cluster sizes) not known to be zero
     PinnedBuf h_misc;
     int n_fg = 0, n_clusters = 0, n_rows = 0, n_cur_tab = 0;
     double cur_tab_amax = -1.0;
@@ -112,6 +137,7 @@ struct ClusterDistState {
 struct ClusterDistStats {
     int n_pieces = 0, n_border = 0, n_long = 0, long_cells = 0, n_replayed_here = 0;
     float ms_local = 0, ms_global = 0;   // own labelling / tables, union-find, long-cluster statistics and replays
+    float ms_replay = 0;                 // (of ms_global) this rank's exact BFS replays
 };
 // The tiled frame's cluster stage on one rank (collective over the tile ranks): win = the rank's
 // window skeleton (own cells exact). The root receives every cluster's record in pre.
@@ -126,7 +152,7 @@ void cluster_dist(ClusterDistState &D, const aos_comm &cm, const TilePlan &t, co
 // and sharing lines with the main replay's fields slowed both down by ~40 % on the EPYC host.
 // Device buffers of the facet builder (calcVoronoi + getVoronoiFacetList on the GPU, gvd.hip).
 // raw = the exported Subdiv2D state in one buffer (quad-edges | points | firstEdge | type), one H2D copy
-struct FacetBufs { DevBuf raw, face, cnt, off, scan_tmp; PinnedBuf h_stage; int *qe = nullptr, *vf = nullptr, *vt = nullptr; };
+struct FacetBufs { DevBuf raw, face, cnt, off, scan_tmp; LookBackScratch lb; PinnedBuf h_stage; int *qe = nullptr, *vf = nullptr, *vt = nullptr; };
 
 struct alignas(128) CellsWork {
     Subdiv2D sd;                               // extractCellBoundaries' Subdiv2D
@@ -177,6 +203,7 @@ struct GvdState {
     std::vector<int32_t> labels, cluster_idx, label_counts, label_clusters, label_types, edges_out;
     std::vector<float> lengths, clearances;
     int n_merged = 0, n_vor_edges = 0, n_bpts = 0;
+    int pairs_cap = 0;   // capacity of the g6 pair lists (from the last frame's pair count)
     float ms_merge = 0, ms_delaunay = 0, ms_graph = 0, ms_total = 0;
     // markers (aos_gvd_markers)
     bool have_markers = false;

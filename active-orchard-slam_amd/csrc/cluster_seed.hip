@@ -13,8 +13,6 @@
 // maximal independent set of the conflict graph in candidate order; the GPU builds the graph
 // with a uniform hash and decides the set in rounds (a candidate is kept once every earlier
 // conflicting candidate is removed, removed once one of them is kept).
-#include <hipcub/hipcub.hpp>
-
 #include <algorithm>
 #include <atomic>
 #include <cmath>
@@ -26,6 +24,7 @@
 
 #include "cluster_dev.h"
 #include "cluster_seed.h"
+#include "dev_prims.h"
 
 namespace aos {
 
@@ -53,7 +52,8 @@ __global__ void k_fg(const uint64_t *skel, uint64_t *fg, int *cnt, GridC g, cons
     cnt[wi] = __popcll(o);
 }
 
-__global__ void k_fg_list(const uint64_t *fg, const int *off, int *list, GridC g) {
+// (parent != nullptr: also the union-find's initial parents, parent[k] = k)
+__global__ void k_fg_list(const uint64_t *fg, const int *off, int *list, GridC g, int *parent) {
     int c = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
     if (c >= g.WW || y >= g.H) return;
     size_t wi = (size_t)y * g.WW + c;
@@ -62,6 +62,7 @@ __global__ void k_fg_list(const uint64_t *fg, const int *off, int *list, GridC g
     while (w) {
         int b = __ffsll((long long)w) - 1;
         w &= w - 1;
+        if (parent) parent[k] = k;
         list[k++] = y * g.W + c * 64 + b;
     }
 }
@@ -98,16 +99,40 @@ __global__ void k_ccl_flatten(int *parent, int *is_root, int n) {
     parent[i] = x;
     is_root[i] = (x == i);
 }
-__global__ void k_cluster_ids(const int *parent, const int *rank, int n, int *cid_of) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) cid_of[i] = rank[parent[i]];
+// Counting sort of the foreground cells by cluster id (cluster = rank of the cell's root among the roots,
+// i.e. raster order of first cells): per cell its id and its rank inside the cluster. A cluster holds
+// thousands of cells and the list is in raster order, so a block's 256 cells touch few clusters: they are
+// counted in an LDS table first and each block adds one total per cluster to the global counter.
+// The order inside a cluster is the blocks' atomics order; k_cluster_stats is order-free and the BFS
+// replay starts from the smallest cell.
+constexpr int kClTB = 256, kClSlots = 512;
+__global__ __launch_bounds__(kClTB) void k_cluster_count(const int *parent, const int *rank, int n, int *cid_of, int *crank,
+                                                       int *cl_cnt) {
+    __shared__ int key[kClSlots], cnt[kClSlots];
+    const int tid = threadIdx.x, i = blockIdx.x * kClTB + tid;
+    for (int k = tid; k < kClSlots; k += kClTB) { key[k] = -1; cnt[k] = 0; }
+    __syncthreads();
+    int cid = -1, slot = 0, lr = 0;
+    if (i < n) {
+        cid = rank[parent[i]];
+        cid_of[i] = cid;
+        slot = (int)(((unsigned)cid * 2654435761u) >> 23) & (kClSlots - 1);
+        for (;;) {   // (at most kClTB distinct ids per block: a free slot always exists)
+            const int old = atomicCAS(&key[slot], -1, cid);
+            if (old == -1 || old == cid) break;
+            slot = (slot + 1) & (kClSlots - 1);
+        }
+        lr = atomicAdd(&cnt[slot], 1);
+    }
+    __syncthreads();
+    for (int k = tid; k < kClSlots; k += kClTB)
+        if (key[k] >= 0) cnt[k] = atomicAdd(&cl_cnt[key[k]], cnt[k]);   // the block's base in the cluster
+    __syncthreads();
+    if (i < n) crank[i] = cnt[slot] + lr;
 }
-// clusters are contiguous after the stable sort by id: record where each one starts
-__global__ void k_run_starts(const int *sorted_cid, int n, int *off, int ncl) {
-    int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n) return;
-    if (k == 0 || sorted_cid[k - 1] != sorted_cid[k]) off[sorted_cid[k]] = k;
-    if (k == n - 1) off[ncl] = n;
+__global__ void k_cluster_scatter(const int *list, const int *cid_of, const int *crank, const int *off, int n, int *cells) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) cells[off[cid_of[i]] + crank[i]] = list[i];
 }
 
 // ------------------------------------------------------------------ per-cluster statistics
@@ -320,7 +345,8 @@ static void host_bfs_replay(const int *cells, int n, const GridC &g, const doubl
         tab[h] = cells[k];
     }
     q.resize(n);
-    const int start = cells[0];   // first raster cell of the component
+    int start = cells[0];   // first raster cell of the component (the cells come in any order)
+    for (int k = 1; k < n; ++k) start = std::min(start, cells[k]);
     tab[slot_of(start)] |= (int)0x80000000;
     q[0] = start;
     int head = 0, tail = 1;
@@ -563,6 +589,15 @@ __global__ void k_endpoint_candidates(const RowDev *rows, int n_rows, double2 *c
     ok[s] = 1;
 }
 
+// /voronoi_seeds order (seed_gen:1670-1710): virtual, ray, endpoint seeds (counts on the device)
+__global__ void k_concat3(const double2 *a, const double2 *b, const double2 *c, const int *cnt, double2 *out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int na = cnt[0], nb = cnt[1], nc = cnt[2];
+    if (i < na) out[i] = a[i];
+    else if (i < na + nb) out[i] = b[i - na];
+    else if (i < na + nb + nc) out[i] = c[i - na - nb];
+}
+
 // ------------------------------------------------------------------ host orchestration
 template <class T> static T *dev(DevBuf &b, size_t n) { return static_cast<T *>(b.ensure(sizeof(T) * std::max<size_t>(n, 1))); }
 
@@ -581,17 +616,16 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
     const size_t Cw = (size_t)g.WW * g.H;
     uint64_t *d_fg = nullptr;
     int *d_wc = nullptr, *d_wo = nullptr;
-    size_t tb = 0;
     const dim3 gw2(cdiv(g.WW, 64), g.H);
     if (!in.pre) {
         d_fg = dev<uint64_t>(S.fg_bits, Cw);
         d_wc = dev<int>(S.word_cnt, Cw + 1); d_wo = dev<int>(S.word_off, Cw + 1);
-        AOS_HIP(hipMemsetAsync(d_wc + Cw, 0, sizeof(int), s));
         k_fg<<<gw2, 64, 0, s>>>(in.skel_bits, d_fg, d_wc, g, d_poly, np);
-        AOS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (int *)nullptr, (int *)nullptr, (int)Cw + 1, s));
-        AOS_HIP(hipcub::DeviceScan::ExclusiveSum(S.scan_tmp.ensure(tb), tb, d_wc, d_wo, (int)Cw + 1, s));
+        scan_1p(S.lb, d_wc, d_wo, (int)Cw, false, s);
         AOS_HIP(hipMemcpyAsync(h_sc, d_wo + Cw, sizeof(int), hipMemcpyDeviceToHost, s));
+        AOS_HIP(hipMemcpyAsync(h_sc + 1, S.lb.err_word(s), sizeof(int), hipMemcpyDeviceToHost, s));
         S.dedup.sev.sync(s);
+        if (h_sc[1]) throw std::runtime_error("cluster stage: scan failed on the device");
     }
     const int nf = in.pre ? in.pre->n_fg : h_sc[0];
     S.n_fg = nf;
@@ -605,33 +639,29 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         out.n_bfs = in.pre->n_bfs;
     } else if (nf > 0) {
         int *d_list = dev<int>(S.fg_list, nf);
-        k_fg_list<<<gw2, 64, 0, s>>>(d_fg, d_wo, d_list, g);
         int *d_par = dev<int>(S.parent, nf), *d_isroot = dev<int>(S.root_flag, nf + 1), *d_rank = dev<int>(S.root_rank, nf + 1);
-        k_ccl_init<<<cdiv(nf, 256), 256, 0, s>>>(d_par, nf);
+        k_fg_list<<<gw2, 64, 0, s>>>(d_fg, d_wo, d_list, g, d_par);
         k_ccl_union<<<cdiv(nf, 256), 256, 0, s>>>(d_list, nf, d_fg, d_wo, g, d_par);
-        AOS_HIP(hipMemsetAsync(d_isroot + nf, 0, sizeof(int), s));
         k_ccl_flatten<<<cdiv(nf, 256), 256, 0, s>>>(d_par, d_isroot, nf);
-        size_t tb2 = 0;
-        AOS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, (int *)nullptr, (int *)nullptr, nf + 1, s));
-        void *tmp = S.scan_tmp.ensure(std::max(tb, tb2));
-        AOS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, d_isroot, d_rank, nf + 1, s));
+        scan_1p(S.lb, d_isroot, d_rank, nf, false, s);
         AOS_HIP(hipMemcpyAsync(h_sc, d_rank + nf, sizeof(int), hipMemcpyDeviceToHost, s));
+        AOS_HIP(hipMemcpyAsync(h_sc + 1, S.lb.err_word(s), sizeof(int), hipMemcpyDeviceToHost, s));
         S.dedup.sev.sync(s);
+        if (h_sc[1]) throw std::runtime_error("cluster stage: scan failed on the device");
         const int ncl = h_sc[0];
         S.n_clusters = ncl;
-        // bucket the foreground cells by cluster id: stable radix sort (keeps raster order inside a
-        // cluster) instead of per-cell atomics on ~100 hot counters
+        // bucket the foreground cells by cluster id: counting sort (k_cluster_count)
+        const size_t cc0 = S.cl_count.cap;
+        int *d_ccnt = dev<int>(S.cl_count, ncl + 1);
+        if (S.cl_count.cap != cc0 || S.cl_count_dirty) AOS_HIP(hipMemsetAsync(d_ccnt, 0, S.cl_count.cap, s));
+        S.cl_count_dirty = true;
         int *d_off = dev<int>(S.cl_off, ncl + 1);
-        int *d_cid = dev<int>(S.cl_cursor, 2 * (size_t)nf), *d_scid = d_cid + nf;
+        int *d_cid = dev<int>(S.cl_cursor, 2 * (size_t)nf), *d_crank = d_cid + nf;
         int *d_cells = dev<int>(S.cl_cells, nf);
-        k_cluster_ids<<<cdiv(nf, 256), 256, 0, s>>>(d_par, d_rank, nf, d_cid);
-        int bits = 1;
-        while ((1 << bits) <= ncl) ++bits;
-        size_t tbs = 0;
-        AOS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbs, d_cid, d_scid, d_list, d_cells, nf, 0, bits, s));
-        tmp = S.scan_tmp.ensure(std::max(std::max(tb, tb2), tbs));
-        AOS_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tbs, d_cid, d_scid, d_list, d_cells, nf, 0, bits, s));
-        k_run_starts<<<cdiv(nf, 256), 256, 0, s>>>(d_scid, nf, d_off, ncl);
+        k_cluster_count<<<cdiv(nf, kClTB), kClTB, 0, s>>>(d_par, d_rank, nf, d_cid, d_crank, d_ccnt);
+        scan_1p(S.lb, d_ccnt, d_off, ncl, true, s);   // (leaves the counts zero)
+        S.cl_count_dirty = false;
+        k_cluster_scatter<<<cdiv(nf, 256), 256, 0, s>>>(d_list, d_cid, d_crank, d_off, nf, d_cells);
         ClusterRec *d_rec = dev<ClusterRec>(S.rec, ncl);
         launch_cluster_stats(d_off, d_cells, ncl, g, d_poly, np, static_cast<float>(in.cluster_min_length), d_rec, s);
         S.h_rec.resize(ncl);
@@ -641,9 +671,9 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         for (const auto &r : S.h_rec) n_bfs += (r.flags & 2) != 0;
         out.n_bfs = n_bfs;
         if (n_bfs) {
-            // The replayed clusters' cells (raster order) come over in one copy. Replays are independent
-            // (each writes only its own ClusterRec), so they run in parallel over clusters on up to
-            // kReplayThreads host threads: at 8192^2 every row cluster needs one (sums > 2^24).
+            // The replayed clusters' cells come over in one copy. Replays are independent (each writes only
+            // its own ClusterRec), so they run in parallel over clusters on up to kReplayThreads host threads:
+            // at 8192^2 every row cluster needs one (sums > 2^24).
             std::vector<long long> off(ncl + 1, 0);
             for (int c = 0; c < ncl; ++c) off[c + 1] = off[c] + S.h_rec[c].n;
             std::vector<int> ids;
@@ -700,21 +730,27 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
     }
     if (rows.empty()) return;
 
-    // ---- seeds
+    // ---- seeds: virtual seeds (a11), endpoint-ray seeds (a12) and endpoint seeds (:1451-1496), each a
+    // first-come 0.5 m de-duplication of its candidates in order; the three run back to back on the device
+    // (the two small ones in one launch) and one kernel concatenates them: two host waits in all
     DedupScratch &scr = S.dedup;
     const int nr = (int)rows.size();
     RowDev *d_rows = dev<RowDev>(S.row_idx, nr);
     AOS_HIP(hipMemcpyAsync(d_rows, rows.data(), sizeof(RowDev) * nr, hipMemcpyHostToDevice, s));
     const int nslots = rows.back().slot0 + 3 * rows.back().k;
-    const int ncand = std::max(nslots, 6 * nr);
-    double2 *d_cand = dev<double2>(S.cand_xy, ncand);
-    int *d_ok = dev<int>(S.cand_ok, ncand);
-    double2 *d_seeds = dev<double2>(S.seed_out, (size_t)nslots + 8 * nr);
-    const HashG h = make_hash(g.minx - 50.0, g.maxx + 50.0, g.miny - 50.0, g.maxy + 50.0, 0.5);
-    int n_virtual = 0, n_ray = 0, n_end = 0;
+    const size_t ncand = (size_t)nslots + 8 * (size_t)nr;
+    double2 *d_cand = dev<double2>(S.cand_xy, ncand), *d_rcand = d_cand + nslots, *d_ecand = d_rcand + 6 * nr;
+    int *d_ok = dev<int>(S.cand_ok, ncand), *d_rok = d_ok + nslots, *d_eok = d_rok + 6 * nr;
+    double2 *d_vout = dev<double2>(S.hash_sorted, ncand), *d_rout = d_vout + nslots, *d_eout = d_rout + 6 * nr;
+    double2 *d_seeds = dev<double2>(S.seed_out, ncand);
+    int *d_cnt = dev<int>(S.misc, 8);   // kept counts: virtual, ray, endpoint
+    const double hx0 = g.minx - 50.0, hx1 = g.maxx + 50.0, hy0 = g.miny - 50.0, hy1 = g.maxy + 50.0;
     if (nslots > 0) {
         k_virtual_candidates<<<cdiv(nslots, 128), 128, 0, s>>>(d_rows, nr, nslots, in.skel_bits, g, d_poly, np, d_cand, d_ok);
-        n_virtual = greedy_dedup(scr, d_cand, d_ok, nslots, kConflictLess, 0.5, h, d_seeds, nullptr, s, h_sc);
+        greedy_dedup_async(scr, d_cand, d_ok, nslots, kConflictLess, 0.5, make_hash_n(hx0, hx1, hy0, hy1, 0.5, nslots),
+                           d_vout, nullptr, nullptr, d_cnt, s);
+    } else {
+        AOS_HIP(hipMemsetAsync(d_cnt, 0, sizeof(int), s));
     }
     RayAngles ang{};
     const double degs[3] = {0.0, -90.0, 90.0};
@@ -733,14 +769,34 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         S.cur_tab_amax = g.amax;
     }
     k_endpoint_rays<<<6 * nr, 64, 0, s>>>(d_rows, nr, in.skel_bits, g, ang, d_poly, np,
-                                          static_cast<const double *>(S.cur_tab.p), S.n_cur_tab, d_cand, d_ok);
-    n_ray = greedy_dedup(scr, d_cand, d_ok, 6 * nr, kConflictLess, 0.5, h, d_seeds + n_virtual, nullptr, s, h_sc);
-    k_endpoint_candidates<<<cdiv(2 * nr, 64), 64, 0, s>>>(d_rows, nr, d_cand, d_ok);
-    n_end = greedy_dedup(scr, d_cand, d_ok, 2 * nr, kConflictLess, 0.5, h, d_seeds + n_virtual + n_ray, nullptr, s, h_sc);
+                                          static_cast<const double *>(S.cur_tab.p), S.n_cur_tab, d_rcand, d_rok);
+    k_endpoint_candidates<<<cdiv(2 * nr, 64), 64, 0, s>>>(d_rows, nr, d_ecand, d_eok);
+    if (6 * nr <= kSmallMax) {
+        const HashG hs = small_hash(hx0, hx1, hy0, hy1, 0.5);
+        SmallDedup sd{};
+        sd.prob[0] = SmallProb{d_rcand, d_rok, 6 * nr, hs, d_rout, d_cnt + 1};
+        sd.prob[1] = SmallProb{d_ecand, d_eok, 2 * nr, hs, d_eout, d_cnt + 2};
+        sd.mode = kConflictLess;
+        sd.thr = 0.5;
+        greedy_dedup_small(scr, sd, 2, s);
+    } else {
+        greedy_dedup_async(scr, d_rcand, d_rok, 6 * nr, kConflictLess, 0.5, make_hash_n(hx0, hx1, hy0, hy1, 0.5, 6 * nr),
+                           d_rout, nullptr, nullptr, d_cnt + 1, s);
+        greedy_dedup_async(scr, d_ecand, d_eok, 2 * nr, kConflictLess, 0.5, make_hash_n(hx0, hx1, hy0, hy1, 0.5, 2 * nr),
+                           d_eout, nullptr, nullptr, d_cnt + 2, s);
+    }
+    k_concat3<<<cdiv((long long)ncand, 256), 256, 0, s>>>(d_vout, d_rout, d_eout, d_cnt, d_seeds);
+    AOS_HIP(hipMemcpyAsync(h_sc, d_cnt, 3 * sizeof(int), hipMemcpyDeviceToHost, s));
+    AOS_HIP(hipMemcpyAsync(h_sc + 3, dedup_err(scr, s), sizeof(int), hipMemcpyDeviceToHost, s));
+    S.dedup.sev.sync(s);
+    dedup_check(scr, h_sc[3]);
+    const int n_virtual = h_sc[0], n_ray = h_sc[1], n_end = h_sc[2];
     const int ntot = n_virtual + n_ray + n_end;
     std::vector<double> all(2 * (size_t)ntot);
-    if (ntot) AOS_HIP(hipMemcpyAsync(all.data(), d_seeds, sizeof(double2) * ntot, hipMemcpyDeviceToHost, s));
-    S.dedup.sev.sync(s);
+    if (ntot) {
+        AOS_HIP(hipMemcpyAsync(all.data(), d_seeds, sizeof(double2) * ntot, hipMemcpyDeviceToHost, s));
+        S.dedup.sev.sync(s);
+    }
     out.virtual_xy.assign(all.begin(), all.begin() + 2 * n_virtual);
     out.ray_xy.assign(all.begin() + 2 * n_virtual, all.begin() + 2 * (n_virtual + n_ray));
     out.endpoint_xy.assign(all.begin() + 2 * (n_virtual + n_ray), all.end());

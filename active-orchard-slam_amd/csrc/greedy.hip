@@ -1,21 +1,29 @@
-// Greedy first-come de-duplication on the GPU (see cluster_seed.h).
+// Greedy first-come de-duplication on the GPU (see cluster_seed.h), and the primitives it is built on
+// (dev_prims.h): a single-pass look-back scan and a counting-sort cell index.
 //
 // Reference loops of the form
 //   for c in candidates (in order): if no already-kept k conflicts with c: keep c
 // (seed_gen:2076-2085, 1964-1974, 1460-1470; gvd:98-125; voronoi_diagram.cpp:156-204) keep exactly
-// the lexicographically-first maximal independent set (LFMIS) of the conflict graph. We hash the
-// candidates into cells no smaller than the conflict radius, list each candidate's EARLIER
-// conflicting candidates (CSR), and decide the LFMIS in rounds over the whole grid:
-// undecided c becomes kept when all listed predecessors are removed, removed once one is kept.
-// Decisions are facts about the final set, so in-place updates are safe; the smallest undecided
-// index always decides, so the loop terminates.
-#include <hipcub/hipcub.hpp>
-
+// the lexicographically-first maximal independent set (LFMIS) of the conflict graph. The candidates are
+// hashed into cells no smaller than the conflict radius (a counting sort: count, scan, scatter), and one
+// fused kernel (k_lfmis) then does the rest:
+//   * each thread lists its candidate's EARLIER conflicting candidates (3 x 3 cells) in LDS;
+//   * it waits until its list decides it: kept once every listed candidate is removed, removed once one
+//     is kept. A candidate waits only for smaller indices, and blocks take their index ranges in launch
+//     order (dev_prims.h), so the smallest undecided candidate can always decide: no deadlock, and the
+//     set is the LFMIS whatever the timing (decisions are facts about the final set);
+//   * the block's kept candidates are compacted in index order with a decoupled look-back over the
+//     blocks' kept counts.
+// Four launches per de-duplication and no host round trip (round 3: a radix sort, two conflict passes, a
+// scan, batches of rounds and a read-back per batch, ~25 launches). Problems of at most kSmallMax
+// candidates run in one workgroup each (k_dedup_small: index, rounds and compaction in LDS).
 #include <algorithm>
 #include <climits>
+#include <cstring>
 #include <stdexcept>
 
 #include "cluster_seed.h"
+#include "dev_prims.h"
 
 namespace aos {
 
@@ -32,12 +40,126 @@ HashG make_hash(double minx, double maxx, double miny, double maxy, double cell)
     return h;
 }
 
-__device__ __forceinline__ void hash_cell(const HashG &h, double x, double y, int &cx, int &cy) {
-    double fx = (x - h.x0) * h.inv, fy = (y - h.y0) * h.inv;
-    cx = !(fx > 0.0) ? 0 : (fx >= (double)(h.nx - 1) ? h.nx - 1 : (int)fx);
-    cy = !(fy > 0.0) ? 0 : (fy >= (double)(h.ny - 1) ? h.ny - 1 : (int)fy);
+static HashG make_hash_cap(double minx, double maxx, double miny, double maxy, double cell, double cap) {
+    double c = cell;
+    HashG h = make_hash(minx, maxx, miny, maxy, c);
+    while ((double)h.nx * (double)h.ny > cap) {
+        c *= 1.25;
+        h = make_hash(minx, maxx, miny, maxy, c);
+    }
+    return h;
 }
 
+HashG make_hash_n(double minx, double maxx, double miny, double maxy, double cell, long long n, double cells_per_item) {
+    return make_hash_cap(minx, maxx, miny, maxy, cell, std::max(4096.0, cells_per_item * (double)std::max(n, 1LL)));
+}
+
+// ------------------------------------------------------------------ look-back scratch
+LookBack LookBackScratch::take(int blocks, hipStream_t s) {
+    const size_t need = sizeof(unsigned long long) * (size_t)std::max(blocks, 1);
+    const size_t cap0 = part.cap;
+    part.ensure(need);
+    if (part.cap != cap0) AOS_HIP(hipMemsetAsync(part.p, 0, part.cap, s));
+    if (!ticket.p) {
+        ticket.ensure(64);
+        AOS_HIP(hipMemsetAsync(ticket.p, 0, 64, s));
+    }
+    if (++epoch >= (1u << 30)) {   // (30-bit tags: clear the words once per 2^30 launches)
+        epoch = 1;
+        AOS_HIP(hipMemsetAsync(part.p, 0, part.cap, s));
+    }
+    return LookBack{part.as<unsigned long long>(), ticket.as<unsigned>(), epoch, err_word(s)};
+}
+
+int *LookBackScratch::err_word(hipStream_t s) {
+    if (ext_err) return ext_err;
+    if (!err.p) {
+        err.ensure(64);
+        AOS_HIP(hipMemsetAsync(err.p, 0, 64, s));
+    }
+    return err.as<int>();
+}
+
+// ------------------------------------------------------------------ single-pass scan
+constexpr int kScanTB = 256, kScanPer = 8, kScanTile = kScanTB * kScanPer;
+__global__ __launch_bounds__(kScanTB) void k_scan_1p(int *in, int *out, int n, int zero_in, LookBack L) {
+    __shared__ int sh_vid, wsum[kScanTB / 64], sh_excl;
+    const int vid = lb_block_id(L, &sh_vid);
+    const long long base = (long long)vid * kScanTile + (long long)threadIdx.x * kScanPer;
+    int v[kScanPer], run = 0;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+        const long long i = base + k;
+        v[k] = i < n ? in[i] : 0;
+        run += v[k];
+    }
+    if (zero_in)
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k)
+            if (base + k < n) in[base + k] = 0;
+    int agg;
+    const int before = block_excl_scan<kScanTB>(run, wsum, &agg);
+    if (threadIdx.x < 64) {
+        const unsigned e = lb_exclusive(L, vid, (unsigned)agg);
+        if (threadIdx.x == 0) sh_excl = (int)e;
+    }
+    __syncthreads();
+    int acc = sh_excl + before;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+        const long long i = base + k;
+        if (i <= n) out[i] = acc;
+        acc += v[k];
+    }
+}
+
+void scan_1p(LookBackScratch &lb, int *in, int *out, int n, bool zero_in, hipStream_t s) {
+    const int blocks = cdiv((long long)n + 1, kScanTile);
+    const LookBack L = lb.take(blocks, s);
+    k_scan_1p<<<blocks, kScanTB, 0, s>>>(in, out, n, zero_in ? 1 : 0, L);
+    AOS_HIP(hipGetLastError());
+}
+
+// ------------------------------------------------------------------ cell index (counting sort)
+__global__ void k_ci_count(const double2 *p, const int *ok, int n, const int *n_dev, HashG h, int *cnt, int *rank) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if ((ok && !ok[i]) || (n_dev && i >= *n_dev)) { rank[i] = -1; return; }
+    int cx, cy;
+    hash_cell(h, p[i].x, p[i].y, cx, cy);
+    const int b = cy * h.nx + cx;
+    rank[i] = atomicAdd(&cnt[b], 1);
+}
+__global__ void k_ci_scatter(const double2 *p, const int *rank, int n, HashG h, const int *start, int *items) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int r = rank[i];
+    if (r < 0) return;
+    int cx, cy;
+    hash_cell(h, p[i].x, p[i].y, cx, cy);
+    items[start[cy * h.nx + cx] + r] = i;
+}
+
+template <class T> static T *dev(DevBuf &b, size_t n) { return static_cast<T *>(b.ensure(sizeof(T) * std::max<size_t>(n, 1))); }
+
+CellIdx cell_index_build(CellScratch &S, const double2 *p, const int *ok, int n, const HashG &h, hipStream_t s,
+                         const int *n_dev) {
+    const long long nb = (long long)h.nx * h.ny;
+    if (nb >= INT_MAX) throw std::runtime_error("cell index: too many buckets");
+    const size_t cap0 = S.cnt.cap;
+    int *cnt = dev<int>(S.cnt, (size_t)nb + 1);
+    if (S.dirty || S.cnt.cap != cap0) AOS_HIP(hipMemsetAsync(cnt, 0, S.cnt.cap, s));
+    int *start = dev<int>(S.start, (size_t)nb + 1), *items = dev<int>(S.items, n), *rank = dev<int>(S.rank, n);
+    S.dirty = true;
+    if (n > 0) k_ci_count<<<cdiv(n, 256), 256, 0, s>>>(p, ok, n, n_dev, h, cnt, rank);
+    scan_1p(S.lb, cnt, start, (int)nb, true, s);   // (leaves the counts zero for the next build)
+    S.dirty = false;
+    if (n > 0) k_ci_scatter<<<cdiv(n, 256), 256, 0, s>>>(p, rank, n, h, start, items);
+    AOS_HIP(hipGetLastError());
+    return CellIdx{h, start, items};
+}
+
+// ------------------------------------------------------------------ conflict tests
 // x86-64 cvttsd2si semantics of static_cast<int>(double): out of range / NaN -> INT_MIN
 __device__ __forceinline__ int x86_trunc_i32(double v) {
     return (v > -2147483649.0 && v < 2147483648.0) ? (int)v : INT_MIN;
@@ -54,158 +176,265 @@ __device__ __forceinline__ bool conflict(double2 a, double2 b, int mode, double 
     return mode == kConflictLessEq ? (d <= thr) : (d < thr);
 }
 
-// (also zeroes the scans' tail slots ccount[n] and f[n], instead of two memset blits)
-__global__ void k_hash_keys(const double2 *p, const int *ok, int n, HashG h, int *keys, int *idx, int *tail0,
-                            int *tail1) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == 0) { *tail0 = 0; *tail1 = 0; }
-    if (i >= n) return;
-    int cx, cy;
-    hash_cell(h, p[i].x, p[i].y, cx, cy);
-    keys[i] = ok[i] ? cy * h.nx + cx : INT_MAX;
-    idx[i] = i;
+// ------------------------------------------------------------------ fused LFMIS + compaction
+// state[i] = epoch << 2 | s, s = 1 kept, 2 removed (a word of another epoch: undecided). OWNER (the GVD
+// merge, gvd:93-125): a removed candidate waits for every listed candidate and records the smallest kept
+// one as its owner; a kept candidate owns itself; not-ok candidates get INT_MAX.
+constexpr int kLfTB = 256, kLfList = 16;
+struct LfArgs {
+    const double2 *p; const int *ok; int n; int mode; double thr;
+    CellIdx ci;
+    int *state; unsigned epoch;
+    LookBack lb;
+    double2 *out; int *kept_index; int *owner; int *count;
+    int *pos_of;   // nullable: per candidate, its position in out, or -1
+};
+
+template <bool OWNER>
+__global__ __launch_bounds__(kLfTB) void k_lfmis(LfArgs A) {
+    __shared__ int sh_vid, wsum[kLfTB / 64], sh_excl;
+    __shared__ int lst[kLfList * kLfTB];   // lst[k * kLfTB + tid]: the thread's k-th listed candidate
+    const int tid = threadIdx.x;
+    const int vid = lb_block_id(A.lb, &sh_vid);
+    const int i = vid * kLfTB + tid;
+    const unsigned tag = A.epoch << 2;
+    int s = 0, nl = 0, own = INT_MAX;
+    bool over = false;
+    double2 pi = make_double2(0.0, 0.0);
+    int cx = 0, cy = 0;
+    if (i < A.n) {
+        if (A.ok && !A.ok[i]) {
+            s = 2;
+        } else {
+            pi = A.p[i];
+            hash_cell(A.ci.h, pi.x, pi.y, cx, cy);
+            for (int yy = max(cy - 1, 0); yy <= min(cy + 1, A.ci.h.ny - 1); ++yy) {
+                int k0, k1;
+                ci_row(A.ci, yy, cx, k0, k1);
+                for (int k = k0; k < k1; ++k) {
+                    const int j = A.ci.items[k];
+                    if (j < i && conflict(pi, A.p[j], A.mode, A.thr)) {
+                        if (nl < kLfList) lst[nl * kLfTB + tid] = j;
+                        else over = true;
+                        ++nl;
+                    }
+                }
+            }
+            if (nl == 0) { s = 1; own = i; }
+        }
+        if (s) st_i32(&A.state[i], (int)(tag | (unsigned)s));
+    }
+    // wait for the listed candidates (over: more than kLfList, re-walk the cells each time)
+    unsigned spins = 0;
+    while (i < A.n && s == 0) {
+        bool any_kept = false, any_und = false;
+        int mk = INT_MAX;
+        auto look = [&](int j) {
+            const unsigned w = (unsigned)ld_i32(&A.state[j]);
+            if ((w & ~3u) != tag) { any_und = true; return; }
+            if ((w & 3u) == 1u) { any_kept = true; mk = min(mk, j); }
+        };
+        if (!over) {
+            for (int k = 0; k < nl && (OWNER || !any_kept); ++k) look(lst[k * kLfTB + tid]);
+        } else {
+            for (int yy = max(cy - 1, 0); yy <= min(cy + 1, A.ci.h.ny - 1); ++yy) {
+                int k0, k1;
+                ci_row(A.ci, yy, cx, k0, k1);
+                for (int k = k0; k < k1; ++k) {
+                    const int j = A.ci.items[k];
+                    if (j < i && conflict(pi, A.p[j], A.mode, A.thr)) look(j);
+                }
+            }
+        }
+        if (OWNER) {
+            if (!any_und) { s = any_kept ? 2 : 1; own = any_kept ? mk : i; }
+        } else {
+            if (any_kept) s = 2;
+            else if (!any_und) { s = 1; own = i; }
+        }
+        if (s) {
+            st_i32(&A.state[i], (int)(tag | (unsigned)s));
+        } else if (++spins > kSpinCap) {
+            atomicOr(A.lb.err, 2);
+            s = 3;
+        } else {
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    if (OWNER && i < A.n) A.owner[i] = own;
+    // kept candidates of the block, in index order, after the kept of all earlier blocks
+    const int kept = (i < A.n && s == 1) ? 1 : 0;
+    int agg;
+    const int r = block_excl_scan<kLfTB>(kept, wsum, &agg);
+    if (tid < 64) {
+        const unsigned e = lb_exclusive(A.lb, vid, (unsigned)agg);
+        if (tid == 0) {
+            sh_excl = (int)e;
+            if (vid == (int)gridDim.x - 1) *A.count = (int)e + agg;
+        }
+    }
+    __syncthreads();
+    if (kept) {
+        const int pos = sh_excl + r;
+        A.out[pos] = pi;
+        if (A.kept_index) A.kept_index[pos] = i;
+    }
+    if (A.pos_of && i < A.n) A.pos_of[i] = kept ? sh_excl + r : -1;
 }
 
-__device__ __forceinline__ int lower_bound_key(const int *keys, int n, int k) {
-    int lo = 0, hi = n;
-    while (lo < hi) { int m = (lo + hi) >> 1; if (keys[m] < k) lo = m + 1; else hi = m; }
-    return lo;
-}
-
-__device__ __forceinline__ int lower_bound_in(const int *keys, int lo, int hi, int k) {
-    while (lo < hi) { int m = (lo + hi) >> 1; if (keys[m] < k) lo = m + 1; else hi = m; }
-    return lo;
-}
-
-// First sorted index of every hash row (cell ids are row-major): narrows each cell lookup of
-// k_conflicts from a binary search over all n keys (~17 dependent loads) to one over one row's keys.
-__global__ void k_row_starts(const int *skeys, int n, HashG h, int *rowstart) {
-    const int yy = blockIdx.x * blockDim.x + threadIdx.x;
-    if (yy <= h.ny) rowstart[yy] = lower_bound_key(skeys, n, yy * h.nx);
-}
-
-// coff == nullptr: count pass; else fill pass
-__global__ void k_conflicts(const double2 *p, const int *ok, int n, HashG h, const int *skeys, const int *sidx,
-                            const int *rowstart, int mode, double thr, const int *coff, int *ccount, int *clist,
-                            long long cap) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    if (!ok[i]) { if (!coff) ccount[i] = 0; return; }
-    int cx, cy;
-    hash_cell(h, p[i].x, p[i].y, cx, cy);
-    const double2 pi = p[i];
-    int c = 0, w = coff ? coff[i] : 0;
-    for (int yy = max(cy - 1, 0); yy <= min(cy + 1, h.ny - 1); ++yy) {
-        const int hi = rowstart[yy + 1];
-        const int k0 = lower_bound_in(skeys, rowstart[yy], hi, yy * h.nx + max(cx - 1, 0));
-        const int k1 = lower_bound_in(skeys, k0, hi, yy * h.nx + min(cx + 1, h.nx - 1) + 1);
-        for (int k = k0; k < k1; ++k) {
-            int j = sidx[k];
-            if (j < i && conflict(pi, p[j], mode, thr)) {
-                if (coff && (long long)w + c < cap) clist[w + c] = j;   // overflow: host re-runs with the exact size
-                ++c;
+// ------------------------------------------------------------------ small problems: one workgroup each
+constexpr int kSmallTB = 1024, kSmallPer = kSmallMax / kSmallTB, kSmallBuckets = 2048;
+__global__ __launch_bounds__(kSmallTB) void k_dedup_small(SmallDedup A) {
+    const SmallProb &P = A.prob[blockIdx.x];
+    __shared__ double2 pts[kSmallMax];
+    __shared__ int st[kSmallMax], items[kSmallMax], bstart[kSmallBuckets + 1], wsum[kSmallTB / 64];
+    const int tid = threadIdx.x, n = P.n;
+    const HashG &h = P.h;
+    const int nb = h.nx * h.ny;   // <= kSmallBuckets (host)
+    for (int b = tid; b <= nb; b += kSmallTB) bstart[b] = 0;
+    __syncthreads();
+    int bk[kSmallPer], rk[kSmallPer];
+#pragma unroll
+    for (int k = 0; k < kSmallPer; ++k) {
+        const int i = tid * kSmallPer + k;
+        bk[k] = -1;
+        if (i < n) {
+            const double2 q = P.p[i];
+            pts[i] = q;
+            const bool ok = !P.ok || P.ok[i];
+            st[i] = ok ? 0 : 2;
+            if (ok) {
+                int cx, cy;
+                hash_cell(h, q.x, q.y, cx, cy);
+                bk[k] = cy * h.nx + cx;
+                rk[k] = atomicAdd(&bstart[bk[k] + 1], 1);
             }
         }
     }
-    if (!coff) ccount[i] = c;
-}
-
-__global__ void k_greedy_init(const int *ok, int n, int *state) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) state[i] = ok[i] ? 0 : 2;
-}
-// One round over all undecided candidates, any number of workgroups. States are read with
-// agent-scope loads (another workgroup may have decided a predecessor in this very round); a
-// stale read only postpones a decision to a later round. undecided[0] counts candidates still
-// undecided when this round looked at them: 0 means the set is complete, and the later rounds of a
-// batch (prev_undecided = the previous round's counter) return at once.
-__global__ void k_greedy_round(int n, const int *coff, const int *clist, int *state, int *undecided,
-                               const int *prev_undecided) {
-    if (prev_undecided && *prev_undecided == 0) return;
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    bool und = false;
-    if (i < n && __hip_atomic_load(&state[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-        bool any_kept = false, any_undec = false;
-        for (int k = coff[i]; k < coff[i + 1]; ++k) {
-            int sj = __hip_atomic_load(&state[clist[k]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (sj == 1) { any_kept = true; break; }
-            if (sj == 0) any_undec = true;
+    __syncthreads();
+    {   // bucket starts: each thread scans its run of 2 buckets (nb <= 2048)
+        const int b0 = 2 * tid + 1;
+        const int c0 = b0 <= nb ? bstart[b0] : 0, c1 = b0 + 1 <= nb ? bstart[b0 + 1] : 0;
+        int tot;
+        const int before = block_excl_scan<kSmallTB>(c0 + c1, wsum, &tot);
+        if (b0 <= nb) bstart[b0] = before + c0;
+        if (b0 + 1 <= nb) bstart[b0 + 1] = before + c0 + c1;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kSmallPer; ++k)
+        if (bk[k] >= 0) items[bstart[bk[k]] + rk[k]] = tid * kSmallPer + k;
+    __syncthreads();
+    // rounds over the undecided candidates (a stale LDS read only postpones a decision)
+    for (int round = 0;; ++round) {
+        bool und = false;
+#pragma unroll
+        for (int k = 0; k < kSmallPer; ++k) {
+            const int i = tid * kSmallPer + k;
+            if (i >= n || st[i] != 0) continue;
+            const double2 q = pts[i];
+            int cx, cy;
+            hash_cell(h, q.x, q.y, cx, cy);
+            bool kept_c = false, und_c = false;
+            for (int yy = max(cy - 1, 0); yy <= min(cy + 1, h.ny - 1) && !kept_c; ++yy) {
+                const int k0 = bstart[yy * h.nx + max(cx - 1, 0)], k1 = bstart[yy * h.nx + min(cx + 1, h.nx - 1) + 1];
+                for (int kk = k0; kk < k1; ++kk) {
+                    const int j = items[kk];
+                    if (j >= i || !conflict(q, pts[j], A.mode, A.thr)) continue;
+                    const int sj = st[j];
+                    if (sj == 1) { kept_c = true; break; }
+                    if (sj == 0) und_c = true;
+                }
+            }
+            if (kept_c) st[i] = 2;
+            else if (!und_c) st[i] = 1;
+            else und = true;
         }
-        int ns = any_kept ? 2 : (any_undec ? 0 : 1);
-        if (ns) __hip_atomic_store(&state[i], ns, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else und = true;
+        if (!__syncthreads_or(und)) break;
+        if (round > n + 2) {   // (cannot happen: the smallest undecided candidate decides every round)
+            if (tid == 0) atomicOr(A.err, 4);
+            break;
+        }
     }
-    unsigned long long m = __ballot(und);
-    if ((threadIdx.x & 63) == 0 && m) atomicAdd(undecided, (int)__popcll(m));
+    // compaction in index order
+    int c = 0;
+#pragma unroll
+    for (int k = 0; k < kSmallPer; ++k) {
+        const int i = tid * kSmallPer + k;
+        c += (i < n && st[i] == 1) ? 1 : 0;
+    }
+    int tot;
+    int pos = block_excl_scan<kSmallTB>(c, wsum, &tot);
+#pragma unroll
+    for (int k = 0; k < kSmallPer; ++k) {
+        const int i = tid * kSmallPer + k;
+        if (i < n && st[i] == 1) P.out[pos++] = pts[i];
+    }
+    if (tid == 0) *P.count = tot;
 }
 
-__global__ void k_kept_flags(const int *state, int n, int *f) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) f[i] = state[i] == 1;
-}
-// (thread 0 also gathers the batch's three read-back scalars into one slot run: one D2H copy, not three)
-__global__ void k_compact(const double2 *p, const int *f, const int *pos, int n, double2 *out, int *kept_index,
-                          const int *und_last, const int *n_conf, int *scalars) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == 0) { scalars[0] = *und_last; scalars[1] = *n_conf; scalars[2] = pos[n]; }
-    if (i < n && f[i]) {
-        out[pos[i]] = p[i];
-        if (kept_index) kept_index[pos[i]] = i;
+// ------------------------------------------------------------------ host API
+void greedy_dedup_async(DedupScratch &S, const double2 *cand, const int *ok, int n, int mode, double thr, const HashG &h,
+                        double2 *out, int *kept_index, int *owner, int *d_count, hipStream_t s, int *pos_of) {
+    if (n <= 0) {
+        AOS_HIP(hipMemsetAsync(d_count, 0, sizeof(int), s));
+        return;
     }
+    S.cells.lb.ext_err = dedup_err(S, s);   // (one error word for all of S's launches)
+    S.ci = cell_index_build(S.cells, cand, ok, n, h, s);
+    const size_t cap0 = S.state.cap;
+    int *state = dev<int>(S.state, n);
+    if (S.state.cap != cap0) AOS_HIP(hipMemsetAsync(state, 0, S.state.cap, s));   // (epoch 0: undecided)
+    if (++S.epoch >= (1u << 29)) {
+        S.epoch = 1;
+        AOS_HIP(hipMemsetAsync(state, 0, S.state.cap, s));
+    }
+    const int blocks = cdiv(n, kLfTB);
+    LfArgs A{cand, ok, n, mode, thr, S.ci, state, S.epoch, S.lb.take(blocks, s), out, kept_index, owner, d_count, pos_of};
+    if (owner) k_lfmis<true><<<blocks, kLfTB, 0, s>>>(A);
+    else k_lfmis<false><<<blocks, kLfTB, 0, s>>>(A);
+    AOS_HIP(hipGetLastError());
 }
 
-template <class T> static T *dev(DevBuf &b, size_t n) { return static_cast<T *>(b.ensure(sizeof(T) * std::max<size_t>(n, 1))); }
+int *dedup_err(DedupScratch &S, hipStream_t s) { return S.lb.err_word(s); }
+
+void dedup_check(DedupScratch &S, int err_word) {
+    if (!err_word) return;
+    // a stale ticket or a wait past the cap (never expected): reset the shared words, report
+    S.lb.ticket.release();
+    S.lb.err.release();
+    S.lb.part.release();
+    S.cells.lb.ticket.release();
+    S.cells.lb.part.release();
+    S.cells.lb.ext_err = nullptr;
+    S.cells.dirty = true;
+    throw std::runtime_error("greedy de-duplication: device wait failed (error word " + std::to_string(err_word) + ")");
+}
 
 int greedy_dedup(DedupScratch &S, const double2 *cand, const int *ok, int n, int mode, double thr, const HashG &h,
                  double2 *out, int *kept_index_out, hipStream_t s, int *h_scalar) {
     if (n <= 0) return 0;
-    int *keys = dev<int>(S.keys, n), *idx = dev<int>(S.idx, n), *skeys = dev<int>(S.skeys, n), *sidx = dev<int>(S.sidx, n);
-    int *ccount = dev<int>(S.ccount, n + 1), *coff = dev<int>(S.coff, n + 1);
-    int *f = dev<int>(S.f, n + 1), *pos = dev<int>(S.pos, n + 1);
-    k_hash_keys<<<cdiv(n, 256), 256, 0, s>>>(cand, ok, n, h, keys, idx, ccount + n, f + n);
-    size_t tb = 0, tb2 = 0;
-    AOS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys, skeys, idx, sidx, n, 0, 32, s));
-    AOS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, (int *)nullptr, (int *)nullptr, n + 1, s));
-    void *tmp = S.tmp.ensure(std::max(tb, tb2));
-    AOS_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys, skeys, idx, sidx, n, 0, 32, s));
-    int *rows = dev<int>(S.rows, (size_t)h.ny + 1);
-    k_row_starts<<<cdiv(h.ny + 1, 256), 256, 0, s>>>(skeys, n, h, rows);
-    k_conflicts<<<cdiv(n, 256), 256, 0, s>>>(cand, ok, n, h, skeys, sidx, rows, mode, thr, nullptr, ccount, nullptr, 0);
-    AOS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, ccount, coff, n + 1, s));
-    // Optimistic capacity for the conflict lists (no read-back of the exact total before the rounds):
-    // the total comes back with the first round batch; on overflow the lists are rebuilt exactly.
-    long long cap = std::max<long long>((long long)(S.clist.cap / sizeof(int)), 8LL * n);
-    int *clist = dev<int>(S.clist, (size_t)cap);
-    int *state = dev<int>(S.state, n);
-    constexpr int kBatch = 6;
-    int *und = dev<int>(S.und, kBatch + 3);   // round counters, then the three read-back scalars
-    auto fill = [&]() {
-        k_conflicts<<<cdiv(n, 256), 256, 0, s>>>(cand, ok, n, h, skeys, sidx, rows, mode, thr, coff, nullptr, clist, cap);
-        k_greedy_init<<<cdiv(n, 256), 256, 0, s>>>(ok, n, state);
-    };
-    fill();
-    for (int done_rounds = 0;;) {
-        // a batch of rounds, then (speculatively) the compaction of the kept set, one read-back
-        AOS_HIP(hipMemsetAsync(und, 0, sizeof(int) * kBatch, s));
-        for (int r = 0; r < kBatch; ++r)
-            k_greedy_round<<<cdiv(n, 256), 256, 0, s>>>(n, coff, clist, state, und + r, r ? und + r - 1 : nullptr);
-        k_kept_flags<<<cdiv(n, 256), 256, 0, s>>>(state, n, f);
-        AOS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, f, pos, n + 1, s));
-        k_compact<<<cdiv(n, 256), 256, 0, s>>>(cand, f, pos, n, out, kept_index_out, und + kBatch - 1, coff + n, und + kBatch);
-        AOS_HIP(hipMemcpyAsync(h_scalar, und + kBatch, 3 * sizeof(int), hipMemcpyDeviceToHost, s));
-        S.sev.sync(s);
-        S.n_conf = h_scalar[1];
-        if ((long long)S.n_conf > cap) {   // conflict lists were truncated: rebuild at the exact size
-            cap = S.n_conf;
-            clist = dev<int>(S.clist, (size_t)cap);
-            fill();
-            done_rounds = 0;
-            continue;
-        }
-        done_rounds += kBatch;
-        if (h_scalar[0] == 0) return h_scalar[2];
-        if (done_rounds > n + kBatch) throw std::runtime_error("greedy de-duplication did not converge");
-    }
+    int *d = dev<int>(S.misc, 2);
+    greedy_dedup_async(S, cand, ok, n, mode, thr, h, out, kept_index_out, nullptr, d, s);
+    AOS_HIP(hipMemcpyAsync(h_scalar, d, sizeof(int), hipMemcpyDeviceToHost, s));
+    AOS_HIP(hipMemcpyAsync(h_scalar + 1, dedup_err(S, s), sizeof(int), hipMemcpyDeviceToHost, s));
+    S.sev.sync(s);
+    dedup_check(S, h_scalar[1]);
+    return h_scalar[0];
+}
+
+void greedy_dedup_small(DedupScratch &S, SmallDedup A, int nprob, hipStream_t s) {
+    if (nprob <= 0) return;
+    for (int k = 0; k < nprob; ++k)
+        if (A.prob[k].n > kSmallMax || (long long)A.prob[k].h.nx * A.prob[k].h.ny > kSmallBuckets)
+            throw std::logic_error("greedy_dedup_small: problem too large");
+    A.err = dedup_err(S, s);
+    k_dedup_small<<<nprob, kSmallTB, 0, s>>>(A);
+    AOS_HIP(hipGetLastError());
+}
+
+HashG small_hash(double minx, double maxx, double miny, double maxy, double cell) {
+    return make_hash_cap(minx, maxx, miny, maxy, cell, (double)kSmallBuckets);
 }
 
 }  // namespace aos

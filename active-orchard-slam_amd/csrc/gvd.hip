@@ -9,8 +9,6 @@
 //  g7 filterNodesAndEdgesOutsideGrid          GPU  compaction
 //  g8 TL/TR/BL/BR label points                GPU  per (row, label) arg-min / castRay
 //  g9 publishGraph labels                     GPU  per node
-#include <hipcub/hipcub.hpp>
-
 #include <algorithm>
 #include <chrono>
 #include <cfloat>
@@ -48,85 +46,75 @@ __device__ __forceinline__ bool occ_trunc(const int8_t *sk, const GridG &g, doub
 }
 
 // ------------------------------------------------------------------ g1 merge
-// owner[j] = smallest earlier kept (leader) candidate conflicting with j, or j for leaders
-__global__ void k_fill_ones(int *a, int n) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) a[i] = 1;
-}
-
-__global__ void k_merge_owner(const int *state, const int *coff, const int *clist, int n, int *owner, int *idx) {
-    int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
-    int o = INT_MAX;
-    if (state[j] == 1) o = j;
-    else if (state[j] == 2)
-        for (int k = coff[j]; k < coff[j + 1]; ++k) { int i = clist[k]; if (state[i] == 1) o = min(o, i); }
-    owner[j] = o;
-    idx[j] = j;
-}
-// members of each leader are contiguous (stable sort by owner keeps ascending j): sum in order
-__global__ void k_merge_sum(const double2 *raw, const int *sorted_owner, const int *sorted_j, int n, const int *leaders,
-                            int n_leaders, double2 *merged) {
-    int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= n_leaders) return;
+// merged seed r = the mean of its leader's members (owner == leader, the leader first), summed in index
+// order as voronoiSeedsCallback does (gvd:116-123). Members conflict with the leader (<= 0.5 m), so they
+// sit in its 3 x 3 cells of the de-duplication's index: taken in increasing index, one pass each.
+__global__ void k_merge_members(const double2 *raw, CellIdx ci, const int *owner, const int *leaders, const int *count,
+                                double2 *merged) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= *count) return;
     const int L = leaders[r];
-    int lo = 0, hi = n;
-    while (lo < hi) { int m = (lo + hi) >> 1; if (sorted_owner[m] < L) lo = m + 1; else hi = m; }
+    const double2 pl = raw[L];
+    int cx, cy;
+    hash_cell(ci.h, pl.x, pl.y, cx, cy);
     double sx = 0.0, sy = 0.0;
-    int cnt = 0;
-    for (int k = lo; k < n && sorted_owner[k] == L; ++k) { double2 p = raw[sorted_j[k]]; sx += p.x; sy += p.y; ++cnt; }
+    int cnt = 0, cur = -1;
+    for (;;) {
+        int nxt = INT_MAX;
+        for (int yy = max(cy - 1, 0); yy <= min(cy + 1, ci.h.ny - 1); ++yy) {
+            int k0, k1;
+            ci_row(ci, yy, cx, k0, k1);
+            for (int k = k0; k < k1; ++k) {
+                const int j = ci.items[k];
+                if (j > cur && j < nxt && owner[j] == L) nxt = j;
+            }
+        }
+        if (nxt == INT_MAX) break;
+        const double2 q = raw[nxt];
+        sx += q.x; sy += q.y;
+        ++cnt;
+        cur = nxt;
+    }
     merged[r] = make_double2(sx / (double)cnt, sy / (double)cnt);
 }
 
 // ------------------------------------------------------------------ g5/g6 helpers
-__global__ void k_edges_to_occ(const float *e, int ne, double2 *occ, int *ok) {
+// Sizes the host has not read stay on the device: M boundary points (*M_dev, <= no), P pairs
+// (poff[no]), Mn nodes, ... Kernels are launched over host-known upper bounds and return past the
+// device count; the per-item arrays the scans read are zero there.
+__global__ void k_edges_to_occ(const float *e, int ne, double2 *occ) {
     int o = blockIdx.x * blockDim.x + threadIdx.x;
     if (o >= 2 * ne) return;
     int k = o >> 1;
     occ[o] = (o & 1) ? make_double2((double)e[4 * k + 2], (double)e[4 * k + 3]) : make_double2((double)e[4 * k], (double)e[4 * k + 1]);
-    ok[o] = 1;
-}
-__global__ void k_cell_keys(const double2 *p, int n, HashG h, int *keys, int *idx) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    double fx = (p[i].x - h.x0) * h.inv, fy = (p[i].y - h.y0) * h.inv;
-    int cx = !(fx > 0.0) ? 0 : (fx >= (double)(h.nx - 1) ? h.nx - 1 : (int)fx);
-    int cy = !(fy > 0.0) ? 0 : (fy >= (double)(h.ny - 1) ? h.ny - 1 : (int)fy);
-    keys[i] = cy * h.nx + cx;
-    idx[i] = i;
-}
-__device__ __forceinline__ void cell_of(const HashG &h, double x, double y, int &cx, int &cy) {
-    double fx = (x - h.x0) * h.inv, fy = (y - h.y0) * h.inv;
-    cx = !(fx > 0.0) ? 0 : (fx >= (double)(h.nx - 1) ? h.nx - 1 : (int)fx);
-    cy = !(fy > 0.0) ? 0 : (fy >= (double)(h.ny - 1) ? h.ny - 1 : (int)fy);
-}
-__device__ __forceinline__ int lb(const int *keys, int n, int k) {
-    int lo = 0, hi = n;
-    while (lo < hi) { int m = (lo + hi) >> 1; if (keys[m] < k) lo = m + 1; else hi = m; }
-    return lo;
 }
 
-// findNearestBoundaryPoint (gvd:812-824): first strict minimum of |bp_i - q| over i.
-// The nearest lies within 5 cm (extractBoundaryPoints kept it or a conflicting point within
-// 5 cm / the same 1 cm key), so the 3x3 cells of the 5 cm hash suffice; brute force otherwise.
-__global__ void k_nearest(const double2 *occ, int n_occ, const double2 *bp, int M, HashG h, const int *skeys,
-                          const int *sidx, int *near_out) {
+// findNearestBoundaryPoint (gvd:812-824): first strict minimum of |bp_i - q| over i = the (distance, i)
+// lexicographic minimum. The boundary points are the kept candidates of the extractBoundaryPoints
+// de-duplication (pos_of[c] = their index), found through its cell index (cells >= 0.5 m). The nearest
+// lies within 5 cm (extractBoundaryPoints kept it or a conflicting point within 5 cm / the same 1 cm
+// key), inside q's 3 x 3 cells; brute force otherwise.
+__global__ void k_nearest(const double2 *occ, int n_occ, CellIdx ci, const int *pos_of, const double2 *bp, const int *M_dev,
+                          int *near_out) {
     int o = blockIdx.x * blockDim.x + threadIdx.x;
     if (o >= n_occ) return;
     const double2 q = occ[o];
     int cx, cy;
-    cell_of(h, q.x, q.y, cx, cy);
+    hash_cell(ci.h, q.x, q.y, cx, cy);
     double best = 1.7976931348623157e308;
     int bi = -1;
-    for (int yy = max(cy - 1, 0); yy <= min(cy + 1, h.ny - 1); ++yy) {
-        int k0 = lb(skeys, M, yy * h.nx + max(cx - 1, 0)), k1 = lb(skeys, M, yy * h.nx + min(cx + 1, h.nx - 1) + 1);
+    for (int yy = max(cy - 1, 0); yy <= min(cy + 1, ci.h.ny - 1); ++yy) {
+        int k0, k1;
+        ci_row(ci, yy, cx, k0, k1);
         for (int k = k0; k < k1; ++k) {
-            int i = sidx[k];
-            double dx = bp[i].x - q.x, dy = bp[i].y - q.y, d = sqrt(dx * dx + dy * dy);
+            const int c = ci.items[k], i = pos_of[c];
+            if (i < 0) continue;
+            double dx = occ[c].x - q.x, dy = occ[c].y - q.y, d = sqrt(dx * dx + dy * dy);
             if (d < best || (d == best && i < bi)) { best = d; bi = i; }
         }
     }
     if (!(best < 0.05)) {  // safety net: exact brute force
+        const int M = *M_dev;
         best = 1.7976931348623157e308; bi = -1;
         for (int i = 0; i < M; ++i) {
             double dx = bp[i].x - q.x, dy = bp[i].y - q.y, d = sqrt(dx * dx + dy * dy);
@@ -136,23 +124,26 @@ __global__ void k_nearest(const double2 *occ, int n_occ, const double2 *bp, int 
     near_out[o] = bi;
 }
 
-// all pairs i < j with 1e-6 < |bp_i - bp_j| <= 0.5 (gvd:861-894), CSR per i, j ascending
-__global__ void k_pairs(const double2 *bp, int M, HashG h, const int *skeys, const int *sidx, const int *poff, int *pcount,
-                        int *plist) {
+// all pairs i < j with 1e-6 < |bp_i - bp_j| <= 0.5 (gvd:861-894), CSR per i, j ascending (count pass:
+// poff == nullptr; entries past cap are dropped and flag the caller, who reruns with the exact size)
+__global__ void k_pairs(const double2 *bp, int no, const int *M_dev, CellIdx ci, const int *pos_of, const double2 *occ,
+                        const int *poff, int *pcount, int *plist, int cap) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= M) return;
+    if (i >= no) return;
+    if (i >= *M_dev) { if (!poff) pcount[i] = 0; return; }
     const double2 p = bp[i];
     int cx, cy;
-    cell_of(h, p.x, p.y, cx, cy);
+    hash_cell(ci.h, p.x, p.y, cx, cy);
     int c = 0, w = poff ? poff[i] : 0;
-    for (int yy = max(cy - 1, 0); yy <= min(cy + 1, h.ny - 1); ++yy) {
-        int k0 = lb(skeys, M, yy * h.nx + max(cx - 1, 0)), k1 = lb(skeys, M, yy * h.nx + min(cx + 1, h.nx - 1) + 1);
+    for (int yy = max(cy - 1, 0); yy <= min(cy + 1, ci.h.ny - 1); ++yy) {
+        int k0, k1;
+        ci_row(ci, yy, cx, k0, k1);
         for (int k = k0; k < k1; ++k) {
-            int j = sidx[k];
+            const int cc = ci.items[k], j = pos_of[cc];
             if (j <= i) continue;
-            double dx = p.x - bp[j].x, dy = p.y - bp[j].y, d = sqrt(dx * dx + dy * dy);
+            double dx = p.x - occ[cc].x, dy = p.y - occ[cc].y, d = sqrt(dx * dx + dy * dy);
             if (d <= 0.5 && d > 1e-6) {
-                if (poff) {  // insertion into the sorted run
+                if (poff && w + c < cap) {  // insertion into the sorted run
                     int pos = w + c;
                     while (pos > w && plist[pos - 1] > j) { plist[pos] = plist[pos - 1]; --pos; }
                     plist[pos] = j;
@@ -164,34 +155,34 @@ __global__ void k_pairs(const double2 *bp, int M, HashG h, const int *skeys, con
     if (!poff) pcount[i] = c;
 }
 
-// candidate edge occurrences: [0, E) Voronoi edges, [E, E + P) pairs. from/to keep the direction
-// in which the reference samples the segment.
-__global__ void k_candidates(const int *near_idx, int ne, const int *poff, const int *plist, int M, int np,
-                             int2 *ft, unsigned long long *key, int *valid) {
+// candidate edge occurrences: [0, E) Voronoi edges, [E, E + P) pairs (P = poff[no] <= cap). from/to keep
+// the direction in which the reference samples the segment.
+__global__ void k_candidates(const int *near_idx, int ne, const int *poff, const int *plist, const int *M_dev, int no,
+                             int cap, int2 *ft) {
     int c = blockIdx.x * blockDim.x + threadIdx.x;
+    const int np = min(poff[no], cap);
     if (c >= ne + np) return;
     int a, b;
     if (c < ne) { a = near_idx[2 * c]; b = near_idx[2 * c + 1]; }
     else {
-        int k = c - ne, lo = 0, hi = M - 1;  // owner i of pair slot k
+        int k = c - ne, lo = 0, hi = *M_dev - 1;  // owner i of pair slot k
         while (lo < hi) { int m = (lo + hi + 1) >> 1; if (poff[m] <= k) lo = m; else hi = m - 1; }
         a = lo; b = plist[k];
     }
-    int ok = a >= 0 && b >= 0 && a != b;
     ft[c] = make_int2(a, b);
-    int lo_ = min(a, b), hi_ = max(a, b);
-    key[c] = ok ? ((unsigned long long)(unsigned)lo_ << 32) | (unsigned)hi_ : ~0ull;
-    valid[c] = ok;
 }
 
 // edgePassesThroughOccupiedPixels (gvd:320-359) on the framed skeleton. Samples whose t-range
-// cannot touch the grid are skipped (they read no cell), which keeps far hull edges cheap.
-__global__ void k_occupancy(const int2 *ft, const int *valid, int nc, const double2 *bp, const int8_t *sk, GridG g,
-                            int *pass) {
+// cannot touch the grid are skipped (they read no cell), which keeps far hull edges cheap. A passing
+// occurrence (a != b, both valid, no occupied sample) is counted in the group of its smaller node
+// (grank: its rank there) for the first-occurrence selection.
+__global__ void k_occupancy(const int2 *ft, const int *poff, int no, int ne, int cap, const double2 *bp, const int8_t *sk,
+                            GridG g, int *pass, int *gcnt, int *grank) {
     int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= nc) return;
-    if (!valid[c]) { pass[c] = 0; return; }
-    const double2 s = bp[ft[c].x], e = bp[ft[c].y];
+    if (c >= ne + min(poff[no], cap)) return;
+    const int2 e2 = ft[c];
+    if (!(e2.x >= 0 && e2.y >= 0 && e2.x != e2.y)) { pass[c] = 0; return; }
+    const double2 s = bp[e2.x], e = bp[e2.y];
     double ex = e.x - s.x, ey = e.y - s.y;
     double len = sqrt(ex * ex + ey * ey);
     bool hit = false;
@@ -234,36 +225,51 @@ __global__ void k_occupancy(const int2 *ft, const int *valid, int nc, const doub
         }
     }
     pass[c] = hit ? 0 : 1;
+    if (!hit) grank[c] = atomicAdd(&gcnt[min(e2.x, e2.y)], 1);
 }
-
-__global__ void k_pass_keys(const unsigned long long *key, const int *pass, int nc, unsigned long long *k2, int *occ_idx) {
-    int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= nc) return;
-    k2[c] = pass[c] ? key[c] : ~0ull;
-    occ_idx[c] = c;
+// The edge of key (a < b) is added by its first passing occurrence (gvd:840-857): a passing occurrence
+// is selected iff no smaller passing occurrence in its group (smaller node a) has the same larger node.
+__global__ void k_group_scatter(const int2 *ft, const int *pass, const int *poff, int no, int ne, int cap, const int *goff,
+                                const int *grank, int *glist) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= ne + min(poff[no], cap) || !pass[c]) return;
+    glist[goff[min(ft[c].x, ft[c].y)] + grank[c]] = c;
 }
-__global__ void k_first_of_key(const unsigned long long *sk, const int *socc, int nc, int *selected) {
-    int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= nc) return;
-    if (sk[k] == ~0ull) return;
-    if (k == 0 || sk[k - 1] != sk[k]) selected[socc[k]] = 1;
+__global__ void k_select(const int2 *ft, const int *pass, const int *poff, int no, int ne, int cap, const int *goff,
+                         const int *glist, int *selected) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= ne + cap) return;
+    int sel = 0;
+    if (c < ne + min(poff[no], cap) && pass[c]) {
+        const int a = min(ft[c].x, ft[c].y), b = max(ft[c].x, ft[c].y);
+        sel = 1;
+        for (int k = goff[a]; k < goff[a + 1]; ++k) {
+            const int c2 = glist[k];
+            if (c2 < c && max(ft[c2].x, ft[c2].y) == b) { sel = 0; break; }
+        }
+    }
+    selected[c] = sel;
 }
 
 // ------------------------------------------------------------------ g7 filter
-__global__ void k_inside(const double2 *bp, int M, GridG g, int *f) {
+__global__ void k_inside(const double2 *bp, int no, const int *M_dev, GridG g, int *f) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= M) return;
-    double2 p = bp[i];
-    f[i] = p.x >= g.minx && p.x <= g.maxx && p.y >= g.miny && p.y <= g.maxy;
+    if (i >= no) return;
+    int v = 0;
+    if (i < *M_dev) {
+        double2 p = bp[i];
+        v = p.x >= g.minx && p.x <= g.maxx && p.y >= g.miny && p.y <= g.maxy;
+    }
+    f[i] = v;
 }
-__global__ void k_gather_nodes(const double2 *bp, const int *f, const int *pos, int M, double2 *nodes) {
+__global__ void k_gather_nodes(const double2 *bp, const int *f, const int *pos, int no, double2 *nodes) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < M && f[i]) nodes[pos[i]] = bp[i];
+    if (i < no && f[i]) nodes[pos[i]] = bp[i];
 }
-// selected candidate c -> record (a<b); keep if both nodes stay (and stay distinct)
-__global__ void k_edge_keep(const int *selected, const int2 *ft, int nc, const int *inside, const int *pos, int *keep) {
+// selected candidate c -> record (a<b); keep if both nodes stay (and stay distinct); 0 past the candidates
+__global__ void k_edge_keep(const int *selected, const int2 *ft, int ncap, const int *inside, const int *pos, int *keep) {
     int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= nc) return;
+    if (c >= ncap) return;
     int k = 0;
     if (selected[c]) {
         int a = min(ft[c].x, ft[c].y), b = max(ft[c].x, ft[c].y);
@@ -271,10 +277,10 @@ __global__ void k_edge_keep(const int *selected, const int2 *ft, int nc, const i
     }
     keep[c] = k;
 }
-__global__ void k_edge_emit(const int *keep, const int *kpos, const int2 *ft, int nc, const int *pos, const double2 *nodes,
+__global__ void k_edge_emit(const int *keep, const int *kpos, const int2 *ft, int ncap, const int *pos, const double2 *nodes,
                             int *edges, float *len) {
     int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= nc || !keep[c]) return;
+    if (c >= ncap || !keep[c]) return;
     int a = pos[min(ft[c].x, ft[c].y)], b = pos[max(ft[c].x, ft[c].y)];
     if (a > b) { int t = a; a = b; b = t; }
     double dx = nodes[b].x - nodes[a].x, dy = nodes[b].y - nodes[a].y;  // (to - from).norm()
@@ -286,14 +292,14 @@ __global__ void k_edge_emit(const int *keep, const int *kpos, const int2 *ft, in
 // ------------------------------------------------------------------ g8 label points
 struct LabelRow { double ex, ey, ox, oy; double deg, cs, sn; };  // endpoint, other endpoint, angle, host cos/sin
 // one workgroup per (row, label): arg-min over the filtered nodes (gvd:731-774); castRay fallback (:788)
-// Pass 0 reads only the nodes of the 3 x 3 cells (of >= 5.01 m: the hash hl over the sorted node keys
-// lsk / lsi) around the endpoint, which hold every node with z <= 25 (1 + 1e-12); a job scanned all
-// ~10^5 nodes before (≈ 177 us per C2 frame).
-__global__ __launch_bounds__(256) void k_label_points(const LabelRow *jobs, int nj, const double2 *nodes, int Mn, GridG g,
-                                                      const int8_t *sk, HashG hl, const int *lsk, const int *lsi,
-                                                      double2 *pts, int *valid) {
+// Pass 0 reads only the nodes of the 3 x 3 cells (of >= 5.01 m: the cell index cn over the nodes)
+// around the endpoint, which hold every node with z <= 25 (1 + 1e-12); a job scanned all ~10^5 nodes
+// before (≈ 177 us per C2 frame).
+__global__ __launch_bounds__(256) void k_label_points(const LabelRow *jobs, int nj, const double2 *nodes, const int *Mn_dev,
+                                                      GridG g, const int8_t *sk, CellIdx cn, double2 *pts, int *valid) {
     const int jb = blockIdx.x;
     if (jb >= nj) return;
+    const int Mn = *Mn_dev;
     const LabelRow J = jobs[jb];
     double mdx = J.ox - J.ex, mdy = J.oy - J.ey;
     double ml = sqrt(mdx * mdx + mdy * mdy);
@@ -308,7 +314,7 @@ __global__ __launch_bounds__(256) void k_label_points(const LabelRow *jobs, int 
     __shared__ double sb[256];
     __shared__ int si[256];
     int cx, cy;
-    cell_of(hl, J.ex, J.ey, cx, cy);
+    hash_cell(cn.h, J.ex, J.ey, cx, cy);
     for (int pass = 0; pass < 2; ++pass) {
         double best = 1.7976931348623157e308;
         int bi = INT_MAX;
@@ -327,9 +333,10 @@ __global__ __launch_bounds__(256) void k_label_points(const LabelRow *jobs, int 
             if (dist < best || (dist == best && i < bi)) { best = dist; bi = i; }
         };
         if (pass == 0) {
-            for (int yy = max(cy - 1, 0); yy <= min(cy + 1, hl.ny - 1); ++yy) {
-                const int k0 = lb(lsk, Mn, yy * hl.nx + max(cx - 1, 0)), k1 = lb(lsk, Mn, yy * hl.nx + min(cx + 1, hl.nx - 1) + 1);
-                for (int k = k0 + threadIdx.x; k < k1; k += blockDim.x) test(lsi[k]);
+            for (int yy = max(cy - 1, 0); yy <= min(cy + 1, cn.h.ny - 1); ++yy) {
+                int k0, k1;
+                ci_row(cn, yy, cx, k0, k1);
+                for (int k = k0 + threadIdx.x; k < k1; k += blockDim.x) test(cn.items[k]);
             }
         } else {
             for (int i = threadIdx.x; i < Mn; i += blockDim.x) test(i);
@@ -395,36 +402,28 @@ __global__ __launch_bounds__(256) void k_label_points(const LabelRow *jobs, int 
 }
 
 // ------------------------------------------------------------------ g9 node labels (publishGraph gvd:920-995)
-// label point j = 4 r + k (valid ones) -> its cell of the 0.1 m hash hq; invalid -> INT_MAX
-__global__ void k_label_keys(const double2 *lp, const int *lv, int nj, HashG hq, int *keys, int *idx) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= nj) return;
-    int cx, cy;
-    cell_of(hq, lp[j].x, lp[j].y, cx, cy);
-    keys[j] = lv[j] ? cy * hq.nx + cx : INT_MAX;
-    idx[j] = j;
-}
 // A node matches label point j iff |dx|, |dy| < 0.1 (and the reference's distance test), so only the
-// label points of its 3 x 3 cells of the 0.1 m hash can match (qsk / qsj: sorted keys and their j); the
-// matches are put back in (r, k) order. More than kNodeMatch matches: the plain loop over every label point.
+// label points of its 3 x 3 cells of the label points' cell index cq (cells >= 0.1 m) can match; the
+// matches are put back in (r, k) order. More than kNodeMatch matches: the plain loop over every label
+// point. Count pass (off == nullptr) over [0, no): 0 past the Mn nodes.
 constexpr int kNodeMatch = 16;
-__global__ void k_node_labels(const double2 *nodes, int Mn, const double2 *lp, const int *lv, int n_rows, HashG hq,
-                              const int *qsk, const int *qsj, int *mask, int *cidx, int *count, const int *off,
-                              int *lcl, int *lty) {
+__global__ void k_node_labels(const double2 *nodes, int no, const int *Mn_dev, const double2 *lp, const int *lv, int n_rows,
+                              CellIdx cq, int *mask, int *cidx, int *count, const int *off, int *lcl, int *lty) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= Mn) return;
+    if (i >= no) return;
+    if (i >= *Mn_dev) { if (!off) count[i] = 0; return; }
     const double2 p = nodes[i];
     int m = 0, ci = -1, cnt = 0, w = off ? off[i] : 0;
     {
         int js[kNodeMatch], nm = 0;
         bool over = false;
         int cx, cy;
-        cell_of(hq, p.x, p.y, cx, cy);
-        const int nq = 4 * n_rows;
-        for (int yy = max(cy - 1, 0); yy <= min(cy + 1, hq.ny - 1); ++yy) {
-            const int k0 = lb(qsk, nq, yy * hq.nx + max(cx - 1, 0)), k1 = lb(qsk, nq, yy * hq.nx + min(cx + 1, hq.nx - 1) + 1);
+        hash_cell(cq.h, p.x, p.y, cx, cy);
+        for (int yy = max(cy - 1, 0); yy <= min(cy + 1, cq.h.ny - 1); ++yy) {
+            int k0, k1;
+            ci_row(cq, yy, cx, k0, k1);
             for (int q = k0; q < k1; ++q) {
-                const int j = qsj[q];
+                const int j = cq.items[q];
                 double dx = p.x - lp[j].x, dy = p.y - lp[j].y;
                 if (!(fabs(dx) < 0.1) || !(fabs(dy) < 0.1)) continue;
                 if (sqrt(dx * dx + dy * dy) < 0.1) {
@@ -462,6 +461,12 @@ __global__ void k_node_labels(const double2 *nodes, int Mn, const double2 *lp, c
             }
         }
     if (!off) { mask[i] = m; cidx[i] = ci; count[i] = cnt; }
+}
+
+// the device scalars the host needs, gathered for one read-back
+struct Peek { const int *src[8]; int n; };
+__global__ void k_peek(Peek P, int *dst) {
+    if (threadIdx.x < P.n) dst[threadIdx.x] = *P.src[threadIdx.x];
 }
 
 // ------------------------------------------------------------------ output gather
@@ -573,7 +578,11 @@ struct GvdScratch {
     DevBuf raw, ok, leaders, merged, owner, oidx, sowner, sidx, tmp, edges_f, occ, occ_ok, bp, kept_occ, keys, idx, skeys,
         sidx2, near_idx, pk, pidx, pskeys, psidx, pcount, poff, plist, ft, ckey, cvalid, pass, k2, occ_idx, sk2, socc, selected,
         inside, ipos, nodes, keep, kpos, edges, lens, jobs, nkeys, nidx, qkeys, qidx, lpts, lval, lmask, lcidx, lcount, loff, lcl, lty, scan_tmp,
-        gather;
+        gather, misc, gcnt, goff, glist;
+    bool gcnt_dirty = true;           // gcnt (edge groups' counts) not known to be zero
+    CellScratch ci_nodes, ci_labels;  // g8 / g9 indices (g5 / g6 use the de-duplication's own)
+    CellIdx cq{};
+    LookBackScratch lb;               // the graph's single-pass scans
     FacetBufs fb;
 };
 static GvdScratch &scratch(GvdState &G) {
@@ -583,13 +592,6 @@ static GvdScratch &scratch(GvdState &G) {
 void free_gvd_scratch(GvdState &G) {
     delete static_cast<GvdScratch *>(G.scratch);   // DevBuf members free themselves
     G.scratch = nullptr;
-}
-
-static void scan_excl(DevBuf &tmpb, const int *in, int *out, int n, hipStream_t s) {
-    size_t tb = 0;
-    AOS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, n, s));
-    void *t = tmpb.ensure(tb);
-    AOS_HIP(hipcub::DeviceScan::ExclusiveSum(t, tb, in, out, n, s));
 }
 
 // Facets of a replayed Subdiv2D on the GPU: uploads the quad-edge state, computes every face's
@@ -613,10 +615,12 @@ static int facets_count(FacetBufs &F, const Subdiv2D &sd, Subdiv2D::Raw &R, int 
     int *d_cnt = dev<int>(F.cnt, R.n_vtx + 1), *d_off = dev<int>(F.off, R.n_vtx + 2);   // off[n_vtx + 1]: walk error
     k_vor_faces<<<cdiv(2 * R.n_rec, 256), 256, 0, s>>>(F.qe, R.n_rec, d_vp, d_face, d_off + R.n_vtx + 1);
     k_facet_count<<<cdiv(R.n_vtx, 256), 256, 0, s>>>(F.qe, F.vf, F.vt, R.n_vtx, d_cnt, d_off + R.n_vtx + 1);
-    scan_excl(F.scan_tmp, d_cnt, d_off, R.n_vtx + 1, s);
+    scan_1p(F.lb, d_cnt, d_off, R.n_vtx, false, s);
     AOS_HIP(hipMemcpyAsync(h_sc, d_off + R.n_vtx, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+    AOS_HIP(hipMemcpyAsync(h_sc + 2, F.lb.err_word(s), sizeof(int), hipMemcpyDeviceToHost, s));
     sev.sync(s);
     if (h_sc[1]) throw std::runtime_error("Subdiv2D facet walk did not close");
+    if (h_sc[2]) throw std::runtime_error("Subdiv2D facets: single-pass scan failed on the device");
     return h_sc[0];
 }
 static void facets_emit(FacetBufs &F, const Subdiv2D::Raw &R, float4 *edges, hipStream_t s) {
@@ -857,29 +861,22 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     std::memcpy(h_seeds, in.seeds_host, sizeof(double2) * (size_t)n);
     AOS_HIP(hipMemcpyAsync(d_raw, h_seeds, sizeof(double2) * n, hipMemcpyHostToDevice, s));
     tr.mark("h2d");
-    int *d_ok = dev<int>(S.ok, n);
-    k_fill_ones<<<cdiv(n, 256), 256, 0, s>>>(d_ok, n);
-    const HashG hm = make_hash(g.minx - 60.0, g.maxx + 60.0, g.miny - 60.0, g.maxy + 60.0, 0.5);
-    double2 *d_lead_pts = dev<double2>(S.merged, n);
-    int *d_leaders = dev<int>(S.leaders, n);
-    const int nl = greedy_dedup(G.dedup, d_raw, d_ok, n, kConflictLessEq, 0.5, hm, d_lead_pts, d_leaders, s, h_sc);
-    tr.mark("dedup");
-    int *d_owner = dev<int>(S.owner, n), *d_oidx = dev<int>(S.oidx, n), *d_sowner = dev<int>(S.sowner, n),
-        *d_sj = dev<int>(S.sidx, n);
-    k_merge_owner<<<cdiv(n, 256), 256, 0, s>>>(G.dedup.state.as<int>(), G.dedup.coff.as<int>(), G.dedup.clist.as<int>(), n,
-                                                d_owner, d_oidx);
-    {
-        size_t tb = 0;
-        AOS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, d_owner, d_sowner, d_oidx, d_sj, n, 0, 32, s));
-        void *t = S.tmp.ensure(tb);
-        AOS_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, d_owner, d_sowner, d_oidx, d_sj, n, 0, 32, s));
-    }
-    double2 *d_merged = d_lead_pts;  // overwritten in leader order
-    k_merge_sum<<<cdiv(nl, 128), 128, 0, s>>>(d_raw, d_sowner, d_sj, n, d_leaders, nl, d_merged);
-    std::vector<double> merged(2 * (size_t)nl);
-    AOS_HIP(hipMemcpyAsync(h_seeds, d_merged, sizeof(double2) * nl, hipMemcpyDeviceToHost, s));
+    const HashG hm = make_hash_n(g.minx - 60.0, g.maxx + 60.0, g.miny - 60.0, g.maxy + 60.0, 0.5, n);
+    double2 *d_merged = dev<double2>(S.merged, n);
+    int *d_leaders = dev<int>(S.leaders, n), *d_owner = dev<int>(S.owner, n);
+    int *d_cnt = dev<int>(S.misc, 8);
+    // leaders (the kept seeds) -> d_merged, overwritten in leader order by their means
+    greedy_dedup_async(G.dedup, d_raw, nullptr, n, kConflictLessEq, 0.5, hm, d_merged, d_leaders, d_owner, d_cnt, s);
+    k_merge_members<<<cdiv(n, 128), 128, 0, s>>>(d_raw, G.dedup.ci, d_owner, d_leaders, d_cnt, d_merged);
+    // (the whole buffer comes back with the count: one host wait)
+    AOS_HIP(hipMemcpyAsync(h_seeds, d_merged, sizeof(double2) * n, hipMemcpyDeviceToHost, s));
+    AOS_HIP(hipMemcpyAsync(h_sc, d_cnt, sizeof(int), hipMemcpyDeviceToHost, s));
+    AOS_HIP(hipMemcpyAsync(h_sc + 1, dedup_err(G.dedup, s), sizeof(int), hipMemcpyDeviceToHost, s));
     G.sev.sync(s);
+    dedup_check(G.dedup, h_sc[1]);
     tr.mark("merge");
+    const int nl = h_sc[0];
+    std::vector<double> merged(2 * (size_t)nl);
     std::memcpy(merged.data(), h_seeds, sizeof(double2) * (size_t)nl);
     G.n_merged = nl;
     AOS_HIP(hipEventRecord(ev[7], s));
@@ -935,158 +932,136 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
         return true;
     }
 
-    // ---- g5 boundary points
+    // ---- g5 boundary points: the 2E edge ends, de-duplicated (1 cm key or < 5 cm) through a cell index of
+    // cells >= 0.5 m, which g6 reuses for its nearest-point and pair searches (pos_of: ends -> points)
     const int no = 2 * ne;
     double2 *d_occ = dev<double2>(S.occ, no);
-    int *d_occ_ok = dev<int>(S.occ_ok, no);
-    k_edges_to_occ<<<cdiv(no, 256), 256, 0, s>>>(d_ef, ne, d_occ, d_occ_ok);
-    const HashG h5 = make_hash(g.minx - 10.0, g.maxx + 10.0, g.miny - 10.0, g.maxy + 10.0, 0.05);
+    k_edges_to_occ<<<cdiv(no, 256), 256, 0, s>>>(d_ef, ne, d_occ);
+    const HashG h5 = make_hash_n(g.minx - 10.0, g.maxx + 10.0, g.miny - 10.0, g.maxy + 10.0, 0.5, no);
     double2 *d_bp = dev<double2>(S.bp, no);
-    int *d_kept_occ = dev<int>(S.kept_occ, no);
+    int *d_pos_of = dev<int>(S.kept_occ, no);
+    int *d_sc = dev<int>(S.misc, 16);   // [0] M
     const double thr5 = 0.05 * 0.05;
-    const int M = greedy_dedup(G.dedup, d_occ, d_occ_ok, no, kConflictKeyOrSq, thr5, h5, d_bp, d_kept_occ, s, h_sc);
-    G.n_bpts = M;
-    tr.mark("bpts");
+    greedy_dedup_async(G.dedup, d_occ, nullptr, no, kConflictKeyOrSq, thr5, h5, d_bp, nullptr, nullptr, d_sc, s, d_pos_of);
+    const CellIdx cio = G.dedup.ci;
+    const int *d_M = d_sc;
 
     // ---- g6 graph edges
-    int *d_keys = dev<int>(S.keys, M), *d_idx = dev<int>(S.idx, M), *d_skeys = dev<int>(S.skeys, M), *d_sidx = dev<int>(S.sidx2, M);
-    k_cell_keys<<<cdiv(M, 256), 256, 0, s>>>(d_bp, M, h5, d_keys, d_idx);
-    {
-        size_t tb = 0;
-        AOS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, d_keys, d_skeys, d_idx, d_sidx, M, 0, 32, s));
-        void *t = S.tmp.ensure(tb);
-        AOS_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, d_keys, d_skeys, d_idx, d_sidx, M, 0, 32, s));
-    }
     int *d_near = dev<int>(S.near_idx, no);
-    k_nearest<<<cdiv(no, 256), 256, 0, s>>>(d_occ, no, d_bp, M, h5, d_skeys, d_sidx, d_near);
-    const HashG hp = make_hash(g.minx - 10.0, g.maxx + 10.0, g.miny - 10.0, g.maxy + 10.0, 0.5);
-    int *d_pk = dev<int>(S.pk, M), *d_pidx = dev<int>(S.pidx, M), *d_psk = dev<int>(S.pskeys, M), *d_psi = dev<int>(S.psidx, M);
-    k_cell_keys<<<cdiv(M, 256), 256, 0, s>>>(d_bp, M, hp, d_pk, d_pidx);
-    {
-        size_t tb = 0;
-        AOS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, d_pk, d_psk, d_pidx, d_psi, M, 0, 32, s));
-        void *t = S.tmp.ensure(tb);
-        AOS_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, d_pk, d_psk, d_pidx, d_psi, M, 0, 32, s));
-    }
-    int *d_pcount = dev<int>(S.pcount, M + 1), *d_poff = dev<int>(S.poff, M + 1);
-    AOS_HIP(hipMemsetAsync(d_pcount + M, 0, sizeof(int), s));
-    k_pairs<<<cdiv(M, 256), 256, 0, s>>>(d_bp, M, hp, d_psk, d_psi, nullptr, d_pcount, nullptr);
-    scan_excl(S.scan_tmp, d_pcount, d_poff, M + 1, s);
-    AOS_HIP(hipMemcpyAsync(h_sc, d_poff + M, sizeof(int), hipMemcpyDeviceToHost, s));
-    G.sev.sync(s);
-    const int np_ = h_sc[0];
-    tr.mark("pairs");
-    int *d_plist = dev<int>(S.plist, np_);
-    k_pairs<<<cdiv(M, 256), 256, 0, s>>>(d_bp, M, hp, d_psk, d_psi, d_poff, nullptr, d_plist);
-    const int nc = ne + np_;
-    int2 *d_ft = dev<int2>(S.ft, nc);
-    unsigned long long *d_ck = dev<unsigned long long>(S.ckey, nc);
-    int *d_cv = dev<int>(S.cvalid, nc), *d_pass = dev<int>(S.pass, nc);
-    k_candidates<<<cdiv(nc, 256), 256, 0, s>>>(d_near, ne, d_poff, d_plist, M, np_, d_ft, d_ck, d_cv);
-    k_occupancy<<<cdiv(nc, 64), 64, 0, s>>>(d_ft, d_cv, nc, d_bp, in.d_skeleton, g, d_pass);
-    unsigned long long *d_k2 = dev<unsigned long long>(S.k2, nc), *d_sk2 = dev<unsigned long long>(S.sk2, nc);
-    int *d_oi = dev<int>(S.occ_idx, nc), *d_soi = dev<int>(S.socc, nc);
-    k_pass_keys<<<cdiv(nc, 256), 256, 0, s>>>(d_ck, d_pass, nc, d_k2, d_oi);
-    {
-        size_t tb = 0;
-        AOS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, d_k2, d_sk2, d_oi, d_soi, nc, 0, 64, s));
-        void *t = S.tmp.ensure(tb);
-        AOS_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, d_k2, d_sk2, d_oi, d_soi, nc, 0, 64, s));
-    }
-    int *d_sel = dev<int>(S.selected, nc);
-    AOS_HIP(hipMemsetAsync(d_sel, 0, sizeof(int) * nc, s));
-    k_first_of_key<<<cdiv(nc, 256), 256, 0, s>>>(d_sk2, d_soi, nc, d_sel);
-
-    // ---- g7 filter
-    int *d_in = dev<int>(S.inside, M + 1), *d_ipos = dev<int>(S.ipos, M + 1);
-    AOS_HIP(hipMemsetAsync(d_in + M, 0, sizeof(int), s));
-    k_inside<<<cdiv(M, 256), 256, 0, s>>>(d_bp, M, g, d_in);
-    scan_excl(S.scan_tmp, d_in, d_ipos, M + 1, s);
-    int *d_keep = dev<int>(S.keep, nc + 1), *d_kpos = dev<int>(S.kpos, nc + 1);
-    AOS_HIP(hipMemsetAsync(d_keep + nc, 0, sizeof(int), s));
-    k_edge_keep<<<cdiv(nc, 256), 256, 0, s>>>(d_sel, d_ft, nc, d_in, d_ipos, d_keep);
-    scan_excl(S.scan_tmp, d_keep, d_kpos, nc + 1, s);
-    AOS_HIP(hipMemcpyAsync(h_sc, d_ipos + M, sizeof(int), hipMemcpyDeviceToHost, s));
-    AOS_HIP(hipMemcpyAsync(h_sc + 1, d_kpos + nc, sizeof(int), hipMemcpyDeviceToHost, s));
-    G.sev.sync(s);
-    const int Mn = h_sc[0], Ne = h_sc[1];
-    tr.mark("filter");
-    double2 *d_nodes = dev<double2>(S.nodes, Mn);
-    k_gather_nodes<<<cdiv(M, 256), 256, 0, s>>>(d_bp, d_in, d_ipos, M, d_nodes);
-    int *d_edges = dev<int>(S.edges, 2 * (size_t)Ne);
-    float *d_lens = dev<float>(S.lens, Ne);
-    k_edge_emit<<<cdiv(nc, 256), 256, 0, s>>>(d_keep, d_kpos, d_ft, nc, d_ipos, d_nodes, d_edges, d_lens);
-
-    // ---- g8 label points for the exploration rows (gvd:130-150, 485-556)
-    std::vector<LabelRow> jobs;
+    k_nearest<<<cdiv(no, 256), 256, 0, s>>>(d_occ, no, cio, d_pos_of, d_bp, d_M, d_near);
+    int *d_pcount = dev<int>(S.pcount, no), *d_poff = dev<int>(S.poff, no + 1);
+    k_pairs<<<cdiv(no, 256), 256, 0, s>>>(d_bp, no, d_M, cio, d_pos_of, d_occ, nullptr, d_pcount, nullptr, 0);
+    scan_1p(S.lb, d_pcount, d_poff, no, false, s);
+    // The pair lists get a capacity from the last frame (P is read back only with the frame's sizes below);
+    // a frame with more pairs runs the rest again with the exact size.
+    int cap = G.pairs_cap > 0 ? G.pairs_cap : std::max(1024, 2 * no);
+    int Mn = 0, Ne = 0, n_entries = 0;
     const int nrows = in.n_rows_poses / 2;
-    if (Mn > 0) {
-        for (int r = 0; r < nrows; ++r) {
-            double sx = in.rows_info[4 * r], sy = in.rows_info[4 * r + 1], ex = in.rows_info[4 * r + 2], ey = in.rows_info[4 * r + 3];
-            if (sx > ex) { std::swap(sx, ex); std::swap(sy, ey); }
-            // castRay angle terms (gvd:574-581): +90 -> cos(a), sin(a); -90 -> cos(-a), sin(-a)
-            const double am = -90.0 * M_PI / 180.0, ap = 90.0 * M_PI / 180.0;
-            const double cm = std::cos(-am), sm = std::sin(-am), cp = std::cos(ap), sp = std::sin(ap);
-            jobs.push_back({sx, sy, ex, ey, -90.0, cm, sm});
-            jobs.push_back({sx, sy, ex, ey, 90.0, cp, sp});
-            jobs.push_back({ex, ey, sx, sy, -90.0, cm, sm});
-            jobs.push_back({ex, ey, sx, sy, 90.0, cp, sp});
-        }
+    const int nj = 4 * nrows;
+    std::vector<LabelRow> jobs;
+    for (int r = 0; r < nrows; ++r) {   // the exploration rows' label jobs (gvd:130-150, 485-556)
+        double sx = in.rows_info[4 * r], sy = in.rows_info[4 * r + 1], ex = in.rows_info[4 * r + 2], ey = in.rows_info[4 * r + 3];
+        if (sx > ex) { std::swap(sx, ex); std::swap(sy, ey); }
+        // castRay angle terms (gvd:574-581): +90 -> cos(a), sin(a); -90 -> cos(-a), sin(-a)
+        const double am = -90.0 * M_PI / 180.0, ap = 90.0 * M_PI / 180.0;
+        const double cm = std::cos(-am), sm = std::sin(-am), cp = std::cos(ap), sp = std::sin(ap);
+        jobs.push_back({sx, sy, ex, ey, -90.0, cm, sm});
+        jobs.push_back({sx, sy, ex, ey, 90.0, cp, sp});
+        jobs.push_back({ex, ey, sx, sy, -90.0, cm, sm});
+        jobs.push_back({ex, ey, sx, sy, 90.0, cp, sp});
     }
-    const int nj = (int)jobs.size();
+    LabelRow *d_jobs = dev<LabelRow>(S.jobs, nj);
+    if (nj) AOS_HIP(hipMemcpyAsync(d_jobs, jobs.data(), sizeof(LabelRow) * nj, hipMemcpyHostToDevice, s));
     double2 *d_lp = dev<double2>(S.lpts, nj);
     int *d_lv = dev<int>(S.lval, nj);
-    if (nj) {
-        LabelRow *d_jobs = dev<LabelRow>(S.jobs, nj);
-        AOS_HIP(hipMemcpyAsync(d_jobs, jobs.data(), sizeof(LabelRow) * nj, hipMemcpyHostToDevice, s));
-        // the nodes hashed in cells of 5.01 m (k_label_points' pass 0)
-        const HashG hl = make_hash(g.minx - 10.0, g.maxx + 10.0, g.miny - 10.0, g.maxy + 10.0, 5.01);
-        int *d_nk = dev<int>(S.nkeys, 2 * (size_t)Mn), *d_ni = dev<int>(S.nidx, 2 * (size_t)Mn);
-        k_cell_keys<<<cdiv(Mn, 256), 256, 0, s>>>(d_nodes, Mn, hl, d_nk, d_ni);
-        size_t tb = 0;
-        AOS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, d_nk, d_nk + Mn, d_ni, d_ni + Mn, Mn, 0, 32, s));
-        AOS_HIP(hipcub::DeviceRadixSort::SortPairs(S.tmp.ensure(tb), tb, d_nk, d_nk + Mn, d_ni, d_ni + Mn, Mn, 0, 32, s));
-        k_label_points<<<nj, 256, 0, s>>>(d_jobs, nj, d_nodes, Mn, g, in.d_skeleton, hl, d_nk + Mn, d_ni + Mn, d_lp, d_lv);
-    }
-    // ---- g9 node labels
-    int *d_mask = dev<int>(S.lmask, Mn), *d_cidx = dev<int>(S.lcidx, Mn), *d_lcnt = dev<int>(S.lcount, Mn + 1),
-        *d_loff = dev<int>(S.loff, Mn + 1);
-    const int nlr = nj / 4;
-    int n_entries = 0;
-    const HashG hq = make_hash(g.minx - 1.0, g.maxx + 1.0, g.miny - 1.0, g.maxy + 1.0, 0.1);
-    int *d_qk = dev<int>(S.qkeys, 2 * (size_t)std::max(nj, 1)), *d_qj = dev<int>(S.qidx, 2 * (size_t)std::max(nj, 1));
-    if (Mn > 0 && nj > 0) {   // the label points hashed in cells of 0.1 m (k_node_labels)
-        k_label_keys<<<cdiv(nj, 256), 256, 0, s>>>(d_lp, d_lv, nj, hq, d_qk, d_qj);
-        size_t tb = 0;
-        AOS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, d_qk, d_qk + nj, d_qj, d_qj + nj, nj, 0, 32, s));
-        AOS_HIP(hipcub::DeviceRadixSort::SortPairs(S.tmp.ensure(tb), tb, d_qk, d_qk + nj, d_qj, d_qj + nj, nj, 0, 32, s));
-    }
-    if (Mn > 0) {
-        AOS_HIP(hipMemsetAsync(d_lcnt + Mn, 0, sizeof(int), s));
-        k_node_labels<<<cdiv(Mn, 256), 256, 0, s>>>(d_nodes, Mn, d_lp, d_lv, nlr, hq, d_qk + nj, d_qj + nj, d_mask, d_cidx,
-                                                    d_lcnt, nullptr, nullptr, nullptr);
-        scan_excl(S.scan_tmp, d_lcnt, d_loff, Mn + 1, s);
-        AOS_HIP(hipMemcpyAsync(h_sc, d_loff + Mn, sizeof(int), hipMemcpyDeviceToHost, s));
+    double2 *d_nodes = dev<double2>(S.nodes, no);
+    int *d_in = dev<int>(S.inside, no), *d_ipos = dev<int>(S.ipos, no + 1);
+    int *d_mask = dev<int>(S.lmask, no), *d_cidx = dev<int>(S.lcidx, no), *d_lcnt = dev<int>(S.lcount, no),
+        *d_loff = dev<int>(S.loff, no + 1);
+    int *d_edges = nullptr, *d_lcl = nullptr, *d_lty = nullptr;
+    float *d_lens = nullptr;
+    int *h_sz = h_sc + 8;
+    for (int attempt = 0;; ++attempt) {
+        const int ncap = ne + cap;
+        int *d_plist = dev<int>(S.plist, cap);
+        k_pairs<<<cdiv(no, 256), 256, 0, s>>>(d_bp, no, d_M, cio, d_pos_of, d_occ, d_poff, nullptr, d_plist, cap);
+        int2 *d_ft = dev<int2>(S.ft, ncap);
+        int *d_pass = dev<int>(S.pass, ncap), *d_grank = dev<int>(S.occ_idx, ncap), *d_sel = dev<int>(S.selected, ncap);
+        const size_t gc0 = S.gcnt.cap;
+        int *d_gcnt = dev<int>(S.gcnt, no);
+        if (S.gcnt.cap != gc0 || S.gcnt_dirty) AOS_HIP(hipMemsetAsync(d_gcnt, 0, S.gcnt.cap, s));
+        S.gcnt_dirty = true;
+        int *d_goff = dev<int>(S.goff, no + 1), *d_glist = dev<int>(S.glist, ncap);
+        k_candidates<<<cdiv(ncap, 256), 256, 0, s>>>(d_near, ne, d_poff, d_plist, d_M, no, cap, d_ft);
+        k_occupancy<<<cdiv(ncap, 64), 64, 0, s>>>(d_ft, d_poff, no, ne, cap, d_bp, in.d_skeleton, g, d_pass, d_gcnt, d_grank);
+        scan_1p(S.lb, d_gcnt, d_goff, no, true, s);   // (leaves the group counts zero)
+        S.gcnt_dirty = false;
+        k_group_scatter<<<cdiv(ncap, 256), 256, 0, s>>>(d_ft, d_pass, d_poff, no, ne, cap, d_goff, d_grank, d_glist);
+        k_select<<<cdiv(ncap, 256), 256, 0, s>>>(d_ft, d_pass, d_poff, no, ne, cap, d_goff, d_glist, d_sel);
+
+        // ---- g7 filter
+        k_inside<<<cdiv(no, 256), 256, 0, s>>>(d_bp, no, d_M, g, d_in);
+        scan_1p(S.lb, d_in, d_ipos, no, false, s);
+        int *d_keep = dev<int>(S.keep, ncap), *d_kpos = dev<int>(S.kpos, ncap + 1);
+        k_edge_keep<<<cdiv(ncap, 256), 256, 0, s>>>(d_sel, d_ft, ncap, d_in, d_ipos, d_keep);
+        scan_1p(S.lb, d_keep, d_kpos, ncap, false, s);
+        k_gather_nodes<<<cdiv(no, 256), 256, 0, s>>>(d_bp, d_in, d_ipos, no, d_nodes);
+        d_edges = dev<int>(S.edges, 2 * (size_t)ncap);
+        d_lens = dev<float>(S.lens, ncap);
+        k_edge_emit<<<cdiv(ncap, 256), 256, 0, s>>>(d_keep, d_kpos, d_ft, ncap, d_ipos, d_nodes, d_edges, d_lens);
+        const int *d_Mn = d_ipos + no;
+
+        // ---- g8 label points for the exploration rows: the nodes in cells of >= 5.01 m
+        if (nj) {
+            const HashG hl = make_hash_n(g.minx - 10.0, g.maxx + 10.0, g.miny - 10.0, g.maxy + 10.0, 5.01, no);
+            const CellIdx cn = cell_index_build(S.ci_nodes, d_nodes, nullptr, no, hl, s, d_Mn);
+            k_label_points<<<nj, 256, 0, s>>>(d_jobs, nj, d_nodes, d_Mn, g, in.d_skeleton, cn, d_lp, d_lv);
+        }
+        // ---- g9 node labels: the valid label points in cells of >= 0.1 m
+        const HashG hq = make_hash_n(g.minx - 1.0, g.maxx + 1.0, g.miny - 1.0, g.maxy + 1.0, 0.1, nj);
+        const CellIdx cq = S.cq = cell_index_build(S.ci_labels, d_lp, d_lv, nj, hq, s);
+        k_node_labels<<<cdiv(no, 256), 256, 0, s>>>(d_nodes, no, d_Mn, d_lp, d_lv, nrows, cq, d_mask, d_cidx, d_lcnt, nullptr,
+                                                    nullptr, nullptr);
+        scan_1p(S.lb, d_lcnt, d_loff, no, false, s);
+        // the frame's sizes and error words: one read-back
+        Peek pk{{d_M, d_poff + no, d_Mn, d_kpos + ncap, d_loff + no, dedup_err(G.dedup, s), S.lb.err_word(s),
+                 S.ci_nodes.lb.err_word(s)}, 8};
+        k_peek<<<1, 64, 0, s>>>(pk, d_sc + 8);
+        AOS_HIP(hipMemcpyAsync(h_sz, d_sc + 8, 8 * sizeof(int), hipMemcpyDeviceToHost, s));
         G.sev.sync(s);
-        n_entries = h_sc[0];
+        if (h_sz[5] || h_sz[6] || h_sz[7]) {
+            if (h_sz[6] || h_sz[7]) throw std::runtime_error("GVD graph: single-pass scan failed on the device");
+            dedup_check(G.dedup, h_sz[5]);
+        }
+        const int P_ = h_sz[1];
+        G.pairs_cap = std::max(1024, P_ + P_ / 4);
+        if (P_ <= cap) {
+            G.n_bpts = h_sz[0];
+            Mn = h_sz[2]; Ne = h_sz[3]; n_entries = h_sz[4];
+            break;
+        }
+        if (attempt) throw std::runtime_error("GVD graph: pair lists overflowed twice");
+        cap = G.pairs_cap;
     }
-    tr.mark("labels");
-    int *d_lcl = dev<int>(S.lcl, n_entries), *d_lty = dev<int>(S.lty, n_entries);
+    tr.mark("graph");
+    const int nj_out = Mn > 0 ? nj : 0;   // (no nodes: no label jobs, gvd:485-556 finds nothing to label)
+    d_lcl = dev<int>(S.lcl, n_entries);
+    d_lty = dev<int>(S.lty, n_entries);
     if (n_entries)
-        k_node_labels<<<cdiv(Mn, 256), 256, 0, s>>>(d_nodes, Mn, d_lp, d_lv, nlr, hq, d_qk + nj, d_qj + nj, nullptr, nullptr,
-                                                    nullptr, d_loff, d_lcl, d_lty);
+        k_node_labels<<<cdiv(Mn, 256), 256, 0, s>>>(d_nodes, Mn, d_ipos + no, d_lp, d_lv, nrows, S.cq, nullptr,
+                                                    nullptr, nullptr, d_loff, d_lcl, d_lty);
 
     // ---- outputs: one gather kernel, one D2H copy into the state's pinned buffer, host copies out
     G.nodes_xy.resize(2 * (size_t)Mn); G.labels.resize(Mn); G.cluster_idx.resize(Mn); G.label_counts.resize(Mn);
     G.label_clusters.resize(n_entries); G.label_types.resize(n_entries);
     G.edges_out.resize(2 * (size_t)Ne); G.lengths.resize(Ne); G.clearances.assign(Ne, 0.0f);
-    G.row_label_xy.resize(2 * (size_t)nj); G.row_label_valid.resize(nj);
+    G.row_label_xy.resize(2 * (size_t)nj_out); G.row_label_valid.resize(nj_out);
     struct Out { const void *d; void *h; long long words; };
     const Out outs[] = {{d_nodes, G.nodes_xy.data(), 4LL * Mn}, {d_mask, G.labels.data(), Mn}, {d_cidx, G.cluster_idx.data(), Mn},
                         {d_lcnt, G.label_counts.data(), Mn}, {d_lcl, G.label_clusters.data(), n_entries},
                         {d_lty, G.label_types.data(), n_entries}, {d_edges, G.edges_out.data(), 2LL * Ne},
-                        {d_lens, G.lengths.data(), Ne}, {d_lp, G.row_label_xy.data(), 4LL * nj},
-                        {d_lv, G.row_label_valid.data(), nj}};
+                        {d_lens, G.lengths.data(), Ne}, {d_lp, G.row_label_xy.data(), 4LL * nj_out},
+                        {d_lv, G.row_label_valid.data(), nj_out}};
     SegList sl{};
     for (const Out &o : outs) {
         if (o.words <= 0) continue;

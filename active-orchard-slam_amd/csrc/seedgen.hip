@@ -387,9 +387,13 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
     // the big-tile kernels run once a frame of this handle has needed them, and on every frame that cannot
     // be redone (a tiled rank, a redo); a frame that finds a big tile without them is redone (ror_collect)
     L.big_ok = ror_big_seen || !allow_guess || o.limit_box;
-    if (store_ok && ms.dense == is_dense && ms.n_points == map_scan_begin && n_points > ms.n_points) {
+    if (store_ok && ms.dense == is_dense && ms.n_points == map_scan_begin && n_points >= ms.n_points) {
         const RorLaunch a = geom_of(L), b = ms.L;
-        if (!std::memcmp(&a, &b, sizeof(RorLaunch))) { ror_stage_append(L, rbits); return; }
+        if (!std::memcmp(&a, &b, sizeof(RorLaunch))) {
+            if (n_points > ms.n_points) ror_stage_append(L, rbits);
+            else ror_stage_unchanged();
+            return;
+        }
     }
     const int nt = L.ntiles;
     const int G = rt_part_blocks(L);
@@ -403,9 +407,6 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
     DevBuf &stage_buf = map_mode ? ms.st[ms.cur] : sorted;
     unsigned long long *d_cnt = static_cast<unsigned long long *>(counters.ensure(8 * kRorCounters + 16));
     unsigned long long *d_own = d_cnt + kRorCounters;   // [0] binned points, [1] overflow flag
-    size_t st = scan_temp_bytes(nt + 1);
-    void *d_st = scan_tmp.ensure(st);
-    AOS_HIP(hipMemsetAsync(d_tot + nt, 0, sizeof(int), s));
     AOS_HIP(hipMemsetAsync(d_cnt, 0, 8 * kRorCounters + 16, s));
     AOS_HIP(hipMemsetAsync(rbits, 0, sizeof(uint64_t) * (size_t)o.Hr * WWr, s));
     if (d_kept) AOS_HIP(hipMemsetAsync(d_kept, 0, sizeof(int) * nt, s));
@@ -418,7 +419,7 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
     int *d_part = static_cast<int *>(pt_binslot.ensure(sizeof(int) * rt_colpart_ints(L, G)));
     launch_rt_count(L, d_H, G, d_part, d_tot, d_own, s);
     AOS_HIP(hipEventRecord(ev[13], s));
-    launch_exclusive_scan(d_tot, d_ts, nt + 1, d_st, st, s);
+    scan_1p(ror_lb, d_tot, d_ts, nt, false, s);
     // The staged array holds own + halo copies. With a capacity from an earlier frame the scatter
     // runs at once and reports an overflow (the frame is then redone with the size it read back,
     // run_seedgen); without one, or when the caller cannot redo (a tiled frame), the size is read
@@ -469,8 +470,6 @@ void aos_ctx::ror_stage_append(RorLaunch L, uint64_t *rbits) {
     int *d_sts = static_cast<int *>(ms.scan_ts.ensure(sizeof(int) * (nt + 1)));
     unsigned long long *d_cnt = static_cast<unsigned long long *>(counters.ensure(8 * kRorCounters + 16));
     unsigned long long *d_own = d_cnt + kRorCounters;
-    size_t st = scan_temp_bytes(nt + 1);
-    void *d_st = scan_tmp.ensure(st);
     // a point lands in at most 4 tiles: the scan's staging and the merged store cannot overflow
     const size_t scan_cap = 4 * (size_t)scan_n + 1024;
     float4 *d_scan = static_cast<float4 *>(ms.scan_st.ensure(sizeof(float4) * scan_cap));
@@ -480,7 +479,6 @@ void aos_ctx::ror_stage_append(RorLaunch L, uint64_t *rbits) {
     float4 *d_new = static_cast<float4 *>(ms.st[nxt].ensure(sizeof(float4) * cap));
     int *d_nts = static_cast<int *>(ms.ts[nxt].ensure(sizeof(int) * (nt + 1)));
     float4 *d_scratch = static_cast<float4 *>(ror_scratch.ensure(sizeof(float4) * cap));
-    AOS_HIP(hipMemsetAsync(d_tot + nt, 0, sizeof(int), s));
     AOS_HIP(hipMemsetAsync(d_cnt, 0, 8 * kRorCounters + 16, s));
     Ls.staged_cap = (int)scan_cap;
     Ls.overflow = reinterpret_cast<int *>(d_own + 1);
@@ -488,7 +486,7 @@ void aos_ctx::ror_stage_append(RorLaunch L, uint64_t *rbits) {
     int *d_part = static_cast<int *>(pt_binslot.ensure(sizeof(int) * rt_colpart_ints(Ls, G)));
     launch_rt_count(Ls, d_H, G, d_part, d_tot, d_own, s);
     AOS_HIP(hipEventRecord(ev[13], s));
-    launch_exclusive_scan(d_tot, d_sts, nt + 1, d_st, st, s);
+    scan_1p(ror_lb, d_tot, d_sts, nt, false, s);
     AOS_HIP(hipEventRecord(ev[14], s));
     launch_rt_scatter(Ls, d_H, d_sts, G, d_scan, s);
     AOS_HIP(hipEventRecord(ev[10], s));
@@ -505,6 +503,17 @@ void aos_ctx::ror_stage_append(RorLaunch L, uint64_t *rbits) {
     AOS_HIP(hipMemcpyAsync(h + 4, d_own, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     // committed by ror_collect (the old store ms.st[ms.cur] stays intact until then)
     ms.pend = MapStore::Pending{true, true, ms.L, ms.dense, n_points, nxt};
+}
+
+// A streaming map's frame with no new points in the map (a tiled rank whose box the scan missed: ADVICE
+// r03): the kept set, the raster bits (ORed into across appends) and the kept count (counters) are the last
+// frame's, so the stage is skipped; the store is recommitted as it is.
+void aos_ctx::ror_stage_unchanged() {
+    for (int e : {12, 13, 14, 10, 11}) AOS_HIP(hipEventRecord(ev[e], stream));
+    int *h = static_cast<int *>(h_stats.p);
+    h[2] = (int)ms.n_staged;   // (binned 0 new points and no overflow: zeroed by ror_stage)
+    ms.pend = MapStore::Pending{true, true, ms.L, ms.dense, n_points, ms.cur};
+    ++ror_skipped;
 }
 
 // After the frame's sync: binned count, staged size, and whether the scatter overflowed its guess.
@@ -643,10 +652,20 @@ void aos_ctx::thin_check_flags(const int *d_flags, const int *h_flags, int n_rea
 }
 
 void aos_ctx::run_seedgen(bool want_host, aos_seedgen_out &out) {
-    // a frame whose ROR scatter outgrew its size guess is redone once with the size it read back
-    for (int attempt = 0; attempt < 2; ++attempt)
-        if (!run_seedgen_once(want_host, out, attempt == 0)) return;
-    throw std::runtime_error("ROR staging overflowed twice");
+    // A frame is served (have_frame) only once every check passed: finish_frame sets it before the ROR
+    // overflow and thinning-convergence checks of the deferred path, so every way out of here that is not
+    // a good frame (a redo, a throw, a HIP error in between) clears it again.
+    try {
+        // a frame whose ROR scatter outgrew its size guess is redone once with the size it read back
+        for (int attempt = 0; attempt < 2; ++attempt) {
+            if (!run_seedgen_once(want_host, out, attempt == 0)) return;
+            have_frame = false;
+        }
+        throw std::runtime_error("ROR staging overflowed twice");
+    } catch (...) {
+        have_frame = false;
+        throw;
+    }
 }
 
 bool aos_ctx::run_seedgen_once(bool want_host, aos_seedgen_out &out, bool allow_guess) {
@@ -690,7 +709,8 @@ bool aos_ctx::run_seedgen_once(bool want_host, aos_seedgen_out &out, bool allow_
     // Launches past convergence return at once (k_thin_block reads the previous iteration's flag on the
     // device), so the first batch is sized from the last frame's T (at least 2 launches) and later
     // batches double: a frame pays one host round trip in the common case, a few when T jumps.
-    const int cap_launches = std::max(3, max_iters / K);
+    int cap_launches = std::max(3, max_iters / K);
+    if (const char *e = getenv("AOS_DEBUG_THIN_CAP")) cap_launches = std::max(1, atoi(e));   // (tests: force non-convergence)
     int launched = 0;
     const uint64_t *src = d_open;
     ThinOwn whole{0, g.H, 0, g.WW, 1};

@@ -16,6 +16,7 @@
 // tiles are all-gathered and the root rank finishes the frame (a6, a8-a16) on the whole map
 // exactly like aos_seedgen_process: every output is byte-identical to the single-GPU frame.
 #include <algorithm>
+#include <chrono>
 #include <climits>
 #include <cstring>
 #include <stdexcept>
@@ -175,7 +176,75 @@ void aos_ctx::tile_halo_exchange(uint64_t *win, const TilePlan &t, const aos_com
     AOS_HIP(hipGetLastError());
 }
 
+// The frame's collectives go through a wrapper that times every callback (host wall clock, which for a
+// collective includes the wait for the slowest rank), so a tiled run can say where its time went:
+// aos_tiled_stats_get (verdict r03: comm time separately from compute).
+namespace {
+struct TimedComm {
+    aos_comm inner;
+    double ms_gather = 0.0, ms_reduce = 0.0;
+    int n_gather = 0, n_reduce = 0;
+    uint64_t bytes_gather = 0;
+};
+double ms_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+int timed_gather(void *u, uint64_t bytes) {
+    TimedComm &t = *static_cast<TimedComm *>(u);
+    const auto t0 = std::chrono::steady_clock::now();
+    const int r = t.inner.all_gather(t.inner.user, bytes);
+    t.ms_gather += ms_since(t0);
+    ++t.n_gather;
+    t.bytes_gather += bytes;
+    return r;
+}
+int timed_reduce(void *u, int32_t *v, int32_t n) {
+    TimedComm &t = *static_cast<TimedComm *>(u);
+    const auto t0 = std::chrono::steady_clock::now();
+    const int r = t.inner.all_reduce_max(t.inner.user, v, n);
+    t.ms_reduce += ms_since(t0);
+    ++t.n_reduce;
+    return r;
+}
+}  // namespace
+
 void aos_ctx::run_tiled(const aos_comm &cm, int tiles_x, int tiles_y, int root, bool want_host, aos_seedgen_out &out) {
+    TimedComm tc{cm};
+    aos_comm w = cm;
+    w.user = &tc;
+    w.all_gather = cm.all_gather ? timed_gather : nullptr;
+    w.all_reduce_max = cm.all_reduce_max ? timed_reduce : nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    const uint64_t skipped0 = ror_skipped;
+    auto record = [&]() {
+        tstats = aos_tiled_stats{};
+        tstats.ms_frame = (float)ms_since(t0);
+        tstats.ms_comm_gather = (float)tc.ms_gather;
+        tstats.ms_comm_reduce = (float)tc.ms_reduce;
+        tstats.n_gather = tc.n_gather;
+        tstats.n_reduce = tc.n_reduce;
+        tstats.bytes_gather = tc.bytes_gather;
+        tstats.ms_cluster_local = cdist_stats.ms_local;
+        tstats.ms_cluster_global = cdist_stats.ms_global;
+        tstats.ms_replay = cdist_stats.ms_replay;
+        tstats.n_replayed = cdist_stats.n_replayed_here;
+        tstats.ror_skipped = ror_skipped != skipped0 ? 1 : 0;
+        tstats.is_root = cm.rank == root ? 1 : 0;
+    };
+    try {
+        run_tiled_frame(w, tiles_x, tiles_y, root, want_host, out);
+    } catch (...) {
+        record();
+        throw;
+    }
+    record();
+    tstats.ms_ror = out.ms_ror;
+    tstats.ms_thin = out.ms_thin;
+    tstats.ms_cluster = out.ms_cluster;
+    tstats.ms_seeds = out.ms_seeds;
+}
+
+void aos_ctx::run_tiled_frame(const aos_comm &cm, int tiles_x, int tiles_y, int root, bool want_host, aos_seedgen_out &out) {
     std::memset(&out, 0, sizeof(out));
     have_frame = false;
     tiled_frame = true;
@@ -254,13 +323,20 @@ void aos_ctx::run_tiled(const aos_comm &cm, int tiles_x, int tiles_y, int root, 
     unsigned long long *h_cnt = static_cast<unsigned long long *>(h_stats.ensure(64 + 8 * kRorCounters)) + 8;
     AOS_HIP(hipMemcpyAsync(h_cnt, counters.p, 8 * kRorCounters, hipMemcpyDeviceToHost, s));
     AOS_HIP(hipStreamSynchronize(s));
-    (void)ror_collect();   // sized by a read-back: no overflow
+    // (sized by a read-back, so no staging overflow is expected; a streaming store's merge can still
+    // overflow a stale size: the bits travel with the counts and every rank fails the frame together)
+    const bool ror_over = ror_collect();
+    const int ror_bits = ror_over ? (int)reinterpret_cast<const unsigned long long *>(static_cast<const int *>(h_stats.p) + 4)[1] : 0;
     uint64_t mine_cnt = 0;
     for (int i = 0; i < kRorCounters; ++i) mine_cnt += h_cnt[i];
-    std::vector<int32_t> slots(2 * (size_t)cm.world, 0);
+    std::vector<int32_t> slots(2 * (size_t)cm.world + 1, 0);
     slots[2 * cm.rank] = (int32_t)(mine_cnt & 0x7fffffff);
     slots[2 * cm.rank + 1] = (int32_t)(mine_cnt >> 31);
+    slots[2 * cm.world] = ror_bits;
     comm_max(cm, slots.data(), (int)slots.size());
+    if (slots[2 * cm.world])
+        throw std::runtime_error("tiled frame: ROR stage overflow on a rank (bits " + std::to_string(slots[2 * cm.world]) +
+                                 ": 1 staged capacity / store merge, 2 a tile beyond the LDS capacity)");
     uint64_t total = 0;
     for (int r = 0; r < cm.world; ++r) total += (uint64_t)slots[2 * r] | ((uint64_t)slots[2 * r + 1] << 31);
 

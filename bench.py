@@ -35,6 +35,7 @@ for sub in ("tools", "active-orchard-slam_amd"):
     sys.path.insert(0, os.path.join(ROOT, sub))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+WATCHDOG_EXIT = 3      # exit status of a run whose tiled section hung (its watchdog fired)
 # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE summaries (tools/pmc_traffic.py) of the ROR stage, per config,
 # for the kernels of this build's ROR design. A config or design without a committed PMC run gets null.
 ROR_DESIGN = "r03"
@@ -252,7 +253,10 @@ def tiled_extra(a, E, dist, main_out, stream: bool = False) -> dict:
         if E["rank"] == 0 and res["main_out"] is not None:
             res["main_out"][key] = {"error": res["error"]}
             print(json.dumps(res["main_out"]), flush=True)
-        os._exit(0)   # every rank's own watchdog fires: none is left waiting in a collective
+        print(f"bench: {res['error']}", file=sys.stderr, flush=True)
+        # every rank's own watchdog fires: none is left waiting in a collective; the exit status says the run
+        # did not complete (the main line above still carries the single-map measurement)
+        os._exit(WATCHDOG_EXIT)
     timer = threading.Timer(limit, watchdog)
     timer.daemon = True
     timer.start()
@@ -264,8 +268,47 @@ def tiled_extra(a, E, dist, main_out, stream: bool = False) -> dict:
     timer.cancel()
     if o is None:
         return None
-    keep = ("value", "unit", "ms_per_step", "frame_latency_ms", "root_serial_ms", "config", "frame", "stages_ms", "stream")
+    keep = ("value", "unit", "ms_per_step", "frame_latency_ms", "root_serial_ms", "root_serial_split_ms", "per_rank",
+            "config", "frame", "stages_ms", "stream")
     return {k: o[k] for k in keep if k in o}
+
+
+def tiled_breakdown(res, pend, warmup: int, world: int, rank: int, dist):
+    """Per rank, the timed tiled frames' averages of aos_tiled_stats (host clock): the whole call, the time
+    inside the all-gather / all-reduce callbacks (a collective includes the wait for the slowest rank), and
+    the rest (compute); and, over the root frames of all ranks, the root's serial part split into the
+    cluster stage (of which the exact BFS replays run on the root), rows + seeds and the GVD's GPU prefix
+    (the seed merge, before its job goes to the background). Returns (per-rank list, split) on rank 0."""
+    keys = ("ms_frame", "ms_comm_gather", "ms_comm_reduce", "ms_ror", "ms_thin", "ms_cluster_local",
+            "ms_cluster_global", "ms_replay")
+    sts = [gs["tiled_stats"] for gs, _ in res if "tiled_stats" in gs]
+    mine = {"rank": rank, "frames": len(sts)}
+    for k in keys:
+        mine[k] = round(sum(t[k] for t in sts) / max(1, len(sts)), 3)
+    mine["ms_compute"] = round(mine["ms_frame"] - mine["ms_comm_gather"] - mine["ms_comm_reduce"], 3)
+    mine["collectives_per_frame"] = round(sum(t["n_gather"] + t["n_reduce"] for t in sts) / max(1, len(sts)), 1)
+    mine["gather_MB_per_frame"] = round(sum(t["bytes_gather"] for t in sts) / max(1, len(sts)) / 1e6, 3)
+    mine["ror_skipped_frames"] = sum(t["ror_skipped"] for t in sts)
+    root_frames = [(k, t) for k, (gs, _) in enumerate(res) if gs.get("root") for t in [gs.get("tiled_stats")] if t]
+    gstart = pend.get("gvd_start", {})
+    mine_root = [(t["ms_cluster"], t["ms_replay"], t["ms_seeds"], 1e3 * gstart.get(warmup + k, 0.0)) for k, t in root_frames]
+    if world > 1:
+        allr = [None] * world
+        dist.all_gather_object(allr, (mine, mine_root))
+    else:
+        allr = [(mine, mine_root)]
+    if rank != 0:
+        return None, None
+    per_rank = [m for m, _ in allr]
+    roots = [r for _, rr in allr for r in rr]
+    split = None
+    if roots:
+        n = len(roots)
+        split = {"cluster_stage": round(sum(r[0] for r in roots) / n, 3),
+                 "of_which_replays_on_root": round(sum(r[1] for r in roots) / n, 3),
+                 "rows_and_seeds": round(sum(r[2] for r in roots) / n, 3),
+                 "gvd_prefix": round(sum(r[3] for r in roots) / n, 3), "root_frames": n}
+    return per_rank, split
 
 
 def run(a, E, dist, quiet=False):
@@ -274,6 +317,8 @@ def run(a, E, dist, quiet=False):
 
     import aos_gpu
     import orchard
+    if os.environ.get("AOS_NUMPY_HUGEPAGE") != "1":
+        aos_gpu.disable_numpy_hugepage()   # (the markers copies: DESIGN §7b; AOS_NUMPY_HUGEPAGE=1 keeps numpy's default)
     world, rank, gpu, dev, red_dev, backend = E["world"], E["rank"], E["gpu"], E["dev"], E["red_dev"], E["backend"]
 
     cfg = orchard.CONFIGS[a.config]
@@ -435,6 +480,7 @@ def run(a, E, dist, quiet=False):
             ctx.gvd_async()
             pend["fifo"].append(k)
             t3 = time.perf_counter()
+            pend.setdefault("gvd_start", {})[k] = t3 - t2   # the GVD's GPU prefix (seed merge) before it goes async
             if last:
                 while pend["fifo"]:
                     gg = finish(pend["fifo"].pop(0))
@@ -498,6 +544,10 @@ def run(a, E, dist, quiet=False):
     # sequential: every step is one whole frame, so the median step is the median per-frame wall-clock
     # (the max over ranks at N > 1); pipelined: frames overlap and the timed-region throughput is the rate
     value = value_mean if main_pipe else units / med
+
+    tiled_ranks = tiled_split = None
+    if a.tiled:
+        tiled_ranks, tiled_split = tiled_breakdown(res, pend, a.warmup, world, rank, dist)
 
     stage = {}
     n_gvd = sum(1 for _, ggs in res if ggs is not None)
@@ -656,6 +706,9 @@ def run(a, E, dist, quiet=False):
             if roots:
                 out["root_serial_ms"] = round(sum(gs["ms"].get("cluster", 0.0) + gs["ms"].get("seeds", 0.0)
                                                   for gs in roots) / len(roots), 3)
+            if tiled_ranks is not None:
+                out["per_rank"] = tiled_ranks
+                out["root_serial_split_ms"] = tiled_split
             if frame_lat:
                 out["frame_latency_ms"] = {"p50": round(_median(frame_lat), 2), "max": round(frame_lat[-1], 2)}
         if world == 1 and not a.no_cpu_baseline and not a.stream:

@@ -268,6 +268,27 @@ int aos_tiled_seedgen_process(aos_ctx *ctx, const aos_comm *comm, int32_t tiles_
 int aos_tiled_map_append(aos_ctx *ctx, const aos_comm *comm, int32_t tiles_x, int32_t tiles_y, int32_t root,
                          const aos_cloud_view *scan, int want_host, aos_seedgen_out *out);
 
+/* Where this rank's last tiled frame (aos_tiled_seedgen_process / aos_tiled_map_append) spent its time
+ * (no reference counterpart: the reference runs one map on one core). Host wall clock; a collective's
+ * time includes the wait for the slowest rank. */
+typedef struct aos_tiled_stats {
+    float ms_frame;            /* the whole call on this rank                                        */
+    float ms_comm_gather;      /* inside aos_comm.all_gather (halo strips, tables, the final grids)  */
+    float ms_comm_reduce;      /* inside aos_comm.all_reduce_max (thinning flags, counts, sizes)     */
+    int32_t n_gather, n_reduce;
+    uint64_t bytes_gather;     /* all-gather payload sent by this rank                               */
+    float ms_ror, ms_thin;     /* device stage times (HIP events), as aos_seedgen_out                */
+    float ms_cluster;          /* cluster stage, from the final all-gather (device events)           */
+    float ms_seeds;            /* root: rows + seeds                                                 */
+    float ms_cluster_local;    /* own-tile labelling and piece tables (host clock)                   */
+    float ms_cluster_global;   /* union-find, long-cluster statistics and replays (incl. collectives) */
+    float ms_replay;           /* of which: this rank's exact BFS replays                            */
+    int32_t n_replayed;        /* clusters replayed on this rank                                     */
+    int32_t ror_skipped;       /* streaming: 1 if no new point reached this rank's box (stage skipped) */
+    int32_t is_root;
+} aos_tiled_stats;
+int aos_tiled_stats_get(aos_ctx *ctx, aos_tiled_stats *out);
+
 /* Border union-find of per-tile cluster pieces: the numbering step of the tiled frame's distributed
  * cluster stage (csrc/cluster_dist.hip; it replaces clusterOccupiedCells' whole-map raster scan + BFS
  * labelling, aos_seed_gen_node.cpp:970-1049, for clusters that cross tiles). Host code: no GPU needed.

@@ -72,7 +72,8 @@ def test_independent_tile_per_rank():
 
 def _hang_worker(q):
     """bench.tiled_extra with a tiled run that never returns (a collective that hangs): its watchdog must
-    print rank 0's main result with the tiled error and end the process with status 0."""
+    print rank 0's main result with the tiled error and end the process with a non-zero status, so the hang
+    shows in the run's exit code (verdict r03)."""
     import argparse
     os.environ["AOS_BENCH_TILED_TIMEOUT"] = "1"
     bench.run = lambda *a, **k: time.sleep(3600)
@@ -85,7 +86,8 @@ def test_tiled_extra_watchdog_and_error(capfd):
     code = ("import sys; sys.path.insert(0, %r); sys.path.insert(0, %r); import test_bench_dist as t; "
             "t._hang_worker(None)" % (ROOT, os.path.join(ROOT, "tests")))
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
-    assert p.returncode == 0
+    assert p.returncode == bench.WATCHDOG_EXIT != 0
+    assert "did not finish" in p.stderr
     line = [x for x in p.stdout.splitlines() if x.startswith("{")][-1]
     import json
     d = json.loads(line)
@@ -123,3 +125,22 @@ def test_tiled_stream_extra_configuration():
         assert bench.parse(["--tiled", "--stream"]).config == "C2" and bench.parse(["--tiled"]).config == "C3"
     finally:
         bench.run = old
+
+
+def test_tiled_breakdown_keys():
+    """--gpus N tiled lines: per rank, the frame split into time inside the all-gather / all-reduce callbacks
+    and compute, and the root's serial part split into cluster stage (replays), rows + seeds and GVD prefix."""
+    def st(root, frame, gather, reduce, cluster=0.0, replay=0.0, seeds=0.0, skipped=0):
+        return {"ms_frame": frame, "ms_comm_gather": gather, "ms_comm_reduce": reduce, "n_gather": 5, "n_reduce": 3,
+                "bytes_gather": 2_000_000, "ms_ror": 1.0, "ms_thin": 0.5, "ms_cluster": cluster, "ms_seeds": seeds,
+                "ms_cluster_local": 0.2, "ms_cluster_global": 0.7, "ms_replay": replay, "n_replayed": 1,
+                "ror_skipped": skipped, "is_root": int(root)}
+    res = [({"root": True, "tiled_stats": st(True, 10.0, 2.0, 1.0, cluster=3.0, replay=1.5, seeds=1.0)}, None),
+           ({"root": False, "tiled_stats": st(False, 8.0, 3.0, 1.0, skipped=1)}, None)]
+    pend = {"gvd_start": {4: 0.004}}
+    per_rank, split = bench.tiled_breakdown(res, pend, warmup=4, world=1, rank=0, dist=None)
+    r0 = per_rank[0]
+    assert r0["frames"] == 2 and r0["ms_frame"] == 9.0 and r0["ms_comm_gather"] == 2.5 and r0["ms_comm_reduce"] == 1.0
+    assert r0["ms_compute"] == 5.5 and r0["collectives_per_frame"] == 8.0 and r0["ror_skipped_frames"] == 1
+    assert split == {"cluster_stage": 3.0, "of_which_replays_on_root": 1.5, "rows_and_seeds": 1.0, "gvd_prefix": 4.0,
+                     "root_frames": 1}

@@ -1,0 +1,66 @@
+#!/bin/bash
+# One parameterised GPU evidence run (replaces round 3's one-off gpu_r03*.sh launchers). Steps are named
+# in STEPS (space separated, run in order; each GPU step has its own time limit and the chain stops at the
+# first failure):
+#   pytest   the -m gpu parity suite (PYTEST_ARGS: extra pytest arguments, e.g. -k expr)
+#   smoke    __graft_entry__.smoke()
+#   bench    the default bench line (BENCH_ARGS, default --no-cpu-baseline)
+#   stream   the C4 streaming bench
+#   kt       rocprofv3 --kernel-trace --stats of the sequential C2 loop
+#   ktc3     the same on one C3 frame set (bench --config C3 on one GPU)
+#   pmc      FETCH_SIZE and WRITE_SIZE passes (separate runs) -> TAG_pmc_traffic.json
+# Usage: TAG=r04a STEPS="pytest smoke bench kt" tools/gpu_run.sh
+set -e
+R=$PWD
+TAG=${TAG:-r04x}
+STEPS=${STEPS:-"pytest smoke bench kt"}
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+for step in $STEPS; do
+  echo "[$TAG] $step $(date +%T)"
+  case $step in
+    pytest)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread $PYTEST_ARGS \
+        > gpurun_out/${TAG}_pytest_gpu.log 2>&1 || { tail -60 gpurun_out/${TAG}_pytest_gpu.log; exit 1; }
+      tail -1 gpurun_out/${TAG}_pytest_gpu.log ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 \
+        || { tail -20 gpurun_out/${TAG}_smoke.log; exit 1; }
+      tail -1 gpurun_out/${TAG}_smoke.log ;;
+    bench)
+      timeout -k 10 600 python -u bench.py ${BENCH_ARGS:---no-cpu-baseline} > gpurun_out/${TAG}_bench.log \
+        2> gpurun_out/${TAG}_bench.err || { tail -20 gpurun_out/${TAG}_bench.err; exit 1; }
+      grep '^{' gpurun_out/${TAG}_bench.log | cut -c1-400 ;;
+    stream)
+      timeout -k 10 400 python -u bench.py --stream --steps 20 --warmup 2 > gpurun_out/${TAG}_stream.log \
+        2> gpurun_out/${TAG}_stream.err || { tail -20 gpurun_out/${TAG}_stream.err; exit 1; }
+      grep '^{' gpurun_out/${TAG}_stream.log | cut -c1-300 ;;
+    kt)
+      rm -rf gpurun_out/${TAG}_kt
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${TAG}_kt -o kt \
+        -- python3 $R/bench.py --no-cpu-baseline --no-pipelined-rate --no-device-rate --steps 10 --warmup 2 \
+        > $R/gpurun_out/${TAG}_kt.log 2>&1)
+      python3 tools/kt_summary.py gpurun_out/${TAG}_kt 12 > gpurun_out/${TAG}_kt_summary.txt
+      head -30 gpurun_out/${TAG}_kt_summary.txt ;;
+    ktc3)
+      rm -rf gpurun_out/${TAG}_ktc3
+      (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${TAG}_ktc3 -o kt \
+        -- python3 $R/bench.py --config C3 --no-cpu-baseline --no-pipelined-rate --no-device-rate --steps 3 --warmup 1 \
+        > $R/gpurun_out/${TAG}_ktc3.log 2>&1)
+      python3 tools/kt_summary.py gpurun_out/${TAG}_ktc3 4 > gpurun_out/${TAG}_ktc3_summary.txt
+      head -30 gpurun_out/${TAG}_ktc3_summary.txt ;;
+    pmc)
+      rm -rf gpurun_out/${TAG}_fetch gpurun_out/${TAG}_write
+      (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/${TAG}_fetch -o fetch \
+        -- python3 $R/bench.py --no-cpu-baseline --no-pipelined-rate --no-device-rate --steps 3 --warmup 1 \
+        > $R/gpurun_out/${TAG}_fetch.log 2>&1)
+      (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/${TAG}_write -o write \
+        -- python3 $R/bench.py --no-cpu-baseline --no-pipelined-rate --no-device-rate --steps 3 --warmup 1 \
+        > $R/gpurun_out/${TAG}_write.log 2>&1)
+      python3 tools/pmc_traffic.py $(ls gpurun_out/${TAG}_fetch/*counter_collection.csv | head -1) \
+        $(ls gpurun_out/${TAG}_write/*counter_collection.csv | head -1) gpurun_out/${TAG}_pmc_traffic.json ;;
+    *)
+      echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "[$TAG] done $(date +%T)"
