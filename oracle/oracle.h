@@ -130,6 +130,7 @@ void orc_free_path(void *handle);
 void orc_free_seedgen(void *handle);
 void orc_free_gvd(void *handle);
 void orc_free_facets(void *handle);
+void orc_free_subdiv_state(void *handle);
 
 /* ---------- single-stage entry points (KATs / cross-checks) ---------- */
 void orc_ror(const float *xyz, uint64_t n, int32_t is_dense, double radius, int32_t min_pts, uint8_t *keep);
@@ -137,6 +138,10 @@ void orc_inflate(const int8_t *in, uint32_t w, uint32_t h, int32_t cells, int8_t
 void orc_open_cross(const uint8_t *in01, uint32_t w, uint32_t h, uint8_t *out01);
 int32_t orc_thin(const uint8_t *in01, uint32_t w, uint32_t h, uint8_t *out01);
 /* Subdiv2D facets: returns handle; facets flattened (x,y floats), offsets n_facets+1. */
+/* Test hook: raw Subdiv2D state after inserting xy (float pairs) into Subdiv2D(rect = x, y, w, h). */
+void *orc_subdiv_state(const float *xy, int32_t n, const float *rect, int32_t rect_mode, int32_t *n_q, const int32_t **qe,
+                       int32_t *n_v, const int32_t **vfirst, const int32_t **vtype, const float **vxy, const int32_t **inserted,
+                       int32_t *n_facets, const int32_t **offsets, const float **pts);
 void *orc_subdiv_facets(const double *seeds_xy, int32_t n, double min_x, double max_x, double min_y,
                         double max_y, int32_t rect_mode, int32_t *n_facets, const int32_t **offsets,
                         const float **pts, const float **centers);

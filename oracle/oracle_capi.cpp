@@ -139,6 +139,28 @@ void *orc_subdiv_facets(const double *seeds_xy, int32_t n, double min_x, double 
     return H;
 }
 
+// qe: next[4] of every quad-edge, then pt[4] of every quad-edge (n_q of each); vertices: firstEdge, type, xy
+struct SubdivStateHandle { std::vector<int> qe, vfirst, vtype, inserted; std::vector<float> vxy; FacetHandle f; };
+void *orc_subdiv_state(const float *xy, int32_t n, const float *rect, int32_t rect_mode, int32_t *n_q, const int32_t **qe,
+                       int32_t *n_v, const int32_t **vfirst, const int32_t **vtype, const float **vxy, const int32_t **inserted,
+                       int32_t *n_facets, const int32_t **offsets, const float **pts) {
+    auto *H = new (std::nothrow) SubdivStateHandle();
+    subdiv_raw_state(xy, n, rect, rect_mode, H->qe, H->vfirst, H->vtype, H->vxy, H->f.F, H->inserted);
+    *n_q = (int32_t)(H->qe.size() / 8);
+    *qe = H->qe.data();
+    *n_v = (int32_t)H->vfirst.size();
+    *vfirst = H->vfirst.data(); *vtype = H->vtype.data(); *vxy = H->vxy.data(); *inserted = H->inserted.data();
+    H->f.off.push_back(0);
+    for (auto &fc : H->f.F.facets) {
+        for (auto &p : fc) { H->f.pts.push_back(p.first); H->f.pts.push_back(p.second); }
+        H->f.off.push_back((int32_t)(H->f.pts.size() / 2));
+    }
+    *n_facets = (int32_t)H->f.F.facets.size();
+    *offsets = H->f.off.data(); *pts = H->f.pts.data();
+    return H;
+}
+void orc_free_subdiv_state(void *h) { delete static_cast<SubdivStateHandle *>(h); }
+
 void orc_free_seedgen(void *h) { delete static_cast<SeedGenResult *>(h); }
 void orc_free_gvd(void *h) { delete static_cast<GvdHandle *>(h); }
 void orc_free_facets(void *h) { delete static_cast<FacetHandle *>(h); }

@@ -294,6 +294,31 @@ class Subdiv {
 static inline int cv_round(float v) { return (int)std::lrint(v); }
 }  // namespace
 
+// Test hook (known-answer tests, tests/test_subdiv_host.py): a Subdiv2D on the rectangle as given
+// (mode 1: the implicit Rect2f -> Rect conversion), the points inserted in order, then the raw state in
+// OpenCV's layout: per quad-edge next[4] + pt[4] (before calcVoronoi: pt[1] = pt[3] = 0), per vertex
+// firstEdge / type / point, and getVoronoiFacetList's facets (which runs calcVoronoi).
+void subdiv_raw_state(const float *xy, int n, const float rect[4], int rect_mode, std::vector<int> &qe,
+                      std::vector<int> &vfirst, std::vector<int> &vtype, std::vector<float> &vxy, Facets &facets,
+                      std::vector<int> &inserted) {
+    Subdiv sd;
+    float rx = rect[0], ry = rect[1], rw = rect[2], rh = rect[3];
+    if (rect_mode == 1) { rx = (float)cv_round(rx); ry = (float)cv_round(ry); rw = (float)cv_round(rw); rh = (float)cv_round(rh); }
+    sd.init(rx, ry, rw, rh);
+    inserted.clear();
+    for (int i = 0; i < n; ++i) inserted.push_back(sd.insert(P2f{xy[2 * i], xy[2 * i + 1]}) ? 1 : 0);
+    auto dump = [&]() {
+        qe.clear(); vfirst.clear(); vtype.clear(); vxy.clear();
+        for (const auto &q : sd.qedges)
+            for (int k = 0; k < 4; ++k) qe.push_back(q.next[k]);
+        for (size_t i = 0; i < sd.qedges.size(); ++i)
+            for (int k = 0; k < 4; ++k) qe.push_back(sd.qedges[i].pt[k]);
+        for (const auto &v : sd.vtx) { vfirst.push_back(v.firstEdge); vtype.push_back(v.type); vxy.push_back(v.pt.x); vxy.push_back(v.pt.y); }
+    };
+    dump();   // the insert state (no Voronoi points)
+    sd.getVoronoiFacetList(facets);
+}
+
 // VoronoiDiagram::compute voronoi_diagram.cpp:16-94 up to the facet list
 void subdiv_voronoi_facets(const std::vector<V2> &seeds, double min_x, double max_x, double min_y, double max_y,
                            int rect_mode, Facets &out, float *rect_out) {

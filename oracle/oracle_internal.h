@@ -100,6 +100,9 @@ struct Facets {
     std::vector<std::vector<std::pair<float, float>>> facets;
     std::vector<std::pair<float, float>> centers;
 };
+void subdiv_raw_state(const float *xy, int n, const float rect[4], int rect_mode, std::vector<int> &qe,
+                      std::vector<int> &vfirst, std::vector<int> &vtype, std::vector<float> &vxy, Facets &facets,
+                      std::vector<int> &inserted);
 void subdiv_voronoi_facets(const std::vector<V2> &seeds, double min_x, double max_x, double min_y, double max_y,
                            int rect_mode, Facets &out, float *rect_out = nullptr);
 void voronoi_compute(const std::vector<V2> &seeds, double min_x, double max_x, double min_y, double max_y, int rect_mode,

@@ -103,7 +103,10 @@ def lib():
         L.orc_gvd_run.argtypes = [P(Params), P(GvdIn), P(GvdOut)]
         L.orc_path_plan.restype = ctypes.c_void_p
         L.orc_path_plan.argtypes = [P(PathGraph), ctypes.c_void_p, c_d, c_d, c_f, c_u, c_u, P(PathQuery), P(PathOut)]
-        for f in ("orc_free_seedgen", "orc_free_gvd", "orc_free_facets", "orc_free_path"):
+        L.orc_subdiv_state.restype = ctypes.c_void_p
+        L.orc_subdiv_state.argtypes = [ctypes.c_void_p, c_i, ctypes.c_void_p, c_i, P(c_i), P(P(c_i)), P(c_i), P(P(c_i)),
+                                       P(P(c_i)), P(P(c_f)), P(P(c_i)), P(c_i), P(P(c_i)), P(P(c_f))]
+        for f in ("orc_free_seedgen", "orc_free_gvd", "orc_free_facets", "orc_free_path", "orc_free_subdiv_state"):
             getattr(L, f).argtypes = [ctypes.c_void_p]
         L.orc_ror.argtypes = [ctypes.c_void_p, c_u64, c_i, c_d, c_i, ctypes.c_void_p]
         L.orc_inflate.argtypes = [ctypes.c_void_p, c_u, c_u, c_i, ctypes.c_void_p]
@@ -262,6 +265,31 @@ def subdiv_facets(seeds: np.ndarray, bounds, rect_mode=0):
     finally:
         lib().orc_free_facets(h)
     return [facets[o[i]:o[i + 1]] for i in range(n)], centers
+
+
+def subdiv_state(points, rect, rect_mode=0) -> dict:
+    """Test hook: the raw OpenCV-layout state of a Subdiv2D(rect) after inserting `points` (float32 pairs)
+    in order: next / pt per quad-edge (pt[1] = pt[3] = 0: before calcVoronoi), firstEdge / type / point per
+    vertex, whether each insert succeeded, and getVoronoiFacetList's facets (in vertex order)."""
+    xy = np.ascontiguousarray(points, dtype=np.float32).reshape(-1)
+    r = np.ascontiguousarray(rect, dtype=np.float32)
+    nq, nv, nf = c_i(), c_i(), c_i()
+    qe, vf, vt, ins, off = P(c_i)(), P(c_i)(), P(c_i)(), P(c_i)(), P(c_i)()
+    vxy, pts = P(c_f)(), P(c_f)()
+    h = lib().orc_subdiv_state(xy.ctypes.data, xy.size // 2, r.ctypes.data, rect_mode, ctypes.byref(nq), ctypes.byref(qe),
+                               ctypes.byref(nv), ctypes.byref(vf), ctypes.byref(vt), ctypes.byref(vxy), ctypes.byref(ins),
+                               ctypes.byref(nf), ctypes.byref(off), ctypes.byref(pts))
+    try:
+        q = _arr(qe, 8 * nq.value, np.int32)
+        o = _arr(off, nf.value + 1, np.int32)
+        f = _arr(pts, 2 * int(o[-1]) if nf.value else 0, np.float32).reshape(-1, 2)
+        out = {"next": q[:4 * nq.value].reshape(-1, 4), "pt": q[4 * nq.value:].reshape(-1, 4),
+               "first_edge": _arr(vf, nv.value, np.int32), "type": _arr(vt, nv.value, np.int32),
+               "vxy": _arr(vxy, 2 * nv.value, np.float32).reshape(-1, 2), "inserted": _arr(ins, xy.size // 2, np.int32),
+               "facets": [f[o[i]:o[i + 1]] for i in range(nf.value)]}
+    finally:
+        lib().orc_free_subdiv_state(h)
+    return out
 
 
 def path_plan(graph: dict, grid: dict, initial_waypoint_reached=True, initial_waypoint=(8.0, 0.0), target=-1,

@@ -2,7 +2,7 @@
 # One parameterised GPU evidence run (replaces round 3's one-off gpu_r03*.sh launchers). Steps are named
 # in STEPS (space separated, run in order; each GPU step has its own time limit and the chain stops at the
 # first failure):
-#   pytest   the -m gpu parity suite (PYTEST_ARGS: extra pytest arguments, e.g. -k expr)
+#   pytest   the -m gpu parity suite (PYTEST_K: a -k expression)
 #   smoke    __graft_entry__.smoke()
 #   bench    the default bench line (BENCH_ARGS, default --no-cpu-baseline)
 #   stream   the C4 streaming bench
@@ -20,7 +20,7 @@ for step in $STEPS; do
   echo "[$TAG] $step $(date +%T)"
   case $step in
     pytest)
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread $PYTEST_ARGS \
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} \
         > gpurun_out/${TAG}_pytest_gpu.log 2>&1 || { tail -60 gpurun_out/${TAG}_pytest_gpu.log; exit 1; }
       tail -1 gpurun_out/${TAG}_pytest_gpu.log ;;
     smoke)
