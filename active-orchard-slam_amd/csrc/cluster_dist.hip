@@ -36,58 +36,6 @@ namespace aos {
 
 static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
-// ------------------------------------------------------------------ host union-find over pieces
-int cluster_union(int W, int H, int n_pieces, const int *piece_root, int n_border, const int *bcell, const int *broot,
-                  int *piece_cluster) {
-    if (W <= 0 || H <= 0 || n_pieces < 0 || n_border < 0) throw std::invalid_argument("cluster_union: bad sizes");
-    // pieces by root cell (roots are distinct: a cell belongs to one piece)
-    std::vector<std::pair<int, int>> by_root((size_t)n_pieces);
-    for (int i = 0; i < n_pieces; ++i) by_root[i] = {piece_root[i], i};
-    std::sort(by_root.begin(), by_root.end());
-    for (int i = 1; i < n_pieces; ++i)
-        if (by_root[i].first == by_root[i - 1].first) throw std::invalid_argument("cluster_union: duplicate piece root");
-    auto piece_of_root = [&](int r) {
-        auto it = std::lower_bound(by_root.begin(), by_root.end(), std::make_pair(r, INT_MIN));
-        if (it == by_root.end() || it->first != r) throw std::invalid_argument("cluster_union: border cell of an unknown piece");
-        return it->second;
-    };
-    std::vector<int> parent((size_t)n_pieces);
-    std::iota(parent.begin(), parent.end(), 0);
-    auto find = [&](int x) {
-        while (parent[x] != x) { parent[x] = parent[parent[x]]; x = parent[x]; }
-        return x;
-    };
-    auto unite = [&](int a, int b) {   // the piece with the smaller first cell stays the representative
-        a = find(a); b = find(b);
-        if (a == b) return;
-        if (piece_root[a] < piece_root[b]) parent[b] = a;
-        else parent[a] = b;
-    };
-    std::unordered_map<int, int> cell_piece;
-    cell_piece.reserve((size_t)n_border * 2 + 16);
-    for (int i = 0; i < n_border; ++i) cell_piece.emplace(bcell[i], piece_of_root(broot[i]));
-    // each adjacent pair once, from its smaller cell: E, SW, S, SE
-    const int dxs[4] = {1, -1, 0, 1}, dys[4] = {0, 1, 1, 1};
-    for (const auto &kv : cell_piece) {
-        const int p = kv.first, y = p / W, x = p - y * W;
-        for (int k = 0; k < 4; ++k) {
-            const int nx = x + dxs[k], ny = y + dys[k];
-            if (nx < 0 || nx >= W || ny >= H) continue;
-            auto it = cell_piece.find(ny * W + nx);
-            if (it != cell_piece.end()) unite(kv.second, it->second);
-        }
-    }
-    // clusters in raster order of their first cell
-    std::vector<int> reps;
-    for (int i = 0; i < n_pieces; ++i)
-        if (find(i) == i) reps.push_back(i);
-    std::sort(reps.begin(), reps.end(), [&](int a, int b) { return piece_root[a] < piece_root[b]; });
-    std::vector<int> id((size_t)n_pieces, -1);
-    for (size_t k = 0; k < reps.size(); ++k) id[reps[k]] = (int)k;
-    for (int i = 0; i < n_pieces; ++i) piece_cluster[i] = id[find(i)];
-    return (int)reps.size();
-}
-
 // ------------------------------------------------------------------ the rank's own cells (device)
 // Own region of the window skeleton: rows [y0, y0 + nr), words [c0, c0 + nc) of the map, at row oy /
 // word oc of the window (row pitch WWl).

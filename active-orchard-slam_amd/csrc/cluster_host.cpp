@@ -1,0 +1,231 @@
+// Host-side parts of the cluster stage (a8-a10), kept in a plain C++ file so the sanitizer build
+// (tests/sanitize: ASan + UBSan, no GPU) runs exactly the code the product links:
+//   * host_bfs_replay / replay_clusters: clusterOccupiedCells' FIFO BFS (seed_gen:1007-1049) and its
+//     order-dependent statistics, for the clusters without the GPU's order-free certificate;
+//   * cluster_union: the border union-find of the tiled frame's distributed cluster stage (aos_cluster_union);
+//   * assemble_rows: convertClustersToTreeRows' row arrays (seed_gen:1329-1406) and the std::sort-ed
+//     cluster_info / rows_info outputs (seed_gen:1515-1565, 2546-2582).
+#include <algorithm>
+#include <atomic>
+#include <climits>
+#include <cmath>
+#include <exception>
+#include <mutex>
+#include <numeric>
+#include <stdexcept>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "cluster_geom.h"
+#include "cluster_seed.h"
+
+namespace aos {
+
+constexpr int kReplayThreads = 8;   // host threads for the exact BFS replays of one frame
+
+// ------------------------------------------------------------------ exact BFS replay
+// clusterOccupiedCells' FIFO BFS (seed_gen:1007-1049) and the order-dependent statistics that follow
+// (float centre sums :1030-1046, first-strict-maximum endpoints :1354-1395) for the rare clusters
+// without the order-free certificate. This is a serial chain of dependent steps: it runs on the host
+// core next to the GPU (the cluster's cells come over in raster order), ~10 ns per step.
+static void host_bfs_replay(const int *cells, int n, const GridC &g, const double *poly, int np, float min_length,
+                            ClusterRec &r, std::vector<int> &q, std::vector<int> &tab) {
+    int cap = 64;
+    while (cap < 2 * n) cap <<= 1;
+    const unsigned mask = (unsigned)cap - 1;
+    tab.assign(cap, -1);
+    auto slot_of = [&](int key) -> int {   // key present -> its slot, else -1
+        unsigned h = ((unsigned)key * 2654435761u) & mask;
+        for (;;) {
+            int v = tab[h];
+            if (v == -1) return -1;
+            if ((v & 0x7fffffff) == key) return (int)h;
+            h = (h + 1) & mask;
+        }
+    };
+    for (int k = 0; k < n; ++k) {
+        unsigned h = ((unsigned)cells[k] * 2654435761u) & mask;
+        while (tab[h] != -1) h = (h + 1) & mask;
+        tab[h] = cells[k];
+    }
+    q.resize(n);
+    int start = cells[0];   // first raster cell of the component (the cells come in any order)
+    for (int k = 1; k < n; ++k) start = std::min(start, cells[k]);
+    tab[slot_of(start)] |= (int)0x80000000;
+    q[0] = start;
+    int head = 0, tail = 1;
+    const int dxs[8] = {-1, -1, -1, 0, 0, 1, 1, 1}, dys[8] = {-1, 0, 1, -1, 1, -1, 0, 1};
+    while (head < tail) {
+        const int p = q[head++], cy = p / g.W, cx = p - cy * g.W;
+        for (int i = 0; i < 8; ++i) {
+            const int nx = cx + dxs[i], ny = cy + dys[i];
+            if (nx < 0 || nx >= g.W || ny < 0 || ny >= g.H) continue;
+            const int h = slot_of(ny * g.W + nx);
+            if (h < 0 || tab[h] < 0) continue;
+            tab[h] |= (int)0x80000000;
+            q[tail++] = ny * g.W + nx;
+        }
+    }
+    if (tail != n) throw std::runtime_error("BFS replay: cluster is not 8-connected");
+    float sum_x = 0.0f, sum_y = 0.0f;
+    for (int k = 0; k < n; ++k) { int p = q[k], y = p / g.W; sum_x += (float)(p - y * g.W); sum_y += (float)y; }
+    r.cx = sum_x / (float)n;
+    r.cy = sum_y / (float)n;
+    bool row = false;
+    if (r.length >= min_length) {
+        float cwx = (float)(g.ox + (double)(r.cx * g.res)), cwy = (float)(g.oy + (double)(r.cy * g.res));
+        r.center = make_double2(cwx, cwy);
+        row = d_pip(cwx, cwy, poly, np);
+    }
+    if (row) {
+        double mx = 0.0; int fi = 0; double fx = 0, fy = 0;
+        for (int k = 0; k < n; ++k) {
+            double2 w = cell_w(g, q[k]);
+            double dx = w.x - r.center.x, dy = w.y - r.center.y, d2 = dx * dx + dy * dy;
+            if (d2 > mx) { mx = d2; fi = k; double s = std::sqrt(d2); fx = dx / s; fy = dy / s; }
+        }
+        double mo = 0.0; int si = 0;
+        for (int k = 0; k < n; ++k) {
+            if (k == fi) continue;
+            double2 w = cell_w(g, q[k]);
+            double dx = w.x - r.center.x, dy = w.y - r.center.y, d2 = dx * dx + dy * dy;
+            double nx = dx, ny = dy;
+            if (d2 > 0.0) { double s = std::sqrt(d2); nx = dx / s; ny = dy / s; }
+            if (nx * fx + ny * fy < 0.0 && d2 > mo) { mo = d2; si = k; }
+        }
+        if (mo == 0.0) {
+            double2 wf = cell_w(g, q[fi]);
+            for (int k = 0; k < n; ++k) {
+                if (k == fi) continue;
+                double2 w = cell_w(g, q[k]);
+                double dx = w.x - wf.x, dy = w.y - wf.y, d2 = dx * dx + dy * dy;
+                if (d2 > mo) { mo = d2; si = k; }
+            }
+        }
+        r.start = cell_w(g, q[fi]);
+        r.end = cell_w(g, q[si]);
+    }
+    r.flags = (row ? 1 : 0) | 4;  // 4: replayed
+}
+
+// The exact replays of a frame, in parallel over clusters on up to kReplayThreads host threads (each
+// writes only its own record).
+void replay_clusters(const std::vector<ReplayJob> &jobs, const GridC &g, const double *poly, int np, float min_len,
+                     ClusterRec *rec) {
+    if (jobs.empty()) return;
+    std::atomic<int> next{0};
+    std::exception_ptr err;
+    std::mutex mu;
+    auto work = [&]() {
+        std::vector<int> q, tab;
+        for (int i; (i = next.fetch_add(1)) < (int)jobs.size();) {
+            const ReplayJob &j = jobs[i];
+            try {
+                host_bfs_replay(j.cells, j.n, g, poly, np, min_len, rec[j.c], q, tab);
+            } catch (...) {
+                std::lock_guard<std::mutex> lk(mu);
+                if (!err) err = std::current_exception();
+            }
+        }
+    };
+    const int nt = std::min<int>((int)jobs.size(), kReplayThreads);
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(work);
+    work();
+    for (auto &t : th) t.join();
+    if (err) std::rethrow_exception(err);
+}
+
+// ------------------------------------------------------------------ host union-find over pieces
+int cluster_union(int W, int H, int n_pieces, const int *piece_root, int n_border, const int *bcell, const int *broot,
+                  int *piece_cluster) {
+    if (W <= 0 || H <= 0 || n_pieces < 0 || n_border < 0) throw std::invalid_argument("cluster_union: bad sizes");
+    // pieces by root cell (roots are distinct: a cell belongs to one piece)
+    std::vector<std::pair<int, int>> by_root((size_t)n_pieces);
+    for (int i = 0; i < n_pieces; ++i) by_root[i] = {piece_root[i], i};
+    std::sort(by_root.begin(), by_root.end());
+    for (int i = 1; i < n_pieces; ++i)
+        if (by_root[i].first == by_root[i - 1].first) throw std::invalid_argument("cluster_union: duplicate piece root");
+    auto piece_of_root = [&](int r) {
+        auto it = std::lower_bound(by_root.begin(), by_root.end(), std::make_pair(r, INT_MIN));
+        if (it == by_root.end() || it->first != r) throw std::invalid_argument("cluster_union: border cell of an unknown piece");
+        return it->second;
+    };
+    std::vector<int> parent((size_t)n_pieces);
+    std::iota(parent.begin(), parent.end(), 0);
+    auto find = [&](int x) {
+        while (parent[x] != x) { parent[x] = parent[parent[x]]; x = parent[x]; }
+        return x;
+    };
+    auto unite = [&](int a, int b) {   // the piece with the smaller first cell stays the representative
+        a = find(a); b = find(b);
+        if (a == b) return;
+        if (piece_root[a] < piece_root[b]) parent[b] = a;
+        else parent[a] = b;
+    };
+    std::unordered_map<int, int> cell_piece;
+    cell_piece.reserve((size_t)n_border * 2 + 16);
+    for (int i = 0; i < n_border; ++i) cell_piece.emplace(bcell[i], piece_of_root(broot[i]));
+    // each adjacent pair once, from its smaller cell: E, SW, S, SE
+    const int dxs[4] = {1, -1, 0, 1}, dys[4] = {0, 1, 1, 1};
+    for (const auto &kv : cell_piece) {
+        const int p = kv.first, y = p / W, x = p - y * W;
+        for (int k = 0; k < 4; ++k) {
+            const int nx = x + dxs[k], ny = y + dys[k];
+            if (nx < 0 || nx >= W || ny >= H) continue;
+            auto it = cell_piece.find(ny * W + nx);
+            if (it != cell_piece.end()) unite(kv.second, it->second);
+        }
+    }
+    // clusters in raster order of their first cell
+    std::vector<int> reps;
+    for (int i = 0; i < n_pieces; ++i)
+        if (find(i) == i) reps.push_back(i);
+    std::sort(reps.begin(), reps.end(), [&](int a, int b) { return piece_root[a] < piece_root[b]; });
+    std::vector<int> id((size_t)n_pieces, -1);
+    for (size_t k = 0; k < reps.size(); ++k) id[reps[k]] = (int)k;
+    for (int i = 0; i < n_pieces; ++i) piece_cluster[i] = id[find(i)];
+    return (int)reps.size();
+}
+
+// convertClustersToTreeRows (seed_gen:1329-1406) over the records in cluster order: the row arrays and
+// each row's virtual-seed slots; then cluster_info (publishClusterInfo :1515-1565) and rows_info
+// (:2546-2582), std::sort on the host with the reference comparators (same libstdc++ algorithm => same
+// order on ties).
+void assemble_rows(const std::vector<ClusterRec> &rec, SeedStageOut &out, std::vector<RowDev> &rows) {
+    rows.clear();
+    int slot = 0;
+    for (const auto &r : rec) {
+        if (!(r.flags & 1)) continue;
+        out.row_center.push_back(r.center.x); out.row_center.push_back(r.center.y);
+        out.row_start.push_back(r.start.x); out.row_start.push_back(r.start.y);
+        out.row_end.push_back(r.end.x); out.row_end.push_back(r.end.y);
+        out.row_length.push_back((double)r.length);
+        RowDev d{r.start.x, r.start.y, r.end.x, r.end.y, 0, slot};
+        double dx = r.end.x - r.start.x, dy = r.end.y - r.start.y;
+        double dist = std::sqrt(dx * dx + dy * dy);
+        if (!(dist < 1.0) && !(std::sqrt(dx * dx + dy * dy) < 1e-6)) d.k = static_cast<int>(std::floor(dist / 1.0));
+        slot += 3 * d.k;
+        rows.push_back(d);
+    }
+    const size_t n_rows = rows.size();
+    struct CI { size_t index; float cx, cy; };
+    std::vector<CI> infos;
+    for (size_t i = 0; i < n_rows; ++i)
+        infos.push_back({i, (float)out.row_center[2 * i], (float)out.row_center[2 * i + 1]});
+    std::sort(infos.begin(), infos.end(), [](const CI &a, const CI &b) { return a.cy < b.cy; });
+    for (const auto &ci : infos) { out.cluster_info.push_back(ci.cx); out.cluster_info.push_back(ci.cy); }
+    struct TR { double cx, cy, sx, sy, ex, ey; };
+    std::vector<TR> tr;
+    for (size_t i = 0; i < n_rows; ++i)
+        tr.push_back({out.row_center[2 * i], out.row_center[2 * i + 1], out.row_start[2 * i], out.row_start[2 * i + 1],
+                      out.row_end[2 * i], out.row_end[2 * i + 1]});
+    std::sort(tr.begin(), tr.end(), [](const TR &a, const TR &b) {
+        if (std::abs(a.cy - b.cy) < 1e-6) return a.cx < b.cx;
+        return a.cy < b.cy;
+    });
+    for (const auto &t : tr) { out.rows_info.insert(out.rows_info.end(), {t.sx, t.sy, t.ex, t.ey}); }
+}
+
+}  // namespace aos

@@ -111,10 +111,14 @@ struct GridC;
 // k_cluster_stats over clusters given as runs of raster-ordered cells (off[n_clusters + 1], cells)
 void launch_cluster_stats(const int *off, const int *cells, int n_clusters, const GridC &g, const double *poly, int np,
                           float min_length, ClusterRec *rec, hipStream_t s);
-// exact FIFO-BFS replays (host, parallel over clusters); cells of a job in raster order, n of them
+// exact FIFO-BFS replays (host, parallel over clusters; cluster_host.cpp); cells of a job in any order (the BFS
+// starts from the smallest), n of them
 struct ReplayJob { int c; const int *cells; int n; };
 void replay_clusters(const std::vector<ReplayJob> &jobs, const GridC &g, const double *poly, int np, float min_len,
                      ClusterRec *rec);
+
+// a tree row as the seed kernels take it: start / end (world), k base seeds, first virtual-seed slot
+struct RowDev { double sx, sy, ex, ey; int k; int slot0; };
 
 struct SeedStageOut {
     int n_clusters_all = 0;
@@ -128,6 +132,8 @@ struct SeedStageOut {
 
 void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStageOut &out, hipStream_t stream,
                             hipEvent_t ev_mid);
+// the row arrays, the rows' seed slots and the sorted cluster_info / rows_info (host; cluster_host.cpp)
+void assemble_rows(const std::vector<ClusterRec> &rec, SeedStageOut &out, std::vector<RowDev> &rows);
 
 // ------------------------------------------------------------------ distributed a8-a10 (cluster_dist.hip)
 struct ClusterDistState {

@@ -14,22 +14,18 @@
 // with a uniform hash and decides the set in rounds (a candidate is kept once every earlier
 // conflicting candidate is removed, removed once one of them is kept).
 #include <algorithm>
-#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <exception>
-#include <mutex>
 #include <stdexcept>
-#include <thread>
 
 #include "cluster_dev.h"
 #include "cluster_seed.h"
-#include "dev_prims.h"
+#include "dev_prims_device.h"
 
 namespace aos {
 
 static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
-constexpr int kReplayThreads = 8;   // host threads for the exact BFS replays of one frame
 
 // ------------------------------------------------------------------ foreground = skeleton inside polygon
 __global__ void k_fg(const uint64_t *skel, uint64_t *fg, int *cnt, GridC g, const double *poly, int np) {
@@ -319,119 +315,6 @@ __global__ __launch_bounds__(256) void k_cluster_stats(StatArgs A) {
     if (threadIdx.x == 0) A.rec[cid] = r;
 }
 
-// ------------------------------------------------------------------ exact BFS replay (host)
-// clusterOccupiedCells' FIFO BFS (seed_gen:1007-1049) and the order-dependent statistics that follow
-// (float centre sums :1030-1046, first-strict-maximum endpoints :1354-1395) for the rare clusters
-// without the order-free certificate. This is a serial chain of dependent steps: it runs on the host
-// core next to the GPU (the cluster's cells come over in raster order), ~10 ns per step.
-static void host_bfs_replay(const int *cells, int n, const GridC &g, const double *poly, int np, float min_length,
-                            ClusterRec &r, std::vector<int> &q, std::vector<int> &tab) {
-    int cap = 64;
-    while (cap < 2 * n) cap <<= 1;
-    const unsigned mask = (unsigned)cap - 1;
-    tab.assign(cap, -1);
-    auto slot_of = [&](int key) -> int {   // key present -> its slot, else -1
-        unsigned h = ((unsigned)key * 2654435761u) & mask;
-        for (;;) {
-            int v = tab[h];
-            if (v == -1) return -1;
-            if ((v & 0x7fffffff) == key) return (int)h;
-            h = (h + 1) & mask;
-        }
-    };
-    for (int k = 0; k < n; ++k) {
-        unsigned h = ((unsigned)cells[k] * 2654435761u) & mask;
-        while (tab[h] != -1) h = (h + 1) & mask;
-        tab[h] = cells[k];
-    }
-    q.resize(n);
-    int start = cells[0];   // first raster cell of the component (the cells come in any order)
-    for (int k = 1; k < n; ++k) start = std::min(start, cells[k]);
-    tab[slot_of(start)] |= (int)0x80000000;
-    q[0] = start;
-    int head = 0, tail = 1;
-    const int dxs[8] = {-1, -1, -1, 0, 0, 1, 1, 1}, dys[8] = {-1, 0, 1, -1, 1, -1, 0, 1};
-    while (head < tail) {
-        const int p = q[head++], cy = p / g.W, cx = p - cy * g.W;
-        for (int i = 0; i < 8; ++i) {
-            const int nx = cx + dxs[i], ny = cy + dys[i];
-            if (nx < 0 || nx >= g.W || ny < 0 || ny >= g.H) continue;
-            const int h = slot_of(ny * g.W + nx);
-            if (h < 0 || tab[h] < 0) continue;
-            tab[h] |= (int)0x80000000;
-            q[tail++] = ny * g.W + nx;
-        }
-    }
-    if (tail != n) throw std::runtime_error("BFS replay: cluster is not 8-connected");
-    float sum_x = 0.0f, sum_y = 0.0f;
-    for (int k = 0; k < n; ++k) { int p = q[k], y = p / g.W; sum_x += (float)(p - y * g.W); sum_y += (float)y; }
-    r.cx = sum_x / (float)n;
-    r.cy = sum_y / (float)n;
-    bool row = false;
-    if (r.length >= min_length) {
-        float cwx = (float)(g.ox + (double)(r.cx * g.res)), cwy = (float)(g.oy + (double)(r.cy * g.res));
-        r.center = make_double2(cwx, cwy);
-        row = d_pip(cwx, cwy, poly, np);
-    }
-    if (row) {
-        double mx = 0.0; int fi = 0; double fx = 0, fy = 0;
-        for (int k = 0; k < n; ++k) {
-            double2 w = cell_w(g, q[k]);
-            double dx = w.x - r.center.x, dy = w.y - r.center.y, d2 = dx * dx + dy * dy;
-            if (d2 > mx) { mx = d2; fi = k; double s = std::sqrt(d2); fx = dx / s; fy = dy / s; }
-        }
-        double mo = 0.0; int si = 0;
-        for (int k = 0; k < n; ++k) {
-            if (k == fi) continue;
-            double2 w = cell_w(g, q[k]);
-            double dx = w.x - r.center.x, dy = w.y - r.center.y, d2 = dx * dx + dy * dy;
-            double nx = dx, ny = dy;
-            if (d2 > 0.0) { double s = std::sqrt(d2); nx = dx / s; ny = dy / s; }
-            if (nx * fx + ny * fy < 0.0 && d2 > mo) { mo = d2; si = k; }
-        }
-        if (mo == 0.0) {
-            double2 wf = cell_w(g, q[fi]);
-            for (int k = 0; k < n; ++k) {
-                if (k == fi) continue;
-                double2 w = cell_w(g, q[k]);
-                double dx = w.x - wf.x, dy = w.y - wf.y, d2 = dx * dx + dy * dy;
-                if (d2 > mo) { mo = d2; si = k; }
-            }
-        }
-        r.start = cell_w(g, q[fi]);
-        r.end = cell_w(g, q[si]);
-    }
-    r.flags = (row ? 1 : 0) | 4;  // 4: replayed
-}
-
-// The exact replays of a frame, in parallel over clusters on up to kReplayThreads host threads (each
-// writes only its own record).
-void replay_clusters(const std::vector<ReplayJob> &jobs, const GridC &g, const double *poly, int np, float min_len,
-                     ClusterRec *rec) {
-    if (jobs.empty()) return;
-    std::atomic<int> next{0};
-    std::exception_ptr err;
-    std::mutex mu;
-    auto work = [&]() {
-        std::vector<int> q, tab;
-        for (int i; (i = next.fetch_add(1)) < (int)jobs.size();) {
-            const ReplayJob &j = jobs[i];
-            try {
-                host_bfs_replay(j.cells, j.n, g, poly, np, min_len, rec[j.c], q, tab);
-            } catch (...) {
-                std::lock_guard<std::mutex> lk(mu);
-                if (!err) err = std::current_exception();
-            }
-        }
-    };
-    const int nt = std::min<int>((int)jobs.size(), kReplayThreads);
-    std::vector<std::thread> th;
-    for (int t = 1; t < nt; ++t) th.emplace_back(work);
-    work();
-    for (auto &t : th) t.join();
-    if (err) std::rethrow_exception(err);
-}
-
 void launch_cluster_stats(const int *off, const int *cells, int n_clusters, const GridC &g, const double *poly, int np,
                           float min_length, ClusterRec *rec, hipStream_t s) {
     if (n_clusters <= 0) return;
@@ -441,7 +324,6 @@ void launch_cluster_stats(const int *off, const int *cells, int n_clusters, cons
 }
 
 // ------------------------------------------------------------------ rays
-struct RowDev { double sx, sy, ex, ey; int k; int slot0; };
 
 // raycastToOccupiedCell seed_gen:1730-1771 on the frameless skeleton
 // Marching loops are latency chains of dependent skeleton lookups; the sample positions are not
@@ -688,46 +570,11 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
             replay_clusters(jobs, g, hp.data(), np, static_cast<float>(in.cluster_min_length), S.h_rec.data());
         }
     }
-    {   // ---- tree rows in cluster order (convertClustersToTreeRows, seed_gen:1329-1406)
-        int slot = 0;
-        for (const auto &r : S.h_rec) {
-            if (!(r.flags & 1)) continue;
-            out.row_center.push_back(r.center.x); out.row_center.push_back(r.center.y);
-            out.row_start.push_back(r.start.x); out.row_start.push_back(r.start.y);
-            out.row_end.push_back(r.end.x); out.row_end.push_back(r.end.y);
-            out.row_length.push_back((double)r.length);
-            RowDev d{r.start.x, r.start.y, r.end.x, r.end.y, 0, slot};
-            double dx = r.end.x - r.start.x, dy = r.end.y - r.start.y;
-            double dist = std::sqrt(dx * dx + dy * dy);
-            if (!(dist < 1.0) && !(std::sqrt(dx * dx + dy * dy) < 1e-6)) d.k = static_cast<int>(std::floor(dist / 1.0));
-            slot += 3 * d.k;
-            rows.push_back(d);
-        }
-    }
+    assemble_rows(S.h_rec, out, rows);   // (host: cluster_host.cpp)
     out.n_clusters_all = S.n_clusters;
     S.n_rows = (int)rows.size();
     if (ev_mid) AOS_HIP(hipEventRecord(ev_mid, s));
 
-    // cluster_info (publishClusterInfo :1515-1565) and rows_info (:2546-2582): std::sort on the
-    // host with the reference comparators (same libstdc++ algorithm => same order on ties).
-    {
-        struct CI { size_t index; float cx, cy; };
-        std::vector<CI> infos;
-        for (size_t i = 0; i < S.n_rows; ++i)
-            infos.push_back({i, (float)out.row_center[2 * i], (float)out.row_center[2 * i + 1]});
-        std::sort(infos.begin(), infos.end(), [](const CI &a, const CI &b) { return a.cy < b.cy; });
-        for (const auto &ci : infos) { out.cluster_info.push_back(ci.cx); out.cluster_info.push_back(ci.cy); }
-        struct TR { double cx, cy, sx, sy, ex, ey; };
-        std::vector<TR> tr;
-        for (int i = 0; i < S.n_rows; ++i)
-            tr.push_back({out.row_center[2 * i], out.row_center[2 * i + 1], out.row_start[2 * i], out.row_start[2 * i + 1],
-                          out.row_end[2 * i], out.row_end[2 * i + 1]});
-        std::sort(tr.begin(), tr.end(), [](const TR &a, const TR &b) {
-            if (std::abs(a.cy - b.cy) < 1e-6) return a.cx < b.cx;
-            return a.cy < b.cy;
-        });
-        for (const auto &t : tr) { out.rows_info.insert(out.rows_info.end(), {t.sx, t.sy, t.ex, t.ey}); }
-    }
     if (rows.empty()) return;
 
     // ---- seeds: virtual seeds (a11), endpoint-ray seeds (a12) and endpoint seeds (:1451-1496), each a

@@ -1,0 +1,120 @@
+// Device-side helpers of dev_prims.h (hash cells, cell-index rows, look-back): included by the .hip files
+// only (dev_prims.h stays host-compilable for the sanitizer build). Not part of the ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "dev_prims.h"
+
+namespace aos {
+
+__device__ __forceinline__ void hash_cell(const HashG &h, double x, double y, int &cx, int &cy) {
+    const double fx = (x - h.x0) * h.inv, fy = (y - h.y0) * h.inv;
+    cx = !(fx > 0.0) ? 0 : (fx >= (double)(h.nx - 1) ? h.nx - 1 : (int)fx);
+    cy = !(fy > 0.0) ? 0 : (fy >= (double)(h.ny - 1) ? h.ny - 1 : (int)fy);
+}
+
+// the run of the 3 buckets (cx - 1 .. cx + 1) of row yy (clamped): [k0, k1)
+__device__ __forceinline__ void ci_row(const CellIdx &c, int yy, int cx, int &k0, int &k1) {
+    const int b = yy * c.h.nx;
+    k0 = c.start[b + max(cx - 1, 0)];
+    k1 = c.start[b + min(cx + 1, c.h.nx - 1) + 1];
+}
+
+__device__ __forceinline__ unsigned long long ld_u64(const unsigned long long *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_u64(unsigned long long *p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int ld_i32(const int *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void st_i32(int *p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// The block's id in launch order: a block only ever waits for blocks with smaller ids, which have all
+// started (they drew their ids first), so the waits cannot deadlock whatever the dispatch order.
+__device__ __forceinline__ int lb_block_id(const LookBack &L, int *sh) {
+    if (threadIdx.x == 0) {
+        const unsigned v = atomicAdd(L.ticket, 1u);
+        if (v == gridDim.x - 1) __hip_atomic_store(L.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v >= gridDim.x) atomicOr(L.err, 1);
+        *sh = (int)(v % gridDim.x);
+    }
+    __syncthreads();
+    return *sh;
+}
+
+__device__ __forceinline__ unsigned wave_sum_u32(unsigned v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// Wave 0 of block vid (all 64 lanes): publishes the block's aggregate, walks back over the
+// predecessors' words 64 at a time, publishes the inclusive prefix; returns the exclusive prefix.
+__device__ inline unsigned lb_exclusive(const LookBack &L, int vid, unsigned agg) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long tagA = (unsigned long long)((L.epoch << 2) | 1u) << 32;
+    const unsigned long long tagP = (unsigned long long)((L.epoch << 2) | 2u) << 32;
+    if (vid == 0) {
+        if (lane == 0) st_u64(&L.part[0], tagP | agg);
+        return 0;
+    }
+    if (lane == 0) st_u64(&L.part[vid], tagA | agg);
+    unsigned excl = 0;
+    int base = vid - 1;
+    unsigned spins = 0;
+    for (;;) {
+        const int j = base - lane;
+        unsigned flag = 2, val = 0;
+        for (;;) {
+            if (j >= 0) {
+                const unsigned long long w = ld_u64(&L.part[j]);
+                const unsigned tag = (unsigned)(w >> 32);
+                flag = (tag >> 2) == L.epoch ? (tag & 3u) : 0u;
+                val = (unsigned)w;
+            }
+            if (__all(flag != 0)) break;
+            if (++spins > kSpinCap) {
+                if (lane == 0) atomicOr(L.err, 1);
+                flag = 2;
+                val = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        const unsigned long long pm = __ballot(flag == 2);
+        if (pm) {
+            const int k = __ffsll((long long)pm) - 1;
+            excl += wave_sum_u32(lane <= k ? val : 0u);
+            break;
+        }
+        excl += wave_sum_u32(val);
+        base -= 64;
+    }
+    if (lane == 0) st_u64(&L.part[vid], tagP | (unsigned long long)(excl + agg));
+    return excl;
+}
+
+// Exclusive scan of one value per thread over a block of NT threads (NT a multiple of 64); total -> *tot
+template <int NT>
+__device__ __forceinline__ int block_excl_scan(int v, int *wsum, int *tot) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(incl, o);
+        if (lane >= o) incl += t;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    int before = 0, all = 0;
+#pragma unroll
+    for (int k = 0; k < NT / 64; ++k) {
+        const int s = wsum[k];
+        before += k < w ? s : 0;
+        all += s;
+    }
+    *tot = all;
+    __syncthreads();
+    return before + incl - v;
+}
+
+}  // namespace aos

@@ -23,7 +23,7 @@
 #include <stdexcept>
 
 #include "cluster_seed.h"
-#include "dev_prims.h"
+#include "dev_prims_device.h"
 
 namespace aos {
 

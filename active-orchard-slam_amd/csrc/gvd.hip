@@ -20,6 +20,7 @@
 #include <thread>
 
 #include "aos_ctx.h"
+#include "dev_prims_device.h"
 #include "subdiv2d.h"
 
 namespace aos {
