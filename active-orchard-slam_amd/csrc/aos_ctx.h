@@ -61,10 +61,10 @@ struct aos_ctx {
     uint64_t map_scan_begin = 0;     // map points before the last aos_map_append
 
     // ---- device buffers
-    aos::DevBuf cloud_copy, bin_count, bin_start, pt_binslot, sorted, ror_scratch, ror_bigbins, scan_tmp, counters;
+    aos::DevBuf cloud_copy, bin_count, bin_start, sorted, ror_scratch, ror_bigbins, scan_tmp, counters;
     aos::DevBuf raster_bits, infl_bits, open_bits, thin_a, thin_b, thin_act, occ_bytes, skel_bytes, flags;
     aos::DevBuf thin_out;   // the converged skeleton bits, picked on the device (launch_thin_pick)
-    aos::LookBackScratch ror_lb;           // single-pass scans of the ROR stage (tile starts)
+    aos::LookBackScratch ror_lb;           // look-back words of the ROR column scan (k_rt_colscan)
     aos::DevBuf full_infl, full_skel;      // tiled frames: the whole map, assembled on the root rank
     aos::PinnedBuf h_small, h_stats;
     // Host -> device upload of a large pageable buffer (a PointCloud2 message): kUpThreads host
@@ -193,6 +193,7 @@ struct aos_ctx {
     void ror_stage(const aos::FrameGeom &g, const RorOwn &o, uint64_t *rbits, bool allow_guess);
     bool ror_collect();   // after the stream synchronised: true if the ROR scatter overflowed
     void ror_stage_append(aos::RorLaunch L, uint64_t *rbits);   // streaming map: one scan on the tile store
+    aos::LookBack ror_lookback(const aos::RorLaunch &L, int G, unsigned long long *d_own);
     void ror_stage_unchanged();   // streaming map: no new points since the committed store
     uint64_t ror_skipped = 0;     // frames that skipped the ROR stage that way
     void finish_frame(const aos::FrameGeom &g, bool want_host, const uint64_t *clipped_total, aos_seedgen_out &out,

@@ -121,10 +121,15 @@ struct RorLaunch {
 constexpr int kRtMaxTiles = 36000;   // tiles per frame (LDS histogram of the partition passes: 144 KB)
 void rt_configure(RorLaunch &L, int Hr, int WWr, double est_binned, int force_tb = 0);
 int rt_part_blocks(const RorLaunch &L);   // G: workgroups (= cloud chunks) of the partition passes
-// H: G x ntiles ints (row per workgroup). The count pass leaves per-tile prefixes over the workgroups
-// in H and the tile totals in tot[0..ntiles); tstart = exclusive scan of tot (ntiles + 1 entries).
-size_t rt_colpart_ints(const RorLaunch &L, int G);   // scratch of the column scan (part)
-void launch_rt_count(const RorLaunch &L, int *H, int G, int *part, int *tot, unsigned long long *n_own, hipStream_t s);
+// H: rt_h_ints ints, G x ntiles (row per workgroup) + G per-workgroup binned counts. The count pass (two
+// launches: count, k_rt_colscan) leaves per-tile prefixes over the workgroups in H, the tile starts in ts
+// (ntiles + 1 entries, ts[ntiles] = staged total) and the binned count in *n_own; lb: a look-back of
+// rt_colscan_words words whose err word gets bit 4 on a stuck wait.
+struct LookBack;
+size_t rt_h_ints(const RorLaunch &L, int G);
+int rt_colscan_words(const RorLaunch &L, int G);
+void launch_rt_count(const RorLaunch &L, int *H, int G, int *ts, unsigned long long *n_own, const LookBack &lb,
+                     hipStream_t s);
 void launch_rt_scatter(const RorLaunch &L, int *H, const int *tstart, int G, float4 *staged, hipStream_t s);
 // kept_tile (nullable): per-tile kept counts; dirty (nullable): a tile is counted iff dirty[t+1] > dirty[t]
 // scratch: staged-sized; bigbins: rt_bigbins_ints(L) ints (tiles beyond the LDS capacity are sorted there)
@@ -138,6 +143,8 @@ void launch_rt_ror(const RorLaunch &L, const int *tstart, float4 *staged, float4
 void launch_rt_merge(const float4 *old_st, const int *old_ts, const float4 *scan_st, const int *scan_ts, float4 *new_st,
                      int *new_ts, int ntiles, int cap, int *overflow, hipStream_t s);
 void launch_rt_sum_kept(const int *kept_tile, int ntiles, unsigned long long *counters, hipStream_t s);
+// reads n staged records (brings their lines into the Infinity Cache before the scatter writes them)
+void launch_rt_touch(const float4 *p, size_t n, hipStream_t s);
 // PointCloud2 records (any float32 x/y/z offsets) -> float4 (x, y, z, 0)
 void launch_pack_xyz(const uint8_t *cloud, uint64_t n, uint32_t step, uint32_t ox, uint32_t oy, uint32_t oz, float4 *out,
                      hipStream_t s);

@@ -85,6 +85,7 @@ struct ClusterSeedState {
     DevBuf cand_xy, cand_ok, cand_state, hash_count, hash_start, hash_slot, hash_sorted, seed_out, misc, scan_tmp;
     LookBackScratch lb;           // the stage's single-pass scans
     bool cl_count_dirty = true;   // cl_count (cluster sizes) not known to be zero
+    PinnedBuf h_cells;   // the replayed clusters' cells (one DMA; round 3's zeroed pageable vector cost ~1.5 ms at C3)
     PinnedBuf h_misc;
     int n_fg = 0, n_clusters = 0, n_rows = 0, n_cur_tab = 0;
     double cur_tab_amax = -1.0;

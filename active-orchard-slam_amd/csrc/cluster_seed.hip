@@ -562,11 +562,11 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
             for (int c = 0; c < ncl; ++c)
                 if (S.h_rec[c].flags & 2) ids.push_back(c);
             const long long lo = off[ids.front()], hi = off[ids.back() + 1];
-            std::vector<int> hc((size_t)(hi - lo));
-            AOS_HIP(hipMemcpyAsync(hc.data(), d_cells + lo, sizeof(int) * (hi - lo), hipMemcpyDeviceToHost, s));
+            int *hc = static_cast<int *>(S.h_cells.ensure(sizeof(int) * (size_t)(hi - lo)));
+            AOS_HIP(hipMemcpyAsync(hc, d_cells + lo, sizeof(int) * (hi - lo), hipMemcpyDeviceToHost, s));
             S.dedup.sev.sync(s);
             std::vector<ReplayJob> jobs;
-            for (int c : ids) jobs.push_back({c, hc.data() + (off[c] - lo), S.h_rec[c].n});
+            for (int c : ids) jobs.push_back({c, hc + (off[c] - lo), S.h_rec[c].n});
             replay_clusters(jobs, g, hp.data(), np, static_cast<float>(in.cluster_min_length), S.h_rec.data());
         }
     }

@@ -48,8 +48,9 @@ __device__ __forceinline__ unsigned wave_sum_u32(unsigned v) {
 }
 
 // Wave 0 of block vid (all 64 lanes): publishes the block's aggregate, walks back over the
-// predecessors' words 64 at a time, publishes the inclusive prefix; returns the exclusive prefix.
-__device__ inline unsigned lb_exclusive(const LookBack &L, int vid, unsigned agg) {
+// predecessors' words 64 at a time, publishes the inclusive prefix; returns the exclusive prefix. A wait
+// past kSpinCap ORs errbit into *L.err.
+__device__ inline unsigned lb_exclusive(const LookBack &L, int vid, unsigned agg, int errbit = 1) {
     const int lane = threadIdx.x & 63;
     const unsigned long long tagA = (unsigned long long)((L.epoch << 2) | 1u) << 32;
     const unsigned long long tagP = (unsigned long long)((L.epoch << 2) | 2u) << 32;
@@ -73,7 +74,7 @@ __device__ inline unsigned lb_exclusive(const LookBack &L, int vid, unsigned agg
             }
             if (__all(flag != 0)) break;
             if (++spins > kSpinCap) {
-                if (lane == 0) atomicOr(L.err, 1);
+                if (lane == 0) atomicOr(L.err, errbit);
                 flag = 2;
                 val = 0;
                 break;

@@ -36,6 +36,7 @@
 #include <type_traits>
 
 #include "aos_internal.h"
+#include "dev_prims_device.h"
 
 namespace aos {
 
@@ -125,8 +126,14 @@ __device__ __forceinline__ bool rt_in(const RorLaunch &L, float4 p, float4 q) {
 #ifndef AOS_RT_G
 #define AOS_RT_G 512
 #endif
-#ifndef AOS_RT_COUNT_EXP
-#define AOS_RT_COUNT_EXP 0
+#ifndef AOS_RT_SCAT   // scatter pass walk: 2 = batched first-tile claims (experiment)
+#define AOS_RT_SCAT 0
+#endif
+#ifndef AOS_RT_COLROWS   // rows of H per k_rt_colscan block
+#define AOS_RT_COLROWS 32
+#endif
+#ifndef AOS_RT_NT   // nontemporal cloud loads: bit 0 count pass, bit 1 scatter pass
+#define AOS_RT_NT 0
 #endif
 constexpr int kRtCountPer = AOS_RT_CPER, kRtScatterPer = AOS_RT_SPER, kRtCountTB = AOS_RT_CTB, kRtScatterTB = 512;
 constexpr int kRtChunkQ = 4096;   // chunk granularity (points): a multiple of both passes' sub-chunks
@@ -145,7 +152,7 @@ __device__ __forceinline__ int rt_xcd_block(int b, int n) {
 
 template <bool SCATTER, int LAY, int kRtTB, int kRtPer>
 __global__ __launch_bounds__(kRtTB) void k_rt_part(RorLaunch L, int *H, const int *tstart, uint64_t chunk,
-                                                   float4 *staged, unsigned long long *n_own) {
+                                                   float4 *staged, unsigned *own_out) {
     constexpr int kRtSub = kRtTB * kRtPer;
     extern __shared__ int hist[];        // [ntiles]: counts (count pass) / cursors (scatter pass)
     // chunk w: the chunks of one XCD are contiguous, so the scatter runs of chunks w and w + 1 (adjacent in
@@ -164,7 +171,11 @@ __global__ __launch_bounds__(kRtTB) void k_rt_part(RorLaunch L, int *H, const in
     using Rec = typename std::conditional<LAY == 1, float4, float3>::type;
     auto ld = [&](unsigned i, Rec &o) {
         const uint8_t *rec = cbase + i * (unsigned)(LAY == 1 ? 16 : LAY == 2 ? 12 : L.step);
-        if (LAY == 0) {
+        if (LAY != 0 && (AOS_RT_NT & (SCATTER ? 2 : 1))) {
+            typedef float vrec __attribute__((ext_vector_type(LAY == 1 ? 4 : 3)));
+            const vrec v = __builtin_nontemporal_load(reinterpret_cast<const vrec *>(rec));
+            o.x = v.x; o.y = v.y; o.z = v.z;
+        } else if (LAY == 0) {
             o.x = *reinterpret_cast<const float *>(rec + L.ox);
             o.y = *reinterpret_cast<const float *>(rec + L.oy);
             o.z = *reinterpret_cast<const float *>(rec + L.oz);
@@ -184,32 +195,98 @@ __global__ __launch_bounds__(kRtTB) void k_rt_part(RorLaunch L, int *H, const in
         }
     };
     auto walk = [&](const Rec (&pt)[kRtPer], unsigned base) {
+#if AOS_RT_SCAT == 2
+        if (SCATTER) {
+            // batched: every point's first-tile claim in flight at once (LDS atomics with return; + 0 from a
+            // point that is not binned), then the stores, then the halo copies behind one branch
+            int pos[kRtPer], t00[kRtPer], oti[kRtPer];
+            unsigned halo = 0, okm = 0;
+#pragma unroll
+            for (int j = 0; j < kRtPer; ++j) {
+                const float x = pt[j].x, y = pt[j].y, z = pt[j].z;
+                const bool ok = base + (unsigned)(j * kRtTB + tid) < cnt && rt_binned(L, x, y, z);
+                int bx, by, tx0, tx1, ty0, ty1;
+                rt_bin(L, ok ? x : L.bminx, ok ? y : L.bminy, bx, by);
+                rt_tiles(L, bx, by, tx0, tx1, ty0, ty1);
+                t00[j] = ty0 * L.ntx + tx0;
+                oti[j] = (by >> L.TBs) * L.ntx + (bx >> L.TBs);
+                halo |= (ok ? ((tx1 > tx0 ? 1u : 0u) | (ty1 > ty0 ? 2u : 0u)) : 0u) << (2 * j);
+                okm |= (ok ? 1u : 0u) << j;
+                pos[j] = atomicAdd(&hist[t00[j]], ok ? 1 : 0);
+            }
+            own += __builtin_popcount(okm);
+#pragma unroll
+            for (int j = 0; j < kRtPer; ++j) {
+                if (!((okm >> j) & 1u)) continue;
+                const float x = pt[j].x, y = pt[j].y, z = pt[j].z;
+                const float w = __int_as_float(t00[j] == oti[j] && rt_candidate(L, x, y, z) ? 1 : 0);
+                if (pos[j] < L.staged_cap) staged[pos[j]] = make_float4(x, y, z, w);
+                else *L.overflow = 1;
+            }
+            if (halo) {
+#pragma unroll
+                for (int j = 0; j < kRtPer; ++j) {
+                    const unsigned h = (halo >> (2 * j)) & 3u;
+                    if (!h) continue;
+                    const float x = pt[j].x, y = pt[j].y, z = pt[j].z;
+                    const bool cand = rt_candidate(L, x, y, z);
+                    auto put = [&](int t) {
+                        const float4 v = make_float4(x, y, z, __int_as_float(t == oti[j] && cand ? 1 : 0));
+                        const int p2 = atomicAdd(&hist[t], 1);
+                        if (p2 < L.staged_cap) staged[p2] = v;
+                        else *L.overflow = 1;
+                    };
+                    if (h & 1u) put(t00[j] + 1);
+                    if (h & 2u) put(t00[j] + L.ntx);
+                    if (h == 3u) put(t00[j] + L.ntx + 1);
+                }
+            }
+            return;
+        }
+#endif
 #pragma unroll
         for (int j = 0; j < kRtPer; ++j) {
             const float x = pt[j].x, y = pt[j].y, z = pt[j].z;
+            if (!SCATTER) {
+                // count: branch-free except for the halo tiles. The first tile of the point's (1 or 2) x (1 or
+                // 2) tiles gets + ok (+ 0 from a point that is past the chunk or not binned: its bins are the
+                // box corner's); round 3's nested tile loops spent ~18 us of the pass on branches
+                const bool ok = base + (unsigned)(j * kRtTB + tid) < cnt && rt_binned(L, x, y, z);
+                own += ok ? 1u : 0u;
+                int bx, by, tx0, tx1, ty0, ty1;
+                rt_bin(L, ok ? x : L.bminx, ok ? y : L.bminy, bx, by);
+                rt_tiles(L, bx, by, tx0, tx1, ty0, ty1);
+                const int t00 = ty0 * L.ntx + tx0;
+                const bool hx = tx1 > tx0, hy = ty1 > ty0;
+                atomicAdd(&hist[t00], ok ? 1 : 0);
+                if (ok && (hx || hy)) {
+                    if (hx) atomicAdd(&hist[t00 + 1], 1);
+                    if (hy) atomicAdd(&hist[t00 + L.ntx], 1);
+                    if (hx && hy) atomicAdd(&hist[t00 + L.ntx + 1], 1);
+                }
+                continue;
+            }
             if (base + (unsigned)(j * kRtTB + tid) >= cnt || !rt_binned(L, x, y, z)) continue;
-            ++own;
-#if AOS_RT_COUNT_EXP == 2   // (timing experiment: 2 = loads and the bounds test only)
-            if (!SCATTER) continue;
-#endif
             int bx, by, tx0, tx1, ty0, ty1;
             rt_bin(L, x, y, bx, by);
             rt_tiles(L, bx, by, tx0, tx1, ty0, ty1);
             const int otile = (by >> L.TBs) * L.ntx + (bx >> L.TBs);
-            const float4 q = make_float4(x, y, z, __int_as_float(SCATTER && rt_candidate(L, x, y, z) ? 1 : 0));
+            const float4 q = make_float4(x, y, z, __int_as_float(rt_candidate(L, x, y, z) ? 1 : 0));
             for (int ty = ty0; ty <= ty1; ++ty)
                 for (int tx = tx0; tx <= tx1; ++tx) {
                     const int t = ty * L.ntx + tx;
-                    if (SCATTER) {
-                        float4 v = q;
-                        if (t != otile) v.w = __int_as_float(0);   // a halo copy is never tested there
-                        const int pos = atomicAdd(&hist[t], 1);
-                        if (pos < L.staged_cap) staged[pos] = v;    // else: overflow, the frame is redone
-                        else *L.overflow = 1;
+                    float4 v = q;
+                    if (t != otile) v.w = __int_as_float(0);   // a halo copy is never tested there
+                    const int pos = atomicAdd(&hist[t], 1);
+                    if (pos < L.staged_cap) {                   // else: overflow, the frame is redone
+                        if (AOS_RT_NT & 4) {
+                            typedef float v4f __attribute__((ext_vector_type(4)));
+                            __builtin_nontemporal_store(v4f{v.x, v.y, v.z, v.w}, reinterpret_cast<v4f *>(staged + pos));
+                        } else {
+                            staged[pos] = v;
+                        }
                     } else {
-#if AOS_RT_COUNT_EXP != 1   // (timing experiment: 1 = no LDS histogram)
-                        atomicAdd(&hist[t], 1);
-#endif
+                        *L.overflow = 1;
                     }
                 }
         }
@@ -226,46 +303,112 @@ __global__ __launch_bounds__(kRtTB) void k_rt_part(RorLaunch L, int *H, const in
     if (!SCATTER) {
         __syncthreads();
         for (int t = tid; t < L.ntiles; t += kRtTB) row[t] = hist[t];
+        // the workgroup's binned points: one plain store (k_rt_colscan sums them; round 3's per-wave global
+        // atomic on one counter cost the pass ~17 us, tools/rorbench)
         for (int o = 32; o > 0; o >>= 1) own += __shfl_xor(own, o);
-        if ((tid & 63) == 0 && own) atomicAdd(n_own, (unsigned long long)own);
+        __shared__ unsigned own_w[kRtTB / 64];
+        if ((tid & 63) == 0) own_w[tid >> 6] = own;
+        __syncthreads();
+        if (tid == 0) {
+            unsigned t = 0;
+            for (int k = 0; k < kRtTB / 64; ++k) t += own_w[k];
+            own_out[w] = t;
+        }
     }
 }
 
-// H rows -> per-tile exclusive prefixes over the workgroups (in place) and tile totals, in three fully
-// parallel steps over (tile, group of kColRows rows): group sums, a scan of the group sums per tile,
-// then each group rewrites its rows as running prefixes. Thread = tile, so every access is a row run.
-constexpr int kColRows = 32, kColTB = 256;
-__global__ __launch_bounds__(kColTB) void k_rt_colsum(const int *H, int *part, int ntiles, int G) {
-    const int t = blockIdx.x * kColTB + threadIdx.x, g = blockIdx.y;
-    if (t >= ntiles) return;
-    const int r1 = min(G, (g + 1) * kColRows);
-    int sum = 0;
-    for (int r = g * kColRows; r < r1; ++r) sum += H[(size_t)r * ntiles + t];
-    part[(size_t)g * ntiles + t] = sum;
-}
-__global__ __launch_bounds__(kColTB) void k_rt_colpre(int *part, int *tot, int ntiles, int ng) {
-    const int t = blockIdx.x * kColTB + threadIdx.x;
-    if (t >= ntiles) return;
-    int run = 0;
-    for (int g = 0; g < ng; ++g) {
-        const size_t i = (size_t)g * ntiles + t;
-        const int v = part[i];
-        part[i] = run;
-        run += v;
+// H rows -> per-tile exclusive prefixes over the workgroups (in place), the tile starts (exclusive sum of the
+// tile totals, ts[ntiles] = staged total) and the binned count, in ONE launch (round 3 took four: group sums,
+// group prefixes, row rewrite, tile-start scan). Block (g, b) holds rows [g kColRows, (g + 1) kColRows) of
+// tiles [b kColTB, (b + 1) kColTB) in registers (thread = tile: every access is a row run), publishes its
+// per-tile sums as look-back words, walks back over the row groups above it until a prefix word, rewrites its
+// rows as running prefixes; the last row group's blocks then hold the tile totals and chain the tile-start
+// scan over b. Blocks take ids in launch order, row-group major, so a block only waits for blocks of smaller
+// ids (started before it): no deadlock whatever the dispatch order. Words carry the launch's epoch (no init).
+constexpr int kColRows = AOS_RT_COLROWS, kColTB = 256;
+struct ColScan {
+    int *H;                  // G rows of ntiles counts -> exclusive prefixes over the rows
+    int *ts;                 // [ntiles + 1] tile starts
+    const unsigned *own;     // [G] binned points per count workgroup
+    unsigned long long *n_own;
+    int ntiles, G, ng, ntb;
+    LookBack L;              // part: ng x ntiles column words, then ntb tile-chain words; err bit 4 on a stuck wait
+};
+__global__ __launch_bounds__(kColTB) void k_rt_colscan(ColScan C) {
+    __shared__ int sh_vid, wsum[kColTB / 64], sh_tot, sh_pre;
+    __shared__ unsigned long long sh_own[kColTB / 64];
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        const unsigned v = atomicAdd(C.L.ticket, 1u);
+        if (v == gridDim.x - 1) __hip_atomic_store(C.L.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v >= gridDim.x) atomicOr(C.L.err, 4);
+        sh_vid = (int)(v % gridDim.x);
     }
-    tot[t] = run;
-}
-__global__ __launch_bounds__(kColTB) void k_rt_colfix(int *H, const int *part, int ntiles, int G) {
-    const int t = blockIdx.x * kColTB + threadIdx.x, g = blockIdx.y;
-    if (t >= ntiles) return;
-    const int r1 = min(G, (g + 1) * kColRows);
-    int run = part[(size_t)g * ntiles + t];
-    for (int r = g * kColRows; r < r1; ++r) {
-        const size_t i = (size_t)r * ntiles + t;
-        const int v = H[i];
-        H[i] = run;
-        run += v;
+    __syncthreads();
+    const int vid = sh_vid, g = vid / C.ntb, b = vid - g * C.ntb;
+    const int t = b * kColTB + tid, r0 = g * kColRows, nr = min(C.G - r0, kColRows);
+    const bool live = t < C.ntiles;
+    const unsigned long long tagA = (unsigned long long)((C.L.epoch << 2) | 1u) << 32;
+    const unsigned long long tagP = (unsigned long long)((C.L.epoch << 2) | 2u) << 32;
+    int v[kColRows], run = 0;
+    if (live) {
+        int agg = 0;
+#pragma unroll
+        for (int r = 0; r < kColRows; ++r) {
+            v[r] = r < nr ? C.H[(size_t)(r0 + r) * C.ntiles + t] : 0;
+            agg += v[r];
+        }
+        unsigned long long *w = C.L.part + (size_t)g * C.ntiles + t;
+        if (g > 0) {
+            st_u64(w, tagA | (unsigned)agg);
+            unsigned spins = 0;
+            for (int gp = g - 1; gp >= 0; --gp) {
+                unsigned long long x;
+                unsigned flag;
+                for (;;) {
+                    x = ld_u64(C.L.part + (size_t)gp * C.ntiles + t);
+                    const unsigned tag = (unsigned)(x >> 32);
+                    flag = (tag >> 2) == C.L.epoch ? (tag & 3u) : 0u;
+                    if (flag) break;
+                    if (++spins > kSpinCap) { atomicOr(C.L.err, 4); flag = 2; x = 0; break; }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                run += (int)(unsigned)x;
+                if (flag == 2) break;
+            }
+        }
+        st_u64(w, tagP | (unsigned)(run + agg));
+#pragma unroll
+        for (int r = 0; r < kColRows; ++r)
+            if (r < nr) {
+                C.H[(size_t)(r0 + r) * C.ntiles + t] = run;
+                run += v[r];
+            }
     }
+    if (vid == 0) {   // the binned count: the count workgroups' own sums (no global atomic in the count pass)
+        unsigned long long o = 0;
+        for (int k = tid; k < C.G; k += kColTB) o += C.own[k];
+        for (int k = 32; k > 0; k >>= 1) o += __shfl_xor(o, k);
+        if ((tid & 63) == 0) sh_own[tid >> 6] = o;
+        __syncthreads();
+        if (tid == 0) {
+            unsigned long long tot = 0;
+            for (int k = 0; k < kColTB / 64; ++k) tot += sh_own[k];
+            *C.n_own = tot;
+        }
+    }
+    if (g != C.ng - 1) return;   // (uniform per block)
+    // tile starts: run is now tile t's total
+    const int local = block_excl_scan<kColTB>(live ? run : 0, wsum, &sh_tot);
+    if (tid < 64) {
+        LookBack T = C.L;
+        T.part += (size_t)C.ng * C.ntiles;
+        const unsigned pre = lb_exclusive(T, b, (unsigned)sh_tot, 4);
+        if (tid == 0) sh_pre = (int)pre;
+    }
+    __syncthreads();
+    if (live) C.ts[t] = sh_pre + local;
+    if (b == C.ntb - 1 && tid == 0) C.ts[C.ntiles] = sh_pre + sh_tot;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -873,7 +1016,7 @@ uint64_t rt_chunk(const RorLaunch &L, int G) {
 }
 
 template <bool SCATTER, int LAY>
-static void rt_part(const RorLaunch &L, int *H, const int *tstart, int G, float4 *staged, unsigned long long *n_own,
+static void rt_part(const RorLaunch &L, int *H, const int *tstart, int G, float4 *staged, unsigned *own_out,
                     hipStream_t s) {
     constexpr int TB = SCATTER ? kRtScatterTB : kRtCountTB, PER = SCATTER ? kRtScatterPer : kRtCountPer;
     static_assert(kRtChunkQ % (TB * PER) == 0 || (TB * PER) % kRtChunkQ == 0, "chunk granularity");
@@ -884,7 +1027,7 @@ static void rt_part(const RorLaunch &L, int *H, const int *tstart, int G, float4
     if (lds > 64 * 1024)   // the tile histogram exceeds the default dynamic-LDS limit (gfx950: 160 KB)
         AOS_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rt_part<SCATTER, LAY, TB, PER>),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    k_rt_part<SCATTER, LAY, TB, PER><<<G, TB, lds, s>>>(L, H, tstart, rt_chunk(L, G), staged, n_own);
+    k_rt_part<SCATTER, LAY, TB, PER><<<G, TB, lds, s>>>(L, H, tstart, rt_chunk(L, G), staged, own_out);
     AOS_HIP(hipGetLastError());
 }
 static int rt_layout(const RorLaunch &L) {
@@ -892,20 +1035,22 @@ static int rt_layout(const RorLaunch &L) {
     return 0;
 }
 
-size_t rt_colpart_ints(const RorLaunch &L, int G) { return (size_t)L.ntiles * ((G + kColRows - 1) / kColRows); }
+size_t rt_h_ints(const RorLaunch &L, int G) { return (size_t)L.ntiles * G + G; }
+int rt_colscan_words(const RorLaunch &L, int G) {
+    return ((G + kColRows - 1) / kColRows) * L.ntiles + (L.ntiles + kColTB - 1) / kColTB;
+}
 
-void launch_rt_count(const RorLaunch &L, int *H, int G, int *part, int *tot, unsigned long long *n_own, hipStream_t s) {
-    if (!L.n) return;
+void launch_rt_count(const RorLaunch &L, int *H, int G, int *ts, unsigned long long *n_own, const LookBack &lb,
+                     hipStream_t s) {
+    if (!L.n || !L.ntiles) return;
+    unsigned *own = reinterpret_cast<unsigned *>(H + (size_t)L.ntiles * G);
     switch (rt_layout(L)) {
-        case 1: rt_part<false, 1>(L, H, nullptr, G, nullptr, n_own, s); break;
-        case 2: rt_part<false, 2>(L, H, nullptr, G, nullptr, n_own, s); break;
-        default: rt_part<false, 0>(L, H, nullptr, G, nullptr, n_own, s);
+        case 1: rt_part<false, 1>(L, H, nullptr, G, nullptr, own, s); break;
+        case 2: rt_part<false, 2>(L, H, nullptr, G, nullptr, own, s); break;
+        default: rt_part<false, 0>(L, H, nullptr, G, nullptr, own, s);
     }
-    const int ng = (G + kColRows - 1) / kColRows;
-    const dim3 grid((L.ntiles + kColTB - 1) / kColTB, ng);
-    k_rt_colsum<<<grid, kColTB, 0, s>>>(H, part, L.ntiles, G);
-    k_rt_colpre<<<grid.x, kColTB, 0, s>>>(part, tot, L.ntiles, ng);
-    k_rt_colfix<<<grid, kColTB, 0, s>>>(H, part, L.ntiles, G);
+    ColScan C{H, ts, own, n_own, L.ntiles, G, (G + kColRows - 1) / kColRows, (L.ntiles + kColTB - 1) / kColTB, lb};
+    k_rt_colscan<<<C.ng * C.ntb, kColTB, 0, s>>>(C);
     AOS_HIP(hipGetLastError());
 }
 
@@ -948,6 +1093,21 @@ void launch_rt_merge(const float4 *old_st, const int *old_ts, const float4 *scan
 
 void launch_rt_sum_kept(const int *kept_tile, int ntiles, unsigned long long *counters, hipStream_t s) {
     k_rt_sum_kept<<<1, 1024, 0, s>>>(kept_tile, ntiles, counters);
+    AOS_HIP(hipGetLastError());
+}
+
+// Reads the staged array once, so that its lines sit in the Infinity Cache when the scatter writes them.
+// The scatter writes ~40 B runs per (workgroup, tile): on lines that missed the cache those partial writes
+// cost it 115-124 us instead of 88 (tools/rorbench, RORBENCH_PRETOUCH; the product's staged array is evicted
+// by the rest of the frame). Launched while the cloud's upload DMAs run (upload_pack), when the GPU is idle.
+__global__ __launch_bounds__(256) void k_rt_touch(const float4 *p, size_t n) {
+    float a = 0.f;
+    for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) a += p[i].x;
+    asm volatile("" ::"v"(a));   // (keeps the loads)
+}
+void launch_rt_touch(const float4 *p, size_t n, hipStream_t s) {
+    if (!n) return;
+    k_rt_touch<<<2048, 256, 0, s>>>(p, n);
     AOS_HIP(hipGetLastError());
 }
 

@@ -17,7 +17,7 @@
 using namespace aos;
 
 void aos_ctx::release() {
-    for (DevBuf *b : {&cloud_copy, &bin_count, &bin_start, &pt_binslot, &sorted, &ror_scratch, &ror_bigbins, &scan_tmp, &counters,
+    for (DevBuf *b : {&cloud_copy, &bin_count, &bin_start, &sorted, &ror_scratch, &ror_bigbins, &scan_tmp, &counters,
                       &raster_bits, &infl_bits, &open_bits, &thin_a, &thin_b, &thin_out, &thin_act, &occ_bytes, &skel_bytes, &flags,
                       &full_infl, &full_skel, &map_buf, &scan_stage})
         b->release();
@@ -90,7 +90,14 @@ void aos_ctx::upload_pack(void *dst, const aos_cloud_view &v, bool prefetch) {
         }
     // the handle's stream may still read dst (the previous frame): the copies start after it (a prefetch
     // writes the spare buffer, which no queued work reads)
-    if (!prefetch) AOS_HIP(hipEventRecord(ev[15], stream));
+    if (!prefetch) {
+        AOS_HIP(hipEventRecord(ev[15], stream));
+        // while the DMAs run (they wait for ev[15] only): the last frame's staged array is read once so that
+        // the scatter's partial-line writes hit the Infinity Cache (launch_rt_touch)
+        static const bool touch = [] { const char *e = getenv("AOS_STAGED_TOUCH"); return !e || atoi(e) != 0; }();
+        if (touch && ror_staged_max > 0)
+            launch_rt_touch(sorted.as<float4>(), std::min(sorted.cap / sizeof(float4), (size_t)ror_staged_max), stream);
+    }
     const uint64_t per = (n + nth - 1) / nth;
     const uint8_t *src = static_cast<const uint8_t *>(v.data);
     const bool std16 = v.point_step == 16 && v.off_x == 0 && v.off_y == 4 && v.off_z == 8;
@@ -330,6 +337,14 @@ int thin_iterations(const int *flags, int iters_run) {
 
 }  // namespace aos
 
+// The count pass's column-scan look-back: its err word is the frame's overflow word (d_own[1], read back
+// with the frame's stats), bit 4 = a stuck wait (ror_collect throws).
+LookBack aos_ctx::ror_lookback(const RorLaunch &L, int G, unsigned long long *d_own) {
+    LookBack lb = ror_lb.take(rt_colscan_words(L, G), stream);
+    lb.err = reinterpret_cast<int *>(d_own + 1);
+    return lb;
+}
+
 // a1-a4: ROR restricted to the points that can reach the (own) cells, clip, exclusion discs, raster
 // straight into the bit-packed window rbits (o.Hr rows of ceil(o.Wr / 64) words, zeroed here), by the
 // tile walk of ror.hip. Records ev[12] / ev[13] / ev[14] / ev[10] / ev[11] around its passes and
@@ -397,11 +412,9 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
     }
     const int nt = L.ntiles;
     const int G = rt_part_blocks(L);
-    const size_t nH = (size_t)nt * G;
 
-    int *d_H = static_cast<int *>(bin_count.ensure(sizeof(int) * nH));
-    int *d_tot = static_cast<int *>(bin_start.ensure(sizeof(int) * 2 * (nt + 1)));
-    int *d_ts = d_tot + (nt + 1);
+    int *d_H = static_cast<int *>(bin_count.ensure(sizeof(int) * rt_h_ints(L, G)));
+    int *d_ts = static_cast<int *>(bin_start.ensure(sizeof(int) * (nt + 1)));
     if (map_mode) d_ts = static_cast<int *>(ms.ts[ms.cur].ensure(sizeof(int) * (nt + 1)));
     int *d_kept = map_mode ? static_cast<int *>(ms.kept.ensure(sizeof(int) * nt)) : nullptr;
     DevBuf &stage_buf = map_mode ? ms.st[ms.cur] : sorted;
@@ -416,10 +429,8 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
     const bool any = n_points > 0 && !(is_dense && n_points < (uint64_t)L.need);
     if (!any) return;
     AOS_HIP(hipEventRecord(ev[12], s));
-    int *d_part = static_cast<int *>(pt_binslot.ensure(sizeof(int) * rt_colpart_ints(L, G)));
-    launch_rt_count(L, d_H, G, d_part, d_tot, d_own, s);
+    launch_rt_count(L, d_H, G, d_ts, d_own, ror_lookback(L, G, d_own), s);
     AOS_HIP(hipEventRecord(ev[13], s));
-    scan_1p(ror_lb, d_tot, d_ts, nt, false, s);
     // The staged array holds own + halo copies. With a capacity from an earlier frame the scatter
     // runs at once and reports an overflow (the frame is then redone with the size it read back,
     // run_seedgen); without one, or when the caller cannot redo (a tiled frame), the size is read
@@ -465,8 +476,7 @@ void aos_ctx::ror_stage_append(RorLaunch L, uint64_t *rbits) {
     Ls.cloud = map_buf.as<uint8_t>() + sizeof(float4) * ms.n_points;
     Ls.n = scan_n; Ls.step = 16; Ls.ox = 0; Ls.oy = 4; Ls.oz = 8;
     const int G = rt_part_blocks(Ls);
-    int *d_H = static_cast<int *>(ms.scan_H.ensure(sizeof(int) * (size_t)nt * G));
-    int *d_tot = static_cast<int *>(bin_start.ensure(sizeof(int) * 2 * (nt + 1)));
+    int *d_H = static_cast<int *>(ms.scan_H.ensure(sizeof(int) * rt_h_ints(Ls, G)));
     int *d_sts = static_cast<int *>(ms.scan_ts.ensure(sizeof(int) * (nt + 1)));
     unsigned long long *d_cnt = static_cast<unsigned long long *>(counters.ensure(8 * kRorCounters + 16));
     unsigned long long *d_own = d_cnt + kRorCounters;
@@ -483,10 +493,8 @@ void aos_ctx::ror_stage_append(RorLaunch L, uint64_t *rbits) {
     Ls.staged_cap = (int)scan_cap;
     Ls.overflow = reinterpret_cast<int *>(d_own + 1);
     AOS_HIP(hipEventRecord(ev[12], s));
-    int *d_part = static_cast<int *>(pt_binslot.ensure(sizeof(int) * rt_colpart_ints(Ls, G)));
-    launch_rt_count(Ls, d_H, G, d_part, d_tot, d_own, s);
+    launch_rt_count(Ls, d_H, G, d_sts, d_own, ror_lookback(Ls, G, d_own), s);
     AOS_HIP(hipEventRecord(ev[13], s));
-    scan_1p(ror_lb, d_tot, d_sts, nt, false, s);
     AOS_HIP(hipEventRecord(ev[14], s));
     launch_rt_scatter(Ls, d_H, d_sts, G, d_scan, s);
     AOS_HIP(hipEventRecord(ev[10], s));
@@ -525,6 +533,10 @@ bool aos_ctx::ror_collect() {
     h[0] = (int)binned;
     ror_est_binned = binned;
     ror_staged_max = std::max<double>(ror_staged_max, (double)h[2]);
+    if (u[1] & 4) {
+        ms.pend.on = false;
+        throw std::runtime_error("ROR column scan: a look-back wait exceeded its cap (kSpinCap)");
+    }
     if (u[1] & 2) ror_big_seen = true;
     if (ms.pend.on && u[1] == 0) {   // commit the streaming map's tile store
         ms.valid = true;

@@ -337,8 +337,6 @@ void subdiv_voronoi_facets(const std::vector<V2> &seeds, double min_x, double ma
     Subdiv sd;
     if (rect_mode == 1) {  // implicit Rect2f -> Rect (saturate_cast<int> = cvRound)
         int ix = cv_round(rx), iy = cv_round(ry), iw = cv_round(rw), ih = cv_round(rh);
-        float big = 3.f * (float)std::max(iw, ih);
-        (void)big;
         sd.init((float)ix, (float)iy, (float)iw, (float)ih);
     } else {
         sd.init(rx, ry, rw, rh);

@@ -9,6 +9,10 @@
 #   kt       rocprofv3 --kernel-trace --stats of the sequential C2 loop
 #   ktc3     the same on one C3 frame set (bench --config C3 on one GPU)
 #   pmc      FETCH_SIZE and WRITE_SIZE passes (separate runs) -> TAG_pmc_traffic.json
+#   tiled    the rotating-root test, then bench.py --tiled at RANKS (default "1 2 4"; 2 and 4 ranks share the
+#            box's GPU over gloo)
+#   tiledstream  bench.py --tiled --stream at 1 rank, then the driver's --gpus 2 flow over gloo
+#   rorpmc   tools/rorbench binaries (RORBENCH, built in-tree beforehand): kernel trace + two SQ passes
 # Usage: TAG=r04a STEPS="pytest smoke bench kt" tools/gpu_run.sh
 set -e
 R=$PWD
@@ -59,6 +63,45 @@ for step in $STEPS; do
         > $R/gpurun_out/${TAG}_write.log 2>&1)
       python3 tools/pmc_traffic.py $(ls gpurun_out/${TAG}_fetch/*counter_collection.csv | head -1) \
         $(ls gpurun_out/${TAG}_write/*counter_collection.csv | head -1) gpurun_out/${TAG}_pmc_traffic.json ;;
+    tiled)
+      timeout -k 10 600 python -u -m pytest tests/test_gpu_tiled.py -x -v --timeout 400 --timeout-method thread -k rotating \
+        > gpurun_out/${TAG}_pytest_rot.log 2>&1 || { tail -40 gpurun_out/${TAG}_pytest_rot.log; exit 1; }
+      tail -1 gpurun_out/${TAG}_pytest_rot.log
+      for n in ${RANKS:-1 2 4}; do
+        log=gpurun_out/${TAG}_tiled_${n}.log
+        if [ "$n" = 1 ]; then
+          timeout -k 10 400 python -u bench.py --tiled --steps 8 --warmup 2 --no-cpu-baseline > $log 2>&1 || { tail -20 $log; exit 1; }
+        else
+          AOS_BENCH_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
+            --master-addr 127.0.0.1 --master-port $((29600 + n)) bench.py --gpus $n --tiled --steps 8 --warmup 2 \
+            --no-cpu-baseline > $log 2>&1 || { tail -30 $log; exit 1; }
+        fi
+        grep '^{' $log | cut -c1-300
+      done ;;
+    tiledstream)
+      timeout -k 10 300 python -u bench.py --tiled --stream --steps 10 --warmup 2 --no-cpu-baseline \
+        > gpurun_out/${TAG}_ts1.log 2> gpurun_out/${TAG}_ts1.err || { tail -30 gpurun_out/${TAG}_ts1.err; exit 1; }
+      grep '^{' gpurun_out/${TAG}_ts1.log | cut -c1-300
+      AOS_BENCH_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+        --master-addr 127.0.0.1 --master-port 29631 bench.py --gpus 2 --steps 8 --warmup 3 --no-cpu-baseline \
+        > gpurun_out/${TAG}_ts2.log 2>&1 || { tail -30 gpurun_out/${TAG}_ts2.log; exit 1; }
+      grep '^{' gpurun_out/${TAG}_ts2.log | cut -c1-300 ;;
+    rorpmc)
+      for b in ${RORBENCH:-tools/rorbench/rorbench}; do
+        n=$(basename $b)
+        timeout -k 10 120 $R/$b 4096 10000000 10 12 > gpurun_out/${TAG}_${n}.log 2>&1 || { tail -5 gpurun_out/${TAG}_${n}.log; exit 1; }
+        tail -2 gpurun_out/${TAG}_${n}.log
+        rm -rf gpurun_out/${TAG}_${n}_kt gpurun_out/${TAG}_${n}_sq1 gpurun_out/${TAG}_${n}_sq2
+        (cd /tmp && timeout -s KILL 90 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${TAG}_${n}_kt -o kt \
+          -- $R/$b 4096 10000000 4 12 > $R/gpurun_out/${TAG}_${n}_kt.log 2>&1)
+        (cd /tmp && timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+          SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d $R/gpurun_out/${TAG}_${n}_sq1 -o sq1 \
+          -- $R/$b 4096 10000000 2 12 > $R/gpurun_out/${TAG}_${n}_sq1.log 2>&1)
+        (cd /tmp && timeout -s KILL 90 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR \
+          SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $R/gpurun_out/${TAG}_${n}_sq2 -o sq2 \
+          -- $R/$b 4096 10000000 2 12 > $R/gpurun_out/${TAG}_${n}_sq2.log 2>&1)
+        python3 tools/pmc_summary.py gpurun_out/${TAG}_${n}_sq1 gpurun_out/${TAG}_${n}_sq2 || true
+      done ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac

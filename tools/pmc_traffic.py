@@ -32,9 +32,10 @@ def main():
         w, nw = write[k]
         out["kernels"][k] = {"fetch_bytes_raw": f, "fetch_bytes": 2.0 * f, "write_bytes": w,
                              "bytes_per_launch": 2.0 * f + w, "launches": [nf, nw]}
-    # the ROR stage a1-a4 (one launch of each per frame): count + column scan (k_rt_colsum / colpre /
-    # colfix) + scatter + the big-tile kernels (k_rt_big*) + the per-tile neighbour counts (k_rt_ror<...>)
-    parts = [k for k in out["kernels"] if k.startswith(("k_rt_part", "k_rt_col", "k_rt_big", "k_rt_ror"))]
+    # the ROR stage a1-a4 (one launch of each per frame): count + column scan (k_rt_colscan; round 3:
+    # k_rt_colsum / colpre / colfix) + scatter + the big-tile kernels (k_rt_big*) + the per-tile neighbour
+    # counts (k_rt_ror<...>) + the staged array's read-ahead during the upload (k_rt_touch, round 4)
+    parts = [k for k in out["kernels"] if k.startswith(("k_rt_part", "k_rt_col", "k_rt_big", "k_rt_ror", "k_rt_touch"))]
     if parts:
         out["kernels"]["ror_stage"] = {"bytes_per_launch": sum(out["kernels"][k]["bytes_per_launch"] for k in parts),
                                        "kernels": sorted(parts)}

@@ -1,14 +1,13 @@
 #!/bin/bash
-# Count-pass variants of the ROR partition (ror.hip compile-time knobs), built here and run on the box by
-# run_count_variants.sh: packed 12-B cloud, warm (back to back) and cold (512 MB overwritten between frames).
+# Variants of the ROR partition (ror.hip compile-time knobs), built here and run on the box by
+# run_count_variants.sh. Usage: tools/rorbench/count_variants.sh "_tag:-DKNOB=v -DKNOB2=w" ...
+# (round 4 sets: count-pass block shapes — AOS_RT_CTB / AOS_RT_G / AOS_RT_CPER / AOS_RT_COUNT_EXP —, then
+# nontemporal loads / stores, AOS_RT_NT)
 set -e
 D=$(dirname "$0")
-build() { TAG=$1 DEFS="$2" "$D/build.sh" >/dev/null; echo "built rorbench$1: $2"; }
-build _base ""
-build _exp1 "-DAOS_RT_COUNT_EXP=1"
-build _exp2 "-DAOS_RT_COUNT_EXP=2"
-build _tb512 "-DAOS_RT_CTB=512"
-build _tb1024 "-DAOS_RT_CTB=1024"
-build _g1024 "-DAOS_RT_G=1024"
-build _cper16 "-DAOS_RT_CPER=16"
-build _tb512c4 "-DAOS_RT_CTB=512 -DAOS_RT_CPER=4"
+rm -f "$D"/rorbench_*
+for v in "$@"; do
+  tag=${v%%:*}; defs=${v#*:}
+  TAG=$tag DEFS="$defs" "$D/build.sh" >/dev/null
+  echo "built rorbench$tag: $defs"
+done

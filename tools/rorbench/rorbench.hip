@@ -28,18 +28,16 @@ void orchard_generate_range(const orchard_cfg *c, const double *tree_x, const do
                             uint64_t begin, uint64_t end, uint8_t *out);
 }
 
-namespace aos {
-size_t scan_temp_bytes(int n) {
-    size_t t = 0;
-    AOS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t, (const int *)nullptr, (int *)nullptr, n));
-    return t;
-}
-void launch_exclusive_scan(const int *in, int *out, int n, void *temp, size_t temp_bytes, hipStream_t s) {
-    AOS_HIP(hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, in, out, n, s));
-}
-}  // namespace aos
 
 using namespace aos;
+
+// RORBENCH_PRETOUCH: 1 = memset the staged array, 2 = read it once, before the cloud upload (outside the timed
+// stage; RORBENCH_UPLOAD=1: the cloud is re-uploaded each frame also with flush_mb > 0): does the scatter's partial-line writing run faster once the array's lines are in the Infinity Cache?
+__global__ void k_touch(const float4 *p, size_t n, float *sink) {
+    float a = 0.f;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) a += p[i].x;
+    if (a == 1234.5f) *sink = a;
+}
 
 int main(int argc, char **argv) {
     const int grid_n = argc > 1 ? atoi(argv[1]) : 4096;
@@ -71,6 +69,12 @@ int main(int argc, char **argv) {
     uint8_t *d_cloud;
     AOS_HIP(hipMalloc(&d_cloud, (size_t)pstep * n));
     AOS_HIP(hipMemcpy(d_cloud, cloud.data(), (size_t)pstep * n, hipMemcpyHostToDevice));
+    // flush_mb < 0: the product's state instead — the cloud uploaded again from pinned host memory each frame
+    uint8_t *h_pinned = nullptr;
+    if (flush_mb < 0 || getenv("RORBENCH_UPLOAD")) {
+        AOS_HIP(hipHostMalloc(reinterpret_cast<void **>(&h_pinned), (size_t)pstep * n, 0));
+        std::memcpy(h_pinned, cloud.data(), (size_t)pstep * n);
+    }
 
     RorLaunch L{};
     L.cloud = d_cloud; L.n = n; L.step = pstep; L.ox = 0; L.oy = 4; L.oz = 8; L.is_dense = 1;
@@ -94,42 +98,48 @@ int main(int argc, char **argv) {
     AOS_HIP(hipStreamCreate(&s));
     hipEvent_t e[7];
     for (auto &x : e) AOS_HIP(hipEventCreate(&x));
-    int *d_H = nullptr, *d_tot = nullptr; void *d_st = nullptr; float4 *d_staged = nullptr, *d_scr = nullptr;
+    int *d_H = nullptr, *d_tot = nullptr; float4 *d_staged = nullptr, *d_scr = nullptr;
+    unsigned long long *d_lb = nullptr; size_t cap_lb = 0;
+    const int pretouch = getenv("RORBENCH_PRETOUCH") ? atoi(getenv("RORBENCH_PRETOUCH")) : 0;
     unsigned long long *d_cnt; uint64_t *d_bits; int *d_big = nullptr; size_t cap_big = 0;
     AOS_HIP(hipMalloc(&d_cnt, 8 * (kRorCounters + 2)));
     AOS_HIP(hipMalloc(&d_bits, 8ull * WW * H));
-    size_t cap_H = 0, cap_st = 0, cap_staged = 0, cap_t = 0;
+    size_t cap_H = 0, cap_staged = 0, cap_t = 0;
     double acc[6] = {0, 0, 0, 0, 0, 0};
     for (int f = 0; f < frames + 2; ++f) {
         rt_configure(L, H, WW, est);
         const int G = rt_part_blocks(L);
         const int nt = L.ntiles;
         const size_t nH = (size_t)nt * G;
-        if (nH > cap_H) { if (d_H) AOS_HIP(hipFree(d_H)); AOS_HIP(hipMalloc(&d_H, 4 * nH)); cap_H = nH; }
-        if ((size_t)nt + 1 > cap_t) { if (d_tot) AOS_HIP(hipFree(d_tot)); AOS_HIP(hipMalloc(&d_tot, 8 * (nt + 1))); cap_t = nt + 1; }
-        int *d_ts = d_tot + (nt + 1);
-        const size_t st = scan_temp_bytes(nt + 1);
-        if (st > cap_st) { if (d_st) AOS_HIP(hipFree(d_st)); AOS_HIP(hipMalloc(&d_st, st)); cap_st = st; }
-        AOS_HIP(hipMemsetAsync(d_tot + nt, 0, 4, s));
+        if (rt_h_ints(L, G) > cap_H) { if (d_H) AOS_HIP(hipFree(d_H)); cap_H = rt_h_ints(L, G); AOS_HIP(hipMalloc(&d_H, 4 * cap_H)); }
+        if ((size_t)nt + 1 > cap_t) { if (d_tot) AOS_HIP(hipFree(d_tot)); AOS_HIP(hipMalloc(&d_tot, 4 * (nt + 1))); cap_t = nt + 1; }
+        int *d_ts = d_tot;
+        const size_t words = rt_colscan_words(L, G);
+        if (words > cap_lb) {   // look-back words (epoch-tagged: zeroed once), ticket
+            if (d_lb) AOS_HIP(hipFree(d_lb));
+            AOS_HIP(hipMalloc(&d_lb, 8 * words + 64)); AOS_HIP(hipMemset(d_lb, 0, 8 * words + 64)); cap_lb = words;
+        }
+        const LookBack lb{d_lb, reinterpret_cast<unsigned *>(d_lb + cap_lb), (unsigned)(f + 1),
+                          reinterpret_cast<int *>(d_cnt + kRorCounters + 1)};
         AOS_HIP(hipMemsetAsync(d_cnt, 0, 8 * (kRorCounters + 2), s));
         AOS_HIP(hipMemsetAsync(d_bits, 0, 8ull * WW * H, s));
         if (d_flush) AOS_HIP(hipMemsetAsync(d_flush, f & 0xff, (size_t)flush_mb << 20, s));
-        AOS_HIP(hipEventRecord(e[0], s));
-        if (pstep == 12) rt_part<false, 2>(L, d_H, nullptr, G, nullptr, d_cnt + kRorCounters, s);   // (launch_rt_count, split)
-        else rt_part<false, 1>(L, d_H, nullptr, G, nullptr, d_cnt + kRorCounters, s);
-        AOS_HIP(hipEventRecord(e[6], s));
-        {
-            static int *d_part = nullptr;
-            if (!d_part) AOS_HIP(hipMalloc(&d_part, 4 * rt_colpart_ints(L, G) * 4));
-            const int ng = (G + kColRows - 1) / kColRows;
-            const dim3 grid((L.ntiles + kColTB - 1) / kColTB, ng);
-            k_rt_colsum<<<grid, kColTB, 0, s>>>(d_H, d_part, L.ntiles, G);
-            k_rt_colpre<<<grid.x, kColTB, 0, s>>>(d_part, d_tot, L.ntiles, ng);
-            k_rt_colfix<<<grid, kColTB, 0, s>>>(d_H, d_part, L.ntiles, G);
+        if (pretouch && d_staged) {   // outside the timed stage: in the product it would overlap the upload
+            if (pretouch == 1) AOS_HIP(hipMemsetAsync(d_staged, 0, 16ull * cap_staged, s));
+            else k_touch<<<2048, 256, 0, s>>>(d_staged, cap_staged, reinterpret_cast<float *>(d_bits));
         }
-        AOS_HIP(hipEventRecord(e[1], s));
-        launch_exclusive_scan(d_tot, d_ts, nt + 1, d_st, st, s);
+        if (h_pinned) AOS_HIP(hipMemcpyAsync(d_cloud, h_pinned, (size_t)pstep * n, hipMemcpyHostToDevice, s));
+        AOS_HIP(hipEventRecord(e[0], s));
         AOS_HIP(hipEventRecord(e[2], s));
+        {   // launch_rt_count with an event between its two launches (count kernel, k_rt_colscan)
+            unsigned *own = reinterpret_cast<unsigned *>(d_H + nH);
+            if (pstep == 12) rt_part<false, 2>(L, d_H, nullptr, G, nullptr, own, s);
+            else rt_part<false, 1>(L, d_H, nullptr, G, nullptr, own, s);
+            AOS_HIP(hipEventRecord(e[6], s));
+            ColScan C{d_H, d_ts, own, d_cnt + kRorCounters, nt, G, (G + kColRows - 1) / kColRows, (nt + kColTB - 1) / kColTB, lb};
+            k_rt_colscan<<<C.ng * C.ntb, kColTB, 0, s>>>(C);
+            AOS_HIP(hipEventRecord(e[1], s));
+        }
         int total = 0;
         unsigned long long own = 0;
         AOS_HIP(hipMemcpyAsync(&total, d_ts + nt, 4, hipMemcpyDeviceToHost, s));
@@ -150,12 +160,12 @@ int main(int argc, char **argv) {
         AOS_HIP(hipEventRecord(e[5], s));
         AOS_HIP(hipStreamSynchronize(s));
         float t[6];
-        AOS_HIP(hipEventElapsedTime(&t[0], e[0], e[1]));
-        AOS_HIP(hipEventElapsedTime(&t[1], e[1], e[2]));
+        AOS_HIP(hipEventElapsedTime(&t[0], e[2], e[1]));
+        AOS_HIP(hipEventElapsedTime(&t[1], e[0], e[2]));
         AOS_HIP(hipEventElapsedTime(&t[2], e[3], e[4]));
         AOS_HIP(hipEventElapsedTime(&t[3], e[4], e[5]));
         AOS_HIP(hipEventElapsedTime(&t[4], e[0], e[5]));
-        AOS_HIP(hipEventElapsedTime(&t[5], e[0], e[6]));
+        AOS_HIP(hipEventElapsedTime(&t[5], e[2], e[6]));
         if (f >= 2) for (int k = 0; k < 6; ++k) acc[k] += t[k] / frames;
         if (f == frames + 1) {
             std::vector<uint64_t> bits((size_t)WW * H);
@@ -165,13 +175,15 @@ int main(int argc, char **argv) {
             unsigned long long pc = 0, kept = 0, hsh = 1469598103934665603ull;
             for (uint64_t w : bits) { pc += __builtin_popcountll(w); hsh = (hsh ^ w) * 1099511628211ull; }
             for (auto v : cnt) kept += v;
-            printf("grid %dx%d n %llu TB %d tiles %d G %d staged %d binned %llu | raster cells %llu kept %llu hash %016llx\n", W, H,
-                   (unsigned long long)n, L.TB, L.ntiles, G, total, own, pc, kept, hsh);
+            unsigned long long err = 0;
+            AOS_HIP(hipMemcpy(&err, d_cnt + kRorCounters + 1, 8, hipMemcpyDeviceToHost));
+            printf("grid %dx%d n %llu TB %d tiles %d G %d staged %d binned %llu | raster cells %llu kept %llu hash %016llx err %llu\n", W, H,
+                   (unsigned long long)n, L.TB, L.ntiles, G, total, own, pc, kept, hsh, err);
         }
     }
     const double b = 12.0 * n + (double)W * H;
     printf("(count kernel %.1f us, column scan %.1f us)\n", 1e3 * acc[5], 1e3 * (acc[0] - acc[5]));
-    printf("count %.1f us  scan %.1f us  scatter %.1f us  tiles %.1f us  | stage %.1f us (incl. read-back gap)  "
+    printf("count %.1f us  pretouch %.1f us  scatter %.1f us  tiles %.1f us  | stage %.1f us (incl. read-back gap)  "
            "§8d bytes %.0f MB -> %.3f TB/s = %.3f of 8 TB/s; count pass 12N: %.3f of peak\n",
            1e3 * acc[0], 1e3 * acc[1], 1e3 * acc[2], 1e3 * acc[3], 1e3 * acc[4], b / 1e6, b / (acc[4] * 1e-3) / 1e12,
            b / (acc[4] * 1e-3) / 8e12, 12.0 * n / (acc[0] * 1e-3) / 8e12);
