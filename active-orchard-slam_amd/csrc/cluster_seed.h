@@ -85,6 +85,8 @@ struct ClusterSeedState {
     DevBuf cand_xy, cand_ok, cand_state, hash_count, hash_start, hash_slot, hash_sorted, seed_out, misc, scan_tmp;
     LookBackScratch lb;           // the stage's single-pass scans
     bool cl_count_dirty = true;   // cl_count (cluster sizes) not known to be zero
+    PinnedBuf h_recbuf, h_up_poly, h_up_rows;   // cluster records read back; host -> device staging
+    PinnedBuf h_seeds;   // the frame's seeds (one DMA into pinned memory: no staging copy, no page faults)
     PinnedBuf h_cells;   // the replayed clusters' cells (one DMA; round 3's zeroed pageable vector cost ~1.5 ms at C3)
     PinnedBuf h_misc;
     int n_fg = 0, n_clusters = 0, n_rows = 0, n_cur_tab = 0;
@@ -125,10 +127,11 @@ struct SeedStageOut {
     int n_clusters_all = 0;
     int n_bfs = 0;
     std::vector<double> row_center, row_start, row_end, row_length;  // all_tree_rows order
-    std::vector<double> virtual_xy, ray_xy, endpoint_xy;
     std::vector<double> rows_info, cluster_info;
-    const double *d_voronoi = nullptr;  // device copy of the concatenated seeds
-    int n_voronoi = 0;
+    // the concatenated seeds (virtual, ray, endpoint): device copy, and the host copy in the stage's pinned
+    // buffer (valid until the stage runs again)
+    const double *d_voronoi = nullptr, *h_voronoi = nullptr;
+    int n_voronoi = 0, n_virtual = 0, n_ray = 0, n_endpoint = 0;
 };
 
 void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStageOut &out, hipStream_t stream,

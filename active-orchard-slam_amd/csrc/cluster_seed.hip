@@ -491,7 +491,10 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
     double *d_poly = dev<double>(S.poly, 2 * np);
     std::vector<double> hp(2 * np);
     for (int i = 0; i < np; ++i) { hp[2 * i] = poly[i].first; hp[2 * i + 1] = poly[i].second; }
-    AOS_HIP(hipMemcpyAsync(d_poly, hp.data(), sizeof(double) * 2 * np, hipMemcpyHostToDevice, s));
+    // host -> device through pinned staging buffers (each written once per frame, after the last frame's sync)
+    double *h_up = static_cast<double *>(S.h_up_poly.ensure(sizeof(double) * 2 * np));
+    std::copy(hp.begin(), hp.end(), h_up);
+    copy_from_host(d_poly, h_up, sizeof(double) * 2 * np, s);
     int *h_sc = static_cast<int *>(S.h_misc.ensure(4096));
 
     // ---- foreground list (raster order)
@@ -504,8 +507,7 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         d_wc = dev<int>(S.word_cnt, Cw + 1); d_wo = dev<int>(S.word_off, Cw + 1);
         k_fg<<<gw2, 64, 0, s>>>(in.skel_bits, d_fg, d_wc, g, d_poly, np);
         scan_1p(S.lb, d_wc, d_wo, (int)Cw, false, s);
-        AOS_HIP(hipMemcpyAsync(h_sc, d_wo + Cw, sizeof(int), hipMemcpyDeviceToHost, s));
-        AOS_HIP(hipMemcpyAsync(h_sc + 1, S.lb.err_word(s), sizeof(int), hipMemcpyDeviceToHost, s));
+        peek_to_host(h_sc, {d_wo + Cw, S.lb.err_word(s)}, s);
         S.dedup.sev.sync(s);
         if (h_sc[1]) throw std::runtime_error("cluster stage: scan failed on the device");
     }
@@ -526,8 +528,7 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         k_ccl_union<<<cdiv(nf, 256), 256, 0, s>>>(d_list, nf, d_fg, d_wo, g, d_par);
         k_ccl_flatten<<<cdiv(nf, 256), 256, 0, s>>>(d_par, d_isroot, nf);
         scan_1p(S.lb, d_isroot, d_rank, nf, false, s);
-        AOS_HIP(hipMemcpyAsync(h_sc, d_rank + nf, sizeof(int), hipMemcpyDeviceToHost, s));
-        AOS_HIP(hipMemcpyAsync(h_sc + 1, S.lb.err_word(s), sizeof(int), hipMemcpyDeviceToHost, s));
+        peek_to_host(h_sc, {d_rank + nf, S.lb.err_word(s)}, s);
         S.dedup.sev.sync(s);
         if (h_sc[1]) throw std::runtime_error("cluster stage: scan failed on the device");
         const int ncl = h_sc[0];
@@ -547,8 +548,10 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         ClusterRec *d_rec = dev<ClusterRec>(S.rec, ncl);
         launch_cluster_stats(d_off, d_cells, ncl, g, d_poly, np, static_cast<float>(in.cluster_min_length), d_rec, s);
         S.h_rec.resize(ncl);
-        AOS_HIP(hipMemcpyAsync(S.h_rec.data(), d_rec, sizeof(ClusterRec) * ncl, hipMemcpyDeviceToHost, s));
+        ClusterRec *hr = static_cast<ClusterRec *>(S.h_recbuf.ensure(sizeof(ClusterRec) * (size_t)ncl));
+        copy_to_host(hr, d_rec, sizeof(ClusterRec) * ncl, s);
         S.dedup.sev.sync(s);
+        std::copy(hr, hr + ncl, S.h_rec.begin());
         int n_bfs = 0;
         for (const auto &r : S.h_rec) n_bfs += (r.flags & 2) != 0;
         out.n_bfs = n_bfs;
@@ -563,7 +566,7 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
                 if (S.h_rec[c].flags & 2) ids.push_back(c);
             const long long lo = off[ids.front()], hi = off[ids.back() + 1];
             int *hc = static_cast<int *>(S.h_cells.ensure(sizeof(int) * (size_t)(hi - lo)));
-            AOS_HIP(hipMemcpyAsync(hc, d_cells + lo, sizeof(int) * (hi - lo), hipMemcpyDeviceToHost, s));
+            copy_to_host(hc, d_cells + lo, sizeof(int) * (hi - lo), s);
             S.dedup.sev.sync(s);
             std::vector<ReplayJob> jobs;
             for (int c : ids) jobs.push_back({c, hc + (off[c] - lo), S.h_rec[c].n});
@@ -583,7 +586,11 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
     DedupScratch &scr = S.dedup;
     const int nr = (int)rows.size();
     RowDev *d_rows = dev<RowDev>(S.row_idx, nr);
-    AOS_HIP(hipMemcpyAsync(d_rows, rows.data(), sizeof(RowDev) * nr, hipMemcpyHostToDevice, s));
+    {
+        RowDev *hr = static_cast<RowDev *>(S.h_up_rows.ensure(sizeof(RowDev) * (size_t)nr));
+        std::copy(rows.begin(), rows.end(), hr);
+        copy_from_host(d_rows, hr, sizeof(RowDev) * nr, s);
+    }
     const int nslots = rows.back().slot0 + 3 * rows.back().k;
     const size_t ncand = (size_t)nslots + 8 * (size_t)nr;
     double2 *d_cand = dev<double2>(S.cand_xy, ncand), *d_rcand = d_cand + nslots, *d_ecand = d_rcand + 6 * nr;
@@ -633,20 +640,18 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
                            d_eout, nullptr, nullptr, d_cnt + 2, s);
     }
     k_concat3<<<cdiv((long long)ncand, 256), 256, 0, s>>>(d_vout, d_rout, d_eout, d_cnt, d_seeds);
-    AOS_HIP(hipMemcpyAsync(h_sc, d_cnt, 3 * sizeof(int), hipMemcpyDeviceToHost, s));
-    AOS_HIP(hipMemcpyAsync(h_sc + 3, dedup_err(scr, s), sizeof(int), hipMemcpyDeviceToHost, s));
+    peek_to_host(h_sc, {d_cnt, d_cnt + 1, d_cnt + 2, dedup_err(scr, s)}, s);
     S.dedup.sev.sync(s);
     dedup_check(scr, h_sc[3]);
     const int n_virtual = h_sc[0], n_ray = h_sc[1], n_end = h_sc[2];
     const int ntot = n_virtual + n_ray + n_end;
-    std::vector<double> all(2 * (size_t)ntot);
+    double *hs = static_cast<double *>(S.h_seeds.ensure(sizeof(double2) * (size_t)std::max(ntot, 1)));
     if (ntot) {
-        AOS_HIP(hipMemcpyAsync(all.data(), d_seeds, sizeof(double2) * ntot, hipMemcpyDeviceToHost, s));
+        copy_to_host(hs, d_seeds, sizeof(double2) * ntot, s);
         S.dedup.sev.sync(s);
     }
-    out.virtual_xy.assign(all.begin(), all.begin() + 2 * n_virtual);
-    out.ray_xy.assign(all.begin() + 2 * n_virtual, all.begin() + 2 * (n_virtual + n_ray));
-    out.endpoint_xy.assign(all.begin() + 2 * (n_virtual + n_ray), all.end());
+    out.h_voronoi = hs;
+    out.n_virtual = n_virtual; out.n_ray = n_ray; out.n_endpoint = n_end;
     out.d_voronoi = reinterpret_cast<const double *>(d_seeds);
     out.n_voronoi = ntot;
 }

@@ -11,6 +11,7 @@
 
 #include <climits>
 #include <cstdint>
+#include <initializer_list>
 
 #include "aos_internal.h"
 
@@ -62,5 +63,16 @@ struct CellScratch {
 };
 CellIdx cell_index_build(CellScratch &S, const double2 *p, const int *ok, int n, const HashG &h, hipStream_t s,
                          const int *n_dev = nullptr);
+
+// ------------------------------------------------------------------ read-backs without the copy engine
+// Small read-backs in the middle of a frame (counts, error words, cluster records, seeds) are stored into
+// pinned host memory by a kernel instead of hipMemcpyAsync: a D2H copy is queued on the DMA engine behind the
+// frame's 2 x 16.8 MB OccupancyGrid copies (~0.3 ms each at C2), which delayed every host wait of the
+// cluster / seed stage until they had finished. h_dst: pinned host memory (PinnedBuf); the values are the
+// host's once the stream has been synchronised. AOS_ZC_READBACK=0: hipMemcpyAsync instead (A/B).
+constexpr int kPeekMax = 8;
+void peek_to_host(int *h_dst, std::initializer_list<const int *> srcs, hipStream_t s);
+void copy_to_host(void *h_dst, const void *d_src, size_t bytes, hipStream_t s);
+void copy_from_host(void *d_dst, const void *h_src, size_t bytes, hipStream_t s);   // h_src pinned
 
 }  // namespace aos

@@ -19,6 +19,7 @@
 // candidates run in one workgroup each (k_dedup_small: index, rounds and compaction in LDS).
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 
@@ -394,6 +395,55 @@ void greedy_dedup_async(DedupScratch &S, const double2 *cand, const int *ok, int
     if (owner) k_lfmis<true><<<blocks, kLfTB, 0, s>>>(A);
     else k_lfmis<false><<<blocks, kLfTB, 0, s>>>(A);
     AOS_HIP(hipGetLastError());
+}
+
+// ------------------------------------------------------------------ read-backs without the copy engine
+static bool zc_readback() {
+    static const bool on = [] { const char *e = getenv("AOS_ZC_READBACK"); return !e || atoi(e) != 0; }();
+    return on;
+}
+struct PeekArgs { const int *src[kPeekMax]; int n; };
+__global__ void k_peek_host(PeekArgs P, int *h_dst) {
+    if ((int)threadIdx.x < P.n) h_dst[threadIdx.x] = *P.src[threadIdx.x];
+}
+void peek_to_host(int *h_dst, std::initializer_list<const int *> srcs, hipStream_t s) {
+    if ((int)srcs.size() > kPeekMax) throw std::runtime_error("peek_to_host: too many values");
+    if (!zc_readback()) {
+        int k = 0;
+        for (const int *p : srcs) AOS_HIP(hipMemcpyAsync(h_dst + k++, p, sizeof(int), hipMemcpyDeviceToHost, s));
+        return;
+    }
+    PeekArgs P{};
+    for (const int *p : srcs) P.src[P.n++] = p;
+    k_peek_host<<<1, 64, 0, s>>>(P, h_dst);
+    AOS_HIP(hipGetLastError());
+}
+// 16-byte words while both ends are 16-byte aligned and the size a multiple of 16, else 4-byte words, else bytes
+template <class W>
+__global__ void k_copy_host(W *h_dst, const W *d_src, size_t n) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        h_dst[i] = d_src[i];
+}
+static void copy_kernel(void *h_dst, const void *d_src, size_t bytes, hipStream_t s) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(h_dst) | reinterpret_cast<uintptr_t>(d_src) | bytes;
+    auto go = [&](auto *dst, const auto *src, size_t n) {
+        const int blocks = (int)std::min<size_t>(256, (n + 255) / 256);
+        k_copy_host<<<blocks, 256, 0, s>>>(dst, src, n);
+    };
+    if (!(a & 15)) go(static_cast<uint4 *>(h_dst), static_cast<const uint4 *>(d_src), bytes / 16);
+    else if (!(a & 3)) go(static_cast<unsigned *>(h_dst), static_cast<const unsigned *>(d_src), bytes / 4);
+    else go(static_cast<unsigned char *>(h_dst), static_cast<const unsigned char *>(d_src), bytes);
+    AOS_HIP(hipGetLastError());
+}
+void copy_to_host(void *h_dst, const void *d_src, size_t bytes, hipStream_t s) {
+    if (!bytes) return;
+    if (zc_readback()) copy_kernel(h_dst, d_src, bytes, s);
+    else AOS_HIP(hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, s));
+}
+void copy_from_host(void *d_dst, const void *h_src, size_t bytes, hipStream_t s) {
+    if (!bytes) return;
+    if (zc_readback()) copy_kernel(d_dst, h_src, bytes, s);
+    else AOS_HIP(hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, s));
 }
 
 int *dedup_err(DedupScratch &S, hipStream_t s) { return S.lb.err_word(s); }

@@ -94,6 +94,17 @@ __device__ __forceinline__ bool rt_candidate(const RorLaunch &L, float x, float 
     return true;
 }
 
+// generateOccupancyGrid's cell index (int)(a / res), a = (double)x - origin, without the f64 division in
+// the common case: q = a * (1 / res) is within 3.3e-16 |q| of the rounded quotient, so its truncation is
+// the quotient's unless an integer lies within that distance; q within 1e-14 |q| of an integer takes the
+// exact division. (Two f64 divisions per kept candidate were ~20 % of k_rt_ror's VALU issue.)
+__device__ __forceinline__ int rt_cell(double a, double res, double inv_res) {
+    const double q = a * inv_res;
+    const double t = trunc(q), d = fabs(q - t), tol = fabs(q) * 1e-14 + 1e-300;
+    if (d < tol || d > 1.0 - tol) return (int)(a / res);
+    return (int)t;
+}
+
 // dense: (double)d2 <= r2, i.e. d2 <= r2df; non-dense: d2 < r2f, i.e. d2 <= the float below r2f: both are
 // d2 <= L.r2cmp (rt_configure), one compare in the inner loops
 __device__ __forceinline__ bool rt_in(const RorLaunch &L, float4 p, float4 q) {
@@ -417,19 +428,27 @@ __global__ __launch_bounds__(kColTB) void k_rt_colscan(ColScan C) {
 #define AOS_RT_THREADS 512
 #endif
 constexpr int kRorThreads = AOS_RT_THREADS, kRorCap = 2048, kRorPer = kRorCap / kRorThreads;
-#ifndef AOS_RT_VARIANT   // timing experiments only (tools/ab_rt.sh): 1 = no neighbour scan, 2 = no raster
+#ifndef AOS_RT_VARIANT   // timing experiments only (tools/rorbench): 1 = no neighbour scan, 2 = no raster,
+                         // 3 = load + bin histogram only, 4 = load + counting sort only
 #define AOS_RT_VARIANT 0
 #endif
 
+
+// record i of a neighbour list ending at k1 (a batch of 4 may run past it: those records are not counted).
+// A global list (big tiles) is clamped to stay inside its allocation; a fitting tile's LDS list has 3 records
+// of padding, so the batch reads at one base address with immediate offsets.
+__device__ __forceinline__ float4 rt_at(const float4 *P, int i, int k1) { return P[min(i, k1 - 1)]; }
+struct LdsList { const float4 *p; };
+__device__ __forceinline__ float4 rt_at(LdsList P, int i, int) { return P.p[i]; }
 
 template <class Pts>
 __device__ __forceinline__ int rt_scan(const RorLaunch &L, float4 p, Pts pts, int k0, int k1, int cnt) {
     for (int k = k0; k < k1 && cnt < L.need; k += 4) {
         float4 q[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) q[j] = pts[min(k + j, k1 - 1)];
+        for (int j = 0; j < 4; ++j) q[j] = rt_at(pts, k + j, k1);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) cnt += (k + j < k1 && rt_in(L, p, q[j])) ? 1 : 0;
+        for (int j = 0; j < 4; ++j) cnt += ((k + j < k1) & rt_in(L, p, q[j])) ? 1 : 0;   // (no short circuit: no branch)
     }
     return cnt;
 }
@@ -450,9 +469,9 @@ __device__ __forceinline__ int rt_scan_b(const RorLaunch &L, float4 p, Pts pts, 
     for (; k < k1 && cnt < L.need && budget > 0; k += 4, budget -= 4) {
         float4 q[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) q[j] = pts[min(k + j, k1 - 1)];
+        for (int j = 0; j < 4; ++j) q[j] = rt_at(pts, k + j, k1);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) cnt += (k + j < k1 && rt_in(L, p, q[j])) ? 1 : 0;
+        for (int j = 0; j < 4; ++j) cnt += ((k + j < k1) & rt_in(L, p, q[j])) ? 1 : 0;   // (no short circuit: no branch)
     }
     if (k < k1 && cnt < L.need) budget = -1;   // cut short: undecided
     return cnt;
@@ -655,7 +674,7 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
                                                         const float4 *scratch, uint64_t *rbits,
                                                         unsigned long long *counters, int *kept_tile,
                                                         const int *dirty, BigBufs B) {
-    __shared__ float4 pts[BIG ? 1 : kRorCap];
+    __shared__ float4 pts[BIG ? 1 : kRorCap + 3];   // (+ 3: rt_at's padding)
     __shared__ int bstart[(BIG ? kBigBins : kRtMaxLocalBins) + 1];
     __shared__ unsigned long long win[kRtWinWords];
     __shared__ unsigned kept_wg;
@@ -721,6 +740,7 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
             }
         }
         __syncthreads();
+        if (AOS_RT_VARIANT == 3) return;   // (timing: load + histogram only)
         // exclusive bin offsets: bstart[b] = points in bins < b. Thread t sums a run of kSeg bins,
         // one block scan over the run totals, then each run is written back.
         constexpr int kSeg = (kRtMaxLocalBins + kRorThreads - 1) / kRorThreads;
@@ -755,15 +775,17 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
         for (int j = 0; j < kRorPer; ++j)
             if (rk[j] >= 0) pts[bstart[rt_lbin(L, q[j], bx0, by0, LB)] + rk[j]] = q[j];
         __syncthreads();
+        if (AOS_RT_VARIANT == 4) return;   // (timing: load + counting sort only)
     }
     float4 *P = const_cast<float4 *>(scratch) + a;
     unsigned kept_n = 0;
     // w: 0 a neighbour only, 1 a candidate, 2 a candidate a streaming map already found kept (the keep
     // decision is monotone as points are added: it stays kept, its cell is already in the raster)
     const bool store = kept_tile != nullptr;
+    const double res_d = (double)L.res, inv_res = 1.0 / res_d;
     auto prev_kept = [&](float4 p) {   // kept in an earlier frame: counted, not re-tested
-        const int gx = (int)(((double)p.x - L.origin_x) / (double)L.res);
-        const int gy = (int)(((double)p.y - L.origin_y) / (double)L.res);
+        const int gx = rt_cell((double)p.x - L.origin_x, res_d, inv_res);
+        const int gy = rt_cell((double)p.y - L.origin_y, res_d, inv_res);
         const int cx = min(max(gx, 0), L.W - 1), cy = min(max(gy, 0), L.H - 1);
         if (cx >= L.rx0 && cx < L.rx1 && cy >= L.ry0 && cy < L.ry1) ++kept_n;
     };
@@ -773,8 +795,8 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
             else pts[k].w = __int_as_float(2);
         }
         // kept: counted iff its clamped cell is owned, rastered iff inside the grid (seed_gen:606-619)
-        const int gx = (int)(((double)p.x - L.origin_x) / (double)L.res);
-        const int gy = (int)(((double)p.y - L.origin_y) / (double)L.res);
+        const int gx = rt_cell((double)p.x - L.origin_x, res_d, inv_res);
+        const int gy = rt_cell((double)p.y - L.origin_y, res_d, inv_res);
         const int cx = min(max(gx, 0), L.W - 1), cy = min(max(gy, 0), L.H - 1);
         if (cx < L.rx0 || cx >= L.rx1 || cy < L.ry0 || cy >= L.ry1) return;
         ++kept_n;
@@ -821,7 +843,7 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
         for (int i = 0; i < nr && cnt < L.need && budget >= 0; ++i) {
             int r0, r1;
             range(counted, lx, ly, i, r0, r1);
-            cnt = BIG ? rt_scan_b(L, p, P, r0, r1, cnt, budget) : rt_scan_b(L, p, pts, r0, r1, cnt, budget);
+            cnt = BIG ? rt_scan_b(L, p, P, r0, r1, cnt, budget) : rt_scan_b(L, p, LdsList{pts}, r0, r1, cnt, budget);
         }
         if (cnt < L.need && budget < 0) {        // undecided within the budget
             const int slot = atomicAdd(&q_n, 1);
@@ -830,7 +852,7 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
             for (int i = 0; i < nr && cnt < L.need; ++i) {
                 int r0, r1;
                 range(counted, lx, ly, i, r0, r1);
-                cnt = BIG ? rt_scan(L, p, P, r0, r1, cnt) : rt_scan(L, p, pts, r0, r1, cnt);
+                cnt = BIG ? rt_scan(L, p, P, r0, r1, cnt) : rt_scan(L, p, LdsList{pts}, r0, r1, cnt);
             }
         }
         decide(p, k, cnt);
@@ -851,7 +873,7 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
                 for (int r = 0; r < 3 && cnt < L.need && budget >= 0; ++r) {
                     int r0, r1;
                     range(false, lx, ly, r, r0, r1);
-                    cnt = rt_scan_b(L, p, pts, r0, r1, cnt, budget);
+                    cnt = rt_scan_b(L, p, LdsList{pts}, r0, r1, cnt, budget);
                 }
                 if (cnt < L.need && budget < 0) {
                     const int slot = atomicAdd(&q2_n, 1);
@@ -860,7 +882,7 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
                     for (int r = 0; r < 3 && cnt < L.need; ++r) {
                         int r0, r1;
                         range(false, lx, ly, r, r0, r1);
-                        cnt = rt_scan(L, p, pts, r0, r1, cnt);
+                        cnt = rt_scan(L, p, LdsList{pts}, r0, r1, cnt);
                     }
                 }
                 decide(p, k, cnt);

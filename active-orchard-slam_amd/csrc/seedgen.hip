@@ -882,11 +882,9 @@ void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *c
 
     h_row_center = std::move(so.row_center); h_row_start = std::move(so.row_start);
     h_row_end = std::move(so.row_end); h_row_length = std::move(so.row_length);
-    n_virtual = (int)so.virtual_xy.size() / 2; n_ray = (int)so.ray_xy.size() / 2; n_endpoint = (int)so.endpoint_xy.size() / 2;
-    h_voronoi.clear();
-    h_voronoi.insert(h_voronoi.end(), so.virtual_xy.begin(), so.virtual_xy.end());
-    h_voronoi.insert(h_voronoi.end(), so.ray_xy.begin(), so.ray_xy.end());
-    h_voronoi.insert(h_voronoi.end(), so.endpoint_xy.begin(), so.endpoint_xy.end());
+    n_virtual = so.n_virtual; n_ray = so.n_ray; n_endpoint = so.n_endpoint;
+    if (so.n_voronoi) h_voronoi.assign(so.h_voronoi, so.h_voronoi + 2 * (size_t)so.n_voronoi);
+    else h_voronoi.clear();
     h_rows_info = std::move(so.rows_info);
     h_cluster_info = std::move(so.cluster_info);
     n_clusters_all = so.n_clusters_all;
