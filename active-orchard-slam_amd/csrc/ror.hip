@@ -480,9 +480,55 @@ template <class Pts>
 __device__ __forceinline__ int rt_wave_scan(const RorLaunch &L, float4 p, Pts pts, int k0, int k1, int cnt, int lane) {
     for (int base = k0; base < k1 && cnt < L.need; base += 64) {   // (cnt is wave-uniform)
         const int j = base + lane;
-        const bool hit = j < k1 && rt_in(L, p, pts[min(j, k1 - 1)]);
+        const bool hit = (j < k1) & rt_in(L, p, rt_at(pts, min(j, k1 - 1), k1));
         cnt += (int)__popcll(__ballot(hit));
     }
+    return cnt;
+}
+
+// A fitting tile's points in LDS as four arrays (x, y, z, w bits; 16-byte aligned, 4 records of padding):
+// a batch of 4 neighbours is three 16-byte reads from an aligned index, and the squared distances of two
+// neighbours at a time are packed f32 operations (v_pk_add / v_pk_mul: the same IEEE results element by
+// element, in FLANN's order). The batch starts at the aligned index below k0; slots outside [k0, k1) are
+// not counted (the budget only schedules work: it never changes a count).
+#ifndef AOS_RT_SOA
+#define AOS_RT_SOA 0
+#endif
+#ifndef AOS_RT_SOA_BUDGET
+#define AOS_RT_SOA_BUDGET 1
+#endif
+struct LdsSoA { float *x, *y, *z; int *w; };
+__device__ __forceinline__ float4 rt_at(LdsSoA P, int i, int) { return make_float4(P.x[i], P.y[i], P.z[i], __int_as_float(P.w[i])); }
+typedef float rt_f2 __attribute__((ext_vector_type(2)));
+typedef float rt_f4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ int rt_batch4(const RorLaunch &L, rt_f2 px, rt_f2 py, rt_f2 pz, LdsSoA P, int k, int k0, int k1) {
+    const rt_f4 X = *reinterpret_cast<const rt_f4 *>(P.x + k), Y = *reinterpret_cast<const rt_f4 *>(P.y + k),
+                Z = *reinterpret_cast<const rt_f4 *>(P.z + k);
+    rt_f2 dx = px - X.xy, dy = py - Y.xy, dz = pz - Z.xy;
+    rt_f2 a = dx * dx;
+    a = a + dy * dy;
+    a = a + dz * dz;
+    dx = px - X.zw; dy = py - Y.zw; dz = pz - Z.zw;
+    rt_f2 b = dx * dx;
+    b = b + dy * dy;
+    b = b + dz * dz;
+    const float r = L.r2cmp;
+    return (int)((k >= k0) & (k < k1) & (a.x <= r)) + (int)((k + 1 >= k0) & (k + 1 < k1) & (a.y <= r)) +
+           (int)((k + 2 >= k0) & (k + 2 < k1) & (b.x <= r)) + (int)((k + 3 >= k0) & (k + 3 < k1) & (b.y <= r));
+}
+__device__ __forceinline__ int rt_scan(const RorLaunch &L, float4 p, LdsSoA P, int k0, int k1, int cnt) {
+    const rt_f2 px = {p.x, p.x}, py = {p.y, p.y}, pz = {p.z, p.z};
+    for (int k = k0 & ~3; k < k1 && cnt < L.need; k += 4) cnt += rt_batch4(L, px, py, pz, P, k, k0, k1);
+    return cnt;
+}
+__device__ __forceinline__ int rt_scan_b(const RorLaunch &L, float4 p, LdsSoA P, int k0, int k1, int cnt, int &budget) {
+    const rt_f2 px = {p.x, p.x}, py = {p.y, p.y}, pz = {p.z, p.z};
+    int k = k0 & ~3;
+#if AOS_RT_SOA_BUDGET
+    budget += k0 - k;   // the aligned batch's slots below k0 are not the candidate's budget
+#endif
+    for (; k < k1 && cnt < L.need && budget > 0; k += 4, budget -= 4) cnt += rt_batch4(L, px, py, pz, P, k, k0, k1);
+    if (k < k1 && cnt < L.need) budget = -1;   // cut short: undecided
     return cnt;
 }
 #ifndef AOS_RT_BUDGET_LDS
@@ -674,7 +720,21 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
                                                         const float4 *scratch, uint64_t *rbits,
                                                         unsigned long long *counters, int *kept_tile,
                                                         const int *dirty, BigBufs B) {
+#if AOS_RT_SOA
+    __shared__ __attribute__((aligned(16))) float s_x[BIG ? 4 : kRorCap + 4], s_y[BIG ? 4 : kRorCap + 4],
+        s_z[BIG ? 4 : kRorCap + 4];
+    __shared__ int s_w[BIG ? 4 : kRorCap + 4];
+    const LdsSoA LP{s_x, s_y, s_z, s_w};
+    auto lp_get = [&](int k) { return rt_at(LP, k, 0); };
+    auto lp_put = [&](int k, float4 v) { s_x[k] = v.x; s_y[k] = v.y; s_z[k] = v.z; s_w[k] = __float_as_int(v.w); };
+    auto lp_setw = [&](int k, float w) { s_w[k] = __float_as_int(w); };
+#else
     __shared__ float4 pts[BIG ? 1 : kRorCap + 3];   // (+ 3: rt_at's padding)
+    const LdsList LP{pts};
+    auto lp_get = [&](int k) { return pts[k]; };
+    auto lp_put = [&](int k, float4 v) { pts[k] = v; };
+    auto lp_setw = [&](int k, float w) { pts[k].w = w; };
+#endif
     __shared__ int bstart[(BIG ? kBigBins : kRtMaxLocalBins) + 1];
     __shared__ unsigned long long win[kRtWinWords];
     __shared__ unsigned kept_wg;
@@ -773,7 +833,7 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < kRorPer; ++j)
-            if (rk[j] >= 0) pts[bstart[rt_lbin(L, q[j], bx0, by0, LB)] + rk[j]] = q[j];
+            if (rk[j] >= 0) lp_put(bstart[rt_lbin(L, q[j], bx0, by0, LB)] + rk[j], q[j]);
         __syncthreads();
         if (AOS_RT_VARIANT == 4) return;   // (timing: load + counting sort only)
     }
@@ -792,7 +852,7 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
     auto on_kept = [&](float4 p, int k) {
         if (store) {   // remembered in the tile store (written back below)
             if (BIG) P[k].w = __int_as_float(2);   // (neighbour scans of other threads read only x, y, z)
-            else pts[k].w = __int_as_float(2);
+            else lp_setw(k, __int_as_float(2));
         }
         // kept: counted iff its clamped cell is owned, rastered iff inside the grid (seed_gen:606-619)
         const int gx = rt_cell((double)p.x - L.origin_x, res_d, inv_res);
@@ -826,11 +886,11 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
         else if (store) {                       // below need: remember the full count
             const float cw = __int_as_float(1 | kWCounted | (cnt << kWCntShift));
             if (BIG) P[k].w = cw;
-            else pts[k].w = cw;
+            else lp_setw(k, cw);
         }
     };
     for (int k = k0 + tid; k < k1; k += kRorThreads) {
-        const float4 p = BIG ? P[k] : pts[k];
+        const float4 p = BIG ? P[k] : lp_get(k);
         const int w = __float_as_int(p.w), cls = w & kWClass;
         if (!cls) continue;                     // neighbour only
         if (cls == 2) { prev_kept(p); continue; }
@@ -843,7 +903,7 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
         for (int i = 0; i < nr && cnt < L.need && budget >= 0; ++i) {
             int r0, r1;
             range(counted, lx, ly, i, r0, r1);
-            cnt = BIG ? rt_scan_b(L, p, P, r0, r1, cnt, budget) : rt_scan_b(L, p, LdsList{pts}, r0, r1, cnt, budget);
+            cnt = BIG ? rt_scan_b(L, p, P, r0, r1, cnt, budget) : rt_scan_b(L, p, LP, r0, r1, cnt, budget);
         }
         if (cnt < L.need && budget < 0) {        // undecided within the budget
             const int slot = atomicAdd(&q_n, 1);
@@ -852,7 +912,7 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
             for (int i = 0; i < nr && cnt < L.need; ++i) {
                 int r0, r1;
                 range(counted, lx, ly, i, r0, r1);
-                cnt = BIG ? rt_scan(L, p, P, r0, r1, cnt) : rt_scan(L, p, LdsList{pts}, r0, r1, cnt);
+                cnt = BIG ? rt_scan(L, p, P, r0, r1, cnt) : rt_scan(L, p, LP, r0, r1, cnt);
             }
         }
         decide(p, k, cnt);
@@ -865,7 +925,7 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
             // long walks run packed together; the few still undecided after that, one wave each
             for (int i = tid; i < nq; i += kRorThreads) {
                 const int k = q_k[i];
-                const float4 p = pts[k];
+                const float4 p = lp_get(k);
                 int bx, by;
                 rt_bin(L, p.x, p.y, bx, by);
                 const int lx = bx - bx0, ly = by - by0;
@@ -873,7 +933,7 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
                 for (int r = 0; r < 3 && cnt < L.need && budget >= 0; ++r) {
                     int r0, r1;
                     range(false, lx, ly, r, r0, r1);
-                    cnt = rt_scan_b(L, p, LdsList{pts}, r0, r1, cnt, budget);
+                    cnt = rt_scan_b(L, p, LP, r0, r1, cnt, budget);
                 }
                 if (cnt < L.need && budget < 0) {
                     const int slot = atomicAdd(&q2_n, 1);
@@ -882,7 +942,7 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
                     for (int r = 0; r < 3 && cnt < L.need; ++r) {
                         int r0, r1;
                         range(false, lx, ly, r, r0, r1);
-                        cnt = rt_scan(L, p, LdsList{pts}, r0, r1, cnt);
+                        cnt = rt_scan(L, p, LP, r0, r1, cnt);
                     }
                 }
                 decide(p, k, cnt);
@@ -891,7 +951,7 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
             const int nq2 = min(q2_n, kRtQ2Cap);
             for (int i = tid >> 6; i < nq2; i += kRorThreads / 64) {
                 const int k = q2_k[i];
-                const float4 p = pts[k];
+                const float4 p = lp_get(k);
                 int bx, by;
                 rt_bin(L, p.x, p.y, bx, by);
                 const int lx = bx - bx0, ly = by - by0;
@@ -899,14 +959,14 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
                 for (int r = 0; r < 3 && cnt < L.need; ++r) {
                     int r0, r1;
                     range(false, lx, ly, r, r0, r1);
-                    cnt = rt_wave_scan(L, p, pts, r0, r1, cnt, lane);
+                    cnt = rt_wave_scan(L, p, LP, r0, r1, cnt, lane);
                 }
                 if (lane == 0) decide(p, k, cnt);
             }
         } else   // big tiles: one wave each
         for (int i = tid >> 6; i < nq; i += kRorThreads / 64) {
             const int k = q_k[i];
-            const float4 p = BIG ? P[k] : pts[k];
+            const float4 p = BIG ? P[k] : lp_get(k);
             const int w = __float_as_int(p.w);
             int bx, by;
             rt_bin(L, p.x, p.y, bx, by);
@@ -916,7 +976,7 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
             for (int r = 0; r < (counted ? 9 : 3) && cnt < L.need; ++r) {
                 int r0, r1;
                 range(counted, lx, ly, r, r0, r1);
-                cnt = BIG ? rt_wave_scan(L, p, P, r0, r1, cnt, lane) : rt_wave_scan(L, p, pts, r0, r1, cnt, lane);
+                cnt = BIG ? rt_wave_scan(L, p, P, r0, r1, cnt, lane) : rt_wave_scan(L, p, LP, r0, r1, cnt, lane);
             }
             if (lane == 0) decide(p, k, cnt);
         }
@@ -926,7 +986,7 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
     // fitting tile rewrites its list, a big tile's chunk its range of the sorted scratch list
     if (store)
         for (int k = k0 + tid; k < k1; k += kRorThreads) {
-            float4 v = BIG ? P[k] : pts[k];
+            float4 v = BIG ? P[k] : lp_get(k);
             v.w = __int_as_float(__float_as_int(v.w) | kWOld);
             staged[a + k] = v;
         }

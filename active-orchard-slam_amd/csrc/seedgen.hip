@@ -71,6 +71,13 @@ int aos_ctx::up_threads() {
     return n;
 }
 
+// AOS_STAGED_TOUCH: 1 (default) the staged array is read while the upload DMAs run; 2 on a side stream beside
+// the count pass, after the upload (A/B); 0 never
+static int staged_touch_mode() {
+    static const int m = [] { const char *e = getenv("AOS_STAGED_TOUCH"); return e ? atoi(e) : 1; }();
+    return m;
+}
+
 void aos_ctx::upload_pack(void *dst, const aos_cloud_view &v, bool prefetch) {
     // chunks of AOS_UP_CHUNK_KB (default 2 MB): the last DMAs start soon after the last gather, so the upload
     // ends ~one chunk's DMA after the gather instead of one slot per thread later (8 MB slots: ~1 ms)
@@ -94,8 +101,7 @@ void aos_ctx::upload_pack(void *dst, const aos_cloud_view &v, bool prefetch) {
         AOS_HIP(hipEventRecord(ev[15], stream));
         // while the DMAs run (they wait for ev[15] only): the last frame's staged array is read once so that
         // the scatter's partial-line writes hit the Infinity Cache (launch_rt_touch)
-        static const bool touch = [] { const char *e = getenv("AOS_STAGED_TOUCH"); return !e || atoi(e) != 0; }();
-        if (touch && ror_staged_max > 0)
+        if (staged_touch_mode() == 1 && ror_staged_max > 0)
             launch_rt_touch(sorted.as<float4>(), std::min(sorted.cap / sizeof(float4), (size_t)ror_staged_max), stream);
     }
     const uint64_t per = (n + nth - 1) / nth;
@@ -428,9 +434,21 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
     // no keepable candidate either: the local test is exact.
     const bool any = n_points > 0 && !(is_dense && n_points < (uint64_t)L.need);
     if (!any) return;
+    const bool side_touch = staged_touch_mode() == 2 && !map_mode && ror_staged_max > 0;
+    if (side_touch) {   // (A/B: the staged array's read-ahead beside the count pass)
+        if (!copy_stream) {
+            AOS_HIP(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
+            AOS_HIP(hipEventCreateWithFlags(&copy_ready, hipEventDisableTiming));
+        }
+        AOS_HIP(hipEventRecord(copy_ready, s));
+        AOS_HIP(hipStreamWaitEvent(copy_stream, copy_ready, 0));
+        launch_rt_touch(sorted.as<float4>(), std::min(sorted.cap / sizeof(float4), (size_t)ror_staged_max), copy_stream);
+        AOS_HIP(hipEventRecord(copy_ready, copy_stream));
+    }
     AOS_HIP(hipEventRecord(ev[12], s));
     launch_rt_count(L, d_H, G, d_ts, d_own, ror_lookback(L, G, d_own), s);
     AOS_HIP(hipEventRecord(ev[13], s));
+    if (side_touch) AOS_HIP(hipStreamWaitEvent(s, copy_ready, 0));
     // The staged array holds own + halo copies. With a capacity from an earlier frame the scatter
     // runs at once and reports an overflow (the frame is then redone with the size it read back,
     // run_seedgen); without one, or when the caller cannot redo (a tiled frame), the size is read
