@@ -9,6 +9,7 @@
 #include <atomic>
 #include <climits>
 #include <cmath>
+#include <cstdlib>
 #include <exception>
 #include <mutex>
 #include <numeric>
@@ -29,8 +30,50 @@ constexpr int kReplayThreads = 8;   // host threads for the exact BFS replays of
 // (float centre sums :1030-1046, first-strict-maximum endpoints :1354-1395) for the rare clusters
 // without the order-free certificate. This is a serial chain of dependent steps: it runs on the host
 // core next to the GPU (the cluster's cells come over in raster order), ~10 ns per step.
-static void host_bfs_replay(const int *cells, int n, const GridC &g, const double *poly, int np, float min_length,
-                            ClusterRec &r, std::vector<int> &q, std::vector<int> &tab) {
+// The FIFO BFS over the cluster's cells from its smallest (first raster) cell, into q. Membership and the
+// visited marks live in a bitmap over the cluster's bounding box when that box is small against n (row
+// clusters: a few cells wide), else in an open-addressing hash of the cells: the same order either way.
+static void bfs_order(const int *cells, int n, const GridC &g, std::vector<int> &q, std::vector<int> &tab,
+                      std::vector<uint64_t> &bm) {
+    const int dxs[8] = {-1, -1, -1, 0, 0, 1, 1, 1}, dys[8] = {-1, 0, 1, -1, 1, -1, 0, 1};
+    q.resize(n);
+    int start = cells[0], x0 = INT_MAX, x1 = INT_MIN, y0 = INT_MAX, y1 = INT_MIN;
+    for (int k = 0; k < n; ++k) {
+        const int p = cells[k], y = p / g.W, x = p - y * g.W;
+        start = std::min(start, p);
+        x0 = std::min(x0, x); x1 = std::max(x1, x); y0 = std::min(y0, y); y1 = std::max(y1, y);
+    }
+    const long long bw = (long long)x1 - x0 + 1, area = bw * ((long long)y1 - y0 + 1);
+    static const bool force_hash = [] { const char *e = getenv("AOS_REPLAY_HASH"); return e && atoi(e) != 0; }();
+    if (!force_hash && area <= std::max<long long>(64ll * n, 1 << 16)) {   // (AOS_REPLAY_HASH=1: tests)
+        bm.assign((size_t)((area + 63) / 64), 0ull);
+        auto bit = [&](int x, int y) { return (long long)(y - y0) * bw + (x - x0); };
+        for (int k = 0; k < n; ++k) {
+            const int p = cells[k], y = p / g.W, x = p - y * g.W;
+            const long long b = bit(x, y);
+            bm[(size_t)(b >> 6)] |= 1ull << (b & 63);
+        }
+        const long long b0 = bit(start % g.W, start / g.W);
+        bm[(size_t)(b0 >> 6)] &= ~(1ull << (b0 & 63));   // set bit = in the cluster, not yet queued
+        q[0] = start;
+        int head = 0, tail = 1;
+        while (head < tail) {
+            const int p = q[head++], cy = p / g.W, cx = p - cy * g.W;
+            for (int i = 0; i < 8; ++i) {
+                const int nx = cx + dxs[i], ny = cy + dys[i];
+                if (nx < x0 || nx > x1 || ny < y0 || ny > y1) continue;
+                const long long b = bit(nx, ny);
+                uint64_t &w = bm[(size_t)(b >> 6)];
+                const uint64_t m = 1ull << (b & 63);
+                if (!(w & m)) continue;
+                w &= ~m;
+                if (tail >= n) throw std::runtime_error("BFS replay: cluster cells repeat");
+                q[tail++] = ny * g.W + nx;
+            }
+        }
+        if (tail != n) throw std::runtime_error("BFS replay: cluster is not 8-connected");
+        return;
+    }
     int cap = 64;
     while (cap < 2 * n) cap <<= 1;
     const unsigned mask = (unsigned)cap - 1;
@@ -49,13 +92,9 @@ static void host_bfs_replay(const int *cells, int n, const GridC &g, const doubl
         while (tab[h] != -1) h = (h + 1) & mask;
         tab[h] = cells[k];
     }
-    q.resize(n);
-    int start = cells[0];   // first raster cell of the component (the cells come in any order)
-    for (int k = 1; k < n; ++k) start = std::min(start, cells[k]);
-    tab[slot_of(start)] |= (int)0x80000000;
+    tab[slot_of(start)] |= (int)0x80000000;   // (start: the first raster cell; the cells come in any order)
     q[0] = start;
     int head = 0, tail = 1;
-    const int dxs[8] = {-1, -1, -1, 0, 0, 1, 1, 1}, dys[8] = {-1, 0, 1, -1, 1, -1, 0, 1};
     while (head < tail) {
         const int p = q[head++], cy = p / g.W, cx = p - cy * g.W;
         for (int i = 0; i < 8; ++i) {
@@ -68,6 +107,11 @@ static void host_bfs_replay(const int *cells, int n, const GridC &g, const doubl
         }
     }
     if (tail != n) throw std::runtime_error("BFS replay: cluster is not 8-connected");
+}
+
+static void host_bfs_replay(const int *cells, int n, const GridC &g, const double *poly, int np, float min_length,
+                            ClusterRec &r, std::vector<int> &q, std::vector<int> &tab, std::vector<uint64_t> &bm) {
+    bfs_order(cells, n, g, q, tab, bm);
     float sum_x = 0.0f, sum_y = 0.0f;
     for (int k = 0; k < n; ++k) { int p = q[k], y = p / g.W; sum_x += (float)(p - y * g.W); sum_y += (float)y; }
     r.cx = sum_x / (float)n;
@@ -119,10 +163,11 @@ void replay_clusters(const std::vector<ReplayJob> &jobs, const GridC &g, const d
     std::mutex mu;
     auto work = [&]() {
         std::vector<int> q, tab;
+        std::vector<uint64_t> bm;
         for (int i; (i = next.fetch_add(1)) < (int)jobs.size();) {
             const ReplayJob &j = jobs[i];
             try {
-                host_bfs_replay(j.cells, j.n, g, poly, np, min_len, rec[j.c], q, tab);
+                host_bfs_replay(j.cells, j.n, g, poly, np, min_len, rec[j.c], q, tab, bm);
             } catch (...) {
                 std::lock_guard<std::mutex> lk(mu);
                 if (!err) err = std::current_exception();

@@ -44,10 +44,10 @@ def test_host_subdiv2d_under_asan_ubsan(built):
     assert "0 failed so far" in out.splitlines()[-1]
 
 
-def _cluster_run(built, mode, blob, tmp_path):
+def _cluster_run(built, mode, blob, tmp_path, env=None):
     fi, fo = tmp_path / f"in_{mode}.bin", tmp_path / f"out_{mode}.bin"
     fi.write_bytes(blob)
-    out = _run([os.path.join(built, "san_cluster"), mode, str(fi), str(fo)])
+    out = _run([os.path.join(built, "san_cluster"), mode, str(fi), str(fo)], env=env)
     assert f"san_cluster {mode} ok" in out
     return fo.read_bytes()
 
@@ -78,9 +78,12 @@ def test_cluster_union_under_asan_ubsan(built, tiles, tmp_path):
     assert ncl == n and np.array_equal(pc, cid_map[root // W, root % W])
 
 
-def test_cluster_replays_and_rows_under_asan_ubsan(built, tmp_path):
+@pytest.mark.parametrize("visited", ["bitmap", "hash"])
+def test_cluster_replays_and_rows_under_asan_ubsan(built, tmp_path, visited):
     """Every cluster of a C1 frame through the exact BFS replay (cells shuffled: the replay starts from the
-    smallest) and the row assembly, vs the oracle's cluster centres, rows, rows_info and cluster_info."""
+    smallest) and the row assembly, vs the oracle's cluster centres, rows, rows_info and cluster_info; with
+    the visited marks in the bounding-box bitmap (the product's choice at C1) and in the hash
+    (AOS_REPLAY_HASH=1, the choice for clusters whose box is large against their size)."""
     import oracle_py as O
     import orchard
     cfg = orchard.CONFIGS["C1"]
@@ -98,7 +101,7 @@ def test_cluster_replays_and_rows_under_asan_ubsan(built, tmp_path):
         lin = (xy[:, 1].astype(np.int64) * W + xy[:, 0]).astype(np.int32)
         rng.shuffle(lin)
         blob += np.int32(len(lin)).tobytes() + np.float32(o["cluster_length"][c]).tobytes() + lin.tobytes()
-    raw = _cluster_run(built, "R", blob, tmp_path)
+    raw = _cluster_run(built, "R", blob, tmp_path, env={"AOS_REPLAY_HASH": "1" if visited == "hash" else "0"})
     ncl = len(off) - 1
     rec = np.frombuffer(raw[:ncl * 60], dtype=np.dtype([("flags", "<i4"), ("cx", "<f4"), ("cy", "<f4"),
                                                         ("c", "<f8", 6)]))
