@@ -47,6 +47,9 @@ __device__ __forceinline__ bool bit_at(const uint64_t *bits, int WW, int x, int 
 __device__ __forceinline__ int ld_parent(int *parent, int i) {
     return __hip_atomic_load(&parent[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// root of x. (Round 4 measured path halving here, ECL-CC style: the C2 flatten got shallower trees,
+// 53 -> 23 us, but the halving stores made the union kernel 139 -> 247 us: every walker's agent-scope
+// store and load goes past the XCD's L2. Not adopted.)
 __device__ __forceinline__ int uf_find(int *parent, int x) {
     while (true) {
         int p = ld_parent(parent, x);

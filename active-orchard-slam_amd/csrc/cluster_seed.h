@@ -81,6 +81,7 @@ void dedup_check(DedupScratch &S, int err_word);
 struct ClusterSeedState {
     DedupScratch dedup;
     DevBuf fg_bits, word_cnt, word_off, fg_list, parent, root_flag, root_rank, cl_count, cl_off, cl_cursor, cl_cells;
+    DevBuf ccl_edges;   // k_ccl_local's cross-chunk links: count, pad, then (i, j) pairs
     DevBuf rec, row_idx, poly, cur_tab;
     DevBuf cand_xy, cand_ok, cand_state, hash_count, hash_start, hash_slot, hash_sorted, seed_out, misc, scan_tmp;
     LookBackScratch lb;           // the stage's single-pass scans

@@ -38,9 +38,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 WATCHDOG_EXIT = 3      # exit status of a run whose tiled section hung (its watchdog fired)
 # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE summaries (tools/pmc_traffic.py) of the ROR stage, per config,
 # for the kernels of this build's ROR design. A config or design without a committed PMC run gets null.
-ROR_DESIGN = "r03"
+ROR_DESIGN = "r04"
 PMC_FILES = {("C2", "r02"): os.path.join(ROOT, "profiles", "r02q_pmc_traffic.json"),
-             ("C2", "r03"): os.path.join(ROOT, "profiles", "r03fin_pmc_traffic.json")}
+             ("C2", "r03"): os.path.join(ROOT, "profiles", "r03fin_pmc_traffic.json"),
+             ("C2", "r04"): os.path.join(ROOT, "profiles", "r04i_pmc_traffic.json")}
 
 
 def parse(argv=None):
