@@ -15,6 +15,7 @@
 // conflicting candidate is removed, removed once one of them is kept).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <stdexcept>
@@ -93,7 +94,9 @@ __global__ void k_ccl_union(const int *list, int n, const uint64_t *fg, const in
 // global index of its chunk root; links into an earlier chunk are appended to a cross-edge list that
 // k_ccl_cross then unions globally (C2: ~10^4 edges instead of ~10^6 global unions). The smaller index is
 // always the root, as in k_ccl_union, so the roots and the flattened labels are the same.
-constexpr int kCclChunk = 2048, kCclTB = 256;
+// chunk and block size (AOS_CCL_CHUNK / AOS_CCL_TB override them for A/B runs)
+static int ccl_chunk() { static const int v = [] { const char *e = getenv("AOS_CCL_CHUNK"); return e ? std::max(64, std::min(16384, atoi(e))) : 2048; }(); return v; }
+static int ccl_tb() { static const int v = [] { const char *e = getenv("AOS_CCL_TB"); return e ? std::max(64, std::min(1024, atoi(e))) / 64 * 64 : 256; }(); return v; }
 __device__ __forceinline__ int lds_find(int *lp, int x) {
     for (int p; (p = __hip_atomic_load(&lp[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != x;) x = p;
     return x;
@@ -108,14 +111,14 @@ __device__ __forceinline__ void lds_union(int *lp, int i, int j) {
         b = lds_find(lp, b);
     }
 }
-__global__ __launch_bounds__(kCclTB) void k_ccl_local(const int *list, int n, const uint64_t *fg, const int *off, GridC g,
-                                                      int *parent, int2 *edges, int *n_edges, int cap) {
-    __shared__ int lp[kCclChunk];
-    const int base = blockIdx.x * kCclChunk, m = min(kCclChunk, n - base);
-    for (int i = threadIdx.x; i < m; i += kCclTB) lp[i] = i;
+__global__ __launch_bounds__(1024) void k_ccl_local(const int *list, int n, const uint64_t *fg, const int *off, GridC g,
+                                                    int *parent, int2 *edges, int *n_edges, int cap, int chunk) {
+    extern __shared__ int lp[];   // [chunk]
+    const int base = blockIdx.x * chunk, m = min(chunk, n - base), nt = blockDim.x;
+    for (int i = threadIdx.x; i < m; i += nt) lp[i] = i;
     __syncthreads();
     const int ndx[4] = {-1, 0, 1, -1}, ndy[4] = {-1, -1, -1, 0};
-    for (int i = threadIdx.x; i < m; i += kCclTB) {
+    for (int i = threadIdx.x; i < m; i += nt) {
         const int p = list[base + i], y = p / g.W, x = p - y * g.W;
         for (int k = 0; k < 4; ++k) {
             const int j = fg_index(fg, off, g, x + ndx[k], y + ndy[k]);   // (a raster predecessor: j < base + i)
@@ -129,7 +132,7 @@ __global__ __launch_bounds__(kCclTB) void k_ccl_local(const int *list, int n, co
         }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < m; i += kCclTB) parent[base + i] = base + lds_find(lp, i);
+    for (int i = threadIdx.x; i < m; i += nt) parent[base + i] = base + lds_find(lp, i);
 }
 __global__ void k_ccl_cross(const int2 *edges, const int *n_edges, int cap, int *parent) {
     const int ne = min(*n_edges, cap);
@@ -591,7 +594,9 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         int *d_ne = dev<int>(S.ccl_edges, 2 + 2 * (size_t)ecap);
         int2 *d_edges = reinterpret_cast<int2 *>(d_ne + 2);   // (8-byte aligned: DevBuf bases are)
         AOS_HIP(hipMemsetAsync(d_ne, 0, sizeof(int), s));
-        k_ccl_local<<<cdiv(nf, kCclChunk), kCclTB, 0, s>>>(d_list, nf, d_fg, d_wo, g, d_par, d_edges, d_ne, ecap - 1);
+        const int chunk = ccl_chunk();
+        k_ccl_local<<<cdiv(nf, chunk), ccl_tb(), sizeof(int) * chunk, s>>>(d_list, nf, d_fg, d_wo, g, d_par, d_edges, d_ne,
+                                                                          ecap - 1, chunk);
         k_ccl_cross<<<256, 256, 0, s>>>(d_edges, d_ne, ecap - 1, d_par);
         k_ccl_union_if<<<cdiv(nf, 256), 256, 0, s>>>(d_list, nf, d_fg, d_wo, g, d_par, d_ne, ecap - 1);
         k_ccl_flatten<<<cdiv(nf, 256), 256, 0, s>>>(d_par, d_isroot, nf);
