@@ -225,7 +225,7 @@ struct MinOp { template <class T> __device__ T operator()(T a, T b) const { retu
 struct AddOp { template <class T> __device__ T operator()(T a, T b) const { return a + b; } };
 
 // one workgroup per cluster
-__global__ __launch_bounds__(256) void k_cluster_stats(StatArgs A) {
+__global__ __launch_bounds__(512) void k_cluster_stats(StatArgs A) {   // (512 threads: the long row clusters set its time)
     __shared__ long long shl[8];
     __shared__ int shi[8];
     __shared__ double shd[8];
@@ -384,7 +384,7 @@ void launch_cluster_stats(const int *off, const int *cells, int n_clusters, cons
                           float min_length, ClusterRec *rec, hipStream_t s) {
     if (n_clusters <= 0) return;
     StatArgs A{off, cells, nullptr, n_clusters, g, poly, np, min_length, rec};
-    k_cluster_stats<<<n_clusters, 256, 0, s>>>(A);
+    k_cluster_stats<<<n_clusters, 512, 0, s>>>(A);
     AOS_HIP(hipGetLastError());
 }
 

@@ -486,51 +486,6 @@ __device__ __forceinline__ int rt_wave_scan(const RorLaunch &L, float4 p, Pts pt
     return cnt;
 }
 
-// A fitting tile's points in LDS as four arrays (x, y, z, w bits; 16-byte aligned, 4 records of padding):
-// a batch of 4 neighbours is three 16-byte reads from an aligned index, and the squared distances of two
-// neighbours at a time are packed f32 operations (v_pk_add / v_pk_mul: the same IEEE results element by
-// element, in FLANN's order). The batch starts at the aligned index below k0; slots outside [k0, k1) are
-// not counted (the budget only schedules work: it never changes a count).
-#ifndef AOS_RT_SOA
-#define AOS_RT_SOA 0
-#endif
-#ifndef AOS_RT_SOA_BUDGET
-#define AOS_RT_SOA_BUDGET 1
-#endif
-struct LdsSoA { float *x, *y, *z; int *w; };
-__device__ __forceinline__ float4 rt_at(LdsSoA P, int i, int) { return make_float4(P.x[i], P.y[i], P.z[i], __int_as_float(P.w[i])); }
-typedef float rt_f2 __attribute__((ext_vector_type(2)));
-typedef float rt_f4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ int rt_batch4(const RorLaunch &L, rt_f2 px, rt_f2 py, rt_f2 pz, LdsSoA P, int k, int k0, int k1) {
-    const rt_f4 X = *reinterpret_cast<const rt_f4 *>(P.x + k), Y = *reinterpret_cast<const rt_f4 *>(P.y + k),
-                Z = *reinterpret_cast<const rt_f4 *>(P.z + k);
-    rt_f2 dx = px - X.xy, dy = py - Y.xy, dz = pz - Z.xy;
-    rt_f2 a = dx * dx;
-    a = a + dy * dy;
-    a = a + dz * dz;
-    dx = px - X.zw; dy = py - Y.zw; dz = pz - Z.zw;
-    rt_f2 b = dx * dx;
-    b = b + dy * dy;
-    b = b + dz * dz;
-    const float r = L.r2cmp;
-    return (int)((k >= k0) & (k < k1) & (a.x <= r)) + (int)((k + 1 >= k0) & (k + 1 < k1) & (a.y <= r)) +
-           (int)((k + 2 >= k0) & (k + 2 < k1) & (b.x <= r)) + (int)((k + 3 >= k0) & (k + 3 < k1) & (b.y <= r));
-}
-__device__ __forceinline__ int rt_scan(const RorLaunch &L, float4 p, LdsSoA P, int k0, int k1, int cnt) {
-    const rt_f2 px = {p.x, p.x}, py = {p.y, p.y}, pz = {p.z, p.z};
-    for (int k = k0 & ~3; k < k1 && cnt < L.need; k += 4) cnt += rt_batch4(L, px, py, pz, P, k, k0, k1);
-    return cnt;
-}
-__device__ __forceinline__ int rt_scan_b(const RorLaunch &L, float4 p, LdsSoA P, int k0, int k1, int cnt, int &budget) {
-    const rt_f2 px = {p.x, p.x}, py = {p.y, p.y}, pz = {p.z, p.z};
-    int k = k0 & ~3;
-#if AOS_RT_SOA_BUDGET
-    budget += k0 - k;   // the aligned batch's slots below k0 are not the candidate's budget
-#endif
-    for (; k < k1 && cnt < L.need && budget > 0; k += 4, budget -= 4) cnt += rt_batch4(L, px, py, pz, P, k, k0, k1);
-    if (k < k1 && cnt < L.need) budget = -1;   // cut short: undecided
-    return cnt;
-}
 #ifndef AOS_RT_BUDGET_LDS
 #define AOS_RT_BUDGET_LDS 12
 #endif
@@ -720,21 +675,11 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
                                                         const float4 *scratch, uint64_t *rbits,
                                                         unsigned long long *counters, int *kept_tile,
                                                         const int *dirty, BigBufs B) {
-#if AOS_RT_SOA
-    __shared__ __attribute__((aligned(16))) float s_x[BIG ? 4 : kRorCap + 4], s_y[BIG ? 4 : kRorCap + 4],
-        s_z[BIG ? 4 : kRorCap + 4];
-    __shared__ int s_w[BIG ? 4 : kRorCap + 4];
-    const LdsSoA LP{s_x, s_y, s_z, s_w};
-    auto lp_get = [&](int k) { return rt_at(LP, k, 0); };
-    auto lp_put = [&](int k, float4 v) { s_x[k] = v.x; s_y[k] = v.y; s_z[k] = v.z; s_w[k] = __float_as_int(v.w); };
-    auto lp_setw = [&](int k, float w) { s_w[k] = __float_as_int(w); };
-#else
     __shared__ float4 pts[BIG ? 1 : kRorCap + 3];   // (+ 3: rt_at's padding)
     const LdsList LP{pts};
     auto lp_get = [&](int k) { return pts[k]; };
     auto lp_put = [&](int k, float4 v) { pts[k] = v; };
     auto lp_setw = [&](int k, float w) { pts[k].w = w; };
-#endif
     __shared__ int bstart[(BIG ? kBigBins : kRtMaxLocalBins) + 1];
     __shared__ unsigned long long win[kRtWinWords];
     __shared__ unsigned kept_wg;

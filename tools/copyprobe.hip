@@ -13,6 +13,9 @@
 
 // ~20 µs of streaming work over 4 MB (like k_fg over the skeleton bits + polygon tests)
 __global__ void k_peek1(int *h, const int *d) { if (threadIdx.x == 0) *h = *d; }
+__global__ void k_copy16(uint4 *h, const uint4 *d, size_t n) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) h[i] = d[i];
+}
 __global__ void k_work(const unsigned long long *in, unsigned long long *out, size_t n, int reps) {
     const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -97,6 +100,32 @@ extern "C" int copyprobe_main(int argc, char **argv) {
             CK(hipDeviceSynchronize());
             if (r >= 2) (mode ? t_peek : t_small) += us / reps;
         }
+    }
+    // the big copy as a kernel of G workgroups storing into pinned host memory, alone and beside k_work
+    for (int G : {8, 16, 32, 64, 256}) {
+        float tca = 0, tcb = 0, tkb2 = 0;
+        for (int r = 0; r < reps + 2; ++r) {
+            float a, b;
+            CK(hipEventRecord(c0, sc));
+            k_copy16<<<G, 256, 0, sc>>>(static_cast<uint4 *>(h), static_cast<const uint4 *>(d), bytes / 16);
+            CK(hipEventRecord(c1, sc));
+            CK(hipStreamSynchronize(sc));
+            CK(hipEventElapsedTime(&a, c0, c1));
+            if (r >= 2) tca += a / reps;
+            CK(hipEventRecord(c0, sc));
+            k_copy16<<<G, 256, 0, sc>>>(static_cast<uint4 *>(h), static_cast<const uint4 *>(d), bytes / 16);
+            CK(hipEventRecord(c1, sc));
+            CK(hipStreamWaitEvent(sk, c0, 0));
+            CK(hipEventRecord(k0, sk));
+            k_work<<<nw / 256, 256, 0, sk>>>(wi, wo, nw, 64);
+            CK(hipEventRecord(k1, sk));
+            CK(hipDeviceSynchronize());
+            CK(hipEventElapsedTime(&a, c0, c1));
+            CK(hipEventElapsedTime(&b, k0, k1));
+            if (r >= 2) { tcb += a / reps; tkb2 += b / reps; }
+        }
+        printf("kernel copy G %3d: alone %.1f us (%.1f GB/s); beside k_work: copy %.1f us, k_work %.1f us\n", G, 1e3 * tca,
+               bytes / (tca * 1e-3) / 1e9, 1e3 * tcb, 1e3 * tkb2);
     }
     printf("4-byte read-back beside the big copy: hipMemcpyAsync %.1f us, peek kernel %.1f us\n", t_small, t_peek);
     printf("event-chained: copy %.1f us, kernel after the copy's start %.1f us\n", 1e3 * tpc, 1e3 * tpk);
