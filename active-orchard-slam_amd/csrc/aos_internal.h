@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdio>
 #include <string>
 #include <utility>
 #include <vector>
@@ -41,6 +42,20 @@ struct DeviceScope {
 // with its host time, against the process-wide trace clock (trace_ms)
 double trace_ms();
 bool trace_on();
+// AOS_TRACE=1: a stage's host timeline on stderr (ms since the stage started, at each host sync)
+struct HostTrace {
+    const char *tag;
+    const bool on = trace_on();
+    const double t0 = on ? trace_ms() : 0.0;
+    std::string line;
+    void mark(const char *what) {
+        if (!on) return;
+        char b[64];
+        snprintf(b, sizeof(b), " %s %.3f", what, trace_ms() - t0);
+        line += b;
+    }
+    ~HostTrace() { if (on) fprintf(stderr, "[aos trace %s] at %.2f:%s\n", tag, t0, line.c_str()); }
+};
 void trace_alloc(const char *kind, size_t bytes, double t0);
 // Owning, growable device allocation (freed on destruction; not copyable).
 struct DevBuf {
@@ -153,6 +168,8 @@ void launch_pack_xyz_box(const uint8_t *cloud, uint64_t n, uint32_t step, uint32
                          const float box[4], float4 *out, unsigned long long *count, hipStream_t s);
 void launch_inflate(const uint64_t *in, uint64_t *out, const FrameGeom &g, hipStream_t s);
 void launch_bits_to_bytes(const uint64_t *bits, int8_t *out, const FrameGeom &g, int frame, hipStream_t s);
+// int8 {0,100} grid (C bytes) -> ceil(C / 64) words of bits; a byte that is neither sets *err
+void launch_pack_grid(const int8_t *g, size_t C, uint64_t *bits, int *err, hipStream_t s);
 void launch_open(const uint64_t *in, uint64_t *out, const FrameGeom &g, hipStream_t s);
 // Zhang-Suen temporal block: KIT iterations per launch; flags[0] = non-empty after iteration 1,
 // flags[1 + k] = iteration k (0-based) deleted something.

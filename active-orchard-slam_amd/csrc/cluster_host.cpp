@@ -134,9 +134,10 @@ static void host_bfs_replay(const int *cells, int n, const GridC &g, const doubl
             if (k == fi) continue;
             double2 w = cell_w(g, q[k]);
             double dx = w.x - r.center.x, dy = w.y - r.center.y, d2 = dx * dx + dy * dy;
+            if (!(d2 > mo)) continue;   // (the same test, its cheap half first: the normalisation only for a new max)
             double nx = dx, ny = dy;
             if (d2 > 0.0) { double s = std::sqrt(d2); nx = dx / s; ny = dy / s; }
-            if (nx * fx + ny * fy < 0.0 && d2 > mo) { mo = d2; si = k; }
+            if (nx * fx + ny * fy < 0.0) { mo = d2; si = k; }
         }
         if (mo == 0.0) {
             double2 wf = cell_w(g, q[fi]);

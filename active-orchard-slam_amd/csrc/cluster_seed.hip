@@ -549,6 +549,7 @@ __global__ void k_concat3(const double2 *a, const double2 *b, const double2 *c, 
 template <class T> static T *dev(DevBuf &b, size_t n) { return static_cast<T *>(b.ensure(sizeof(T) * std::max<size_t>(n, 1))); }
 
 void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStageOut &out, hipStream_t s, hipEvent_t ev_mid) {
+    HostTrace tr{"cluster"};
     const FrameGeom &fg = *in.g;
     const GridC g = make_gridc(fg);
     const Poly &poly = *in.poly;
@@ -574,6 +575,7 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         scan_1p(S.lb, d_wc, d_wo, (int)Cw, false, s);
         peek_to_host(h_sc, {d_wo + Cw, S.lb.err_word(s)}, s);
         S.dedup.sev.sync(s);
+        tr.mark("fg");
         if (h_sc[1]) throw std::runtime_error("cluster stage: scan failed on the device");
     }
     const int nf = in.pre ? in.pre->n_fg : h_sc[0];
@@ -603,6 +605,7 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         scan_1p(S.lb, d_isroot, d_rank, nf, false, s);
         peek_to_host(h_sc, {d_rank + nf, S.lb.err_word(s)}, s);
         S.dedup.sev.sync(s);
+        tr.mark("roots");
         if (h_sc[1]) throw std::runtime_error("cluster stage: scan failed on the device");
         const int ncl = h_sc[0];
         S.n_clusters = ncl;
@@ -624,6 +627,7 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         ClusterRec *hr = static_cast<ClusterRec *>(S.h_recbuf.ensure(sizeof(ClusterRec) * (size_t)ncl));
         copy_to_host(hr, d_rec, sizeof(ClusterRec) * ncl, s);
         S.dedup.sev.sync(s);
+        tr.mark("recs");
         std::copy(hr, hr + ncl, S.h_rec.begin());
         int n_bfs = 0;
         for (const auto &r : S.h_rec) n_bfs += (r.flags & 2) != 0;
@@ -641,12 +645,15 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
             int *hc = static_cast<int *>(S.h_cells.ensure(sizeof(int) * (size_t)(hi - lo)));
             copy_to_host(hc, d_cells + lo, sizeof(int) * (hi - lo), s);
             S.dedup.sev.sync(s);
+            tr.mark("cells");
             std::vector<ReplayJob> jobs;
             for (int c : ids) jobs.push_back({c, hc + (off[c] - lo), S.h_rec[c].n});
             replay_clusters(jobs, g, hp.data(), np, static_cast<float>(in.cluster_min_length), S.h_rec.data());
+            tr.mark("replays");
         }
     }
     assemble_rows(S.h_rec, out, rows);   // (host: cluster_host.cpp)
+    tr.mark("rows");
     out.n_clusters_all = S.n_clusters;
     S.n_rows = (int)rows.size();
     if (ev_mid) AOS_HIP(hipEventRecord(ev_mid, s));
@@ -693,6 +700,7 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         double *d = dev<double>(S.cur_tab, t.size());
         AOS_HIP(hipMemcpyAsync(d, t.data(), sizeof(double) * t.size(), hipMemcpyHostToDevice, s));
         S.dedup.sev.sync(s);
+        tr.mark("curtab");
         S.cur_tab_amax = g.amax;
     }
     k_endpoint_rays<<<6 * nr, 64, 0, s>>>(d_rows, nr, in.skel_bits, g, ang, d_poly, np,
@@ -715,6 +723,7 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
     k_concat3<<<cdiv((long long)ncand, 256), 256, 0, s>>>(d_vout, d_rout, d_eout, d_cnt, d_seeds);
     peek_to_host(h_sc, {d_cnt, d_cnt + 1, d_cnt + 2, dedup_err(scr, s)}, s);
     S.dedup.sev.sync(s);
+    tr.mark("seedcnt");
     dedup_check(scr, h_sc[3]);
     const int n_virtual = h_sc[0], n_ray = h_sc[1], n_end = h_sc[2];
     const int ntot = n_virtual + n_ray + n_end;
@@ -722,6 +731,7 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
     if (ntot) {
         copy_to_host(hs, d_seeds, sizeof(double2) * ntot, s);
         S.dedup.sev.sync(s);
+        tr.mark("seeds");
     }
     out.h_voronoi = hs;
     out.n_virtual = n_virtual; out.n_ray = n_ray; out.n_endpoint = n_end;

@@ -819,22 +819,9 @@ void markers_wait(GvdState &G, bool rethrow) {
     }
 }
 
-// AOS_TRACE=1: host timeline of each GVD call on stderr (ms since the call started, at each host sync)
-struct HostTrace {
-    const bool on = trace_on();
-    const double t0 = on ? trace_ms() : 0.0;
-    std::string line;
-    void mark(const char *what) {
-        if (!on) return;
-        char b[64];
-        snprintf(b, sizeof(b), " %s %.2f", what, trace_ms() - t0);
-        line += b;
-    }
-    ~HostTrace() { if (on) fprintf(stderr, "[aos trace gvd] at %.2f:%s\n", t0, line.c_str()); }
-};
 
 bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipStream_t s, hipEvent_t *ev) {
-    HostTrace tr;
+    HostTrace tr{"gvd"};
     GvdScratch &S = scratch(G);
     G.nodes_xy.clear(); G.labels.clear(); G.cluster_idx.clear(); G.label_counts.clear();
     G.label_clusters.clear(); G.label_types.clear(); G.edges_out.clear(); G.lengths.clear(); G.clearances.clear();

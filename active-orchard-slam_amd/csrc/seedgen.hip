@@ -877,7 +877,9 @@ void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *c
         AOS_HIP(hipMemcpyAsync(h_occ.p, d_occ, C, hipMemcpyDeviceToHost, copy_stream));
         AOS_HIP(hipMemcpyAsync(h_skel.p, d_skel, C, hipMemcpyDeviceToHost, copy_stream));
     };
+    HostTrace tr{"finish"};
     if (want_host && grid_copy_mode == 0) issue_grid_copy();
+    tr.mark("copy_issued");
 
     // ---------------- a8-a15 clusters, tree rows, seeds
     SeedStageIn sin{skel_bits, &geom, &poly, P.cluster_min_length, pre};
@@ -888,8 +890,11 @@ void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *c
 
     unsigned long long *h_cnt = static_cast<unsigned long long *>(h_stats.ensure(64 + 8 * kRorCounters)) + 8;
     if (!clipped_total) AOS_HIP(hipMemcpyAsync(h_cnt, counters.p, 8 * kRorCounters, hipMemcpyDeviceToHost, s));
+    tr.mark("stage_done");
     AOS_HIP(hipStreamSynchronize(s));
+    tr.mark("stream_synced");
     if (want_host) AOS_HIP(hipStreamSynchronize(copy_stream));
+    tr.mark("copies_synced");
     if (clipped_total) {
         n_clipped = *clipped_total;
     } else {

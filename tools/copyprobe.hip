@@ -35,9 +35,14 @@ extern "C" int copyprobe_main(int argc, char **argv) {
     unsigned long long *wi, *wo;
     CK(hipMalloc(&wi, 8 * nw)); CK(hipMalloc(&wo, 8 * nw));
     CK(hipMemset(wi, 0, 8 * nw));
-    hipStream_t sc, sk;
+    // argv[3] = k: k streams are created between the copy stream and the kernel stream (HIP maps streams onto
+    // GPU_MAX_HW_QUEUES hardware queues round-robin: with 4 queues, k = 3 puts both on one queue)
+    const int gap = argc > 3 ? atoi(argv[3]) : 0;
+    hipStream_t sc, sk, dummy[64];
     CK(hipStreamCreateWithFlags(&sc, hipStreamNonBlocking));
+    for (int i = 0; i < gap && i < 64; ++i) CK(hipStreamCreateWithFlags(&dummy[i], hipStreamNonBlocking));
     CK(hipStreamCreateWithFlags(&sk, hipStreamNonBlocking));
+    printf("streams between the copy and the kernel stream: %d\n", gap);
     hipEvent_t c0, c1, k0, k1;
     for (hipEvent_t *e : {&c0, &c1, &k0, &k1}) CK(hipEventCreate(e));
     float tc = 0, tk = 0, tkb = 0, tcb = 0;
