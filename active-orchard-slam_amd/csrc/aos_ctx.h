@@ -17,7 +17,7 @@ struct aos_ctx {
     aos_params P{};
     int device = 0;
     hipStream_t stream = nullptr;
-    std::array<hipEvent_t, 16> ev{};
+    std::array<hipEvent_t, 18> ev{};   // (16, 17: AOS_TRACE splits of the cluster stage)
     aos::Poly poly;
 
     // ---- last cloud (reprocess reuses it: seed_gen:244, 283-285)

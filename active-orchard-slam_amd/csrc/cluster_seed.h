@@ -136,7 +136,7 @@ struct SeedStageOut {
 };
 
 void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStageOut &out, hipStream_t stream,
-                            hipEvent_t ev_mid);
+                            hipEvent_t ev_mid, const hipEvent_t *ev_split = nullptr);
 // the row arrays, the rows' seed slots and the sorted cluster_info / rows_info (host; cluster_host.cpp)
 void assemble_rows(const std::vector<ClusterRec> &rec, SeedStageOut &out, std::vector<RowDev> &rows);
 

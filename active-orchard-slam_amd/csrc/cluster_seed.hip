@@ -548,8 +548,10 @@ __global__ void k_concat3(const double2 *a, const double2 *b, const double2 *c, 
 // ------------------------------------------------------------------ host orchestration
 template <class T> static T *dev(DevBuf &b, size_t n) { return static_cast<T *>(b.ensure(sizeof(T) * std::max<size_t>(n, 1))); }
 
-void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStageOut &out, hipStream_t s, hipEvent_t ev_mid) {
+void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStageOut &out, hipStream_t s, hipEvent_t ev_mid,
+                            const hipEvent_t *ev_split) {
     HostTrace tr{"cluster"};
+    if (ev_split) AOS_HIP(hipEventRecord(ev_split[0], s));   // (AOS_TRACE: the stage's first kernel is next)
     const FrameGeom &fg = *in.g;
     const GridC g = make_gridc(fg);
     const Poly &poly = *in.poly;
@@ -626,6 +628,7 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         S.h_rec.resize(ncl);
         ClusterRec *hr = static_cast<ClusterRec *>(S.h_recbuf.ensure(sizeof(ClusterRec) * (size_t)ncl));
         copy_to_host(hr, d_rec, sizeof(ClusterRec) * ncl, s);
+        if (ev_split) AOS_HIP(hipEventRecord(ev_split[1], s));   // (AOS_TRACE: the GPU part ends here)
         S.dedup.sev.sync(s);
         tr.mark("recs");
         std::copy(hr, hr + ncl, S.h_rec.begin());

@@ -884,7 +884,7 @@ void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *c
     // ---------------- a8-a15 clusters, tree rows, seeds
     SeedStageIn sin{skel_bits, &geom, &poly, P.cluster_min_length, pre};
     SeedStageOut so;
-    run_cluster_seed_stage(cs, sin, so, s, ev[4]);
+    run_cluster_seed_stage(cs, sin, so, s, ev[4], trace_on() ? &ev[16] : nullptr);
     AOS_HIP(hipEventRecord(ev[5], s));
     if (want_host && grid_copy_mode == 1) issue_grid_copy();
 
@@ -937,6 +937,9 @@ void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *c
     // (a tiled frame: its cluster stage starts at ev[6], after the grids' all-gather)
     out.ms_ror = ms(0, 1); out.ms_grid = ms(1, 2); out.ms_thin = ms(2, 3); out.ms_cluster = ms(pre ? 6 : 3, 4);
     out.ms_seeds = ms(4, 5); out.ms_total = ms(0, 5);
+    if (trace_on() && !pre)
+        fprintf(stderr, "[aos trace events] thin_end->stage_start %.3f stage_gpu %.3f gpu_end->rows %.3f (ms)\n", ms(3, 16),
+                ms(16, 17), ms(17, 4));
     out.n_binned = static_cast<const int *>(h_stats.p)[0];   // (ror_collect)
     out.ms_ror_count = out.n_binned ? ms(10, 11) : 0.0f;
     out.ms_ror_bin = out.n_binned ? ms(12, 13) : 0.0f;

@@ -1,8 +1,8 @@
-# read-backs through kernel stores (AOS_ZC_READBACK=1, default) vs hipMemcpyAsync (0), in an order that separates
-# the setting from the process-to-process alternation of the cluster-stage figure (each GPU step its own limit)
+# GPU-side splits of the cluster stage (AOS_TRACE) over consecutive bench processes
 set -e
 mkdir -p gpurun_out
-for v in 1 0 0 1 1 0 0 1; do
-  AOS_ZC_READBACK=$v timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-pipelined-rate --no-device-rate --steps 12 --warmup 3 > gpurun_out/r04n_zc.log 2>&1
-  echo "AOS_ZC_READBACK=$v: $(grep '^{' gpurun_out/r04n_zc.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); s=d['stages_ms']; print(d['frame_ms']['p50'], s['seedgen_cluster'], s['seedgen_seeds'], s['seedgen_total'])")"
+for k in 1 2 3 4; do
+  AOS_TRACE=1 timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-pipelined-rate --no-device-rate --steps 6 --warmup 2 > gpurun_out/r04o_trace_$k.log 2> gpurun_out/r04o_trace_$k.err
+  echo "== process $k: $(grep '^{' gpurun_out/r04o_trace_$k.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['frame_ms']['p50'], d['stages_ms']['seedgen_cluster'])")"
+  grep "aos trace events\|aos trace cluster" gpurun_out/r04o_trace_$k.err | tail -4
 done
