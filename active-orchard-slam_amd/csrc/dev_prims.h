@@ -74,5 +74,8 @@ constexpr int kPeekMax = 8;
 void peek_to_host(int *h_dst, std::initializer_list<const int *> srcs, hipStream_t s);
 void copy_to_host(void *h_dst, const void *d_src, size_t bytes, hipStream_t s);
 void copy_from_host(void *d_dst, const void *h_src, size_t bytes, hipStream_t s);   // h_src pinned
+// A bulk copy by a kernel of at most `blocks` workgroups (one side may be pinned host memory): the published
+// grids' D2H (finish_frame), where hipMemcpyAsync now and then held the host for ~3-7 ms (AOS_TRACE)
+void copy_kernel_bulk(void *dst, const void *src, size_t bytes, int blocks, hipStream_t s);
 
 }  // namespace aos

@@ -424,10 +424,10 @@ __global__ void k_copy_host(W *h_dst, const W *d_src, size_t n) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
         h_dst[i] = d_src[i];
 }
-static void copy_kernel(void *h_dst, const void *d_src, size_t bytes, hipStream_t s) {
+static void copy_kernel(void *h_dst, const void *d_src, size_t bytes, hipStream_t s, int max_blocks = 256) {
     const uintptr_t a = reinterpret_cast<uintptr_t>(h_dst) | reinterpret_cast<uintptr_t>(d_src) | bytes;
     auto go = [&](auto *dst, const auto *src, size_t n) {
-        const int blocks = (int)std::min<size_t>(256, (n + 255) / 256);
+        const int blocks = (int)std::min<size_t>((size_t)max_blocks, (n + 255) / 256);
         k_copy_host<<<blocks, 256, 0, s>>>(dst, src, n);
     };
     if (!(a & 15)) go(static_cast<uint4 *>(h_dst), static_cast<const uint4 *>(d_src), bytes / 16);
@@ -439,6 +439,9 @@ void copy_to_host(void *h_dst, const void *d_src, size_t bytes, hipStream_t s) {
     if (!bytes) return;
     if (zc_readback()) copy_kernel(h_dst, d_src, bytes, s);
     else AOS_HIP(hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, s));
+}
+void copy_kernel_bulk(void *dst, const void *src, size_t bytes, int blocks, hipStream_t s) {
+    if (bytes) copy_kernel(dst, src, bytes, s, blocks);
 }
 void copy_from_host(void *d_dst, const void *h_src, size_t bytes, hipStream_t s) {
     if (!bytes) return;
