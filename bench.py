@@ -551,12 +551,16 @@ def run(a, E, dist, quiet=False):
         tiled_ranks, tiled_split = tiled_breakdown(res, pend, a.warmup, world, rank, dist)
 
     stage = {}
+    per_stage = {}   # every timed frame's value per stage: stages_ms_p50 beside the means
     n_gvd = sum(1 for _, ggs in res if ggs is not None)
     for gs, ggs in res:
         for key, v in gs["ms"].items():
             stage["seedgen_" + key] = stage.get("seedgen_" + key, 0.0) + v / len(res)
+            per_stage.setdefault("seedgen_" + key, []).append(v)
         for key, v in (ggs["ms"].items() if ggs is not None else ()):
             stage["gvd_" + key] = stage.get("gvd_" + key, 0.0) + v / n_gvd
+            per_stage.setdefault("gvd_" + key, []).append(v)
+    stage_p50 = {k: round(_median(v), 3) for k, v in per_stage.items()}
 
     extra = {}
     if not a.stream and not a.tiled and not main_pipe and not a.no_pipelined_rate:
@@ -674,6 +678,9 @@ def run(a, E, dist, quiet=False):
                         "timed_frames_with_markers": mk_frames,
                         "returned_as": "copies" if a.markers_copy else "views of the library-owned arrays (ABI ownership rule)"},
             "stages_ms": {k: round(v, 3) for k, v in avg.items()},
+            # (medians: a frame in which the host was held, e.g. 3-7 ms inside hipMemcpyAsync of the grids,
+            # moves a stage's mean by ~0.5 ms over 12-20 frames)
+            "stages_ms_p50": stage_p50,
             "frame": {"T": T, "rows": len(g["row_length"]), "seeds": len(g["voronoi_seeds"]),
                       "nodes": len(gg["nodes"]), "edges": len(gg["edges"]), "n_binned": g["n_binned"],
                       "n_clipped": g["n_clipped"]},
