@@ -23,7 +23,7 @@
 
 namespace aos {
 
-constexpr int kReplayThreads = 8;   // host threads for the exact BFS replays of one frame
+constexpr int kReplayThreads = 16;   // host threads for the exact BFS replays of one frame (the box share: 16 cores)
 
 // ------------------------------------------------------------------ exact BFS replay
 // clusterOccupiedCells' FIFO BFS (seed_gen:1007-1049) and the order-dependent statistics that follow
