@@ -71,8 +71,9 @@ int aos_ctx::up_threads() {
     return n;
 }
 
-// AOS_STAGED_TOUCH: 1 (default) the staged array is read while the upload DMAs run; 2 on a side stream beside
-// the count pass, after the upload (A/B); 0 never
+// AOS_STAGED_TOUCH: 1 (default) the staged array is read while the upload DMAs run; 0 never. (Round 4 also
+// measured it beside the count pass on a second stream and on the stage's stream before the count pass: both
+// slower, profiles/r04h_ror_variants_touch_ab.txt, r04t_touch_placement_ab.txt.)
 static int staged_touch_mode() {
     static const int m = [] { const char *e = getenv("AOS_STAGED_TOUCH"); return e ? atoi(e) : 1; }();
     return m;
@@ -434,21 +435,9 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
     // no keepable candidate either: the local test is exact.
     const bool any = n_points > 0 && !(is_dense && n_points < (uint64_t)L.need);
     if (!any) return;
-    const bool side_touch = staged_touch_mode() == 2 && !map_mode && ror_staged_max > 0;
-    if (side_touch) {   // (A/B: the staged array's read-ahead beside the count pass)
-        if (!copy_stream) {
-            AOS_HIP(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
-            AOS_HIP(hipEventCreateWithFlags(&copy_ready, hipEventDisableTiming));
-        }
-        AOS_HIP(hipEventRecord(copy_ready, s));
-        AOS_HIP(hipStreamWaitEvent(copy_stream, copy_ready, 0));
-        launch_rt_touch(sorted.as<float4>(), std::min(sorted.cap / sizeof(float4), (size_t)ror_staged_max), copy_stream);
-        AOS_HIP(hipEventRecord(copy_ready, copy_stream));
-    }
     AOS_HIP(hipEventRecord(ev[12], s));
     launch_rt_count(L, d_H, G, d_ts, d_own, ror_lookback(L, G, d_own), s);
     AOS_HIP(hipEventRecord(ev[13], s));
-    if (side_touch) AOS_HIP(hipStreamWaitEvent(s, copy_ready, 0));
     // The staged array holds own + halo copies. With a capacity from an earlier frame the scatter
     // runs at once and reports an overflow (the frame is then redone with the size it read back,
     // run_seedgen); without one, or when the caller cannot redo (a tiled frame), the size is read
