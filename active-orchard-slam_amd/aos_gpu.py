@@ -80,7 +80,8 @@ class SeedGenOut(ctypes.Structure):
                 ("rows_info_xy", P(c_d)), ("n_cluster_info", c_i), ("cluster_info_xy", P(c_d)),
                 ("ms_ror", c_f), ("ms_grid", c_f), ("ms_thin", c_f), ("ms_cluster", c_f), ("ms_seeds", c_f),
                 ("ms_total", c_f), ("n_binned", ctypes.c_uint64), ("ms_ror_count", c_f),
-                ("ms_ror_bin", c_f), ("ms_ror_scatter", c_f), ("thin_graph", c_i), ("thin_launches", c_i)]
+                ("ms_ror_bin", c_f), ("ms_ror_scatter", c_f), ("thin_graph", c_i), ("thin_launches", c_i),
+                ("n_ror_read", c_u64)]
 
 
 class GvdIn(ctypes.Structure):
@@ -319,7 +320,7 @@ def _seedgen_dict(o: SeedGenOut, want_host: bool, copy_grids: bool = True) -> di
         "ms": {"ror": o.ms_ror, "grid": o.ms_grid, "thin": o.ms_thin, "cluster": o.ms_cluster, "seeds": o.ms_seeds,
                "total": o.ms_total, "ror_count": o.ms_ror_count,
                "ror_bin": o.ms_ror_bin, "ror_scatter": o.ms_ror_scatter},
-        "n_binned": o.n_binned, "thin_graph": o.thin_graph, "thin_launches": o.thin_launches,
+        "n_binned": o.n_binned, "thin_graph": o.thin_graph, "thin_launches": o.thin_launches, "n_ror_read": o.n_ror_read,
     }
     nv, nrr = o.n_virtual, o.n_ray
     seeds = r["voronoi_seeds"]

@@ -70,7 +70,7 @@ struct aos_ctx {
     // Host -> device upload of a large pageable buffer (a PointCloud2 message): kUpThreads host
     // threads copy 2 MB chunks into rings of pinned slots, each DMA'd on the thread's stream (tools/upload_ab.py:
     // 4-8 threads and 1-8 MB chunks all upload C2's 120 MB in 3-4 ms on the box, the H2D DMA's ~40 GB/s).
-    static constexpr int kUpThreads = 16;   // capacity; up_threads() of them gather (AOS_UP_THREADS, default 4)
+    static constexpr int kUpThreads = 16;   // capacity; up_threads() of them gather (AOS_UP_THREADS, default 8)
     static int up_threads();
     static constexpr int kUpSlots = 4;      // pinned slots per thread (a ring: gather one while others DMA)
     struct Uploader {
@@ -79,9 +79,31 @@ struct aos_ctx {
         hipEvent_t ev[kUpThreads][kUpSlots] = {}, done[kUpThreads] = {};
         bool used[kUpThreads][kUpSlots] = {};
     } up;
+    // A host cloud is split while it is gathered (upload_pack): the points inside `box`, the ROR stage's
+    // binned box for the polygon and parameters current at upload time (ror_stage: no point outside it
+    // can be binned), go to the device, packed at the front of the cloud buffer in chunk-arrival order (the
+    // ROR results do not depend on point order); the others stay in `rest` (pinned host memory, thread t's
+    // run at byte rbeg[t], rn[t] points). A frame whose binned box is not inside `box` (the polygon changed:
+    // aos_seedgen_reprocess) first copies the rest behind the front (cloud_for_box).
+    struct CloudSplit {
+        aos::PinnedBuf rest;
+        uint64_t rbeg[kUpThreads] = {}, rn[kUpThreads] = {};
+        int nth = 0;
+        uint64_t n_front = 0, n_all = 0;
+        float box[6] = {};          // bminx, bmaxx, bminy, bmaxy, bminz, bmaxz
+        bool on = false;            // split (else all n_all points are on the device)
+        bool whole = false;         // the rest was copied behind the front
+        hipEvent_t copied = nullptr;   // that copy (recorded on the handle's stream; rest is rewritten after it)
+        bool copy_pending = false;
+        void swap_with(CloudSplit &o);
+    } split_cur, split_next;
+    static bool split_enabled();    // AOS_UP_SPLIT (default 1)
+    bool split_box(const aos::Poly &poly, float box[6]) const;   // false: do not split
+    uint64_t cloud_for_box(const float b[6]);   // device points the ROR stage reads for binned box b
     // prefetch = true (aos_cloud_prefetch): dst is not read by queued work and the handle's stream is not
-    // made to wait; the consumer waits for up.done[] (set_cloud)
-    void upload_pack(void *dst, const aos_cloud_view &v, bool prefetch = false);   // -> packed x, y, z (12 B)
+    // made to wait; the consumer waits for up.done[] (set_cloud). sp: the split's state (box[] and on set
+    // by the caller; on = false: no split)
+    void upload_pack(void *dst, const aos_cloud_view &v, CloudSplit &sp, bool prefetch = false);
     void release_uploader();
     // aos_cloud_prefetch: the next frame's cloud uploaded into cloud_next on a background thread
     struct Prefetch {
@@ -91,6 +113,8 @@ struct aos_ctx {
         size_t bytes = 0;
         bool active = false;
         std::exception_ptr err;
+        float box[6] = {};
+        bool split = false;
     } pf;
     aos::DevBuf cloud_next;
     void prefetch_start(const aos_cloud_view &v);
@@ -196,6 +220,7 @@ struct aos_ctx {
     aos::LookBack ror_lookback(const aos::RorLaunch &L, int G, unsigned long long *d_own);
     void ror_stage_unchanged();   // streaming map: no new points since the committed store
     uint64_t ror_skipped = 0;     // frames that skipped the ROR stage that way
+    uint64_t ror_read = 0;        // points this frame's partition passes read (aos_seedgen_out::n_ror_read)
     void finish_frame(const aos::FrameGeom &g, bool want_host, const uint64_t *clipped_total, aos_seedgen_out &out,
                       const aos::PreClusters *pre = nullptr);
     void run_seedgen(bool want_host, aos_seedgen_out &out);

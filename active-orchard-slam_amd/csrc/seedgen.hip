@@ -3,6 +3,7 @@
 // every per-point / per-cell stage runs on the GPU. The tiled multi-GPU frame (tiled.hip) reuses
 // ror_stage and finish_frame.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <climits>
 #include <cmath>
@@ -13,6 +14,7 @@
 #include <thread>
 
 #include "aos_ctx.h"
+#include "cloud_split.h"
 
 using namespace aos;
 
@@ -41,6 +43,12 @@ void aos_ctx::release() {
     gvd_async_stop();   // joins the jobs in flight (they use the lanes' GvdStates)
     try { prefetch_join(); } catch (...) {}
     release_uploader();
+    for (CloudSplit *sp : {&split_cur, &split_next}) {
+        if (sp->copied) { (void)hipEventSynchronize(sp->copied); (void)hipEventDestroy(sp->copied); sp->copied = nullptr; }
+        sp->copy_pending = false;
+        sp->rest.release();
+        sp->on = false;
+    }
     free_path_state(path_state);
     path_state = nullptr;
     have_gvd = false;
@@ -61,12 +69,16 @@ void aos_ctx::release() {
 // stages it through pinned memory on one thread. Here up_threads() threads each take a range of points,
 // gather their x, y, z floats (12 of the record's point_step bytes: the only fields the path reads) into
 // a ring of kUpSlots pinned 2 MB slots and DMA them on their own streams, so 25 % fewer bytes cross PCIe
-// for the common 16-byte record and the device gets a packed float3 cloud (step 12). The handle's stream
-// waits for all of them. The caller's buffer is only read during the call.
+// for the common 16-byte record and the device gets a packed float3 cloud (step 12). With the split
+// (CloudSplit, default) only the points inside the binned box go into the slots (C2: 49.5 % of the cloud);
+// the others go to the pinned rest buffer (cloud_split.cpp: AVX-512 compress, 4 records per register). The
+// handle's stream waits for all of them. The caller's buffer is only read during the call.
+// Round 4 (profiles/r04v_split_ab.txt): C2's upload ends 2.2-2.8 ms after it starts with the split at 8
+// threads, 2.4-3.8 ms without it (4 / 8 / 16 threads); the DMA no longer trails the gather.
 int aos_ctx::up_threads() {
     static const int n = [] {
         const char *e = getenv("AOS_UP_THREADS");
-        return e ? std::max(1, std::min(kUpThreads, atoi(e))) : 4;
+        return e ? std::max(1, std::min(kUpThreads, atoi(e))) : 8;
     }();
     return n;
 }
@@ -79,7 +91,56 @@ static int staged_touch_mode() {
     return m;
 }
 
-void aos_ctx::upload_pack(void *dst, const aos_cloud_view &v, bool prefetch) {
+bool aos_ctx::split_enabled() {
+    static const bool on = [] { const char *e = getenv("AOS_UP_SPLIT"); return !e || atoi(e) != 0; }();
+    return on;
+}
+
+// The ROR stage's binned box for polygon poly (ror_stage computes the same floats the same way)
+static void binned_box(const FrameGeom &g, const aos_params &P, float b[6]) {
+    const float m = ror_margin(P);
+    b[0] = g.minx - m; b[1] = g.maxx + m; b[2] = g.miny - m; b[3] = g.maxy + m;
+    b[4] = P.clipping_minz - m; b[5] = P.clipping_maxz + m;
+}
+
+bool aos_ctx::split_box(const Poly &pg, float box[6]) const {
+    if (!split_enabled()) return false;
+    binned_box(frame_geom(pg, P), P, box);
+    for (int i = 0; i < 6; ++i)
+        if (!std::isfinite(box[i])) return false;
+    return box[0] <= box[1] && box[2] <= box[3] && box[4] <= box[5];
+}
+
+void aos_ctx::CloudSplit::swap_with(CloudSplit &o) {
+    std::swap(rest.p, o.rest.p); std::swap(rest.cap, o.rest.cap);
+    std::swap(rbeg, o.rbeg); std::swap(rn, o.rn); std::swap(nth, o.nth);
+    std::swap(n_front, o.n_front); std::swap(n_all, o.n_all); std::swap(box, o.box);
+    std::swap(on, o.on); std::swap(whole, o.whole); std::swap(copied, o.copied); std::swap(copy_pending, o.copy_pending);
+}
+
+// Device points of the handle's host cloud that a ROR stage with binned box b reads: the front when b lies
+// inside the split's box, else (first time) the rest is copied behind the front on the handle's stream.
+uint64_t aos_ctx::cloud_for_box(const float b[6]) {
+    CloudSplit &sp = split_cur;
+    if (!sp.on || sp.whole) return sp.n_all;
+    if (b[0] >= sp.box[0] && b[1] <= sp.box[1] && b[2] >= sp.box[2] && b[3] <= sp.box[3] && b[4] >= sp.box[4] &&
+        b[5] <= sp.box[5])
+        return sp.n_front;
+    uint64_t at = sp.n_front;
+    for (int t = 0; t < sp.nth; ++t) {
+        if (!sp.rn[t]) continue;
+        AOS_HIP(hipMemcpyAsync(cloud_copy.as<char>() + 12 * at, sp.rest.as<char>() + sp.rbeg[t], 12 * sp.rn[t],
+                               hipMemcpyHostToDevice, stream));
+        at += sp.rn[t];
+    }
+    if (!sp.copied) AOS_HIP(hipEventCreateWithFlags(&sp.copied, hipEventDisableTiming));
+    AOS_HIP(hipEventRecord(sp.copied, stream));
+    sp.copy_pending = true;
+    sp.whole = true;
+    return sp.n_all;
+}
+
+void aos_ctx::upload_pack(void *dst, const aos_cloud_view &v, CloudSplit &sp, bool prefetch) {
     // chunks of AOS_UP_CHUNK_KB (default 2 MB): the last DMAs start soon after the last gather, so the upload
     // ends ~one chunk's DMA after the gather instead of one slot per thread later (8 MB slots: ~1 ms)
     static const uint64_t kChunkPts = [] {
@@ -107,42 +168,62 @@ void aos_ctx::upload_pack(void *dst, const aos_cloud_view &v, bool prefetch) {
     }
     const uint64_t per = (n + nth - 1) / nth;
     const uint8_t *src = static_cast<const uint8_t *>(v.data);
-    const bool std16 = v.point_step == 16 && v.off_x == 0 && v.off_y == 4 && v.off_z == 8;
+    // split (CloudSplit): points inside the box go to the slot (the device front), the others to the rest
+    const bool split = sp.on;
+    if (sp.copy_pending) { AOS_HIP(hipEventSynchronize(sp.copied)); sp.copy_pending = false; }   // rest is read
+    float *rest = split ? static_cast<float *>(sp.rest.ensure(12 * (size_t)n + kPackSlack * (nth + 1))) : nullptr;
+    const float *box = sp.box;
+    const PackLayout lay{v.point_step, v.off_x, v.off_y, v.off_z};
+    std::atomic<uint64_t> front{0};
+    uint64_t rn[kUpThreads] = {};
     std::exception_ptr err[kUpThreads];
     auto work = [&](int t) {
         try {
             AOS_HIP(hipSetDevice(device));
             if (!prefetch) AOS_HIP(hipStreamWaitEvent(up.st[t], ev[15], 0));
             const uint64_t p0 = std::min(n, per * t), p1 = std::min(n, per * (t + 1));
+            float *rr = split ? rest + 3 * p0 + (kPackSlack / 4) * t : nullptr;   // (kPackSlack between runs)
+            uint64_t nr = 0;
             int k = 0;
             for (uint64_t c = p0; c < p1; c += kChunkPts, k = (k + 1) % kUpSlots) {
                 const uint64_t m = std::min(kChunkPts, p1 - c);
                 if (up.used[t][k]) AOS_HIP(hipEventSynchronize(up.ev[t][k]));   // its last DMA is done
                 float *o = static_cast<float *>(up.slot[t][k].p);
-                if (std16) {
-                    const float *r = reinterpret_cast<const float *>(src + 16 * c);
-                    for (uint64_t i = 0; i < m; ++i) { o[3 * i] = r[4 * i]; o[3 * i + 1] = r[4 * i + 1]; o[3 * i + 2] = r[4 * i + 2]; }
+                uint64_t f = m;
+                if (split) {
+                    uint64_t r = 0;
+                    f = pack_split(src + c * (uint64_t)v.point_step, m, lay, box, o, rr + 3 * nr, &r);
+                    nr += r;
                 } else {
-                    for (uint64_t i = 0; i < m; ++i) {
-                        const uint8_t *rec = src + (c + i) * (uint64_t)v.point_step;
-                        std::memcpy(o + 3 * i, rec + v.off_x, 4);
-                        std::memcpy(o + 3 * i + 1, rec + v.off_y, 4);
-                        std::memcpy(o + 3 * i + 2, rec + v.off_z, 4);
-                    }
+                    pack_all(src + c * (uint64_t)v.point_step, m, lay, o);
                 }
-                AOS_HIP(hipMemcpyAsync(static_cast<char *>(dst) + 12 * c, o, 12 * m, hipMemcpyHostToDevice, up.st[t]));
+                if (!f) continue;   // (the slot's last DMA, if any, stays its event)
+                const uint64_t at = split ? front.fetch_add(f) : c;
+                AOS_HIP(hipMemcpyAsync(static_cast<char *>(dst) + 12 * at, o, 12 * f, hipMemcpyHostToDevice, up.st[t]));
                 AOS_HIP(hipEventRecord(up.ev[t][k], up.st[t]));
                 up.used[t][k] = true;
             }
+            rn[t] = nr;
             AOS_HIP(hipEventRecord(up.done[t], up.st[t]));
         } catch (...) { err[t] = std::current_exception(); }
     };
+    HostTrace tr{"upload"};
     std::thread th[kUpThreads - 1];
     for (int t = 1; t < nth; ++t) th[t - 1] = std::thread(work, t);
     work(0);
     for (int t = 1; t < nth; ++t) th[t - 1].join();
     for (int t = 0; t < nth; ++t)
         if (err[t]) std::rethrow_exception(err[t]);
+    sp.nth = nth; sp.n_all = n; sp.n_front = split ? front.load() : n; sp.whole = !split;
+    for (int t = 0; t < kUpThreads; ++t) {   // (byte offsets of the threads' rest runs)
+        sp.rbeg[t] = t < nth ? 12 * std::min(n, per * t) + kPackSlack * t : 0;
+        sp.rn[t] = t < nth ? rn[t] : 0;
+    }
+    tr.mark("gathered");
+    if (tr.on) {   // (AOS_TRACE only: wait for the DMAs to see when the cloud is in HBM)
+        for (int t = 0; t < nth; ++t) AOS_HIP(hipEventSynchronize(up.done[t]));
+        tr.mark("dma_done");
+    }
     if (!prefetch)
         for (int t = 0; t < nth; ++t) AOS_HIP(hipStreamWaitEvent(stream, up.done[t], 0));
 }
@@ -154,13 +235,14 @@ void aos_ctx::prefetch_start(const aos_cloud_view &v) {
     const size_t bytes = (size_t)v.n_points * v.point_step;
     if (v.on_device || bytes < (32u << 20)) return;   // nothing to hide
     void *dst = cloud_next.ensure(12 * (size_t)v.n_points);
+    split_next.on = split_box(poly, split_next.box);   // (the polygon now; ror_stage checks it still holds)
     pf.view = v;
     pf.src = v.data;
     pf.bytes = bytes;
     pf.err = nullptr;
     pf.active = true;
     pf.th = std::thread([this, dst]() {
-        try { upload_pack(dst, pf.view, true); } catch (...) { pf.err = std::current_exception(); }
+        try { upload_pack(dst, pf.view, split_next, true); } catch (...) { pf.err = std::current_exception(); }
     });
 }
 
@@ -208,10 +290,13 @@ void aos_ctx::set_cloud(const aos_cloud_view &v) {
             // the prefetched copy of this very view: it becomes the frame's cloud once its DMAs are done
             std::swap(cloud_copy.p, cloud_next.p);
             std::swap(cloud_copy.cap, cloud_next.cap);
+            split_cur.swap_with(split_next);
             for (int t = 0; t < up_threads(); ++t) AOS_HIP(hipStreamWaitEvent(stream, up.done[t], 0));
         } else {
             void *dst = cloud_copy.ensure(std::max<size_t>(12 * (size_t)v.n_points, 16));
-            if (bytes) upload_pack(dst, v);
+            split_cur.on = bytes && split_box(poly, split_cur.box);
+            split_cur.whole = true; split_cur.n_all = split_cur.n_front = 0;   // (until the upload succeeds)
+            if (bytes) upload_pack(dst, v, split_cur);
         }
         dc = cloud_copy.as<uint8_t>();
     }
@@ -370,6 +455,11 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
         L.bminx = std::max(L.bminx, o.box[0]); L.bminy = std::max(L.bminy, o.box[1]);
         L.bmaxx = std::min(L.bmaxx, o.box[2]); L.bmaxy = std::min(L.bmaxy, o.box[3]);
     }
+    if (d_cloud == cloud_copy.as<uint8_t>() && n_points) {   // a host cloud: its split front, or all of it
+        const float b[6] = {L.bminx, L.bmaxx, L.bminy, L.bmaxy, L.bminz, L.bmaxz};
+        L.n = cloud_for_box(b);
+    }
+    ror_read = L.n;
     float cs_ = (float)(P.ror_radius * 1.001);
     const double ext = std::max((double)L.bmaxx - L.bminx, (double)L.bmaxy - L.bminy);
     if (ext / cs_ > 8192.0) cs_ = (float)(ext / 8192.0);  // cap the bin grid; coarser bins stay exact
@@ -412,6 +502,7 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
     if (store_ok && ms.dense == is_dense && ms.n_points == map_scan_begin && n_points >= ms.n_points) {
         const RorLaunch a = geom_of(L), b = ms.L;
         if (!std::memcmp(&a, &b, sizeof(RorLaunch))) {
+            ror_read = n_points - ms.n_points;   // (the scan)
             if (n_points > ms.n_points) ror_stage_append(L, rbits);
             else ror_stage_unchanged();
             return;
@@ -433,7 +524,7 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
     // PCL dense kNN needs k = min_pts + 1 points in the whole cloud (else every point is removed).
     // A tile's shard holds every neighbour of its own candidates, so a shard with fewer points has
     // no keepable candidate either: the local test is exact.
-    const bool any = n_points > 0 && !(is_dense && n_points < (uint64_t)L.need);
+    const bool any = L.n > 0 && !(is_dense && n_points < (uint64_t)L.need);
     if (!any) return;
     AOS_HIP(hipEventRecord(ev[12], s));
     launch_rt_count(L, d_H, G, d_ts, d_own, ror_lookback(L, G, d_own), s);
@@ -951,6 +1042,7 @@ void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *c
     out.ms_ror_scatter = out.n_binned ? ms(14, 10) : 0.0f;
     out.thin_graph = tiled_frame ? 0 : last_thin_graph;
     out.thin_launches = last_thin_launches;
+    out.n_ror_read = ror_read;
 }
 
 int aos_ctx::debug_grid(const char *which, int8_t *dst, uint64_t capacity) {

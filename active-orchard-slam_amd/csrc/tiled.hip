@@ -383,4 +383,5 @@ void aos_ctx::run_tiled_frame(const aos_comm &cm, int tiles_x, int tiles_y, int 
     out.ms_ror_count = out.n_binned ? ms(10, 11) : 0.0f;
     out.ms_ror_bin = out.n_binned ? ms(12, 13) : 0.0f;
     out.ms_ror_scatter = out.n_binned ? ms(14, 10) : 0.0f;
+    out.n_ror_read = ror_read;
 }

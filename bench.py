@@ -38,10 +38,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 WATCHDOG_EXIT = 3      # exit status of a run whose tiled section hung (its watchdog fired)
 # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE summaries (tools/pmc_traffic.py) of the ROR stage, per config,
 # for the kernels of this build's ROR design. A config or design without a committed PMC run gets null.
-ROR_DESIGN = "r04"
+ROR_DESIGN = "r04v"   # (r04v: the host cloud split at upload; the partition passes read the front only)
 PMC_FILES = {("C2", "r02"): os.path.join(ROOT, "profiles", "r02q_pmc_traffic.json"),
              ("C2", "r03"): os.path.join(ROOT, "profiles", "r03fin_pmc_traffic.json"),
-             ("C2", "r04"): os.path.join(ROOT, "profiles", "r04i_pmc_traffic.json")}
+             ("C2", "r04"): os.path.join(ROOT, "profiles", "r04i_pmc_traffic.json"),
+             ("C2", "r04v"): os.path.join(ROOT, "profiles", "r04w_pmc_traffic.json")}
 
 
 def parse(argv=None):
@@ -596,7 +597,9 @@ def run(a, E, dist, quiet=False):
     # (count, tile scan, scatter, per-tile neighbour count), timed live with HIP events on the handle's
     # stream (aos_seedgen_out.ms_ror_*), averaged over the timed frames. `kernels` gives each launch's
     # time and the count pass's own figure (it is the one launch that reads the cloud: 12 N).
-    n_all = float(n)   # the points this rank's ROR kernels read (tiled: its tile's shard)
+    # the points this frame's ROR partition passes read: a host cloud's split front (the points inside the binned
+    # box: the upload keeps the others in host memory), a streaming append's scan, a tiled rank's shard
+    n_all = float(g.get("n_ror_read") or n)
     T = g["thin_iters"]
     t_cnt, t_scat, t_ror = avg["seedgen_ror_bin"], avg["seedgen_ror_scatter"], avg["seedgen_ror_count"]
     t_stage = avg.get("seedgen_ror_kernels", t_cnt + t_scat + t_ror)
@@ -612,7 +615,9 @@ def run(a, E, dist, quiet=False):
     roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
             "kernel": "ROR stage a1-a4 (k_rt_part<count>, k_rt_colscan, k_rt_part<scatter>, k_rt_ror)",
-            "alg_bytes_per_launch": b_ror, "alg_bytes_model": "SURVEY §8d: 12 B per input point + 1 B per cell (raster)",
+            "alg_bytes_per_launch": b_ror,
+            "alg_bytes_model": ("SURVEY §8d: 12 B per point the stage reads + 1 B per cell (raster); a host cloud's "
+                                "upload sends only the points inside the binned box (units_per_launch of n_input)"),
             "ms_per_launch": round(t_stage, 4), "units_per_launch": n_all,
             "traffic_source": src if traffic is not None else
             f"no rocprofv3 --pmc run committed for config {a.config} / ROR design {ROR_DESIGN}",
@@ -627,7 +632,7 @@ def run(a, E, dist, quiet=False):
                  "achieved_GBs": round(b_thin / (t_thin * 1e-3) / 1e9, 1) if t_thin > 0 else 0.0}
     thin_roof["frac"] = round(thin_roof["achieved_GBs"] / HBM_PEAK_GBS, 4)
     # BASELINE.md:35-37 frame-level figure: B_alg = 12 N + C (6 + 4 T) over the per-frame wall-clock
-    b_frame = 12.0 * n_all + cells * (6.0 + 4.0 * T)
+    b_frame = 12.0 * float(n) + cells * (6.0 + 4.0 * T)   # (every input point is read once on the host)
     t_frame = med if not main_pipe else (_median(frame_lat) * 1e-3 if frame_lat else med)
     frame_roof = {"alg_bytes": b_frame, "frame_ms": round(t_frame * 1e3, 3),
                   "achieved_GBs": round(b_frame / t_frame / 1e9, 2),

@@ -117,6 +117,10 @@ typedef struct aos_seedgen_out {
      * a hipGraph, 2 that graph captured this frame (then launched); thin_launches = k_thin_block
      * launches issued (8 Zhang-Suen iterations each, launches past convergence return at once) */
     int32_t thin_graph, thin_launches;
+    /* points the ROR stage's partition passes read: a host cloud's upload keeps on the device only the
+     * points near the clip box of the polygon current at upload time (the others stay in pinned host
+     * memory until a frame's box needs them); otherwise every point of the cloud / map */
+    uint64_t n_ror_read;
 } aos_seedgen_out;
 
 /* GVD inputs when not fed from this handle's seed-gen frame. */

@@ -39,6 +39,13 @@ def test_oracle_under_asan_ubsan(built):
     assert "all frames ok" in out
 
 
+def test_upload_split_under_asan_ubsan(built):
+    """The uploader's host gather / split (csrc/cloud_split.cpp: AVX-512 and scalar paths) vs a plain
+    restatement on random clouds of four layouts with NaN / inf / on-face points, exact-size outputs."""
+    out = _run([os.path.join(built, "san_split")])
+    assert " 0 failed" in out
+
+
 def test_host_subdiv2d_under_asan_ubsan(built):
     out = _run([os.path.join(built, "san_sdcheck")], env={"AOS_SDCHECK_REPS": "2"})
     assert "0 failed so far" in out.splitlines()[-1]

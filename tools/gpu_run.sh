@@ -62,7 +62,8 @@ for step in $STEPS; do
         -- python3 $R/bench.py --no-cpu-baseline --no-pipelined-rate --no-device-rate --steps 3 --warmup 1 \
         > $R/gpurun_out/${TAG}_write.log 2>&1)
       python3 tools/pmc_traffic.py $(ls gpurun_out/${TAG}_fetch/*counter_collection.csv | head -1) \
-        $(ls gpurun_out/${TAG}_write/*counter_collection.csv | head -1) gpurun_out/${TAG}_pmc_traffic.json ;;
+        $(ls gpurun_out/${TAG}_write/*counter_collection.csv | head -1) gpurun_out/${TAG}_pmc_traffic.json
+      cp gpurun_out/${TAG}_pmc_traffic.json profiles/ ;;   # (a later bench step of this call reads it)
     tiled)
       timeout -k 10 600 python -u -m pytest tests/test_gpu_tiled.py -x -v --timeout 400 --timeout-method thread -k rotating \
         > gpurun_out/${TAG}_pytest_rot.log 2>&1 || { tail -40 gpurun_out/${TAG}_pytest_rot.log; exit 1; }
