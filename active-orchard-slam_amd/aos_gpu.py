@@ -332,19 +332,22 @@ def _seedgen_dict(o: SeedGenOut, want_host: bool, copy_grids: bool = True) -> di
     return r
 
 
-def _gvd_dict(o: GvdOut) -> dict:
+def _gvd_dict(o: GvdOut, copy: bool = True) -> dict:
+    """copy=False: views of the library-owned arrays, valid until the next call on the handle (the ABI's
+    ownership rule; what a node publishing from them sees)."""
     nn, ne = o.num_nodes, o.num_edges
+    a = _arr if copy else _view_arr
     return {
         "published": bool(o.published), "resolution": o.resolution, "origin": (o.origin_x, o.origin_y),
-        "nodes": _arr(o.nodes_xy, 2 * nn, np.float64).reshape(-1, 2),
-        "node_labels": _arr(o.node_labels, nn, np.int32),
-        "node_cluster_indices": _arr(o.node_cluster_indices, nn, np.int32),
-        "node_label_counts": _arr(o.node_label_counts, nn, np.int32),
-        "node_label_clusters": _arr(o.node_label_clusters, o.n_label_entries, np.int32),
-        "node_label_types": _arr(o.node_label_types, o.n_label_entries, np.int32),
-        "edges": _arr(o.edges, 2 * ne, np.int32).reshape(-1, 2),
-        "edge_lengths": _arr(o.edge_lengths, ne, np.float32),
-        "edge_clearances": _arr(o.edge_clearances, ne, np.float32),
+        "nodes": a(o.nodes_xy, 2 * nn, np.float64).reshape(-1, 2),
+        "node_labels": a(o.node_labels, nn, np.int32),
+        "node_cluster_indices": a(o.node_cluster_indices, nn, np.int32),
+        "node_label_counts": a(o.node_label_counts, nn, np.int32),
+        "node_label_clusters": a(o.node_label_clusters, o.n_label_entries, np.int32),
+        "node_label_types": a(o.node_label_types, o.n_label_entries, np.int32),
+        "edges": a(o.edges, 2 * ne, np.int32).reshape(-1, 2),
+        "edge_lengths": a(o.edge_lengths, ne, np.float32),
+        "edge_clearances": a(o.edge_clearances, ne, np.float32),
         "n_merged": o.n_merged_seeds, "n_vor_edges": o.n_voronoi_edges, "n_boundary_raw": o.n_boundary_points,
         "ms": {"merge": o.ms_merge, "delaunay": o.ms_delaunay, "graph": o.ms_graph, "total": o.ms_total,
                "cells": o.ms_cells},
@@ -466,10 +469,10 @@ class Ctx:
         _check(lib().aos_seedgen_reprocess(self.h, int(want_host), ctypes.byref(o)))
         return _seedgen_dict(o, want_host)
 
-    def gvd_from_seedgen(self) -> dict:
+    def gvd_from_seedgen(self, copy: bool = True) -> dict:
         o = GvdOut()
         _check(lib().aos_gvd_from_seedgen(self.h, ctypes.byref(o)))
-        return _gvd_dict(o)
+        return _gvd_dict(o, copy)
 
     def path_plan(self, query: PathQuery | None = None, graph: dict | None = None, skeleton=None, info: dict | None = None,
                   on_device: bool = False) -> dict:
@@ -520,11 +523,11 @@ class Ctx:
         """Up to `depth` background GVD jobs in flight (aos_gvd_pipeline_depth)."""
         _check(lib().aos_gvd_pipeline_depth(self.h, int(depth)))
 
-    def gvd_wait(self) -> dict:
+    def gvd_wait(self, copy: bool = True) -> dict:
         """The graph of the background GVD (aos_gvd_wait)."""
         o = GvdOut()
         _check(lib().aos_gvd_wait(self.h, ctypes.byref(o)))
-        return _gvd_dict(o)
+        return _gvd_dict(o, copy)
 
     def gvd_markers(self, collected: bool = False, copy: bool = True, view: bool = False) -> dict:
         """/gvd/markers content of the last GVD call (aos_gvd_markers_get); collected=True: of the frame

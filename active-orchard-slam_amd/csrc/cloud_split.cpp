@@ -40,9 +40,46 @@ uint64_t split_scalar(const uint8_t *src, uint64_t i0, uint64_t m, const PackLay
     return f;
 }
 
+// An output stream written with nontemporal stores: points are compressed into a 4 KB staging buffer (L1) and
+// leave it as whole 64-byte lines (_mm512_stream_ps), so the output's lines are never read for ownership: the
+// slots and the rest buffer (120 MB at C2) are only read by the DMA engine or by a later rest copy. The first
+// floats up to the destination's 64-byte boundary and the last partial line use plain stores.
+// (Box A/B, tools/sdcheck/var/ntp: 8 threads over 10 M points, 1.29-1.30 ms instead of 1.56-1.60 with stores of
+// whole registers at the output's end; profiles/r04y_ntp.txt.)
+struct NtStream {
+    static constexpr int kBuf = 1024;   // floats
+    alignas(64) float buf[kBuf + 64];
+    float *dst = nullptr;
+    int bn = 0;
+    bool aligned = false;
+    void start(float *d) { dst = d; bn = 0; aligned = false; }
+    __attribute__((target("avx512f"))) void flush(bool final) {
+        int i = 0;
+        if (!aligned) {
+            int head = (int)(((64 - ((uintptr_t)dst & 63)) & 63) / 4);
+            if (head > bn && !final) return;
+            head = head < bn ? head : bn;
+            for (; i < head; ++i) dst[i] = buf[i];
+            dst += head;
+            aligned = true;
+        }
+        if (final) {
+            for (int k = 0; k < bn - i; ++k) dst[k] = buf[i + k];
+            dst += bn - i;
+            bn = 0;
+            return;
+        }
+        const int full = (bn - i) & ~15;
+        for (int k = 0; k < full; k += 16) _mm512_stream_ps(dst + k, _mm512_loadu_ps(buf + i + k));
+        dst += full;
+        i += full;
+        std::memmove(buf, buf + i, sizeof(float) * (size_t)(bn - i));
+        bn -= i;
+    }
+};
 // 16-byte records, four per 512-bit register (x y z w | x y z w | ...). One compare pair gives each lane's
 // test; a record is inside when its x, y, z lanes pass (w lanes forced). Its x, y, z lanes are compressed
-// to the front of a register stored whole at the output's end (the next store overwrites the tail).
+// into the stream of its output.
 __attribute__((target("avx512f,popcnt"))) uint64_t split_avx512(const uint8_t *src, uint64_t m, const float b[6],
                                                                 float *front, float *rest, uint64_t &nr_out,
                                                                 uint64_t &done) {
@@ -51,6 +88,9 @@ __attribute__((target("avx512f,popcnt"))) uint64_t split_avx512(const uint8_t *s
                                      b[4], ninf);
     const __m512 hi = _mm512_setr_ps(b[1], b[3], b[5], pinf, b[1], b[3], b[5], pinf, b[1], b[3], b[5], pinf, b[1], b[3],
                                      b[5], pinf);
+    static thread_local NtStream F, R;
+    F.start(front);
+    R.start(rest);
     const float *p = reinterpret_cast<const float *>(src);
     uint64_t f = 0, nr = 0;
     const uint64_t m4 = m & ~uint64_t(3);
@@ -60,15 +100,21 @@ __attribute__((target("avx512f,popcnt"))) uint64_t split_avx512(const uint8_t *s
                            0x8888u;
         const unsigned r = t & (t >> 1) & (t >> 2) & (t >> 3) & 0x1111u;   // bit 4k: record k inside
         const unsigned k = (unsigned)_mm_popcnt_u32(r);
-        _mm512_storeu_ps(front + 3 * f, _mm512_maskz_compress_ps((__mmask16)(r * 7u), v));
-        _mm512_storeu_ps(rest + 3 * nr, _mm512_maskz_compress_ps((__mmask16)((r ^ 0x1111u) * 7u), v));
+        _mm512_storeu_ps(F.buf + F.bn, _mm512_maskz_compress_ps((__mmask16)(r * 7u), v));
+        _mm512_storeu_ps(R.buf + R.bn, _mm512_maskz_compress_ps((__mmask16)((r ^ 0x1111u) * 7u), v));
+        F.bn += 3 * (int)k;
+        R.bn += 3 * (int)(4 - k);
         f += k; nr += 4 - k;
+        if (F.bn >= NtStream::kBuf) F.flush(false);
+        if (R.bn >= NtStream::kBuf) R.flush(false);
     }
+    F.flush(true);
+    R.flush(true);
+    _mm_sfence();   // the streamed lines are visible before the caller hands the slot to the DMA
     nr_out = nr;
     done = m4;
     return f;
 }
-
 }  // namespace
 
 bool pack_simd() {

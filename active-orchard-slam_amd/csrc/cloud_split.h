@@ -8,8 +8,8 @@ namespace aos {
 
 struct PackLayout { uint32_t step, ox, oy, oz; };   // point_step; byte offsets of float32 x, y, z
 
-// Both outputs of pack_split need this many writable bytes past their last point (the AVX-512 path stores
-// whole 64-byte registers, of which the valid points are a prefix).
+// Both outputs of pack_split may need this many writable bytes past their last point (kept for output paths
+// that store whole 64-byte registers; the AVX-512 path now writes exactly its points).
 constexpr size_t kPackSlack = 64;
 
 // All m records -> out (12 m bytes).

@@ -417,7 +417,7 @@ def run(a, E, dist, quiet=False):
 
     def finish(j):   # pipelined: frame j's graph; its markers at the next finish (or the drain)
         flush_markers()
-        gg = ctx.gvd_wait()
+        gg = ctx.gvd_wait(copy=False)
         if pend["mk"].get(j):
             pend["mk_frame"] = j
         else:
@@ -499,7 +499,7 @@ def run(a, E, dist, quiet=False):
             collect()
         tb = time.perf_counter()
         mk = markers_for(k)
-        gg = ctx.gvd_from_seedgen()
+        gg = ctx.gvd_from_seedgen(copy=False)   # (views of the library's arrays, as the seed-gen grids)
         pend["mk_pending"] = mk
         if a.trace:
             print(f"[trace] step {k}: seed-gen {1e3 * (ta - t0):.2f} ms (device {g['ms']['total']:.2f}), collect "
