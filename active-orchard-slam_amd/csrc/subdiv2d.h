@@ -123,7 +123,7 @@ class Subdiv2D {
     void swap_loop(int curr_edge, int first_point, int curr_point);
     void flip_tests_scalar(const int *es, int n, const V2d &P, int *out) const;
     void flip_tests_avx2(const int *es, int n, const V2d &P, int *out) const;
-    bool insert_cavity(int e0, int curr_point);
+    template <bool SIMD> bool insert_cavity(int e0, int curr_point);
     void calc_voronoi();   // calcVoronoi on the exported layout (qx), creating the virtual vertices
     int facet_next(int e) const;
 };
