@@ -3,7 +3,7 @@
 set -e
 cp tools/sdcheck/var/c2_seeds.bin tools/sdcheck/c2_seeds.bin
 for r in 1 2 3 4; do
-  for b in c00 c10 c01 c11; do
+  for b in d0 d1; do
     echo "$b $(timeout -k 5 60 taskset -c 2 tools/sdcheck/var/tm_$b 5)"
   done
 done
