@@ -12,6 +12,7 @@
 
 #include "aos_internal.h"
 #include "cluster_seed.h"
+#include "host_pool.h"
 
 struct aos_ctx {
     aos_params P{};
@@ -79,6 +80,7 @@ struct aos_ctx {
         hipEvent_t ev[kUpThreads][kUpSlots] = {}, done[kUpThreads] = {};
         bool used[kUpThreads][kUpSlots] = {};
     } up;
+    aos::HostPool up_pool;                  // the gather threads (upload_pack)
     // A host cloud is split while it is gathered (upload_pack): the points inside `box`, the ROR stage's
     // binned box for the polygon and parameters current at upload time (ror_stage: no point outside it
     // can be binned), go to the device, packed at the front of the cloud buffer in chunk-arrival order (the

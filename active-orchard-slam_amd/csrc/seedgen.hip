@@ -208,10 +208,7 @@ void aos_ctx::upload_pack(void *dst, const aos_cloud_view &v, CloudSplit &sp, bo
         } catch (...) { err[t] = std::current_exception(); }
     };
     HostTrace tr{"upload"};
-    std::thread th[kUpThreads - 1];
-    for (int t = 1; t < nth; ++t) th[t - 1] = std::thread(work, t);
-    work(0);
-    for (int t = 1; t < nth; ++t) th[t - 1].join();
+    up_pool.run(nth, work);   // (parked workers: round 4 spawned nth - 1 threads per upload)
     for (int t = 0; t < nth; ++t)
         if (err[t]) std::rethrow_exception(err[t]);
     sp.nth = nth; sp.n_all = n; sp.n_front = split ? front.load() : n; sp.whole = !split;
@@ -255,6 +252,7 @@ bool aos_ctx::prefetch_join() {
 }
 
 void aos_ctx::release_uploader() {
+    up_pool.stop();
     for (int t = 0; t < kUpThreads; ++t) {
         if (up.st[t]) {
             (void)hipStreamSynchronize(up.st[t]);

@@ -66,7 +66,7 @@ int Subdiv2D::new_point(float x, float y, int type) {
     free_p = vfirst[v];
     vp[v] = V2f{x, y}; vfirst[v] = 0; vtype[v] = type;
     if (vd.size() < vp.size()) vd.resize(vp.size());
-    vd[v] = V2d{(double)x, (double)y, (double)x * x + (double)y * y, 0.0};
+    vd[v] = V2d{(double)x, (double)y, (double)x * x + (double)y * y, 0, 0};
     return v;
 }
 
@@ -118,7 +118,7 @@ void Subdiv2D::init_delaunay(float rx, float ry, float rw, float rh, int rect_mo
     vp.clear(); vd.clear(); vfirst.clear(); vtype.clear(); rec.clear();
     recent = 0;
     tlx = rx; tly = ry; brx = rx + rw; bry = ry + rh;
-    vp.push_back(V2f{0.f, 0.f}); vd.push_back(V2d{0.0, 0.0, 0.0, 0.0}); vfirst.push_back(0); vtype.push_back(-1);
+    vp.push_back(V2f{0.f, 0.f}); vd.push_back(V2d{0.0, 0.0, 0.0, 0, 0}); vfirst.push_back(0); vtype.push_back(-1);
     rec.push_back(Rec{{0, 0}, {0, 0}, {0, 0}, 0, 0});                          // quad-edge 0 (NULL)
     free_q = 0; free_p = 0;
     const int pA = new_point(rx + big, ry, 0), pB = new_point(rx, ry + big, 0), pC = new_point(rx - big, ry - big, 0);
@@ -299,14 +299,16 @@ AOS_AVX2 void Subdiv2D::flip_tests_avx2(const int *es, int n, const V2d &P, int 
 template <bool SIMD>
 bool Subdiv2D::insert_cavity(int e0, int p) {
     const size_t nv = vp.size();
-    if (vstamp.size() < nv) { vstamp.resize(2 * nv + 64, 0); vspoke.resize(2 * nv + 64, 0); }
-    if (++stamp >= (1 << 29)) { std::fill(vstamp.begin(), vstamp.end(), 0); stamp = 1; }
+    // the marks live in the vertex's own line (V2d::stamp / spoke): the DFS reads them right after the
+    // vertex's coordinates (C2 replay 25.3-26.1 -> 25.1-25.9 ms on the box, profiles/r04z_replay_dfs.txt)
+    (void)nv;
+    if (++stamp >= (1 << 29)) { for (V2d &x : vd) x.stamp = 0; stamp = 1; }
     const int sA = 2 * stamp, sUsed = 2 * stamp + 1;   // two marks per insert: has a spoke / on the boundary
     const int eB = lnext(e0), eA = lnext(eB);          // root link edges in walk order: eA, eB, e0
     if (lnext(eA) != e0) return false;
     const int first = org(e0), v1 = org(eB), v2 = org(eA);
     if (first == v1 || v1 == v2 || v2 == first) return false;
-    vstamp[first] = vstamp[v1] = vstamp[v2] = sA;
+    vd[first].stamp = vd[v1].stamp = vd[v2].stamp = sA;
 
     const V2d P = vd[p];
     auto area = [](const V2d &a, const V2d &b, const V2d &c) { return (b.x - a.x) * (c.y - a.y) - (b.y - a.y) * (c.x - a.x); };
@@ -346,9 +348,9 @@ bool Subdiv2D::insert_cavity(int e0, int p) {
         known = -1;
         if (flip) {
             const int t = oprev(e), w = dst(t);
-            if (vstamp[w] == sA || w == p || nf + 4 >= (int)cap) return false;   // the cavity would wrap a vertex
-            vstamp[w] = sA;
-            vspoke[w] = e;                                   // e becomes w -> p
+            if (vd[w].stamp == sA || w == p || nf + 4 >= (int)cap) return false;   // the cavity would wrap a vertex
+            vd[w].stamp = sA;
+            vd[w].spoke = e;                                   // e becomes w -> p
             fl[nf] = e; ap[nf] = w; ++nf;
             stk[sp++] = t;                                   // u -> w, after the w -> v subtree
             e = sym(onext(sym(e)));                          // w -> v
@@ -377,8 +379,8 @@ bool Subdiv2D::insert_cavity(int e0, int p) {
     const int *xs = bu;
     for (int k = 0; k < m; ++k) {   // the boundary closes: Org(L_k) = Dst(L_k+1), each vertex once
         const int x = xs[k];
-        if (bv[k + 1 == m ? 0 : k + 1] != x || vstamp[x] != sA) return false;
-        vstamp[x] = sUsed;
+        if (bv[k + 1 == m ? 0 : k + 1] != x || vd[x].stamp != sA) return false;
+        vd[x].stamp = sUsed;
     }
 
     // ---- certified: the connects (reference code, they number the three new quad-edges), then
@@ -386,11 +388,11 @@ bool Subdiv2D::insert_cavity(int e0, int p) {
     int base = new_edge();
     set_pts(base, first, p);
     splice(base, e0);
-    vspoke[first] = base;
+    vd[first].spoke = base;
     int ce = e0;
     do {
         base = connect(ce, sym(base));
-        vspoke[org(base)] = base;
+        vd[org(base)].spoke = base;
         ce = oprev(base);
     } while (dst(ce) != first);
     for (int i = 0; i < nf; ++i) {   // swapEdges: setEdgePoints(e, apex, p)
@@ -403,7 +405,7 @@ bool Subdiv2D::insert_cavity(int e0, int p) {
     // rings: around x_k = Org(L_k) the wedge between L_k and Sym L_k+1 now holds only the spoke;
     // around p the spokes run counter-clockwise x_k -> x_k-1 (the walk is clockwise)
     int *sp_ = cav_apex.data();   // apexes are written: reuse for the spokes S_k (x_k -> p)
-    for (int k = 0; k < m; ++k) sp_[k] = vspoke[xs[k]];
+    for (int k = 0; k < m; ++k) sp_[k] = vd[xs[k]].spoke;
     for (int k = 0; k < m; ++k) {
         const int k1 = k + 1 == m ? 0 : k + 1, k0 = k == 0 ? m - 1 : k - 1;
         const int L = bd[k], Ln = bd[k1], S = sp_[k];

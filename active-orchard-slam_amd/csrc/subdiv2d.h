@@ -84,7 +84,7 @@ class Subdiv2D {
     // 26.0-26.6 ms on the box, profiles/r04z_replay_dfs.txt)
     struct alignas(32) Rec { int on[2], op[2], org[2], link, pad; };   // d = 0: e = 4q, d = 1: Sym e = 4q + 2
     struct V2f { float x, y; };
-    struct alignas(32) V2d { double x, y, n2, pad; };
+    struct alignas(32) V2d { double x, y, n2; int stamp, spoke; };   // stamp / spoke: insert_cavity scratch
     std::vector<Rec> rec;
     std::vector<V2f> vp;
     std::vector<V2d> vd;   // exact double copies of vp plus x*x + y*y, for the predicates
@@ -93,8 +93,8 @@ class Subdiv2D {
     int free_q = 0, free_p = 0, recent = 0;
     bool force_loop = false, use_avx2 = false;
     // cavity DFS scratch: stack of link edges, swapped edges with their apex, boundary edges in walk
-    // order (with their end points), per-vertex spoke (valid while vstamp[v] == stamp)
-    std::vector<int> dfs_stack, cav_flip, cav_apex, cav_bnd, cav_bu, cav_bv, vspoke, vstamp;
+    // order (with their end points); per vertex (V2d) the spoke, valid while its stamp is this insert's
+    std::vector<int> dfs_stack, cav_flip, cav_apex, cav_bnd, cav_bu, cav_bv;
     int stamp = 0;
     float tlx = 0, tly = 0, brx = 0, bry = 0;
 

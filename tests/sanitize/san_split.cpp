@@ -3,6 +3,9 @@
 // on the AVX-512 and the scalar path, with outputs allocated exactly (points + kPackSlack) so that any
 // write past the slack is a heap overflow.
 #include "cloud_split.h"
+#include "host_pool.h"
+
+#include <atomic>
 
 #include <cmath>
 #include <cstdio>
@@ -70,6 +73,21 @@ int main() {
         for (uint64_t n : {0ull, 1ull, 3ull, 4ull, 5ull, 7ull, 8ull, 63ull, 64ull, 1000ull, 4099ull, 100003ull})
             for (bool simd : {true, false}) { check(n, l, rng, simd); ++cases; }
     pack_set_simd(true);
+    // the uploader's worker pool (host_pool.h): every index runs exactly once per job, jobs of varying width,
+    // a stop and a restart in between
+    {
+        HostPool pool;
+        std::atomic<int> hits[16];
+        for (int it = 0; it < 3000; ++it) {
+            const int n = 1 + it % 16;
+            for (auto &h : hits) h = 0;
+            pool.run(n, [&](int i) { hits[i].fetch_add(1); });
+            for (int i = 0; i < 16; ++i)
+                if (hits[i].load() != (i < n ? 1 : 0)) { printf("FAIL pool job %d (n %d): index %d ran %d times\n", it, n, i, hits[i].load()); ++fails; break; }
+            if (it == 1500) pool.stop();
+        }
+        ++cases;
+    }
     printf("san_split: %d cases, %d failed (AVX-512 path %s)\n", cases, fails, pack_simd() ? "on" : "not available");
     return fails ? 1 : 0;
 }

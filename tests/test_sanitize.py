@@ -46,6 +46,12 @@ def test_upload_split_under_asan_ubsan(built):
     assert " 0 failed" in out
 
 
+def test_upload_pool_under_tsan(built):
+    """The uploader's worker pool (csrc/host_pool.h) and the split, under ThreadSanitizer."""
+    out = _run([os.path.join(built, "san_split_tsan")], env={"TSAN_OPTIONS": "halt_on_error=1"})
+    assert " 0 failed" in out
+
+
 def test_host_subdiv2d_under_asan_ubsan(built):
     out = _run([os.path.join(built, "san_sdcheck")], env={"AOS_SDCHECK_REPS": "2"})
     assert "0 failed so far" in out.splitlines()[-1]
