@@ -910,12 +910,15 @@ bool aos_ctx::run_seedgen_once(bool want_host, aos_seedgen_out &out, bool allow_
     return false;
 }
 
-// The published grids' D2H: hipMemcpyAsync (DMA), or a kernel of kGridCopyBlocks workgroups with
+// The published grids' D2H: hipMemcpyAsync (DMA), or a kernel of grid_copy_blocks() workgroups with
 // AOS_GRID_COPY_KERNEL=1. Round 4's host timelines (AOS_TRACE) caught hipMemcpyAsync of the grids holding the
 // host for 3-7 ms in some frames of some processes (that frame's seed-gen: 9 ms instead of 1.5); the kernel
 // copy never holds the host, but beside the cluster stage it stretches the stage's kernels from 0.32 to
 // 0.87 ms in every frame (profiles/r04p_grid_copy_kernel_ab.txt), so the DMA stays the default.
-constexpr int kGridCopyBlocks = 64;
+static int grid_copy_blocks() {   // AOS_GRID_COPY_BLOCKS (default 64)
+    static const int b = [] { const char *e = getenv("AOS_GRID_COPY_BLOCKS"); return e ? std::max(1, atoi(e)) : 64; }();
+    return b;
+}
 static bool grid_copy_kernel() {
     static const bool on = [] { const char *e = getenv("AOS_GRID_COPY_KERNEL"); return e && atoi(e) != 0; }();
     return on;
@@ -964,8 +967,8 @@ void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *c
         AOS_HIP(hipEventRecord(copy_ready, s));
         AOS_HIP(hipStreamWaitEvent(copy_stream, copy_ready, 0));
         if (grid_copy_kernel()) {   // (a kernel launch never holds the host; see copy_kernel_bulk)
-            copy_kernel_bulk(h_occ.p, d_occ, C, kGridCopyBlocks, copy_stream);
-            copy_kernel_bulk(h_skel.p, d_skel, C, kGridCopyBlocks, copy_stream);
+            copy_kernel_bulk(h_occ.p, d_occ, C, grid_copy_blocks(), copy_stream);
+            copy_kernel_bulk(h_skel.p, d_skel, C, grid_copy_blocks(), copy_stream);
         } else {
             AOS_HIP(hipMemcpyAsync(h_occ.p, d_occ, C, hipMemcpyDeviceToHost, copy_stream));
             AOS_HIP(hipMemcpyAsync(h_skel.p, d_skel, C, hipMemcpyDeviceToHost, copy_stream));
