@@ -7,6 +7,7 @@
 #include <cfloat>
 #include <cmath>
 #include <cstring>
+#include <functional>
 
 namespace aos {
 
@@ -446,18 +447,23 @@ Subdiv2D::Raw Subdiv2D::raw() {
     return Raw{qx.data(), n, reinterpret_cast<const float *>(vp.data()), vfirst.data(), vtype.data(), (int)vp.size()};
 }
 
-Subdiv2D::Raw Subdiv2D::raw_into(void *dst) const {
+Subdiv2D::Raw Subdiv2D::raw_into(void *dst, int chunk_recs, const std::function<void(size_t, size_t)> &written) const {
     const int n = (int)rec.size(), nv = (int)vp.size();
     int *qe = static_cast<int *>(dst);
     auto rot3 = [](int x) { return (x & ~3) + ((x + 3) & 3); };
-    for (int q = 0; q < n; ++q) {   // every record written (free ones and #0 as zeros), as raw()'s zero-filled qx
-        const Rec &r = rec[q];
-        int o[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (q > 0 && r.on[0] > 0) {
-            o[0] = r.on[0]; o[1] = rot3(r.op[0]); o[2] = r.on[1]; o[3] = rot3(r.op[1]);
-            o[4] = r.org[0]; o[6] = r.org[1];
+    const int step = chunk_recs > 0 ? chunk_recs : std::max(n, 1);
+    for (int q0 = 0; q0 < n; q0 += step) {
+        const int q1 = std::min(n, q0 + step);
+        for (int q = q0; q < q1; ++q) {   // every record written (free ones and #0 as zeros), as raw()'s zero-filled qx
+            const Rec &r = rec[q];
+            int o[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            if (q > 0 && r.on[0] > 0) {
+                o[0] = r.on[0]; o[1] = rot3(r.op[0]); o[2] = r.on[1]; o[3] = rot3(r.op[1]);
+                o[4] = r.org[0]; o[6] = r.org[1];
+            }
+            std::memcpy(qe + 8 * (size_t)q, o, sizeof(o));
         }
-        std::memcpy(qe + 8 * (size_t)q, o, sizeof(o));
+        if (written && q1 < n) written(sizeof(int) * 8 * (size_t)q0, sizeof(int) * 8 * (size_t)(q1 - q0));
     }
     char *p = reinterpret_cast<char *>(qe + 8 * (size_t)n);
     float *vpo = reinterpret_cast<float *>(p);

@@ -37,6 +37,7 @@
 #pragma once
 #include <cstddef>
 #include <cstdint>
+#include <functional>
 #include <vector>
 
 namespace aos {
@@ -77,7 +78,9 @@ class Subdiv2D {
     // the same state written straight into dst (raw_bytes() bytes: qe | vp | vfirst | vtype), e.g. the
     // pinned staging buffer of the GPU facet builder: no zero-fill, export buffer or second copy
     size_t raw_bytes() const { return (8 * sizeof(int) * rec.size()) + (sizeof(V2f) + 2 * sizeof(int)) * vp.size(); }
-    Raw raw_into(void *dst) const;
+    // written(offset, bytes): called after each chunk_recs records but the last, so that the caller can start
+    // copying what is written (the rest, from the last call's end to raw_bytes(), once raw_into returns)
+    Raw raw_into(void *dst, int chunk_recs = 0, const std::function<void(size_t, size_t)> &written = {}) const;
 
   private:
     // (32-byte aligned: a record or a vertex never straddles two cache lines; the C2 replay 26.3-27.0 ->
