@@ -431,7 +431,7 @@ class Ctx:
         if is_root:
             return {**_seedgen_dict(o, want_host), "root": True, "tiled_stats": self.tiled_stats()}
         return {"root": False, "width": o.info.width, "height": o.info.height, "thin_iters": o.thin_iters,
-                "n_clipped": o.n_clipped, "n_input": o.n_input, "n_binned": o.n_binned,
+                "n_clipped": o.n_clipped, "n_input": o.n_input, "n_binned": o.n_binned, "n_ror_read": o.n_ror_read,
                 "ms": {"ror": o.ms_ror, "grid": o.ms_grid, "thin": o.ms_thin, "total": o.ms_total,
                        "ror_count": o.ms_ror_count, "ror_bin": o.ms_ror_bin, "ror_scatter": o.ms_ror_scatter},
                 "tiled_stats": self.tiled_stats()}

@@ -534,11 +534,15 @@ def run(a, E, dist, quiet=False):
             root_lat = [float(x) for x in t.tolist()]
         frame_lat = sorted(1e3 * x for x in root_lat)
     g, gg = res[-1]
-    if a.tiled:   # the frame statistics of this rank's last root frame (its seeds, rows and graph)
-        roots = [(gs, ggs) for gs, ggs in res if gs.get("root") and ggs is not None] or \
-                [(gs, ggs) for gs, ggs in res if ggs is not None]
-        if roots:
-            g, gg = roots[-1]
+    if a.tiled:   # the frame statistics of this rank's last root frame (its seeds and rows) and last graph
+        # (pipelined: a step returns an older frame's graph, so the two are picked separately; a rank whose
+        # timed steps held no root frame reports the counts it has)
+        gr = [gs for gs, _ in res if gs.get("root")]
+        gq = [ggs for _, ggs in res if ggs is not None]
+        if gr:
+            g = gr[-1]
+        if gq:
+            gg = gq[-1]
     cells = g["width"] * g["height"]
     units = (cells / 1e6) * (1 if a.tiled else world)   # Mcells per step over all ranks
     med = _median(per)
@@ -686,9 +690,9 @@ def run(a, E, dist, quiet=False):
             # (medians: a frame in which the host was held, e.g. 3-7 ms inside hipMemcpyAsync of the grids,
             # moves a stage's mean by ~0.5 ms over 12-20 frames)
             "stages_ms_p50": stage_p50,
-            "frame": {"T": T, "rows": len(g["row_length"]), "seeds": len(g["voronoi_seeds"]),
-                      "nodes": len(gg["nodes"]), "edges": len(gg["edges"]), "n_binned": g["n_binned"],
-                      "n_clipped": g["n_clipped"]},
+            "frame": {"T": T, "rows": len(g.get("row_length", ())), "seeds": len(g.get("voronoi_seeds", ())),
+                      "nodes": len(gg["nodes"]) if gg else 0, "edges": len(gg["edges"]) if gg else 0,
+                      "n_binned": g.get("n_binned"), "n_clipped": g.get("n_clipped")},
             "roofline": roof,
             "thin_roofline": thin_roof,
             "frame_roofline": frame_roof,
