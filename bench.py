@@ -275,6 +275,15 @@ def tiled_extra(a, E, dist, main_out, stream: bool = False) -> dict:
     return {k: o[k] for k in keep if k in o}
 
 
+def pick_tiled_frames(res, g, gg):
+    """The frame statistics a tiled rank reports: its last root frame (seeds, rows) and its last collected
+    graph, picked separately (pipelined: a step returns an older frame's graph; with rotating roots a rank's
+    steps mostly return non-root results). A rank whose timed steps held no root frame keeps (g, gg)."""
+    gr = [gs for gs, _ in res if gs.get("root")]
+    gq = [ggs for _, ggs in res if ggs is not None]
+    return (gr[-1] if gr else g), (gq[-1] if gq else gg)
+
+
 def tiled_breakdown(res, pend, warmup: int, world: int, rank: int, dist):
     """Per rank, the timed tiled frames' averages of aos_tiled_stats (host clock): the whole call, the time
     inside the all-gather / all-reduce callbacks (a collective includes the wait for the slowest rank), and
@@ -534,15 +543,8 @@ def run(a, E, dist, quiet=False):
             root_lat = [float(x) for x in t.tolist()]
         frame_lat = sorted(1e3 * x for x in root_lat)
     g, gg = res[-1]
-    if a.tiled:   # the frame statistics of this rank's last root frame (its seeds and rows) and last graph
-        # (pipelined: a step returns an older frame's graph, so the two are picked separately; a rank whose
-        # timed steps held no root frame reports the counts it has)
-        gr = [gs for gs, _ in res if gs.get("root")]
-        gq = [ggs for _, ggs in res if ggs is not None]
-        if gr:
-            g = gr[-1]
-        if gq:
-            gg = gq[-1]
+    if a.tiled:
+        g, gg = pick_tiled_frames(res, g, gg)
     cells = g["width"] * g["height"]
     units = (cells / 1e6) * (1 if a.tiled else world)   # Mcells per step over all ranks
     med = _median(per)

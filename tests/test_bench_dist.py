@@ -144,3 +144,17 @@ def test_tiled_breakdown_keys():
     assert r0["ms_compute"] == 5.5 and r0["collectives_per_frame"] == 8.0 and r0["ror_skipped_frames"] == 1
     assert split == {"cluster_stage": 3.0, "of_which_replays_on_root": 1.5, "rows_and_seeds": 1.0, "gvd_prefix": 4.0,
                      "root_frames": 1}
+
+
+def test_pick_tiled_frames_rotating_roots():
+    """bench --tiled at 4 ranks (rotating roots, pipelined GVD): rank 0's timed steps are mostly non-root
+    results, and a step's graph is an older frame's. The report takes the last root frame and the last graph
+    separately (round 4: pairing them made a 4-rank run look up rows in a non-root result)."""
+    nonroot = {"root": False, "width": 8, "height": 8, "thin_iters": 3}
+    root = {"root": True, "width": 8, "height": 8, "thin_iters": 3, "row_length": [1.0], "voronoi_seeds": [[0, 0]]}
+    graph = {"nodes": [[0, 0]], "edges": []}
+    res = [(nonroot, None), (root, None), (nonroot, graph), (nonroot, None)]
+    g, gg = bench.pick_tiled_frames(res, res[-1][0], res[-1][1])
+    assert g is root and gg is graph
+    g, gg = bench.pick_tiled_frames([(nonroot, None)], nonroot, None)   # no root frame, no graph
+    assert g is nonroot and gg is None
