@@ -217,7 +217,7 @@ struct aos_ctx {
     void map_append_box(const aos_cloud_view &scan, const float box[4]);   // tiled streaming map
     void map_grow(uint64_t n);
     void ror_stage(const aos::FrameGeom &g, const RorOwn &o, uint64_t *rbits, bool allow_guess);
-    bool ror_collect();   // after the stream synchronised: true if the ROR scatter overflowed
+    bool ror_collect(bool throw_stuck = true);   // after the stream synchronised: true if the ROR scatter overflowed
     void ror_stage_append(aos::RorLaunch L, uint64_t *rbits);   // streaming map: one scan on the tile store
     aos::LookBack ror_lookback(const aos::RorLaunch &L, int G, unsigned long long *d_own);
     void ror_stage_unchanged();   // streaming map: no new points since the committed store

@@ -620,8 +620,10 @@ void aos_ctx::ror_stage_unchanged() {
     ++ror_skipped;
 }
 
-// After the frame's sync: binned count, staged size, and whether the scatter overflowed its guess.
-bool aos_ctx::ror_collect() {
+// After the frame's sync: binned count, staged size, and whether the scatter overflowed its guess. A stuck
+// look-back (bit 4) throws unless throw_stuck is false (a tiled rank: its bits go to every rank first, so
+// all ranks fail the frame together instead of one leaving the others in a collective: ADVICE r04).
+bool aos_ctx::ror_collect(bool throw_stuck) {
     int *h = static_cast<int *>(h_stats.p);
     const unsigned long long *u = reinterpret_cast<const unsigned long long *>(h + 4);
     double binned = (double)u[0];
@@ -631,7 +633,8 @@ bool aos_ctx::ror_collect() {
     ror_staged_max = std::max<double>(ror_staged_max, (double)h[2]);
     if (u[1] & 4) {
         ms.pend.on = false;
-        throw std::runtime_error("ROR column scan: a look-back wait exceeded its cap (kSpinCap)");
+        if (throw_stuck) throw std::runtime_error("ROR column scan: a look-back wait exceeded its cap (kSpinCap)");
+        return true;
     }
     if (u[1] & 2) ror_big_seen = true;
     if (ms.pend.on && u[1] == 0) {   // commit the streaming map's tile store

@@ -325,7 +325,9 @@ void aos_ctx::run_tiled_frame(const aos_comm &cm, int tiles_x, int tiles_y, int 
     AOS_HIP(hipStreamSynchronize(s));
     // (sized by a read-back, so no staging overflow is expected; a streaming store's merge can still
     // overflow a stale size: the bits travel with the counts and every rank fails the frame together)
-    const bool ror_over = ror_collect();
+    if (const char *e = getenv("AOS_DEBUG_ROR_STUCK_RANK"))   // (tests: this rank's column scan "got stuck")
+        if (atoi(e) == cm.rank) reinterpret_cast<unsigned long long *>(static_cast<int *>(h_stats.p) + 4)[1] |= 4;
+    const bool ror_over = ror_collect(false);   // (bit 4, a stuck look-back, travels with the others)
     const int ror_bits = ror_over ? (int)reinterpret_cast<const unsigned long long *>(static_cast<const int *>(h_stats.p) + 4)[1] : 0;
     uint64_t mine_cnt = 0;
     for (int i = 0; i < kRorCounters; ++i) mine_cnt += h_cnt[i];
@@ -336,7 +338,8 @@ void aos_ctx::run_tiled_frame(const aos_comm &cm, int tiles_x, int tiles_y, int 
     comm_max(cm, slots.data(), (int)slots.size());
     if (slots[2 * cm.world])
         throw std::runtime_error("tiled frame: ROR stage overflow on a rank (bits " + std::to_string(slots[2 * cm.world]) +
-                                 ": 1 staged capacity / store merge, 2 a tile beyond the LDS capacity)");
+                                 ": 1 staged capacity / store merge, 2 a tile beyond the LDS capacity, 4 a stuck look-back "
+                                 "wait in the ROR column scan)");
     uint64_t total = 0;
     for (int r = 0; r < cm.world; ++r) total += (uint64_t)slots[2 * r] | ((uint64_t)slots[2 * r + 1] << 31);
 

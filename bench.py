@@ -36,6 +36,7 @@ for sub in ("tools", "active-orchard-slam_amd"):
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 WATCHDOG_EXIT = 3      # exit status of a run whose tiled section hung (its watchdog fired)
+TILED_ERROR_EXIT = 4   # exit status of a run whose tiled / tiled_stream section raised (after the main line)
 # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE summaries (tools/pmc_traffic.py) of the ROR stage, per config,
 # for the kernels of this build's ROR design. A config or design without a committed PMC run gets null.
 ROR_DESIGN = "r04v"   # (r04v: the host cloud split at upload; the partition passes read the front only)
@@ -86,6 +87,10 @@ def parse(argv=None):
     ap.add_argument("--markers-copy", action="store_true",
                     help="copy the markers into fresh Python arrays (default: views of the library-owned arrays, "
                          "as the grids are returned)")
+    ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--sustain-s", type=float, default=None,
+                    help="seconds of the sustained pipelined leg when the CPU baseline runs in its child process "
+                         "(default: as long as the child's frame takes, at most 300 s)")
     ap.add_argument("--fixed-root", action="store_true",
                     help="--tiled: rank 0 finishes every frame (default: frame k's root is rank k mod N, so the "
                          "whole-map stages and the GVD jobs rotate over the ranks)")
@@ -127,6 +132,15 @@ def timed_region(step, steps: int, warmup: int, world: int, sync, dist=None, dev
 def throughput(units_per_step: float, world: int, steps: int, dt: float) -> float:
     """Whole-job rate: units processed by all ranks / max-over-ranks wall time."""
     return units_per_step * world * steps / dt
+
+
+def ror_points_read(res, n_default: int) -> float:
+    """Mean over the timed frames of the points the ROR stage's partition passes read (aos_seedgen_out.n_ror_read);
+    a frame that skipped the stage (a tiled streaming rank the scan missed) counts 0. n_default only for results
+    that carry no such field."""
+    vals = [gs.get("n_ror_read") for gs, _ in res]
+    vals = [float(v) if v is not None else float(n_default) for v in vals]
+    return sum(vals) / len(vals) if vals else float(n_default)
 
 
 def _median(xs):
@@ -196,8 +210,70 @@ def _progress(msg: str) -> None:
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
+def spawn_cpu_baseline(a):
+    """The CPU baseline runs in a child process pinned to one core of this process's CPU set; this process keeps
+    the other cores (set before torch and the library start any thread, so every later thread inherits it). The
+    child builds its cloud at once and starts the timed oracle frame when told to (after the main timed region),
+    while this process runs the sustained pipelined leg on the GPU. Started before anything touches the GPU (no
+    exec from a process that has initialised it). Returns the Popen, or None (then the baseline runs inline)."""
+    import subprocess
+    allowed = sorted(os.sched_getaffinity(0))
+    if len(allowed) < 2:
+        return None
+    core = allowed[0]
+    try:
+        p = subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-baseline-child", "--cpu-config",
+                              a.cpu_config], stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True,
+                             preexec_fn=lambda: os.sched_setaffinity(0, {core}))
+    except OSError:
+        return None
+    os.sched_setaffinity(0, set(allowed) - {core})
+    p.core = core
+    return p
+
+
+def cpu_baseline_child(a) -> None:
+    """--cpu-baseline-child: wait for 'go' on stdin, time the oracle frame, print its JSON line."""
+    import orchard
+    orchard.generate(orchard.CONFIGS[a.cpu_config])   # (page in the generator and numpy before the clock)
+    if sys.stdin.readline().strip() != "go":
+        return
+    print(json.dumps(cpu_baseline(a.cpu_config)), flush=True)
+
+
+def start_cpu_baseline(child) -> None:
+    try:
+        child.stdin.write("go\n")
+        child.stdin.flush()
+        child.stdin.close()
+    except (BrokenPipeError, OSError, ValueError):
+        pass
+
+
+def finish_cpu_baseline(child) -> dict:
+    """The child's result (waits for it; its frame started when the sustained leg did)."""
+    if child.stdin and not child.stdin.closed:
+        start_cpu_baseline(child)
+    so = child.stdout.read()
+    child.wait(timeout=1800)
+    lines = [x for x in (so or "").splitlines() if x.startswith("{")]
+    if child.returncode != 0 or not lines:
+        return {"error": f"CPU baseline child exited {child.returncode}"}
+    r = json.loads(lines[-1])
+    r["sample"] += ("; timed in a child process pinned to its own core while this process ran the sustained "
+                    "pipelined GPU leg on the other cores")
+    return r
+
+
 def main():
     a = parse()
+    if a.cpu_baseline_child:
+        cpu_baseline_child(a)
+        return
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    cpu_child = None
+    if world == 1 and not (a.no_cpu_baseline or a.stream or a.tiled) and os.environ.get("AOS_BENCH_CPU_INLINE") != "1":
+        cpu_child = spawn_cpu_baseline(a)
     _progress("importing torch")
     import torch  # (import before libaos_gpu: shared HIP runtime, see aos_gpu.lib)
     import torch.distributed as dist
@@ -217,21 +293,47 @@ def main():
         else:
             dist.init_process_group(backend)
     red_dev = dev if backend == "nccl" else torch.device("cpu")
-    E = {"world": world, "rank": rank, "gpu": gpu, "dev": dev, "red_dev": red_dev, "backend": backend}
+    E = {"world": world, "rank": rank, "gpu": gpu, "dev": dev, "red_dev": red_dev, "backend": backend,
+         "cpu_child": cpu_child}
     out = run(a, E, dist)
+    sys.exit(report(a, E, dist, out))
+
+
+def report(a, E, dist, out) -> int:
+    """After the main measurement: the --gpus N launch's tiled extras, rank 0's JSON line, the process group's
+    end. Returns the exit status: non-zero when a tiled section raised (the line is printed regardless)."""
+    world, rank = E["world"], E["rank"]
+    extras = {}
     if world > 1 and not (a.tiled or a.stream or a.no_tiled_rate):
         # the multi-GPU launch also measures the one-map design (SURVEY §8e, BASELINE configs[3]): C3 split
         # into tiling_for(N) tiles over the same ranks, halos and flags over the library's RCCL communicator
-        t = tiled_extra(a, E, dist, out)
+        extras["tiled"] = tiled_extra(a, E, dist, out)
         if out is not None:
-            out["tiled"] = t
-        t = tiled_extra(a, E, dist, out, stream=True)
+            out["tiled"] = extras["tiled"]
+        extras["tiled_stream"] = tiled_extra(a, E, dist, out, stream=True)
         if out is not None:
-            out["tiled_stream"] = t
+            out["tiled_stream"] = extras["tiled_stream"]
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    code = exit_status(extras)   # (every rank: a rank whose tiled section raised exits non-zero)
+    if code:
+        print(f"bench: a tiled section failed (exit {code}); the main line above holds the single-map measurement",
+              file=sys.stderr, flush=True)
+    return code
+
+
+def exit_status(out) -> int:
+    """Non-zero when the --gpus N launch's tiled / tiled_stream section raised: the line is still printed (the
+    single-map measurement is valid), but the run did not complete what it was asked to measure."""
+    if not isinstance(out, dict):
+        return 0
+    for key in ("tiled", "tiled_stream"):
+        t = out.get(key)
+        if isinstance(t, dict) and "error" in t:
+            return TILED_ERROR_EXIT
+    return 0
 
 
 def tiled_extra(a, E, dist, main_out, stream: bool = False) -> dict:
@@ -594,6 +696,32 @@ def run(a, E, dist, quiet=False):
         extra["device_resident"] = {"value": round(units / dmed, 3), "median_ms": round(dmed * 1e3, 3),
                                     "ms_per_step": round(ddt / a.steps * 1e3, 3),
                                     "io": "cloud already in HBM, OccupancyGrids left in HBM, GvdGraph + seeds to host"}
+    child = E.get("cpu_child") if (world == 1 and not quiet) else None
+    if child is not None:
+        # the CPU baseline's frame runs in its child (pinned to its own core) from now on; meanwhile this process
+        # keeps the GPU busy with the pipelined loop in chunks of 40 frames (each with 2 untimed warmup frames
+        # and its own drain) until the child is done: a sustained-rate figure beside the short legs above
+        start_cpu_baseline(child)
+        limit = a.sustain_s if a.sustain_s is not None else 300.0
+        _progress(f"CPU baseline (oracle, child process pinned to core {child.core}) beside the sustained "
+                  f"pipelined leg (<= {limit:.0f} s)")
+        t_s0, s_frames, s_time, s_lat = time.perf_counter(), 0, 0.0, []
+        while True:
+            reset(True, host_io, 40, 2)
+            sdt, sres, _ = timed_region(step, 40, 2, 1, sync)
+            s_frames += len(sres)
+            s_time += sdt
+            s_lat += [1e3 * pend["lat"][k] for k in range(2, 42) if k in pend["lat"]]
+            el = time.perf_counter() - t_s0
+            if el >= limit or (a.sustain_s is None and child.poll() is not None):
+                break
+        s_lat.sort()
+        extra["sustained_pipelined"] = {
+            "value": round(units * s_frames / s_time, 3), "unit": "Mcells/s", "depth": mode["depth"],
+            "frames": s_frames, "seconds": round(s_time, 2),
+            "frame_latency_ms": {"p50": round(_median(s_lat), 2), "max": round(s_lat[-1], 2)} if s_lat else None,
+            "what": "the pipelined loop run for as long as the CPU baseline's frame takes (chunks of 40 frames, "
+                    "drained at each chunk's end); this process's threads exclude the child's core"}
     avg = stage
 
     # Roofline (SURVEY §8d algorithmic bytes, HBM-bound; no MFMA). Per frame B_alg = 12 N + C (6 + 4 T):
@@ -605,7 +733,8 @@ def run(a, E, dist, quiet=False):
     # time and the count pass's own figure (it is the one launch that reads the cloud: 12 N).
     # the points this frame's ROR partition passes read: a host cloud's split front (the points inside the binned
     # box: the upload keeps the others in host memory), a streaming append's scan, a tiled rank's shard
-    n_all = float(g.get("n_ror_read") or n)
+    # (averaged over the same timed frames as the stage times; a frame that skipped the stage read 0 points)
+    n_all = ror_points_read(res, n)
     T = g["thin_iters"]
     t_cnt, t_scat, t_ror = avg["seedgen_ror_bin"], avg["seedgen_ror_scatter"], avg["seedgen_ror_count"]
     t_stage = avg.get("seedgen_ror_kernels", t_cnt + t_scat + t_ror)
@@ -735,7 +864,9 @@ def run(a, E, dist, quiet=False):
                 out["root_serial_split_ms"] = tiled_split
             if frame_lat:
                 out["frame_latency_ms"] = {"p50": round(_median(frame_lat), 2), "max": round(frame_lat[-1], 2)}
-        if world == 1 and not a.no_cpu_baseline and not a.stream:
+        if child is not None:
+            out["cpu_baseline"] = finish_cpu_baseline(child)
+        elif world == 1 and not a.no_cpu_baseline and not a.stream:
             _progress(f"CPU baseline (oracle, 1 thread pinned) on {a.cpu_config}")
             out["cpu_baseline"] = cpu_baseline(a.cpu_config)
     ctx.close()

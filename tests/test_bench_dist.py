@@ -158,3 +158,62 @@ def test_pick_tiled_frames_rotating_roots():
     assert g is root and gg is graph
     g, gg = bench.pick_tiled_frames([(nonroot, None)], nonroot, None)   # no root frame, no graph
     assert g is nonroot and gg is None
+
+
+def _tiled_raise_worker():
+    """bench.report for a --gpus 2 launch whose tiled sections raise (e.g. RCCL failing to load on the 8-GPU
+    node): rank 0 prints the main line with the errors and the process exits non-zero (verdict r04 item 5)."""
+    import argparse
+
+    class FakeDist:
+        def destroy_process_group(self):
+            pass
+
+    def boom(*a, **k):
+        raise RuntimeError("ncclCommInitRank: unhandled system error")
+    bench.run = boom
+    a = argparse.Namespace(steps=20, warmup=5, tiled=False, stream=False, config="C2", no_cpu_baseline=False,
+                           no_tiled_rate=False)
+    E = {"world": 2, "rank": 0}
+    sys.exit(bench.report(a, E, FakeDist(), {"value": 1.0}))
+
+
+def test_tiled_error_exits_nonzero():
+    import json
+    import subprocess
+    code = ("import sys; sys.path.insert(0, %r); sys.path.insert(0, %r); import test_bench_dist as t; "
+            "t._tiled_raise_worker()" % (ROOT, os.path.join(ROOT, "tests")))
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert p.returncode == bench.TILED_ERROR_EXIT != 0, p.stderr
+    d = json.loads([x for x in p.stdout.splitlines() if x.startswith("{")][-1])
+    assert d["value"] == 1.0
+    assert "ncclCommInitRank" in d["tiled"]["error"] and "ncclCommInitRank" in d["tiled_stream"]["error"]
+    assert "tiled section failed" in p.stderr
+    # a clean run exits 0; a tiled section that returned a result is not an error
+    assert bench.exit_status({"tiled": {"value": 3.0}, "tiled_stream": None}) == 0
+    assert bench.exit_status(None) == 0
+
+
+def test_ror_points_read_mean_over_timed_frames():
+    """The roofline's bytes: the mean of n_ror_read over the timed frames; a skipped stage reads 0."""
+    res = [({"n_ror_read": 100}, None), ({"n_ror_read": 0}, None), ({"n_ror_read": 200}, None)]
+    assert bench.ror_points_read(res, 999) == 100.0
+    assert bench.ror_points_read([({}, None)], 7) == 7.0
+
+
+def test_cpu_baseline_child_process():
+    """The CPU baseline in its own process pinned to one core (started before the GPU is touched, told to start
+    after the main timed region); this process keeps the other cores."""
+    import argparse
+    allowed = os.sched_getaffinity(0)
+    try:
+        child = bench.spawn_cpu_baseline(argparse.Namespace(cpu_config="C0"))
+        if child is None:   # a one-core CPU set: the baseline runs inline
+            assert len(allowed) < 2
+            return
+        assert child.core not in os.sched_getaffinity(0)
+        r = bench.finish_cpu_baseline(child)
+    finally:
+        os.sched_setaffinity(0, allowed)
+    assert child.returncode == 0 and r["cores"] == 1 and r["kind"] == "port" and r["value"] > 0
+    assert r["pinned_core"] == child.core and "child process" in r["sample"]

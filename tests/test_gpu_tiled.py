@@ -348,3 +348,50 @@ def test_group_stream_4x2_equals_single_gpu_stream():
         grp.map_append(orchard.generate_scan(cfg, 400))
     grp.close()
     single.close()
+
+
+def test_tiled_stuck_lookback_fails_every_rank(monkeypatch):
+    """A tiled rank whose ROR column scan reports a stuck look-back (bit 4 of its overflow word, injected with
+    AOS_DEBUG_ROR_STUCK_RANK) must not leave the frame alone: the bit travels with the kept counts in the
+    max-reduction, so every rank raises the same error and none is left inside a collective.
+    The group is never aborted here: a rank that left early would show as a barrier timeout instead."""
+    cfg = orchard.CONFIGS["C1"]
+    cloud, poly = orchard.generate(cfg, n_points=400_000), orchard.polygon(cfg)
+    world = 2
+    params = aos_gpu.default_params(grid_resolution=cfg.res)
+    plans = [T.tile_plan(params, poly, 2, 1, r) for r in range(world)]
+    group = T.ThreadGroup(world, timeout=60)
+    ctxs = [aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res)) for _ in range(world)]
+    comms = [group.comm(r, plans[r]["exchange_bytes"], "cuda:0") for r in range(world)]
+    for c in ctxs:
+        c.set_polygon(poly)
+    errs = [None] * world
+
+    def work(r):
+        try:
+            ctxs[r].tiled_seedgen(comms[r], 2, 1, T.shard(cloud, plans[r]["points_box"]), root=0)
+        except BaseException as e:   # noqa: BLE001
+            errs[r] = e
+
+    monkeypatch.setenv("AOS_DEBUG_ROR_STUCK_RANK", "1")
+    ts = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(180)
+    monkeypatch.delenv("AOS_DEBUG_ROR_STUCK_RANK")
+    for r in range(world):
+        assert isinstance(errs[r], RuntimeError) and "bits 4" in str(errs[r]) and "look-back" in str(errs[r]), (r, errs[r])
+    # both handles still work on the next frame
+    out = [None] * world
+
+    def again(r):
+        out[r] = ctxs[r].tiled_seedgen(comms[r], 2, 1, T.shard(cloud, plans[r]["points_box"]), root=0)
+    ts = [threading.Thread(target=again, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(180)
+    assert out[0] is not None and out[0]["root"] and out[1] is not None
+    for c in ctxs:
+        c.close()
