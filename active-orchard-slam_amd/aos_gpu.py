@@ -52,7 +52,14 @@ class Params(ctypes.Structure):
     _fields_ = [("clipping_minz", c_f), ("clipping_maxz", c_f), ("clipping_minx", c_f), ("clipping_maxx", c_f),
                 ("clipping_miny", c_f), ("clipping_maxy", c_f), ("grid_resolution", c_f), ("inflation_radius", c_f),
                 ("cluster_min_length", c_d), ("ror_radius", c_d), ("ror_min_neighbors", c_i),
-                ("subdiv_rect_mode", c_i), ("max_graph_publish_rate", c_d), ("gvd_markers", c_i), ("thin_graph", c_i)]
+                ("subdiv_rect_mode", c_i), ("max_graph_publish_rate", c_d), ("gvd_markers", c_i), ("thin_graph", c_i),
+                ("gvd_count_evals", c_i)]
+
+
+class GvdEvals(ctypes.Structure):
+    _fields_ = [("counted", c_i), ("n_label_jobs", c_i), ("edge_ends", c_u64), ("boundary_points", c_u64),
+                ("filtered_nodes", c_u64), ("ref_nearest", c_u64), ("ref_pairs", c_u64), ("ref_labels", c_u64),
+                ("gpu_nearest", c_u64), ("gpu_pairs", c_u64), ("gpu_samples", c_u64), ("gpu_labels", c_u64)]
 
 
 class GvdMarkers(ctypes.Structure):
@@ -165,11 +172,13 @@ def _path_dict(o: PathOut) -> dict:
 
 AllGatherFn = ctypes.CFUNCTYPE(c_i, c_vp, c_u64)
 AllReduceMaxFn = ctypes.CFUNCTYPE(c_i, c_vp, P(c_i), c_i)
+AllToAllFn = ctypes.CFUNCTYPE(c_i, c_vp, P(c_u64))
 
 
 class Comm(ctypes.Structure):
     _fields_ = [("user", c_vp), ("rank", c_i), ("world", c_i), ("send_buf", c_vp), ("recv_buf", c_vp),
-                ("buf_bytes", c_u64), ("all_gather", AllGatherFn), ("all_reduce_max", AllReduceMaxFn)]
+                ("buf_bytes", c_u64), ("all_gather", AllGatherFn), ("all_reduce_max", AllReduceMaxFn),
+                ("all_to_all", AllToAllFn)]
 
 
 class TilePlan(ctypes.Structure):
@@ -228,6 +237,8 @@ def lib():
         L.aos_gvd_wait.argtypes = [c_vp, P(GvdOut)]
         L.aos_gvd_pipeline_depth.argtypes = [c_vp, c_i]
         L.aos_gvd_set_markers.argtypes = [c_vp, c_i]
+        L.aos_gvd_set_count_evals.argtypes = [c_vp, c_i]
+        L.aos_gvd_evals_get.argtypes = [c_vp, P(GvdEvals)]
         L.aos_rccl_unique_id.argtypes = [c_vp]
         L.aos_rccl_create.argtypes = [c_vp, c_i, c_i, c_i, c_u64, P(c_vp)]
         L.aos_rccl_comm.argtypes = [c_vp]
@@ -518,6 +529,17 @@ class Ctx:
     def gvd_set_markers(self, on: bool) -> None:
         """publishMarkers' cells for the following GVD calls (aos_gvd_set_markers); off: on demand."""
         _check(lib().aos_gvd_set_markers(self.h, int(bool(on))))
+
+    def gvd_set_count_evals(self, on: bool) -> None:
+        """Count the GVD graph searches' work in the following GVD calls (aos_gvd_set_count_evals)."""
+        _check(lib().aos_gvd_set_count_evals(self.h, int(bool(on))))
+
+    def gvd_evals(self) -> dict:
+        """SURVEY §8d's pair evaluations of the last counted GVD call (aos_gvd_evals_get): the reference's
+        (ref_*) and the GPU kernels' (gpu_*) distance / sample evaluations."""
+        e = GvdEvals()
+        _check(lib().aos_gvd_evals_get(self.h, ctypes.byref(e)))
+        return {k: int(getattr(e, k)) for k, _ in GvdEvals._fields_}
 
     def gvd_pipeline_depth(self, depth: int) -> None:
         """Up to `depth` background GVD jobs in flight (aos_gvd_pipeline_depth)."""

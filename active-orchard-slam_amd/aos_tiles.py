@@ -15,7 +15,7 @@ import ctypes
 
 import numpy as np
 
-from aos_gpu import AllGatherFn, AllReduceMaxFn, Comm, Params, TilePlan, _check, lib
+from aos_gpu import AllGatherFn, AllReduceMaxFn, AllToAllFn, Comm, Params, TilePlan, _check, lib
 
 
 def tile_plan(params: Params, poly_xy, tiles_x: int, tiles_y: int, rank: int) -> dict:
@@ -61,8 +61,18 @@ class _CommBase:
         self.error = None
         self._ag = AllGatherFn(self._all_gather_cb)
         self._ar = AllReduceMaxFn(self._all_reduce_cb)
+        self._a2a = AllToAllFn(self._all_to_all_cb)
         self.c = Comm(None, rank, world, self.send.data_ptr(), self.recv.data_ptr(), self.buf_bytes, self._ag,
-                      self._ar)
+                      self._ar, self._a2a)
+
+    def without_all_to_all(self):
+        """The same communicator without the optional all_to_all (the library then routes through all_gather)."""
+        self.c.all_to_all = AllToAllFn()
+        return self
+
+    def _splits(self, counts):
+        m = np.ctypeslib.as_array(counts, shape=(self.world * self.world,)).reshape(self.world, self.world)
+        return [int(x) for x in m[self.rank, :]], [int(x) for x in m[:, self.rank]]
 
     def _sync(self):
         if self.device.type == "cuda":
@@ -75,6 +85,17 @@ class _CommBase:
             self._sync()
             return 0
         except BaseException as e:   # noqa: BLE001 — re-raised by Ctx.tiled_seedgen
+            self.error = e
+            self.abort()
+            return -1
+
+    def _all_to_all_cb(self, user, counts):
+        try:
+            send_split, recv_split = self._splits(counts)
+            self.all_to_all(send_split, recv_split)
+            self._sync()
+            return 0
+        except BaseException as e:   # noqa: BLE001
             self.error = e
             self.abort()
             return -1
@@ -111,6 +132,18 @@ class TorchDistComm(_CommBase):
         parts = [torch.empty_like(s) for _ in range(self.world)]
         self.dist.all_gather(parts, s, group=self.group)
         self.recv[: n * self.world].copy_(torch.cat(parts))
+
+    def all_to_all(self, send_split, recv_split):
+        import torch
+        ns, nr = sum(send_split), sum(recv_split)
+        if self.nccl:
+            self.dist.all_to_all_single(self.recv[:nr], self.send[:ns], output_split_sizes=recv_split,
+                                        input_split_sizes=send_split, group=self.group)
+            return
+        out = torch.empty(nr, dtype=torch.uint8)
+        self.dist.all_to_all_single(out, self.send[:ns].cpu(), output_split_sizes=recv_split,
+                                    input_split_sizes=send_split, group=self.group)
+        self.recv[:nr].copy_(out)
 
     def all_reduce_max(self, a: np.ndarray) -> np.ndarray:
         import torch
@@ -187,6 +220,21 @@ class _ThreadComm(_CommBase):
             self.recv[r * n:(r + 1) * n].copy_(g.slots[r])
         self._sync()
         g.barrier.wait()   # every rank has read every send buffer before any is overwritten
+
+    def all_to_all(self, send_split, recv_split):
+        g = self.g
+        g.slots[self.rank] = (self.send, send_split)
+        g.barrier.wait()
+        at = 0
+        for r in range(self.world):
+            buf, split = g.slots[r]
+            off = sum(split[:self.rank])
+            n = split[self.rank]
+            assert n == recv_split[r]
+            self.recv[at:at + n].copy_(buf[off:off + n])
+            at += n
+        self._sync()
+        g.barrier.wait()
 
     def all_reduce_max(self, a: np.ndarray) -> np.ndarray:
         g = self.g

@@ -12,6 +12,7 @@
 
 #include "aos_internal.h"
 #include "cluster_seed.h"
+#include "grid_host.h"
 #include "host_pool.h"
 
 struct aos_ctx {
@@ -155,8 +156,10 @@ struct aos_ctx {
 
     // ---- host-side outputs of the last frame
     aos::PinnedBuf h_occ, h_skel;   // the two OccupancyGrids (pinned: the D2H runs at DMA speed)
+    aos::PinnedBuf h_occ_bits, h_skel_bits;   // their bit-packed device grids (the default read-back, grid_host.h)
+    aos::GridExpander expander;               // expands them on host threads beside the cluster / seed stage
     hipStream_t copy_stream = nullptr;   // their D2H, beside the cluster / seed stage
-    hipEvent_t copy_ready = nullptr;
+    hipEvent_t copy_ready = nullptr, copy_done = nullptr;
     std::vector<double> h_row_center, h_row_start, h_row_end, h_row_length, h_voronoi, h_rows_info, h_cluster_info;
     int n_virtual = 0, n_ray = 0, n_endpoint = 0, n_clusters_all = 0, n_bfs_replayed = 0;
 

@@ -70,6 +70,7 @@ void aos_default_params(aos_params *p) {
     p->max_graph_publish_rate = 10.0;
     p->gvd_markers = 1;
     p->thin_graph = 1;
+    p->gvd_count_evals = 0;
 }
 
 int aos_create(const aos_params *p, int device, aos_ctx **out) {
@@ -268,6 +269,22 @@ int aos_gvd_set_markers(aos_ctx *c, int32_t on) {
     if (!c) { set_error("aos_gvd_set_markers: null handle"); return AOS_E_INVALID; }
     c->P.gvd_markers = on ? 1 : 0;
     return AOS_OK;
+}
+
+int aos_gvd_set_count_evals(aos_ctx *c, int32_t on) {
+    if (!c) { set_error("aos_gvd_set_count_evals: null handle"); return AOS_E_INVALID; }
+    c->P.gvd_count_evals = on ? 1 : 0;
+    return AOS_OK;
+}
+
+int aos_gvd_evals_get(aos_ctx *c, aos_gvd_evals *out) {
+    if (!c || !out) { set_error("aos_gvd_evals_get: null argument"); return AOS_E_INVALID; }
+    AOS_GUARD_BEGIN
+    DeviceScope dev_scope(c->device);
+    c->gvd_view_settle();   // (the result aos_gvd_wait collected last, as markers and planning use)
+    *out = c->gs().evals;
+    return AOS_OK;
+    AOS_GUARD_END
 }
 
 int aos_gvd_pipeline_depth(aos_ctx *c, int32_t depth) {

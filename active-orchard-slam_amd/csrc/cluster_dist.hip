@@ -3,31 +3,32 @@
 //
 // clusterOccupiedCells (seed_gen:970-1049) numbers the 8-connected skeleton clusters in raster order
 // of their first cell (its scan + BFS discovery order). Per frame:
-//  1. every rank labels the foreground (skeleton inside the polygon) of its OWN cells with the GPU
-//     union-find (root = first raster cell): pieces, with n, integer sums and bbox per piece, and the
-//     piece of every foreground cell on the tile's edge (border cells);
-//  2. the piece tables and border cells are all-gathered; every rank runs the same host union-find
-//     (cluster_union): two pieces are one cluster iff two of their border cells are 8-adjacent. A
-//     cluster's first cell is the smallest first cell of its pieces, so clusters are numbered exactly
-//     as on one GPU;
-//  3. n and the exact integer sums add up over pieces; a cluster whose bbox diagonal is shorter than
-//     cluster_min_length cannot be a row (length = max pairwise distance <= the diagonal), so its
-//     record needs no cells. Only the cells of the other ("long") clusters are all-gathered, as
-//     (cluster, cell) keys; every rank sorts them on its GPU and runs the whole-map stage's statistics
-//     kernel on them (the same kernel on the same raster-ordered cells => the same records);
-//  4. the exact BFS replays (clusters without the order-free certificate, all rows at 8192^2) are
-//     split over the ranks' host cores (largest first, to the least loaded rank) and the replayed
-//     records are all-gathered.
-// The root then goes on with rows and seeds from the records (run_cluster_seed_stage, PreClusters).
-#include <hipcub/hipcub.hpp>
-
+//  1. every rank labels the foreground (skeleton inside the polygon) of its OWN cells with the whole-map
+//     stage's union-find kernels (ccl_label: block-local union-find in LDS): pieces, named by their first
+//     raster cell. One pass aggregates per piece n, the exact integer sums and the bbox (LDS-combined per
+//     workgroup: one global atomic per (workgroup, piece) instead of seven per cell), gives every cell its
+//     rank inside its piece, and lists the piece of every foreground cell on an inner tile edge;
+//  2. the piece tables and border cells are all-gathered (one size reduction, one all-gather); every rank
+//     runs the same host union-find (cluster_union): two pieces are one cluster iff two of their border
+//     cells are 8-adjacent. A cluster's first cell is the smallest first cell of its pieces, so clusters are
+//     numbered exactly as on one GPU;
+//  3. n and the sums add up over pieces; a cluster whose bbox diagonal is shorter than cluster_min_length
+//     cannot be a row (length = max pairwise distance <= the diagonal), so its record needs no cells. Every
+//     other ("long") cluster gets ONE owner rank, the same plan on every rank (largest first, to the least
+//     loaded rank), and its cells go to that rank only: one personalised exchange (aos_comm.all_to_all;
+//     without it, through all_gather), whose sizes every rank already knows from the piece table;
+//  4. the owner puts each cluster's pieces together (one segment copy), runs the whole-map stage's
+//     statistics kernel on them (the same kernel on the same cells => the same record) and, for a cluster
+//     without the order-free certificate (every row at 8192^2), the exact BFS replay on its own host cores;
+//     then the owners' records are all-gathered.
+// The root goes on with rows and seeds from the records (run_cluster_seed_stage, PreClusters).
 #include <algorithm>
 #include <chrono>
 #include <climits>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <stdexcept>
-#include <unordered_map>
 
 #include "cluster_dev.h"
 #include "cluster_seed.h"
@@ -44,6 +45,7 @@ struct TileView {
     int Wt;   // own width in cells: min(W, 64 (c0 + nc)) - 64 c0
 };
 
+// own foreground (compact: nc words x nr rows) and its popcount per word
 __global__ void k_dist_fg(const uint64_t *win, TileView T, GridC g, const double *poly, int np, uint64_t *fg, int *cnt) {
     __shared__ double xc[kRowCrossMax];
     __shared__ int nxc;
@@ -65,112 +67,110 @@ __global__ void k_dist_fg(const uint64_t *win, TileView T, GridC g, const double
     cnt[(size_t)r * T.nc + k] = __popcll(o);
 }
 
-__global__ void k_dist_list(const uint64_t *fg, const int *off, TileView T, int W, int *list) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x, r = blockIdx.y;
-    if (k >= T.nc || r >= T.nr) return;
-    const size_t wi = (size_t)r * T.nc + k;
-    uint64_t w = fg[wi];
-    int j = off[wi];
-    while (w) {
-        const int b = __ffsll((long long)w) - 1;
-        w &= w - 1;
-        list[j++] = (T.y0 + r) * W + 64 * (T.c0 + k) + b;   // the map's raster index
-    }
-}
+// piece tables, SoA: n | root | minx | maxx | miny | maxy (ints), sx | sy (u64)
+struct PieceDev { int *n, *root, *mnx, *mxx, *mny, *mxy; unsigned long long *sx, *sy; };
+struct PieceRec { int root, n; long long sx, sy; int minx, maxx, miny, maxy; };   // 40 B, the gathered table
 
-__device__ __forceinline__ int dist_index(const uint64_t *fg, const int *off, const TileView &T, int lx, int ly) {
-    if (lx < 0 || ly < 0 || lx >= T.Wt || ly >= T.nr) return -1;   // (outside the own region)
-    const size_t wi = (size_t)ly * T.nc + (lx >> 6);
-    const uint64_t w = fg[wi];
-    const int b = lx & 63;
-    if (!((w >> b) & 1ull)) return -1;
-    return off[wi] + __popcll(w & ((1ull << b) - 1));
-}
-
-__global__ void k_dist_init(int *parent, int n) {
+__global__ void k_piece_init(PieceDev P, const int *n_pieces, int cap) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) parent[i] = i;
-}
-__global__ void k_dist_union(const int *list, int n, const uint64_t *fg, const int *off, TileView T, int W, int *parent) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int p = list[i], gy = p / W, ly = gy - T.y0, lx = p - gy * W - 64 * T.c0;
-    const int ndx[4] = {-1, 0, 1, -1}, ndy[4] = {-1, -1, -1, 0};
-    for (int k = 0; k < 4; ++k) {
-        const int j = dist_index(fg, off, T, lx + ndx[k], ly + ndy[k]);
-        if (j >= 0) uf_union(parent, i, j);
-    }
-}
-__global__ void k_dist_flatten(int *parent, int *is_root, int n) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    int x = i;
-    while (parent[x] != x) x = parent[x];
-    parent[i] = x;
-    is_root[i] = (x == i);
-}
-
-// pieces: n, sums, bbox by atomics; root = the first cell (the piece's smallest list index)
-struct PieceDev { int *n, *root, *box; unsigned long long *sx, *sy; };   // box: minx, maxx, miny, maxy per piece
-__global__ void k_dist_piece_init(PieceDev P, int np) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= np) return;
+    if (i >= cap || i >= *n_pieces) return;
     P.n[i] = 0; P.sx[i] = 0; P.sy[i] = 0;
-    P.box[4 * i] = INT_MAX; P.box[4 * i + 1] = INT_MIN; P.box[4 * i + 2] = INT_MAX; P.box[4 * i + 3] = INT_MIN;
-}
-__global__ void k_dist_piece(const int *list, const int *parent, const int *rank, int n, int W, TileView T, PieceDev P,
-                             int2 *border, int *n_border) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int p = list[i], y = p / W, x = p - y * W, root = parent[i], id = rank[root];
-    atomicAdd(&P.n[id], 1);
-    atomicAdd(&P.sx[id], (unsigned long long)x);
-    atomicAdd(&P.sy[id], (unsigned long long)y);
-    atomicMin(&P.box[4 * id], x); atomicMax(&P.box[4 * id + 1], x);
-    atomicMin(&P.box[4 * id + 2], y); atomicMax(&P.box[4 * id + 3], y);
-    if (root == i) P.root[id] = p;
-    const int lx = x - 64 * T.c0, ly = y - T.y0;
-    if (lx == 0 || ly == 0 || lx == T.Wt - 1 || ly == T.nr - 1)
-        border[atomicAdd(n_border, 1)] = make_int2(p, list[root]);
+    P.mnx[i] = INT_MAX; P.mxx[i] = INT_MIN; P.mny[i] = INT_MAX; P.mxy[i] = INT_MIN;
 }
 
-// (long-cluster index << 32 | cell) of the own cells of long clusters (lidx[piece] >= 0)
-__global__ void k_dist_keys(const int *list, const int *parent, const int *rank, int n, const int *lidx,
-                            unsigned long long *keys, int *n_keys) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int l = lidx[rank[parent[i]]];
-    if (l < 0) return;
-    keys[atomicAdd(n_keys, 1)] = ((unsigned long long)l << 32) | (unsigned)list[i];
+// One workgroup = kPcTB consecutive cells of the raster-ordered list: a handful of pieces. Their counts, sums
+// and bboxes are combined in an LDS table first; each workgroup then adds one total per piece to the global
+// tables, and the atomicAdd on the piece's n returns the workgroup's base inside the piece, so every cell
+// gets a unique rank inside its piece (prank). Border cells: the piece of each foreground cell on an inner
+// edge of the own region (a map edge has no neighbour tile).
+constexpr int kPcTB = 256, kPcSlots = 512;
+__global__ __launch_bounds__(kPcTB) void k_piece_agg(const int *list, const int *parent, const int *rank, int nf, TileView T,
+                                                      int W, int H, PieceDev P, int *pid_of, int *prank, int2 *border,
+                                                      int *n_border) {
+    __shared__ int key[kPcSlots], cnt[kPcSlots], mnx[kPcSlots], mxx[kPcSlots], mny[kPcSlots], mxy[kPcSlots];
+    __shared__ unsigned long long ssx[kPcSlots], ssy[kPcSlots];
+    const int tid = threadIdx.x, i = blockIdx.x * kPcTB + tid;
+    for (int k = tid; k < kPcSlots; k += kPcTB) {
+        key[k] = -1; cnt[k] = 0; ssx[k] = 0; ssy[k] = 0;
+        mnx[k] = INT_MAX; mxx[k] = INT_MIN; mny[k] = INT_MAX; mxy[k] = INT_MIN;
+    }
+    __syncthreads();
+    int slot = 0, lr = 0;
+    if (i < nf) {
+        const int l = list[i], ly = l / T.Wt, lx = l - ly * T.Wt;
+        const int x = 64 * T.c0 + lx, y = T.y0 + ly;
+        const int root = parent[i], pid = rank[root];
+        pid_of[i] = pid;
+        slot = (int)(((unsigned)pid * 2654435761u) >> 23) & (kPcSlots - 1);
+        for (;;) {   // (at most kPcTB distinct ids per workgroup: a free slot always exists)
+            const int old = atomicCAS(&key[slot], -1, pid);
+            if (old == -1 || old == pid) break;
+            slot = (slot + 1) & (kPcSlots - 1);
+        }
+        lr = atomicAdd(&cnt[slot], 1);
+        atomicAdd(&ssx[slot], (unsigned long long)x);
+        atomicAdd(&ssy[slot], (unsigned long long)y);
+        atomicMin(&mnx[slot], x); atomicMax(&mxx[slot], x);
+        atomicMin(&mny[slot], y); atomicMax(&mxy[slot], y);
+        if (root == i) P.root[pid] = y * W + x;
+        const bool edge = (lx == 0 && T.c0 > 0) || (ly == 0 && T.y0 > 0) || (lx == T.Wt - 1 && x + 1 < W) ||
+                          (ly == T.nr - 1 && y + 1 < H);
+        if (edge) {
+            const int l0 = list[root], ry = T.y0 + l0 / T.Wt, rx = 64 * T.c0 + l0 % T.Wt;
+            border[atomicAdd(n_border, 1)] = make_int2(y * W + x, ry * W + rx);
+        }
+    }
+    __syncthreads();
+    for (int k = tid; k < kPcSlots; k += kPcTB) {
+        const int id = key[k];
+        if (id < 0) continue;
+        cnt[k] = atomicAdd(&P.n[id], cnt[k]);   // (now the workgroup's base inside the piece)
+        atomicAdd(&P.sx[id], ssx[k]);
+        atomicAdd(&P.sy[id], ssy[k]);
+        atomicMin(&P.mnx[id], mnx[k]); atomicMax(&P.mxx[id], mxx[k]);
+        atomicMin(&P.mny[id], mny[k]); atomicMax(&P.mxy[id], mxy[k]);
+    }
+    __syncthreads();
+    if (i < nf) prank[i] = cnt[slot] + lr;
 }
 
-// sorted keys -> cells and the runs of the long clusters
-__global__ void k_dist_runs(const unsigned long long *keys, int n, int n_long, int *cells, int *off) {
+// the gathered blob of this rank: PieceRec[n_pieces] then int2 border[n_border]
+__global__ void k_piece_pack(PieceDev P, const int *n_pieces, const int2 *border, const int *n_border, int cap,
+                             uint8_t *blob) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const unsigned long long k = keys[i];
-    const int l = (int)(k >> 32);
-    cells[i] = (int)(unsigned)(k & 0xffffffffull);
-    if (i == 0 || (int)(keys[i - 1] >> 32) != l) off[l] = i;
-    if (i == n - 1) off[n_long] = n;
+    const int np = *n_pieces, nb = *n_border;
+    if (i < np && i < cap) {
+        PieceRec r{P.root[i], P.n[i], (long long)P.sx[i], (long long)P.sy[i], P.mnx[i], P.mxx[i], P.mny[i], P.mxy[i]};
+        reinterpret_cast<PieceRec *>(blob)[i] = r;
+    }
+    if (i < nb && i < cap) reinterpret_cast<int2 *>(blob + sizeof(PieceRec) * (size_t)np)[i] = border[i];
+}
+
+// the cells of long pieces, each to its slot in the send layout (destination-major, then cluster, piece)
+__global__ void k_route(const int *list, const int *pid_of, const int *prank, int nf, const int *poff, TileView T, int W,
+                        int *out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nf) return;
+    const int o = poff[pid_of[i]];
+    if (o < 0) return;
+    const int l = list[i], ly = l / T.Wt, lx = l - ly * T.Wt;
+    out[o + prank[i]] = (T.y0 + ly) * W + 64 * T.c0 + lx;
+}
+
+// one workgroup per segment: landing[src, src + n) -> cells[dst, dst + n) (a cluster's pieces side by side)
+struct Seg { long long src, dst; int n, pad; };
+__global__ void k_segments(const Seg *segs, const int *landing, int *cells) {
+    const Seg s = segs[blockIdx.x];
+    for (int k = threadIdx.x; k < s.n; k += blockDim.x) cells[s.dst + k] = landing[s.src + k];
 }
 
 // ------------------------------------------------------------------ collectives of variable size
 static void comm_max(const aos_comm &cm, int32_t *v, int n) {
     if (cm.all_reduce_max(cm.user, v, n) != 0) throw CommError{"aos_comm.all_reduce_max failed"};
 }
-// every rank's byte count (each rank fills its own slot; max = the slot's value)
-static std::vector<uint64_t> gather_sizes(const aos_comm &cm, uint64_t mine) {
-    std::vector<int32_t> slots(2 * (size_t)cm.world, 0);
-    slots[2 * cm.rank] = (int32_t)(mine & 0x7fffffff);
-    slots[2 * cm.rank + 1] = (int32_t)(mine >> 31);
-    comm_max(cm, slots.data(), (int)slots.size());
-    std::vector<uint64_t> sz((size_t)cm.world);
-    for (int r = 0; r < cm.world; ++r) sz[r] = (uint64_t)(uint32_t)slots[2 * r] | ((uint64_t)(uint32_t)slots[2 * r + 1] << 31);
-    return sz;
-}
 // All-gather of sizes[r] bytes per rank through the communicator's fixed buffers, in chunks of
-// buf_bytes: rank r's bytes land at dst + (sizes[0] + ... + sizes[r - 1]). src / dst: device or host.
+// buf_bytes: rank r's bytes land at dst + (sizes[0] + ... + sizes[r - 1]). src / dst: device or pinned host
+// memory (host ends move by kernel stores: copy_to_host / copy_from_host).
 static void gather_bytes(const aos_comm &cm, hipStream_t s, const void *src, bool src_dev,
                          const std::vector<uint64_t> &sizes, void *dst, bool dst_dev) {
     const uint64_t B = cm.buf_bytes & ~7ull;
@@ -182,26 +182,90 @@ static void gather_bytes(const aos_comm &cm, hipStream_t s, const void *src, boo
     for (uint64_t off = 0; off < maxb; off += B) {
         const uint64_t c = std::min(B, maxb - off);
         const uint64_t m = mine > off ? std::min(c, mine - off) : 0;
-        if (m)
-            AOS_HIP(hipMemcpyAsync(cm.send_buf, static_cast<const uint8_t *>(src) + off, m,
-                                   src_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
+        if (m) {
+            const uint8_t *p = static_cast<const uint8_t *>(src) + off;
+            if (src_dev) AOS_HIP(hipMemcpyAsync(cm.send_buf, p, m, hipMemcpyDeviceToDevice, s));
+            else copy_from_host(cm.send_buf, p, m, s);
+        }
         AOS_HIP(hipStreamSynchronize(s));
         if (cm.all_gather(cm.user, c) != 0) throw CommError{"aos_comm.all_gather failed"};
         for (int r = 0; r < cm.world; ++r) {
             const uint64_t v = sizes[r] > off ? std::min(c, sizes[r] - off) : 0;
-            if (v)
-                AOS_HIP(hipMemcpyAsync(static_cast<uint8_t *>(dst) + at[r] + off,
-                                       static_cast<const uint8_t *>(cm.recv_buf) + (uint64_t)r * c, v,
-                                       dst_dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, s));
+            if (!v) continue;
+            uint8_t *d = static_cast<uint8_t *>(dst) + at[r] + off;
+            const uint8_t *q = static_cast<const uint8_t *>(cm.recv_buf) + (uint64_t)r * c;
+            if (dst_dev) AOS_HIP(hipMemcpyAsync(d, q, v, hipMemcpyDeviceToDevice, s));
+            else copy_to_host(d, q, v, s);
         }
         AOS_HIP(hipStreamSynchronize(s));   // (the next chunk's all-gather rewrites recv_buf)
     }
 }
 
-struct PieceRec { int root, n; long long sx, sy; int minx, maxx, miny, maxy; };
-struct ReplayOut { int l, pad; ClusterRec r; };
-
 template <class T> static T *dptr(DevBuf &b, size_t n) { return static_cast<T *>(b.ensure(sizeof(T) * std::max<size_t>(n, 1))); }
+template <class T> static T *hptr(PinnedBuf &b, size_t n) { return static_cast<T *>(b.ensure(sizeof(T) * std::max<size_t>(n, 1))); }
+
+struct OwnedOut { int l, pad; ClusterRec r; };
+
+// The personalised exchange of the long clusters' cells. cnt[s * W + d]: bytes rank s sends to rank d (known
+// on every rank). send: this rank's route buffer (device, destination-major). Returns the device buffer the
+// blocks addressed to this rank landed in and, per source s, where s's block for this rank starts in it.
+static const int *exchange_cells(const aos_comm &cm, ClusterDistState &D, hipStream_t s, const std::vector<uint64_t> &cnt,
+                                 const int *send, std::vector<uint64_t> &src_base) {
+    const int W = cm.world, me = cm.rank;
+    src_base.assign((size_t)W, 0);
+    if (W == 1) return send;
+    std::vector<uint64_t> row((size_t)W, 0), col((size_t)W, 0);
+    for (int a = 0; a < W; ++a)
+        for (int b = 0; b < W; ++b) { row[a] += cnt[(size_t)a * W + b]; col[b] += cnt[(size_t)a * W + b]; }
+    if (!cm.all_to_all) {   // through all_gather: everyone's route buffer, then this rank's blocks from it
+        uint8_t *all = dptr<uint8_t>(D.landing, std::accumulate(row.begin(), row.end(), (uint64_t)0));
+        gather_bytes(cm, s, send, true, row, all, true);
+        uint64_t at = 0;
+        for (int r = 0; r < W; ++r) {
+            uint64_t pre = 0;
+            for (int q = 0; q < me; ++q) pre += cnt[(size_t)r * W + q];
+            src_base[r] = (at + pre) / 4;
+            at += row[r];
+        }
+        return reinterpret_cast<const int *>(all);
+    }
+    uint64_t roff = 0;
+    for (int r = 0; r < W; ++r) { src_base[r] = roff / 4; roff += cnt[(size_t)r * W + me]; }
+    int *land = dptr<int>(D.landing, roff / 4);
+    // rounds of at most q bytes per pair keep every row sum <= buf_bytes and column sum <= world * buf_bytes
+    uint64_t q = (cm.buf_bytes / (uint64_t)W) & ~7ull;
+    const char *qe = getenv("AOS_DEBUG_A2A_ROUND_BYTES");   // (read per call: tests set it for one frame)
+    const uint64_t q_cap = qe ? strtoull(qe, 0, 10) : 0ull;
+    if (q_cap) q = std::min(q, std::max<uint64_t>(8, q_cap & ~7ull));   // (tests: force many rounds)
+    if (!q) throw CommError{"aos_comm.buf_bytes too small for the cluster exchange"};
+    uint64_t most = 0;
+    for (uint64_t c : cnt) most = std::max(most, c);
+    std::vector<uint64_t> so((size_t)W, 0);
+    for (int d = 1; d < W; ++d) so[d] = so[d - 1] + cnt[(size_t)me * W + d - 1];
+    std::vector<uint64_t> c((size_t)W * W);
+    for (uint64_t off = 0; off < std::max<uint64_t>(most, 1); off += q) {
+        for (size_t k = 0; k < c.size(); ++k) c[k] = cnt[k] > off ? std::min(q, cnt[k] - off) : 0;
+        uint64_t at = 0;
+        for (int d = 0; d < W; ++d) {
+            const uint64_t n = c[(size_t)me * W + d];
+            if (n) AOS_HIP(hipMemcpyAsync(static_cast<uint8_t *>(cm.send_buf) + at,
+                                          reinterpret_cast<const uint8_t *>(send) + so[d] + off, n,
+                                          hipMemcpyDeviceToDevice, s));
+            at += n;
+        }
+        AOS_HIP(hipStreamSynchronize(s));
+        if (cm.all_to_all(cm.user, c.data()) != 0) throw CommError{"aos_comm.all_to_all failed"};
+        at = 0;
+        for (int r = 0; r < W; ++r) {
+            const uint64_t n = c[(size_t)r * W + me];
+            if (n) AOS_HIP(hipMemcpyAsync(reinterpret_cast<uint8_t *>(land) + src_base[r] * 4 + off,
+                                          static_cast<const uint8_t *>(cm.recv_buf) + at, n, hipMemcpyDeviceToDevice, s));
+            at += n;
+        }
+        AOS_HIP(hipStreamSynchronize(s));   // (the next round rewrites recv_buf)
+    }
+    return land;
+}
 
 // ------------------------------------------------------------------ the rank's part of a frame
 void cluster_dist(ClusterDistState &D, const aos_comm &cm, const TilePlan &t, const FrameGeom &fg, const Poly &poly,
@@ -211,96 +275,85 @@ void cluster_dist(ClusterDistState &D, const aos_comm &cm, const TilePlan &t, co
     pre = PreClusters();
     st = ClusterDistStats();
     const GridC g = make_gridc(fg);
-    const int W = g.W;
-    const int np = (int)poly.size();
-    std::vector<double> hp(2 * (size_t)np);
-    for (int i = 0; i < np; ++i) { hp[2 * i] = poly[i].first; hp[2 * i + 1] = poly[i].second; }
-    double *d_poly = dptr<double>(D.poly, hp.size());
-    AOS_HIP(hipMemcpyAsync(d_poly, hp.data(), sizeof(double) * hp.size(), hipMemcpyHostToDevice, s));
+    const int W = g.W, world = cm.world, me = cm.rank;
+    const int npoly = (int)poly.size();
+    double *hp = hptr<double>(D.h_poly, 2 * (size_t)npoly);
+    for (int i = 0; i < npoly; ++i) { hp[2 * i] = poly[i].first; hp[2 * i + 1] = poly[i].second; }
+    double *d_poly = dptr<double>(D.poly, 2 * (size_t)npoly);
+    copy_from_host(d_poly, hp, sizeof(double) * 2 * npoly, s);
     TileView T{t.y0, t.y1 - t.y0, t.c0, t.c1 - t.c0, t.y0 - t.wy0, t.c0 - t.wc0, t.lg.WW, 0};
     T.Wt = std::min(W, 64 * t.c1) - 64 * t.c0;
-    int *h = static_cast<int *>(D.h.ensure(64));
+    int *h = hptr<int>(D.h, 16);
 
-    // ---- 1. own foreground, pieces, border cells
+    // ---- 1. own foreground, pieces, border cells (the whole-map stage's labelling on the own region)
     const size_t Cw = (size_t)T.nc * T.nr;
     uint64_t *d_fg = dptr<uint64_t>(D.fg, Cw);
-    int *d_cnt = dptr<int>(D.cnt, Cw + 1), *d_off = dptr<int>(D.off, Cw + 1);
-    AOS_HIP(hipMemsetAsync(d_cnt + Cw, 0, sizeof(int), s));
-    const dim3 gw(cdiv(T.nc, 64), T.nr);
-    k_dist_fg<<<gw, 64, 0, s>>>(win, T, g, d_poly, np, d_fg, d_cnt);
-    size_t tb = 0;
-    AOS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (int *)nullptr, (int *)nullptr, (int)Cw + 1, s));
-    AOS_HIP(hipcub::DeviceScan::ExclusiveSum(D.tmp.ensure(tb), tb, d_cnt, d_off, (int)Cw + 1, s));
-    AOS_HIP(hipMemcpyAsync(h, d_off + Cw, sizeof(int), hipMemcpyDeviceToHost, s));
-    AOS_HIP(hipStreamSynchronize(s));
-    const int nf = h[0];
-    int *d_list = dptr<int>(D.list, nf), *d_par = dptr<int>(D.parent, nf);
-    int *d_isroot = dptr<int>(D.isroot, (size_t)nf + 1), *d_rank = dptr<int>(D.rank, (size_t)nf + 1);
-    int npieces = 0;
-    if (nf > 0) {
-        k_dist_list<<<gw, 64, 0, s>>>(d_fg, d_off, T, W, d_list);
-        k_dist_init<<<cdiv(nf, 256), 256, 0, s>>>(d_par, nf);
-        k_dist_union<<<cdiv(nf, 256), 256, 0, s>>>(d_list, nf, d_fg, d_off, T, W, d_par);
-        AOS_HIP(hipMemsetAsync(d_isroot + nf, 0, sizeof(int), s));
-        k_dist_flatten<<<cdiv(nf, 256), 256, 0, s>>>(d_par, d_isroot, nf);
-        size_t tb2 = 0;
-        AOS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, (int *)nullptr, (int *)nullptr, nf + 1, s));
-        AOS_HIP(hipcub::DeviceScan::ExclusiveSum(D.tmp.ensure(std::max(tb, tb2)), tb2, d_isroot, d_rank, nf + 1, s));
-        AOS_HIP(hipMemcpyAsync(h, d_rank + nf, sizeof(int), hipMemcpyDeviceToHost, s));
-        AOS_HIP(hipStreamSynchronize(s));
-        npieces = h[0];
-    }
-    // piece arrays: n | root | box (4) ints, sx | sy u64; border (cell, root) pairs and their count
-    const size_t PI = (size_t)std::max(npieces, 1);
-    int *d_pint = dptr<int>(D.pieces, 6 * PI + 4 * PI);   // 6 ints + 2 u64 (= 4 ints) per piece
-    PieceDev P{d_pint, d_pint + PI, d_pint + 2 * PI, reinterpret_cast<unsigned long long *>(d_pint + 6 * PI),
-               reinterpret_cast<unsigned long long *>(d_pint + 8 * PI)};
-    int2 *d_border = dptr<int2>(D.border, (size_t)nf);
+    int *d_cnt = dptr<int>(D.cnt, Cw);
+    k_dist_fg<<<dim3(cdiv(T.nc, 64), T.nr), 64, 0, s>>>(win, T, g, d_poly, npoly, d_fg, d_cnt);
+    GridC gl{};   // the own region as an image: local raster index = ly * Wt + lx
+    gl.W = T.Wt; gl.H = T.nr; gl.WW = T.nc;
+    int err = 0;
+    const int nf = ccl_label(D.ccl, d_fg, d_cnt, gl, s, h, &err);
+    const int *d_list = D.ccl.list_p, *d_par = D.ccl.parent_p, *d_rank = D.ccl.rank_p;
+    const int *d_np = d_rank + nf;   // (pieces: on the device)
+    const size_t PC = (size_t)std::max(nf, 1);
+    int *pi = dptr<int>(D.pieces, 6 * PC + 4 * PC);
+    PieceDev P{pi, pi + PC, pi + 2 * PC, pi + 3 * PC, pi + 4 * PC, pi + 5 * PC,
+               reinterpret_cast<unsigned long long *>(pi + 6 * PC), reinterpret_cast<unsigned long long *>(pi + 8 * PC)};
+    int *d_pid = dptr<int>(D.pid, PC), *d_prank = dptr<int>(D.prank, PC);
+    int2 *d_border = dptr<int2>(D.border, PC);
     int *d_nb = dptr<int>(D.counts, 2);
-    AOS_HIP(hipMemsetAsync(d_nb, 0, 2 * sizeof(int), s));
-    std::vector<PieceRec> mine((size_t)npieces);
-    std::vector<int> h_n(npieces), h_root(npieces), h_box(4 * (size_t)npieces);
-    std::vector<unsigned long long> h_sx(npieces), h_sy(npieces);
-    int nb = 0;
-    std::vector<int2> h_border;
-    if (npieces > 0) {
-        k_dist_piece_init<<<cdiv(npieces, 256), 256, 0, s>>>(P, npieces);
-        k_dist_piece<<<cdiv(nf, 256), 256, 0, s>>>(d_list, d_par, d_rank, nf, W, T, P, d_border, d_nb);
-        AOS_HIP(hipMemcpyAsync(h_n.data(), P.n, sizeof(int) * npieces, hipMemcpyDeviceToHost, s));
-        AOS_HIP(hipMemcpyAsync(h_root.data(), P.root, sizeof(int) * npieces, hipMemcpyDeviceToHost, s));
-        AOS_HIP(hipMemcpyAsync(h_box.data(), P.box, sizeof(int) * 4 * npieces, hipMemcpyDeviceToHost, s));
-        AOS_HIP(hipMemcpyAsync(h_sx.data(), P.sx, 8 * (size_t)npieces, hipMemcpyDeviceToHost, s));
-        AOS_HIP(hipMemcpyAsync(h_sy.data(), P.sy, 8 * (size_t)npieces, hipMemcpyDeviceToHost, s));
-        AOS_HIP(hipMemcpyAsync(h, d_nb, sizeof(int), hipMemcpyDeviceToHost, s));
-        AOS_HIP(hipStreamSynchronize(s));
-        nb = h[0];
-        h_border.resize(nb);
-        if (nb) AOS_HIP(hipMemcpyAsync(h_border.data(), d_border, sizeof(int2) * nb, hipMemcpyDeviceToHost, s));
-        AOS_HIP(hipStreamSynchronize(s));
-        for (int i = 0; i < npieces; ++i)
-            mine[i] = PieceRec{h_root[i], h_n[i], (long long)h_sx[i], (long long)h_sy[i], h_box[4 * i], h_box[4 * i + 1],
-                               h_box[4 * i + 2], h_box[4 * i + 3]};
+    uint8_t *d_blob = dptr<uint8_t>(D.blob, (sizeof(PieceRec) + sizeof(int2)) * PC);
+    AOS_HIP(hipMemsetAsync(d_nb, 0, sizeof(int), s));
+    if (nf > 0) {
+        k_piece_init<<<cdiv(nf, 256), 256, 0, s>>>(P, d_np, nf);
+        k_piece_agg<<<cdiv(nf, kPcTB), kPcTB, 0, s>>>(d_list, d_par, d_rank, nf, T, W, g.H, P, d_pid, d_prank, d_border, d_nb);
+        k_piece_pack<<<cdiv(nf, 256), 256, 0, s>>>(P, d_np, d_border, d_nb, nf, d_blob);
+        AOS_HIP(hipGetLastError());
     }
+    peek_to_host(h + 2, {d_np, d_nb, D.ccl.lb.err_word(s)}, s);
+    AOS_HIP(hipStreamSynchronize(s));
+    const int npieces = nf > 0 ? h[2] : 0, nb = nf > 0 ? h[3] : 0;
+    err |= h[4];
     const auto t1 = clk::now();
 
-    // ---- 2. all-gather the tables; the same union-find on every rank
-    const std::vector<uint64_t> psz = gather_sizes(cm, sizeof(PieceRec) * (uint64_t)npieces);
-    const std::vector<uint64_t> bsz = gather_sizes(cm, sizeof(int2) * (uint64_t)nb);
-    uint64_t ptot = 0, btot = 0;
-    for (int r = 0; r < cm.world; ++r) { ptot += psz[r]; btot += bsz[r]; }
-    std::vector<PieceRec> all(ptot / sizeof(PieceRec));
-    std::vector<int2> allb(btot / sizeof(int2));
-    gather_bytes(cm, s, mine.data(), false, psz, all.data(), false);
-    gather_bytes(cm, s, h_border.data(), false, bsz, allb.data(), false);
-    const int NP = (int)all.size();
-    std::vector<int> proot(NP), pcl(NP), bc(allb.size()), br(allb.size());
+    // ---- 2. all-gather the tables (every rank's sizes and error word first); the same union-find on every rank
+    std::vector<int32_t> slots(2 * (size_t)world + 1, 0);
+    slots[2 * me] = npieces;
+    slots[2 * me + 1] = nb;
+    slots[2 * world] = err ? 1 : 0;
+    comm_max(cm, slots.data(), (int)slots.size());
+    if (slots[2 * world]) throw std::runtime_error("tiled cluster stage: a single-pass scan failed on a rank's device");
+    std::vector<uint64_t> bsz((size_t)world);
+    std::vector<int> rp0((size_t)world + 1, 0);   // first piece of rank r in the gathered table
+    uint64_t btot = 0;
+    int NB = 0;
+    for (int r = 0; r < world; ++r) {
+        bsz[r] = sizeof(PieceRec) * (uint64_t)slots[2 * r] + sizeof(int2) * (uint64_t)slots[2 * r + 1];
+        btot += bsz[r];
+        rp0[r + 1] = rp0[r] + slots[2 * r];
+        NB += slots[2 * r + 1];
+    }
+    uint8_t *hall = hptr<uint8_t>(D.h_all, btot);
+    gather_bytes(cm, s, d_blob, true, bsz, hall, false);
+    const int NP = rp0[world];
+    std::vector<PieceRec> all((size_t)NP);
+    std::vector<int> proot(NP), pcl(NP), bc((size_t)NB), br((size_t)NB);
+    {
+        uint64_t at = 0;
+        int nbk = 0;
+        for (int r = 0; r < world; ++r) {
+            const int n_p = slots[2 * r], n_b = slots[2 * r + 1];
+            std::memcpy(all.data() + rp0[r], hall + at, sizeof(PieceRec) * (size_t)n_p);
+            const int2 *b = reinterpret_cast<const int2 *>(hall + at + sizeof(PieceRec) * (size_t)n_p);
+            for (int k = 0; k < n_b; ++k, ++nbk) { bc[nbk] = b[k].x; br[nbk] = b[k].y; }
+            at += bsz[r];
+        }
+    }
     for (int i = 0; i < NP; ++i) proot[i] = all[i].root;
-    for (size_t i = 0; i < allb.size(); ++i) { bc[i] = allb[i].x; br[i] = allb[i].y; }
-    const int ncl = cluster_union(W, g.H, NP, proot.data(), (int)allb.size(), bc.data(), br.data(), pcl.data());
-    int my0 = 0;   // this rank's first piece in the gathered table
-    for (int r = 0; r < cm.rank; ++r) my0 += (int)(psz[r] / sizeof(PieceRec));
+    const int ncl = cluster_union(W, g.H, NP, proot.data(), NB, bc.data(), br.data(), pcl.data());
 
-    // ---- 3. per-cluster sums; long clusters
+    // ---- 3. per-cluster sums; long clusters and their owners
     struct Agg { long long sx = 0, sy = 0; int n = 0, minx = INT_MAX, maxx = INT_MIN, miny = INT_MAX, maxy = INT_MIN; };
     std::vector<Agg> agg((size_t)ncl);
     long long n_fg = 0;
@@ -321,88 +374,129 @@ void cluster_dist(ClusterDistState &D, const aos_comm &cm, const TilePlan &t, co
         if (diag >= min_len) { long_of[c] = (int)long_ids.size(); long_ids.push_back(c); long_cells += a.n; }
     }
     const int nlong = (int)long_ids.size();
+    st.n_long = nlong;
+    st.long_cells = (int)long_cells;
     std::vector<ClusterRec> lrec((size_t)nlong);
     if (nlong > 0) {
-        // ---- own cells of long clusters as keys, all-gathered, sorted: runs of raster-ordered cells
-        std::vector<int> lidx((size_t)std::max(npieces, 1), -1);
-        long long my_keys = 0;
-        for (int i = 0; i < npieces; ++i) {
-            lidx[i] = long_of[pcl[my0 + i]];
-            if (lidx[i] >= 0) my_keys += mine[i].n;
-        }
-        int *d_lidx = dptr<int>(D.lidx, lidx.size());
-        unsigned long long *d_keys = dptr<unsigned long long>(D.keys, (size_t)my_keys);
-        AOS_HIP(hipMemcpyAsync(d_lidx, lidx.data(), sizeof(int) * lidx.size(), hipMemcpyHostToDevice, s));
-        if (my_keys > 0) {
-            AOS_HIP(hipMemsetAsync(d_nb + 1, 0, sizeof(int), s));
-            k_dist_keys<<<cdiv(nf, 256), 256, 0, s>>>(d_list, d_par, d_rank, nf, d_lidx, d_keys, d_nb + 1);
-        }
-        const std::vector<uint64_t> ksz = gather_sizes(cm, 8ull * (uint64_t)my_keys);
-        const int nk = (int)long_cells;
-        unsigned long long *d_all = dptr<unsigned long long>(D.keys_all, 2 * (size_t)nk);
-        gather_bytes(cm, s, d_keys, true, ksz, d_all, true);
-        int bits = 1;
-        while ((1 << bits) <= nlong) ++bits;
-        size_t tbs = 0;
-        AOS_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tbs, d_all, d_all + nk, nk, 0, 32 + bits, s));
-        AOS_HIP(hipcub::DeviceRadixSort::SortKeys(D.tmp.ensure(std::max(std::max(tb, tbs), (size_t)64)), tbs, d_all,
-                                                  d_all + nk, nk, 0, 32 + bits, s));
-        int *d_cells = dptr<int>(D.cells, (size_t)nk), *d_coff = dptr<int>(D.coff, (size_t)nlong + 1);
-        k_dist_runs<<<cdiv(nk, 256), 256, 0, s>>>(d_all + nk, nk, nlong, d_cells, d_coff);
-        ClusterRec *d_rec = dptr<ClusterRec>(D.rec, (size_t)nlong);
-        launch_cluster_stats(d_coff, d_cells, nlong, g, d_poly, np, min_len, d_rec, s);
-        AOS_HIP(hipMemcpyAsync(lrec.data(), d_rec, sizeof(ClusterRec) * nlong, hipMemcpyDeviceToHost, s));
-        AOS_HIP(hipStreamSynchronize(s));
-        st.n_long = nlong;
-        st.long_cells = nk;
-
-        // ---- 4. replays: largest first, each to the least loaded rank (the same plan on every rank)
-        std::vector<int> flagged;
-        for (int l = 0; l < nlong; ++l)
-            if (lrec[l].flags & 2) flagged.push_back(l);
-        std::stable_sort(flagged.begin(), flagged.end(), [&](int a, int b) { return lrec[a].n > lrec[b].n; });
-        std::vector<long long> load((size_t)cm.world, 0);
-        std::vector<int> my_jobs;
-        for (int l : flagged) {
+        // owners: largest first, each to the least loaded rank (ties: the lowest rank) -- the same on every rank
+        std::vector<int> order((size_t)nlong), owner((size_t)nlong);
+        std::iota(order.begin(), order.end(), 0);
+        std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return agg[long_ids[a]].n > agg[long_ids[b]].n; });
+        std::vector<long long> load((size_t)world, 0);
+        for (int l : order) {
             const int r = (int)(std::min_element(load.begin(), load.end()) - load.begin());
-            load[r] += lrec[l].n;
-            if (r == cm.rank) my_jobs.push_back(l);
+            load[r] += agg[long_ids[l]].n;
+            owner[l] = r;
         }
-        pre.n_bfs = (int)flagged.size();
-        std::vector<long long> coff((size_t)nlong + 1);
-        std::vector<int> hoff((size_t)nlong + 1);
-        AOS_HIP(hipMemcpyAsync(hoff.data(), d_coff, sizeof(int) * (nlong + 1), hipMemcpyDeviceToHost, s));
-        AOS_HIP(hipStreamSynchronize(s));
-        long long my_cells = 0;
-        for (int l : my_jobs) my_cells += lrec[l].n;
-        std::vector<int> hc((size_t)my_cells);
-        std::vector<ReplayJob> jobs;
-        long long at = 0;
-        for (int l : my_jobs) {
-            AOS_HIP(hipMemcpyAsync(hc.data() + at, d_cells + hoff[l], sizeof(int) * lrec[l].n, hipMemcpyDeviceToHost, s));
-            jobs.push_back({l, hc.data() + at, lrec[l].n});
-            at += lrec[l].n;
+        // every rank's send layout: destination, then long cluster, then piece (all ranks compute all of them)
+        std::vector<std::vector<int>> lpieces((size_t)nlong);   // the pieces of each long cluster, by table index
+        for (int i = 0; i < NP; ++i)
+            if (long_of[pcl[i]] >= 0) lpieces[long_of[pcl[i]]].push_back(i);
+        std::vector<int> by_owner((size_t)nlong);   // long clusters ordered by (owner, id)
+        std::iota(by_owner.begin(), by_owner.end(), 0);
+        std::stable_sort(by_owner.begin(), by_owner.end(), [&](int a, int b) { return owner[a] < owner[b]; });
+        std::vector<uint64_t> cnt((size_t)world * world, 0);
+        std::vector<long long> piece_off((size_t)NP, -1);   // element offset inside its rank's send buffer
+        std::vector<long long> rank_at((size_t)world, 0);
+        auto rank_of = [&](int i) { return (int)(std::upper_bound(rp0.begin(), rp0.end(), i) - rp0.begin()) - 1; };
+        for (int l : by_owner)
+            for (int i : lpieces[l]) {
+                const int r = rank_of(i);
+                piece_off[i] = rank_at[r];
+                rank_at[r] += all[i].n;
+                cnt[(size_t)r * world + owner[l]] += 4ull * (uint64_t)all[i].n;
+            }
+        // ---- route the own cells of long pieces into the send layout
+        const long long my_send = rank_at[me];
+        int *d_send = dptr<int>(D.sendbuf, (size_t)my_send);
+        if (my_send > 0) {
+            int *hpo = hptr<int>(D.h_poff, (size_t)npieces);
+            for (int p = 0; p < npieces; ++p) hpo[p] = (int)piece_off[rp0[me] + p];
+            int *d_poff = dptr<int>(D.poff, (size_t)npieces);
+            copy_from_host(d_poff, hpo, sizeof(int) * npieces, s);
+            k_route<<<cdiv(nf, 256), 256, 0, s>>>(d_list, d_pid, d_prank, nf, d_poff, T, W, d_send);
+            AOS_HIP(hipGetLastError());
         }
-        AOS_HIP(hipStreamSynchronize(s));
-        const auto tr0 = clk::now();
-        replay_clusters(jobs, g, hp.data(), np, min_len, lrec.data());
-        st.ms_replay = std::chrono::duration<float, std::milli>(clk::now() - tr0).count();
-        st.n_replayed_here = (int)my_jobs.size();
-        std::vector<ReplayOut> outs;
-        for (int l : my_jobs) outs.push_back(ReplayOut{l, 0, lrec[l]});
-        const std::vector<uint64_t> rsz = gather_sizes(cm, sizeof(ReplayOut) * (uint64_t)outs.size());
-        uint64_t rtot = 0;
-        for (int r = 0; r < cm.world; ++r) rtot += rsz[r];
-        std::vector<ReplayOut> allr(rtot / sizeof(ReplayOut));
-        gather_bytes(cm, s, outs.data(), false, rsz, allr.data(), false);
-        for (const auto &o : allr) lrec[o.l] = o.r;
+        // ---- 4. exchange; the owned clusters' pieces side by side; statistics
+        std::vector<uint64_t> src_base;
+        const int *land = exchange_cells(cm, D, s, cnt, d_send, src_base);
+        std::vector<int> mine_l;   // owned long clusters, by id
+        for (int l = 0; l < nlong; ++l)
+            if (owner[l] == me) mine_l.push_back(l);
+        const int nown = (int)mine_l.size();
+        // s's block for this rank: s's pieces of the owned clusters by (cluster id, table index) -- the order
+        // s routed them in; a cluster's pieces in table order are rank-major, so one walk gives every segment
+        std::vector<Seg> segs;
+        std::vector<int> coff((size_t)nown + 1, 0);
+        {
+            std::vector<long long> blk_at((size_t)world, 0);
+            long long at = 0;
+            for (int j = 0; j < nown; ++j) {
+                coff[j] = (int)at;
+                for (int i : lpieces[mine_l[j]]) {
+                    const int r = rank_of(i);
+                    segs.push_back(Seg{(long long)src_base[r] + blk_at[r], at, all[i].n, 0});
+                    blk_at[r] += all[i].n;
+                    at += all[i].n;
+                }
+            }
+            coff[nown] = (int)at;
+        }
+        const int n_owned_cells = coff[nown];
+        if (nown > 0) {
+            Seg *hs = hptr<Seg>(D.h_segs, segs.size());
+            std::copy(segs.begin(), segs.end(), hs);
+            Seg *d_segs = dptr<Seg>(D.segs, segs.size());
+            copy_from_host(d_segs, hs, sizeof(Seg) * segs.size(), s);
+            int *hco = hptr<int>(D.h_coff, (size_t)nown + 1);
+            std::copy(coff.begin(), coff.end(), hco);
+            int *d_coff = dptr<int>(D.coff, (size_t)nown + 1);
+            copy_from_host(d_coff, hco, sizeof(int) * (nown + 1), s);
+            int *d_cells = dptr<int>(D.cells, (size_t)n_owned_cells);
+            k_segments<<<(int)segs.size(), 256, 0, s>>>(d_segs, land, d_cells);
+            ClusterRec *d_rec = dptr<ClusterRec>(D.rec, (size_t)nown);
+            launch_cluster_stats(d_coff, d_cells, nown, g, d_poly, npoly, min_len, d_rec, s);
+            ClusterRec *hr = hptr<ClusterRec>(D.h_rec, (size_t)nown);
+            copy_to_host(hr, d_rec, sizeof(ClusterRec) * nown, s);
+            AOS_HIP(hipStreamSynchronize(s));
+            std::vector<ClusterRec> orec(hr, hr + nown);
+            std::vector<int> flagged;
+            for (int j = 0; j < nown; ++j)
+                if (orec[j].flags & 2) flagged.push_back(j);
+            if (!flagged.empty()) {   // the owned flagged clusters' cells in one copy, then the exact replays
+                const int lo = coff[flagged.front()], hi = coff[flagged.back() + 1];
+                int *hc = hptr<int>(D.h_cells, (size_t)(hi - lo));
+                copy_to_host(hc, d_cells + lo, sizeof(int) * (size_t)(hi - lo), s);
+                AOS_HIP(hipStreamSynchronize(s));
+                std::vector<ReplayJob> jobs;
+                for (int j : flagged) jobs.push_back({j, hc + (coff[j] - lo), orec[j].n});
+                const auto tr0 = clk::now();
+                replay_clusters(jobs, g, hp, npoly, min_len, orec.data());
+                st.ms_replay = std::chrono::duration<float, std::milli>(clk::now() - tr0).count();
+                st.n_replayed_here = (int)flagged.size();
+            }
+            for (int j = 0; j < nown; ++j) lrec[mine_l[j]] = orec[j];
+        }
+        // ---- the owners' records to every rank (sizes known: the plan)
+        std::vector<uint64_t> rsz((size_t)world, 0);
+        for (int l = 0; l < nlong; ++l) rsz[owner[l]] += sizeof(OwnedOut);
+        OwnedOut *ho = hptr<OwnedOut>(D.h_out, (size_t)std::max(nown, 1));
+        for (int j = 0; j < nown; ++j) ho[j] = OwnedOut{mine_l[j], 0, lrec[mine_l[j]]};
+        OwnedOut *ha = hptr<OwnedOut>(D.h_tab, (size_t)nlong);
+        gather_bytes(cm, s, ho, false, rsz, ha, false);
+        int n_bfs_long = 0;
+        for (int k = 0; k < nlong; ++k) {
+            lrec[ha[k].l] = ha[k].r;
+            n_bfs_long += (ha[k].r.flags & 2) != 0;
+        }
+        pre.n_bfs = n_bfs_long;
     }
     const auto t2 = clk::now();
     st.n_pieces = npieces;
     st.n_border = nb;
     st.ms_local = std::chrono::duration<float, std::milli>(t1 - t0).count();
     st.ms_global = std::chrono::duration<float, std::milli>(t2 - t1).count();
-    if (cm.rank != root) return;
+    if (me != root) return;
 
     // ---- the root's records, in cluster order
     pre.rec.assign((size_t)ncl, ClusterRec{});

@@ -141,9 +141,22 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
 void assemble_rows(const std::vector<ClusterRec> &rec, SeedStageOut &out, std::vector<RowDev> &rows);
 
 // ------------------------------------------------------------------ distributed a8-a10 (cluster_dist.hip)
+// The union-find labelling of a foreground (bits, g.WW words x g.H rows; cnt: popcount per word) into the
+// raster-ordered list of its cells (local raster indices), parent[i] = list index of the first cell of i's
+// component and rank[] = the exclusive scan of the roots (rank[nf] = components, left on the device): the
+// whole-map stage's kernels (cluster_seed.hip). Returns nf (one host wait); *err = the scans' error word.
+struct GridC;
+struct CclScratch {
+    DevBuf off, list, parent, isroot, rank, edges;
+    LookBackScratch lb;
+    int *off_p = nullptr, *list_p = nullptr, *parent_p = nullptr, *rank_p = nullptr;
+};
+int ccl_label(CclScratch &B, const uint64_t *fg, int *cnt, const GridC &g, hipStream_t s, int *h_pinned2, int *err);
+
 struct ClusterDistState {
-    DevBuf poly, fg, cnt, off, list, parent, isroot, rank, pieces, border, counts, lidx, keys, keys_all, cells, coff, rec, tmp;
-    PinnedBuf h;
+    CclScratch ccl;
+    DevBuf poly, fg, cnt, pieces, pid, prank, border, counts, blob, poff, sendbuf, landing, segs, cells, coff, rec;
+    PinnedBuf h, h_poly, h_poff, h_segs, h_coff, h_rec, h_cells, h_out, h_tab, h_all;   // (one per upload / read-back)
 };
 struct ClusterDistStats {
     int n_pieces = 0, n_border = 0, n_long = 0, long_cells = 0, n_replayed_here = 0;
@@ -207,6 +220,8 @@ struct GvdState {
     void *scratch = nullptr;   // GvdScratch (gvd.hip), freed by free_gvd_scratch
     PinnedBuf h_seeds;   // seeds in / merged seeds out (g1)
     PinnedBuf h_out;     // the GvdGraph arrays, gathered on the device and copied back in one DMA
+    PinnedBuf h_evals;   // the graph searches' work counters (aos_params.gvd_count_evals)
+    aos_gvd_evals evals{};
     SyncEvent sev;       // host waits of this state's GVD calls (the stream may be shared by several lanes)
     Subdiv2D subdiv;   // host insert replay; kept across frames to reuse its allocations
     // host outputs

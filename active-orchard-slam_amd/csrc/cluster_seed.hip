@@ -548,6 +548,43 @@ __global__ void k_concat3(const double2 *a, const double2 *b, const double2 *c, 
 // ------------------------------------------------------------------ host orchestration
 template <class T> static T *dev(DevBuf &b, size_t n) { return static_cast<T *>(b.ensure(sizeof(T) * std::max<size_t>(n, 1))); }
 
+// The whole-map stage's labelling on any foreground given as bits (the tiled frame's own region, cluster_dist.hip):
+// list, block-local union-find in LDS, cross-chunk unions, flatten, root ranks. One host wait (for nf); the
+// component count stays on the device at rank + nf. err: the single-pass scans' error word (read with nf).
+int ccl_label(CclScratch &B, const uint64_t *fg, int *cnt, const GridC &g, hipStream_t s, int *h_pinned2, int *err) {
+    const size_t Cw = (size_t)g.WW * g.H;
+    int *d_off = dev<int>(B.off, Cw + 1);
+    scan_1p(B.lb, cnt, d_off, (int)Cw, false, s);
+    peek_to_host(h_pinned2, {d_off + Cw, B.lb.err_word(s)}, s);
+    AOS_HIP(hipStreamSynchronize(s));
+    *err = h_pinned2[1];
+    const int nf = *err ? 0 : h_pinned2[0];
+    B.list_p = dev<int>(B.list, nf);
+    B.parent_p = dev<int>(B.parent, nf);
+    int *d_isroot = dev<int>(B.isroot, (size_t)nf + 1);
+    B.rank_p = dev<int>(B.rank, (size_t)nf + 1);
+    B.off_p = d_off;
+    if (nf == 0) {
+        AOS_HIP(hipMemsetAsync(B.rank_p, 0, sizeof(int), s));
+        return 0;
+    }
+    const dim3 gw2(cdiv(g.WW, 64), g.H);
+    k_fg_list<<<gw2, 64, 0, s>>>(fg, d_off, B.list_p, g, nullptr);
+    const int ecap = std::max(4096, nf / 4);
+    int *d_ne = dev<int>(B.edges, 2 + 2 * (size_t)ecap);
+    int2 *d_edges = reinterpret_cast<int2 *>(d_ne + 2);
+    AOS_HIP(hipMemsetAsync(d_ne, 0, sizeof(int), s));
+    const int chunk = ccl_chunk();
+    k_ccl_local<<<cdiv(nf, chunk), ccl_tb(), sizeof(int) * chunk, s>>>(B.list_p, nf, fg, d_off, g, B.parent_p, d_edges, d_ne,
+                                                                      ecap - 1, chunk);
+    k_ccl_cross<<<256, 256, 0, s>>>(d_edges, d_ne, ecap - 1, B.parent_p);
+    k_ccl_union_if<<<cdiv(nf, 256), 256, 0, s>>>(B.list_p, nf, fg, d_off, g, B.parent_p, d_ne, ecap - 1);
+    k_ccl_flatten<<<cdiv(nf, 256), 256, 0, s>>>(B.parent_p, d_isroot, nf);
+    scan_1p(B.lb, d_isroot, B.rank_p, nf, false, s);
+    AOS_HIP(hipGetLastError());
+    return nf;
+}
+
 void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStageOut &out, hipStream_t s, hipEvent_t ev_mid,
                             const hipEvent_t *ev_split) {
     HostTrace tr{"cluster"};

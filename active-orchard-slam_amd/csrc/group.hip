@@ -83,6 +83,33 @@ int local_all_gather(void *user, uint64_t bytes) {
     return g.barrier() ? 0 : -1;   // nobody repacks its send buffer before every rank has read it
 }
 
+// every rank pulls the blocks addressed to it out of the others' send buffers (peer copies over xGMI)
+int local_all_to_all(void *user, const uint64_t *counts) {
+    Member &me = *static_cast<Member *>(user);
+    LocalGroup &g = *me.g;
+    if (!g.barrier()) return -1;   // every rank's send buffer is packed
+    if (hipSetDevice(me.device) != hipSuccess) { g.abort(); return -1; }
+    const int W = g.world;
+    uint64_t roff = 0;
+    for (int r = 0; r < W; ++r) {
+        const Member &src = *g.m[r];
+        uint64_t soff = 0;   // rank r's block for me in its send buffer
+        for (int q = 0; q < me.rank; ++q) soff += counts[(size_t)r * W + q];
+        const uint64_t n = counts[(size_t)r * W + me.rank];
+        if (n) {
+            char *dst = static_cast<char *>(me.recv.p) + roff;
+            const char *sp = static_cast<const char *>(src.send.p) + soff;
+            const hipError_t e = src.device == me.device
+                                     ? hipMemcpyAsync(dst, sp, n, hipMemcpyDeviceToDevice, me.stream)
+                                     : hipMemcpyPeerAsync(dst, me.device, sp, src.device, n, me.stream);
+            if (e != hipSuccess) { g.abort(); return -1; }
+        }
+        roff += n;
+    }
+    if (hipStreamSynchronize(me.stream) != hipSuccess) { g.abort(); return -1; }
+    return g.barrier() ? 0 : -1;
+}
+
 int local_all_reduce_max(void *user, int32_t *v, int32_t n) {
     Member &me = *static_cast<Member *>(user);
     LocalGroup &g = *me.g;
@@ -219,7 +246,8 @@ static int group_run(aos_group *G, int32_t root, aos_seedgen_out *root_out, cons
             set_error(std::string(what) + ": HIP error " + hipGetErrorString(e.e));
             return AOS_E_HIP;
         }
-        comms[r] = aos_comm{&m, r, world, m.send.p, m.recv.p, plan.exchange_bytes, local_all_gather, local_all_reduce_max};
+        comms[r] = aos_comm{&m, r, world, m.send.p, m.recv.p, plan.exchange_bytes, local_all_gather, local_all_reduce_max,
+                            local_all_to_all};
     }
     {
         std::lock_guard<std::mutex> l(G->g.mu);

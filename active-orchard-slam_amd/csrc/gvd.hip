@@ -95,8 +95,12 @@ __global__ void k_edges_to_occ(const float *e, int ne, double2 *occ) {
 // de-duplication (pos_of[c] = their index), found through its cell index (cells >= 0.5 m). The nearest
 // lies within 5 cm (extractBoundaryPoints kept it or a conflicting point within 5 cm / the same 1 cm
 // key), inside q's 3 x 3 cells; brute force otherwise.
+// evals (nullable, aos_params.gvd_count_evals): the number of candidates examined, added per thread
+__device__ __forceinline__ void eval_add(unsigned long long *evals, int k, long long v) {
+    if (evals && v > 0) atomicAdd(&evals[k], (unsigned long long)v);
+}
 __global__ void k_nearest(const double2 *occ, int n_occ, CellIdx ci, const int *pos_of, const double2 *bp, const int *M_dev,
-                          int *near_out) {
+                          int *near_out, unsigned long long *evals) {
     int o = blockIdx.x * blockDim.x + threadIdx.x;
     if (o >= n_occ) return;
     const double2 q = occ[o];
@@ -104,9 +108,11 @@ __global__ void k_nearest(const double2 *occ, int n_occ, CellIdx ci, const int *
     hash_cell(ci.h, q.x, q.y, cx, cy);
     double best = 1.7976931348623157e308;
     int bi = -1;
+    long long ne = 0;
     for (int yy = max(cy - 1, 0); yy <= min(cy + 1, ci.h.ny - 1); ++yy) {
         int k0, k1;
         ci_row(ci, yy, cx, k0, k1);
+        ne += k1 - k0;
         for (int k = k0; k < k1; ++k) {
             const int c = ci.items[k], i = pos_of[c];
             if (i < 0) continue;
@@ -121,14 +127,16 @@ __global__ void k_nearest(const double2 *occ, int n_occ, CellIdx ci, const int *
             double dx = bp[i].x - q.x, dy = bp[i].y - q.y, d = sqrt(dx * dx + dy * dy);
             if (d < best) { best = d; bi = i; }
         }
+        ne += M;
     }
     near_out[o] = bi;
+    eval_add(evals, 0, ne);
 }
 
 // all pairs i < j with 1e-6 < |bp_i - bp_j| <= 0.5 (gvd:861-894), CSR per i, j ascending (count pass:
 // poff == nullptr; entries past cap are dropped and flag the caller, who reruns with the exact size)
 __global__ void k_pairs(const double2 *bp, int no, const int *M_dev, CellIdx ci, const int *pos_of, const double2 *occ,
-                        const int *poff, int *pcount, int *plist, int cap) {
+                        const int *poff, int *pcount, int *plist, int cap, unsigned long long *evals) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= no) return;
     if (i >= *M_dev) { if (!poff) pcount[i] = 0; return; }
@@ -136,9 +144,11 @@ __global__ void k_pairs(const double2 *bp, int no, const int *M_dev, CellIdx ci,
     int cx, cy;
     hash_cell(ci.h, p.x, p.y, cx, cy);
     int c = 0, w = poff ? poff[i] : 0;
+    long long ne = 0;
     for (int yy = max(cy - 1, 0); yy <= min(cy + 1, ci.h.ny - 1); ++yy) {
         int k0, k1;
         ci_row(ci, yy, cx, k0, k1);
+        ne += k1 - k0;
         for (int k = k0; k < k1; ++k) {
             const int cc = ci.items[k], j = pos_of[cc];
             if (j <= i) continue;
@@ -154,6 +164,7 @@ __global__ void k_pairs(const double2 *bp, int no, const int *M_dev, CellIdx ci,
         }
     }
     if (!poff) pcount[i] = c;
+    eval_add(evals, 1, ne);
 }
 
 // candidate edge occurrences: [0, E) Voronoi edges, [E, E + P) pairs (P = poff[no] <= cap). from/to keep
@@ -178,7 +189,7 @@ __global__ void k_candidates(const int *near_idx, int ne, const int *poff, const
 // occurrence (a != b, both valid, no occupied sample) is counted in the group of its smaller node
 // (grank: its rank there) for the first-occurrence selection.
 __global__ void k_occupancy(const int2 *ft, const int *poff, int no, int ne, int cap, const double2 *bp, const int8_t *sk,
-                            GridG g, int *pass, int *gcnt, int *grank) {
+                            GridG g, int *pass, int *gcnt, int *grank, unsigned long long *evals) {
     int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= ne + min(poff[no], cap)) return;
     const int2 e2 = ft[c];
@@ -210,6 +221,7 @@ __global__ void k_occupancy(const int2 *ft, const int *poff, int no, int ne, int
             else { i0 = max(0, (int)floor(lo_t * num) - 2); i1 = min(num, (int)ceil(hi_t * num) + 2); }
         }
         for (int ib = i0; ib <= i1 && num >= 0 && !hit; ib += 16) {   // 16 independent samples in flight
+            if (evals) eval_add(evals, 2, min(16, i1 - ib + 1));
             bool h16[16];
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
@@ -297,7 +309,8 @@ struct LabelRow { double ex, ey, ox, oy; double deg, cs, sn; };  // endpoint, ot
 // around the endpoint, which hold every node with z <= 25 (1 + 1e-12); a job scanned all ~10^5 nodes
 // before (≈ 177 us per C2 frame).
 __global__ __launch_bounds__(256) void k_label_points(const LabelRow *jobs, int nj, const double2 *nodes, const int *Mn_dev,
-                                                      GridG g, const int8_t *sk, CellIdx cn, double2 *pts, int *valid) {
+                                                      GridG g, const int8_t *sk, CellIdx cn, double2 *pts, int *valid,
+                                                      unsigned long long *evals) {
     const int jb = blockIdx.x;
     if (jb >= nj) return;
     const int Mn = *Mn_dev;
@@ -320,10 +333,12 @@ __global__ __launch_bounds__(256) void k_label_points(const LabelRow *jobs, int 
     int cx, cy;
     hash_cell(cn.h, J.ex, J.ey, cx, cy);
     const double two_cells = 2.0 / cn.h.inv * (1.0 - 1e-9);
+    long long ntest = 0;
     for (int pass = 0; pass < 3; ++pass) {
         double best = 1.7976931348623157e308;
         int bi = INT_MAX;
         auto test = [&](int i) {
+            ++ntest;
             double dx = nodes[i].x - J.ex, dy = nodes[i].y - J.ey;
             double z = dx * dx + dy * dy;
             if (pass == 0 && !(z <= 25.0 * (1.0 + 1e-12))) return;
@@ -365,7 +380,16 @@ __global__ __launch_bounds__(256) void k_label_points(const LabelRow *jobs, int 
         if (si[0] != INT_MAX && (pass != 1 || sb[0] < two_cells)) break;
         __syncthreads();
     }
+    eval_add(evals, 3, ntest);
     if (threadIdx.x != 0) return;
+    if (evals) {   // the radii the reference scans all nodes for: 5, 7, 9, 2 diag until one has a candidate
+        const double r[4] = {5.0, 7.0, 9.0, g.diag2};
+        int scans = 4;
+        if (si[0] != INT_MAX)
+            for (int k = 0; k < 4; ++k)
+                if (sb[0] <= r[k]) { scans = k + 1; break; }
+        atomicAdd(&evals[4], (unsigned long long)scans);
+    }
     if (si[0] != INT_MAX) { pts[jb] = nodes[si[0]]; valid[jb] = 1; return; }
     // castRay gvd:558-684 (angles +-90: cos/sin from the host table in J.deg's sign)
     double ex = J.ox - J.ex, ey = J.oy - J.ey;
@@ -590,7 +614,7 @@ struct GvdScratch {
     DevBuf raw, ok, leaders, merged, owner, oidx, sowner, sidx, tmp, edges_f, occ, occ_ok, bp, kept_occ, keys, idx, skeys,
         sidx2, near_idx, pk, pidx, pskeys, psidx, pcount, poff, plist, ft, ckey, cvalid, pass, k2, occ_idx, sk2, socc, selected,
         inside, ipos, nodes, keep, kpos, edges, lens, jobs, nkeys, nidx, qkeys, qidx, lpts, lval, lmask, lcidx, lcount, loff, lcl, lty, scan_tmp,
-        gather, misc, gcnt, goff, glist;
+        gather, misc, gcnt, goff, glist, evals;
     bool gcnt_dirty = true;           // gcnt (edge groups' counts) not known to be zero
     CellScratch ci_nodes, ci_labels;  // g8 / g9 indices (g5 / g6 use the de-duplication's own)
     CellIdx cq{};
@@ -956,9 +980,14 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
 
     // ---- g6 graph edges
     int *d_near = dev<int>(S.near_idx, no);
-    k_nearest<<<cdiv(no, 256), 256, 0, s>>>(d_occ, no, cio, d_pos_of, d_bp, d_M, d_near);
+    unsigned long long *d_evals = nullptr;   // (aos_params.gvd_count_evals)
+    if (P.gvd_count_evals) {
+        d_evals = dev<unsigned long long>(S.evals, 8);
+        AOS_HIP(hipMemsetAsync(d_evals, 0, 8 * sizeof(unsigned long long), s));
+    }
+    k_nearest<<<cdiv(no, 256), 256, 0, s>>>(d_occ, no, cio, d_pos_of, d_bp, d_M, d_near, d_evals);
     int *d_pcount = dev<int>(S.pcount, no), *d_poff = dev<int>(S.poff, no + 1);
-    k_pairs<<<cdiv(no, 256), 256, 0, s>>>(d_bp, no, d_M, cio, d_pos_of, d_occ, nullptr, d_pcount, nullptr, 0);
+    k_pairs<<<cdiv(no, 256), 256, 0, s>>>(d_bp, no, d_M, cio, d_pos_of, d_occ, nullptr, d_pcount, nullptr, 0, d_evals);
     scan_1p(S.lb, d_pcount, d_poff, no, false, s);
     // The pair lists get a capacity from the last frame (P is read back only with the frame's sizes below);
     // a frame with more pairs runs the rest again with the exact size.
@@ -992,7 +1021,7 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     for (int attempt = 0;; ++attempt) {
         const int ncap = ne + cap;
         int *d_plist = dev<int>(S.plist, cap);
-        k_pairs<<<cdiv(no, 256), 256, 0, s>>>(d_bp, no, d_M, cio, d_pos_of, d_occ, d_poff, nullptr, d_plist, cap);
+        k_pairs<<<cdiv(no, 256), 256, 0, s>>>(d_bp, no, d_M, cio, d_pos_of, d_occ, d_poff, nullptr, d_plist, cap, d_evals);
         int2 *d_ft = dev<int2>(S.ft, ncap);
         int *d_pass = dev<int>(S.pass, ncap), *d_grank = dev<int>(S.occ_idx, ncap), *d_sel = dev<int>(S.selected, ncap);
         const size_t gc0 = S.gcnt.cap;
@@ -1001,7 +1030,8 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
         S.gcnt_dirty = true;
         int *d_goff = dev<int>(S.goff, no + 1), *d_glist = dev<int>(S.glist, ncap);
         k_candidates<<<cdiv(ncap, 256), 256, 0, s>>>(d_near, ne, d_poff, d_plist, d_M, no, cap, d_ft);
-        k_occupancy<<<cdiv(ncap, 64), 64, 0, s>>>(d_ft, d_poff, no, ne, cap, d_bp, in.d_skeleton, g, d_pass, d_gcnt, d_grank);
+        k_occupancy<<<cdiv(ncap, 64), 64, 0, s>>>(d_ft, d_poff, no, ne, cap, d_bp, in.d_skeleton, g, d_pass, d_gcnt, d_grank,
+                                                  d_evals);
         scan_1p(S.lb, d_gcnt, d_goff, no, true, s);   // (leaves the group counts zero)
         S.gcnt_dirty = false;
         k_group_scatter<<<cdiv(ncap, 256), 256, 0, s>>>(d_ft, d_pass, d_poff, no, ne, cap, d_goff, d_grank, d_glist);
@@ -1023,7 +1053,7 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
         if (nj) {
             const HashG hl = make_hash_n(g.minx - 10.0, g.maxx + 10.0, g.miny - 10.0, g.maxy + 10.0, 5.01, no);
             const CellIdx cn = cell_index_build(S.ci_nodes, d_nodes, nullptr, no, hl, s, d_Mn);
-            k_label_points<<<nj, 256, 0, s>>>(d_jobs, nj, d_nodes, d_Mn, g, in.d_skeleton, cn, d_lp, d_lv);
+            k_label_points<<<nj, 256, 0, s>>>(d_jobs, nj, d_nodes, d_Mn, g, in.d_skeleton, cn, d_lp, d_lv, d_evals);
         }
         // ---- g9 node labels: the valid label points in cells of >= 0.1 m
         const HashG hq = make_hash_n(g.minx - 1.0, g.maxx + 1.0, g.miny - 1.0, g.maxy + 1.0, 0.1, nj);
@@ -1084,9 +1114,23 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
         k_gather_words<<<cdiv(total, 256), 256, 0, s>>>(sl, d_g);
         AOS_HIP(hipMemcpyAsync(h_out, d_g, sizeof(int) * (size_t)total, hipMemcpyDeviceToHost, s));
     }
+    unsigned long long *h_ev = d_evals ? static_cast<unsigned long long *>(G.h_evals.ensure(8 * sizeof(unsigned long long))) : nullptr;
+    if (d_evals) AOS_HIP(hipMemcpyAsync(h_ev, d_evals, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     AOS_HIP(hipEventRecord(ev[9], s));
     G.sev.sync(s);
     tr.mark("out");
+    G.evals = aos_gvd_evals{};
+    if (h_ev) {   // the work of the searches (SURVEY §8d "pair evaluations"), the reference's beside the GPU's
+        aos_gvd_evals &E = G.evals;
+        const uint64_t M = (uint64_t)G.n_bpts;
+        E.counted = 1;
+        E.n_label_jobs = nj_out;
+        E.edge_ends = (uint64_t)no; E.boundary_points = M; E.filtered_nodes = (uint64_t)Mn;
+        E.ref_nearest = (uint64_t)no * M;                        // gvd:812-824 per edge end, every boundary point
+        E.ref_pairs = M ? M * (M - 1) / 2 : 0;                   // gvd:861-894
+        E.ref_labels = nj_out ? h_ev[4] * (uint64_t)Mn : 0;      // gvd:731-774, once per radius tried
+        E.gpu_nearest = h_ev[0]; E.gpu_pairs = h_ev[1]; E.gpu_samples = h_ev[2]; E.gpu_labels = h_ev[3];
+    }
     for (const Out &o : outs)
         if (o.words > 0) { std::memcpy(o.h, h_out, sizeof(int) * (size_t)o.words); h_out += o.words; }
     G.have_markers = P.gvd_markers != 0;

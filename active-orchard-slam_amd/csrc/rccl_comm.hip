@@ -13,6 +13,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "aos_ctx.h"
 
@@ -24,6 +25,10 @@ struct RcclApi {
     ncclResult_t (*comm_init_rank)(ncclComm_t *, int, ncclUniqueId, int);
     ncclResult_t (*all_gather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t);
     ncclResult_t (*all_reduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t);
+    ncclResult_t (*send)(const void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
+    ncclResult_t (*recv)(void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
+    ncclResult_t (*group_start)();
+    ncclResult_t (*group_end)();
     ncclResult_t (*comm_destroy)(ncclComm_t);
     const char *(*error_string)(ncclResult_t);
 };
@@ -45,6 +50,10 @@ const RcclApi &rccl_api() {
         api.comm_init_rank = reinterpret_cast<decltype(api.comm_init_rank)>(sym("ncclCommInitRank"));
         api.all_gather = reinterpret_cast<decltype(api.all_gather)>(sym("ncclAllGather"));
         api.all_reduce = reinterpret_cast<decltype(api.all_reduce)>(sym("ncclAllReduce"));
+        api.send = reinterpret_cast<decltype(api.send)>(sym("ncclSend"));
+        api.recv = reinterpret_cast<decltype(api.recv)>(sym("ncclRecv"));
+        api.group_start = reinterpret_cast<decltype(api.group_start)>(sym("ncclGroupStart"));
+        api.group_end = reinterpret_cast<decltype(api.group_end)>(sym("ncclGroupEnd"));
         api.comm_destroy = reinterpret_cast<decltype(api.comm_destroy)>(sym("ncclCommDestroy"));
         api.error_string = reinterpret_cast<decltype(api.error_string)>(sym("ncclGetErrorString"));
     });
@@ -84,6 +93,40 @@ static int rc_all_gather(void *user, uint64_t bytes) {
         DeviceScope ds(r->device);
         if (bytes > r->c.buf_bytes) return 1;
         rccl_check(api, api.all_gather(r->send.p, r->recv.p, bytes, ncclUint8, r->comm, r->stream), "ncclAllGather");
+        return hipStreamSynchronize(r->stream) == hipSuccess ? 0 : 1;
+    } catch (...) {
+        return 1;
+    }
+}
+
+// point-to-point blocks of the personalised exchange: one ncclGroupStart / ncclGroupEnd around a send and a
+// receive per peer (the own block is a device copy); every link of the xGMI mesh carries its pair at once
+static int rc_all_to_all(void *user, const uint64_t *counts) {
+    aos_rccl *r = static_cast<aos_rccl *>(user);
+    try {
+        const RcclApi &api = rccl_api();
+        DeviceScope ds(r->device);
+        const int W = r->c.world, me = r->c.rank;
+        uint64_t soff = 0, roff = 0;
+        std::vector<uint64_t> so(W), ro(W);
+        for (int q = 0; q < W; ++q) {
+            so[q] = soff; soff += counts[(size_t)me * W + q];
+            ro[q] = roff; roff += counts[(size_t)q * W + me];
+        }
+        if (soff > r->c.buf_bytes || roff > r->c.buf_bytes * (uint64_t)W) return 1;
+        const char *sb = static_cast<const char *>(r->send.p);
+        char *rb = static_cast<char *>(r->recv.p);
+        if (const uint64_t n = counts[(size_t)me * W + me])
+            AOS_HIP(hipMemcpyAsync(rb + ro[me], sb + so[me], n, hipMemcpyDeviceToDevice, r->stream));
+        rccl_check(api, api.group_start(), "ncclGroupStart");
+        for (int q = 0; q < W; ++q) {
+            if (q == me) continue;
+            if (const uint64_t n = counts[(size_t)me * W + q])
+                rccl_check(api, api.send(sb + so[q], n, ncclUint8, q, r->comm, r->stream), "ncclSend");
+            if (const uint64_t n = counts[(size_t)q * W + me])
+                rccl_check(api, api.recv(rb + ro[q], n, ncclUint8, q, r->comm, r->stream), "ncclRecv");
+        }
+        rccl_check(api, api.group_end(), "ncclGroupEnd");
         return hipStreamSynchronize(r->stream) == hipSuccess ? 0 : 1;
     } catch (...) {
         return 1;
@@ -133,6 +176,7 @@ aos_rccl *rccl_create(const uint8_t *id, int rank, int world, int device, uint64
     r->c.buf_bytes = buf_bytes;
     r->c.all_gather = rc_all_gather;
     r->c.all_reduce_max = rc_all_reduce_max;
+    r->c.all_to_all = rc_all_to_all;
     return r;
 }
 

@@ -24,9 +24,12 @@ void aos_ctx::release() {
                       &full_infl, &full_skel, &map_buf, &scan_stage})
         b->release();
     thin_graphs_release();
+    try { expander.join(); } catch (...) {}   // (before its buffers go)
     if (copy_stream) {
         (void)hipStreamSynchronize(copy_stream);
         (void)hipEventDestroy(copy_ready);
+        if (copy_done) (void)hipEventDestroy(copy_done);
+        copy_done = nullptr;
         (void)hipStreamDestroy(copy_stream);
         copy_stream = nullptr;
     }
@@ -34,6 +37,8 @@ void aos_ctx::release() {
     h_stats.release();
     h_occ.release();
     h_skel.release();
+    h_occ_bits.release();
+    h_skel_bits.release();
     for (DevBuf *b : {&cs.fg_bits, &cs.word_cnt, &cs.word_off, &cs.fg_list, &cs.parent, &cs.root_flag, &cs.root_rank,
                       &cs.cl_count, &cs.cl_off, &cs.cl_cursor, &cs.cl_cells, &cs.rec, &cs.row_idx, &cs.cur_tab,
                       &cs.poly, &cs.cand_xy, &cs.cand_ok, &cs.cand_state, &cs.hash_count,
@@ -913,11 +918,21 @@ bool aos_ctx::run_seedgen_once(bool want_host, aos_seedgen_out &out, bool allow_
     return false;
 }
 
-// The published grids' D2H: hipMemcpyAsync (DMA), or a kernel of grid_copy_blocks() workgroups with
-// AOS_GRID_COPY_KERNEL=1. Round 4's host timelines (AOS_TRACE) caught hipMemcpyAsync of the grids holding the
-// host for 3-7 ms in some frames of some processes (that frame's seed-gen: 9 ms instead of 1.5); the kernel
-// copy never holds the host, but beside the cluster stage it stretches the stage's kernels from 0.32 to
-// 0.87 ms in every frame (profiles/r04p_grid_copy_kernel_ab.txt), so the DMA stays the default.
+// The published grids' D2H. Default (AOS_GRID_READBACK=1, round 5): the two bit-packed grids (the inflated
+// grid and the frameless skeleton, W*H/8 bytes each) cross PCIe and host threads expand them to the {0, 100}
+// bytes with the frame / rectangle while the cluster stage runs (grid_host.cpp). Round 4's traces showed the
+// byte grids' D2H as runtime blit kernels (__amd_rocclr_copyBuffer, 0.65 ms per C2 frame, 2.6 ms at C3) that
+// stretched the cluster stage's kernels beside them (k_fg 18 -> 280 us): the bits are 8x fewer bytes through
+// them. AOS_GRID_READBACK=0: the byte grids by hipMemcpyAsync (round 4), or AOS_GRID_COPY_KERNEL=1 by a kernel of
+// grid_copy_blocks() workgroups.
+static int grid_readback_bits() {
+    static const int v = [] { const char *e = getenv("AOS_GRID_READBACK"); return e ? atoi(e) : 1; }();
+    return v;
+}
+static int grid_expand_threads() {   // AOS_GRID_EXPAND_THREADS (default 8)
+    static const int v = [] { const char *e = getenv("AOS_GRID_EXPAND_THREADS"); return e ? std::max(1, atoi(e)) : 8; }();
+    return v;
+}
 static int grid_copy_blocks() {   // AOS_GRID_COPY_BLOCKS (default 64)
     static const int b = [] { const char *e = getenv("AOS_GRID_COPY_BLOCKS"); return e ? std::max(1, atoi(e)) : 64; }();
     return b;
@@ -939,6 +954,7 @@ void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *c
     // ---------------- a16 /skeletonized_occupancy_grid = skeleton + polygon bbox rectangle
     int8_t *d_skel = static_cast<int8_t *>(skel_bytes.ensure(C));
     launch_bits_to_bytes(skel_bits, d_skel, g, 0, s);
+    int rect[4] = {0, 0, 0, 0};   // markPolygonBoundaryAsOccupied's rectangle: gx0, gy0, gx1, gy1
     {
         double hminx = poly[0].first, hmaxx = poly[0].first, hminy = poly[0].second, hmaxy = poly[0].second;
         for (const auto &pt : poly) {
@@ -953,23 +969,45 @@ void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *c
             gx = gx < 0 ? 0 : (gx >= g.W ? g.W - 1 : gx);
             gy = gy < 0 ? 0 : (gy >= g.H ? g.H - 1 : gy);
         };
-        int gx0, gy0, gx1, gy1;
-        w2g(static_cast<float>(hminx - margin), static_cast<float>(hminy - margin), gx0, gy0);
-        w2g(static_cast<float>(hmaxx + margin), static_cast<float>(hmaxy + margin), gx1, gy1);
-        launch_draw_rect(d_skel, g, gx0, gy0, gx1, gy1, s);
+        w2g(static_cast<float>(hminx - margin), static_cast<float>(hminy - margin), rect[0], rect[1]);
+        w2g(static_cast<float>(hmaxx + margin), static_cast<float>(hmaxy + margin), rect[2], rect[3]);
+        launch_draw_rect(d_skel, g, rect[0], rect[1], rect[2], rect[3], s);
     }
     // the two published grids go to host memory on the copy stream while the cluster / seed stage runs
     // (AOS_GRID_COPY=1: after it instead; the copy's blit kernels share the CUs with the stage's kernels)
     static const int grid_copy_mode = [] { const char *e = getenv("AOS_GRID_COPY"); return e ? atoi(e) : 0; }();
+    const bool as_bits = grid_readback_bits() != 0;
     auto issue_grid_copy = [&]() {
         h_occ.ensure(std::max<size_t>(C, 1)); h_skel.ensure(std::max<size_t>(C, 1));
         if (!copy_stream) {
             AOS_HIP(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
             AOS_HIP(hipEventCreateWithFlags(&copy_ready, hipEventDisableTiming));
+            AOS_HIP(hipEventCreateWithFlags(&copy_done, hipEventDisableTiming));
         }
         AOS_HIP(hipEventRecord(copy_ready, s));
         AOS_HIP(hipStreamWaitEvent(copy_stream, copy_ready, 0));
-        if (grid_copy_kernel()) {   // (a kernel launch never holds the host; see copy_kernel_bulk)
+        if (as_bits) {
+            const size_t nb = 8 * (size_t)g.WW * g.H;
+            const uint64_t *ib = tiled_frame ? full_infl.as<uint64_t>() : infl_bits.as<uint64_t>();
+            uint64_t *hob = static_cast<uint64_t *>(h_occ_bits.ensure(std::max<size_t>(nb, 8)));
+            uint64_t *hsb = static_cast<uint64_t *>(h_skel_bits.ensure(std::max<size_t>(nb, 8)));
+            AOS_HIP(hipMemcpyAsync(hob, ib, nb, hipMemcpyDeviceToHost, copy_stream));
+            AOS_HIP(hipMemcpyAsync(hsb, skel_bits, nb, hipMemcpyDeviceToHost, copy_stream));
+            AOS_HIP(hipEventRecord(copy_done, copy_stream));
+            GridExpander::Job j{};
+            const int dev = device;
+            hipEvent_t e = copy_done;
+            j.wait = [dev, e] {
+                AOS_HIP(hipSetDevice(dev));
+                AOS_HIP(hipEventSynchronize(e));
+            };
+            j.occ_bits = hob; j.skel_bits = hsb;
+            j.occ = h_occ.as<int8_t>(); j.skel = h_skel.as<int8_t>();
+            j.W = g.W; j.H = g.H; j.WW = g.WW; j.frame = 5;
+            j.rect[0] = rect[0]; j.rect[1] = rect[1]; j.rect[2] = rect[2]; j.rect[3] = rect[3];
+            j.threads = grid_expand_threads();
+            expander.start(j);
+        } else if (grid_copy_kernel()) {   // (a kernel launch never holds the host; see copy_kernel_bulk)
             copy_kernel_bulk(h_occ.p, d_occ, C, grid_copy_blocks(), copy_stream);
             copy_kernel_bulk(h_skel.p, d_skel, C, grid_copy_blocks(), copy_stream);
         } else {
@@ -993,7 +1031,10 @@ void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *c
     tr.mark("stage_done");
     AOS_HIP(hipStreamSynchronize(s));
     tr.mark("stream_synced");
-    if (want_host) AOS_HIP(hipStreamSynchronize(copy_stream));
+    if (want_host) {
+        if (as_bits) expander.join();   // (rethrows a failed wait)
+        else AOS_HIP(hipStreamSynchronize(copy_stream));
+    }
     tr.mark("copies_synced");
     if (clipped_total) {
         n_clipped = *clipped_total;

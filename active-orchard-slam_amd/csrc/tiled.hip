@@ -198,6 +198,15 @@ int timed_gather(void *u, uint64_t bytes) {
     t.bytes_gather += bytes;
     return r;
 }
+int timed_all_to_all(void *u, const uint64_t *counts) {   // (counted with the all-gathers: data movement)
+    TimedComm &t = *static_cast<TimedComm *>(u);
+    const auto t0 = std::chrono::steady_clock::now();
+    const int r = t.inner.all_to_all(t.inner.user, counts);
+    t.ms_gather += ms_since(t0);
+    ++t.n_gather;
+    for (int d = 0; d < t.inner.world; ++d) t.bytes_gather += counts[(size_t)t.inner.rank * t.inner.world + d];
+    return r;
+}
 int timed_reduce(void *u, int32_t *v, int32_t n) {
     TimedComm &t = *static_cast<TimedComm *>(u);
     const auto t0 = std::chrono::steady_clock::now();
@@ -214,6 +223,7 @@ void aos_ctx::run_tiled(const aos_comm &cm, int tiles_x, int tiles_y, int root, 
     w.user = &tc;
     w.all_gather = cm.all_gather ? timed_gather : nullptr;
     w.all_reduce_max = cm.all_reduce_max ? timed_reduce : nullptr;
+    w.all_to_all = cm.all_to_all ? timed_all_to_all : nullptr;
     const auto t0 = std::chrono::steady_clock::now();
     const uint64_t skipped0 = ror_skipped;
     auto record = [&]() {

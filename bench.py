@@ -89,7 +89,7 @@ def parse(argv=None):
                          "as the grids are returned)")
     ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--sustain-s", type=float, default=None,
-                    help="seconds of the sustained pipelined leg when the CPU baseline runs in its child process "
+                    help="seconds of the sustained device-resident seed-gen leg while the CPU baseline runs in its child "
                          "(default: as long as the child's frame takes, at most 300 s)")
     ap.add_argument("--fixed-root", action="store_true",
                     help="--tiled: rank 0 finishes every frame (default: frame k's root is rank k mod N, so the "
@@ -214,7 +214,7 @@ def spawn_cpu_baseline(a):
     """The CPU baseline runs in a child process pinned to one core of this process's CPU set; this process keeps
     the other cores (set before torch and the library start any thread, so every later thread inherits it). The
     child builds its cloud at once and starts the timed oracle frame when told to (after the main timed region),
-    while this process runs the sustained pipelined leg on the GPU. Started before anything touches the GPU (no
+    while this process runs the sustained seed-gen leg on the GPU. Started before anything touches the GPU (no
     exec from a process that has initialised it). Returns the Popen, or None (then the baseline runs inline)."""
     import subprocess
     allowed = sorted(os.sched_getaffinity(0))
@@ -260,8 +260,8 @@ def finish_cpu_baseline(child) -> dict:
     if child.returncode != 0 or not lines:
         return {"error": f"CPU baseline child exited {child.returncode}"}
     r = json.loads(lines[-1])
-    r["sample"] += ("; timed in a child process pinned to its own core while this process ran the sustained "
-                    "pipelined GPU leg on the other cores")
+    r["sample"] += ("; timed in a child process pinned to its own core while this process ran device-resident "
+                    "seed-gen frames on the GPU from the other cores")
     return r
 
 
@@ -696,32 +696,53 @@ def run(a, E, dist, quiet=False):
         extra["device_resident"] = {"value": round(units / dmed, 3), "median_ms": round(dmed * 1e3, 3),
                                     "ms_per_step": round(ddt / a.steps * 1e3, 3),
                                     "io": "cloud already in HBM, OccupancyGrids left in HBM, GvdGraph + seeds to host"}
+    if not (a.stream or a.tiled):
+        # SURVEY §8d's GVD figure: the graph phase's "pair evaluations" (one counted frame outside the timed
+        # region: the counts are a function of the frame's inputs; rates over the timed frames' graph phase)
+        ctx.gvd_set_count_evals(True)
+        ctx.seedgen(d_cloud.data_ptr(), n_points=n, on_device=True, want_host=False)
+        ctx.gvd_set_markers(False)
+        ctx.gvd_from_seedgen(copy=False)
+        ev = ctx.gvd_evals()
+        ctx.gvd_set_count_evals(False)
+        t_graph = stage_p50.get("gvd_graph", 0.0)
+        ref = ev["ref_nearest"] + ev["ref_pairs"] + ev["ref_labels"]
+        gpu = ev["gpu_nearest"] + ev["gpu_pairs"] + ev["gpu_labels"]
+        extra["gvd_evals"] = {
+            **ev, "graph_ms_p50": t_graph,
+            "ref_pair_evals_per_s": round(ref / (t_graph * 1e-3), 1) if t_graph > 0 else None,
+            "gpu_pair_evals_per_s": round(gpu / (t_graph * 1e-3), 1) if t_graph > 0 else None,
+            "gpu_samples_per_s": round(ev["gpu_samples"] / (t_graph * 1e-3), 1) if t_graph > 0 else None,
+            "what": "the GVD graph phase's searches (g6 nearest boundary point per edge end, gvd:812-824; pairs "
+                    "<= 0.5 m, gvd:861-894; occupancy samples, gvd:320-359; label points, gvd:686-790): ref_* = the "
+                    "distance evaluations the reference makes on this frame, gpu_* = the candidates the kernels "
+                    "examined (cell-index neighbourhoods); rates over the timed frames' graph phase (p50, all "
+                    "of its kernels); per-kernel times in the committed kernel trace"}
     child = E.get("cpu_child") if (world == 1 and not quiet) else None
     if child is not None:
         # the CPU baseline's frame runs in its child (pinned to its own core) from now on; meanwhile this process
-        # keeps the GPU busy with the pipelined loop in chunks of 40 frames (each with 2 untimed warmup frames
-        # and its own drain) until the child is done: a sustained-rate figure beside the short legs above
+        # keeps the GPU busy with device-resident seed-gen frames (cloud in HBM, grids left there, no GVD): GPU
+        # work with little host work beside it (the GVD's host replays would compete with the child for memory
+        # bandwidth and slow the baseline down), and a sustained seed-gen rate beside the short legs above
         start_cpu_baseline(child)
         limit = a.sustain_s if a.sustain_s is not None else 300.0
         _progress(f"CPU baseline (oracle, child process pinned to core {child.core}) beside the sustained "
-                  f"pipelined leg (<= {limit:.0f} s)")
-        t_s0, s_frames, s_time, s_lat = time.perf_counter(), 0, 0.0, []
+                  f"device-resident seed-gen leg (<= {limit:.0f} s)")
+        t_s0, s_frames, s_gpu = time.perf_counter(), 0, []
         while True:
-            reset(True, host_io, 40, 2)
-            sdt, sres, _ = timed_region(step, 40, 2, 1, sync)
-            s_frames += len(sres)
-            s_time += sdt
-            s_lat += [1e3 * pend["lat"][k] for k in range(2, 42) if k in pend["lat"]]
+            gs = ctx.seedgen(d_cloud.data_ptr(), n_points=n, on_device=True, want_host=False)
+            s_frames += 1
+            s_gpu.append(gs["ms"]["total"])
             el = time.perf_counter() - t_s0
-            if el >= limit or (a.sustain_s is None and child.poll() is not None):
+            if el >= limit or (a.sustain_s is None and s_frames % 50 == 0 and child.poll() is not None):
                 break
-        s_lat.sort()
-        extra["sustained_pipelined"] = {
-            "value": round(units * s_frames / s_time, 3), "unit": "Mcells/s", "depth": mode["depth"],
-            "frames": s_frames, "seconds": round(s_time, 2),
-            "frame_latency_ms": {"p50": round(_median(s_lat), 2), "max": round(s_lat[-1], 2)} if s_lat else None,
-            "what": "the pipelined loop run for as long as the CPU baseline's frame takes (chunks of 40 frames, "
-                    "drained at each chunk's end); this process's threads exclude the child's core"}
+        sync()
+        el = time.perf_counter() - t_s0
+        extra["sustained_seedgen"] = {
+            "value": round(cells / 1e6 * s_frames / el, 3), "unit": "Mcells/s", "frames": s_frames,
+            "seconds": round(el, 2), "gpu_stages_ms_p50": round(_median(s_gpu), 3),
+            "what": "device-resident seed-gen frames (a1-a16, cloud in HBM, grids left in HBM, no GVD) back to back "
+                    "for as long as the CPU baseline's frame takes; this process's threads exclude the child's core"}
     avg = stage
 
     # Roofline (SURVEY §8d algorithmic bytes, HBM-bound; no MFMA). Per frame B_alg = 12 N + C (6 + 4 T):

@@ -60,6 +60,8 @@ typedef struct aos_params {
                                                 a second Subdiv2D on its own host thread */
     int32_t thin_graph;                      /* 1 (default): the first thinning batch of a frame is a
                                                 replayed hipGraph; 0: plain kernel launches */
+    int32_t gvd_count_evals;                 /* 0 (default); 1: the GVD graph phase counts the work of its
+                                                searches (aos_gvd_evals_get; a few atomics per workgroup) */
 } aos_params;
 
 void aos_default_params(aos_params *p);
@@ -190,6 +192,21 @@ int aos_gvd_pipeline_depth(aos_ctx *ctx, int32_t depth);   /* 1..16 GVD jobs in 
  * published frames only. A background job keeps the value it had when it started. With 0,
  * aos_gvd_markers_get computes the cells of the current frame on demand (synchronously). */
 int aos_gvd_set_markers(aos_ctx *ctx, int32_t on);
+/* SURVEY §8d's GVD figure, "pair evaluations": the distance / sample evaluations of the graph phase's searches
+ * in the last GVD call that ran with aos_params.gvd_count_evals = 1 (aos_gvd_set_count_evals). ref_* are what
+ * the reference evaluates for the same inputs: findNearestBoundaryPoint scans every boundary point for each of
+ * the 2E edge ends (gvd:812-824), the pair loop every i < j (gvd:861-894), findVoronoiBoundaryPointNearEndpoint
+ * every filtered node once per radius it tries (gvd:686-790); gpu_* are the candidates this build's kernels
+ * examined (k_nearest, k_pairs' two passes, k_occupancy's grid samples, k_label_points). */
+typedef struct aos_gvd_evals {
+    int32_t counted;                      /* 1: the last GVD call counted                                  */
+    int32_t n_label_jobs;                 /* 4 per exploration row                                         */
+    uint64_t edge_ends, boundary_points, filtered_nodes;   /* 2E, M, M'                                   */
+    uint64_t ref_nearest, ref_pairs, ref_labels;
+    uint64_t gpu_nearest, gpu_pairs, gpu_samples, gpu_labels;
+} aos_gvd_evals;
+int aos_gvd_set_count_evals(aos_ctx *ctx, int32_t on);
+int aos_gvd_evals_get(aos_ctx *ctx, aos_gvd_evals *out);
 
 /* ---------------------------------------------------------------------------------------------
  * Streaming ingest (BASELINE.json configs[4]). The handle keeps the global
@@ -226,6 +243,14 @@ typedef struct aos_comm {
     int (*all_gather)(void *user, uint64_t bytes);
     /* element-wise max over ranks of n int32 values in host memory, in place */
     int (*all_reduce_max)(void *user, int32_t *values, int32_t n);
+    /* Optional (NULL: the library routes through all_gather instead). Personalised exchange:
+     * counts[s * world + d] = bytes rank s sends to rank d, the same world x world matrix on every rank.
+     * send_buf holds this rank's blocks for d = 0, 1, ... back to back; on return recv_buf holds the blocks
+     * addressed to this rank from s = 0, 1, ... back to back. The library keeps every row sum <= buf_bytes
+     * and every column sum <= world * buf_bytes (larger exchanges are split into rounds). RCCL: grouped
+     * ncclSend / ncclRecv; torch.distributed: all_to_all_single. Used by the distributed cluster stage to
+     * send each long cluster's cells to the one rank that measures (and replays) it. */
+    int (*all_to_all)(void *user, const uint64_t *counts);
 } aos_comm;
 
 /* RCCL communicator (one process per GPU, e.g. a torch.distributed launch): an aos_comm whose
@@ -277,10 +302,11 @@ int aos_tiled_map_append(aos_ctx *ctx, const aos_comm *comm, int32_t tiles_x, in
  * time includes the wait for the slowest rank. */
 typedef struct aos_tiled_stats {
     float ms_frame;            /* the whole call on this rank                                        */
-    float ms_comm_gather;      /* inside aos_comm.all_gather (halo strips, tables, the final grids)  */
+    float ms_comm_gather;      /* inside aos_comm.all_gather / all_to_all (halo strips, tables, the final
+                                  grids, the long clusters' cells)                                    */
     float ms_comm_reduce;      /* inside aos_comm.all_reduce_max (thinning flags, counts, sizes)     */
     int32_t n_gather, n_reduce;
-    uint64_t bytes_gather;     /* all-gather payload sent by this rank                               */
+    uint64_t bytes_gather;     /* all-gather / all-to-all payload sent by this rank                  */
     float ms_ror, ms_thin;     /* device stage times (HIP events), as aos_seedgen_out                */
     float ms_cluster;          /* cluster stage, from the final all-gather (device events)           */
     float ms_seeds;            /* root: rows + seeds                                                 */

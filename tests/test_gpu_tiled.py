@@ -33,13 +33,15 @@ def _single(cloud, poly, res):
     return g, grids, gg
 
 
-def _tiled_threads(cloud, poly, res, tiles_x, tiles_y, root, shard=True):
+def _tiled_threads(cloud, poly, res, tiles_x, tiles_y, root, shard=True, a2a=True):
     world = tiles_x * tiles_y
     params = aos_gpu.default_params(grid_resolution=res)
     plans = [T.tile_plan(params, poly, tiles_x, tiles_y, r) for r in range(world)]
     group = T.ThreadGroup(world, timeout=120)
     ctxs = [aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=res)) for _ in range(world)]
     comms = [group.comm(r, plans[r]["exchange_bytes"], "cuda:0") for r in range(world)]
+    if not a2a:
+        comms = [c.without_all_to_all() for c in comms]
     out, errors = [None] * world, []
 
     def work(r):
@@ -87,6 +89,19 @@ def test_tiled_c1_equals_single_gpu(tiles, root):
     cfg = orchard.CONFIGS["C1"]
     cloud, poly = orchard.generate(cfg), orchard.polygon(cfg)
     _assert_same(_single(cloud, poly, cfg.res), _tiled_threads(cloud, poly, cfg.res, *tiles, root))
+
+
+@pytest.mark.parametrize("mode", ["all_gather", "rounds"])
+def test_tiled_c1_cell_exchange_paths(mode, monkeypatch):
+    """The distributed cluster stage sends each long cluster's cells to its one owner rank. Both other routes
+    give the same frame: a communicator without all_to_all (the cells travel by all_gather and each owner
+    picks its blocks), and an exchange split into many small rounds (AOS_DEBUG_A2A_ROUND_BYTES)."""
+    cfg = orchard.CONFIGS["C1"]
+    cloud, poly = orchard.generate(cfg), orchard.polygon(cfg)
+    if mode == "rounds":
+        monkeypatch.setenv("AOS_DEBUG_A2A_ROUND_BYTES", "4096")
+    tiled = _tiled_threads(cloud, poly, cfg.res, 2, 2, 1, a2a=mode != "all_gather")
+    _assert_same(_single(cloud, poly, cfg.res), tiled)
 
 
 def test_tiled_rotating_roots_with_background_gvd():

@@ -52,6 +52,14 @@ def test_upload_pool_under_tsan(built):
     assert " 0 failed" in out
 
 
+def test_grid_expansion_under_asan_ubsan_and_tsan(built):
+    """The published OccupancyGrids' host expansion from the bit-packed device grids (csrc/grid_host.cpp, the
+    default read-back since round 5) vs a per-cell restatement of k_bits_to_bytes / k_draw_rect, through the
+    background expander and its thread pool; the same under ThreadSanitizer."""
+    assert " 0 failed" in _run([os.path.join(built, "san_grid")])
+    assert " 0 failed" in _run([os.path.join(built, "san_grid_tsan")], env={"TSAN_OPTIONS": "halt_on_error=1"})
+
+
 def test_host_subdiv2d_under_asan_ubsan(built):
     out = _run([os.path.join(built, "san_sdcheck")], env={"AOS_SDCHECK_REPS": "2"})
     assert "0 failed so far" in out.splitlines()[-1]

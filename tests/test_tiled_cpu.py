@@ -110,15 +110,32 @@ def _comm_worker(rank, world, port, q):
     rc = c.c.all_gather(None, 48)                      # as libaos_gpu calls it
     v = (ctypes.c_int32 * 3)(rank, 5 - rank, -rank)
     rc2 = c.c.all_reduce_max(None, v, 3)
-    q.put((rank, rc, rc2, c.recv[: 48 * world].numpy().copy(), list(v)))
+    recv_ag = c.recv[: 48 * world].numpy().copy()
+    # the personalised exchange (the cluster stage's cell routing): rank s sends A2A[s][d] bytes to rank d
+    counts = (ctypes.c_uint64 * (world * world))(*[x for row in A2A for x in row])
+    at = 0
+    for d in range(world):
+        c.send[at:at + A2A[rank][d]] = 100 + 10 * rank + d
+        at += A2A[rank][d]
+    rc3 = c.c.all_to_all(None, counts)
+    nr = sum(A2A[s][rank] for s in range(world))
+    q.put((rank, rc, rc2, recv_ag, list(v), rc3, c.recv[:nr].numpy().copy()))
     dist.destroy_process_group()
 
 
+A2A = [[3, 5], [0, 7]]   # bytes rank s sends to rank d (an empty block included)
+
+
+def _a2a_expected(rank, world):
+    return np.concatenate([np.full(A2A[s][rank], 100 + 10 * s + rank, np.uint8) for s in range(world)])
+
+
 def test_torch_dist_comm_gloo_world2():
-    for rank, rc, rc2, recv, v in _spawn(_comm_worker, 2):
-        assert rc == 0 and rc2 == 0
+    for rank, rc, rc2, recv, v, rc3, recv3 in _spawn(_comm_worker, 2):
+        assert rc == 0 and rc2 == 0 and rc3 == 0
         assert np.array_equal(recv, np.concatenate([np.arange(48, dtype=np.uint8) + 10 * r for r in range(2)]))
         assert v == [1, 5, 0]
+        assert np.array_equal(recv3, _a2a_expected(rank, 2))
 
 
 # ---------------------------------------------------------------- distributed cluster labelling
@@ -270,16 +287,27 @@ def test_thread_group_comm():
         rc = c.c.all_gather(None, 8)
         v = (ctypes.c_int32 * 2)(r, -r)
         rc2 = c.c.all_reduce_max(None, v, 2)
-        res[r] = (rc, rc2, c.recv[:24].numpy().copy(), list(v))
+        recv_ag = c.recv[:24].numpy().copy()
+        m = [[(s + 2 * d) % 4 for d in range(world)] for s in range(world)]
+        at = 0
+        for d in range(world):
+            c.send[at:at + m[r][d]] = 50 + 10 * r + d
+            at += m[r][d]
+        rc3 = c.c.all_to_all(None, (ctypes.c_uint64 * 9)(*[x for row in m for x in row]))
+        want = np.concatenate([np.full(m[s][r], 50 + 10 * s + r, np.uint8) for s in range(world)])
+        ok3 = np.array_equal(c.recv[:len(want)].numpy(), want)
+        res[r] = (rc, rc2, recv_ag, list(v), rc3, ok3)
 
     ts = [threading.Thread(target=work, args=(r,)) for r in range(world)]
     for t in ts:
         t.start()
     for t in ts:
         t.join(60)
-    for rc, rc2, recv, v in res:
-        assert rc == 0 and rc2 == 0 and v == [2, 0]
+    for rc, rc2, recv, v, rc3, ok3 in res:
+        assert rc == 0 and rc2 == 0 and v == [2, 0] and rc3 == 0 and ok3
         assert np.array_equal(recv, np.repeat(np.arange(1, 4, dtype=np.uint8), 8))
+    # a communicator without the optional callback exposes a NULL pointer (the library then uses all_gather)
+    assert not comms[0].without_all_to_all().c.all_to_all
 
 
 # ---------------------------------------------------------------- schedule emulation

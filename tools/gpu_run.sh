@@ -53,6 +53,12 @@ for step in $STEPS; do
         > $R/gpurun_out/${TAG}_ktc3.log 2>&1)
       python3 tools/kt_summary.py gpurun_out/${TAG}_ktc3 4 > gpurun_out/${TAG}_ktc3_summary.txt
       head -30 gpurun_out/${TAG}_ktc3_summary.txt ;;
+    kttiled)
+      rm -rf gpurun_out/${TAG}_kttiled
+      (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${TAG}_kttiled -o kt \
+        -- python3 $R/bench.py --tiled --steps 4 --warmup 1 --no-cpu-baseline > $R/gpurun_out/${TAG}_kttiled.log 2>&1)
+      python3 tools/kt_summary.py gpurun_out/${TAG}_kttiled 5 > gpurun_out/${TAG}_kttiled_summary.txt
+      head -40 gpurun_out/${TAG}_kttiled_summary.txt ;;
     pmc)
       rm -rf gpurun_out/${TAG}_fetch gpurun_out/${TAG}_write
       (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/${TAG}_fetch -o fetch \
