@@ -141,21 +141,22 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
 void assemble_rows(const std::vector<ClusterRec> &rec, SeedStageOut &out, std::vector<RowDev> &rows);
 
 // ------------------------------------------------------------------ distributed a8-a10 (cluster_dist.hip)
-// The union-find labelling of a foreground (bits, g.WW words x g.H rows; cnt: popcount per word) into the
-// raster-ordered list of its cells (local raster indices), parent[i] = list index of the first cell of i's
-// component and rank[] = the exclusive scan of the roots (rank[nf] = components, left on the device): the
-// whole-map stage's kernels (cluster_seed.hip). Returns nf (one host wait); *err = the scans' error word.
+// The union-find labelling of a foreground (bits, g.WW words x g.H rows; off: the exclusive scan of the words'
+// popcounts, off[Cw] = nf, made by the producer with B.lb) into the raster-ordered list of its cells (local
+// raster indices), parent[i] = list index of the first cell of i's component and rank[] = the exclusive scan of
+// the roots (rank[nf] = components, left on the device): the whole-map stage's kernels (cluster_seed.hip).
+// Returns nf (one host wait); *err = the scans' error word.
 struct GridC;
 struct CclScratch {
-    DevBuf off, list, parent, isroot, rank, edges;
+    DevBuf off, list, parent, rank, edges;
     LookBackScratch lb;
-    int *off_p = nullptr, *list_p = nullptr, *parent_p = nullptr, *rank_p = nullptr;
+    int *list_p = nullptr, *parent_p = nullptr, *rank_p = nullptr;
 };
-int ccl_label(CclScratch &B, const uint64_t *fg, int *cnt, const GridC &g, hipStream_t s, int *h_pinned2, int *err);
+int ccl_label(CclScratch &B, const uint64_t *fg, const int *off, const GridC &g, hipStream_t s, int *h_pinned2, int *err);
 
 struct ClusterDistState {
     CclScratch ccl;
-    DevBuf poly, fg, cnt, pieces, pid, prank, border, counts, blob, poff, sendbuf, landing, segs, cells, coff, rec;
+    DevBuf poly, fg, pieces, pid, prank, border, counts, blob, poff, sendbuf, landing, segs, cells, coff, rec;
     PinnedBuf h, h_poly, h_poff, h_segs, h_coff, h_rec, h_cells, h_out, h_tab, h_all;   // (one per upload / read-back)
 };
 struct ClusterDistStats {

@@ -29,24 +29,32 @@ namespace aos {
 static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 // ------------------------------------------------------------------ foreground = skeleton inside polygon
-__global__ void k_fg(const uint64_t *skel, uint64_t *fg, int *cnt, GridC g, const double *poly, int np) {
+// One 64-thread block per 64 words of a row (gx blocks per row), in look-back order: the foreground words and,
+// fused, the exclusive scan of their popcounts (off[wi] = foreground cells before word wi, off[Cw] = nf).
+__global__ __launch_bounds__(64) void k_fg(const uint64_t *skel, uint64_t *fg, int *off, GridC g, const double *poly, int np,
+                                           int gx, LookBack L) {
     __shared__ double xc[kRowCrossMax];
-    __shared__ int nxc;
-    const int c = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    __shared__ int nxc, sh_vid;
+    __shared__ LbScanShared sh;
+    const int vid = lb_block_id(L, &sh_vid);
+    const int y = vid / gx, c = (vid - y * gx) * 64 + (int)threadIdx.x;
     const double wy = y < g.H ? cell_world(g.oy, y, g.res) : 0.0;
     const bool rowwise = row_crossings(poly, np, wy, xc, &nxc);   // (block-uniform; synchronises)
-    if (c >= g.WW || y >= g.H) return;
-    size_t wi = (size_t)y * g.WW + c;
-    uint64_t w = skel[wi], o = 0;
-    while (w) {
-        int b = __ffsll((long long)w) - 1;
-        w &= w - 1;
-        int x = c * 64 + b;
-        const double wx = cell_world(g.ox, x, g.res);
-        if (rowwise ? pip_row(wx, xc, nxc) : d_pip(wx, wy, poly, np)) o |= 1ull << b;
+    const bool live = c < g.WW && y < g.H;
+    const size_t wi = (size_t)y * g.WW + c;
+    uint64_t o = 0;
+    if (live) {
+        uint64_t w = skel[wi];
+        while (w) {
+            int b = __ffsll((long long)w) - 1;
+            w &= w - 1;
+            int x = c * 64 + b;
+            const double wx = cell_world(g.ox, x, g.res);
+            if (rowwise ? pip_row(wx, xc, nxc) : d_pip(wx, wy, poly, np)) o |= 1ull << b;
+        }
+        fg[wi] = o;
     }
-    fg[wi] = o;
-    cnt[wi] = __popcll(o);
+    lb_scan_store_at<64>(L, vid, __popcll(o), live ? (long long)wi : -1, (long long)g.WW * g.H - 1, off, sh);
 }
 
 // (parent != nullptr: also the union-find's initial parents, parent[k] = k)
@@ -152,13 +160,25 @@ __global__ void k_ccl_union_if(const int *list, int n, const uint64_t *fg, const
         if (j >= 0) uf_union(parent, i, j);
     }
 }
-__global__ void k_ccl_flatten(int *parent, int *is_root, int n) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    int x = i;   // (a read-only walk: a halving store into another thread's entry could land after its root)
-    for (int p; (p = ld_parent(parent, x)) != x;) x = p;
-    __hip_atomic_store(&parent[i], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    is_root[i] = (x == i);
+// parent[i] := the root; with the roots' exclusive scan fused: rank[r] = the cluster id of root r (the roots'
+// raster order = the reference's discovery order), rank[n] = the number of clusters
+__global__ __launch_bounds__(256) void k_ccl_flatten(int *parent, int *rank, int n, LookBack L) {
+    __shared__ int sh_vid;
+    __shared__ LbScanShared sh;
+    const int vid = lb_block_id(L, &sh_vid);
+    const int i = vid * 256 + (int)threadIdx.x;
+    int root = 0;
+    if (i < n) {
+        int x = i;   // (a read-only walk: a halving store into another thread's entry could land after its root)
+        for (int p; (p = ld_parent(parent, x)) != x;) x = p;
+        __hip_atomic_store(&parent[i], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        root = x == i;
+    }
+    lb_scan_store<256>(L, vid, root, n, rank, sh);
+}
+static void ccl_flatten_rank(LookBackScratch &lb, int *parent, int *rank, int n, hipStream_t s) {
+    const int blocks = cdiv((long long)n + 1, 256);
+    k_ccl_flatten<<<blocks, 256, 0, s>>>(parent, rank, n, lb.take(blocks, s));
 }
 // Counting sort of the foreground cells by cluster id (cluster = rank of the cell's root among the roots,
 // i.e. raster order of first cells): per cell its id and its rank inside the cluster. A cluster holds
@@ -551,19 +571,16 @@ template <class T> static T *dev(DevBuf &b, size_t n) { return static_cast<T *>(
 // The whole-map stage's labelling on any foreground given as bits (the tiled frame's own region, cluster_dist.hip):
 // list, block-local union-find in LDS, cross-chunk unions, flatten, root ranks. One host wait (for nf); the
 // component count stays on the device at rank + nf. err: the single-pass scans' error word (read with nf).
-int ccl_label(CclScratch &B, const uint64_t *fg, int *cnt, const GridC &g, hipStream_t s, int *h_pinned2, int *err) {
+int ccl_label(CclScratch &B, const uint64_t *fg, const int *off, const GridC &g, hipStream_t s, int *h_pinned2, int *err) {
     const size_t Cw = (size_t)g.WW * g.H;
-    int *d_off = dev<int>(B.off, Cw + 1);
-    scan_1p(B.lb, cnt, d_off, (int)Cw, false, s);
+    const int *d_off = off;
     peek_to_host(h_pinned2, {d_off + Cw, B.lb.err_word(s)}, s);
     AOS_HIP(hipStreamSynchronize(s));
     *err = h_pinned2[1];
     const int nf = *err ? 0 : h_pinned2[0];
     B.list_p = dev<int>(B.list, nf);
     B.parent_p = dev<int>(B.parent, nf);
-    int *d_isroot = dev<int>(B.isroot, (size_t)nf + 1);
     B.rank_p = dev<int>(B.rank, (size_t)nf + 1);
-    B.off_p = d_off;
     if (nf == 0) {
         AOS_HIP(hipMemsetAsync(B.rank_p, 0, sizeof(int), s));
         return 0;
@@ -579,8 +596,7 @@ int ccl_label(CclScratch &B, const uint64_t *fg, int *cnt, const GridC &g, hipSt
                                                                       ecap - 1, chunk);
     k_ccl_cross<<<256, 256, 0, s>>>(d_edges, d_ne, ecap - 1, B.parent_p);
     k_ccl_union_if<<<cdiv(nf, 256), 256, 0, s>>>(B.list_p, nf, fg, d_off, g, B.parent_p, d_ne, ecap - 1);
-    k_ccl_flatten<<<cdiv(nf, 256), 256, 0, s>>>(B.parent_p, d_isroot, nf);
-    scan_1p(B.lb, d_isroot, B.rank_p, nf, false, s);
+    ccl_flatten_rank(B.lb, B.parent_p, B.rank_p, nf, s);
     AOS_HIP(hipGetLastError());
     return nf;
 }
@@ -605,13 +621,13 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
     // ---- foreground list (raster order)
     const size_t Cw = (size_t)g.WW * g.H;
     uint64_t *d_fg = nullptr;
-    int *d_wc = nullptr, *d_wo = nullptr;
+    int *d_wo = nullptr;
     const dim3 gw2(cdiv(g.WW, 64), g.H);
     if (!in.pre) {
         d_fg = dev<uint64_t>(S.fg_bits, Cw);
-        d_wc = dev<int>(S.word_cnt, Cw + 1); d_wo = dev<int>(S.word_off, Cw + 1);
-        k_fg<<<gw2, 64, 0, s>>>(in.skel_bits, d_fg, d_wc, g, d_poly, np);
-        scan_1p(S.lb, d_wc, d_wo, (int)Cw, false, s);
+        d_wo = dev<int>(S.word_off, Cw + 1);
+        const int fblocks = gw2.x * gw2.y;
+        k_fg<<<fblocks, 64, 0, s>>>(in.skel_bits, d_fg, d_wo, g, d_poly, np, (int)gw2.x, S.lb.take(fblocks, s));
         peek_to_host(h_sc, {d_wo + Cw, S.lb.err_word(s)}, s);
         S.dedup.sev.sync(s);
         tr.mark("fg");
@@ -629,7 +645,7 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         out.n_bfs = in.pre->n_bfs;
     } else if (nf > 0) {
         int *d_list = dev<int>(S.fg_list, nf);
-        int *d_par = dev<int>(S.parent, nf), *d_isroot = dev<int>(S.root_flag, nf + 1), *d_rank = dev<int>(S.root_rank, nf + 1);
+        int *d_par = dev<int>(S.parent, nf), *d_rank = dev<int>(S.root_rank, nf + 1);
         k_fg_list<<<gw2, 64, 0, s>>>(d_fg, d_wo, d_list, g, nullptr);
         const int ecap = std::max(4096, nf / 4);
         int *d_ne = dev<int>(S.ccl_edges, 2 + 2 * (size_t)ecap);
@@ -640,8 +656,7 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
                                                                           ecap - 1, chunk);
         k_ccl_cross<<<256, 256, 0, s>>>(d_edges, d_ne, ecap - 1, d_par);
         k_ccl_union_if<<<cdiv(nf, 256), 256, 0, s>>>(d_list, nf, d_fg, d_wo, g, d_par, d_ne, ecap - 1);
-        k_ccl_flatten<<<cdiv(nf, 256), 256, 0, s>>>(d_par, d_isroot, nf);
-        scan_1p(S.lb, d_isroot, d_rank, nf, false, s);
+        ccl_flatten_rank(S.lb, d_par, d_rank, nf, s);
         peek_to_host(h_sc, {d_rank + nf, S.lb.err_word(s)}, s);
         S.dedup.sev.sync(s);
         tr.mark("roots");

@@ -118,4 +118,37 @@ __device__ __forceinline__ int block_excl_scan(int v, int *wsum, int *tot) {
     return before + incl - v;
 }
 
+// The exclusive scan of a producer kernel's per-item values, fused into the producer (round 5: one launch and
+// one pass less than producer + k_scan_1p). Block vid (lb_block_id) owns items [vid NT, (vid + 1) NT); the
+// grid covers n + 1 items (the host launches lb_scan_blocks(n, NT)), every thread of every block calls this
+// with its item's value (0 past n), and out[i] = v[0] + ... + v[i - 1] for i in [0, n] (out[n] = the total).
+struct LbScanShared { int wsum[16], tot, excl; };
+template <int NT>
+__device__ __forceinline__ void lb_scan_store(const LookBack &L, int vid, int v, int n, int *out, LbScanShared &sh) {
+    const int i = vid * NT + (int)threadIdx.x;
+    const int before = block_excl_scan<NT>(v, sh.wsum, &sh.tot);
+    if (threadIdx.x < 64) {
+        const unsigned e = lb_exclusive(L, vid, (unsigned)sh.tot);
+        if (threadIdx.x == 0) sh.excl = (int)e;
+    }
+    __syncthreads();
+    if (i <= n) out[i] = sh.excl + before;
+}
+// The same for producers whose blocks own runs of items that are not NT long (a 2-D grid over the rows of a
+// bit grid): the thread's item index i (-1: none; items increase with thread index inside a block and with
+// vid across blocks), out[i] = the exclusive prefix and, from the thread holding item last, out[last + 1] =
+// the total.
+template <int NT>
+__device__ __forceinline__ void lb_scan_store_at(const LookBack &L, int vid, int v, long long i, long long last, int *out,
+                                                 LbScanShared &sh) {
+    const int before = block_excl_scan<NT>(v, sh.wsum, &sh.tot);
+    if (threadIdx.x < 64) {
+        const unsigned e = lb_exclusive(L, vid, (unsigned)sh.tot);
+        if (threadIdx.x == 0) sh.excl = (int)e;
+    }
+    __syncthreads();
+    if (i >= 0) out[i] = sh.excl + before;
+    if (i == last) out[i + 1] = sh.excl + before + v;
+}
+
 }  // namespace aos

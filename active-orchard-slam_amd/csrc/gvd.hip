@@ -135,15 +135,14 @@ __global__ void k_nearest(const double2 *occ, int n_occ, CellIdx ci, const int *
 
 // all pairs i < j with 1e-6 < |bp_i - bp_j| <= 0.5 (gvd:861-894), CSR per i, j ascending (count pass:
 // poff == nullptr; entries past cap are dropped and flag the caller, who reruns with the exact size)
-__global__ void k_pairs(const double2 *bp, int no, const int *M_dev, CellIdx ci, const int *pos_of, const double2 *occ,
-                        const int *poff, int *pcount, int *plist, int cap, unsigned long long *evals) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= no) return;
-    if (i >= *M_dev) { if (!poff) pcount[i] = 0; return; }
+// (poff == nullptr: the count pass, with the pairs' exclusive scan fused: pcount = the offsets, [no] = total)
+template <bool COUNT>
+__device__ __forceinline__ int pairs_of(int i, const double2 *bp, CellIdx ci, const int *pos_of, const double2 *occ,
+                                        const int *poff, int *plist, int cap, unsigned long long *evals) {
     const double2 p = bp[i];
     int cx, cy;
     hash_cell(ci.h, p.x, p.y, cx, cy);
-    int c = 0, w = poff ? poff[i] : 0;
+    int c = 0, w = COUNT ? 0 : poff[i];
     long long ne = 0;
     for (int yy = max(cy - 1, 0); yy <= min(cy + 1, ci.h.ny - 1); ++yy) {
         int k0, k1;
@@ -154,7 +153,7 @@ __global__ void k_pairs(const double2 *bp, int no, const int *M_dev, CellIdx ci,
             if (j <= i) continue;
             double dx = p.x - occ[cc].x, dy = p.y - occ[cc].y, d = sqrt(dx * dx + dy * dy);
             if (d <= 0.5 && d > 1e-6) {
-                if (poff && w + c < cap) {  // insertion into the sorted run
+                if (!COUNT && w + c < cap) {  // insertion into the sorted run
                     int pos = w + c;
                     while (pos > w && plist[pos - 1] > j) { plist[pos] = plist[pos - 1]; --pos; }
                     plist[pos] = j;
@@ -163,8 +162,23 @@ __global__ void k_pairs(const double2 *bp, int no, const int *M_dev, CellIdx ci,
             }
         }
     }
-    if (!poff) pcount[i] = c;
     eval_add(evals, 1, ne);
+    return c;
+}
+__global__ __launch_bounds__(256) void k_pairs_count(const double2 *bp, int no, const int *M_dev, CellIdx ci, const int *pos_of,
+                                                     const double2 *occ, int *poff, unsigned long long *evals, LookBack L) {
+    __shared__ int sh_vid;
+    __shared__ LbScanShared sh;
+    const int vid = lb_block_id(L, &sh_vid);
+    const int i = vid * 256 + (int)threadIdx.x;
+    const int c = i < no && i < *M_dev ? pairs_of<true>(i, bp, ci, pos_of, occ, nullptr, nullptr, 0, evals) : 0;
+    lb_scan_store<256>(L, vid, c, no, poff, sh);
+}
+__global__ void k_pairs(const double2 *bp, int no, const int *M_dev, CellIdx ci, const int *pos_of, const double2 *occ,
+                        const int *poff, int *plist, int cap, unsigned long long *evals) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= no || i >= *M_dev) return;
+    (void)pairs_of<false>(i, bp, ci, pos_of, occ, poff, plist, cap, evals);
 }
 
 // candidate edge occurrences: [0, E) Voronoi edges, [E, E + P) pairs (P = poff[no] <= cap). from/to keep
@@ -265,30 +279,40 @@ __global__ void k_select(const int2 *ft, const int *pass, const int *poff, int n
 }
 
 // ------------------------------------------------------------------ g7 filter
-__global__ void k_inside(const double2 *bp, int no, const int *M_dev, GridG g, int *f) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= no) return;
+// (with the flags' exclusive scan fused: pos[i] = kept nodes before i, pos[no] = M')
+__global__ __launch_bounds__(256) void k_inside(const double2 *bp, int no, const int *M_dev, GridG g, int *f, int *pos,
+                                                LookBack L) {
+    __shared__ int sh_vid;
+    __shared__ LbScanShared sh;
+    const int vid = lb_block_id(L, &sh_vid);
+    const int i = vid * 256 + (int)threadIdx.x;
     int v = 0;
-    if (i < *M_dev) {
+    if (i < no && i < *M_dev) {
         double2 p = bp[i];
         v = p.x >= g.minx && p.x <= g.maxx && p.y >= g.miny && p.y <= g.maxy;
     }
-    f[i] = v;
+    if (i < no) f[i] = v;
+    lb_scan_store<256>(L, vid, v, no, pos, sh);
 }
 __global__ void k_gather_nodes(const double2 *bp, const int *f, const int *pos, int no, double2 *nodes) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < no && f[i]) nodes[pos[i]] = bp[i];
 }
 // selected candidate c -> record (a<b); keep if both nodes stay (and stay distinct); 0 past the candidates
-__global__ void k_edge_keep(const int *selected, const int2 *ft, int ncap, const int *inside, const int *pos, int *keep) {
-    int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= ncap) return;
+// (with the keep flags' exclusive scan fused: kpos[c] = kept edges before c, kpos[ncap] = the total)
+__global__ __launch_bounds__(256) void k_edge_keep(const int *selected, const int2 *ft, int ncap, const int *inside, const int *pos,
+                                                   int *keep, int *kpos, LookBack L) {
+    __shared__ int sh_vid;
+    __shared__ LbScanShared sh;
+    const int vid = lb_block_id(L, &sh_vid);
+    const int c = vid * 256 + (int)threadIdx.x;
     int k = 0;
-    if (selected[c]) {
+    if (c < ncap && selected[c]) {
         int a = min(ft[c].x, ft[c].y), b = max(ft[c].x, ft[c].y);
         k = inside[a] && inside[b] && pos[a] != pos[b];
     }
-    keep[c] = k;
+    if (c < ncap) keep[c] = k;
+    lb_scan_store<256>(L, vid, k, ncap, kpos, sh);
 }
 __global__ void k_edge_emit(const int *keep, const int *kpos, const int2 *ft, int ncap, const int *pos, const double2 *nodes,
                             int *edges, float *len) {
@@ -443,13 +467,13 @@ __global__ __launch_bounds__(256) void k_label_points(const LabelRow *jobs, int 
 // matches are put back in (r, k) order. More than kNodeMatch matches: the plain loop over every label
 // point. Count pass (off == nullptr) over [0, no): 0 past the Mn nodes.
 constexpr int kNodeMatch = 16;
-__global__ void k_node_labels(const double2 *nodes, int no, const int *Mn_dev, const double2 *lp, const int *lv, int n_rows,
-                              CellIdx cq, int *mask, int *cidx, int *count, const int *off, int *lcl, int *lty) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= no) return;
-    if (i >= *Mn_dev) { if (!off) count[i] = 0; return; }
+// node i's label mask, first matching row and number of (row, type) entries; off != nullptr: the entries too
+__device__ __forceinline__ int node_labels_of(int i, const double2 *nodes, const double2 *lp, const int *lv, int n_rows,
+                                              const CellIdx &cq, int &mask_out, int &cidx_out, const int *off, int *lcl,
+                                              int *lty) {
     const double2 p = nodes[i];
-    int m = 0, ci = -1, cnt = 0, w = off ? off[i] : 0;
+    int m = 0, ci = -1, cnt = 0;
+    const int w = off ? off[i] : 0;
     {
         int js[kNodeMatch], nm = 0;
         bool over = false;
@@ -478,8 +502,8 @@ __global__ void k_node_labels(const double2 *nodes, int no, const int *Mn_dev, c
                 ++cnt;
                 if (ci == -1) ci = r;
             }
-            if (!off) { mask[i] = m; cidx[i] = ci; count[i] = cnt; }
-            return;
+            mask_out = m; cidx_out = ci;
+            return cnt;
         }
     }
     for (int r = 0; r < n_rows; ++r)
@@ -496,7 +520,33 @@ __global__ void k_node_labels(const double2 *nodes, int no, const int *Mn_dev, c
                 if (ci == -1) ci = r;
             }
         }
-    if (!off) { mask[i] = m; cidx[i] = ci; count[i] = cnt; }
+    mask_out = m; cidx_out = ci;
+    return cnt;
+}
+// count pass over [0, no) (0 past the Mn nodes), the entries' exclusive scan fused: off[i], off[no] = total
+__global__ __launch_bounds__(256) void k_node_labels_count(const double2 *nodes, int no, const int *Mn_dev, const double2 *lp,
+                                                           const int *lv, int n_rows, CellIdx cq, int *mask, int *cidx,
+                                                           int *count, int *off, LookBack L) {
+    __shared__ int sh_vid;
+    __shared__ LbScanShared sh;
+    const int vid = lb_block_id(L, &sh_vid);
+    const int i = vid * 256 + (int)threadIdx.x;
+    int cnt = 0;
+    if (i < no && i < *Mn_dev) {
+        int m = 0, ci = -1;
+        cnt = node_labels_of(i, nodes, lp, lv, n_rows, cq, m, ci, nullptr, nullptr, nullptr);
+        mask[i] = m; cidx[i] = ci;
+    }
+    if (i < no) count[i] = cnt;
+    lb_scan_store<256>(L, vid, cnt, no, off, sh);
+}
+// fill pass over the Mn nodes: the (row, type) entries at off[i]
+__global__ void k_node_labels_fill(const double2 *nodes, int Mn, const double2 *lp, const int *lv, int n_rows, CellIdx cq,
+                                   const int *off, int *lcl, int *lty) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= Mn) return;
+    int m, ci;
+    (void)node_labels_of(i, nodes, lp, lv, n_rows, cq, m, ci, off, lcl, lty);
 }
 
 // the device scalars the host needs, gathered for one read-back
@@ -577,19 +627,23 @@ __global__ void k_vor_faces(const int *qe, int n_rec, const float2 *vp, float2 *
 constexpr int kMaxFacet = 1 << 16;
 __device__ __forceinline__ float2 dual_face(const float2 *face, int t) { return face[2 * (t >> 2) + ((t & 3) == 1 ? 1 : 0)]; }
 
-__global__ void k_facet_count(const int *qe, const int *vfirst, const int *vtype, int nv, int *cnt, int *err) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k == 0) cnt[nv] = 0;   // the scan's tail slot
-    if (k >= nv) return;
+// (the facet sizes' exclusive scan is fused: off[k] = edges before vertex k, off[nv] = the total)
+__global__ __launch_bounds__(256) void k_facet_count(const int *qe, const int *vfirst, const int *vtype, int nv, int *cnt,
+                                                     int *off, int *err, LookBack L) {
+    __shared__ int sh_vid;
+    __shared__ LbScanShared sh;
+    const int vid = lb_block_id(L, &sh_vid);
+    const int k = vid * 256 + (int)threadIdx.x;
     int c = 0;
-    if (k >= 4 && vtype[k] == 0) {
+    if (k < nv && k >= 4 && vtype[k] == 0) {
         const int f = vfirst[k], start = (f & ~3) + ((f + 1) & 3);
         int t = start;
         do { ++c; t = q_get(qe, t, 0x13); } while (t != start && c < kMaxFacet);
         if (c >= kMaxFacet) atomicOr(err, 1);
         if (c < 2) c = 0;
     }
-    cnt[k] = c;
+    if (k < nv) cnt[k] = c;
+    lb_scan_store<256>(L, vid, c, nv, off, sh);
 }
 __global__ void k_facet_emit(const int *qe, const int *vfirst, const int *off, const int *cnt, int nv, const float2 *face,
                              float4 *edges) {
@@ -659,8 +713,11 @@ static int facets_count(FacetBufs &F, const Subdiv2D &sd, Subdiv2D::Raw &R, int 
     float2 *d_face = dev<float2>(F.face, 2 * (size_t)R.n_rec);
     int *d_cnt = dev<int>(F.cnt, R.n_vtx + 1), *d_off = dev<int>(F.off, R.n_vtx + 2);   // off[n_vtx + 1]: walk error
     k_vor_faces<<<cdiv(2 * R.n_rec, 256), 256, 0, s>>>(F.qe, R.n_rec, d_vp, d_face, d_off + R.n_vtx + 1);
-    k_facet_count<<<cdiv(R.n_vtx, 256), 256, 0, s>>>(F.qe, F.vf, F.vt, R.n_vtx, d_cnt, d_off + R.n_vtx + 1);
-    scan_1p(F.lb, d_cnt, d_off, R.n_vtx, false, s);
+    {
+        const int blocks = cdiv((long long)R.n_vtx + 1, 256);
+        k_facet_count<<<blocks, 256, 0, s>>>(F.qe, F.vf, F.vt, R.n_vtx, d_cnt, d_off, d_off + R.n_vtx + 1,
+                                             F.lb.take(blocks, s));
+    }
     AOS_HIP(hipMemcpyAsync(h_sc, d_off + R.n_vtx, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
     AOS_HIP(hipMemcpyAsync(h_sc + 2, F.lb.err_word(s), sizeof(int), hipMemcpyDeviceToHost, s));
     sev.sync(s);
@@ -986,9 +1043,11 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
         AOS_HIP(hipMemsetAsync(d_evals, 0, 8 * sizeof(unsigned long long), s));
     }
     k_nearest<<<cdiv(no, 256), 256, 0, s>>>(d_occ, no, cio, d_pos_of, d_bp, d_M, d_near, d_evals);
-    int *d_pcount = dev<int>(S.pcount, no), *d_poff = dev<int>(S.poff, no + 1);
-    k_pairs<<<cdiv(no, 256), 256, 0, s>>>(d_bp, no, d_M, cio, d_pos_of, d_occ, nullptr, d_pcount, nullptr, 0, d_evals);
-    scan_1p(S.lb, d_pcount, d_poff, no, false, s);
+    int *d_poff = dev<int>(S.poff, no + 1);
+    {
+        const int blocks = cdiv((long long)no + 1, 256);
+        k_pairs_count<<<blocks, 256, 0, s>>>(d_bp, no, d_M, cio, d_pos_of, d_occ, d_poff, d_evals, S.lb.take(blocks, s));
+    }
     // The pair lists get a capacity from the last frame (P is read back only with the frame's sizes below);
     // a frame with more pairs runs the rest again with the exact size.
     int cap = G.pairs_cap > 0 ? G.pairs_cap : std::max(1024, 2 * no);
@@ -1021,7 +1080,7 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     for (int attempt = 0;; ++attempt) {
         const int ncap = ne + cap;
         int *d_plist = dev<int>(S.plist, cap);
-        k_pairs<<<cdiv(no, 256), 256, 0, s>>>(d_bp, no, d_M, cio, d_pos_of, d_occ, d_poff, nullptr, d_plist, cap, d_evals);
+        k_pairs<<<cdiv(no, 256), 256, 0, s>>>(d_bp, no, d_M, cio, d_pos_of, d_occ, d_poff, d_plist, cap, d_evals);
         int2 *d_ft = dev<int2>(S.ft, ncap);
         int *d_pass = dev<int>(S.pass, ncap), *d_grank = dev<int>(S.occ_idx, ncap), *d_sel = dev<int>(S.selected, ncap);
         const size_t gc0 = S.gcnt.cap;
@@ -1038,11 +1097,15 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
         k_select<<<cdiv(ncap, 256), 256, 0, s>>>(d_ft, d_pass, d_poff, no, ne, cap, d_goff, d_glist, d_sel);
 
         // ---- g7 filter
-        k_inside<<<cdiv(no, 256), 256, 0, s>>>(d_bp, no, d_M, g, d_in);
-        scan_1p(S.lb, d_in, d_ipos, no, false, s);
+        {
+            const int blocks = cdiv((long long)no + 1, 256);
+            k_inside<<<blocks, 256, 0, s>>>(d_bp, no, d_M, g, d_in, d_ipos, S.lb.take(blocks, s));
+        }
         int *d_keep = dev<int>(S.keep, ncap), *d_kpos = dev<int>(S.kpos, ncap + 1);
-        k_edge_keep<<<cdiv(ncap, 256), 256, 0, s>>>(d_sel, d_ft, ncap, d_in, d_ipos, d_keep);
-        scan_1p(S.lb, d_keep, d_kpos, ncap, false, s);
+        {
+            const int blocks = cdiv((long long)ncap + 1, 256);
+            k_edge_keep<<<blocks, 256, 0, s>>>(d_sel, d_ft, ncap, d_in, d_ipos, d_keep, d_kpos, S.lb.take(blocks, s));
+        }
         k_gather_nodes<<<cdiv(no, 256), 256, 0, s>>>(d_bp, d_in, d_ipos, no, d_nodes);
         d_edges = dev<int>(S.edges, 2 * (size_t)ncap);
         d_lens = dev<float>(S.lens, ncap);
@@ -1058,9 +1121,11 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
         // ---- g9 node labels: the valid label points in cells of >= 0.1 m
         const HashG hq = make_hash_n(g.minx - 1.0, g.maxx + 1.0, g.miny - 1.0, g.maxy + 1.0, 0.1, nj);
         const CellIdx cq = S.cq = cell_index_build(S.ci_labels, d_lp, d_lv, nj, hq, s);
-        k_node_labels<<<cdiv(no, 256), 256, 0, s>>>(d_nodes, no, d_Mn, d_lp, d_lv, nrows, cq, d_mask, d_cidx, d_lcnt, nullptr,
-                                                    nullptr, nullptr);
-        scan_1p(S.lb, d_lcnt, d_loff, no, false, s);
+        {
+            const int blocks = cdiv((long long)no + 1, 256);
+            k_node_labels_count<<<blocks, 256, 0, s>>>(d_nodes, no, d_Mn, d_lp, d_lv, nrows, cq, d_mask, d_cidx, d_lcnt, d_loff,
+                                                       S.lb.take(blocks, s));
+        }
         // the frame's sizes and error words: one read-back
         Peek pk{{d_M, d_poff + no, d_Mn, d_kpos + ncap, d_loff + no, dedup_err(G.dedup, s), S.lb.err_word(s),
                  S.ci_nodes.lb.err_word(s)}, 8};
@@ -1086,8 +1151,7 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     d_lcl = dev<int>(S.lcl, n_entries);
     d_lty = dev<int>(S.lty, n_entries);
     if (n_entries)
-        k_node_labels<<<cdiv(Mn, 256), 256, 0, s>>>(d_nodes, Mn, d_ipos + no, d_lp, d_lv, nrows, S.cq, nullptr,
-                                                    nullptr, nullptr, d_loff, d_lcl, d_lty);
+        k_node_labels_fill<<<cdiv(Mn, 256), 256, 0, s>>>(d_nodes, Mn, d_lp, d_lv, nrows, S.cq, d_loff, d_lcl, d_lty);
 
     // ---- outputs: one gather kernel, one D2H copy into the state's pinned buffer, host copies out
     G.nodes_xy.resize(2 * (size_t)Mn); G.labels.resize(Mn); G.cluster_idx.resize(Mn); G.label_counts.resize(Mn);
