@@ -213,7 +213,7 @@ static void gather_bytes(const aos_comm &cm, hipStream_t s, const void *src, boo
 template <class T> static T *dptr(DevBuf &b, size_t n) { return static_cast<T *>(b.ensure(sizeof(T) * std::max<size_t>(n, 1))); }
 template <class T> static T *hptr(PinnedBuf &b, size_t n) { return static_cast<T *>(b.ensure(sizeof(T) * std::max<size_t>(n, 1))); }
 
-struct OwnedOut { int l, pad; ClusterRec r; };
+struct OwnedOut { int l, replayed; ClusterRec r; };
 
 // The personalised exchange of the long clusters' cells. cnt[s * W + d]: bytes rank s sends to rank d (known
 // on every rank). send: this rank's route buffer (device, destination-major). Returns the device buffer the
@@ -455,6 +455,7 @@ void cluster_dist(ClusterDistState &D, const aos_comm &cm, const TilePlan &t, co
             coff[nown] = (int)at;
         }
         const int n_owned_cells = coff[nown];
+        std::vector<int> replayed((size_t)nown, 0);   // the owned clusters replayed here
         if (nown > 0) {
             Seg *hs = hptr<Seg>(D.h_segs, segs.size());
             std::copy(segs.begin(), segs.end(), hs);
@@ -474,7 +475,7 @@ void cluster_dist(ClusterDistState &D, const aos_comm &cm, const TilePlan &t, co
             std::vector<ClusterRec> orec(hr, hr + nown);
             std::vector<int> flagged;
             for (int j = 0; j < nown; ++j)
-                if (orec[j].flags & 2) flagged.push_back(j);
+                if (orec[j].flags & 2) { flagged.push_back(j); replayed[j] = 1; }
             if (!flagged.empty()) {   // the owned flagged clusters' cells in one copy, then the exact replays
                 const int lo = coff[flagged.front()], hi = coff[flagged.back() + 1];
                 int *hc = hptr<int>(D.h_cells, (size_t)(hi - lo));
@@ -493,13 +494,13 @@ void cluster_dist(ClusterDistState &D, const aos_comm &cm, const TilePlan &t, co
         std::vector<uint64_t> rsz((size_t)world, 0);
         for (int l = 0; l < nlong; ++l) rsz[owner[l]] += sizeof(OwnedOut);
         OwnedOut *ho = hptr<OwnedOut>(D.h_out, (size_t)std::max(nown, 1));
-        for (int j = 0; j < nown; ++j) ho[j] = OwnedOut{mine_l[j], 0, lrec[mine_l[j]]};
+        for (int j = 0; j < nown; ++j) ho[j] = OwnedOut{mine_l[j], replayed[j], lrec[mine_l[j]]};
         OwnedOut *ha = hptr<OwnedOut>(D.h_tab, (size_t)nlong);
         gather_bytes(cm, s, ho, false, rsz, ha, false);
-        int n_bfs_long = 0;
+        int n_bfs_long = 0;   // (a replay clears the record's flag: the owners say which they replayed)
         for (int k = 0; k < nlong; ++k) {
             lrec[ha[k].l] = ha[k].r;
-            n_bfs_long += (ha[k].r.flags & 2) != 0;
+            n_bfs_long += ha[k].replayed;
         }
         pre.n_bfs = n_bfs_long;
     }
