@@ -46,34 +46,26 @@ struct TileView {
     int Wt;   // own width in cells: min(W, 64 (c0 + nc)) - 64 c0
 };
 
-// own foreground (compact: nc words x nr rows) and, fused, the exclusive scan of its popcounts per word
-// (off[Cw] = nf); blocks of 64 words of a row (gx per row) in look-back order
-__global__ __launch_bounds__(64) void k_dist_fg(const uint64_t *win, TileView T, GridC g, const double *poly, int np,
-                                                uint64_t *fg, int *off, int gx, LookBack L) {
+// own foreground (compact: nc words x nr rows) and its popcount per word
+__global__ void k_dist_fg(const uint64_t *win, TileView T, GridC g, const double *poly, int np, uint64_t *fg, int *cnt) {
     __shared__ double xc[kRowCrossMax];
-    __shared__ int nxc, sh_vid;
-    __shared__ LbScanShared sh;
-    const int vid = lb_block_id(L, &sh_vid);
-    const int r = vid / gx, k = (vid - r * gx) * 64 + (int)threadIdx.x;
+    __shared__ int nxc;
+    const int k = blockIdx.x * blockDim.x + threadIdx.x, r = blockIdx.y;
     const int gy = T.y0 + r;
     const double wy = cell_world(g.oy, gy, g.res);
     const bool rowwise = row_crossings(poly, np, wy, xc, &nxc);   // (block-uniform; synchronises)
-    const bool live = k < T.nc && r < T.nr;
-    uint64_t o = 0;
-    if (live) {
-        uint64_t w = win[(size_t)(T.oy + r) * T.WWl + T.oc + k];
-        while (w) {
-            const int b = __ffsll((long long)w) - 1;
-            w &= w - 1;
-            const int gxc = 64 * (T.c0 + k) + b;
-            if (gxc >= g.W) continue;
-            const double wx = cell_world(g.ox, gxc, g.res);
-            if (rowwise ? pip_row(wx, xc, nxc) : d_pip(wx, wy, poly, np)) o |= 1ull << b;
-        }
-        fg[(size_t)r * T.nc + k] = o;
+    if (k >= T.nc || r >= T.nr) return;
+    uint64_t w = win[(size_t)(T.oy + r) * T.WWl + T.oc + k], o = 0;
+    while (w) {
+        const int b = __ffsll((long long)w) - 1;
+        w &= w - 1;
+        const int gx = 64 * (T.c0 + k) + b;
+        if (gx >= g.W) continue;
+        const double wx = cell_world(g.ox, gx, g.res);
+        if (rowwise ? pip_row(wx, xc, nxc) : d_pip(wx, wy, poly, np)) o |= 1ull << b;
     }
-    const long long wi = (long long)r * T.nc + k;
-    lb_scan_store_at<64>(L, vid, __popcll(o), live ? wi : -1, (long long)T.nc * T.nr - 1, off, sh);
+    fg[(size_t)r * T.nc + k] = o;
+    cnt[(size_t)r * T.nc + k] = __popcll(o);
 }
 
 // piece tables, SoA: n | root | minx | maxx | miny | maxy (ints), sx | sy (u64)
@@ -297,11 +289,9 @@ void cluster_dist(ClusterDistState &D, const aos_comm &cm, const TilePlan &t, co
     // ---- 1. own foreground, pieces, border cells (the whole-map stage's labelling on the own region)
     const size_t Cw = (size_t)T.nc * T.nr;
     uint64_t *d_fg = dptr<uint64_t>(D.fg, Cw);
-    int *d_off = dptr<int>(D.ccl.off, Cw + 1);
-    {
-        const int gx = cdiv(T.nc, 64), blocks = gx * T.nr;
-        k_dist_fg<<<blocks, 64, 0, s>>>(win, T, g, d_poly, npoly, d_fg, d_off, gx, D.ccl.lb.take(blocks, s));
-    }
+    int *d_cnt = dptr<int>(D.cnt, Cw), *d_off = dptr<int>(D.ccl.off, Cw + 1);
+    k_dist_fg<<<dim3(cdiv(T.nc, 64), T.nr), 64, 0, s>>>(win, T, g, d_poly, npoly, d_fg, d_cnt);
+    scan_1p(D.ccl.lb, d_cnt, d_off, (int)Cw, false, s);
     GridC gl{};   // the own region as an image: local raster index = ly * Wt + lx
     gl.W = T.Wt; gl.H = T.nr; gl.WW = T.nc;
     int err = 0;

@@ -148,7 +148,7 @@ void assemble_rows(const std::vector<ClusterRec> &rec, SeedStageOut &out, std::v
 // Returns nf (one host wait); *err = the scans' error word.
 struct GridC;
 struct CclScratch {
-    DevBuf off, list, parent, rank, edges;
+    DevBuf off, list, parent, isroot, rank, edges;
     LookBackScratch lb;
     int *list_p = nullptr, *parent_p = nullptr, *rank_p = nullptr;
 };
@@ -156,7 +156,7 @@ int ccl_label(CclScratch &B, const uint64_t *fg, const int *off, const GridC &g,
 
 struct ClusterDistState {
     CclScratch ccl;
-    DevBuf poly, fg, pieces, pid, prank, border, counts, blob, poff, sendbuf, landing, segs, cells, coff, rec;
+    DevBuf poly, fg, cnt, pieces, pid, prank, border, counts, blob, poff, sendbuf, landing, segs, cells, coff, rec;
     PinnedBuf h, h_poly, h_poff, h_segs, h_coff, h_rec, h_cells, h_out, h_tab, h_all;   // (one per upload / read-back)
 };
 struct ClusterDistStats {

@@ -29,32 +29,28 @@ namespace aos {
 static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 // ------------------------------------------------------------------ foreground = skeleton inside polygon
-// One 64-thread block per 64 words of a row (gx blocks per row), in look-back order: the foreground words and,
-// fused, the exclusive scan of their popcounts (off[wi] = foreground cells before word wi, off[Cw] = nf).
-__global__ __launch_bounds__(64) void k_fg(const uint64_t *skel, uint64_t *fg, int *off, GridC g, const double *poly, int np,
-                                           int gx, LookBack L) {
+// The foreground words and their popcounts (k_scan_1p turns them into the words' offsets). (Round 5 measured the
+// scan fused into this kernel with a decoupled look-back: 117 us instead of 18 + 9 at C2 -- the 4096 one-wave
+// blocks waited on their predecessors' work, so few ran at once; the fusion stays only where blocks are
+// uniform and short, k_facet_count.)
+__global__ void k_fg(const uint64_t *skel, uint64_t *fg, int *cnt, GridC g, const double *poly, int np) {
     __shared__ double xc[kRowCrossMax];
-    __shared__ int nxc, sh_vid;
-    __shared__ LbScanShared sh;
-    const int vid = lb_block_id(L, &sh_vid);
-    const int y = vid / gx, c = (vid - y * gx) * 64 + (int)threadIdx.x;
+    __shared__ int nxc;
+    const int c = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
     const double wy = y < g.H ? cell_world(g.oy, y, g.res) : 0.0;
     const bool rowwise = row_crossings(poly, np, wy, xc, &nxc);   // (block-uniform; synchronises)
-    const bool live = c < g.WW && y < g.H;
-    const size_t wi = (size_t)y * g.WW + c;
-    uint64_t o = 0;
-    if (live) {
-        uint64_t w = skel[wi];
-        while (w) {
-            int b = __ffsll((long long)w) - 1;
-            w &= w - 1;
-            int x = c * 64 + b;
-            const double wx = cell_world(g.ox, x, g.res);
-            if (rowwise ? pip_row(wx, xc, nxc) : d_pip(wx, wy, poly, np)) o |= 1ull << b;
-        }
-        fg[wi] = o;
+    if (c >= g.WW || y >= g.H) return;
+    size_t wi = (size_t)y * g.WW + c;
+    uint64_t w = skel[wi], o = 0;
+    while (w) {
+        int b = __ffsll((long long)w) - 1;
+        w &= w - 1;
+        int x = c * 64 + b;
+        const double wx = cell_world(g.ox, x, g.res);
+        if (rowwise ? pip_row(wx, xc, nxc) : d_pip(wx, wy, poly, np)) o |= 1ull << b;
     }
-    lb_scan_store_at<64>(L, vid, __popcll(o), live ? (long long)wi : -1, (long long)g.WW * g.H - 1, off, sh);
+    fg[wi] = o;
+    cnt[wi] = __popcll(o);
 }
 
 // (parent != nullptr: also the union-find's initial parents, parent[k] = k)
@@ -160,25 +156,19 @@ __global__ void k_ccl_union_if(const int *list, int n, const uint64_t *fg, const
         if (j >= 0) uf_union(parent, i, j);
     }
 }
-// parent[i] := the root; with the roots' exclusive scan fused: rank[r] = the cluster id of root r (the roots'
-// raster order = the reference's discovery order), rank[n] = the number of clusters
-__global__ __launch_bounds__(256) void k_ccl_flatten(int *parent, int *rank, int n, LookBack L) {
-    __shared__ int sh_vid;
-    __shared__ LbScanShared sh;
-    const int vid = lb_block_id(L, &sh_vid);
-    const int i = vid * 256 + (int)threadIdx.x;
-    int root = 0;
-    if (i < n) {
-        int x = i;   // (a read-only walk: a halving store into another thread's entry could land after its root)
-        for (int p; (p = ld_parent(parent, x)) != x;) x = p;
-        __hip_atomic_store(&parent[i], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        root = x == i;
-    }
-    lb_scan_store<256>(L, vid, root, n, rank, sh);
+__global__ void k_ccl_flatten(int *parent, int *is_root, int n) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int x = i;   // (a read-only walk: a halving store into another thread's entry could land after its root)
+    for (int p; (p = ld_parent(parent, x)) != x;) x = p;
+    __hip_atomic_store(&parent[i], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    is_root[i] = (x == i);
 }
-static void ccl_flatten_rank(LookBackScratch &lb, int *parent, int *rank, int n, hipStream_t s) {
-    const int blocks = cdiv((long long)n + 1, 256);
-    k_ccl_flatten<<<blocks, 256, 0, s>>>(parent, rank, n, lb.take(blocks, s));
+// parent[i] := the root; rank[r] = the cluster id of root r (the roots' raster order = the reference's discovery
+// order), rank[n] = the number of clusters
+static void ccl_flatten_rank(LookBackScratch &lb, int *parent, int *is_root, int *rank, int n, hipStream_t s) {
+    k_ccl_flatten<<<cdiv(n, 256), 256, 0, s>>>(parent, is_root, n);
+    scan_1p(lb, is_root, rank, n, false, s);
 }
 // Counting sort of the foreground cells by cluster id (cluster = rank of the cell's root among the roots,
 // i.e. raster order of first cells): per cell its id and its rank inside the cluster. A cluster holds
@@ -484,12 +474,18 @@ struct RayAngles { double cs[3], sn[3]; int pos_branch[3]; };  // 0, -90, +90 de
 // tabulates it once with the same double adds (cur_tab[i] = value at step i; the table ends with the
 // first value > absolute_max_distance). Each lane evaluates its step with an unconditional (clamped)
 // skeleton load; the first lane with an event (loop end, left the grid, occupied cell) decides.
+// (k_endpoint_candidates folded in: the first ray block of row r also writes the row's two endpoint seed
+// candidates, start then end, into ecand / eok [2r, 2r + 1] -- seed_gen:1451-1496's order)
 __global__ __launch_bounds__(64) void k_endpoint_rays(const RowDev *rows, int n_rows, const uint64_t *skel, GridC g,
                                                       RayAngles ang, const double *poly, int np, const double *cur_tab,
-                                                      int n_tab, double2 *cand, int *ok) {
+                                                      int n_tab, double2 *cand, int *ok, double2 *ecand, int *eok) {
     const int s = blockIdx.x, lane = threadIdx.x;
     if (s >= n_rows * 6) return;
     const RowDev R = rows[s / 6];
+    if (s % 6 == 0 && lane < 2) {
+        ecand[2 * (s / 6) + lane] = lane ? make_double2(R.ex, R.ey) : make_double2(R.sx, R.sy);
+        eok[2 * (s / 6) + lane] = 1;
+    }
     const int k = s % 6, a = k % 3;
     double stx = k < 3 ? R.sx : R.ex, sty = k < 3 ? R.sy : R.ey;
     double otx = k < 3 ? R.ex : R.sx, oty = k < 3 ? R.ey : R.sy;
@@ -548,13 +544,6 @@ __global__ __launch_bounds__(64) void k_endpoint_rays(const RowDev *rows, int n_
     }
 }
 
-__global__ void k_endpoint_candidates(const RowDev *rows, int n_rows, double2 *cand, int *ok) {
-    int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= 2 * n_rows) return;
-    const RowDev R = rows[s >> 1];
-    cand[s] = (s & 1) ? make_double2(R.ex, R.ey) : make_double2(R.sx, R.sy);
-    ok[s] = 1;
-}
 
 // /voronoi_seeds order (seed_gen:1670-1710): virtual, ray, endpoint seeds (counts on the device)
 __global__ void k_concat3(const double2 *a, const double2 *b, const double2 *c, const int *cnt, double2 *out) {
@@ -596,7 +585,7 @@ int ccl_label(CclScratch &B, const uint64_t *fg, const int *off, const GridC &g,
                                                                       ecap - 1, chunk);
     k_ccl_cross<<<256, 256, 0, s>>>(d_edges, d_ne, ecap - 1, B.parent_p);
     k_ccl_union_if<<<cdiv(nf, 256), 256, 0, s>>>(B.list_p, nf, fg, d_off, g, B.parent_p, d_ne, ecap - 1);
-    ccl_flatten_rank(B.lb, B.parent_p, B.rank_p, nf, s);
+    ccl_flatten_rank(B.lb, B.parent_p, dev<int>(B.isroot, nf), B.rank_p, nf, s);
     AOS_HIP(hipGetLastError());
     return nf;
 }
@@ -625,9 +614,10 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
     const dim3 gw2(cdiv(g.WW, 64), g.H);
     if (!in.pre) {
         d_fg = dev<uint64_t>(S.fg_bits, Cw);
+        int *d_wc = dev<int>(S.word_cnt, Cw);
         d_wo = dev<int>(S.word_off, Cw + 1);
-        const int fblocks = gw2.x * gw2.y;
-        k_fg<<<fblocks, 64, 0, s>>>(in.skel_bits, d_fg, d_wo, g, d_poly, np, (int)gw2.x, S.lb.take(fblocks, s));
+        k_fg<<<gw2, 64, 0, s>>>(in.skel_bits, d_fg, d_wc, g, d_poly, np);
+        scan_1p(S.lb, d_wc, d_wo, (int)Cw, false, s);
         peek_to_host(h_sc, {d_wo + Cw, S.lb.err_word(s)}, s);
         S.dedup.sev.sync(s);
         tr.mark("fg");
@@ -645,7 +635,7 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         out.n_bfs = in.pre->n_bfs;
     } else if (nf > 0) {
         int *d_list = dev<int>(S.fg_list, nf);
-        int *d_par = dev<int>(S.parent, nf), *d_rank = dev<int>(S.root_rank, nf + 1);
+        int *d_par = dev<int>(S.parent, nf), *d_isroot = dev<int>(S.root_flag, nf), *d_rank = dev<int>(S.root_rank, nf + 1);
         k_fg_list<<<gw2, 64, 0, s>>>(d_fg, d_wo, d_list, g, nullptr);
         const int ecap = std::max(4096, nf / 4);
         int *d_ne = dev<int>(S.ccl_edges, 2 + 2 * (size_t)ecap);
@@ -656,7 +646,7 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
                                                                           ecap - 1, chunk);
         k_ccl_cross<<<256, 256, 0, s>>>(d_edges, d_ne, ecap - 1, d_par);
         k_ccl_union_if<<<cdiv(nf, 256), 256, 0, s>>>(d_list, nf, d_fg, d_wo, g, d_par, d_ne, ecap - 1);
-        ccl_flatten_rank(S.lb, d_par, d_rank, nf, s);
+        ccl_flatten_rank(S.lb, d_par, d_isroot, d_rank, nf, s);
         peek_to_host(h_sc, {d_rank + nf, S.lb.err_word(s)}, s);
         S.dedup.sev.sync(s);
         tr.mark("roots");
@@ -759,8 +749,7 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         S.cur_tab_amax = g.amax;
     }
     k_endpoint_rays<<<6 * nr, 64, 0, s>>>(d_rows, nr, in.skel_bits, g, ang, d_poly, np,
-                                          static_cast<const double *>(S.cur_tab.p), S.n_cur_tab, d_rcand, d_rok);
-    k_endpoint_candidates<<<cdiv(2 * nr, 64), 64, 0, s>>>(d_rows, nr, d_ecand, d_eok);
+                                          static_cast<const double *>(S.cur_tab.p), S.n_cur_tab, d_rcand, d_rok, d_ecand, d_eok);
     if (6 * nr <= kSmallMax) {
         const HashG hs = small_hash(hx0, hx1, hy0, hy1, 0.5);
         SmallDedup sd{};

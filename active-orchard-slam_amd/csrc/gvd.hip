@@ -83,12 +83,6 @@ __global__ void k_merge_members(const double2 *raw, CellIdx ci, const int *owner
 // Sizes the host has not read stay on the device: M boundary points (*M_dev, <= no), P pairs
 // (poff[no]), Mn nodes, ... Kernels are launched over host-known upper bounds and return past the
 // device count; the per-item arrays the scans read are zero there.
-__global__ void k_edges_to_occ(const float *e, int ne, double2 *occ) {
-    int o = blockIdx.x * blockDim.x + threadIdx.x;
-    if (o >= 2 * ne) return;
-    int k = o >> 1;
-    occ[o] = (o & 1) ? make_double2((double)e[4 * k + 2], (double)e[4 * k + 3]) : make_double2((double)e[4 * k], (double)e[4 * k + 1]);
-}
 
 // findNearestBoundaryPoint (gvd:812-824): first strict minimum of |bp_i - q| over i = the (distance, i)
 // lexicographic minimum. The boundary points are the kept candidates of the extractBoundaryPoints
@@ -100,7 +94,7 @@ __device__ __forceinline__ void eval_add(unsigned long long *evals, int k, long 
     if (evals && v > 0) atomicAdd(&evals[k], (unsigned long long)v);
 }
 __global__ void k_nearest(const double2 *occ, int n_occ, CellIdx ci, const int *pos_of, const double2 *bp, const int *M_dev,
-                          int *near_out, unsigned long long *evals) {
+                          int *near_out, unsigned long long *evals) {   // near_out: the ft array's first 2E ints
     int o = blockIdx.x * blockDim.x + threadIdx.x;
     if (o >= n_occ) return;
     const double2 q = occ[o];
@@ -138,7 +132,7 @@ __global__ void k_nearest(const double2 *occ, int n_occ, CellIdx ci, const int *
 // (poff == nullptr: the count pass, with the pairs' exclusive scan fused: pcount = the offsets, [no] = total)
 template <bool COUNT>
 __device__ __forceinline__ int pairs_of(int i, const double2 *bp, CellIdx ci, const int *pos_of, const double2 *occ,
-                                        const int *poff, int *plist, int cap, unsigned long long *evals) {
+                                        const int *poff, int2 *plist, int cap, unsigned long long *evals) {
     const double2 p = bp[i];
     int cx, cy;
     hash_cell(ci.h, p.x, p.y, cx, cy);
@@ -155,8 +149,8 @@ __device__ __forceinline__ int pairs_of(int i, const double2 *bp, CellIdx ci, co
             if (d <= 0.5 && d > 1e-6) {
                 if (!COUNT && w + c < cap) {  // insertion into the sorted run
                     int pos = w + c;
-                    while (pos > w && plist[pos - 1] > j) { plist[pos] = plist[pos - 1]; --pos; }
-                    plist[pos] = j;
+                    while (pos > w && plist[pos - 1].y > j) { plist[pos] = plist[pos - 1]; --pos; }
+                    plist[pos] = make_int2(i, j);
                 }
                 ++c;
             }
@@ -165,38 +159,22 @@ __device__ __forceinline__ int pairs_of(int i, const double2 *bp, CellIdx ci, co
     eval_add(evals, 1, ne);
     return c;
 }
-__global__ __launch_bounds__(256) void k_pairs_count(const double2 *bp, int no, const int *M_dev, CellIdx ci, const int *pos_of,
-                                                     const double2 *occ, int *poff, unsigned long long *evals, LookBack L) {
-    __shared__ int sh_vid;
-    __shared__ LbScanShared sh;
-    const int vid = lb_block_id(L, &sh_vid);
-    const int i = vid * 256 + (int)threadIdx.x;
-    const int c = i < no && i < *M_dev ? pairs_of<true>(i, bp, ci, pos_of, occ, nullptr, nullptr, 0, evals) : 0;
-    lb_scan_store<256>(L, vid, c, no, poff, sh);
+__global__ void k_pairs_count(const double2 *bp, int no, const int *M_dev, CellIdx ci, const int *pos_of, const double2 *occ,
+                              int *pcount, unsigned long long *evals) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= no) return;
+    pcount[i] = i < *M_dev ? pairs_of<true>(i, bp, ci, pos_of, occ, nullptr, nullptr, 0, evals) : 0;
 }
 __global__ void k_pairs(const double2 *bp, int no, const int *M_dev, CellIdx ci, const int *pos_of, const double2 *occ,
-                        const int *poff, int *plist, int cap, unsigned long long *evals) {
+                        const int *poff, int2 *plist, int cap, unsigned long long *evals) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= no || i >= *M_dev) return;
     (void)pairs_of<false>(i, bp, ci, pos_of, occ, poff, plist, cap, evals);
 }
 
-// candidate edge occurrences: [0, E) Voronoi edges, [E, E + P) pairs (P = poff[no] <= cap). from/to keep
-// the direction in which the reference samples the segment.
-__global__ void k_candidates(const int *near_idx, int ne, const int *poff, const int *plist, const int *M_dev, int no,
-                             int cap, int2 *ft) {
-    int c = blockIdx.x * blockDim.x + threadIdx.x;
-    const int np = min(poff[no], cap);
-    if (c >= ne + np) return;
-    int a, b;
-    if (c < ne) { a = near_idx[2 * c]; b = near_idx[2 * c + 1]; }
-    else {
-        int k = c - ne, lo = 0, hi = *M_dev - 1;  // owner i of pair slot k
-        while (lo < hi) { int m = (lo + hi + 1) >> 1; if (poff[m] <= k) lo = m; else hi = m - 1; }
-        a = lo; b = plist[k];
-    }
-    ft[c] = make_int2(a, b);
-}
+// Candidate edge occurrences ft: [0, E) the Voronoi edges (k_nearest writes both ends' nearest boundary
+// points: ft[c] = (near(2c), near(2c + 1))), [E, E + P) the pairs (P = poff[no] <= cap; k_pairs writes (i, j),
+// j ascending per i). from/to keep the direction in which the reference samples the segment.
 
 // edgePassesThroughOccupiedPixels (gvd:320-359) on the framed skeleton. Samples whose t-range
 // cannot touch the grid are skipped (they read no cell), which keeps far hull edges cheap. A passing
@@ -279,40 +257,28 @@ __global__ void k_select(const int2 *ft, const int *pass, const int *poff, int n
 }
 
 // ------------------------------------------------------------------ g7 filter
-// (with the flags' exclusive scan fused: pos[i] = kept nodes before i, pos[no] = M')
-__global__ __launch_bounds__(256) void k_inside(const double2 *bp, int no, const int *M_dev, GridG g, int *f, int *pos,
-                                                LookBack L) {
-    __shared__ int sh_vid;
-    __shared__ LbScanShared sh;
-    const int vid = lb_block_id(L, &sh_vid);
-    const int i = vid * 256 + (int)threadIdx.x;
+__global__ void k_inside(const double2 *bp, int no, const int *M_dev, GridG g, int *f) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= no) return;
     int v = 0;
-    if (i < no && i < *M_dev) {
+    if (i < *M_dev) {
         double2 p = bp[i];
         v = p.x >= g.minx && p.x <= g.maxx && p.y >= g.miny && p.y <= g.maxy;
     }
-    if (i < no) f[i] = v;
-    lb_scan_store<256>(L, vid, v, no, pos, sh);
-}
-__global__ void k_gather_nodes(const double2 *bp, const int *f, const int *pos, int no, double2 *nodes) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < no && f[i]) nodes[pos[i]] = bp[i];
+    f[i] = v;
 }
 // selected candidate c -> record (a<b); keep if both nodes stay (and stay distinct); 0 past the candidates
-// (with the keep flags' exclusive scan fused: kpos[c] = kept edges before c, kpos[ncap] = the total)
-__global__ __launch_bounds__(256) void k_edge_keep(const int *selected, const int2 *ft, int ncap, const int *inside, const int *pos,
-                                                   int *keep, int *kpos, LookBack L) {
-    __shared__ int sh_vid;
-    __shared__ LbScanShared sh;
-    const int vid = lb_block_id(L, &sh_vid);
-    const int c = vid * 256 + (int)threadIdx.x;
+// (and the kept nodes gathered, nodes[pos[i]] = bp[i] for i < no: k_gather_nodes folded in)
+__global__ void k_edge_keep(const int *selected, const int2 *ft, int ncap, const int *inside, const int *pos, int *keep,
+                            const double2 *bp, int no, double2 *nodes) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c < no && inside[c]) nodes[pos[c]] = bp[c];
     int k = 0;
     if (c < ncap && selected[c]) {
         int a = min(ft[c].x, ft[c].y), b = max(ft[c].x, ft[c].y);
         k = inside[a] && inside[b] && pos[a] != pos[b];
     }
     if (c < ncap) keep[c] = k;
-    lb_scan_store<256>(L, vid, k, ncap, kpos, sh);
 }
 __global__ void k_edge_emit(const int *keep, const int *kpos, const int2 *ft, int ncap, const int *pos, const double2 *nodes,
                             int *edges, float *len) {
@@ -523,22 +489,18 @@ __device__ __forceinline__ int node_labels_of(int i, const double2 *nodes, const
     mask_out = m; cidx_out = ci;
     return cnt;
 }
-// count pass over [0, no) (0 past the Mn nodes), the entries' exclusive scan fused: off[i], off[no] = total
-__global__ __launch_bounds__(256) void k_node_labels_count(const double2 *nodes, int no, const int *Mn_dev, const double2 *lp,
-                                                           const int *lv, int n_rows, CellIdx cq, int *mask, int *cidx,
-                                                           int *count, int *off, LookBack L) {
-    __shared__ int sh_vid;
-    __shared__ LbScanShared sh;
-    const int vid = lb_block_id(L, &sh_vid);
-    const int i = vid * 256 + (int)threadIdx.x;
+// count pass over [0, no) (0 past the Mn nodes)
+__global__ void k_node_labels_count(const double2 *nodes, int no, const int *Mn_dev, const double2 *lp, const int *lv, int n_rows,
+                                    CellIdx cq, int *mask, int *cidx, int *count) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= no) return;
     int cnt = 0;
-    if (i < no && i < *Mn_dev) {
+    if (i < *Mn_dev) {
         int m = 0, ci = -1;
         cnt = node_labels_of(i, nodes, lp, lv, n_rows, cq, m, ci, nullptr, nullptr, nullptr);
         mask[i] = m; cidx[i] = ci;
     }
-    if (i < no) count[i] = cnt;
-    lb_scan_store<256>(L, vid, cnt, no, off, sh);
+    count[i] = cnt;
 }
 // fill pass over the Mn nodes: the (row, type) entries at off[i]
 __global__ void k_node_labels_fill(const double2 *nodes, int Mn, const double2 *lp, const int *lv, int n_rows, CellIdx cq,
@@ -645,22 +607,33 @@ __global__ __launch_bounds__(256) void k_facet_count(const int *qe, const int *v
     if (k < nv) cnt[k] = c;
     lb_scan_store<256>(L, vid, c, nv, off, sh);
 }
+// OCC: the edges' ends straight as the g5 boundary-point candidates (double: edge k -> occ[2k] start, occ[2k + 1]
+// end; the GVD's edges_ are double from the float facet points), else float4 edges (the markers' cells)
+template <bool OCC>
 __global__ void k_facet_emit(const int *qe, const int *vfirst, const int *off, const int *cnt, int nv, const float2 *face,
-                             float4 *edges) {
+                             float4 *edges, double2 *occ) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= nv || cnt[k] == 0) return;
     const int f = vfirst[k], start = (f & ~3) + ((f + 1) & 3), n = cnt[k];
-    float4 *o = edges + off[k];
+    const int o = off[k];
+    auto put = [&](int i, float2 a, float2 b) {
+        if (OCC) {
+            occ[2 * (size_t)(o + i)] = make_double2((double)a.x, (double)a.y);
+            occ[2 * (size_t)(o + i) + 1] = make_double2((double)b.x, (double)b.y);
+        } else {
+            edges[o + i] = make_float4(a.x, a.y, b.x, b.y);
+        }
+    };
     const float2 first = dual_face(face, start);
     float2 prev = first;
     int t = q_get(qe, start, 0x13);
     for (int i = 1; i < n; ++i) {
         const float2 cur = dual_face(face, t);
-        o[i - 1] = make_float4(prev.x, prev.y, cur.x, cur.y);
+        put(i - 1, prev, cur);
         prev = cur;
         t = q_get(qe, t, 0x13);
     }
-    o[n - 1] = make_float4(prev.x, prev.y, first.x, first.y);
+    put(n - 1, prev, first);
 }
 
 // ------------------------------------------------------------------ orchestration
@@ -725,9 +698,13 @@ static int facets_count(FacetBufs &F, const Subdiv2D &sd, Subdiv2D::Raw &R, int 
     if (h_sc[2]) throw std::runtime_error("Subdiv2D facets: single-pass scan failed on the device");
     return h_sc[0];
 }
-static void facets_emit(FacetBufs &F, const Subdiv2D::Raw &R, float4 *edges, hipStream_t s) {
-    k_facet_emit<<<cdiv(R.n_vtx, 256), 256, 0, s>>>(F.qe, F.vf, F.off.as<int>(), F.cnt.as<int>(), R.n_vtx,
-                                                   F.face.as<float2>(), edges);
+static void facets_emit(FacetBufs &F, const Subdiv2D::Raw &R, float4 *edges, hipStream_t s, double2 *occ = nullptr) {
+    if (occ)
+        k_facet_emit<true><<<cdiv(R.n_vtx, 256), 256, 0, s>>>(F.qe, F.vf, F.off.as<int>(), F.cnt.as<int>(), R.n_vtx,
+                                                             F.face.as<float2>(), nullptr, occ);
+    else
+        k_facet_emit<false><<<cdiv(R.n_vtx, 256), 256, 0, s>>>(F.qe, F.vf, F.off.as<int>(), F.cnt.as<int>(), R.n_vtx,
+                                                              F.face.as<float2>(), edges, nullptr);
 }
 
 // publishMarkers' Voronoi cells (gvd:1098-1194): VoronoiDiagram::extractCellBoundaries
@@ -976,7 +953,7 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     // ---- g3/g4 finite filter, bounds, Subdiv2D inserts (host replay) -> facets / Voronoi edges (GPU)
     auto t0 = std::chrono::steady_clock::now();
     int ne = 0;
-    float *d_ef = nullptr;
+    double2 *d_occ = nullptr;
     {
         double min_x = g.minx, max_x = g.maxx, min_y = g.miny, max_y = g.maxy;
         if (!std::isfinite(min_x) || !std::isfinite(max_x) || !std::isfinite(min_y) || !std::isfinite(max_y)) return false;
@@ -1007,8 +984,8 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
             Subdiv2D::Raw R{};
             ne = facets_count(S.fb, sd, R, h_sc, s, G.sev);
             tr.mark("facets");
-            d_ef = dev<float>(S.edges_f, 4 * (size_t)std::max(ne, 1));
-            if (ne) facets_emit(S.fb, R, reinterpret_cast<float4 *>(d_ef), s);
+            d_occ = dev<double2>(S.occ, 2 * (size_t)std::max(ne, 1));   // (g5's candidates: the edge ends)
+            if (ne) facets_emit(S.fb, R, nullptr, s, d_occ);
         }
     }
     auto t1 = std::chrono::steady_clock::now();
@@ -1024,8 +1001,6 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     // ---- g5 boundary points: the 2E edge ends, de-duplicated (1 cm key or < 5 cm) through a cell index of
     // cells >= 0.5 m, which g6 reuses for its nearest-point and pair searches (pos_of: ends -> points)
     const int no = 2 * ne;
-    double2 *d_occ = dev<double2>(S.occ, no);
-    k_edges_to_occ<<<cdiv(no, 256), 256, 0, s>>>(d_ef, ne, d_occ);
     const HashG h5 = make_hash_n(g.minx - 10.0, g.maxx + 10.0, g.miny - 10.0, g.maxy + 10.0, 0.5, no);
     double2 *d_bp = dev<double2>(S.bp, no);
     int *d_pos_of = dev<int>(S.kept_occ, no);
@@ -1036,18 +1011,14 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     const int *d_M = d_sc;
 
     // ---- g6 graph edges
-    int *d_near = dev<int>(S.near_idx, no);
     unsigned long long *d_evals = nullptr;   // (aos_params.gvd_count_evals)
     if (P.gvd_count_evals) {
         d_evals = dev<unsigned long long>(S.evals, 8);
         AOS_HIP(hipMemsetAsync(d_evals, 0, 8 * sizeof(unsigned long long), s));
     }
-    k_nearest<<<cdiv(no, 256), 256, 0, s>>>(d_occ, no, cio, d_pos_of, d_bp, d_M, d_near, d_evals);
-    int *d_poff = dev<int>(S.poff, no + 1);
-    {
-        const int blocks = cdiv((long long)no + 1, 256);
-        k_pairs_count<<<blocks, 256, 0, s>>>(d_bp, no, d_M, cio, d_pos_of, d_occ, d_poff, d_evals, S.lb.take(blocks, s));
-    }
+    int *d_pcount = dev<int>(S.pcount, no), *d_poff = dev<int>(S.poff, no + 1);
+    k_pairs_count<<<cdiv(no, 256), 256, 0, s>>>(d_bp, no, d_M, cio, d_pos_of, d_occ, d_pcount, d_evals);
+    scan_1p(S.lb, d_pcount, d_poff, no, false, s);
     // The pair lists get a capacity from the last frame (P is read back only with the frame's sizes below);
     // a frame with more pairs runs the rest again with the exact size.
     int cap = G.pairs_cap > 0 ? G.pairs_cap : std::max(1024, 2 * no);
@@ -1079,34 +1050,29 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     int *h_sz = h_sc + 8;
     for (int attempt = 0;; ++attempt) {
         const int ncap = ne + cap;
-        int *d_plist = dev<int>(S.plist, cap);
-        k_pairs<<<cdiv(no, 256), 256, 0, s>>>(d_bp, no, d_M, cio, d_pos_of, d_occ, d_poff, d_plist, cap, d_evals);
         int2 *d_ft = dev<int2>(S.ft, ncap);
+        unsigned long long *ev_k = attempt ? nullptr : d_evals;   // (a rerun with the exact pair capacity is not counted)
+        k_nearest<<<cdiv(no, 256), 256, 0, s>>>(d_occ, no, cio, d_pos_of, d_bp, d_M, reinterpret_cast<int *>(d_ft), ev_k);
+        k_pairs<<<cdiv(no, 256), 256, 0, s>>>(d_bp, no, d_M, cio, d_pos_of, d_occ, d_poff, d_ft + ne, cap, ev_k);
         int *d_pass = dev<int>(S.pass, ncap), *d_grank = dev<int>(S.occ_idx, ncap), *d_sel = dev<int>(S.selected, ncap);
         const size_t gc0 = S.gcnt.cap;
         int *d_gcnt = dev<int>(S.gcnt, no);
         if (S.gcnt.cap != gc0 || S.gcnt_dirty) AOS_HIP(hipMemsetAsync(d_gcnt, 0, S.gcnt.cap, s));
         S.gcnt_dirty = true;
         int *d_goff = dev<int>(S.goff, no + 1), *d_glist = dev<int>(S.glist, ncap);
-        k_candidates<<<cdiv(ncap, 256), 256, 0, s>>>(d_near, ne, d_poff, d_plist, d_M, no, cap, d_ft);
         k_occupancy<<<cdiv(ncap, 64), 64, 0, s>>>(d_ft, d_poff, no, ne, cap, d_bp, in.d_skeleton, g, d_pass, d_gcnt, d_grank,
-                                                  d_evals);
+                                                  ev_k);
         scan_1p(S.lb, d_gcnt, d_goff, no, true, s);   // (leaves the group counts zero)
         S.gcnt_dirty = false;
         k_group_scatter<<<cdiv(ncap, 256), 256, 0, s>>>(d_ft, d_pass, d_poff, no, ne, cap, d_goff, d_grank, d_glist);
         k_select<<<cdiv(ncap, 256), 256, 0, s>>>(d_ft, d_pass, d_poff, no, ne, cap, d_goff, d_glist, d_sel);
 
         // ---- g7 filter
-        {
-            const int blocks = cdiv((long long)no + 1, 256);
-            k_inside<<<blocks, 256, 0, s>>>(d_bp, no, d_M, g, d_in, d_ipos, S.lb.take(blocks, s));
-        }
+        k_inside<<<cdiv(no, 256), 256, 0, s>>>(d_bp, no, d_M, g, d_in);
+        scan_1p(S.lb, d_in, d_ipos, no, false, s);
         int *d_keep = dev<int>(S.keep, ncap), *d_kpos = dev<int>(S.kpos, ncap + 1);
-        {
-            const int blocks = cdiv((long long)ncap + 1, 256);
-            k_edge_keep<<<blocks, 256, 0, s>>>(d_sel, d_ft, ncap, d_in, d_ipos, d_keep, d_kpos, S.lb.take(blocks, s));
-        }
-        k_gather_nodes<<<cdiv(no, 256), 256, 0, s>>>(d_bp, d_in, d_ipos, no, d_nodes);
+        k_edge_keep<<<cdiv(std::max(ncap, no), 256), 256, 0, s>>>(d_sel, d_ft, ncap, d_in, d_ipos, d_keep, d_bp, no, d_nodes);
+        scan_1p(S.lb, d_keep, d_kpos, ncap, false, s);
         d_edges = dev<int>(S.edges, 2 * (size_t)ncap);
         d_lens = dev<float>(S.lens, ncap);
         k_edge_emit<<<cdiv(ncap, 256), 256, 0, s>>>(d_keep, d_kpos, d_ft, ncap, d_ipos, d_nodes, d_edges, d_lens);
@@ -1116,16 +1082,13 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
         if (nj) {
             const HashG hl = make_hash_n(g.minx - 10.0, g.maxx + 10.0, g.miny - 10.0, g.maxy + 10.0, 5.01, no);
             const CellIdx cn = cell_index_build(S.ci_nodes, d_nodes, nullptr, no, hl, s, d_Mn);
-            k_label_points<<<nj, 256, 0, s>>>(d_jobs, nj, d_nodes, d_Mn, g, in.d_skeleton, cn, d_lp, d_lv, d_evals);
+            k_label_points<<<nj, 256, 0, s>>>(d_jobs, nj, d_nodes, d_Mn, g, in.d_skeleton, cn, d_lp, d_lv, ev_k);
         }
         // ---- g9 node labels: the valid label points in cells of >= 0.1 m
         const HashG hq = make_hash_n(g.minx - 1.0, g.maxx + 1.0, g.miny - 1.0, g.maxy + 1.0, 0.1, nj);
         const CellIdx cq = S.cq = cell_index_build(S.ci_labels, d_lp, d_lv, nj, hq, s);
-        {
-            const int blocks = cdiv((long long)no + 1, 256);
-            k_node_labels_count<<<blocks, 256, 0, s>>>(d_nodes, no, d_Mn, d_lp, d_lv, nrows, cq, d_mask, d_cidx, d_lcnt, d_loff,
-                                                       S.lb.take(blocks, s));
-        }
+        k_node_labels_count<<<cdiv(no, 256), 256, 0, s>>>(d_nodes, no, d_Mn, d_lp, d_lv, nrows, cq, d_mask, d_cidx, d_lcnt);
+        scan_1p(S.lb, d_lcnt, d_loff, no, false, s);
         // the frame's sizes and error words: one read-back
         Peek pk{{d_M, d_poff + no, d_Mn, d_kpos + ncap, d_loff + no, dedup_err(G.dedup, s), S.lb.err_word(s),
                  S.ci_nodes.lb.err_word(s)}, 8};

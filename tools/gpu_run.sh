@@ -9,6 +9,7 @@
 #   kt       rocprofv3 --kernel-trace --stats of the sequential C2 loop
 #   ktc3     the same on one C3 frame set (bench --config C3 on one GPU)
 #   pmc      FETCH_SIZE and WRITE_SIZE passes (separate runs) -> TAG_pmc_traffic.json
+#   pmcc3    the same on C3 (bench --config C3, one GPU) -> TAG_c3_pmc_traffic.json
 #   tiled    the rotating-root test, then bench.py --tiled at RANKS (default "1 2 4"; 2 and 4 ranks share the
 #            box's GPU over gloo)
 #   tiledstream  bench.py --tiled --stream at 1 rank, then the driver's --gpus 2 flow over gloo
@@ -70,6 +71,16 @@ for step in $STEPS; do
       python3 tools/pmc_traffic.py $(ls gpurun_out/${TAG}_fetch/*counter_collection.csv | head -1) \
         $(ls gpurun_out/${TAG}_write/*counter_collection.csv | head -1) gpurun_out/${TAG}_pmc_traffic.json
       cp gpurun_out/${TAG}_pmc_traffic.json profiles/ ;;   # (a later bench step of this call reads it)
+    pmcc3)
+      rm -rf gpurun_out/${TAG}_c3fetch gpurun_out/${TAG}_c3write
+      (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/${TAG}_c3fetch -o fetch \
+        -- python3 $R/bench.py --config C3 --no-cpu-baseline --no-pipelined-rate --no-device-rate --steps 2 --warmup 1 \
+        > $R/gpurun_out/${TAG}_c3fetch.log 2>&1)
+      (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/${TAG}_c3write -o write \
+        -- python3 $R/bench.py --config C3 --no-cpu-baseline --no-pipelined-rate --no-device-rate --steps 2 --warmup 1 \
+        > $R/gpurun_out/${TAG}_c3write.log 2>&1)
+      python3 tools/pmc_traffic.py $(ls gpurun_out/${TAG}_c3fetch/*counter_collection.csv | head -1) \
+        $(ls gpurun_out/${TAG}_c3write/*counter_collection.csv | head -1) gpurun_out/${TAG}_c3_pmc_traffic.json ;;
     tiled)
       timeout -k 10 600 python -u -m pytest tests/test_gpu_tiled.py -x -v --timeout 400 --timeout-method thread -k rotating \
         > gpurun_out/${TAG}_pytest_rot.log 2>&1 || { tail -40 gpurun_out/${TAG}_pytest_rot.log; exit 1; }
