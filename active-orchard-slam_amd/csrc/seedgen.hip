@@ -933,6 +933,28 @@ static int grid_expand_threads() {   // AOS_GRID_EXPAND_THREADS (default 8)
     static const int v = [] { const char *e = getenv("AOS_GRID_EXPAND_THREADS"); return e ? std::max(1, atoi(e)) : 8; }();
     return v;
 }
+// The grids' D2H runs as the runtime's blit kernels (under the HIP runtime torch loads). Beside the cluster stage
+// they held the CUs its kernels needed: k_fg took 45 us instead of 18.6 beside the 2 MB bits copy at C2, 159
+// instead of 24 beside the 8 MB at C3 (round-5 traces, tools/kt_overlap.py). The copy stream is created with a CU
+// mask (hipExtStreamCreateWithCUMask) of AOS_COPY_CUS CUs (default 16 of the 256, spread over the id range;
+// 0: no mask), so its blit waves stay on those CUs and the stage's kernels keep the rest: PCIe, not CUs, bounds
+// the copy.
+static void create_copy_stream(hipStream_t *st) {
+    static const int want = [] { const char *e = getenv("AOS_COPY_CUS"); return e ? std::max(0, atoi(e)) : 16; }();
+    int dev = 0, ncu = 0;
+    AOS_HIP(hipGetDevice(&dev));
+    AOS_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    if (want <= 0 || want >= ncu) {
+        AOS_HIP(hipStreamCreateWithFlags(st, hipStreamNonBlocking));
+        return;
+    }
+    std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+    for (int k = 0; k < want; ++k) {
+        const int cu = (int)((long long)k * ncu / want);
+        mask[cu >> 5] |= 1u << (cu & 31);
+    }
+    AOS_HIP(hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data()));
+}
 static int grid_copy_blocks() {   // AOS_GRID_COPY_BLOCKS (default 64)
     static const int b = [] { const char *e = getenv("AOS_GRID_COPY_BLOCKS"); return e ? std::max(1, atoi(e)) : 64; }();
     return b;
@@ -980,7 +1002,7 @@ void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *c
     auto issue_grid_copy = [&]() {
         h_occ.ensure(std::max<size_t>(C, 1)); h_skel.ensure(std::max<size_t>(C, 1));
         if (!copy_stream) {
-            AOS_HIP(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
+            create_copy_stream(&copy_stream);
             AOS_HIP(hipEventCreateWithFlags(&copy_ready, hipEventDisableTiming));
             AOS_HIP(hipEventCreateWithFlags(&copy_done, hipEventDisableTiming));
         }
