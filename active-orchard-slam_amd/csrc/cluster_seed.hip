@@ -101,6 +101,12 @@ __global__ void k_ccl_union(const int *list, int n, const uint64_t *fg, const in
 // chunk and block size (AOS_CCL_CHUNK / AOS_CCL_TB override them for A/B runs)
 static int ccl_chunk() { static const int v = [] { const char *e = getenv("AOS_CCL_CHUNK"); return e ? std::max(64, std::min(16384, atoi(e))) : 2048; }(); return v; }
 static int ccl_tb() { static const int v = [] { const char *e = getenv("AOS_CCL_TB"); return e ? std::max(64, std::min(1024, atoi(e))) / 64 * 64 : 256; }(); return v; }
+// capacity of k_ccl_local's cross-chunk link list (AOS_DEBUG_CCL_ECAP, read per call: tests force the overflow
+// fallback of k_ccl_cross with a tiny list)
+static int ccl_edge_cap(int nf) {
+    const char *e = getenv("AOS_DEBUG_CCL_ECAP");
+    return e ? std::max(2, atoi(e)) : std::max(4096, nf / 4);
+}
 __device__ __forceinline__ int lds_find(int *lp, int x) {
     for (int p; (p = __hip_atomic_load(&lp[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != x;) x = p;
     return x;
@@ -138,22 +144,24 @@ __global__ __launch_bounds__(1024) void k_ccl_local(const int *list, int n, cons
     __syncthreads();
     for (int i = threadIdx.x; i < m; i += nt) parent[base + i] = base + lds_find(lp, i);
 }
-__global__ void k_ccl_cross(const int2 *edges, const int *n_edges, int cap, int *parent) {
-    const int ne = min(*n_edges, cap);
-    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < ne; e += gridDim.x * blockDim.x)
-        uf_union(parent, edges[e].x, edges[e].y);
-}
-// the fallback when the cross-edge list overflowed (never at C1-C4): every link again, globally
-__global__ void k_ccl_union_if(const int *list, int n, const uint64_t *fg, const int *off, GridC g, int *parent,
-                               const int *n_edges, int cap) {
-    if (*n_edges <= cap) return;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    int p = list[i], y = p / g.W, x = p - y * g.W;
+// The cross-chunk links, unioned globally; when the list overflowed (never at C1-C4) every link of every cell
+// again instead (the fallback, in the same launch: round 4's separate k_ccl_union_if returned at once in
+// every frame)
+__global__ void k_ccl_cross(const int2 *edges, const int *n_edges, int cap, int *parent, const int *list, int n,
+                            const uint64_t *fg, const int *off, GridC g) {
+    const int stride = gridDim.x * blockDim.x;
+    if (*n_edges <= cap) {
+        const int ne = *n_edges;
+        for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < ne; e += stride) uf_union(parent, edges[e].x, edges[e].y);
+        return;
+    }
     const int ndx[4] = {-1, 0, 1, -1}, ndy[4] = {-1, -1, -1, 0};
-    for (int k = 0; k < 4; ++k) {
-        int j = fg_index(fg, off, g, x + ndx[k], y + ndy[k]);
-        if (j >= 0) uf_union(parent, i, j);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const int p = list[i], y = p / g.W, x = p - y * g.W;
+        for (int k = 0; k < 4; ++k) {
+            const int j = fg_index(fg, off, g, x + ndx[k], y + ndy[k]);
+            if (j >= 0) uf_union(parent, i, j);
+        }
     }
 }
 __global__ void k_ccl_flatten(int *parent, int *is_root, int n) {
@@ -576,15 +584,14 @@ int ccl_label(CclScratch &B, const uint64_t *fg, const int *off, const GridC &g,
     }
     const dim3 gw2(cdiv(g.WW, 64), g.H);
     k_fg_list<<<gw2, 64, 0, s>>>(fg, d_off, B.list_p, g, nullptr);
-    const int ecap = std::max(4096, nf / 4);
+    const int ecap = ccl_edge_cap(nf);
     int *d_ne = dev<int>(B.edges, 2 + 2 * (size_t)ecap);
     int2 *d_edges = reinterpret_cast<int2 *>(d_ne + 2);
     AOS_HIP(hipMemsetAsync(d_ne, 0, sizeof(int), s));
     const int chunk = ccl_chunk();
     k_ccl_local<<<cdiv(nf, chunk), ccl_tb(), sizeof(int) * chunk, s>>>(B.list_p, nf, fg, d_off, g, B.parent_p, d_edges, d_ne,
                                                                       ecap - 1, chunk);
-    k_ccl_cross<<<256, 256, 0, s>>>(d_edges, d_ne, ecap - 1, B.parent_p);
-    k_ccl_union_if<<<cdiv(nf, 256), 256, 0, s>>>(B.list_p, nf, fg, d_off, g, B.parent_p, d_ne, ecap - 1);
+    k_ccl_cross<<<256, 256, 0, s>>>(d_edges, d_ne, ecap - 1, B.parent_p, B.list_p, nf, fg, d_off, g);
     ccl_flatten_rank(B.lb, B.parent_p, dev<int>(B.isroot, nf), B.rank_p, nf, s);
     AOS_HIP(hipGetLastError());
     return nf;
@@ -637,15 +644,14 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         int *d_list = dev<int>(S.fg_list, nf);
         int *d_par = dev<int>(S.parent, nf), *d_isroot = dev<int>(S.root_flag, nf), *d_rank = dev<int>(S.root_rank, nf + 1);
         k_fg_list<<<gw2, 64, 0, s>>>(d_fg, d_wo, d_list, g, nullptr);
-        const int ecap = std::max(4096, nf / 4);
+        const int ecap = ccl_edge_cap(nf);
         int *d_ne = dev<int>(S.ccl_edges, 2 + 2 * (size_t)ecap);
         int2 *d_edges = reinterpret_cast<int2 *>(d_ne + 2);   // (8-byte aligned: DevBuf bases are)
         AOS_HIP(hipMemsetAsync(d_ne, 0, sizeof(int), s));
         const int chunk = ccl_chunk();
         k_ccl_local<<<cdiv(nf, chunk), ccl_tb(), sizeof(int) * chunk, s>>>(d_list, nf, d_fg, d_wo, g, d_par, d_edges, d_ne,
                                                                           ecap - 1, chunk);
-        k_ccl_cross<<<256, 256, 0, s>>>(d_edges, d_ne, ecap - 1, d_par);
-        k_ccl_union_if<<<cdiv(nf, 256), 256, 0, s>>>(d_list, nf, d_fg, d_wo, g, d_par, d_ne, ecap - 1);
+        k_ccl_cross<<<256, 256, 0, s>>>(d_edges, d_ne, ecap - 1, d_par, d_list, nf, d_fg, d_wo, g);
         ccl_flatten_rank(S.lb, d_par, d_isroot, d_rank, nf, s);
         peek_to_host(h_sc, {d_rank + nf, S.lb.err_word(s)}, s);
         S.dedup.sev.sync(s);

@@ -396,3 +396,21 @@ def test_gvd_markers_background_job_overlaps_next_frame():
     _assert_markers(m, og)
     c.gvd_from_seedgen()
     c.close()                     # job still in flight
+
+
+def test_ccl_link_list_overflow_fallback(monkeypatch):
+    """k_ccl_local hands its cross-chunk links to k_ccl_cross through a list; when the list overflows, the same
+    launch unions every link of every cell instead. A C1 frame with a 2-entry list (AOS_DEBUG_CCL_ECAP) equals
+    the default frame, clusters and seeds included."""
+    cfg = orchard.CONFIGS["C1"]
+    cloud, poly = orchard.generate(cfg), orchard.polygon(cfg)
+    ctx = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res))
+    ctx.set_polygon(poly)
+    a = ctx.seedgen(cloud)
+    monkeypatch.setenv("AOS_DEBUG_CCL_ECAP", "2")
+    b = ctx.seedgen(cloud)
+    monkeypatch.delenv("AOS_DEBUG_CCL_ECAP")
+    ctx.close()
+    assert a["n_clusters_all"] == b["n_clusters_all"] and a["n_bfs_replayed"] == b["n_bfs_replayed"]
+    for k in ("row_center", "row_start", "row_end", "row_length", "voronoi_seeds", "cluster_info", "rows_info"):
+        assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), k
