@@ -160,6 +160,9 @@ struct aos_ctx {
     aos::GridExpander expander;               // expands them on host threads beside the cluster / seed stage
     hipStream_t copy_stream = nullptr;   // their D2H, beside the cluster / seed stage
     hipEvent_t copy_ready = nullptr, copy_done = nullptr;
+    bool infl_bits_sent = false;         // this frame's inflated-grid bits are already on the copy stream
+    void grid_d2h(void *h, const void *d, size_t bytes);   // on the copy stream, after the work queued so far
+    void grid_copy_wait();
     std::vector<double> h_row_center, h_row_start, h_row_end, h_row_length, h_voronoi, h_rows_info, h_cluster_info;
     int n_virtual = 0, n_ray = 0, n_endpoint = 0, n_clusters_all = 0, n_bfs_replayed = 0;
 
@@ -220,7 +223,8 @@ struct aos_ctx {
     void map_append_box(const aos_cloud_view &scan, const float box[4]);   // tiled streaming map
     void map_grow(uint64_t n);
     void ror_stage(const aos::FrameGeom &g, const RorOwn &o, uint64_t *rbits, bool allow_guess);
-    bool ror_collect(bool throw_stuck = true);   // after the stream synchronised: true if the ROR scatter overflowed
+    bool ror_collect(bool throw_stuck = true);
+    void ror_stats_to_host(const int *d_staged_total, const unsigned long long *d_own);   // after the stream synchronised: true if the ROR scatter overflowed
     void ror_stage_append(aos::RorLaunch L, uint64_t *rbits);   // streaming map: one scan on the tile store
     aos::LookBack ror_lookback(const aos::RorLaunch &L, int G, unsigned long long *d_own);
     void ror_stage_unchanged();   // streaming map: no new points since the committed store

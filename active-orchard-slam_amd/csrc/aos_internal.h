@@ -143,8 +143,10 @@ int rt_part_blocks(const RorLaunch &L);   // G: workgroups (= cloud chunks) of t
 struct LookBack;
 size_t rt_h_ints(const RorLaunch &L, int G);
 int rt_colscan_words(const RorLaunch &L, int G);
+// clr: buffers the count launch zeroes before the stage's later kernels write them (no fill launches)
+struct RtClear { uint64_t *w = nullptr; size_t nw = 0; unsigned long long *c = nullptr; int nc = 0; int *k = nullptr; int nk = 0; };
 void launch_rt_count(const RorLaunch &L, int *H, int G, int *ts, unsigned long long *n_own, const LookBack &lb,
-                     hipStream_t s);
+                     hipStream_t s, const RtClear &clr = RtClear{});
 void launch_rt_scatter(const RorLaunch &L, int *H, const int *tstart, int G, float4 *staged, hipStream_t s);
 // kept_tile (nullable): per-tile kept counts; dirty (nullable): a tile is counted iff dirty[t+1] > dirty[t]
 // scratch: staged-sized; bigbins: rt_bigbins_ints(L) ints (tiles beyond the LDS capacity are sorted there)
@@ -166,11 +168,17 @@ void launch_pack_xyz(const uint8_t *cloud, uint64_t n, uint32_t step, uint32_t o
 // the records with x in [box[0], box[2]] and y in [box[1], box[3]] -> out[*count ...] (atomics order)
 void launch_pack_xyz_box(const uint8_t *cloud, uint64_t n, uint32_t step, uint32_t ox, uint32_t oy, uint32_t oz,
                          const float box[4], float4 *out, unsigned long long *count, hipStream_t s);
-void launch_inflate(const uint64_t *in, uint64_t *out, const FrameGeom &g, hipStream_t s);
-void launch_bits_to_bytes(const uint64_t *bits, int8_t *out, const FrameGeom &g, int frame, hipStream_t s);
+// (bytes != nullptr: the inflated grid's int8 {0, 100} bytes with a `frame`-cell border in the same launch)
+void launch_inflate(const uint64_t *in, uint64_t *out, const FrameGeom &g, hipStream_t s, int8_t *bytes = nullptr,
+                    int frame = 0);
+// rect (nullable): gx0, gy0, gx1, gy1 of markPolygonBoundaryAsOccupied's rectangle, drawn in the same launch
+struct ByteRect { int gx0, gy0, gx1, gy1; };
+void launch_bits_to_bytes(const uint64_t *bits, int8_t *out, const FrameGeom &g, int frame, hipStream_t s,
+                          const int *rect = nullptr);
 // int8 {0,100} grid (C bytes) -> ceil(C / 64) words of bits; a byte that is neither sets *err
 void launch_pack_grid(const int8_t *g, size_t C, uint64_t *bits, int *err, hipStream_t s);
-void launch_open(const uint64_t *in, uint64_t *out, const FrameGeom &g, hipStream_t s);
+// (zero: nzero ints cleared in the same launch, the thinning flags)
+void launch_open(const uint64_t *in, uint64_t *out, const FrameGeom &g, hipStream_t s, int *zero = nullptr, int nzero = 0);
 // Zhang-Suen temporal block: KIT iterations per launch; flags[0] = non-empty after iteration 1,
 // flags[1 + k] = iteration k (0-based) deleted something.
 constexpr int kThinItersPerLaunch = 8;
@@ -184,10 +192,10 @@ struct ThinOwn { int y0, y1, c0, c1, early_exit; const int *act_prev = nullptr; 
 int thin_tiles(const FrameGeom &g);
 void launch_thin_block(const uint64_t *in, uint64_t *out, const FrameGeom &g, int base_iter, int *flags,
                        const ThinOwn &own, hipStream_t s);
-void launch_draw_rect(int8_t *grid, const FrameGeom &g, int gx0, int gy0, int gx1, int gy1, hipStream_t s);
 // the converged thinning buffer (from the device flags) -> out, n words (no host round trip)
+// (h_flags: pinned, receives flags[0, nh) in the same launch)
 void launch_thin_pick(const int *flags, int launched, const uint64_t *b0, const uint64_t *b1, uint64_t *out, size_t n,
-                      hipStream_t s);
+                      hipStream_t s, int *h_flags = nullptr, int nh = 0);
 void launch_zero_ints(int *p, int n, hipStream_t s);   // a kernel (no memset node in a captured graph)
 size_t scan_temp_bytes(int n);
 void launch_exclusive_scan(const int *in, int *out, int n, void *temp, size_t temp_bytes, hipStream_t s);

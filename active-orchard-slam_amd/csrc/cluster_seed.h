@@ -87,6 +87,7 @@ struct ClusterSeedState {
     LookBackScratch lb;           // the stage's single-pass scans
     bool cl_count_dirty = true;   // cl_count (cluster sizes) not known to be zero
     PinnedBuf h_recbuf, h_up_poly, h_up_rows;   // cluster records read back; host -> device staging
+    std::vector<double> poly_up;                 // the polygon in `poly` (uploaded again only when it changes)
     PinnedBuf h_seeds;   // the frame's seeds (one DMA into pinned memory: no staging copy, no page faults)
     PinnedBuf h_cells;   // the replayed clusters' cells (one DMA; round 3's zeroed pageable vector cost ~1.5 ms at C3)
     PinnedBuf h_misc;
@@ -114,7 +115,8 @@ struct SeedStageIn {
 struct GridC;
 // k_cluster_stats over clusters given as runs of raster-ordered cells (off[n_clusters + 1], cells)
 void launch_cluster_stats(const int *off, const int *cells, int n_clusters, const GridC &g, const double *poly, int np,
-                          float min_length, ClusterRec *rec, hipStream_t s);
+                          float min_length, ClusterRec *rec, hipStream_t s,
+                          ClusterRec *hrec = nullptr);   // hrec: pinned host copy of the records, same launch
 // exact FIFO-BFS replays (host, parallel over clusters; cluster_host.cpp); cells of a job in any order (the BFS
 // starts from the smallest), n of them
 struct ReplayJob { int c; const int *cells; int n; };

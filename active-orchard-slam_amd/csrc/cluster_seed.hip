@@ -53,9 +53,11 @@ __global__ void k_fg(const uint64_t *skel, uint64_t *fg, int *cnt, GridC g, cons
     cnt[wi] = __popcll(o);
 }
 
-// (parent != nullptr: also the union-find's initial parents, parent[k] = k)
-__global__ void k_fg_list(const uint64_t *fg, const int *off, int *list, GridC g, int *parent) {
+// (parent != nullptr: also the union-find's initial parents, parent[k] = k; zero != nullptr: *zero = 0, the
+// cross-chunk link count of k_ccl_local, without a fill launch)
+__global__ void k_fg_list(const uint64_t *fg, const int *off, int *list, GridC g, int *parent, int *zero) {
     int c = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    if (zero && c == 0 && y == 0) *zero = 0;
     if (c >= g.WW || y >= g.H) return;
     size_t wi = (size_t)y * g.WW + c;
     uint64_t w = fg[wi];
@@ -107,6 +109,7 @@ static int ccl_edge_cap(int nf) {
     const char *e = getenv("AOS_DEBUG_CCL_ECAP");
     return e ? std::max(2, atoi(e)) : std::max(4096, nf / 4);
 }
+constexpr int kCclBatch = 4;   // k_ccl_local: cells per thread whose neighbour lookups are in flight together
 __device__ __forceinline__ int lds_find(int *lp, int x) {
     for (int p; (p = __hip_atomic_load(&lp[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != x;) x = p;
     return x;
@@ -128,16 +131,46 @@ __global__ __launch_bounds__(1024) void k_ccl_local(const int *list, int n, cons
     for (int i = threadIdx.x; i < m; i += nt) lp[i] = i;
     __syncthreads();
     const int ndx[4] = {-1, 0, 1, -1}, ndy[4] = {-1, -1, -1, 0};
-    for (int i = threadIdx.x; i < m; i += nt) {
-        const int p = list[base + i], y = p / g.W, x = p - y * g.W;
-        for (int k = 0; k < 4; ++k) {
-            const int j = fg_index(fg, off, g, x + ndx[k], y + ndy[k]);   // (a raster predecessor: j < base + i)
-            if (j < 0) continue;
-            if (j >= base) {
-                lds_union(lp, i, j - base);
-            } else {
-                const int e = atomicAdd(n_edges, 1);
-                if (e < cap) edges[e] = make_int2(base + i, j);
+    // kCclBatch cells per thread at a time, their 4 x kCclBatch neighbour lookups issued together (the fg words,
+    // then the offsets of the set bits) before any union: round 4 walked each cell's lookups as a chain of
+    // dependent global load pairs between LDS unions, so the kernel waited on load latency cell after cell
+    constexpr int B = kCclBatch;
+    for (int i0 = threadIdx.x; i0 < m; i0 += B * nt) {
+        int wi[B][4], bit[B][4], jj[B][4];
+        uint64_t w[B][4];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            const int i = i0 + b * nt;
+            const int p = i < m ? list[base + i] : 0, y = p / g.W, x = p - y * g.W;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int nx = x + ndx[k], ny = y + ndy[k];   // (a raster predecessor: its index is < base + i)
+                const bool ok = i < m && nx >= 0 && ny >= 0 && nx < g.W;
+                wi[b][k] = ok ? ny * g.WW + (nx >> 6) : 0;
+                bit[b][k] = nx & 63;
+                w[b][k] = ok ? fg[wi[b][k]] : 0ull;
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < B; ++b)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint64_t v = w[b][k];
+                jj[b][k] = ((v >> bit[b][k]) & 1ull) ? off[wi[b][k]] + __popcll(v & ((1ull << bit[b][k]) - 1)) : -1;
+            }
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            const int i = i0 + b * nt;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int j = jj[b][k];
+                if (j < 0) continue;
+                if (j >= base) {
+                    lds_union(lp, i, j - base);
+                } else {
+                    const int e = atomicAdd(n_edges, 1);
+                    if (e < cap) edges[e] = make_int2(base + i, j);
+                }
             }
         }
     }
@@ -223,6 +256,7 @@ struct StatArgs {
     const double *poly; int np;
     float min_length;
     ClusterRec *rec;
+    ClusterRec *hrec;         // nullable: pinned host copy of rec, stored by the same threads
 };
 
 template <typename T, typename Op>
@@ -395,13 +429,16 @@ __global__ __launch_bounds__(512) void k_cluster_stats(StatArgs A) {   // (512 t
         }
     }
     r.flags = (row ? 1 : 0) | (needs_bfs ? 2 : 0);
-    if (threadIdx.x == 0) A.rec[cid] = r;
+    if (threadIdx.x == 0) {
+        A.rec[cid] = r;
+        if (A.hrec) A.hrec[cid] = r;
+    }
 }
 
 void launch_cluster_stats(const int *off, const int *cells, int n_clusters, const GridC &g, const double *poly, int np,
-                          float min_length, ClusterRec *rec, hipStream_t s) {
+                          float min_length, ClusterRec *rec, hipStream_t s, ClusterRec *hrec) {
     if (n_clusters <= 0) return;
-    StatArgs A{off, cells, nullptr, n_clusters, g, poly, np, min_length, rec};
+    StatArgs A{off, cells, nullptr, n_clusters, g, poly, np, min_length, rec, hrec};
     k_cluster_stats<<<n_clusters, 512, 0, s>>>(A);
     AOS_HIP(hipGetLastError());
 }
@@ -554,12 +591,21 @@ __global__ __launch_bounds__(64) void k_endpoint_rays(const RowDev *rows, int n_
 
 
 // /voronoi_seeds order (seed_gen:1670-1710): virtual, ray, endpoint seeds (counts on the device)
-__global__ void k_concat3(const double2 *a, const double2 *b, const double2 *c, const int *cnt, double2 *out) {
+// The seeds and their counts also go straight into pinned host memory (h_out, h_cnt[0..2], h_cnt[3] = the
+// de-duplications' error word): one launch and one host wait instead of a count read-back, a wait, a copy and a
+// second wait.
+__global__ void k_concat3(const double2 *a, const double2 *b, const double2 *c, const int *cnt, double2 *out, double2 *h_out,
+                          int *h_cnt, const int *err) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int na = cnt[0], nb = cnt[1], nc = cnt[2];
-    if (i < na) out[i] = a[i];
-    else if (i < na + nb) out[i] = b[i - na];
-    else if (i < na + nb + nc) out[i] = c[i - na - nb];
+    if (i == 0) { h_cnt[0] = na; h_cnt[1] = nb; h_cnt[2] = nc; h_cnt[3] = *err; }
+    double2 v;
+    if (i < na) v = a[i];
+    else if (i < na + nb) v = b[i - na];
+    else if (i < na + nb + nc) v = c[i - na - nb];
+    else return;
+    out[i] = v;
+    h_out[i] = v;
 }
 
 // ------------------------------------------------------------------ host orchestration
@@ -583,11 +629,10 @@ int ccl_label(CclScratch &B, const uint64_t *fg, const int *off, const GridC &g,
         return 0;
     }
     const dim3 gw2(cdiv(g.WW, 64), g.H);
-    k_fg_list<<<gw2, 64, 0, s>>>(fg, d_off, B.list_p, g, nullptr);
     const int ecap = ccl_edge_cap(nf);
     int *d_ne = dev<int>(B.edges, 2 + 2 * (size_t)ecap);
     int2 *d_edges = reinterpret_cast<int2 *>(d_ne + 2);
-    AOS_HIP(hipMemsetAsync(d_ne, 0, sizeof(int), s));
+    k_fg_list<<<gw2, 64, 0, s>>>(fg, d_off, B.list_p, g, nullptr, d_ne);
     const int chunk = ccl_chunk();
     k_ccl_local<<<cdiv(nf, chunk), ccl_tb(), sizeof(int) * chunk, s>>>(B.list_p, nf, fg, d_off, g, B.parent_p, d_edges, d_ne,
                                                                       ecap - 1, chunk);
@@ -605,13 +650,18 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
     const GridC g = make_gridc(fg);
     const Poly &poly = *in.poly;
     const int np = (int)poly.size();
+    const size_t pc0 = S.poly.cap;
     double *d_poly = dev<double>(S.poly, 2 * np);
     std::vector<double> hp(2 * np);
     for (int i = 0; i < np; ++i) { hp[2 * i] = poly[i].first; hp[2 * i + 1] = poly[i].second; }
-    // host -> device through pinned staging buffers (each written once per frame, after the last frame's sync)
-    double *h_up = static_cast<double *>(S.h_up_poly.ensure(sizeof(double) * 2 * np));
-    std::copy(hp.begin(), hp.end(), h_up);
-    copy_from_host(d_poly, h_up, sizeof(double) * 2 * np, s);
+    // host -> device through a pinned staging buffer, only when the polygon (or its buffer) changed
+    if (S.poly.cap != pc0 || hp != S.poly_up) {
+        double *h_up = static_cast<double *>(S.h_up_poly.ensure(sizeof(double) * 2 * np));
+        std::copy(hp.begin(), hp.end(), h_up);
+        S.poly_up.clear();   // (until the copy is queued)
+        copy_from_host(d_poly, h_up, sizeof(double) * 2 * np, s);
+        S.poly_up = hp;
+    }
     int *h_sc = static_cast<int *>(S.h_misc.ensure(4096));
 
     // ---- foreground list (raster order)
@@ -643,11 +693,10 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
     } else if (nf > 0) {
         int *d_list = dev<int>(S.fg_list, nf);
         int *d_par = dev<int>(S.parent, nf), *d_isroot = dev<int>(S.root_flag, nf), *d_rank = dev<int>(S.root_rank, nf + 1);
-        k_fg_list<<<gw2, 64, 0, s>>>(d_fg, d_wo, d_list, g, nullptr);
         const int ecap = ccl_edge_cap(nf);
         int *d_ne = dev<int>(S.ccl_edges, 2 + 2 * (size_t)ecap);
         int2 *d_edges = reinterpret_cast<int2 *>(d_ne + 2);   // (8-byte aligned: DevBuf bases are)
-        AOS_HIP(hipMemsetAsync(d_ne, 0, sizeof(int), s));
+        k_fg_list<<<gw2, 64, 0, s>>>(d_fg, d_wo, d_list, g, nullptr, d_ne);
         const int chunk = ccl_chunk();
         k_ccl_local<<<cdiv(nf, chunk), ccl_tb(), sizeof(int) * chunk, s>>>(d_list, nf, d_fg, d_wo, g, d_par, d_edges, d_ne,
                                                                           ecap - 1, chunk);
@@ -672,10 +721,9 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         S.cl_count_dirty = false;
         k_cluster_scatter<<<cdiv(nf, 256), 256, 0, s>>>(d_list, d_cid, d_crank, d_off, nf, d_cells);
         ClusterRec *d_rec = dev<ClusterRec>(S.rec, ncl);
-        launch_cluster_stats(d_off, d_cells, ncl, g, d_poly, np, static_cast<float>(in.cluster_min_length), d_rec, s);
         S.h_rec.resize(ncl);
         ClusterRec *hr = static_cast<ClusterRec *>(S.h_recbuf.ensure(sizeof(ClusterRec) * (size_t)ncl));
-        copy_to_host(hr, d_rec, sizeof(ClusterRec) * ncl, s);
+        launch_cluster_stats(d_off, d_cells, ncl, g, d_poly, np, static_cast<float>(in.cluster_min_length), d_rec, s, hr);
         if (ev_split) AOS_HIP(hipEventRecord(ev_split[1], s));   // (AOS_TRACE: the GPU part ends here)
         S.dedup.sev.sync(s);
         tr.mark("recs");
@@ -770,19 +818,14 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         greedy_dedup_async(scr, d_ecand, d_eok, 2 * nr, kConflictLess, 0.5, make_hash_n(hx0, hx1, hy0, hy1, 0.5, 2 * nr),
                            d_eout, nullptr, nullptr, d_cnt + 2, s);
     }
-    k_concat3<<<cdiv((long long)ncand, 256), 256, 0, s>>>(d_vout, d_rout, d_eout, d_cnt, d_seeds);
-    peek_to_host(h_sc, {d_cnt, d_cnt + 1, d_cnt + 2, dedup_err(scr, s)}, s);
+    double *hs = static_cast<double *>(S.h_seeds.ensure(sizeof(double2) * std::max<size_t>(ncand, 1)));
+    k_concat3<<<cdiv((long long)ncand, 256), 256, 0, s>>>(d_vout, d_rout, d_eout, d_cnt, d_seeds,
+                                                          reinterpret_cast<double2 *>(hs), h_sc, dedup_err(scr, s));
     S.dedup.sev.sync(s);
-    tr.mark("seedcnt");
+    tr.mark("seeds");
     dedup_check(scr, h_sc[3]);
     const int n_virtual = h_sc[0], n_ray = h_sc[1], n_end = h_sc[2];
     const int ntot = n_virtual + n_ray + n_end;
-    double *hs = static_cast<double *>(S.h_seeds.ensure(sizeof(double2) * (size_t)std::max(ntot, 1)));
-    if (ntot) {
-        copy_to_host(hs, d_seeds, sizeof(double2) * ntot, s);
-        S.dedup.sev.sync(s);
-        tr.mark("seeds");
-    }
     out.h_voronoi = hs;
     out.n_virtual = n_virtual; out.n_ray = n_ray; out.n_endpoint = n_end;
     out.d_voronoi = reinterpret_cast<const double *>(d_seeds);

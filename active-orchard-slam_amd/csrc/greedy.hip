@@ -184,6 +184,7 @@ __device__ __forceinline__ bool conflict(double2 a, double2 b, int mode, double 
 constexpr int kLfTB = 256, kLfList = 16;
 struct LfArgs {
     const double2 *p; const int *ok; int n; int mode; double thr;
+    int self_conflict;   // conflict(p, p) holds: an exact copy of an earlier candidate is removed at once (below)
     CellIdx ci;
     int *state; unsigned epoch;
     LookBack lb;
@@ -209,19 +210,28 @@ __global__ __launch_bounds__(kLfTB) void k_lfmis(LfArgs A) {
         } else {
             pi = A.p[i];
             hash_cell(A.ci.h, pi.x, pi.y, cx, cy);
-            for (int yy = max(cy - 1, 0); yy <= min(cy + 1, A.ci.h.ny - 1); ++yy) {
+            // An exact copy of an earlier candidate j is removed whatever j's fate (without OWNER): it conflicts
+            // with j and with everything j conflicts with, so either j is kept or an earlier kept candidate
+            // removed j and removes it too. The GVD's boundary points are facet polygon corners, each Voronoi
+            // vertex ~6 times: most candidates decide here without waiting for their predecessors.
+            bool dup = false;
+            for (int yy = max(cy - 1, 0); yy <= min(cy + 1, A.ci.h.ny - 1) && !dup; ++yy) {
                 int k0, k1;
                 ci_row(A.ci, yy, cx, k0, k1);
                 for (int k = k0; k < k1; ++k) {
                     const int j = A.ci.items[k];
-                    if (j < i && conflict(pi, A.p[j], A.mode, A.thr)) {
+                    if (j >= i) continue;
+                    const double2 pj = A.p[j];
+                    if (!OWNER && A.self_conflict && pj.x == pi.x && pj.y == pi.y) { dup = true; break; }
+                    if (conflict(pi, pj, A.mode, A.thr)) {
                         if (nl < kLfList) lst[nl * kLfTB + tid] = j;
                         else over = true;
                         ++nl;
                     }
                 }
             }
-            if (nl == 0) { s = 1; own = i; }
+            if (dup) s = 2;
+            else if (nl == 0) { s = 1; own = i; }
         }
         if (s) st_i32(&A.state[i], (int)(tag | (unsigned)s));
     }
@@ -391,7 +401,9 @@ void greedy_dedup_async(DedupScratch &S, const double2 *cand, const int *ok, int
         AOS_HIP(hipMemsetAsync(state, 0, S.state.cap, s));
     }
     const int blocks = cdiv(n, kLfTB);
-    LfArgs A{cand, ok, n, mode, thr, S.ci, state, S.epoch, S.lb.take(blocks, s), out, kept_index, owner, d_count, pos_of};
+    const bool self = mode == kConflictKeyOrSq || (mode == kConflictLessEq && thr >= 0.0) || (mode == kConflictLess && thr > 0.0);
+    LfArgs A{cand, ok, n, mode, thr, self ? 1 : 0, S.ci, state, S.epoch, S.lb.take(blocks, s), out, kept_index, owner, d_count,
+             pos_of};
     if (owner) k_lfmis<true><<<blocks, kLfTB, 0, s>>>(A);
     else k_lfmis<false><<<blocks, kLfTB, 0, s>>>(A);
     AOS_HIP(hipGetLastError());

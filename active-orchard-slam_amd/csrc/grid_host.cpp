@@ -94,6 +94,12 @@ void GridExpander::start(const Job &j) {
     cv_.notify_all();
 }
 
+void GridExpander::drain() {
+    std::unique_lock<std::mutex> l(mu_);
+    done_.wait(l, [&] { return !busy_; });
+    err_ = nullptr;
+}
+
 void GridExpander::join() {
     std::unique_lock<std::mutex> l(mu_);
     done_.wait(l, [&] { return !busy_; });

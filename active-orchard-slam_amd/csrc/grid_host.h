@@ -19,7 +19,7 @@ namespace aos {
 // row y = cell (x, y)); frame > 0: every cell within `frame` cells of the grid's edge is 100 (seed_gen:708-757).
 void expand_grid_rows(const uint64_t *bits, int WW, int W, int H, int frame, int y0, int y1, int8_t *out);
 // markPolygonBoundaryAsOccupied's rectangle (seed_gen:772-870): rows gy0, gy1 over [min x, max x] and columns
-// gx0, gx1 over [min y, max y] set to 100 (the device kernel k_draw_rect, grid_kernels.hip)
+// gx0, gx1 over [min y, max y] set to 100 (on the device: grid_extra, grid_kernels.hip)
 void draw_rect_host(int8_t *grid, int W, int H, int gx0, int gy0, int gx1, int gy1);
 
 // One background job per frame: wait for the bits' D2H (wait()), expand both grids on `threads` host threads,
@@ -40,6 +40,7 @@ class GridExpander {
     ~GridExpander();
     void start(const Job &j);
     void join();
+    void drain();   // waits for a running job without its error (that job's frame has failed already)
     bool busy() const { return busy_; }
 
   private:

@@ -81,11 +81,52 @@ __device__ __forceinline__ uint64_t pad_mask(int c, int WW, int W) {
 }
 
 // ------------------------------------------------------------------------------------------
+// Bits -> int8 {0, 100} bytes, one 64-cell word per thread: 64 bytes as four 16-byte stores when rows are
+// 16-byte aligned (W % 16 == 0), so a wave writes 4 KB in one run (round 4's byte-per-thread kernel, with
+// a 64-bit division per cell, ran at ~0.6 TB/s: 29 us per C2 grid).
+__device__ __forceinline__ unsigned nib_bytes(unsigned b) {   // 4 bits -> 4 bytes of {0, 100}
+    return ((b & 1u) ? 100u : 0u) | ((b & 2u) ? 100u << 8 : 0u) | ((b & 4u) ? 100u << 16 : 0u) | ((b & 8u) ? 100u << 24 : 0u);
+}
+__device__ __forceinline__ void store_word_bytes(int8_t *o, uint64_t v, int nb, bool vec) {
+    if (vec && nb == 64) {
+        uint4 *q = reinterpret_cast<uint4 *>(o);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const unsigned h = (unsigned)(v >> (16 * k));
+            q[k] = make_uint4(nib_bytes(h & 15u), nib_bytes((h >> 4) & 15u), nib_bytes((h >> 8) & 15u), nib_bytes((h >> 12) & 15u));
+        }
+    } else {
+        for (int b = 0; b < nb; ++b) o[b] = ((v >> b) & 1ull) ? 100 : 0;
+    }
+}
+// the cells [lo, hi] of the word that starts at cell x0, as bits
+__device__ __forceinline__ uint64_t run_bits(int lo, int hi, int x0) {
+    const int a = max(lo - x0, 0), b = min(hi - x0, 63);
+    if (a > b) return 0ull;
+    return (b - a == 63 ? ~0ull : ((1ull << (b - a + 1)) - 1)) << a;
+}
+// The cells a published grid adds to its bits in word (x0, y): the `frame`-cell border of /occupancy_grid
+// (markBoundariesAsOccupied, seed_gen:708-757) and the polygon rectangle of /skeletonized_occupancy_grid
+// (markPolygonBoundaryAsOccupied, seed_gen:772-870: rows gy0 / gy1 over [xlo, xhi], columns gx0 / gx1 over
+// [ylo, yhi]; r.gx0 < 0: none)
+__device__ __forceinline__ uint64_t grid_extra(int x0, int y, int W, int H, int frame, const ByteRect &r) {
+    uint64_t m = 0;
+    if (frame > 0) m = (y < frame || y >= H - frame) ? ~0ull : (run_bits(0, frame - 1, x0) | run_bits(W - frame, W - 1, x0));
+    if (r.gx0 >= 0) {
+        const int xlo = min(r.gx0, r.gx1), xhi = max(r.gx0, r.gx1), ylo = min(r.gy0, r.gy1), yhi = max(r.gy0, r.gy1);
+        if (y == r.gy0 || y == r.gy1) m |= run_bits(xlo, xhi, x0);
+        if (y >= ylo && y <= yhi) m |= run_bits(r.gx0, r.gx0, x0) | run_bits(r.gx1, r.gx1, x0);
+    }
+    return m;
+}
+
 // a5 applyInflation (seed_gen:933-967): cell = 100 iff an occupied raster cell lies within the
 // integer disc dx^2 + dy^2 <= R^2 — an exact bounded squared-EDT threshold, computed as an OR
 // of horizontally dilated rows: row y+dy dilated by w(dy) = floor(sqrt(R^2 - dy^2)).
 struct InflTab { int w[64]; };   // w(dy), passed by value: concurrent handles share no device global
-__global__ void k_inflate(const uint64_t *in, uint64_t *out, int W, int H, int WW, int R, InflTab wt) {
+// (bytes != nullptr: also /occupancy_grid's bytes with the `frame` border, from the word in registers)
+__global__ void k_inflate(const uint64_t *in, uint64_t *out, int W, int H, int WW, int R, InflTab wt, int8_t *bytes,
+                          int frame) {
     int c = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
     if (c >= WW || y >= H) return;
     uint64_t acc = 0;
@@ -101,9 +142,13 @@ __global__ void k_inflate(const uint64_t *in, uint64_t *out, int W, int H, int W
         for (int s = 1; s <= w; ++s) h |= (b >> s) | (d << (64 - s)) | (b << s) | (a >> (64 - s));
         acc |= h;
     }
-    out[(size_t)y * WW + c] = acc & pad_mask(c, WW, W);
+    acc &= pad_mask(c, WW, W);
+    out[(size_t)y * WW + c] = acc;
+    if (bytes)
+        store_word_bytes(bytes + (size_t)y * W + 64 * c, acc | grid_extra(64 * c, y, W, H, frame, ByteRect{-1, 0, 0, 0}),
+                         min(64, W - 64 * c), (W & 15) == 0);
 }
-void launch_inflate(const uint64_t *in, uint64_t *out, const FrameGeom &g, hipStream_t s) {
+void launch_inflate(const uint64_t *in, uint64_t *out, const FrameGeom &g, hipStream_t s, int8_t *bytes, int frame) {
     InflTab wt{};
     for (int dy = 0; dy <= g.R && dy < 64; ++dy) {
         int w = 0;
@@ -111,21 +156,21 @@ void launch_inflate(const uint64_t *in, uint64_t *out, const FrameGeom &g, hipSt
         wt.w[dy] = w;
     }
     dim3 grid(cdiv(g.WW, 64), g.H);
-    k_inflate<<<grid, 64, 0, s>>>(in, out, g.W, g.H, g.WW, g.R, wt);
+    k_inflate<<<grid, 64, 0, s>>>(in, out, g.W, g.H, g.WW, g.R, wt, bytes, frame);
 }
 
-// bits -> int8 {0,100} with an optional `frame`-cell border (markBoundariesAsOccupied, seed_gen:708-757)
-__global__ void k_bits_to_bytes(const uint64_t *bits, int8_t *out, int W, int H, int WW, int frame) {
-    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (size_t)W * H) return;
-    int y = (int)(i / W), x = (int)(i - (size_t)y * W);
-    bool v = (bits[(size_t)y * WW + (x >> 6)] >> (x & 63)) & 1ull;
-    if (frame > 0 && (x < frame || y < frame || x >= W - frame || y >= H - frame)) v = true;
-    out[i] = v ? 100 : 0;
+// bits -> int8 {0,100} with the optional frame border and rectangle (grid_extra)
+__global__ void k_bits_to_bytes(const uint64_t *bits, int8_t *out, int W, int H, int WW, int frame, ByteRect r) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    if (c >= WW || y >= H) return;
+    const uint64_t v = bits[(size_t)y * WW + c] | grid_extra(64 * c, y, W, H, frame, r);
+    store_word_bytes(out + (size_t)y * W + 64 * c, v, min(64, W - 64 * c), (W & 15) == 0);
 }
-void launch_bits_to_bytes(const uint64_t *bits, int8_t *out, const FrameGeom &g, int frame, hipStream_t s) {
-    size_t n = (size_t)g.W * g.H;
-    k_bits_to_bytes<<<cdiv(n, 256), 256, 0, s>>>(bits, out, g.W, g.H, g.WW, frame);
+void launch_bits_to_bytes(const uint64_t *bits, int8_t *out, const FrameGeom &g, int frame, hipStream_t s, const int *rect) {
+    if (reinterpret_cast<uintptr_t>(out) & 15) throw std::logic_error("launch_bits_to_bytes: output not 16-byte aligned");
+    const ByteRect r = rect ? ByteRect{rect[0], rect[1], rect[2], rect[3]} : ByteRect{-1, 0, 0, 0};
+    dim3 grid(cdiv(g.WW, 64), g.H);
+    k_bits_to_bytes<<<grid, 64, 0, s>>>(bits, out, g.W, g.H, g.WW, frame, r);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -142,17 +187,20 @@ __device__ __forceinline__ uint64_t erode_at(const uint64_t *in, int r, int k, i
     uint64_t ev = (c >> 1) | (ld_er(in, r, k + 1, H, WW, W) << 63);
     return (c & wv & ev & ld_er(in, r - 1, k, H, WW, W) & ld_er(in, r + 1, k, H, WW, W)) & pad_mask(k, WW, W);
 }
-__global__ void k_open(const uint64_t *in, uint64_t *out, int W, int H, int WW) {
+// (zero != nullptr: the thinning flags zero[0, nzero) are cleared by the blocks of row 0: no fill launch)
+__global__ void k_open(const uint64_t *in, uint64_t *out, int W, int H, int WW, int *zero, int nzero) {
     int k = blockIdx.x * blockDim.x + threadIdx.x, r = blockIdx.y;
+    if (zero && r == 0)
+        for (int i = k; i < nzero; i += gridDim.x * blockDim.x) zero[i] = 0;
     if (k >= WW || r >= H) return;
     uint64_t e = erode_at(in, r, k, H, WW, W);
     uint64_t d = e | erode_at(in, r - 1, k, H, WW, W) | erode_at(in, r + 1, k, H, WW, W) |
                  (e << 1) | (erode_at(in, r, k - 1, H, WW, W) >> 63) | (e >> 1) | (erode_at(in, r, k + 1, H, WW, W) << 63);
     out[(size_t)r * WW + k] = d & pad_mask(k, WW, W);
 }
-void launch_open(const uint64_t *in, uint64_t *out, const FrameGeom &g, hipStream_t s) {
+void launch_open(const uint64_t *in, uint64_t *out, const FrameGeom &g, hipStream_t s, int *zero, int nzero) {
     dim3 grid(cdiv(g.WW, 64), g.H);
-    k_open<<<grid, 64, 0, s>>>(in, out, g.W, g.H, g.WW);
+    k_open<<<grid, 64, 0, s>>>(in, out, g.W, g.H, g.WW, zero, nzero);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -324,9 +372,13 @@ void launch_zero_ints(int *p, int n, hipStream_t s) {
 
 // The thinning result without a host round trip: the last launch that ran (launch j runs iff j == 0 or
 // iteration j*K-1 deleted something) wrote bufs[last & 1]; it is copied into out for the later stages.
+// (h_flags != nullptr: block 0 also stores the first nh flags into that pinned host buffer, the frame's
+// convergence check: no copy-engine read-back)
 __global__ void k_thin_pick(const int *flags, int launched, int K, const uint64_t *b0, const uint64_t *b1, uint64_t *out,
-                            size_t n) {
+                            size_t n, int *h_flags, int nh) {
     __shared__ int last_s;
+    if (h_flags && blockIdx.x == 0)
+        for (int i = threadIdx.x; i < nh; i += blockDim.x) h_flags[i] = flags[i];
     if (threadIdx.x == 0) {
         int last = 0;
         for (int j = 1; j < launched; ++j) {
@@ -340,8 +392,8 @@ __global__ void k_thin_pick(const int *flags, int launched, int K, const uint64_
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) out[i] = src[i];
 }
 void launch_thin_pick(const int *flags, int launched, const uint64_t *b0, const uint64_t *b1, uint64_t *out, size_t n,
-                      hipStream_t s) {
-    k_thin_pick<<<512, 256, 0, s>>>(flags, launched, KIT, b0, b1, out, n);
+                      hipStream_t s, int *h_flags, int nh) {
+    k_thin_pick<<<512, 256, 0, s>>>(flags, launched, KIT, b0, b1, out, n, h_flags, nh);
     AOS_HIP(hipGetLastError());
 }
 
@@ -350,26 +402,6 @@ void launch_thin_block(const uint64_t *in, uint64_t *out, const FrameGeom &g, in
     static_assert(2 * KIT <= HR && 2 * KIT <= TH && 2 * KIT <= 64 * TWW, "the copy-through rule needs a tile >= 2 KIT cells");
     dim3 grid(cdiv(g.WW, TWW), cdiv(g.H, TH));
     k_thin_block<<<grid, kThinTB, 0, s>>>(in, out, g.W, g.H, g.WW, base_iter, flags, own);
-}
-
-// a16 markPolygonBoundaryAsOccupied (seed_gen:772-825): the bbox +- 2.5 m rectangle in grid cells;
-// drawLineInGrid (Bresenham, :828-870) of an axis-aligned segment is the straight run of cells.
-__global__ void k_draw_rect(int8_t *grid, int W, int H, int gx0, int gy0, int gx1, int gy1) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    int xlo = min(gx0, gx1), xhi = max(gx0, gx1), ylo = min(gy0, gy1), yhi = max(gy0, gy1);
-    int nx = xhi - xlo + 1, ny = yhi - ylo + 1;
-    if (i < nx) {
-        grid[(size_t)gy0 * W + xlo + i] = 100;
-        grid[(size_t)gy1 * W + xlo + i] = 100;
-    } else if (i < nx + ny) {
-        int j = i - nx;
-        grid[(size_t)(ylo + j) * W + gx0] = 100;
-        grid[(size_t)(ylo + j) * W + gx1] = 100;
-    }
-}
-void launch_draw_rect(int8_t *grid, const FrameGeom &g, int gx0, int gy0, int gx1, int gy1, hipStream_t s) {
-    int n = abs(gx1 - gx0) + abs(gy1 - gy0) + 2;
-    k_draw_rect<<<cdiv(n, 256), 256, 0, s>>>(grid, g.W, g.H, gx0, gy0, gx1, gy1);
 }
 
 }  // namespace aos

@@ -50,9 +50,12 @@ __device__ __forceinline__ bool occ_trunc(const int8_t *sk, const GridG &g, doub
 // merged seed r = the mean of its leader's members (owner == leader, the leader first), summed in index
 // order as voronoiSeedsCallback does (gvd:116-123). Members conflict with the leader (<= 0.5 m), so they
 // sit in its 3 x 3 cells of the de-duplication's index: taken in increasing index, one pass each.
+// (h_merged / h_sc: pinned host copies of the means, and of the count and the merge's error word (h_sc[0], [1]),
+// stored by the same launch: no copy-engine read-backs)
 __global__ void k_merge_members(const double2 *raw, CellIdx ci, const int *owner, const int *leaders, const int *count,
-                                double2 *merged) {
+                                double2 *merged, double2 *h_merged, int *h_sc, const int *err) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r == 0) { h_sc[0] = *count; h_sc[1] = *err; }
     if (r >= *count) return;
     const int L = leaders[r];
     const double2 pl = raw[L];
@@ -76,7 +79,7 @@ __global__ void k_merge_members(const double2 *raw, CellIdx ci, const int *owner
         ++cnt;
         cur = nxt;
     }
-    merged[r] = make_double2(sx / (double)cnt, sy / (double)cnt);
+    merged[r] = h_merged[r] = make_double2(sx / (double)cnt, sy / (double)cnt);
 }
 
 // ------------------------------------------------------------------ g5/g6 helpers
@@ -180,55 +183,100 @@ __global__ void k_pairs(const double2 *bp, int no, const int *M_dev, CellIdx ci,
 // cannot touch the grid are skipped (they read no cell), which keeps far hull edges cheap. A passing
 // occurrence (a != b, both valid, no occupied sample) is counted in the group of its smaller node
 // (grank: its rank there) for the first-occurrence selection.
-__global__ void k_occupancy(const int2 *ft, const int *poff, int no, int ne, int cap, const double2 *bp, const int8_t *sk,
-                            GridG g, int *pass, int *gcnt, int *grank, unsigned long long *evals) {
-    int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= ne + min(poff[no], cap)) return;
-    const int2 e2 = ft[c];
-    if (!(e2.x >= 0 && e2.y >= 0 && e2.x != e2.y)) { pass[c] = 0; return; }
-    const double2 s = bp[e2.x], e = bp[e2.y];
-    double ex = e.x - s.x, ey = e.y - s.y;
-    double len = sqrt(ex * ex + ey * ey);
-    bool hit = false;
-    if (len >= 1e-6) {
-        const double step = g.res * 0.5;
-        double q = len / step;
-        int num = (q > -2147483649.0 && q < 2147483647.0) ? (int)q + 1 : INT_MIN + 1;  // x86 int conversion
-        double dx = ex / len, dy = ey / len;
-        // candidate sample window: cells exist only for world x in (ox - res, ox + W res), same for y
-        int i0 = 0, i1 = num;
-        if (num > 64) {
-            double lo_t = 0.0, hi_t = 1.0;
-            const double gx0 = g.ox - 2 * g.res, gx1 = g.ox + (g.W + 2) * g.res;
-            const double gy0 = g.oy - 2 * g.res, gy1 = g.oy + (g.H + 2) * g.res;
-            auto clip = [&](double p0, double dp, double a, double b) {
-                if (dp == 0.0) { if (p0 < a || p0 > b) { lo_t = 1.0; hi_t = 0.0; } return; }
-                double t0 = (a - p0) / dp, t1 = (b - p0) / dp;
-                if (t0 > t1) { double t = t0; t0 = t1; t1 = t; }
-                lo_t = fmax(lo_t, t0); hi_t = fmin(hi_t, t1);
-            };
-            clip(s.x, ex, gx0, gx1);
-            clip(s.y, ey, gy0, gy1);
-            if (lo_t > hi_t) { i0 = 1; i1 = 0; }
-            else { i0 = max(0, (int)floor(lo_t * num) - 2); i1 = min(num, (int)ceil(hi_t * num) + 2); }
-        }
-        for (int ib = i0; ib <= i1 && num >= 0 && !hit; ib += 16) {   // 16 independent samples in flight
-            if (evals) eval_add(evals, 2, min(16, i1 - ib + 1));
-            bool h16[16];
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const int i = ib + j;
-                h16[j] = false;
-                if (i <= i1) {
-                    double t = (i == num) ? 1.0 : ((double)i / (double)num);
-                    double px = s.x + (t * dx) * len, py = s.y + (t * dy) * len;
-                    h16[j] = occ_trunc(sk, g, px, py);
-                }
+// Round 5: the samples of a block's occurrences are flattened and spread over all of its threads (an
+// exclusive scan of the per-occurrence sample counts in LDS; a sample finds its occurrence by binary search),
+// kOccPer independent lookups per thread per round, and a sample of an occurrence already hit is skipped.
+// Round 4 walked each occurrence's samples on one lane, 16 per round: a wave waited for its longest edge (a
+// passing edge between two tree rows: every sample read), ~90 us per C2 frame. The hit test is an OR over
+// the samples, so the order they are read in never shows.
+constexpr int kOccTB = 256, kOccPer = 8;
+__global__ __launch_bounds__(kOccTB) void k_occupancy(const int2 *ft, const int *poff, int no, int ne, int cap,
+                                                      const double2 *bp, const int8_t *sk, GridG g, int *pass, int *gcnt,
+                                                      int *grank, unsigned long long *evals) {
+    __shared__ int pre[kOccTB + 1], hit_s[kOccTB], wsum[kOccTB / 64], tot_s;
+    __shared__ double sx_s[kOccTB], sy_s[kOccTB], ux_s[kOccTB], uy_s[kOccTB], len_s[kOccTB];
+    __shared__ int num_s[kOccTB], i0_s[kOccTB];
+    const int tid = threadIdx.x, c = blockIdx.x * kOccTB + tid;
+    const int nocc = ne + min(poff[no], cap);
+    int2 e2 = make_int2(-1, -1);
+    bool valid = false;
+    int nsamp = 0;
+    if (c < nocc) {
+        e2 = ft[c];
+        valid = e2.x >= 0 && e2.y >= 0 && e2.x != e2.y;
+    }
+    if (valid) {
+        const double2 s = bp[e2.x], e = bp[e2.y];
+        double ex = e.x - s.x, ey = e.y - s.y;
+        double len = sqrt(ex * ex + ey * ey);
+        if (len >= 1e-6) {
+            const double step = g.res * 0.5;
+            double q = len / step;
+            int num = (q > -2147483649.0 && q < 2147483647.0) ? (int)q + 1 : INT_MIN + 1;  // x86 int conversion
+            // candidate sample window: cells exist only for world x in (ox - res, ox + W res), same for y
+            int i0 = 0, i1 = num;
+            if (num > 64) {
+                double lo_t = 0.0, hi_t = 1.0;
+                const double gx0 = g.ox - 2 * g.res, gx1 = g.ox + (g.W + 2) * g.res;
+                const double gy0 = g.oy - 2 * g.res, gy1 = g.oy + (g.H + 2) * g.res;
+                auto clip = [&](double p0, double dp, double a, double b) {
+                    if (dp == 0.0) { if (p0 < a || p0 > b) { lo_t = 1.0; hi_t = 0.0; } return; }
+                    double t0 = (a - p0) / dp, t1 = (b - p0) / dp;
+                    if (t0 > t1) { double t = t0; t0 = t1; t1 = t; }
+                    lo_t = fmax(lo_t, t0); hi_t = fmin(hi_t, t1);
+                };
+                clip(s.x, ex, gx0, gx1);
+                clip(s.y, ey, gy0, gy1);
+                if (lo_t > hi_t) { i0 = 1; i1 = 0; }
+                else { i0 = max(0, (int)floor(lo_t * num) - 2); i1 = min(num, (int)ceil(hi_t * num) + 2); }
             }
-#pragma unroll
-            for (int j = 0; j < 16; ++j) hit |= h16[j];
+            if (num >= 0 && i1 >= i0) nsamp = i1 - i0 + 1;
+            sx_s[tid] = s.x; sy_s[tid] = s.y; ux_s[tid] = ex / len; uy_s[tid] = ey / len; len_s[tid] = len;
+            num_s[tid] = num; i0_s[tid] = i0;
         }
     }
+    hit_s[tid] = 0;
+    const int before = block_excl_scan<kOccTB>(nsamp, wsum, &tot_s);   // (synchronises)
+    pre[tid] = before;
+    if (tid == 0) pre[kOccTB] = tot_s;
+    __syncthreads();
+    const int T = pre[kOccTB];
+    long long nread = 0;
+    for (int q0 = 0; q0 < T; q0 += kOccTB * kOccPer) {
+        bool h[kOccPer];
+        int oo[kOccPer];
+#pragma unroll
+        for (int u = 0; u < kOccPer; ++u) {
+            const int q = q0 + u * kOccTB + tid;
+            h[u] = false;
+            oo[u] = -1;
+            if (q >= T) continue;
+            int lo = 0, hi = kOccTB - 1;   // the occurrence o with pre[o] <= q < pre[o + 1]
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (pre[mid] <= q) lo = mid; else hi = mid - 1;
+            }
+            if (hit_s[lo]) continue;
+            oo[u] = lo;
+            const int i = i0_s[lo] + (q - pre[lo]), num = num_s[lo];
+            const double t = (i == num) ? 1.0 : ((double)i / (double)num);
+            const double len = len_s[lo];
+            const double px = sx_s[lo] + (t * ux_s[lo]) * len, py = sy_s[lo] + (t * uy_s[lo]) * len;
+            h[u] = occ_trunc(sk, g, px, py);
+            ++nread;
+        }
+#pragma unroll
+        for (int u = 0; u < kOccPer; ++u)
+            if (h[u]) hit_s[oo[u]] = 1;
+        __syncthreads();
+    }
+    if (evals) {
+        for (int o = 32; o > 0; o >>= 1) nread += __shfl_xor(nread, o);
+        if ((tid & 63) == 0) eval_add(evals, 2, nread);
+    }
+    if (c >= nocc) return;
+    if (!valid) { pass[c] = 0; return; }
+    const bool hit = hit_s[tid] != 0;
     pass[c] = hit ? 0 : 1;
     if (!hit) grank[c] = atomicAdd(&gcnt[min(e2.x, e2.y)], 1);
 }
@@ -511,15 +559,9 @@ __global__ void k_node_labels_fill(const double2 *nodes, int Mn, const double2 *
     (void)node_labels_of(i, nodes, lp, lv, n_rows, cq, m, ci, off, lcl, lty);
 }
 
-// the device scalars the host needs, gathered for one read-back
-struct Peek { const int *src[8]; int n; };
-__global__ void k_peek(Peek P, int *dst) {
-    if (threadIdx.x < P.n) dst[threadIdx.x] = *P.src[threadIdx.x];
-}
-
 // ------------------------------------------------------------------ output gather
-// The GvdGraph arrays (4-byte words) packed back to back into one device buffer, so the host receives them
-// with one DMA instead of one copy per array.
+// The GvdGraph arrays (4-byte words) packed back to back into the state's pinned host buffer by one launch (no
+// device staging buffer and no copy-engine read-back).
 constexpr int kMaxSegs = 12;
 struct SegList { const int *src[kMaxSegs]; long long off[kMaxSegs + 1]; int n; };
 __global__ void k_gather_words(SegList L, int *dst) {
@@ -641,7 +683,7 @@ struct GvdScratch {
     DevBuf raw, ok, leaders, merged, owner, oidx, sowner, sidx, tmp, edges_f, occ, occ_ok, bp, kept_occ, keys, idx, skeys,
         sidx2, near_idx, pk, pidx, pskeys, psidx, pcount, poff, plist, ft, ckey, cvalid, pass, k2, occ_idx, sk2, socc, selected,
         inside, ipos, nodes, keep, kpos, edges, lens, jobs, nkeys, nidx, qkeys, qidx, lpts, lval, lmask, lcidx, lcount, loff, lcl, lty, scan_tmp,
-        gather, misc, gcnt, goff, glist, evals;
+        misc, gcnt, goff, glist, evals;
     bool gcnt_dirty = true;           // gcnt (edge groups' counts) not known to be zero
     CellScratch ci_nodes, ci_labels;  // g8 / g9 indices (g5 / g6 use the de-duplication's own)
     CellIdx cq{};
@@ -691,8 +733,7 @@ static int facets_count(FacetBufs &F, const Subdiv2D &sd, Subdiv2D::Raw &R, int 
         k_facet_count<<<blocks, 256, 0, s>>>(F.qe, F.vf, F.vt, R.n_vtx, d_cnt, d_off, d_off + R.n_vtx + 1,
                                              F.lb.take(blocks, s));
     }
-    AOS_HIP(hipMemcpyAsync(h_sc, d_off + R.n_vtx, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
-    AOS_HIP(hipMemcpyAsync(h_sc + 2, F.lb.err_word(s), sizeof(int), hipMemcpyDeviceToHost, s));
+    peek_to_host(h_sc, {d_off + R.n_vtx, d_off + R.n_vtx + 1, F.lb.err_word(s)}, s);
     sev.sync(s);
     if (h_sc[1]) throw std::runtime_error("Subdiv2D facet walk did not close");
     if (h_sc[2]) throw std::runtime_error("Subdiv2D facets: single-pass scan failed on the device");
@@ -933,11 +974,9 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     int *d_cnt = dev<int>(S.misc, 8);
     // leaders (the kept seeds) -> d_merged, overwritten in leader order by their means
     greedy_dedup_async(G.dedup, d_raw, nullptr, n, kConflictLessEq, 0.5, hm, d_merged, d_leaders, d_owner, d_cnt, s);
-    k_merge_members<<<cdiv(n, 128), 128, 0, s>>>(d_raw, G.dedup.ci, d_owner, d_leaders, d_cnt, d_merged);
-    // (the whole buffer comes back with the count: one host wait)
-    AOS_HIP(hipMemcpyAsync(h_seeds, d_merged, sizeof(double2) * n, hipMemcpyDeviceToHost, s));
-    AOS_HIP(hipMemcpyAsync(h_sc, d_cnt, sizeof(int), hipMemcpyDeviceToHost, s));
-    AOS_HIP(hipMemcpyAsync(h_sc + 1, dedup_err(G.dedup, s), sizeof(int), hipMemcpyDeviceToHost, s));
+    // (the means and the count come back from the same launch: one host wait)
+    k_merge_members<<<cdiv(n, 128), 128, 0, s>>>(d_raw, G.dedup.ci, d_owner, d_leaders, d_cnt, d_merged,
+                                                 reinterpret_cast<double2 *>(h_seeds), h_sc, dedup_err(G.dedup, s));
     G.sev.sync(s);
     dedup_check(G.dedup, h_sc[1]);
     tr.mark("merge");
@@ -1060,7 +1099,7 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
         if (S.gcnt.cap != gc0 || S.gcnt_dirty) AOS_HIP(hipMemsetAsync(d_gcnt, 0, S.gcnt.cap, s));
         S.gcnt_dirty = true;
         int *d_goff = dev<int>(S.goff, no + 1), *d_glist = dev<int>(S.glist, ncap);
-        k_occupancy<<<cdiv(ncap, 64), 64, 0, s>>>(d_ft, d_poff, no, ne, cap, d_bp, in.d_skeleton, g, d_pass, d_gcnt, d_grank,
+        k_occupancy<<<cdiv(ncap, kOccTB), kOccTB, 0, s>>>(d_ft, d_poff, no, ne, cap, d_bp, in.d_skeleton, g, d_pass, d_gcnt, d_grank,
                                                   ev_k);
         scan_1p(S.lb, d_gcnt, d_goff, no, true, s);   // (leaves the group counts zero)
         S.gcnt_dirty = false;
@@ -1090,10 +1129,8 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
         k_node_labels_count<<<cdiv(no, 256), 256, 0, s>>>(d_nodes, no, d_Mn, d_lp, d_lv, nrows, cq, d_mask, d_cidx, d_lcnt);
         scan_1p(S.lb, d_lcnt, d_loff, no, false, s);
         // the frame's sizes and error words: one read-back
-        Peek pk{{d_M, d_poff + no, d_Mn, d_kpos + ncap, d_loff + no, dedup_err(G.dedup, s), S.lb.err_word(s),
-                 S.ci_nodes.lb.err_word(s)}, 8};
-        k_peek<<<1, 64, 0, s>>>(pk, d_sc + 8);
-        AOS_HIP(hipMemcpyAsync(h_sz, d_sc + 8, 8 * sizeof(int), hipMemcpyDeviceToHost, s));
+        peek_to_host(h_sz, {d_M, d_poff + no, d_Mn, d_kpos + ncap, d_loff + no, dedup_err(G.dedup, s), S.lb.err_word(s),
+                            S.ci_nodes.lb.err_word(s)}, s);
         G.sev.sync(s);
         if (h_sz[5] || h_sz[6] || h_sz[7]) {
             if (h_sz[6] || h_sz[7]) throw std::runtime_error("GVD graph: single-pass scan failed on the device");
@@ -1136,11 +1173,7 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     }
     const long long total = sl.off[sl.n];
     int *h_out = static_cast<int *>(G.h_out.ensure(sizeof(int) * (size_t)std::max(total, 1LL)));
-    if (total) {
-        int *d_g = dev<int>(S.gather, (size_t)total);
-        k_gather_words<<<cdiv(total, 256), 256, 0, s>>>(sl, d_g);
-        AOS_HIP(hipMemcpyAsync(h_out, d_g, sizeof(int) * (size_t)total, hipMemcpyDeviceToHost, s));
-    }
+    if (total) k_gather_words<<<cdiv(total, 256), 256, 0, s>>>(sl, h_out);   // (straight into the pinned buffer)
     unsigned long long *h_ev = d_evals ? static_cast<unsigned long long *>(G.h_evals.ensure(8 * sizeof(unsigned long long))) : nullptr;
     if (d_evals) AOS_HIP(hipMemcpyAsync(h_ev, d_evals, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     AOS_HIP(hipEventRecord(ev[9], s));

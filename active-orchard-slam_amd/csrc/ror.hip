@@ -163,12 +163,18 @@ __device__ __forceinline__ int rt_xcd_block(int b, int n) {
 
 template <bool SCATTER, int LAY, int kRtTB, int kRtPer>
 __global__ __launch_bounds__(kRtTB) void k_rt_part(RorLaunch L, int *H, const int *tstart, uint64_t chunk,
-                                                   float4 *staged, unsigned *own_out) {
+                                                   float4 *staged, unsigned *own_out, RtClear clr) {
     constexpr int kRtSub = kRtTB * kRtPer;
     extern __shared__ int hist[];        // [ntiles]: counts (count pass) / cursors (scatter pass)
     // chunk w: the chunks of one XCD are contiguous, so the scatter runs of chunks w and w + 1 (adjacent in
     // every tile's range) are written through the same L2 and their shared lines merge there
     const int tid = threadIdx.x, w = rt_xcd_block(blockIdx.x, gridDim.x);
+    if (!SCATTER) {   // the stage's zeroed outputs (raster bits, counters, kept counts): no fill launches
+        const size_t stride = (size_t)gridDim.x * kRtTB, i0 = (size_t)blockIdx.x * kRtTB + tid;
+        for (size_t i = i0; i < clr.nw; i += stride) clr.w[i] = 0ull;
+        for (size_t i = i0; i < (size_t)clr.nc; i += stride) clr.c[i] = 0ull;
+        for (size_t i = i0; i < (size_t)clr.nk; i += stride) clr.k[i] = 0;
+    }
     int *row = H + (size_t)w * L.ntiles;
     for (int t = tid; t < L.ntiles; t += kRtTB) hist[t] = SCATTER ? tstart[t] + row[t] : 0;
     __syncthreads();
@@ -1044,7 +1050,7 @@ uint64_t rt_chunk(const RorLaunch &L, int G) {
 
 template <bool SCATTER, int LAY>
 static void rt_part(const RorLaunch &L, int *H, const int *tstart, int G, float4 *staged, unsigned *own_out,
-                    hipStream_t s) {
+                    hipStream_t s, const RtClear &clr = RtClear{}) {
     constexpr int TB = SCATTER ? kRtScatterTB : kRtCountTB, PER = SCATTER ? kRtScatterPer : kRtCountPer;
     static_assert(kRtChunkQ % (TB * PER) == 0 || (TB * PER) % kRtChunkQ == 0, "chunk granularity");
     const size_t lds = sizeof(int) * (size_t)L.ntiles;
@@ -1054,7 +1060,7 @@ static void rt_part(const RorLaunch &L, int *H, const int *tstart, int G, float4
     if (lds > 64 * 1024)   // the tile histogram exceeds the default dynamic-LDS limit (gfx950: 160 KB)
         AOS_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rt_part<SCATTER, LAY, TB, PER>),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    k_rt_part<SCATTER, LAY, TB, PER><<<G, TB, lds, s>>>(L, H, tstart, rt_chunk(L, G), staged, own_out);
+    k_rt_part<SCATTER, LAY, TB, PER><<<G, TB, lds, s>>>(L, H, tstart, rt_chunk(L, G), staged, own_out, clr);
     AOS_HIP(hipGetLastError());
 }
 static int rt_layout(const RorLaunch &L) {
@@ -1068,13 +1074,13 @@ int rt_colscan_words(const RorLaunch &L, int G) {
 }
 
 void launch_rt_count(const RorLaunch &L, int *H, int G, int *ts, unsigned long long *n_own, const LookBack &lb,
-                     hipStream_t s) {
-    if (!L.n || !L.ntiles) return;
+                     hipStream_t s, const RtClear &clr) {
+    if (!L.n || !L.ntiles) throw std::logic_error("launch_rt_count: no points or tiles");   // (the callers check)
     unsigned *own = reinterpret_cast<unsigned *>(H + (size_t)L.ntiles * G);
     switch (rt_layout(L)) {
-        case 1: rt_part<false, 1>(L, H, nullptr, G, nullptr, own, s); break;
-        case 2: rt_part<false, 2>(L, H, nullptr, G, nullptr, own, s); break;
-        default: rt_part<false, 0>(L, H, nullptr, G, nullptr, own, s);
+        case 1: rt_part<false, 1>(L, H, nullptr, G, nullptr, own, s, clr); break;
+        case 2: rt_part<false, 2>(L, H, nullptr, G, nullptr, own, s, clr); break;
+        default: rt_part<false, 0>(L, H, nullptr, G, nullptr, own, s, clr);
     }
     ColScan C{H, ts, own, n_own, L.ntiles, G, (G + kColRows - 1) / kColRows, (L.ntiles + kColTB - 1) / kColTB, lb};
     k_rt_colscan<<<C.ng * C.ntb, kColTB, 0, s>>>(C);

@@ -521,16 +521,23 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
     DevBuf &stage_buf = map_mode ? ms.st[ms.cur] : sorted;
     unsigned long long *d_cnt = static_cast<unsigned long long *>(counters.ensure(8 * kRorCounters + 16));
     unsigned long long *d_own = d_cnt + kRorCounters;   // [0] binned points, [1] overflow flag
-    AOS_HIP(hipMemsetAsync(d_cnt, 0, 8 * kRorCounters + 16, s));
-    AOS_HIP(hipMemsetAsync(rbits, 0, sizeof(uint64_t) * (size_t)o.Hr * WWr, s));
-    if (d_kept) AOS_HIP(hipMemsetAsync(d_kept, 0, sizeof(int) * nt, s));
     // PCL dense kNN needs k = min_pts + 1 points in the whole cloud (else every point is removed).
     // A tile's shard holds every neighbour of its own candidates, so a shard with fewer points has
     // no keepable candidate either: the local test is exact.
     const bool any = L.n > 0 && !(is_dense && n_points < (uint64_t)L.need);
-    if (!any) return;
+    // the counters, raster bits and kept counts start at zero: cleared by the count launch (no fills)
+    RtClear clr;
+    clr.w = rbits; clr.nw = (size_t)o.Hr * WWr;
+    clr.c = d_cnt; clr.nc = kRorCounters + 2;
+    clr.k = d_kept; clr.nk = d_kept ? nt : 0;
+    if (!any) {
+        AOS_HIP(hipMemsetAsync(d_cnt, 0, 8 * kRorCounters + 16, s));
+        AOS_HIP(hipMemsetAsync(rbits, 0, sizeof(uint64_t) * clr.nw, s));
+        if (d_kept) AOS_HIP(hipMemsetAsync(d_kept, 0, sizeof(int) * nt, s));
+        return;
+    }
     AOS_HIP(hipEventRecord(ev[12], s));
-    launch_rt_count(L, d_H, G, d_ts, d_own, ror_lookback(L, G, d_own), s);
+    launch_rt_count(L, d_H, G, d_ts, d_own, ror_lookback(L, G, d_own), s, clr);
     AOS_HIP(hipEventRecord(ev[13], s));
     // The staged array holds own + halo copies. With a capacity from an earlier frame the scatter
     // runs at once and reports an overflow (the frame is then redone with the size it read back,
@@ -557,8 +564,7 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
     launch_rt_ror(L, d_ts, d_staged, d_scratch, d_big, rbits, d_cnt, d_kept, nullptr, s);
     AOS_HIP(hipEventRecord(ev[11], s));
     // binned points, staged total, overflow flag: read with the frame's other stats (finish_frame)
-    AOS_HIP(hipMemcpyAsync(h + 2, d_ts + nt, sizeof(int), hipMemcpyDeviceToHost, s));
-    AOS_HIP(hipMemcpyAsync(h + 4, d_own, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    ror_stats_to_host(d_ts + nt, d_own);
     if (map_mode)   // the store will hold the whole map (committed by ror_collect: no overflow)
         ms.pend = MapStore::Pending{true, false, geom_of(L), is_dense, n_points, ms.cur};
 }
@@ -590,11 +596,12 @@ void aos_ctx::ror_stage_append(RorLaunch L, uint64_t *rbits) {
     float4 *d_new = static_cast<float4 *>(ms.st[nxt].ensure(sizeof(float4) * cap));
     int *d_nts = static_cast<int *>(ms.ts[nxt].ensure(sizeof(int) * (nt + 1)));
     float4 *d_scratch = static_cast<float4 *>(ror_scratch.ensure(sizeof(float4) * cap));
-    AOS_HIP(hipMemsetAsync(d_cnt, 0, 8 * kRorCounters + 16, s));
     Ls.staged_cap = (int)scan_cap;
     Ls.overflow = reinterpret_cast<int *>(d_own + 1);
     AOS_HIP(hipEventRecord(ev[12], s));
-    launch_rt_count(Ls, d_H, G, d_sts, d_own, ror_lookback(Ls, G, d_own), s);
+    RtClear clr;
+    clr.c = d_cnt; clr.nc = kRorCounters + 2;
+    launch_rt_count(Ls, d_H, G, d_sts, d_own, ror_lookback(Ls, G, d_own), s, clr);
     AOS_HIP(hipEventRecord(ev[13], s));
     AOS_HIP(hipEventRecord(ev[14], s));
     launch_rt_scatter(Ls, d_H, d_sts, G, d_scan, s);
@@ -607,9 +614,7 @@ void aos_ctx::ror_stage_append(RorLaunch L, uint64_t *rbits) {
     launch_rt_ror(L, d_nts, d_new, d_scratch, d_big, rbits, d_cnt, ms.kept.as<int>(), d_sts, s);
     launch_rt_sum_kept(ms.kept.as<int>(), nt, d_cnt, s);
     AOS_HIP(hipEventRecord(ev[11], s));
-    int *h = static_cast<int *>(h_stats.p);
-    AOS_HIP(hipMemcpyAsync(h + 2, d_nts + nt, sizeof(int), hipMemcpyDeviceToHost, s));
-    AOS_HIP(hipMemcpyAsync(h + 4, d_own, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    ror_stats_to_host(d_nts + nt, d_own);
     // committed by ror_collect (the old store ms.st[ms.cur] stays intact until then)
     ms.pend = MapStore::Pending{true, true, ms.L, ms.dense, n_points, nxt};
 }
@@ -623,6 +628,14 @@ void aos_ctx::ror_stage_unchanged() {
     h[2] = (int)ms.n_staged;   // (binned 0 new points and no overflow: zeroed by ror_stage)
     ms.pend = MapStore::Pending{true, true, ms.L, ms.dense, n_points, ms.cur};
     ++ror_skipped;
+}
+
+// The stage's staged total (h[2]) and binned count + overflow bits (h + 4: two u64) into the pinned stats, read
+// after the frame's sync (ror_collect): one kernel store instead of two copy-engine read-backs
+void aos_ctx::ror_stats_to_host(const int *d_staged_total, const unsigned long long *d_own) {
+    int *h = static_cast<int *>(h_stats.p);
+    const int *o = reinterpret_cast<const int *>(d_own);
+    peek_to_host(h + 2, {d_staged_total, d_staged_total, o, o + 1, o + 2, o + 3}, stream);
 }
 
 // After the frame's sync: binned count, staged size, and whether the scatter overflowed its guess. A stuck
@@ -664,8 +677,8 @@ bool aos_ctx::ror_collect(bool throw_stuck) {
 // flags buffer when it copies them, and W, H, WW, R, the launch count, the flags length) and re-captured
 // when any of them changes; the per-launch act_prev / act_next alternation is a function of the launch
 // index from 0, the same on every replay. Graph shapes (AOS_THIN_GRAPH, for the diagnosis of round 2's
-// failure, tools/thin_graph_probe.py): 1 (default) kernels only, the flags cleared by a kernel and read
-// back outside the graph; 2 round 1's shape: memset node + kernels + D2H copy node; 3 memset node +
+// failure, tools/thin_graph_probe.py): 1 (default) kernels only, the flags cleared by the opening kernel and
+// read back outside the graph; 2 round 1's shape: memset node + kernels + D2H copy node; 3 memset node +
 // kernels; 4 clearing kernel + kernels + D2H copy node. Returns true when the graph copied the flags
 // of the batch to h_flags itself.
 bool aos_ctx::thin_first_batch(const FrameGeom &g, const uint64_t *d_ibits, uint64_t *d_open, uint64_t *const bufs[2],
@@ -681,8 +694,7 @@ bool aos_ctx::thin_first_batch(const FrameGeom &g, const uint64_t *d_ibits, uint
     const int shape = thin_graph_shape;
     last_thin_graph = 0;
     if (shape == 0) {
-        AOS_HIP(hipMemsetAsync(d_flags, 0, sizeof(int) * nflags, s));
-        launch_open(d_ibits, d_open, g, s);
+        launch_open(d_ibits, d_open, g, s, d_flags, nflags);   // (clears the flags)
         launch_next(batch_n);
         return false;
     }
@@ -708,9 +720,15 @@ bool aos_ctx::thin_first_batch(const FrameGeom &g, const uint64_t *d_ibits, uint
         hipGraph_t graph = nullptr;
         AOS_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
         try {
-            if (memset_node) AOS_HIP(hipMemsetAsync(d_flags, 0, sizeof(int) * nflags, s));
-            else launch_zero_ints(d_flags, nflags, s);
-            launch_open(d_ibits, d_open, g, s);
+            if (memset_node) {
+                AOS_HIP(hipMemsetAsync(d_flags, 0, sizeof(int) * nflags, s));
+                launch_open(d_ibits, d_open, g, s);
+            } else if (shape == 4) {
+                launch_zero_ints(d_flags, nflags, s);
+                launch_open(d_ibits, d_open, g, s);
+            } else {
+                launch_open(d_ibits, d_open, g, s, d_flags, nflags);   // (clears the flags: no clearing node)
+            }
             launch_next(batch_n);
             if (copy_node)
                 AOS_HIP(hipMemcpyAsync(h_flags, d_flags, sizeof(int) * (1 + batch_n * K), hipMemcpyDeviceToHost, s));
@@ -767,6 +785,8 @@ void aos_ctx::thin_check_flags(const int *d_flags, const int *h_flags, int n_rea
     }
 }
 
+static int grid_readback_bits();
+
 void aos_ctx::run_seedgen(bool want_host, aos_seedgen_out &out) {
     // A frame is served (have_frame) only once every check passed: finish_frame sets it before the ROR
     // overflow and thinning-convergence checks of the deferred path, so every way out of here that is not
@@ -808,9 +828,17 @@ bool aos_ctx::run_seedgen_once(bool want_host, aos_seedgen_out &out, bool allow_
     // ---------------- a5 inflation, a6 frame -> /occupancy_grid
     uint64_t *d_ibits = static_cast<uint64_t *>(infl_bits.ensure(Cw * 8));
     int8_t *d_occ = static_cast<int8_t *>(occ_bytes.ensure((size_t)g.W * g.H));
-    launch_inflate(d_rbits, d_ibits, g, s);
-    launch_bits_to_bytes(d_ibits, d_occ, g, 5, s);
+    launch_inflate(d_rbits, d_ibits, g, s, d_occ, 5);   // (the bytes with the 5-cell frame in the same launch)
     AOS_HIP(hipEventRecord(ev[2], s));
+    // /occupancy_grid's bits cross PCIe now, beside thinning, instead of beside the cluster stage's read-backs
+    // (finish_frame sends the skeleton's)
+    infl_bits_sent = false;
+    if (want_host && grid_readback_bits()) {
+        expander.drain();   // (a failed frame's expansion may still read the buffer)
+        const size_t nb = 8 * Cw;
+        grid_d2h(h_occ_bits.ensure(std::max<size_t>(nb, 8)), d_ibits, nb);
+        infl_bits_sent = true;
+    }
 
     // ---------------- a7 opening + Zhang-Suen (temporal blocks of kThinItersPerLaunch iterations)
     uint64_t *d_open = static_cast<uint64_t *>(open_bits.ensure(Cw * 8));
@@ -858,8 +886,7 @@ bool aos_ctx::run_seedgen_once(bool want_host, aos_seedgen_out &out, bool allow_
     int round0 = 0;
     if (defer && !flags_in_graph) {
         uint64_t *d_out = static_cast<uint64_t *>(thin_out.ensure(Cw * 8));
-        launch_thin_pick(d_flags, launched, bufs[0], bufs[1], d_out, Cw, s);
-        AOS_HIP(hipMemcpyAsync(h_flags, d_flags, sizeof(int) * (1 + launched * K), hipMemcpyDeviceToHost, s));
+        launch_thin_pick(d_flags, launched, bufs[0], bufs[1], d_out, Cw, s, h_flags, 1 + launched * K);
         AOS_HIP(hipEventRecord(ev[3], s));
         skel_bits = d_out;
         const double t_thin = since();
@@ -955,6 +982,20 @@ static void create_copy_stream(hipStream_t *st) {
     }
     AOS_HIP(hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data()));
 }
+void aos_ctx::grid_d2h(void *h, const void *d, size_t bytes) {
+    grid_copy_wait();
+    AOS_HIP(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, copy_stream));
+}
+// the copy stream (created on first use) waits for the work queued on the handle's stream so far
+void aos_ctx::grid_copy_wait() {
+    if (!copy_stream) {
+        create_copy_stream(&copy_stream);
+        AOS_HIP(hipEventCreateWithFlags(&copy_ready, hipEventDisableTiming));
+        AOS_HIP(hipEventCreateWithFlags(&copy_done, hipEventDisableTiming));
+    }
+    AOS_HIP(hipEventRecord(copy_ready, stream));
+    AOS_HIP(hipStreamWaitEvent(copy_stream, copy_ready, 0));
+}
 static int grid_copy_blocks() {   // AOS_GRID_COPY_BLOCKS (default 64)
     static const int b = [] { const char *e = getenv("AOS_GRID_COPY_BLOCKS"); return e ? std::max(1, atoi(e)) : 64; }();
     return b;
@@ -975,7 +1016,6 @@ void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *c
 
     // ---------------- a16 /skeletonized_occupancy_grid = skeleton + polygon bbox rectangle
     int8_t *d_skel = static_cast<int8_t *>(skel_bytes.ensure(C));
-    launch_bits_to_bytes(skel_bits, d_skel, g, 0, s);
     int rect[4] = {0, 0, 0, 0};   // markPolygonBoundaryAsOccupied's rectangle: gx0, gy0, gx1, gy1
     {
         double hminx = poly[0].first, hmaxx = poly[0].first, hminy = poly[0].second, hmaxy = poly[0].second;
@@ -993,7 +1033,6 @@ void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *c
         };
         w2g(static_cast<float>(hminx - margin), static_cast<float>(hminy - margin), rect[0], rect[1]);
         w2g(static_cast<float>(hmaxx + margin), static_cast<float>(hmaxy + margin), rect[2], rect[3]);
-        launch_draw_rect(d_skel, g, rect[0], rect[1], rect[2], rect[3], s);
     }
     // the two published grids go to host memory on the copy stream while the cluster / seed stage runs
     // (AOS_GRID_COPY=1: after it instead; the copy's blit kernels share the CUs with the stage's kernels)
@@ -1001,20 +1040,14 @@ void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *c
     const bool as_bits = grid_readback_bits() != 0;
     auto issue_grid_copy = [&]() {
         h_occ.ensure(std::max<size_t>(C, 1)); h_skel.ensure(std::max<size_t>(C, 1));
-        if (!copy_stream) {
-            create_copy_stream(&copy_stream);
-            AOS_HIP(hipEventCreateWithFlags(&copy_ready, hipEventDisableTiming));
-            AOS_HIP(hipEventCreateWithFlags(&copy_done, hipEventDisableTiming));
-        }
-        AOS_HIP(hipEventRecord(copy_ready, s));
-        AOS_HIP(hipStreamWaitEvent(copy_stream, copy_ready, 0));
         if (as_bits) {
             const size_t nb = 8 * (size_t)g.WW * g.H;
-            const uint64_t *ib = tiled_frame ? full_infl.as<uint64_t>() : infl_bits.as<uint64_t>();
+            if (!infl_bits_sent) expander.drain();   // (a failed frame's expansion may still read the buffers)
             uint64_t *hob = static_cast<uint64_t *>(h_occ_bits.ensure(std::max<size_t>(nb, 8)));
             uint64_t *hsb = static_cast<uint64_t *>(h_skel_bits.ensure(std::max<size_t>(nb, 8)));
-            AOS_HIP(hipMemcpyAsync(hob, ib, nb, hipMemcpyDeviceToHost, copy_stream));
-            AOS_HIP(hipMemcpyAsync(hsb, skel_bits, nb, hipMemcpyDeviceToHost, copy_stream));
+            if (!infl_bits_sent)   // (a tiled frame: the gathered inflated grid)
+                grid_d2h(hob, tiled_frame ? full_infl.as<uint64_t>() : infl_bits.as<uint64_t>(), nb);
+            grid_d2h(hsb, skel_bits, nb);
             AOS_HIP(hipEventRecord(copy_done, copy_stream));
             GridExpander::Job j{};
             const int dev = device;
@@ -1030,15 +1063,19 @@ void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *c
             j.threads = grid_expand_threads();
             expander.start(j);
         } else if (grid_copy_kernel()) {   // (a kernel launch never holds the host; see copy_kernel_bulk)
+            grid_copy_wait();
             copy_kernel_bulk(h_occ.p, d_occ, C, grid_copy_blocks(), copy_stream);
             copy_kernel_bulk(h_skel.p, d_skel, C, grid_copy_blocks(), copy_stream);
         } else {
-            AOS_HIP(hipMemcpyAsync(h_occ.p, d_occ, C, hipMemcpyDeviceToHost, copy_stream));
-            AOS_HIP(hipMemcpyAsync(h_skel.p, d_skel, C, hipMemcpyDeviceToHost, copy_stream));
+            grid_d2h(h_occ.p, d_occ, C);
+            grid_d2h(h_skel.p, d_skel, C);
         }
     };
     HostTrace tr{"finish"};
-    if (want_host && grid_copy_mode == 0) issue_grid_copy();
+    // the bits are final: their D2H starts before the byte expansion (the byte copies of the other modes after it)
+    if (want_host && grid_copy_mode == 0 && as_bits) issue_grid_copy();
+    launch_bits_to_bytes(skel_bits, d_skel, g, 0, s, rect);   // (a16: the rectangle drawn in the same launch)
+    if (want_host && grid_copy_mode == 0 && !as_bits) issue_grid_copy();
     tr.mark("copy_issued");
 
     // ---------------- a8-a15 clusters, tree rows, seeds

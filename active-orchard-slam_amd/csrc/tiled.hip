@@ -258,6 +258,7 @@ void aos_ctx::run_tiled_frame(const aos_comm &cm, int tiles_x, int tiles_y, int 
     std::memset(&out, 0, sizeof(out));
     have_frame = false;
     tiled_frame = true;
+    infl_bits_sent = false;
     skel_bits = nullptr;
     const FrameGeom g = frame_geom(poly, P);
     geom = g;
