@@ -85,11 +85,12 @@ struct aos_ctx {
     // A host cloud is split while it is gathered (upload_pack): the points inside `box`, the ROR stage's
     // binned box for the polygon and parameters current at upload time (ror_stage: no point outside it
     // can be binned), go to the device, packed at the front of the cloud buffer in chunk-arrival order (the
-    // ROR results do not depend on point order); the others stay in `rest` (pinned host memory, thread t's
-    // run at byte rbeg[t], rn[t] points). A frame whose binned box is not inside `box` (the polygon changed:
-    // aos_seedgen_reprocess) first copies the rest behind the front (cloud_for_box).
+    // ROR results do not depend on point order); the others stay in `rest` (pageable host memory: it is copied
+    // only when the polygon grows, so it holds no page-locked memory — 2 x 12 n bytes at C2 with a prefetch —
+    // ADVICE r04; thread t's run at byte rbeg[t], rn[t] points). A frame whose binned box is not inside `box`
+    // (the polygon changed: aos_seedgen_reprocess) first copies the rest behind the front (cloud_for_box).
     struct CloudSplit {
-        aos::PinnedBuf rest;
+        aos::HostBuf rest;
         uint64_t rbeg[kUpThreads] = {}, rn[kUpThreads] = {};
         int nth = 0;
         uint64_t n_front = 0, n_all = 0;

@@ -4,6 +4,8 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
+#include <new>
 #include <string>
 #include <utility>
 #include <vector>
@@ -100,6 +102,28 @@ struct PinnedBuf {
     }
     template <class T> T *as() const { return static_cast<T *>(p); }
     void release() { if (p) (void)hipHostFree(p); p = nullptr; cap = 0; }
+};
+
+// Owning, growable pageable host allocation (64-byte aligned): host data the device reads only now and then
+// (the rest of a split cloud: copied only when the polygon grows), kept out of page-locked memory.
+struct HostBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    HostBuf() = default;
+    HostBuf(const HostBuf &) = delete;
+    HostBuf &operator=(const HostBuf &) = delete;
+    ~HostBuf() { release(); }
+    void *ensure(size_t bytes) {
+        if (bytes <= cap) return p;
+        release();
+        const size_t c = (bytes + bytes / 8 + 256 + 63) / 64 * 64;
+        p = std::aligned_alloc(64, c);
+        if (!p) throw std::bad_alloc();
+        cap = c;
+        return p;
+    }
+    template <class T> T *as() const { return static_cast<T *>(p); }
+    void release() { std::free(p); p = nullptr; cap = 0; }
 };
 
 typedef std::vector<std::pair<double, double>> Poly;

@@ -155,14 +155,14 @@ static void host_bfs_replay(const int *cells, int n, const GridC &g, const doubl
 }
 
 // The exact replays of a frame, in parallel over clusters on up to kReplayThreads host threads (each
-// writes only its own record).
+// writes only its own record): the pool's parked workers when one is given (no thread start per frame).
 void replay_clusters(const std::vector<ReplayJob> &jobs, const GridC &g, const double *poly, int np, float min_len,
-                     ClusterRec *rec) {
+                     ClusterRec *rec, HostPool *pool) {
     if (jobs.empty()) return;
     std::atomic<int> next{0};
     std::exception_ptr err;
     std::mutex mu;
-    auto work = [&]() {
+    auto work = [&](int) {
         std::vector<int> q, tab;
         std::vector<uint64_t> bm;
         for (int i; (i = next.fetch_add(1)) < (int)jobs.size();) {
@@ -176,10 +176,14 @@ void replay_clusters(const std::vector<ReplayJob> &jobs, const GridC &g, const d
         }
     };
     const int nt = std::min<int>((int)jobs.size(), kReplayThreads);
-    std::vector<std::thread> th;
-    for (int t = 1; t < nt; ++t) th.emplace_back(work);
-    work();
-    for (auto &t : th) t.join();
+    if (pool) {
+        pool->run(nt, work);
+    } else {
+        std::vector<std::thread> th;
+        for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
+        work(0);
+        for (auto &t : th) t.join();
+    }
     if (err) std::rethrow_exception(err);
 }
 

@@ -2,6 +2,7 @@
 #pragma once
 #include <condition_variable>
 #include <exception>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <thread>
@@ -9,6 +10,7 @@
 
 #include "aos_internal.h"
 #include "dev_prims.h"
+#include "host_pool.h"
 #include "subdiv2d.h"
 
 namespace aos {
@@ -94,6 +96,7 @@ struct ClusterSeedState {
     int n_fg = 0, n_clusters = 0, n_rows = 0, n_cur_tab = 0;
     double cur_tab_amax = -1.0;
     std::vector<ClusterRec> h_rec;
+    HostPool replay_pool;   // the BFS replays' host threads (replay_clusters)
 };
 
 // a8-a10 computed elsewhere (the tiled frame's distributed cluster stage, cluster_dist.hip): every
@@ -110,6 +113,9 @@ struct SeedStageIn {
     const Poly *poly;
     double cluster_min_length;
     const PreClusters *pre = nullptr;   // set: skip a8-a10 (labelling, statistics, replays)
+    // called once the foreground count's read-back is queued (at the start with pre): the published grids'
+    // D2H goes there, after k_fg, so the copy shares neither k_fg's CUs nor PCIe with that read-back
+    std::function<void()> after_fg;
 };
 
 struct GridC;
@@ -121,7 +127,7 @@ void launch_cluster_stats(const int *off, const int *cells, int n_clusters, cons
 // starts from the smallest), n of them
 struct ReplayJob { int c; const int *cells; int n; };
 void replay_clusters(const std::vector<ReplayJob> &jobs, const GridC &g, const double *poly, int np, float min_len,
-                     ClusterRec *rec);
+                     ClusterRec *rec, HostPool *pool = nullptr);
 
 // a tree row as the seed kernels take it: start / end (world), k base seeds, first virtual-seed slot
 struct RowDev { double sx, sy, ex, ey; int k; int slot0; };
@@ -222,7 +228,7 @@ struct GvdState {
     PinnedBuf h_misc;
     void *scratch = nullptr;   // GvdScratch (gvd.hip), freed by free_gvd_scratch
     PinnedBuf h_seeds;   // seeds in / merged seeds out (g1)
-    PinnedBuf h_out;     // the GvdGraph arrays, gathered on the device and copied back in one DMA
+    PinnedBuf h_out;     // the GvdGraph arrays, gathered into it by one kernel (k_gather_words)
     PinnedBuf h_evals;   // the graph searches' work counters (aos_params.gvd_count_evals)
     aos_gvd_evals evals{};
     SyncEvent sev;       // host waits of this state's GVD calls (the stream may be shared by several lanes)

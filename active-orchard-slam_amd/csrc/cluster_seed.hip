@@ -110,9 +110,20 @@ static int ccl_edge_cap(int nf) {
     return e ? std::max(2, atoi(e)) : std::max(4096, nf / 4);
 }
 constexpr int kCclBatch = 4;   // k_ccl_local: cells per thread whose neighbour lookups are in flight together
+// Root of x with path halving: x is pointed at its grandparent as the walk passes (a parent always has the
+// smaller index, so the grandparent is an ancestor and no cycle can form; a root is never written: only entries
+// already read as non-roots are). The chunk's unions arrive in no particular order along the skeleton's lines,
+// and without halving their chains grew to hundreds of links that every later find walked again. (The global
+// union-find keeps its read-only walks: agent-scope stores past the XCD's L2 cost more than they saved, round 4.)
 __device__ __forceinline__ int lds_find(int *lp, int x) {
-    for (int p; (p = __hip_atomic_load(&lp[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != x;) x = p;
-    return x;
+    for (;;) {
+        const int p = __hip_atomic_load(&lp[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (p == x) return x;
+        const int g = __hip_atomic_load(&lp[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (g == p) return p;
+        __hip_atomic_store(&lp[x], g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        x = g;
+    }
 }
 __device__ __forceinline__ void lds_union(int *lp, int i, int j) {
     int a = lds_find(lp, i), b = lds_find(lp, j);
@@ -646,6 +657,7 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
                             const hipEvent_t *ev_split) {
     HostTrace tr{"cluster"};
     if (ev_split) AOS_HIP(hipEventRecord(ev_split[0], s));   // (AOS_TRACE: the stage's first kernel is next)
+    if (in.pre && in.after_fg) in.after_fg();
     const FrameGeom &fg = *in.g;
     const GridC g = make_gridc(fg);
     const Poly &poly = *in.poly;
@@ -676,6 +688,7 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         k_fg<<<gw2, 64, 0, s>>>(in.skel_bits, d_fg, d_wc, g, d_poly, np);
         scan_1p(S.lb, d_wc, d_wo, (int)Cw, false, s);
         peek_to_host(h_sc, {d_wo + Cw, S.lb.err_word(s)}, s);
+        if (in.after_fg) in.after_fg();
         S.dedup.sev.sync(s);
         tr.mark("fg");
         if (h_sc[1]) throw std::runtime_error("cluster stage: scan failed on the device");
@@ -747,7 +760,7 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
             tr.mark("cells");
             std::vector<ReplayJob> jobs;
             for (int c : ids) jobs.push_back({c, hc + (off[c] - lo), S.h_rec[c].n});
-            replay_clusters(jobs, g, hp.data(), np, static_cast<float>(in.cluster_min_length), S.h_rec.data());
+            replay_clusters(jobs, g, hp.data(), np, static_cast<float>(in.cluster_min_length), S.h_rec.data(), &S.replay_pool);
             tr.mark("replays");
         }
     }

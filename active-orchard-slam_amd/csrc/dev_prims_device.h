@@ -20,6 +20,28 @@ __device__ __forceinline__ void ci_row(const CellIdx &c, int yy, int cx, int &k0
     k1 = c.start[b + min(cx + 1, c.h.nx - 1) + 1];
 }
 
+// The items of a cell-index run [k0, k1) in batches of B whose loads are in flight together: B item indices, then
+// load(j) for each (the caller's per-item reads, independent of one another), then use(j, v) in run order. A run
+// walked one item at a time is a chain of two or three dependent global loads per item (round 5: the GVD
+// searches spent most of their time waiting on it). use returns false to stop the walk; walk_items returns
+// false when it was stopped.
+template <int B, class Load, class Use>
+__device__ __forceinline__ bool walk_items(const int *items, int k0, int k1, Load load, Use use) {
+    for (int k = k0; k < k1; k += B) {
+        int j[B];
+#pragma unroll
+        for (int u = 0; u < B; ++u) j[u] = k + u < k1 ? items[k + u] : -1;
+        decltype(load(0)) v[B];
+#pragma unroll
+        for (int u = 0; u < B; ++u)
+            if (j[u] >= 0) v[u] = load(j[u]);
+#pragma unroll
+        for (int u = 0; u < B; ++u)
+            if (j[u] >= 0 && !use(j[u], v[u])) return false;
+    }
+    return true;
+}
+
 __device__ __forceinline__ unsigned long long ld_u64(const unsigned long long *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

@@ -218,17 +218,16 @@ __global__ __launch_bounds__(kLfTB) void k_lfmis(LfArgs A) {
             for (int yy = max(cy - 1, 0); yy <= min(cy + 1, A.ci.h.ny - 1) && !dup; ++yy) {
                 int k0, k1;
                 ci_row(A.ci, yy, cx, k0, k1);
-                for (int k = k0; k < k1; ++k) {
-                    const int j = A.ci.items[k];
-                    if (j >= i) continue;
-                    const double2 pj = A.p[j];
-                    if (!OWNER && A.self_conflict && pj.x == pi.x && pj.y == pi.y) { dup = true; break; }
+                dup = !walk_items<8>(A.ci.items, k0, k1, [&](int j) { return A.p[j]; }, [&](int j, double2 pj) {
+                    if (j >= i) return true;
+                    if (!OWNER && A.self_conflict && pj.x == pi.x && pj.y == pi.y) return false;   // (dup)
                     if (conflict(pi, pj, A.mode, A.thr)) {
                         if (nl < kLfList) lst[nl * kLfTB + tid] = j;
                         else over = true;
                         ++nl;
                     }
-                }
+                    return true;
+                });
             }
             if (dup) s = 2;
             else if (nl == 0) { s = 1; own = i; }

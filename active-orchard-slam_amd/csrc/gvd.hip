@@ -106,16 +106,17 @@ __global__ void k_nearest(const double2 *occ, int n_occ, CellIdx ci, const int *
     double best = 1.7976931348623157e308;
     int bi = -1;
     long long ne = 0;
+    struct PosPt { int i; double2 p; };
     for (int yy = max(cy - 1, 0); yy <= min(cy + 1, ci.h.ny - 1); ++yy) {
         int k0, k1;
         ci_row(ci, yy, cx, k0, k1);
         ne += k1 - k0;
-        for (int k = k0; k < k1; ++k) {
-            const int c = ci.items[k], i = pos_of[c];
-            if (i < 0) continue;
-            double dx = occ[c].x - q.x, dy = occ[c].y - q.y, d = sqrt(dx * dx + dy * dy);
-            if (d < best || (d == best && i < bi)) { best = d; bi = i; }
-        }
+        walk_items<8>(ci.items, k0, k1, [&](int c) { return PosPt{pos_of[c], occ[c]}; }, [&](int, const PosPt &v) {
+            if (v.i < 0) return true;
+            double dx = v.p.x - q.x, dy = v.p.y - q.y, d = sqrt(dx * dx + dy * dy);
+            if (d < best || (d == best && v.i < bi)) { best = d; bi = v.i; }
+            return true;
+        });
     }
     if (!(best < 0.05)) {  // safety net: exact brute force
         const int M = *M_dev;
@@ -141,14 +142,15 @@ __device__ __forceinline__ int pairs_of(int i, const double2 *bp, CellIdx ci, co
     hash_cell(ci.h, p.x, p.y, cx, cy);
     int c = 0, w = COUNT ? 0 : poff[i];
     long long ne = 0;
+    struct PosPt { int j; double2 q; };
     for (int yy = max(cy - 1, 0); yy <= min(cy + 1, ci.h.ny - 1); ++yy) {
         int k0, k1;
         ci_row(ci, yy, cx, k0, k1);
         ne += k1 - k0;
-        for (int k = k0; k < k1; ++k) {
-            const int cc = ci.items[k], j = pos_of[cc];
-            if (j <= i) continue;
-            double dx = p.x - occ[cc].x, dy = p.y - occ[cc].y, d = sqrt(dx * dx + dy * dy);
+        walk_items<8>(ci.items, k0, k1, [&](int cc) { return PosPt{pos_of[cc], occ[cc]}; }, [&](int, const PosPt &v) {
+            const int j = v.j;
+            if (j <= i) return true;
+            double dx = p.x - v.q.x, dy = p.y - v.q.y, d = sqrt(dx * dx + dy * dy);
             if (d <= 0.5 && d > 1e-6) {
                 if (!COUNT && w + c < cap) {  // insertion into the sorted run
                     int pos = w + c;
@@ -157,7 +159,8 @@ __device__ __forceinline__ int pairs_of(int i, const double2 *bp, CellIdx ci, co
                 }
                 ++c;
             }
-        }
+            return true;
+        });
     }
     eval_add(evals, 1, ne);
     return c;
@@ -184,8 +187,9 @@ __global__ void k_pairs(const double2 *bp, int no, const int *M_dev, CellIdx ci,
 // occurrence (a != b, both valid, no occupied sample) is counted in the group of its smaller node
 // (grank: its rank there) for the first-occurrence selection.
 // Round 5: the samples of a block's occurrences are flattened and spread over all of its threads (an
-// exclusive scan of the per-occurrence sample counts in LDS; a sample finds its occurrence by binary search),
-// kOccPer independent lookups per thread per round, and a sample of an occurrence already hit is skipped.
+// exclusive scan of the per-occurrence sample counts in LDS), each thread taking kOccPer consecutive samples per
+// round (one binary search for the first one's occurrence) whose lookups are in flight together, and a sample
+// of an occurrence already hit is skipped.
 // Round 4 walked each occurrence's samples on one lane, 16 per round: a wave waited for its longest edge (a
 // passing edge between two tree rows: every sample read), ~90 us per C2 frame. The hit test is an OR over
 // the samples, so the order they are read in never shows.
@@ -245,23 +249,30 @@ __global__ __launch_bounds__(kOccTB) void k_occupancy(const int2 *ft, const int 
     for (int q0 = 0; q0 < T; q0 += kOccTB * kOccPer) {
         bool h[kOccPer];
         int oo[kOccPer];
+        // the thread's kOccPer consecutive samples: one search for the first one's occurrence, then forward
+        const int qb = q0 + tid * kOccPer;
+        int o = 0;
+        if (qb < T) {
+            int lo = 0, hi = kOccTB - 1;   // the occurrence o with pre[o] <= qb < pre[o + 1]
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (pre[mid] <= qb) lo = mid; else hi = mid - 1;
+            }
+            o = lo;
+        }
 #pragma unroll
         for (int u = 0; u < kOccPer; ++u) {
-            const int q = q0 + u * kOccTB + tid;
+            const int q = qb + u;
             h[u] = false;
             oo[u] = -1;
             if (q >= T) continue;
-            int lo = 0, hi = kOccTB - 1;   // the occurrence o with pre[o] <= q < pre[o + 1]
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (pre[mid] <= q) lo = mid; else hi = mid - 1;
-            }
-            if (hit_s[lo]) continue;
-            oo[u] = lo;
-            const int i = i0_s[lo] + (q - pre[lo]), num = num_s[lo];
+            while (pre[o + 1] <= q) ++o;   // (q < T = pre[kOccTB]: o stays below kOccTB)
+            if (hit_s[o]) continue;
+            oo[u] = o;
+            const int i = i0_s[o] + (q - pre[o]), num = num_s[o];
             const double t = (i == num) ? 1.0 : ((double)i / (double)num);
-            const double len = len_s[lo];
-            const double px = sx_s[lo] + (t * ux_s[lo]) * len, py = sy_s[lo] + (t * uy_s[lo]) * len;
+            const double len = len_s[o];
+            const double px = sx_s[o] + (t * ux_s[o]) * len, py = sy_s[o] + (t * uy_s[o]) * len;
             h[u] = occ_trunc(sk, g, px, py);
             ++nread;
         }
@@ -564,12 +575,26 @@ __global__ void k_node_labels_fill(const double2 *nodes, int Mn, const double2 *
 // device staging buffer and no copy-engine read-back).
 constexpr int kMaxSegs = 12;
 struct SegList { const int *src[kMaxSegs]; long long off[kMaxSegs + 1]; int n; };
+// (four words per thread, one 16-byte store: host memory is written across PCIe, where 4-byte stores ran at
+// ~20 GB/s, 59 us for the C2 graph)
 __global__ void k_gather_words(SegList L, int *dst) {
-    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= L.off[L.n]) return;
+    const long long i0 = 4 * ((long long)blockIdx.x * blockDim.x + threadIdx.x), n = L.off[L.n];
+    if (i0 >= n) return;
+    int v[4];
     int k = 0;
-    while (i >= L.off[k + 1]) ++k;
-    dst[i] = L.src[k][i - L.off[k]];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const long long i = i0 + u;
+        v[u] = 0;
+        if (i >= n) continue;
+        while (i >= L.off[k + 1]) ++k;
+        v[u] = L.src[k][i - L.off[k]];
+    }
+    if (i0 + 4 <= n) {
+        *reinterpret_cast<int4 *>(dst + i0) = make_int4(v[0], v[1], v[2], v[3]);
+    } else {
+        for (int u = 0; u < 4 && i0 + u < n; ++u) dst[i0 + u] = v[u];
+    }
 }
 
 // ------------------------------------------------------------------ g4 facets (calcVoronoi + getVoronoiFacetList)
@@ -1173,7 +1198,7 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
     }
     const long long total = sl.off[sl.n];
     int *h_out = static_cast<int *>(G.h_out.ensure(sizeof(int) * (size_t)std::max(total, 1LL)));
-    if (total) k_gather_words<<<cdiv(total, 256), 256, 0, s>>>(sl, h_out);   // (straight into the pinned buffer)
+    if (total) k_gather_words<<<cdiv(cdiv(total, 4), 256), 256, 0, s>>>(sl, h_out);   // (straight into the pinned buffer)
     unsigned long long *h_ev = d_evals ? static_cast<unsigned long long *>(G.h_evals.ensure(8 * sizeof(unsigned long long))) : nullptr;
     if (d_evals) AOS_HIP(hipMemcpyAsync(h_ev, d_evals, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     AOS_HIP(hipEventRecord(ev[9], s));

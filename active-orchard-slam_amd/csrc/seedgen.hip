@@ -76,7 +76,7 @@ void aos_ctx::release() {
 // a ring of kUpSlots pinned 2 MB slots and DMA them on their own streams, so 25 % fewer bytes cross PCIe
 // for the common 16-byte record and the device gets a packed float3 cloud (step 12). With the split
 // (CloudSplit, default) only the points inside the binned box go into the slots (C2: 49.5 % of the cloud);
-// the others go to the pinned rest buffer (cloud_split.cpp: AVX-512 compress, 4 records per register). The
+// the others go to the (pageable) rest buffer (cloud_split.cpp: AVX-512 compress, 4 records per register). The
 // handle's stream waits for all of them. The caller's buffer is only read during the call.
 // Round 4 (profiles/r04v_split_ab.txt): C2's upload ends 2.2-2.8 ms after it starts with the split at 8
 // threads, 2.4-3.8 ms without it (4 / 8 / 16 threads); the DMA no longer trails the gather.
@@ -962,12 +962,13 @@ static int grid_expand_threads() {   // AOS_GRID_EXPAND_THREADS (default 8)
 }
 // The grids' D2H runs as the runtime's blit kernels (under the HIP runtime torch loads). Beside the cluster stage
 // they held the CUs its kernels needed: k_fg took 45 us instead of 18.6 beside the 2 MB bits copy at C2, 159
-// instead of 24 beside the 8 MB at C3 (round-5 traces, tools/kt_overlap.py). The copy stream is created with a CU
-// mask (hipExtStreamCreateWithCUMask) of AOS_COPY_CUS CUs (default 16 of the 256, spread over the id range;
-// 0: no mask), so its blit waves stay on those CUs and the stage's kernels keep the rest: PCIe, not CUs, bounds
-// the copy.
+// instead of 24 beside the 8 MB at C3 (round-5 traces, tools/kt_overlap.py). AOS_COPY_CUS = k > 0 creates the copy
+// stream with a CU mask (hipExtStreamCreateWithCUMask) of k CUs spread over the id range, so its blit waves stay
+// there. Measured and not adopted (profiles/r05g_copy_cus_ab.txt): with 16 CUs seed-gen took 1.47-1.49 ms per C2
+// frame instead of 1.24-1.27 (thinning and k_fg slower beside the masked copy). Default 0: no mask; the copies are
+// placed where they meet the fewest kernels instead (the inflated grid beside thinning, the skeleton after k_fg).
 static void create_copy_stream(hipStream_t *st) {
-    static const int want = [] { const char *e = getenv("AOS_COPY_CUS"); return e ? std::max(0, atoi(e)) : 16; }();
+    static const int want = [] { const char *e = getenv("AOS_COPY_CUS"); return e ? std::max(0, atoi(e)) : 0; }();
     int dev = 0, ncu = 0;
     AOS_HIP(hipGetDevice(&dev));
     AOS_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
@@ -1072,18 +1073,26 @@ void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *c
         }
     };
     HostTrace tr{"finish"};
-    // the bits are final: their D2H starts before the byte expansion (the byte copies of the other modes after it)
-    if (want_host && grid_copy_mode == 0 && as_bits) issue_grid_copy();
     launch_bits_to_bytes(skel_bits, d_skel, g, 0, s, rect);   // (a16: the rectangle drawn in the same launch)
-    if (want_host && grid_copy_mode == 0 && !as_bits) issue_grid_copy();
+    // the bits go once the cluster stage has queued k_fg and its count read-back (SeedStageIn::after_fg; round 5
+    // traces: beside k_fg the copy's blit kernel took k_fg from 19 to 49 us, and the read-back waited behind it on
+    // PCIe); the byte copies of the other modes right away
+    bool copy_issued = false;
+    auto copy_now = [&]() {
+        if (copy_issued) return;
+        copy_issued = true;
+        issue_grid_copy();
+    };
+    if (want_host && grid_copy_mode == 0 && !as_bits) copy_now();
     tr.mark("copy_issued");
 
     // ---------------- a8-a15 clusters, tree rows, seeds
     SeedStageIn sin{skel_bits, &geom, &poly, P.cluster_min_length, pre};
+    if (want_host && grid_copy_mode == 0 && as_bits) sin.after_fg = copy_now;
     SeedStageOut so;
     run_cluster_seed_stage(cs, sin, so, s, ev[4], trace_on() ? &ev[16] : nullptr);
     AOS_HIP(hipEventRecord(ev[5], s));
-    if (want_host && grid_copy_mode == 1) issue_grid_copy();
+    if (want_host && (grid_copy_mode == 1 || as_bits)) copy_now();   // (a stage that did not call after_fg)
 
     unsigned long long *h_cnt = static_cast<unsigned long long *>(h_stats.ensure(64 + 8 * kRorCounters)) + 8;
     if (!clipped_total) AOS_HIP(hipMemcpyAsync(h_cnt, counters.p, 8 * kRorCounters, hipMemcpyDeviceToHost, s));

@@ -14,6 +14,8 @@
 #            box's GPU over gloo)
 #   tiledstream  bench.py --tiled --stream at 1 rank, then the driver's --gpus 2 flow over gloo
 #   rorpmc   tools/rorbench binaries (RORBENCH, built in-tree beforehand): kernel trace + two SQ passes
+#   trace    AOS_TRACE=1 host timelines (per stage: ms at each host sync) of a short C2 run
+#   pmcsq    two SQ counter passes over the C2 bench for the kernels matching PMC_KERNELS
 # Usage: TAG=r04a STEPS="pytest smoke bench kt" tools/gpu_run.sh
 set -e
 R=$PWD
@@ -81,6 +83,23 @@ for step in $STEPS; do
         > $R/gpurun_out/${TAG}_c3write.log 2>&1)
       python3 tools/pmc_traffic.py $(ls gpurun_out/${TAG}_c3fetch/*counter_collection.csv | head -1) \
         $(ls gpurun_out/${TAG}_c3write/*counter_collection.csv | head -1) gpurun_out/${TAG}_c3_pmc_traffic.json ;;
+    trace)   # AOS_TRACE host timelines of a short C2 run -> TAG_trace.err
+      AOS_TRACE=1 timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-pipelined-rate --no-device-rate --steps 6 \
+        --warmup 2 > gpurun_out/${TAG}_trace.log 2> gpurun_out/${TAG}_trace.err || { tail -20 gpurun_out/${TAG}_trace.err; exit 1; }
+      grep -c "aos trace" gpurun_out/${TAG}_trace.err ;;
+    pmcsq)   # two SQ passes over the C2 bench for the kernels in PMC_KERNELS (a regex) -> TAG_pmcsq.txt
+      K=${PMC_KERNELS:-k_occupancy|k_lfmis|k_ccl_local|k_scan_1p|k_rt_ror}
+      rm -rf gpurun_out/${TAG}_sq1 gpurun_out/${TAG}_sq2
+      (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+        SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --kernel-include-regex "$K" --output-format csv \
+        -d $R/gpurun_out/${TAG}_sq1 -o sq1 -- python3 $R/bench.py --no-cpu-baseline --no-pipelined-rate --no-device-rate \
+        --steps 3 --warmup 1 > $R/gpurun_out/${TAG}_sq1.log 2>&1)
+      (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR \
+        SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex "$K" --output-format csv \
+        -d $R/gpurun_out/${TAG}_sq2 -o sq2 -- python3 $R/bench.py --no-cpu-baseline --no-pipelined-rate --no-device-rate \
+        --steps 3 --warmup 1 > $R/gpurun_out/${TAG}_sq2.log 2>&1)
+      python3 tools/pmc_summary.py gpurun_out/${TAG}_sq1 gpurun_out/${TAG}_sq2 > gpurun_out/${TAG}_pmcsq.txt
+      cat gpurun_out/${TAG}_pmcsq.txt ;;
     tiled)
       timeout -k 10 600 python -u -m pytest tests/test_gpu_tiled.py -x -v --timeout 400 --timeout-method thread -k rotating \
         > gpurun_out/${TAG}_pytest_rot.log 2>&1 || { tail -40 gpurun_out/${TAG}_pytest_rot.log; exit 1; }
