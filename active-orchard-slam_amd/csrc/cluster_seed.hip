@@ -102,7 +102,9 @@ __global__ void k_ccl_union(const int *list, int n, const uint64_t *fg, const in
 // always the root, as in k_ccl_union, so the roots and the flattened labels are the same.
 // chunk and block size (AOS_CCL_CHUNK / AOS_CCL_TB override them for A/B runs)
 static int ccl_chunk() { static const int v = [] { const char *e = getenv("AOS_CCL_CHUNK"); return e ? std::max(64, std::min(16384, atoi(e))) : 2048; }(); return v; }
-static int ccl_tb() { static const int v = [] { const char *e = getenv("AOS_CCL_TB"); return e ? std::max(64, std::min(1024, atoi(e))) / 64 * 64 : 256; }(); return v; }
+// (1024 threads: k_ccl_local 77 -> 52 us per C2 frame against 256, 60 with 512; 1024-cell chunks 58, 4096 with 1024
+// threads 69: profiles/r05j_ccl_ab.txt)
+static int ccl_tb() { static const int v = [] { const char *e = getenv("AOS_CCL_TB"); return e ? std::max(64, std::min(1024, atoi(e))) / 64 * 64 : 1024; }(); return v; }
 // capacity of k_ccl_local's cross-chunk link list (AOS_DEBUG_CCL_ECAP, read per call: tests force the overflow
 // fallback of k_ccl_cross with a tiny list)
 static int ccl_edge_cap(int nf) {
@@ -791,13 +793,6 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
     double2 *d_seeds = dev<double2>(S.seed_out, ncand);
     int *d_cnt = dev<int>(S.misc, 8);   // kept counts: virtual, ray, endpoint
     const double hx0 = g.minx - 50.0, hx1 = g.maxx + 50.0, hy0 = g.miny - 50.0, hy1 = g.maxy + 50.0;
-    if (nslots > 0) {
-        k_virtual_candidates<<<cdiv(nslots, 128), 128, 0, s>>>(d_rows, nr, nslots, in.skel_bits, g, d_poly, np, d_cand, d_ok);
-        greedy_dedup_async(scr, d_cand, d_ok, nslots, kConflictLess, 0.5, make_hash_n(hx0, hx1, hy0, hy1, 0.5, nslots),
-                           d_vout, nullptr, nullptr, d_cnt, s);
-    } else {
-        AOS_HIP(hipMemsetAsync(d_cnt, 0, sizeof(int), s));
-    }
     RayAngles ang{};
     const double degs[3] = {0.0, -90.0, 90.0};
     for (int a = 0; a < 3; ++a) {  // seed_gen:1796-1803, evaluated with the host libm
@@ -815,6 +810,16 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         tr.mark("curtab");
         S.cur_tab_amax = g.amax;
     }
+    if (nslots > 0) {
+        k_virtual_candidates<<<cdiv(nslots, 128), 128, 0, s>>>(d_rows, nr, nslots, in.skel_bits, g, d_poly, np, d_cand, d_ok);
+        greedy_dedup_async(scr, d_cand, d_ok, nslots, kConflictLess, 0.5, make_hash_n(hx0, hx1, hy0, hy1, 0.5, nslots),
+                           d_vout, nullptr, nullptr, d_cnt, s);
+    } else {
+        AOS_HIP(hipMemsetAsync(d_cnt, 0, sizeof(int), s));
+    }
+    // (Round 5 measured the endpoint-ray chain on a second stream with a hardware queue of its own, beside the
+    // virtual-seed chain: the look-back kernels of the one waited longer beside the other, the stage took 0.25 ms
+    // instead of 0.21-0.23; profiles/r05l_kt_summary.txt. Serial.)
     k_endpoint_rays<<<6 * nr, 64, 0, s>>>(d_rows, nr, in.skel_bits, g, ang, d_poly, np,
                                           static_cast<const double *>(S.cur_tab.p), S.n_cur_tab, d_rcand, d_rok, d_ecand, d_eok);
     if (6 * nr <= kSmallMax) {

@@ -1081,11 +1081,11 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
         AOS_HIP(hipMemsetAsync(d_evals, 0, 8 * sizeof(unsigned long long), s));
     }
     int *d_pcount = dev<int>(S.pcount, no), *d_poff = dev<int>(S.poff, no + 1);
-    k_pairs_count<<<cdiv(no, 256), 256, 0, s>>>(d_bp, no, d_M, cio, d_pos_of, d_occ, d_pcount, d_evals);
-    scan_1p(S.lb, d_pcount, d_poff, no, false, s);
     // The pair lists get a capacity from the last frame (P is read back only with the frame's sizes below);
     // a frame with more pairs runs the rest again with the exact size.
     int cap = G.pairs_cap > 0 ? G.pairs_cap : std::max(1024, 2 * no);
+    k_pairs_count<<<cdiv(no, 256), 256, 0, s>>>(d_bp, no, d_M, cio, d_pos_of, d_occ, d_pcount, d_evals);
+    scan_1p(S.lb, d_pcount, d_poff, no, false, s);
     int Mn = 0, Ne = 0, n_entries = 0;
     const int nrows = in.n_rows_poses / 2;
     const int nj = 4 * nrows;
@@ -1116,6 +1116,7 @@ bool run_gvd_stage(GvdState &G, const aos_params &P, const GvdStageIn &in, hipSt
         const int ncap = ne + cap;
         int2 *d_ft = dev<int2>(S.ft, ncap);
         unsigned long long *ev_k = attempt ? nullptr : d_evals;   // (a rerun with the exact pair capacity is not counted)
+        // (round 5 measured k_nearest on a second stream beside the pair count, scan and lists: no gain, r05l)
         k_nearest<<<cdiv(no, 256), 256, 0, s>>>(d_occ, no, cio, d_pos_of, d_bp, d_M, reinterpret_cast<int *>(d_ft), ev_k);
         k_pairs<<<cdiv(no, 256), 256, 0, s>>>(d_bp, no, d_M, cio, d_pos_of, d_occ, d_poff, d_ft + ne, cap, ev_k);
         int *d_pass = dev<int>(S.pass, ncap), *d_grank = dev<int>(S.occ_idx, ncap), *d_sel = dev<int>(S.selected, ncap);

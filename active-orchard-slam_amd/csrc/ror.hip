@@ -213,7 +213,7 @@ __global__ __launch_bounds__(kRtTB) void k_rt_part(RorLaunch L, int *H, const in
     };
     auto walk = [&](const Rec (&pt)[kRtPer], unsigned base) {
 #if AOS_RT_SCAT == 2
-        if (SCATTER) {
+        if (SCATTER && !L.rec12) {
             // batched: every point's first-tile claim in flight at once (LDS atomics with return; + 0 from a
             // point that is not binned), then the stores, then the halo copies behind one branch
             int pos[kRtPer], t00[kRtPer], oti[kRtPer];
@@ -287,6 +287,15 @@ __global__ __launch_bounds__(kRtTB) void k_rt_part(RorLaunch L, int *H, const in
             int bx, by, tx0, tx1, ty0, ty1;
             rt_bin(L, x, y, bx, by);
             rt_tiles(L, bx, by, tx0, tx1, ty0, ty1);
+            if (L.rec12) {   // 12-byte records: the tile pass recomputes the class from x, y, z and its tile
+                for (int ty = ty0; ty <= ty1; ++ty)
+                    for (int tx = tx0; tx <= tx1; ++tx) {
+                        const int pos = atomicAdd(&hist[ty * L.ntx + tx], 1);
+                        if (pos < L.staged_cap) reinterpret_cast<float3 *>(staged)[pos] = make_float3(x, y, z);
+                        else *L.overflow = 1;
+                    }
+                continue;
+            }
             const int otile = (by >> L.TBs) * L.ntx + (bx >> L.TBs);
             const float4 q = make_float4(x, y, z, __int_as_float(rt_candidate(L, x, y, z) ? 1 : 0));
             for (int ty = ty0; ty <= ty1; ++ty)
@@ -746,7 +755,15 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
             const int k = tid + j * kRorThreads;
             rk[j] = -1;
             if (k < n) {
-                q[j] = staged[a + k];
+                if (L.rec12) {   // class: an own clip candidate (its bin's tile is this one) or a neighbour only
+                    const float3 r = reinterpret_cast<const float3 *>(staged)[a + k];
+                    int bx, by;
+                    rt_bin(L, r.x, r.y, bx, by);
+                    const bool own = (by >> L.TBs) * L.ntx + (bx >> L.TBs) == t && rt_candidate(L, r.x, r.y, r.z);
+                    q[j] = make_float4(r.x, r.y, r.z, __int_as_float(own ? 1 : 0));
+                } else {
+                    q[j] = staged[a + k];
+                }
                 rk[j] = atomicAdd(&bstart[rt_lbin(L, q[j], bx0, by0, LB) + 1], 1);
             }
         }

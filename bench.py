@@ -43,7 +43,8 @@ ROR_DESIGN = "r04v"   # (r04v: the host cloud split at upload; the partition pas
 PMC_FILES = {("C2", "r02"): os.path.join(ROOT, "profiles", "r02q_pmc_traffic.json"),
              ("C2", "r03"): os.path.join(ROOT, "profiles", "r03fin_pmc_traffic.json"),
              ("C2", "r04"): os.path.join(ROOT, "profiles", "r04i_pmc_traffic.json"),
-             ("C2", "r04v"): os.path.join(ROOT, "profiles", "r04w_pmc_traffic.json")}
+             ("C2", "r04v"): os.path.join(ROOT, "profiles", "r04w_pmc_traffic.json"),
+             ("C3", "r04v"): os.path.join(ROOT, "profiles", "r05_c3_pmc_traffic.json")}
 
 
 def parse(argv=None):
