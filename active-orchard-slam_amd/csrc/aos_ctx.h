@@ -149,7 +149,6 @@ struct aos_ctx {
     double ror_est_binned = 0;             // binned points of the last frame (sizes the ROR tiles)
     double ror_staged_max = 0;             // largest staged (own + halo) count seen (sizes the scatter)
     bool ror_big_seen = false;             // a frame had a ROR tile beyond the LDS capacity (ror.hip big_ok)
-    int ror_rec_bytes = 16;                // the last whole-map frame's staged record size (RorLaunch::rec12)
 
     // ---- cluster / row / seed stage (cluster_seed.hip); tiled frames: distributed a8-a10 (cluster_dist.hip)
     aos::ClusterSeedState cs;

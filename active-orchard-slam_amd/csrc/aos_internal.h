@@ -156,8 +156,6 @@ struct RorLaunch {
     int staged_cap; int *overflow;   // staged array capacity; | 1 when the scatter exceeds it, | 2 when a tile
                                      // beyond the LDS capacity was found with big_ok = 0 (the frame is redone)
     int big_ok;                      // launch the big-tile kernels (ror.hip); 0 skips their five launches
-    int rec12;                       // staged records are 12 B (x, y, z) and the tile pass recomputes the class
-                                     // (whole-map frames without big tiles; 0: float4 with the class in w)
 };
 constexpr int kRtMaxTiles = 36000;   // tiles per frame (LDS histogram of the partition passes: 144 KB)
 void rt_configure(RorLaunch &L, int Hr, int WWr, double est_binned, int force_tb = 0);

@@ -98,11 +98,18 @@ __device__ __forceinline__ bool rt_candidate(const RorLaunch &L, float x, float 
 // the common case: q = a * (1 / res) is within 3.3e-16 |q| of the rounded quotient, so its truncation is
 // the quotient's unless an integer lies within that distance; q within 1e-14 |q| of an integer takes the
 // exact division. (Two f64 divisions per kept candidate were ~20 % of k_rt_ror's VALU issue.)
+// The exact division sits behind a wave-uniform branch: as a plain per-lane branch the compiler if-converted
+// it, so every call paid the f64 division sequence (~20 f64 instructions) whatever the lanes needed.
 __device__ __forceinline__ int rt_cell(double a, double res, double inv_res) {
     const double q = a * inv_res;
     const double t = trunc(q), d = fabs(q - t), tol = fabs(q) * 1e-14 + 1e-300;
-    if (d < tol || d > 1.0 - tol) return (int)(a / res);
-    return (int)t;
+    const bool exact = d < tol || d > 1.0 - tol;
+    int c = (int)t;
+    if (__builtin_amdgcn_ballot_w64(exact)) {   // (rare: some lane of the wave is within tol of an integer)
+        const int e = (int)(a / res);
+        c = exact ? e : c;
+    }
+    return c;
 }
 
 // dense: (double)d2 <= r2, i.e. d2 <= r2df; non-dense: d2 < r2f, i.e. d2 <= the float below r2f: both are
@@ -137,8 +144,8 @@ __device__ __forceinline__ bool rt_in(const RorLaunch &L, float4 p, float4 q) {
 #ifndef AOS_RT_G
 #define AOS_RT_G 512
 #endif
-#ifndef AOS_RT_SCAT   // scatter pass walk: 2 = batched first-tile claims (experiment)
-#define AOS_RT_SCAT 0
+#ifndef AOS_RT_STB   // scatter pass block size
+#define AOS_RT_STB 512
 #endif
 #ifndef AOS_RT_COLROWS   // rows of H per k_rt_colscan block
 #define AOS_RT_COLROWS 32
@@ -146,7 +153,7 @@ __device__ __forceinline__ bool rt_in(const RorLaunch &L, float4 p, float4 q) {
 #ifndef AOS_RT_NT   // nontemporal cloud loads: bit 0 count pass, bit 1 scatter pass
 #define AOS_RT_NT 0
 #endif
-constexpr int kRtCountPer = AOS_RT_CPER, kRtScatterPer = AOS_RT_SPER, kRtCountTB = AOS_RT_CTB, kRtScatterTB = 512;
+constexpr int kRtCountPer = AOS_RT_CPER, kRtScatterPer = AOS_RT_SPER, kRtCountTB = AOS_RT_CTB, kRtScatterTB = AOS_RT_STB;
 constexpr int kRtChunkQ = 4096;   // chunk granularity (points): a multiple of both passes' sub-chunks
 
 // tiles whose bins a point's 3 x 3 bins touch: [tx0, tx1] x [ty0, ty1], own tile (bx / TB, by / TB)
@@ -212,55 +219,6 @@ __global__ __launch_bounds__(kRtTB) void k_rt_part(RorLaunch L, int *H, const in
         }
     };
     auto walk = [&](const Rec (&pt)[kRtPer], unsigned base) {
-#if AOS_RT_SCAT == 2
-        if (SCATTER && !L.rec12) {
-            // batched: every point's first-tile claim in flight at once (LDS atomics with return; + 0 from a
-            // point that is not binned), then the stores, then the halo copies behind one branch
-            int pos[kRtPer], t00[kRtPer], oti[kRtPer];
-            unsigned halo = 0, okm = 0;
-#pragma unroll
-            for (int j = 0; j < kRtPer; ++j) {
-                const float x = pt[j].x, y = pt[j].y, z = pt[j].z;
-                const bool ok = base + (unsigned)(j * kRtTB + tid) < cnt && rt_binned(L, x, y, z);
-                int bx, by, tx0, tx1, ty0, ty1;
-                rt_bin(L, ok ? x : L.bminx, ok ? y : L.bminy, bx, by);
-                rt_tiles(L, bx, by, tx0, tx1, ty0, ty1);
-                t00[j] = ty0 * L.ntx + tx0;
-                oti[j] = (by >> L.TBs) * L.ntx + (bx >> L.TBs);
-                halo |= (ok ? ((tx1 > tx0 ? 1u : 0u) | (ty1 > ty0 ? 2u : 0u)) : 0u) << (2 * j);
-                okm |= (ok ? 1u : 0u) << j;
-                pos[j] = atomicAdd(&hist[t00[j]], ok ? 1 : 0);
-            }
-            own += __builtin_popcount(okm);
-#pragma unroll
-            for (int j = 0; j < kRtPer; ++j) {
-                if (!((okm >> j) & 1u)) continue;
-                const float x = pt[j].x, y = pt[j].y, z = pt[j].z;
-                const float w = __int_as_float(t00[j] == oti[j] && rt_candidate(L, x, y, z) ? 1 : 0);
-                if (pos[j] < L.staged_cap) staged[pos[j]] = make_float4(x, y, z, w);
-                else *L.overflow = 1;
-            }
-            if (halo) {
-#pragma unroll
-                for (int j = 0; j < kRtPer; ++j) {
-                    const unsigned h = (halo >> (2 * j)) & 3u;
-                    if (!h) continue;
-                    const float x = pt[j].x, y = pt[j].y, z = pt[j].z;
-                    const bool cand = rt_candidate(L, x, y, z);
-                    auto put = [&](int t) {
-                        const float4 v = make_float4(x, y, z, __int_as_float(t == oti[j] && cand ? 1 : 0));
-                        const int p2 = atomicAdd(&hist[t], 1);
-                        if (p2 < L.staged_cap) staged[p2] = v;
-                        else *L.overflow = 1;
-                    };
-                    if (h & 1u) put(t00[j] + 1);
-                    if (h & 2u) put(t00[j] + L.ntx);
-                    if (h == 3u) put(t00[j] + L.ntx + 1);
-                }
-            }
-            return;
-        }
-#endif
 #pragma unroll
         for (int j = 0; j < kRtPer; ++j) {
             const float x = pt[j].x, y = pt[j].y, z = pt[j].z;
@@ -287,24 +245,15 @@ __global__ __launch_bounds__(kRtTB) void k_rt_part(RorLaunch L, int *H, const in
             int bx, by, tx0, tx1, ty0, ty1;
             rt_bin(L, x, y, bx, by);
             rt_tiles(L, bx, by, tx0, tx1, ty0, ty1);
-            if (L.rec12) {   // 12-byte records: the tile pass recomputes the class from x, y, z and its tile
-                for (int ty = ty0; ty <= ty1; ++ty)
-                    for (int tx = tx0; tx <= tx1; ++tx) {
-                        const int pos = atomicAdd(&hist[ty * L.ntx + tx], 1);
-                        if (pos < L.staged_cap) reinterpret_cast<float3 *>(staged)[pos] = make_float3(x, y, z);
-                        else *L.overflow = 1;
-                    }
-                continue;
-            }
             const int otile = (by >> L.TBs) * L.ntx + (bx >> L.TBs);
-            const float4 q = make_float4(x, y, z, __int_as_float(rt_candidate(L, x, y, z) ? 1 : 0));
+            const int cls = rt_candidate(L, x, y, z) ? 1 : 0;
             for (int ty = ty0; ty <= ty1; ++ty)
                 for (int tx = tx0; tx <= tx1; ++tx) {
                     const int t = ty * L.ntx + tx;
-                    float4 v = q;
-                    if (t != otile) v.w = __int_as_float(0);   // a halo copy is never tested there
+                    const int w = t == otile ? cls : 0;   // a halo copy is never tested there
                     const int pos = atomicAdd(&hist[t], 1);
                     if (pos < L.staged_cap) {                   // else: overflow, the frame is redone
+                        const float4 v = make_float4(x, y, z, __int_as_float(w));
                         if (AOS_RT_NT & 4) {
                             typedef float v4f __attribute__((ext_vector_type(4)));
                             __builtin_nontemporal_store(v4f{v.x, v.y, v.z, v.w}, reinterpret_cast<v4f *>(staged + pos));
@@ -748,24 +697,17 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
     __syncthreads();
     // counting sort of a fitting tile: histogram (ranks kept in registers), scan, place
     float4 q[BIG ? 1 : kRorPer];
-    int rk[BIG ? 1 : kRorPer];
+    int rk[BIG ? 1 : kRorPer], lb[BIG ? 1 : kRorPer];
     if (!BIG) {
+        // the tile's records: all loads in flight before the first use (an index past the tile re-reads its
+        // last record, n >= 1 here; rk = -1 marks it)
+#pragma unroll
+        for (int j = 0; j < kRorPer; ++j) q[j] = staged[a + min(tid + j * kRorThreads, n - 1)];
 #pragma unroll
         for (int j = 0; j < kRorPer; ++j) {
             const int k = tid + j * kRorThreads;
-            rk[j] = -1;
-            if (k < n) {
-                if (L.rec12) {   // class: an own clip candidate (its bin's tile is this one) or a neighbour only
-                    const float3 r = reinterpret_cast<const float3 *>(staged)[a + k];
-                    int bx, by;
-                    rt_bin(L, r.x, r.y, bx, by);
-                    const bool own = (by >> L.TBs) * L.ntx + (bx >> L.TBs) == t && rt_candidate(L, r.x, r.y, r.z);
-                    q[j] = make_float4(r.x, r.y, r.z, __int_as_float(own ? 1 : 0));
-                } else {
-                    q[j] = staged[a + k];
-                }
-                rk[j] = atomicAdd(&bstart[rt_lbin(L, q[j], bx0, by0, LB) + 1], 1);
-            }
+            lb[j] = rt_lbin(L, q[j], bx0, by0, LB);
+            rk[j] = k < n ? atomicAdd(&bstart[lb[j] + 1], 1) : -1;
         }
         __syncthreads();
         if (AOS_RT_VARIANT == 3) return;   // (timing: load + histogram only)
@@ -801,12 +743,17 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < kRorPer; ++j)
-            if (rk[j] >= 0) lp_put(bstart[rt_lbin(L, q[j], bx0, by0, LB)] + rk[j], q[j]);
+            if (rk[j] >= 0) lp_put(bstart[lb[j]] + rk[j], q[j]);
         __syncthreads();
         if (AOS_RT_VARIANT == 4) return;   // (timing: load + counting sort only)
     }
     float4 *P = const_cast<float4 *>(scratch) + a;
     unsigned kept_n = 0;
+    auto local_of = [&](float4 p, int &lx, int &ly) {   // a record's bin in the tile's local grid
+        int bx, by;
+        rt_bin(L, p.x, p.y, bx, by);
+        lx = bx - bx0; ly = by - by0;
+    };
     // w: 0 a neighbour only, 1 a candidate, 2 a candidate a streaming map already found kept (the keep
     // decision is monotone as points are added: it stays kept, its cell is already in the raster)
     const bool store = kept_tile != nullptr;
@@ -862,9 +809,8 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
         const int w = __float_as_int(p.w), cls = w & kWClass;
         if (!cls) continue;                     // neighbour only
         if (cls == 2) { prev_kept(p); continue; }
-        int bx, by;
-        rt_bin(L, p.x, p.y, bx, by);
-        const int lx = bx - bx0, ly = by - by0;
+        int lx, ly;
+        local_of(p, lx, ly);
         const bool counted = BIG && (w & kWCounted);   // the store's points are counted: the new ones only
         const int nr = counted ? 9 : 3, cnt0 = AOS_RT_VARIANT == 1 ? L.need : (counted ? w >> kWCntShift : 0);
         int cnt = cnt0, budget = BIG ? kRtBudgetBig : kRtBudgetLds;
@@ -894,9 +840,8 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
             for (int i = tid; i < nq; i += kRorThreads) {
                 const int k = q_k[i];
                 const float4 p = lp_get(k);
-                int bx, by;
-                rt_bin(L, p.x, p.y, bx, by);
-                const int lx = bx - bx0, ly = by - by0;
+                int lx, ly;
+                local_of(p, lx, ly);
                 int cnt = 0, budget = kRtBudget2;
                 for (int r = 0; r < 3 && cnt < L.need && budget >= 0; ++r) {
                     int r0, r1;
@@ -920,9 +865,8 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
             for (int i = tid >> 6; i < nq2; i += kRorThreads / 64) {
                 const int k = q2_k[i];
                 const float4 p = lp_get(k);
-                int bx, by;
-                rt_bin(L, p.x, p.y, bx, by);
-                const int lx = bx - bx0, ly = by - by0;
+                int lx, ly;
+                local_of(p, lx, ly);
                 int cnt = 0;
                 for (int r = 0; r < 3 && cnt < L.need; ++r) {
                     int r0, r1;
@@ -936,9 +880,8 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
             const int k = q_k[i];
             const float4 p = BIG ? P[k] : lp_get(k);
             const int w = __float_as_int(p.w);
-            int bx, by;
-            rt_bin(L, p.x, p.y, bx, by);
-            const int lx = bx - bx0, ly = by - by0;
+            int lx, ly;
+            local_of(p, lx, ly);
             const bool counted = BIG && (w & kWCounted);
             int cnt = counted ? w >> kWCntShift : 0;
             for (int r = 0; r < (counted ? 9 : 3) && cnt < L.need; ++r) {

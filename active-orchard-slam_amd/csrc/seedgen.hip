@@ -168,9 +168,8 @@ void aos_ctx::upload_pack(void *dst, const aos_cloud_view &v, CloudSplit &sp, bo
         AOS_HIP(hipEventRecord(ev[15], stream));
         // while the DMAs run (they wait for ev[15] only): the last frame's staged array is read once so that
         // the scatter's partial-line writes hit the Infinity Cache (launch_rt_touch)
-        if (staged_touch_mode() == 1 && ror_staged_max > 0)   // (the last frame's records: ror_rec_bytes each)
-            launch_rt_touch(sorted.as<float4>(),
-                            std::min(sorted.cap / sizeof(float4), (size_t)(ror_staged_max * ror_rec_bytes / 16.0) + 1), stream);
+        if (staged_touch_mode() == 1 && ror_staged_max > 0)   // (the last frame's records)
+            launch_rt_touch(sorted.as<float4>(), std::min(sorted.cap / sizeof(float4), (size_t)ror_staged_max + 1), stream);
     }
     const uint64_t per = (n + nth - 1) / nth;
     const uint8_t *src = static_cast<const uint8_t *>(v.data);
@@ -498,13 +497,11 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
     auto geom_of = [](RorLaunch x) {
         x.cloud = nullptr; x.n = 0; x.step = x.ox = x.oy = x.oz = 0; x.staged_cap = 0; x.overflow = nullptr;
         x.big_ok = 0;
-        x.rec12 = 0;
         return x;
     };
     // the big-tile kernels run once a frame of this handle has needed them, and on every frame that cannot
     // be redone (a tiled rank, a redo); a frame that finds a big tile without them is redone (ror_collect)
     L.big_ok = ror_big_seen || !allow_guess || o.limit_box;
-    L.rec12 = 0;   // (set below for a whole-map frame without big tiles)
     if (store_ok && ms.dense == is_dense && ms.n_points == map_scan_begin && n_points >= ms.n_points) {
         const RorLaunch a = geom_of(L), b = ms.L;
         if (!std::memcmp(&a, &b, sizeof(RorLaunch))) {
@@ -558,15 +555,11 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
     }
     float4 *d_staged = stage_buf.as<float4>();
     L.staged_cap = (int)std::min<size_t>(stage_buf.cap / sizeof(float4), (size_t)INT_MAX);
-    // AOS_RT_REC12=1: 12-byte staged records (x, y, z; the tile pass recomputes the class from them and its tile), 25 %
-    // fewer bytes through the scatter's partial-line writes and the tile pass's reads. Measured and not adopted
-    // (profiles/r05k_rorbench.txt, alternating, identical raster hashes): scatter 89-90 -> 96-97 us and tile pass
-    // 122 -> 126 us on the C2 cloud; the 12-byte stores and loads are not 16-byte aligned and the class costs the
-    // VALU-bound tile pass more than the bytes saved. Never for a streaming store (its records carry kept marks and
-    // counts) nor with the big-tile kernels (they sort float4 records).
-    static const bool rec12_on = [] { const char *e = getenv("AOS_RT_REC12"); return e && atoi(e) != 0; }();
-    L.rec12 = rec12_on && !map_mode && !L.big_ok ? 1 : 0;   // (default off: measured slower, below)
-    ror_rec_bytes = L.rec12 ? 12 : 16;
+    // Records are float4 (x, y, z, w = the class). Round 5 measured and removed two other forms (rorbench, C2 cloud,
+    // identical raster hashes): 12-byte records with the class recomputed by the tile pass (scatter 89-90 -> 96-97 us,
+    // tile pass 122 -> 126: 12-byte accesses are not 16-byte aligned, profiles/r05k_rorbench.txt), and w carrying the
+    // record's local bin in its tile so the tile pass does not recompute it (tile pass unchanged at 113-115 us, scatter
+    // +2-4 us: the tile pass is not bound by that arithmetic, profiles/r05n_ror_ab.txt).
     float4 *d_scratch = static_cast<float4 *>(ror_scratch.ensure(sizeof(float4) * (size_t)L.staged_cap));
     L.overflow = reinterpret_cast<int *>(d_own + 1);
     AOS_HIP(hipEventRecord(ev[14], s));

@@ -92,7 +92,6 @@ int main(int argc, char **argv) {
     if ((double)L.r2df > L.r2) L.r2df = std::nextafter(L.r2df, 0.0f);
     L.need = 3;
     L.origin_x = minx; L.origin_y = miny; L.res = res; L.W = W; L.H = H;
-    L.rec12 = getenv("RORBENCH_REC12") ? atoi(getenv("RORBENCH_REC12")) : 0;   // (1: 12-byte staged records, not adopted)
     L.rx0 = 0; L.ry0 = 0; L.rx1 = W; L.ry1 = H; L.wx0 = 0; L.wy0 = 0; L.Wr = W;
     double est = 0.5 * (double)n;
     hipStream_t s;
