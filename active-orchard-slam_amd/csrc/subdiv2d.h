@@ -31,9 +31,8 @@
 //   * vtx[apex].firstEdge = e, and vtx[p].firstEdge = Sym of the last swap in walk order;
 //   * the rings are the cyclic orders of the final star, which the walk order of the boundary
 //     (link) edges fixes; the unique onext/oprev values are stored directly.
-// The swap loop stays as the reference path (on-edge inserts, and any cavity the DFS cannot
-// certify: a vertex seen twice, a boundary that does not close). tools/sdcheck compares the two
-// paths' complete state after every insert.
+// The swap loop stays as the reference path (on-edge inserts, and any walk that meets an apex that is
+// already a cavity vertex). tools/sdcheck compares the two paths' complete state after every insert.
 #pragma once
 #include <cstddef>
 #include <cstdint>
@@ -41,6 +40,10 @@
 #include <vector>
 
 namespace aos {
+
+// per-phase counters of a build with -DAOS_SD_PROF (tools/sdcheck/sdprof.cpp); TSC ticks
+struct SdProf { unsigned long long t_locate = 0, t_dfs = 0, t_write = 0, loc_iters = 0, dfs_steps = 0; };
+extern SdProf g_sdprof;
 
 class Subdiv2D {
   public:
@@ -95,9 +98,9 @@ class Subdiv2D {
     std::vector<int> qx;              // export buffer (Raw::qe)
     int free_q = 0, free_p = 0, recent = 0;
     bool force_loop = false, use_avx2 = false;
-    // cavity DFS scratch: stack of link edges, swapped edges with their apex, boundary edges in walk
-    // order (with their end points); per vertex (V2d) the spoke, valid while its stamp is this insert's
-    std::vector<int> dfs_stack, cav_flip, cav_apex, cav_bnd, cav_bu, cav_bv;
+    // cavity DFS scratch: stack of link edges, boundary edges in walk order (with their origins); per
+    // vertex (V2d) the spoke, valid while its stamp is this insert's
+    std::vector<int> dfs_stack, cav_bnd, cav_bu;
     int stamp = 0;
     float tlx = 0, tly = 0, brx = 0, bry = 0;
 

@@ -82,7 +82,9 @@ int main(int argc, char **argv) {
     const float m = (float)(0.2 * 1.01) + 1e-4f;
     L.bminx = L.cminx - m; L.bmaxx = L.cmaxx + m; L.bminy = L.cminy - m; L.bmaxy = L.cmaxy + m;
     L.bminz = L.cminz - m; L.bmaxz = L.cmaxz + m;
-    float cs_ = (float)(0.2 * 1.001);
+    // RORBENCH_CS: another bin side (m), e.g. 1.6 for ~66 tiles: the scatter's runs per (workgroup, tile) become
+    // line-sized (an experiment on the partition only: such tiles exceed the LDS tile pass, which then skips them)
+    float cs_ = getenv("RORBENCH_CS") ? (float)atof(getenv("RORBENCH_CS")) : (float)(0.2 * 1.001);
     const double ext = std::max((double)L.bmaxx - L.bminx, (double)L.bmaxy - L.bminy);
     if (ext / cs_ > 8192.0) cs_ = (float)(ext / 8192.0);
     L.inv_cs = 1.0f / cs_;

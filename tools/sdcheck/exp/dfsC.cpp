@@ -1,12 +1,11 @@
 // Host Delaunay with cv::Subdiv2D semantics — see subdiv2d.h. Compiled -ffp-contract=off.
-#include "subdiv2d.h"
+#include "subdiv2d.h"  // (variant dfsC: dfsA + the ring pass of wrC)
 
 #include <immintrin.h>
 
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
-#include <cstddef>
 #include <cstring>
 #include <functional>
 
@@ -311,26 +310,22 @@ AOS_AVX2 void Subdiv2D::flip_tests_avx2(const int *es, int n, const V2d &P, int 
     for (int i = 0; i < n; ++i) out[i] = (mask >> i) & 1;
 }
 
-// The ring pass of insert_cavity over plain restrict pointers (the Rec / V2d layouts as ints: a record is on[2],
-// op[2], org[2], link, pad; a vertex's spoke sits at int 7 of its 32 bytes): one pass over the boundary L_k
-// (k in walk order) writes every field of spoke S_k = x_k -> p (on / op / org in both directions), the two ring
-// links of the boundary edges next to it and vtx[x_k].firstEdge = S_k. In a function of its own the compiler keeps
-// the loop's values in registers (round 5 on the box: the replay's write phase 7.9 -> 5.3 ms with the certification
-// change below, profiles/r05s_sdprof.txt).
-__attribute__((noinline)) static void ring_pass(int *__restrict R, int *__restrict vfirst, const int *__restrict spoke,
-                                                const int *__restrict bd, const int *__restrict bu, int m, int p) {
+// wrC: the ring pass over plain restrict pointers (records as 8 ints: on[2], op[2], org[2], link, pad; spoke at
+// a 32-byte stride in the vertex records)
+__attribute__((noinline)) static void ring_write(int *__restrict R, int *__restrict vfirst, const int *__restrict spoke,
+                                                 const int *__restrict bd, const int *__restrict bu, int m, int p) {
     auto sp = [&](int x) { return spoke[8 * (size_t)x]; };
     int Sm = sp(bu[m - 1]), S = sp(bu[0]);
     for (int k = 0; k < m; ++k) {
         const int k1 = k + 1 == m ? 0 : k + 1;
         const int L = bd[k], Ln = bd[k1], x = bu[k], Sn = sp(bu[k1]);
-        R[8 * (size_t)(L >> 2) + ((L >> 1) & 1)] = S;                          // Onext(L_k) = S_k
+        R[8 * (size_t)(L >> 2) + ((L >> 1) & 1)] = S;                          // on(L) = S
         const int sLn = Ln ^ 2;
-        R[8 * (size_t)(sLn >> 2) + 2 + ((sLn >> 1) & 1)] = S;                  // Oprev(Sym L_k+1) = S_k
+        R[8 * (size_t)(sLn >> 2) + 2 + ((sLn >> 1) & 1)] = S;                  // op(Sym Ln) = S
         int *r = R + 8 * (size_t)(S >> 2);
         const int d = (S >> 1) & 1;
-        r[d] = sLn; r[2 + d] = L; r[4 + d] = x;                                // S_k: x_k -> p
-        r[d ^ 1] = Sm ^ 2; r[2 + (d ^ 1)] = Sn ^ 2; r[4 + (d ^ 1)] = p;        // Sym S_k: around p, counter-clockwise
+        r[d] = sLn; r[2 + d] = L; r[4 + d] = x;
+        r[d ^ 1] = Sm ^ 2; r[2 + (d ^ 1)] = Sn ^ 2; r[4 + (d ^ 1)] = p;
         vfirst[x] = S;
         Sm = S; S = Sn;
     }
@@ -346,7 +341,7 @@ bool Subdiv2D::insert_cavity(int e0, int p) {
     // vertex's coordinates (C2 replay 25.3-26.1 -> 25.1-25.9 ms on the box, profiles/r04z_replay_dfs.txt)
     (void)nv;
     if (++stamp >= (1 << 29)) { for (V2d &x : vd) x.stamp = 0; stamp = 1; }
-    const int sA = 2 * stamp;   // this insert's mark: a cavity vertex (the three corners and every apex)
+    const int sA = 2 * stamp, sUsed = 2 * stamp + 1;   // two marks per insert: has a spoke / on the boundary
     const int eB = lnext(e0), eA = lnext(eB);          // root link edges in walk order: eA, eB, e0
     if (lnext(eA) != e0) return false;
     const int first = org(e0), v1 = org(eB), v2 = org(eA);
@@ -358,12 +353,12 @@ bool Subdiv2D::insert_cavity(int e0, int p) {
     // scratch sized for the worst case: every swap adds one apex, one stacked edge and one boundary edge
     const size_t cap = vp.size() + 8;
     if (dfs_stack.size() < cap) {
-        dfs_stack.resize(2 * cap); cav_bnd.resize(2 * cap);
-        cav_bu.resize(2 * cap);
+        dfs_stack.resize(2 * cap); cav_flip.resize(2 * cap); cav_apex.resize(2 * cap); cav_bnd.resize(2 * cap);
+        cav_bu.resize(2 * cap); cav_bv.resize(2 * cap);
     }
-    int *stk = dfs_stack.data(), *bd = cav_bnd.data();
-    int *bu = cav_bu.data();
-    int sp = 0, nf = 0, nb = 0, last_flip = 0;
+    int *stk = dfs_stack.data(), *fl = cav_flip.data(), *ap = cav_apex.data(), *bd = cav_bnd.data();
+    int *bu = cav_bu.data(), *bv = cav_bv.data();
+    int sp = 0, nf = 0, nb = 0;
     stk[sp++] = e0; stk[sp++] = eB;
     int e = eA;
     // Pre-order walk; every test reads the old triangle right of the link edge (never incident to p).
@@ -373,61 +368,101 @@ bool Subdiv2D::insert_cavity(int e0, int p) {
     // The test is evaluated whole and combined without a branch: the orientation test is nearly always true
     // and the in-circle sum's operands are already loaded (box A/B: 28.0-28.6 -> 26.1-26.5 ms for the C2
     // seeds together with the SIMD batches compiled out of the default path, profiles/r04z_replay_dfs.txt).
-    int known = -1;   // 1: e is known to swap (decided in a batch; SIMD only)
     SDP_T0(t_dfs);
-    for (;;) {
-        SDP_INC(dfs_steps);
-        bool flip;
-        if (SIMD && known == 1) {
-            flip = true;
-        } else {
-            const int t = oprev(e);
-            const V2d &T = vd[dst(t)], &O = vd[org(e)], &D = vd[dst(e)];
+    if constexpr (!SIMD) {
+        // The walk carries the tested edge's end points: the first child of a swapped edge u -> v is w -> v
+        // (its origin the apex just found, its destination unchanged), so a descent loads only the new apex;
+        // a popped edge loads its two ends.
+        int oi = org(e), di = dst(e);
+        V2d O = vd[oi], D = vd[di];
+        for (;;) {
+            SDP_INC(dfs_steps);
+            const int t = oprev(e), w = dst(t);
+            const V2d &T = vd[w];
             const double aTDO = area(T, D, O);   // same expressions and order as swap_loop
             double val = T.n2 * area(D, P, O);
             val -= D.n2 * area(T, P, O);
             val += P.n2 * aTDO;
             val -= O.n2 * area(T, D, P);
-            flip = (aTDO > 0) & (val < -(FLT_EPSILON * 0.125));
-        }
-        known = -1;
-        if (flip) {
-            const int t = oprev(e), w = dst(t);
-            if (vd[w].stamp == sA || w == p || nf + 4 >= (int)cap) return false;   // the cavity would wrap a vertex
-            vd[w].stamp = sA;
-            vd[w].spoke = e;                                   // e becomes w -> p
-            last_flip = e; ++nf;
-            stk[sp++] = t;                                   // u -> w, after the w -> v subtree
-            e = sym(onext(sym(e)));                          // w -> v
-            continue;
-        }
-        bd[nb] = e; bu[nb] = org(e); ++nb;
-        if (SIMD) {
-            int d[4];
-            while (sp >= 4) {
-                const int b[4] = {stk[sp - 1], stk[sp - 2], stk[sp - 3], stk[sp - 4]};
-                flip_tests_avx2(b, 4, P, d);
-                int i = 0;
-                for (; i < 4 && !d[i]; ++i) {
-                    const int x = b[i];
-                    bd[nb] = x; bu[nb] = org(x); ++nb;
-                }
-                sp -= i;
-                if (i < 4) { known = 1; break; }
+            if ((aTDO > 0) & (val < -(FLT_EPSILON * 0.125))) {
+                if (T.stamp >= sA || w == p || nf + 4 >= (int)cap) return false;   // the cavity would wrap a vertex
+                vd[w].stamp = sA;
+                vd[w].spoke = e;                                 // e becomes w -> p
+                fl[nf] = e; ap[nf] = w; ++nf;
+                stk[sp++] = t;                                   // u -> w, after the w -> v subtree
+                e = sym(onext(sym(e)));                          // w -> v
+                O = T; oi = w;
+                continue;
             }
+            // a boundary edge: its origin a cavity vertex not used before, the boundary closing as it grows
+            if (vd[oi].stamp != sA || (nb > 0 && bu[nb - 1] != di)) return false;
+            vd[oi].stamp = sUsed;
+            bd[nb] = e; bu[nb] = oi; bv[nb] = di; ++nb;
+            if (sp == 0) break;
+            e = stk[--sp];
+            oi = org(e); di = dst(e);
+            O = vd[oi]; D = vd[di];
         }
-        if (sp == 0) break;
-        e = stk[--sp];
+    } else {
+    int known = -1;   // 1: e is known to swap (decided in a batch; SIMD only)
+        SDP_T0(t_dfs);
+        for (;;) {
+            SDP_INC(dfs_steps);
+            bool flip;
+            if (SIMD && known == 1) {
+                flip = true;
+            } else {
+                const int t = oprev(e);
+                const V2d &T = vd[dst(t)], &O = vd[org(e)], &D = vd[dst(e)];
+                const double aTDO = area(T, D, O);   // same expressions and order as swap_loop
+                double val = T.n2 * area(D, P, O);
+                val -= D.n2 * area(T, P, O);
+                val += P.n2 * aTDO;
+                val -= O.n2 * area(T, D, P);
+                flip = (aTDO > 0) & (val < -(FLT_EPSILON * 0.125));
+            }
+            known = -1;
+            if (flip) {
+                const int t = oprev(e), w = dst(t);
+                if (vd[w].stamp >= sA || w == p || nf + 4 >= (int)cap) return false;   // the cavity would wrap a vertex
+                vd[w].stamp = sA;
+                vd[w].spoke = e;                                   // e becomes w -> p
+                fl[nf] = e; ap[nf] = w; ++nf;
+                stk[sp++] = t;                                   // u -> w, after the w -> v subtree
+                e = sym(onext(sym(e)));                          // w -> v
+                continue;
+            }
+            {   // a boundary edge: its origin a cavity vertex not used before, the boundary closing as it grows
+                const int x = org(e), y = dst(e);
+                if (vd[x].stamp != sA || (nb > 0 && bu[nb - 1] != y)) return false;
+                vd[x].stamp = sUsed;
+                bd[nb] = e; bu[nb] = x; bv[nb] = y; ++nb;
+            }
+            if (SIMD) {
+                int d[4];
+                while (sp >= 4) {
+                    const int b[4] = {stk[sp - 1], stk[sp - 2], stk[sp - 3], stk[sp - 4]};
+                    flip_tests_avx2(b, 4, P, d);
+                    int i = 0;
+                    for (; i < 4 && !d[i]; ++i) {
+                        const int x = b[i], ox = org(x), dx = dst(x);
+                        if (vd[ox].stamp != sA || (nb > 0 && bu[nb - 1] != dx)) return false;
+                        vd[ox].stamp = sUsed;
+                        bd[nb] = x; bu[nb] = ox; bv[nb] = dx; ++nb;
+                    }
+                    sp -= i;
+                    if (i < 4) { known = 1; break; }
+                }
+            }
+            if (sp == 0) break;
+            e = stk[--sp];
+        }
     }
     SDP_ADD(t_dfs, t_dfs);
     SDP_T0(t_wr);
-    // Why no certification of the boundary is needed (round 4 checked it after the walk): by induction over the walk,
-    // a tested edge u -> v emits boundary edges forming a chain from v back to u (a leaf emits itself; a swapped
-    // edge with apex w emits the chain of w -> v, then that of u -> w), whose origins are u and the apexes below it.
-    // So the three root chains always close into one cycle of 3 + nf edges, and its vertices are distinct exactly
-    // when every apex is new, which the walk checks at each swap (the C2 replay 25.6-26.4 -> 22.6-23.1 ms on the
-    // box with ring_pass; tools/sdcheck still compares every insert's full state with the swap loop).
     const int m = nb;
+    if (m != 3 + nf || bv[0] != bu[m - 1]) return false;   // (the rest of the closure: checked as it grew)
+
     // ---- certified: the connects (reference code, they number the three new quad-edges), then
     // the bulk write of the swaps' outcome
     int base = new_edge();
@@ -440,11 +475,12 @@ bool Subdiv2D::insert_cavity(int e0, int p) {
         vd[org(base)].spoke = base;
         ce = oprev(base);
     } while (dst(ce) != first);
-    if (nf) vfirst[p] = sym(last_flip);
-    // swapEdges' setEdgePoints(e, apex, p) and vtx[apex].firstEdge = e, and the rings of the final star: ring_pass
-    static_assert(sizeof(Rec) == 32 && offsetof(Rec, op) == 8 && offsetof(Rec, org) == 16, "ring_pass: Rec layout");
-    static_assert(sizeof(V2d) == 32 && offsetof(V2d, spoke) == 28, "ring_pass: V2d layout");
-    ring_pass(reinterpret_cast<int *>(rec.data()), vfirst.data(), &vd[0].spoke, bd, bu, m, p);
+    if (nf) vfirst[p] = sym(fl[nf - 1]);
+    // One pass over the boundary L_k (x_k -> x_k+1 clockwise), k in walk order: spoke S_k = x_k -> p is the swapped
+    // edge whose apex is x_k (swapEdges: setEdgePoints(e, apex, p), vtx[apex].firstEdge = e) or a connect's edge.
+    // Around x_k the wedge between L_k and Sym L_k+1 now holds only S_k; around p the spokes run counter-clockwise.
+    // Every field of S_k's record is written here (on / op / org in both directions).
+    ring_write(reinterpret_cast<int *>(rec.data()), vfirst.data(), &vd[0].spoke, bd, bu, m, p);
     SDP_ADD(t_write, t_wr);
     return true;
 }
