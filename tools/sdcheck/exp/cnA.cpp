@@ -1,5 +1,5 @@
 // Host Delaunay with cv::Subdiv2D semantics — see subdiv2d.h. Compiled -ffp-contract=off.
-#include "subdiv2d.h"
+#include "subdiv2d.h"  // (variant cnA: the connects reduced to their quad-edge allocations)
 
 #include <immintrin.h>
 
@@ -63,12 +63,12 @@ int Subdiv2D::right_of(float px, float py, int e) const {   // isRightOf: sign o
 // newEdge: a fresh quad-edge whose primal edges are singleton rings; free quad-edges are reused LIFO
 int Subdiv2D::new_edge() {
     if (free_q <= 0) {
-        rec.push_back(Rec{});
+        rec.push_back(Rec{{0, 0}, {0, 0}, {0, 0}, 0, 0});
         free_q = (int)rec.size() - 1;
     }
     const int q = free_q, e = q * 4;
-    free_q = rec[q].h[0].x;
-    rec[q] = Rec{{Half{e, e, 0, 0}, Half{e + 2, e + 2, 0, 0}}};
+    free_q = rec[q].link;
+    rec[q] = Rec{{e, e + 2}, {e, e + 2}, {0, 0}, 0, 0};
     return e;
 }
 
@@ -86,8 +86,8 @@ int Subdiv2D::new_point(float x, float y, int type) {
 }
 
 void Subdiv2D::set_pts(int e, int o, int d) {   // setEdgePoints
-    orgr(e) = o;
-    orgr(sym(e)) = d;
+    rec[e >> 2].org[dir(e)] = o;
+    rec[e >> 2].org[dir(e) ^ 1] = d;
     vfirst[o] = e;
     vfirst[d] = sym(e);
 }
@@ -115,8 +115,8 @@ void Subdiv2D::delete_edge(int e) {   // deleteEdge
     const int se = sym(e);
     splice(se, oprev(se));
     const int q = e >> 2;
-    rec[q].h[0].on = 0;        // free marker (OpenCV: next[0] = 0)
-    rec[q].h[0].x = free_q;
+    rec[q].on[0] = 0;          // free marker (OpenCV: next[0] = 0)
+    rec[q].link = free_q;
     free_q = q;
 }
 
@@ -134,7 +134,7 @@ void Subdiv2D::init_delaunay(float rx, float ry, float rw, float rh, int rect_mo
     recent = 0;
     tlx = rx; tly = ry; brx = rx + rw; bry = ry + rh;
     vp.push_back(V2f{0.f, 0.f}); vd.push_back(V2d{0.0, 0.0, 0.0, 0, 0}); vfirst.push_back(0); vtype.push_back(-1);
-    rec.push_back(Rec{});                                                      // quad-edge 0 (NULL)
+    rec.push_back(Rec{{0, 0}, {0, 0}, {0, 0}, 0, 0});                          // quad-edge 0 (NULL)
     free_q = 0; free_p = 0;
     const int pA = new_point(rx + big, ry, 0), pB = new_point(rx, ry + big, 0), pC = new_point(rx - big, ry - big, 0);
     const int eAB = new_edge(), eBC = new_edge(), eCA = new_edge();
@@ -319,18 +319,18 @@ AOS_AVX2 void Subdiv2D::flip_tests_avx2(const int *es, int n, const V2d &P, int 
 // change below, profiles/r05s_sdprof.txt).
 __attribute__((noinline)) static void ring_pass(int *__restrict R, int *__restrict vfirst, const int *__restrict spoke,
                                                 const int *__restrict bd, const int *__restrict bu, int m, int p) {
-    // directed edge e's fields at R[2 e] (onext), R[2 e + 1] (oprev), R[2 e + 2] (origin)
     auto sp = [&](int x) { return spoke[8 * (size_t)x]; };
     int Sm = sp(bu[m - 1]), S = sp(bu[0]);
     for (int k = 0; k < m; ++k) {
         const int k1 = k + 1 == m ? 0 : k + 1;
         const int L = bd[k], Ln = bd[k1], x = bu[k], Sn = sp(bu[k1]);
-        const int sLn = Ln ^ 2, sS = S ^ 2;
-        R[2 * (ptrdiff_t)L] = S;                                       // Onext(L_k) = S_k
-        R[2 * (ptrdiff_t)sLn + 1] = S;                                 // Oprev(Sym L_k+1) = S_k
-        int *a = R + 2 * (ptrdiff_t)S, *b = R + 2 * (ptrdiff_t)sS;
-        a[0] = sLn; a[1] = L; a[2] = x;                                // S_k: x_k -> p
-        b[0] = Sm ^ 2; b[1] = Sn ^ 2; b[2] = p;                        // Sym S_k: around p, counter-clockwise
+        R[8 * (size_t)(L >> 2) + ((L >> 1) & 1)] = S;                          // Onext(L_k) = S_k
+        const int sLn = Ln ^ 2;
+        R[8 * (size_t)(sLn >> 2) + 2 + ((sLn >> 1) & 1)] = S;                  // Oprev(Sym L_k+1) = S_k
+        int *r = R + 8 * (size_t)(S >> 2);
+        const int d = (S >> 1) & 1;
+        r[d] = sLn; r[2 + d] = L; r[4 + d] = x;                                // S_k: x_k -> p
+        r[d ^ 1] = Sm ^ 2; r[2 + (d ^ 1)] = Sn ^ 2; r[4 + (d ^ 1)] = p;        // Sym S_k: around p, counter-clockwise
         vfirst[x] = S;
         Sm = S; S = Sn;
     }
@@ -428,18 +428,15 @@ bool Subdiv2D::insert_cavity(int e0, int p) {
     // when every apex is new, which the walk checks at each swap (the C2 replay 25.6-26.4 -> 22.6-23.1 ms on the
     // box with ring_pass; tools/sdcheck still compares every insert's full state with the swap loop).
     const int m = nb;
-    // ---- the outcome. OpenCV's two connectEdges (after the first newEdge + splice) number the three new quad-edges
-    // first -> p, v1 -> p, v2 -> p in that order; everything else they write (the rings of first, v1, v2 and p next to
-    // the new edges, their end points, firstEdge) is rewritten by ring_pass, which sets every field of every spoke and
-    // the ring links of the boundary edges on both sides of it. So only their allocations are kept (the C2 replay
-    // 22.6-23.1 -> 21.8-22.2 ms on the box; tools/sdcheck: identical full state after every insert).
+    // ---- certified: the connects (reference code, they number the three new quad-edges), then
+    // the bulk write of the swaps' outcome
     const int c0 = new_edge(), c1 = new_edge(), c2 = new_edge();   // first -> p, v1 -> p, v2 -> p
     vd[first].spoke = c0; vd[v1].spoke = c1; vd[v2].spoke = c2;
-    vfirst[p] = sym(nf ? last_flip : c2);   // the last setEdgePoints with p as destination
+    vfirst[p] = sym(nf ? last_flip : c2);
     // swapEdges' setEdgePoints(e, apex, p) and vtx[apex].firstEdge = e, and the rings of the final star: ring_pass
-    static_assert(sizeof(Rec) == 32 && sizeof(Half) == 16 && offsetof(Half, op) == 4 && offsetof(Half, org) == 8, "ring_pass: Rec layout");
+    static_assert(sizeof(Rec) == 32 && offsetof(Rec, op) == 8 && offsetof(Rec, org) == 16, "ring_pass: Rec layout");
     static_assert(sizeof(V2d) == 32 && offsetof(V2d, spoke) == 28, "ring_pass: V2d layout");
-    ring_pass(ri(), vfirst.data(), &vd[0].spoke, bd, bu, m, p);
+    ring_pass(reinterpret_cast<int *>(rec.data()), vfirst.data(), &vd[0].spoke, bd, bu, m, p);
     SDP_ADD(t_write, t_wr);
     return true;
 }
@@ -450,7 +447,7 @@ bool Subdiv2D::same_state(const Subdiv2D &o) const {
         return false;
     for (size_t q = 0; q < rec.size(); ++q)
         for (int d = 0; d < 2; ++d)
-            if (rec[q].h[d].on != o.rec[q].h[d].on || rec[q].h[d].op != o.rec[q].h[d].op || rec[q].h[d].org != o.rec[q].h[d].org)
+            if (rec[q].on[d] != o.rec[q].on[d] || rec[q].op[d] != o.rec[q].op[d] || rec[q].org[d] != o.rec[q].org[d])
                 return false;
     for (size_t v = 0; v < vp.size(); ++v)
         if (vfirst[v] != o.vfirst[v] || vtype[v] != o.vtype[v] || vp[v].x != o.vp[v].x || vp[v].y != o.vp[v].y)
@@ -468,9 +465,9 @@ Subdiv2D::Raw Subdiv2D::raw() {
     for (int q = 1; q < n; ++q) {
         const Rec &r = rec[q];
         int *o = &qx[8 * (size_t)q];
-        if (r.h[0].on <= 0) continue;   // free
-        o[0] = r.h[0].on; o[1] = rot3(r.h[0].op); o[2] = r.h[1].on; o[3] = rot3(r.h[1].op);
-        o[4] = r.h[0].org; o[6] = r.h[1].org;
+        if (r.on[0] <= 0) continue;   // free
+        o[0] = r.on[0]; o[1] = rot3(r.op[0]); o[2] = r.on[1]; o[3] = rot3(r.op[1]);
+        o[4] = r.org[0]; o[6] = r.org[1];
     }
     return Raw{qx.data(), n, reinterpret_cast<const float *>(vp.data()), vfirst.data(), vtype.data(), (int)vp.size()};
 }
@@ -485,9 +482,9 @@ Subdiv2D::Raw Subdiv2D::raw_into(void *dst, int chunk_recs, const std::function<
         for (int q = q0; q < q1; ++q) {   // every record written (free ones and #0 as zeros), as raw()'s zero-filled qx
             const Rec &r = rec[q];
             int o[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            if (q > 0 && r.h[0].on > 0) {
-                o[0] = r.h[0].on; o[1] = rot3(r.h[0].op); o[2] = r.h[1].on; o[3] = rot3(r.h[1].op);
-                o[4] = r.h[0].org; o[6] = r.h[1].org;
+            if (q > 0 && r.on[0] > 0) {
+                o[0] = r.on[0]; o[1] = rot3(r.op[0]); o[2] = r.on[1]; o[3] = rot3(r.op[1]);
+                o[4] = r.org[0]; o[6] = r.org[1];
             }
             std::memcpy(qe + 8 * (size_t)q, o, sizeof(o));
         }

@@ -1,5 +1,5 @@
 // Host Delaunay with cv::Subdiv2D semantics — see subdiv2d.h. Compiled -ffp-contract=off.
-#include "subdiv2d.h"
+#include "subdiv2d.h"  // (variant lay1: cnA + directed-edge halves at byte 8 e)
 
 #include <immintrin.h>
 
@@ -428,14 +428,11 @@ bool Subdiv2D::insert_cavity(int e0, int p) {
     // when every apex is new, which the walk checks at each swap (the C2 replay 25.6-26.4 -> 22.6-23.1 ms on the
     // box with ring_pass; tools/sdcheck still compares every insert's full state with the swap loop).
     const int m = nb;
-    // ---- the outcome. OpenCV's two connectEdges (after the first newEdge + splice) number the three new quad-edges
-    // first -> p, v1 -> p, v2 -> p in that order; everything else they write (the rings of first, v1, v2 and p next to
-    // the new edges, their end points, firstEdge) is rewritten by ring_pass, which sets every field of every spoke and
-    // the ring links of the boundary edges on both sides of it. So only their allocations are kept (the C2 replay
-    // 22.6-23.1 -> 21.8-22.2 ms on the box; tools/sdcheck: identical full state after every insert).
+    // ---- certified: the connects (reference code, they number the three new quad-edges), then
+    // the bulk write of the swaps' outcome
     const int c0 = new_edge(), c1 = new_edge(), c2 = new_edge();   // first -> p, v1 -> p, v2 -> p
     vd[first].spoke = c0; vd[v1].spoke = c1; vd[v2].spoke = c2;
-    vfirst[p] = sym(nf ? last_flip : c2);   // the last setEdgePoints with p as destination
+    vfirst[p] = sym(nf ? last_flip : c2);
     // swapEdges' setEdgePoints(e, apex, p) and vtx[apex].firstEdge = e, and the rings of the final star: ring_pass
     static_assert(sizeof(Rec) == 32 && sizeof(Half) == 16 && offsetof(Half, op) == 4 && offsetof(Half, org) == 8, "ring_pass: Rec layout");
     static_assert(sizeof(V2d) == 32 && offsetof(V2d, spoke) == 28, "ring_pass: V2d layout");
