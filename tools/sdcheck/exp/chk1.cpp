@@ -1,5 +1,5 @@
 // Host Delaunay with cv::Subdiv2D semantics — see subdiv2d.h. Compiled -ffp-contract=off.
-#include "subdiv2d.h"
+#include "subdiv2d.h"  // (variant chk1: redundant flip-path checks dropped, vd grows with its siblings)
 
 #include <immintrin.h>
 
