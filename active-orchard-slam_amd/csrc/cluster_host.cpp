@@ -10,6 +10,7 @@
 #include <climits>
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 #include <exception>
 #include <mutex>
 #include <numeric>
@@ -30,45 +31,78 @@ constexpr int kReplayThreads = 16;   // host threads for the exact BFS replays o
 // (float centre sums :1030-1046, first-strict-maximum endpoints :1354-1395) for the rare clusters
 // without the order-free certificate. This is a serial chain of dependent steps: it runs on the host
 // core next to the GPU (the cluster's cells come over in raster order), ~10 ns per step.
-// The FIFO BFS over the cluster's cells from its smallest (first raster) cell, into q. Membership and the
-// visited marks live in a bitmap over the cluster's bounding box when that box is small against n (row
-// clusters: a few cells wide), else in an open-addressing hash of the cells: the same order either way.
-static void bfs_order(const int *cells, int n, const GridC &g, std::vector<int> &q, std::vector<int> &tab,
-                      std::vector<uint64_t> &bm) {
-    const int dxs[8] = {-1, -1, -1, 0, 0, 1, 1, 1}, dys[8] = {-1, 0, 1, -1, 1, -1, 0, 1};
+// Raster id -> (x, y) without an integer division per cell (~25 cycles each; round 4's replay divided 5-6 times per
+// cell): the double quotient is within a few ulps of p / W, so its truncation is the quotient or one off.
+struct DivW {
+    int W; double inv;
+    explicit DivW(int w) : W(w), inv(1.0 / (double)w) {}
+    void xy(int p, int &x, int &y) const {
+        long long q = (long long)((double)p * inv);
+        if (q * W > p) --q; else if ((q + 1) * W <= p) ++q;
+        y = (int)q; x = p - (int)q * W;
+    }
+};
+struct XY { int x, y; };
+
+// The FIFO BFS over the cluster's cells from its smallest (first raster) cell, into q as (x, y). Membership and the
+// visited marks live in a bitmap over the cluster's bounding box when that box is small against n (row clusters: a
+// few cells wide), else in an open-addressing hash of the cells: the same order either way.
+// Round 5: the bitmap has a zero border of one cell, so a popped cell reads its 3 x 3 neighbourhood as three 3-bit
+// fields (unaligned 64-bit loads of a byte array) into one mask in the reference's neighbour order, and walks only the
+// set bits; the queue holds (x, y), so no division at all (C3's ~450 replays: profiles/r05y_*).
+static void bfs_order(const int *cells, int n, const GridC &g, std::vector<XY> &q, std::vector<int> &tab,
+                      std::vector<uint8_t> &bm) {
+    static const int dxs[8] = {-1, -1, -1, 0, 0, 1, 1, 1}, dys[8] = {-1, 0, 1, -1, 1, -1, 0, 1};
+    const DivW dw(g.W);
     q.resize(n);
     int start = cells[0], x0 = INT_MAX, x1 = INT_MIN, y0 = INT_MAX, y1 = INT_MIN;
     for (int k = 0; k < n; ++k) {
-        const int p = cells[k], y = p / g.W, x = p - y * g.W;
+        const int p = cells[k];
+        int x, y;
+        dw.xy(p, x, y);
         start = std::min(start, p);
         x0 = std::min(x0, x); x1 = std::max(x1, x); y0 = std::min(y0, y); y1 = std::max(y1, y);
     }
+    int sx, sy;
+    dw.xy(start, sx, sy);
     const long long bw = (long long)x1 - x0 + 1, area = bw * ((long long)y1 - y0 + 1);
     static const bool force_hash = [] { const char *e = getenv("AOS_REPLAY_HASH"); return e && atoi(e) != 0; }();
     if (!force_hash && area <= std::max<long long>(64ll * n, 1 << 16)) {   // (AOS_REPLAY_HASH=1: tests)
-        bm.assign((size_t)((area + 63) / 64), 0ull);
-        auto bit = [&](int x, int y) { return (long long)(y - y0) * bw + (x - x0); };
+        const long long pw = bw + 2, ph = (long long)y1 - y0 + 3;        // (the one-cell zero border)
+        bm.assign((size_t)((pw * ph + 7) / 8 + 16), 0);
+        uint8_t *B = bm.data();
+        auto bit = [&](int x, int y) { return (long long)(y - y0 + 1) * pw + (x - x0 + 1); };
         for (int k = 0; k < n; ++k) {
-            const int p = cells[k], y = p / g.W, x = p - y * g.W;
+            int x, y;
+            dw.xy(cells[k], x, y);
             const long long b = bit(x, y);
-            bm[(size_t)(b >> 6)] |= 1ull << (b & 63);
+            B[b >> 3] |= (uint8_t)(1u << (b & 7));
         }
-        const long long b0 = bit(start % g.W, start / g.W);
-        bm[(size_t)(b0 >> 6)] &= ~(1ull << (b0 & 63));   // set bit = in the cluster, not yet queued
-        q[0] = start;
+        const long long b0 = bit(sx, sy);
+        B[b0 >> 3] &= (uint8_t)~(1u << (b0 & 7));   // set bit = in the cluster, not yet queued
+        auto load3 = [&](long long i) {             // bits i, i + 1, i + 2 (i >= 0: the border)
+            uint64_t w;
+            std::memcpy(&w, B + (i >> 3), 8);
+            return (unsigned)(w >> (i & 7)) & 7u;
+        };
+        const long long off[8] = {-pw - 1, -1, pw - 1, -pw, pw, -pw + 1, 1, pw + 1};
+        q[0] = XY{sx, sy};
         int head = 0, tail = 1;
         while (head < tail) {
-            const int p = q[head++], cy = p / g.W, cx = p - cy * g.W;
-            for (int i = 0; i < 8; ++i) {
-                const int nx = cx + dxs[i], ny = cy + dys[i];
-                if (nx < x0 || nx > x1 || ny < y0 || ny > y1) continue;
-                const long long b = bit(nx, ny);
-                uint64_t &w = bm[(size_t)(b >> 6)];
-                const uint64_t m = 1ull << (b & 63);
-                if (!(w & m)) continue;
-                w &= ~m;
+            const XY c = q[head++];
+            const long long b = bit(c.x, c.y);
+            const unsigned rm = load3(b - pw - 1), r0 = load3(b - 1), rp = load3(b + pw - 1);
+            // the neighbour order (dx, dy) of dxs / dys: column x - 1 (rows y - 1, y, y + 1), column x (y - 1, y + 1),
+            // column x + 1 (y - 1, y, y + 1)
+            unsigned m = (rm & 1u) | (r0 & 1u) << 1 | (rp & 1u) << 2 | (rm & 2u) << 2 | (rp & 2u) << 3 | (rm & 4u) << 3 |
+                         (r0 & 4u) << 4 | (rp & 4u) << 5;
+            while (m) {
+                const int i = __builtin_ctz(m);
+                m &= m - 1;
+                const long long nb = b + off[i];
+                B[nb >> 3] &= (uint8_t)~(1u << (nb & 7));
                 if (tail >= n) throw std::runtime_error("BFS replay: cluster cells repeat");
-                q[tail++] = ny * g.W + nx;
+                q[tail++] = XY{c.x + dxs[i], c.y + dys[i]};
             }
         }
         if (tail != n) throw std::runtime_error("BFS replay: cluster is not 8-connected");
@@ -93,27 +127,28 @@ static void bfs_order(const int *cells, int n, const GridC &g, std::vector<int> 
         tab[h] = cells[k];
     }
     tab[slot_of(start)] |= (int)0x80000000;   // (start: the first raster cell; the cells come in any order)
-    q[0] = start;
+    q[0] = XY{sx, sy};
     int head = 0, tail = 1;
     while (head < tail) {
-        const int p = q[head++], cy = p / g.W, cx = p - cy * g.W;
+        const XY c = q[head++];
         for (int i = 0; i < 8; ++i) {
-            const int nx = cx + dxs[i], ny = cy + dys[i];
+            const int nx = c.x + dxs[i], ny = c.y + dys[i];
             if (nx < 0 || nx >= g.W || ny < 0 || ny >= g.H) continue;
             const int h = slot_of(ny * g.W + nx);
             if (h < 0 || tab[h] < 0) continue;
             tab[h] |= (int)0x80000000;
-            q[tail++] = ny * g.W + nx;
+            if (tail >= n) throw std::runtime_error("BFS replay: cluster cells repeat");
+            q[tail++] = XY{nx, ny};
         }
     }
     if (tail != n) throw std::runtime_error("BFS replay: cluster is not 8-connected");
 }
 
 static void host_bfs_replay(const int *cells, int n, const GridC &g, const double *poly, int np, float min_length,
-                            ClusterRec &r, std::vector<int> &q, std::vector<int> &tab, std::vector<uint64_t> &bm) {
+                            ClusterRec &r, std::vector<XY> &q, std::vector<int> &tab, std::vector<uint8_t> &bm) {
     bfs_order(cells, n, g, q, tab, bm);
     float sum_x = 0.0f, sum_y = 0.0f;
-    for (int k = 0; k < n; ++k) { int p = q[k], y = p / g.W; sum_x += (float)(p - y * g.W); sum_y += (float)y; }
+    for (int k = 0; k < n; ++k) { sum_x += (float)q[k].x; sum_y += (float)q[k].y; }
     r.cx = sum_x / (float)n;
     r.cy = sum_y / (float)n;
     bool row = false;
@@ -123,16 +158,19 @@ static void host_bfs_replay(const int *cells, int n, const GridC &g, const doubl
         row = d_pip(cwx, cwy, poly, np);
     }
     if (row) {
+        auto cw = [&](int k) {   // cell_w of the k-th BFS cell
+            return make_double2((double)cell_world(g.ox, q[k].x, g.res), (double)cell_world(g.oy, q[k].y, g.res));
+        };
         double mx = 0.0; int fi = 0; double fx = 0, fy = 0;
         for (int k = 0; k < n; ++k) {
-            double2 w = cell_w(g, q[k]);
+            double2 w = cw(k);
             double dx = w.x - r.center.x, dy = w.y - r.center.y, d2 = dx * dx + dy * dy;
             if (d2 > mx) { mx = d2; fi = k; double s = std::sqrt(d2); fx = dx / s; fy = dy / s; }
         }
         double mo = 0.0; int si = 0;
         for (int k = 0; k < n; ++k) {
             if (k == fi) continue;
-            double2 w = cell_w(g, q[k]);
+            double2 w = cw(k);
             double dx = w.x - r.center.x, dy = w.y - r.center.y, d2 = dx * dx + dy * dy;
             if (!(d2 > mo)) continue;   // (the same test, its cheap half first: the normalisation only for a new max)
             double nx = dx, ny = dy;
@@ -140,16 +178,16 @@ static void host_bfs_replay(const int *cells, int n, const GridC &g, const doubl
             if (nx * fx + ny * fy < 0.0) { mo = d2; si = k; }
         }
         if (mo == 0.0) {
-            double2 wf = cell_w(g, q[fi]);
+            double2 wf = cw(fi);
             for (int k = 0; k < n; ++k) {
                 if (k == fi) continue;
-                double2 w = cell_w(g, q[k]);
+                double2 w = cw(k);
                 double dx = w.x - wf.x, dy = w.y - wf.y, d2 = dx * dx + dy * dy;
                 if (d2 > mo) { mo = d2; si = k; }
             }
         }
-        r.start = cell_w(g, q[fi]);
-        r.end = cell_w(g, q[si]);
+        r.start = cw(fi);
+        r.end = cw(si);
     }
     r.flags = (row ? 1 : 0) | 4;  // 4: replayed
 }
@@ -163,8 +201,9 @@ void replay_clusters(const std::vector<ReplayJob> &jobs, const GridC &g, const d
     std::exception_ptr err;
     std::mutex mu;
     auto work = [&](int) {
-        std::vector<int> q, tab;
-        std::vector<uint64_t> bm;
+        std::vector<XY> q;
+        std::vector<int> tab;
+        std::vector<uint8_t> bm;
         for (int i; (i = next.fetch_add(1)) < (int)jobs.size();) {
             const ReplayJob &j = jobs[i];
             try {
