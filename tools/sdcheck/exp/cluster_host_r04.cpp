@@ -1,3 +1,4 @@
+// Round-4 form of active-orchard-slam_amd/csrc/cluster_host.cpp (namespace aos_old), kept for tools/sdcheck/bfsbench.cpp A/B only.
 // Host-side parts of the cluster stage (a8-a10), kept in a plain C++ file so the sanitizer build
 // (tests/sanitize: ASan + UBSan, no GPU) runs exactly the code the product links:
 //   * host_bfs_replay / replay_clusters: clusterOccupiedCells' FIFO BFS (seed_gen:1007-1049) and its
@@ -10,7 +11,6 @@
 #include <climits>
 #include <cmath>
 #include <cstdlib>
-#include <cstring>
 #include <exception>
 #include <mutex>
 #include <numeric>
@@ -22,7 +22,7 @@
 #include "cluster_geom.h"
 #include "cluster_seed.h"
 
-namespace aos {
+namespace aos_old { using namespace aos;
 
 constexpr int kReplayThreads = 16;   // host threads for the exact BFS replays of one frame (the box share: 16 cores)
 
@@ -31,83 +31,45 @@ constexpr int kReplayThreads = 16;   // host threads for the exact BFS replays o
 // (float centre sums :1030-1046, first-strict-maximum endpoints :1354-1395) for the rare clusters
 // without the order-free certificate. This is a serial chain of dependent steps: it runs on the host
 // core next to the GPU (the cluster's cells come over in raster order), ~10 ns per step.
-// Raster id -> (x, y) without an integer division per cell (~25 cycles each; round 4's replay divided 5-6 times per
-// cell): the double quotient is within a few ulps of p / W, so its truncation is the quotient or one off.
-struct DivW {
-    int W; double inv;
-    explicit DivW(int w) : W(w), inv(1.0 / (double)w) {}
-    void xy(int p, int &x, int &y) const {
-        long long q = (long long)((double)p * inv);
-        if (q * W > p) --q; else if ((q + 1) * W <= p) ++q;
-        y = (int)q; x = p - (int)q * W;
-    }
-};
-struct XY { int x, y; };
-
-// The FIFO BFS over the cluster's cells from its smallest (first raster) cell, into q as (x, y). Membership and the
-// visited marks live in a bitmap over the cluster's bounding box when that box is small against n (row clusters: a
-// few cells wide), else in an open-addressing hash of the cells: the same order either way.
-// Round 5: the bitmap has a zero border of one cell, so a popped cell reads its 3 x 3 neighbourhood as three 3-bit
-// fields (unaligned 64-bit loads of a byte array) into one mask in the reference's neighbour order, and walks only the
-// set bits; the queue holds (x, y), so no division at all (C3's ~450 replays: profiles/r05y_*).
-static void bfs_order(const int *cells, int n, const GridC &g, std::vector<XY> &q, std::vector<int> &tab,
-                      std::vector<uint8_t> &bm) {
-    static const int dxs[8] = {-1, -1, -1, 0, 0, 1, 1, 1}, dys[8] = {-1, 0, 1, -1, 1, -1, 0, 1};
-    const DivW dw(g.W);
+// The FIFO BFS over the cluster's cells from its smallest (first raster) cell, into q. Membership and the
+// visited marks live in a bitmap over the cluster's bounding box when that box is small against n (row
+// clusters: a few cells wide), else in an open-addressing hash of the cells: the same order either way.
+static void bfs_order(const int *cells, int n, const GridC &g, std::vector<int> &q, std::vector<int> &tab,
+                      std::vector<uint64_t> &bm) {
+    const int dxs[8] = {-1, -1, -1, 0, 0, 1, 1, 1}, dys[8] = {-1, 0, 1, -1, 1, -1, 0, 1};
     q.resize(n);
     int start = cells[0], x0 = INT_MAX, x1 = INT_MIN, y0 = INT_MAX, y1 = INT_MIN;
     for (int k = 0; k < n; ++k) {
-        const int p = cells[k];
-        int x, y;
-        dw.xy(p, x, y);
+        const int p = cells[k], y = p / g.W, x = p - y * g.W;
         start = std::min(start, p);
         x0 = std::min(x0, x); x1 = std::max(x1, x); y0 = std::min(y0, y); y1 = std::max(y1, y);
     }
-    int sx, sy;
-    dw.xy(start, sx, sy);
     const long long bw = (long long)x1 - x0 + 1, area = bw * ((long long)y1 - y0 + 1);
     static const bool force_hash = [] { const char *e = getenv("AOS_REPLAY_HASH"); return e && atoi(e) != 0; }();
     if (!force_hash && area <= std::max<long long>(64ll * n, 1 << 16)) {   // (AOS_REPLAY_HASH=1: tests)
-        // rows of RW 64-bit words over the box plus a one-cell zero border (and one spare word per row, so a 3-bit
-        // window is always inside two words); a set bit = in the cluster, not yet queued. Every access is an aligned
-        // 64-bit word: a queued cell's bit is cleared by a word store that later word loads of the same address read
-        // forwarded (round-5 first form: byte stores under unaligned 8-byte loads, which wait for the stores to retire).
-        const long long pw = bw + 2, ph = (long long)y1 - y0 + 3;
-        const long long RW = (pw + 63) / 64 + 1;
-        bm.assign((size_t)(8 * RW * ph), 0);
-        uint64_t *B = reinterpret_cast<uint64_t *>(bm.data());
-        auto setb = [&](long long r, long long c) { B[r * RW + (c >> 6)] |= 1ull << (c & 63); };
+        bm.assign((size_t)((area + 63) / 64), 0ull);
+        auto bit = [&](int x, int y) { return (long long)(y - y0) * bw + (x - x0); };
         for (int k = 0; k < n; ++k) {
-            int x, y;
-            dw.xy(cells[k], x, y);
-            setb(y - y0 + 1, x - x0 + 1);
+            const int p = cells[k], y = p / g.W, x = p - y * g.W;
+            const long long b = bit(x, y);
+            bm[(size_t)(b >> 6)] |= 1ull << (b & 63);
         }
-        {
-            const long long r = sy - y0 + 1, c = sx - x0 + 1;
-            B[r * RW + (c >> 6)] &= ~(1ull << (c & 63));
-        }
-        auto win3 = [&](long long r, long long c) {   // bits c, c + 1, c + 2 of row r (c >= 0: the border)
-            const uint64_t *w = B + r * RW + (c >> 6);
-            const unsigned __int128 v = ((unsigned __int128)w[1] << 64) | w[0];
-            return (unsigned)(v >> (c & 63)) & 7u;
-        };
-        q[0] = XY{sx, sy};
+        const long long b0 = bit(start % g.W, start / g.W);
+        bm[(size_t)(b0 >> 6)] &= ~(1ull << (b0 & 63));   // set bit = in the cluster, not yet queued
+        q[0] = start;
         int head = 0, tail = 1;
         while (head < tail) {
-            const XY c = q[head++];
-            const long long r = c.y - y0 + 1, cc = c.x - x0 + 1;
-            const unsigned rm = win3(r - 1, cc - 1), r0 = win3(r, cc - 1), rp = win3(r + 1, cc - 1);
-            // the neighbour order (dx, dy) of dxs / dys: column x - 1 (rows y - 1, y, y + 1), column x (y - 1, y + 1),
-            // column x + 1 (y - 1, y, y + 1)
-            unsigned m = (rm & 1u) | (r0 & 1u) << 1 | (rp & 1u) << 2 | (rm & 2u) << 2 | (rp & 2u) << 3 | (rm & 4u) << 3 |
-                         (r0 & 4u) << 4 | (rp & 4u) << 5;
-            while (m) {
-                const int i = __builtin_ctz(m);
-                m &= m - 1;
-                const long long nr = r + dys[i], nc = cc + dxs[i];
-                B[nr * RW + (nc >> 6)] &= ~(1ull << (nc & 63));
+            const int p = q[head++], cy = p / g.W, cx = p - cy * g.W;
+            for (int i = 0; i < 8; ++i) {
+                const int nx = cx + dxs[i], ny = cy + dys[i];
+                if (nx < x0 || nx > x1 || ny < y0 || ny > y1) continue;
+                const long long b = bit(nx, ny);
+                uint64_t &w = bm[(size_t)(b >> 6)];
+                const uint64_t m = 1ull << (b & 63);
+                if (!(w & m)) continue;
+                w &= ~m;
                 if (tail >= n) throw std::runtime_error("BFS replay: cluster cells repeat");
-                q[tail++] = XY{c.x + dxs[i], c.y + dys[i]};
+                q[tail++] = ny * g.W + nx;
             }
         }
         if (tail != n) throw std::runtime_error("BFS replay: cluster is not 8-connected");
@@ -132,28 +94,27 @@ static void bfs_order(const int *cells, int n, const GridC &g, std::vector<XY> &
         tab[h] = cells[k];
     }
     tab[slot_of(start)] |= (int)0x80000000;   // (start: the first raster cell; the cells come in any order)
-    q[0] = XY{sx, sy};
+    q[0] = start;
     int head = 0, tail = 1;
     while (head < tail) {
-        const XY c = q[head++];
+        const int p = q[head++], cy = p / g.W, cx = p - cy * g.W;
         for (int i = 0; i < 8; ++i) {
-            const int nx = c.x + dxs[i], ny = c.y + dys[i];
+            const int nx = cx + dxs[i], ny = cy + dys[i];
             if (nx < 0 || nx >= g.W || ny < 0 || ny >= g.H) continue;
             const int h = slot_of(ny * g.W + nx);
             if (h < 0 || tab[h] < 0) continue;
             tab[h] |= (int)0x80000000;
-            if (tail >= n) throw std::runtime_error("BFS replay: cluster cells repeat");
-            q[tail++] = XY{nx, ny};
+            q[tail++] = ny * g.W + nx;
         }
     }
     if (tail != n) throw std::runtime_error("BFS replay: cluster is not 8-connected");
 }
 
 static void host_bfs_replay(const int *cells, int n, const GridC &g, const double *poly, int np, float min_length,
-                            ClusterRec &r, std::vector<XY> &q, std::vector<int> &tab, std::vector<uint8_t> &bm) {
+                            ClusterRec &r, std::vector<int> &q, std::vector<int> &tab, std::vector<uint64_t> &bm) {
     bfs_order(cells, n, g, q, tab, bm);
     float sum_x = 0.0f, sum_y = 0.0f;
-    for (int k = 0; k < n; ++k) { sum_x += (float)q[k].x; sum_y += (float)q[k].y; }
+    for (int k = 0; k < n; ++k) { int p = q[k], y = p / g.W; sum_x += (float)(p - y * g.W); sum_y += (float)y; }
     r.cx = sum_x / (float)n;
     r.cy = sum_y / (float)n;
     bool row = false;
@@ -163,53 +124,33 @@ static void host_bfs_replay(const int *cells, int n, const GridC &g, const doubl
         row = d_pip(cwx, cwy, poly, np);
     }
     if (row) {
-        auto cw = [&](int k) {   // cell_w of the k-th BFS cell
-            return make_double2((double)cell_world(g.ox, q[k].x, g.res), (double)cell_world(g.oy, q[k].y, g.res));
-        };
-        // the first strict maximum of d2, then its direction (the reference normalises at every new maximum; only the
-        // last one's values survive, and they are the same operations on the same operands)
         double mx = 0.0; int fi = 0; double fx = 0, fy = 0;
         for (int k = 0; k < n; ++k) {
-            double2 w = cw(k);
+            double2 w = cell_w(g, q[k]);
             double dx = w.x - r.center.x, dy = w.y - r.center.y, d2 = dx * dx + dy * dy;
-            if (d2 > mx) { mx = d2; fi = k; }
-        }
-        if (mx > 0.0) {
-            double2 w = cw(fi);
-            double dx = w.x - r.center.x, dy = w.y - r.center.y, d2 = dx * dx + dy * dy;
-            double s = std::sqrt(d2); fx = dx / s; fy = dy / s;
+            if (d2 > mx) { mx = d2; fi = k; double s = std::sqrt(d2); fx = dx / s; fy = dy / s; }
         }
         double mo = 0.0; int si = 0;
         for (int k = 0; k < n; ++k) {
             if (k == fi) continue;
-            double2 w = cw(k);
+            double2 w = cell_w(g, q[k]);
             double dx = w.x - r.center.x, dy = w.y - r.center.y, d2 = dx * dx + dy * dy;
             if (!(d2 > mo)) continue;   // (the same test, its cheap half first: the normalisation only for a new max)
-            // the sign of the normalised dot product nx fx + ny fy is that of dx fx + dy fy whenever the latter is not
-            // within rounding of zero (both round within a few ulps of |dx fx| + |dy fy|, over s > 0); near zero the
-            // reference's own expression decides
-            const double pa = dx * fx, pb = dy * fy, dd = pa + pb;
-            bool opposite;
-            if (std::fabs(dd) > 1e-12 * (std::fabs(pa) + std::fabs(pb))) {
-                opposite = dd < 0.0;
-            } else {
-                double nx = dx, ny = dy;
-                if (d2 > 0.0) { double s = std::sqrt(d2); nx = dx / s; ny = dy / s; }
-                opposite = nx * fx + ny * fy < 0.0;
-            }
-            if (opposite) { mo = d2; si = k; }
+            double nx = dx, ny = dy;
+            if (d2 > 0.0) { double s = std::sqrt(d2); nx = dx / s; ny = dy / s; }
+            if (nx * fx + ny * fy < 0.0) { mo = d2; si = k; }
         }
         if (mo == 0.0) {
-            double2 wf = cw(fi);
+            double2 wf = cell_w(g, q[fi]);
             for (int k = 0; k < n; ++k) {
                 if (k == fi) continue;
-                double2 w = cw(k);
+                double2 w = cell_w(g, q[k]);
                 double dx = w.x - wf.x, dy = w.y - wf.y, d2 = dx * dx + dy * dy;
                 if (d2 > mo) { mo = d2; si = k; }
             }
         }
-        r.start = cw(fi);
-        r.end = cw(si);
+        r.start = cell_w(g, q[fi]);
+        r.end = cell_w(g, q[si]);
     }
     r.flags = (row ? 1 : 0) | 4;  // 4: replayed
 }
@@ -223,9 +164,8 @@ void replay_clusters(const std::vector<ReplayJob> &jobs, const GridC &g, const d
     std::exception_ptr err;
     std::mutex mu;
     auto work = [&](int) {
-        std::vector<XY> q;
-        std::vector<int> tab;
-        std::vector<uint8_t> bm;
+        std::vector<int> q, tab;
+        std::vector<uint64_t> bm;
         for (int i; (i = next.fetch_add(1)) < (int)jobs.size();) {
             const ReplayJob &j = jobs[i];
             try {
