@@ -72,7 +72,7 @@ struct aos_ctx {
     // Host -> device upload of a large pageable buffer (a PointCloud2 message): kUpThreads host
     // threads copy 2 MB chunks into rings of pinned slots, each DMA'd on the thread's stream (tools/upload_ab.py:
     // 4-8 threads and 1-8 MB chunks all upload C2's 120 MB in 3-4 ms on the box, the H2D DMA's ~40 GB/s).
-    static constexpr int kUpThreads = 16;   // capacity; up_threads() of them gather (AOS_UP_THREADS, default 8)
+    static constexpr int kUpThreads = 16;   // capacity; up_threads() of them gather (AOS_UP_THREADS, default 16)
     static int up_threads();
     static constexpr int kUpSlots = 4;      // pinned slots per thread (a ring: gather one while others DMA)
     struct Uploader {

@@ -80,10 +80,13 @@ void aos_ctx::release() {
 // handle's stream waits for all of them. The caller's buffer is only read during the call.
 // Round 4 (profiles/r04v_split_ab.txt): C2's upload ends 2.2-2.8 ms after it starts with the split at 8
 // threads, 2.4-3.8 ms without it (4 / 8 / 16 threads); the DMA no longer trails the gather.
+// Default 16 (the box's core share per GPU): the gather is bound by each core's memory bandwidth (10 M points: 160 MB
+// read, 120 MB written), and 16 threads took ~0.8 ms off the C2 frame against 8 (bench A/B, two rounds alternating:
+// frame p50 23.19-23.32 -> 22.09-22.13 ms on one box, profiles/r05zb_upload_threads.txt).
 int aos_ctx::up_threads() {
     static const int n = [] {
         const char *e = getenv("AOS_UP_THREADS");
-        return e ? std::max(1, std::min(kUpThreads, atoi(e))) : 8;
+        return e ? std::max(1, std::min(kUpThreads, atoi(e))) : kUpThreads;
     }();
     return n;
 }
