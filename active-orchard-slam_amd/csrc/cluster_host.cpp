@@ -5,6 +5,8 @@
 //   * cluster_union: the border union-find of the tiled frame's distributed cluster stage (aos_cluster_union);
 //   * assemble_rows: convertClustersToTreeRows' row arrays (seed_gen:1329-1406) and the std::sort-ed
 //     cluster_info / rows_info outputs (seed_gen:1515-1565, 2546-2582).
+#include <sched.h>
+
 #include <algorithm>
 #include <atomic>
 #include <climits>
@@ -25,6 +27,16 @@
 namespace aos {
 
 constexpr int kReplayThreads = 16;   // host threads for the exact BFS replays of one frame (the box share: 16 cores)
+
+int host_cpu_share() {
+    static const int n = [] {
+        cpu_set_t set;
+        CPU_ZERO(&set);
+        if (sched_getaffinity(0, sizeof(set), &set) != 0) return 16;
+        return std::max(1, CPU_COUNT(&set));
+    }();
+    return n;
+}
 
 // ------------------------------------------------------------------ exact BFS replay
 // clusterOccupiedCells' FIFO BFS (seed_gen:1007-1049) and the order-dependent statistics that follow
@@ -236,7 +248,7 @@ void replay_clusters(const std::vector<ReplayJob> &jobs, const GridC &g, const d
             }
         }
     };
-    const int nt = std::min<int>((int)jobs.size(), kReplayThreads);
+    const int nt = std::min<int>((int)jobs.size(), std::min(kReplayThreads, host_cpu_share()));
     if (pool) {
         pool->run(nt, work);
     } else {

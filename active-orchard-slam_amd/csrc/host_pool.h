@@ -11,6 +11,11 @@
 
 namespace aos {
 
+// CPUs of the calling thread's affinity set (read once: the first call comes from the thread that created the
+// handle); the library sizes its host thread pools to at most this (a bench that pins its CPU baseline child to one of
+// the process's cores leaves the process one core fewer: 16 gather threads on 15 cores stretched the upload's tail).
+int host_cpu_share();
+
 class HostPool {
   public:
     HostPool() = default;

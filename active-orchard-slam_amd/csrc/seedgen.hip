@@ -15,6 +15,7 @@
 
 #include "aos_ctx.h"
 #include "cloud_split.h"
+#include "host_pool.h"
 
 using namespace aos;
 
@@ -86,7 +87,7 @@ void aos_ctx::release() {
 int aos_ctx::up_threads() {
     static const int n = [] {
         const char *e = getenv("AOS_UP_THREADS");
-        return e ? std::max(1, std::min(kUpThreads, atoi(e))) : kUpThreads;
+        return e ? std::max(1, std::min(kUpThreads, atoi(e))) : std::min(kUpThreads, host_cpu_share());
     }();
     return n;
 }
