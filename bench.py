@@ -39,12 +39,15 @@ WATCHDOG_EXIT = 3      # exit status of a run whose tiled section hung (its watc
 TILED_ERROR_EXIT = 4   # exit status of a run whose tiled / tiled_stream section raised (after the main line)
 # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE summaries (tools/pmc_traffic.py) of the ROR stage, per config,
 # for the kernels of this build's ROR design. A config or design without a committed PMC run gets null.
-ROR_DESIGN = "r04v"   # (r04v: the host cloud split at upload; the partition passes read the front only)
+ROR_DESIGN = "r05"    # (r04v: the host cloud split at upload; the partition passes read the front only. r05: + the tile
+                      # pass's batched loads and branch on the exact division: the same kernels and bytes)
 PMC_FILES = {("C2", "r02"): os.path.join(ROOT, "profiles", "r02q_pmc_traffic.json"),
              ("C2", "r03"): os.path.join(ROOT, "profiles", "r03fin_pmc_traffic.json"),
              ("C2", "r04"): os.path.join(ROOT, "profiles", "r04i_pmc_traffic.json"),
              ("C2", "r04v"): os.path.join(ROOT, "profiles", "r04w_pmc_traffic.json"),
-             ("C3", "r04v"): os.path.join(ROOT, "profiles", "r05_c3_pmc_traffic.json")}
+             ("C3", "r04v"): os.path.join(ROOT, "profiles", "r05_c3_pmc_traffic.json"),
+             ("C2", "r05"): os.path.join(ROOT, "profiles", "r05zc_pmc_traffic.json"),
+             ("C3", "r05"): os.path.join(ROOT, "profiles", "r05_c3_pmc_traffic.json")}
 
 
 def parse(argv=None):
