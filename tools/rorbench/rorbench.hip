@@ -64,6 +64,24 @@ int main(int argc, char **argv) {
     const float res = 0.1f;
     const int W = (int)std::ceil(std::max(0.f, maxx - minx) / res), H = (int)std::ceil(std::max(0.f, maxy - miny) / res);
     const int WW = (W + 63) / 64;
+    // RORBENCH_STRIPS=K: the cloud grouped into K equal-width x strips of the clip box (stable within a strip), as a
+    // host split could hand over the front (the partition's (workgroup, tile) runs become ~K x longer)
+    if (const char *ks = getenv("RORBENCH_STRIPS")) {
+        const int K = atoi(ks);
+        if (K > 1) {
+            std::vector<uint8_t> out(cloud.size());
+            std::vector<uint64_t> cnt(K + 1, 0);
+            auto strip = [&](uint64_t i) {
+                float x; std::memcpy(&x, cloud.data() + 16 * i, 4);
+                int k = (int)((x - minx) / (maxx - minx) * K);
+                return k < 0 ? 0 : (k >= K ? K - 1 : k);
+            };
+            for (uint64_t i = 0; i < n; ++i) ++cnt[strip(i) + 1];
+            for (int k = 0; k < K; ++k) cnt[k + 1] += cnt[k];
+            for (uint64_t i = 0; i < n; ++i) std::memcpy(out.data() + 16 * cnt[strip(i)]++, cloud.data() + 16 * i, 16);
+            cloud.swap(out);
+        }
+    }
     if (pstep == 12)
         for (uint64_t i = 0; i < n; ++i) std::memmove(cloud.data() + 12 * i, cloud.data() + 16 * i, 12);
     uint8_t *d_cloud;
