@@ -5,8 +5,6 @@
 //   * cluster_union: the border union-find of the tiled frame's distributed cluster stage (aos_cluster_union);
 //   * assemble_rows: convertClustersToTreeRows' row arrays (seed_gen:1329-1406) and the std::sort-ed
 //     cluster_info / rows_info outputs (seed_gen:1515-1565, 2546-2582).
-#include <sched.h>
-
 #include <algorithm>
 #include <atomic>
 #include <climits>
@@ -28,15 +26,7 @@ namespace aos {
 
 constexpr int kReplayThreads = 16;   // host threads for the exact BFS replays of one frame (the box share: 16 cores)
 
-int host_cpu_share() {
-    static const int n = [] {
-        cpu_set_t set;
-        CPU_ZERO(&set);
-        if (sched_getaffinity(0, sizeof(set), &set) != 0) return 16;
-        return std::max(1, CPU_COUNT(&set));
-    }();
-    return n;
-}
+
 
 // ------------------------------------------------------------------ exact BFS replay
 // clusterOccupiedCells' FIFO BFS (seed_gen:1007-1049) and the order-dependent statistics that follow
@@ -63,7 +53,7 @@ struct XY { int x, y; };
 // fields (unaligned 64-bit loads of a byte array) into one mask in the reference's neighbour order, and walks only the
 // set bits; the queue holds (x, y), so no division at all (C3's ~450 replays: profiles/r05y_*).
 static void bfs_order(const int *cells, int n, const GridC &g, std::vector<XY> &q, std::vector<int> &tab,
-                      std::vector<uint8_t> &bm) {
+                      std::vector<uint64_t> &bm) {
     static const int dxs[8] = {-1, -1, -1, 0, 0, 1, 1, 1}, dys[8] = {-1, 0, 1, -1, 1, -1, 0, 1};
     const DivW dw(g.W);
     q.resize(n);
@@ -86,8 +76,8 @@ static void bfs_order(const int *cells, int n, const GridC &g, std::vector<XY> &
         // forwarded (round-5 first form: byte stores under unaligned 8-byte loads, which wait for the stores to retire).
         const long long pw = bw + 2, ph = (long long)y1 - y0 + 3;
         const long long RW = (pw + 63) / 64 + 1;
-        bm.assign((size_t)(8 * RW * ph), 0);
-        uint64_t *B = reinterpret_cast<uint64_t *>(bm.data());
+        bm.assign((size_t)(RW * ph), 0ull);
+        uint64_t *B = bm.data();
         auto setb = [&](long long r, long long c) { B[r * RW + (c >> 6)] |= 1ull << (c & 63); };
         for (int k = 0; k < n; ++k) {
             int x, y;
@@ -162,7 +152,7 @@ static void bfs_order(const int *cells, int n, const GridC &g, std::vector<XY> &
 }
 
 static void host_bfs_replay(const int *cells, int n, const GridC &g, const double *poly, int np, float min_length,
-                            ClusterRec &r, std::vector<XY> &q, std::vector<int> &tab, std::vector<uint8_t> &bm) {
+                            ClusterRec &r, std::vector<XY> &q, std::vector<int> &tab, std::vector<uint64_t> &bm) {
     bfs_order(cells, n, g, q, tab, bm);
     float sum_x = 0.0f, sum_y = 0.0f;
     for (int k = 0; k < n; ++k) { sum_x += (float)q[k].x; sum_y += (float)q[k].y; }
@@ -237,7 +227,7 @@ void replay_clusters(const std::vector<ReplayJob> &jobs, const GridC &g, const d
     auto work = [&](int) {
         std::vector<XY> q;
         std::vector<int> tab;
-        std::vector<uint8_t> bm;
+        std::vector<uint64_t> bm;
         for (int i; (i = next.fetch_add(1)) < (int)jobs.size();) {
             const ReplayJob &j = jobs[i];
             try {

@@ -2,6 +2,8 @@
 // seedgen.hip upload_pack). Spawning the gather threads per frame started the last of them ~0.15 ms after
 // the first; parked workers are woken together.
 #pragma once
+#include <sched.h>
+
 #include <condition_variable>
 #include <cstdint>
 #include <functional>
@@ -14,7 +16,15 @@ namespace aos {
 // CPUs of the calling thread's affinity set (read once: the first call comes from the thread that created the
 // handle); the library sizes its host thread pools to at most this (a bench that pins its CPU baseline child to one of
 // the process's cores leaves the process one core fewer: 16 gather threads on 15 cores stretched the upload's tail).
-int host_cpu_share();
+inline int host_cpu_share() {
+    static const int n = [] {
+        cpu_set_t set;
+        CPU_ZERO(&set);
+        if (sched_getaffinity(0, sizeof(set), &set) != 0) return 16;
+        return CPU_COUNT(&set) > 0 ? CPU_COUNT(&set) : 1;
+    }();
+    return n;
+}
 
 class HostPool {
   public:
