@@ -351,10 +351,8 @@ __attribute__((noinline)) static void ring_pass(int *__restrict R, int *__restri
 // the DFS cannot certify the cavity; the caller then runs the connects and the swap loop.
 template <bool SIMD>
 bool Subdiv2D::insert_cavity(int e0, int p) {
-    const size_t nv = vp.size();
     // the marks live in the vertex's own line (V2d::stamp / spoke): the DFS reads them right after the
     // vertex's coordinates (C2 replay 25.3-26.1 -> 25.1-25.9 ms on the box, profiles/r04z_replay_dfs.txt)
-    (void)nv;
     if (++stamp >= (1 << 29)) { for (V2d &x : vd) x.stamp = 0; stamp = 1; }
     const int sA = 2 * stamp;   // this insert's mark: a cavity vertex (the three corners and every apex)
     const int eB = lnext(e0), eA = lnext(eB);          // root link edges in walk order: eA, eB, e0
@@ -378,8 +376,8 @@ bool Subdiv2D::insert_cavity(int e0, int p) {
     int e = eA;
     // Pre-order walk; every test reads the old triangle right of the link edge (never incident to p).
     // The first child (w -> v) is walked at once; the second (u -> w) waits on the stack. Once the walk
-    // reaches a boundary edge it pops the stacked edges, whose tests are independent of each other:
-    // they are evaluated four at a time (AVX2) until one swaps.
+    // reaches a boundary edge it pops the stacked edges, whose tests are independent of each other (the SIMD
+    // instantiation, off by default, evaluates them four at a time until one swaps).
     // The test is evaluated whole and combined without a branch: the orientation test is nearly always true
     // and the in-circle sum's operands are already loaded (box A/B: 28.0-28.6 -> 26.1-26.5 ms for the C2
     // seeds together with the SIMD batches compiled out of the default path, profiles/r04z_replay_dfs.txt).
