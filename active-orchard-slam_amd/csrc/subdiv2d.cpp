@@ -485,22 +485,46 @@ Subdiv2D::Raw Subdiv2D::raw() {
     return Raw{qx.data(), n, reinterpret_cast<const float *>(vp.data()), vfirst.data(), vtype.data(), (int)vp.size()};
 }
 
+// Records [q0, q1) in OpenCV's layout {next[4], pt[4]} (free ones and #0 as zeros). The AVX2 form moves a record
+// with one load, one permute and one store (round 5: the export is on the frame's path between the last insert and
+// the GPU facet builder).
+static void export_recs_scalar(const int *R, int *out, int q0, int q1) {
+    auto rot3 = [](int x) { return (x & ~3) + ((x + 3) & 3); };
+    for (int q = q0; q < q1; ++q) {
+        const int *r = R + 8 * (size_t)q;   // {on, op, org, x} of Sym-direction 0, then 1
+        int o[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (q > 0 && r[0] > 0) {
+            o[0] = r[0]; o[1] = rot3(r[1]); o[2] = r[4]; o[3] = rot3(r[5]);
+            o[4] = r[2]; o[6] = r[6];
+        }
+        std::memcpy(out + 8 * (size_t)q, o, sizeof(o));
+    }
+}
+AOS_AVX2 static void export_recs_avx2(const int *R, int *out, int q0, int q1) {
+    if (q0 == 0 && q1 > 0) { export_recs_scalar(R, out, 0, 1); q0 = 1; }
+    const __m256i perm = _mm256_setr_epi32(0, 1, 4, 5, 2, 0, 6, 0);   // on0 op0 on1 op1 org0 . org1 .
+    const __m256i keep = _mm256_setr_epi32(-1, -1, -1, -1, -1, 0, -1, 0);
+    const __m256i m3 = _mm256_set1_epi32(3), not3 = _mm256_set1_epi32(~3), zero = _mm256_setzero_si256();
+    for (int q = q0; q < q1; ++q) {
+        const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(R + 8 * (size_t)q));
+        const __m256i w = _mm256_permutevar8x32_epi32(v, perm);
+        const __m256i rot = _mm256_add_epi32(_mm256_and_si256(w, not3), _mm256_and_si256(_mm256_add_epi32(w, m3), m3));
+        __m256i o = _mm256_and_si256(_mm256_blend_epi32(w, rot, 0x0a), keep);
+        const __m256i live = _mm256_cmpgt_epi32(_mm256_permutevar8x32_epi32(v, zero), zero);   // on0 > 0
+        o = _mm256_and_si256(o, live);
+        _mm256_storeu_si256(reinterpret_cast<__m256i *>(out + 8 * (size_t)q), o);
+    }
+}
+
 Subdiv2D::Raw Subdiv2D::raw_into(void *dst, int chunk_recs, const std::function<void(size_t, size_t)> &written) const {
     const int n = (int)rec.size(), nv = (int)vp.size();
     int *qe = static_cast<int *>(dst);
-    auto rot3 = [](int x) { return (x & ~3) + ((x + 3) & 3); };
+    static const bool avx2 = simd_ok();
     const int step = chunk_recs > 0 ? chunk_recs : std::max(n, 1);
     for (int q0 = 0; q0 < n; q0 += step) {
         const int q1 = std::min(n, q0 + step);
-        for (int q = q0; q < q1; ++q) {   // every record written (free ones and #0 as zeros), as raw()'s zero-filled qx
-            const Rec &r = rec[q];
-            int o[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            if (q > 0 && r.h[0].on > 0) {
-                o[0] = r.h[0].on; o[1] = rot3(r.h[0].op); o[2] = r.h[1].on; o[3] = rot3(r.h[1].op);
-                o[4] = r.h[0].org; o[6] = r.h[1].org;
-            }
-            std::memcpy(qe + 8 * (size_t)q, o, sizeof(o));
-        }
+        if (avx2) export_recs_avx2(ri(), qe, q0, q1);
+        else export_recs_scalar(ri(), qe, q0, q1);
         if (written && q1 < n) written(sizeof(int) * 8 * (size_t)q0, sizeof(int) * 8 * (size_t)(q1 - q0));
     }
     char *p = reinterpret_cast<char *>(qe + 8 * (size_t)n);
