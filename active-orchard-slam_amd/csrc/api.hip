@@ -183,6 +183,12 @@ int aos_map_append(aos_ctx *c, const aos_cloud_view *scan, int want_host, aos_se
 
 int aos_gvd_process(aos_ctx *c, const aos_gvd_in *in, aos_gvd_out *out) {
     if (!c || !in || !out) { set_error("aos_gvd_process: null argument"); return AOS_E_INVALID; }
+    // counts and their arrays (an empty seed or row list is the callbacks' early return, not an error)
+    if (in->n_seeds < 0 || in->n_rows_poses < 0 || (in->n_seeds > 0 && !in->seeds_xy) ||
+        (in->n_rows_poses > 0 && !in->rows_info_xy) || ((size_t)in->info.width * in->info.height > 0 && !in->skeleton)) {
+        set_error("aos_gvd_process: negative count, or a null array for a non-empty seed / row list or skeleton grid");
+        return AOS_E_INVALID;
+    }
     AOS_GUARD_BEGIN
     DeviceScope dev_scope(c->device);
     c->run_gvd_external(*in, *out);

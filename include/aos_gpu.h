@@ -156,6 +156,8 @@ void aos_destroy(aos_ctx *ctx);
 int aos_set_polygon(aos_ctx *ctx, const double *xy, uint32_t n_points);  /* n < 3: ignored (:253) */
 int aos_seedgen_process(aos_ctx *ctx, const aos_cloud_view *cloud, int want_host, aos_seedgen_out *out);
 int aos_seedgen_reprocess(aos_ctx *ctx, int want_host, aos_seedgen_out *out);
+/* aos_gvd_process: AOS_E_INVALID for a negative count or a null array behind a non-empty seed / row list or
+ * grid; empty lists are processGraph's early returns (status 0, published 0); non-finite seeds are filtered. */
 int aos_gvd_process(aos_ctx *ctx, const aos_gvd_in *in, aos_gvd_out *out);
 int aos_gvd_from_seedgen(aos_ctx *ctx, aos_gvd_out *out);
 /* Pipelined form: the reference runs seed-gen and the GVD as two nodes, so frame k + 1's seed-gen
