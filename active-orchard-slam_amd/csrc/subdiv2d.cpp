@@ -369,10 +369,14 @@ bool Subdiv2D::insert_cavity(int e0, int p) {
         dfs_stack.resize(2 * cap); cav_bnd.resize(2 * cap);
         cav_bu.resize(2 * cap);
     }
-    int *stk = dfs_stack.data(), *bd = cav_bnd.data();
-    int *bu = cav_bu.data();
-    int sp = 0, nf = 0, nb = 0, last_flip = 0;
-    stk[sp++] = e0; stk[sp++] = eB;
+    int *const stk = dfs_stack.data(), *const bd = cav_bnd.data(), *const bu = cav_bu.data();
+    // The stack and the boundary lists are bumped pointers and no flip counter is kept (last_flip < 0: no flip): with
+    // fewer live values the walk keeps them in registers (the flip path had reloaded four spilled base pointers and
+    // incremented a counter in memory; round 5 on the box: walk 11.7-13.3 -> 10.5-10.6 ms, the C2 replay 17.0-17.7 ->
+    // 15.8-16.2 ms, profiles/r05zq_sdprof.txt).
+    int *top = stk, *bdp = bd, *bup = bu;
+    int last_flip = -1;
+    *top++ = e0; *top++ = eB;
     int e = eA;
     // Pre-order walk; every test reads the old triangle right of the link edge (never incident to p).
     // The first child (w -> v) is walked at once; the second (u -> w) waits on the stack. Once the walk
@@ -385,12 +389,12 @@ bool Subdiv2D::insert_cavity(int e0, int p) {
     SDP_T0(t_dfs);
     for (;;) {
         SDP_INC(dfs_steps);
+        const int t = oprev(e), w = dst(t);
         bool flip;
         if (SIMD && known == 1) {
             flip = true;
         } else {
-            const int t = oprev(e);
-            const V2d &T = vd[dst(t)], &O = vd[org(e)], &D = vd[dst(e)];
+            const V2d &T = vd[w], &O = vd[org(e)], &D = vd[dst(e)];
             const double aTDO = area(T, D, O);   // same expressions and order as swap_loop
             double val = T.n2 * area(D, P, O);
             val -= D.n2 * area(T, P, O);
@@ -400,41 +404,42 @@ bool Subdiv2D::insert_cavity(int e0, int p) {
         }
         known = -1;
         if (flip) {
-            const int t = oprev(e), w = dst(t);
             // the cavity would wrap a vertex. (w is never p: p has no edge yet. The scratch cannot overflow: every
-            // swap adds a distinct vertex, so nf < vertices <= cap - 8.)
-            if (vd[w].stamp == sA) return false;
-            vd[w].stamp = sA;
-            vd[w].spoke = e;                                   // e becomes w -> p
-            last_flip = e; ++nf;
-            stk[sp++] = t;                                   // u -> w, after the w -> v subtree
-            e = sym(onext(sym(e)));                          // w -> v
+            // swap adds a distinct vertex, so the swaps are fewer than the vertices <= cap - 8.)
+            V2d &W = vd[w];
+            if (W.stamp == sA) return false;
+            W.stamp = sA;
+            W.spoke = e;                                       // e becomes w -> p
+            last_flip = e;
+            *top++ = t;                                        // u -> w, after the w -> v subtree
+            e = sym(onext(sym(e)));                            // w -> v
             continue;
         }
-        bd[nb] = e; bu[nb] = org(e); ++nb;
+        *bdp++ = e; *bup++ = org(e);
         if (SIMD) {
             int d[4];
-            while (sp >= 4) {
-                const int b[4] = {stk[sp - 1], stk[sp - 2], stk[sp - 3], stk[sp - 4]};
+            while (top - stk >= 4) {
+                const int b[4] = {top[-1], top[-2], top[-3], top[-4]};
                 flip_tests_avx2(b, 4, P, d);
                 int i = 0;
                 for (; i < 4 && !d[i]; ++i) {
                     const int x = b[i];
-                    bd[nb] = x; bu[nb] = org(x); ++nb;
+                    *bdp++ = x; *bup++ = org(x);
                 }
-                sp -= i;
+                top -= i;
                 if (i < 4) { known = 1; break; }
             }
         }
-        if (sp == 0) break;
-        e = stk[--sp];
+        if (top == stk) break;
+        e = *--top;
     }
+    const int nb = (int)(bdp - bd);
     SDP_ADD(t_dfs, t_dfs);
     SDP_T0(t_wr);
     // Why no certification of the boundary is needed (round 4 checked it after the walk): by induction over the walk,
     // a tested edge u -> v emits boundary edges forming a chain from v back to u (a leaf emits itself; a swapped
     // edge with apex w emits the chain of w -> v, then that of u -> w), whose origins are u and the apexes below it.
-    // So the three root chains always close into one cycle of 3 + nf edges, and its vertices are distinct exactly
+    // So the three root chains always close into one cycle of 3 + (swaps) edges, and its vertices are distinct exactly
     // when every apex is new, which the walk checks at each swap (the C2 replay 25.6-26.4 -> 22.6-23.1 ms on the
     // box with ring_pass; tools/sdcheck still compares every insert's full state with the swap loop).
     const int m = nb;
@@ -445,7 +450,7 @@ bool Subdiv2D::insert_cavity(int e0, int p) {
     // 22.6-23.1 -> 21.8-22.2 ms on the box; tools/sdcheck: identical full state after every insert).
     const int c0 = new_edge(), c1 = new_edge(), c2 = new_edge();   // first -> p, v1 -> p, v2 -> p
     vd[first].spoke = c0; vd[v1].spoke = c1; vd[v2].spoke = c2;
-    vfirst[p] = sym(nf ? last_flip : c2);   // the last setEdgePoints with p as destination
+    vfirst[p] = sym(last_flip >= 0 ? last_flip : c2);   // the last setEdgePoints with p as destination
     // swapEdges' setEdgePoints(e, apex, p) and vtx[apex].firstEdge = e, and the rings of the final star: ring_pass
     static_assert(sizeof(Rec) == 32 && sizeof(Half) == 16 && offsetof(Half, op) == 4 && offsetof(Half, org) == 8, "ring_pass: Rec layout");
     static_assert(sizeof(V2d) == 32 && offsetof(V2d, spoke) == 28, "ring_pass: V2d layout");
