@@ -53,7 +53,7 @@ struct XY { int x, y; };
 // fields (unaligned 64-bit loads of a byte array) into one mask in the reference's neighbour order, and walks only the
 // set bits; the queue holds (x, y), so no division at all (C3's ~450 replays: profiles/r05y_*).
 static void bfs_order(const int *cells, int n, const GridC &g, std::vector<XY> &q, std::vector<int> &tab,
-                      std::vector<uint64_t> &bm) {
+                      std::vector<uint64_t> &bm, float &sum_x, float &sum_y) {
     static const int dxs[8] = {-1, -1, -1, 0, 0, 1, 1, 1}, dys[8] = {-1, 0, 1, -1, 1, -1, 0, 1};
     const DivW dw(g.W);
     q.resize(n);
@@ -93,10 +93,15 @@ static void bfs_order(const int *cells, int n, const GridC &g, std::vector<XY> &
             const unsigned __int128 v = ((unsigned __int128)w[1] << 64) | w[0];
             return (unsigned)(v >> (c & 63)) & 7u;
         };
-        q[0] = XY{sx, sy};
+        // the centre sums ride along in pop order (the float additions of seed_gen:1030-1046 in the same order). The
+        // queue cannot overrun: a cell is queued once, when its bit is cleared, and at most n bits are set.
+        XY *const Q = q.data();
+        Q[0] = XY{sx, sy};
         int head = 0, tail = 1;
+        float ax = 0.0f, ay = 0.0f;
         while (head < tail) {
-            const XY c = q[head++];
+            const XY c = Q[head++];
+            ax += (float)c.x; ay += (float)c.y;
             const long long r = c.y - y0 + 1, cc = c.x - x0 + 1;
             const unsigned rm = win3(r - 1, cc - 1), r0 = win3(r, cc - 1), rp = win3(r + 1, cc - 1);
             // the neighbour order (dx, dy) of dxs / dys: column x - 1 (rows y - 1, y, y + 1), column x (y - 1, y + 1),
@@ -108,11 +113,11 @@ static void bfs_order(const int *cells, int n, const GridC &g, std::vector<XY> &
                 m &= m - 1;
                 const long long nr = r + dys[i], nc = cc + dxs[i];
                 B[nr * RW + (nc >> 6)] &= ~(1ull << (nc & 63));
-                if (tail >= n) throw std::runtime_error("BFS replay: cluster cells repeat");
-                q[tail++] = XY{c.x + dxs[i], c.y + dys[i]};
+                Q[tail++] = XY{c.x + dxs[i], c.y + dys[i]};
             }
         }
-        if (tail != n) throw std::runtime_error("BFS replay: cluster is not 8-connected");
+        if (tail != n) throw std::runtime_error("BFS replay: cluster is not 8-connected (or its cells repeat)");
+        sum_x = ax; sum_y = ay;
         return;
     }
     int cap = 64;
@@ -149,13 +154,15 @@ static void bfs_order(const int *cells, int n, const GridC &g, std::vector<XY> &
         }
     }
     if (tail != n) throw std::runtime_error("BFS replay: cluster is not 8-connected");
+    float ax = 0.0f, ay = 0.0f;
+    for (int k = 0; k < n; ++k) { ax += (float)q[k].x; ay += (float)q[k].y; }
+    sum_x = ax; sum_y = ay;
 }
 
 static void host_bfs_replay(const int *cells, int n, const GridC &g, const double *poly, int np, float min_length,
                             ClusterRec &r, std::vector<XY> &q, std::vector<int> &tab, std::vector<uint64_t> &bm) {
-    bfs_order(cells, n, g, q, tab, bm);
-    float sum_x = 0.0f, sum_y = 0.0f;
-    for (int k = 0; k < n; ++k) { sum_x += (float)q[k].x; sum_y += (float)q[k].y; }
+    float sum_x, sum_y;
+    bfs_order(cells, n, g, q, tab, bm, sum_x, sum_y);
     r.cx = sum_x / (float)n;
     r.cy = sum_y / (float)n;
     bool row = false;
