@@ -57,11 +57,14 @@ static void bfs_order(const int *cells, int n, const GridC &g, std::vector<XY> &
     static const int dxs[8] = {-1, -1, -1, 0, 0, 1, 1, 1}, dys[8] = {-1, 0, 1, -1, 1, -1, 0, 1};
     const DivW dw(g.W);
     q.resize(n);
+    // the cells' (x, y) go to the queue's storage first: the bitmap pass below reads them back instead of dividing again
+    XY *const Q = q.data();
     int start = cells[0], x0 = INT_MAX, x1 = INT_MIN, y0 = INT_MAX, y1 = INT_MIN;
     for (int k = 0; k < n; ++k) {
         const int p = cells[k];
         int x, y;
         dw.xy(p, x, y);
+        Q[k] = XY{x, y};
         start = std::min(start, p);
         x0 = std::min(x0, x); x1 = std::max(x1, x); y0 = std::min(y0, y); y1 = std::max(y1, y);
     }
@@ -79,11 +82,7 @@ static void bfs_order(const int *cells, int n, const GridC &g, std::vector<XY> &
         bm.assign((size_t)(RW * ph), 0ull);
         uint64_t *B = bm.data();
         auto setb = [&](long long r, long long c) { B[r * RW + (c >> 6)] |= 1ull << (c & 63); };
-        for (int k = 0; k < n; ++k) {
-            int x, y;
-            dw.xy(cells[k], x, y);
-            setb(y - y0 + 1, x - x0 + 1);
-        }
+        for (int k = 0; k < n; ++k) setb(Q[k].y - y0 + 1, Q[k].x - x0 + 1);
         {
             const long long r = sy - y0 + 1, c = sx - x0 + 1;
             B[r * RW + (c >> 6)] &= ~(1ull << (c & 63));
@@ -95,7 +94,6 @@ static void bfs_order(const int *cells, int n, const GridC &g, std::vector<XY> &
         };
         // the centre sums ride along in pop order (the float additions of seed_gen:1030-1046 in the same order). The
         // queue cannot overrun: a cell is queued once, when its bit is cleared, and at most n bits are set.
-        XY *const Q = q.data();
         Q[0] = XY{sx, sy};
         int head = 0, tail = 1;
         float ax = 0.0f, ay = 0.0f;
