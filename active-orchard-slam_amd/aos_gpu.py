@@ -267,6 +267,10 @@ def lib():
         L.aos_stream.restype = c_vp
         L.aos_stream.argtypes = [c_vp]
         L.aos_cluster_union.argtypes = [c_i, c_i, c_i, c_vp, c_i, c_vp, c_vp, c_vp, P(c_i)]
+        L.aos_debug_faults.restype = None
+        L.aos_debug_faults.argtypes = [c_i, c_u64]
+        L.aos_comm_init.restype = None
+        L.aos_comm_init.argtypes = [c_vp]
         _lib = L
     return _lib
 
@@ -591,6 +595,12 @@ class Ctx:
 
     def stream(self) -> int:
         return lib().aos_stream(self.h)
+
+
+def debug_faults(ror_stuck_rank: int = -1, a2a_round_bytes: int = 0) -> None:
+    """aos_debug_faults (test hooks, process-wide): a tiled rank that reports a stuck ROR look-back, and the
+    cluster exchange's round-size cap; the defaults turn both off."""
+    lib().aos_debug_faults(int(ror_stuck_rank), int(a2a_round_bytes))
 
 
 class Group:

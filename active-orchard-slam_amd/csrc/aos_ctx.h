@@ -143,7 +143,7 @@ struct aos_ctx {
     void thin_graphs_release();
     bool thin_first_batch(const aos::FrameGeom &g, const uint64_t *d_ibits, uint64_t *d_open, uint64_t *const bufs[2],
                           int *d_flags, int *h_flags, int *d_act, int nflags, int &batch_n, int cap_launches,
-                          const std::function<void(int)> &launch_next);
+                          const std::function<void(int)> &launch_next, const std::function<void()> &after_open);
     void thin_check_flags(const int *d_flags, const int *h_flags, int n_read, int nflags);
     uint64_t n_ror_kept = 0, n_clipped = 0;
     double ror_est_binned = 0;             // binned points of the last frame (sizes the ROR tiles)
@@ -236,9 +236,11 @@ struct aos_ctx {
     void run_seedgen(bool want_host, aos_seedgen_out &out);
     bool run_seedgen_once(bool want_host, aos_seedgen_out &out, bool allow_guess);   // true: redo
     void run_tiled(const aos_comm &cm, int tiles_x, int tiles_y, int root, bool want_host, aos_seedgen_out &out);
-    void run_tiled_frame(const aos_comm &cm, int tiles_x, int tiles_y, int root, bool want_host, aos_seedgen_out &out);
+    void run_tiled_frame(aos::FrameComm &fc, int tiles_x, int tiles_y, int root, bool want_host, aos_seedgen_out &out);
     aos_tiled_stats tstats{};   // the last tiled frame's breakdown (aos_tiled_stats_get)
-    void tile_halo_exchange(uint64_t *win, const aos::TilePlan &t, const aos_comm &cm);
+    std::vector<hipEvent_t> coll_ev;   // FrameComm: begin / end events of the frame's enqueued collectives
+    aos::DevBuf coll_red;              // FrameComm: the reduced thinning flags
+    void tile_halo_exchange(uint64_t *win, const aos::TilePlan &t, aos::FrameComm &fc);
     void run_gvd_external(const aos_gvd_in &in, aos_gvd_out &out);
     void run_gvd_from_frame(aos_gvd_out &out);
     void run_path_plan(const aos_path_graph *graph, const int8_t *skeleton, int skeleton_on_device,

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -221,8 +222,6 @@ void launch_thin_block(const uint64_t *in, uint64_t *out, const FrameGeom &g, in
 void launch_thin_pick(const int *flags, int launched, const uint64_t *b0, const uint64_t *b1, uint64_t *out, size_t n,
                       hipStream_t s, int *h_flags = nullptr, int nh = 0);
 void launch_zero_ints(int *p, int n, hipStream_t s);   // a kernel (no memset node in a captured graph)
-size_t scan_temp_bytes(int n);
-void launch_exclusive_scan(const int *in, int *out, int n, void *temp, size_t temp_bytes, hipStream_t s);
 
 // ------------------------------------------------------------------ frame helpers (seedgen.hip)
 FrameGeom frame_geom(const Poly &poly, const aos_params &P);
@@ -232,6 +231,10 @@ int thin_iterations(const int *flags, int iters_run);
 
 // ------------------------------------------------------------------ tiled frames (tiled.hip)
 struct CommError { std::string what; };
+// aos_debug_faults (test hooks): the tiled rank that reports a stuck ROR look-back (-1: none), and the
+// cluster exchange's round-size cap in bytes (0: none)
+extern std::atomic<int> g_debug_stuck_rank;
+extern std::atomic<uint64_t> g_debug_a2a_round;
 // RCCL communicator (rccl_comm.hip; aos_rccl_* in the ABI)
 void rccl_unique_id(uint8_t *id);
 aos_rccl *rccl_create(const uint8_t *id, int rank, int world, int device, uint64_t buf_bytes);
@@ -253,5 +256,43 @@ struct TilePlan {
 void free_path_state(void *p);   // path.hip
 
 TilePlan make_tile_plan(const FrameGeom &g, float margin, int tiles_x, int tiles_y, int rank);
+
+// Collectives enqueued on the frame's stream: the frame's kernels and its exchanges are ordered by the stream
+// alone, and the host waits only where it reads a result. The library's RCCL communicator provides them
+// (rccl_comm.hip); a caller's aos_comm runs through its synchronous callbacks instead. Failures throw CommError.
+struct StreamColl {
+    void *impl = nullptr;
+    void (*all_gather)(void *impl, uint64_t bytes, hipStream_t s) = nullptr;         // as aos_comm.all_gather
+    void (*gather)(void *impl, uint64_t bytes, int root, hipStream_t s) = nullptr;   // the root's recv_buf only
+    void (*max_dev)(void *impl, int32_t *d, int n, hipStream_t s) = nullptr;         // device int32, in place
+    void (*all_to_all)(void *impl, const uint64_t *counts, hipStream_t s) = nullptr; // as aos_comm.all_to_all
+};
+bool rccl_stream_coll(const aos_comm &cm, StreamColl &out);   // true: cm is the library's RCCL communicator
+
+// A tiled frame's view of its communicator (tiled.hip): the stream-ordered collectives when the communicator
+// has them, else the aos_comm callbacks (the stream is drained before each: they are called with it idle).
+// Counts the collectives and the bytes this rank sends, and times them: host clock around a callback (a
+// collective includes the wait for the slowest rank), HIP events around an enqueued one.
+struct FrameComm {
+    const aos_comm &c;
+    StreamColl sc;
+    std::vector<hipEvent_t> &ev;   // a persistent pool (the handle's): begin / end pairs of enqueued collectives
+    DevBuf &red;                   // device scratch of max_flags
+    int ev_used = 0;
+    double ms_gather = 0.0, ms_reduce = 0.0;   // host clock
+    int n_gather = 0, n_reduce = 0;
+    uint64_t bytes_sent = 0;
+    FrameComm(const aos_comm &cm, std::vector<hipEvent_t> &pool, DevBuf &scratch);
+    bool ordered() const { return sc.all_gather != nullptr; }
+    bool has_all_to_all() const { return ordered() ? sc.all_to_all != nullptr : c.all_to_all != nullptr; }
+    void all_gather(uint64_t bytes, hipStream_t s);
+    // rank r's send_buf[0, bytes) -> the root's recv_buf[r * bytes, (r + 1) * bytes); the other ranks' recv_buf is
+    // not written when the communicator has a personalised exchange (else it is an all-gather)
+    void gather(uint64_t bytes, int root, hipStream_t s);
+    void all_to_all(const uint64_t *counts, hipStream_t s);
+    void max_host(int32_t *v, int n);                            // host int32, in place (no stream involved)
+    void max_flags(const int *d, int32_t *h, int n, hipStream_t s);   // device ints -> their max over ranks in h (waits)
+    float ms_enqueued();   // the enqueued collectives' device time so far (waits for the last one)
+};
 
 }  // namespace aos

@@ -1,6 +1,7 @@
 // libaos_gpu.so — C ABI + per-handle orchestration of the seed-gen / GVD hot path on MI355X.
 // One handle = one device + one HIP stream; all stage buffers stay resident in HBM.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -52,6 +53,11 @@ using namespace aos;
         set_error(std::string("error: ") + e.what());                                                         \
         return AOS_E_STATE;                                                                                   \
     }
+
+namespace aos {
+std::atomic<int> g_debug_stuck_rank{-1};
+std::atomic<uint64_t> g_debug_a2a_round{0};
+}  // namespace aos
 
 extern "C" {
 
@@ -113,6 +119,15 @@ void aos_destroy(aos_ctx *c) {
 }
 
 void *aos_stream(aos_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+void aos_debug_faults(int32_t ror_stuck_rank, uint64_t a2a_round_bytes) {
+    aos::g_debug_stuck_rank.store(ror_stuck_rank, std::memory_order_relaxed);
+    aos::g_debug_a2a_round.store(a2a_round_bytes, std::memory_order_relaxed);
+}
+
+void aos_comm_init(aos_comm *comm) {
+    if (comm) std::memset(comm, 0, sizeof(*comm));
+}
 
 int aos_set_polygon(aos_ctx *c, const double *xy, uint32_t n) {
     if (!c) { set_error("null handle"); return AOS_E_INVALID; }

@@ -166,14 +166,13 @@ __global__ void k_segments(const Seg *segs, const int *landing, int *cells) {
 }
 
 // ------------------------------------------------------------------ collectives of variable size
-static void comm_max(const aos_comm &cm, int32_t *v, int n) {
-    if (cm.all_reduce_max(cm.user, v, n) != 0) throw CommError{"aos_comm.all_reduce_max failed"};
-}
 // All-gather of sizes[r] bytes per rank through the communicator's fixed buffers, in chunks of
 // buf_bytes: rank r's bytes land at dst + (sizes[0] + ... + sizes[r - 1]). src / dst: device or pinned host
-// memory (host ends move by kernel stores: copy_to_host / copy_from_host).
-static void gather_bytes(const aos_comm &cm, hipStream_t s, const void *src, bool src_dev,
-                         const std::vector<uint64_t> &sizes, void *dst, bool dst_dev) {
+// memory (host ends move by kernel stores: copy_to_host / copy_from_host). Stream-ordered collectives need no
+// wait between the chunks (the stream orders each chunk's copies around its all-gather); a host dst is waited for.
+static void gather_bytes(FrameComm &fc, hipStream_t s, const void *src, bool src_dev, const std::vector<uint64_t> &sizes,
+                         void *dst, bool dst_dev) {
+    const aos_comm &cm = fc.c;
     const uint64_t B = cm.buf_bytes & ~7ull;
     if (!B) throw CommError{"aos_comm.buf_bytes too small"};
     uint64_t maxb = 0;
@@ -188,8 +187,7 @@ static void gather_bytes(const aos_comm &cm, hipStream_t s, const void *src, boo
             if (src_dev) AOS_HIP(hipMemcpyAsync(cm.send_buf, p, m, hipMemcpyDeviceToDevice, s));
             else copy_from_host(cm.send_buf, p, m, s);
         }
-        AOS_HIP(hipStreamSynchronize(s));
-        if (cm.all_gather(cm.user, c) != 0) throw CommError{"aos_comm.all_gather failed"};
+        fc.all_gather(c, s);
         for (int r = 0; r < cm.world; ++r) {
             const uint64_t v = sizes[r] > off ? std::min(c, sizes[r] - off) : 0;
             if (!v) continue;
@@ -198,8 +196,8 @@ static void gather_bytes(const aos_comm &cm, hipStream_t s, const void *src, boo
             if (dst_dev) AOS_HIP(hipMemcpyAsync(d, q, v, hipMemcpyDeviceToDevice, s));
             else copy_to_host(d, q, v, s);
         }
-        AOS_HIP(hipStreamSynchronize(s));   // (the next chunk's all-gather rewrites recv_buf)
     }
+    if (!dst_dev || !fc.ordered()) AOS_HIP(hipStreamSynchronize(s));   // (host data read next / recv_buf reused)
 }
 
 template <class T> static T *dptr(DevBuf &b, size_t n) { return static_cast<T *>(b.ensure(sizeof(T) * std::max<size_t>(n, 1))); }
@@ -207,20 +205,23 @@ template <class T> static T *hptr(PinnedBuf &b, size_t n) { return static_cast<T
 
 struct OwnedOut { int l, replayed; ClusterRec r; };
 
+static uint64_t debug_a2a_round_bytes() { return g_debug_a2a_round.load(std::memory_order_relaxed); }   // (aos_debug_faults)
+
 // The personalised exchange of the long clusters' cells. cnt[s * W + d]: bytes rank s sends to rank d (known
 // on every rank). send: this rank's route buffer (device, destination-major). Returns the device buffer the
 // blocks addressed to this rank landed in and, per source s, where s's block for this rank starts in it.
-static const int *exchange_cells(const aos_comm &cm, ClusterDistState &D, hipStream_t s, const std::vector<uint64_t> &cnt,
+static const int *exchange_cells(FrameComm &fc, ClusterDistState &D, hipStream_t s, const std::vector<uint64_t> &cnt,
                                  const int *send, std::vector<uint64_t> &src_base) {
+    const aos_comm &cm = fc.c;
     const int W = cm.world, me = cm.rank;
     src_base.assign((size_t)W, 0);
     if (W == 1) return send;
     std::vector<uint64_t> row((size_t)W, 0), col((size_t)W, 0);
     for (int a = 0; a < W; ++a)
         for (int b = 0; b < W; ++b) { row[a] += cnt[(size_t)a * W + b]; col[b] += cnt[(size_t)a * W + b]; }
-    if (!cm.all_to_all) {   // through all_gather: everyone's route buffer, then this rank's blocks from it
+    if (!fc.has_all_to_all()) {   // through all_gather: everyone's route buffer, then this rank's blocks from it
         uint8_t *all = dptr<uint8_t>(D.landing, std::accumulate(row.begin(), row.end(), (uint64_t)0));
-        gather_bytes(cm, s, send, true, row, all, true);
+        gather_bytes(fc, s, send, true, row, all, true);
         uint64_t at = 0;
         for (int r = 0; r < W; ++r) {
             uint64_t pre = 0;
@@ -235,8 +236,7 @@ static const int *exchange_cells(const aos_comm &cm, ClusterDistState &D, hipStr
     int *land = dptr<int>(D.landing, roff / 4);
     // rounds of at most q bytes per pair keep every row sum <= buf_bytes and column sum <= world * buf_bytes
     uint64_t q = (cm.buf_bytes / (uint64_t)W) & ~7ull;
-    const char *qe = getenv("AOS_DEBUG_A2A_ROUND_BYTES");   // (read per call: tests set it for one frame)
-    const uint64_t q_cap = qe ? strtoull(qe, 0, 10) : 0ull;
+    const uint64_t q_cap = debug_a2a_round_bytes();   // (tests: force many rounds)
     if (q_cap) q = std::min(q, std::max<uint64_t>(8, q_cap & ~7ull));   // (tests: force many rounds)
     if (!q) throw CommError{"aos_comm.buf_bytes too small for the cluster exchange"};
     uint64_t most = 0;
@@ -254,8 +254,7 @@ static const int *exchange_cells(const aos_comm &cm, ClusterDistState &D, hipStr
                                           hipMemcpyDeviceToDevice, s));
             at += n;
         }
-        AOS_HIP(hipStreamSynchronize(s));
-        if (cm.all_to_all(cm.user, c.data()) != 0) throw CommError{"aos_comm.all_to_all failed"};
+        fc.all_to_all(c.data(), s);
         at = 0;
         for (int r = 0; r < W; ++r) {
             const uint64_t n = c[(size_t)r * W + me];
@@ -263,16 +262,17 @@ static const int *exchange_cells(const aos_comm &cm, ClusterDistState &D, hipStr
                                           static_cast<const uint8_t *>(cm.recv_buf) + at, n, hipMemcpyDeviceToDevice, s));
             at += n;
         }
-        AOS_HIP(hipStreamSynchronize(s));   // (the next round rewrites recv_buf)
+        if (!fc.ordered()) AOS_HIP(hipStreamSynchronize(s));   // (the next round rewrites recv_buf)
     }
     return land;
 }
 
 // ------------------------------------------------------------------ the rank's part of a frame
-void cluster_dist(ClusterDistState &D, const aos_comm &cm, const TilePlan &t, const FrameGeom &fg, const Poly &poly,
+void cluster_dist(ClusterDistState &D, FrameComm &fc, const TilePlan &t, const FrameGeom &fg, const Poly &poly,
                   float min_len, const uint64_t *win, int root, hipStream_t s, PreClusters &pre, ClusterDistStats &st) {
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
+    const aos_comm &cm = fc.c;
     pre = PreClusters();
     st = ClusterDistStats();
     const GridC g = make_gridc(fg);
@@ -324,7 +324,7 @@ void cluster_dist(ClusterDistState &D, const aos_comm &cm, const TilePlan &t, co
     slots[2 * me] = npieces;
     slots[2 * me + 1] = nb;
     slots[2 * world] = err ? 1 : 0;
-    comm_max(cm, slots.data(), (int)slots.size());
+    fc.max_host(slots.data(), (int)slots.size());
     if (slots[2 * world]) throw std::runtime_error("tiled cluster stage: a single-pass scan failed on a rank's device");
     std::vector<uint64_t> bsz((size_t)world);
     std::vector<int> rp0((size_t)world + 1, 0);   // first piece of rank r in the gathered table
@@ -337,7 +337,7 @@ void cluster_dist(ClusterDistState &D, const aos_comm &cm, const TilePlan &t, co
         NB += slots[2 * r + 1];
     }
     uint8_t *hall = hptr<uint8_t>(D.h_all, btot);
-    gather_bytes(cm, s, d_blob, true, bsz, hall, false);
+    gather_bytes(fc, s, d_blob, true, bsz, hall, false);
     const int NP = rp0[world];
     std::vector<PieceRec> all((size_t)NP);
     std::vector<int> proot(NP), pcl(NP), bc((size_t)NB), br((size_t)NB);
@@ -421,7 +421,7 @@ void cluster_dist(ClusterDistState &D, const aos_comm &cm, const TilePlan &t, co
         }
         // ---- 4. exchange; the owned clusters' pieces side by side; statistics
         std::vector<uint64_t> src_base;
-        const int *land = exchange_cells(cm, D, s, cnt, d_send, src_base);
+        const int *land = exchange_cells(fc, D, s, cnt, d_send, src_base);
         std::vector<int> mine_l;   // owned long clusters, by id
         for (int l = 0; l < nlong; ++l)
             if (owner[l] == me) mine_l.push_back(l);
@@ -467,7 +467,8 @@ void cluster_dist(ClusterDistState &D, const aos_comm &cm, const TilePlan &t, co
             for (int j = 0; j < nown; ++j)
                 if (orec[j].flags & 2) { flagged.push_back(j); replayed[j] = 1; }
             if (!flagged.empty()) {   // the owned flagged clusters' cells in one copy, then the exact replays
-                const int lo = coff[flagged.front()], hi = coff[flagged.back() + 1];
+                // (from a 16-byte boundary in whole 16-byte words: the copy kernel's uint4 form; d_cells has slack)
+                const int lo = coff[flagged.front()] & ~3, hi = (coff[flagged.back() + 1] + 3) & ~3;
                 int *hc = hptr<int>(D.h_cells, (size_t)(hi - lo));
                 copy_to_host(hc, d_cells + lo, sizeof(int) * (size_t)(hi - lo), s);
                 AOS_HIP(hipStreamSynchronize(s));
@@ -486,7 +487,7 @@ void cluster_dist(ClusterDistState &D, const aos_comm &cm, const TilePlan &t, co
         OwnedOut *ho = hptr<OwnedOut>(D.h_out, (size_t)std::max(nown, 1));
         for (int j = 0; j < nown; ++j) ho[j] = OwnedOut{mine_l[j], replayed[j], lrec[mine_l[j]]};
         OwnedOut *ha = hptr<OwnedOut>(D.h_tab, (size_t)nlong);
-        gather_bytes(cm, s, ho, false, rsz, ha, false);
+        gather_bytes(fc, s, ho, false, rsz, ha, false);
         int n_bfs_long = 0;   // (a replay clears the record's flag: the owners say which they replayed)
         for (int k = 0; k < nlong; ++k) {
             lrec[ha[k].l] = ha[k].r;

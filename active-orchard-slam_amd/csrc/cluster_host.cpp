@@ -52,9 +52,47 @@ struct XY { int x, y; };
 // Round 5: the bitmap has a zero border of one cell, so a popped cell reads its 3 x 3 neighbourhood as three 3-bit
 // fields (unaligned 64-bit loads of a byte array) into one mask in the reference's neighbour order, and walks only the
 // set bits; the queue holds (x, y), so no division at all (C3's ~450 replays: profiles/r05y_*).
+static const int kDxs[8] = {-1, -1, -1, 0, 0, 1, 1, 1}, kDys[8] = {-1, 0, 1, -1, 1, -1, 0, 1};
+
+// The FIFO walk over a bordered box bitmap B (RW words per row; a set bit = in the cluster, not yet queued; bit c of
+// row r = cell (x0 + c - 1, y0 + r - 1)) from (sx, sy), whose bit is already clear. Q receives the cells in pop
+// order; at most cap of them (returns -1 past it), else their number. The centre sums ride along in pop order (the
+// float additions of seed_gen:1030-1046 in the same order).
+static long long bfs_walk(uint64_t *B, long long RW, int x0, int y0, int sx, int sy, XY *Q, long long cap, float &sum_x,
+                          float &sum_y) {
+    auto win3 = [&](long long r, long long c) {   // bits c, c + 1, c + 2 of row r (c >= 0: the border)
+        const uint64_t *w = B + r * RW + (c >> 6);
+        const unsigned __int128 v = ((unsigned __int128)w[1] << 64) | w[0];
+        return (unsigned)(v >> (c & 63)) & 7u;
+    };
+    Q[0] = XY{sx, sy};
+    long long head = 0, tail = 1;
+    float ax = 0.0f, ay = 0.0f;
+    while (head < tail) {
+        const XY c = Q[head++];
+        ax += (float)c.x; ay += (float)c.y;
+        const long long r = c.y - y0 + 1, cc = c.x - x0 + 1;
+        const unsigned rm = win3(r - 1, cc - 1), r0 = win3(r, cc - 1), rp = win3(r + 1, cc - 1);
+        // the neighbour order (dx, dy) of kDxs / kDys: column x - 1 (rows y - 1, y, y + 1), column x (y - 1, y + 1),
+        // column x + 1 (y - 1, y, y + 1)
+        unsigned m = (rm & 1u) | (r0 & 1u) << 1 | (rp & 1u) << 2 | (rm & 2u) << 2 | (rp & 2u) << 3 | (rm & 4u) << 3 |
+                     (r0 & 4u) << 4 | (rp & 4u) << 5;
+        while (m) {
+            const int i = __builtin_ctz(m);
+            m &= m - 1;
+            const long long nr = r + kDys[i], nc = cc + kDxs[i];
+            B[nr * RW + (nc >> 6)] &= ~(1ull << (nc & 63));
+            if (tail >= cap) return -1;
+            Q[tail++] = XY{c.x + kDxs[i], c.y + kDys[i]};
+        }
+    }
+    sum_x = ax; sum_y = ay;
+    return tail;
+}
+
 static void bfs_order(const int *cells, int n, const GridC &g, std::vector<XY> &q, std::vector<int> &tab,
                       std::vector<uint64_t> &bm, float &sum_x, float &sum_y) {
-    static const int dxs[8] = {-1, -1, -1, 0, 0, 1, 1, 1}, dys[8] = {-1, 0, 1, -1, 1, -1, 0, 1};
+    static const int *const dxs = kDxs, *const dys = kDys;
     const DivW dw(g.W);
     q.resize(n);
     // the cells' (x, y) go to the queue's storage first: the bitmap pass below reads them back instead of dividing again
@@ -87,35 +125,8 @@ static void bfs_order(const int *cells, int n, const GridC &g, std::vector<XY> &
             const long long r = sy - y0 + 1, c = sx - x0 + 1;
             B[r * RW + (c >> 6)] &= ~(1ull << (c & 63));
         }
-        auto win3 = [&](long long r, long long c) {   // bits c, c + 1, c + 2 of row r (c >= 0: the border)
-            const uint64_t *w = B + r * RW + (c >> 6);
-            const unsigned __int128 v = ((unsigned __int128)w[1] << 64) | w[0];
-            return (unsigned)(v >> (c & 63)) & 7u;
-        };
-        // the centre sums ride along in pop order (the float additions of seed_gen:1030-1046 in the same order). The
-        // queue cannot overrun: a cell is queued once, when its bit is cleared, and at most n bits are set.
-        Q[0] = XY{sx, sy};
-        int head = 0, tail = 1;
-        float ax = 0.0f, ay = 0.0f;
-        while (head < tail) {
-            const XY c = Q[head++];
-            ax += (float)c.x; ay += (float)c.y;
-            const long long r = c.y - y0 + 1, cc = c.x - x0 + 1;
-            const unsigned rm = win3(r - 1, cc - 1), r0 = win3(r, cc - 1), rp = win3(r + 1, cc - 1);
-            // the neighbour order (dx, dy) of dxs / dys: column x - 1 (rows y - 1, y, y + 1), column x (y - 1, y + 1),
-            // column x + 1 (y - 1, y, y + 1)
-            unsigned m = (rm & 1u) | (r0 & 1u) << 1 | (rp & 1u) << 2 | (rm & 2u) << 2 | (rp & 2u) << 3 | (rm & 4u) << 3 |
-                         (r0 & 4u) << 4 | (rp & 4u) << 5;
-            while (m) {
-                const int i = __builtin_ctz(m);
-                m &= m - 1;
-                const long long nr = r + dys[i], nc = cc + dxs[i];
-                B[nr * RW + (nc >> 6)] &= ~(1ull << (nc & 63));
-                Q[tail++] = XY{c.x + dxs[i], c.y + dys[i]};
-            }
-        }
+        const long long tail = bfs_walk(B, RW, x0, y0, sx, sy, Q, n, sum_x, sum_y);
         if (tail != n) throw std::runtime_error("BFS replay: cluster is not 8-connected (or its cells repeat)");
-        sum_x = ax; sum_y = ay;
         return;
     }
     int cap = 64;
@@ -157,10 +168,59 @@ static void bfs_order(const int *cells, int n, const GridC &g, std::vector<XY> &
     sum_x = ax; sum_y = ay;
 }
 
-static void host_bfs_replay(const int *cells, int n, const GridC &g, const double *poly, int np, float min_length,
-                            ClusterRec &r, std::vector<XY> &q, std::vector<int> &tab, std::vector<uint64_t> &bm) {
+// The same walk over the frameless skeleton's bits in host memory (the published grid's read-back, bit x of word
+// y * WW + x / 64), restricted to the cluster's bounding box, from its first raster cell: no copy of the cluster's
+// cells. Inside the box the skeleton's cells reachable from the first cell are the cluster's cells unless the polygon
+// cuts the box (skeleton cells outside it are not foreground): then the walk meets more than n cells and returns
+// false (the caller replays that cluster from its cells).
+static bool bfs_order_bits(const uint64_t *bits, const GridC &g, const ClusterRec &r, std::vector<XY> &q,
+                           std::vector<uint64_t> &bm, float &sum_x, float &sum_y) {
+    const int n = r.n, x0 = r.bx0, x1 = r.bx1, y0 = r.by0, y1 = r.by1;
+    const int sy = r.first / g.W, sx = r.first - sy * g.W;
+    if (n <= 0 || x0 > x1 || y0 > y1 || sx < x0 || sx > x1 || sy < y0 || sy > y1) return false;
+    const long long bw = (long long)x1 - x0 + 1, pw = bw + 2, ph = (long long)y1 - y0 + 3;
+    const long long RW = (pw + 63) / 64 + 1;
+    bm.assign((size_t)(RW * ph), 0ull);
+    uint64_t *B = bm.data();
+    // row y of the box -> bitmap row y - y0 + 1, bit c <- cell x0 + c - 1 for c in [1, bw]; the border stays zero
+    auto src64 = [&](const uint64_t *row, long long sb) -> uint64_t {   // cells sb .. sb + 63 of a skeleton row
+        const long long w = sb >> 6;   // (sb >= -1: arithmetic shift)
+        const int o = (int)(sb & 63);
+        const uint64_t lo = (w >= 0 && w < g.WW) ? row[w] : 0ull;
+        const uint64_t hi = (w + 1 >= 0 && w + 1 < g.WW) ? row[w + 1] : 0ull;
+        return o ? (lo >> o) | (hi << (64 - o)) : lo;
+    };
+    for (int y = y0; y <= y1; ++y) {
+        const uint64_t *row = bits + (size_t)y * g.WW;
+        uint64_t *out = B + (long long)(y - y0 + 1) * RW;
+        for (long long k = 0; k * 64 < pw; ++k) {
+            uint64_t v = src64(row, (long long)x0 - 1 + 64 * k);
+            const long long c0 = 64 * k;   // bitmap bits [c0, c0 + 64): keep c in [1, bw]
+            if (c0 == 0) v &= ~1ull;
+            if (c0 + 64 > bw + 1) {
+                const long long keep = bw + 1 - c0;   // bits below keep
+                v = keep <= 0 ? 0ull : (keep >= 64 ? v : v & ((1ull << keep) - 1));
+            }
+            out[k] = v;
+        }
+    }
+    {
+        const long long rr = sy - y0 + 1, c = sx - x0 + 1;
+        if (!(B[rr * RW + (c >> 6)] >> (c & 63) & 1)) return false;   // (not a skeleton cell: records and bits disagree)
+        B[rr * RW + (c >> 6)] &= ~(1ull << (c & 63));
+    }
+    q.resize((size_t)n);
+    return bfs_walk(B, RW, x0, y0, sx, sy, q.data(), n, sum_x, sum_y) == n;
+}
+
+// cells != nullptr: replay from the cluster's cells; else from the skeleton bits (returns false when they do not give
+// the cluster, see bfs_order_bits)
+static bool host_bfs_replay(const int *cells, const uint64_t *bits, int n, const GridC &g, const double *poly, int np,
+                            float min_length, ClusterRec &r, std::vector<XY> &q, std::vector<int> &tab,
+                            std::vector<uint64_t> &bm) {
     float sum_x, sum_y;
-    bfs_order(cells, n, g, q, tab, bm, sum_x, sum_y);
+    if (cells) bfs_order(cells, n, g, q, tab, bm, sum_x, sum_y);
+    else if (!bfs_order_bits(bits, g, r, q, bm, sum_x, sum_y)) return false;
     r.cx = sum_x / (float)n;
     r.cy = sum_y / (float)n;
     bool row = false;
@@ -219,13 +279,15 @@ static void host_bfs_replay(const int *cells, int n, const GridC &g, const doubl
         r.end = cw(si);
     }
     r.flags = (row ? 1 : 0) | 4;  // 4: replayed
+    return true;
 }
 
 // The exact replays of a frame, in parallel over clusters on up to kReplayThreads host threads (each
 // writes only its own record): the pool's parked workers when one is given (no thread start per frame).
 void replay_clusters(const std::vector<ReplayJob> &jobs, const GridC &g, const double *poly, int np, float min_len,
-                     ClusterRec *rec, HostPool *pool) {
+                     ClusterRec *rec, HostPool *pool, std::vector<int> *failed) {
     if (jobs.empty()) return;
+    std::vector<char> bad(jobs.size(), 0);
     std::atomic<int> next{0};
     std::exception_ptr err;
     std::mutex mu;
@@ -236,7 +298,7 @@ void replay_clusters(const std::vector<ReplayJob> &jobs, const GridC &g, const d
         for (int i; (i = next.fetch_add(1)) < (int)jobs.size();) {
             const ReplayJob &j = jobs[i];
             try {
-                host_bfs_replay(j.cells, j.n, g, poly, np, min_len, rec[j.c], q, tab, bm);
+                if (!host_bfs_replay(j.cells, j.bits, j.n, g, poly, np, min_len, rec[j.c], q, tab, bm)) bad[i] = 1;
             } catch (...) {
                 std::lock_guard<std::mutex> lk(mu);
                 if (!err) err = std::current_exception();
@@ -253,6 +315,11 @@ void replay_clusters(const std::vector<ReplayJob> &jobs, const GridC &g, const d
         for (auto &t : th) t.join();
     }
     if (err) std::rethrow_exception(err);
+    for (size_t i = 0; i < jobs.size(); ++i) {
+        if (!bad[i]) continue;
+        if (!failed) throw std::logic_error("replay_clusters: a skeleton-bits replay failed without a fallback");
+        failed->push_back((int)i);
+    }
 }
 
 // ------------------------------------------------------------------ host union-find over pieces

@@ -24,6 +24,9 @@ struct ClusterRec {
     float length;            // cluster.length (m)
     int flags;               // bit0: row (length >= min && centre in polygon); bit1: needs BFS order
     double2 center, start, end;  // world (double from float)
+    int bx0, by0, bx1, by1;  // bounding box (cells, inclusive)
+    int first;               // first raster cell (y * W + x): where clusterOccupiedCells' BFS starts
+    int pad_;
 };
 
 // ------------------------------------------------------------------ greedy first-come de-duplication
@@ -94,6 +97,7 @@ struct ClusterSeedState {
     PinnedBuf h_cells;   // the replayed clusters' cells (one DMA; round 3's zeroed pageable vector cost ~1.5 ms at C3)
     PinnedBuf h_misc;
     int n_fg = 0, n_clusters = 0, n_rows = 0, n_cur_tab = 0;
+    int n_replay_from_bits = 0;   // the last frame's exact replays that walked the host skeleton bits
     double cur_tab_amax = -1.0;
     std::vector<ClusterRec> h_rec;
     HostPool replay_pool;   // the BFS replays' host threads (replay_clusters)
@@ -116,6 +120,9 @@ struct SeedStageIn {
     // called once the foreground count's read-back is queued (at the start with pre): the published grids'
     // D2H goes there, after k_fg, so the copy shares neither k_fg's CUs nor PCIe with that read-back
     std::function<void()> after_fg;
+    // (nullable) the frameless skeleton's bits in host memory, WW words per row, once they are there (waits for
+    // their read-back; returns null when they are not sent): the exact BFS replays walk them (cluster_host.cpp)
+    std::function<const uint64_t *()> host_skel_bits;
 };
 
 struct GridC;
@@ -125,9 +132,12 @@ void launch_cluster_stats(const int *off, const int *cells, int n_clusters, cons
                           ClusterRec *hrec = nullptr);   // hrec: pinned host copy of the records, same launch
 // exact FIFO-BFS replays (host, parallel over clusters; cluster_host.cpp); cells of a job in any order (the BFS
 // starts from the smallest), n of them
-struct ReplayJob { int c; const int *cells; int n; };
+// cells == nullptr: from bits (the frameless skeleton in host memory, WW words per row) over the record's box from its
+// first cell; a job whose bits do not give its cluster (the polygon cuts the box) leaves its record unchanged and its
+// index goes to *failed (the caller replays it from its cells)
+struct ReplayJob { int c; const int *cells; int n; const uint64_t *bits = nullptr; };
 void replay_clusters(const std::vector<ReplayJob> &jobs, const GridC &g, const double *poly, int np, float min_len,
-                     ClusterRec *rec, HostPool *pool = nullptr);
+                     ClusterRec *rec, HostPool *pool = nullptr, std::vector<int> *failed = nullptr);
 
 // a tree row as the seed kernels take it: start / end (world), k base seeds, first virtual-seed slot
 struct RowDev { double sx, sy, ex, ey; int k; int slot0; };
@@ -176,7 +186,7 @@ struct ClusterDistStats {
 // window skeleton (own cells exact). The root receives every cluster's record in pre.
 int cluster_union(int W, int H, int n_pieces, const int *piece_root, int n_border, const int *bcell, const int *broot,
                   int *piece_cluster);
-void cluster_dist(ClusterDistState &D, const aos_comm &cm, const TilePlan &t, const FrameGeom &g, const Poly &poly,
+void cluster_dist(ClusterDistState &D, FrameComm &fc, const TilePlan &t, const FrameGeom &g, const Poly &poly,
                   float min_len, const uint64_t *win, int root, hipStream_t s, PreClusters &pre, ClusterDistStats &st);
 
 // ------------------------------------------------------------------ GVD

@@ -300,16 +300,18 @@ __global__ __launch_bounds__(512) void k_cluster_stats(StatArgs A) {   // (512 t
     const int b = A.off[cid], e = A.off[cid + 1], n = e - b;
     const GridC &g = A.g;
     long long sx = 0, sy = 0;
-    int mnx = INT_MAX, mxx = INT_MIN, mny = INT_MAX, mxy = INT_MIN;
+    int mnx = INT_MAX, mxx = INT_MIN, mny = INT_MAX, mxy = INT_MIN, first = INT_MAX;
     for (int k = b + threadIdx.x; k < e; k += blockDim.x) {
         int p = A.cells[k], y = p / g.W, x = p - y * g.W;
         sx += x; sy += y;
         mnx = min(mnx, x); mxx = max(mxx, x); mny = min(mny, y); mxy = max(mxy, y);
+        first = min(first, p);
     }
     sx = block_reduce(sx, shl, AddOp());
     sy = block_reduce(sy, shl, AddOp());
     mnx = block_reduce(mnx, shi, MinOp()); mxx = block_reduce(mxx, shi, MaxOp());
     mny = block_reduce(mny, shi, MinOp()); mxy = block_reduce(mxy, shi, MaxOp());
+    first = block_reduce(first, shi, MinOp());
     // ---- max pairwise squared distance (cluster.length, seed_gen:1063-1073), pruned exactly:
     // LB = d^2 between the cells of extreme x / extreme y; a cell can belong to a farther pair only
     // if its distance to the farthest bbox corner reaches LB.
@@ -356,6 +358,7 @@ __global__ __launch_bounds__(512) void k_cluster_stats(StatArgs A) {   // (512 t
 
     ClusterRec r{};
     r.sx = sx; r.sy = sy; r.n = n; r.maxd2 = maxd2;
+    r.bx0 = mnx; r.by0 = mny; r.bx1 = mxx; r.by1 = mxy; r.first = first;
     r.flags = 0;
     const bool exact_sums = sx <= (1ll << 24) && sy <= (1ll << 24);
     r.cx = (float)sx / (float)n;       // sum_x / cells.size() (float / float)
@@ -747,23 +750,45 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         for (const auto &r : S.h_rec) n_bfs += (r.flags & 2) != 0;
         out.n_bfs = n_bfs;
         if (n_bfs) {
-            // The replayed clusters' cells come over in one copy. Replays are independent (each writes only
-            // its own ClusterRec), so they run in parallel over clusters on up to kReplayThreads host threads:
-            // at 8192^2 every row cluster needs one (sums > 2^24).
-            std::vector<long long> off(ncl + 1, 0);
-            for (int c = 0; c < ncl; ++c) off[c + 1] = off[c] + S.h_rec[c].n;
+            // Replays are independent (each writes only its own ClusterRec), so they run in parallel over clusters
+            // on up to kReplayThreads host threads: at 8192^2 every row cluster needs one (sums > 2^24). When the
+            // frameless skeleton's bits come to the host anyway (the published grid's read-back), the replays walk
+            // them over each cluster's box: no copy of the clusters' cells (C3: 7.6 MB on PCIe beside the grids'
+            // read-back, round-5 traces). The clusters the bits do not give (a polygon cutting the box), and every
+            // flagged cluster without the bits, replay from their cells, which come over in one copy.
             std::vector<int> ids;
             for (int c = 0; c < ncl; ++c)
                 if (S.h_rec[c].flags & 2) ids.push_back(c);
-            const long long lo = off[ids.front()], hi = off[ids.back() + 1];
-            int *hc = static_cast<int *>(S.h_cells.ensure(sizeof(int) * (size_t)(hi - lo)));
-            copy_to_host(hc, d_cells + lo, sizeof(int) * (hi - lo), s);
-            S.dedup.sev.sync(s);
-            tr.mark("cells");
-            std::vector<ReplayJob> jobs;
-            for (int c : ids) jobs.push_back({c, hc + (off[c] - lo), S.h_rec[c].n});
-            replay_clusters(jobs, g, hp.data(), np, static_cast<float>(in.cluster_min_length), S.h_rec.data(), &S.replay_pool);
-            tr.mark("replays");
+            const uint64_t *hbits = in.host_skel_bits ? in.host_skel_bits() : nullptr;
+            S.n_replay_from_bits = 0;
+            if (hbits) {
+                tr.mark("bits");
+                std::vector<ReplayJob> jobs;
+                for (int c : ids) jobs.push_back({c, nullptr, S.h_rec[c].n, hbits});
+                std::vector<int> failed, rest;
+                replay_clusters(jobs, g, hp.data(), np, static_cast<float>(in.cluster_min_length), S.h_rec.data(),
+                                &S.replay_pool, &failed);
+                tr.mark("replays_bits");
+                for (int i : failed) rest.push_back(jobs[i].c);
+                S.n_replay_from_bits = (int)(ids.size() - rest.size());
+                ids.swap(rest);
+            }
+            if (!ids.empty()) {
+                std::vector<long long> off(ncl + 1, 0);
+                for (int c = 0; c < ncl; ++c) off[c + 1] = off[c] + S.h_rec[c].n;
+                // from a 16-byte boundary, in whole 16-byte words (the copy kernel's uint4 form); d_cells has slack
+                // past nf (DevBuf)
+                const long long lo = off[ids.front()] & ~3LL, hi = (off[ids.back() + 1] + 3) & ~3LL;
+                int *hc = static_cast<int *>(S.h_cells.ensure(sizeof(int) * (size_t)(hi - lo)));
+                copy_to_host(hc, d_cells + lo, sizeof(int) * (hi - lo), s);
+                S.dedup.sev.sync(s);
+                tr.mark("cells");
+                std::vector<ReplayJob> jobs;
+                for (int c : ids) jobs.push_back({c, hc + (off[c] - lo), S.h_rec[c].n});
+                replay_clusters(jobs, g, hp.data(), np, static_cast<float>(in.cluster_min_length), S.h_rec.data(),
+                                &S.replay_pool);
+                tr.mark("replays");
+            }
         }
     }
     assemble_rows(S.h_rec, out, rows);   // (host: cluster_host.cpp)

@@ -82,42 +82,106 @@ int *LookBackScratch::err_word(hipStream_t s) {
 }
 
 // ------------------------------------------------------------------ single-pass scan
-constexpr int kScanTB = 256, kScanPer = 8, kScanTile = kScanTB * kScanPer;
+// out[i] = in[0] + ... + in[i - 1] for i in [0, n] (out[n] = the total); zero_in: in[0, n) is left zero.
+// A block scans kScanTile ints. Its loads and stores are lane-contiguous 16-byte words: thread t moves ints
+// [4t, 4t + 4) of each of the tile's kScanPer / 4 quarters, so a wave instruction covers 1 KB of consecutive
+// memory (round 5 read 8 consecutive ints per lane as dwords at a 32-byte lane stride: 2 KB touched per 256 B
+// moved). The quarters are scanned one after another inside the block, then the blocks chain by a decoupled
+// look-back. Problems of at most kScanSmall + 1 ints take one workgroup with a running carry (no ticket, no
+// look-back words).
+constexpr int kScanTB = 256, kScanPer = 8, kScanTile = kScanTB * kScanPer, kScanQ = kScanPer / 4;
+constexpr int kScanSmallTB = 1024, kScanSmall = 16 * 1024;
+
+template <bool VEC>
+__device__ __forceinline__ int4 scan_load4(const int *in, long long i, int n) {
+    if (VEC && i + 4 <= n) return *reinterpret_cast<const int4 *>(in + i);
+    int4 v;
+    v.x = i < n ? in[i] : 0;
+    v.y = i + 1 < n ? in[i + 1] : 0;
+    v.z = i + 2 < n ? in[i + 2] : 0;
+    v.w = i + 3 < n ? in[i + 3] : 0;
+    return v;
+}
+// exclusive prefixes of v (starting at acc) -> out[i .. i + 3], the entries <= n
+template <bool VEC>
+__device__ __forceinline__ void scan_store4(int *out, long long i, int n, int4 v, int acc) {
+    int4 o;
+    o.x = acc; o.y = o.x + v.x; o.z = o.y + v.y; o.w = o.z + v.z;
+    if (VEC && i + 4 <= n + 1) { *reinterpret_cast<int4 *>(out + i) = o; return; }
+    if (i <= n) out[i] = o.x;
+    if (i + 1 <= n) out[i + 1] = o.y;
+    if (i + 2 <= n) out[i + 2] = o.z;
+    if (i + 3 <= n) out[i + 3] = o.w;
+}
+template <bool VEC>
+__device__ __forceinline__ void scan_zero4(int *in, long long i, int n) {
+    if (VEC && i + 4 <= n) { *reinterpret_cast<int4 *>(in + i) = make_int4(0, 0, 0, 0); return; }
+    for (int k = 0; k < 4; ++k)
+        if (i + k < n) in[i + k] = 0;
+}
+
+template <bool VEC>
 __global__ __launch_bounds__(kScanTB) void k_scan_1p(int *in, int *out, int n, int zero_in, LookBack L) {
     __shared__ int sh_vid, wsum[kScanTB / 64], sh_excl;
     const int vid = lb_block_id(L, &sh_vid);
-    const long long base = (long long)vid * kScanTile + (long long)threadIdx.x * kScanPer;
-    int v[kScanPer], run = 0;
+    const long long base = (long long)vid * kScanTile + 4LL * threadIdx.x;
+    int4 v[kScanQ];
+    int run[kScanQ];
 #pragma unroll
-    for (int k = 0; k < kScanPer; ++k) {
-        const long long i = base + k;
-        v[k] = i < n ? in[i] : 0;
-        run += v[k];
+    for (int q = 0; q < kScanQ; ++q) {
+        v[q] = scan_load4<VEC>(in, base + (long long)q * 4 * kScanTB, n);
+        run[q] = v[q].x + v[q].y + v[q].z + v[q].w;
     }
     if (zero_in)
 #pragma unroll
-        for (int k = 0; k < kScanPer; ++k)
-            if (base + k < n) in[base + k] = 0;
-    int agg;
-    const int before = block_excl_scan<kScanTB>(run, wsum, &agg);
+        for (int q = 0; q < kScanQ; ++q) scan_zero4<VEC>(in, base + (long long)q * 4 * kScanTB, n);
+    int before[kScanQ], tot[kScanQ], agg = 0;
+#pragma unroll
+    for (int q = 0; q < kScanQ; ++q) {
+        before[q] = block_excl_scan<kScanTB>(run[q], wsum, &tot[q]);
+        agg += tot[q];
+    }
     if (threadIdx.x < 64) {
         const unsigned e = lb_exclusive(L, vid, (unsigned)agg);
         if (threadIdx.x == 0) sh_excl = (int)e;
     }
     __syncthreads();
-    int acc = sh_excl + before;
+    int acc = sh_excl;
 #pragma unroll
-    for (int k = 0; k < kScanPer; ++k) {
-        const long long i = base + k;
-        if (i <= n) out[i] = acc;
-        acc += v[k];
+    for (int q = 0; q < kScanQ; ++q) {
+        scan_store4<VEC>(out, base + (long long)q * 4 * kScanTB, n, v[q], acc + before[q]);
+        acc += tot[q];
+    }
+}
+
+// one workgroup, n + 1 <= kScanSmall + 1: tiles of 4 kScanSmallTB ints with a running carry
+template <bool VEC>
+__global__ __launch_bounds__(kScanSmallTB) void k_scan_small(int *in, int *out, int n, int zero_in) {
+    __shared__ int wsum[kScanSmallTB / 64];
+    int carry = 0;
+    for (long long t0 = 0; t0 <= n; t0 += 4 * kScanSmallTB) {
+        const long long i = t0 + 4LL * threadIdx.x;
+        const int4 v = scan_load4<VEC>(in, i, n);
+        if (zero_in) scan_zero4<VEC>(in, i, n);
+        int tot;
+        const int before = block_excl_scan<kScanSmallTB>(v.x + v.y + v.z + v.w, wsum, &tot);
+        scan_store4<VEC>(out, i, n, v, carry + before);
+        carry += tot;
     }
 }
 
 void scan_1p(LookBackScratch &lb, int *in, int *out, int n, bool zero_in, hipStream_t s) {
+    const bool vec = !((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15);
+    if (n <= kScanSmall) {
+        if (vec) k_scan_small<true><<<1, kScanSmallTB, 0, s>>>(in, out, n, zero_in ? 1 : 0);
+        else k_scan_small<false><<<1, kScanSmallTB, 0, s>>>(in, out, n, zero_in ? 1 : 0);
+        AOS_HIP(hipGetLastError());
+        return;
+    }
     const int blocks = cdiv((long long)n + 1, kScanTile);
     const LookBack L = lb.take(blocks, s);
-    k_scan_1p<<<blocks, kScanTB, 0, s>>>(in, out, n, zero_in ? 1 : 0, L);
+    if (vec) k_scan_1p<true><<<blocks, kScanTB, 0, s>>>(in, out, n, zero_in ? 1 : 0, L);
+    else k_scan_1p<false><<<blocks, kScanTB, 0, s>>>(in, out, n, zero_in ? 1 : 0, L);
     AOS_HIP(hipGetLastError());
 }
 

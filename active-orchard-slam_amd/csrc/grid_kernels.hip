@@ -7,8 +7,6 @@
 // Layout in HBM: occupancy-type grids are bit-packed, one uint64 word = 64 consecutive cells of
 // a row (bit i = cell x = 64*c + i), WW = ceil(W/64) words per row, padding bits zero. Byte grids
 // (int8 {0,100}) exist only for the published OccupancyGrid outputs.
-#include <hipcub/hipcub.hpp>
-
 #include <climits>
 #include <stdexcept>
 
@@ -19,15 +17,6 @@ namespace aos {
 static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 // (a1-a4, ROR + clip + raster: ror.hip)
-
-size_t scan_temp_bytes(int n) {
-    size_t t = 0;
-    AOS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t, (const int *)nullptr, (int *)nullptr, n));
-    return t;
-}
-void launch_exclusive_scan(const int *in, int *out, int n, void *temp, size_t temp_bytes, hipStream_t s) {
-    AOS_HIP(hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, in, out, n, s));
-}
 
 // ------------------------------------------------------------------------------------------
 // Streaming ingest: a scan's records -> the map's float4 (x, y, z, 0) layout (aos_map_append).

@@ -42,6 +42,14 @@ struct LocalGroup {
     uint64_t phase = 0;
     bool aborted = false;
     std::vector<std::vector<int32_t>> red;   // all-reduce slots
+    // AOS_GROUP_SERIAL=1 (measurement: tools/tiling_overhead.py): one rank at a time has GPU work in flight. A rank
+    // holds `gpu` from its frame's start to its next collective (whose caller has drained its stream) and again
+    // around the collective's own copies, so the ranks' kernels never overlap on a shared GPU and a kernel trace
+    // sums each rank's work as it would run alone.
+    bool serial = false;
+    std::mutex gpu;
+    void hold() { if (serial) gpu.lock(); }
+    void drop() { if (serial) gpu.unlock(); }
 
     // returns false if the group was aborted (or a rank stalled for 10 minutes)
     bool barrier() {
@@ -66,10 +74,20 @@ struct LocalGroup {
     }
 };
 
+// (serial groups: the caller holds the GPU token when a collective starts and gets it back when it returns)
+struct SerialGap {
+    LocalGroup &g;
+    explicit SerialGap(LocalGroup &grp) : g(grp) { g.drop(); }
+    ~SerialGap() { g.hold(); }
+};
+
 int local_all_gather(void *user, uint64_t bytes) {
     Member &me = *static_cast<Member *>(user);
     LocalGroup &g = *me.g;
+    SerialGap gap(g);
     if (!g.barrier()) return -1;   // every rank's send buffer is packed
+    std::unique_lock<std::mutex> tok(g.gpu, std::defer_lock);
+    if (g.serial) tok.lock();
     if (hipSetDevice(me.device) != hipSuccess) { g.abort(); return -1; }
     for (int r = 0; r < g.world; ++r) {
         const Member &src = *g.m[r];
@@ -80,6 +98,7 @@ int local_all_gather(void *user, uint64_t bytes) {
         if (e != hipSuccess) { g.abort(); return -1; }
     }
     if (hipStreamSynchronize(me.stream) != hipSuccess) { g.abort(); return -1; }
+    if (tok.owns_lock()) tok.unlock();
     return g.barrier() ? 0 : -1;   // nobody repacks its send buffer before every rank has read it
 }
 
@@ -87,7 +106,10 @@ int local_all_gather(void *user, uint64_t bytes) {
 int local_all_to_all(void *user, const uint64_t *counts) {
     Member &me = *static_cast<Member *>(user);
     LocalGroup &g = *me.g;
+    SerialGap gap(g);
     if (!g.barrier()) return -1;   // every rank's send buffer is packed
+    std::unique_lock<std::mutex> tok(g.gpu, std::defer_lock);
+    if (g.serial) tok.lock();
     if (hipSetDevice(me.device) != hipSuccess) { g.abort(); return -1; }
     const int W = g.world;
     uint64_t roff = 0;
@@ -107,12 +129,14 @@ int local_all_to_all(void *user, const uint64_t *counts) {
         roff += n;
     }
     if (hipStreamSynchronize(me.stream) != hipSuccess) { g.abort(); return -1; }
+    if (tok.owns_lock()) tok.unlock();
     return g.barrier() ? 0 : -1;
 }
 
 int local_all_reduce_max(void *user, int32_t *v, int32_t n) {
     Member &me = *static_cast<Member *>(user);
     LocalGroup &g = *me.g;
+    SerialGap gap(g);
     g.red[me.rank].assign(v, v + n);
     if (!g.barrier()) return -1;
     for (int r = 0; r < g.world; ++r) {
@@ -151,6 +175,10 @@ int aos_group_create(const aos_params *p, const int32_t *devices, int32_t tiles_
     G->tiles_y = tiles_y;
     const int world = tiles_x * tiles_y;
     G->g.world = world;
+    {
+        const char *e = getenv("AOS_GROUP_SERIAL");
+        G->g.serial = e && atoi(e) != 0;
+    }
     for (int r = 0; r < world; ++r) G->g.m.emplace_back(new Member());
     G->g.red.resize(world);
     for (int r = 0; r < world; ++r) {
@@ -259,7 +287,13 @@ static int group_run(aos_group *G, int32_t root, aos_seedgen_out *root_out, cons
     int fail_rank = -1, fail_rc = AOS_OK;
     std::string fail_msg;
     auto run = [&](int r) {
+        G->g.hold();   // (serial groups: the frame's first GPU work; the collectives hand the token on)
         const int rc = frame(r, &comms[r], &outs[r]);
+        if (G->g.serial) {   // (its last work is done before the token goes: the next rank's trace starts clean)
+            DeviceScope dev(G->g.m[r]->device);
+            (void)hipDeviceSynchronize();
+        }
+        G->g.drop();
         if (rc != AOS_OK) {
             {
                 std::lock_guard<std::mutex> l(fail_mu);

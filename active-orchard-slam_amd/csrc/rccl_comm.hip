@@ -86,13 +86,16 @@ void rccl_unique_id(uint8_t *id) {
     std::memcpy(id, &u, sizeof(u));
 }
 
+static void sc_all_gather(void *impl, uint64_t bytes, hipStream_t s);
+static void sc_all_to_all(void *impl, const uint64_t *counts, hipStream_t s);
+
+// the aos_comm callbacks: the stream-ordered collectives below on the communicator's own stream, then a wait
 static int rc_all_gather(void *user, uint64_t bytes) {
     aos_rccl *r = static_cast<aos_rccl *>(user);
     try {
-        const RcclApi &api = rccl_api();
         DeviceScope ds(r->device);
         if (bytes > r->c.buf_bytes) return 1;
-        rccl_check(api, api.all_gather(r->send.p, r->recv.p, bytes, ncclUint8, r->comm, r->stream), "ncclAllGather");
+        sc_all_gather(r, bytes, r->stream);
         return hipStreamSynchronize(r->stream) == hipSuccess ? 0 : 1;
     } catch (...) {
         return 1;
@@ -104,29 +107,8 @@ static int rc_all_gather(void *user, uint64_t bytes) {
 static int rc_all_to_all(void *user, const uint64_t *counts) {
     aos_rccl *r = static_cast<aos_rccl *>(user);
     try {
-        const RcclApi &api = rccl_api();
         DeviceScope ds(r->device);
-        const int W = r->c.world, me = r->c.rank;
-        uint64_t soff = 0, roff = 0;
-        std::vector<uint64_t> so(W), ro(W);
-        for (int q = 0; q < W; ++q) {
-            so[q] = soff; soff += counts[(size_t)me * W + q];
-            ro[q] = roff; roff += counts[(size_t)q * W + me];
-        }
-        if (soff > r->c.buf_bytes || roff > r->c.buf_bytes * (uint64_t)W) return 1;
-        const char *sb = static_cast<const char *>(r->send.p);
-        char *rb = static_cast<char *>(r->recv.p);
-        if (const uint64_t n = counts[(size_t)me * W + me])
-            AOS_HIP(hipMemcpyAsync(rb + ro[me], sb + so[me], n, hipMemcpyDeviceToDevice, r->stream));
-        rccl_check(api, api.group_start(), "ncclGroupStart");
-        for (int q = 0; q < W; ++q) {
-            if (q == me) continue;
-            if (const uint64_t n = counts[(size_t)me * W + q])
-                rccl_check(api, api.send(sb + so[q], n, ncclUint8, q, r->comm, r->stream), "ncclSend");
-            if (const uint64_t n = counts[(size_t)q * W + me])
-                rccl_check(api, api.recv(rb + ro[q], n, ncclUint8, q, r->comm, r->stream), "ncclRecv");
-        }
-        rccl_check(api, api.group_end(), "ncclGroupEnd");
+        sc_all_to_all(r, counts, r->stream);
         return hipStreamSynchronize(r->stream) == hipSuccess ? 0 : 1;
     } catch (...) {
         return 1;
@@ -147,6 +129,81 @@ static int rc_all_reduce_max(void *user, int32_t *v, int32_t n) {
     } catch (...) {
         return 1;
     }
+}
+
+// ---- the same collectives enqueued on the caller's stream (StreamColl, aos_internal.h): no host wait; the frame's
+// kernels before and after them are ordered by the stream. RCCL takes any stream of the communicator's device.
+static void sc_all_gather(void *impl, uint64_t bytes, hipStream_t s) {
+    aos_rccl *r = static_cast<aos_rccl *>(impl);
+    const RcclApi &api = rccl_api();
+    DeviceScope ds(r->device);
+    if (bytes > r->c.buf_bytes) throw CommError{"all_gather larger than the RCCL buffers"};
+    rccl_check(api, api.all_gather(r->send.p, r->recv.p, bytes, ncclUint8, r->comm, s), "ncclAllGather");
+}
+
+// rank q's send_buf[0, bytes) -> the root's recv_buf[q * bytes, ...): each rank sends one block, only the root
+// receives (W - 1 blocks; its own block is a device copy)
+static void sc_gather(void *impl, uint64_t bytes, int root, hipStream_t s) {
+    aos_rccl *r = static_cast<aos_rccl *>(impl);
+    const RcclApi &api = rccl_api();
+    DeviceScope ds(r->device);
+    const int W = r->c.world, me = r->c.rank;
+    if (bytes > r->c.buf_bytes) throw CommError{"gather larger than the RCCL buffers"};
+    if (root < 0 || root >= W) throw CommError{"gather: root outside the communicator"};
+    if (!bytes) return;
+    char *rb = static_cast<char *>(r->recv.p);
+    if (me == root) AOS_HIP(hipMemcpyAsync(rb + (uint64_t)me * bytes, r->send.p, bytes, hipMemcpyDeviceToDevice, s));
+    if (W == 1) return;
+    rccl_check(api, api.group_start(), "ncclGroupStart");
+    if (me == root) {
+        for (int q = 0; q < W; ++q)
+            if (q != me) rccl_check(api, api.recv(rb + (uint64_t)q * bytes, bytes, ncclUint8, q, r->comm, s), "ncclRecv");
+    } else {
+        rccl_check(api, api.send(r->send.p, bytes, ncclUint8, root, r->comm, s), "ncclSend");
+    }
+    rccl_check(api, api.group_end(), "ncclGroupEnd");
+}
+
+static void sc_max_dev(void *impl, int32_t *d, int n, hipStream_t s) {
+    aos_rccl *r = static_cast<aos_rccl *>(impl);
+    const RcclApi &api = rccl_api();
+    DeviceScope ds(r->device);
+    if (n > 0) rccl_check(api, api.all_reduce(d, d, (size_t)n, ncclInt32, ncclMax, r->comm, s), "ncclAllReduce");
+}
+
+static void sc_all_to_all(void *impl, const uint64_t *counts, hipStream_t s) {
+    aos_rccl *r = static_cast<aos_rccl *>(impl);
+    const RcclApi &api = rccl_api();
+    DeviceScope ds(r->device);
+    const int W = r->c.world, me = r->c.rank;
+    uint64_t soff = 0, roff = 0;
+    std::vector<uint64_t> so(W), ro(W);
+    for (int q = 0; q < W; ++q) {
+        so[q] = soff; soff += counts[(size_t)me * W + q];
+        ro[q] = roff; roff += counts[(size_t)q * W + me];
+    }
+    if (soff > r->c.buf_bytes || roff > r->c.buf_bytes * (uint64_t)W) throw CommError{"all_to_all larger than the RCCL buffers"};
+    const char *sb = static_cast<const char *>(r->send.p);
+    char *rb = static_cast<char *>(r->recv.p);
+    if (const uint64_t n = counts[(size_t)me * W + me]) AOS_HIP(hipMemcpyAsync(rb + ro[me], sb + so[me], n, hipMemcpyDeviceToDevice, s));
+    if (W == 1) return;
+    rccl_check(api, api.group_start(), "ncclGroupStart");
+    for (int q = 0; q < W; ++q) {
+        if (q == me) continue;
+        if (const uint64_t n = counts[(size_t)me * W + q]) rccl_check(api, api.send(sb + so[q], n, ncclUint8, q, r->comm, s), "ncclSend");
+        if (const uint64_t n = counts[(size_t)q * W + me]) rccl_check(api, api.recv(rb + ro[q], n, ncclUint8, q, r->comm, s), "ncclRecv");
+    }
+    rccl_check(api, api.group_end(), "ncclGroupEnd");
+}
+
+bool rccl_stream_coll(const aos_comm &cm, StreamColl &out) {
+    if (cm.all_gather != rc_all_gather || !cm.user) return false;   // (a caller's communicator: its callbacks)
+    out.impl = cm.user;
+    out.all_gather = sc_all_gather;
+    out.gather = sc_gather;
+    out.max_dev = sc_max_dev;
+    out.all_to_all = sc_all_to_all;
+    return true;
 }
 
 aos_rccl *rccl_create(const uint8_t *id, int rank, int world, int device, uint64_t buf_bytes) {

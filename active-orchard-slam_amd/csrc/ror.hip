@@ -27,8 +27,6 @@
 // largest float whose double is <= r^2); non-dense: radius search d2 < float(r^2). The point itself
 // has d2 = 0 and is counted by the same test (not counted when r = 0 on a non-dense cloud, as FLANN's
 // strict test does). Cells: generateOccupancyGrid's (int)(((double)x - origin) / (double)res).
-#include <hipcub/hipcub.hpp>
-
 #include <algorithm>
 #include <climits>
 #include <cmath>
@@ -522,8 +520,7 @@ __global__ __launch_bounds__(256) void k_rt_biglist(RorLaunch L, const int *tsta
 
 // choff[i] = chunks of the big tiles before list entry i; choff[nbig] = all chunks
 __global__ __launch_bounds__(1024) void k_rt_bigchunks(const int *tstart, BigBufs B) {
-    typedef hipcub::BlockScan<int, 1024> Scan;
-    __shared__ typename Scan::TempStorage tmp;
+    __shared__ int wsum[1024 / 64];
     const int nbig = B.list[0];
     int base = 0;
     for (int i0 = 0; i0 < nbig; i0 += 1024) {
@@ -533,11 +530,10 @@ __global__ __launch_bounds__(1024) void k_rt_bigchunks(const int *tstart, BigBuf
             const int t = B.list[1 + i];
             c = (tstart[t + 1] - tstart[t] + kBigChunk - 1) / kBigChunk;
         }
-        int before, total;
-        Scan(tmp).ExclusiveSum(c, before, total);
+        int total;
+        const int before = block_excl_scan<1024>(c, wsum, &total);   // (ends with a barrier)
         if (i < nbig) B.choff[i] = base + before;
         base += total;
-        __syncthreads();
     }
     if (threadIdx.x == 0) B.choff[nbig] = base;
 }
@@ -578,8 +574,7 @@ __global__ __launch_bounds__(kBigTB) void k_rt_bighist(RorLaunch L, const int *t
 
 __global__ __launch_bounds__(1024) void k_rt_bigscan(RorLaunch L, const int *tstart, BigBufs B) {
     constexpr int kSeg = (kBigBins + 1023) / 1024;
-    typedef hipcub::BlockScan<int, 1024> Scan;
-    __shared__ typename Scan::TempStorage tmp;
+    __shared__ int wsum[1024 / 64];
     const int nbig = B.list[0], nlb = 2 * (L.TB + 2) * (L.TB + 2);
     for (int i = blockIdx.x; i < nbig; i += gridDim.x) {
         const int t = B.list[1 + i];
@@ -591,9 +586,8 @@ __global__ __launch_bounds__(1024) void k_rt_bigscan(RorLaunch L, const int *tst
             v[j] = b < nlb ? tot[b] : 0;
             run += v[j];
         }
-        int before;
-        Scan(tmp).ExclusiveSum(run, before);
-        __syncthreads();
+        int total;
+        int before = block_excl_scan<1024>(run, wsum, &total);
 #pragma unroll
         for (int j = 0; j < kSeg; ++j) {
             const int b = threadIdx.x * kSeg + j;

@@ -22,8 +22,10 @@ using namespace aos;
 void aos_ctx::release() {
     for (DevBuf *b : {&cloud_copy, &bin_count, &bin_start, &sorted, &ror_scratch, &ror_bigbins, &scan_tmp, &counters,
                       &raster_bits, &infl_bits, &open_bits, &thin_a, &thin_b, &thin_out, &thin_act, &occ_bytes, &skel_bytes, &flags,
-                      &full_infl, &full_skel, &map_buf, &scan_stage})
+                      &full_infl, &full_skel, &map_buf, &scan_stage, &coll_red})
         b->release();
+    for (hipEvent_t e : coll_ev) (void)hipEventDestroy(e);
+    coll_ev.clear();
     thin_graphs_release();
     try { expander.join(); } catch (...) {}   // (before its buffers go)
     if (copy_stream) {
@@ -692,7 +694,7 @@ bool aos_ctx::ror_collect(bool throw_stuck) {
 // of the batch to h_flags itself.
 bool aos_ctx::thin_first_batch(const FrameGeom &g, const uint64_t *d_ibits, uint64_t *d_open, uint64_t *const bufs[2],
                                int *d_flags, int *h_flags, int *d_act, int nflags, int &batch_n, int cap_launches,
-                               const std::function<void(int)> &launch_next) {
+                               const std::function<void(int)> &launch_next, const std::function<void()> &after_open) {
     hipStream_t s = stream;
     const int K = kThinItersPerLaunch;
     if (thin_graph_shape < 0) {
@@ -702,8 +704,14 @@ bool aos_ctx::thin_first_batch(const FrameGeom &g, const uint64_t *d_ibits, uint
     }
     const int shape = thin_graph_shape;
     last_thin_graph = 0;
-    if (shape == 0) {
+    // The opening runs outside the graph (shapes 0 and 1) so that after_open (the inflated grid's read-back) can
+    // be queued behind it: the read-back's blit kernel beside k_open took it from ~40 to 110 us at C3 (round-5
+    // trace); beside thinning the copy meets long, LDS-bound launches instead.
+    if (shape <= 1) {
         launch_open(d_ibits, d_open, g, s, d_flags, nflags);   // (clears the flags)
+        after_open();
+    }
+    if (shape == 0) {
         launch_next(batch_n);
         return false;
     }
@@ -735,9 +743,7 @@ bool aos_ctx::thin_first_batch(const FrameGeom &g, const uint64_t *d_ibits, uint
             } else if (shape == 4) {
                 launch_zero_ints(d_flags, nflags, s);
                 launch_open(d_ibits, d_open, g, s);
-            } else {
-                launch_open(d_ibits, d_open, g, s, d_flags, nflags);   // (clears the flags: no clearing node)
-            }
+            }   // (shape 1: the opening, which clears the flags, ran before the graph)
             launch_next(batch_n);
             if (copy_node)
                 AOS_HIP(hipMemcpyAsync(h_flags, d_flags, sizeof(int) * (1 + batch_n * K), hipMemcpyDeviceToHost, s));
@@ -757,6 +763,7 @@ bool aos_ctx::thin_first_batch(const FrameGeom &g, const uint64_t *d_ibits, uint
     } else {
         last_thin_graph = 1;
     }
+    if (shape > 1) after_open();   // (diagnostic shapes: the opening is inside the graph)
     AOS_HIP(hipGraphLaunch(tg->exec, s));
     return copy_node;
 }
@@ -839,15 +846,16 @@ bool aos_ctx::run_seedgen_once(bool want_host, aos_seedgen_out &out, bool allow_
     int8_t *d_occ = static_cast<int8_t *>(occ_bytes.ensure((size_t)g.W * g.H));
     launch_inflate(d_rbits, d_ibits, g, s, d_occ, 5);   // (the bytes with the 5-cell frame in the same launch)
     AOS_HIP(hipEventRecord(ev[2], s));
-    // /occupancy_grid's bits cross PCIe now, beside thinning, instead of beside the cluster stage's read-backs
-    // (finish_frame sends the skeleton's)
+    // /occupancy_grid's bits cross PCIe beside thinning (after the opening: thin_first_batch), instead of beside
+    // the cluster stage's read-backs (finish_frame sends the skeleton's)
     infl_bits_sent = false;
-    if (want_host && grid_readback_bits()) {
+    auto send_infl_bits = [&]() {
+        if (!want_host || !grid_readback_bits()) return;
         expander.drain();   // (a failed frame's expansion may still read the buffer)
         const size_t nb = 8 * Cw;
         grid_d2h(h_occ_bits.ensure(std::max<size_t>(nb, 8)), d_ibits, nb);
         infl_bits_sent = true;
-    }
+    };
 
     // ---------------- a7 opening + Zhang-Suen (temporal blocks of kThinItersPerLaunch iterations)
     uint64_t *d_open = static_cast<uint64_t *>(open_bits.ensure(Cw * 8));
@@ -880,7 +888,7 @@ bool aos_ctx::run_seedgen_once(bool want_host, aos_seedgen_out &out, bool allow_
     };
     int batch_n = std::min(cap_launches, std::max(2, (thin_iters_prev + 2 + K - 1) / K));
     const bool flags_in_graph = thin_first_batch(g, d_ibits, d_open, bufs, d_flags, h_flags, d_act, nflags, batch_n,
-                                                 cap_launches, launch_next);
+                                                 cap_launches, launch_next, send_infl_bits);
     launched = batch_n;
     src = bufs[(batch_n - 1) & 1];
     const uint64_t *final_buf = d_open;
@@ -1049,10 +1057,12 @@ void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *c
     static const int grid_copy_mode = [] { const char *e = getenv("AOS_GRID_COPY"); return e ? atoi(e) : 0; }();
     const bool as_bits = grid_readback_bits() != 0;
     auto issue_grid_copy = [&]() {
+        // (a failed frame's expansion may still write h_occ / h_skel and read the bit buffers: drained before
+        // any of them can be reallocated; ADVICE r05. A no-op when the inflated bits' send drained it.)
+        expander.drain();
         h_occ.ensure(std::max<size_t>(C, 1)); h_skel.ensure(std::max<size_t>(C, 1));
         if (as_bits) {
             const size_t nb = 8 * (size_t)g.WW * g.H;
-            if (!infl_bits_sent) expander.drain();   // (a failed frame's expansion may still read the buffers)
             uint64_t *hob = static_cast<uint64_t *>(h_occ_bits.ensure(std::max<size_t>(nb, 8)));
             uint64_t *hsb = static_cast<uint64_t *>(h_skel_bits.ensure(std::max<size_t>(nb, 8)));
             if (!infl_bits_sent)   // (a tiled frame: the gathered inflated grid)
@@ -1097,7 +1107,17 @@ void aos_ctx::finish_frame(const FrameGeom &g, bool want_host, const uint64_t *c
 
     // ---------------- a8-a15 clusters, tree rows, seeds
     SeedStageIn sin{skel_bits, &geom, &poly, P.cluster_min_length, pre};
-    if (want_host && grid_copy_mode == 0 && as_bits) sin.after_fg = copy_now;
+    if (want_host && grid_copy_mode == 0 && as_bits) {
+        sin.after_fg = copy_now;
+        // the replays walk the skeleton's bits once their read-back (queued by after_fg) is done
+        static const bool replay_bits = [] { const char *e = getenv("AOS_REPLAY_BITS"); return !e || atoi(e) != 0; }();
+        if (replay_bits)
+            sin.host_skel_bits = [&]() -> const uint64_t * {
+                if (!copy_issued) return nullptr;
+                AOS_HIP(hipEventSynchronize(copy_done));
+                return static_cast<const uint64_t *>(h_skel_bits.p);
+            };
+    }
     SeedStageOut so;
     run_cluster_seed_stage(cs, sin, so, s, ev[4], trace_on() ? &ev[16] : nullptr);
     AOS_HIP(hipEventRecord(ev[5], s));

@@ -148,11 +148,115 @@ __global__ void k_unpack_full2(const uint64_t *recv, TileSplit S, int WW, int H,
     b[(long long)y * WW + c] = src[n + i];
 }
 
-static void comm_all_gather(const aos_comm &cm, uint64_t bytes) {
-    if (cm.all_gather(cm.user, bytes) != 0) throw CommError{"aos_comm.all_gather failed"};
+static double ms_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
-static void comm_max(const aos_comm &cm, int32_t *v, int n) {
-    if (cm.all_reduce_max(cm.user, v, n) != 0) throw CommError{"aos_comm.all_reduce_max failed"};
+
+// ------------------------------------------------------------------ FrameComm (aos_internal.h)
+FrameComm::FrameComm(const aos_comm &cm, std::vector<hipEvent_t> &pool, DevBuf &scratch) : c(cm), ev(pool), red(scratch) {
+    rccl_stream_coll(cm, sc);
+}
+
+namespace {
+// events around one enqueued collective (the pool grows once, then is reused frame after frame)
+struct EnqTimer {
+    FrameComm &f;
+    hipStream_t s;
+    EnqTimer(FrameComm &fc, hipStream_t st) : f(fc), s(st) { mark(); }
+    ~EnqTimer() { mark(); }
+    void mark() {
+        if ((int)f.ev.size() <= f.ev_used) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return;   // (timing only)
+            f.ev.push_back(e);
+        }
+        if (hipEventRecord(f.ev[f.ev_used], s) == hipSuccess) ++f.ev_used;
+    }
+};
+}  // namespace
+
+float FrameComm::ms_enqueued() {
+    if (ev_used < 2) return 0.0f;
+    (void)hipEventSynchronize(ev[ev_used - 1]);
+    float tot = 0.0f;
+    for (int i = 0; i + 1 < ev_used; i += 2) {
+        float v = 0.0f;
+        if (hipEventElapsedTime(&v, ev[i], ev[i + 1]) == hipSuccess) tot += v;
+    }
+    return tot;
+}
+
+void FrameComm::all_gather(uint64_t bytes, hipStream_t s) {
+    ++n_gather;
+    bytes_sent += bytes;
+    if (ordered()) {
+        EnqTimer t(*this, s);
+        sc.all_gather(sc.impl, bytes, s);
+        return;
+    }
+    AOS_HIP(hipStreamSynchronize(s));   // (the callbacks run with the stream idle: the send buffer is packed)
+    const auto t0 = std::chrono::steady_clock::now();
+    const int r = c.all_gather(c.user, bytes);
+    ms_gather += ms_since(t0);
+    if (r != 0) throw CommError{"aos_comm.all_gather failed"};
+}
+
+void FrameComm::all_to_all(const uint64_t *counts, hipStream_t s) {
+    ++n_gather;
+    for (int d = 0; d < c.world; ++d) bytes_sent += counts[(size_t)c.rank * c.world + d];
+    if (ordered()) {
+        EnqTimer t(*this, s);
+        sc.all_to_all(sc.impl, counts, s);
+        return;
+    }
+    if (!c.all_to_all) throw std::logic_error("FrameComm::all_to_all without aos_comm.all_to_all");
+    AOS_HIP(hipStreamSynchronize(s));
+    const auto t0 = std::chrono::steady_clock::now();
+    const int r = c.all_to_all(c.user, counts);
+    ms_gather += ms_since(t0);
+    if (r != 0) throw CommError{"aos_comm.all_to_all failed"};
+}
+
+void FrameComm::gather(uint64_t bytes, int root, hipStream_t s) {
+    if (ordered()) {
+        ++n_gather;
+        bytes_sent += c.rank == root ? 0 : bytes;
+        EnqTimer t(*this, s);
+        sc.gather(sc.impl, bytes, root, s);
+        return;
+    }
+    if (!c.all_to_all) return all_gather(bytes, s);
+    // the personalised exchange with one non-zero column: every rank's block to the root (its own included),
+    // landing at block r of the root's recv_buf as an all-gather would put it
+    std::vector<uint64_t> counts((size_t)c.world * c.world, 0);
+    for (int r = 0; r < c.world; ++r) counts[(size_t)r * c.world + root] = bytes;
+    all_to_all(counts.data(), s);
+}
+
+void FrameComm::max_host(int32_t *v, int n) {
+    ++n_reduce;
+    const auto t0 = std::chrono::steady_clock::now();
+    const int r = c.all_reduce_max(c.user, v, n);
+    ms_reduce += ms_since(t0);
+    if (r != 0) throw CommError{"aos_comm.all_reduce_max failed"};
+}
+
+void FrameComm::max_flags(const int *d, int32_t *h, int n, hipStream_t s) {
+    if (ordered()) {   // the reduction on the device, then one read-back and one wait
+        ++n_reduce;
+        int32_t *dr = static_cast<int32_t *>(red.ensure(sizeof(int32_t) * (size_t)std::max(n, 1)));
+        AOS_HIP(hipMemcpyAsync(dr, d, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToDevice, s));
+        {
+            EnqTimer t(*this, s);
+            sc.max_dev(sc.impl, dr, n, s);
+        }
+        AOS_HIP(hipMemcpyAsync(h, dr, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost, s));
+        AOS_HIP(hipStreamSynchronize(s));
+        return;
+    }
+    AOS_HIP(hipMemcpyAsync(h, d, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost, s));
+    AOS_HIP(hipStreamSynchronize(s));
+    max_host(h, n);
 }
 
 }  // namespace aos
@@ -160,80 +264,34 @@ static void comm_max(const aos_comm &cm, int32_t *v, int n) {
 using namespace aos;
 
 // Refresh the halo of a window grid (in place) from the neighbours' border strips.
-void aos_ctx::tile_halo_exchange(uint64_t *win, const TilePlan &t, const aos_comm &cm) {
+void aos_ctx::tile_halo_exchange(uint64_t *win, const TilePlan &t, FrameComm &fc) {
     if (!t.hy && !t.hw) return;
     const int nr = t.y1 - t.y0, nc = t.c1 - t.c0;
     const long long n = 2LL * t.hy * nc + 2LL * nr * t.hw;
     k_pack_border<<<cdiv(n, 256), 256, 0, stream>>>(win, t.lg.WW, t.y0 - t.wy0, t.c0 - t.wc0, nr, nc, t.hy, t.hw,
-                                                    static_cast<uint64_t *>(cm.send_buf));
+                                                    static_cast<uint64_t *>(fc.c.send_buf));
     AOS_HIP(hipGetLastError());
-    AOS_HIP(hipStreamSynchronize(stream));
-    comm_all_gather(cm, 8ull * (uint64_t)t.max_border);
+    fc.all_gather(8ull * (uint64_t)t.max_border, stream);
     const TileSplit S = split_of(t, t.max_border);
     dim3 grid(cdiv(t.lg.WW, 64), t.lg.H);
     k_unpack_halo<<<grid, 64, 0, stream>>>(win, t.lg.WW, t.lg.H, t.wy0, t.wc0, t.y0, t.y1, t.c0, t.c1, S,
-                                           static_cast<const uint64_t *>(cm.recv_buf));
+                                           static_cast<const uint64_t *>(fc.c.recv_buf));
     AOS_HIP(hipGetLastError());
 }
 
-// The frame's collectives go through a wrapper that times every callback (host wall clock, which for a
-// collective includes the wait for the slowest rank), so a tiled run can say where its time went:
-// aos_tiled_stats_get (verdict r03: comm time separately from compute).
-namespace {
-struct TimedComm {
-    aos_comm inner;
-    double ms_gather = 0.0, ms_reduce = 0.0;
-    int n_gather = 0, n_reduce = 0;
-    uint64_t bytes_gather = 0;
-};
-double ms_since(std::chrono::steady_clock::time_point t0) {
-    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-}
-int timed_gather(void *u, uint64_t bytes) {
-    TimedComm &t = *static_cast<TimedComm *>(u);
-    const auto t0 = std::chrono::steady_clock::now();
-    const int r = t.inner.all_gather(t.inner.user, bytes);
-    t.ms_gather += ms_since(t0);
-    ++t.n_gather;
-    t.bytes_gather += bytes;
-    return r;
-}
-int timed_all_to_all(void *u, const uint64_t *counts) {   // (counted with the all-gathers: data movement)
-    TimedComm &t = *static_cast<TimedComm *>(u);
-    const auto t0 = std::chrono::steady_clock::now();
-    const int r = t.inner.all_to_all(t.inner.user, counts);
-    t.ms_gather += ms_since(t0);
-    ++t.n_gather;
-    for (int d = 0; d < t.inner.world; ++d) t.bytes_gather += counts[(size_t)t.inner.rank * t.inner.world + d];
-    return r;
-}
-int timed_reduce(void *u, int32_t *v, int32_t n) {
-    TimedComm &t = *static_cast<TimedComm *>(u);
-    const auto t0 = std::chrono::steady_clock::now();
-    const int r = t.inner.all_reduce_max(t.inner.user, v, n);
-    t.ms_reduce += ms_since(t0);
-    ++t.n_reduce;
-    return r;
-}
-}  // namespace
-
 void aos_ctx::run_tiled(const aos_comm &cm, int tiles_x, int tiles_y, int root, bool want_host, aos_seedgen_out &out) {
-    TimedComm tc{cm};
-    aos_comm w = cm;
-    w.user = &tc;
-    w.all_gather = cm.all_gather ? timed_gather : nullptr;
-    w.all_reduce_max = cm.all_reduce_max ? timed_reduce : nullptr;
-    w.all_to_all = cm.all_to_all ? timed_all_to_all : nullptr;
+    FrameComm fc(cm, coll_ev, coll_red);
     const auto t0 = std::chrono::steady_clock::now();
     const uint64_t skipped0 = ror_skipped;
     auto record = [&]() {
         tstats = aos_tiled_stats{};
         tstats.ms_frame = (float)ms_since(t0);
-        tstats.ms_comm_gather = (float)tc.ms_gather;
-        tstats.ms_comm_reduce = (float)tc.ms_reduce;
-        tstats.n_gather = tc.n_gather;
-        tstats.n_reduce = tc.n_reduce;
-        tstats.bytes_gather = tc.bytes_gather;
+        tstats.ms_comm_gather = (float)fc.ms_gather;
+        tstats.ms_comm_reduce = (float)fc.ms_reduce;
+        if (fc.ordered()) tstats.ms_comm_gather += fc.ms_enqueued();   // (device time of the enqueued ones)
+        tstats.n_gather = fc.n_gather;
+        tstats.n_reduce = fc.n_reduce;
+        tstats.bytes_gather = fc.bytes_sent;
         tstats.ms_cluster_local = cdist_stats.ms_local;
         tstats.ms_cluster_global = cdist_stats.ms_global;
         tstats.ms_replay = cdist_stats.ms_replay;
@@ -242,7 +300,7 @@ void aos_ctx::run_tiled(const aos_comm &cm, int tiles_x, int tiles_y, int root, 
         tstats.is_root = cm.rank == root ? 1 : 0;
     };
     try {
-        run_tiled_frame(w, tiles_x, tiles_y, root, want_host, out);
+        run_tiled_frame(fc, tiles_x, tiles_y, root, want_host, out);
     } catch (...) {
         record();
         throw;
@@ -254,7 +312,8 @@ void aos_ctx::run_tiled(const aos_comm &cm, int tiles_x, int tiles_y, int root, 
     tstats.ms_seeds = out.ms_seeds;
 }
 
-void aos_ctx::run_tiled_frame(const aos_comm &cm, int tiles_x, int tiles_y, int root, bool want_host, aos_seedgen_out &out) {
+void aos_ctx::run_tiled_frame(FrameComm &fc, int tiles_x, int tiles_y, int root, bool want_host, aos_seedgen_out &out) {
+    const aos_comm &cm = fc.c;
     std::memset(&out, 0, sizeof(out));
     have_frame = false;
     tiled_frame = true;
@@ -284,7 +343,7 @@ void aos_ctx::run_tiled_frame(const aos_comm &cm, int tiles_x, int tiles_y, int 
 
     // ---- raster halo from the neighbours, a5 inflation on the window
     uint64_t *d_ibits = static_cast<uint64_t *>(infl_bits.ensure(Cwl * 8));
-    tile_halo_exchange(d_rbits, t, cm);
+    tile_halo_exchange(d_rbits, t, fc);
     launch_inflate(d_rbits, d_ibits, lg, s);
     AOS_HIP(hipEventRecord(ev[2], s));
 
@@ -315,15 +374,13 @@ void aos_ctx::run_tiled_frame(const aos_comm &cm, int tiles_x, int tiles_y, int 
         }
         if (halo) budget -= 2LL * K * nl;
         const int nf = 1 + launched * K;
-        AOS_HIP(hipMemcpyAsync(h_flags, d_flags, sizeof(int) * nf, hipMemcpyDeviceToHost, s));
-        AOS_HIP(hipStreamSynchronize(s));
+        fc.max_flags(d_flags, h_flags, nf, s);   // (the period's one host wait: the stop rule runs on the host)
         fl.assign(h_flags, h_flags + nf);
-        comm_max(cm, fl.data(), nf);
         T = thin_iterations(fl.data(), launched * K);
         if (T) break;
         if (launched * K > max_iters) throw std::runtime_error("thinning did not converge");
         if (halo) {
-            tile_halo_exchange(cur, t, cm);
+            tile_halo_exchange(cur, t, fc);
             budget = t.G;
         }
     }
@@ -336,8 +393,8 @@ void aos_ctx::run_tiled_frame(const aos_comm &cm, int tiles_x, int tiles_y, int 
     AOS_HIP(hipStreamSynchronize(s));
     // (sized by a read-back, so no staging overflow is expected; a streaming store's merge can still
     // overflow a stale size: the bits travel with the counts and every rank fails the frame together)
-    if (const char *e = getenv("AOS_DEBUG_ROR_STUCK_RANK"))   // (tests: this rank's column scan "got stuck")
-        if (atoi(e) == cm.rank) reinterpret_cast<unsigned long long *>(static_cast<int *>(h_stats.p) + 4)[1] |= 4;
+    if (g_debug_stuck_rank.load(std::memory_order_relaxed) == cm.rank)   // (tests: this rank's column scan "got stuck")
+        reinterpret_cast<unsigned long long *>(static_cast<int *>(h_stats.p) + 4)[1] |= 4;
     const bool ror_over = ror_collect(false);   // (bit 4, a stuck look-back, travels with the others)
     const int ror_bits = ror_over ? (int)reinterpret_cast<const unsigned long long *>(static_cast<const int *>(h_stats.p) + 4)[1] : 0;
     uint64_t mine_cnt = 0;
@@ -346,7 +403,7 @@ void aos_ctx::run_tiled_frame(const aos_comm &cm, int tiles_x, int tiles_y, int 
     slots[2 * cm.rank] = (int32_t)(mine_cnt & 0x7fffffff);
     slots[2 * cm.rank + 1] = (int32_t)(mine_cnt >> 31);
     slots[2 * cm.world] = ror_bits;
-    comm_max(cm, slots.data(), (int)slots.size());
+    fc.max_host(slots.data(), (int)slots.size());
     if (slots[2 * cm.world])
         throw std::runtime_error("tiled frame: ROR stage overflow on a rank (bits " + std::to_string(slots[2 * cm.world]) +
                                  ": 1 staged capacity / store merge, 2 a tile beyond the LDS capacity, 4 a stuck look-back "
@@ -354,13 +411,13 @@ void aos_ctx::run_tiled_frame(const aos_comm &cm, int tiles_x, int tiles_y, int 
     uint64_t total = 0;
     for (int r = 0; r < cm.world; ++r) total += (uint64_t)slots[2 * r] | ((uint64_t)slots[2 * r + 1] << 31);
 
-    // ---- all-gather the own skeleton + inflated words; the root finishes the frame on the whole map
+    // ---- the own skeleton + inflated words to the root, which finishes the frame on the whole map (only the root
+    // receives them when the communicator has a personalised exchange: the other ranks need no whole-map grid)
     const int nr = t.y1 - t.y0, nc = t.c1 - t.c0;
     k_pack_own2<<<cdiv((long long)nr * nc, 256), 256, 0, s>>>(cur, d_ibits, lg.WW, t.y0 - t.wy0, t.c0 - t.wc0, nr,
                                                                nc, static_cast<uint64_t *>(cm.send_buf));
     AOS_HIP(hipGetLastError());
-    AOS_HIP(hipStreamSynchronize(s));
-    comm_all_gather(cm, 16ull * (uint64_t)t.max_own);
+    fc.gather(16ull * (uint64_t)t.max_own, root, s);
     uint64_t *fs = nullptr;
     if (cm.rank == root) {
         const size_t Cw = (size_t)g.WW * g.H;
@@ -377,7 +434,7 @@ void aos_ctx::run_tiled_frame(const aos_comm &cm, int tiles_x, int tiles_y, int 
     // ---- a8-a10 over the ranks: own-tile labelling, border union-find, shared statistics / replays
     AOS_HIP(hipEventRecord(ev[6], s));
     PreClusters pre;
-    cluster_dist(cdist, cm, t, g, poly, static_cast<float>(P.cluster_min_length), cur, root, s, pre, cdist_stats);
+    cluster_dist(cdist, fc, t, g, poly, static_cast<float>(P.cluster_min_length), cur, root, s, pre, cdist_stats);
     if (cm.rank == root) {
         skel_bits = fs;
         finish_frame(g, want_host, &total, out, &pre);

@@ -234,7 +234,11 @@ int aos_map_append(aos_ctx *ctx, const aos_cloud_view *scan, int want_host, aos_
  * ncclAllGather / ncclAllReduce on the same buffers). send_buf / recv_buf are device memory on
  * this rank's GPU, registered once; the library packs into send_buf and reads recv_buf. Both
  * callbacks are collective (every rank makes the same calls in the same order), are called with
- * the handle's stream idle, and must have completed when they return. Return 0 on success. */
+ * the handle's stream idle, and must have completed when they return. Return 0 on success.
+ * The library calls every non-NULL callback, including the optional ones at the end: fill the struct
+ * from a zeroed one (aos_comm_init, or `aos_comm c = {0};`) so that a caller built against an older
+ * header leaves the newer fields NULL. aos_rccl_comm's communicator is the library's own: with it, a
+ * tiled frame enqueues its collectives on the handle's stream instead (no host wait around them). */
 typedef struct aos_comm {
     void *user;
     int32_t rank, world;                 /* world = tiles_x * tiles_y; rank r = tile (r % tiles_x, r / tiles_x) */
@@ -254,6 +258,7 @@ typedef struct aos_comm {
      * send each long cluster's cells to the one rank that measures (and replays) it. */
     int (*all_to_all)(void *user, const uint64_t *counts);
 } aos_comm;
+void aos_comm_init(aos_comm *comm);   /* all fields zero / NULL */
 
 /* RCCL communicator (one process per GPU, e.g. a torch.distributed launch): an aos_comm whose
  * exchange buffers live in HBM, all-gather = ncclAllGather over xGMI, max all-reduce =
@@ -429,6 +434,11 @@ int aos_path_plan(aos_ctx *ctx, const aos_path_graph *graph, const int8_t *skele
 int aos_debug_grid(aos_ctx *ctx, const char *which, int8_t *dst, uint64_t capacity);
 /* Stream of the handle (hipStream_t as void*) for callers that time with their own events. */
 void *aos_stream(aos_ctx *ctx);
+/* Test hooks (fault injection for the tiled path's error tests; process-wide, not for production use):
+ * ror_stuck_rank >= 0: that tiled rank reports a stuck look-back wait in its ROR column scan (every rank
+ * must then fail the frame together); a2a_round_bytes > 0: the distributed cluster stage's personalised
+ * exchange moves at most that many bytes per rank pair and round. (-1, 0) turns both off (the default). */
+void aos_debug_faults(int32_t ror_stuck_rank, uint64_t a2a_round_bytes);
 
 #ifdef __cplusplus
 }

@@ -7,6 +7,11 @@
 //                                  then per cluster: n (i32) length (f32) cells[n] (i32, any order)
 //                              out: per cluster flags (i32) cx cy (f32) center start end (f64 x 2 each);
 //                                   then n_rows (i32) rows_info[4 n_rows] cluster_info[2 n_rows] (f64)
+//   san_cluster B <in> <out>   in: as R, then n_extra (i32) extra[n_extra] (i32: skeleton cells outside every cluster)
+//                              the replays walk a skeleton bit grid (every cluster's cells + the extra cells) over
+//                              each cluster's box from its first cell; the ones that fail replay from their cells
+//                              out: as R, then n_failed (i32)
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <stdexcept>
@@ -49,7 +54,7 @@ int main(int argc, char **argv) {
         const int ncl = aos::cluster_union(W, H, np, root.data(), nb, bcell.data(), broot.data(), pc.data());
         put(fo, (int32_t)ncl);
         put(fo, pc);
-    } else if (mode == "R") {
+    } else if (mode == "R" || mode == "B") {
         aos::GridC g{};
         g.ox = in.get<double>(); g.oy = in.get<double>(); g.res = in.get<float>();
         g.W = in.get<int32_t>(); g.H = in.get<int32_t>();
@@ -67,7 +72,33 @@ int main(int argc, char **argv) {
             rec[c].length = in.get<float>();
             cells[c] = in.vec<int32_t>(n);
         }
-        for (int c = 0; c < ncl; ++c) jobs.push_back({c, cells[c].data(), (int)cells[c].size()});
+        int n_failed = 0;
+        if (mode == "B") {
+            const int nx = in.get<int32_t>();
+            const std::vector<int32_t> extra = in.vec<int32_t>(nx);
+            std::vector<uint64_t> bits((size_t)g.WW * g.H, 0ull);
+            auto set = [&](int p) { const int y = p / g.W, x = p - y * g.W; bits[(size_t)y * g.WW + x / 64] |= 1ull << (x % 64); };
+            for (int c = 0; c < ncl; ++c) {
+                aos::ClusterRec &r = rec[c];
+                r.bx0 = r.by0 = INT32_MAX; r.bx1 = r.by1 = -1; r.first = INT32_MAX;
+                for (int p : cells[c]) {
+                    set(p);
+                    const int y = p / g.W, x = p - y * g.W;
+                    r.bx0 = std::min(r.bx0, x); r.bx1 = std::max(r.bx1, x);
+                    r.by0 = std::min(r.by0, y); r.by1 = std::max(r.by1, y);
+                    r.first = std::min(r.first, p);
+                }
+            }
+            for (int p : extra) set(p);
+            for (int c = 0; c < ncl; ++c) jobs.push_back({c, nullptr, (int)cells[c].size(), bits.data()});
+            std::vector<int> failed;
+            aos::replay_clusters(jobs, g, poly.data(), np, min_len, rec.data(), nullptr, &failed);
+            n_failed = (int)failed.size();
+            jobs.clear();
+            for (int i : failed) jobs.push_back({i, cells[i].data(), (int)cells[i].size()});
+        } else {
+            for (int c = 0; c < ncl; ++c) jobs.push_back({c, cells[c].data(), (int)cells[c].size()});
+        }
         aos::replay_clusters(jobs, g, poly.data(), np, min_len, rec.data());
         for (const auto &r : rec) {
             put(fo, (int32_t)r.flags); put(fo, r.cx); put(fo, r.cy);
@@ -79,6 +110,7 @@ int main(int argc, char **argv) {
         put(fo, (int32_t)rows.size());
         put(fo, so.rows_info);
         put(fo, so.cluster_info);
+        if (mode == "B") put(fo, (int32_t)n_failed);
     } else {
         fprintf(stderr, "unknown mode %s\n", mode.c_str());
         return 2;

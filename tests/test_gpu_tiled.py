@@ -92,15 +92,18 @@ def test_tiled_c1_equals_single_gpu(tiles, root):
 
 
 @pytest.mark.parametrize("mode", ["all_gather", "rounds"])
-def test_tiled_c1_cell_exchange_paths(mode, monkeypatch):
+def test_tiled_c1_cell_exchange_paths(mode):
     """The distributed cluster stage sends each long cluster's cells to its one owner rank. Both other routes
     give the same frame: a communicator without all_to_all (the cells travel by all_gather and each owner
-    picks its blocks), and an exchange split into many small rounds (AOS_DEBUG_A2A_ROUND_BYTES)."""
+    picks its blocks), and an exchange split into many small rounds (aos_debug_faults)."""
     cfg = orchard.CONFIGS["C1"]
     cloud, poly = orchard.generate(cfg), orchard.polygon(cfg)
     if mode == "rounds":
-        monkeypatch.setenv("AOS_DEBUG_A2A_ROUND_BYTES", "4096")
-    tiled = _tiled_threads(cloud, poly, cfg.res, 2, 2, 1, a2a=mode != "all_gather")
+        aos_gpu.debug_faults(a2a_round_bytes=4096)
+    try:
+        tiled = _tiled_threads(cloud, poly, cfg.res, 2, 2, 1, a2a=mode != "all_gather")
+    finally:
+        aos_gpu.debug_faults()
     _assert_same(_single(cloud, poly, cfg.res), tiled)
 
 
@@ -365,9 +368,9 @@ def test_group_stream_4x2_equals_single_gpu_stream():
     single.close()
 
 
-def test_tiled_stuck_lookback_fails_every_rank(monkeypatch):
+def test_tiled_stuck_lookback_fails_every_rank():
     """A tiled rank whose ROR column scan reports a stuck look-back (bit 4 of its overflow word, injected with
-    AOS_DEBUG_ROR_STUCK_RANK) must not leave the frame alone: the bit travels with the kept counts in the
+    aos_debug_faults) must not leave the frame alone: the bit travels with the kept counts in the
     max-reduction, so every rank raises the same error and none is left inside a collective.
     The group is never aborted here: a rank that left early would show as a barrier timeout instead."""
     cfg = orchard.CONFIGS["C1"]
@@ -388,13 +391,15 @@ def test_tiled_stuck_lookback_fails_every_rank(monkeypatch):
         except BaseException as e:   # noqa: BLE001
             errs[r] = e
 
-    monkeypatch.setenv("AOS_DEBUG_ROR_STUCK_RANK", "1")
-    ts = [threading.Thread(target=work, args=(r,)) for r in range(world)]
-    for t in ts:
-        t.start()
-    for t in ts:
-        t.join(180)
-    monkeypatch.delenv("AOS_DEBUG_ROR_STUCK_RANK")
+    aos_gpu.debug_faults(ror_stuck_rank=1)
+    try:
+        ts = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(180)
+    finally:
+        aos_gpu.debug_faults()
     for r in range(world):
         assert isinstance(errs[r], RuntimeError) and "bits 4" in str(errs[r]) and "look-back" in str(errs[r]), (r, errs[r])
     # both handles still work on the next frame
@@ -410,3 +415,40 @@ def test_tiled_stuck_lookback_fails_every_rank(monkeypatch):
     assert out[0] is not None and out[0]["root"] and out[1] is not None
     for c in ctxs:
         c.close()
+
+
+@pytest.mark.parametrize("tiles", [(2, 1), (2, 2)])
+def test_rccl_ranks_as_processes(tiles, tmp_path):
+    """The library's RCCL communicator between real ranks: `world` processes on the box's one GPU, each with its
+    own NCCL_HOSTID so that RCCL accepts them (it refuses two ranks on one device of one host) and links them
+    over its socket transport on loopback. Every frame's collectives are the production path's: ncclAllGather
+    of the halo strips and piece tables, ncclAllReduce(max) of the thinning flags, the send-to-root of the
+    final tiles and the grouped ncclSend / ncclRecv of the cluster exchange (also in 4 KB rounds), all enqueued
+    on the frame's stream. Roots rotate; each root's frame, grids and GvdGraph equal the single-GPU frame
+    (tests/rccl_rank_child.py)."""
+    import subprocess
+    import sys
+    world = tiles[0] * tiles[1]
+    here = os.path.dirname(os.path.abspath(__file__))
+    uid = str(tmp_path / "uid.bin")
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, NCCL_HOSTID=f"aos-rank-{r}", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(here, "rccl_rank_child.py"), str(r), str(world),
+                                       str(tiles[0]), str(tiles[1]), uid], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=150)[0])
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for r, (p, o) in enumerate(zip(procs, outs)):
+        assert p.returncode == 0 and "RCCL_RANK_OK" in o, f"rank {r} rc={p.returncode}:\n{o[-3000:]}"
+    reports = [json.loads(o.split("RCCL_RANK_OK ", 1)[1].splitlines()[0]) for o in outs]
+    print(json.dumps(reports))
+    # non-root ranks send their final tiles to the root only: a rank's bytes per frame stay below an all-gather's
+    for rep in reports:
+        assert len(rep["frames"]) == world + 1

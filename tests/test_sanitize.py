@@ -99,12 +99,16 @@ def test_cluster_union_under_asan_ubsan(built, tiles, tmp_path):
     assert ncl == n and np.array_equal(pc, cid_map[root // W, root % W])
 
 
-@pytest.mark.parametrize("visited", ["bitmap", "hash"])
+@pytest.mark.parametrize("visited", ["bitmap", "hash", "bits"])
 def test_cluster_replays_and_rows_under_asan_ubsan(built, tmp_path, visited):
     """Every cluster of a C1 frame through the exact BFS replay (cells shuffled: the replay starts from the
     smallest) and the row assembly, vs the oracle's cluster centres, rows, rows_info and cluster_info; with
     the visited marks in the bounding-box bitmap (the product's choice at C1) and in the hash
-    (AOS_REPLAY_HASH=1, the choice for clusters whose box is large against their size)."""
+    (AOS_REPLAY_HASH=1, the choice for clusters whose box is large against their size). "bits": the replays walk
+    a skeleton bit grid over each cluster's box from its first cell (the product's path when the skeleton's bits
+    come to the host), with extra skeleton cells that belong to no cluster: one 8-adjacent to each of a few
+    clusters inside their box (a polygon cutting the box: those replays must fail and go through their cells),
+    and some in other clusters' boxes but adjacent to none (no effect)."""
     import oracle_py as O
     import orchard
     cfg = orchard.CONFIGS["C1"]
@@ -122,7 +126,43 @@ def test_cluster_replays_and_rows_under_asan_ubsan(built, tmp_path, visited):
         lin = (xy[:, 1].astype(np.int64) * W + xy[:, 0]).astype(np.int32)
         rng.shuffle(lin)
         blob += np.int32(len(lin)).tobytes() + np.float32(o["cluster_length"][c]).tobytes() + lin.tobytes()
-    raw = _cluster_run(built, "R", blob, tmp_path, env={"AOS_REPLAY_HASH": "1" if visited == "hash" else "0"})
+    expect_failed = None
+    if visited == "bits":
+        taken = set()
+        for c in range(len(off) - 1):
+            xy = cells[off[c]:off[c + 1]]
+            taken.update((xy[:, 1].astype(np.int64) * W + xy[:, 0]).tolist())
+        extra, expect_failed = [], 0
+        for c in range(0, len(off) - 1, 7):   # a cell 8-adjacent to the cluster's first cell, inside its box
+            xy = cells[off[c]:off[c + 1]]
+            x0, x1, y0, y1 = xy[:, 0].min(), xy[:, 0].max(), xy[:, 1].min(), xy[:, 1].max()
+            fy, fx = divmod(int((xy[:, 1].astype(np.int64) * W + xy[:, 0]).min()), W)
+            for dx, dy in ((1, 0), (1, 1), (0, 1), (-1, 1)):
+                x, y = fx + dx, fy + dy
+                if x0 <= x <= x1 and y0 <= y <= y1 and y * W + x not in taken:
+                    extra.append(y * W + x)
+                    taken.add(y * W + x)
+                    expect_failed += 1
+                    break
+        # (a cell inside a box but two cells away from every cell of every cluster changes nothing)
+        for c in range(3, len(off) - 1, 11):
+            xy = cells[off[c]:off[c + 1]]
+            x0, x1, y0, y1 = xy[:, 0].min(), xy[:, 0].max(), xy[:, 1].min(), xy[:, 1].max()
+            for y in range(y0, y1 + 1):
+                for x in range(x0, x1 + 1):
+                    if all((y + j) * W + (x + i) not in taken for i in (-2, -1, 0, 1, 2) for j in (-2, -1, 0, 1, 2)):
+                        extra.append(y * W + x)
+                        taken.add(y * W + x)
+                        break
+                else:
+                    continue
+                break
+        blob += np.int32(len(extra)).tobytes() + np.array(extra, np.int32).tobytes()
+    mode = "B" if visited == "bits" else "R"
+    raw = _cluster_run(built, mode, blob, tmp_path, env={"AOS_REPLAY_HASH": "1" if visited == "hash" else "0"})
+    if mode == "B":
+        assert int(np.frombuffer(raw[-4:], np.int32)[0]) == expect_failed > 0
+        raw = raw[:-4]
     ncl = len(off) - 1
     rec = np.frombuffer(raw[:ncl * 60], dtype=np.dtype([("flags", "<i4"), ("cx", "<f4"), ("cy", "<f4"),
                                                         ("c", "<f8", 6)]))
