@@ -267,6 +267,7 @@ def lib():
         L.aos_stream.restype = c_vp
         L.aos_stream.argtypes = [c_vp]
         L.aos_cluster_union.argtypes = [c_i, c_i, c_i, c_vp, c_i, c_vp, c_vp, c_vp, P(c_i)]
+        L.aos_debug_scan.argtypes = [c_vp, c_vp, c_vp, c_i, c_i]
         L.aos_debug_faults.restype = None
         L.aos_debug_faults.argtypes = [c_i, c_u64]
         L.aos_comm_init.restype = None
@@ -592,6 +593,10 @@ class Ctx:
         out = np.zeros(shape, dtype=np.int8)
         _check(lib().aos_debug_grid(self.h, which.encode(), out.ctypes.data, out.size))
         return out
+
+    def debug_scan(self, d_in: int, d_out: int, n: int, zero_in: bool = False):
+        """aos_debug_scan on device pointers: d_out[0..n] = the exclusive prefix sums of d_in[0..n)."""
+        _check(lib().aos_debug_scan(self.h, d_in, d_out, int(n), int(zero_in)))
 
     def stream(self) -> int:
         return lib().aos_stream(self.h)

@@ -240,6 +240,7 @@ struct aos_ctx {
     aos_tiled_stats tstats{};   // the last tiled frame's breakdown (aos_tiled_stats_get)
     std::vector<hipEvent_t> coll_ev;   // FrameComm: begin / end events of the frame's enqueued collectives
     aos::DevBuf coll_red;              // FrameComm: the reduced thinning flags
+    aos::LookBackScratch debug_lb;     // aos_debug_scan
     void tile_halo_exchange(uint64_t *win, const aos::TilePlan &t, aos::FrameComm &fc);
     void run_gvd_external(const aos_gvd_in &in, aos_gvd_out &out);
     void run_gvd_from_frame(aos_gvd_out &out);

@@ -435,6 +435,20 @@ int aos_path_plan(aos_ctx *c, const aos_path_graph *graph, const int8_t *skeleto
     AOS_GUARD_END
 }
 
+int aos_debug_scan(aos_ctx *c, int32_t *d_in, int32_t *d_out, int32_t n, int zero_in) {
+    if (!c || (n > 0 && (!d_in || !d_out)) || n < 0) { set_error("aos_debug_scan: bad argument"); return AOS_E_INVALID; }
+    AOS_GUARD_BEGIN
+    DeviceScope dev_scope(c->device);
+    aos::scan_1p(c->debug_lb, d_in, d_out, n, zero_in != 0, c->stream);
+    int *err = c->debug_lb.err_word(c->stream);
+    int h = 0;
+    AOS_HIP(hipMemcpyAsync(&h, err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    AOS_HIP(hipStreamSynchronize(c->stream));
+    if (h) { set_error("aos_debug_scan: look-back error word " + std::to_string(h)); return AOS_E_HIP; }
+    return AOS_OK;
+    AOS_GUARD_END
+}
+
 int aos_debug_grid(aos_ctx *c, const char *which, int8_t *dst, uint64_t capacity) {
     if (!c || !which || !dst) { set_error("aos_debug_grid: null argument"); return AOS_E_INVALID; }
     if (!c->have_frame) { set_error("aos_debug_grid: no frame"); return AOS_E_STATE; }

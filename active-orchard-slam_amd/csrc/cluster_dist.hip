@@ -171,7 +171,7 @@ __global__ void k_segments(const Seg *segs, const int *landing, int *cells) {
 // memory (host ends move by kernel stores: copy_to_host / copy_from_host). Stream-ordered collectives need no
 // wait between the chunks (the stream orders each chunk's copies around its all-gather); a host dst is waited for.
 static void gather_bytes(FrameComm &fc, hipStream_t s, const void *src, bool src_dev, const std::vector<uint64_t> &sizes,
-                         void *dst, bool dst_dev) {
+                         void *dst, bool dst_dev, PinnedBuf &h_recv) {
     const aos_comm &cm = fc.c;
     const uint64_t B = cm.buf_bytes & ~7ull;
     if (!B) throw CommError{"aos_comm.buf_bytes too small"};
@@ -188,16 +188,28 @@ static void gather_bytes(FrameComm &fc, hipStream_t s, const void *src, bool src
             else copy_from_host(cm.send_buf, p, m, s);
         }
         fc.all_gather(c, s);
+        if (!dst_dev) {   // the chunk's whole receive buffer in one read-back, then each rank's bytes on the host
+            uint64_t last = 0;   // (up to the last rank's bytes in this chunk)
+            for (int r = 0; r < cm.world; ++r)
+                if (sizes[r] > off) last = (uint64_t)r * c + std::min(c, sizes[r] - off);
+            uint8_t *h = static_cast<uint8_t *>(h_recv.ensure(std::max<uint64_t>(last, 16)));
+            // (whole 16-byte words while they stay inside recv_buf's world * buf_bytes: the copy kernel's uint4 form)
+            copy_to_host(h, cm.recv_buf, std::min<uint64_t>((last + 15) & ~15ull, (uint64_t)cm.world * cm.buf_bytes), s);
+            AOS_HIP(hipStreamSynchronize(s));
+            for (int r = 0; r < cm.world; ++r) {
+                const uint64_t v = sizes[r] > off ? std::min(c, sizes[r] - off) : 0;
+                if (v) std::memcpy(static_cast<uint8_t *>(dst) + at[r] + off, h + (uint64_t)r * c, v);
+            }
+            continue;
+        }
         for (int r = 0; r < cm.world; ++r) {
             const uint64_t v = sizes[r] > off ? std::min(c, sizes[r] - off) : 0;
-            if (!v) continue;
-            uint8_t *d = static_cast<uint8_t *>(dst) + at[r] + off;
-            const uint8_t *q = static_cast<const uint8_t *>(cm.recv_buf) + (uint64_t)r * c;
-            if (dst_dev) AOS_HIP(hipMemcpyAsync(d, q, v, hipMemcpyDeviceToDevice, s));
-            else copy_to_host(d, q, v, s);
+            if (v) AOS_HIP(hipMemcpyAsync(static_cast<uint8_t *>(dst) + at[r] + off,
+                                          static_cast<const uint8_t *>(cm.recv_buf) + (uint64_t)r * c, v,
+                                          hipMemcpyDeviceToDevice, s));
         }
+        if (!fc.ordered()) AOS_HIP(hipStreamSynchronize(s));   // (the next chunk's all-gather rewrites recv_buf)
     }
-    if (!dst_dev || !fc.ordered()) AOS_HIP(hipStreamSynchronize(s));   // (host data read next / recv_buf reused)
 }
 
 template <class T> static T *dptr(DevBuf &b, size_t n) { return static_cast<T *>(b.ensure(sizeof(T) * std::max<size_t>(n, 1))); }
@@ -221,7 +233,7 @@ static const int *exchange_cells(FrameComm &fc, ClusterDistState &D, hipStream_t
         for (int b = 0; b < W; ++b) { row[a] += cnt[(size_t)a * W + b]; col[b] += cnt[(size_t)a * W + b]; }
     if (!fc.has_all_to_all()) {   // through all_gather: everyone's route buffer, then this rank's blocks from it
         uint8_t *all = dptr<uint8_t>(D.landing, std::accumulate(row.begin(), row.end(), (uint64_t)0));
-        gather_bytes(fc, s, send, true, row, all, true);
+        gather_bytes(fc, s, send, true, row, all, true, D.h_recv);
         uint64_t at = 0;
         for (int r = 0; r < W; ++r) {
             uint64_t pre = 0;
@@ -337,7 +349,7 @@ void cluster_dist(ClusterDistState &D, FrameComm &fc, const TilePlan &t, const F
         NB += slots[2 * r + 1];
     }
     uint8_t *hall = hptr<uint8_t>(D.h_all, btot);
-    gather_bytes(fc, s, d_blob, true, bsz, hall, false);
+    gather_bytes(fc, s, d_blob, true, bsz, hall, false, D.h_recv);
     const int NP = rp0[world];
     std::vector<PieceRec> all((size_t)NP);
     std::vector<int> proot(NP), pcl(NP), bc((size_t)NB), br((size_t)NB);
@@ -487,7 +499,7 @@ void cluster_dist(ClusterDistState &D, FrameComm &fc, const TilePlan &t, const F
         OwnedOut *ho = hptr<OwnedOut>(D.h_out, (size_t)std::max(nown, 1));
         for (int j = 0; j < nown; ++j) ho[j] = OwnedOut{mine_l[j], replayed[j], lrec[mine_l[j]]};
         OwnedOut *ha = hptr<OwnedOut>(D.h_tab, (size_t)nlong);
-        gather_bytes(fc, s, ho, false, rsz, ha, false);
+        gather_bytes(fc, s, ho, false, rsz, ha, false, D.h_recv);
         int n_bfs_long = 0;   // (a replay clears the record's flag: the owners say which they replayed)
         for (int k = 0; k < nlong; ++k) {
             lrec[ha[k].l] = ha[k].r;

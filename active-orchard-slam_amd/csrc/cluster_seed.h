@@ -176,6 +176,7 @@ struct ClusterDistState {
     CclScratch ccl;
     DevBuf poly, fg, cnt, pieces, pid, prank, border, counts, blob, poff, sendbuf, landing, segs, cells, coff, rec;
     PinnedBuf h, h_poly, h_poff, h_segs, h_coff, h_rec, h_cells, h_out, h_tab, h_all;   // (one per upload / read-back)
+    PinnedBuf h_recv;   // gather_bytes: a chunk's receive buffer in host memory (one read-back per chunk)
 };
 struct ClusterDistStats {
     int n_pieces = 0, n_border = 0, n_long = 0, long_cells = 0, n_replayed_here = 0;

@@ -87,10 +87,12 @@ int *LookBackScratch::err_word(hipStream_t s) {
 // [4t, 4t + 4) of each of the tile's kScanPer / 4 quarters, so a wave instruction covers 1 KB of consecutive
 // memory (round 5 read 8 consecutive ints per lane as dwords at a 32-byte lane stride: 2 KB touched per 256 B
 // moved). The quarters are scanned one after another inside the block, then the blocks chain by a decoupled
-// look-back. Problems of at most kScanSmall + 1 ints take one workgroup with a running carry (no ticket, no
+// look-back. A tile is 8192 ints: the look-back of a block that meets only aggregates walks back 64 blocks per
+// step, so the chain's length sets the launch's time (C3 trace, 2048-int tiles: 2.1 M ints in 22.8 us, 1032
+// blocks). Problems of at most kScanSmall + 1 ints take one workgroup with a running carry (no ticket, no
 // look-back words).
-constexpr int kScanTB = 256, kScanPer = 8, kScanTile = kScanTB * kScanPer, kScanQ = kScanPer / 4;
-constexpr int kScanSmallTB = 1024, kScanSmall = 16 * 1024;
+constexpr int kScanTB = 256, kScanPer = 32, kScanTile = kScanTB * kScanPer, kScanQ = kScanPer / 4;
+constexpr int kScanSmallTB = 1024, kScanSmall = 64 * 1024;
 
 template <bool VEC>
 __device__ __forceinline__ int4 scan_load4(const int *in, long long i, int n) {
@@ -120,9 +122,45 @@ __device__ __forceinline__ void scan_zero4(int *in, long long i, int n) {
         if (i + k < n) in[i + k] = 0;
 }
 
+// Exclusive prefixes of NQ runs per thread over a block of NT threads, the runs ordered quarter-major (every thread's
+// run[0], then every thread's run[1], ...): before[q] = the sum of the runs ahead of (q, thread); returns the sum of all.
+// One barrier: each quarter's wave-inclusive scan by shuffles, the NQ x NT / 64 wave totals through LDS (wt), then
+// every thread adds up the totals ahead of it (NQ block scans one after another took two barriers each).
+template <int NQ, int NT>
+__device__ __forceinline__ int block_excl_scan_q(const int (&run)[NQ], int (&before)[NQ], int *wt) {
+    constexpr int NW = NT / 64;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int incl[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        incl[q] = run[q];
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(incl[q], o);
+            if (lane >= o) incl[q] += t;
+        }
+        if (lane == 63) wt[q * NW + w] = incl[q];
+    }
+    __syncthreads();
+    int acc = 0;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        int wb = 0, qt = 0;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) {
+            const int x = wt[q * NW + k];
+            wb += k < w ? x : 0;
+            qt += x;
+        }
+        before[q] = acc + wb + incl[q] - run[q];
+        acc += qt;
+    }
+    return acc;
+}
+
 template <bool VEC>
 __global__ __launch_bounds__(kScanTB) void k_scan_1p(int *in, int *out, int n, int zero_in, LookBack L) {
-    __shared__ int sh_vid, wsum[kScanTB / 64], sh_excl;
+    __shared__ int sh_vid, wt[kScanQ * kScanTB / 64], sh_excl;
     const int vid = lb_block_id(L, &sh_vid);
     const long long base = (long long)vid * kScanTile + 4LL * threadIdx.x;
     int4 v[kScanQ];
@@ -135,37 +173,41 @@ __global__ __launch_bounds__(kScanTB) void k_scan_1p(int *in, int *out, int n, i
     if (zero_in)
 #pragma unroll
         for (int q = 0; q < kScanQ; ++q) scan_zero4<VEC>(in, base + (long long)q * 4 * kScanTB, n);
-    int before[kScanQ], tot[kScanQ], agg = 0;
-#pragma unroll
-    for (int q = 0; q < kScanQ; ++q) {
-        before[q] = block_excl_scan<kScanTB>(run[q], wsum, &tot[q]);
-        agg += tot[q];
-    }
+    int before[kScanQ];
+    const int agg = block_excl_scan_q<kScanQ, kScanTB>(run, before, wt);
     if (threadIdx.x < 64) {
         const unsigned e = lb_exclusive(L, vid, (unsigned)agg);
         if (threadIdx.x == 0) sh_excl = (int)e;
     }
     __syncthreads();
-    int acc = sh_excl;
+    const int excl = sh_excl;
 #pragma unroll
-    for (int q = 0; q < kScanQ; ++q) {
-        scan_store4<VEC>(out, base + (long long)q * 4 * kScanTB, n, v[q], acc + before[q]);
-        acc += tot[q];
-    }
+    for (int q = 0; q < kScanQ; ++q) scan_store4<VEC>(out, base + (long long)q * 4 * kScanTB, n, v[q], excl + before[q]);
 }
 
-// one workgroup, n + 1 <= kScanSmall + 1: tiles of 4 kScanSmallTB ints with a running carry
+// one workgroup, n + 1 <= kScanSmall + 1: tiles of kScanSmallQ x 4 kScanSmallTB ints with a running carry (the wave
+// totals double-buffered: one barrier per tile)
+constexpr int kScanSmallQ = 4;
 template <bool VEC>
 __global__ __launch_bounds__(kScanSmallTB) void k_scan_small(int *in, int *out, int n, int zero_in) {
-    __shared__ int wsum[kScanSmallTB / 64];
-    int carry = 0;
-    for (long long t0 = 0; t0 <= n; t0 += 4 * kScanSmallTB) {
-        const long long i = t0 + 4LL * threadIdx.x;
-        const int4 v = scan_load4<VEC>(in, i, n);
-        if (zero_in) scan_zero4<VEC>(in, i, n);
-        int tot;
-        const int before = block_excl_scan<kScanSmallTB>(v.x + v.y + v.z + v.w, wsum, &tot);
-        scan_store4<VEC>(out, i, n, v, carry + before);
+    __shared__ int wt[2][kScanSmallQ * kScanSmallTB / 64];
+    int carry = 0, par = 0;
+    for (long long t0 = 0; t0 <= n; t0 += kScanSmallQ * 4 * kScanSmallTB, par ^= 1) {
+        const long long i0 = t0 + 4LL * threadIdx.x;
+        int4 v[kScanSmallQ];
+        int run[kScanSmallQ], before[kScanSmallQ];
+#pragma unroll
+        for (int q = 0; q < kScanSmallQ; ++q) {
+            v[q] = scan_load4<VEC>(in, i0 + (long long)q * 4 * kScanSmallTB, n);
+            run[q] = v[q].x + v[q].y + v[q].z + v[q].w;
+        }
+        if (zero_in)
+#pragma unroll
+            for (int q = 0; q < kScanSmallQ; ++q) scan_zero4<VEC>(in, i0 + (long long)q * 4 * kScanSmallTB, n);
+        const int tot = block_excl_scan_q<kScanSmallQ, kScanSmallTB>(run, before, wt[par]);
+#pragma unroll
+        for (int q = 0; q < kScanSmallQ; ++q)
+            scan_store4<VEC>(out, i0 + (long long)q * 4 * kScanSmallTB, n, v[q], carry + before[q]);
         carry += tot;
     }
 }

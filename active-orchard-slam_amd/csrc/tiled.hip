@@ -364,8 +364,11 @@ void aos_ctx::run_tiled_frame(FrameComm &fc, int tiles_x, int tiles_y, int root,
     long long budget = halo ? t.G - g.R - 2 : LLONG_MAX;   // sub-iterations the halo still supports
     std::vector<int32_t> fl;
     for (int period = 0;; ++period) {
-        const int nl = halo ? (int)(budget / (2 * K)) : (period == 0 ? 3 : 4);
+        int nl = halo ? (int)(budget / (2 * K)) : (period == 0 ? 3 : 4);
         if (nl < 1) throw std::logic_error("tile halo too small for one thinning launch");
+        // the first period stops where the last frame's T says the thinning ends (as the single-GPU frame sizes
+        // its first batch): a tiled launch cannot skip itself past convergence, so a spare one costs a full pass
+        if (period == 0) nl = std::min(nl, std::max(2, (thin_iters + 2 + K - 1) / K));
         for (int j = 0; j < nl; ++j) {
             uint64_t *dst = bufs[launched & 1];
             launch_thin_block(cur, dst, lg, launched * K, d_flags, mine, s);

@@ -432,6 +432,10 @@ int aos_path_plan(aos_ctx *ctx, const aos_path_graph *graph, const int8_t *skele
 /* Diagnostics: copy an internal device grid of the last frame to host as int8 {0,100}.
  * which: "raster", "inflated", "opened", "skeleton_frameless". */
 int aos_debug_grid(aos_ctx *ctx, const char *which, int8_t *dst, uint64_t capacity);
+/* Diagnostics: the library's single-pass exclusive scan (its counting sorts' and compactions' primitive) on the
+ * handle's stream: d_out[i] = d_in[0] + ... + d_in[i - 1] for i in [0, n] (n + 1 outputs), device int32 arrays on
+ * the handle's GPU; zero_in: d_in is left zero. Returns once done. */
+int aos_debug_scan(aos_ctx *ctx, int32_t *d_in, int32_t *d_out, int32_t n, int zero_in);
 /* Stream of the handle (hipStream_t as void*) for callers that time with their own events. */
 void *aos_stream(aos_ctx *ctx);
 /* Test hooks (fault injection for the tiled path's error tests; process-wide, not for production use):

@@ -87,6 +87,10 @@ for step in $STEPS; do
       AOS_TRACE=1 timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-pipelined-rate --no-device-rate --steps 6 \
         --warmup 2 > gpurun_out/${TAG}_trace.log 2> gpurun_out/${TAG}_trace.err || { tail -20 gpurun_out/${TAG}_trace.err; exit 1; }
       grep -c "aos trace" gpurun_out/${TAG}_trace.err ;;
+    tracec3)   # the same on C3 -> TAG_tracec3.err
+      AOS_TRACE=1 timeout -k 10 400 python -u bench.py --config C3 --no-cpu-baseline --no-pipelined-rate --no-device-rate \
+        --steps 4 --warmup 1 > gpurun_out/${TAG}_tracec3.log 2> gpurun_out/${TAG}_tracec3.err || { tail -20 gpurun_out/${TAG}_tracec3.err; exit 1; }
+      grep -c "aos trace" gpurun_out/${TAG}_tracec3.err ;;
     pmcsq)   # two SQ passes over the C2 bench for the kernels in PMC_KERNELS (a regex) -> TAG_pmcsq.txt
       K=${PMC_KERNELS:-k_occupancy|k_lfmis|k_ccl_local|k_scan_1p|k_rt_ror}
       rm -rf gpurun_out/${TAG}_sq1 gpurun_out/${TAG}_sq2
@@ -123,6 +127,16 @@ for step in $STEPS; do
         --master-addr 127.0.0.1 --master-port 29631 bench.py --gpus 2 --steps 8 --warmup 3 --no-cpu-baseline \
         > gpurun_out/${TAG}_ts2.log 2>&1 || { tail -30 gpurun_out/${TAG}_ts2.log; exit 1; }
       grep '^{' gpurun_out/${TAG}_ts2.log | cut -c1-300 ;;
+    rccl2)   # the driver's --gpus 2 flow over RCCL itself on the one GPU (AOS_BENCH_RCCL_SHARED_GPU: a NCCL_HOSTID per
+             # rank, RCCL's socket transport on loopback): the independent maps, then the tiled C3 / C4 extras
+      AOS_BENCH_RCCL_SHARED_GPU=1 timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+        --master-addr 127.0.0.1 --master-port 29651 bench.py --gpus 2 --steps 8 --warmup 2 --no-cpu-baseline \
+        > gpurun_out/${TAG}_rccl2.log 2>&1 || { tail -30 gpurun_out/${TAG}_rccl2.log; exit 1; }
+      grep '^{' gpurun_out/${TAG}_rccl2.log | cut -c1-400 ;;
+    c3bench)
+      timeout -k 10 600 python -u bench.py --config C3 --no-cpu-baseline --no-pipelined-rate --no-device-rate --steps 6 \
+        --warmup 2 > gpurun_out/${TAG}_c3_bench.log 2> gpurun_out/${TAG}_c3_bench.err || { tail -20 gpurun_out/${TAG}_c3_bench.err; exit 1; }
+      grep '^{' gpurun_out/${TAG}_c3_bench.log | cut -c1-300 ;;
     rorpmc)
       for b in ${RORBENCH:-tools/rorbench/rorbench}; do
         n=$(basename $b)
