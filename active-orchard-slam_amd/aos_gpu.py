@@ -192,7 +192,7 @@ class TiledStats(ctypes.Structure):
     _fields_ = [("ms_frame", c_f), ("ms_comm_gather", c_f), ("ms_comm_reduce", c_f), ("n_gather", c_i),
                 ("n_reduce", c_i), ("bytes_gather", c_u64), ("ms_ror", c_f), ("ms_thin", c_f), ("ms_cluster", c_f),
                 ("ms_seeds", c_f), ("ms_cluster_local", c_f), ("ms_cluster_global", c_f), ("ms_replay", c_f),
-                ("n_replayed", c_i), ("ror_skipped", c_i), ("is_root", c_i)]
+                ("n_replayed", c_i), ("ror_skipped", c_i), ("is_root", c_i), ("bytes_recv", c_u64)]
 
 
 def build() -> str:

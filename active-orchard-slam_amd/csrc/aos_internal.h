@@ -266,6 +266,9 @@ struct StreamColl {
     void (*gather)(void *impl, uint64_t bytes, int root, hipStream_t s) = nullptr;   // the root's recv_buf only
     void (*max_dev)(void *impl, int32_t *d, int n, hipStream_t s) = nullptr;         // device int32, in place
     void (*all_to_all)(void *impl, const uint64_t *counts, hipStream_t s) = nullptr; // as aos_comm.all_to_all
+    // send_buf[0, bytes) to every rank r with peer[r] != 0 and each such rank's block into recv_buf[r * bytes, ...):
+    // an all-gather restricted to a symmetric set of peers (the halo exchange: the tiles next to this one)
+    void (*exchange)(void *impl, uint64_t bytes, const uint8_t *peer, hipStream_t s) = nullptr;
 };
 bool rccl_stream_coll(const aos_comm &cm, StreamColl &out);   // true: cm is the library's RCCL communicator
 
@@ -281,11 +284,14 @@ struct FrameComm {
     int ev_used = 0;
     double ms_gather = 0.0, ms_reduce = 0.0;   // host clock
     int n_gather = 0, n_reduce = 0;
-    uint64_t bytes_sent = 0;
+    uint64_t bytes_sent = 0, bytes_recv = 0;
     FrameComm(const aos_comm &cm, std::vector<hipEvent_t> &pool, DevBuf &scratch);
     bool ordered() const { return sc.all_gather != nullptr; }
     bool has_all_to_all() const { return ordered() ? sc.all_to_all != nullptr : c.all_to_all != nullptr; }
     void all_gather(uint64_t bytes, hipStream_t s);
+    // recv_buf[r * bytes, ...) = rank r's send_buf[0, bytes) for every r with peer[r] != 0 (peer symmetric over the
+    // ranks); other blocks of recv_buf undefined. An all-gather when the communicator has no point-to-point form.
+    void neighbour_exchange(uint64_t bytes, const uint8_t *peer, hipStream_t s);
     // rank r's send_buf[0, bytes) -> the root's recv_buf[r * bytes, (r + 1) * bytes); the other ranks' recv_buf is
     // not written when the communicator has a personalised exchange (else it is an all-gather)
     void gather(uint64_t bytes, int root, hipStream_t s);

@@ -196,6 +196,25 @@ static void sc_all_to_all(void *impl, const uint64_t *counts, hipStream_t s) {
     rccl_check(api, api.group_end(), "ncclGroupEnd");
 }
 
+// the halo exchange: this rank's strips to each peer, each peer's strips into its block (grouped point-to-point:
+// a rank receives its 3-8 neighbours' strips instead of every rank's)
+static void sc_exchange(void *impl, uint64_t bytes, const uint8_t *peer, hipStream_t s) {
+    aos_rccl *r = static_cast<aos_rccl *>(impl);
+    const RcclApi &api = rccl_api();
+    DeviceScope ds(r->device);
+    const int W = r->c.world, me = r->c.rank;
+    if (bytes > r->c.buf_bytes) throw CommError{"exchange larger than the RCCL buffers"};
+    if (!bytes || W == 1) return;
+    char *rb = static_cast<char *>(r->recv.p);
+    rccl_check(api, api.group_start(), "ncclGroupStart");
+    for (int q = 0; q < W; ++q) {
+        if (q == me || !peer[q]) continue;
+        rccl_check(api, api.send(r->send.p, bytes, ncclUint8, q, r->comm, s), "ncclSend");
+        rccl_check(api, api.recv(rb + (uint64_t)q * bytes, bytes, ncclUint8, q, r->comm, s), "ncclRecv");
+    }
+    rccl_check(api, api.group_end(), "ncclGroupEnd");
+}
+
 bool rccl_stream_coll(const aos_comm &cm, StreamColl &out) {
     if (cm.all_gather != rc_all_gather || !cm.user) return false;   // (a caller's communicator: its callbacks)
     out.impl = cm.user;
@@ -203,6 +222,7 @@ bool rccl_stream_coll(const aos_comm &cm, StreamColl &out) {
     out.gather = sc_gather;
     out.max_dev = sc_max_dev;
     out.all_to_all = sc_all_to_all;
+    out.exchange = sc_exchange;
     return true;
 }
 

@@ -20,6 +20,7 @@
 #include <climits>
 #include <cstring>
 #include <stdexcept>
+#include <vector>
 
 #include "aos_ctx.h"
 
@@ -189,6 +190,7 @@ float FrameComm::ms_enqueued() {
 void FrameComm::all_gather(uint64_t bytes, hipStream_t s) {
     ++n_gather;
     bytes_sent += bytes;
+    bytes_recv += (uint64_t)(c.world - 1) * bytes;
     if (ordered()) {
         EnqTimer t(*this, s);
         sc.all_gather(sc.impl, bytes, s);
@@ -201,9 +203,22 @@ void FrameComm::all_gather(uint64_t bytes, hipStream_t s) {
     if (r != 0) throw CommError{"aos_comm.all_gather failed"};
 }
 
+void FrameComm::neighbour_exchange(uint64_t bytes, const uint8_t *peer, hipStream_t s) {
+    if (!ordered() || !sc.exchange) return all_gather(bytes, s);
+    ++n_gather;
+    for (int r = 0; r < c.world; ++r)
+        if (r != c.rank && peer[r]) { bytes_sent += bytes; bytes_recv += bytes; }
+    EnqTimer t(*this, s);
+    sc.exchange(sc.impl, bytes, peer, s);
+}
+
 void FrameComm::all_to_all(const uint64_t *counts, hipStream_t s) {
     ++n_gather;
-    for (int d = 0; d < c.world; ++d) bytes_sent += counts[(size_t)c.rank * c.world + d];
+    for (int d = 0; d < c.world; ++d)
+        if (d != c.rank) {
+            bytes_sent += counts[(size_t)c.rank * c.world + d];
+            bytes_recv += counts[(size_t)d * c.world + c.rank];
+        }
     if (ordered()) {
         EnqTimer t(*this, s);
         sc.all_to_all(sc.impl, counts, s);
@@ -221,6 +236,7 @@ void FrameComm::gather(uint64_t bytes, int root, hipStream_t s) {
     if (ordered()) {
         ++n_gather;
         bytes_sent += c.rank == root ? 0 : bytes;
+        bytes_recv += c.rank == root ? (uint64_t)(c.world - 1) * bytes : 0;
         EnqTimer t(*this, s);
         sc.gather(sc.impl, bytes, root, s);
         return;
@@ -271,7 +287,15 @@ void aos_ctx::tile_halo_exchange(uint64_t *win, const TilePlan &t, FrameComm &fc
     k_pack_border<<<cdiv(n, 256), 256, 0, stream>>>(win, t.lg.WW, t.y0 - t.wy0, t.c0 - t.wc0, nr, nc, t.hy, t.hw,
                                                     static_cast<uint64_t *>(fc.c.send_buf));
     AOS_HIP(hipGetLastError());
-    fc.all_gather(8ull * (uint64_t)t.max_border, stream);
+    // the strips go to the tiles next to this one only (8-neighbourhood: a halo word lies in an adjacent tile,
+    // the plan keeps every tile at least as large as the halo); symmetric, so every rank pairs its sends
+    std::vector<uint8_t> peer((size_t)fc.c.world, 0);
+    for (int dy = -1; dy <= 1; ++dy)
+        for (int dx = -1; dx <= 1; ++dx) {
+            const int x = t.tx + dx, y = t.ty + dy;
+            if ((dx || dy) && x >= 0 && x < t.tiles_x && y >= 0 && y < t.tiles_y) peer[(size_t)y * t.tiles_x + x] = 1;
+        }
+    fc.neighbour_exchange(8ull * (uint64_t)t.max_border, peer.data(), stream);
     const TileSplit S = split_of(t, t.max_border);
     dim3 grid(cdiv(t.lg.WW, 64), t.lg.H);
     k_unpack_halo<<<grid, 64, 0, stream>>>(win, t.lg.WW, t.lg.H, t.wy0, t.wc0, t.y0, t.y1, t.c0, t.c1, S,
@@ -292,6 +316,7 @@ void aos_ctx::run_tiled(const aos_comm &cm, int tiles_x, int tiles_y, int root, 
         tstats.n_gather = fc.n_gather;
         tstats.n_reduce = fc.n_reduce;
         tstats.bytes_gather = fc.bytes_sent;
+        tstats.bytes_recv = fc.bytes_recv;
         tstats.ms_cluster_local = cdist_stats.ms_local;
         tstats.ms_cluster_global = cdist_stats.ms_global;
         tstats.ms_replay = cdist_stats.ms_replay;

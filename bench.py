@@ -431,6 +431,9 @@ def tiled_breakdown(res, pend, warmup: int, world: int, rank: int, dist):
     mine["ms_compute"] = round(mine["ms_frame"] - mine["ms_comm_gather"] - mine["ms_comm_reduce"], 3)
     mine["collectives_per_frame"] = round(sum(t["n_gather"] + t["n_reduce"] for t in sts) / max(1, len(sts)), 1)
     mine["gather_MB_per_frame"] = round(sum(t["bytes_gather"] for t in sts) / max(1, len(sts)) / 1e6, 3)
+    mine["recv_MB_per_frame"] = round(sum(t.get("bytes_recv", 0) for t in sts) / max(1, len(sts)) / 1e6, 3)
+    nonroot = [t for t in sts if not t["is_root"]]
+    mine["recv_MB_nonroot_frame"] = round(sum(t.get("bytes_recv", 0) for t in nonroot) / max(1, len(nonroot)) / 1e6, 3)
     mine["ror_skipped_frames"] = sum(t["ror_skipped"] for t in sts)
     root_frames = [(k, t) for k, (gs, _) in enumerate(res) if gs.get("root") for t in [gs.get("tiled_stats")] if t]
     gstart = pend.get("gvd_start", {})

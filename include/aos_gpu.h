@@ -323,6 +323,8 @@ typedef struct aos_tiled_stats {
     int32_t n_replayed;        /* clusters replayed on this rank                                     */
     int32_t ror_skipped;       /* streaming: 1 if no new point reached this rank's box (stage skipped) */
     int32_t is_root;
+    uint64_t bytes_recv;       /* payload this rank received (halo strips, tables, the final tiles on the root, the
+                                  owned clusters' cells, records)                                     */
 } aos_tiled_stats;
 int aos_tiled_stats_get(aos_ctx *ctx, aos_tiled_stats *out);
 

@@ -85,7 +85,8 @@ def main():
             for key in GVD_KEYS:
                 assert np.array_equal(gg[key], gg1[key]), (k, key)
         report["frames"].append({"root": root, "rounds": rounds, "n_gather": st["n_gather"],
-                                 "gather_MB": round(st["bytes_gather"] / 1e6, 3), "ms_frame": round(st["ms_frame"], 2),
+                                 "gather_MB": round(st["bytes_gather"] / 1e6, 3), "recv_MB": round(st["bytes_recv"] / 1e6, 3),
+                                 "ms_frame": round(st["ms_frame"], 2),
                                  "ms_comm_gather": round(st["ms_comm_gather"], 2)})
     ctx.close()
     comm.close()

@@ -417,14 +417,15 @@ def test_tiled_stuck_lookback_fails_every_rank():
         c.close()
 
 
-@pytest.mark.parametrize("tiles", [(2, 1), (2, 2)])
+@pytest.mark.parametrize("tiles", [(2, 1), (3, 2)])
 def test_rccl_ranks_as_processes(tiles, tmp_path):
     """The library's RCCL communicator between real ranks: `world` processes on the box's one GPU, each with its
     own NCCL_HOSTID so that RCCL accepts them (it refuses two ranks on one device of one host) and links them
     over its socket transport on loopback. Every frame's collectives are the production path's: ncclAllGather
-    of the halo strips and piece tables, ncclAllReduce(max) of the thinning flags, the send-to-root of the
-    final tiles and the grouped ncclSend / ncclRecv of the cluster exchange (also in 4 KB rounds), all enqueued
-    on the frame's stream. Roots rotate; each root's frame, grids and GvdGraph equal the single-GPU frame
+    of the piece tables, grouped ncclSend / ncclRecv of the halo strips between neighbouring tiles only (3 x 2:
+    corner tiles have 3 neighbours, the middle column 5), ncclAllReduce(max) of the thinning flags, the
+    send-to-root of the final tiles and the grouped ncclSend / ncclRecv of the cluster exchange (also in 4 KB
+    rounds), all enqueued on the frame's stream. Roots rotate; each root's frame, grids and GvdGraph equal the single-GPU frame
     (tests/rccl_rank_child.py)."""
     import subprocess
     import sys
@@ -449,6 +450,10 @@ def test_rccl_ranks_as_processes(tiles, tmp_path):
         assert p.returncode == 0 and "RCCL_RANK_OK" in o, f"rank {r} rc={p.returncode}:\n{o[-3000:]}"
     reports = [json.loads(o.split("RCCL_RANK_OK ", 1)[1].splitlines()[0]) for o in outs]
     print(json.dumps(reports))
-    # non-root ranks send their final tiles to the root only: a rank's bytes per frame stay below an all-gather's
     for rep in reports:
         assert len(rep["frames"]) == world + 1
+    # a non-root rank receives no final tiles (they go to the root only), and its halo strips from its neighbours only
+    for k in range(world + 1):
+        root = reports[0]["frames"][k]["root"]
+        recv = [rep["frames"][k]["recv_MB"] for rep in reports]
+        assert all(recv[r] < recv[root] for r in range(world) if r != root), (k, recv)

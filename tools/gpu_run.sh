@@ -133,6 +133,11 @@ for step in $STEPS; do
         --master-addr 127.0.0.1 --master-port 29651 bench.py --gpus 2 --steps 8 --warmup 2 --no-cpu-baseline \
         > gpurun_out/${TAG}_rccl2.log 2>&1 || { tail -30 gpurun_out/${TAG}_rccl2.log; exit 1; }
       grep '^{' gpurun_out/${TAG}_rccl2.log | cut -c1-400 ;;
+    rccl6)   # the tiled C3 frame over 6 RCCL ranks on the one GPU (3 x 2 tiles: halo strips to neighbours only)
+      AOS_BENCH_RCCL_SHARED_GPU=1 timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 6 \
+        --master-addr 127.0.0.1 --master-port 29652 bench.py --gpus 6 --tiled --steps 6 --warmup 2 --no-cpu-baseline \
+        > gpurun_out/${TAG}_rccl6.log 2>&1 || { tail -30 gpurun_out/${TAG}_rccl6.log; exit 1; }
+      grep '^{' gpurun_out/${TAG}_rccl6.log | cut -c1-400 ;;
     c3bench)
       timeout -k 10 600 python -u bench.py --config C3 --no-cpu-baseline --no-pipelined-rate --no-device-rate --steps 6 \
         --warmup 2 > gpurun_out/${TAG}_c3_bench.log 2> gpurun_out/${TAG}_c3_bench.err || { tail -20 gpurun_out/${TAG}_c3_bench.err; exit 1; }
