@@ -127,7 +127,8 @@ struct aos_ctx {
     aos::FrameGeom geom{};                 // the whole map
     bool tiled_frame = false;
     int thin_iters = 0, thin_iters_prev = 0;   // (the previous frame's T sizes the first thinning batch)
-    // First thinning batch (flags reset, opening, n temporal-block launches) as hipGraphs, one per batch
+    // First thinning batch (n temporal-block launches; the opening, which clears the flags, runs just before it so the
+    // inflated grid's read-back can be queued behind it) as hipGraphs, one per batch
     // size n (a power of two), captured on first use and replayed while every pointer and size baked into
     // the graph is unchanged (seedgen.hip thin_first_batch). Graph shape: AOS_THIN_GRAPH (see there).
     struct ThinGraph {

@@ -4,9 +4,11 @@
 // max-reduction of the thinning flags one ncclAllReduce(ncclMax) of a small int32 array.
 //
 // RCCL is opened at run time (dlopen of librccl.so.1), so libaos_gpu.so loads without it and a
-// process that never asks for the communicator never initialises RCCL. The callbacks are
+// process that never asks for the communicator never initialises RCCL. The aos_comm callbacks are
 // collective and synchronous (aos_comm contract, include/aos_gpu.h): each one enqueues on the
-// communicator's own stream and waits for it.
+// communicator's own stream and waits for it. A tiled frame that recognises this communicator
+// (rccl_stream_coll) enqueues the same collectives on its own stream instead (StreamColl: no host wait),
+// plus two point-to-point forms: the halo strips to the neighbouring tiles only, the final tiles to the root.
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 

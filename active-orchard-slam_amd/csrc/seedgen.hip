@@ -679,7 +679,8 @@ bool aos_ctx::ror_collect(bool throw_stuck) {
     return u[1] != 0;
 }
 
-// First thinning batch of a whole-map frame: flags reset, opening, batch_n temporal-block launches
+// First thinning batch of a whole-map frame: flags reset, opening, after_open (the inflated grid's read-back),
+// batch_n temporal-block launches
 // (launch_next issues them and keeps the caller's launch state). With AOS_THIN_GRAPH != 0 the batch is a
 // hipGraph (BASELINE configs[4]: hipGraph-captured thinning; aos_params.thin_graph), one per batch size,
 // batch_n rounded up to a
@@ -688,8 +689,8 @@ bool aos_ctx::ror_collect(bool throw_stuck) {
 // flags buffer when it copies them, and W, H, WW, R, the launch count, the flags length) and re-captured
 // when any of them changes; the per-launch act_prev / act_next alternation is a function of the launch
 // index from 0, the same on every replay. Graph shapes (AOS_THIN_GRAPH, for the diagnosis of round 2's
-// failure, tools/thin_graph_probe.py): 1 (default) kernels only, the flags cleared by the opening kernel and
-// read back outside the graph; 2 round 1's shape: memset node + kernels + D2H copy node; 3 memset node +
+// failure, tools/thin_graph_probe.py): 1 (default) the thinning launches only, the opening (which clears the flags)
+// launched just before the graph and the flags read back outside it; 2 round 1's shape: memset node + kernels + D2H copy node; 3 memset node +
 // kernels; 4 clearing kernel + kernels + D2H copy node. Returns true when the graph copied the flags
 // of the batch to h_flags itself.
 bool aos_ctx::thin_first_batch(const FrameGeom &g, const uint64_t *d_ibits, uint64_t *d_open, uint64_t *const bufs[2],

@@ -6,15 +6,18 @@
 // with the single-GPU kernels unchanged. A window edge that is not a map edge acts as an image
 // border. That can only corrupt cells from the edge inward: R cells for the inflation, 2 for the
 // opening and 1 per Zhang-Suen sub-iteration. Before the damage reaches the tile, the halo is
-// refreshed from the neighbours' exact border strips (one all-gather of every tile's strips):
+// refreshed from the neighbours' exact border strips (each tile's strips to its 3-8 neighbouring tiles; an
+// all-gather through a communicator without point-to-point collectives):
 //   ROR + raster (own cells) -> exchange -> inflate -> open -> thin (G - R - 2 sub-iterations)
 //   -> [exchange -> thin (G sub-iterations)]* until converged.
 // Convergence is global: each rank flags the iterations that deleted one of its OWN cells, the
 // flags are max-reduced over ranks and the ximgproc stopping rule runs on the reduced flags. After
 // the first iteration that deletes nothing anywhere the map is a fixed point, so the extra
 // iterations of the last period change no own cell. Finally the bit-packed skeleton and inflated
-// tiles are all-gathered and the root rank finishes the frame (a6, a8-a16) on the whole map
-// exactly like aos_seedgen_process: every output is byte-identical to the single-GPU frame.
+// tiles go to the frame's root, which finishes the frame (a6, a16, seeds) on the whole map exactly like
+// aos_seedgen_process, with a8-a10 shared over the ranks (cluster_dist.hip): every output is
+// byte-identical to the single-GPU frame. With the library's RCCL communicator the collectives are
+// enqueued on the frame's stream (FrameComm / StreamColl): the host waits once per thinning period.
 #include <algorithm>
 #include <chrono>
 #include <climits>
