@@ -162,19 +162,22 @@ FrameComm::FrameComm(const aos_comm &cm, std::vector<hipEvent_t> &pool, DevBuf &
 }
 
 namespace {
-// events around one enqueued collective (the pool grows once, then is reused frame after frame)
+// events around one enqueued collective (the pool grows once, then is reused frame after frame); a pair that
+// cannot be created or recorded is left out of the timing, never half-counted
 struct EnqTimer {
     FrameComm &f;
     hipStream_t s;
-    EnqTimer(FrameComm &fc, hipStream_t st) : f(fc), s(st) { mark(); }
-    ~EnqTimer() { mark(); }
-    void mark() {
-        if ((int)f.ev.size() <= f.ev_used) {
+    bool ok = false;
+    EnqTimer(FrameComm &fc, hipStream_t st) : f(fc), s(st) {
+        while ((int)f.ev.size() < f.ev_used + 2) {
             hipEvent_t e;
             if (hipEventCreate(&e) != hipSuccess) return;   // (timing only)
             f.ev.push_back(e);
         }
-        if (hipEventRecord(f.ev[f.ev_used], s) == hipSuccess) ++f.ev_used;
+        ok = hipEventRecord(f.ev[f.ev_used], s) == hipSuccess;
+    }
+    ~EnqTimer() {
+        if (ok && hipEventRecord(f.ev[f.ev_used + 1], s) == hipSuccess) f.ev_used += 2;
     }
 };
 }  // namespace

@@ -817,6 +817,17 @@ def run(a, E, dist, quiet=False):
     thin_roof = {"alg_bytes": b_thin, "ms": round(t_thin, 4),
                  "achieved_GBs": round(b_thin / (t_thin * 1e-3) / 1e9, 1) if t_thin > 0 else 0.0}
     thin_roof["frac"] = round(thin_roof["achieved_GBs"] / HBM_PEAK_GBS, 4)
+    # the model above counts SURVEY §8d's 1 B per cell per sub-iteration; the bit-packed, temporally blocked kernel
+    # moves far less: its measured HBM bytes (the committed PMC passes) over the same stage time
+    t_pmc, t_src = (None, None) if (a.stream or a.tiled) else pmc_traffic(a.config, "k_thin_block")
+    if t_pmc is not None:
+        nl = g.get("thin_launches") or 0
+        thin_roof.update({"what": "achieved/frac: SURVEY §8d's model bytes (4 C T) over the stage; hbm_*: the kernel's "
+                                  "measured HBM bytes (FETCH x2 + WRITE, per launch x this frame's launches) over it; the "
+                                  "kernel is LDS / VALU bound",
+                          "hbm_bytes_per_frame": round(t_pmc * nl, 1), "launches": nl,
+                          "hbm_GBs": round(t_pmc * nl / (t_thin * 1e-3) / 1e9, 1) if t_thin > 0 else None,
+                          "hbm_source": t_src})
     # BASELINE.md:35-37 frame-level figure: B_alg = 12 N + C (6 + 4 T) over the per-frame wall-clock
     b_frame = 12.0 * float(n) + cells * (6.0 + 4.0 * T)   # (every input point is read once on the host)
     t_frame = med if not main_pipe else (_median(frame_lat) * 1e-3 if frame_lat else med)
