@@ -270,6 +270,9 @@ def lib():
         L.aos_debug_scan.argtypes = [c_vp, c_vp, c_vp, c_i, c_i]
         L.aos_debug_faults.restype = None
         L.aos_debug_faults.argtypes = [c_i, c_u64]
+        L.aos_debug_replay.restype = None
+        L.aos_debug_replay.argtypes = [c_i, c_i, c_i]
+        L.aos_replay_counts.argtypes = [c_vp, ctypes.POINTER(ctypes.c_int32)]
         L.aos_comm_init.restype = None
         L.aos_comm_init.argtypes = [c_vp]
         _lib = L
@@ -598,6 +601,12 @@ class Ctx:
         """aos_debug_scan on device pointers: d_out[0..n] = the exclusive prefix sums of d_in[0..n)."""
         _check(lib().aos_debug_scan(self.h, d_in, d_out, int(n), int(zero_in)))
 
+    def replay_counts(self) -> dict:
+        """aos_replay_counts: the last seed-gen frame's exact BFS replays, in all and by where they ran."""
+        out = (ctypes.c_int32 * 4)()
+        _check(lib().aos_replay_counts(self.h, out))
+        return {"all": out[0], "gpu": out[1], "host_bits": out[2], "host_cells": out[3]}
+
     def stream(self) -> int:
         return lib().aos_stream(self.h)
 
@@ -606,6 +615,13 @@ def debug_faults(ror_stuck_rank: int = -1, a2a_round_bytes: int = 0) -> None:
     """aos_debug_faults (test hooks, process-wide): a tiled rank that reports a stuck ROR look-back, and the
     cluster exchange's round-size cap; the defaults turn both off."""
     lib().aos_debug_faults(int(ror_stuck_rank), int(a2a_round_bytes))
+
+
+def debug_replay(gpu_min_clusters: int = -1, ring_cap: int = 0, replay_all: bool = False) -> None:
+    """aos_debug_replay (test hook, process-wide): the flagged-cluster count from which a seed-gen frame replays
+    its clusters on the GPU (-1: the library default; 0: always), a smaller queue ring for the GPU walk (0: 64),
+    and replay_all: every cluster replayed, certified or not. No arguments: the defaults."""
+    lib().aos_debug_replay(int(gpu_min_clusters), int(ring_cap), int(bool(replay_all)))
 
 
 class Group:

@@ -57,6 +57,9 @@ using namespace aos;
 namespace aos {
 std::atomic<int> g_debug_stuck_rank{-1};
 std::atomic<uint64_t> g_debug_a2a_round{0};
+std::atomic<int> g_debug_replay_min{-1};
+std::atomic<int> g_debug_replay_ring{0};
+std::atomic<bool> g_debug_replay_all{false};
 }  // namespace aos
 
 extern "C" {
@@ -123,6 +126,21 @@ void *aos_stream(aos_ctx *c) { return c ? (void *)c->stream : nullptr; }
 void aos_debug_faults(int32_t ror_stuck_rank, uint64_t a2a_round_bytes) {
     aos::g_debug_stuck_rank.store(ror_stuck_rank, std::memory_order_relaxed);
     aos::g_debug_a2a_round.store(a2a_round_bytes, std::memory_order_relaxed);
+}
+
+void aos_debug_replay(int32_t gpu_min_clusters, int32_t ring_cap, int32_t replay_all) {
+    aos::g_debug_replay_all.store(replay_all != 0, std::memory_order_relaxed);
+    aos::g_debug_replay_min.store(gpu_min_clusters < 0 ? -1 : gpu_min_clusters, std::memory_order_relaxed);
+    aos::g_debug_replay_ring.store(ring_cap > 0 ? ring_cap : 0, std::memory_order_relaxed);
+}
+
+int aos_replay_counts(aos_ctx *c, int32_t out[4]) {
+    if (!c || !out) { set_error("aos_replay_counts: null argument"); return AOS_E_INVALID; }
+    out[0] = c->n_bfs_replayed;
+    out[1] = c->cs.n_replay_gpu;
+    out[2] = c->cs.n_replay_from_bits;
+    out[3] = c->cs.n_replay_cells;
+    return AOS_OK;
 }
 
 void aos_comm_init(aos_comm *comm) {

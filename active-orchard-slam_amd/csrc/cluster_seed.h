@@ -1,5 +1,6 @@
 // Cluster / tree-row / seed stage and GVD stage state. Not part of the ABI.
 #pragma once
+#include <climits>
 #include <condition_variable>
 #include <exception>
 #include <functional>
@@ -98,6 +99,10 @@ struct ClusterSeedState {
     PinnedBuf h_misc;
     int n_fg = 0, n_clusters = 0, n_rows = 0, n_cur_tab = 0;
     int n_replay_from_bits = 0;   // the last frame's exact replays that walked the host skeleton bits
+    int n_replay_gpu = 0;         // ... that ran on the GPU (replay_gpu.hip)
+    int n_replay_cells = 0;       // ... that replayed from the clusters' cells on the host
+    DevBuf replay_ids, replay_order;   // the GPU replays' cluster list and their BFS orders
+    PinnedBuf h_replay;                // the list's upload staging and the replays' status words
     double cur_tab_amax = -1.0;
     std::vector<ClusterRec> h_rec;
     HostPool replay_pool;   // the BFS replays' host threads (replay_clusters)
@@ -138,6 +143,22 @@ void launch_cluster_stats(const int *off, const int *cells, int n_clusters, cons
 struct ReplayJob { int c; const int *cells; int n; const uint64_t *bits = nullptr; };
 void replay_clusters(const std::vector<ReplayJob> &jobs, const GridC &g, const double *poly, int np, float min_len,
                      ClusterRec *rec, HostPool *pool = nullptr, std::vector<int> *failed = nullptr);
+// The same replays on the GPU (replay_gpu.hip), one wave per cluster, for frames with many of them: d_ids (device)
+// lists n_jobs clusters whose bordered box bitmap takes at most lds_words 32-bit words (replay_bitmap_words; -1: not
+// on the GPU). A replayed cluster's record is updated in rec and hrec (pinned) and h_status[j] = 0; a cluster the
+// GPU leaves (frontier wider than 64 cells, inconsistent cells) keeps its records and h_status[j] = 1.
+constexpr size_t kReplayLdsBytes = 64 * 1024;
+// Not by default: a wave walks ~0.5 us per cell (C3's 215 row replays: 5.2 ms on the GPU, 1.4 ms on 16 host threads,
+// profiles/r06/r06g_*), so the host threads replay every frame's clusters unless a test asks (aos_debug_replay).
+constexpr int kGpuReplayMin = INT_MAX;
+long long replay_bitmap_words(const ClusterRec &r);
+void launch_gpu_replays(const int *d_ids, int n_jobs, int lds_words, const int *off, const int *cells, ClusterRec *rec,
+                        ClusterRec *hrec, int *h_status, int *order, const GridC &g, const double *poly, int np,
+                        float min_length, hipStream_t s);
+// aos_debug_replay (tests): the flagged-cluster count from which a frame replays on the GPU (-1: kGpuReplayMin), and
+// a smaller queue ring for the GPU walk (0: 64), so that wide frontiers reach the host fallback
+extern std::atomic<int> g_debug_replay_min, g_debug_replay_ring;
+extern std::atomic<bool> g_debug_replay_all;   // ... and every cluster replayed, certified or not
 
 // a tree row as the seed kernels take it: start / end (world), k base seeds, first virtual-seed slot
 struct RowDev { double sx, sy, ex, ey; int k; int slot0; };

@@ -703,6 +703,7 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
     out = SeedStageOut();
     S.n_clusters = 0;
     S.h_rec.clear();
+    S.n_replay_from_bits = S.n_replay_gpu = S.n_replay_cells = 0;
     std::vector<RowDev> rows;
     if (in.pre) {   // labelled and measured by the tile ranks (cluster_dist.hip)
         S.h_rec = in.pre->rec;
@@ -746,6 +747,8 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
         S.dedup.sev.sync(s);
         tr.mark("recs");
         std::copy(hr, hr + ncl, S.h_rec.begin());
+        if (g_debug_replay_all.load(std::memory_order_relaxed))
+            for (auto &r : S.h_rec) r.flags |= 2;
         int n_bfs = 0;
         for (const auto &r : S.h_rec) n_bfs += (r.flags & 2) != 0;
         out.n_bfs = n_bfs;
@@ -759,8 +762,40 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
             std::vector<int> ids;
             for (int c = 0; c < ncl; ++c)
                 if (S.h_rec[c].flags & 2) ids.push_back(c);
-            const uint64_t *hbits = in.host_skel_bits ? in.host_skel_bits() : nullptr;
-            S.n_replay_from_bits = 0;
+            const int gpu_min = g_debug_replay_min.load(std::memory_order_relaxed) >= 0
+                                    ? g_debug_replay_min.load(std::memory_order_relaxed) : kGpuReplayMin;
+            if ((int)ids.size() >= gpu_min) {
+                // many replays (C3: every row cluster): all at once on the GPU, one wave each (replay_gpu.hip), from
+                // the cells already on the device; the few it leaves go on below
+                std::vector<int> gids, rest;
+                long long maxw = 0;
+                for (int c : ids) {
+                    const long long w = replay_bitmap_words(S.h_rec[c]);
+                    if (w > 0 && w * 4 <= (long long)kReplayLdsBytes) { gids.push_back(c); maxw = std::max(maxw, w); }
+                    else rest.push_back(c);
+                }
+                if (!gids.empty()) {
+                    const int nj = (int)gids.size();
+                    int *h_ids = static_cast<int *>(S.h_replay.ensure(sizeof(int) * 2 * (size_t)nj));
+                    int *h_st = h_ids + nj;
+                    std::copy(gids.begin(), gids.end(), h_ids);
+                    std::fill(h_st, h_st + nj, 1);
+                    int *d_ids = dev<int>(S.replay_ids, nj);
+                    copy_from_host(d_ids, h_ids, sizeof(int) * nj, s);
+                    launch_gpu_replays(d_ids, nj, (int)maxw, d_off, d_cells, d_rec, hr, h_st, dev<int>(S.replay_order, nf),
+                                       g, d_poly, np, static_cast<float>(in.cluster_min_length), s);
+                    S.dedup.sev.sync(s);
+                    tr.mark("replays_gpu");
+                    for (int j = 0; j < nj; ++j) {
+                        if (h_st[j]) { rest.push_back(gids[j]); continue; }
+                        S.h_rec[gids[j]] = hr[gids[j]];
+                        ++S.n_replay_gpu;
+                    }
+                    std::sort(rest.begin(), rest.end());
+                }
+                ids.swap(rest);
+            }
+            const uint64_t *hbits = !ids.empty() && in.host_skel_bits ? in.host_skel_bits() : nullptr;
             if (hbits) {
                 tr.mark("bits");
                 std::vector<ReplayJob> jobs;
@@ -788,6 +823,7 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
                 replay_clusters(jobs, g, hp.data(), np, static_cast<float>(in.cluster_min_length), S.h_rec.data(),
                                 &S.replay_pool);
                 tr.mark("replays");
+                S.n_replay_cells = (int)ids.size();
             }
         }
     }

@@ -900,7 +900,9 @@ def run(a, E, dist, quiet=False):
             "stages_ms_p50": stage_p50,
             "frame": {"T": T, "rows": len(g.get("row_length", ())), "seeds": len(g.get("voronoi_seeds", ())),
                       "nodes": len(gg["nodes"]) if gg else 0, "edges": len(gg["edges"]) if gg else 0,
-                      "n_binned": g.get("n_binned"), "n_clipped": g.get("n_clipped")},
+                      "n_binned": g.get("n_binned"), "n_clipped": g.get("n_clipped"),
+                      # the last frame's exact BFS replays (clusters without the order-free certificate) by where they ran
+                      "bfs_replays": None if a.tiled else ctx.replay_counts()},
             "gpu_utilisation": gpu_util,
             "roofline": roof,
             "thin_roofline": thin_roof,

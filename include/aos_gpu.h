@@ -445,6 +445,18 @@ void *aos_stream(aos_ctx *ctx);
  * must then fail the frame together); a2a_round_bytes > 0: the distributed cluster stage's personalised
  * exchange moves at most that many bytes per rank pair and round. (-1, 0) turns both off (the default). */
 void aos_debug_faults(int32_t ror_stuck_rank, uint64_t a2a_round_bytes);
+/* Test hook (process-wide): a seed-gen frame replays its clusters without the order-free certificate on the GPU
+ * (one wave per cluster) once it has at least gpu_min_clusters of them, else on host threads. -1: the default
+ * (never: the host walk is faster); 0: always on the GPU (where a cluster's box fits the wave's LDS
+ * bitmap).
+ * ring_cap in [1, 63]: the GPU walk gives a cluster up to the host once more than that many cells are queued
+ * (default 0: 64), so tests reach the fallback. replay_all != 0: every cluster is replayed, also those with the
+ * order-free certificate (whose records the replay must reproduce). (-1, 0, 0): the defaults. */
+void aos_debug_replay(int32_t gpu_min_clusters, int32_t ring_cap, int32_t replay_all);
+/* Diagnostics: the last single-GPU seed-gen frame's exact BFS replays: out[0] = all of them (n_bfs_replayed),
+ * out[1] = on the GPU, out[2] = on host threads over the skeleton bits, out[3] = on host threads from the clusters'
+ * cells. */
+int aos_replay_counts(aos_ctx *ctx, int32_t out[4]);
 
 #ifdef __cplusplus
 }

@@ -186,7 +186,27 @@ def _line_cloud(segments, step=0.05):
     return rec.view(np.uint8).reshape(len(p), 16)
 
 
-def test_argmax_ties_force_exact_bfs_replay():
+@pytest.fixture(params=["host", "gpu"])
+def replay_where(request):
+    """Where the frame's exact BFS replays run: host threads, or the GPU walk (replay_gpu.hip) for every flagged
+    cluster however few (the library's default sends a frame there from 32 flagged clusters on)."""
+    aos_gpu.debug_replay(0 if request.param == "gpu" else 1 << 30)
+    yield request.param
+    aos_gpu.debug_replay()
+
+
+def _check_replay_counts(c, g, where):
+    rc = c.replay_counts()
+    assert rc["all"] == g["n_bfs_replayed"]
+    assert rc["gpu"] + rc["host_bits"] + rc["host_cells"] == rc["all"], rc
+    if where == "gpu":
+        assert rc["gpu"] == rc["all"], rc
+    else:
+        assert rc["gpu"] == 0, rc
+    return rc
+
+
+def test_argmax_ties_force_exact_bfs_replay(replay_where):
     # origin 0 (polygon bbox starts at 2.5) and res 0.25: world coordinates are exact in float, so a
     # straight skeleton bar symmetric about its centre has exactly tied end distances
     cloud = _line_cloud([(10.0, 60.0, 20.0), (15.0, 55.25, 40.0), (5.0, 5.0, 60.0)])
@@ -196,17 +216,49 @@ def test_argmax_ties_force_exact_bfs_replay():
     g = c.seedgen(cloud)
     o = O.seedgen(cloud, poly, O.default_params(grid_resolution=0.25))
     assert g["n_bfs_replayed"] >= 1
+    _check_replay_counts(c, g, replay_where)
     assert_seedgen_parity(g, o)
     assert_gvd_parity(c.gvd_from_seedgen(), O.gvd(o["voronoi_seeds"], o["rows_info"], o))
     c.close()
 
 
-def test_c2_seedgen_parity_with_large_sums():
+def test_c2_seedgen_parity_with_large_sums(replay_where):
     """4096^2: two merged-row clusters have coordinate sums > 2^24 (float sums order-dependent)."""
     cfg = orchard.CONFIGS["C2"]
     c, g, o = run_both(cfg)
     assert g["n_bfs_replayed"] >= 1
+    _check_replay_counts(c, g, replay_where)
     assert_seedgen_parity(g, o)
+    c.close()
+
+
+@pytest.mark.parametrize("ring_cap", [0, 2])
+def test_gpu_replay_of_every_cluster_equals_certified_records(ring_cap):
+    """Every C1 cluster replayed by the GPU walk (aos_debug_replay replay_all), certified or not: the rows, seeds
+    and GvdGraph equal the frame whose certified clusters kept the order-free statistics (k_cluster_stats) and the
+    oracle. ring_cap 2: a walk with more than 2 queued cells gives its cluster up to the host threads (the
+    fallback), so both paths serve one frame."""
+    cfg = orchard.CONFIGS["C1"]
+    cloud, poly = orchard.generate(cfg), orchard.polygon(cfg)
+    c = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res))
+    c.set_polygon(poly)
+    base = c.seedgen(cloud)
+    gg_base = c.gvd_from_seedgen()
+    try:
+        aos_gpu.debug_replay(0, ring_cap, replay_all=True)
+        g = c.seedgen(cloud)
+        rc = c.replay_counts()
+        gg = c.gvd_from_seedgen()
+    finally:
+        aos_gpu.debug_replay()
+    assert rc["all"] == g["n_clusters_all"] == base["n_clusters_all"] > 10, rc
+    if ring_cap == 0:
+        assert rc["gpu"] == rc["all"], rc
+    else:
+        assert 0 < rc["gpu"] < rc["all"], rc
+    assert_seedgen_parity(g, {**base, "cluster_length": np.zeros(base["n_clusters_all"])})
+    for k in ("nodes", "edges", "edge_lengths", "edge_clearances", "node_labels"):
+        assert np.array_equal(gg[k], gg_base[k]), k
     c.close()
 
 

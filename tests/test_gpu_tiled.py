@@ -27,6 +27,7 @@ def _single(cloud, poly, res):
     c = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=res))
     c.set_polygon(poly)
     g = c.seedgen(cloud)
+    g["replay_counts"] = c.replay_counts()
     grids = {w: c.debug_grid(w, (g["height"], g["width"])) for w in GRIDS}
     gg = c.gvd_from_seedgen()
     c.close()
@@ -271,7 +272,24 @@ def test_c3_single_gpu_against_golden(c3_single):
     hashes (tests/golden/c3_sha256.json)."""
     g, _, gg = c3_single
     assert (g["width"], g["height"]) == (8192, 8192)
+    # every row cluster has coordinate sums > 2^24: exact BFS replays, on the host threads over the skeleton bits
+    rc = g["replay_counts"]
+    assert rc["all"] == g["n_bfs_replayed"] >= 200 and rc["host_bits"] == rc["all"], rc
     _assert_golden("c3", g, gg)
+
+
+def test_c3_gpu_replays_equal_host(c3_scene, c3_single):
+    """C3's ~215 row-cluster replays through the GPU walk (replay_gpu.hip, one wave per cluster; aos_debug_replay):
+    the frame equals the host-replayed one."""
+    cfg, cloud, poly = c3_scene
+    aos_gpu.debug_replay(0)
+    try:
+        single = _single(cloud, poly, cfg.res)
+    finally:
+        aos_gpu.debug_replay()
+    rc = single[0]["replay_counts"]
+    assert rc["gpu"] == rc["all"] == c3_single[0]["n_bfs_replayed"], rc
+    _assert_same(c3_single, (single[0], [], single[1], single[2]))
 
 
 def test_group_c3_tiling_for_8_vs_single_and_golden(c3_scene, c3_single):

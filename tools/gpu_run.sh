@@ -14,6 +14,7 @@
 #            box's GPU over gloo)
 #   tiledstream  bench.py --tiled --stream at 1 rank, then the driver's --gpus 2 flow over gloo
 #   rorpmc   tools/rorbench binaries (RORBENCH, built in-tree beforehand): kernel trace + two SQ passes
+#   bfsreal  the host BFS replay A/B on real skeleton clusters (tools/sdcheck/bfs_real.sh; CPU only)
 #   trace    AOS_TRACE=1 host timelines (per stage: ms at each host sync) of a short C2 run
 #   pmcsq    two SQ counter passes over the C2 bench for the kernels matching PMC_KERNELS
 # Usage: TAG=r04a STEPS="pytest smoke bench kt" tools/gpu_run.sh
@@ -138,6 +139,9 @@ for step in $STEPS; do
         --master-addr 127.0.0.1 --master-port 29652 bench.py --gpus 6 --tiled --steps 6 --warmup 2 --no-cpu-baseline \
         > gpurun_out/${TAG}_rccl6.log 2>&1 || { tail -30 gpurun_out/${TAG}_rccl6.log; exit 1; }
       grep '^{' gpurun_out/${TAG}_rccl6.log | cut -c1-400 ;;
+    bfsreal)   # the host BFS replay A/B on real C1 row clusters (tools/sdcheck/bfs_real.sh) on the box's EPYC
+      timeout -k 10 300 bash tools/sdcheck/bfs_real.sh > gpurun_out/${TAG}_bfs_real.txt 2>&1 || { tail -20 gpurun_out/${TAG}_bfs_real.txt; exit 1; }
+      tail -14 gpurun_out/${TAG}_bfs_real.txt ;;
     c3bench)
       timeout -k 10 600 python -u bench.py --config C3 --no-cpu-baseline --no-pipelined-rate --no-device-rate --steps 6 \
         --warmup 2 > gpurun_out/${TAG}_c3_bench.log 2> gpurun_out/${TAG}_c3_bench.err || { tail -20 gpurun_out/${TAG}_c3_bench.err; exit 1; }

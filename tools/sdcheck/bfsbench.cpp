@@ -1,5 +1,5 @@
 // BFS-replay timing (the cluster stage's exact replays, cluster_host.cpp) on synthetic row clusters of ~9 k cells:
-// the product vs the round-4 form (tools/sdcheck/exp/cluster_host_r04.cpp), one cluster at a time on one thread.
+// the product vs the round-6 form (tools/sdcheck/exp/cluster_host_r06.cpp), one cluster at a time on one thread.
 // Env: STRAIGHT=1 rows within two cells of a line (bitmap path), NOROW=1 centres only (no endpoint search).
 #include <chrono>
 #include <cstdio>
@@ -9,7 +9,7 @@
 #include <cstdlib>
 #include "cluster_geom.h"
 #include "cluster_seed.h"
-namespace aos_old { void replay_clusters(const std::vector<aos::ReplayJob> &, const aos::GridC &, const double *, int, float, aos::ClusterRec *, aos::HostPool *); }
+namespace aos_old { void replay_clusters(const std::vector<aos::ReplayJob> &, const aos::GridC &, const double *, int, float, aos::ClusterRec *, aos::HostPool *, std::vector<int> *); }
 int main() {
     aos::GridC g{}; g.ox = -10.5; g.oy = 3.25; g.res = 0.1f; g.W = 8192; g.H = 8192; g.WW = 128;
     double poly[8] = {-1e4, -1e4, 1e4, -1e4, 1e4, 1e4, -1e4, 1e4};
@@ -28,8 +28,12 @@ int main() {
         auto t0 = std::chrono::steady_clock::now();
         for (auto &j : jobs) { std::vector<aos::ReplayJob> one{{0, j.cells, j.n}}; aos::replay_clusters(one, g, poly, 4, 1.f, &a[j.c], nullptr); }
         auto t1 = std::chrono::steady_clock::now();
-        for (auto &j : jobs) { std::vector<aos::ReplayJob> one{{0, j.cells, j.n}}; aos_old::replay_clusters(one, g, poly, 4, 1.f, &b[j.c], nullptr); }
+        for (auto &j : jobs) { std::vector<aos::ReplayJob> one{{0, j.cells, j.n}}; aos_old::replay_clusters(one, g, poly, 4, 1.f, &b[j.c], nullptr, nullptr); }
         auto t2 = std::chrono::steady_clock::now();
+        for (int c = 0; c < 64; ++c)
+            if (a[c].cx != b[c].cx || a[c].cy != b[c].cy || a[c].start.x != b[c].start.x || a[c].end.y != b[c].end.y || a[c].flags != b[c].flags) {
+                printf("MISMATCH cluster %d\n", c); return 1;
+            }
         printf("new %.1f us/cluster  old %.1f us/cluster (n ~ %zu)\n", std::chrono::duration<double, std::micro>(t1 - t0).count() / 64,
                std::chrono::duration<double, std::micro>(t2 - t1).count() / 64, cl[0].size());
     }

@@ -1,3 +1,4 @@
+// Round-6 form of active-orchard-slam_amd/csrc/cluster_host.cpp (namespace aos_old), kept for tools/sdcheck/bfsbench.cpp A/B only.
 // Host-side parts of the cluster stage (a8-a10), kept in a plain C++ file so the sanitizer build
 // (tests/sanitize: ASan + UBSan, no GPU) runs exactly the code the product links:
 //   * host_bfs_replay / replay_clusters: clusterOccupiedCells' FIFO BFS (seed_gen:1007-1049) and its
@@ -22,7 +23,7 @@
 #include "cluster_geom.h"
 #include "cluster_seed.h"
 
-namespace aos {
+namespace aos_old { using namespace aos;
 
 constexpr int kReplayThreads = 16;   // host threads for the exact BFS replays of one frame (the box share: 16 cores)
 
@@ -54,104 +55,36 @@ struct XY { int x, y; };
 // set bits; the queue holds (x, y), so no division at all (C3's ~450 replays: profiles/r05y_*).
 static const int kDxs[8] = {-1, -1, -1, 0, 0, 1, 1, 1}, kDys[8] = {-1, 0, 1, -1, 1, -1, 0, 1};
 
-// One entry per 3 x 3 window of the bitmap (bits 0-2: row y - 1, 3-5: row y, 6-8: row y + 1; the first bit of each
-// row is column x - 1): the set neighbours' direction indices into kDxs / kDys in the reference's order, 3 bits each
-// (bits 0-23), and their number (bits 24-27). A step then pushes without a branch (round 6; the round-5 walk looped
-// over the set bits, one mispredicted exit per step).
-struct WinTab {
-    uint32_t e[512];
-    WinTab() {
-        for (int w = 0; w < 512; ++w) {
-            uint32_t code = 0, k = 0;
-            for (int i = 0; i < 8; ++i)
-                if (w >> ((kDys[i] + 1) * 3 + kDxs[i] + 1) & 1) code |= (uint32_t)i << (3 * k++);
-            e[w] = code | k << 24;
-        }
-    }
-};
-static const WinTab kWin;
-// the direction's (dx, dy) as the packed XY difference (x: low 32 bits, y: high; x + dx >= 0 for a queued cell)
-static const int64_t kDxy[8] = {
-    -(int64_t(1) << 32) - 1, -1, (int64_t(1) << 32) - 1, -(int64_t(1) << 32), int64_t(1) << 32,
-    -(int64_t(1) << 32) + 1, 1, (int64_t(1) << 32) + 1};
-
 // The FIFO walk over a bordered box bitmap B (RW words per row; a set bit = in the cluster, not yet queued; bit c of
 // row r = cell (x0 + c - 1, y0 + r - 1)) from (sx, sy), whose bit is already clear. Q receives the cells in pop
-// order and has room for cap + 8 entries; at most cap cells (returns -1 past it), else their number. The centre sums
-// ride along in pop order (the float additions of seed_gen:1030-1046 in the same order).
-// A step reads the popped cell's window (three unaligned 3-bit fields), looks its pushes up in kWin, writes all 8
-// queue slots past the tail (the ones past the count are overwritten later) and clears the whole window: its set
-// bits are exactly the cells it queues, the rest are clear already. Per step that is one chain of a queue load, the
-// window loads, one table load and the queue stores, no data-dependent branch.
-// Runs: a row cluster's skeleton is a horizontal line walked from its left end with one cell queued (C1: 37 k of
-// 41 k pops). When a step leaves exactly its right neighbour e queued, e's own column and the one left of it hold
-// nothing unqueued above or below (they were in the step's window), so from e on each pop queues exactly the next
-// cell to its right for as long as that cell is set and the cells above and below it are not: the run's length is
-// the trailing ones of (row y & ~(row y - 1 | row y + 1)) from e + 1, 64 columns per word pair. The run's pops are
-// then the queue writes of e + 1 ... e + k, their bits cleared by word, and the float sums added one cell at a time in
-// the same order (only the additions stay serial: ~4 cycles a cell instead of the step's chain).
+// order; at most cap of them (returns -1 past it), else their number. The centre sums ride along in pop order (the
+// float additions of seed_gen:1030-1046 in the same order).
 static long long bfs_walk(uint64_t *B, long long RW, int x0, int y0, int sx, int sy, XY *Q, long long cap, float &sum_x,
                           float &sum_y) {
-    static_assert(sizeof(XY) == 8, "XY packs into 64 bits");
+    auto win3 = [&](long long r, long long c) {   // bits c, c + 1, c + 2 of row r (c >= 0: the border)
+        const uint64_t *w = B + r * RW + (c >> 6);
+        const unsigned __int128 v = ((unsigned __int128)w[1] << 64) | w[0];
+        return (unsigned)(v >> (c & 63)) & 7u;
+    };
     Q[0] = XY{sx, sy};
     long long head = 0, tail = 1;
     float ax = 0.0f, ay = 0.0f;
     while (head < tail) {
         const XY c = Q[head++];
         ax += (float)c.x; ay += (float)c.y;
-        // bitmap columns c0 .. c0 + 2 = cells x - 1 .. x + 1 of rows y - 1 .. y + 1
-        const long long c0 = (long long)c.x - x0;
-        uint64_t *w = B + ((long long)c.y - y0) * RW + (c0 >> 6);
-        const int sh = (int)(c0 & 63);
-        auto win3 = [&](const uint64_t *p) { return (unsigned)((((unsigned __int128)p[1] << 64) | p[0]) >> sh) & 7u; };
-        const uint32_t e = kWin.e[win3(w) | win3(w + RW) << 3 | win3(w + 2 * RW) << 6];
-        int64_t c64;
-        std::memcpy(&c64, &c, 8);
-        for (int i = 0; i < 8; ++i) {
-            const int64_t v = c64 + kDxy[(e >> (3 * i)) & 7u];
-            std::memcpy(&Q[tail + i], &v, 8);
-        }
-        tail += e >> 24;
-        const uint64_t lo = ~(7ull << sh), hi = ~(3ull >> (63 - sh));
-        w[0] &= lo; w[1] &= hi; w[RW] &= lo; w[RW + 1] &= hi; w[2 * RW] &= lo; w[2 * RW + 1] &= hi;
-        if (tail > cap) return -1;
-        if (e == (6u | 1u << 24) && tail - head == 1) {   // one push, (dx, dy) = (1, 0), and nothing else queued
-            // bitmap columns s, s + 1, ... of the popped cell's row = cells x + 2, x + 3, ...: e = (x + 1, y)
-            const long long s0 = c0 + 3;
-            const uint64_t *rr = w + RW - (c0 >> 6);   // the row's first word
-            long long k = 0;
-            for (;;) {
-                const long long s = s0 + k, wi = s >> 6;
-                const int o = (int)(s & 63);
-                auto bits64 = [&](const uint64_t *row) {
-                    return (uint64_t)((((unsigned __int128)row[wi + 1] << 64) | row[wi]) >> o);
-                };
-                const uint64_t ok = bits64(rr) & ~(bits64(rr - RW) | bits64(rr + RW));
-                const int t = ok == ~0ull ? 64 : __builtin_ctzll(~ok);
-                k += t;
-                if (t < 64 || s + 64 + 64 > RW * 64) break;   // (the next word pair must still lie in the row)
-            }
-            if (k > 0) {
-                if (tail + k > cap) return -1;
-                const int ex = c.x + 1, y = c.y;
-                const float fy = (float)y;
-                for (long long j = 0; j < k; ++j) {
-                    Q[head + 1 + j] = XY{ex + 1 + (int)j, y};
-                    ax += (float)(ex + (int)j); ay += fy;
-                }
-                // clear row y's columns s0 .. s0 + k - 1 (the cells queued by the run)
-                uint64_t *rw = w + RW - (c0 >> 6);
-                for (long long b = s0, end = s0 + k; b < end;) {
-                    const long long wi = b >> 6;
-                    const int o = (int)(b & 63);
-                    const long long nb = std::min<long long>(end, (wi + 1) << 6);
-                    const int len = (int)(nb - b);
-                    rw[wi] &= ~((len == 64 ? ~0ull : ((1ull << len) - 1)) << o);
-                    b = nb;
-                }
-                head += k;
-                tail = head + 1;
-            }
+        const long long r = c.y - y0 + 1, cc = c.x - x0 + 1;
+        const unsigned rm = win3(r - 1, cc - 1), r0 = win3(r, cc - 1), rp = win3(r + 1, cc - 1);
+        // the neighbour order (dx, dy) of kDxs / kDys: column x - 1 (rows y - 1, y, y + 1), column x (y - 1, y + 1),
+        // column x + 1 (y - 1, y, y + 1)
+        unsigned m = (rm & 1u) | (r0 & 1u) << 1 | (rp & 1u) << 2 | (rm & 2u) << 2 | (rp & 2u) << 3 | (rm & 4u) << 3 |
+                     (r0 & 4u) << 4 | (rp & 4u) << 5;
+        while (m) {
+            const int i = __builtin_ctz(m);
+            m &= m - 1;
+            const long long nr = r + kDys[i], nc = cc + kDxs[i];
+            B[nr * RW + (nc >> 6)] &= ~(1ull << (nc & 63));
+            if (tail >= cap) return -1;
+            Q[tail++] = XY{c.x + kDxs[i], c.y + kDys[i]};
         }
     }
     sum_x = ax; sum_y = ay;
@@ -162,7 +95,7 @@ static void bfs_order(const int *cells, int n, const GridC &g, std::vector<XY> &
                       std::vector<uint64_t> &bm, float &sum_x, float &sum_y) {
     static const int *const dxs = kDxs, *const dys = kDys;
     const DivW dw(g.W);
-    q.resize((size_t)n + 8);   // (+ 8: bfs_walk writes 8 slots past the tail)
+    q.resize(n);
     // the cells' (x, y) go to the queue's storage first: the bitmap pass below reads them back instead of dividing again
     XY *const Q = q.data();
     int start = cells[0], x0 = INT_MAX, x1 = INT_MIN, y0 = INT_MAX, y1 = INT_MIN;
@@ -277,7 +210,7 @@ static bool bfs_order_bits(const uint64_t *bits, const GridC &g, const ClusterRe
         if (!(B[rr * RW + (c >> 6)] >> (c & 63) & 1)) return false;   // (not a skeleton cell: records and bits disagree)
         B[rr * RW + (c >> 6)] &= ~(1ull << (c & 63));
     }
-    q.resize((size_t)n + 8);
+    q.resize((size_t)n);
     return bfs_walk(B, RW, x0, y0, sx, sy, q.data(), n, sum_x, sum_y) == n;
 }
 
@@ -298,106 +231,53 @@ static bool host_bfs_replay(const int *cells, const uint64_t *bits, int n, const
         row = d_pip(cwx, cwy, poly, np);
     }
     if (row) {
-        // The cells' world coordinates (cell_w) and squared distances to the centre, computed once into arrays by plain
-        // loops the compiler vectorises (round 6: the three scalar passes were ~60 % of a row replay once the walk
-        // took runs). Each cell goes through the same IEEE operations as in the scalar form, so every value is the
-        // same; maxima are exact in any order, and the first index holding one is found by a scan.
-        static thread_local std::vector<double> wbuf;
-        wbuf.resize(3 * (size_t)n);
-        double *const WX = wbuf.data(), *const WY = WX + n, *const D2 = WY + n;
-        const double ox = g.ox, oy = g.oy, cx = r.center.x, cy = r.center.y;
-        const float res = g.res;
-        const XY *const Q = q.data();
-        for (int j = 0; j < n; ++j) {
-            const double wx = (double)cell_world(ox, Q[j].x, res), wy = (double)cell_world(oy, Q[j].y, res);
-            const double dx = wx - cx, dy = wy - cy;
-            WX[j] = wx; WY[j] = wy; D2[j] = dx * dx + dy * dy;
-        }
-        double m4[4] = {0.0, 0.0, 0.0, 0.0};
-        int k = 0;
-        for (; k + 4 <= n; k += 4)
-            for (int l = 0; l < 4; ++l) m4[l] = D2[k + l] > m4[l] ? D2[k + l] : m4[l];
-        for (; k < n; ++k) m4[0] = D2[k] > m4[0] ? D2[k] : m4[0];
-        // the first index k (!= skip) with D2[k] == v and pred(k), or -1 (blocks of 8 tested together)
-        auto first_eq = [&](double v, int skip, auto pred) {
-            int k0 = 0;
-            for (; k0 + 8 <= n; k0 += 8) {
-                int hit = 0;
-                for (int l = 0; l < 8; ++l) hit |= D2[k0 + l] == v;
-                if (!hit) continue;
-                for (int l = 0; l < 8; ++l)
-                    if (D2[k0 + l] == v && k0 + l != skip && pred(k0 + l)) return k0 + l;
-            }
-            for (; k0 < n; ++k0)
-                if (D2[k0] == v && k0 != skip && pred(k0)) return k0;
-            return -1;
+        auto cw = [&](int k) {   // cell_w of the k-th BFS cell
+            return make_double2((double)cell_world(g.ox, q[k].x, g.res), (double)cell_world(g.oy, q[k].y, g.res));
         };
         // the first strict maximum of d2, then its direction (the reference normalises at every new maximum; only the
         // last one's values survive, and they are the same operations on the same operands)
-        const double mx = std::max(std::max(m4[0], m4[1]), std::max(m4[2], m4[3]));
-        int fi = 0;
-        double fx = 0, fy = 0;
+        double mx = 0.0; int fi = 0; double fx = 0, fy = 0;
+        for (int k = 0; k < n; ++k) {
+            double2 w = cw(k);
+            double dx = w.x - r.center.x, dy = w.y - r.center.y, d2 = dx * dx + dy * dy;
+            if (d2 > mx) { mx = d2; fi = k; }
+        }
         if (mx > 0.0) {
-            fi = first_eq(mx, -1, [](int) { return true; });
-            const double dx = WX[fi] - cx, dy = WY[fi] - cy, d2 = dx * dx + dy * dy;
-            const double s = std::sqrt(d2);
-            fx = dx / s; fy = dy / s;
+            double2 w = cw(fi);
+            double dx = w.x - r.center.x, dy = w.y - r.center.y, d2 = dx * dx + dy * dy;
+            double s = std::sqrt(d2); fx = dx / s; fy = dy / s;
         }
-        // the sign of the normalised dot product nx fx + ny fy is that of dx fx + dy fy whenever the latter is not
-        // within rounding of zero (both round within a few ulps of |dx fx| + |dy fy|, over s > 0); near zero the
-        // reference's own expression decides
-        auto opposite_exact = [&](int j) {
-            const double dx = WX[j] - cx, dy = WY[j] - cy, d2 = D2[j];
+        double mo = 0.0; int si = 0;
+        for (int k = 0; k < n; ++k) {
+            if (k == fi) continue;
+            double2 w = cw(k);
+            double dx = w.x - r.center.x, dy = w.y - r.center.y, d2 = dx * dx + dy * dy;
+            if (!(d2 > mo)) continue;   // (the same test, its cheap half first: the normalisation only for a new max)
+            // the sign of the normalised dot product nx fx + ny fy is that of dx fx + dy fy whenever the latter is not
+            // within rounding of zero (both round within a few ulps of |dx fx| + |dy fy|, over s > 0); near zero the
+            // reference's own expression decides
             const double pa = dx * fx, pb = dy * fy, dd = pa + pb;
-            if (std::fabs(dd) > 1e-12 * (std::fabs(pa) + std::fabs(pb))) return dd < 0.0;
-            double nx = dx, ny = dy;
-            if (d2 > 0.0) { const double s = std::sqrt(d2); nx = dx / s; ny = dy / s; }
-            return nx * fx + ny * fy < 0.0;
-        };
-        // the largest d2 among the cells (not fi) on the far side of the first direction: vectorised over the cells
-        // whose side is clear; a cell within rounding of the perpendicular (rare) sends the cluster through the exact
-        // scalar loop
-        double o4[4] = {0.0, 0.0, 0.0, 0.0};
-        int unsure = 0;
-        k = 0;
-        for (; k + 4 <= n; k += 4)
-            for (int l = 0; l < 4; ++l) {
-                const int j = k + l;
-                const double dx = WX[j] - cx, dy = WY[j] - cy, d2 = D2[j];
-                const double pa = dx * fx, pb = dy * fy, dd = pa + pb;
-                const bool clear = std::fabs(dd) > 1e-12 * (std::fabs(pa) + std::fabs(pb));
-                const bool take = clear && dd < 0.0 && j != fi;
-                unsure |= !clear && j != fi && d2 > 0.0;
-                o4[l] = take && d2 > o4[l] ? d2 : o4[l];
+            bool opposite;
+            if (std::fabs(dd) > 1e-12 * (std::fabs(pa) + std::fabs(pb))) {
+                opposite = dd < 0.0;
+            } else {
+                double nx = dx, ny = dy;
+                if (d2 > 0.0) { double s = std::sqrt(d2); nx = dx / s; ny = dy / s; }
+                opposite = nx * fx + ny * fy < 0.0;
             }
-        for (; k < n; ++k) {
-            const double dx = WX[k] - cx, dy = WY[k] - cy, d2 = D2[k];
-            const double pa = dx * fx, pb = dy * fy, dd = pa + pb;
-            const bool clear = std::fabs(dd) > 1e-12 * (std::fabs(pa) + std::fabs(pb));
-            unsure |= !clear && k != fi && d2 > 0.0;
-            o4[0] = clear && dd < 0.0 && k != fi && d2 > o4[0] ? d2 : o4[0];
+            if (opposite) { mo = d2; si = k; }
         }
-        double mo = 0.0;
-        int si = 0;
-        if (!unsure) {
-            mo = std::max(std::max(o4[0], o4[1]), std::max(o4[2], o4[3]));
-            if (mo > 0.0) si = first_eq(mo, fi, opposite_exact);
-        } else {
-            for (int j = 0; j < n; ++j) {
-                if (j == fi || !(D2[j] > mo)) continue;
-                if (opposite_exact(j)) { mo = D2[j]; si = j; }
+        if (mo == 0.0) {
+            double2 wf = cw(fi);
+            for (int k = 0; k < n; ++k) {
+                if (k == fi) continue;
+                double2 w = cw(k);
+                double dx = w.x - wf.x, dy = w.y - wf.y, d2 = dx * dx + dy * dy;
+                if (d2 > mo) { mo = d2; si = k; }
             }
         }
-        if (mo == 0.0) {   // farthest from the first endpoint
-            const double fwx = WX[fi], fwy = WY[fi];
-            for (int j = 0; j < n; ++j) {
-                if (j == fi) continue;
-                const double dx = WX[j] - fwx, dy = WY[j] - fwy, d2 = dx * dx + dy * dy;
-                if (d2 > mo) { mo = d2; si = j; }
-            }
-        }
-        r.start = make_double2(WX[fi], WY[fi]);
-        r.end = make_double2(WX[si], WY[si]);
+        r.start = cw(fi);
+        r.end = cw(si);
     }
     r.flags = (row ? 1 : 0) | 4;  // 4: replayed
     return true;
