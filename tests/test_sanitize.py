@@ -178,3 +178,184 @@ def test_cluster_replays_and_rows_under_asan_ubsan(built, tmp_path, visited):
     assert np.array_equal(rows["c"][:, 2:4], o["row_start"])
     assert np.array_equal(rows["c"][:, 4:6], o["row_end"])
     assert np.array_equal(rows_info, o["rows_info"]) and np.array_equal(cluster_info, o["cluster_info"])
+
+
+def _synthetic_structures(W, H, rng):
+    """Thin 8-connected structures, one per band of rows, for the replay walk's edge cases: horizontal lines of
+    every length around the 64-bit word boundaries at several x offsets (the run path), lines with diagonal steps,
+    two-cell-thick stretches, branches (combs, plus signs: wide frontiers), a peak whose first raster cell lies in
+    the middle (the walk goes both ways), vertical lines, random blobs, long wiggly lines whose coordinate sums pass
+    2^24 (order-dependent float sums), and lines on the grid's borders. Returns the list of cell-id arrays."""
+    out, y = [], 0
+    def add(cells, height):
+        nonlocal y
+        out.append(np.array(sorted({cy * W + cx for cx, cy in cells}), np.int64))
+        y += height + 3
+    add([(x, 0) for x in range(0, 70)], 1)                       # top border, from x = 0
+    for L in (1, 2, 3, 62, 63, 64, 65, 66, 127, 128, 129, 130, 191, 192, 193, 257):
+        for x0 in (1, 61, 62, 63, 64, 65, 127):
+            add([(x0 + i, y) for i in range(L)], 1)
+    for k in range(12):                                          # lines with diagonal steps
+        x0, L, cells, yy = int(rng.integers(0, 200)), int(rng.integers(50, 400)), [], y + 4
+        for i in range(L):
+            if rng.random() < 0.06:
+                yy += int(rng.choice([-1, 1]))
+                yy = min(max(yy, y), y + 8)
+            cells.append((x0 + i, yy))
+        add(cells, 9)
+    for k in range(8):                                           # two-cell-thick stretches
+        x0, L = int(rng.integers(0, 100)), int(rng.integers(80, 300))
+        cells = [(x0 + i, y + 1) for i in range(L)]
+        cells += [(x0 + i, y + (0 if k % 2 else 2)) for i in range(L) if rng.random() < 0.3]
+        add(cells, 3)
+    for k in range(4):                                           # combs: teeth below a bar
+        x0, L, gap, tooth = 3 + k, 200, 2 + k, 5 + 3 * k
+        cells = [(x0 + i, y) for i in range(L)]
+        cells += [(x0 + i, y + j) for i in range(0, L, gap) for j in range(1, tooth)]
+        add(cells, tooth)
+    add([(50 + i, y + 10) for i in range(-10, 11)] + [(50, y + 10 + j) for j in range(-10, 11)], 21)   # plus
+    add([(100 + i, y + 20 - min(i, 40 - i) // 2) for i in range(41)], 21)        # a peak: first cell mid-line
+    add([(300 + i, y + 20 - min(i, 80 - i) // 4) for i in range(81)], 21)
+    for x0 in (0, 63, 64, 700):                                  # vertical lines
+        add([(x0, y + j) for j in range(40)], 40)
+    for k in range(6):                                           # random blobs (growth from a seed)
+        cells, frontier = {(20 + 10 * k, y + 6)}, [(20 + 10 * k, y + 6)]
+        while len(cells) < 40 + 20 * k:
+            cx, cy = frontier[int(rng.integers(0, len(frontier)))]
+            nx, ny = cx + int(rng.integers(-1, 2)), cy + int(rng.integers(-1, 2))
+            if y <= ny <= y + 12 and 0 <= nx < W and (nx, ny) not in cells:
+                cells.add((nx, ny)); frontier.append((nx, ny))
+        add(cells, 12)
+    for k in range(3):                                           # long lines: float sums past 2^24
+        x0, L, cells, yy = 1500 + 100 * k, 6000, [], y + 2
+        for i in range(L):
+            if k and rng.random() < 0.01:
+                yy = min(max(yy + int(rng.choice([-1, 1])), y), y + 4)
+            cells.append((x0 + i, yy))
+        add(cells, 5)
+    add([(W - 70 + i, y) for i in range(70)], 1)                  # ends on the right border
+    add([(W - 1, y + j) for j in range(30)], 30)                  # right-border column
+    assert y < H, y
+    return out
+
+
+def _reference_replay(cells, W, ox, oy, res, min_len, length):
+    """clusterOccupiedCells' FIFO BFS (seed_gen:1007-1049) with the float centre sums and the first-strict-maximum
+    endpoints (:1354-1395) as host_bfs_replay computes them, in plain Python (float32 via numpy, doubles as Python
+    floats): the walk's checker."""
+    import collections
+    import math
+    f32 = np.float32
+    res32 = f32(res)
+    cs = set(int(c) for c in cells)
+    start = min(cs)
+    seen, q, order = {start}, collections.deque([start]), []
+    dxs, dys = (-1, -1, -1, 0, 0, 1, 1, 1), (-1, 0, 1, -1, 1, -1, 0, 1)
+    while q:
+        c = q.popleft()
+        order.append(c)
+        y, x = divmod(c, W)
+        for dx, dy in zip(dxs, dys):
+            nb = (y + dy) * W + (x + dx)
+            if 0 <= x + dx < W and nb in cs and nb not in seen:
+                seen.add(nb); q.append(nb)
+    assert len(order) == len(cs)
+    sx, sy = f32(0), f32(0)
+    for c in order:
+        y, x = divmod(c, W)
+        sx = f32(sx + f32(x)); sy = f32(sy + f32(y))
+    n = len(order)
+    cx, cy = f32(sx / f32(n)), f32(sy / f32(n))
+    def cwf(o, i):
+        return float(f32(o + float(f32(f32(i) * res32))))
+    def cw(k):
+        y, x = divmod(order[k], W)
+        return cwf(ox, x), cwf(oy, y)
+    row = f32(length) >= f32(min_len)
+    center = start_p = end_p = None
+    if row:
+        center = (float(f32(ox + float(f32(cx * res32)))), float(f32(oy + float(f32(cy * res32)))))
+        mx, fi, fx, fy = 0.0, 0, 0.0, 0.0
+        for k in range(n):
+            wx, wy = cw(k)
+            d2 = (wx - center[0]) * (wx - center[0]) + (wy - center[1]) * (wy - center[1])
+            if d2 > mx:
+                mx, fi = d2, k
+        if mx > 0.0:
+            wx, wy = cw(fi)
+            dx, dy = wx - center[0], wy - center[1]
+            s = math.sqrt(dx * dx + dy * dy)
+            fx, fy = dx / s, dy / s
+        mo, si = 0.0, 0
+        for k in range(n):
+            if k == fi:
+                continue
+            wx, wy = cw(k)
+            dx, dy = wx - center[0], wy - center[1]
+            d2 = dx * dx + dy * dy
+            if not d2 > mo:
+                continue
+            pa, pb = dx * fx, dy * fy
+            dd = pa + pb
+            if abs(dd) > 1e-12 * (abs(pa) + abs(pb)):
+                opp = dd < 0.0
+            else:
+                nx, ny = dx, dy
+                if d2 > 0.0:
+                    s = math.sqrt(d2); nx, ny = dx / s, dy / s
+                opp = nx * fx + ny * fy < 0.0
+            if opp:
+                mo, si = d2, k
+        if mo == 0.0:
+            fwx, fwy = cw(fi)
+            for k in range(n):
+                if k == fi:
+                    continue
+                wx, wy = cw(k)
+                d2 = (wx - fwx) * (wx - fwx) + (wy - fwy) * (wy - fwy)
+                if d2 > mo:
+                    mo, si = d2, k
+        start_p, end_p = cw(fi), cw(si)
+    return row, cx, cy, center, start_p, end_p
+
+
+@pytest.mark.parametrize("mode", ["R", "B"])
+def test_replay_walk_synthetic_structures_under_asan_ubsan(built, tmp_path, mode):
+    """The exact BFS replay's walk (cluster_host.cpp: the run path along horizontal lines, the table-driven general
+    step, the vectorised endpoint search) on synthetic structures built for its edge cases (_synthetic_structures),
+    from the clusters' cells (R) and over a skeleton bit grid (B), under ASan / UBSan, against a plain Python FIFO
+    BFS with the reference's neighbour order, float32 sums and endpoint rules: every centre and endpoint bit-exact."""
+    from scipy import ndimage
+    W, H = 8192, 1800
+    rng = np.random.default_rng(11)
+    structs = _synthetic_structures(W, H, rng)
+    grid = np.zeros((H, W), bool)
+    for s in structs:
+        grid.reshape(-1)[s] = True
+    _, ncomp = ndimage.label(grid, structure=np.ones((3, 3)))
+    assert ncomp == len(structs)   # (each structure one 8-connected cluster, none touching another)
+    ox, oy, res, min_len = -10.5, 3.25, 0.1, 1.0
+    lengths = [100.0 if i % 5 else 0.5 for i in range(len(structs))]   # every fifth one below the row length
+    poly = np.array([[-1e4, -1e4], [1e4, -1e4], [1e4, 1e4], [-1e4, 1e4]], np.float64)
+    blob = (np.array([ox, oy], np.float64).tobytes() + np.float32(res).tobytes()
+            + np.array([W, H, len(poly)], np.int32).tobytes() + poly.reshape(-1).tobytes()
+            + np.float32(min_len).tobytes() + np.int32(len(structs)).tobytes())
+    for s, L in zip(structs, lengths):
+        lin = s.astype(np.int32).copy()
+        rng.shuffle(lin)
+        blob += np.int32(len(lin)).tobytes() + np.float32(L).tobytes() + lin.tobytes()
+    if mode == "B":
+        blob += np.int32(0).tobytes()
+    raw = _cluster_run(built, mode, blob, tmp_path, env={"AOS_REPLAY_HASH": "0"})
+    if mode == "B":
+        assert int(np.frombuffer(raw[-4:], np.int32)[0]) == 0
+        raw = raw[:-4]
+    rec = np.frombuffer(raw[:len(structs) * 60], dtype=np.dtype([("flags", "<i4"), ("cx", "<f4"), ("cy", "<f4"),
+                                                                   ("c", "<f8", 6)]))
+    for i, (s, L) in enumerate(zip(structs, lengths)):
+        row, cx, cy, center, sp, ep = _reference_replay(s, W, ox, oy, res, min_len, L)
+        r = rec[i]
+        assert (r["cx"], r["cy"]) == (cx, cy), i
+        assert bool(r["flags"] & 1) == row and (r["flags"] & 4), i
+        if row:
+            assert tuple(r["c"][0:2]) == center and tuple(r["c"][2:4]) == sp and tuple(r["c"][4:6]) == ep, i
