@@ -145,16 +145,18 @@ void replay_clusters(const std::vector<ReplayJob> &jobs, const GridC &g, const d
                      ClusterRec *rec, HostPool *pool = nullptr, std::vector<int> *failed = nullptr);
 // The same replays on the GPU (replay_gpu.hip), one wave per cluster, for frames with many of them: d_ids (device)
 // lists n_jobs clusters whose bordered box bitmap takes at most lds_words 32-bit words (replay_bitmap_words; -1: not
-// on the GPU). A replayed cluster's record is updated in rec and hrec (pinned) and h_status[j] = 0; a cluster the
-// GPU leaves (frontier wider than 64 cells, inconsistent cells) keeps its records and h_status[j] = 1.
+// on the GPU), walked over the foreground bits fg (g.WW words per row); order: nf ints of scratch (cluster c at
+// off[c]). A replayed cluster's record is updated in rec and hrec (pinned) and h_status[j] = 0; a cluster the GPU
+// leaves (frontier wider than 64 cells, records that disagree with the grid) keeps its records and h_status[j] = 1.
 constexpr size_t kReplayLdsBytes = 64 * 1024;
 // Not by default: a wave walks ~0.5 us per cell (C3's 215 row replays: 5.2 ms on the GPU, 1.4 ms on 16 host threads,
 // profiles/r06/r06g_*), so the host threads replay every frame's clusters unless a test asks (aos_debug_replay).
 constexpr int kGpuReplayMin = INT_MAX;
 long long replay_bitmap_words(const ClusterRec &r);
-void launch_gpu_replays(const int *d_ids, int n_jobs, int lds_words, const int *off, const int *cells, ClusterRec *rec,
+void launch_gpu_replays(const int *d_ids, int n_jobs, int lds_words, const int *off, const uint64_t *fg, ClusterRec *rec,
                         ClusterRec *hrec, int *h_status, int *order, const GridC &g, const double *poly, int np,
-                        float min_length, hipStream_t s);
+                        float min_length, hipStream_t s, long long *h_prof = nullptr);
+void print_replay_prof(const long long *prof, int n_jobs);   // (AOS_REPLAY_PROF=1: h_prof's phase counters)
 // aos_debug_replay (tests): the flagged-cluster count from which a frame replays on the GPU (-1: kGpuReplayMin), and
 // a smaller queue ring for the GPU walk (0: 64), so that wide frontiers reach the host fallback
 extern std::atomic<int> g_debug_replay_min, g_debug_replay_ring;

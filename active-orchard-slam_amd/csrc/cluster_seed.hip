@@ -776,16 +776,19 @@ void run_cluster_seed_stage(ClusterSeedState &S, const SeedStageIn &in, SeedStag
                 }
                 if (!gids.empty()) {
                     const int nj = (int)gids.size();
-                    int *h_ids = static_cast<int *>(S.h_replay.ensure(sizeof(int) * 2 * (size_t)nj));
+                    static const bool prof = [] { const char *e = getenv("AOS_REPLAY_PROF"); return e && atoi(e) != 0; }();
+                    int *h_ids = static_cast<int *>(S.h_replay.ensure(sizeof(int) * 2 * (size_t)nj + (prof ? 64 * (size_t)nj + 64 : 0)));
                     int *h_st = h_ids + nj;
+                    long long *h_prof = prof ? reinterpret_cast<long long *>(h_ids + ((2 * (size_t)nj + 1) & ~(size_t)1)) : nullptr;
                     std::copy(gids.begin(), gids.end(), h_ids);
                     std::fill(h_st, h_st + nj, 1);
                     int *d_ids = dev<int>(S.replay_ids, nj);
                     copy_from_host(d_ids, h_ids, sizeof(int) * nj, s);
-                    launch_gpu_replays(d_ids, nj, (int)maxw, d_off, d_cells, d_rec, hr, h_st, dev<int>(S.replay_order, nf),
-                                       g, d_poly, np, static_cast<float>(in.cluster_min_length), s);
+                    launch_gpu_replays(d_ids, nj, (int)maxw, d_off, d_fg, d_rec, hr, h_st, dev<int>(S.replay_order, nf),
+                                       g, d_poly, np, static_cast<float>(in.cluster_min_length), s, h_prof);
                     S.dedup.sev.sync(s);
                     tr.mark("replays_gpu");
+                    if (h_prof) print_replay_prof(h_prof, nj);
                     for (int j = 0; j < nj; ++j) {
                         if (h_st[j]) { rest.push_back(gids[j]); continue; }
                         S.h_rec[gids[j]] = hr[gids[j]];

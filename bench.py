@@ -465,6 +465,8 @@ def run(a, E, dist, quiet=False):
     import orchard
     if os.environ.get("AOS_NUMPY_HUGEPAGE") != "1":
         aos_gpu.disable_numpy_hugepage()   # (the markers copies: DESIGN §7b; AOS_NUMPY_HUGEPAGE=1 keeps numpy's default)
+    if os.environ.get("AOS_BENCH_REPLAY_GPU"):   # A/B runs: the exact BFS replays from this many clusters on the GPU
+        aos_gpu.debug_replay(int(os.environ["AOS_BENCH_REPLAY_GPU"]))
     world, rank, gpu, dev, red_dev, backend = E["world"], E["rank"], E["gpu"], E["dev"], E["red_dev"], E["backend"]
 
     cfg = orchard.CONFIGS[a.config]
