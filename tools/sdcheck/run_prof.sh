@@ -17,6 +17,6 @@ names="base prof"
 for v in ${SD_VARIANTS:-}; do n=$(basename $(dirname $v))_$(basename $v .cpp); n=${n#exp_}; build $n $v; build ${n}_prof $v -DAOS_SD_PROF; names="$names $n ${n}_prof"; done
 for r in $(seq 1 ${ROUNDS:-3}); do
   for n in $names; do
-    echo "$n: $(timeout -k 5 120 taskset -c 2 $B/$n $D/c2_seeds.bin 5)"
+    echo "$n: $(timeout -k 5 300 taskset -c 2 $B/$n ${SD_SEEDS:-$D/c2_seeds.bin} ${SD_REPS:-5})"
   done
 done
