@@ -176,6 +176,7 @@ void launch_rt_scatter(const RorLaunch &L, int *H, const int *tstart, int G, flo
 // kept_tile (nullable): per-tile kept counts; dirty (nullable): a tile is counted iff dirty[t+1] > dirty[t]
 // scratch: staged-sized; bigbins: rt_bigbins_ints(L) ints (tiles beyond the LDS capacity are sorted there)
 size_t rt_bigbins_ints(const RorLaunch &L);
+int rt_lds_tile_cap();   // records a tile may hold for k_rt_ror<false> (LDS); larger tiles take the big-tile kernels
 // kept_tile != nullptr (a streaming map's store): kept candidates are marked (w = 2) in staged, which
 // is rewritten bin-sorted per tile
 void launch_rt_ror(const RorLaunch &L, const int *tstart, float4 *staged, float4 *scratch, int *bigbins,

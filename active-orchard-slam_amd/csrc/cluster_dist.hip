@@ -72,8 +72,9 @@ __global__ void k_dist_fg(const uint64_t *win, TileView T, GridC g, const double
 struct PieceDev { int *n, *root, *mnx, *mxx, *mny, *mxy; unsigned long long *sx, *sy; };
 struct PieceRec { int root, n; long long sx, sy; int minx, maxx, miny, maxy; };   // 40 B, the gathered table
 
-__global__ void k_piece_init(PieceDev P, const int *n_pieces, int cap) {
+__global__ void k_piece_init(PieceDev P, const int *n_pieces, int cap, int *n_border) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) *n_border = 0;   // (k_piece_agg counts the border cells: no fill launch)
     if (i >= cap || i >= *n_pieces) return;
     P.n[i] = 0; P.sx[i] = 0; P.sy[i] = 0;
     P.mnx[i] = INT_MAX; P.mxx[i] = INT_MIN; P.mny[i] = INT_MAX; P.mxy[i] = INT_MIN;
@@ -318,9 +319,8 @@ void cluster_dist(ClusterDistState &D, FrameComm &fc, const TilePlan &t, const F
     int2 *d_border = dptr<int2>(D.border, PC);
     int *d_nb = dptr<int>(D.counts, 2);
     uint8_t *d_blob = dptr<uint8_t>(D.blob, (sizeof(PieceRec) + sizeof(int2)) * PC);
-    AOS_HIP(hipMemsetAsync(d_nb, 0, sizeof(int), s));
     if (nf > 0) {
-        k_piece_init<<<cdiv(nf, 256), 256, 0, s>>>(P, d_np, nf);
+        k_piece_init<<<cdiv(nf, 256), 256, 0, s>>>(P, d_np, nf, d_nb);
         k_piece_agg<<<cdiv(nf, kPcTB), kPcTB, 0, s>>>(d_list, d_par, d_rank, nf, T, W, g.H, P, d_pid, d_prank, d_border, d_nb);
         k_piece_pack<<<cdiv(nf, 256), 256, 0, s>>>(P, d_np, d_border, d_nb, nf, d_blob);
         AOS_HIP(hipGetLastError());

@@ -303,7 +303,7 @@ struct ColScan {
     int *H;                  // G rows of ntiles counts -> exclusive prefixes over the rows
     int *ts;                 // [ntiles + 1] tile starts
     const unsigned *own;     // [G] binned points per count workgroup
-    unsigned long long *n_own;
+    unsigned long long *n_own;   // [0] binned points, [2] the largest tile's record count (atomicMax)
     int ntiles, G, ng, ntb;
     LookBack L;              // part: ng x ntiles column words, then ntb tile-chain words; err bit 4 on a stuck wait
 };
@@ -373,6 +373,11 @@ __global__ __launch_bounds__(kColTB) void k_rt_colscan(ColScan C) {
     if (g != C.ng - 1) return;   // (uniform per block)
     // tile starts: run is now tile t's total
     const int local = block_excl_scan<kColTB>(live ? run : 0, wsum, &sh_tot);
+    {   // the largest tile (a frame that cannot be redone skips the big-tile kernels when it fits the LDS cap)
+        int mx = live ? run : 0;
+        for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+        if ((tid & 63) == 0 && mx > 0) atomicMax(C.n_own + 2, (unsigned long long)mx);
+    }
     if (tid < 64) {
         LookBack T = C.L;
         T.part += (size_t)C.ng * C.ntiles;
@@ -1049,6 +1054,8 @@ void launch_rt_scatter(const RorLaunch &L, int *H, const int *tstart, int G, flo
         default: rt_part<true, 0>(L, H, tstart, G, staged, nullptr, s);
     }
 }
+
+int rt_lds_tile_cap() { return kRorCap; }
 
 size_t rt_bigbins_ints(const RorLaunch &L) {
     return 2 * (size_t)L.ntiles * (2 * (L.TB + 2) * (L.TB + 2) + 1) + 1 + L.ntiles + L.ntiles + 1;

@@ -525,8 +525,8 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
     if (map_mode) d_ts = static_cast<int *>(ms.ts[ms.cur].ensure(sizeof(int) * (nt + 1)));
     int *d_kept = map_mode ? static_cast<int *>(ms.kept.ensure(sizeof(int) * nt)) : nullptr;
     DevBuf &stage_buf = map_mode ? ms.st[ms.cur] : sorted;
-    unsigned long long *d_cnt = static_cast<unsigned long long *>(counters.ensure(8 * kRorCounters + 16));
-    unsigned long long *d_own = d_cnt + kRorCounters;   // [0] binned points, [1] overflow flag
+    unsigned long long *d_cnt = static_cast<unsigned long long *>(counters.ensure(8 * kRorCounters + 24));
+    unsigned long long *d_own = d_cnt + kRorCounters;   // [0] binned points, [1] overflow flag, [2] largest tile
     // PCL dense kNN needs k = min_pts + 1 points in the whole cloud (else every point is removed).
     // A tile's shard holds every neighbour of its own candidates, so a shard with fewer points has
     // no keepable candidate either: the local test is exact.
@@ -534,10 +534,10 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
     // the counters, raster bits and kept counts start at zero: cleared by the count launch (no fills)
     RtClear clr;
     clr.w = rbits; clr.nw = (size_t)o.Hr * WWr;
-    clr.c = d_cnt; clr.nc = kRorCounters + 2;
+    clr.c = d_cnt; clr.nc = kRorCounters + 3;
     clr.k = d_kept; clr.nk = d_kept ? nt : 0;
     if (!any) {
-        AOS_HIP(hipMemsetAsync(d_cnt, 0, 8 * kRorCounters + 16, s));
+        AOS_HIP(hipMemsetAsync(d_cnt, 0, 8 * kRorCounters + 24, s));
         AOS_HIP(hipMemsetAsync(rbits, 0, sizeof(uint64_t) * clr.nw, s));
         if (d_kept) AOS_HIP(hipMemsetAsync(d_kept, 0, sizeof(int) * nt, s));
         return;
@@ -553,8 +553,12 @@ void aos_ctx::ror_stage(const FrameGeom &g, const RorOwn &o, uint64_t *rbits, bo
     const size_t cap_now = stage_buf.cap / sizeof(float4);
     const bool guess = allow_guess && ror_staged_max > 0 && cap_now >= (size_t)(ror_staged_max * 1.1);
     if (!guess) {
-        AOS_HIP(hipMemcpyAsync(h + 2, d_ts + nt, sizeof(int), hipMemcpyDeviceToHost, s));
+        // the staged total and the largest tile (h[3]: rewritten by ror_stats_to_host later)
+        peek_to_host(h + 2, {d_ts + nt, reinterpret_cast<const int *>(d_own + 2)}, s);
         AOS_HIP(hipStreamSynchronize(s));
+        // the big-tile kernels only for a frame that has a tile beyond the LDS cap (a tiled rank launched all six
+        // on every frame: ~27 us per rank, profiles/r06/r06d_tiling.json)
+        if (!map_mode && h[3] <= rt_lds_tile_cap()) L.big_ok = 0;
         const size_t need = (size_t)std::max(h[2], 1);
         ror_staged_max = std::max<double>(ror_staged_max, (double)need);
         stage_buf.ensure(sizeof(float4) * (size_t)(need * 1.15 + 1024));
@@ -596,7 +600,7 @@ void aos_ctx::ror_stage_append(RorLaunch L, uint64_t *rbits) {
     const int G = rt_part_blocks(Ls);
     int *d_H = static_cast<int *>(ms.scan_H.ensure(sizeof(int) * rt_h_ints(Ls, G)));
     int *d_sts = static_cast<int *>(ms.scan_ts.ensure(sizeof(int) * (nt + 1)));
-    unsigned long long *d_cnt = static_cast<unsigned long long *>(counters.ensure(8 * kRorCounters + 16));
+    unsigned long long *d_cnt = static_cast<unsigned long long *>(counters.ensure(8 * kRorCounters + 24));
     unsigned long long *d_own = d_cnt + kRorCounters;
     // a point lands in at most 4 tiles: the scan's staging and the merged store cannot overflow
     const size_t scan_cap = 4 * (size_t)scan_n + 1024;
@@ -611,7 +615,7 @@ void aos_ctx::ror_stage_append(RorLaunch L, uint64_t *rbits) {
     Ls.overflow = reinterpret_cast<int *>(d_own + 1);
     AOS_HIP(hipEventRecord(ev[12], s));
     RtClear clr;
-    clr.c = d_cnt; clr.nc = kRorCounters + 2;
+    clr.c = d_cnt; clr.nc = kRorCounters + 3;
     launch_rt_count(Ls, d_H, G, d_sts, d_own, ror_lookback(Ls, G, d_own), s, clr);
     AOS_HIP(hipEventRecord(ev[13], s));
     AOS_HIP(hipEventRecord(ev[14], s));

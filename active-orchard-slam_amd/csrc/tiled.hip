@@ -386,8 +386,7 @@ void aos_ctx::run_tiled_frame(FrameComm &fc, int tiles_x, int tiles_y, int root,
     const bool halo = t.hy || t.hw;
     const int nflags = 2 + max_iters + t.G / 2 + 4 * K;   // a period may run G / 2 iterations past T
     int *d_flags = static_cast<int *>(flags.ensure(sizeof(int) * nflags));
-    AOS_HIP(hipMemsetAsync(d_flags, 0, sizeof(int) * nflags, s));
-    launch_open(d_ibits, d_open, lg, s);
+    launch_open(d_ibits, d_open, lg, s, d_flags, nflags);   // (the opening clears the flags: no fill launch)
     int *h_flags = static_cast<int *>(h_small.ensure(sizeof(int) * nflags));
     const ThinOwn mine{t.y0 - t.wy0, t.y1 - t.wy0, t.c0 - t.wc0, t.c1 - t.wc0, 0};
     uint64_t *cur = d_open;
