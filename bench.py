@@ -39,15 +39,18 @@ WATCHDOG_EXIT = 3      # exit status of a run whose tiled section hung (its watc
 TILED_ERROR_EXIT = 4   # exit status of a run whose tiled / tiled_stream section raised (after the main line)
 # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE summaries (tools/pmc_traffic.py) of the ROR stage, per config,
 # for the kernels of this build's ROR design. A config or design without a committed PMC run gets null.
-ROR_DESIGN = "r05"    # (r04v: the host cloud split at upload; the partition passes read the front only. r05: + the tile
-                      # pass's batched loads and branch on the exact division: the same kernels and bytes)
+ROR_DESIGN = "r06"    # (r04v: the host cloud split at upload; the partition passes read the front only. r05: + the tile
+                      # pass's batched loads and branch on the exact division: the same kernels and bytes. r06: the
+                      # column scan also max-reduces the tile totals; passes re-collected at the round-6 build)
 PMC_FILES = {("C2", "r02"): os.path.join(ROOT, "profiles", "r02q_pmc_traffic.json"),
              ("C2", "r03"): os.path.join(ROOT, "profiles", "r03fin_pmc_traffic.json"),
              ("C2", "r04"): os.path.join(ROOT, "profiles", "r04i_pmc_traffic.json"),
              ("C2", "r04v"): os.path.join(ROOT, "profiles", "r04w_pmc_traffic.json"),
              ("C3", "r04v"): os.path.join(ROOT, "profiles", "r05_c3_pmc_traffic.json"),
              ("C2", "r05"): os.path.join(ROOT, "profiles", "r05zc_pmc_traffic.json"),
-             ("C3", "r05"): os.path.join(ROOT, "profiles", "r05_c3_pmc_traffic.json")}
+             ("C3", "r05"): os.path.join(ROOT, "profiles", "r05_c3_pmc_traffic.json"),
+             ("C2", "r06"): os.path.join(ROOT, "profiles", "r06", "r06o_pmc_traffic.json"),
+             ("C3", "r06"): os.path.join(ROOT, "profiles", "r06", "r06o_c3_pmc_traffic.json")}
 # rocprofv3 --kernel-trace --stats summaries (tools/kt_summary.py) of the sequential loop at this build: the median
 # trace frame's kernel time (every kernel of a frame, copies included), beside the live stage spans
 KT_FILES = {"C2": os.path.join(ROOT, "profiles", "r06", "r06i_kt_summary.txt")}
