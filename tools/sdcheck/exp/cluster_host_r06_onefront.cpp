@@ -1,3 +1,4 @@
+// Round-6 one-front-run form of active-orchard-slam_amd/csrc/cluster_host.cpp (namespace aos_old), kept for tools/sdcheck/bfs_real.sh A/B only.
 // Host-side parts of the cluster stage (a8-a10), kept in a plain C++ file so the sanitizer build
 // (tests/sanitize: ASan + UBSan, no GPU) runs exactly the code the product links:
 //   * host_bfs_replay / replay_clusters: clusterOccupiedCells' FIFO BFS (seed_gen:1007-1049) and its
@@ -22,7 +23,7 @@
 #include "cluster_geom.h"
 #include "cluster_seed.h"
 
-namespace aos {
+namespace aos_old { using namespace aos;
 
 constexpr int kReplayThreads = 16;   // host threads for the exact BFS replays of one frame (the box share: 16 cores)
 
@@ -84,119 +85,19 @@ static const int64_t kDxy[8] = {
 // bits are exactly the cells it queues, the rest are clear already. Per step that is one chain of a queue load, the
 // window loads, one table load and the queue stores, no data-dependent branch.
 // Runs: a row cluster's skeleton is a horizontal line walked from its left end with one cell queued (C1: 37 k of
-// 41 k pops), or, when its first raster cell lies mid-line, from there with two cells queued, one front going each way.
-// A queued cell whose 3 x 3 window holds exactly one unqueued cell, its left or right neighbour T, queues T and
-// nothing else when it pops; then T's own column and the one behind it hold nothing unqueued above or below (they
-// were in the window), so from T on each pop queues exactly the next cell ahead for as long as that cell is set and
-// the cells above and below it are not: the run's length is the trailing (leading, going left) ones of
-// row y & ~(row y - 1 | row y + 1) beyond T, 64 columns per word pair. With one or two such fronts queued (two: not
-// the same target, not facing each other on one row; a front's run stops before any unqueued cell next to the other
-// front's run, so the two never meet), R rounds of the FIFO pop the fronts' cells alternately, each queueing the next
-// one: the queue writes and the bit clears go by rows, the float sums one cell at a time in the same order (only the
-// additions stay serial: ~4 cycles a cell instead of the step's chain).
+// 41 k pops). When a step leaves exactly its right neighbour e queued, e's own column and the one left of it hold
+// nothing unqueued above or below (they were in the step's window), so from e on each pop queues exactly the next
+// cell to its right for as long as that cell is set and the cells above and below it are not: the run's length is
+// the trailing ones of (row y & ~(row y - 1 | row y + 1)) from e + 1, 64 columns per word pair. The run's pops are
+// then the queue writes of e + 1 ... e + k, their bits cleared by word, and the float sums added one cell at a time in
+// the same order (only the additions stay serial: ~4 cycles a cell instead of the step's chain).
 static long long bfs_walk(uint64_t *B, long long RW, int x0, int y0, int sx, int sy, XY *Q, long long cap, float &sum_x,
                           float &sum_y) {
     static_assert(sizeof(XY) == 8, "XY packs into 64 bits");
     Q[0] = XY{sx, sy};
     long long head = 0, tail = 1;
     float ax = 0.0f, ay = 0.0f;
-    // the 3 x 3 window of cell p as the 9-bit kWin index (bitmap columns c0 .. c0 + 2 = cells x - 1 .. x + 1)
-    auto window = [&](const XY &p) {
-        const long long c0 = (long long)p.x - x0;
-        const uint64_t *w = B + ((long long)p.y - y0) * RW + (c0 >> 6);
-        const int sh = (int)(c0 & 63);
-        auto win3 = [&](const uint64_t *q) { return (unsigned)((((unsigned __int128)q[1] << 64) | q[0]) >> sh) & 7u; };
-        return win3(w) | win3(w + RW) << 3 | win3(w + 2 * RW) << 6;
-    };
-    // cells beyond bitmap column s (itself first) of bitmap row r, going d = +1 / -1, that are set with nothing set
-    // above or below: a front's run length
-    auto run_len = [&](long long r, long long s, int d) -> long long {
-        const uint64_t *R0 = B + r * RW, *Rm = R0 - RW, *Rp = R0 + RW;
-        long long k = 0;
-        for (;;) {
-            const long long cur = s + d * k;
-            uint64_t ok;
-            int t;
-            if (d > 0) {   // bits cur .. cur + 63, bit 0 = cur
-                const long long wi = cur >> 6;
-                if (wi + 1 >= RW) break;
-                const int o = (int)(cur & 63);
-                auto b64 = [&](const uint64_t *row) { return (uint64_t)((((unsigned __int128)row[wi + 1] << 64) | row[wi]) >> o); };
-                ok = b64(R0) & ~(b64(Rm) | b64(Rp));
-                t = ok == ~0ull ? 64 : __builtin_ctzll(~ok);
-            } else {       // bits cur - 63 .. cur, bit 63 = cur (columns below 0 read as 0)
-                if (cur < 0) break;
-                auto b64 = [&](const uint64_t *row) -> uint64_t {
-                    if (cur < 63) return row[0] << (63 - cur);
-                    const long long lo = cur - 63, wi = lo >> 6;
-                    const int o = (int)(lo & 63);
-                    return (uint64_t)((((unsigned __int128)row[wi + 1] << 64) | row[wi]) >> o);
-                };
-                ok = b64(R0) & ~(b64(Rm) | b64(Rp));
-                t = ok == ~0ull ? 64 : __builtin_clzll(~ok);
-            }
-            k += t;
-            if (t < 64) break;
-        }
-        return k;
-    };
-    bool hint = false;   // the last step left one or two cells queued after a single horizontal push
     while (head < tail) {
-        if (hint) {
-            hint = false;
-            const int m = (int)(tail - head);
-            XY F[2];
-            int d[2];
-            bool ok = true;
-            for (int i = 0; i < m && ok; ++i) {
-                F[i] = Q[head + i];
-                const unsigned w9 = window(F[i]);
-                d[i] = w9 == (1u << 5) ? 1 : (w9 == (1u << 3) ? -1 : 0);
-                ok = d[i] != 0;
-            }
-            if (ok && m == 2)
-                ok = !(F[0].y == F[1].y && (F[0].x + d[0] == F[1].x + d[1] ||
-                                            (d[0] == -d[1] && (long long)(F[1].x - F[0].x) * d[0] > 0)));
-            if (ok) {
-                long long R = LLONG_MAX;
-                for (int i = 0; i < m; ++i)   // (beyond the target: its column + d)
-                    R = std::min(R, 1 + run_len((long long)F[i].y - y0 + 1, (long long)F[i].x - x0 + 1 + 2 * d[i], d[i]));
-                if (head + m * (R + 1) > cap) return -1;
-                // the rounds' pops in FIFO order (the sums) and their pushes (entries head + m j + i, j = 1 .. R)
-                if (m == 1) {
-                    const int x = F[0].x, dx = d[0], y = F[0].y;
-                    const float fy = (float)y;
-                    for (int j = 0; j < (int)R; ++j) { ax += (float)(x + j * dx); ay += fy; }
-                    XY *q = Q + head + 1;
-                    for (int j = 1; j <= (int)R; ++j) q[j - 1] = XY{x + j * dx, y};
-                } else {
-                    const int xa = F[0].x, da = d[0], ya = F[0].y, xb = F[1].x, db = d[1], yb = F[1].y;
-                    const float fya = (float)ya, fyb = (float)yb;
-                    for (int j = 0; j < (int)R; ++j) {
-                        ax += (float)(xa + j * da); ay += fya;
-                        ax += (float)(xb + j * db); ay += fyb;
-                    }
-                    XY *q = Q + head + 2;
-                    for (int j = 1; j <= (int)R; ++j) { q[2 * j - 2] = XY{xa + j * da, ya}; q[2 * j - 1] = XY{xb + j * db, yb}; }
-                }
-                for (int i = 0; i < m; ++i) {
-                    // clear the pushed cells' bits: bitmap columns of x + d .. x + R d in the front's row
-                    const long long cA = (long long)F[i].x - x0 + 1 + d[i], cB = (long long)F[i].x - x0 + 1 + R * d[i];
-                    uint64_t *row = B + ((long long)F[i].y - y0 + 1) * RW;
-                    for (long long bb = std::min(cA, cB), end = std::max(cA, cB) + 1; bb < end;) {
-                        const long long wi = bb >> 6;
-                        const int o = (int)(bb & 63);
-                        const long long nb = std::min<long long>(end, (wi + 1) << 6);
-                        const int len = (int)(nb - bb);
-                        row[wi] &= ~((len == 64 ? ~0ull : ((1ull << len) - 1)) << o);
-                        bb = nb;
-                    }
-                }
-                head += m * R;
-                tail = head + m;
-                continue;
-            }
-        }
         const XY c = Q[head++];
         ax += (float)c.x; ay += (float)c.y;
         // bitmap columns c0 .. c0 + 2 = cells x - 1 .. x + 1 of rows y - 1 .. y + 1
@@ -215,7 +116,44 @@ static long long bfs_walk(uint64_t *B, long long RW, int x0, int y0, int sx, int
         const uint64_t lo = ~(7ull << sh), hi = ~(3ull >> (63 - sh));
         w[0] &= lo; w[1] &= hi; w[RW] &= lo; w[RW + 1] &= hi; w[2 * RW] &= lo; w[2 * RW + 1] &= hi;
         if (tail > cap) return -1;
-        hint = (e == (1u | 1u << 24) || e == (6u | 1u << 24)) && tail - head <= 2;
+        if (e == (6u | 1u << 24) && tail - head == 1) {   // one push, (dx, dy) = (1, 0), and nothing else queued
+            // bitmap columns s, s + 1, ... of the popped cell's row = cells x + 2, x + 3, ...: e = (x + 1, y)
+            const long long s0 = c0 + 3;
+            const uint64_t *rr = w + RW - (c0 >> 6);   // the row's first word
+            long long k = 0;
+            for (;;) {
+                const long long s = s0 + k, wi = s >> 6;
+                const int o = (int)(s & 63);
+                auto bits64 = [&](const uint64_t *row) {
+                    return (uint64_t)((((unsigned __int128)row[wi + 1] << 64) | row[wi]) >> o);
+                };
+                const uint64_t ok = bits64(rr) & ~(bits64(rr - RW) | bits64(rr + RW));
+                const int t = ok == ~0ull ? 64 : __builtin_ctzll(~ok);
+                k += t;
+                if (t < 64 || s + 64 + 64 > RW * 64) break;   // (the next word pair must still lie in the row)
+            }
+            if (k > 0) {
+                if (tail + k > cap) return -1;
+                const int ex = c.x + 1, y = c.y;
+                const float fy = (float)y;
+                for (long long j = 0; j < k; ++j) {
+                    Q[head + 1 + j] = XY{ex + 1 + (int)j, y};
+                    ax += (float)(ex + (int)j); ay += fy;
+                }
+                // clear row y's columns s0 .. s0 + k - 1 (the cells queued by the run)
+                uint64_t *rw = w + RW - (c0 >> 6);
+                for (long long b = s0, end = s0 + k; b < end;) {
+                    const long long wi = b >> 6;
+                    const int o = (int)(b & 63);
+                    const long long nb = std::min<long long>(end, (wi + 1) << 6);
+                    const int len = (int)(nb - b);
+                    rw[wi] &= ~((len == 64 ? ~0ull : ((1ull << len) - 1)) << o);
+                    b = nb;
+                }
+                head += k;
+                tail = head + 1;
+            }
+        }
     }
     sum_x = ax; sum_y = ay;
     return tail;
@@ -489,14 +427,7 @@ void replay_clusters(const std::vector<ReplayJob> &jobs, const GridC &g, const d
             }
         }
     };
-    // one core of the share is left to the markers' replay, which runs beside the next frame's seed-gen (C3: every
-    // frame): 16 replay threads and that worker on 16 cores had the scheduler time-slice a replay in the last round
-    // (AOS_REPLAY_THREADS: A/B runs)
-    static const int max_t = [] {
-        const char *e = getenv("AOS_REPLAY_THREADS");
-        return e ? std::max(1, atoi(e)) : std::min(kReplayThreads, std::max(1, host_cpu_share() - 1));
-    }();
-    const int nt = std::min<int>((int)jobs.size(), max_t);
+    const int nt = std::min<int>((int)jobs.size(), std::min(kReplayThreads, host_cpu_share()));
     if (pool) {
         pool->run(nt, work);
     } else {
