@@ -161,6 +161,8 @@ void aos_ctx::upload_pack(void *dst, const aos_cloud_view &v, CloudSplit &sp, bo
     }();
     const uint64_t n = v.n_points;
     const int nth = up_threads();
+    // AOS_UP_STREAMS (A/B runs): the threads' copies share this many streams (thread t: stream t mod it)
+    static const int n_up_streams = [] { const char *e = getenv("AOS_UP_STREAMS"); return e ? std::max(1, atoi(e)) : kUpThreads; }();
     for (int t = 0; t < nth; ++t)
         if (!up.st[t]) {
             AOS_HIP(hipStreamCreateWithFlags(&up.st[t], hipStreamNonBlocking));
@@ -191,7 +193,8 @@ void aos_ctx::upload_pack(void *dst, const aos_cloud_view &v, CloudSplit &sp, bo
     auto work = [&](int t) {
         try {
             AOS_HIP(hipSetDevice(device));
-            if (!prefetch) AOS_HIP(hipStreamWaitEvent(up.st[t], ev[15], 0));
+            hipStream_t ust = up.st[t % std::min(nth, n_up_streams)];
+            if (!prefetch) AOS_HIP(hipStreamWaitEvent(ust, ev[15], 0));
             const uint64_t p0 = std::min(n, per * t), p1 = std::min(n, per * (t + 1));
             float *rr = split ? rest + 3 * p0 + (kPackSlack / 4) * t : nullptr;   // (kPackSlack between runs)
             uint64_t nr = 0;
@@ -210,12 +213,12 @@ void aos_ctx::upload_pack(void *dst, const aos_cloud_view &v, CloudSplit &sp, bo
                 }
                 if (!f) continue;   // (the slot's last DMA, if any, stays its event)
                 const uint64_t at = split ? front.fetch_add(f) : c;
-                AOS_HIP(hipMemcpyAsync(static_cast<char *>(dst) + 12 * at, o, 12 * f, hipMemcpyHostToDevice, up.st[t]));
-                AOS_HIP(hipEventRecord(up.ev[t][k], up.st[t]));
+                AOS_HIP(hipMemcpyAsync(static_cast<char *>(dst) + 12 * at, o, 12 * f, hipMemcpyHostToDevice, ust));
+                AOS_HIP(hipEventRecord(up.ev[t][k], ust));
                 up.used[t][k] = true;
             }
             rn[t] = nr;
-            AOS_HIP(hipEventRecord(up.done[t], up.st[t]));
+            AOS_HIP(hipEventRecord(up.done[t], ust));
         } catch (...) { err[t] = std::current_exception(); }
     };
     HostTrace tr{"upload"};
