@@ -270,91 +270,143 @@ struct StatArgs {
     float min_length;
     ClusterRec *rec;
     ClusterRec *hrec;         // nullable: pinned host copy of rec, stored by the same threads
+    int lds_cap;              // clusters of at most this many cells are read from global memory once (kStatLds or 0)
 };
-
-template <typename T, typename Op>
-__device__ T block_reduce(T v, T *sh, Op op) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    for (int o = 32; o > 0; o >>= 1) v = op(v, __shfl_xor(v, o));
-    __syncthreads();
-    if (lane == 0) sh[wid] = v;
-    __syncthreads();
-    T r = sh[0];
-    for (int k = 1; k < nw; ++k) r = op(r, sh[k]);
-    __syncthreads();
-    return r;
-}
 
 struct MaxOp { template <class T> __device__ T operator()(T a, T b) const { return a > b ? a : b; } };
 struct MinOp { template <class T> __device__ T operator()(T a, T b) const { return a < b ? a : b; } };
 struct AddOp { template <class T> __device__ T operator()(T a, T b) const { return a + b; } };
 
-// one workgroup per cluster
-__global__ __launch_bounds__(512) void k_cluster_stats(StatArgs A) {   // (512 threads: the long row clusters set its time)
-    __shared__ long long shl[8];
-    __shared__ int shi[8];
-    __shared__ double shd[8];
+// K reductions in one barrier: shuffles inside each wave, one LDS slot per (value, wave), every thread combines the
+// slots. sh holds K * 16 values and belongs to this call alone (the next call uses other slots), so no barrier
+// follows it.
+template <int K, typename T, typename... Ops>
+__device__ __forceinline__ void block_reduce_k(T (&v)[K], T *sh, Ops... ops) {
+    static_assert(sizeof...(Ops) == K, "one operator per value");
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    auto one = [&](int i, auto op) {
+        for (int o = 32; o > 0; o >>= 1) v[i] = op(v[i], __shfl_xor(v[i], o));
+        if (lane == 0) sh[16 * i + wid] = v[i];
+    };
+    {
+        int i = 0;
+        (one(i++, ops), ...);
+    }
+    __syncthreads();
+    auto all = [&](int i, auto op) {
+        T r = sh[16 * i];
+        for (int w = 1; w < nw; ++w) r = op(r, sh[16 * i + w]);
+        v[i] = r;
+    };
+    int i = 0;
+    (all(i++, ops), ...);
+}
+
+__device__ __forceinline__ double2 cell_wxy(const GridC &g, int x, int y) {   // cell_w of the cell (x, y)
+    return make_double2((double)cell_world(g.ox, x, g.res), (double)cell_world(g.oy, y, g.res));
+}
+
+// One workgroup per cluster. The first pass reads the cluster's cells from global memory (four loads in flight per
+// thread) and keeps them in LDS as packed (y << 16 | x); the seven later passes (extreme cells, length candidates,
+// the endpoint maxima and their arguments) read LDS, and the reductions of a pass share one barrier. Round 5 read
+// the cells from global memory and divided p by W in every pass, with a three-barrier reduction per value (18 of
+// them): 49.7 us per C2 frame (profiles/r06/r06t_kt_summary.txt), set by the three ~8000-cell row clusters.
+// Clusters beyond the LDS (or grids of 65536 columns or rows and more: lds_cap 0) read global memory in every pass.
+constexpr int kStatTB = 512, kStatLds = 16384;   // 64 KB of cells
+__global__ __launch_bounds__(kStatTB) void k_cluster_stats(StatArgs A) {
+    __shared__ unsigned cc[kStatLds];
+    __shared__ long long shl[2 * 16];
+    __shared__ int shi[16 * 16];
+    __shared__ double shd[3 * 16];
     __shared__ int cand[2048];
     __shared__ int ncand;
-    const int cid = blockIdx.x;
+    const int cid = blockIdx.x, tid = threadIdx.x;
     const int b = A.off[cid], e = A.off[cid + 1], n = e - b;
     const GridC &g = A.g;
+    const int W = g.W;
+    const bool lds = n <= A.lds_cap;
+    auto xy_at = [&](int k, int &x, int &y) {
+        if (lds) {
+            const unsigned v = cc[k];
+            x = (int)(v & 0xffffu); y = (int)(v >> 16);
+        } else {
+            const int p = A.cells[b + k];
+            y = p / W; x = p - y * W;
+        }
+    };
     long long sx = 0, sy = 0;
     int mnx = INT_MAX, mxx = INT_MIN, mny = INT_MAX, mxy = INT_MIN, first = INT_MAX;
-    for (int k = b + threadIdx.x; k < e; k += blockDim.x) {
-        int p = A.cells[k], y = p / g.W, x = p - y * g.W;
-        sx += x; sy += y;
-        mnx = min(mnx, x); mxx = max(mxx, x); mny = min(mny, y); mxy = max(mxy, y);
-        first = min(first, p);
+    for (int k0 = tid; k0 < n; k0 += 4 * kStatTB) {
+        int pv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int k = k0 + u * kStatTB;
+            pv[u] = k < n ? A.cells[b + k] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int p = pv[u];
+            if (p < 0) continue;
+            const int y = p / W, x = p - y * W;
+            if (lds) cc[k0 + u * kStatTB] = (unsigned)x | ((unsigned)y << 16);
+            sx += x; sy += y;
+            mnx = min(mnx, x); mxx = max(mxx, x); mny = min(mny, y); mxy = max(mxy, y);
+            first = min(first, p);
+        }
     }
-    sx = block_reduce(sx, shl, AddOp());
-    sy = block_reduce(sy, shl, AddOp());
-    mnx = block_reduce(mnx, shi, MinOp()); mxx = block_reduce(mxx, shi, MaxOp());
-    mny = block_reduce(mny, shi, MinOp()); mxy = block_reduce(mxy, shi, MaxOp());
-    first = block_reduce(first, shi, MinOp());
+    {
+        long long l2[2] = {sx, sy};
+        block_reduce_k(l2, shl, AddOp(), AddOp());
+        sx = l2[0]; sy = l2[1];
+        int i5[5] = {mnx, mxx, mny, mxy, first};
+        block_reduce_k(i5, shi, MinOp(), MaxOp(), MinOp(), MaxOp(), MinOp());   // (its barrier also publishes cc)
+        mnx = i5[0]; mxx = i5[1]; mny = i5[2]; mxy = i5[3]; first = i5[4];
+    }
     // ---- max pairwise squared distance (cluster.length, seed_gen:1063-1073), pruned exactly:
     // LB = d^2 between the cells of extreme x / extreme y; a cell can belong to a farther pair only
     // if its distance to the farthest bbox corner reaches LB.
-    int ax = INT_MAX, bx_ = INT_MAX, ay = INT_MAX, by_ = INT_MAX;  // pixel ids with min/max x, min/max y
-    for (int k = b + threadIdx.x; k < e; k += blockDim.x) {
-        int p = A.cells[k], y = p / g.W, x = p - y * g.W;
-        if (x == mnx) ax = min(ax, p);
-        if (x == mxx) bx_ = min(bx_, p);
-        if (y == mny) ay = min(ay, p);
-        if (y == mxy) by_ = min(by_, p);
+    int ext[4] = {INT_MAX, INT_MAX, INT_MAX, INT_MAX};   // pixel ids with min/max x, min/max y
+    for (int k = tid; k < n; k += kStatTB) {
+        int x, y;
+        xy_at(k, x, y);
+        const int p = y * W + x;
+        if (x == mnx) ext[0] = min(ext[0], p);
+        if (x == mxx) ext[1] = min(ext[1], p);
+        if (y == mny) ext[2] = min(ext[2], p);
+        if (y == mxy) ext[3] = min(ext[3], p);
     }
-    ax = block_reduce(ax, shi, MinOp()); bx_ = block_reduce(bx_, shi, MinOp());
-    ay = block_reduce(ay, shi, MinOp()); by_ = block_reduce(by_, shi, MinOp());
+    if (tid == 0) ncand = 0;
+    block_reduce_k(ext, shi + 5 * 16, MinOp(), MinOp(), MinOp(), MinOp());
     auto d2p = [&](int p, int q) {
-        int py = p / g.W, px = p - py * g.W, qy = q / g.W, qx = q - qy * g.W;
+        int py = p / W, px = p - py * W, qy = q / W, qx = q - qy * W;
         int dx = px - qx, dy = py - qy;
         return dx * dx + dy * dy;
     };
-    const int LB = max(d2p(ax, bx_), d2p(ay, by_));
-    if (threadIdx.x == 0) ncand = 0;
-    __syncthreads();
-    for (int k = b + threadIdx.x; k < e; k += blockDim.x) {
-        int p = A.cells[k], y = p / g.W, x = p - y * g.W;
+    const int LB = max(d2p(ext[0], ext[1]), d2p(ext[2], ext[3]));
+    for (int k = tid; k < n; k += kStatTB) {
+        int x, y;
+        xy_at(k, x, y);
         int dxm = max(x - mnx, mxx - x), dym = max(y - mny, mxy - y);
         if (dxm * dxm + dym * dym >= LB) {
             int s = atomicAdd(&ncand, 1);
-            if (s < 2048) cand[s] = p;
+            if (s < 2048) cand[s] = y * W + x;
         }
     }
     __syncthreads();
     int maxd2 = LB;
     const int nc = ncand;
     if (nc <= 2048) {
-        const long long pairs = (long long)nc * nc;
-        for (long long t = threadIdx.x; t < pairs; t += blockDim.x) {
-            int i = (int)(t / nc), j = (int)(t - (long long)i * nc);
-            if (j > i) maxd2 = max(maxd2, d2p(cand[i], cand[j]));
-        }
+        for (int i = 0; i < nc; ++i)
+            for (int j = i + 1 + tid; j < nc; j += kStatTB) maxd2 = max(maxd2, d2p(cand[i], cand[j]));
     } else {  // too many candidates: exact brute force over all pairs
         for (int i = b; i < e; ++i)
-            for (int k = i + 1 + threadIdx.x; k < e; k += blockDim.x) maxd2 = max(maxd2, d2p(A.cells[i], A.cells[k]));
+            for (int k = i + 1 + tid; k < e; k += kStatTB) maxd2 = max(maxd2, d2p(A.cells[i], A.cells[k]));
     }
-    maxd2 = block_reduce(maxd2, shi, MaxOp());
+    {
+        int m[1] = {maxd2};
+        block_reduce_k(m, shi + 9 * 16, MaxOp());
+        maxd2 = m[0];
+    }
 
     ClusterRec r{};
     r.sx = sx; r.sy = sy; r.n = n; r.maxd2 = maxd2;
@@ -373,89 +425,105 @@ __global__ __launch_bounds__(512) void k_cluster_stats(StatArgs A) {   // (512 t
     }
     if (row && !needs_bfs) {
         // first endpoint: first cell with strictly maximal |wp - centre|^2 (seed_gen:1354-1367)
-        double m1 = 0.0;
-        for (int k = b + threadIdx.x; k < e; k += blockDim.x) {
-            double2 w = cell_w(g, A.cells[k]);
+        double m1[1] = {0.0};
+        for (int k = tid; k < n; k += kStatTB) {
+            int x, y;
+            xy_at(k, x, y);
+            double2 w = cell_wxy(g, x, y);
             double dx = w.x - r.center.x, dy = w.y - r.center.y;
-            m1 = fmax(m1, dx * dx + dy * dy);
+            m1[0] = fmax(m1[0], dx * dx + dy * dy);
         }
-        m1 = block_reduce(m1, shd, MaxOp());
-        int cnt = 0, arg = INT_MAX;
-        for (int k = b + threadIdx.x; k < e; k += blockDim.x) {
-            double2 w = cell_w(g, A.cells[k]);
+        block_reduce_k(m1, shd, MaxOp());
+        int ca[2] = {0, INT_MAX};   // count, smallest cell of the maximum
+        for (int k = tid; k < n; k += kStatTB) {
+            int x, y;
+            xy_at(k, x, y);
+            double2 w = cell_wxy(g, x, y);
             double dx = w.x - r.center.x, dy = w.y - r.center.y;
-            if (dx * dx + dy * dy == m1 && m1 > 0.0) { ++cnt; arg = min(arg, A.cells[k]); }
+            if (dx * dx + dy * dy == m1[0] && m1[0] > 0.0) { ++ca[0]; ca[1] = min(ca[1], y * W + x); }
         }
-        cnt = block_reduce(cnt, shi, AddOp());
-        arg = block_reduce(arg, shi, MinOp());
-        if (cnt != 1) needs_bfs = true;
+        block_reduce_k(ca, shi + 10 * 16, AddOp(), MinOp());
+        const int arg = ca[1];
+        if (ca[0] != 1) needs_bfs = true;
         if (!needs_bfs) {
             const double2 wf = cell_w(g, arg);
             double fdx = wf.x - r.center.x, fdy = wf.y - r.center.y;
             double z = fdx * fdx + fdy * fdy, s = sqrt(z);
             const double fx = fdx / s, fy = fdy / s;  // first_direction = diff.normalized()
             // second endpoint: dot(normalized(diff), first_dir) < 0, strictly maximal (seed_gen:1369-1385)
-            double m2 = 0.0;
-            for (int k = b + threadIdx.x; k < e; k += blockDim.x) {
-                int p = A.cells[k];
-                if (p == arg) continue;
-                double2 w = cell_w(g, p);
+            double m2[1] = {0.0};
+            for (int k = tid; k < n; k += kStatTB) {
+                int x, y;
+                xy_at(k, x, y);
+                if (y * W + x == arg) continue;
+                double2 w = cell_wxy(g, x, y);
                 double dx = w.x - r.center.x, dy = w.y - r.center.y, d2 = dx * dx + dy * dy;
                 double nx = dx, ny = dy;
                 if (d2 > 0.0) { double q = sqrt(d2); nx = dx / q; ny = dy / q; }
-                if (nx * fx + ny * fy < 0.0) m2 = fmax(m2, d2);
+                if (nx * fx + ny * fy < 0.0) m2[0] = fmax(m2[0], d2);
             }
-            m2 = block_reduce(m2, shd, MaxOp());
-            int cnt2 = 0, arg2 = INT_MAX;
-            bool fallback = !(m2 > 0.0);
-            for (int k = b + threadIdx.x; k < e; k += blockDim.x) {
-                int p = A.cells[k];
-                if (p == arg) continue;
-                double2 w = cell_w(g, p);
-                if (!fallback) {
+            block_reduce_k(m2, shd + 16, MaxOp());
+            int ca2[2] = {0, INT_MAX};
+            const bool fallback = !(m2[0] > 0.0);
+            if (!fallback) {
+                for (int k = tid; k < n; k += kStatTB) {
+                    int x, y;
+                    xy_at(k, x, y);
+                    const int p = y * W + x;
+                    if (p == arg) continue;
+                    double2 w = cell_wxy(g, x, y);
                     double dx = w.x - r.center.x, dy = w.y - r.center.y, d2 = dx * dx + dy * dy;
                     double nx = dx, ny = dy;
                     if (d2 > 0.0) { double q = sqrt(d2); nx = dx / q; ny = dy / q; }
-                    if (nx * fx + ny * fy < 0.0 && d2 == m2) { ++cnt2; arg2 = min(arg2, p); }
+                    if (nx * fx + ny * fy < 0.0 && d2 == m2[0]) { ++ca2[0]; ca2[1] = min(ca2[1], p); }
+                }
+            } else {  // farthest from the first endpoint (seed_gen:1387-1399)
+                double m3[1] = {0.0};
+                for (int k = tid; k < n; k += kStatTB) {
+                    int x, y;
+                    xy_at(k, x, y);
+                    if (y * W + x == arg) continue;
+                    double2 w = cell_wxy(g, x, y);
+                    double dx = w.x - wf.x, dy = w.y - wf.y;
+                    m3[0] = fmax(m3[0], dx * dx + dy * dy);
+                }
+                block_reduce_k(m3, shd + 32, MaxOp());
+                for (int k = tid; k < n; k += kStatTB) {
+                    int x, y;
+                    xy_at(k, x, y);
+                    const int p = y * W + x;
+                    if (p == arg) continue;
+                    double2 w = cell_wxy(g, x, y);
+                    double dx = w.x - wf.x, dy = w.y - wf.y;
+                    if (dx * dx + dy * dy == m3[0] && m3[0] > 0.0) { ++ca2[0]; ca2[1] = min(ca2[1], p); }
                 }
             }
-            if (fallback) {  // farthest from the first endpoint (seed_gen:1387-1399)
-                double m3 = 0.0;
-                for (int k = b + threadIdx.x; k < e; k += blockDim.x) {
-                    int p = A.cells[k];
-                    if (p == arg) continue;
-                    double2 w = cell_w(g, p);
-                    double dx = w.x - wf.x, dy = w.y - wf.y;
-                    m3 = fmax(m3, dx * dx + dy * dy);
-                }
-                m3 = block_reduce(m3, shd, MaxOp());
-                for (int k = b + threadIdx.x; k < e; k += blockDim.x) {
-                    int p = A.cells[k];
-                    if (p == arg) continue;
-                    double2 w = cell_w(g, p);
-                    double dx = w.x - wf.x, dy = w.y - wf.y;
-                    if (dx * dx + dy * dy == m3 && m3 > 0.0) { ++cnt2; arg2 = min(arg2, p); }
-                }
-            }
-            cnt2 = block_reduce(cnt2, shi, AddOp());
-            arg2 = block_reduce(arg2, shi, MinOp());
-            if (cnt2 != 1) needs_bfs = true;  // (fallback with max 0 keeps index 0 -> BFS replay)
+            block_reduce_k(ca2, shi + 12 * 16, AddOp(), MinOp());
+            if (ca2[0] != 1) needs_bfs = true;  // (fallback with max 0 keeps index 0 -> BFS replay)
             r.start = wf;
-            if (!needs_bfs) r.end = cell_w(g, arg2);
+            if (!needs_bfs) r.end = cell_w(g, ca2[1]);
         }
     }
     r.flags = (row ? 1 : 0) | (needs_bfs ? 2 : 0);
-    if (threadIdx.x == 0) {
+    if (tid == 0) {
         A.rec[cid] = r;
         if (A.hrec) A.hrec[cid] = r;
     }
 }
 
+// clusters read from global memory once when they fit the LDS (AOS_DEBUG_STATS_LDS=0, read per call: every pass
+// from global memory, the path of larger clusters and of grids of 65536 columns or rows and more)
+static int stats_lds_cap(const GridC &g) {
+    const char *e = getenv("AOS_DEBUG_STATS_LDS");
+    if (e && atoi(e) == 0) return 0;
+    return g.W <= 65536 && g.H <= 65536 ? kStatLds : 0;
+}
+
 void launch_cluster_stats(const int *off, const int *cells, int n_clusters, const GridC &g, const double *poly, int np,
                           float min_length, ClusterRec *rec, hipStream_t s, ClusterRec *hrec) {
     if (n_clusters <= 0) return;
-    StatArgs A{off, cells, nullptr, n_clusters, g, poly, np, min_length, rec, hrec};
-    k_cluster_stats<<<n_clusters, 512, 0, s>>>(A);
+    StatArgs A{off, cells, nullptr, n_clusters, g, poly, np, min_length, rec, hrec, stats_lds_cap(g)};
+    k_cluster_stats<<<n_clusters, kStatTB, 0, s>>>(A);
     AOS_HIP(hipGetLastError());
 }
 

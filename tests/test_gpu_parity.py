@@ -340,6 +340,40 @@ def test_dense_patches_overflow_the_lds_row_ring():
     _full_frame_parity(cloud, orchard.polygon(cfg), cfg.res)
 
 
+def test_big_tile_after_frames_without_one_on_the_same_handle():
+    """The big-tile ROR kernels are skipped on frames whose largest tile fits LDS (seedgen.hip ror_stage: the
+    peeked tile maximum) and on guessed frames of a handle that never needed them; a guessed frame that then
+    finds a big tile sets overflow bit 2 and is redone with them (ror_collect). Sequence on one handle:
+    spread extra points (no big tile, fixes the staging guess) -> dense patches (the guessed frame's redo)
+    -> spread -> dense again (big kernels on from then on), each frame vs the oracle."""
+    cfg = orchard.CONFIGS["C0"]
+    base = orchard.generate(cfg).view(np.float32).reshape(-1, 4)
+    poly = orchard.polygon(cfg)
+    rng = np.random.default_rng(12)
+
+    def with_extra(dense):
+        n = 16000
+        p = np.zeros((n, 4), np.float32)
+        if dense:
+            c = np.repeat(np.array([[20.0, 2.0], [40.3, 5.5], [71.9, 12.5], [10.0, 30.0]]), n // 4, axis=0)
+            p[:, :2] = c + rng.uniform(-0.25, 0.25, (n, 2))
+        else:
+            p[:, 0] = rng.uniform(2.0, 95.0, n)
+            p[:, 1] = rng.uniform(2.0, 40.0, n)
+        p[:, 2] = rng.uniform(-0.3, 0.4, n)
+        return np.concatenate([base, p]).view(np.uint8).reshape(-1, 16)
+
+    c = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res))
+    c.set_polygon(poly)
+    for dense in (False, True, False, True):
+        cloud = with_extra(dense)
+        g = c.seedgen(cloud)
+        o = O.seedgen(cloud, poly, O.default_params(grid_resolution=cfg.res))
+        assert_seedgen_parity(g, o)
+        assert_gvd_parity(c.gvd_from_seedgen(), O.gvd(o["voronoi_seeds"], o["rows_info"], o))
+    c.close()
+
+
 def test_rotated_orchard_concave_polygon_and_odd_resolution():
     """Rows at 30 degrees, an L-shaped exploration polygon, 0.15 m cells (R = 5)."""
     cfg = orchard.CONFIGS["C0"]
@@ -462,6 +496,24 @@ def test_ccl_link_list_overflow_fallback(monkeypatch):
     monkeypatch.setenv("AOS_DEBUG_CCL_ECAP", "2")
     b = ctx.seedgen(cloud)
     monkeypatch.delenv("AOS_DEBUG_CCL_ECAP")
+    ctx.close()
+    assert a["n_clusters_all"] == b["n_clusters_all"] and a["n_bfs_replayed"] == b["n_bfs_replayed"]
+    for k in ("row_center", "row_start", "row_end", "row_length", "voronoi_seeds", "cluster_info", "rows_info"):
+        assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), k
+
+
+def test_cluster_stats_global_memory_path(monkeypatch):
+    """k_cluster_stats keeps a cluster's cells in LDS when it fits (kStatLds cells, grids below 65536 columns and
+    rows) and otherwise reads global memory in every pass. A C1 frame with the LDS copy off (AOS_DEBUG_STATS_LDS=0)
+    equals the default frame: records, replays, rows and seeds."""
+    cfg = orchard.CONFIGS["C1"]
+    cloud, poly = orchard.generate(cfg), orchard.polygon(cfg)
+    ctx = aos_gpu.Ctx(aos_gpu.default_params(grid_resolution=cfg.res))
+    ctx.set_polygon(poly)
+    a = ctx.seedgen(cloud)
+    monkeypatch.setenv("AOS_DEBUG_STATS_LDS", "0")
+    b = ctx.seedgen(cloud)
+    monkeypatch.delenv("AOS_DEBUG_STATS_LDS")
     ctx.close()
     assert a["n_clusters_all"] == b["n_clusters_all"] and a["n_bfs_replayed"] == b["n_bfs_replayed"]
     for k in ("row_center", "row_start", "row_end", "row_length", "voronoi_seeds", "cluster_info", "rows_info"):
