@@ -23,6 +23,7 @@
 #include "cluster_dev.h"
 #include "cluster_seed.h"
 #include "dev_prims_device.h"
+#include "dev_wave.h"
 
 namespace aos {
 
@@ -277,53 +278,57 @@ struct MaxOp { template <class T> __device__ T operator()(T a, T b) const { retu
 struct MinOp { template <class T> __device__ T operator()(T a, T b) const { return a < b ? a : b; } };
 struct AddOp { template <class T> __device__ T operator()(T a, T b) const { return a + b; } };
 
-// K reductions in one barrier: shuffles inside each wave, one LDS slot per (value, wave), every thread combines the
-// slots. sh holds K * 16 values and belongs to this call alone (the next call uses other slots), so no barrier
-// follows it.
-template <int K, typename T, typename... Ops>
-__device__ __forceinline__ void block_reduce_k(T (&v)[K], T *sh, Ops... ops) {
-    static_assert(sizeof...(Ops) == K, "one operator per value");
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    auto one = [&](int i, auto op) {
-        for (int o = 32; o > 0; o >>= 1) v[i] = op(v[i], __shfl_xor(v[i], o));
-        if (lane == 0) sh[16 * i + wid] = v[i];
-    };
-    {
-        int i = 0;
-        (one(i++, ops), ...);
+// The strict maximum of a pass (seed_gen:1354-1399's "first cell with a strictly larger value"): the largest value d,
+// how many cells reach it and the smallest of them. Order-free: the pass's cells in any order give the same triple.
+struct ArgMax {
+    double d; int c, a;
+    __device__ void add(double v, int p) {
+        if (v > d) { d = v; c = 1; a = p; }
+        else if (v == d) { ++c; a = min(a, p); }
     }
-    __syncthreads();
-    auto all = [&](int i, auto op) {
-        T r = sh[16 * i];
-        for (int w = 1; w < nw; ++w) r = op(r, sh[16 * i + w]);
-        v[i] = r;
-    };
-    int i = 0;
-    (all(i++, ops), ...);
-}
+    template <int CTRL, int RM> __device__ ArgMax dpp(const ArgMax &old) const {
+        return ArgMax{dpp_f64<CTRL, RM>(old.d, d), dpp_i32<CTRL, RM>(old.c, c), dpp_i32<CTRL, RM>(old.a, a)};
+    }
+    __device__ ArgMax lane63() const { return ArgMax{lane63_f64(d), lane63_i32(c), lane63_i32(a)}; }
+};
+struct ArgMaxOp {
+    __device__ ArgMax operator()(const ArgMax &x, const ArgMax &y) const {
+        if (y.d > x.d) return y;
+        if (x.d > y.d) return x;
+        return ArgMax{x.d, x.c + y.c, min(x.a, y.a)};
+    }
+};
+__device__ constexpr ArgMax kArgMaxNone{-1.0, 0, INT_MAX};
 
 __device__ __forceinline__ double2 cell_wxy(const GridC &g, int x, int y) {   // cell_w of the cell (x, y)
     return make_double2((double)cell_world(g.ox, x, g.res), (double)cell_world(g.oy, y, g.res));
 }
 
-// One workgroup per cluster. The first pass reads the cluster's cells from global memory (four loads in flight per
-// thread) and keeps them in LDS as packed (y << 16 | x); the seven later passes (extreme cells, length candidates,
-// the endpoint maxima and their arguments) read LDS, and the reductions of a pass share one barrier. Round 5 read
-// the cells from global memory and divided p by W in every pass, with a three-barrier reduction per value (18 of
-// them): 49.7 us per C2 frame (profiles/r06/r06t_kt_summary.txt), set by the three ~8000-cell row clusters.
+// One workgroup per cluster, three passes over its cells (a fourth in the rare fallback of the second endpoint):
+//  1. from global memory (four loads in flight per thread), kept in LDS as packed (y << 16 | x): the coordinate sums,
+//     and min over the keys (x, p), (W - 1 - x, p), (y, p), (H - 1 - y, p) -- the bounding box, the extreme cells of
+//     the length bound and (the smallest p) the first cell at once;
+//  2. the length candidates and the first endpoint's strict maximum (ArgMax: max, count, smallest cell) around the
+//     centre, computed for every cluster (it is used only for rows: seed_gen:1354-1367);
+//  3. the second endpoint's strict maximum (seed_gen:1369-1385).
+// Reductions run on DPP row moves (dev_wave.h), one barrier each. Before: one pass per maximum and per argument, every
+// pass from global memory with a division by W per cell, 18 three-barrier shuffle reductions; 49.7 us per C2 frame
+// (round-6 start, profiles/r06/r06t_kt_summary.txt), 36.7 us with the LDS copy alone (r06y), where each pass cost
+// ~3-4 us of which ~2 us was its ds_bpermute reduction chains (in-kernel s_memrealtime stamps per pass).
 // Clusters beyond the LDS (or grids of 65536 columns or rows and more: lds_cap 0) read global memory in every pass.
 constexpr int kStatTB = 512, kStatLds = 16384;   // 64 KB of cells
 __global__ __launch_bounds__(kStatTB) void k_cluster_stats(StatArgs A) {
+    constexpr int NW = kStatTB / 64;
     __shared__ unsigned cc[kStatLds];
-    __shared__ long long shl[2 * 16];
-    __shared__ int shi[16 * 16];
-    __shared__ double shd[3 * 16];
+    __shared__ long long s_l[6][NW];
+    __shared__ ArgMax s_m[2][NW];
+    __shared__ int s_i[NW];
     __shared__ int cand[2048];
     __shared__ int ncand;
-    const int cid = blockIdx.x, tid = threadIdx.x;
+    const int cid = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int b = A.off[cid], e = A.off[cid + 1], n = e - b;
     const GridC &g = A.g;
-    const int W = g.W;
+    const int W = g.W, H = g.H;
     const bool lds = n <= A.lds_cap;
     auto xy_at = [&](int k, int &x, int &y) {
         if (lds) {
@@ -334,8 +339,10 @@ __global__ __launch_bounds__(kStatTB) void k_cluster_stats(StatArgs A) {
             y = p / W; x = p - y * W;
         }
     };
+    auto key = [](int hi, int p) { return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)p); };
+    // ---- pass 1
     long long sx = 0, sy = 0;
-    int mnx = INT_MAX, mxx = INT_MIN, mny = INT_MAX, mxy = INT_MIN, first = INT_MAX;
+    long long kx0 = LLONG_MAX, kx1 = LLONG_MAX, ky0 = LLONG_MAX, ky1 = LLONG_MAX;
     for (int k0 = tid; k0 < n; k0 += 4 * kStatTB) {
         int pv[4];
 #pragma unroll
@@ -350,48 +357,58 @@ __global__ __launch_bounds__(kStatTB) void k_cluster_stats(StatArgs A) {
             const int y = p / W, x = p - y * W;
             if (lds) cc[k0 + u * kStatTB] = (unsigned)x | ((unsigned)y << 16);
             sx += x; sy += y;
-            mnx = min(mnx, x); mxx = max(mxx, x); mny = min(mny, y); mxy = max(mxy, y);
-            first = min(first, p);
+            kx0 = min(kx0, key(x, p)); kx1 = min(kx1, key(W - 1 - x, p));
+            ky0 = min(ky0, key(y, p)); ky1 = min(ky1, key(H - 1 - y, p));
         }
     }
-    {
-        long long l2[2] = {sx, sy};
-        block_reduce_k(l2, shl, AddOp(), AddOp());
-        sx = l2[0]; sy = l2[1];
-        int i5[5] = {mnx, mxx, mny, mxy, first};
-        block_reduce_k(i5, shi, MinOp(), MaxOp(), MinOp(), MaxOp(), MinOp());   // (its barrier also publishes cc)
-        mnx = i5[0]; mxx = i5[1]; mny = i5[2]; mxy = i5[3]; first = i5[4];
+    if (tid == 0) ncand = 0;
+    sx = wave_reduce(sx, 0ll, AddOp()); sy = wave_reduce(sy, 0ll, AddOp());
+    kx0 = wave_reduce(kx0, LLONG_MAX, MinOp()); kx1 = wave_reduce(kx1, LLONG_MAX, MinOp());
+    ky0 = wave_reduce(ky0, LLONG_MAX, MinOp()); ky1 = wave_reduce(ky1, LLONG_MAX, MinOp());
+    if (lane == 0) {
+        s_l[0][wid] = sx; s_l[1][wid] = sy; s_l[2][wid] = kx0; s_l[3][wid] = kx1; s_l[4][wid] = ky0; s_l[5][wid] = ky1;
     }
+    __syncthreads();   // (also publishes cc and ncand)
+    sx = s_l[0][0]; sy = s_l[1][0]; kx0 = s_l[2][0]; kx1 = s_l[3][0]; ky0 = s_l[4][0]; ky1 = s_l[5][0];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {
+        sx += s_l[0][w]; sy += s_l[1][w];
+        kx0 = min(kx0, s_l[2][w]); kx1 = min(kx1, s_l[3][w]); ky0 = min(ky0, s_l[4][w]); ky1 = min(ky1, s_l[5][w]);
+    }
+    const int mnx = (int)(kx0 >> 32), mxx = W - 1 - (int)(kx1 >> 32), mny = (int)(ky0 >> 32), mxy = H - 1 - (int)(ky1 >> 32);
+    const int first = (int)(unsigned)ky0;   // the smallest p has the smallest y
     // ---- max pairwise squared distance (cluster.length, seed_gen:1063-1073), pruned exactly:
     // LB = d^2 between the cells of extreme x / extreme y; a cell can belong to a farther pair only
     // if its distance to the farthest bbox corner reaches LB.
-    int ext[4] = {INT_MAX, INT_MAX, INT_MAX, INT_MAX};   // pixel ids with min/max x, min/max y
-    for (int k = tid; k < n; k += kStatTB) {
-        int x, y;
-        xy_at(k, x, y);
-        const int p = y * W + x;
-        if (x == mnx) ext[0] = min(ext[0], p);
-        if (x == mxx) ext[1] = min(ext[1], p);
-        if (y == mny) ext[2] = min(ext[2], p);
-        if (y == mxy) ext[3] = min(ext[3], p);
-    }
-    if (tid == 0) ncand = 0;
-    block_reduce_k(ext, shi + 5 * 16, MinOp(), MinOp(), MinOp(), MinOp());
     auto d2p = [&](int p, int q) {
         int py = p / W, px = p - py * W, qy = q / W, qx = q - qy * W;
         int dx = px - qx, dy = py - qy;
         return dx * dx + dy * dy;
     };
-    const int LB = max(d2p(ext[0], ext[1]), d2p(ext[2], ext[3]));
+    const int LB = max(d2p((int)(unsigned)kx0, (int)(unsigned)kx1), d2p((int)(unsigned)ky0, (int)(unsigned)ky1));
+    ClusterRec r{};
+    r.sx = sx; r.sy = sy; r.n = n;
+    r.bx0 = mnx; r.by0 = mny; r.bx1 = mxx; r.by1 = mxy; r.first = first;
+    r.cx = (float)sx / (float)n;       // sum_x / cells.size() (float / float)
+    r.cy = (float)sy / (float)n;
+    const float cwx = (float)(g.ox + (double)(r.cx * g.res)), cwy = (float)(g.oy + (double)(r.cy * g.res));
+    const double2 ctr = make_double2(cwx, cwy);
+    // ---- pass 2
+    ArgMax m1 = kArgMaxNone;   // |wp - centre|^2
     for (int k = tid; k < n; k += kStatTB) {
         int x, y;
         xy_at(k, x, y);
-        int dxm = max(x - mnx, mxx - x), dym = max(y - mny, mxy - y);
+        const int dxm = max(x - mnx, mxx - x), dym = max(y - mny, mxy - y);
         if (dxm * dxm + dym * dym >= LB) {
-            int s = atomicAdd(&ncand, 1);
+            const int s = atomicAdd(&ncand, 1);
             if (s < 2048) cand[s] = y * W + x;
         }
+        const double2 w = cell_wxy(g, x, y);
+        const double dx = w.x - ctr.x, dy = w.y - ctr.y;
+        m1.add(dx * dx + dy * dy, y * W + x);
     }
+    m1 = wave_reduce(m1, kArgMaxNone, ArgMaxOp());
+    if (lane == 0) s_m[0][wid] = m1;
     __syncthreads();
     int maxd2 = LB;
     const int nc = ncand;
@@ -402,106 +419,73 @@ __global__ __launch_bounds__(kStatTB) void k_cluster_stats(StatArgs A) {
         for (int i = b; i < e; ++i)
             for (int k = i + 1 + tid; k < e; k += kStatTB) maxd2 = max(maxd2, d2p(A.cells[i], A.cells[k]));
     }
-    {
-        int m[1] = {maxd2};
-        block_reduce_k(m, shi + 9 * 16, MaxOp());
-        maxd2 = m[0];
-    }
-
-    ClusterRec r{};
-    r.sx = sx; r.sy = sy; r.n = n; r.maxd2 = maxd2;
-    r.bx0 = mnx; r.by0 = mny; r.bx1 = mxx; r.by1 = mxy; r.first = first;
+    maxd2 = wave_reduce(maxd2, INT_MIN, MaxOp());
+    if (lane == 0) s_i[wid] = maxd2;
+    __syncthreads();
+    m1 = s_m[0][0];
+    maxd2 = s_i[0];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) { m1 = ArgMaxOp()(m1, s_m[0][w]); maxd2 = max(maxd2, s_i[w]); }
+    r.maxd2 = maxd2;
     r.flags = 0;
     const bool exact_sums = sx <= (1ll << 24) && sy <= (1ll << 24);
-    r.cx = (float)sx / (float)n;       // sum_x / cells.size() (float / float)
-    r.cy = (float)sy / (float)n;
     r.length = (float)(sqrt((double)maxd2) * (double)g.res);
     bool needs_bfs = !exact_sums;
     bool row = false;
     if (r.length >= A.min_length) {
-        float cwx = (float)(g.ox + (double)(r.cx * g.res)), cwy = (float)(g.oy + (double)(r.cy * g.res));
-        r.center = make_double2(cwx, cwy);
+        r.center = ctr;
         row = d_pip(cwx, cwy, A.poly, A.np);
     }
-    if (row && !needs_bfs) {
+    if (row && !needs_bfs) {   // (uniform over the block)
         // first endpoint: first cell with strictly maximal |wp - centre|^2 (seed_gen:1354-1367)
-        double m1[1] = {0.0};
-        for (int k = tid; k < n; k += kStatTB) {
-            int x, y;
-            xy_at(k, x, y);
-            double2 w = cell_wxy(g, x, y);
-            double dx = w.x - r.center.x, dy = w.y - r.center.y;
-            m1[0] = fmax(m1[0], dx * dx + dy * dy);
-        }
-        block_reduce_k(m1, shd, MaxOp());
-        int ca[2] = {0, INT_MAX};   // count, smallest cell of the maximum
-        for (int k = tid; k < n; k += kStatTB) {
-            int x, y;
-            xy_at(k, x, y);
-            double2 w = cell_wxy(g, x, y);
-            double dx = w.x - r.center.x, dy = w.y - r.center.y;
-            if (dx * dx + dy * dy == m1[0] && m1[0] > 0.0) { ++ca[0]; ca[1] = min(ca[1], y * W + x); }
-        }
-        block_reduce_k(ca, shi + 10 * 16, AddOp(), MinOp());
-        const int arg = ca[1];
-        if (ca[0] != 1) needs_bfs = true;
+        const int arg = m1.a;
+        if (!(m1.d > 0.0) || m1.c != 1) needs_bfs = true;
         if (!needs_bfs) {
             const double2 wf = cell_w(g, arg);
             double fdx = wf.x - r.center.x, fdy = wf.y - r.center.y;
             double z = fdx * fdx + fdy * fdy, s = sqrt(z);
             const double fx = fdx / s, fy = fdy / s;  // first_direction = diff.normalized()
-            // second endpoint: dot(normalized(diff), first_dir) < 0, strictly maximal (seed_gen:1369-1385)
-            double m2[1] = {0.0};
+            // ---- pass 3: second endpoint, dot(normalized(diff), first_dir) < 0, strictly maximal (seed_gen:1369-1385)
+            ArgMax m2 = kArgMaxNone;
             for (int k = tid; k < n; k += kStatTB) {
                 int x, y;
                 xy_at(k, x, y);
-                if (y * W + x == arg) continue;
-                double2 w = cell_wxy(g, x, y);
+                const int p = y * W + x;
+                if (p == arg) continue;
+                const double2 w = cell_wxy(g, x, y);
                 double dx = w.x - r.center.x, dy = w.y - r.center.y, d2 = dx * dx + dy * dy;
                 double nx = dx, ny = dy;
                 if (d2 > 0.0) { double q = sqrt(d2); nx = dx / q; ny = dy / q; }
-                if (nx * fx + ny * fy < 0.0) m2[0] = fmax(m2[0], d2);
+                if (nx * fx + ny * fy < 0.0) m2.add(d2, p);
             }
-            block_reduce_k(m2, shd + 16, MaxOp());
-            int ca2[2] = {0, INT_MAX};
-            const bool fallback = !(m2[0] > 0.0);
-            if (!fallback) {
+            m2 = wave_reduce(m2, kArgMaxNone, ArgMaxOp());
+            if (lane == 0) s_m[1][wid] = m2;
+            __syncthreads();
+            m2 = s_m[1][0];
+#pragma unroll
+            for (int w = 1; w < NW; ++w) m2 = ArgMaxOp()(m2, s_m[1][w]);
+            if (!(m2.d > 0.0)) {  // farthest from the first endpoint (seed_gen:1387-1399)
+                __syncthreads();   // (s_m[1] is read above and written again below)
+                m2 = kArgMaxNone;
                 for (int k = tid; k < n; k += kStatTB) {
                     int x, y;
                     xy_at(k, x, y);
                     const int p = y * W + x;
                     if (p == arg) continue;
-                    double2 w = cell_wxy(g, x, y);
-                    double dx = w.x - r.center.x, dy = w.y - r.center.y, d2 = dx * dx + dy * dy;
-                    double nx = dx, ny = dy;
-                    if (d2 > 0.0) { double q = sqrt(d2); nx = dx / q; ny = dy / q; }
-                    if (nx * fx + ny * fy < 0.0 && d2 == m2[0]) { ++ca2[0]; ca2[1] = min(ca2[1], p); }
-                }
-            } else {  // farthest from the first endpoint (seed_gen:1387-1399)
-                double m3[1] = {0.0};
-                for (int k = tid; k < n; k += kStatTB) {
-                    int x, y;
-                    xy_at(k, x, y);
-                    if (y * W + x == arg) continue;
-                    double2 w = cell_wxy(g, x, y);
+                    const double2 w = cell_wxy(g, x, y);
                     double dx = w.x - wf.x, dy = w.y - wf.y;
-                    m3[0] = fmax(m3[0], dx * dx + dy * dy);
+                    m2.add(dx * dx + dy * dy, p);
                 }
-                block_reduce_k(m3, shd + 32, MaxOp());
-                for (int k = tid; k < n; k += kStatTB) {
-                    int x, y;
-                    xy_at(k, x, y);
-                    const int p = y * W + x;
-                    if (p == arg) continue;
-                    double2 w = cell_wxy(g, x, y);
-                    double dx = w.x - wf.x, dy = w.y - wf.y;
-                    if (dx * dx + dy * dy == m3[0] && m3[0] > 0.0) { ++ca2[0]; ca2[1] = min(ca2[1], p); }
-                }
+                m2 = wave_reduce(m2, kArgMaxNone, ArgMaxOp());
+                if (lane == 0) s_m[1][wid] = m2;
+                __syncthreads();
+                m2 = s_m[1][0];
+#pragma unroll
+                for (int w = 1; w < NW; ++w) m2 = ArgMaxOp()(m2, s_m[1][w]);
             }
-            block_reduce_k(ca2, shi + 12 * 16, AddOp(), MinOp());
-            if (ca2[0] != 1) needs_bfs = true;  // (fallback with max 0 keeps index 0 -> BFS replay)
+            if (!(m2.d > 0.0) || m2.c != 1) needs_bfs = true;  // (fallback with max 0 keeps index 0 -> BFS replay)
             r.start = wf;
-            if (!needs_bfs) r.end = cell_w(g, ca2[1]);
+            if (!needs_bfs) r.end = cell_w(g, m2.a);
         }
     }
     r.flags = (row ? 1 : 0) | (needs_bfs ? 2 : 0);
