@@ -112,7 +112,8 @@ static int ccl_edge_cap(int nf) {
     const char *e = getenv("AOS_DEBUG_CCL_ECAP");
     return e ? std::max(2, atoi(e)) : std::max(4096, nf / 4);
 }
-constexpr int kCclBatch = 4;   // k_ccl_local: cells per thread whose neighbour lookups are in flight together
+constexpr int kCclBatch = 2;        // k_ccl_local: cells per thread whose neighbour lookups are in flight together
+constexpr int kCclEdgeLds = 1024;   // k_ccl_local: cross-chunk links gathered per block before the global append
 // Root of x with path halving: x is pointed at its grandparent as the walk passes (a parent always has the
 // smaller index, so the grandparent is an ancestor and no cycle can form; a root is never written: only entries
 // already read as non-roots are). The chunk's unions arrive in no particular order along the skeleton's lines,
@@ -138,27 +139,81 @@ __device__ __forceinline__ void lds_union(int *lp, int i, int j) {
         b = lds_find(lp, b);
     }
 }
+struct IMaxOp { __device__ int operator()(int a, int b) const { return a > b ? a : b; } };
+// Horizontal runs are labelled before any union (round 6): lp[i] = the first cell of i's run of x-adjacent cells inside
+// the chunk, by a max-scan of the run starts (each thread a contiguous segment; DPP wave scan, one barrier). The orchard
+// skeleton is long horizontal lines, and linking each cell to its left neighbour by concurrent unions built chains as
+// long as the runs (hundreds of cells) that the finds then walked with path halving: C2 50 us, C3 161 us per frame
+// (profiles/r06/r06z_kt*_summary.txt). A run's start is its smallest index, so the forest keeps the invariant of the
+// unions (a parent has the smaller index) and every component's root is still its smallest cell: the labels are
+// unchanged. Only the three upper links go through lookups and unions; a chunk's first cell links left into the
+// previous chunk through the cross-edge list, as before. The cross-chunk links (a line's cells link up into the same
+// line's previous grid row, ~10^4 links at C3) gather in LDS and reach the global list with one atomic per block: one
+// global atomic per link on the one counter had serialised the launch (in-kernel s_memrealtime stamps per block: C3
+// blocks waited up to 100 us in their first phase behind it). With batches of 2 cells (42 VGPRs, two 1024-thread
+// blocks per CU): C2 50 -> 13 us, C3 161 -> 23 us per frame; chunks of 4096 or 512-thread blocks were slower at C2.
 __global__ __launch_bounds__(1024) void k_ccl_local(const int *list, int n, const uint64_t *fg, const int *off, GridC g,
                                                     int *parent, int2 *edges, int *n_edges, int cap, int chunk) {
     extern __shared__ int lp[];   // [chunk]
-    const int base = blockIdx.x * chunk, m = min(chunk, n - base), nt = blockDim.x;
-    for (int i = threadIdx.x; i < m; i += nt) lp[i] = i;
+    __shared__ int wmax[16];
+    __shared__ int2 s_edge[kCclEdgeLds];
+    __shared__ int s_ne, s_ebase;
+    const int base = blockIdx.x * chunk, m = min(chunk, n - base), nt = blockDim.x, tid = threadIdx.x;
+    {
+        const int S = (m + nt - 1) / nt, s0 = tid * S;
+        int run = -1;
+        for (int k = 0; k < S; ++k) {
+            const int i = s0 + k;
+            if (i >= m) break;
+            const int p = list[base + i];
+            const bool start = i == 0 || p % g.W == 0 || list[base + i - 1] != p - 1;
+            if (start) run = i;
+            lp[i] = run;
+        }
+        const int before = wave_scan_excl(run, -1, IMaxOp());
+        if ((tid & 63) == 63) wmax[tid >> 6] = max(before, run);
+        __syncthreads();
+        int carry = before;
+        for (int w = 0; w < (tid >> 6); ++w) carry = max(carry, wmax[w]);
+        for (int k = 0; k < S; ++k) {
+            const int i = s0 + k;
+            if (i >= m) break;
+            if (lp[i] < 0) lp[i] = carry;   // (cell 0 starts a run: carry >= 0 here)
+        }
+        if (tid == 0) s_ne = 0;
+    }
     __syncthreads();
-    const int ndx[4] = {-1, 0, 1, -1}, ndy[4] = {-1, -1, -1, 0};
-    // kCclBatch cells per thread at a time, their 4 x kCclBatch neighbour lookups issued together (the fg words,
+    // The cross-chunk links gather in LDS and go to the global list with one atomic per block (round 6: one global
+    // atomic per link on one counter serialised the C3 launch, ~10^4 links)
+    auto cross = [&](int a, int b) {
+        const int e = atomicAdd(&s_ne, 1);
+        if (e < kCclEdgeLds) {
+            s_edge[e] = make_int2(a, b);
+        } else {
+            const int ge = atomicAdd(n_edges, 1);
+            if (ge < cap) edges[ge] = make_int2(a, b);
+        }
+    };
+    if (tid == 0 && base > 0) {   // the chunk's first cell and its left neighbour in the previous chunk
+        const int p = list[base];
+        if (p % g.W != 0 && list[base - 1] == p - 1) cross(base, base - 1);
+    }
+    const int ndx[3] = {-1, 0, 1};   // (the row above: raster predecessors, their indices < base + i)
+    // kCclBatch cells per thread at a time, their 3 x kCclBatch neighbour lookups issued together (the fg words,
     // then the offsets of the set bits) before any union: round 4 walked each cell's lookups as a chain of
     // dependent global load pairs between LDS unions, so the kernel waited on load latency cell after cell
     constexpr int B = kCclBatch;
-    for (int i0 = threadIdx.x; i0 < m; i0 += B * nt) {
-        int wi[B][4], bit[B][4], jj[B][4];
-        uint64_t w[B][4];
+    const int S = (m + nt - 1) / nt, s0 = tid * S, s1 = min(s0 + S, m);   // (the segment of the run scan)
+    for (int i0 = s0; i0 < s1; i0 += B) {
+        int wi[B][3], bit[B][3], jj[B][3];
+        uint64_t w[B][3];
 #pragma unroll
         for (int b = 0; b < B; ++b) {
-            const int i = i0 + b * nt;
+            const int i = i0 + b < s1 ? i0 + b : m;
             const int p = i < m ? list[base + i] : 0, y = p / g.W, x = p - y * g.W;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int nx = x + ndx[k], ny = y + ndy[k];   // (a raster predecessor: its index is < base + i)
+            for (int k = 0; k < 3; ++k) {
+                const int nx = x + ndx[k], ny = y - 1;
                 const bool ok = i < m && nx >= 0 && ny >= 0 && nx < g.W;
                 wi[b][k] = ok ? ny * g.WW + (nx >> 6) : 0;
                 bit[b][k] = nx & 63;
@@ -168,28 +223,29 @@ __global__ __launch_bounds__(1024) void k_ccl_local(const int *list, int n, cons
 #pragma unroll
         for (int b = 0; b < B; ++b)
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < 3; ++k) {
                 const uint64_t v = w[b][k];
                 jj[b][k] = ((v >> bit[b][k]) & 1ull) ? off[wi[b][k]] + __popcll(v & ((1ull << bit[b][k]) - 1)) : -1;
             }
 #pragma unroll
         for (int b = 0; b < B; ++b) {
-            const int i = i0 + b * nt;
+            const int i = i0 + b;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < 3; ++k) {
                 const int j = jj[b][k];
                 if (j < 0) continue;
-                if (j >= base) {
-                    lds_union(lp, i, j - base);
-                } else {
-                    const int e = atomicAdd(n_edges, 1);
-                    if (e < cap) edges[e] = make_int2(base + i, j);
-                }
+                if (j >= base) lds_union(lp, i, j - base);
+                else cross(base + i, j);
             }
         }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < m; i += nt) parent[base + i] = base + lds_find(lp, i);
+    const int nl = min(s_ne, kCclEdgeLds);
+    if (tid == 0 && nl) s_ebase = atomicAdd(n_edges, nl);
+    for (int i = tid; i < m; i += nt) parent[base + i] = base + lds_find(lp, i);
+    __syncthreads();
+    for (int k = tid; k < nl; k += nt)
+        if (s_ebase + k < cap) edges[s_ebase + k] = s_edge[k];
 }
 // The cross-chunk links, unioned globally; when the list overflowed (never at C1-C4) every link of every cell
 // again instead (the fallback, in the same launch: round 4's separate k_ccl_union_if returned at once in

@@ -59,4 +59,20 @@ __device__ __forceinline__ T wave_reduce(T v, T id, Op op) {
     return lane63(v);
 }
 
+// The wave's inclusive scan of v under op (lane i: v_0 op ... op v_i), and the exclusive one (lane 0: id).
+template <class T, class Op>
+__device__ __forceinline__ T wave_scan_incl(T v, T id, Op op) {
+    v = op(v, dpp_move<0x111, 0xf>(id, v));   // row_shr:1, 2, 4, 8: inclusive inside each row of 16 lanes
+    v = op(v, dpp_move<0x112, 0xf>(id, v));
+    v = op(v, dpp_move<0x114, 0xf>(id, v));
+    v = op(v, dpp_move<0x118, 0xf>(id, v));
+    v = op(v, dpp_move<0x142, 0xa>(id, v));   // row_bcast:15: row 0's total into row 1, row 2's into row 3
+    v = op(v, dpp_move<0x143, 0xc>(id, v));   // row_bcast:31: rows 0-1's total into rows 2 and 3
+    return v;
+}
+template <class T, class Op>
+__device__ __forceinline__ T wave_scan_excl(T v, T id, Op op) {
+    return dpp_move<0x138, 0xf>(id, wave_scan_incl(v, id, op));   // wave_shr:1
+}
+
 }  // namespace aos

@@ -25,6 +25,7 @@
 
 #include "cluster_seed.h"
 #include "dev_prims_device.h"
+#include "dev_wave.h"
 
 namespace aos {
 
@@ -228,14 +229,37 @@ void scan_1p(LookBackScratch &lb, int *in, int *out, int n, bool zero_in, hipStr
 }
 
 // ------------------------------------------------------------------ cell index (counting sort)
-__global__ void k_ci_count(const double2 *p, const int *ok, int n, const int *n_dev, HashG h, int *cnt, int *rank) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    if ((ok && !ok[i]) || (n_dev && i >= *n_dev)) { rank[i] = -1; return; }
-    int cx, cy;
-    hash_cell(h, p[i].x, p[i].y, cx, cy);
-    const int b = cy * h.nx + cx;
-    rank[i] = atomicAdd(&cnt[b], 1);
+// One atomic per run of equal buckets in a wave (round 6): the points arrive in spatial order (raster-ordered lists,
+// rows of seeds), so a wave's lanes mostly share a few buckets and per-lane atomics on one counter were serialised:
+// k_ci_count took 10.1 us per launch against k_ci_scatter's 5.1 at C2 and 24.8 against 6.5 at C3 (6 launches per
+// frame, profiles/r06/r06za_kt*_summary.txt). A run's head (its bucket differs from the lane before, DPP wave_shr:1)
+// adds the run's length and each lane takes head's base + its offset in the run: the ranks inside a bucket stay a
+// permutation of 0 .. count - 1 (their order was the atomics' order before, too).
+__global__ __launch_bounds__(256) void k_ci_count(const double2 *p, const int *ok, int n, const int *n_dev, HashG h,
+                                                  int *cnt, int *rank) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x, lane = threadIdx.x & 63;
+    int b = -1;   // (no bucket: past n, or not a point)
+    if (i < n) {
+        if ((ok && !ok[i]) || (n_dev && i >= *n_dev)) {
+            rank[i] = -1;
+        } else {
+            int cx, cy;
+            hash_cell(h, p[i].x, p[i].y, cx, cy);
+            b = cy * h.nx + cx;
+        }
+    }
+    const int prev = dpp_i32<0x138>(INT_MIN, b);   // wave_shr:1 (lane 0: INT_MIN)
+    const unsigned long long heads = __ballot(b != prev);
+    const unsigned long long upto = lane == 63 ? ~0ull : (2ull << lane) - 1;
+    const int hl = 63 - __clzll((long long)(heads & upto));   // this lane's run head
+    int base = 0;
+    if (lane == hl && b >= 0) {
+        const unsigned long long after = heads & ~upto;
+        const int next = after ? __ffsll((long long)after) - 1 : 64;
+        base = atomicAdd(&cnt[b], next - lane);
+    }
+    base = __shfl(base, hl);
+    if (b >= 0) rank[i] = base + lane - hl;
 }
 __global__ void k_ci_scatter(const double2 *p, const int *rank, int n, HashG h, const int *start, int *items) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
