@@ -109,14 +109,20 @@ __device__ __forceinline__ uint64_t grid_extra(int x0, int y, int W, int H, int 
     return m;
 }
 
+// The word-per-thread grid kernels run in blocks of 64 words x kRowBlk rows (round 6; one-row blocks before: k_open
+// 8.1-9.7 -> 6.6-8.1 us per C2 launch, k_inflate and k_bits_to_bytes unchanged, profiles/r06/r06zd_kt_summary.txt)
+constexpr int kRowBlk = 4;
+static const dim3 kRowBlock(64, kRowBlk);
+static dim3 row_grid(int WW, int H) { return dim3(cdiv(WW, 64), cdiv(H, kRowBlk)); }
+
 // a5 applyInflation (seed_gen:933-967): cell = 100 iff an occupied raster cell lies within the
 // integer disc dx^2 + dy^2 <= R^2 — an exact bounded squared-EDT threshold, computed as an OR
 // of horizontally dilated rows: row y+dy dilated by w(dy) = floor(sqrt(R^2 - dy^2)).
 struct InflTab { int w[64]; };   // w(dy), passed by value: concurrent handles share no device global
 // (bytes != nullptr: also /occupancy_grid's bytes with the `frame` border, from the word in registers)
-__global__ void k_inflate(const uint64_t *in, uint64_t *out, int W, int H, int WW, int R, InflTab wt, int8_t *bytes,
-                          int frame) {
-    int c = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+__global__ __launch_bounds__(64 * kRowBlk) void k_inflate(const uint64_t *in, uint64_t *out, int W, int H, int WW, int R,
+                                                         InflTab wt, int8_t *bytes, int frame) {
+    int c = blockIdx.x * 64 + threadIdx.x, y = blockIdx.y * kRowBlk + threadIdx.y;
     if (c >= WW || y >= H) return;
     uint64_t acc = 0;
     for (int dy = -R; dy <= R; ++dy) {
@@ -144,13 +150,13 @@ void launch_inflate(const uint64_t *in, uint64_t *out, const FrameGeom &g, hipSt
         while ((w + 1) * (w + 1) + dy * dy <= g.R * g.R) ++w;
         wt.w[dy] = w;
     }
-    dim3 grid(cdiv(g.WW, 64), g.H);
-    k_inflate<<<grid, 64, 0, s>>>(in, out, g.W, g.H, g.WW, g.R, wt, bytes, frame);
+    k_inflate<<<row_grid(g.WW, g.H), kRowBlock, 0, s>>>(in, out, g.W, g.H, g.WW, g.R, wt, bytes, frame);
 }
 
 // bits -> int8 {0,100} with the optional frame border and rectangle (grid_extra)
-__global__ void k_bits_to_bytes(const uint64_t *bits, int8_t *out, int W, int H, int WW, int frame, ByteRect r) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+__global__ __launch_bounds__(64 * kRowBlk) void k_bits_to_bytes(const uint64_t *bits, int8_t *out, int W, int H, int WW,
+                                                               int frame, ByteRect r) {
+    const int c = blockIdx.x * 64 + threadIdx.x, y = blockIdx.y * kRowBlk + threadIdx.y;
     if (c >= WW || y >= H) return;
     const uint64_t v = bits[(size_t)y * WW + c] | grid_extra(64 * c, y, W, H, frame, r);
     store_word_bytes(out + (size_t)y * W + 64 * c, v, min(64, W - 64 * c), (W & 15) == 0);
@@ -158,8 +164,7 @@ __global__ void k_bits_to_bytes(const uint64_t *bits, int8_t *out, int W, int H,
 void launch_bits_to_bytes(const uint64_t *bits, int8_t *out, const FrameGeom &g, int frame, hipStream_t s, const int *rect) {
     if (reinterpret_cast<uintptr_t>(out) & 15) throw std::logic_error("launch_bits_to_bytes: output not 16-byte aligned");
     const ByteRect r = rect ? ByteRect{rect[0], rect[1], rect[2], rect[3]} : ByteRect{-1, 0, 0, 0};
-    dim3 grid(cdiv(g.WW, 64), g.H);
-    k_bits_to_bytes<<<grid, 64, 0, s>>>(bits, out, g.W, g.H, g.WW, frame, r);
+    k_bits_to_bytes<<<row_grid(g.WW, g.H), kRowBlock, 0, s>>>(bits, out, g.W, g.H, g.WW, frame, r);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -177,10 +182,11 @@ __device__ __forceinline__ uint64_t erode_at(const uint64_t *in, int r, int k, i
     return (c & wv & ev & ld_er(in, r - 1, k, H, WW, W) & ld_er(in, r + 1, k, H, WW, W)) & pad_mask(k, WW, W);
 }
 // (zero != nullptr: the thinning flags zero[0, nzero) are cleared by the blocks of row 0: no fill launch)
-__global__ void k_open(const uint64_t *in, uint64_t *out, int W, int H, int WW, int *zero, int nzero) {
-    int k = blockIdx.x * blockDim.x + threadIdx.x, r = blockIdx.y;
+__global__ __launch_bounds__(64 * kRowBlk) void k_open(const uint64_t *in, uint64_t *out, int W, int H, int WW, int *zero,
+                                                      int nzero) {
+    int k = blockIdx.x * 64 + threadIdx.x, r = blockIdx.y * kRowBlk + threadIdx.y;
     if (zero && r == 0)
-        for (int i = k; i < nzero; i += gridDim.x * blockDim.x) zero[i] = 0;
+        for (int i = k; i < nzero; i += gridDim.x * 64) zero[i] = 0;
     if (k >= WW || r >= H) return;
     uint64_t e = erode_at(in, r, k, H, WW, W);
     uint64_t d = e | erode_at(in, r - 1, k, H, WW, W) | erode_at(in, r + 1, k, H, WW, W) |
@@ -188,8 +194,7 @@ __global__ void k_open(const uint64_t *in, uint64_t *out, int W, int H, int WW, 
     out[(size_t)r * WW + k] = d & pad_mask(k, WW, W);
 }
 void launch_open(const uint64_t *in, uint64_t *out, const FrameGeom &g, hipStream_t s, int *zero, int nzero) {
-    dim3 grid(cdiv(g.WW, 64), g.H);
-    k_open<<<grid, 64, 0, s>>>(in, out, g.W, g.H, g.WW, zero, nzero);
+    k_open<<<row_grid(g.WW, g.H), kRowBlock, 0, s>>>(in, out, g.W, g.H, g.WW, zero, nzero);
 }
 
 // ------------------------------------------------------------------------------------------
