@@ -56,13 +56,19 @@ __global__ void k_dist_fg(const uint64_t *win, TileView T, GridC g, const double
     const bool rowwise = row_crossings(poly, np, wy, xc, &nxc);   // (block-uniform; synchronises)
     if (k >= T.nc || r >= T.nr) return;
     uint64_t w = win[(size_t)(T.oy + r) * T.WWl + T.oc + k], o = 0;
-    while (w) {
-        const int b = __ffsll((long long)w) - 1;
-        w &= w - 1;
-        const int gx = 64 * (T.c0 + k) + b;
-        if (gx >= g.W) continue;
-        const double wx = cell_world(g.ox, gx, g.res);
-        if (rowwise ? pip_row(wx, xc, nxc) : d_pip(wx, wy, poly, np)) o |= 1ull << b;
+    const int x0 = 64 * (T.c0 + k);
+    if (rowwise && __popcll(w) >= kPipWordMin) {
+        const uint64_t valid = g.W - x0 >= 64 ? ~0ull : (1ull << (g.W - x0)) - 1;   // (cells gx < W)
+        o = w & valid & pip_row_word(g.ox, g.res, x0, xc, nxc);
+    } else {
+        while (w) {
+            const int b = __ffsll((long long)w) - 1;
+            w &= w - 1;
+            const int gx = x0 + b;
+            if (gx >= g.W) continue;
+            const double wx = cell_world(g.ox, gx, g.res);
+            if (rowwise ? pip_row(wx, xc, nxc) : d_pip(wx, wy, poly, np)) o |= 1ull << b;
+        }
     }
     fg[(size_t)r * T.nc + k] = o;
     cnt[(size_t)r * T.nc + k] = __popcll(o);

@@ -43,12 +43,16 @@ __global__ void k_fg(const uint64_t *skel, uint64_t *fg, int *cnt, GridC g, cons
     if (c >= g.WW || y >= g.H) return;
     size_t wi = (size_t)y * g.WW + c;
     uint64_t w = skel[wi], o = 0;
-    while (w) {
-        int b = __ffsll((long long)w) - 1;
-        w &= w - 1;
-        int x = c * 64 + b;
-        const double wx = cell_world(g.ox, x, g.res);
-        if (rowwise ? pip_row(wx, xc, nxc) : d_pip(wx, wy, poly, np)) o |= 1ull << b;
+    if (rowwise && __popcll(w) >= kPipWordMin) {
+        o = w & pip_row_word(g.ox, g.res, c * 64, xc, nxc);
+    } else {
+        while (w) {
+            int b = __ffsll((long long)w) - 1;
+            w &= w - 1;
+            int x = c * 64 + b;
+            const double wx = cell_world(g.ox, x, g.res);
+            if (rowwise ? pip_row(wx, xc, nxc) : d_pip(wx, wy, poly, np)) o |= 1ull << b;
+        }
     }
     fg[wi] = o;
     cnt[wi] = __popcll(o);
