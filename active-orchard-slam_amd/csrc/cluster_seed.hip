@@ -673,33 +673,50 @@ __global__ __launch_bounds__(64) void k_endpoint_rays(const RowDev *rows, int n_
     { double z = rx * rx + ry * ry; if (z > 0.0) { double q = sqrt(z); rx = rx / q; ry = ry / q; } }
     double resx = 0, resy = 0;
     bool done = false;
-    for (int base = 0; base < n_tab; base += 64) {
-        const int i = base + lane;
-        const double cur = cur_tab[i < n_tab ? i : n_tab - 1];
-        const bool valid = i < n_tab && cur <= g.amax;
-        const double px = stx + rx * cur, py = sty + ry * cur;
-        const bool ins = px >= g.minx && px <= g.maxx && py >= g.miny && py <= g.maxy;
-        bool inr = false;
-        int mx = 0, my = 0;
-        if (ins) {
-            mx = (int)((px - g.ox) / (double)g.res); my = (int)((py - g.oy) / (double)g.res);
-            inr = mx >= 0 && mx < g.W && my >= 0 && my < g.H;
-        }
-        const int cx = inr ? mx : 0, cy = inr ? my : 0;
-        const uint64_t w = skel[(size_t)cy * g.WW + (cx >> 6)];
-        const bool occ = inr && ((w >> (cx & 63)) & 1ull);
-        const bool ev = !valid || !ins || occ;
-        const unsigned long long m = __ballot(ev);
-        if (m) {
-            const int j = __ffsll((long long)m) - 1;
-            const double qx = __shfl(px, j), qy = __shfl(py, j);
-            const bool qvalid = __shfl((int)valid, j), qins = __shfl((int)ins, j);
-            if (qvalid) {
-                done = true;
-                if (!qins) { resx = fmax(g.minx, fmin(g.maxx, qx)); resy = fmax(g.miny, fmin(g.maxy, qy)); }
-                else { resx = qx; resy = qy; }
+    // kRayBatch groups of 64 steps per trip, their skeleton loads in flight together, then the groups' events in step
+    // order (round 6: one group per trip waited for one load per 64 steps; rays that cross the map run ~100 groups)
+    // (C2 41 -> 31 us, C3 87 -> 74 us, profiles/r06/r06zi_kt*_summary.txt; 16 groups were slower, 188 VGPRs and more steps
+    // past the event, r06zj; the divisions through the reciprocal changed nothing, r06zk)
+    constexpr int kRayBatch = 4;
+    for (int base = 0; base < n_tab && !done; base += 64 * kRayBatch) {
+        double px[kRayBatch], py[kRayBatch];
+        bool valid[kRayBatch], ins[kRayBatch], occ[kRayBatch];
+        uint64_t w[kRayBatch];
+        int cx[kRayBatch];
+#pragma unroll
+        for (int u = 0; u < kRayBatch; ++u) {
+            const int i = base + 64 * u + lane;
+            const double cur = cur_tab[i < n_tab ? i : n_tab - 1];
+            valid[u] = i < n_tab && cur <= g.amax;
+            px[u] = stx + rx * cur; py[u] = sty + ry * cur;
+            ins[u] = px[u] >= g.minx && px[u] <= g.maxx && py[u] >= g.miny && py[u] <= g.maxy;
+            bool inr = false;
+            int mx = 0, my = 0;
+            if (ins[u]) {
+                mx = (int)((px[u] - g.ox) / (double)g.res); my = (int)((py[u] - g.oy) / (double)g.res);
+                inr = mx >= 0 && mx < g.W && my >= 0 && my < g.H;
             }
-            break;
+            cx[u] = inr ? mx : -1;
+            const int cy = inr ? my : 0;
+            w[u] = skel[(size_t)cy * g.WW + ((inr ? mx : 0) >> 6)];
+        }
+#pragma unroll
+        for (int u = 0; u < kRayBatch; ++u) {
+            occ[u] = cx[u] >= 0 && ((w[u] >> (cx[u] & 63)) & 1ull);
+            const bool ev = !valid[u] || !ins[u] || occ[u];
+            const unsigned long long m = __ballot(ev);
+            if (m) {
+                const int j = __ffsll((long long)m) - 1;
+                const double qx = __shfl(px[u], j), qy = __shfl(py[u], j);
+                const bool qvalid = __shfl((int)valid[u], j), qins = __shfl((int)ins[u], j);
+                if (qvalid) {
+                    done = true;
+                    if (!qins) { resx = fmax(g.minx, fmin(g.maxx, qx)); resy = fmax(g.miny, fmin(g.maxy, qy)); }
+                    else { resx = qx; resy = qy; }
+                }
+                base = n_tab;   // (the walk ends at the first event, found or not)
+                break;
+            }
         }
     }
     if (!done) {
