@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include "dev_prims.h"
+#include "dev_wave.h"
 
 namespace aos {
 
@@ -64,10 +65,9 @@ __device__ __forceinline__ int lb_block_id(const LookBack &L, int *sh) {
     return *sh;
 }
 
-__device__ __forceinline__ unsigned wave_sum_u32(unsigned v) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
+struct IAdd { __device__ int operator()(int a, int b) const { return a + b; } };
+// (DPP row moves, dev_wave.h: the look-back's sums sit on the scans' critical path)
+__device__ __forceinline__ unsigned wave_sum_u32(unsigned v) { return (unsigned)wave_reduce((int)v, 0, IAdd()); }
 
 // Wave 0 of block vid (all 64 lanes): publishes the block's aggregate, walks back over the
 // predecessors' words 64 at a time, publishes the inclusive prefix; returns the exclusive prefix. A wait
@@ -120,12 +120,7 @@ __device__ inline unsigned lb_exclusive(const LookBack &L, int vid, unsigned agg
 template <int NT>
 __device__ __forceinline__ int block_excl_scan(int v, int *wsum, int *tot) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int incl = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int t = __shfl_up(incl, o);
-        if (lane >= o) incl += t;
-    }
+    const int incl = wave_scan_incl(v, 0, IAdd());
     if (lane == 63) wsum[w] = incl;
     __syncthreads();
     int before = 0, all = 0;

@@ -134,12 +134,7 @@ __device__ __forceinline__ int block_excl_scan_q(const int (&run)[NQ], int (&bef
     int incl[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-        incl[q] = run[q];
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int t = __shfl_up(incl[q], o);
-            if (lane >= o) incl[q] += t;
-        }
+        incl[q] = wave_scan_incl(run[q], 0, IAdd());   // (DPP row moves, dev_wave.h)
         if (lane == 63) wt[q * NW + w] = incl[q];
     }
     __syncthreads();
