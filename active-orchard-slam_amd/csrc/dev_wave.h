@@ -47,6 +47,9 @@ __device__ __forceinline__ long long lane63(long long v) { return lane63_i64(v);
 __device__ __forceinline__ double lane63(double v) { return lane63_f64(v); }
 template <class T> __device__ __forceinline__ T lane63(const T &v) { return v.lane63(); }
 
+struct WAdd { template <class T> __device__ T operator()(T a, T b) const { return a + b; } };
+struct WMax { template <class T> __device__ T operator()(T a, T b) const { return a > b ? a : b; } };
+
 // The wave's reduction of v under op (associative and commutative, id its identity), the same value in every lane.
 template <class T, class Op>
 __device__ __forceinline__ T wave_reduce(T v, T id, Op op) {

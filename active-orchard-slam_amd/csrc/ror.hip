@@ -278,7 +278,7 @@ __global__ __launch_bounds__(kRtTB) void k_rt_part(RorLaunch L, int *H, const in
         for (int t = tid; t < L.ntiles; t += kRtTB) row[t] = hist[t];
         // the workgroup's binned points: one plain store (k_rt_colscan sums them; round 3's per-wave global
         // atomic on one counter cost the pass ~17 us, tools/rorbench)
-        for (int o = 32; o > 0; o >>= 1) own += __shfl_xor(own, o);
+        own = (unsigned)wave_reduce((int)own, 0, WAdd());
         __shared__ unsigned own_w[kRtTB / 64];
         if ((tid & 63) == 0) own_w[tid >> 6] = own;
         __syncthreads();
@@ -361,7 +361,7 @@ __global__ __launch_bounds__(kColTB) void k_rt_colscan(ColScan C) {
     if (vid == 0) {   // the binned count: the count workgroups' own sums (no global atomic in the count pass)
         unsigned long long o = 0;
         for (int k = tid; k < C.G; k += kColTB) o += C.own[k];
-        for (int k = 32; k > 0; k >>= 1) o += __shfl_xor(o, k);
+        o = (unsigned long long)wave_reduce((long long)o, 0ll, WAdd());
         if ((tid & 63) == 0) sh_own[tid >> 6] = o;
         __syncthreads();
         if (tid == 0) {
@@ -375,7 +375,7 @@ __global__ __launch_bounds__(kColTB) void k_rt_colscan(ColScan C) {
     const int local = block_excl_scan<kColTB>(live ? run : 0, wsum, &sh_tot);
     {   // the largest tile (a frame that cannot be redone skips the big-tile kernels when it fits the LDS cap)
         int mx = live ? run : 0;
-        for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+        mx = wave_reduce(mx, 0, WMax());
         if ((tid & 63) == 0 && mx > 0) atomicMax(C.n_own + 2, (unsigned long long)mx);
     }
     if (tid < 64) {
@@ -723,12 +723,7 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
             v[j] = b <= nlb ? bstart[b] : 0;
             run += v[j];
         }
-        int incl = run;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int t = __shfl_up(incl, o);
-            if ((tid & 63) >= o) incl += t;
-        }
+        const int incl = wave_scan_incl(run, 0, WAdd());
         if ((tid & 63) == 63) wsum[tid >> 6] = incl;
         __syncthreads();
         int before = incl - run;
@@ -909,7 +904,7 @@ __global__ __launch_bounds__(kRorThreads) void k_rt_ror(RorLaunch L, const int *
             if (r >= 0 && r < L.Hr && w >= 0 && w < L.WWr)
                 atomicOr(reinterpret_cast<unsigned long long *>(&rbits[(size_t)r * L.WWr + w]), v);
         }
-    for (int o = 32; o > 0; o >>= 1) kept_n += __shfl_xor(kept_n, o);
+    kept_n = (unsigned)wave_reduce((int)kept_n, 0, WAdd());
     if ((tid & 63) == 0 && kept_n) {
         atomicAdd(&counters[(blockIdx.x * (kRorThreads / 64) + (tid >> 6)) & (kRorCounters - 1)],
                   (unsigned long long)kept_n);
@@ -953,7 +948,7 @@ __global__ __launch_bounds__(1024) void k_rt_sum_kept(const int *kept_tile, int 
     unsigned long long v = 0;
     for (int t = threadIdx.x; t < ntiles; t += 1024) v += (unsigned)kept_tile[t];
     if (threadIdx.x > 0 && threadIdx.x < kRorCounters) counters[threadIdx.x] = 0;   // (pass 4's partial adds)
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    v = (unsigned long long)wave_reduce((long long)v, 0ll, WAdd());
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
     __syncthreads();
     if (threadIdx.x == 0) {
