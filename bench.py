@@ -53,7 +53,7 @@ PMC_FILES = {("C2", "r02"): os.path.join(ROOT, "profiles", "r02q_pmc_traffic.jso
              ("C3", "r06"): os.path.join(ROOT, "profiles", "r06", "r06o_c3_pmc_traffic.json")}
 # rocprofv3 --kernel-trace --stats summaries (tools/kt_summary.py) of the sequential loop at this build: the median
 # trace frame's kernel time (every kernel of a frame, copies included), beside the live stage spans
-KT_FILES = {"C2": os.path.join(ROOT, "profiles", "r06", "r06zm_kt_summary.txt")}
+KT_FILES = {"C2": os.path.join(ROOT, "profiles", "r06", "r06zs_kt_summary.txt")}
 
 
 def parse(argv=None):
